@@ -1,0 +1,1 @@
+"""Namespace scaffolding mirroring the reference Java package net.jgp.labs."""

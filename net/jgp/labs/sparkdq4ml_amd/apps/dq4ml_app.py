@@ -1,0 +1,107 @@
+"""Behavioural equivalent of ``DataQuality4MachineLearningApp`` (``DataQuality4MachineLearningApp.java:26-156``):
+session -> register the two DQ UDFs -> CSV load -> rename -> rule 1 -> SQL clean-up -> rule 2 ->
+SQL clean-up -> label -> VectorAssembler -> LinearRegression(maxIter 40, regParam 1,
+elasticNetParam 1) -> transform/show -> training summary -> predict(40 guests).
+
+    python -m net.jgp.labs.sparkdq4ml_amd.apps.dq4ml_app [--data data/dataset-abstract.csv] [--master local[*]]
+"""
+from __future__ import annotations
+
+import argparse
+import os
+
+from .. import (LinearRegression, SparkSession, VectorAssembler, Vectors, callUDF)
+from ..dq.rules import MinimumPriceDataQualityUdf, PriceCorrelationDataQualityUdf
+from ..sql.types import DataTypes
+from ..utils.javafmt import java_str
+
+DEFAULT_DATA = "data/dataset-abstract.csv"
+
+
+class DataQuality4MachineLearningApp:
+    def __init__(self, data=DEFAULT_DATA, master="local[*]", gram_dtype="fp64"):
+        self.data, self.master, self.gram_dtype = data, master, gram_dtype
+
+    def start(self):
+        spark = SparkSession.builder().appName("DQ4ML").master(self.master).getOrCreate()
+
+        # DQ Section
+        spark.udf().register("minimumPriceRule", MinimumPriceDataQualityUdf(), DataTypes.DoubleType)
+        spark.udf().register("priceCorrelationRule", PriceCorrelationDataQualityUdf(), DataTypes.DoubleType)
+
+        df = spark.read().format("csv").option("inferSchema", "true").option("header", "false").load(self.data)
+        df = df.withColumnRenamed("_c0", "guest")
+        df = df.withColumnRenamed("_c1", "price")
+
+        print("----")
+        print("Load & Format")
+        df.show()
+        print("----")
+
+        df = df.withColumn("price_no_min", callUDF("minimumPriceRule", df.col("price")))
+        print("----")
+        print("1st DQ rule")
+        df.printSchema()
+        df.show(50)
+        print("----")
+
+        df.createOrReplaceTempView("price")
+        df = spark.sql("SELECT cast(guest as int) guest, price_no_min AS price FROM price WHERE price_no_min > 0")
+        print("----")
+        print("1st DQ rule - clean-up")
+        df.printSchema()
+        df.show(50)
+        print("----")
+
+        df = df.withColumn("price_correct_correl", callUDF("priceCorrelationRule", df.col("price"), df.col("guest")))
+        df.createOrReplaceTempView("price")
+        df = spark.sql("SELECT guest, price_correct_correl AS price FROM price WHERE price_correct_correl > 0")
+        print("----")
+        print("2nd DQ rule")
+        df.show(50)
+        print("----")
+
+        # ML Section
+        df = df.withColumn("label", df.col("price"))
+        assembler = VectorAssembler().setInputCols(["guest"]).setOutputCol("features")
+        df = assembler.transform(df)
+        df.printSchema()
+        df.show()
+
+        lr = LinearRegression().setMaxIter(40).setRegParam(1).setElasticNetParam(1).setGramDtype(self.gram_dtype)
+        model = lr.fit(df)
+        model.transform(df).show()
+
+        training_summary = model.summary()
+        print("numIterations: " + java_str(training_summary.totalIterations()))
+        print("objectiveHistory: " + str(Vectors.dense(training_summary.objectiveHistory())))
+        training_summary.residuals().show()
+        print("RMSE: " + java_str(training_summary.rootMeanSquaredError()))
+        print("r2: " + java_str(training_summary.r2()))
+
+        print("Intersection: " + java_str(model.intercept()))
+        print("Regression parameter: " + java_str(model.getRegParam()))
+        print("Tol: " + java_str(model.getTol()))
+
+        feature = 40.0
+        features = Vectors.dense(40.0)
+        p = model.predict(features)
+        print("Prediction for " + java_str(feature) + " guests is " + java_str(p))
+        return model
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
+    ap.add_argument("--data", default=DEFAULT_DATA)
+    ap.add_argument("--master", default="local[*]")
+    ap.add_argument("--gram-dtype", default="fp64", choices=["fp64", "fp32", "bf16", "fp8"])
+    a = ap.parse_args(argv)
+    data = a.data
+    if not os.path.exists(data):
+        here = os.path.join(os.path.dirname(__file__), "..", "..", "..", "..", "..", data)
+        data = here if os.path.exists(here) else data
+    DataQuality4MachineLearningApp(data, a.master, a.gram_dtype).start()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,447 @@
+"""``LinearRegression`` / ``LinearRegressionModel`` / training summary.
+
+The lab builds ``new LinearRegression().setMaxIter(40).setRegParam(1).setElasticNetParam(1)``,
+calls ``fit`` (``DataQuality4MachineLearningApp.java:120-126``), ``model.transform(df).show()``
+(``:129``), reads ``summary().totalIterations/objectiveHistory/residuals/rootMeanSquaredError/r2``
+(``:132-139``), ``intercept/getRegParam/getTol`` (``:141-146``) and ``predict(Vectors.dense(40.0))``
+(``:149-151``).
+
+Execution of ``fit`` (normal-equation path):
+
+1. ``gram_stats`` — one fused device pass over the feature matrix, label, weights and the DQ
+   selection vector (HIP MFMA kernel; f64/f32/bf16/fp8 compute selectable through
+   ``gramDtype``) producing Spark's WLS aggregator statistics;
+2. one RCCL all-reduce of that flat f64 buffer across data-parallel ranks (``parallel.comm``);
+3. the f64 normal-equation solve (native host library / device for large k);
+4. the summary is lazy: predictions and metrics are one more fused device pass on first access.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import numpy as np
+import torch
+
+from ..ops import kernels
+from ..parallel import comm
+from ..sql.dataframe import DataFrame
+from ..sql.expressions import AnalysisException, ColRef, EvalContext, Expr
+from ..sql.plan import Project, execute
+from ..sql.table import ColumnData
+from ..sql.types import DoubleType, VectorUDT, is_numeric
+from ..utils.logging import get_logger
+from .linalg import DenseVector, Vector, Vectors
+from .optim import MAX_NUM_FEATURES, GramStats, weighted_least_squares
+from .param import Param, Params, param_accessors
+
+__all__ = ["LinearRegression", "LinearRegressionModel", "LinearRegressionTrainingSummary",
+           "LinearRegressionSummary"]
+
+log = get_logger("regression")
+
+
+class _JavaFloat(float):
+    """A float that can also be *called* — lets both ``summary.r2`` (pyspark) and
+    ``summary.r2()`` (Java, as in the reference app) work."""
+
+    def __call__(self):
+        return float(self)
+
+
+class _JavaInt(int):
+    def __call__(self):
+        return int(self)
+
+
+class _JavaArray(np.ndarray):
+    def __call__(self):
+        return np.asarray(self)
+
+
+def _jarr(a):
+    return np.asarray(a, dtype=np.float64).view(_JavaArray)
+
+
+_GRAM_DTYPES = ("fp64", "fp32", "bf16", "fp8")
+
+
+class _LRParams(Params):
+    _params = {
+        "featuresCol": Param("featuresCol", "features column name", "features"),
+        "labelCol": Param("labelCol", "label column name", "label"),
+        "predictionCol": Param("predictionCol", "prediction column name", "prediction"),
+        "maxIter": Param("maxIter", "maximum number of iterations (>= 0)", 100, lambda v: v >= 0, converter=int),
+        "regParam": Param("regParam", "regularization parameter (>= 0)", 0.0, lambda v: v >= 0, converter=float),
+        "elasticNetParam": Param("elasticNetParam", "the ElasticNet mixing parameter, in range [0, 1]", 0.0,
+                                 lambda v: 0 <= v <= 1, converter=float),
+        "tol": Param("tol", "the convergence tolerance for iterative algorithms (>= 0)", 1e-6, lambda v: v >= 0, converter=float),
+        "fitIntercept": Param("fitIntercept", "whether to fit an intercept term", True),
+        "standardization": Param("standardization", "whether to standardize the training features before fitting "
+                                                    "the model", True),
+        "weightCol": Param("weightCol", "weight column name. If this is not set or empty, we treat all instance "
+                                        "weights as 1.0", None, has_default=False),
+        "solver": Param("solver", "The solver algorithm for optimization. Supported options: auto, normal, l-bfgs",
+                        "auto", lambda v: v in ("auto", "normal", "l-bfgs")),
+        "aggregationDepth": Param("aggregationDepth", "suggested depth for treeAggregate (>= 2)", 2, lambda v: v >= 2, converter=int),
+        "loss": Param("loss", "The loss function to be optimized. Supported options: squaredError, huber",
+                      "squaredError", lambda v: v in ("squaredError", "huber")),
+        "epsilon": Param("epsilon", "The shape parameter to control the amount of robustness. Must be > 1.0.", 1.35,
+                         lambda v: v > 1.0, converter=float),
+        "gramDtype": Param("gramDtype", "device compute precision of the normal-equation Gram pass "
+                                        "(fp64 | fp32 | bf16 | fp8)", "fp64", lambda v: v in _GRAM_DTYPES),
+    }
+
+
+def _weight_of(params, tbl):
+    if params.isSet("weightCol") and params.getOrDefault("weightCol"):
+        w = tbl.column(params.getOrDefault("weightCol"))
+        return w.values.to(torch.float64) if w.values.dtype != torch.float32 else w.values
+    return None
+
+
+def _features_label(params, df: DataFrame):
+    schema = df.schema
+    fc, lc = params.getOrDefault("featuresCol"), params.getOrDefault("labelCol")
+    try:
+        ft = ColRef(fc).data_type(schema)
+    except AnalysisException:
+        raise ValueError(f"Field \"{fc}\" does not exist.\nAvailable fields: {', '.join(schema.names)}") from None
+    if not isinstance(ft, VectorUDT):
+        raise ValueError(f"requirement failed: Column {fc} must be of type struct<type:tinyint,size:int,"
+                         f"indices:array<int>,values:array<double>> but was actually {ft.simpleString()}.")
+    lt = ColRef(lc).data_type(schema)
+    if not is_numeric(lt):
+        raise ValueError(f"requirement failed: Column {lc} must be of type numeric but was actually of type "
+                         f"{lt.simpleString()}.")
+    tbl = df._table()
+    X = tbl.column(fc)
+    y = tbl.column(lc)
+    return tbl, X, y
+
+
+@param_accessors
+class LinearRegression(_LRParams):
+    uid_prefix = "linReg"
+
+    def __init__(self, uid=None, **kw):
+        super().__init__(uid)
+        for k, v in kw.items():
+            self.set(k, v)
+
+    def fit(self, dataset: DataFrame, params=None) -> "LinearRegressionModel":
+        est = self.copy(params) if params else self
+        return est._train(dataset)
+
+    def _train(self, df: DataFrame) -> "LinearRegressionModel":
+        tbl, X, y = _features_label(self, df)
+        d = int(X.values.shape[0])
+        if d <= 0:
+            raise ValueError("requirement failed: The number of features must be positive.")
+        loss, solver = self.getOrDefault("loss"), self.getOrDefault("solver")
+        if loss == "huber" and solver == "normal":
+            raise ValueError("requirement failed: LinearRegression with huber loss only supports L-BFGS solver.")
+        if loss == "squaredError" and ((solver == "auto" and d <= MAX_NUM_FEATURES) or solver == "normal"):
+            return self._train_wls(df, tbl, X, y, d)
+        from .lbfgs_path import train_lbfgs
+
+        return train_lbfgs(self, df, tbl, X, y, d)
+
+    def _train_wls(self, df, tbl, X, y, d):
+        if X.valid is not None and bool((tbl.sel_mask() & ~X.valid).any()):
+            raise ValueError("features column contains nulls")
+        w = _weight_of(self, tbl)
+        sel = tbl.sel
+        yv, yvalid = y.values, y.valid
+        if yvalid is not None:
+            sel = yvalid if sel is None else (sel & yvalid)
+        flat = kernels.gram_stats(X.values, yv, w, sel, self.getOrDefault("gramDtype"))
+        flat = comm.all_reduce_sum(flat)  # X1: data-parallel Gram all-reduce (RCCL over xGMI)
+        stats = GramStats.from_flat(flat.cpu().numpy(), d)
+        wls = weighted_least_squares(
+            stats, self.getOrDefault("fitIntercept"), float(self.getOrDefault("regParam")),
+            float(self.getOrDefault("elasticNetParam")), bool(self.getOrDefault("standardization")), True,
+            "auto", int(self.getOrDefault("maxIter")), float(self.getOrDefault("tol")))
+        model = LinearRegressionModel(self.uid, DenseVector(wls.coefficients), float(wls.intercept))
+        self.copyValues(model)
+        model._set_summary(LinearRegressionTrainingSummary(model, df, wls.diagInvAtWA, wls.objectiveHistory,
+                                                           stats=stats, solver=wls.solver))
+        return model
+
+
+class PredictExpr(Expr):
+    """``prediction = features . coef + intercept`` (K7, fused device GEMV)."""
+
+    def __init__(self, features: str, coef: np.ndarray, intercept: float):
+        self.features, self.coef, self.intercept = features, coef, intercept
+
+    def children(self):
+        return [ColRef(self.features)]
+
+    def data_type(self, schema):
+        return DoubleType()
+
+    def nullable(self, schema):
+        return False
+
+    def sql_name(self):
+        return "prediction"
+
+    def eval(self, ctx: EvalContext) -> ColumnData:
+        X = ctx.table.column(self.features)
+        return ColumnData(DoubleType(), kernels.predict(X.values, self.coef, self.intercept), X.valid)
+
+
+@param_accessors
+class LinearRegressionModel(_LRParams):
+    uid_prefix = "linReg"
+
+    def __init__(self, uid: Optional[str], coefficients: Vector, intercept: float, scale: float = 1.0):
+        super().__init__(uid)
+        self._coefficients = coefficients if isinstance(coefficients, Vector) else DenseVector(coefficients)
+        self._intercept = _JavaFloat(intercept)
+        self.scale = scale
+        self._summary = None
+
+    # pyspark-style properties that are also callable (Java spelling) -----------------------------
+    @property
+    def coefficients(self):
+        return _CallableVector(self._coefficients.toArray())
+
+    @property
+    def intercept(self):
+        return self._intercept
+
+    @property
+    def numFeatures(self):
+        return _JavaInt(len(self._coefficients))
+
+    def _set_summary(self, s):
+        self._summary = s
+        return self
+
+    @property
+    def hasSummary(self):
+        return self._summary is not None
+
+    @property
+    def summary(self) -> "LinearRegressionTrainingSummary":
+        if self._summary is None:
+            raise RuntimeError(f"No training summary available for this {type(self).__name__}")
+        return self._summary
+
+    def predict(self, features) -> float:
+        v = features.toArray() if isinstance(features, Vector) else np.asarray(features, dtype=np.float64)
+        return _JavaFloat(float(np.dot(self._coefficients.toArray(), v)) + float(self._intercept))
+
+    def transform(self, df: DataFrame) -> DataFrame:
+        fc, pc = self.getOrDefault("featuresCol"), self.getOrDefault("predictionCol")
+        if not pc:
+            return df
+        ColRef(fc).data_type(df.schema)
+        from ..sql.expressions import Alias
+
+        exprs = [ColRef(n) for n in df.columns if n != pc] + \
+                [Alias(PredictExpr(fc, self._coefficients.toArray(), float(self._intercept)), pc)]
+        return DataFrame(Project(df._plan, exprs), df.sparkSession)
+
+    def evaluate(self, df: DataFrame) -> "LinearRegressionSummary":
+        return LinearRegressionSummary(self, df)
+
+    # persistence ---------------------------------------------------------------------------
+    def write(self):
+        from .persistence import LinearRegressionModelWriter
+
+        return LinearRegressionModelWriter(self)
+
+    def save(self, path):
+        self.write().save(path)
+
+    @classmethod
+    def read(cls):
+        from .persistence import LinearRegressionModelReader
+
+        return LinearRegressionModelReader()
+
+    @classmethod
+    def load(cls, path):
+        return cls.read().load(path)
+
+    def __repr__(self):
+        return f"LinearRegressionModel: uid={self.uid}, numFeatures={len(self._coefficients)}"
+
+
+class _CallableVector(DenseVector):
+    def __call__(self):
+        return self
+
+
+class LinearRegressionSummary:
+    """Metrics over ``model.transform(df)`` (``RegressionMetrics`` semantics of Spark 2.4): one fused
+    predict + reduction pass on the device (K7+K8), lazily, shared by every metric."""
+
+    def __init__(self, model: LinearRegressionModel, df: DataFrame, diag_inv=None, stats: GramStats = None):
+        self._model = model
+        self._df = df
+        self._diag_inv = np.zeros(1) if diag_inv is None else np.asarray(diag_inv)
+        self._stats = stats
+        self._m = None
+        self._pred_df = None
+
+    def __call__(self):  # Java spelling: model.summary()
+        return self
+
+    @property
+    def predictions(self) -> DataFrame:
+        if self._pred_df is None:
+            self._pred_df = self._model.transform(self._df)
+        return self._pred_df
+
+    @property
+    def predictionCol(self):
+        return self._model.getOrDefault("predictionCol")
+
+    @property
+    def labelCol(self):
+        return self._model.getOrDefault("labelCol")
+
+    @property
+    def featuresCol(self):
+        return self._model.getOrDefault("featuresCol")
+
+    def _metrics(self):
+        if self._m is None:
+            tbl = self._df._table()
+            X = tbl.column(self.featuresCol)
+            y = tbl.column(self.labelCol)
+            sel = tbl.sel
+            if y.valid is not None:
+                sel = y.valid if sel is None else (sel & y.valid)
+            shift = float(self._stats.bBar) if self._stats is not None else 0.0
+            sums = kernels.regression_metrics(X.values, y.values, self._model._coefficients.toArray(),
+                                              float(self._model._intercept), sel, shift)
+            sums = comm.all_reduce_sum(sums)
+            self._m = _Metrics(sums.cpu().numpy(), shift, not self._model.getOrDefault("fitIntercept"))
+        return self._m
+
+    @property
+    def numInstances(self):
+        return _JavaInt(int(round(self._metrics().n)))
+
+    @property
+    def degreesOfFreedom(self):
+        k = len(self._model._coefficients)
+        return _JavaInt(self.numInstances - k - (1 if self._model.getOrDefault("fitIntercept") else 0))
+
+    @property
+    def explainedVariance(self):
+        return _JavaFloat(self._metrics().ss_reg / self._metrics().n)
+
+    @property
+    def meanAbsoluteError(self):
+        return _JavaFloat(self._metrics().sum_abs_err / self._metrics().n)
+
+    @property
+    def meanSquaredError(self):
+        return _JavaFloat(self._metrics().ss_err / self._metrics().n)
+
+    @property
+    def rootMeanSquaredError(self):
+        return _JavaFloat(np.sqrt(self._metrics().ss_err / self._metrics().n))
+
+    @property
+    def r2(self):
+        m = self._metrics()
+        return _JavaFloat(1.0 - m.ss_err / (m.ss_y if m.through_origin else m.ss_tot))
+
+    @property
+    def r2adj(self):
+        icpt = 1 if self._model.getOrDefault("fitIntercept") else 0
+        n = self.numInstances
+        return _JavaFloat(1 - (1 - self.r2) * (n - icpt) / (n - len(self._model._coefficients) - icpt))
+
+    @property
+    def residuals(self) -> DataFrame:
+        from ..sql.expressions import Alias, BinOp, Cast
+
+        p = self.predictions
+        e = Alias(BinOp("-", Cast(ColRef(self.labelCol), "double"), ColRef(self.predictionCol)), "residuals")
+        return _CallableDF(Project(p._plan, [e]), p.sparkSession)
+
+    @property
+    def devianceResiduals(self):
+        r = self.residuals._table()
+        col = r.columns[0]
+        live = r.sel_mask() & col.valid_mask(r.device)
+        v = col.values[live]
+        if self._model.isSet("weightCol") and self._model.getOrDefault("weightCol"):
+            w = self.predictions._table().column(self._model.getOrDefault("weightCol")).values[live]
+            v = v * torch.sqrt(w.to(torch.float64))
+        return _jarr([float(v.min()), float(v.max())])
+
+    def _require_std_errors(self):
+        if self._diag_inv.shape[0] == 1 and self._diag_inv[0] == 0:
+            raise RuntimeError("No Std. Error of coefficients available for this LinearRegressionModel")
+
+    @property
+    def coefficientStandardErrors(self):
+        self._require_std_errors()
+        rss = self.meanSquaredError * self.numInstances
+        sigma2 = rss / self.degreesOfFreedom
+        return _jarr(np.sqrt(self._diag_inv * sigma2))
+
+    @property
+    def tValues(self):
+        se = self.coefficientStandardErrors
+        est = self._model._coefficients.toArray()
+        if self._model.getOrDefault("fitIntercept"):
+            est = np.concatenate([est, [float(self._model._intercept)]])
+        return _jarr(est / se)
+
+    @property
+    def pValues(self):
+        from scipy.stats import t as student_t
+
+        return _jarr(2.0 * (1.0 - student_t.cdf(np.abs(self.tValues), self.degreesOfFreedom)))
+
+
+class _CallableDF(DataFrame):
+    def __call__(self):
+        return self
+
+
+class LinearRegressionTrainingSummary(LinearRegressionSummary):
+    def __init__(self, model, df, diag_inv, objective_history, stats=None, solver="auto"):
+        super().__init__(model, df, diag_inv, stats)
+        self._history = np.asarray(objective_history, dtype=np.float64)
+        self.solver = solver
+
+    @property
+    def objectiveHistory(self):
+        return _jarr(self._history)
+
+    @property
+    def totalIterations(self):
+        """Spark 2.4: ``objectiveHistory.length``."""
+        return _JavaInt(len(self._history))
+
+
+class _Metrics:
+    """RegressionMetrics from the fused reduction: sums over live rows of
+    [n, y-s, (y-s)^2, r, r^2, |r|, p-s, (p-s)^2] with shift s (numerically stable SStot/SSreg)."""
+
+    def __init__(self, sums, shift, through_origin):
+        n, sy, syy, sr, srr, sabs, sp, spp = (float(v) for v in sums[:8])
+        self.n = n
+        self.through_origin = through_origin
+        mean_y_shifted = sy / n
+        self.mean_y = shift + mean_y_shifted
+        self.ss_err = srr
+        self.sum_abs_err = sabs
+        self.ss_tot = syy - n * mean_y_shifted ** 2
+        # SSy = sum(y^2) = sum((y-s)^2) + 2 s sum(y-s) + n s^2
+        self.ss_y = syy + 2 * shift * sy + n * shift * shift
+        # SSreg = sum((p - ybar)^2) = sum((p-s)^2) - 2 (ybar-s) sum(p-s) + n (ybar-s)^2
+        self.ss_reg = spp - 2 * mean_y_shifted * sp + n * mean_y_shifted ** 2
+
+
+_ = (execute, Vectors)

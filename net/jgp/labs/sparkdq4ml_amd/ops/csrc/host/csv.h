@@ -1,0 +1,55 @@
+// Host CSV scanner with Spark 2.4 CSV-source semantics:
+//   * line terminators \n, \r and \r\n (Hadoop LineRecordReader, non-multiLine mode); the
+//     reference datasets use CR only and have no trailing terminator
+//   * separator / quote / escape configurable (defaults , " \), empty field -> null
+//   * header=false -> columns _c0.._cN-1 with N taken from the first record
+//   * inferSchema -> per-field lattice null < int < long < decimal < double < boolean < string,
+//     per-column tightest common type
+//   * PERMISSIVE: short rows padded with nulls, extra tokens dropped, a field that fails to parse
+//     under the final schema nulls the whole row (Spark's malformed-record handling)
+// Used for local (CPU) sessions and for small files; the device scanner (csrc/hip/csv_scan.hip)
+// implements the same contract for numeric columns on the MI355X.
+#pragma once
+#include <cstdint>
+#include <string>
+#include <vector>
+
+namespace dq4ml {
+
+enum CsvType : int { T_NULL = 0, T_INT = 1, T_LONG = 2, T_DECIMAL = 3, T_DOUBLE = 4, T_BOOL = 5, T_STRING = 6 };
+
+struct CsvOptions {
+  char sep = ',';
+  char quote = '"';
+  char escape = '\\';
+  bool header = false;
+  bool infer_schema = false;
+  std::string null_value;  // empty string => empty field is null
+  char comment = 0;
+  bool ignore_leading_ws = false;
+  bool ignore_trailing_ws = false;
+};
+
+struct CsvColumn {
+  std::string name;
+  int type = T_STRING;
+  std::vector<int64_t> ivals;     // T_INT / T_LONG / T_BOOL
+  std::vector<double> dvals;      // T_DOUBLE / T_DECIMAL
+  std::vector<std::string> svals; // T_STRING
+  std::vector<uint8_t> valid;     // 1 = not null
+};
+
+struct CsvTable {
+  int64_t nrows = 0;
+  std::vector<CsvColumn> cols;
+};
+
+// user_types: optional forced schema (empty => infer or all strings)
+CsvTable csv_scan(const char* data, size_t len, const CsvOptions& opt, const std::vector<int>& user_types,
+                  const std::vector<std::string>& user_names);
+
+// Lattice helpers shared with tests.
+int csv_infer_field(const char* s, size_t n);
+int csv_merge_types(int a, int b);
+
+}  // namespace dq4ml

@@ -1,0 +1,121 @@
+// pybind11 bindings of the host runtime library (_dq4ml_host): normal-equation solvers and the
+// CSV scanner.  Device kernels live in the separate gfx950 module (_dq4ml_hip).
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include "csv.h"
+#include "solvers.h"
+
+namespace py = pybind11;
+using namespace dq4ml;
+
+static std::vector<double> to_vec(const py::array_t<double, py::array::c_style | py::array::forcecast>& a) {
+  return std::vector<double>(a.data(), a.data() + a.size());
+}
+
+static py::array_t<double> to_np(const std::vector<double>& v) {
+  py::array_t<double> a(v.size());
+  std::copy(v.begin(), v.end(), a.mutable_data());
+  return a;
+}
+
+PYBIND11_MODULE(_dq4ml_host, m) {
+  m.doc() = "dq4ml host runtime: f64 normal-equation solvers (Breeze-compatible) and CSV scanner";
+
+  py::register_exception<SingularMatrixError>(m, "SingularMatrixError");
+
+  m.def("dspmv", [](int k, py::array_t<double, py::array::c_style | py::array::forcecast> ap,
+                    py::array_t<double, py::array::c_style | py::array::forcecast> x) {
+    if (ap.size() != (py::ssize_t)k * (k + 1) / 2 || x.size() != k) throw std::invalid_argument("dspmv: bad sizes");
+    std::vector<double> y(k);
+    dspmv(k, ap.data(), x.data(), y.data());
+    return to_np(y);
+  });
+
+  m.def("cholesky_solve", [](int k, py::array_t<double, py::array::c_style | py::array::forcecast> ap,
+                             py::array_t<double, py::array::c_style | py::array::forcecast> b) {
+    if (ap.size() != (py::ssize_t)k * (k + 1) / 2 || b.size() != k) throw std::invalid_argument("cholesky_solve: bad sizes");
+    std::vector<double> x;
+    {
+      py::gil_scoped_release nogil;
+      x = cholesky_solve(k, to_vec(ap), to_vec(b));
+    }
+    return to_np(x);
+  });
+
+  m.def("cholesky_inverse", [](int k, py::array_t<double, py::array::c_style | py::array::forcecast> ap) {
+    if (ap.size() != (py::ssize_t)k * (k + 1) / 2) throw std::invalid_argument("cholesky_inverse: bad size");
+    return to_np(cholesky_inverse(k, to_vec(ap)));
+  });
+
+  m.def(
+      "quasi_newton",
+      [](double bBar, double bbBar, py::array_t<double, py::array::c_style | py::array::forcecast> ab,
+         py::array_t<double, py::array::c_style | py::array::forcecast> aa,
+         py::array_t<double, py::array::c_style | py::array::forcecast> aBar, bool fit_intercept, int max_iter,
+         double tol, py::object l1, int memory) {
+        std::vector<double> l1v;
+        if (!l1.is_none()) l1v = to_vec(l1.cast<py::array_t<double, py::array::c_style | py::array::forcecast>>());
+        const int k = static_cast<int>(ab.size());
+        if (aa.size() != (py::ssize_t)k * (k + 1) / 2) throw std::invalid_argument("quasi_newton: aa size");
+        QNResult r;
+        {
+          auto abv = to_vec(ab), aav = to_vec(aa), abar = to_vec(aBar);
+          py::gil_scoped_release nogil;
+          r = quasi_newton(bBar, bbBar, abv, aav, abar, fit_intercept, max_iter, tol, l1v, memory);
+        }
+        return py::make_tuple(to_np(r.x), to_np(r.objective_history), r.converged_reason);
+      },
+      py::arg("bBar"), py::arg("bbBar"), py::arg("ab"), py::arg("aa"), py::arg("aBar"), py::arg("fit_intercept"),
+      py::arg("max_iter"), py::arg("tol"), py::arg("l1") = py::none(), py::arg("memory") = 10);
+
+  m.def("csv_infer_field", [](const std::string& s) { return csv_infer_field(s.data(), s.size()); });
+  m.def("csv_merge_types", &csv_merge_types);
+
+  m.def(
+      "csv_scan",
+      [](py::bytes data, std::string sep, std::string quote, std::string escape, bool header, bool infer,
+         std::string null_value, std::string comment, bool ilws, bool itws, std::vector<int> user_types,
+         std::vector<std::string> user_names) {
+        std::string buf = data;
+        CsvOptions o;
+        o.sep = sep.empty() ? ',' : sep[0];
+        o.quote = quote.empty() ? '\0' : quote[0];
+        o.escape = escape.empty() ? '\\' : escape[0];
+        o.header = header;
+        o.infer_schema = infer;
+        o.null_value = null_value;
+        o.comment = comment.empty() ? 0 : comment[0];
+        o.ignore_leading_ws = ilws;
+        o.ignore_trailing_ws = itws;
+        CsvTable t;
+        {
+          py::gil_scoped_release nogil;
+          t = csv_scan(buf.data(), buf.size(), o, user_types, user_names);
+        }
+        py::list cols;
+        for (auto& c : t.cols) {
+          py::object vals;
+          if (c.type == T_STRING) {
+            py::list l;
+            for (auto& s : c.svals) l.append(py::str(s));
+            vals = l;
+          } else if (c.type == T_DOUBLE || c.type == T_DECIMAL) {
+            vals = to_np(c.dvals);
+          } else {
+            py::array_t<int64_t> a(c.ivals.size());
+            std::copy(c.ivals.begin(), c.ivals.end(), a.mutable_data());
+            vals = a;
+          }
+          py::array_t<uint8_t> v(c.valid.size());
+          std::copy(c.valid.begin(), c.valid.end(), v.mutable_data());
+          cols.append(py::make_tuple(c.name, c.type, vals, v));
+        }
+        return py::make_tuple(t.nrows, cols);
+      },
+      py::arg("data"), py::arg("sep") = ",", py::arg("quote") = "\"", py::arg("escape") = "\\",
+      py::arg("header") = false, py::arg("infer") = false, py::arg("null_value") = "", py::arg("comment") = "",
+      py::arg("ignore_leading_ws") = false, py::arg("ignore_trailing_ws") = false,
+      py::arg("user_types") = std::vector<int>{}, py::arg("user_names") = std::vector<std::string>{});
+}

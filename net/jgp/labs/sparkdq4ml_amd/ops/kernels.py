@@ -1,0 +1,135 @@
+"""Device-op facade.
+
+Every op takes/returns torch tensors.  CUDA (ROCm) tensors go to the gfx950 kernels of
+``_dq4ml_hip`` — a missing extension is a hard error on a GPU box, never a silent torch
+fallback.  CPU tensors (``local-cpu`` sessions, unit tests) run the host implementations, which
+are also the fp64 oracles of the kernel tests.
+
+Ops:
+  K3  ``selected_indices``   stream compaction of a selection vector
+  K4  ``pack_columns``       columns -> feature-major [d, n] matrix (cast)
+  K5  ``gram_stats``         WLS sufficient statistics (MFMA Gram) of [X | 1 | y] with weights/mask
+  K7+K8 ``predict`` / ``regression_metrics``  fused GEMV + metric reductions
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from . import native
+
+__all__ = ["selected_indices", "pack_columns", "gram_stats", "predict", "regression_metrics",
+           "gram_layout_size"]
+
+
+def _on_gpu(t: torch.Tensor) -> bool:
+    return t.is_cuda
+
+
+def _stream(t: torch.Tensor) -> int:
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+# ------------------------------------------------------------------------------------------
+# K3 — compaction
+# ------------------------------------------------------------------------------------------
+def selected_indices(sel: torch.Tensor, limit: Optional[int] = None) -> torch.Tensor:
+    """Indices (int64) of the true entries of ``sel``, in order; at most ``limit`` of them."""
+    if _on_gpu(sel):
+        from . import device
+
+        return device.compact_indices(sel, limit)
+    idx = torch.nonzero(sel, as_tuple=False).flatten()
+    return idx if limit is None else idx[:limit]
+
+
+# ------------------------------------------------------------------------------------------
+# K4 — pack
+# ------------------------------------------------------------------------------------------
+def pack_columns(parts: Sequence[torch.Tensor], dtype: torch.dtype) -> torch.Tensor:
+    """Stack 1-row/k-row pieces (each ``[k_i, n]``) into one feature-major ``[d, n]`` matrix."""
+    if parts and _on_gpu(parts[0]):
+        from . import device
+
+        return device.pack_columns(list(parts), dtype)
+    return torch.cat([p.to(dtype) for p in parts], dim=0)
+
+
+# ------------------------------------------------------------------------------------------
+# K5 — Gram / WLS statistics
+# ------------------------------------------------------------------------------------------
+def gram_layout_size(d: int) -> int:
+    return 5 + 2 * d + d * (d + 1) // 2
+
+
+def packed_upper(aa: torch.Tensor) -> torch.Tensor:
+    d = aa.shape[0]
+    J = torch.repeat_interleave(torch.arange(d, device=aa.device), torch.arange(1, d + 1, device=aa.device))
+    I = torch.cat([torch.arange(j + 1, device=aa.device) for j in range(d)]) if d else J
+    return aa[I, J]
+
+
+def gram_stats(X: torch.Tensor, y: torch.Tensor, w: Optional[torch.Tensor], sel: Optional[torch.Tensor],
+               compute: str = "fp64") -> torch.Tensor:
+    """Flat f64 ``[count, wSum, wwSum, bSum, bbSum, aSum[d], abSum[d], aaSum packed-upper]`` over
+    live rows (``sel``), with instance weights ``w`` (default 1) — Spark WLS ``Aggregator.add`` over
+    every row, in one pass.  ``X`` is feature-major ``[d, n]``."""
+    d, n = X.shape
+    if y.shape[0] != n or (w is not None and w.shape[0] != n) or (sel is not None and sel.shape[0] != n):
+        raise ValueError("gram_stats: row-count mismatch between features, label, weight and selection")
+    if _on_gpu(X):
+        from . import device
+
+        return device.gram_stats(X, y, w, sel, compute)
+    Xd = X.to(torch.float64)
+    yd = y.to(torch.float64)
+    wv = torch.ones(n, dtype=torch.float64) if w is None else w.to(torch.float64)
+    live = torch.ones(n, dtype=torch.bool) if sel is None else sel
+    wv = torch.where(live, wv, torch.zeros_like(wv))
+    count = float(live.sum())
+    Xw = Xd * wv
+    aa = Xw @ Xd.t()
+    out = torch.empty(gram_layout_size(d), dtype=torch.float64)
+    out[0] = count
+    out[1] = wv.sum()
+    out[2] = (wv * wv).sum()
+    out[3] = (wv * yd).sum()
+    out[4] = (wv * yd * yd).sum()
+    out[5:5 + d] = Xw.sum(1)
+    out[5 + d:5 + 2 * d] = Xw @ yd
+    out[5 + 2 * d:] = packed_upper(aa)
+    return out
+
+
+# ------------------------------------------------------------------------------------------
+# K7 / K8 — predict and regression metrics
+# ------------------------------------------------------------------------------------------
+def predict(X: torch.Tensor, coef: np.ndarray, intercept: float) -> torch.Tensor:
+    if _on_gpu(X):
+        from . import device
+
+        return device.predict(X, coef, intercept)
+    c = torch.as_tensor(np.asarray(coef), dtype=torch.float64)
+    return c @ X.to(torch.float64) + intercept
+
+
+def regression_metrics(X: torch.Tensor, y: torch.Tensor, coef: np.ndarray, intercept: float,
+                       sel: Optional[torch.Tensor], shift: float) -> torch.Tensor:
+    """f64 sums over live rows: [n, Σ(y-s), Σ(y-s)², Σr, Σr², Σ|r|, Σ(p-s), Σ(p-s)²], r = y - p."""
+    if _on_gpu(X):
+        from . import device
+
+        return device.regression_metrics(X, y, coef, intercept, sel, shift)
+    p = predict(X, coef, intercept)
+    yd = y.to(torch.float64)
+    live = torch.ones_like(yd, dtype=torch.bool) if sel is None else sel
+    yd, p = yd[live], p[live]
+    r = yd - p
+    ys, ps = yd - shift, p - shift
+    return torch.stack([torch.tensor(float(yd.numel()), dtype=torch.float64), ys.sum(), (ys * ys).sum(), r.sum(),
+                        (r * r).sum(), r.abs().sum(), ps.sum(), (ps * ps).sum()])
+
+
+_ = (List, native)

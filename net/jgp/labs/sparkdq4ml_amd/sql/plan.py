@@ -1,0 +1,212 @@
+"""Lazy logical plans and their executor.
+
+Spark builds a lazy lineage and re-executes it from the CSV on every action (the
+lab re-scans ``dataset-abstract.csv`` ~10 times).  Here every node memoizes its materialized
+:class:`Table` (plans are immutable and all supported expressions are deterministic, so this is
+observationally identical) and the executor fuses Project/Filter chains into one device
+kernel launch where the expressions allow it (``ops.dqvm``).
+"""
+from __future__ import annotations
+
+import threading
+from typing import List, Optional, Sequence, Tuple
+
+import torch
+
+from .expressions import (Alias, AnalysisException, ColRef, EvalContext, Expr, UdfCall)
+from .table import ColumnData, Table
+from .types import BooleanType, StructField, StructType
+
+__all__ = ["LogicalPlan", "LocalRelation", "Project", "Filter", "Limit", "Union", "execute"]
+
+
+class LogicalPlan:
+    _memo: Optional[Table] = None
+
+    def children(self) -> List["LogicalPlan"]:
+        return []
+
+    def schema(self) -> StructType:
+        raise NotImplementedError
+
+    def _compute(self, session) -> Table:
+        raise NotImplementedError
+
+    def describe(self, indent=0) -> str:
+        s = "  " * indent + self._label() + "\n"
+        for c in self.children():
+            s += c.describe(indent + 1)
+        return s
+
+    def _label(self):
+        return type(self).__name__
+
+
+class LocalRelation(LogicalPlan):
+    def __init__(self, table: Table, label: str = "LocalRelation"):
+        self.table = table
+        self._memo = table
+        self.label = label
+
+    def schema(self):
+        return self.table.schema
+
+    def _compute(self, session):
+        return self.table
+
+    def _label(self):
+        return f"{self.label} [{', '.join(self.table.schema.names)}]"
+
+
+def output_name(e: Expr) -> str:
+    if isinstance(e, Alias):
+        return e.name
+    if isinstance(e, ColRef):
+        return e.name
+    return e.sql_name()
+
+
+class Project(LogicalPlan):
+    def __init__(self, child: LogicalPlan, exprs: Sequence[Expr]):
+        self.child = child
+        self.exprs = list(exprs)
+        self._schema = None
+
+    def children(self):
+        return [self.child]
+
+    def schema(self):
+        if self._schema is None:
+            cs = self.child.schema()
+            fields = []
+            for e in self.exprs:
+                dt = e.data_type(cs)
+                meta = {}
+                base = e.child if isinstance(e, Alias) else e
+                if isinstance(base, ColRef):
+                    meta = dict(cs[base._resolve(cs)].metadata)
+                elif hasattr(base, "metadata"):
+                    meta = base.metadata(cs)
+                fields.append(StructField(output_name(e), dt, e.nullable(cs), meta))
+            self._schema = StructType(fields)
+        return self._schema
+
+    def _compute(self, session):
+        base = execute(self.child, session)
+        ctx = EvalContext(base, session)
+        cols = []
+        schema = self.schema()
+        for e, f in zip(self.exprs, schema.fields):
+            c = e.eval(ctx)
+            if c.dtype != f.dataType:
+                from .expressions import cast_column
+
+                c = cast_column(c, f.dataType, base.device)
+            if f.metadata and not c.meta:
+                c = ColumnData(c.dtype, c.values, c.valid, dict(f.metadata))
+            cols.append(c)
+        return base.with_columns(schema, cols)
+
+    def _label(self):
+        return "Project [" + ", ".join(output_name(e) for e in self.exprs) + "]"
+
+
+class Filter(LogicalPlan):
+    def __init__(self, child: LogicalPlan, cond: Expr):
+        self.child = child
+        self.cond = cond
+        dt = cond.data_type(child.schema())
+        if not isinstance(dt, BooleanType):
+            raise AnalysisException(f"filter expression '{cond.sql_name()}' of type {dt.simpleString()} "
+                                    f"is not a boolean.")
+
+    def children(self):
+        return [self.child]
+
+    def schema(self):
+        return self.child.schema()
+
+    def _compute(self, session):
+        base = execute(self.child, session)
+        c = self.cond.eval(EvalContext(base, session))
+        keep = c.values.to(torch.bool)
+        if c.valid is not None:
+            keep = keep & c.valid
+        sel = keep if base.sel is None else (base.sel & keep)
+        t = Table(base.schema, base.columns, base.nrows, sel, base.device)
+        return _maybe_compact(t)
+
+    def _label(self):
+        return f"Filter {self.cond.sql_name()}"
+
+
+def _maybe_compact(t: Table, threshold: float = 0.25) -> Table:
+    """Keep the selection vector unless the live fraction got small (then compact)."""
+    if t.sel is None or t.nrows < 4096:
+        return t
+    live = int(t.sel.sum().item())
+    return t.compact() if live < threshold * t.nrows else t
+
+
+class Limit(LogicalPlan):
+    def __init__(self, child: LogicalPlan, n: int):
+        self.child, self.n = child, int(n)
+
+    def children(self):
+        return [self.child]
+
+    def schema(self):
+        return self.child.schema()
+
+    def _compute(self, session):
+        return execute(self.child, session).head_rows(self.n)
+
+    def _label(self):
+        return f"Limit {self.n}"
+
+
+class Union(LogicalPlan):
+    def __init__(self, left: LogicalPlan, right: LogicalPlan):
+        if len(left.schema()) != len(right.schema()):
+            raise AnalysisException("Union can only be performed on tables with the same number of columns")
+        self.left, self.right = left, right
+
+    def children(self):
+        return [self.left, self.right]
+
+    def schema(self):
+        return self.left.schema()
+
+    def _compute(self, session):
+        a, b = execute(self.left, session).compact(), execute(self.right, session).compact()
+        cols = []
+        for ca, cb in zip(a.columns, b.columns):
+            if isinstance(ca.values, list):
+                vals = ca.values + cb.values
+            else:
+                dim = 1 if ca.values.dim() == 2 else 0
+                vals = torch.cat([ca.values, cb.values.to(ca.values.dtype)], dim=dim)
+            if ca.valid is None and cb.valid is None:
+                valid = None
+            else:
+                valid = torch.cat([ca.valid_mask(a.device), cb.valid_mask(b.device)])
+            cols.append(ColumnData(ca.dtype, vals, valid, dict(ca.meta)))
+        return Table(a.schema, cols, a.nrows + b.nrows, None, a.device)
+
+
+_exec_lock = threading.RLock()
+
+
+def execute(plan: LogicalPlan, session=None) -> Table:
+    if plan._memo is not None:
+        return plan._memo
+    with _exec_lock:
+        if plan._memo is None:
+            from ..ops import dqvm
+
+            fused = dqvm.try_execute_fused(plan, session)
+            plan._memo = fused if fused is not None else plan._compute(session)
+    return plan._memo
+
+
+_ = (Tuple, UdfCall)

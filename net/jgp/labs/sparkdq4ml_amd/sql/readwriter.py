@@ -1,0 +1,283 @@
+"""``DataFrameReader`` / ``DataFrameWriter``.
+
+The lab reads ``data/dataset-abstract.csv`` with ``format("csv").option("inferSchema","true")
+.option("header","false")`` (``DataQuality4MachineLearningApp.java:52-55``).  Files are scanned
+once at ``load()`` (Spark also runs a schema-inference job there) by
+
+* the device scanner ``csv_scan`` HIP kernel (MI355X sessions, files above
+  ``dq4ml.csv.deviceThresholdBytes``, numeric columns), or
+* the native host scanner (``_dq4ml_host.csv_scan``) otherwise,
+
+both implementing the contract of SURVEY.md S03.
+"""
+from __future__ import annotations
+
+import glob
+import json
+import os
+import shutil
+from typing import Dict, List, Optional
+
+import numpy as np
+import torch
+
+from ..utils.logging import get_logger
+from .localdata import column_from_numpy, column_from_pylist, table_from_data
+from .plan import LocalRelation
+from .table import ColumnData, Table
+from .types import (BooleanType, DecimalType, DoubleType, IntegerType, LongType, StringType,
+                    StructField, StructType, parse_type_name)
+
+__all__ = ["DataFrameReader", "DataFrameWriter", "csv_code_to_type"]
+
+log = get_logger("io")
+
+_CODE2TYPE = {1: IntegerType, 2: LongType, 3: lambda: DecimalType(38, 0), 4: DoubleType, 5: BooleanType,
+              6: StringType, 0: StringType}
+
+
+def csv_code_to_type(code: int):
+    return _CODE2TYPE[int(code)]()
+
+
+def _type_to_code(t) -> int:
+    if isinstance(t, IntegerType):
+        return 1
+    if isinstance(t, LongType):
+        return 2
+    if isinstance(t, DecimalType):
+        return 3
+    if isinstance(t, DoubleType):
+        return 4
+    if isinstance(t, BooleanType):
+        return 5
+    return 6
+
+
+def _truthy(v) -> bool:
+    return str(v).lower() in ("true", "1", "yes")
+
+
+def _expand(paths) -> List[str]:
+    out = []
+    for p in paths:
+        if os.path.isdir(p):
+            out += sorted(f for f in glob.glob(os.path.join(p, "*"))
+                          if not os.path.basename(f).startswith(("_", ".")))
+        elif any(ch in p for ch in "*?["):
+            out += sorted(glob.glob(p))
+        else:
+            if not os.path.exists(p):
+                from .expressions import AnalysisException
+
+                raise AnalysisException(f"Path does not exist: file:{os.path.abspath(p)};")
+            out.append(p)
+    return out
+
+
+class DataFrameReader:
+    def __init__(self, session):
+        self._session = session
+        self._format = "parquet"
+        self._options: Dict[str, str] = {}
+        self._schema: Optional[StructType] = None
+
+    def __call__(self):
+        return self
+
+    def format(self, f: str):
+        self._format = f.lower()
+        return self
+
+    def option(self, key: str, value):
+        self._options[key.lower()] = str(value).lower() if isinstance(value, bool) else str(value)
+        return self
+
+    def options(self, **kw):
+        for k, v in kw.items():
+            self.option(k, v)
+        return self
+
+    def schema(self, s):
+        if isinstance(s, str):
+            fields = []
+            for part in s.split(","):
+                nm, _, tp = part.strip().partition(" ")
+                fields.append(StructField(nm.strip(), parse_type_name(tp.strip()), True))
+            s = StructType(fields)
+        self._schema = s
+        return self
+
+    def load(self, path=None, format=None, **opts):
+        from .dataframe import DataFrame
+
+        if format:
+            self._format = format.lower()
+        for k, v in opts.items():
+            self.option(k, v)
+        paths = path if isinstance(path, (list, tuple)) else [path]
+        files = _expand(paths)
+        if self._format == "csv":
+            table = self._read_csv(files)
+        elif self._format == "parquet":
+            table = self._read_parquet(files)
+        elif self._format == "json":
+            table = self._read_json(files)
+        else:
+            raise ValueError(f"Failed to find data source: {self._format}")
+        return DataFrame(LocalRelation(table, f"Relation[{self._format}] {','.join(paths)}"), self._session)
+
+    def csv(self, path, schema=None, sep=None, header=None, inferSchema=None, **kw):
+        if schema is not None:
+            self.schema(schema)
+        for k, v in (("sep", sep), ("header", header), ("inferSchema", inferSchema)):
+            if v is not None:
+                self.option(k, v)
+        return self.load(path, format="csv", **kw)
+
+    def parquet(self, *paths):
+        return self.load(list(paths), format="parquet")
+
+    def json(self, path):
+        return self.load(path, format="json")
+
+    # ---- csv -------------------------------------------------------------------------------
+    def _read_csv(self, files: List[str]) -> Table:
+        o = self._options
+        dev = self._session.device
+        data = b"".join(self._read_bytes(f) for f in files)
+        header = _truthy(o.get("header", "false"))
+        infer = _truthy(o.get("inferschema", "false"))
+        sep = o.get("sep", o.get("delimiter", ","))
+        sep = "\t" if sep == "\\t" else sep
+        user_types = [_type_to_code(f.dataType) for f in self._schema.fields] if self._schema else []
+        user_names = self._schema.names if self._schema else []
+        thresh = int(self._session.conf.get("dq4ml.csv.deviceThresholdBytes", str(64 << 20)))
+        if dev.type == "cuda" and len(data) >= thresh and not user_types and header is False:
+            from ..ops import csvscan
+
+            t = csvscan.scan_device(data, sep=sep, infer=infer, device=dev)
+            if t is not None:
+                return t
+        from ..ops import native
+
+        nrows, cols = native.host().csv_scan(
+            data, sep=sep, quote=o.get("quote", '"'), escape=o.get("escape", "\\"), header=header,
+            infer=infer, null_value=o.get("nullvalue", ""), comment=o.get("comment", ""),
+            ignore_leading_ws=_truthy(o.get("ignoreleadingwhitespace", "false")),
+            ignore_trailing_ws=_truthy(o.get("ignoretrailingwhitespace", "false")),
+            user_types=user_types, user_names=user_names)
+        fields, columns = [], []
+        for (name, code, vals, valid) in cols:
+            dt = self._schema[len(fields)].dataType if self._schema else csv_code_to_type(code)
+            if isinstance(vals, list):
+                c = column_from_pylist([v if ok else None for v, ok in zip(vals, valid)], StringType(), dev)
+            else:
+                c = column_from_numpy(vals, valid.astype(bool), dt, dev)
+            fields.append(StructField(name, dt, True))
+            columns.append(c)
+        return Table(StructType(fields), columns, nrows, None, dev)
+
+    @staticmethod
+    def _read_bytes(path) -> bytes:
+        with open(path, "rb") as f:
+            return f.read()
+
+    # ---- parquet / json ----------------------------------------------------------------------
+    def _read_parquet(self, files):
+        import pyarrow.parquet as pq
+        import pyarrow as pa
+
+        tables = [pq.read_table(f) for f in files if f.endswith(".parquet") or os.path.isfile(f)]
+        t = pa.concat_tables(tables) if len(tables) > 1 else tables[0]
+        return table_from_data(t.to_pandas(), self._schema, self._session.device)
+
+    def _read_json(self, files):
+        rows = []
+        for f in files:
+            with open(f) as fh:
+                for line in fh:
+                    line = line.strip()
+                    if line:
+                        rows.append(json.loads(line))
+        return table_from_data(rows, self._schema, self._session.device)
+
+
+class DataFrameWriter:
+    def __init__(self, df):
+        self._df = df
+        self._mode = "errorifexists"
+        self._format = "parquet"
+        self._options = {}
+
+    def mode(self, m):
+        self._mode = m.lower()
+        return self
+
+    def format(self, f):
+        self._format = f.lower()
+        return self
+
+    def option(self, k, v):
+        self._options[k.lower()] = str(v)
+        return self
+
+    def _prepare(self, path):
+        if os.path.exists(path):
+            if self._mode in ("overwrite",):
+                shutil.rmtree(path) if os.path.isdir(path) else os.remove(path)
+            elif self._mode in ("ignore",):
+                return False
+            elif self._mode != "append":
+                from .expressions import AnalysisException
+
+                raise AnalysisException(f"path file:{os.path.abspath(path)} already exists.;")
+        os.makedirs(path, exist_ok=True)
+        return True
+
+    def save(self, path):
+        if not self._prepare(path):
+            return
+        if self._format == "csv":
+            self._write_csv(path)
+        elif self._format == "parquet":
+            self._write_parquet(path)
+        else:
+            raise ValueError(self._format)
+        open(os.path.join(path, "_SUCCESS"), "w").close()
+
+    def csv(self, path, mode=None, header=None):
+        if mode:
+            self.mode(mode)
+        if header is not None:
+            self.option("header", header)
+        self._format = "csv"
+        self.save(path)
+
+    def parquet(self, path, mode=None):
+        if mode:
+            self.mode(mode)
+        self._format = "parquet"
+        self.save(path)
+
+    def _write_csv(self, path):
+        from ..utils.javafmt import java_str
+
+        t = self._df._table().compact()
+        sep = self._options.get("sep", ",")
+        cols = [c.to_pylist() for c in t.columns]
+        with open(os.path.join(path, "part-00000.csv"), "w") as f:
+            if _truthy(self._options.get("header", "false")):
+                f.write(sep.join(t.schema.names) + "\n")
+            for r in zip(*cols):
+                f.write(sep.join("" if v is None else java_str(v) for v in r) + "\n")
+
+    def _write_parquet(self, path):
+        import pyarrow as pa
+        import pyarrow.parquet as pq
+
+        pdf = self._df.toPandas()
+        pq.write_table(pa.Table.from_pandas(pdf, preserve_index=False), os.path.join(path, "part-00000.parquet"))
+
+
+_ = (ColumnData, np, torch)

@@ -1,0 +1,202 @@
+"""``SparkSession`` equivalent (``SparkSession.builder().appName("DQ4ML").master("local[*]")
+.getOrCreate()``, ``DataQuality4MachineLearningApp.java:38-41``).
+
+``master`` selects the execution device, mirroring Spark's parallel-width string:
+
+* ``local`` / ``local[N]`` / ``local[*]`` — this node; the session uses the node's MI355X (the
+  GPU of this rank, ``LOCAL_RANK``) when one is visible, else host (CPU) execution;
+* ``mi355x`` / ``mi355x[*]`` / ``gpu`` — require the GPU;
+* ``cpu`` / ``local-cpu[*]`` — force host execution (the unit-test configuration).
+
+Config keys (``.config(k, v)``): ``dq4ml.device``, ``dq4ml.gramDtype`` (fp64|fp32|bf16|fp8),
+``dq4ml.bucketBytes``, ``dq4ml.csv.deviceThresholdBytes``.
+"""
+from __future__ import annotations
+
+import os
+import threading
+from typing import Dict, Optional
+
+import torch
+
+from ..utils.logging import configure_logging, get_logger
+from .dataframe import DataFrame
+from .plan import LocalRelation
+from .table import ColumnData, Table
+from .types import (BooleanType, DoubleType, IntegerType, LongType, StringType, StructField,
+                    StructType, VectorUDT)
+from .udf import UDFRegistration
+
+__all__ = ["SparkSession", "Catalog", "RuntimeConfig"]
+
+log = get_logger("session")
+
+
+class RuntimeConfig:
+    def __init__(self, conf: Dict[str, str]):
+        self._conf = conf
+
+    def get(self, key, default=None):
+        return self._conf.get(key, default)
+
+    def set(self, key, value):
+        self._conf[key] = str(value)
+
+    def getAll(self):
+        return dict(self._conf)
+
+    def __call__(self):
+        return self
+
+
+class Catalog:
+    def __init__(self):
+        self._views = {}
+
+    def dropTempView(self, name):
+        return self._views.pop(name.lower(), None) is not None
+
+    def listTables(self):
+        return sorted(self._views)
+
+    def tableExists(self, name):
+        return name.lower() in self._views
+
+    def __call__(self):
+        return self
+
+
+def _resolve_device(master: str, conf: Dict[str, str]) -> torch.device:
+    forced = conf.get("dq4ml.device") or os.environ.get("DQ4ML_DEVICE")
+    m = (master or "local[*]").lower()
+    if forced:
+        want = forced.lower()
+    elif m.startswith("cpu") or m.startswith("local-cpu"):
+        want = "cpu"
+    elif m.startswith("mi355x") or m.startswith("gpu") or m.startswith("cuda"):
+        want = "cuda"
+    else:
+        want = "auto"
+    if want == "auto":
+        want = "cuda" if torch.cuda.is_available() else "cpu"
+    if want.startswith("cuda"):
+        if not torch.cuda.is_available():
+            raise RuntimeError(f"master '{master}' requires an MI355X but no GPU is visible")
+        idx = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
+        if ":" in want:
+            idx = int(want.split(":")[1])
+        torch.cuda.set_device(idx)
+        return torch.device("cuda", idx)
+    return torch.device("cpu")
+
+
+class SparkSession:
+    _active: Optional["SparkSession"] = None
+    _lock = threading.RLock()
+
+    class Builder:
+        def __init__(self):
+            self._conf: Dict[str, str] = {}
+
+        def __call__(self):
+            return SparkSession.Builder()
+
+        def appName(self, name):
+            self._conf["spark.app.name"] = name
+            return self
+
+        def master(self, m):
+            self._conf["spark.master"] = m
+            return self
+
+        def config(self, key=None, value=None, conf=None):
+            if conf is not None:
+                self._conf.update(conf)
+            elif key is not None:
+                self._conf[key] = str(value)
+            return self
+
+        def enableHiveSupport(self):
+            return self
+
+        def getOrCreate(self) -> "SparkSession":
+            with SparkSession._lock:
+                s = SparkSession._active
+                if s is not None and not s._stopped:
+                    for k, v in self._conf.items():
+                        if k not in ("spark.master",):
+                            s.conf.set(k, v)
+                    return s
+                s = SparkSession(dict(self._conf))
+                SparkSession._active = s
+                return s
+
+    builder = Builder()
+
+    def __init__(self, conf: Dict[str, str]):
+        configure_logging()
+        self._conf = conf
+        self.conf = RuntimeConfig(conf)
+        self.master = conf.get("spark.master", "local[*]")
+        self.appName = conf.get("spark.app.name", "dq4ml")
+        self.device = _resolve_device(self.master, conf)
+        self.udf = UDFRegistration(self)
+        self.catalog = Catalog()
+        self._stopped = False
+        log.debug("session %s on %s (master=%s)", self.appName, self.device, self.master)
+
+    @classmethod
+    def getActiveSession(cls):
+        return cls._active
+
+    # Java-style accessor spellings ------------------------------------------------------------
+    @property
+    def read(self):
+        from .readwriter import DataFrameReader
+
+        return DataFrameReader(self)
+
+    def sql(self, text: str) -> DataFrame:
+        from .parser import plan_sql
+
+        return DataFrame(plan_sql(text, self), self)
+
+    def table(self, name: str) -> DataFrame:
+        from .expressions import AnalysisException
+
+        p = self.catalog._views.get(name.lower())
+        if p is None:
+            raise AnalysisException(f"Table or view not found: {name}")
+        return DataFrame(p, self)
+
+    def range(self, start, end=None, step=1):
+        if end is None:
+            start, end = 0, start
+        v = torch.arange(start, end, step, dtype=torch.int64, device=self.device)
+        schema = StructType([StructField("id", LongType(), False)])
+        return DataFrame(LocalRelation(Table(schema, [ColumnData(LongType(), v)], v.numel(), None, self.device)), self)
+
+    def createDataFrame(self, data, schema=None) -> DataFrame:
+        """From a list of rows/tuples/dicts, a pandas DataFrame or a dict of tensors."""
+        from .localdata import table_from_data
+
+        return DataFrame(LocalRelation(table_from_data(data, schema, self.device)), self)
+
+    def stop(self):
+        self._stopped = True
+        if SparkSession._active is self:
+            SparkSession._active = None
+
+    close = stop
+
+    def sparkContext(self):
+        return self
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.stop()
+
+
+_ = (BooleanType, DoubleType, IntegerType, StringType, VectorUDT)

@@ -1,0 +1,176 @@
+"""Physical columnar storage.
+
+A :class:`Table` is the materialized form of a DataFrame: one :class:`ColumnData` per field plus
+an optional *selection vector* ``sel`` (bool ``[n]``).  Filters (the DQ clean-up SQL at
+``DataQuality4MachineLearningApp.java:77-78,89-90``) only AND into ``sel``; rows are physically
+compacted lazily — when rows must be enumerated (``show``/``collect``) or when the live fraction
+gets small.  Consumers that reduce over rows (Gram aggregation of ``LinearRegression.fit``,
+metrics) take ``sel`` as a 0/1 row weight instead, so the DQ -> assemble -> fit chain never
+scatters rows on the device.
+
+Vector columns (``VectorUDT``) are stored **feature-major** ``[d, n]``: every feature is a
+contiguous column, which is exactly what the MFMA Gram kernel streams.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import List, Optional
+
+import torch
+
+from .types import (BooleanType, DataType, DoubleType, IntegerType, LongType, NullType,
+                    StringType, StructField, StructType, VectorUDT)
+
+__all__ = ["ColumnData", "Table"]
+
+
+@dataclass
+class ColumnData:
+    dtype: DataType
+    values: object  # torch.Tensor [n] | [d, n] (VectorUDT) | list (StringType)
+    valid: Optional[torch.Tensor] = None  # bool [n]; None => no nulls
+    meta: dict = field(default_factory=dict)
+
+    @property
+    def n(self) -> int:
+        if isinstance(self.values, list):
+            return len(self.values)
+        return int(self.values.shape[-1])
+
+    def valid_mask(self, device=None) -> torch.Tensor:
+        if self.valid is not None:
+            return self.valid
+        dev = device if device is not None else (self.values.device if torch.is_tensor(self.values) else "cpu")
+        return torch.ones(self.n, dtype=torch.bool, device=dev)
+
+    def has_nulls(self) -> bool:
+        return self.valid is not None and not bool(self.valid.all())
+
+    def index(self, idx: torch.Tensor) -> "ColumnData":
+        """Gather rows ``idx`` (long tensor)."""
+        if isinstance(self.values, list):
+            il = idx.tolist()
+            vals = [self.values[i] for i in il]
+        elif isinstance(self.dtype, VectorUDT):
+            vals = self.values.index_select(1, idx.to(self.values.device))
+        else:
+            vals = self.values.index_select(0, idx.to(self.values.device))
+        valid = None if self.valid is None else self.valid.index_select(0, idx.to(self.valid.device))
+        return ColumnData(self.dtype, vals, valid, dict(self.meta))
+
+    def slice(self, start: int, stop: int) -> "ColumnData":
+        if isinstance(self.values, list):
+            vals = self.values[start:stop]
+        elif isinstance(self.dtype, VectorUDT):
+            vals = self.values[:, start:stop]
+        else:
+            vals = self.values[start:stop]
+        valid = None if self.valid is None else self.valid[start:stop]
+        return ColumnData(self.dtype, vals, valid, dict(self.meta))
+
+    def to_pylist(self) -> list:
+        """Host python values (None for null) — used by show/collect."""
+        if isinstance(self.values, list):
+            vals = list(self.values)
+        elif isinstance(self.dtype, VectorUDT):
+            from ..models.linalg import DenseVector
+
+            arr = self.values.detach().to("cpu", torch.float64).t().contiguous().numpy()
+            vals = [DenseVector(row.copy()) for row in arr]
+        else:
+            t = self.values.detach().cpu()
+            if isinstance(self.dtype, BooleanType):
+                vals = [bool(v) for v in t.tolist()]
+            elif isinstance(self.dtype, (IntegerType, LongType)):
+                vals = [int(v) for v in t.tolist()]
+            else:
+                vals = [float(v) for v in t.to(torch.float64).tolist()]
+        if self.valid is not None:
+            m = self.valid.detach().cpu().tolist()
+            vals = [v if ok else None for v, ok in zip(vals, m)]
+        return vals
+
+
+class Table:
+    def __init__(self, schema: StructType, columns: List[ColumnData], nrows: int,
+                 sel: Optional[torch.Tensor] = None, device=None):
+        assert len(schema.fields) == len(columns), "schema/column count mismatch"
+        self.schema = schema
+        self.columns = columns
+        self.nrows = int(nrows)
+        self.sel = sel
+        self.device = torch.device(device) if device is not None else torch.device("cpu")
+
+    # -- structure -------------------------------------------------------------------------
+    def column(self, name: str) -> ColumnData:
+        idx = self.index_of(name)
+        return self.columns[idx]
+
+    def index_of(self, name: str) -> int:
+        names = self.schema.names
+        if name in names:
+            return names.index(name)
+        low = [n.lower() for n in names]
+        if name.lower() in low:
+            return low.index(name.lower())
+        raise KeyError(name)
+
+    def has_column(self, name: str) -> bool:
+        try:
+            self.index_of(name)
+            return True
+        except KeyError:
+            return False
+
+    # -- selection -------------------------------------------------------------------------
+    def sel_mask(self) -> torch.Tensor:
+        if self.sel is None:
+            return torch.ones(self.nrows, dtype=torch.bool, device=self.device)
+        return self.sel
+
+    def count(self) -> int:
+        if self.sel is None:
+            return self.nrows
+        return int(self.sel.sum().item())
+
+    def compact(self) -> "Table":
+        """Materialize the selection vector (stream compaction)."""
+        if self.sel is None:
+            return self
+        from ..ops import kernels
+
+        idx = kernels.selected_indices(self.sel)
+        cols = [c.index(idx) for c in self.columns]
+        return Table(self.schema, cols, int(idx.numel()), None, self.device)
+
+    def head_rows(self, k: int) -> "Table":
+        """First ``k`` live rows (``take``), compacting only what is needed."""
+        if self.sel is None:
+            k = min(k, self.nrows)
+            return Table(self.schema, [c.slice(0, k) for c in self.columns], k, None, self.device)
+        from ..ops import kernels
+
+        idx = kernels.selected_indices(self.sel, limit=k)
+        return Table(self.schema, [c.index(idx) for c in self.columns], int(idx.numel()), None, self.device)
+
+    def to_rows(self) -> list:
+        t = self.compact()
+        cols = [c.to_pylist() for c in t.columns]
+        return list(zip(*cols)) if cols else [() for _ in range(t.nrows)]
+
+    def with_columns(self, schema: StructType, columns: List[ColumnData]) -> "Table":
+        return Table(schema, columns, self.nrows, self.sel, self.device)
+
+
+def empty_column(dtype: DataType, n: int, device) -> ColumnData:
+    if isinstance(dtype, StringType):
+        return ColumnData(dtype, [None] * n, torch.zeros(n, dtype=torch.bool, device=device))
+    td = dtype.torch_dtype or torch.float64
+    return ColumnData(dtype, torch.zeros(n, dtype=td, device=device), torch.zeros(n, dtype=torch.bool, device=device))
+
+
+def field_for(name: str, data: ColumnData, nullable: bool = True) -> StructField:
+    return StructField(name, data.dtype, nullable, dict(data.meta))
+
+
+_ = (DoubleType, NullType)
