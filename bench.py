@@ -1,0 +1,125 @@
+#!/usr/bin/env python3
+"""Headline benchmark: rows/sec of ``LinearRegression.fit`` on a synthetic 1e8 x 32 dataset
+(BASELINE.json config #2/#3), bf16 normal equations, data-parallel over N MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--rows R] [--features D] [--dtype bf16]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+One step = one full ``LinearRegression.fit`` through the engine on a DataFrame whose
+``features`` column is an assembled (feature-major, bf16) device matrix and ``label`` an f32
+column: fused MFMA Gram pass over the rank's shard -> RCCL all-reduce of the f64 statistics over
+xGMI -> f64 normal-equation solve -> model.  Rows are sharded across ranks (strong scaling: the
+global dataset is fixed at --rows).  Synthetic data, random-init coefficients; nothing is cached
+between steps.  Rank 0 prints one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+
+def _args(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--rows", type=float, default=1e8, help="global rows (strong scaling)")
+    ap.add_argument("--features", type=int, default=32)
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32", "fp64"])
+    ap.add_argument("--scaling", default="strong", choices=["strong", "weak"])
+    ap.add_argument("--json-out", default=None)
+    return ap.parse_args(argv)
+
+
+def main(argv=None):
+    a = _args(argv)
+    import torch
+
+    from net.jgp.labs.sparkdq4ml_amd import LinearRegression, SparkSession
+    from net.jgp.labs.sparkdq4ml_amd.parallel import comm
+
+    comm.init()
+    rank, world = comm.rank(), comm.world_size()
+    if world != a.gpus and rank == 0:
+        print(f"[bench] warning: --gpus {a.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    spark = SparkSession.builder().appName("bench").master("local[*]").getOrCreate()
+    dev = spark.device
+    on_gpu = dev.type == "cuda"
+
+    total = int(a.rows)
+    if not on_gpu:
+        total = min(total, 2_000_000)  # host smoke run
+    per_rank = total // world if a.scaling == "strong" else total
+    lo = rank * per_rank
+    n = per_rank if (a.scaling == "weak" or rank < world - 1) else total - lo
+    d = a.features
+    gen = torch.Generator(device=dev).manual_seed(1234 + rank)
+    store = {"bf16": torch.bfloat16, "fp32": torch.float32, "fp64": torch.float64}[a.dtype]
+    ld = (n + 63) // 64 * 64
+    Xbuf = torch.empty(d, ld, dtype=store, device=dev)
+    beta = torch.linspace(-2.0, 2.0, d, device=dev, dtype=torch.float32)
+    y = torch.zeros(n, dtype=torch.float32, device=dev)
+    chunk = 1 << 24
+    for s in range(0, n, chunk):
+        e = min(n, s + chunk)
+        xc = torch.randn(d, e - s, generator=gen, device=dev, dtype=torch.float32)
+        Xbuf[:, s:e] = xc.to(store)
+        y[s:e] = beta @ xc + 0.5 + 0.1 * torch.randn(e - s, generator=gen, device=dev, dtype=torch.float32)
+    X = Xbuf[:, :n]
+    df = spark.createDataFrame({"features": X, "label": y})
+    lr = LinearRegression(solver="normal", gramDtype=a.dtype)
+
+    def step():
+        return lr.fit(df)
+
+    for _ in range(a.warmup):
+        model = step()
+    if on_gpu:
+        torch.cuda.synchronize()
+    comm.barrier()
+    if on_gpu:
+        torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        model = step()
+    if on_gpu:
+        torch.cuda.synchronize()
+    comm.barrier()
+    if on_gpu:
+        torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    elapsed = float(comm.all_reduce_max(el).item())
+
+    global_rows = total if a.scaling == "strong" else total * world
+    ms = elapsed / a.steps * 1e3
+    value = global_rows * a.steps / elapsed
+    coef = model.coefficients.toArray()
+    err = float(abs(coef - beta.double().cpu().numpy()).max())
+    if rank == 0:
+        line = {
+            "metric": "rows/sec LinearRegression.fit, 1e8x32 synthetic, at 1/2/4/8 MI355X",
+            "value": value, "unit": "rows/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+            "ms_per_step": ms, "higher_is_better": True, "scaling": a.scaling, "vs_baseline": None,
+            "dtype": a.dtype, "data": "synthetic (random-init coefficients, N(0,1) features)",
+            "config": {"model": f"LinearRegression(normal equations) d={d}", "global_batch": global_rows,
+                       "seq_len": d, "parallelism": f"dp{world}", "rows_per_gpu": n,
+                       "device": str(dev), "coef_max_abs_err": err},
+        }
+        s = json.dumps(line)
+        print(s, flush=True)
+        if a.json_out:
+            with open(a.json_out, "w") as f:
+                f.write(s + "\n")
+    comm.shutdown()
+
+
+if __name__ == "__main__":
+    main()

@@ -98,7 +98,7 @@ def build_hip(force: bool = False) -> str:
             cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
                    "-fvisibility=hidden", "-munsafe-fp-atomics", *_py_includes(),
                    f"-I{os.path.join(CSRC, 'hip')}", *srcs,
-                   f"-L{tl}", "-lamdhip64", f"-Wl,-rpath,{tl}", "-o", tmp]
+                   f"-L{tl}", "-lamdhip64", "-lhiprtc", f"-Wl,-rpath,{tl}", "-o", tmp]
             _run(cmd)
             os.replace(tmp, HIP_SO)
     return HIP_SO

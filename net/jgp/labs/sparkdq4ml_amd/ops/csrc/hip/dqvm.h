@@ -1,0 +1,16 @@
+// Fused DQ kernels: runtime code generation of Project/Filter chains (see dqvm.cpp).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+
+namespace dq4ml {
+
+// Compile HIP source (one extern "C" kernel named `entry` with signature
+// (void* const* ptrs, long long n)) for gfx950 with hipRTC; returns an opaque handle.  Compiled
+// code objects are cached by source text for the life of the process.
+int64_t rtc_compile(const std::string& src, const std::string& entry, std::string* log);
+void rtc_launch(int64_t handle, int grid, int block, void* const* ptrs_dev, int64_t n, hipStream_t st);
+
+}  // namespace dq4ml

@@ -1,0 +1,554 @@
+// K5 — WLS sufficient statistics ("Gram") of a feature-major matrix on MFMA.
+//
+// Replaces Spark's per-row ``WeightedLeastSquares.Aggregator.add`` (BLAS.spr of every row into a
+// packed Gram) triggered by LinearRegression.fit at
+// DataQuality4MachineLearningApp.java:126.  One streaming pass over
+//     X  [d, ld]  feature-major (bf16 / f32 / f64),  y [n],  optional w [n] and selection sel [n]
+// produces   count, Σw, Σw², Σwy, Σwy², Σw·x (d), Σw·x·y (d), Σ w·x·xᵀ (upper)   in f64.
+//
+// Tall-skinny design (d <= 64, memory bound: 1e8 x 32 bf16 = 6.4 GB per pass):
+//  * "superstep" = 64 consecutive rows.  Lane l of a wave owns feature f = l & 31 (bf16/f32
+//    modes) and the row half h = l >> 5, and loads ITS 32 rows of ITS feature as contiguous
+//    16-byte vectors — in feature-major storage that is exactly the A/B fragment of
+//    v_mfma_f32_32x32x16_bf16 (A[i=l&31][k=8h+j]) with the K index permuted (allowed: Σ_k is
+//    order-free as long as A and B use the same permutation, and they are the same registers).
+//    No LDS transpose, no shuffles: 4 loads + 4 MFMAs per 32-feature tile per superstep.
+//  * Upper tile pairs only (d <= 32: 1 pair, d <= 64: 3 pairs).
+//  * Column sums and Xᵀy ride on a second MFMA with B = [w_hi, w_lo, wy_hi, wy_lo, 0...]: the
+//    per-row scalars are computed lane = row (coalesced), split hi/lo into bf16 (≈16-bit
+//    mantissa for the label) and handed to the fragment layout through a 512-byte LDS stripe.
+//  * f64 mode (Spark-parity path) uses v_mfma_f64_16x16x4_f64 with 16-feature tiles and exact
+//    f64 side sums on the VALU.
+//  * Per-wave f32 (bf16 mode) / f64 accumulators -> deterministic in-block wave reduction in
+//    LDS -> one f64 partial slab per block -> ``gram_reduce`` sums slabs in a fixed order (no
+//    atomics: bit-reproducible run to run).
+#include <hip/hip_runtime.h>
+
+#include "common.h"
+#include "gram.h"
+
+namespace dq4ml {
+
+namespace {
+
+constexpr int kBlock = 256;  // 4 waves
+constexpr int kWavesPerBlock = kBlock / kWave;
+
+__device__ __forceinline__ double load_as_f64(const void* p, int dt, int64_t i) {
+  switch (dt) {
+    case DT_F64: return reinterpret_cast<const double*>(p)[i];
+    case DT_F32: return (double)reinterpret_cast<const float*>(p)[i];
+    case DT_BF16: return (double)bf16_bits_to_f32(reinterpret_cast<const uint16_t*>(p)[i]);
+    case DT_I32: return (double)reinterpret_cast<const int32_t*>(p)[i];
+    case DT_I64: return (double)reinterpret_cast<const int64_t*>(p)[i];
+    case DT_U8: return (double)reinterpret_cast<const uint8_t*>(p)[i];
+    default: return 0.0;
+  }
+}
+
+// per-row scalars of row r (lane = row): liveness, weight, label
+struct RowVals {
+  bool live;
+  double w, y, wy;
+};
+
+__device__ __forceinline__ RowVals row_vals(const GramArgs& a, int64_t r) {
+  RowVals v{false, 0.0, 0.0, 0.0};
+  if (r < a.n) {
+    bool live = a.sel ? (a.sel[r] != 0) : true;
+    if (live) {
+      double w = a.w ? load_as_f64(a.w, a.wdt, r) : 1.0;
+      double y = load_as_f64(a.y, a.ydt, r);
+      v.live = true;
+      v.w = w;
+      v.y = y;
+      v.wy = w * y;
+    }
+  }
+  return v;
+}
+
+struct RowAcc {
+  double cnt = 0, ws = 0, wws = 0, bs = 0, bbs = 0;
+  __device__ __forceinline__ void add(const RowVals& v) {
+    if (v.live) {
+      cnt += 1.0;
+      ws += v.w;
+      wws += v.w * v.w;
+      bs += v.wy;
+      bbs += v.wy * v.y;
+    }
+  }
+};
+
+// ---- 32 rows of one feature as 4 bf16x8 fragments --------------------------------------------
+template <typename T>
+__device__ __forceinline__ void load_rows32_bf16(const T* p, int64_t rows_left, bf16x8 (&fr)[4]);
+
+template <>
+__device__ __forceinline__ void load_rows32_bf16<uint16_t>(const uint16_t* p, int64_t rows_left, bf16x8 (&fr)[4]) {
+  if (rows_left >= 32) {
+    const u32x4* q = reinterpret_cast<const u32x4*>(p);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      u32x4 u = __builtin_nontemporal_load(q + i);
+      fr[i] = __builtin_bit_cast(bf16x8, u);
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int e = 8 * i + j;
+        uint16_t b = e < rows_left ? p[e] : uint16_t(0);
+        fr[i][j] = __builtin_bit_cast(__bf16, b);
+      }
+    }
+  }
+}
+
+template <>
+__device__ __forceinline__ void load_rows32_bf16<float>(const float* p, int64_t rows_left, bf16x8 (&fr)[4]) {
+  if (rows_left >= 32) {
+    const f32x4* q = reinterpret_cast<const f32x4*>(p);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      f32x4 a = __builtin_nontemporal_load(q + 2 * i);
+      f32x4 b = __builtin_nontemporal_load(q + 2 * i + 1);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        fr[i][j] = (__bf16)a[j];
+        fr[i][4 + j] = (__bf16)b[j];
+      }
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int e = 8 * i + j;
+        fr[i][j] = (__bf16)(e < rows_left ? p[e] : 0.0f);
+      }
+  }
+}
+
+template <>
+__device__ __forceinline__ void load_rows32_bf16<double>(const double* p, int64_t rows_left, bf16x8 (&fr)[4]) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int e = 8 * i + j;
+      fr[i][j] = (__bf16)(float)(e < rows_left ? p[e] : 0.0);
+    }
+}
+
+// zero the elements of dead rows (binary mask): bits = liveness of the lane's 32 rows
+__device__ __forceinline__ void mask_frags(bf16x8 (&fr)[4], uint32_t bits) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (!((bits >> (8 * i + j)) & 1u)) fr[i][j] = (__bf16)0.0f;
+}
+
+__device__ __forceinline__ void weight_frags(bf16x8 (&fr)[4], const float* wl /* lane's 32 row weights in LDS */) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) fr[i][j] = (__bf16)((float)fr[i][j] * wl[8 * i + j]);
+}
+
+// =============================================================================================
+// bf16 MFMA kernel
+// =============================================================================================
+template <typename TX, int NT, int XMODE>
+__global__ __launch_bounds__(kBlock) void gram_tall_bf16_kernel(GramArgs a) {
+  constexpr int NPAIR = NT * (NT + 1) / 2;
+  // LDS: per wave 4 cols x 64 rows bf16 (W fragments) + 64 f32 row weights; reused for the
+  // block reduction afterwards.
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int f = lane & 31, h = lane >> 5;
+  __bf16* wl = reinterpret_cast<__bf16*>(smem) + wave * (4 * 64);
+  float* wrow = reinterpret_cast<float*>(smem + kWavesPerBlock * 4 * 64 * 2) + wave * 64;
+
+  f32x16 acc[NPAIR];
+  f32x16 accw[NT];
+#pragma unroll
+  for (int p = 0; p < NPAIR; ++p) acc[p] = f32x16{};
+#pragma unroll
+  for (int t = 0; t < NT; ++t) accw[t] = f32x16{};
+  RowAcc ra;
+
+  const TX* X = reinterpret_cast<const TX*>(a.X);
+  const TX* fp[NT];
+  bool fvalid[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int feat = t * 32 + f;
+    fvalid[t] = feat < a.d;
+    fp[t] = X + (int64_t)(fvalid[t] ? feat : 0) * a.ld + 32 * h;
+  }
+
+  const int64_t gw = (int64_t)blockIdx.x * kWavesPerBlock + wave;
+  const int64_t total_waves = (int64_t)gridDim.x * kWavesPerBlock;
+  int64_t s0 = gw * a.spw;
+  int64_t s1 = s0 + a.spw;
+  if (s1 > a.nsuper) s1 = a.nsuper;
+  const bool do_tail = (gw == total_waves - 1) && (a.n > a.nsuper * 64);
+  const int64_t s_end = do_tail ? a.nsuper + 1 : s1;
+  if (do_tail && s0 > a.nsuper) s0 = a.nsuper;
+
+  for (int64_t s = s0; s < s_end; ++s) {
+    const int64_t r0 = s * 64;
+    // 1) per-row scalars, lane = row
+    RowVals rv = row_vals(a, r0 + lane);
+    ra.add(rv);
+    {
+      const float w_hi = (float)(__bf16)(float)rv.w;
+      const __bf16 wy_hi = (__bf16)(float)rv.wy;
+      wl[0 * 64 + lane] = (__bf16)(float)rv.w;
+      wl[1 * 64 + lane] = (__bf16)(float)(rv.w - (double)w_hi);
+      wl[2 * 64 + lane] = wy_hi;
+      wl[3 * 64 + lane] = (__bf16)(float)(rv.wy - (double)(float)wy_hi);
+      if (XMODE == 2) wrow[lane] = (float)rv.w;
+    }
+    const uint64_t live_bits = __ballot(rv.live);
+    // 2) features
+    const int64_t rows_left = a.n - (r0 + 32 * h);
+    bf16x8 fr[NT][4];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      if (fvalid[t]) {
+        load_rows32_bf16<TX>(fp[t] + r0, rows_left, fr[t]);
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) fr[t][i] = bf16x8{};
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    // 3) W fragments (lanes f < 4 read their column; everyone else multiplies zeros)
+    bf16x8 wf[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) wf[i] = bf16x8{};
+    if (f < 4) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) wf[i] = *reinterpret_cast<const bf16x8*>(wl + f * 64 + 32 * h + 8 * i);
+    }
+    // 4) masking / weighting of one operand of XᵀX
+    bf16x8 frw[NT][4];
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) frw[t][i] = fr[t][i];
+    if (XMODE == 1) {
+      const uint32_t bits = (uint32_t)(live_bits >> (32 * h));
+#pragma unroll
+      for (int t = 0; t < NT; ++t) mask_frags(frw[t], bits);
+    } else if (XMODE == 2) {
+#pragma unroll
+      for (int t = 0; t < NT; ++t) weight_frags(frw[t], wrow + 32 * h);
+    }
+    // 5) MFMAs
+    int p = 0;
+#pragma unroll
+    for (int I = 0; I < NT; ++I)
+#pragma unroll
+      for (int J = I; J < NT; ++J, ++p)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[p] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fr[I][i], frw[J][i], acc[p], 0, 0, 0);
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) accw[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fr[t][i], wf[i], accw[t], 0, 0, 0);
+    __builtin_amdgcn_wave_barrier();
+  }
+
+  // ---- block reduction (deterministic: waves add in order) ---------------------------------
+  const int d = a.d;
+  const int P = a.P;
+  __syncthreads();
+  double* red = reinterpret_cast<double*>(smem);
+  for (int i = threadIdx.x; i < P; i += kBlock) red[i] = 0.0;
+  // scalars: wave reduce first
+  double sc[5] = {ra.cnt, ra.ws, ra.wws, ra.bs, ra.bbs};
+#pragma unroll
+  for (int k = 0; k < 5; ++k) sc[k] = wave_sum_f64(sc[k]);
+  __syncthreads();
+  for (int wv = 0; wv < kWavesPerBlock; ++wv) {
+    if (wave == wv) {
+      if (lane == 0) {
+#pragma unroll
+        for (int k = 0; k < 5; ++k) red[k] += sc[k];
+      }
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        // accw[t]: rows = features t*32 + row, cols 0..3 = [w_hi, w_lo, wy_hi, wy_lo]
+        const int col = mfma32_col(lane);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float v = accw[t][r];
+          const float vn = __shfl_down(v, 1, 64);  // col+1 (same row)
+          const int feat = t * 32 + mfma32_row(lane, r);
+          if (feat < d) {
+            if (col == 0) red[5 + feat] += (double)v + (double)vn;
+            if (col == 2) red[5 + d + feat] += (double)v + (double)vn;
+          }
+        }
+      }
+      int p = 0;
+#pragma unroll
+      for (int I = 0; I < NT; ++I)
+#pragma unroll
+        for (int J = I; J < NT; ++J, ++p) {
+          double* tile = red + 5 + 2 * d + p * 1024;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) tile[mfma32_row(lane, r) * 32 + mfma32_col(lane)] += (double)acc[p][r];
+        }
+    }
+    __syncthreads();
+  }
+  double* out = a.partials + (int64_t)blockIdx.x * P;
+  for (int i = threadIdx.x; i < P; i += kBlock) out[i] = red[i];
+}
+
+// =============================================================================================
+// f64 MFMA kernel (v_mfma_f64_16x16x4_f64): Spark-parity precision
+// =============================================================================================
+template <typename TX, int NT>
+__global__ __launch_bounds__(kBlock) void gram_tall_f64_kernel(GramArgs a) {
+  constexpr int NPAIR = NT * (NT + 1) / 2;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int f = lane & 15, q = lane >> 4;
+  double* lw = reinterpret_cast<double*>(smem) + wave * 128;  // [w(64), wy(64)]
+
+  f64x4 acc[NPAIR];
+#pragma unroll
+  for (int p = 0; p < NPAIR; ++p) acc[p] = f64x4{};
+  double cs[NT], ab[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) cs[t] = ab[t] = 0.0;
+  RowAcc ra;
+
+  const TX* X = reinterpret_cast<const TX*>(a.X);
+  const TX* fp[NT];
+  bool fvalid[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int feat = t * 16 + f;
+    fvalid[t] = feat < a.d;
+    fp[t] = X + (int64_t)(fvalid[t] ? feat : 0) * a.ld + 16 * q;
+  }
+  const bool weighted = (a.sel != nullptr) || (a.w != nullptr);
+
+  const int64_t gw = (int64_t)blockIdx.x * kWavesPerBlock + wave;
+  const int64_t total_waves = (int64_t)gridDim.x * kWavesPerBlock;
+  int64_t s0 = gw * a.spw;
+  int64_t s1 = s0 + a.spw;
+  if (s1 > a.nsuper) s1 = a.nsuper;
+  const bool do_tail = (gw == total_waves - 1) && (a.n > a.nsuper * 64);
+  const int64_t s_end = do_tail ? a.nsuper + 1 : s1;
+  if (do_tail && s0 > a.nsuper) s0 = a.nsuper;
+
+  for (int64_t s = s0; s < s_end; ++s) {
+    const int64_t r0 = s * 64;
+    RowVals rv = row_vals(a, r0 + lane);
+    ra.add(rv);
+    lw[lane] = rv.live ? rv.w : 0.0;
+    lw[64 + lane] = rv.live ? rv.wy : 0.0;
+    __builtin_amdgcn_wave_barrier();
+    const int64_t rows_left = a.n - (r0 + 16 * q);
+    double wv[16], wyv[16];
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      wv[e] = lw[16 * q + e];
+      wyv[e] = lw[64 + 16 * q + e];
+    }
+    double x[NT][16];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        double v = 0.0;
+        if (fvalid[t] && e < rows_left) v = (double)fp[t][r0 + e];
+        x[t][e] = v;
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        cs[t] += x[t][e] * wv[e];
+        ab[t] += x[t][e] * wyv[e];
+      }
+    int p = 0;
+#pragma unroll
+    for (int I = 0; I < NT; ++I)
+#pragma unroll
+      for (int J = I; J < NT; ++J, ++p)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const double b = weighted ? x[J][e] * wv[e] : x[J][e];
+          acc[p] = __builtin_amdgcn_mfma_f64_16x16x4f64(x[I][e], b, acc[p], 0, 0, 0);
+        }
+    __builtin_amdgcn_wave_barrier();
+  }
+
+  const int d = a.d;
+  const int P = a.P;
+  __syncthreads();
+  double* red = reinterpret_cast<double*>(smem);
+  for (int i = threadIdx.x; i < P; i += kBlock) red[i] = 0.0;
+  double sc[5] = {ra.cnt, ra.ws, ra.wws, ra.bs, ra.bbs};
+#pragma unroll
+  for (int k = 0; k < 5; ++k) sc[k] = wave_sum_f64(sc[k]);
+  // combine the 4 row-groups q of each feature
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    cs[t] += __shfl_xor(cs[t], 16, 64);
+    cs[t] += __shfl_xor(cs[t], 32, 64);
+    ab[t] += __shfl_xor(ab[t], 16, 64);
+    ab[t] += __shfl_xor(ab[t], 32, 64);
+  }
+  __syncthreads();
+  for (int wvi = 0; wvi < kWavesPerBlock; ++wvi) {
+    if (wave == wvi) {
+      if (lane == 0) {
+#pragma unroll
+        for (int k = 0; k < 5; ++k) red[k] += sc[k];
+      }
+      if (q == 0) {
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+          const int feat = t * 16 + f;
+          if (feat < d) {
+            red[5 + feat] += cs[t];
+            red[5 + d + feat] += ab[t];
+          }
+        }
+      }
+      int p = 0;
+#pragma unroll
+      for (int I = 0; I < NT; ++I)
+#pragma unroll
+        for (int J = I; J < NT; ++J, ++p) {
+          double* tile = red + 5 + 2 * d + p * 256;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) tile[mfma16d_row(lane, r) * 16 + mfma16d_col(lane)] += acc[p][r];
+        }
+    }
+    __syncthreads();
+  }
+  double* out = a.partials + (int64_t)blockIdx.x * P;
+  for (int i = threadIdx.x; i < P; i += kBlock) out[i] = red[i];
+}
+
+// =============================================================================================
+// slab reduction -> packed-upper flat layout
+// =============================================================================================
+__global__ __launch_bounds__(256) void gram_reduce_kernel(const double* __restrict__ partials, int nslab, int P,
+                                                         int d, int T, int NT, double* __restrict__ out) {
+  const int64_t K = 5 + 2 * (int64_t)d + (int64_t)d * (d + 1) / 2;
+  for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < K; k += (int64_t)gridDim.x * blockDim.x) {
+    int64_t src;
+    if (k < 5 + 2 * d) {
+      src = k;
+    } else {
+      const int64_t kk = k - (5 + 2 * d);
+      int64_t j = (int64_t)((sqrt(8.0 * (double)kk + 1.0) - 1.0) * 0.5);
+      while (j * (j + 1) / 2 > kk) --j;
+      while ((j + 1) * (j + 2) / 2 <= kk) ++j;
+      const int64_t i = kk - j * (j + 1) / 2;  // i <= j
+      const int64_t I = i / T, J = j / T;
+      const int64_t p = I * NT - I * (I - 1) / 2 + (J - I);
+      src = 5 + 2 * (int64_t)d + p * T * T + (i % T) * T + (j % T);
+    }
+    double s = 0.0;
+    for (int b = 0; b < nslab; ++b) s += partials[(int64_t)b * P + src];
+    out[k] = s;
+  }
+}
+
+}  // namespace
+
+int64_t gram_partial_stride(int mode, int d) {
+  if (mode == GRAM_F64) {
+    const int NT = (d + 15) / 16;
+    return 5 + 2 * (int64_t)d + (int64_t)NT * (NT + 1) / 2 * 256;
+  }
+  const int NT = (d + 31) / 32;
+  return 5 + 2 * (int64_t)d + (int64_t)NT * (NT + 1) / 2 * 1024;
+}
+
+int gram_default_blocks(int64_t n) {
+  const int64_t nsuper = (n + 63) / 64;
+  // aim: >= 16 waves per CU on 256 CUs, but >= 8 supersteps per wave
+  int64_t blocks = (nsuper + 8 * kWavesPerBlock - 1) / (8 * kWavesPerBlock);
+  if (blocks > 1024) blocks = 1024;
+  if (blocks < 1) blocks = 1;
+  return (int)blocks;
+}
+
+template <typename TX, int NT>
+static void launch_bf16_nt(GramArgs& a, int xmode, int blocks, size_t lds, hipStream_t st) {
+  if (xmode == 0) hipLaunchKernelGGL((gram_tall_bf16_kernel<TX, NT, 0>), dim3(blocks), dim3(kBlock), lds, st, a);
+  else if (xmode == 1) hipLaunchKernelGGL((gram_tall_bf16_kernel<TX, NT, 1>), dim3(blocks), dim3(kBlock), lds, st, a);
+  else hipLaunchKernelGGL((gram_tall_bf16_kernel<TX, NT, 2>), dim3(blocks), dim3(kBlock), lds, st, a);
+}
+
+template <typename TX>
+static void launch_f64_x(GramArgs& a, int NT, int blocks, size_t lds, hipStream_t st) {
+  switch (NT) {
+    case 1: hipLaunchKernelGGL((gram_tall_f64_kernel<TX, 1>), dim3(blocks), dim3(kBlock), lds, st, a); break;
+    case 2: hipLaunchKernelGGL((gram_tall_f64_kernel<TX, 2>), dim3(blocks), dim3(kBlock), lds, st, a); break;
+    case 3: hipLaunchKernelGGL((gram_tall_f64_kernel<TX, 3>), dim3(blocks), dim3(kBlock), lds, st, a); break;
+    default: hipLaunchKernelGGL((gram_tall_f64_kernel<TX, 4>), dim3(blocks), dim3(kBlock), lds, st, a); break;
+  }
+}
+
+void gram_tall(int mode, GramArgs a, int xmode, int blocks, double* out, hipStream_t st) {
+  if (a.d < 1 || a.d > 64) throw std::invalid_argument("gram_tall: d must be in [1, 64]");
+  a.nsuper = a.n / 64;
+  const int64_t total_waves = (int64_t)blocks * kWavesPerBlock;
+  a.spw = (a.nsuper + total_waves - 1) / total_waves;
+  if (a.spw < 1) a.spw = 1;
+  a.P = (int)gram_partial_stride(mode, a.d);
+  const size_t red_bytes = (size_t)a.P * sizeof(double);
+  if (mode == GRAM_BF16) {
+    const int NT = (a.d + 31) / 32;
+    size_t lds = kWavesPerBlock * (4 * 64 * 2 + 64 * 4);
+    if (red_bytes > lds) lds = red_bytes;
+    if (a.xdt == DT_BF16) {
+      if (NT == 1) launch_bf16_nt<uint16_t, 1>(a, xmode, blocks, lds, st);
+      else launch_bf16_nt<uint16_t, 2>(a, xmode, blocks, lds, st);
+    } else if (a.xdt == DT_F32) {
+      if (NT == 1) launch_bf16_nt<float, 1>(a, xmode, blocks, lds, st);
+      else launch_bf16_nt<float, 2>(a, xmode, blocks, lds, st);
+    } else if (a.xdt == DT_F64) {
+      if (NT == 1) launch_bf16_nt<double, 1>(a, xmode, blocks, lds, st);
+      else launch_bf16_nt<double, 2>(a, xmode, blocks, lds, st);
+    } else {
+      throw std::invalid_argument("gram_tall: unsupported feature dtype");
+    }
+    DQ_HIP_CHECK(hipGetLastError());
+    hipLaunchKernelGGL(gram_reduce_kernel, dim3(8), dim3(256), 0, st, a.partials, blocks, a.P, a.d, 32, NT, out);
+  } else if (mode == GRAM_F64) {
+    const int NT = (a.d + 15) / 16;
+    size_t lds = kWavesPerBlock * 128 * sizeof(double);
+    if (red_bytes > lds) lds = red_bytes;
+    if (a.xdt == DT_F64) launch_f64_x<double>(a, NT, blocks, lds, st);
+    else if (a.xdt == DT_F32) launch_f64_x<float>(a, NT, blocks, lds, st);
+    else throw std::invalid_argument("gram_tall(f64): unsupported feature dtype");
+    DQ_HIP_CHECK(hipGetLastError());
+    hipLaunchKernelGGL(gram_reduce_kernel, dim3(8), dim3(256), 0, st, a.partials, blocks, a.P, a.d, 16, NT, out);
+  } else {
+    throw std::invalid_argument("gram_tall: unsupported mode");
+  }
+  DQ_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace dq4ml

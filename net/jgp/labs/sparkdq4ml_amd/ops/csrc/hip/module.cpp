@@ -1,0 +1,106 @@
+// pybind11 bindings of the gfx950 kernel module (_dq4ml_hip).  Every entry point takes raw device
+// pointers (ints) plus the HIP stream handle of the calling torch stream; buffers are allocated by
+// the python side (ops/device.py) from torch's caching allocator, so there is no hipMalloc in any
+// launch path (graph-capturable) and kernels run on the same stream as the surrounding torch work.
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include "common.h"
+#include "dqvm.h"
+#include "gram.h"
+#include "gram_wide.h"
+#include "rowops.h"
+
+namespace py = pybind11;
+using namespace dq4ml;
+
+template <typename T>
+static T* P(uintptr_t p) {
+  return reinterpret_cast<T*>(p);
+}
+
+PYBIND11_MODULE(_dq4ml_hip, m) {
+  m.doc() = "dq4ml gfx950 kernels: MFMA Gram, fused DQ VM, compaction, pack, predict/metrics, CSV scan";
+
+  m.def("device_info", []() {
+    int dev = 0;
+    DQ_HIP_CHECK(hipGetDevice(&dev));
+    hipDeviceProp_t p;
+    DQ_HIP_CHECK(hipGetDeviceProperties(&p, dev));
+    py::dict d;
+    d["name"] = std::string(p.name);
+    d["gcnArchName"] = std::string(p.gcnArchName);
+    d["multiProcessorCount"] = p.multiProcessorCount;
+    d["totalGlobalMem"] = (uint64_t)p.totalGlobalMem;
+    d["sharedMemPerBlock"] = (uint64_t)p.sharedMemPerBlock;
+    return d;
+  });
+
+  // ---- Gram (K5) ---------------------------------------------------------------------------
+  m.def("gram_partial_stride", &gram_partial_stride);
+  m.def("gram_default_blocks", &gram_default_blocks);
+  m.def("gram_tall",
+        [](int mode, uintptr_t X, int64_t ld, int d, int64_t n, int xdt, uintptr_t y, int ydt, uintptr_t w, int wdt,
+           uintptr_t sel, int xmode, uintptr_t partials, int blocks, uintptr_t out, uintptr_t stream) {
+          GramArgs a{};
+          a.X = P<const void>(X);
+          a.ld = ld;
+          a.d = d;
+          a.n = n;
+          a.xdt = xdt;
+          a.y = P<const void>(y);
+          a.ydt = ydt;
+          a.w = P<const void>(w);
+          a.wdt = wdt;
+          a.sel = P<const uint8_t>(sel);
+          a.partials = P<double>(partials);
+          gram_tall(mode, a, xmode, blocks, P<double>(out), as_stream(stream));
+        });
+  m.def("gram_wide_workspace", &gram_wide_workspace);
+  m.def("gram_wide",
+        [](int mode, uintptr_t X, int64_t ld, int d, int64_t n, int xdt, uintptr_t scales, uintptr_t ws,
+           int64_t ws_bytes, uintptr_t out, uintptr_t stream) {
+          gram_wide(mode, P<const void>(X), ld, d, n, xdt, P<const float>(scales), P<void>(ws), ws_bytes,
+                    P<double>(out), as_stream(stream));
+        });
+
+  // ---- compaction (K3) -----------------------------------------------------------------------
+  m.def("compact_blocks", &compact_blocks);
+  m.def("compact_count_scan", [](uintptr_t sel, int64_t n, uintptr_t counts, uintptr_t stream) {
+    compact_count_scan(P<const uint8_t>(sel), n, P<int64_t>(counts), as_stream(stream));
+  });
+  m.def("compact_write", [](uintptr_t sel, int64_t n, uintptr_t offsets, int64_t limit, uintptr_t out,
+                            uintptr_t stream) {
+    compact_write(P<const uint8_t>(sel), n, P<const int64_t>(offsets), limit, P<int64_t>(out), as_stream(stream));
+  });
+
+  // ---- pack (K4) -----------------------------------------------------------------------------
+  m.def("pack_columns", [](uintptr_t srcs_dev, int d, int64_t n, uintptr_t out, int odt, int64_t ld, uintptr_t sel,
+                           uintptr_t stream) {
+    pack_columns(P<const PackSrc>(srcs_dev), d, n, P<void>(out), odt, ld, P<const uint8_t>(sel), as_stream(stream));
+  });
+  m.def("pack_src_bytes", []() { return (int)sizeof(PackSrc); });
+
+  // ---- predict / metrics (K7/K8) ---------------------------------------------------------------
+  m.def("predict", [](uintptr_t X, int xdt, int64_t ld, int d, int64_t n, uintptr_t coef, double b, uintptr_t out,
+                      uintptr_t stream) {
+    predict(P<const void>(X), xdt, ld, d, n, P<const double>(coef), b, P<double>(out), as_stream(stream));
+  });
+  m.def("metrics_blocks", &metrics_blocks);
+  m.def("regression_metrics",
+        [](uintptr_t X, int xdt, int64_t ld, int d, int64_t n, uintptr_t y, int ydt, uintptr_t sel, uintptr_t coef,
+           double b, double shift, uintptr_t partials, uintptr_t out, uintptr_t stream) {
+          regression_metrics(P<const void>(X), xdt, ld, d, n, P<const void>(y), ydt, P<const uint8_t>(sel),
+                             P<const double>(coef), b, shift, P<double>(partials), P<double>(out), as_stream(stream));
+        });
+
+  // ---- fused DQ chains: hipRTC whole-stage codegen ----------------------------------------------
+  m.def("rtc_compile", [](const std::string& src, const std::string& entry) {
+    std::string log;
+    int64_t h = rtc_compile(src, entry, &log);
+    return py::make_tuple(h, log);
+  });
+  m.def("rtc_launch", [](int64_t handle, int grid, int block, uintptr_t ptrs_dev, int64_t n, uintptr_t stream) {
+    rtc_launch(handle, grid, block, P<void* const>(ptrs_dev), n, as_stream(stream));
+  });
+}

@@ -1,0 +1,31 @@
+// Row-wise kernels (see rowops.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace dq4ml {
+
+struct PackSrc {
+  const void* ptr;
+  int dt;
+  int pad;
+};
+
+int64_t compact_blocks(int64_t n);
+// counts must hold compact_blocks(n) + 1 int64: exclusive offsets + total at [nb]
+void compact_count_scan(const uint8_t* sel, int64_t n, int64_t* counts, hipStream_t st);
+void compact_write(const uint8_t* sel, int64_t n, const int64_t* offsets, int64_t limit, int64_t* out,
+                   hipStream_t st);
+
+void pack_columns(const PackSrc* srcs_dev, int d, int64_t n, void* out, int odt, int64_t ld, const uint8_t* sel,
+                  hipStream_t st);
+
+void predict(const void* X, int xdt, int64_t ld, int d, int64_t n, const double* coef, double b, double* out,
+             hipStream_t st);
+int metrics_blocks(int64_t n);
+void regression_metrics(const void* X, int xdt, int64_t ld, int d, int64_t n, const void* y, int ydt,
+                        const uint8_t* sel, const double* coef, double b, double shift, double* partials,
+                        double* out, hipStream_t st);
+
+}  // namespace dq4ml

@@ -1,0 +1,244 @@
+// Row-wise kernels: K3 stream compaction of a selection vector, K4 column pack (VectorAssembler),
+// K7 predict and K8 fused predict + regression metrics.
+//
+//  * compact: Spark materializes filtered rows through ``take``/collect (show(n) = take(n+1),
+//    SURVEY.md S05).  Two passes: per-block live counts (wave ballot + popcount), one-block
+//    exclusive scan, then each block writes its indices at its offset — order preserving.
+//  * pack: VectorAssembler.transform (DataQuality4MachineLearningApp.java:110-113) — each input
+//    column becomes one contiguous row of the feature-major [d, ld] output, cast to the output
+//    dtype; dead rows (selection false) can be written as zeros so the Gram kernel needs no mask.
+//  * predict / metrics: LinearRegressionModel.transform (:129) and the RegressionMetrics summary
+//    (:138-139) in ONE pass: ŷ = x·coef + b is never materialized for the metrics, and the 8
+//    moments are reduced per block in f64 (shifted by the label mean for a stable SStot).
+#include <hip/hip_runtime.h>
+
+#include "common.h"
+#include "rowops.h"
+
+namespace dq4ml {
+
+namespace {
+
+__device__ __forceinline__ double ld_f64(const void* p, int dt, int64_t i) {
+  switch (dt) {
+    case DT_F64: return reinterpret_cast<const double*>(p)[i];
+    case DT_F32: return (double)reinterpret_cast<const float*>(p)[i];
+    case DT_BF16: return (double)bf16_bits_to_f32(reinterpret_cast<const uint16_t*>(p)[i]);
+    case DT_I32: return (double)reinterpret_cast<const int32_t*>(p)[i];
+    case DT_I64: return (double)reinterpret_cast<const int64_t*>(p)[i];
+    case DT_U8: return (double)reinterpret_cast<const uint8_t*>(p)[i];
+    default: return 0.0;
+  }
+}
+
+__device__ __forceinline__ void st_from_f64(void* p, int dt, int64_t i, double v) {
+  switch (dt) {
+    case DT_F64: reinterpret_cast<double*>(p)[i] = v; break;
+    case DT_F32: reinterpret_cast<float*>(p)[i] = (float)v; break;
+    case DT_BF16: reinterpret_cast<__bf16*>(p)[i] = (__bf16)(float)v; break;
+    case DT_I32: reinterpret_cast<int32_t*>(p)[i] = (int32_t)v; break;
+    case DT_I64: reinterpret_cast<int64_t*>(p)[i] = (int64_t)v; break;
+    default: break;
+  }
+}
+
+constexpr int kCompactChunk = 4096;  // rows per block (256 threads x 16)
+
+__global__ __launch_bounds__(256) void compact_count_kernel(const uint8_t* __restrict__ sel, int64_t n,
+                                                           int64_t* __restrict__ counts) {
+  __shared__ int64_t wsum[4];
+  const int64_t base = (int64_t)blockIdx.x * kCompactChunk;
+  int64_t c = 0;
+  for (int k = 0; k < kCompactChunk / 256; ++k) {
+    const int64_t r = base + k * 256 + threadIdx.x;
+    const bool live = r < n && sel[r] != 0;
+    const uint64_t b = __ballot(live);
+    c += __popcll(b);
+  }
+  if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) counts[blockIdx.x] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+}
+
+// exclusive scan in place + total at counts[nb]; single block
+__global__ __launch_bounds__(1024) void compact_scan_kernel(int64_t* __restrict__ counts, int64_t nb) {
+  __shared__ int64_t part[1024];
+  const int64_t per = (nb + 1023) / 1024;
+  const int64_t b0 = threadIdx.x * per, b1 = min(nb, b0 + per);
+  int64_t s = 0;
+  for (int64_t b = b0; b < b1; ++b) s += counts[b];
+  part[threadIdx.x] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int64_t run = 0;
+    for (int i = 0; i < 1024; ++i) {
+      const int64_t v = part[i];
+      part[i] = run;
+      run += v;
+    }
+    counts[nb] = run;
+  }
+  __syncthreads();
+  int64_t run = part[threadIdx.x];
+  for (int64_t b = b0; b < b1; ++b) {
+    const int64_t v = counts[b];
+    counts[b] = run;
+    run += v;
+  }
+}
+
+__global__ __launch_bounds__(256) void compact_write_kernel(const uint8_t* __restrict__ sel, int64_t n,
+                                                           const int64_t* __restrict__ offsets, int64_t limit,
+                                                           int64_t* __restrict__ out) {
+  __shared__ int64_t woff[4];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t base = (int64_t)blockIdx.x * kCompactChunk;
+  int64_t off = offsets[blockIdx.x];
+  if (off >= limit) return;  // uniform per block
+  for (int k = 0; k < kCompactChunk / 256; ++k) {
+    const int64_t r = base + k * 256 + threadIdx.x;
+    const bool live = r < n && sel[r] != 0;
+    const uint64_t b = __ballot(live);
+    if (lane == 0) woff[wave] = __popcll(b);
+    __syncthreads();
+    int64_t before = 0;
+    for (int w = 0; w < wave; ++w) before += woff[w];
+    const int64_t total = woff[0] + woff[1] + woff[2] + woff[3];
+    const int64_t pos = off + before + __popcll(b & ((1ull << lane) - 1ull));
+    if (live && pos < limit) out[pos] = r;
+    off += total;
+    __syncthreads();
+  }
+}
+
+// ---- pack --------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void pack_kernel(const PackSrc* __restrict__ srcs, int d, int64_t n,
+                                                  void* __restrict__ out, int odt, int64_t ld,
+                                                  const uint8_t* __restrict__ sel) {
+  const int f = blockIdx.y;
+  if (f >= d) return;
+  const PackSrc s = srcs[f];
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < ld; r += (int64_t)gridDim.x * blockDim.x) {
+    double v = 0.0;
+    if (r < n && (sel == nullptr || sel[r] != 0)) v = ld_f64(s.ptr, s.dt, r);
+    st_from_f64(out, odt, (int64_t)f * ld + r, v);
+  }
+}
+
+// ---- predict / metrics -----------------------------------------------------------------------
+__device__ __forceinline__ double predict_row(const void* X, int xdt, int64_t ld, int d, const double* coef,
+                                              double b, int64_t r) {
+  double acc = b;
+  for (int f = 0; f < d; ++f) acc += coef[f] * ld_f64(X, xdt, (int64_t)f * ld + r);
+  return acc;
+}
+
+__global__ __launch_bounds__(256) void predict_kernel(const void* __restrict__ X, int xdt, int64_t ld, int d,
+                                                     int64_t n, const double* __restrict__ coef, double b,
+                                                     double* __restrict__ out) {
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x)
+    out[r] = predict_row(X, xdt, ld, d, coef, b, r);
+}
+
+__global__ __launch_bounds__(256) void metrics_kernel(const void* __restrict__ X, int xdt, int64_t ld, int d,
+                                                     int64_t n, const void* __restrict__ y, int ydt,
+                                                     const uint8_t* __restrict__ sel,
+                                                     const double* __restrict__ coef, double b, double shift,
+                                                     double* __restrict__ partials) {
+  double m[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
+    if (sel != nullptr && sel[r] == 0) continue;
+    const double p = predict_row(X, xdt, ld, d, coef, b, r);
+    const double yy = ld_f64(y, ydt, r);
+    const double ys = yy - shift, ps = p - shift, res = yy - p;
+    m[0] += 1.0;
+    m[1] += ys;
+    m[2] += ys * ys;
+    m[3] += res;
+    m[4] += res * res;
+    m[5] += fabs(res);
+    m[6] += ps;
+    m[7] += ps * ps;
+  }
+  __shared__ double red[4][8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) m[k] = wave_sum_f64(m[k]);
+  if ((threadIdx.x & 63) == 0) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) red[threadIdx.x >> 6][k] = m[k];
+  }
+  __syncthreads();
+  if (threadIdx.x < 8) {
+    partials[(int64_t)blockIdx.x * 8 + threadIdx.x] =
+        red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+  }
+}
+
+__global__ __launch_bounds__(64) void sum_slabs_kernel(const double* __restrict__ partials, int nslab, int width,
+                                                      double* __restrict__ out) {
+  for (int k = threadIdx.x; k < width; k += blockDim.x) {
+    double s = 0.0;
+    for (int b = 0; b < nslab; ++b) s += partials[(int64_t)b * width + k];
+    out[k] = s;
+  }
+}
+
+}  // namespace
+
+int64_t compact_blocks(int64_t n) { return (n + kCompactChunk - 1) / kCompactChunk; }
+
+void compact_count_scan(const uint8_t* sel, int64_t n, int64_t* counts, hipStream_t st) {
+  const int64_t nb = compact_blocks(n);
+  if (nb == 0) {
+    DQ_HIP_CHECK(hipMemsetAsync(counts, 0, sizeof(int64_t), st));
+    return;
+  }
+  hipLaunchKernelGGL(compact_count_kernel, dim3(nb), dim3(256), 0, st, sel, n, counts);
+  hipLaunchKernelGGL(compact_scan_kernel, dim3(1), dim3(1024), 0, st, counts, nb);
+  DQ_HIP_CHECK(hipGetLastError());
+}
+
+void compact_write(const uint8_t* sel, int64_t n, const int64_t* offsets, int64_t limit, int64_t* out,
+                   hipStream_t st) {
+  const int64_t nb = compact_blocks(n);
+  if (nb == 0 || limit <= 0) return;
+  hipLaunchKernelGGL(compact_write_kernel, dim3(nb), dim3(256), 0, st, sel, n, offsets, limit, out);
+  DQ_HIP_CHECK(hipGetLastError());
+}
+
+void pack_columns(const PackSrc* srcs_dev, int d, int64_t n, void* out, int odt, int64_t ld, const uint8_t* sel,
+                  hipStream_t st) {
+  if (d <= 0 || ld <= 0) return;
+  int64_t gx = (ld + 255) / 256;
+  if (gx > 2048) gx = 2048;
+  hipLaunchKernelGGL(pack_kernel, dim3(gx, d), dim3(256), 0, st, srcs_dev, d, n, out, odt, ld, sel);
+  DQ_HIP_CHECK(hipGetLastError());
+}
+
+void predict(const void* X, int xdt, int64_t ld, int d, int64_t n, const double* coef, double b, double* out,
+             hipStream_t st) {
+  if (n <= 0) return;
+  int64_t g = (n + 255) / 256;
+  if (g > 4096) g = 4096;
+  hipLaunchKernelGGL(predict_kernel, dim3(g), dim3(256), 0, st, X, xdt, ld, d, n, coef, b, out);
+  DQ_HIP_CHECK(hipGetLastError());
+}
+
+int metrics_blocks(int64_t n) {
+  int64_t g = (n + 255) / 256;
+  if (g > 1024) g = 1024;
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+void regression_metrics(const void* X, int xdt, int64_t ld, int d, int64_t n, const void* y, int ydt,
+                        const uint8_t* sel, const double* coef, double b, double shift, double* partials,
+                        double* out, hipStream_t st) {
+  const int g = metrics_blocks(n);
+  hipLaunchKernelGGL(metrics_kernel, dim3(g), dim3(256), 0, st, X, xdt, ld, d, n, y, ydt, sel, coef, b, shift,
+                     partials);
+  hipLaunchKernelGGL(sum_slabs_kernel, dim3(1), dim3(64), 0, st, partials, g, 8, out);
+  DQ_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace dq4ml

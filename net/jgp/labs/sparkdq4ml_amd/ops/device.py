@@ -1,0 +1,235 @@
+"""Python launchers of the gfx950 kernels (``_dq4ml_hip``).
+
+Allocation policy: every output/workspace comes from torch's caching allocator on the current
+device and every kernel runs on ``torch.cuda.current_stream()`` — no hipMalloc/hipMemcpy in any
+launch path, so these ops compose with torch work and HIP-graph capture.  Shapes and dtypes are
+validated HERE, on the host, before any launch (a kernel's indexing assumes them)."""
+from __future__ import annotations
+
+from typing import List, Optional
+
+import numpy as np
+import torch
+
+from . import native
+
+__all__ = ["dtype_code", "gram_stats", "compact_indices", "pack_columns", "predict", "regression_metrics",
+           "GRAM_MODES"]
+
+_DT = {torch.float64: 0, torch.float32: 1, torch.bfloat16: 2, torch.int32: 3, torch.int64: 4, torch.uint8: 5,
+       torch.bool: 5, torch.float16: 6}
+GRAM_MODES = {"fp64": 0, "fp32": 1, "bf16": 2, "fp8": 3}
+
+
+def dtype_code(t: torch.Tensor) -> int:
+    try:
+        return _DT[t.dtype]
+    except KeyError:
+        raise TypeError(f"unsupported dtype {t.dtype}") from None
+
+
+def _stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _ptr(t: Optional[torch.Tensor]) -> int:
+    return 0 if t is None else t.data_ptr()
+
+
+def _check_dev(*ts):
+    dev = None
+    for t in ts:
+        if t is None:
+            continue
+        if not t.is_cuda:
+            raise ValueError("device op given a host tensor")
+        if dev is None:
+            dev = t.device
+        elif t.device != dev:
+            raise ValueError(f"tensors on different devices: {dev} vs {t.device}")
+
+
+def _feature_view(X: torch.Tensor, align_elems: int):
+    """(base tensor, ld): a feature-major view whose rows are ``align_elems``-aligned."""
+    if X.dim() != 2:
+        raise ValueError("feature matrix must be 2-D [d, n]")
+    d, n = X.shape
+    if X.stride(1) != 1 or (d > 1 and X.stride(0) % align_elems) or X.data_ptr() % 16:
+        ld = (n + 63) // 64 * 64
+        buf = torch.zeros(d, ld, dtype=X.dtype, device=X.device)
+        buf[:, :n] = X
+        return buf, ld
+    return X, (X.stride(0) if d > 1 else max(n, 1))
+
+
+# ------------------------------------------------------------------------------------------
+def gram_stats(X, y, w, sel, compute: str = "fp64", x_zero_dead: bool = False, blocks: Optional[int] = None):
+    h = native.hip()
+    _check_dev(X, y, w, sel)
+    d, n = X.shape
+    mode = GRAM_MODES[compute]
+    out = torch.empty(5 + 2 * d + d * (d + 1) // 2, dtype=torch.float64, device=X.device)
+    if n == 0:
+        out.zero_()
+        return out
+    if d > 64 or mode in (1, 3):
+        from . import kernels
+
+        return _gram_fallback_wide(X, y, w, sel, compute)
+    if mode == 2 and X.dtype not in (torch.bfloat16, torch.float32, torch.float64):
+        X = X.to(torch.float32)
+    if mode == 0 and X.dtype not in (torch.float64, torch.float32):
+        X = X.to(torch.float64)
+    align = 16 // X.element_size()
+    Xv, ld = _feature_view(X, align)
+    y = y.contiguous()
+    if y.dtype not in (torch.float64, torch.float32):
+        y = y.to(torch.float64)
+    if w is not None:
+        w = w.contiguous()
+        if w.dtype not in (torch.float64, torch.float32):
+            w = w.to(torch.float64)
+    if sel is not None:
+        sel = sel.contiguous()
+        if sel.dtype != torch.bool:
+            sel = sel.to(torch.bool)
+    if y.numel() != n or (w is not None and w.numel() != n) or (sel is not None and sel.numel() != n):
+        raise ValueError("gram_stats: row-count mismatch")
+    if w is not None:
+        xmode = 2
+    elif sel is not None and not x_zero_dead:
+        xmode = 1
+    else:
+        xmode = 0
+    nb = int(blocks or h.gram_default_blocks(n))
+    P = int(h.gram_partial_stride(mode, d))
+    partials = torch.empty(nb * P, dtype=torch.float64, device=X.device)
+    h.gram_tall(mode, Xv.data_ptr(), int(ld), int(d), int(n), dtype_code(Xv), y.data_ptr(), dtype_code(y),
+                _ptr(w), dtype_code(w) if w is not None else 0, _ptr(sel), xmode, partials.data_ptr(), nb,
+                out.data_ptr(), _stream())
+    return out
+
+
+def _gram_fallback_wide(X, y, w, sel, compute):
+    """d > 64 (until the LDS-tiled MFMA SYRK lands) and fp32/fp8 requests: hipBLAS library GEMM in
+    the requested precision with f64 side sums."""
+    from . import kernels
+
+    d, n = X.shape
+    dt = {"fp64": torch.float64, "fp32": torch.float32, "bf16": torch.bfloat16, "fp8": torch.bfloat16}[compute]
+    wv = torch.ones(n, dtype=torch.float64, device=X.device) if w is None else w.to(torch.float64)
+    if sel is not None:
+        wv = torch.where(sel, wv, torch.zeros_like(wv))
+    Xc = X.to(dt)
+    Xw = (X.to(torch.float64) * wv).to(dt)
+    aa = (Xw @ Xc.t()).to(torch.float64)
+    yd = y.to(torch.float64)
+    out = torch.empty(5 + 2 * d + d * (d + 1) // 2, dtype=torch.float64, device=X.device)
+    live = torch.ones(n, dtype=torch.bool, device=X.device) if sel is None else sel
+    out[0] = live.sum()
+    out[1] = wv.sum()
+    out[2] = (wv * wv).sum()
+    out[3] = (wv * yd).sum()
+    out[4] = (wv * yd * yd).sum()
+    Xd = X.to(torch.float64)
+    out[5:5 + d] = Xd @ wv
+    out[5 + d:5 + 2 * d] = Xd @ (wv * yd)
+    out[5 + 2 * d:] = kernels.packed_upper(aa)
+    return out
+
+
+# ------------------------------------------------------------------------------------------
+def compact_indices(sel: torch.Tensor, limit: Optional[int] = None) -> torch.Tensor:
+    h = native.hip()
+    _check_dev(sel)
+    sel = sel.contiguous()
+    if sel.dtype != torch.bool:
+        sel = sel.to(torch.bool)
+    n = sel.numel()
+    nb = int(h.compact_blocks(n))
+    counts = torch.empty(nb + 1, dtype=torch.int64, device=sel.device)
+    s = _stream()
+    h.compact_count_scan(sel.data_ptr(), n, counts.data_ptr(), s)
+    total = int(counts[nb].item())
+    k = total if limit is None else min(total, int(limit))
+    out = torch.empty(k, dtype=torch.int64, device=sel.device)
+    if k > 0:
+        h.compact_write(sel.data_ptr(), n, counts.data_ptr(), k, out.data_ptr(), s)
+    return out
+
+
+# ------------------------------------------------------------------------------------------
+def pack_columns(parts: List[torch.Tensor], dtype: torch.dtype, sel: Optional[torch.Tensor] = None) -> torch.Tensor:
+    h = native.hip()
+    rows = []
+    for p in parts:
+        _check_dev(p)
+        if p.dim() == 1:
+            p = p.unsqueeze(0)
+        for i in range(p.shape[0]):
+            r = p[i]
+            if not r.is_contiguous():
+                r = r.contiguous()
+            if r.dtype == torch.bool:
+                r = r.to(torch.uint8)
+            rows.append(r)
+    d = len(rows)
+    n = rows[0].numel() if rows else 0
+    for r in rows:
+        if r.numel() != n:
+            raise ValueError("pack_columns: columns of different lengths")
+    ld = (n + 63) // 64 * 64
+    dev = rows[0].device if rows else torch.device("cuda")
+    out = torch.empty(d, max(ld, 1), dtype=dtype, device=dev)
+    srcb = int(h.pack_src_bytes())
+    desc = np.zeros((d, srcb // 8), dtype=np.int64)
+    for i, r in enumerate(rows):
+        desc[i, 0] = r.data_ptr()
+        desc[i, 1] = dtype_code(r)
+    desc_dev = torch.from_numpy(desc.reshape(-1).view(np.uint8).copy()).to(dev, non_blocking=False)
+    keep = rows  # keep sources alive until the kernel is enqueued
+    if sel is not None:
+        sel = sel.contiguous().to(torch.bool)
+    h.pack_columns(desc_dev.data_ptr(), d, n, out.data_ptr(), dtype_code(out), ld, _ptr(sel), _stream())
+    del keep
+    return out[:, :n]
+
+
+# ------------------------------------------------------------------------------------------
+def _coef_dev(coef, device):
+    return torch.as_tensor(np.ascontiguousarray(coef, dtype=np.float64), device=device)
+
+
+def predict(X: torch.Tensor, coef, intercept: float) -> torch.Tensor:
+    h = native.hip()
+    _check_dev(X)
+    d, n = X.shape
+    if X.stride(1) != 1:
+        X = X.contiguous()
+    ld = X.stride(0) if d > 1 else max(n, 1)
+    c = _coef_dev(coef, X.device)
+    if c.numel() != d:
+        raise ValueError("predict: coefficient length != number of features")
+    out = torch.empty(n, dtype=torch.float64, device=X.device)
+    h.predict(X.data_ptr(), dtype_code(X), int(ld), int(d), int(n), c.data_ptr(), float(intercept), out.data_ptr(),
+              _stream())
+    return out
+
+
+def regression_metrics(X, y, coef, intercept, sel, shift):
+    h = native.hip()
+    _check_dev(X, y, sel)
+    d, n = X.shape
+    if X.stride(1) != 1:
+        X = X.contiguous()
+    ld = X.stride(0) if d > 1 else max(n, 1)
+    y = y.contiguous()
+    if sel is not None:
+        sel = sel.contiguous().to(torch.bool)
+    c = _coef_dev(coef, X.device)
+    nb = int(h.metrics_blocks(n))
+    partials = torch.empty(nb * 8, dtype=torch.float64, device=X.device)
+    out = torch.empty(8, dtype=torch.float64, device=X.device)
+    h.regression_metrics(X.data_ptr(), dtype_code(X), int(ld), int(d), int(n), y.data_ptr(), dtype_code(y), _ptr(sel),
+                         c.data_ptr(), float(intercept), float(shift), partials.data_ptr(), out.data_ptr(), _stream())
+    return out

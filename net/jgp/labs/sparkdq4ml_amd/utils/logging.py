@@ -30,7 +30,7 @@ def configure_logging():
     root = logging.getLogger(ROOT)
     root.addHandler(h)
     root.propagate = False
-    root.setLevel(os.environ.get("DQ4ML_LOG_LEVEL", "WARNING").upper())
+    root.setLevel(os.environ.get("DQ4ML_LOG_LEVEL", "ERROR").upper())
     logging.getLogger(ROOT + ".apps").setLevel(logging.DEBUG)
 
 

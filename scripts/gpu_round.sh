@@ -1,0 +1,27 @@
+#!/bin/bash
+# One gpurun call: kernel tests -> bench -> rocprof summary.  Stops at the first GPU fault /
+# abort / timeout (rc not in {0,1}); pytest rc=1 (test failures) still lets the bench run.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+step() {  # name timeout cmd...
+  local name=$1 to=$2; shift 2
+  echo "=== $name" | tee -a gpurun_out/round.log
+  timeout -k 10 "$to" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc" | tee -a gpurun_out/round.log
+  tail -15 "gpurun_out/$name.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
+  return 0
+}
+STEPS=${STEPS:-"info tests bench prof"}
+for s in $STEPS; do
+  case $s in
+    info) step info 300 python -c "import torch,sys; sys.path.insert(0,'.'); from net.jgp.labs.sparkdq4ml_amd.ops import native; print(native.hip().device_info())" ;;
+    tests) step tests 900 python -m pytest tests -m gpu -x -q ;;
+    smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" ;;
+    bench) step bench 600 python bench.py --steps 20 --warmup 3 ;;
+    benchf32) step benchf32 600 python bench.py --steps 10 --warmup 2 --dtype fp32 ;;
+    prof) cd /tmp && export TMPDIR=/tmp && cd - >/dev/null; step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 5 --warmup 1 ;;
+  esac
+done

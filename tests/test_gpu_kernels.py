@@ -1,0 +1,116 @@
+"""Numerics of the gfx950 kernels against plain PyTorch fp64 references (run via gpurun)."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from net.jgp.labs.sparkdq4ml_amd.ops import device, kernels, native  # noqa: E402
+
+
+def _ref_stats(X, y, w, sel):
+    return kernels.gram_stats(X.double().cpu(), y.double().cpu(), None if w is None else w.double().cpu(),
+                              None if sel is None else sel.cpu(), "fp64")
+
+
+def _rel(a, b):
+    a, b = a.double().cpu(), b.double().cpu()
+    scale = b.abs().max().clamp_min(1e-300)
+    return float((a - b).abs().max() / scale)
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _hip():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    native.hip()
+
+
+@pytest.mark.parametrize("d", [1, 5, 32, 33, 64])
+@pytest.mark.parametrize("n", [1, 63, 64, 1000, 100_003])
+def test_gram_f64_matches_oracle(d, n):
+    g = torch.Generator(device="cuda").manual_seed(d * 1000 + n)
+    X = torch.randn(d, n, generator=g, device="cuda", dtype=torch.float64) + 0.5
+    y = torch.randn(n, generator=g, device="cuda", dtype=torch.float64) * 3 + 1
+    out = device.gram_stats(X, y, None, None, "fp64")
+    ref = _ref_stats(X, y, None, None)
+    assert _rel(out, ref) < 1e-12
+
+
+@pytest.mark.parametrize("xdt", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("d", [1, 7, 32, 48, 64])
+@pytest.mark.parametrize("n", [5, 64, 4096 + 17, 250_000])
+def test_gram_bf16_matches_oracle(xdt, d, n):
+    g = torch.Generator(device="cuda").manual_seed(7 * d + n)
+    X = (torch.randn(d, n, generator=g, device="cuda") + 0.25).to(xdt)
+    y = torch.randn(n, generator=g, device="cuda") * 2 + 3
+    out = device.gram_stats(X, y, None, None, "bf16")
+    ref = _ref_stats(X.to(torch.bfloat16).float(), y, None, None)  # oracle on the bf16-rounded features
+    # scalars exact-ish (f64), Gram blocks f32-accumulated
+    assert _rel(out[:5], ref[:5]) < 1e-12
+    assert _rel(out[5:], ref[5:]) < 2e-5
+
+
+@pytest.mark.parametrize("mode", ["fp64", "bf16"])
+def test_gram_with_selection_and_weights(mode):
+    g = torch.Generator(device="cuda").manual_seed(3)
+    d, n = 32, 20_000
+    X = torch.randn(d, n, generator=g, device="cuda", dtype=torch.float64)
+    y = torch.randn(n, generator=g, device="cuda", dtype=torch.float64)
+    sel = torch.rand(n, generator=g, device="cuda") > 0.3
+    w = torch.rand(n, generator=g, device="cuda", dtype=torch.float64) + 0.5
+    Xin = X if mode == "fp64" else X.to(torch.bfloat16)
+    Xref = Xin.double()
+    tol = 1e-12 if mode == "fp64" else 3e-3  # bf16 rounding of w*x in the weighted operand
+    for ww, ss in ((None, sel), (w, None), (w, sel)):
+        out = device.gram_stats(Xin, y, ww, ss, mode)
+        ref = _ref_stats(Xref, y, ww, ss)
+        assert _rel(out[:5], ref[:5]) < 1e-12
+        assert _rel(out[5:], ref[5:]) < tol, (ww is None, ss is None)
+
+
+def test_gram_deterministic():
+    g = torch.Generator(device="cuda").manual_seed(11)
+    X = torch.randn(32, 300_000, generator=g, device="cuda").to(torch.bfloat16)
+    y = torch.randn(300_000, generator=g, device="cuda")
+    a = device.gram_stats(X, y, None, None, "bf16")
+    b = device.gram_stats(X, y, None, None, "bf16")
+    assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("n", [0, 1, 4095, 4096, 100_001])
+@pytest.mark.parametrize("limit", [None, 21])
+def test_compact_indices(n, limit):
+    g = torch.Generator(device="cuda").manual_seed(n + 1)
+    sel = torch.rand(n, generator=g, device="cuda") > 0.5
+    got = device.compact_indices(sel, limit)
+    ref = torch.nonzero(sel.cpu()).flatten()
+    if limit is not None:
+        ref = ref[:limit]
+    assert torch.equal(got.cpu(), ref)
+
+
+def test_pack_columns():
+    a = torch.arange(100, device="cuda", dtype=torch.int32)
+    b = torch.randn(100, device="cuda", dtype=torch.float64)
+    v = torch.randn(3, 100, device="cuda", dtype=torch.float32)
+    for dt in (torch.float64, torch.float32, torch.bfloat16):
+        out = device.pack_columns([a, b, v], dt)
+        ref = torch.cat([a.unsqueeze(0).to(dt), b.unsqueeze(0).to(dt), v.to(dt)])
+        assert out.shape == (5, 100)
+        assert torch.equal(out.cpu(), ref.cpu())
+
+
+def test_predict_and_metrics():
+    g = torch.Generator(device="cuda").manual_seed(5)
+    d, n = 7, 10_007
+    X = torch.randn(d, n, generator=g, device="cuda", dtype=torch.float64)
+    y = torch.randn(n, generator=g, device="cuda", dtype=torch.float64)
+    sel = torch.rand(n, generator=g, device="cuda") > 0.2
+    coef = np.linspace(-1, 1, d)
+    p = device.predict(X, coef, 0.25)
+    pref = kernels.predict(X.cpu(), coef, 0.25)
+    assert _rel(p, pref) < 1e-13
+    m = device.regression_metrics(X, y, coef, 0.25, sel, 0.1)
+    mref = kernels.regression_metrics(X.cpu(), y.cpu(), coef, 0.25, sel.cpu(), 0.1)
+    assert _rel(m, mref) < 1e-12
