@@ -27,6 +27,8 @@ struct GramArgs {
 
 int64_t gram_partial_stride(int mode, int d);
 int gram_default_blocks(int64_t n);
+// grid that exactly fills the chip for the kernel instantiation (occupancy-sized, persistent-style)
+int gram_plan_blocks(int mode, int d, int64_t n, int xdt, int xmode);
 // xmode: 0 = X already zero on dead rows (or no sel/w), 1 = binary mask from sel, 2 = general weights
 void gram_tall(int mode, GramArgs a, int xmode, int blocks, double* out, hipStream_t st);
 

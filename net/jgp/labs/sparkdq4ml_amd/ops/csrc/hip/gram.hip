@@ -163,7 +163,7 @@ __device__ __forceinline__ void weight_frags(bf16x8 (&fr)[4], const float* wl /*
 // bf16 MFMA kernel
 // =============================================================================================
 template <typename TX, int NT, int XMODE>
-__global__ __launch_bounds__(kBlock) void gram_tall_bf16_kernel(GramArgs a) {
+__global__ __launch_bounds__(kBlock, 2) void gram_tall_bf16_kernel(GramArgs a) {
   constexpr int NPAIR = NT * (NT + 1) / 2;
   // LDS: per wave 4 cols x 64 rows bf16 (W fragments) + 64 f32 row weights; reused for the
   // block reduction afterwards.
@@ -198,11 +198,9 @@ __global__ __launch_bounds__(kBlock) void gram_tall_bf16_kernel(GramArgs a) {
   int64_t s1 = s0 + a.spw;
   if (s1 > a.nsuper) s1 = a.nsuper;
   const bool do_tail = (gw == total_waves - 1) && (a.n > a.nsuper * 64);
-  const int64_t s_end = do_tail ? a.nsuper + 1 : s1;
-  if (do_tail && s0 > a.nsuper) s0 = a.nsuper;
 
-  for (int64_t s = s0; s < s_end; ++s) {
-    const int64_t r0 = s * 64;
+  // One superstep of compute on already-loaded feature fragments.
+  auto compute = [&](int64_t r0, bf16x8 (&fr)[NT][4]) {
     // 1) per-row scalars, lane = row
     RowVals rv = row_vals(a, r0 + lane);
     ra.add(rv);
@@ -216,20 +214,8 @@ __global__ __launch_bounds__(kBlock) void gram_tall_bf16_kernel(GramArgs a) {
       if (XMODE == 2) wrow[lane] = (float)rv.w;
     }
     const uint64_t live_bits = __ballot(rv.live);
-    // 2) features
-    const int64_t rows_left = a.n - (r0 + 32 * h);
-    bf16x8 fr[NT][4];
-#pragma unroll
-    for (int t = 0; t < NT; ++t) {
-      if (fvalid[t]) {
-        load_rows32_bf16<TX>(fp[t] + r0, rows_left, fr[t]);
-      } else {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) fr[t][i] = bf16x8{};
-      }
-    }
     __builtin_amdgcn_wave_barrier();
-    // 3) W fragments (lanes f < 4 read their column; everyone else multiplies zeros)
+    // 2) W fragments (lanes f < 4 read their column; everyone else multiplies zeros)
     bf16x8 wf[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) wf[i] = bf16x8{};
@@ -237,7 +223,7 @@ __global__ __launch_bounds__(kBlock) void gram_tall_bf16_kernel(GramArgs a) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) wf[i] = *reinterpret_cast<const bf16x8*>(wl + f * 64 + 32 * h + 8 * i);
     }
-    // 4) masking / weighting of one operand of XᵀX
+    // 3) masking / weighting of one operand of XᵀX
     bf16x8 frw[NT][4];
 #pragma unroll
     for (int t = 0; t < NT; ++t)
@@ -251,7 +237,7 @@ __global__ __launch_bounds__(kBlock) void gram_tall_bf16_kernel(GramArgs a) {
 #pragma unroll
       for (int t = 0; t < NT; ++t) weight_frags(frw[t], wrow + 32 * h);
     }
-    // 5) MFMAs
+    // 4) MFMAs
     int p = 0;
 #pragma unroll
     for (int I = 0; I < NT; ++I)
@@ -264,6 +250,38 @@ __global__ __launch_bounds__(kBlock) void gram_tall_bf16_kernel(GramArgs a) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) accw[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fr[t][i], wf[i], accw[t], 0, 0, 0);
     __builtin_amdgcn_wave_barrier();
+  };
+  auto load = [&](int64_t r0, int64_t rows_left, bf16x8 (&fr)[NT][4]) {
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      if (fvalid[t]) {
+        load_rows32_bf16<TX>(fp[t] + r0, rows_left, fr[t]);
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) fr[t][i] = bf16x8{};
+      }
+    }
+  };
+
+  // full supersteps: register double buffer (loads of s+1 in flight while s computes)
+  if (s0 < s1) {
+    bf16x8 cur[NT][4], nxt[NT][4];
+    load(s0 * 64, 64, cur);
+    for (int64_t s = s0; s < s1; ++s) {
+      if (s + 1 < s1) load((s + 1) * 64, 64, nxt);
+      compute(s * 64, cur);
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) cur[t][i] = nxt[t][i];
+    }
+  }
+  // ragged tail (rows not filling a 64-row superstep): last wave only, guarded loads
+  if (do_tail) {
+    bf16x8 tl[NT][4];
+    const int64_t r0 = a.nsuper * 64;
+    load(r0, a.n - (r0 + 32 * h), tl);
+    compute(r0, tl);
   }
 
   // ---- block reduction (deterministic: waves add in order) ---------------------------------
@@ -450,26 +468,45 @@ __global__ __launch_bounds__(kBlock) void gram_tall_f64_kernel(GramArgs a) {
 // =============================================================================================
 // slab reduction -> packed-upper flat layout
 // =============================================================================================
-__global__ __launch_bounds__(256) void gram_reduce_kernel(const double* __restrict__ partials, int nslab, int P,
-                                                         int d, int T, int NT, double* __restrict__ out) {
+__device__ __forceinline__ int64_t gram_src_index(int64_t k, int d, int T, int NT) {
+  if (k < 5 + 2 * (int64_t)d) return k;
+  const int64_t kk = k - (5 + 2 * (int64_t)d);
+  int64_t j = (int64_t)((sqrt(8.0 * (double)kk + 1.0) - 1.0) * 0.5);
+  while (j * (j + 1) / 2 > kk) --j;
+  while ((j + 1) * (j + 2) / 2 <= kk) ++j;
+  const int64_t i = kk - j * (j + 1) / 2;  // i <= j
+  const int64_t I = i / T, J = j / T;
+  const int64_t p = I * NT - I * (I - 1) / 2 + (J - I);
+  return 5 + 2 * (int64_t)d + p * T * T + (i % T) * T + (j % T);
+}
+
+// 64 outputs per block; 16 slab groups of 64 threads each sum a strided share of the slabs
+// (coalesced 512-B rows), then a fixed-order LDS combine: deterministic.
+__global__ __launch_bounds__(1024) void gram_reduce_kernel(const double* __restrict__ partials, int nslab, int P,
+                                                          int d, int T, int NT, double* __restrict__ out) {
+  __shared__ double part[16][64];
   const int64_t K = 5 + 2 * (int64_t)d + (int64_t)d * (d + 1) / 2;
-  for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < K; k += (int64_t)gridDim.x * blockDim.x) {
-    int64_t src;
-    if (k < 5 + 2 * d) {
-      src = k;
-    } else {
-      const int64_t kk = k - (5 + 2 * d);
-      int64_t j = (int64_t)((sqrt(8.0 * (double)kk + 1.0) - 1.0) * 0.5);
-      while (j * (j + 1) / 2 > kk) --j;
-      while ((j + 1) * (j + 2) / 2 <= kk) ++j;
-      const int64_t i = kk - j * (j + 1) / 2;  // i <= j
-      const int64_t I = i / T, J = j / T;
-      const int64_t p = I * NT - I * (I - 1) / 2 + (J - I);
-      src = 5 + 2 * (int64_t)d + p * T * T + (i % T) * T + (j % T);
+  const int c = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int64_t k = (int64_t)blockIdx.x * 64 + c;
+  double s = 0.0;
+  if (k < K) {
+    const int64_t src = gram_src_index(k, d, T, NT);
+    const double* p = partials + src;
+    int b = g;
+    for (; b + 48 < nslab; b += 64) {
+      const double v0 = p[(int64_t)b * P], v1 = p[(int64_t)(b + 16) * P];
+      const double v2 = p[(int64_t)(b + 32) * P], v3 = p[(int64_t)(b + 48) * P];
+      s += (v0 + v1) + (v2 + v3);
     }
-    double s = 0.0;
-    for (int b = 0; b < nslab; ++b) s += partials[(int64_t)b * P + src];
-    out[k] = s;
+    for (; b < nslab; b += 16) s += p[(int64_t)b * P];
+  }
+  part[g][c] = s;
+  __syncthreads();
+  if (g == 0 && k < K) {
+    double t = 0.0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) t += part[i][c];
+    out[k] = t;
   }
 }
 
@@ -484,6 +521,11 @@ int64_t gram_partial_stride(int mode, int d) {
   return 5 + 2 * (int64_t)d + (int64_t)NT * (NT + 1) / 2 * 1024;
 }
 
+static int reduce_blocks(int d) {
+  const int64_t K = 5 + 2 * (int64_t)d + (int64_t)d * (d + 1) / 2;
+  return (int)((K + 63) / 64);
+}
+
 int gram_default_blocks(int64_t n) {
   const int64_t nsuper = (n + 63) / 64;
   // aim: >= 16 waves per CU on 256 CUs, but >= 8 supersteps per wave
@@ -493,61 +535,87 @@ int gram_default_blocks(int64_t n) {
   return (int)blocks;
 }
 
-template <typename TX, int NT>
-static void launch_bf16_nt(GramArgs& a, int xmode, int blocks, size_t lds, hipStream_t st) {
-  if (xmode == 0) hipLaunchKernelGGL((gram_tall_bf16_kernel<TX, NT, 0>), dim3(blocks), dim3(kBlock), lds, st, a);
-  else if (xmode == 1) hipLaunchKernelGGL((gram_tall_bf16_kernel<TX, NT, 1>), dim3(blocks), dim3(kBlock), lds, st, a);
-  else hipLaunchKernelGGL((gram_tall_bf16_kernel<TX, NT, 2>), dim3(blocks), dim3(kBlock), lds, st, a);
+template <typename K>
+static int occupancy_blocks(K kern, size_t lds) {
+  int per = 0, dev = 0, cus = 0;
+  DQ_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kern, kBlock, lds));
+  DQ_HIP_CHECK(hipGetDevice(&dev));
+  DQ_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+  if (per < 1) per = 1;
+  return per * cus;
 }
 
-template <typename TX>
-static void launch_f64_x(GramArgs& a, int NT, int blocks, size_t lds, hipStream_t st) {
-  switch (NT) {
-    case 1: hipLaunchKernelGGL((gram_tall_f64_kernel<TX, 1>), dim3(blocks), dim3(kBlock), lds, st, a); break;
-    case 2: hipLaunchKernelGGL((gram_tall_f64_kernel<TX, 2>), dim3(blocks), dim3(kBlock), lds, st, a); break;
-    case 3: hipLaunchKernelGGL((gram_tall_f64_kernel<TX, 3>), dim3(blocks), dim3(kBlock), lds, st, a); break;
-    default: hipLaunchKernelGGL((gram_tall_f64_kernel<TX, 4>), dim3(blocks), dim3(kBlock), lds, st, a); break;
+static size_t bf16_lds(int d) {
+  size_t lds = kWavesPerBlock * (4 * 64 * 2 + 64 * 4);
+  const size_t red = (size_t)gram_partial_stride(GRAM_BF16, d) * sizeof(double);
+  return red > lds ? red : lds;
+}
+
+static size_t f64_lds(int d) {
+  size_t lds = kWavesPerBlock * 128 * sizeof(double);
+  const size_t red = (size_t)gram_partial_stride(GRAM_F64, d) * sizeof(double);
+  return red > lds ? red : lds;
+}
+
+// Dispatch table: call F with the kernel instantiation for (mode, xdt, d, xmode).
+template <typename F>
+static void with_kernel(int mode, int xdt, int d, int xmode, F&& f) {
+  if (mode == GRAM_BF16) {
+    const int NT = (d + 31) / 32;
+#define DQ_BF16_CASE(TX, NTV)                                                     \
+    if (xmode == 0) return f(gram_tall_bf16_kernel<TX, NTV, 0>);                  \
+    if (xmode == 1) return f(gram_tall_bf16_kernel<TX, NTV, 1>);                  \
+    return f(gram_tall_bf16_kernel<TX, NTV, 2>);
+    if (xdt == DT_BF16) { if (NT == 1) { DQ_BF16_CASE(uint16_t, 1) } else { DQ_BF16_CASE(uint16_t, 2) } }
+    if (xdt == DT_F32) { if (NT == 1) { DQ_BF16_CASE(float, 1) } else { DQ_BF16_CASE(float, 2) } }
+    if (xdt == DT_F64) { if (NT == 1) { DQ_BF16_CASE(double, 1) } else { DQ_BF16_CASE(double, 2) } }
+#undef DQ_BF16_CASE
+    throw std::invalid_argument("gram_tall(bf16): unsupported feature dtype");
   }
+  if (mode == GRAM_F64) {
+    const int NT = (d + 15) / 16;
+#define DQ_F64_CASE(TX)                                        \
+    switch (NT) {                                              \
+      case 1: return f(gram_tall_f64_kernel<TX, 1>);           \
+      case 2: return f(gram_tall_f64_kernel<TX, 2>);           \
+      case 3: return f(gram_tall_f64_kernel<TX, 3>);           \
+      default: return f(gram_tall_f64_kernel<TX, 4>);          \
+    }
+    if (xdt == DT_F64) { DQ_F64_CASE(double) }
+    if (xdt == DT_F32) { DQ_F64_CASE(float) }
+#undef DQ_F64_CASE
+    throw std::invalid_argument("gram_tall(f64): unsupported feature dtype");
+  }
+  throw std::invalid_argument("gram_tall: unsupported mode");
+}
+
+int gram_plan_blocks(int mode, int d, int64_t n, int xdt, int xmode) {
+  const size_t lds = mode == GRAM_BF16 ? bf16_lds(d) : f64_lds(d);
+  int full = 1;
+  with_kernel(mode, xdt, d, xmode, [&](auto kern) { full = occupancy_blocks(kern, lds); });
+  // at least ~4 supersteps per wave, at most one full residency wave of blocks
+  const int64_t nsuper = (n + 63) / 64;
+  int64_t want = (nsuper + 4 * kWavesPerBlock - 1) / (4 * kWavesPerBlock);
+  if (want < 1) want = 1;
+  return (int)(want < full ? want : full);
 }
 
 void gram_tall(int mode, GramArgs a, int xmode, int blocks, double* out, hipStream_t st) {
   if (a.d < 1 || a.d > 64) throw std::invalid_argument("gram_tall: d must be in [1, 64]");
+  if (blocks < 1) throw std::invalid_argument("gram_tall: blocks must be >= 1");
   a.nsuper = a.n / 64;
   const int64_t total_waves = (int64_t)blocks * kWavesPerBlock;
   a.spw = (a.nsuper + total_waves - 1) / total_waves;
   if (a.spw < 1) a.spw = 1;
   a.P = (int)gram_partial_stride(mode, a.d);
-  const size_t red_bytes = (size_t)a.P * sizeof(double);
-  if (mode == GRAM_BF16) {
-    const int NT = (a.d + 31) / 32;
-    size_t lds = kWavesPerBlock * (4 * 64 * 2 + 64 * 4);
-    if (red_bytes > lds) lds = red_bytes;
-    if (a.xdt == DT_BF16) {
-      if (NT == 1) launch_bf16_nt<uint16_t, 1>(a, xmode, blocks, lds, st);
-      else launch_bf16_nt<uint16_t, 2>(a, xmode, blocks, lds, st);
-    } else if (a.xdt == DT_F32) {
-      if (NT == 1) launch_bf16_nt<float, 1>(a, xmode, blocks, lds, st);
-      else launch_bf16_nt<float, 2>(a, xmode, blocks, lds, st);
-    } else if (a.xdt == DT_F64) {
-      if (NT == 1) launch_bf16_nt<double, 1>(a, xmode, blocks, lds, st);
-      else launch_bf16_nt<double, 2>(a, xmode, blocks, lds, st);
-    } else {
-      throw std::invalid_argument("gram_tall: unsupported feature dtype");
-    }
-    DQ_HIP_CHECK(hipGetLastError());
-    hipLaunchKernelGGL(gram_reduce_kernel, dim3(8), dim3(256), 0, st, a.partials, blocks, a.P, a.d, 32, NT, out);
-  } else if (mode == GRAM_F64) {
-    const int NT = (a.d + 15) / 16;
-    size_t lds = kWavesPerBlock * 128 * sizeof(double);
-    if (red_bytes > lds) lds = red_bytes;
-    if (a.xdt == DT_F64) launch_f64_x<double>(a, NT, blocks, lds, st);
-    else if (a.xdt == DT_F32) launch_f64_x<float>(a, NT, blocks, lds, st);
-    else throw std::invalid_argument("gram_tall(f64): unsupported feature dtype");
-    DQ_HIP_CHECK(hipGetLastError());
-    hipLaunchKernelGGL(gram_reduce_kernel, dim3(8), dim3(256), 0, st, a.partials, blocks, a.P, a.d, 16, NT, out);
-  } else {
-    throw std::invalid_argument("gram_tall: unsupported mode");
-  }
+  const size_t lds = mode == GRAM_BF16 ? bf16_lds(a.d) : f64_lds(a.d);
+  with_kernel(mode, a.xdt, a.d, xmode,
+              [&](auto kern) { hipLaunchKernelGGL(kern, dim3(blocks), dim3(kBlock), lds, st, a); });
+  DQ_HIP_CHECK(hipGetLastError());
+  const int T = mode == GRAM_BF16 ? 32 : 16;
+  const int NT = (a.d + T - 1) / T;
+  hipLaunchKernelGGL(gram_reduce_kernel, dim3(reduce_blocks(a.d)), dim3(1024), 0, st, a.partials, blocks, a.P, a.d,
+                     T, NT, out);
   DQ_HIP_CHECK(hipGetLastError());
 }
 

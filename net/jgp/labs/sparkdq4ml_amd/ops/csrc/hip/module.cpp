@@ -39,6 +39,7 @@ PYBIND11_MODULE(_dq4ml_hip, m) {
   // ---- Gram (K5) ---------------------------------------------------------------------------
   m.def("gram_partial_stride", &gram_partial_stride);
   m.def("gram_default_blocks", &gram_default_blocks);
+  m.def("gram_plan_blocks", &gram_plan_blocks);
   m.def("gram_tall",
         [](int mode, uintptr_t X, int64_t ld, int d, int64_t n, int xdt, uintptr_t y, int ydt, uintptr_t w, int wdt,
            uintptr_t sel, int xmode, uintptr_t partials, int blocks, uintptr_t out, uintptr_t stream) {

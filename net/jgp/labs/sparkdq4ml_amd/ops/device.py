@@ -101,7 +101,7 @@ def gram_stats(X, y, w, sel, compute: str = "fp64", x_zero_dead: bool = False, b
         xmode = 1
     else:
         xmode = 0
-    nb = int(blocks or h.gram_default_blocks(n))
+    nb = int(blocks or h.gram_plan_blocks(mode, int(d), int(n), dtype_code(Xv), xmode))
     P = int(h.gram_partial_stride(mode, d))
     partials = torch.empty(nb * P, dtype=torch.float64, device=X.device)
     h.gram_tall(mode, Xv.data_ptr(), int(ld), int(d), int(n), dtype_code(Xv), y.data_ptr(), dtype_code(y),
