@@ -23,7 +23,14 @@ struct GramArgs {
   int P;
   int64_t spw;         // supersteps (64 rows) per wave
   int64_t nsuper;      // n / 64
+  int tiled;           // X is MFMA-fragment-ordered bf16 (tile_bf16 layout)
 };
+
+// MFMA-fragment-ordered bf16 feature storage ("tiled"): for superstep s (64 rows), 32-feature
+// tile t, k-step i: 64 lanes x 16 B contiguous, lane l = 32h + f holding rows s*64+32h+8i..+8 of
+// feature 32t+f.  One wave load instruction = 1 KiB contiguous; zero padded to whole supersteps.
+int64_t tiled_elems(int d, int64_t n);
+void tile_bf16(const void* X, int xdt, int64_t ld, int d, int64_t n, void* out, hipStream_t st);
 
 int64_t gram_partial_stride(int mode, int d);
 int gram_default_blocks(int64_t n);

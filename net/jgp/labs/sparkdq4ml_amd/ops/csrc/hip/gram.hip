@@ -162,7 +162,7 @@ __device__ __forceinline__ void weight_frags(bf16x8 (&fr)[4], const float* wl /*
 // =============================================================================================
 // bf16 MFMA kernel
 // =============================================================================================
-template <typename TX, int NT, int XMODE>
+template <typename TX, int NT, int XMODE, bool TILED>
 __global__ __launch_bounds__(kBlock, 2) void gram_tall_bf16_kernel(GramArgs a) {
   constexpr int NPAIR = NT * (NT + 1) / 2;
   // LDS: per wave 4 cols x 64 rows bf16 (W fragments) + 64 f32 row weights; reused for the
@@ -252,6 +252,15 @@ __global__ __launch_bounds__(kBlock, 2) void gram_tall_bf16_kernel(GramArgs a) {
     __builtin_amdgcn_wave_barrier();
   };
   auto load = [&](int64_t r0, int64_t rows_left, bf16x8 (&fr)[NT][4]) {
+    if constexpr (TILED) {
+      // MFMA-fragment-ordered storage: superstep s, tile t, k-step i = 1 KiB contiguous
+      const u32x4* q = reinterpret_cast<const u32x4*>(a.X) + ((r0 >> 6) * NT) * 4 * 64 + lane;
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) fr[t][i] = __builtin_bit_cast(bf16x8, __builtin_nontemporal_load(q + (t * 4 + i) * 64));
+      return;
+    }
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
       if (fvalid[t]) {
@@ -280,7 +289,7 @@ __global__ __launch_bounds__(kBlock, 2) void gram_tall_bf16_kernel(GramArgs a) {
   if (do_tail) {
     bf16x8 tl[NT][4];
     const int64_t r0 = a.nsuper * 64;
-    load(r0, a.n - (r0 + 32 * h), tl);
+    load(r0, a.n - (r0 + 32 * h), tl);  // tiled storage is zero padded to a whole superstep
     compute(r0, tl);
   }
 
@@ -510,7 +519,83 @@ __global__ __launch_bounds__(1024) void gram_reduce_kernel(const double* __restr
   }
 }
 
+// feature-major [d, ld] (any dtype) -> MFMA-fragment-ordered bf16 tiles (see gram.h)
+template <typename TS>
+__global__ __launch_bounds__(256) void tile_bf16_kernel(const TS* __restrict__ X, int64_t ld, int d, int64_t n,
+                                                       int NT, int64_t nsup, uint16_t* __restrict__ out) {
+  // one thread = one 16-byte chunk (8 rows of one feature)
+  const int64_t nchunks = nsup * NT * 4 * 64;
+  for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < nchunks; c += (int64_t)gridDim.x * blockDim.x) {
+    const int lane = (int)(c & 63);
+    const int i = (int)((c >> 6) & 3);
+    const int64_t st = c >> 8;  // superstep * NT + t
+    const int t = (int)(st % NT);
+    const int64_t s = st / NT;
+    const int f = t * 32 + (lane & 31);
+    const int64_t r = s * 64 + 32 * (lane >> 5) + 8 * i;
+    bf16x8 v;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float x = 0.0f;
+      if (f < d && r + j < n) x = (float)X[(int64_t)f * ld + r + j];
+      v[j] = (__bf16)x;
+    }
+    reinterpret_cast<u32x4*>(out)[c] = __builtin_bit_cast(u32x4, v);
+  }
+}
+
+template <>
+__global__ __launch_bounds__(256) void tile_bf16_kernel<uint16_t>(const uint16_t* __restrict__ X, int64_t ld, int d,
+                                                                 int64_t n, int NT, int64_t nsup,
+                                                                 uint16_t* __restrict__ out) {
+  const int64_t nchunks = nsup * NT * 4 * 64;
+  for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < nchunks; c += (int64_t)gridDim.x * blockDim.x) {
+    const int lane = (int)(c & 63);
+    const int i = (int)((c >> 6) & 3);
+    const int64_t st = c >> 8;
+    const int t = (int)(st % NT);
+    const int64_t s = st / NT;
+    const int f = t * 32 + (lane & 31);
+    const int64_t r = s * 64 + 32 * (lane >> 5) + 8 * i;
+    u32x4 v = {0u, 0u, 0u, 0u};
+    if (f < d) {
+      if (r + 8 <= n && ((ld & 7) == 0)) {
+        v = *reinterpret_cast<const u32x4*>(X + (int64_t)f * ld + r);
+      } else {
+        uint16_t e[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) e[j] = (r + j < n) ? X[(int64_t)f * ld + r + j] : (uint16_t)0;
+        v = __builtin_bit_cast(u32x4, e);
+      }
+    }
+    reinterpret_cast<u32x4*>(out)[c] = v;
+  }
+}
+
 }  // namespace
+
+int64_t tiled_elems(int d, int64_t n) {
+  const int NT = (d + 31) / 32;
+  return ((n + 63) / 64) * NT * 4 * 64 * 8;
+}
+
+void tile_bf16(const void* X, int xdt, int64_t ld, int d, int64_t n, void* out, hipStream_t st) {
+  const int NT = (d + 31) / 32;
+  const int64_t nsup = (n + 63) / 64;
+  const int64_t nchunks = nsup * NT * 256;
+  int64_t g = (nchunks + 255) / 256;
+  if (g > 8192) g = 8192;
+  if (g < 1) g = 1;
+  uint16_t* o = reinterpret_cast<uint16_t*>(out);
+  switch (xdt) {
+    case DT_BF16: hipLaunchKernelGGL(tile_bf16_kernel<uint16_t>, dim3(g), dim3(256), 0, st, (const uint16_t*)X, ld, d, n, NT, nsup, o); break;
+    case DT_F32: hipLaunchKernelGGL(tile_bf16_kernel<float>, dim3(g), dim3(256), 0, st, (const float*)X, ld, d, n, NT, nsup, o); break;
+    case DT_F64: hipLaunchKernelGGL(tile_bf16_kernel<double>, dim3(g), dim3(256), 0, st, (const double*)X, ld, d, n, NT, nsup, o); break;
+    case DT_I32: hipLaunchKernelGGL(tile_bf16_kernel<int32_t>, dim3(g), dim3(256), 0, st, (const int32_t*)X, ld, d, n, NT, nsup, o); break;
+    default: throw std::invalid_argument("tile_bf16: unsupported dtype");
+  }
+  DQ_HIP_CHECK(hipGetLastError());
+}
 
 int64_t gram_partial_stride(int mode, int d) {
   if (mode == GRAM_F64) {
@@ -559,16 +644,18 @@ static size_t f64_lds(int d) {
 
 // Dispatch table: call F with the kernel instantiation for (mode, xdt, d, xmode).
 template <typename F>
-static void with_kernel(int mode, int xdt, int d, int xmode, F&& f) {
+static void with_kernel(int mode, int xdt, int d, int xmode, bool tiled, F&& f) {
   if (mode == GRAM_BF16) {
     const int NT = (d + 31) / 32;
-#define DQ_BF16_CASE(TX, NTV)                                                     \
-    if (xmode == 0) return f(gram_tall_bf16_kernel<TX, NTV, 0>);                  \
-    if (xmode == 1) return f(gram_tall_bf16_kernel<TX, NTV, 1>);                  \
-    return f(gram_tall_bf16_kernel<TX, NTV, 2>);
-    if (xdt == DT_BF16) { if (NT == 1) { DQ_BF16_CASE(uint16_t, 1) } else { DQ_BF16_CASE(uint16_t, 2) } }
-    if (xdt == DT_F32) { if (NT == 1) { DQ_BF16_CASE(float, 1) } else { DQ_BF16_CASE(float, 2) } }
-    if (xdt == DT_F64) { if (NT == 1) { DQ_BF16_CASE(double, 1) } else { DQ_BF16_CASE(double, 2) } }
+#define DQ_BF16_CASE(TX, NTV, TL)                                                 \
+    if (xmode == 0) return f(gram_tall_bf16_kernel<TX, NTV, 0, TL>);              \
+    if (xmode == 1) return f(gram_tall_bf16_kernel<TX, NTV, 1, TL>);              \
+    return f(gram_tall_bf16_kernel<TX, NTV, 2, TL>);
+    if (xdt == DT_BF16 && tiled) { if (NT == 1) { DQ_BF16_CASE(uint16_t, 1, true) } else { DQ_BF16_CASE(uint16_t, 2, true) } }
+    if (tiled) throw std::invalid_argument("gram_tall: tiled storage must be bf16");
+    if (xdt == DT_BF16) { if (NT == 1) { DQ_BF16_CASE(uint16_t, 1, false) } else { DQ_BF16_CASE(uint16_t, 2, false) } }
+    if (xdt == DT_F32) { if (NT == 1) { DQ_BF16_CASE(float, 1, false) } else { DQ_BF16_CASE(float, 2, false) } }
+    if (xdt == DT_F64) { if (NT == 1) { DQ_BF16_CASE(double, 1, false) } else { DQ_BF16_CASE(double, 2, false) } }
 #undef DQ_BF16_CASE
     throw std::invalid_argument("gram_tall(bf16): unsupported feature dtype");
   }
@@ -592,7 +679,7 @@ static void with_kernel(int mode, int xdt, int d, int xmode, F&& f) {
 int gram_plan_blocks(int mode, int d, int64_t n, int xdt, int xmode) {
   const size_t lds = mode == GRAM_BF16 ? bf16_lds(d) : f64_lds(d);
   int full = 1;
-  with_kernel(mode, xdt, d, xmode, [&](auto kern) { full = occupancy_blocks(kern, lds); });
+  with_kernel(mode, xdt, d, xmode, false, [&](auto kern) { full = occupancy_blocks(kern, lds); });
   // at least ~4 supersteps per wave, at most one full residency wave of blocks
   const int64_t nsuper = (n + 63) / 64;
   int64_t want = (nsuper + 4 * kWavesPerBlock - 1) / (4 * kWavesPerBlock);
@@ -609,7 +696,8 @@ void gram_tall(int mode, GramArgs a, int xmode, int blocks, double* out, hipStre
   if (a.spw < 1) a.spw = 1;
   a.P = (int)gram_partial_stride(mode, a.d);
   const size_t lds = mode == GRAM_BF16 ? bf16_lds(a.d) : f64_lds(a.d);
-  with_kernel(mode, a.xdt, a.d, xmode,
+  if (a.tiled && mode != GRAM_BF16) throw std::invalid_argument("gram_tall: tiled storage needs bf16 mode");
+  with_kernel(mode, a.xdt, a.d, xmode, a.tiled != 0,
               [&](auto kern) { hipLaunchKernelGGL(kern, dim3(blocks), dim3(kBlock), lds, st, a); });
   DQ_HIP_CHECK(hipGetLastError());
   const int T = mode == GRAM_BF16 ? 32 : 16;

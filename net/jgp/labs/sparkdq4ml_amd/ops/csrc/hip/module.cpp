@@ -42,8 +42,9 @@ PYBIND11_MODULE(_dq4ml_hip, m) {
   m.def("gram_plan_blocks", &gram_plan_blocks);
   m.def("gram_tall",
         [](int mode, uintptr_t X, int64_t ld, int d, int64_t n, int xdt, uintptr_t y, int ydt, uintptr_t w, int wdt,
-           uintptr_t sel, int xmode, uintptr_t partials, int blocks, uintptr_t out, uintptr_t stream) {
+           uintptr_t sel, int xmode, uintptr_t partials, int blocks, uintptr_t out, uintptr_t stream, int tiled) {
           GramArgs a{};
+          a.tiled = tiled;
           a.X = P<const void>(X);
           a.ld = ld;
           a.d = d;
@@ -57,6 +58,10 @@ PYBIND11_MODULE(_dq4ml_hip, m) {
           a.partials = P<double>(partials);
           gram_tall(mode, a, xmode, blocks, P<double>(out), as_stream(stream));
         });
+  m.def("tiled_elems", &tiled_elems);
+  m.def("tile_bf16", [](uintptr_t X, int xdt, int64_t ld, int d, int64_t n, uintptr_t out, uintptr_t stream) {
+    tile_bf16(P<const void>(X), xdt, ld, d, n, P<void>(out), as_stream(stream));
+  });
   m.def("gram_wide_workspace", &gram_wide_workspace);
   m.def("gram_wide",
         [](int mode, uintptr_t X, int64_t ld, int d, int64_t n, int xdt, uintptr_t scales, uintptr_t ws,

@@ -63,8 +63,33 @@ def _feature_view(X: torch.Tensor, align_elems: int):
 
 
 # ------------------------------------------------------------------------------------------
+class TiledBF16:
+    """MFMA-fragment-ordered bf16 copy of a [d, n] feature matrix (see csrc/hip/gram.h)."""
+
+    def __init__(self, buf: torch.Tensor, d: int, n: int):
+        self.buf, self.d, self.n = buf, d, n
+        self.shape = (d, n)
+        self.device = buf.device
+        self.is_cuda = True
+        self.dtype = torch.bfloat16
+
+
+def tile_bf16(X: torch.Tensor) -> TiledBF16:
+    h = native.hip()
+    _check_dev(X)
+    d, n = X.shape
+    if X.stride(1) != 1:
+        X = X.contiguous()
+    ld = X.stride(0) if d > 1 else max(n, 1)
+    buf = torch.empty(int(h.tiled_elems(d, n)), dtype=torch.bfloat16, device=X.device)
+    h.tile_bf16(X.data_ptr(), dtype_code(X), int(ld), int(d), int(n), buf.data_ptr(), _stream())
+    return TiledBF16(buf, d, n)
+
+
 def gram_stats(X, y, w, sel, compute: str = "fp64", x_zero_dead: bool = False, blocks: Optional[int] = None):
     h = native.hip()
+    if isinstance(X, TiledBF16):
+        return _gram_tiled(h, X, y, w, sel, x_zero_dead, blocks)
     _check_dev(X, y, w, sel)
     d, n = X.shape
     mode = GRAM_MODES[compute]
@@ -106,7 +131,39 @@ def gram_stats(X, y, w, sel, compute: str = "fp64", x_zero_dead: bool = False, b
     partials = torch.empty(nb * P, dtype=torch.float64, device=X.device)
     h.gram_tall(mode, Xv.data_ptr(), int(ld), int(d), int(n), dtype_code(Xv), y.data_ptr(), dtype_code(y),
                 _ptr(w), dtype_code(w) if w is not None else 0, _ptr(sel), xmode, partials.data_ptr(), nb,
-                out.data_ptr(), _stream())
+                out.data_ptr(), _stream(), 0)
+    return out
+
+
+def _prep_rows(y, w, sel, n):
+    y = y.contiguous()
+    if y.dtype not in (torch.float64, torch.float32):
+        y = y.to(torch.float64)
+    if w is not None:
+        w = w.contiguous()
+        if w.dtype not in (torch.float64, torch.float32):
+            w = w.to(torch.float64)
+    if sel is not None:
+        sel = sel.contiguous().to(torch.bool)
+    if y.numel() != n or (w is not None and w.numel() != n) or (sel is not None and sel.numel() != n):
+        raise ValueError("gram_stats: row-count mismatch")
+    return y, w, sel
+
+
+def _gram_tiled(h, T: "TiledBF16", y, w, sel, x_zero_dead, blocks):
+    d, n = T.d, T.n
+    if d > 64:
+        raise ValueError("tiled Gram supports d <= 64")
+    _check_dev(T.buf, y, w, sel)
+    y, w, sel = _prep_rows(y, w, sel, n)
+    out = torch.empty(5 + 2 * d + d * (d + 1) // 2, dtype=torch.float64, device=T.device)
+    xmode = 2 if w is not None else (1 if (sel is not None and not x_zero_dead) else 0)
+    nb = int(blocks or h.gram_plan_blocks(2, int(d), int(n), 2, xmode))
+    P = int(h.gram_partial_stride(2, d))
+    partials = torch.empty(nb * P, dtype=torch.float64, device=T.device)
+    h.gram_tall(2, T.buf.data_ptr(), 0, int(d), int(n), 2, y.data_ptr(), dtype_code(y), _ptr(w),
+                dtype_code(w) if w is not None else 0, _ptr(sel), xmode, partials.data_ptr(), nb, out.data_ptr(),
+                _stream(), 1)
     return out
 
 
