@@ -84,23 +84,24 @@ class VectorAssembleExpr(Expr):
         parts = []
         for c in cols:
             if isinstance(c.dtype, VectorUDT):
-                parts.append(c.values)
+                parts.append(c.dense())
             else:
                 parts.append(c.values.unsqueeze(0) if c.values.dim() == 1 else c.values)
         dt = _DT[self.out_dtype]
-        mat = kernels.pack_columns(parts, dt)
-        valid = None
         if self.handle_invalid == "keep":
-            for c in cols:
-                if c.valid is not None:
-                    mat = mat.clone() if mat is parts[0] else mat
-            row = 0
-            for c, p in zip(cols, parts):
-                k = p.shape[0]
-                if c.valid is not None:
-                    mat[row:row + k, ~c.valid] = float("nan")
-                row += k
-        return ColumnData(VectorUDT(), mat, valid, {"ml_attr": {"num_attrs": int(mat.shape[0])}})
+            parts = [p.to(torch.float64) for p in parts]
+            parts = [p.unsqueeze(0) if p.dim() == 1 else p for p in parts]
+            parts = [torch.where(c.valid_mask(p.device), p, torch.full_like(p, float("nan"))) if c.valid is not None
+                     else p for c, p in zip(cols, parts)]
+        d = sum(1 if p.dim() == 1 else int(p.shape[0]) for p in parts)
+        if dt == torch.bfloat16 and parts and parts[0].is_cuda and d <= 64:
+            # MI355X-native storage: MFMA-fragment-ordered tiles, dead rows zeroed (no Gram mask)
+            mat = kernels.pack_tiled(parts, ctx.table.sel)
+            meta = {"ml_attr": {"num_attrs": d}, "zero_dead": ctx.table.sel}
+        else:
+            mat = kernels.pack_columns(parts, dt)
+            meta = {"ml_attr": {"num_attrs": int(mat.shape[0])}}
+        return ColumnData(VectorUDT(), mat, None, meta)
 
 
 @param_accessors

@@ -154,7 +154,9 @@ class LinearRegression(_LRParams):
         yv, yvalid = y.values, y.valid
         if yvalid is not None:
             sel = yvalid if sel is None else (sel & yvalid)
-        flat = kernels.gram_stats(X.values, yv, w, sel, self.getOrDefault("gramDtype"))
+        zd = X.meta.get("zero_dead", False)
+        x_zero_dead = yvalid is None and (tbl.sel is None or (zd is not False and zd is tbl.sel))
+        flat = kernels.gram_stats(X.values, yv, w, sel, self.getOrDefault("gramDtype"), x_zero_dead=x_zero_dead)
         flat = comm.all_reduce_sum(flat)  # X1: data-parallel Gram all-reduce (RCCL over xGMI)
         stats = GramStats.from_flat(flat.cpu().numpy(), d)
         wls = weighted_least_squares(

@@ -88,16 +88,20 @@ PYBIND11_MODULE(_dq4ml_hip, m) {
   m.def("pack_src_bytes", []() { return (int)sizeof(PackSrc); });
 
   // ---- predict / metrics (K7/K8) ---------------------------------------------------------------
+  m.def("pack_tiled", [](uintptr_t srcs_dev, int d, int64_t n, uintptr_t sel, uintptr_t out, uintptr_t stream) {
+    pack_tiled(P<const PackSrc>(srcs_dev), d, n, P<const uint8_t>(sel), P<void>(out), as_stream(stream));
+  });
   m.def("predict", [](uintptr_t X, int xdt, int64_t ld, int d, int64_t n, uintptr_t coef, double b, uintptr_t out,
-                      uintptr_t stream) {
-    predict(P<const void>(X), xdt, ld, d, n, P<const double>(coef), b, P<double>(out), as_stream(stream));
+                      uintptr_t stream, int tiled) {
+    predict(P<const void>(X), xdt, ld, d, n, P<const double>(coef), b, P<double>(out), as_stream(stream), tiled);
   });
   m.def("metrics_blocks", &metrics_blocks);
   m.def("regression_metrics",
         [](uintptr_t X, int xdt, int64_t ld, int d, int64_t n, uintptr_t y, int ydt, uintptr_t sel, uintptr_t coef,
-           double b, double shift, uintptr_t partials, uintptr_t out, uintptr_t stream) {
+           double b, double shift, uintptr_t partials, uintptr_t out, uintptr_t stream, int tiled) {
           regression_metrics(P<const void>(X), xdt, ld, d, n, P<const void>(y), ydt, P<const uint8_t>(sel),
-                             P<const double>(coef), b, shift, P<double>(partials), P<double>(out), as_stream(stream));
+                             P<const double>(coef), b, shift, P<double>(partials), P<double>(out), as_stream(stream),
+                             tiled);
         });
 
   // ---- fused DQ chains: hipRTC whole-stage codegen ----------------------------------------------

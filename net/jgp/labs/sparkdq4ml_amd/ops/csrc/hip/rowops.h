@@ -21,11 +21,12 @@ void compact_write(const uint8_t* sel, int64_t n, const int64_t* offsets, int64_
 void pack_columns(const PackSrc* srcs_dev, int d, int64_t n, void* out, int odt, int64_t ld, const uint8_t* sel,
                   hipStream_t st);
 
+void pack_tiled(const PackSrc* srcs_dev, int d, int64_t n, const uint8_t* sel, void* out, hipStream_t st);
 void predict(const void* X, int xdt, int64_t ld, int d, int64_t n, const double* coef, double b, double* out,
-             hipStream_t st);
+             hipStream_t st, int tiled);
 int metrics_blocks(int64_t n);
 void regression_metrics(const void* X, int xdt, int64_t ld, int d, int64_t n, const void* y, int ydt,
                         const uint8_t* sel, const double* coef, double b, double shift, double* partials,
-                        double* out, hipStream_t st);
+                        double* out, hipStream_t st, int tiled);
 
 }  // namespace dq4ml

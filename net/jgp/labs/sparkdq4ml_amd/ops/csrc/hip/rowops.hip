@@ -126,29 +126,73 @@ __global__ __launch_bounds__(256) void pack_kernel(const PackSrc* __restrict__ s
 }
 
 // ---- predict / metrics -----------------------------------------------------------------------
+// element offset of (feature f, row r) in the MFMA-fragment-ordered bf16 layout (gram.h)
+__device__ __forceinline__ int64_t tiled_offset(int f, int64_t r, int NT) {
+  const int64_t s = r >> 6;
+  const int h = (int)((r >> 5) & 1), i = (int)((r >> 3) & 3), j = (int)(r & 7);
+  const int t = f >> 5, lane = 32 * h + (f & 31);
+  return ((((s * NT + t) * 4 + i) * 64 + lane) << 3) + j;
+}
+
 __device__ __forceinline__ double predict_row(const void* X, int xdt, int64_t ld, int d, const double* coef,
-                                              double b, int64_t r) {
+                                              double b, int64_t r, int tiled) {
   double acc = b;
+  if (tiled) {
+    const int NT = (d + 31) >> 5;
+    const uint16_t* xb = reinterpret_cast<const uint16_t*>(X);
+    for (int f = 0; f < d; ++f) acc += coef[f] * (double)bf16_bits_to_f32(xb[tiled_offset(f, r, NT)]);
+    return acc;
+  }
   for (int f = 0; f < d; ++f) acc += coef[f] * ld_f64(X, xdt, (int64_t)f * ld + r);
   return acc;
 }
 
+// columns (PackSrc per feature) -> tiled bf16, dead rows (sel == 0) written as zeros
+__global__ __launch_bounds__(256) void pack_tiled_kernel(const PackSrc* __restrict__ srcs, int d, int64_t n,
+                                                        const uint8_t* __restrict__ sel, int NT, int64_t nsup,
+                                                        uint16_t* __restrict__ out) {
+  const int64_t nchunks = nsup * NT * 256;
+  for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < nchunks; c += (int64_t)gridDim.x * blockDim.x) {
+    const int lane = (int)(c & 63);
+    const int i = (int)((c >> 6) & 3);
+    const int64_t st = c >> 8;
+    const int t = (int)(st % NT);
+    const int64_t s = st / NT;
+    const int f = t * 32 + (lane & 31);
+    const int64_t r = s * 64 + 32 * (lane >> 5) + 8 * i;
+    bf16x8 v;
+    if (f < d) {
+      const PackSrc src = srcs[f];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float x = 0.0f;
+        if (r + j < n && (sel == nullptr || sel[r + j] != 0)) x = (float)ld_f64(src.ptr, src.dt, r + j);
+        v[j] = (__bf16)x;
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = (__bf16)0.0f;
+    }
+    reinterpret_cast<u32x4*>(out)[c] = __builtin_bit_cast(u32x4, v);
+  }
+}
+
 __global__ __launch_bounds__(256) void predict_kernel(const void* __restrict__ X, int xdt, int64_t ld, int d,
                                                      int64_t n, const double* __restrict__ coef, double b,
-                                                     double* __restrict__ out) {
+                                                     double* __restrict__ out, int tiled) {
   for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x)
-    out[r] = predict_row(X, xdt, ld, d, coef, b, r);
+    out[r] = predict_row(X, xdt, ld, d, coef, b, r, tiled);
 }
 
 __global__ __launch_bounds__(256) void metrics_kernel(const void* __restrict__ X, int xdt, int64_t ld, int d,
                                                      int64_t n, const void* __restrict__ y, int ydt,
                                                      const uint8_t* __restrict__ sel,
                                                      const double* __restrict__ coef, double b, double shift,
-                                                     double* __restrict__ partials) {
+                                                     double* __restrict__ partials, int tiled) {
   double m[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
     if (sel != nullptr && sel[r] == 0) continue;
-    const double p = predict_row(X, xdt, ld, d, coef, b, r);
+    const double p = predict_row(X, xdt, ld, d, coef, b, r, tiled);
     const double yy = ld_f64(y, ydt, r);
     const double ys = yy - shift, ps = p - shift, res = yy - p;
     m[0] += 1.0;
@@ -215,12 +259,23 @@ void pack_columns(const PackSrc* srcs_dev, int d, int64_t n, void* out, int odt,
   DQ_HIP_CHECK(hipGetLastError());
 }
 
+void pack_tiled(const PackSrc* srcs_dev, int d, int64_t n, const uint8_t* sel, void* out, hipStream_t st) {
+  const int NT = (d + 31) / 32;
+  const int64_t nsup = (n + 63) / 64;
+  int64_t g = (nsup * NT * 256 + 255) / 256;
+  if (g > 8192) g = 8192;
+  if (g < 1) g = 1;
+  hipLaunchKernelGGL(pack_tiled_kernel, dim3(g), dim3(256), 0, st, srcs_dev, d, n, sel, NT, nsup,
+                     reinterpret_cast<uint16_t*>(out));
+  DQ_HIP_CHECK(hipGetLastError());
+}
+
 void predict(const void* X, int xdt, int64_t ld, int d, int64_t n, const double* coef, double b, double* out,
-             hipStream_t st) {
+             hipStream_t st, int tiled) {
   if (n <= 0) return;
   int64_t g = (n + 255) / 256;
   if (g > 4096) g = 4096;
-  hipLaunchKernelGGL(predict_kernel, dim3(g), dim3(256), 0, st, X, xdt, ld, d, n, coef, b, out);
+  hipLaunchKernelGGL(predict_kernel, dim3(g), dim3(256), 0, st, X, xdt, ld, d, n, coef, b, out, tiled);
   DQ_HIP_CHECK(hipGetLastError());
 }
 
@@ -233,10 +288,10 @@ int metrics_blocks(int64_t n) {
 
 void regression_metrics(const void* X, int xdt, int64_t ld, int d, int64_t n, const void* y, int ydt,
                         const uint8_t* sel, const double* coef, double b, double shift, double* partials,
-                        double* out, hipStream_t st) {
+                        double* out, hipStream_t st, int tiled) {
   const int g = metrics_blocks(n);
   hipLaunchKernelGGL(metrics_kernel, dim3(g), dim3(256), 0, st, X, xdt, ld, d, n, y, ydt, sel, coef, b, shift,
-                     partials);
+                     partials, tiled);
   hipLaunchKernelGGL(sum_slabs_kernel, dim3(1), dim3(64), 0, st, partials, g, 8, out);
   DQ_HIP_CHECK(hipGetLastError());
 }

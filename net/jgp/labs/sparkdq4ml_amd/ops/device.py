@@ -63,15 +63,7 @@ def _feature_view(X: torch.Tensor, align_elems: int):
 
 
 # ------------------------------------------------------------------------------------------
-class TiledBF16:
-    """MFMA-fragment-ordered bf16 copy of a [d, n] feature matrix (see csrc/hip/gram.h)."""
-
-    def __init__(self, buf: torch.Tensor, d: int, n: int):
-        self.buf, self.d, self.n = buf, d, n
-        self.shape = (d, n)
-        self.device = buf.device
-        self.is_cuda = True
-        self.dtype = torch.bfloat16
+from .layout import TiledBF16  # noqa: E402
 
 
 def tile_bf16(X: torch.Tensor) -> TiledBF16:
@@ -215,6 +207,50 @@ def compact_indices(sel: torch.Tensor, limit: Optional[int] = None) -> torch.Ten
     return out
 
 
+def _pack_desc(h, parts, dev):
+    rows = []
+    for p in parts:
+        _check_dev(p)
+        if p.dim() == 1:
+            p = p.unsqueeze(0)
+        for i in range(p.shape[0]):
+            r = p[i]
+            if not r.is_contiguous():
+                r = r.contiguous()
+            if r.dtype == torch.bool:
+                r = r.to(torch.uint8)
+            rows.append(r)
+    n = rows[0].numel() if rows else 0
+    for r in rows:
+        if r.numel() != n:
+            raise ValueError("pack: columns of different lengths")
+    srcb = int(h.pack_src_bytes())
+    desc = np.zeros((len(rows), srcb // 8), dtype=np.int64)
+    for i, r in enumerate(rows):
+        desc[i, 0] = r.data_ptr()
+        desc[i, 1] = dtype_code(r)
+    desc_dev = torch.from_numpy(desc.reshape(-1).view(np.uint8).copy()).to(dev)
+    return rows, n, desc_dev
+
+
+def pack_tiled(parts: List[torch.Tensor], sel: Optional[torch.Tensor] = None) -> TiledBF16:
+    h = native.hip()
+    dev = parts[0].device
+    rows, n, desc_dev = _pack_desc(h, parts, dev)
+    d = len(rows)
+    if d > 64:
+        raise ValueError("tiled bf16 storage supports d <= 64")
+    buf = torch.empty(int(h.tiled_elems(d, n)), dtype=torch.bfloat16, device=dev)
+    if sel is not None:
+        _check_dev(sel)
+        sel = sel.contiguous().to(torch.bool)
+        if sel.numel() != n:
+            raise ValueError("pack_tiled: selection length mismatch")
+    h.pack_tiled(desc_dev.data_ptr(), d, n, _ptr(sel), buf.data_ptr(), _stream())
+    del rows
+    return TiledBF16(buf, d, n)
+
+
 # ------------------------------------------------------------------------------------------
 def pack_columns(parts: List[torch.Tensor], dtype: torch.dtype, sel: Optional[torch.Tensor] = None) -> torch.Tensor:
     h = native.hip()
@@ -257,29 +293,35 @@ def _coef_dev(coef, device):
     return torch.as_tensor(np.ascontiguousarray(coef, dtype=np.float64), device=device)
 
 
-def predict(X: torch.Tensor, coef, intercept: float) -> torch.Tensor:
-    h = native.hip()
-    _check_dev(X)
-    d, n = X.shape
+def _x_args(X):
+    """(ptr, dtype code, ld, tiled flag) of a feature matrix."""
+    if isinstance(X, TiledBF16):
+        return X.buf, 2, 0, 1
     if X.stride(1) != 1:
         X = X.contiguous()
-    ld = X.stride(0) if d > 1 else max(n, 1)
+    d, n = X.shape
+    return X, dtype_code(X), (X.stride(0) if d > 1 else max(n, 1)), 0
+
+
+def predict(X, coef, intercept: float) -> torch.Tensor:
+    h = native.hip()
+    d, n = X.shape
+    Xb, xdt, ld, tiled = _x_args(X)
+    _check_dev(Xb)
     c = _coef_dev(coef, X.device)
     if c.numel() != d:
         raise ValueError("predict: coefficient length != number of features")
     out = torch.empty(n, dtype=torch.float64, device=X.device)
-    h.predict(X.data_ptr(), dtype_code(X), int(ld), int(d), int(n), c.data_ptr(), float(intercept), out.data_ptr(),
-              _stream())
+    h.predict(Xb.data_ptr(), xdt, int(ld), int(d), int(n), c.data_ptr(), float(intercept), out.data_ptr(),
+              _stream(), tiled)
     return out
 
 
 def regression_metrics(X, y, coef, intercept, sel, shift):
     h = native.hip()
-    _check_dev(X, y, sel)
     d, n = X.shape
-    if X.stride(1) != 1:
-        X = X.contiguous()
-    ld = X.stride(0) if d > 1 else max(n, 1)
+    Xb, xdt, ld, tiled = _x_args(X)
+    _check_dev(Xb, y, sel)
     y = y.contiguous()
     if sel is not None:
         sel = sel.contiguous().to(torch.bool)
@@ -287,6 +329,7 @@ def regression_metrics(X, y, coef, intercept, sel, shift):
     nb = int(h.metrics_blocks(n))
     partials = torch.empty(nb * 8, dtype=torch.float64, device=X.device)
     out = torch.empty(8, dtype=torch.float64, device=X.device)
-    h.regression_metrics(X.data_ptr(), dtype_code(X), int(ld), int(d), int(n), y.data_ptr(), dtype_code(y), _ptr(sel),
-                         c.data_ptr(), float(intercept), float(shift), partials.data_ptr(), out.data_ptr(), _stream())
+    h.regression_metrics(Xb.data_ptr(), xdt, int(ld), int(d), int(n), y.data_ptr(), dtype_code(y), _ptr(sel),
+                         c.data_ptr(), float(intercept), float(shift), partials.data_ptr(), out.data_ptr(), _stream(),
+                         tiled)
     return out

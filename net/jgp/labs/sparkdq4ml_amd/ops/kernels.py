@@ -57,6 +57,14 @@ def pack_columns(parts: Sequence[torch.Tensor], dtype: torch.dtype) -> torch.Ten
     return torch.cat([p.to(dtype) for p in parts], dim=0)
 
 
+def pack_tiled(parts: Sequence[torch.Tensor], sel: Optional[torch.Tensor] = None):
+    """GPU only: columns -> MFMA-fragment-ordered bf16 (``ops.layout.TiledBF16``); rows outside
+    ``sel`` are written as zeros."""
+    from . import device
+
+    return device.pack_tiled(list(parts), sel)
+
+
 # ------------------------------------------------------------------------------------------
 # K5 — Gram / WLS statistics
 # ------------------------------------------------------------------------------------------
@@ -72,18 +80,18 @@ def packed_upper(aa: torch.Tensor) -> torch.Tensor:
 
 
 def gram_stats(X: torch.Tensor, y: torch.Tensor, w: Optional[torch.Tensor], sel: Optional[torch.Tensor],
-               compute: str = "fp64") -> torch.Tensor:
+               compute: str = "fp64", x_zero_dead: bool = False) -> torch.Tensor:
     """Flat f64 ``[count, wSum, wwSum, bSum, bbSum, aSum[d], abSum[d], aaSum packed-upper]`` over
     live rows (``sel``), with instance weights ``w`` (default 1) — Spark WLS ``Aggregator.add`` over
     every row, in one pass.  ``X`` is feature-major ``[d, n]``."""
     d, n = X.shape
-    if y.shape[0] != n or (w is not None and w.shape[0] != n) or (sel is not None and sel.shape[0] != n):
+    if int(y.shape[0]) != n or (w is not None and w.shape[0] != n) or (sel is not None and sel.shape[0] != n):
         raise ValueError("gram_stats: row-count mismatch between features, label, weight and selection")
     if _on_gpu(X):
         from . import device
 
-        return device.gram_stats(X, y, w, sel, compute)
-    Xd = X.to(torch.float64)
+        return device.gram_stats(X, y, w, sel, compute, x_zero_dead=x_zero_dead)
+    Xd = (X.to_dense() if hasattr(X, "to_dense") else X).to(torch.float64)
     yd = y.to(torch.float64)
     wv = torch.ones(n, dtype=torch.float64) if w is None else w.to(torch.float64)
     live = torch.ones(n, dtype=torch.bool) if sel is None else sel

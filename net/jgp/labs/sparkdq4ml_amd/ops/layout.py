@@ -1,0 +1,69 @@
+"""Physical layouts of assembled feature matrices.
+
+``TiledBF16`` is the MI355X-native storage of a bf16 ``vector`` column: the MFMA-fragment order
+of ``v_mfma_f32_32x32x16_bf16`` (csrc/hip/gram.h).  For superstep ``s`` (64 rows), 32-feature tile
+``t`` and k-step ``i``, the 64 lanes' 16-byte fragments are contiguous, so the Gram kernel's
+every wave load is one contiguous KiB and the pass runs at HBM speed (measured 6.25 TB/s vs
+3.06 TB/s for the same kernel on plain feature-major storage, scripts/gram_ab.py).  Rows are
+zero padded to whole supersteps, features to whole tiles.
+
+Everything that needs individual rows (show/collect/compaction) gathers them with
+:meth:`gather_rows`; the hot consumers (Gram, predict, metrics) read the tiles directly.
+"""
+from __future__ import annotations
+
+import torch
+
+__all__ = ["TiledBF16", "tiled_offsets"]
+
+
+def tiled_offsets(feats: torch.Tensor, rows: torch.Tensor, d: int) -> torch.Tensor:
+    """Element offsets of (feature, row) pairs (broadcast) in the tiled layout."""
+    NT = (d + 31) // 32
+    s = rows >> 6
+    h = (rows >> 5) & 1
+    i = (rows >> 3) & 3
+    j = rows & 7
+    t = feats >> 5
+    lane = 32 * h + (feats & 31)
+    return ((((s * NT + t) * 4 + i) * 64 + lane) << 3) + j
+
+
+class TiledBF16:
+    def __init__(self, buf: torch.Tensor, d: int, n: int):
+        assert buf.dtype == torch.bfloat16 and buf.dim() == 1
+        self.buf, self.d, self.n = buf, int(d), int(n)
+
+    @property
+    def shape(self):
+        return (self.d, self.n)
+
+    @property
+    def device(self):
+        return self.buf.device
+
+    @property
+    def dtype(self):
+        return torch.bfloat16
+
+    @property
+    def is_cuda(self):
+        return self.buf.is_cuda
+
+    def dim(self):
+        return 2
+
+    def gather_rows(self, rows: torch.Tensor) -> torch.Tensor:
+        """Dense ``[d, k]`` bf16 of the given rows."""
+        rows = rows.to(self.buf.device, torch.int64)
+        f = torch.arange(self.d, device=self.buf.device, dtype=torch.int64).unsqueeze(1)
+        return self.buf[tiled_offsets(f, rows.unsqueeze(0), self.d)]
+
+    def to_dense(self) -> torch.Tensor:
+        return self.gather_rows(torch.arange(self.n, device=self.buf.device))
+
+    def slice_rows(self, start: int, stop: int) -> torch.Tensor:
+        return self.gather_rows(torch.arange(start, stop, device=self.buf.device))
+
+    def __repr__(self):
+        return f"TiledBF16(d={self.d}, n={self.n}, device={self.buf.device})"

@@ -121,8 +121,14 @@ def table_from_data(data, schema, device) -> Table:
                 t = torch.as_tensor(v).to(device)
                 if t.dim() == 2:
                     dt = VectorUDT()
-                    c = ColumnData(dt, t.to(torch.float64) if t.dtype not in (torch.float32, torch.bfloat16, torch.float64) else t,
-                                   None, {"ml_attr": {"num_attrs": int(t.shape[0])}})
+                    if t.dtype not in (torch.float32, torch.bfloat16, torch.float64):
+                        t = t.to(torch.float64)
+                    vals = t
+                    if t.is_cuda and t.dtype == torch.bfloat16 and t.shape[0] <= 64:
+                        from ..ops import device as _dev  # ingest into the MFMA-fragment tiled layout
+
+                        vals = _dev.tile_bf16(t)
+                    c = ColumnData(dt, vals, None, {"ml_attr": {"num_attrs": int(t.shape[0])}})
                 else:
                     dt = {torch.float64: DoubleType(), torch.float32: FloatType(), torch.int32: IntegerType(),
                           torch.int64: LongType(), torch.bool: BooleanType()}.get(t.dtype, DoubleType())

@@ -37,6 +37,12 @@ class ColumnData:
             return len(self.values)
         return int(self.values.shape[-1])
 
+    def dense(self):
+        """Feature-major dense tensor of a vector column (materializes a tiled layout)."""
+        from ..ops.layout import TiledBF16
+
+        return self.values.to_dense() if isinstance(self.values, TiledBF16) else self.values
+
     def valid_mask(self, device=None) -> torch.Tensor:
         if self.valid is not None:
             return self.valid
@@ -48,9 +54,13 @@ class ColumnData:
 
     def index(self, idx: torch.Tensor) -> "ColumnData":
         """Gather rows ``idx`` (long tensor)."""
+        from ..ops.layout import TiledBF16
+
         if isinstance(self.values, list):
             il = idx.tolist()
             vals = [self.values[i] for i in il]
+        elif isinstance(self.values, TiledBF16):
+            vals = self.values.gather_rows(idx)
         elif isinstance(self.dtype, VectorUDT):
             vals = self.values.index_select(1, idx.to(self.values.device))
         else:
@@ -59,8 +69,12 @@ class ColumnData:
         return ColumnData(self.dtype, vals, valid, dict(self.meta))
 
     def slice(self, start: int, stop: int) -> "ColumnData":
+        from ..ops.layout import TiledBF16
+
         if isinstance(self.values, list):
             vals = self.values[start:stop]
+        elif isinstance(self.values, TiledBF16):
+            vals = self.values.slice_rows(start, stop)
         elif isinstance(self.dtype, VectorUDT):
             vals = self.values[:, start:stop]
         else:
@@ -75,7 +89,7 @@ class ColumnData:
         elif isinstance(self.dtype, VectorUDT):
             from ..models.linalg import DenseVector
 
-            arr = self.values.detach().to("cpu", torch.float64).t().contiguous().numpy()
+            arr = self.dense().detach().to("cpu", torch.float64).t().contiguous().numpy()
             vals = [DenseVector(row.copy()) for row in arr]
         else:
             t = self.values.detach().cpu()

@@ -114,3 +114,34 @@ def test_predict_and_metrics():
     m = device.regression_metrics(X, y, coef, 0.25, sel, 0.1)
     mref = kernels.regression_metrics(X.cpu(), y.cpu(), coef, 0.25, sel.cpu(), 0.1)
     assert _rel(m, mref) < 1e-12
+
+
+@pytest.mark.parametrize("d", [1, 7, 32, 33, 64])
+@pytest.mark.parametrize("n", [1, 64, 1000, 100_003])
+def test_tiled_layout_roundtrip_and_gram(d, n):
+    from net.jgp.labs.sparkdq4ml_amd.ops.layout import TiledBF16
+
+    g = torch.Generator(device="cuda").manual_seed(d + 17 * n)
+    X = torch.randn(d, n, generator=g, device="cuda").to(torch.bfloat16)
+    y = torch.randn(n, generator=g, device="cuda")
+    T = device.tile_bf16(X)
+    assert isinstance(T, TiledBF16)
+    assert torch.equal(T.to_dense(), X)
+    idx = torch.tensor([0, n // 2, n - 1], device="cuda")
+    assert torch.equal(T.gather_rows(idx), X[:, idx])
+    P = device.pack_tiled([X.float()])
+    assert torch.equal(P.buf, T.buf)
+    a = device.gram_stats(T, y, None, None, "bf16")
+    b = device.gram_stats(X, y, None, None, "bf16")
+    assert torch.equal(a, b)
+    sel = torch.rand(n, generator=g, device="cuda") > 0.4
+    c = device.gram_stats(T, y, None, sel, "bf16")
+    Z = device.pack_tiled([X.float()], sel)
+    e = device.gram_stats(Z, y, None, sel, "bf16", x_zero_dead=True)
+    ref = _ref_stats(X.float(), y, None, sel)
+    assert _rel(c[5:], ref[5:]) < 2e-5 and _rel(e[5:], ref[5:]) < 2e-5
+    coef = np.linspace(-1, 1, d)
+    assert _rel(device.predict(T, coef, 0.5), kernels.predict(X.float().cpu(), coef, 0.5)) < 1e-12
+    m1 = device.regression_metrics(T, y, coef, 0.5, sel, 0.0)
+    m2 = kernels.regression_metrics(X.float().cpu(), y.cpu(), coef, 0.5, sel.cpu(), 0.0)
+    assert _rel(m1, m2) < 1e-10
