@@ -11,6 +11,7 @@ are already all-reduced across ranks; the solve itself is the native f64 host li
 """
 from __future__ import annotations
 
+import functools
 from dataclasses import dataclass
 from typing import Optional
 
@@ -81,8 +82,7 @@ class GramStats:
         return self.aaSum / self.wSum
 
     def diag_aa(self):
-        idx = np.array([j + j * (j + 1) // 2 for j in range(self.k)], dtype=np.int64)
-        return self.aaSum[idx]
+        return self.aaSum[_packed_diag_index(self.k)]
 
     @property
     def aStd(self):
@@ -104,6 +104,7 @@ class WLSModel:
     solver: str
 
 
+@functools.lru_cache(maxsize=64)
 def _packed_diag_index(k):
     return np.array([j + j * (j + 1) // 2 for j in range(k)], dtype=np.int64)
 
@@ -120,6 +121,7 @@ def _solve_cholesky(k, aa, ab):
     return x, inv
 
 
+@functools.lru_cache(maxsize=64)
 def packed_upper_indices(k):
     """(row, col) of every entry of a packed upper column-major matrix, in storage order."""
     J = np.repeat(np.arange(k), np.arange(1, k + 1))
@@ -178,8 +180,7 @@ def weighted_least_squares(stats: GramStats, fit_intercept: bool, reg_param: flo
     aBar = np.where(aStd == 0.0, 0.0, stats.aBar / safe)
     abBar = np.where(aStd == 0.0, 0.0, stats.abBar / (safe * bStd))
     aaBar = stats.aaBar.copy()
-    jj = np.concatenate([np.full(j + 1, j) for j in range(nf)]) if nf else np.zeros(0, np.int64)
-    ii = np.concatenate([np.arange(j + 1) for j in range(nf)]) if nf else np.zeros(0, np.int64)
+    ii, jj = packed_upper_indices(nf)
     denom = aStd[ii] * aStd[jj]
     aaBar = np.where(denom == 0.0, 0.0, aaBar / np.where(denom == 0.0, 1.0, denom))
 

@@ -36,9 +36,13 @@ class Params:
     # ---- core ------------------------------------------------------------------------------
     @classmethod
     def params_list(cls):
+        cached = cls.__dict__.get("_params_cache")
+        if cached is not None:
+            return cached
         out = {}
         for k in reversed(cls.__mro__):
             out.update(getattr(k, "_params", {}) or {})
+        cls._params_cache = out
         return out
 
     def _param(self, name) -> Param:

@@ -31,8 +31,16 @@ namespace dq4ml {
 
 namespace {
 
-constexpr int kBlock = 256;  // 4 waves
+constexpr int kBlock = 256;  // f64 kernel: 4 waves
 constexpr int kWavesPerBlock = kBlock / kWave;
+// bf16 kernel: one block fills a CU (fewer slabs to reduce): 16 waves at <=128 VGPRs (d <= 32),
+// 8 waves at <=256 VGPRs (d <= 64)
+template <int NT, int XMODE>
+struct BF16Geom {
+  static constexpr int kBlock = (NT == 1 && XMODE == 0) ? 1024 : 512;
+  static constexpr int kWaves = kBlock / kWave;
+};
+static int bf16_block(int d, int xmode) { return (d <= 32 && xmode == 0) ? 1024 : 512; }
 
 __device__ __forceinline__ double load_as_f64(const void* p, int dt, int64_t i) {
   switch (dt) {
@@ -163,7 +171,7 @@ __device__ __forceinline__ void weight_frags(bf16x8 (&fr)[4], const float* wl /*
 // bf16 MFMA kernel
 // =============================================================================================
 template <typename TX, int NT, int XMODE, bool TILED>
-__global__ __launch_bounds__(kBlock, 2) void gram_tall_bf16_kernel(GramArgs a) {
+__global__ __launch_bounds__(BF16Geom<NT, XMODE>::kBlock, 1) void gram_tall_bf16_kernel(GramArgs a) {
   constexpr int NPAIR = NT * (NT + 1) / 2;
   // LDS: per wave 4 cols x 64 rows bf16 (W fragments) + 64 f32 row weights; reused for the
   // block reduction afterwards.
@@ -172,7 +180,7 @@ __global__ __launch_bounds__(kBlock, 2) void gram_tall_bf16_kernel(GramArgs a) {
   const int wave = threadIdx.x >> 6;
   const int f = lane & 31, h = lane >> 5;
   __bf16* wl = reinterpret_cast<__bf16*>(smem) + wave * (4 * 64);
-  float* wrow = reinterpret_cast<float*>(smem + kWavesPerBlock * 4 * 64 * 2) + wave * 64;
+  float* wrow = reinterpret_cast<float*>(smem + BF16Geom<NT, XMODE>::kWaves * 4 * 64 * 2) + wave * 64;
 
   f32x16 acc[NPAIR];
   f32x16 accw[NT];
@@ -192,8 +200,8 @@ __global__ __launch_bounds__(kBlock, 2) void gram_tall_bf16_kernel(GramArgs a) {
     fp[t] = X + (int64_t)(fvalid[t] ? feat : 0) * a.ld + 32 * h;
   }
 
-  const int64_t gw = (int64_t)blockIdx.x * kWavesPerBlock + wave;
-  const int64_t total_waves = (int64_t)gridDim.x * kWavesPerBlock;
+  const int64_t gw = (int64_t)blockIdx.x * BF16Geom<NT, XMODE>::kWaves + wave;
+  const int64_t total_waves = (int64_t)gridDim.x * BF16Geom<NT, XMODE>::kWaves;
   int64_t s0 = gw * a.spw;
   int64_t s1 = s0 + a.spw;
   if (s1 > a.nsuper) s1 = a.nsuper;
@@ -298,13 +306,13 @@ __global__ __launch_bounds__(kBlock, 2) void gram_tall_bf16_kernel(GramArgs a) {
   const int P = a.P;
   __syncthreads();
   double* red = reinterpret_cast<double*>(smem);
-  for (int i = threadIdx.x; i < P; i += kBlock) red[i] = 0.0;
+  for (int i = threadIdx.x; i < P; i += BF16Geom<NT, XMODE>::kBlock) red[i] = 0.0;
   // scalars: wave reduce first
   double sc[5] = {ra.cnt, ra.ws, ra.wws, ra.bs, ra.bbs};
 #pragma unroll
   for (int k = 0; k < 5; ++k) sc[k] = wave_sum_f64(sc[k]);
   __syncthreads();
-  for (int wv = 0; wv < kWavesPerBlock; ++wv) {
+  for (int wv = 0; wv < BF16Geom<NT, XMODE>::kWaves; ++wv) {
     if (wave == wv) {
       if (lane == 0) {
 #pragma unroll
@@ -338,7 +346,7 @@ __global__ __launch_bounds__(kBlock, 2) void gram_tall_bf16_kernel(GramArgs a) {
     __syncthreads();
   }
   double* out = a.partials + (int64_t)blockIdx.x * P;
-  for (int i = threadIdx.x; i < P; i += kBlock) out[i] = red[i];
+  for (int i = threadIdx.x; i < P; i += BF16Geom<NT, XMODE>::kBlock) out[i] = red[i];
 }
 
 // =============================================================================================
@@ -621,17 +629,17 @@ int gram_default_blocks(int64_t n) {
 }
 
 template <typename K>
-static int occupancy_blocks(K kern, size_t lds) {
+static int occupancy_blocks(K kern, size_t lds, int block) {
   int per = 0, dev = 0, cus = 0;
-  DQ_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kern, kBlock, lds));
+  DQ_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kern, block, lds));
   DQ_HIP_CHECK(hipGetDevice(&dev));
   DQ_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
   if (per < 1) per = 1;
   return per * cus;
 }
 
-static size_t bf16_lds(int d) {
-  size_t lds = kWavesPerBlock * (4 * 64 * 2 + 64 * 4);
+static size_t bf16_lds(int d, int xmode) {
+  size_t lds = (bf16_block(d, xmode) / kWave) * (4 * 64 * 2 + 64 * 4);
   const size_t red = (size_t)gram_partial_stride(GRAM_BF16, d) * sizeof(double);
   return red > lds ? red : lds;
 }
@@ -677,12 +685,14 @@ static void with_kernel(int mode, int xdt, int d, int xmode, bool tiled, F&& f) 
 }
 
 int gram_plan_blocks(int mode, int d, int64_t n, int xdt, int xmode) {
-  const size_t lds = mode == GRAM_BF16 ? bf16_lds(d) : f64_lds(d);
+  const size_t lds = mode == GRAM_BF16 ? bf16_lds(d, xmode) : f64_lds(d);
   int full = 1;
-  with_kernel(mode, xdt, d, xmode, false, [&](auto kern) { full = occupancy_blocks(kern, lds); });
+  const int block = mode == GRAM_BF16 ? bf16_block(d, xmode) : kBlock;
+  with_kernel(mode, xdt, d, xmode, false, [&](auto kern) { full = occupancy_blocks(kern, lds, block); });
   // at least ~4 supersteps per wave, at most one full residency wave of blocks
   const int64_t nsuper = (n + 63) / 64;
-  int64_t want = (nsuper + 4 * kWavesPerBlock - 1) / (4 * kWavesPerBlock);
+  const int wpb = block / kWave;
+  int64_t want = (nsuper + 4 * wpb - 1) / (4 * wpb);
   if (want < 1) want = 1;
   return (int)(want < full ? want : full);
 }
@@ -691,14 +701,15 @@ void gram_tall(int mode, GramArgs a, int xmode, int blocks, double* out, hipStre
   if (a.d < 1 || a.d > 64) throw std::invalid_argument("gram_tall: d must be in [1, 64]");
   if (blocks < 1) throw std::invalid_argument("gram_tall: blocks must be >= 1");
   a.nsuper = a.n / 64;
-  const int64_t total_waves = (int64_t)blocks * kWavesPerBlock;
+  const int block = mode == GRAM_BF16 ? bf16_block(a.d, xmode) : kBlock;
+  const int64_t total_waves = (int64_t)blocks * (block / kWave);
   a.spw = (a.nsuper + total_waves - 1) / total_waves;
   if (a.spw < 1) a.spw = 1;
   a.P = (int)gram_partial_stride(mode, a.d);
-  const size_t lds = mode == GRAM_BF16 ? bf16_lds(a.d) : f64_lds(a.d);
+  const size_t lds = mode == GRAM_BF16 ? bf16_lds(a.d, xmode) : f64_lds(a.d);
   if (a.tiled && mode != GRAM_BF16) throw std::invalid_argument("gram_tall: tiled storage needs bf16 mode");
   with_kernel(mode, a.xdt, a.d, xmode, a.tiled != 0,
-              [&](auto kern) { hipLaunchKernelGGL(kern, dim3(blocks), dim3(kBlock), lds, st, a); });
+              [&](auto kern) { hipLaunchKernelGGL(kern, dim3(blocks), dim3(block), lds, st, a); });
   DQ_HIP_CHECK(hipGetLastError());
   const int T = mode == GRAM_BF16 ? 32 : 16;
   const int NT = (a.d + T - 1) / T;

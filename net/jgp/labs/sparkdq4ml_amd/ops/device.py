@@ -19,6 +19,15 @@ __all__ = ["dtype_code", "gram_stats", "compact_indices", "pack_columns", "predi
 _DT = {torch.float64: 0, torch.float32: 1, torch.bfloat16: 2, torch.int32: 3, torch.int64: 4, torch.uint8: 5,
        torch.bool: 5, torch.float16: 6}
 GRAM_MODES = {"fp64": 0, "fp32": 1, "bf16": 2, "fp8": 3}
+_plan_cache = {}
+
+
+def _plan_blocks(h, mode, d, n, xdt, xmode):
+    key = (torch.cuda.current_device(), mode, d, n, xdt, xmode)
+    nb = _plan_cache.get(key)
+    if nb is None:
+        nb = _plan_cache[key] = int(h.gram_plan_blocks(mode, int(d), int(n), xdt, xmode))
+    return nb
 
 
 def dtype_code(t: torch.Tensor) -> int:
@@ -118,7 +127,7 @@ def gram_stats(X, y, w, sel, compute: str = "fp64", x_zero_dead: bool = False, b
         xmode = 1
     else:
         xmode = 0
-    nb = int(blocks or h.gram_plan_blocks(mode, int(d), int(n), dtype_code(Xv), xmode))
+    nb = int(blocks or _plan_blocks(h, mode, d, n, dtype_code(Xv), xmode))
     P = int(h.gram_partial_stride(mode, d))
     partials = torch.empty(nb * P, dtype=torch.float64, device=X.device)
     h.gram_tall(mode, Xv.data_ptr(), int(ld), int(d), int(n), dtype_code(Xv), y.data_ptr(), dtype_code(y),
@@ -150,7 +159,7 @@ def _gram_tiled(h, T: "TiledBF16", y, w, sel, x_zero_dead, blocks):
     y, w, sel = _prep_rows(y, w, sel, n)
     out = torch.empty(5 + 2 * d + d * (d + 1) // 2, dtype=torch.float64, device=T.device)
     xmode = 2 if w is not None else (1 if (sel is not None and not x_zero_dead) else 0)
-    nb = int(blocks or h.gram_plan_blocks(2, int(d), int(n), 2, xmode))
+    nb = int(blocks or _plan_blocks(h, 2, d, n, 2, xmode))
     P = int(h.gram_partial_stride(2, d))
     partials = torch.empty(nb * P, dtype=torch.float64, device=T.device)
     h.gram_tall(2, T.buf.data_ptr(), 0, int(d), int(n), 2, y.data_ptr(), dtype_code(y), _ptr(w),
