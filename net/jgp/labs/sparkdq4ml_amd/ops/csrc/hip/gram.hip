@@ -171,7 +171,7 @@ __device__ __forceinline__ void weight_frags(bf16x8 (&fr)[4], const float* wl /*
 // bf16 MFMA kernel
 // =============================================================================================
 template <typename TX, int NT, int XMODE, bool TILED>
-__global__ __launch_bounds__(BF16Geom<NT, XMODE>::kBlock, 1) void gram_tall_bf16_kernel(GramArgs a) {
+__global__ __launch_bounds__((BF16Geom<NT, XMODE>::kBlock), 1) void gram_tall_bf16_kernel(GramArgs a) {
   constexpr int NPAIR = NT * (NT + 1) / 2;
   // LDS: per wave 4 cols x 64 rows bf16 (W fragments) + 64 f32 row weights; reused for the
   // block reduction afterwards.
