@@ -95,13 +95,23 @@ class GramStats:
         return np.maximum(self.diag_aa() / self.wSum - aw * aw, 0.0)
 
 
-@dataclass
 class WLSModel:
-    coefficients: np.ndarray
-    intercept: float
-    diagInvAtWA: np.ndarray
-    objectiveHistory: np.ndarray
-    solver: str
+    """Solution of the normal equations.  ``diagInvAtWA`` (needed only for the summary's standard
+    errors) is computed lazily from the retained system: the fit itself never pays for the
+    O(k^3) inverse."""
+
+    def __init__(self, coefficients, intercept, diag_inv, objective_history, solver):
+        self.coefficients = coefficients
+        self.intercept = intercept
+        self._diag_inv = diag_inv
+        self.objectiveHistory = objective_history
+        self.solver = solver
+
+    @property
+    def diagInvAtWA(self) -> np.ndarray:
+        if callable(self._diag_inv):
+            self._diag_inv = self._diag_inv()
+        return self._diag_inv
 
 
 @functools.lru_cache(maxsize=64)
@@ -110,15 +120,16 @@ def _packed_diag_index(k):
 
 
 def _solve_cholesky(k, aa, ab):
+    """-> (x, callable returning the packed inverse)."""
     h = native.host()
     if k >= DEVICE_SOLVE_MIN_K:
-        return _device_cholesky(k, aa, ab)
+        x, inv = _device_cholesky(k, aa, ab)
+        return x, (lambda: inv)
     try:
         x = h.cholesky_solve(k, aa, ab)
-        inv = h.cholesky_inverse(k, aa)
     except h.SingularMatrixError as e:
         raise SingularMatrixException(str(e)) from None
-    return x, inv
+    return x, (lambda: h.cholesky_inverse(k, aa))
 
 
 @functools.lru_cache(maxsize=64)
@@ -236,11 +247,15 @@ def weighted_least_squares(stats: GramStats, fit_intercept: bool, reg_param: flo
         coef, intercept = x.copy(), 0.0
     coef = coef * np.where(aStd != 0.0, bStd / np.where(aStd == 0, 1.0, aStd), 0.0)
     if aa_inv is not None:
-        d = []
-        for i in range(1, k + 1):
-            mult = 1.0 if (i == k and fit_intercept) else aStd[i - 1] * aStd[i - 1]
-            d.append(aa_inv[i + (i - 1) * i // 2 - 1] / (stats.wSum * mult))
-        diag_inv = np.array(d)
+        inv_fn, wsum = aa_inv, stats.wSum
+
+        def diag_inv():
+            inv = inv_fn()
+            d = []
+            for i in range(1, k + 1):
+                mult = 1.0 if (i == k and fit_intercept) else aStd[i - 1] * aStd[i - 1]
+                d.append(inv[i + (i - 1) * i // 2 - 1] / (wsum * mult))
+            return np.array(d)
     else:
         diag_inv = np.zeros(1)
     return WLSModel(coef, intercept, diag_inv, np.asarray(history, dtype=np.float64), used)

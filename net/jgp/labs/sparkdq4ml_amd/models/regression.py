@@ -165,7 +165,7 @@ class LinearRegression(_LRParams):
             "auto", int(self.getOrDefault("maxIter")), float(self.getOrDefault("tol")))
         model = LinearRegressionModel(self.uid, DenseVector(wls.coefficients), float(wls.intercept))
         self.copyValues(model)
-        model._set_summary(LinearRegressionTrainingSummary(model, df, wls.diagInvAtWA, wls.objectiveHistory,
+        model._set_summary(LinearRegressionTrainingSummary(model, df, wls, wls.objectiveHistory,
                                                            stats=stats, solver=wls.solver))
         return model
 
@@ -284,7 +284,7 @@ class LinearRegressionSummary:
     def __init__(self, model: LinearRegressionModel, df: DataFrame, diag_inv=None, stats: GramStats = None):
         self._model = model
         self._df = df
-        self._diag_inv = np.zeros(1) if diag_inv is None else np.asarray(diag_inv)
+        self._diag_src = diag_inv  # WLSModel (lazy), array, or None
         self._stats = stats
         self._m = None
         self._pred_df = None
@@ -379,6 +379,13 @@ class LinearRegressionSummary:
             w = self.predictions._table().column(self._model.getOrDefault("weightCol")).values[live]
             v = v * torch.sqrt(w.to(torch.float64))
         return _jarr([float(v.min()), float(v.max())])
+
+    @property
+    def _diag_inv(self):
+        src = self._diag_src
+        if src is None:
+            return np.zeros(1)
+        return np.asarray(src.diagInvAtWA if hasattr(src, "diagInvAtWA") else src)
 
     def _require_std_errors(self):
         if self._diag_inv.shape[0] == 1 and self._diag_inv[0] == 0:

@@ -497,32 +497,32 @@ __device__ __forceinline__ int64_t gram_src_index(int64_t k, int d, int T, int N
   return 5 + 2 * (int64_t)d + p * T * T + (i % T) * T + (j % T);
 }
 
-// 64 outputs per block; 16 slab groups of 64 threads each sum a strided share of the slabs
-// (coalesced 512-B rows), then a fixed-order LDS combine: deterministic.
+// 16 outputs per block (128-B coalesced row segments); 64 slab groups of 16 threads each load a
+// strided share of the slabs with independent loads (one latency round for <= 256 slabs), then a
+// fixed-order LDS combine: deterministic.
 __global__ __launch_bounds__(1024) void gram_reduce_kernel(const double* __restrict__ partials, int nslab, int P,
                                                           int d, int T, int NT, double* __restrict__ out) {
-  __shared__ double part[16][64];
+  __shared__ double part[64][17];
   const int64_t K = 5 + 2 * (int64_t)d + (int64_t)d * (d + 1) / 2;
-  const int c = threadIdx.x & 63, g = threadIdx.x >> 6;
-  const int64_t k = (int64_t)blockIdx.x * 64 + c;
+  const int c = threadIdx.x & 15, g = threadIdx.x >> 4;
+  const int64_t k = (int64_t)blockIdx.x * 16 + c;
   double s = 0.0;
   if (k < K) {
     const int64_t src = gram_src_index(k, d, T, NT);
     const double* p = partials + src;
     int b = g;
-    for (; b + 48 < nslab; b += 64) {
-      const double v0 = p[(int64_t)b * P], v1 = p[(int64_t)(b + 16) * P];
-      const double v2 = p[(int64_t)(b + 32) * P], v3 = p[(int64_t)(b + 48) * P];
+    for (; b + 192 < nslab; b += 256) {
+      const double v0 = p[(int64_t)b * P], v1 = p[(int64_t)(b + 64) * P];
+      const double v2 = p[(int64_t)(b + 128) * P], v3 = p[(int64_t)(b + 192) * P];
       s += (v0 + v1) + (v2 + v3);
     }
-    for (; b < nslab; b += 16) s += p[(int64_t)b * P];
+    for (; b < nslab; b += 64) s += p[(int64_t)b * P];
   }
   part[g][c] = s;
   __syncthreads();
-  if (g == 0 && k < K) {
+  if (threadIdx.x < 16 && k < K) {
     double t = 0.0;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) t += part[i][c];
+    for (int i = 0; i < 64; ++i) t += part[i][c];
     out[k] = t;
   }
 }
@@ -616,7 +616,7 @@ int64_t gram_partial_stride(int mode, int d) {
 
 static int reduce_blocks(int d) {
   const int64_t K = 5 + 2 * (int64_t)d + (int64_t)d * (d + 1) / 2;
-  return (int)((K + 63) / 64);
+  return (int)((K + 15) / 16);
 }
 
 int gram_default_blocks(int64_t n) {

@@ -21,6 +21,8 @@ for s in $STEPS; do
     tests) step tests 900 python -m pytest tests -m gpu -x -q ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" ;;
     bench) step bench 600 python bench.py --steps 20 --warmup 3 ;;
+    fitprof) step fitprof 300 env N=1.25e7 python scripts/fit_profile.py ;;
+    dist2) step dist2 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 scripts/dist_rehearsal.py ;;
     benchf32) step benchf32 600 python bench.py --steps 10 --warmup 2 --dtype fp32 ;;
     prof) cd /tmp && export TMPDIR=/tmp && cd - >/dev/null; step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 5 --warmup 1 ;;
   esac
