@@ -301,52 +301,81 @@ __global__ __launch_bounds__((BF16Geom<NT, XMODE>::kBlock), 1) void gram_tall_bf
     compute(r0, tl);
   }
 
-  // ---- block reduction (deterministic: waves add in order) ---------------------------------
+  // ---- block reduction: fixed-shape tree over the waves (deterministic), 4 rounds ------------
+  constexpr int W = BF16Geom<NT, XMODE>::kWaves;
+  constexpr int NV = (NPAIR + NT) * 16;  // f32 accumulator values per lane
   const int d = a.d;
-  const int P = a.P;
-  __syncthreads();
-  double* red = reinterpret_cast<double*>(smem);
-  for (int i = threadIdx.x; i < P; i += BF16Geom<NT, XMODE>::kBlock) red[i] = 0.0;
-  // scalars: wave reduce first
   double sc[5] = {ra.cnt, ra.ws, ra.wws, ra.bs, ra.bbs};
 #pragma unroll
   for (int k = 0; k < 5; ++k) sc[k] = wave_sum_f64(sc[k]);
-  __syncthreads();
-  for (int wv = 0; wv < BF16Geom<NT, XMODE>::kWaves; ++wv) {
-    if (wave == wv) {
-      if (lane == 0) {
+  __syncthreads();  // W stripes are dead from here on: reuse the LDS
+  float* tr = reinterpret_cast<float*>(smem);
+  double* scl = reinterpret_cast<double*>(smem + (size_t)(W / 2) * NV * 64 * sizeof(float));
+  if (lane == 0) {
 #pragma unroll
-        for (int k = 0; k < 5; ++k) red[k] += sc[k];
-      }
+    for (int k = 0; k < 5; ++k) scl[wave * 5 + k] = sc[k];
+  }
 #pragma unroll
-      for (int t = 0; t < NT; ++t) {
-        // accw[t]: rows = features t*32 + row, cols 0..3 = [w_hi, w_lo, wy_hi, wy_lo]
-        const int col = mfma32_col(lane);
+  for (int step = W / 2; step >= 1; step >>= 1) {
+    if (wave >= step && wave < 2 * step) {
+      float* dst = tr + (size_t)(wave - step) * NV * 64 + lane;
+      int v = 0;
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const float v = accw[t][r];
-          const float vn = __shfl_down(v, 1, 64);  // col+1 (same row)
-          const int feat = t * 32 + mfma32_row(lane, r);
-          if (feat < d) {
-            if (col == 0) red[5 + feat] += (double)v + (double)vn;
-            if (col == 2) red[5 + d + feat] += (double)v + (double)vn;
-          }
-        }
-      }
-      int p = 0;
+      for (int p = 0; p < NPAIR; ++p)
 #pragma unroll
-      for (int I = 0; I < NT; ++I)
+        for (int r = 0; r < 16; ++r) dst[(v++) * 64] = acc[p][r];
 #pragma unroll
-        for (int J = I; J < NT; ++J, ++p) {
-          double* tile = red + 5 + 2 * d + p * 1024;
+      for (int t = 0; t < NT; ++t)
 #pragma unroll
-          for (int r = 0; r < 16; ++r) tile[mfma32_row(lane, r) * 32 + mfma32_col(lane)] += (double)acc[p][r];
-        }
+        for (int r = 0; r < 16; ++r) dst[(v++) * 64] = accw[t][r];
+    }
+    __syncthreads();
+    if (wave < step) {
+      const float* src = tr + (size_t)wave * NV * 64 + lane;
+      int v = 0;
+#pragma unroll
+      for (int p = 0; p < NPAIR; ++p)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[p][r] += src[(v++) * 64];
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) accw[t][r] += src[(v++) * 64];
     }
     __syncthreads();
   }
-  double* out = a.partials + (int64_t)blockIdx.x * P;
-  for (int i = threadIdx.x; i < P; i += BF16Geom<NT, XMODE>::kBlock) out[i] = red[i];
+  if (wave == 0) {
+    double* out = a.partials + (int64_t)blockIdx.x * a.P;
+    if (lane < 5) {
+      double t = 0.0;
+      for (int w = 0; w < W; ++w) t += scl[w * 5 + lane];
+      out[lane] = t;
+    }
+    const int col = mfma32_col(lane);
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      // accw[t]: rows = features t*32 + row, cols 0..3 = [w_hi, w_lo, wy_hi, wy_lo]
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float v = accw[t][r];
+        const float vn = __shfl_down(v, 1, 64);  // col+1 (same row)
+        const int feat = t * 32 + mfma32_row(lane, r);
+        if (feat < d) {
+          if (col == 0) out[5 + feat] = (double)v + (double)vn;
+          if (col == 2) out[5 + d + feat] = (double)v + (double)vn;
+        }
+      }
+    }
+    int p = 0;
+#pragma unroll
+    for (int I = 0; I < NT; ++I)
+#pragma unroll
+      for (int J = I; J < NT; ++J, ++p) {
+        double* tile = out + 5 + 2 * d + p * 1024;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) tile[mfma32_row(lane, r) * 32 + col] = (double)acc[p][r];
+      }
+  }
 }
 
 // =============================================================================================
@@ -639,9 +668,11 @@ static int occupancy_blocks(K kern, size_t lds, int block) {
 }
 
 static size_t bf16_lds(int d, int xmode) {
-  size_t lds = (bf16_block(d, xmode) / kWave) * (4 * 64 * 2 + 64 * 4);
-  const size_t red = (size_t)gram_partial_stride(GRAM_BF16, d) * sizeof(double);
-  return red > lds ? red : lds;
+  const int W = bf16_block(d, xmode) / kWave;
+  const int NT = (d + 31) / 32;
+  const size_t stripes = (size_t)W * (4 * 64 * 2 + 64 * 4);
+  const size_t tree = (size_t)(W / 2) * ((NT * (NT + 1) / 2 + NT) * 16) * 64 * sizeof(float) + (size_t)W * 5 * 8;
+  return tree > stripes ? tree : stripes;
 }
 
 static size_t f64_lds(int d) {
