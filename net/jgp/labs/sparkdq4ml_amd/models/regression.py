@@ -132,6 +132,21 @@ class LinearRegression(_LRParams):
         est = self.copy(params) if params else self
         return est._train(dataset)
 
+    # persistence (params only, DefaultParamsWriter layout) -----------------------------------
+    def write(self):
+        from .persistence import ParamsWriter
+
+        return ParamsWriter(self, "org.apache.spark.ml.regression.LinearRegression")
+
+    def save(self, path):
+        self.write().save(path)
+
+    @classmethod
+    def load(cls, path):
+        from .persistence import load_params_only
+
+        return load_params_only(cls, path)
+
     def _train(self, df: DataFrame) -> "LinearRegressionModel":
         tbl, X, y = _features_label(self, df)
         d = int(X.values.shape[0])

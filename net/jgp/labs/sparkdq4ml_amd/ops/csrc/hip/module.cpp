@@ -96,6 +96,13 @@ PYBIND11_MODULE(_dq4ml_hip, m) {
     predict(P<const void>(X), xdt, ld, d, n, P<const double>(coef), b, P<double>(out), as_stream(stream), tiled);
   });
   m.def("metrics_blocks", &metrics_blocks);
+  m.def("huber_pass", [](uintptr_t X, int xdt, int64_t ld, int d, int64_t n, int tiled, uintptr_t y, int ydt, uintptr_t w,
+                         int wdt, uintptr_t sel, uintptr_t ceff, double icpt, double sigma, double eps, uintptr_t mult,
+                         uintptr_t partials, uintptr_t out, uintptr_t stream) {
+    huber_pass(P<const void>(X), xdt, ld, d, n, tiled, P<const void>(y), ydt, P<const void>(w), wdt,
+               P<const uint8_t>(sel), P<const double>(ceff), icpt, sigma, eps, P<double>(mult), P<double>(partials),
+               P<double>(out), as_stream(stream));
+  });
   m.def("regression_metrics",
         [](uintptr_t X, int xdt, int64_t ld, int d, int64_t n, uintptr_t y, int ydt, uintptr_t sel, uintptr_t coef,
            double b, double shift, uintptr_t partials, uintptr_t out, uintptr_t stream, int tiled) {

@@ -297,3 +297,87 @@ void regression_metrics(const void* X, int xdt, int64_t ld, int d, int64_t n, co
 }
 
 }  // namespace dq4ml
+
+// ---- K9: huber loss / gradient pass (LinearRegression loss="huber", Spark HuberAggregator) ------
+namespace dq4ml {
+namespace {
+
+// phase A: per row margin -> loss, per-row gradient multiplier m_r (coefficient of x_j/σ_j),
+// intercept and σ gradient contributions; 5 block partials: loss, wsum, g_icpt, g_sigma, count
+__global__ __launch_bounds__(256) void huber_rows_kernel(const void* __restrict__ X, int xdt, int64_t ld, int d,
+                                                        int64_t n, int tiled, const void* __restrict__ y, int ydt,
+                                                        const void* __restrict__ w, int wdt,
+                                                        const uint8_t* __restrict__ sel,
+                                                        const double* __restrict__ ceff /* c_j/σ_j */,
+                                                        double icpt, double sigma, double eps,
+                                                        double* __restrict__ mult, double* __restrict__ partials) {
+  double acc[4] = {0, 0, 0, 0};
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
+    double m = 0.0;
+    const bool live = sel == nullptr || sel[r] != 0;
+    const double wt = live ? (w ? ld_f64(w, wdt, r) : 1.0) : 0.0;
+    if (wt != 0.0) {
+      const double margin = predict_row(X, xdt, ld, d, ceff, icpt, r, tiled);
+      const double lin = ld_f64(y, ydt, r) - margin;
+      if (fabs(lin) <= sigma * eps) {
+        const double q = lin / sigma;
+        acc[0] += 0.5 * wt * (sigma + lin * lin / sigma);
+        m = -wt * q;
+        acc[2] += -wt * q;
+        acc[3] += 0.5 * wt * (1.0 - q * q);
+      } else {
+        const double sgn = lin >= 0 ? -1.0 : 1.0;
+        acc[0] += 0.5 * wt * (sigma + 2.0 * eps * fabs(lin) - sigma * eps * eps);
+        m = wt * sgn * eps;
+        acc[2] += wt * sgn * eps;
+        acc[3] += 0.5 * wt * (1.0 - eps * eps);
+      }
+      acc[1] += wt;
+    }
+    mult[r] = m;
+  }
+  __shared__ double red[4][4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) acc[k] = wave_sum_f64(acc[k]);
+  if ((threadIdx.x & 63) == 0) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) red[threadIdx.x >> 6][k] = acc[k];
+  }
+  __syncthreads();
+  if (threadIdx.x < 4)
+    partials[(int64_t)blockIdx.x * 4 + threadIdx.x] =
+        red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+}
+
+// phase B: out[j] = Σ_r X[j][r] * v[r]   (one block per feature, fixed-order reduction)
+__global__ __launch_bounds__(256) void xt_vec_kernel(const void* __restrict__ X, int xdt, int64_t ld, int d, int64_t n,
+                                                    int tiled, const double* __restrict__ v, double* __restrict__ out) {
+  const int j = blockIdx.x;
+  const int NT = (d + 31) >> 5;
+  double s = 0.0;
+  for (int64_t r = threadIdx.x; r < n; r += blockDim.x) {
+    const double x = tiled ? (double)bf16_bits_to_f32(reinterpret_cast<const uint16_t*>(X)[tiled_offset(j, r, NT)])
+                           : ld_f64(X, xdt, (int64_t)j * ld + r);
+    s += x * v[r];
+  }
+  __shared__ double red[4];
+  s = wave_sum_f64(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) out[j] = red[0] + red[1] + red[2] + red[3];
+}
+
+}  // namespace
+
+void huber_pass(const void* X, int xdt, int64_t ld, int d, int64_t n, int tiled, const void* y, int ydt,
+                const void* w, int wdt, const uint8_t* sel, const double* ceff, double icpt, double sigma, double eps,
+                double* mult, double* partials, double* out /* [4 + d] */, hipStream_t st) {
+  const int g = metrics_blocks(n);
+  hipLaunchKernelGGL(huber_rows_kernel, dim3(g), dim3(256), 0, st, X, xdt, ld, d, n, tiled, y, ydt, w, wdt, sel, ceff,
+                     icpt, sigma, eps, mult, partials);
+  hipLaunchKernelGGL(sum_slabs_kernel, dim3(1), dim3(64), 0, st, partials, g, 4, out);
+  hipLaunchKernelGGL(xt_vec_kernel, dim3(d), dim3(256), 0, st, X, xdt, ld, d, n, tiled, mult, out + 4);
+  DQ_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace dq4ml

@@ -272,7 +272,9 @@ QNResult quasi_newton(double bBar, double bbBar, const std::vector<double>& ab,
   };
 
   auto backtracking = [&](const State& s, const std::vector<double>& dir) {
-    const double initfval = s.value;
+    // Armijo reference: the regularized (adjusted) objective, consistent with the adjusted
+    // directional derivative used below
+    const double initfval = s.adj_value;
     const double shrink = s.iter < 1 ? 0.1 : 0.5, grow = 2.1, c1 = 1e-4, c2 = 0.9;
     double initd;
     phi(s, dir, 0.0, initd);

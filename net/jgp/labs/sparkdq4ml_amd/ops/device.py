@@ -342,3 +342,20 @@ def regression_metrics(X, y, coef, intercept, sel, shift):
                          c.data_ptr(), float(intercept), float(shift), partials.data_ptr(), out.data_ptr(), _stream(),
                          tiled)
     return out
+
+
+def huber_pass(X, y, w, sel, ceff, icpt, sigma, eps):
+    h = native.hip()
+    d, n = X.shape
+    Xb, xdt, ld, tiled = _x_args(X)
+    _check_dev(Xb, y, w, sel)
+    y, w, sel = _prep_rows(y, w, sel, n)
+    c = _coef_dev(ceff, Xb.device)
+    nb = int(h.metrics_blocks(n))
+    mult = torch.empty(n, dtype=torch.float64, device=Xb.device)
+    partials = torch.empty(nb * 4, dtype=torch.float64, device=Xb.device)
+    out = torch.empty(4 + d, dtype=torch.float64, device=Xb.device)
+    h.huber_pass(Xb.data_ptr(), xdt, int(ld), int(d), int(n), tiled, y.data_ptr(), dtype_code(y), _ptr(w),
+                 dtype_code(w) if w is not None else 0, _ptr(sel), c.data_ptr(), float(icpt), float(sigma), float(eps),
+                 mult.data_ptr(), partials.data_ptr(), out.data_ptr(), _stream())
+    return out

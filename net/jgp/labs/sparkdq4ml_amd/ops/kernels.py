@@ -140,4 +140,39 @@ def regression_metrics(X: torch.Tensor, y: torch.Tensor, coef: np.ndarray, inter
                         (r * r).sum(), r.abs().sum(), ps.sum(), (ps * ps).sum()])
 
 
+# ------------------------------------------------------------------------------------------
+# K9 — huber loss/gradient pass
+# ------------------------------------------------------------------------------------------
+def huber_pass(X, y, w, sel, ceff: np.ndarray, icpt: float, sigma: float, eps: float) -> torch.Tensor:
+    """f64 ``[lossSum, weightSum, g_intercept, g_sigma, Σ_r m_r x_r (d)]`` (Spark HuberAggregator
+    sums before division by the weight sum); ``ceff`` = coefficients / feature std."""
+    if _on_gpu(X if torch.is_tensor(X) else X.buf):
+        from . import device
+
+        return device.huber_pass(X, y, w, sel, ceff, icpt, sigma, eps)
+    Xd = (X.to_dense() if hasattr(X, "to_dense") else X).to(torch.float64)
+    yd = y.to(torch.float64)
+    n = yd.shape[0]
+    wt = torch.ones(n, dtype=torch.float64) if w is None else w.to(torch.float64)
+    if sel is not None:
+        wt = torch.where(sel, wt, torch.zeros_like(wt))
+    margin = torch.as_tensor(ceff, dtype=torch.float64) @ Xd + icpt
+    lin = yd - margin
+    inside = lin.abs() <= sigma * eps
+    q = lin / sigma
+    loss = torch.where(inside, 0.5 * wt * (sigma + lin * lin / sigma),
+                       0.5 * wt * (sigma + 2.0 * eps * lin.abs() - sigma * eps * eps))
+    sgn = torch.where(lin >= 0, -1.0, 1.0).to(torch.float64)
+    m = torch.where(inside, -wt * q, wt * sgn * eps)
+    gs = torch.where(inside, 0.5 * wt * (1.0 - q * q), 0.5 * wt * (1.0 - eps * eps) * torch.ones_like(q))
+    live = wt != 0
+    out = torch.empty(4 + Xd.shape[0], dtype=torch.float64)
+    out[0] = loss[live].sum()
+    out[1] = wt.sum()
+    out[2] = m[live].sum()
+    out[3] = gs[live].sum()
+    out[4:] = Xd @ torch.where(live, m, torch.zeros_like(m))
+    return out
+
+
 _ = (List, native)

@@ -38,3 +38,31 @@ def test_app_transcript_gpu(gpu_session, capsys):
     assert "Prediction for 40.0 guests is 218.00351106" in out
     assert "r2: 0.99653409533" in out
     assert torch.cuda.is_available()
+
+
+def _synth_tensors(n=20_000, d=6, seed=0, outliers=False):
+    g = torch.Generator().manual_seed(seed)
+    X = torch.randn(d, n, generator=g, dtype=torch.float64) + 0.5
+    y = torch.linspace(-1, 2, d, dtype=torch.float64) @ X + 0.7 + 0.3 * torch.randn(n, generator=g, dtype=torch.float64)
+    if outliers:
+        y[::50] += 40.0
+    return X, y
+
+
+@pytest.mark.parametrize("kw", [dict(solver="l-bfgs", regParam=0.05, elasticNetParam=0.5, tol=1e-10, maxIter=300),
+                                dict(loss="huber", maxIter=100), dict(solver="normal", regParam=0.1,
+                                                                       elasticNetParam=0.2)])
+def test_gpu_matches_cpu_solvers(gpu_session, kw):
+    from net.jgp.labs.sparkdq4ml_amd import LinearRegression, SparkSession
+
+    X, y = _synth_tensors(outliers="loss" in kw)
+    dfg = gpu_session.createDataFrame({"features": X.cuda(), "label": y.cuda()})
+    mg = LinearRegression(**kw).fit(dfg)
+    gpu_session.stop()
+    cpu = SparkSession.builder().master("cpu").getOrCreate()
+    mc = LinearRegression(**kw).fit(cpu.createDataFrame({"features": X, "label": y}))
+    cpu.stop()
+    import numpy as np
+
+    np.testing.assert_allclose(mg.coefficients.toArray(), mc.coefficients.toArray(), rtol=1e-6, atol=1e-8)
+    assert float(mg.intercept) == pytest.approx(float(mc.intercept), rel=1e-6, abs=1e-8)

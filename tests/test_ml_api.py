@@ -1,0 +1,134 @@
+"""Spark-ML API surface: Params, Pipeline, RegressionEvaluator, summary extras, L-BFGS path."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import data_path
+from net.jgp.labs.sparkdq4ml_amd import LinearRegression, VectorAssembler, Vectors
+from net.jgp.labs.sparkdq4ml_amd.models.evaluation import RegressionEvaluator
+from net.jgp.labs.sparkdq4ml_amd.models.pipeline import Pipeline, PipelineModel
+
+
+def _df(spark, name="dataset-full.csv"):
+    df = spark.read().format("csv").option("inferSchema", "true").load(data_path(name))
+    return df.withColumnRenamed("_c0", "guest").withColumnRenamed("_c1", "label")
+
+
+def test_params_api():
+    lr = LinearRegression()
+    assert lr.getMaxIter() == 100 and lr.getRegParam() == 0.0 and lr.getTol() == 1e-6
+    assert lr.getSolver() == "auto" and lr.getLoss() == "squaredError" and lr.getEpsilon() == 1.35
+    assert lr.uid.startswith("linReg_")
+    lr.setRegParam(1)
+    assert isinstance(lr.getRegParam(), float)
+    assert "regParam: regularization parameter" in lr.explainParams()
+    with pytest.raises(ValueError):
+        lr.setElasticNetParam(2.0)
+    assert not lr.isSet("weightCol") and lr.isSet("regParam")
+
+
+def test_pipeline_fit_transform_save(cpu_session, tmp_path):
+    df = _df(cpu_session)
+    pipe = Pipeline(stages=[VectorAssembler().setInputCols(["guest"]).setOutputCol("features"),
+                            LinearRegression().setMaxIter(40).setRegParam(1).setElasticNetParam(1)])
+    pm = pipe.fit(df)
+    out = pm.transform(df)
+    assert "prediction" in out.columns
+    lrm = pm.stages[-1]
+    assert lrm.coefficients[0] == pytest.approx(4.7559156221, rel=1e-8)
+    p = str(tmp_path / "pm")
+    pm.save(p)
+    pm2 = PipelineModel.load(p)
+    a = [r.prediction for r in pm.transform(df).select("prediction").take(5)]
+    b = [r.prediction for r in pm2.transform(df).select("prediction").take(5)]
+    assert a == b
+    pipe.save(str(tmp_path / "pipe"))
+    assert len(Pipeline.load(str(tmp_path / "pipe")).getStages()) == 2
+
+
+def test_regression_evaluator_matches_summary(cpu_session):
+    df = VectorAssembler().setInputCols(["guest"]).setOutputCol("features").transform(_df(cpu_session))
+    m = LinearRegression().fit(df)
+    pred = m.transform(df)
+    s = m.summary
+    for name, ref in (("rmse", s.rootMeanSquaredError), ("mse", s.meanSquaredError), ("r2", s.r2),
+                      ("mae", s.meanAbsoluteError), ("var", s.explainedVariance)):
+        assert RegressionEvaluator(metricName=name).evaluate(pred) == pytest.approx(float(ref), rel=1e-10)
+    assert RegressionEvaluator(metricName="r2").isLargerBetter()
+
+
+def test_summary_extras(cpu_session):
+    df = VectorAssembler().setInputCols(["guest"]).setOutputCol("features").transform(_df(cpu_session))
+    m = LinearRegression().fit(df)
+    s = m.summary
+    assert s.numInstances == 1040 and s.degreesOfFreedom == 1038
+    se, t, p = s.coefficientStandardErrors, s.tValues, s.pValues
+    assert se.shape == t.shape == p.shape == (2,)
+    # closed form OLS standard error of the slope
+    X = np.array([r.guest for r in df.select("guest").collect()], dtype=np.float64)
+    resid = s.meanSquaredError * 1040 / 1038
+    assert se[0] == pytest.approx(np.sqrt(resid / ((X - X.mean()) ** 2).sum()), rel=1e-8)
+    assert s.r2adj < s.r2
+    dr = s.devianceResiduals
+    assert dr[0] < 0 < dr[1]
+    lasso = LinearRegression().setRegParam(1).setElasticNetParam(1).fit(df).summary
+    with pytest.raises(RuntimeError):
+        _ = lasso.coefficientStandardErrors
+
+
+def _synth(spark, n=3000, d=4, seed=0, outliers=False):
+    g = torch.Generator().manual_seed(seed)
+    X = torch.randn(d, n, generator=g, dtype=torch.float64) * torch.linspace(0.5, 3, d, dtype=torch.float64).unsqueeze(1) + 1.0
+    beta = torch.linspace(-1, 2, d, dtype=torch.float64)
+    y = beta @ X + 0.7 + 0.3 * torch.randn(n, generator=g, dtype=torch.float64)
+    if outliers:
+        y[::50] += 40.0
+    return spark.createDataFrame({"features": X, "label": y}), X.numpy(), y.numpy()
+
+
+def test_lbfgs_matches_normal_equations_ols(cpu_session):
+    df, X, y = _synth(cpu_session)
+    ne = LinearRegression(solver="normal").fit(df)
+    lb = LinearRegression(solver="l-bfgs", tol=1e-12, maxIter=200).fit(df)
+    np.testing.assert_allclose(lb.coefficients.toArray(), ne.coefficients.toArray(), rtol=1e-7, atol=1e-8)
+    assert lb.intercept == pytest.approx(float(ne.intercept), rel=1e-7)
+    h = lb.summary.objectiveHistory
+    assert np.all(np.diff(h) <= 1e-12)
+
+
+@pytest.mark.parametrize("std", [True, False])
+def test_lbfgs_elasticnet_matches_sklearn(cpu_session, std):
+    from sklearn.linear_model import ElasticNet
+
+    df, X, y = _synth(cpu_session, seed=3)
+    reg, enet = 0.05, 0.5
+    m = LinearRegression(solver="l-bfgs", regParam=reg, elasticNetParam=enet, tol=1e-12, maxIter=500,
+                         standardization=std).fit(df)
+    n = X.shape[1]
+    mx, sx = X.mean(1), X.std(1, ddof=1)
+    ys = y.std(ddof=1)
+    Z = ((X - mx[:, None]) / sx[:, None]).T
+    eff = reg / ys
+    if std:
+        sk = ElasticNet(alpha=eff, l1_ratio=enet, fit_intercept=False, tol=1e-14, max_iter=100000)
+        sk.fit(Z, (y - y.mean()) / ys)
+        coef = sk.coef_ * ys / sx
+    else:  # penalty on the unstandardized coefficients: rescale columns
+        Xc = (X - mx[:, None]).T
+        sk = ElasticNet(alpha=eff, l1_ratio=enet, fit_intercept=False, tol=1e-14, max_iter=100000)
+        sk.fit(Xc, (y - y.mean()) / ys)
+        coef = sk.coef_ * ys
+    np.testing.assert_allclose(m.coefficients.toArray(), coef, rtol=2e-5, atol=1e-7)
+    assert m.intercept == pytest.approx(y.mean() - coef @ mx, rel=1e-5)
+
+
+def test_huber_robust_to_outliers(cpu_session):
+    df, X, y = _synth(cpu_session, outliers=True)
+    ols = LinearRegression(solver="normal").fit(df)
+    hub = LinearRegression(loss="huber", maxIter=200).fit(df)
+    beta = np.linspace(-1, 2, X.shape[0])
+    assert np.abs(hub.coefficients.toArray() - beta).max() < np.abs(ols.coefficients.toArray() - beta).max()
+    assert np.abs(hub.coefficients.toArray() - beta).max() < 0.05
+    assert hub.scale > 0
+    with pytest.raises(ValueError):
+        LinearRegression(loss="huber", solver="normal").fit(df)
