@@ -1,0 +1,52 @@
+"""The fused DQ codegen emits valid gfx950 HIP for the lab's chain (compiled offline with hipcc
+here; executed against the vectorized evaluator in tests/test_gpu_dqvm.py on the MI355X)."""
+import os
+import shutil
+import subprocess
+
+import pytest
+
+from conftest import data_path
+from net.jgp.labs.sparkdq4ml_amd import callUDF
+from net.jgp.labs.sparkdq4ml_amd.dq.rules import register_lab_rules
+from net.jgp.labs.sparkdq4ml_amd.ops import dqvm
+from net.jgp.labs.sparkdq4ml_amd.sql.plan import Filter, Project, execute
+
+
+def _chain(spark):
+    register_lab_rules(spark)
+    df = spark.read().format("csv").option("inferSchema", "true").load(data_path("dataset-abstract.csv"))
+    df = df.withColumnRenamed("_c0", "guest").withColumnRenamed("_c1", "price")
+    df = df.withColumn("price_no_min", callUDF("minimumPriceRule", df.col("price")))
+    df.createOrReplaceTempView("price")
+    df = spark.sql("SELECT cast(guest as int) guest, price_no_min AS price FROM price WHERE price_no_min > 0")
+    df = df.withColumn("price_correct_correl", callUDF("priceCorrelationRule", df.col("price"), df.col("guest")))
+    df.createOrReplaceTempView("price")
+    df = spark.sql("SELECT guest, price_correct_correl AS price, "
+                   "CASE WHEN price_correct_correl > 100 THEN sqrt(guest) ELSE -guest % 3 END AS x "
+                   "FROM price WHERE price_correct_correl > 0 AND guest IS NOT NULL")
+    return df
+
+
+def test_codegen_compiles(cpu_session, tmp_path):
+    df = _chain(cpu_session)
+    nodes, p = [], df._plan
+    while isinstance(p, (Project, Filter)):
+        nodes.append(p)
+        p = p.child
+    nodes.reverse()
+    base = execute(p, cpu_session)
+    src, g, outputs, sel_out = dqvm.compile_chain(nodes, base, check_device=False)
+    assert "atomicOr" not in src  # price has no nulls: rule 1 null check elided
+    assert src.count("live = live &&") == 2
+    assert sel_out is not None
+    kinds = [o[0] for o in outputs]
+    assert kinds == ["new", "new", "new"]
+    hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+    if not os.path.exists(hipcc):
+        pytest.skip("no hipcc")
+    f = tmp_path / "k.hip"
+    f.write_text("#include <hip/hip_runtime.h>\n" + src)
+    r = subprocess.run([hipcc, "--offload-arch=gfx950", "-O3", "-c", str(f), "-o", str(tmp_path / "k.o")],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr + "\n" + src
