@@ -1,0 +1,19 @@
+// K1/K2 device CSV scan (see csv_scan.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace dq4ml {
+
+// type lattice codes (same as the host scanner, csrc/host/csv.h)
+enum CsvTypeCode : int { CT_NULL = 0, CT_INT = 1, CT_LONG = 2, CT_DECIMAL = 3, CT_DOUBLE = 4, CT_BOOL = 5, CT_STRING = 6 };
+
+int64_t csv_count_blocks(int64_t n);
+// counts: csv_count_blocks(n)+1 int64 (exclusive offsets, total at [nb]); ends: total int64 or null
+void csv_line_ends(const uint8_t* buf, int64_t n, int64_t* counts, int64_t* ends, hipStream_t st);
+void csv_parse(const uint8_t* buf, int64_t n, const int64_t* ends, int64_t nlines, int ncols, uint8_t sep,
+               double* dvals, int64_t* ivals, uint8_t* valid, uint8_t* keep, uint32_t* masks, int* flags,
+               hipStream_t st);
+
+}  // namespace dq4ml

@@ -1,0 +1,267 @@
+// K1 + K2: device CSV scan with fused type inference (SURVEY.md S03 contract, numeric columns).
+//
+// Spark reads ``data/dataset-abstract.csv`` with ``inferSchema=true`` (DataQuality4MachineLearningApp
+// .java:53-55): one full pass to infer the per-column type lattice, then univocity parses every
+// line again on every action.  Here the file bytes go to HBM once and three kernels produce typed
+// columns in one parse:
+//   1. line terminators (\n, \r, \r\n — Hadoop LineRecordReader semantics; the lab's files are
+//      CR-only with no trailing terminator): per-block wave-ballot counts -> one-block scan ->
+//      ordered line-end offsets;
+//   2. one thread per line: split on the separator, parse every field speculatively as
+//      int64 AND f64 (Clinger's exact fast path: mantissa < 2^53 and |exp10| <= 22, i.e. correctly
+//      rounded like java.lang.Double.parseDouble), classify it into the lattice null < int < long <
+//      decimal < double < boolean < string, OR the class bits into a per-column mask (LDS atomics,
+//      one global atomic per block per column) — K2 fused into K1, no second pass;
+//   3. the host merges the masks into the column types (X3 all-reduce across ranks when sharded)
+//      and picks int32/int64/f64/bool arrays.  Fields outside the fast path (quotes, >19 digits,
+//      huge exponents, strings) raise a flag and the whole scan is re-done by the host scanner.
+#include <hip/hip_runtime.h>
+
+#include "common.h"
+#include "csv_scan.h"
+
+namespace dq4ml {
+
+namespace {
+
+constexpr int kChunk = 4096;  // bytes per block in the line-boundary passes
+
+__device__ __forceinline__ bool is_term(const uint8_t* b, int64_t i) {
+  const uint8_t c = b[i];
+  return c == '\r' || (c == '\n' && (i == 0 || b[i - 1] != '\r'));
+}
+
+__global__ __launch_bounds__(256) void csv_count_kernel(const uint8_t* __restrict__ b, int64_t n,
+                                                       int64_t* __restrict__ counts) {
+  __shared__ int64_t ws[4];
+  const int64_t base = (int64_t)blockIdx.x * kChunk;
+  int64_t c = 0;
+  for (int k = 0; k < kChunk / 256; ++k) {
+    const int64_t i = base + k * 256 + threadIdx.x;
+    c += __popcll(__ballot(i < n && is_term(b, i)));
+  }
+  if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) counts[blockIdx.x] = ws[0] + ws[1] + ws[2] + ws[3];
+}
+
+__global__ __launch_bounds__(1024) void csv_scan_counts_kernel(int64_t* __restrict__ counts, int64_t nb) {
+  __shared__ int64_t part[1024];
+  const int64_t per = (nb + 1023) / 1024;
+  const int64_t b0 = threadIdx.x * per, b1 = min(nb, b0 + per);
+  int64_t s = 0;
+  for (int64_t i = b0; i < b1; ++i) s += counts[i];
+  part[threadIdx.x] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int64_t run = 0;
+    for (int i = 0; i < 1024; ++i) {
+      const int64_t v = part[i];
+      part[i] = run;
+      run += v;
+    }
+    counts[nb] = run;
+  }
+  __syncthreads();
+  int64_t run = part[threadIdx.x];
+  for (int64_t i = b0; i < b1; ++i) {
+    const int64_t v = counts[i];
+    counts[i] = run;
+    run += v;
+  }
+}
+
+__global__ __launch_bounds__(256) void csv_ends_kernel(const uint8_t* __restrict__ b, int64_t n,
+                                                      const int64_t* __restrict__ offsets, int64_t* __restrict__ ends) {
+  __shared__ int64_t woff[4];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t base = (int64_t)blockIdx.x * kChunk;
+  int64_t off = offsets[blockIdx.x];
+  for (int k = 0; k < kChunk / 256; ++k) {
+    const int64_t i = base + k * 256 + threadIdx.x;
+    const bool t = i < n && is_term(b, i);
+    const uint64_t m = __ballot(t);
+    if (lane == 0) woff[wave] = __popcll(m);
+    __syncthreads();
+    int64_t before = 0;
+    for (int w = 0; w < wave; ++w) before += woff[w];
+    if (t) ends[off + before + __popcll(m & ((1ull << lane) - 1ull))] = i;
+    off += woff[0] + woff[1] + woff[2] + woff[3];
+    __syncthreads();
+  }
+}
+
+__constant__ double kPow10[23] = {1e0,  1e1,  1e2,  1e3,  1e4,  1e5,  1e6,  1e7,  1e8,  1e9,  1e10, 1e11,
+                                  1e12, 1e13, 1e14, 1e15, 1e16, 1e17, 1e18, 1e19, 1e20, 1e21, 1e22};
+
+__device__ __forceinline__ int lower(int c) { return (c >= 'A' && c <= 'Z') ? c + 32 : c; }
+
+__device__ bool match_ci(const uint8_t* p, int len, const char* w, int wl) {
+  if (len != wl) return false;
+  for (int i = 0; i < wl; ++i)
+    if (lower(p[i]) != w[i]) return false;
+  return true;
+}
+
+// classify + parse one field; returns CSV type code, sets *slow when exactness cannot be guaranteed
+__device__ int parse_field(const uint8_t* p, int len, double& dv, int64_t& iv, bool& slow) {
+  dv = 0.0;
+  iv = 0;
+  if (len == 0) return CT_NULL;
+  if (match_ci(p, len, "true", 4)) { iv = 1; dv = 1.0; return CT_BOOL; }
+  if (match_ci(p, len, "false", 5)) return CT_BOOL;
+  int i = 0;
+  bool neg = false;
+  if (p[0] == '+' || p[0] == '-') {
+    neg = p[0] == '-';
+    i = 1;
+  }
+  const int rest = len - i;
+  if (rest == 3 && p[i] == 'N' && p[i + 1] == 'a' && p[i + 2] == 'N' && i == 0) { dv = __builtin_nan(""); return CT_DOUBLE; }
+  if (rest == 8 && p[i] == 'I') {
+    const char* inf = "Infinity";
+    bool ok = true;
+    for (int k = 0; k < 8; ++k) ok &= p[i + k] == (uint8_t)inf[k];
+    if (ok) { dv = neg ? -__builtin_inf() : __builtin_inf(); return CT_DOUBLE; }
+  }
+  uint64_t mant = 0;
+  int ndig = 0, dropped_nz = 0, frac = 0, dropped = 0;
+  bool seen_digit = false, dot = false, isint = true;
+  for (; i < len; ++i) {
+    const int c = p[i];
+    if (c >= '0' && c <= '9') {
+      seen_digit = true;
+      if (ndig < 19) {
+        if (mant != 0 || c != '0') ++ndig;
+        mant = mant * 10 + (c - '0');
+      } else {
+        ++dropped;
+        dropped_nz |= (c != '0');
+      }
+      if (dot) ++frac;
+    } else if (c == '.' && !dot) {
+      dot = true;
+      isint = false;
+    } else {
+      break;
+    }
+  }
+  if (!seen_digit) return CT_STRING;
+  int exp10 = 0;
+  if (i < len && (p[i] == 'e' || p[i] == 'E')) {
+    isint = false;
+    ++i;
+    bool eneg = false;
+    if (i < len && (p[i] == '+' || p[i] == '-')) {
+      eneg = p[i] == '-';
+      ++i;
+    }
+    int ed = 0, ev = 0;
+    for (; i < len && p[i] >= '0' && p[i] <= '9'; ++i, ++ed) ev = ev < 100000 ? ev * 10 + (p[i] - '0') : ev;
+    if (ed == 0) return CT_STRING;
+    exp10 = eneg ? -ev : ev;
+  }
+  if (i < len && (p[i] == 'd' || p[i] == 'D' || p[i] == 'f' || p[i] == 'F') && i == len - 1) {
+    isint = false;
+    ++i;
+  }
+  if (i != len) return CT_STRING;
+  if (isint) {
+    if (dropped) {  // > 19 digits: decimal(p,0) — exact value needs the host path
+      slow = true;
+      return CT_DECIMAL;
+    }
+    if (mant > (uint64_t)INT64_MAX + (neg ? 1u : 0u)) {
+      slow = true;
+      return CT_DECIMAL;
+    }
+    iv = neg ? (int64_t)(0 - mant) : (int64_t)mant;
+    dv = (double)iv;
+    if (mant > (1ull << 53)) slow = true;  // dv would round
+    return (iv >= INT32_MIN && iv <= INT32_MAX) ? CT_INT : CT_LONG;
+  }
+  // double: value = mant * 10^(exp10 - frac + dropped)
+  const int e = exp10 - frac + dropped;
+  if (dropped_nz || mant >= (1ull << 53) || e < -22 || e > 22) {
+    slow = true;
+    dv = (double)mant * (e >= 0 ? pow(10.0, (double)e) : 1.0 / pow(10.0, (double)-e));
+  } else {
+    dv = e >= 0 ? (double)mant * kPow10[e] : (double)mant / kPow10[-e];
+  }
+  if (neg) dv = -dv;
+  return CT_DOUBLE;
+}
+
+constexpr int kMaxCols = 256;
+
+__global__ __launch_bounds__(256) void csv_parse_kernel(const uint8_t* __restrict__ b, int64_t n,
+                                                       const int64_t* __restrict__ ends, int64_t nlines, int ncols,
+                                                       uint8_t sep, double* __restrict__ dvals,
+                                                       int64_t* __restrict__ ivals, uint8_t* __restrict__ valid,
+                                                       uint8_t* __restrict__ keep, uint32_t* __restrict__ masks,
+                                                       int* __restrict__ flags) {
+  __shared__ uint32_t smask[kMaxCols];
+  __shared__ int sflag;
+  for (int c = threadIdx.x; c < ncols; c += blockDim.x) smask[c] = 0;
+  if (threadIdx.x == 0) sflag = 0;
+  __syncthreads();
+  for (int64_t li = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; li < nlines; li += (int64_t)gridDim.x * blockDim.x) {
+    int64_t start = 0;
+    if (li > 0) {
+      const int64_t pe = ends[li - 1];
+      start = pe + 1 + ((b[pe] == '\r' && pe + 1 < n && b[pe + 1] == '\n') ? 1 : 0);
+    }
+    const int64_t end = ends[li];  // exclusive (position of the terminator or n)
+    keep[li] = end > start;
+    int64_t pos = start;
+    bool slow = false;
+    for (int c = 0; c < ncols; ++c) {
+      double dv = 0.0;
+      int64_t iv = 0;
+      int ty = CT_NULL;
+      if (pos <= end && end > start) {
+        int64_t q = pos;
+        while (q < end && b[q] != sep) ++q;
+        const int64_t flen = q - pos;
+        if (flen > 0 && (b[pos] == '"' || b[pos] == '\\')) slow = true;
+        ty = parse_field(b + pos, (int)(flen > 1 << 20 ? 1 << 20 : flen), dv, iv, slow);
+        pos = q + 1;
+      }
+      dvals[(int64_t)c * nlines + li] = dv;
+      ivals[(int64_t)c * nlines + li] = iv;
+      valid[(int64_t)c * nlines + li] = ty != CT_NULL && ty != CT_STRING;
+      if (end > start) atomicOr(&smask[c], 1u << ty);
+    }
+    if (slow) sflag = 1;
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < ncols; c += blockDim.x)
+    if (smask[c]) atomicOr(&masks[c], smask[c]);
+  if (threadIdx.x == 0 && sflag) atomicOr(flags, 1);
+}
+
+}  // namespace
+
+int64_t csv_count_blocks(int64_t n) { return (n + kChunk - 1) / kChunk; }
+
+void csv_line_ends(const uint8_t* buf, int64_t n, int64_t* counts, int64_t* ends, hipStream_t st) {
+  const int64_t nb = csv_count_blocks(n);
+  hipLaunchKernelGGL(csv_count_kernel, dim3(nb), dim3(256), 0, st, buf, n, counts);
+  hipLaunchKernelGGL(csv_scan_counts_kernel, dim3(1), dim3(1024), 0, st, counts, nb);
+  if (ends != nullptr) hipLaunchKernelGGL(csv_ends_kernel, dim3(nb), dim3(256), 0, st, buf, n, counts, ends);
+  DQ_HIP_CHECK(hipGetLastError());
+}
+
+void csv_parse(const uint8_t* buf, int64_t n, const int64_t* ends, int64_t nlines, int ncols, uint8_t sep,
+               double* dvals, int64_t* ivals, uint8_t* valid, uint8_t* keep, uint32_t* masks, int* flags,
+               hipStream_t st) {
+  if (ncols > kMaxCols) throw std::invalid_argument("csv_parse: too many columns for the device scanner");
+  if (nlines <= 0) return;
+  int64_t g = (nlines + 255) / 256;
+  if (g > 16384) g = 16384;
+  hipLaunchKernelGGL(csv_parse_kernel, dim3(g), dim3(256), 0, st, buf, n, ends, nlines, ncols, sep, dvals, ivals,
+                     valid, keep, masks, flags);
+  DQ_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace dq4ml

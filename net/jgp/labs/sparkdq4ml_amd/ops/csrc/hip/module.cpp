@@ -6,6 +6,7 @@
 #include <pybind11/stl.h>
 
 #include "common.h"
+#include "csv_scan.h"
 #include "dqvm.h"
 #include "gram.h"
 #include "gram_wide.h"
@@ -110,6 +111,19 @@ PYBIND11_MODULE(_dq4ml_hip, m) {
                              P<const double>(coef), b, shift, P<double>(partials), P<double>(out), as_stream(stream),
                              tiled);
         });
+
+  // ---- CSV scan (K1/K2) ------------------------------------------------------------------------
+  m.def("csv_count_blocks", &csv_count_blocks);
+  m.def("csv_line_ends", [](uintptr_t buf, int64_t n, uintptr_t counts, uintptr_t ends, uintptr_t stream) {
+    csv_line_ends(P<const uint8_t>(buf), n, P<int64_t>(counts), P<int64_t>(ends), as_stream(stream));
+  });
+  m.def("csv_parse", [](uintptr_t buf, int64_t n, uintptr_t ends, int64_t nlines, int ncols, int sep, uintptr_t dvals,
+                        uintptr_t ivals, uintptr_t valid, uintptr_t keep, uintptr_t masks, uintptr_t flags,
+                        uintptr_t stream) {
+    csv_parse(P<const uint8_t>(buf), n, P<const int64_t>(ends), nlines, ncols, (uint8_t)sep, P<double>(dvals),
+              P<int64_t>(ivals), P<uint8_t>(valid), P<uint8_t>(keep), P<uint32_t>(masks), P<int>(flags),
+              as_stream(stream));
+  });
 
   // ---- fused DQ chains: hipRTC whole-stage codegen ----------------------------------------------
   m.def("rtc_compile", [](const std::string& src, const std::string& entry) {

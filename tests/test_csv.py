@@ -1,0 +1,124 @@
+"""CSV reader contract: host scanner on CPU, device scanner (K1/K2) on the MI355X."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import data_path
+from net.jgp.labs.sparkdq4ml_amd.ops import native
+from net.jgp.labs.sparkdq4ml_amd.ops.csvscan import merge_type_mask, shard_byte_range
+
+CASES = {
+    "cr_only": b"1,23.1\r2,30.0\r3,34.5",
+    "lf_trailing": b"1,2.5\n-3,4e2\n7,-0.125\n",
+    "crlf": b"10,1\r\n20,2\r\n30,3.75\r\n",
+    "empty_lines": b"1,2\n\n3,4\n\n",
+    "short_rows": b"1,2,3\n4,5\n6\n",
+    "long_ints": b"1,3000000000\n2,-5\n",
+    "nulls": b"1,,3\n,2.5,\n",
+    "bools": b"true,1\nFALSE,2\n",
+    "special": b"NaN,1\n-Infinity,2\n1.5d,3\n",
+}
+
+
+def _host(data, infer=True):
+    n, cols = native.host().csv_scan(data, infer=infer)
+    return n, [(c[0], c[1], c[2], c[3]) for c in cols]
+
+
+def test_type_lattice():
+    h = native.host()
+    assert h.csv_infer_field("12") == 1 and h.csv_infer_field("3000000000") == 2
+    assert h.csv_infer_field("123456789012345678901234") == 3 and h.csv_infer_field("1.5") == 4
+    assert h.csv_infer_field("true") == 5 and h.csv_infer_field("abc") == 6 and h.csv_infer_field("") == 0
+    assert h.csv_merge_types(1, 4) == 4 and h.csv_merge_types(1, 2) == 2 and h.csv_merge_types(5, 1) == 6
+    assert merge_type_mask(0b10010) == 4 and merge_type_mask(0b100000) == 5 and merge_type_mask(0b100010) == 6
+
+
+def test_host_cases():
+    n, cols = _host(CASES["cr_only"])
+    assert n == 3 and [c[1] for c in cols] == [1, 4]
+    n, cols = _host(CASES["empty_lines"])
+    assert n == 2
+    n, cols = _host(CASES["short_rows"])
+    assert n == 3 and list(cols[2][3]) == [1, 0, 0] and list(cols[1][3]) == [1, 1, 0]
+    n, cols = _host(CASES["long_ints"])
+    assert cols[1][1] == 2
+    n, cols = _host(CASES["nulls"])
+    assert list(cols[0][3]) == [1, 0] and list(cols[1][3]) == [0, 1]
+    n, cols = _host(b'"a,b",1\n"c""d",2\n')
+    assert cols[0][1] == 6 and cols[0][2] == ["a,b", 'c"d']
+
+
+def test_reader_schema_and_options(cpu_session, tmp_path):
+    df = cpu_session.read().format("csv").option("inferSchema", "true").option("header", "false") \
+        .load(data_path("dataset-full.csv"))
+    assert [(f.name, f.dataType.simpleString()) for f in df.schema.fields] == [("_c0", "int"), ("_c1", "double")]
+    assert df.count() == 1040
+    p = tmp_path / "h.csv"
+    p.write_bytes(b"a;b\n1;x\n2;y\n")
+    df = cpu_session.read().option("header", "true").option("sep", ";").csv(str(p))
+    assert df.columns == ["a", "b"] and [r.b for r in df.collect()] == ["x", "y"]
+    df = cpu_session.read().schema("a double, b string").option("sep", ";").option("header", "true").csv(str(p))
+    assert df.schema.fields[0].dataType.simpleString() == "double"
+    # no inferSchema: all strings
+    df = cpu_session.read().csv(data_path("dataset-small.csv"))
+    assert df.dtypes == [("_c0", "string"), ("_c1", "string")]
+
+
+def test_shard_byte_range_covers_rows():
+    data = open(data_path("dataset-full.csv"), "rb").read()
+    for world in (2, 3, 8):
+        spans = [shard_byte_range(data, r, world) for r in range(world)]
+        assert spans[0][0] == 0 and spans[-1][1] == len(data)
+        assert all(spans[i][1] == spans[i + 1][0] for i in range(world - 1))
+        rows = sum(_host(data[lo:hi])[0] for lo, hi in spans)
+        assert rows == 1040
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", sorted(CASES) + ["dataset-small.csv", "dataset-abstract.csv", "dataset-full.csv"])
+def test_device_scan_matches_host(name):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from net.jgp.labs.sparkdq4ml_amd.ops import csvscan
+
+    data = CASES[name] if name in CASES else open(data_path(name), "rb").read()
+    t = csvscan.scan_device(data, device="cuda")
+    n, cols = _host(data)
+    if any(c[1] in (3, 6) for c in cols):
+        assert t is None  # strings / decimals go to the host scanner
+        return
+    assert t is not None and t.nrows == n
+    for (name_, code, vals, valid), c in zip(cols, t.columns):
+        v = c.valid_mask().cpu().numpy()
+        assert list(v.astype(int)) == list(valid.astype(int))
+        got = c.values.cpu().numpy()
+        ref = np.asarray(vals)
+        if code == 5:
+            ref = ref.astype(bool)
+        np.testing.assert_array_equal(np.where(valid.astype(bool), got.astype(np.float64), 0),
+                                      np.where(valid.astype(bool), ref.astype(np.float64), 0))
+
+
+@pytest.mark.gpu
+def test_device_scan_through_reader(tmp_path):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from net.jgp.labs.sparkdq4ml_amd import SparkSession
+
+    s = SparkSession.getActiveSession()
+    if s is not None:
+        s.stop()
+    rng = np.random.default_rng(0)
+    n = 200_000
+    a = rng.integers(-1000, 1000, n)
+    b = np.round(rng.normal(size=n), 4)
+    p = tmp_path / "big.csv"
+    p.write_text("\n".join(f"{x},{y!r}" for x, y in zip(a, b)))
+    spark = SparkSession.builder().master("mi355x[*]").config("dq4ml.csv.deviceThresholdBytes", 0).getOrCreate()
+    df = spark.read().option("inferSchema", "true").csv(str(p))
+    t = df._table()
+    assert t.columns[0].values.is_cuda and df.dtypes == [("_c0", "int"), ("_c1", "double")]
+    np.testing.assert_array_equal(t.columns[0].values.cpu().numpy(), a)
+    np.testing.assert_array_equal(t.columns[1].values.cpu().numpy(), b)
+    spark.stop()
