@@ -24,7 +24,7 @@ from .param import Param, Params, param_accessors
 __all__ = ["VectorAssembler", "VectorAssembleExpr"]
 
 _DT = {"float64": torch.float64, "double": torch.float64, "float32": torch.float32, "float": torch.float32,
-       "bfloat16": torch.bfloat16, "bf16": torch.bfloat16}
+       "bfloat16": torch.bfloat16, "bf16": torch.bfloat16, "float8": torch.float8_e4m3fn, "fp8": torch.float8_e4m3fn}
 
 
 class VectorAssembleExpr(Expr):
@@ -94,10 +94,18 @@ class VectorAssembleExpr(Expr):
             parts = [torch.where(c.valid_mask(p.device), p, torch.full_like(p, float("nan"))) if c.valid is not None
                      else p for c, p in zip(cols, parts)]
         d = sum(1 if p.dim() == 1 else int(p.shape[0]) for p in parts)
-        if dt == torch.bfloat16 and parts and parts[0].is_cuda and d <= 64:
+        on_dev = bool(parts) and parts[0].is_cuda
+        if dt == torch.bfloat16 and on_dev and d <= 64:
             # MI355X-native storage: MFMA-fragment-ordered tiles, dead rows zeroed (no Gram mask)
             mat = kernels.pack_tiled(parts, ctx.table.sel)
             meta = {"ml_attr": {"num_attrs": d}, "zero_dead": ctx.table.sel}
+        elif on_dev and (dt == torch.float8_e4m3fn or (dt == torch.bfloat16 and d > 64)):
+            # wide fragment layout for the LDS-tiled MFMA SYRK (fp8: per-feature scales)
+            mat = kernels.pack_wide(parts, 8 if dt == torch.float8_e4m3fn else 16, ctx.table.sel)
+            meta = {"ml_attr": {"num_attrs": d}, "zero_dead": ctx.table.sel}
+        elif dt == torch.float8_e4m3fn:  # host engine: fp8 storage is a device layout; keep fp32
+            mat = kernels.pack_columns(parts, torch.float32)
+            meta = {"ml_attr": {"num_attrs": int(mat.shape[0])}}
         else:
             mat = kernels.pack_columns(parts, dt)
             meta = {"ml_attr": {"num_attrs": int(mat.shape[0])}}
@@ -113,7 +121,7 @@ class VectorAssembler(Params):
         "handleInvalid": Param("handleInvalid", "how to handle invalid data (NULL values): error, skip or keep",
                                "error", lambda v: v in ("error", "skip", "keep")),
         "outputDtype": Param("outputDtype", "device storage dtype of the assembled matrix "
-                                            "(float64 | float32 | bfloat16)", "float64", lambda v: v in _DT),
+                                            "(float64 | float32 | bfloat16 | float8)", "float64", lambda v: v in _DT),
     }
 
     def __init__(self, inputCols=None, outputCol=None, handleInvalid=None, outputDtype=None, uid=None):

@@ -6,8 +6,32 @@
 
 namespace dq4ml {
 
-int64_t gram_wide_workspace(int mode, int d, int64_t n);
-void gram_wide(int mode, const void* X, int64_t ld, int d, int64_t n, int xdt, const float* scales, void* ws,
-               int64_t ws_bytes, double* out_full, hipStream_t st);
+struct PackSrcW {
+  const void* ptr;
+  int dt;
+  int pad;
+};
+
+struct WideArgs {
+  const unsigned char* X;     // wide tiled storage, NT = npanels * 8 tiles
+  const unsigned char* Xaug;  // 1-tile tiled storage of [1, y_hi, y_lo] (same element type)
+  int NT;
+  int npanels;                // ceil(d / 256)
+  int d;
+  int64_t nsup;               // supersteps (64 rows)
+  int splitk;
+  const int* pairs;           // [npair][2] panel pairs I <= J over [0, npanels] (npanels = augmentation)
+  float* part;                // [npair * splitk][256][256] f32 partial tiles
+  double aug_scale[3];        // scales of [1, y_hi, y_lo]
+};
+
+int64_t wide_tiled_bytes(int eb, int d, int64_t n);
+int64_t gram_wide_partials(int d, int splitk);
+void feature_amax(const PackSrcW* srcs_dev, int d, int64_t n, const uint8_t* sel, float* amax, hipStream_t st);
+// eb = 16 (bf16) or 8 (fp8 e4m3, values multiplied by inv_scale[f] before conversion)
+void pack_wide(int eb, const PackSrcW* srcs_dev, int d, int64_t n, int nt, const uint8_t* sel, const float* inv_scale,
+               void* out, hipStream_t st);
+// out: flat WLS layout [count, wSum, wwSum, bSum, bbSum, aSum(d), abSum(d), aa packed-upper(d)]
+void gram_wide(int eb, WideArgs a, const int* pairs_dev, const float* scales, double* out, hipStream_t st);
 
 }  // namespace dq4ml

@@ -63,13 +63,33 @@ PYBIND11_MODULE(_dq4ml_hip, m) {
   m.def("tile_bf16", [](uintptr_t X, int xdt, int64_t ld, int d, int64_t n, uintptr_t out, uintptr_t stream) {
     tile_bf16(P<const void>(X), xdt, ld, d, n, P<void>(out), as_stream(stream));
   });
-  m.def("gram_wide_workspace", &gram_wide_workspace);
-  m.def("gram_wide",
-        [](int mode, uintptr_t X, int64_t ld, int d, int64_t n, int xdt, uintptr_t scales, uintptr_t ws,
-           int64_t ws_bytes, uintptr_t out, uintptr_t stream) {
-          gram_wide(mode, P<const void>(X), ld, d, n, xdt, P<const float>(scales), P<void>(ws), ws_bytes,
-                    P<double>(out), as_stream(stream));
-        });
+  m.def("wide_tiled_bytes", &wide_tiled_bytes);
+  m.def("gram_wide_partials", &gram_wide_partials);
+  m.def("pack_wide", [](int eb, uintptr_t srcs_dev, int d, int64_t n, int nt, uintptr_t sel, uintptr_t inv_scale,
+                        uintptr_t out, uintptr_t stream) {
+    pack_wide(eb, P<const PackSrcW>(srcs_dev), d, n, nt, P<const uint8_t>(sel), P<const float>(inv_scale), P<void>(out),
+              as_stream(stream));
+  });
+  m.def("feature_amax", [](uintptr_t srcs_dev, int d, int64_t n, uintptr_t sel, uintptr_t amax, uintptr_t stream) {
+    feature_amax(P<const PackSrcW>(srcs_dev), d, n, P<const uint8_t>(sel), P<float>(amax), as_stream(stream));
+  });
+  m.def("gram_wide", [](int eb, uintptr_t X, uintptr_t Xaug, int nt, int npanels, int d, int64_t nsup, int splitk,
+                        uintptr_t pairs, uintptr_t part, double s1, double syh, double syl, uintptr_t scales,
+                        uintptr_t out, uintptr_t stream) {
+    WideArgs a{};
+    a.X = P<const unsigned char>(X);
+    a.Xaug = P<const unsigned char>(Xaug);
+    a.NT = nt;
+    a.npanels = npanels;
+    a.d = d;
+    a.nsup = nsup;
+    a.splitk = splitk;
+    a.part = P<float>(part);
+    a.aug_scale[0] = s1;
+    a.aug_scale[1] = syh;
+    a.aug_scale[2] = syl;
+    gram_wide(eb, a, P<const int>(pairs), P<const float>(scales), P<double>(out), as_stream(stream));
+  });
 
   // ---- compaction (K3) -----------------------------------------------------------------------
   m.def("compact_blocks", &compact_blocks);

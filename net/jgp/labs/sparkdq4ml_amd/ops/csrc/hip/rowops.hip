@@ -134,9 +134,31 @@ __device__ __forceinline__ int64_t tiled_offset(int f, int64_t r, int NT) {
   return ((((s * NT + t) * 4 + i) * 64 + lane) << 3) + j;
 }
 
+// wide layouts (gram_wide.hip): k-step ki = 16 contiguous rows, 8 B (fp8) / 16 B (bf16) per lane
+__device__ __forceinline__ int64_t wide_offset(int f, int64_t r, int NT) {
+  const int64_t s = r >> 6;
+  const int ki = (int)((r >> 4) & 3), h = (int)((r >> 3) & 1), j = (int)(r & 7);
+  const int t = f >> 5, lane = 32 * h + (f & 31);
+  return ((((s * NT + t) * 4 + ki) * 64 + lane) << 3) + j;  // element index
+}
+
+__device__ __forceinline__ float fp8_to_f32(uint8_t v) {
+  return __builtin_amdgcn_cvt_f32_fp8((int)v, 0);
+}
+
 __device__ __forceinline__ double predict_row(const void* X, int xdt, int64_t ld, int d, const double* coef,
                                               double b, int64_t r, int tiled) {
   double acc = b;
+  if (tiled == 2 || tiled == 3) {  // wide bf16 / wide fp8 (coef pre-multiplied by the fp8 scales)
+    const int NT = ((d + 255) >> 8) * 8;
+    for (int f = 0; f < d; ++f) {
+      const int64_t o = wide_offset(f, r, NT);
+      const float x = tiled == 2 ? bf16_bits_to_f32(reinterpret_cast<const uint16_t*>(X)[o])
+                                 : fp8_to_f32(reinterpret_cast<const uint8_t*>(X)[o]);
+      acc += coef[f] * (double)x;
+    }
+    return acc;
+  }
   if (tiled) {
     const int NT = (d + 31) >> 5;
     const uint16_t* xb = reinterpret_cast<const uint16_t*>(X);
@@ -356,8 +378,11 @@ __global__ __launch_bounds__(256) void xt_vec_kernel(const void* __restrict__ X,
   const int NT = (d + 31) >> 5;
   double s = 0.0;
   for (int64_t r = threadIdx.x; r < n; r += blockDim.x) {
-    const double x = tiled ? (double)bf16_bits_to_f32(reinterpret_cast<const uint16_t*>(X)[tiled_offset(j, r, NT)])
-                           : ld_f64(X, xdt, (int64_t)j * ld + r);
+    double x;
+    if (tiled == 1) x = (double)bf16_bits_to_f32(reinterpret_cast<const uint16_t*>(X)[tiled_offset(j, r, NT)]);
+    else if (tiled == 2) x = (double)bf16_bits_to_f32(reinterpret_cast<const uint16_t*>(X)[wide_offset(j, r, ((d + 255) >> 8) * 8)]);
+    else if (tiled == 3) x = (double)fp8_to_f32(reinterpret_cast<const uint8_t*>(X)[wide_offset(j, r, ((d + 255) >> 8) * 8)]);
+    else x = ld_f64(X, xdt, (int64_t)j * ld + r);
     s += x * v[r];
   }
   __shared__ double red[4];

@@ -18,6 +18,7 @@ from . import native
 __all__ = ["scan_device", "merge_type_mask", "shard_byte_range"]
 
 CT_NULL, CT_INT, CT_LONG, CT_DECIMAL, CT_DOUBLE, CT_BOOL, CT_STRING = range(7)
+STATS = {"device_scans": 0, "fallbacks": 0}
 
 
 def merge_type_mask(mask: int) -> int:
@@ -96,10 +97,13 @@ def scan_device(data: bytes, sep: str = ",", infer: bool = True, device=None, nc
     fl = int(flags.item())
     mk = masks.cpu().numpy().astype(np.int64)
     if fl:
+        STATS["fallbacks"] += 1
         return None
     types = [merge_type_mask(m) for m in mk]
     if any(t in (CT_STRING, CT_DECIMAL) for t in types):
+        STATS["fallbacks"] += 1
         return None
+    STATS["device_scans"] += 1
     fields, cols = [], []
     for c, t in enumerate(types):
         v = valid[c, :nlines]

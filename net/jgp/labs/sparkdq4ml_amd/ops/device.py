@@ -72,7 +72,9 @@ def _feature_view(X: torch.Tensor, align_elems: int):
 
 
 # ------------------------------------------------------------------------------------------
-from .layout import TiledBF16  # noqa: E402
+from .layout import TiledBF16, TiledWide  # noqa: E402
+
+FP8_MAX = 448.0
 
 
 def tile_bf16(X: torch.Tensor) -> TiledBF16:
@@ -89,6 +91,8 @@ def tile_bf16(X: torch.Tensor) -> TiledBF16:
 
 def gram_stats(X, y, w, sel, compute: str = "fp64", x_zero_dead: bool = False, blocks: Optional[int] = None):
     h = native.hip()
+    if isinstance(X, TiledWide):
+        return _gram_wide(h, X, y, w, sel, x_zero_dead)
     if isinstance(X, TiledBF16):
         return _gram_tiled(h, X, y, w, sel, x_zero_dead, blocks)
     _check_dev(X, y, w, sel)
@@ -98,9 +102,10 @@ def gram_stats(X, y, w, sel, compute: str = "fp64", x_zero_dead: bool = False, b
     if n == 0:
         out.zero_()
         return out
+    if d > 64 and mode in (2, 3) and w is None:
+        # ingest into the wide fragment layout once, then the LDS-tiled MFMA SYRK
+        return _gram_wide(h, tile_wide(X, 16 if mode == 2 else 8, sel), y, None, sel, True)
     if d > 64 or mode in (1, 3):
-        from . import kernels
-
         return _gram_fallback_wide(X, y, w, sel, compute)
     if mode == 2 and X.dtype not in (torch.bfloat16, torch.float32, torch.float64):
         X = X.to(torch.float32)
@@ -233,8 +238,7 @@ def _pack_desc(h, parts, dev):
     for r in rows:
         if r.numel() != n:
             raise ValueError("pack: columns of different lengths")
-    srcb = int(h.pack_src_bytes())
-    desc = np.zeros((len(rows), srcb // 8), dtype=np.int64)
+    desc = np.zeros((len(rows), 2), dtype=np.int64)  # PackSrcW {ptr, dt, pad}
     for i, r in enumerate(rows):
         desc[i, 0] = r.data_ptr()
         desc[i, 1] = dtype_code(r)
@@ -303,7 +307,10 @@ def _coef_dev(coef, device):
 
 
 def _x_args(X):
-    """(ptr, dtype code, ld, tiled flag) of a feature matrix."""
+    """(ptr, dtype code, ld, tiled flag) of a feature matrix (fp8 wide: the caller pre-scales the
+    coefficients by ``X.scales``)."""
+    if isinstance(X, TiledWide):
+        return X.buf, 2, 0, 2 if X.eb == 16 else 3
     if isinstance(X, TiledBF16):
         return X.buf, 2, 0, 1
     if X.stride(1) != 1:
@@ -320,6 +327,8 @@ def predict(X, coef, intercept: float) -> torch.Tensor:
     c = _coef_dev(coef, X.device)
     if c.numel() != d:
         raise ValueError("predict: coefficient length != number of features")
+    if isinstance(X, TiledWide) and X.eb == 8:
+        c = c * X.scales.to(torch.float64)
     out = torch.empty(n, dtype=torch.float64, device=X.device)
     h.predict(Xb.data_ptr(), xdt, int(ld), int(d), int(n), c.data_ptr(), float(intercept), out.data_ptr(),
               _stream(), tiled)
@@ -335,6 +344,8 @@ def regression_metrics(X, y, coef, intercept, sel, shift):
     if sel is not None:
         sel = sel.contiguous().to(torch.bool)
     c = _coef_dev(coef, X.device)
+    if isinstance(X, TiledWide) and X.eb == 8:
+        c = c * X.scales.to(torch.float64)
     nb = int(h.metrics_blocks(n))
     partials = torch.empty(nb * 8, dtype=torch.float64, device=X.device)
     out = torch.empty(8, dtype=torch.float64, device=X.device)
@@ -351,6 +362,9 @@ def huber_pass(X, y, w, sel, ceff, icpt, sigma, eps):
     _check_dev(Xb, y, w, sel)
     y, w, sel = _prep_rows(y, w, sel, n)
     c = _coef_dev(ceff, Xb.device)
+    fp8 = isinstance(X, TiledWide) and X.eb == 8
+    if fp8:
+        c = c * X.scales.to(torch.float64)
     nb = int(h.metrics_blocks(n))
     mult = torch.empty(n, dtype=torch.float64, device=Xb.device)
     partials = torch.empty(nb * 4, dtype=torch.float64, device=Xb.device)
@@ -358,4 +372,129 @@ def huber_pass(X, y, w, sel, ceff, icpt, sigma, eps):
     h.huber_pass(Xb.data_ptr(), xdt, int(ld), int(d), int(n), tiled, y.data_ptr(), dtype_code(y), _ptr(w),
                  dtype_code(w) if w is not None else 0, _ptr(sel), c.data_ptr(), float(icpt), float(sigma), float(eps),
                  mult.data_ptr(), partials.data_ptr(), out.data_ptr(), _stream())
+    if fp8:  # the row pass saw q = x / scale
+        out[4:] *= X.scales.to(torch.float64)
+    return out
+
+
+# ------------------------------------------------------------------------------------------
+# wide (d > 64) fragment layouts + LDS-tiled MFMA SYRK
+# ------------------------------------------------------------------------------------------
+def _srcw_desc(h, rows, dev):
+    desc = np.zeros((len(rows), 2), dtype=np.int64)  # PackSrcW {ptr, dt, pad}
+    for i, r in enumerate(rows):
+        desc[i, 0] = r.data_ptr()
+        desc[i, 1] = dtype_code(r)
+    return torch.from_numpy(desc.reshape(-1).view(np.uint8).copy()).to(dev)
+
+
+def _rows_of(parts):
+    rows = []
+    for p in parts:
+        if p.dim() == 1:
+            p = p.unsqueeze(0)
+        for i in range(p.shape[0]):
+            r = p[i]
+            rows.append(r if r.is_contiguous() else r.contiguous())
+    return rows
+
+
+def pack_wide(parts: List[torch.Tensor], eb: int, sel: Optional[torch.Tensor] = None, nt: Optional[int] = None,
+              inv_scale: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None) -> TiledWide:
+    """Columns -> wide fragment layout (eb 16 = bf16, 8 = fp8 with per-feature scales).
+
+    The layout is superstep-major, so row blocks that are multiples of 64 rows pack independently
+    into consecutive byte ranges of one image (``out``: a uint8 view of that range) — used to
+    stream-ingest matrices larger than one staging copy."""
+    h = native.hip()
+    dev = parts[0].device
+    rows = _rows_of(parts)
+    for r in rows:
+        _check_dev(r)
+    d, n = len(rows), rows[0].numel()
+    desc = _srcw_desc(h, rows, dev)
+    if sel is not None:
+        sel = sel.contiguous().to(torch.bool)
+    scales = None
+    if eb == 8 and inv_scale is None:
+        amax = torch.empty(d, dtype=torch.float32, device=dev)
+        h.feature_amax(desc.data_ptr(), d, n, _ptr(sel), amax.data_ptr(), _stream())
+        scales = torch.where(amax > 0, amax / FP8_MAX, torch.ones_like(amax))
+        inv_scale = 1.0 / scales
+    elif eb == 8:
+        scales = 1.0 / inv_scale
+    nt = nt or ((d + 255) // 256) * 8
+    nbytes = ((n + 63) // 64) * nt * 4 * 64 * eb
+    if out is not None:
+        if out.dtype != torch.uint8 or out.numel() != nbytes or not out.is_contiguous() or out.device != dev:
+            raise ValueError(f"pack_wide: out must be a contiguous uint8 tensor of {nbytes} bytes on {dev}")
+        buf = out
+    else:
+        buf = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    h.pack_wide(eb, desc.data_ptr(), d, n, nt, _ptr(sel), _ptr(inv_scale), buf.data_ptr(), _stream())
+    del rows
+    return TiledWide(buf, d, n, eb, scales)
+
+
+def tile_wide(X: torch.Tensor, eb: int, sel: Optional[torch.Tensor] = None) -> TiledWide:
+    return pack_wide([X], eb, sel)
+
+
+def _wide_splitk(P: int, nsup: int, eb: int) -> int:
+    """Split-K so the real (non-augmentation) panel-pair blocks fill whole waves of the 256 CUs
+    (1 block/CU at bf16's 128 KiB LDS, 2 at fp8's 64 KiB)."""
+    npr = P * (P + 1) // 2
+    slots = 256 if eb == 16 else 512
+    best, best_eff = 1, 0.0
+    for k in range(1, 257):
+        if k > nsup:
+            break
+        blocks = npr * k
+        eff = blocks / (-(-blocks // slots) * slots)
+        if blocks >= 2 * slots and eff >= 0.9:
+            return k
+        if eff > best_eff + 1e-9:
+            best, best_eff = k, eff
+    return best
+
+
+def _gram_wide(h, T: TiledWide, y, w, sel, x_zero_dead):
+    if w is not None:  # instance weights: hipBLASLt library GEMM on the dequantized matrix
+        return _gram_fallback_wide(T.to_dense(), y, w, sel, "bf16")
+    if sel is not None and not x_zero_dead:
+        # the stored tiles still hold the dead rows: re-pack once with the selection applied
+        T = pack_wide([T.to_dense()], T.eb, sel.contiguous().to(torch.bool))
+    d, n = T.d, T.n
+    dev = T.device
+    _check_dev(T.buf, y, sel)
+    y, _, sel = _prep_rows(y, None, sel, n)
+    yd = y.to(torch.float64)
+    live = torch.ones(n, dtype=torch.float64, device=dev) if sel is None else sel.to(torch.float64)
+    eb = T.eb
+    if eb == 16:
+        y_hi = yd.to(torch.bfloat16).to(torch.float64)
+        inv = None
+        s_h = s_l = 1.0
+    else:  # y = y_hi + y_lo, each an fp8 value times its own scale (y_hi exactly representable)
+        amax_h = float((yd * live).abs().max()) if n else 0.0
+        s_h = amax_h / FP8_MAX if amax_h > 0 else 1.0
+        y_hi = (yd / s_h).clamp(-FP8_MAX, FP8_MAX).to(torch.float8_e4m3fn).to(torch.float64) * s_h
+    y_lo = yd - y_hi
+    if eb == 8:
+        amax_l = float((y_lo * live).abs().max()) if n else 0.0
+        s_l = amax_l / FP8_MAX if amax_l > 0 else 1.0
+        inv = torch.tensor([1.0, 1.0 / s_h, 1.0 / s_l], dtype=torch.float32, device=dev)
+    cols = [live.to(torch.float32), (y_hi * live).to(torch.float32), (y_lo * live).to(torch.float32)]
+    aug = pack_wide(cols, eb, None, nt=1, inv_scale=inv)
+    P = (d + 255) // 256
+    pairs = [(i, j) for i in range(P + 1) for j in range(i, P + 1)]
+    nsup = max(1, (n + 63) // 64)
+    splitk = _wide_splitk(P, nsup, eb)
+    # f32 MFMA accumulators count rows exactly only below 2^24 per split
+    splitk = max(1, min(max(splitk, -(-nsup * 64 // (1 << 23))), nsup))
+    pairs_dev = torch.tensor(np.asarray(pairs, dtype=np.int32).reshape(-1), device=dev)
+    part = torch.empty(int(h.gram_wide_partials(d, splitk)), dtype=torch.float32, device=dev)
+    out = torch.empty(5 + 2 * d + d * (d + 1) // 2, dtype=torch.float64, device=dev)
+    h.gram_wide(eb, T.buf.data_ptr(), aug.buf.data_ptr(), T.nt, P, d, nsup, splitk, pairs_dev.data_ptr(),
+                part.data_ptr(), 1.0, float(s_h), float(s_l), _ptr(T.scales), out.data_ptr(), _stream())
     return out

@@ -67,3 +67,65 @@ class TiledBF16:
 
     def __repr__(self):
         return f"TiledBF16(d={self.d}, n={self.n}, device={self.buf.device})"
+
+
+def wide_offsets(feats: torch.Tensor, rows: torch.Tensor, d: int) -> torch.Tensor:
+    """Element offsets in the wide (d > 64) fragment layout: k-step = 16 contiguous rows, tiles
+    padded to whole 256-feature panels (csrc/hip/gram_wide.hip)."""
+    NT = ((d + 255) // 256) * 8
+    s = rows >> 6
+    ki = (rows >> 4) & 3
+    h = (rows >> 3) & 1
+    j = rows & 7
+    t = feats >> 5
+    lane = 32 * h + (feats & 31)
+    return ((((s * NT + t) * 4 + ki) * 64 + lane) << 3) + j
+
+
+class TiledWide:
+    """Wide MFMA-fragment storage: bf16 (eb=16) or fp8 e4m3 OCP with per-feature scales (eb=8)."""
+
+    def __init__(self, buf: torch.Tensor, d: int, n: int, eb: int, scales=None):
+        self.buf, self.d, self.n, self.eb = buf, int(d), int(n), int(eb)
+        self.scales = scales  # f32 [d] (fp8 only): x = q * scale
+
+    @property
+    def nt(self):
+        return ((self.d + 255) // 256) * 8
+
+    @property
+    def shape(self):
+        return (self.d, self.n)
+
+    @property
+    def device(self):
+        return self.buf.device
+
+    @property
+    def dtype(self):
+        return torch.bfloat16 if self.eb == 16 else torch.float8_e4m3fn
+
+    @property
+    def is_cuda(self):
+        return self.buf.is_cuda
+
+    def dim(self):
+        return 2
+
+    def gather_rows(self, rows: torch.Tensor) -> torch.Tensor:
+        rows = rows.to(self.buf.device, torch.int64)
+        f = torch.arange(self.d, device=self.buf.device, dtype=torch.int64).unsqueeze(1)
+        off = wide_offsets(f, rows.unsqueeze(0), self.d)
+        if self.eb == 16:
+            return self.buf.view(torch.bfloat16)[off]
+        q = self.buf.view(torch.float8_e4m3fn)[off].to(torch.float32)
+        return q * self.scales.unsqueeze(1)
+
+    def to_dense(self) -> torch.Tensor:
+        return self.gather_rows(torch.arange(self.n, device=self.buf.device))
+
+    def slice_rows(self, start: int, stop: int) -> torch.Tensor:
+        return self.gather_rows(torch.arange(start, stop, device=self.buf.device))
+
+    def __repr__(self):
+        return f"TiledWide(d={self.d}, n={self.n}, eb={self.eb}, device={self.buf.device})"

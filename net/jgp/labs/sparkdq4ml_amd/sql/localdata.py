@@ -124,10 +124,10 @@ def table_from_data(data, schema, device) -> Table:
                     if t.dtype not in (torch.float32, torch.bfloat16, torch.float64):
                         t = t.to(torch.float64)
                     vals = t
-                    if t.is_cuda and t.dtype == torch.bfloat16 and t.shape[0] <= 64:
+                    if t.is_cuda and t.dtype == torch.bfloat16:
                         from ..ops import device as _dev  # ingest into the MFMA-fragment tiled layout
 
-                        vals = _dev.tile_bf16(t)
+                        vals = _dev.tile_bf16(t) if t.shape[0] <= 64 else _dev.tile_wide(t, 16)
                     c = ColumnData(dt, vals, None, {"ml_attr": {"num_attrs": int(t.shape[0])}})
                 else:
                     dt = {torch.float64: DoubleType(), torch.float32: FloatType(), torch.int32: IntegerType(),

@@ -39,9 +39,9 @@ class ColumnData:
 
     def dense(self):
         """Feature-major dense tensor of a vector column (materializes a tiled layout)."""
-        from ..ops.layout import TiledBF16
+        from ..ops.layout import TiledBF16, TiledWide
 
-        return self.values.to_dense() if isinstance(self.values, TiledBF16) else self.values
+        return self.values.to_dense() if isinstance(self.values, (TiledBF16, TiledWide)) else self.values
 
     def valid_mask(self, device=None) -> torch.Tensor:
         if self.valid is not None:
@@ -54,12 +54,12 @@ class ColumnData:
 
     def index(self, idx: torch.Tensor) -> "ColumnData":
         """Gather rows ``idx`` (long tensor)."""
-        from ..ops.layout import TiledBF16
+        from ..ops.layout import TiledBF16, TiledWide
 
         if isinstance(self.values, list):
             il = idx.tolist()
             vals = [self.values[i] for i in il]
-        elif isinstance(self.values, TiledBF16):
+        elif isinstance(self.values, (TiledBF16, TiledWide)):
             vals = self.values.gather_rows(idx)
         elif isinstance(self.dtype, VectorUDT):
             vals = self.values.index_select(1, idx.to(self.values.device))
@@ -69,11 +69,11 @@ class ColumnData:
         return ColumnData(self.dtype, vals, valid, dict(self.meta))
 
     def slice(self, start: int, stop: int) -> "ColumnData":
-        from ..ops.layout import TiledBF16
+        from ..ops.layout import TiledBF16, TiledWide
 
         if isinstance(self.values, list):
             vals = self.values[start:stop]
-        elif isinstance(self.values, TiledBF16):
+        elif isinstance(self.values, (TiledBF16, TiledWide)):
             vals = self.values.slice_rows(start, stop)
         elif isinstance(self.dtype, VectorUDT):
             vals = self.values[:, start:stop]

@@ -18,7 +18,11 @@ STEPS=${STEPS:-"info tests bench prof"}
 for s in $STEPS; do
   case $s in
     info) step info 300 python -c "import torch,sys; sys.path.insert(0,'.'); from net.jgp.labs.sparkdq4ml_amd.ops import native; print(native.hip().device_info())" ;;
-    tests) step tests 900 python -m pytest tests -m gpu -x -q ;;
+    tests) step tests 900 python -m pytest tests -m gpu -q --maxfail=10 --ignore tests/test_gpu_wide.py ;;
+    widetests) step widetests 600 python -m pytest tests/test_gpu_wide.py -m gpu -q --maxfail=5 ;;
+    wide16) step wide16 600 env N=2e6 D=1024 EB=16 python scripts/wide_bench.py ;;
+    wide8) step wide8 900 env N=1e7 D=4096 EB=8 python scripts/wide_bench.py ;;
+    wideprof) (export TMPDIR=/tmp N=2e6 D=4096 EB=8 REPS=3; step wideprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/wideprof -o run --output-format csv -- python scripts/wide_bench.py) || exit $? ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" ;;
     bench) step bench 600 python bench.py --steps 20 --warmup 3 ;;
     fitprof) step fitprof 300 env N=1.25e7 python scripts/fit_profile.py ;;

@@ -114,9 +114,13 @@ def test_device_scan_through_reader(tmp_path):
     a = rng.integers(-1000, 1000, n)
     b = np.round(rng.normal(size=n), 4)
     p = tmp_path / "big.csv"
-    p.write_text("\n".join(f"{x},{y!r}" for x, y in zip(a, b)))
+    p.write_text("\n".join(f"{int(x)},{float(y)!r}" for x, y in zip(a, b)))
     spark = SparkSession.builder().master("mi355x[*]").config("dq4ml.csv.deviceThresholdBytes", 0).getOrCreate()
+    from net.jgp.labs.sparkdq4ml_amd.ops import csvscan
+
+    before = csvscan.STATS["device_scans"]
     df = spark.read().option("inferSchema", "true").csv(str(p))
+    assert csvscan.STATS["device_scans"] == before + 1
     t = df._table()
     assert t.columns[0].values.is_cuda and df.dtypes == [("_c0", "int"), ("_c1", "double")]
     np.testing.assert_array_equal(t.columns[0].values.cpu().numpy(), a)
