@@ -15,6 +15,7 @@ struct PackSrcW {
 struct WideArgs {
   const unsigned char* X;     // wide tiled storage, NT = npanels * 8 tiles
   const unsigned char* Xaug;  // 1-tile tiled storage of [1, y_hi, y_lo] (same element type)
+  const unsigned char* zeros; // >= 16 KiB zero page (streams the empty tiles of the augmentation panel)
   int NT;
   int npanels;                // ceil(d / 256)
   int d;
@@ -25,6 +26,8 @@ struct WideArgs {
   double aug_scale[3];        // scales of [1, y_hi, y_lo]
 };
 
+constexpr int kWideZeroBytes = 16384;
+
 int64_t wide_tiled_bytes(int eb, int d, int64_t n);
 int64_t gram_wide_partials(int d, int splitk);
 void feature_amax(const PackSrcW* srcs_dev, int d, int64_t n, const uint8_t* sel, float* amax, hipStream_t st);
@@ -32,6 +35,7 @@ void feature_amax(const PackSrcW* srcs_dev, int d, int64_t n, const uint8_t* sel
 void pack_wide(int eb, const PackSrcW* srcs_dev, int d, int64_t n, int nt, const uint8_t* sel, const float* inv_scale,
                void* out, hipStream_t st);
 // out: flat WLS layout [count, wSum, wwSum, bSum, bbSum, aSum(d), abSum(d), aa packed-upper(d)]
-void gram_wide(int eb, WideArgs a, const int* pairs_dev, const float* scales, double* out, hipStream_t st);
+void gram_wide(int eb, WideArgs a, const int* pairs_dev, const float* scales, double* out, hipStream_t st,
+               int ring = 4, int waves = 4);
 
 }  // namespace dq4ml

@@ -1,20 +1,28 @@
 // K5-wide: LDS-tiled MFMA SYRK for d > 64 (BASELINE config 5: 1e7 rows x 4096 features, fp8).
 //
 // G = Xᵀ X over rows, upper 256x256 panel pairs only, split-K over row ranges.  MI355X design:
-//  * storage is the MFMA-fragment-ordered tiling (ops/layout.py): for superstep s (64 rows),
-//    32-feature tile t, k-step ki (16 rows) the 64 lanes' fragments are contiguous (16 B/lane for
-//    bf16, 8 B/lane for fp8 e4m3 OCP).  A 256-feature panel of one superstep is therefore ONE
-//    contiguous 32 KiB (bf16) / 16 KiB (fp8) block;
-//  * each stage streams the A and B panels HBM -> LDS with global_load_lds (16 B per lane,
-//    lane-linear — no VGPR staging, no swizzle needed because the image is already in fragment
-//    order and every ds_read is lane-linear, i.e. conflict-free), double buffered;
-//  * 8 waves (2 x 4) per 256x256 block, 128 x 64 per wave: 4 x 2 accumulators of
-//    v_mfma_f32_32x32x16_{bf16,fp8_fp8}; per k-step 6 fragment reads feed 8 MFMAs;
+//  * storage is the MFMA-fragment-ordered tiling (ops/layout.py): per superstep s (64 rows) and
+//    32-feature tile t one 2 KiB chunk holding exactly the operand fragments of the 64 lanes —
+//    bf16: [4 k-steps][64 lanes][16 B] (v_mfma_f32_32x32x16_bf16, K = 16 per k-step); fp8 e4m3:
+//    [2 halves][64 lanes][16 B] (a lane's 32 B = all 64 rows: ONE block-scaled
+//    v_mfma_scale_f32_32x32x64_f8f6f4 with unit E8M0 scales = 2x the bf16 MFMA rate);
+//  * a "stage" is 32 rows (bf16) / 64 rows (fp8) = 16 KiB per 256-feature panel; stages stream
+//    HBM/L2 -> LDS with global_load_lds (16 B per lane, lane-linear, so every later ds_read_b128 is
+//    conflict-free with no swizzle) through a 4-deep ring (128 KiB LDS, 1 block per CU) with COUNTED
+//    vmcnt: three stages stay in flight across the one barrier per stage;
+//  * 4 waves (2 x 2) per 256x256 block, 128 x 128 per wave = 4 x 4 accumulators (256 AGPRs at 1
+//    wave/SIMD): 8 fragment reads feed 16 MFMAs, halving LDS read traffic per MFMA vs 128 x 64;
 //  * the label and the intercept column ride along as an "augmentation" panel [1, y_hi, y_lo]
-//    (a 32-feature tile of its own), so count, Σy, Σy², Σx, Σxy all fall out of the same SYRK —
-//    the augmented [X | 1 | y] Gram of SURVEY.md K5, without re-streaming X;
+//    (a 32-feature tile of its own; the other 7 tiles stream from a zero page so every wave issues
+//    the same number of loads), so count, Σy, Σy², Σx, Σxy fall out of the same SYRK — the
+//    augmented [X | 1 | y] Gram of SURVEY.md K5 without re-streaming X; augmentation blocks skip
+//    the all-zero MFMAs;
+//  * blockIdx -> (split, pair) is XCD-aware (bijective): the blocks one XCD runs together are
+//    consecutive pairs of the same row range, so the panels they share hit that XCD's L2;
 //  * per-column fp8 scales are applied in the f64 slab reduction (deterministic, no atomics).
 #include <hip/hip_runtime.h>
+
+#include <stdexcept>
 
 #include "common.h"
 #include "gram_wide.h"
@@ -23,132 +31,243 @@ namespace dq4ml {
 
 namespace {
 
-constexpr int kWBlock = 512;
-constexpr int kPanel = 256;        // features per panel
-constexpr int kTilesPerPanel = 8;  // 32-feature tiles
+constexpr int kPanel = 256;           // features per panel
+constexpr int kTilesPerPanel = 8;     // 32-feature tiles
+constexpr int kChunk = 2048;          // bytes of one (tile, stage) image
+constexpr int kPanelStage = kTilesPerPanel * kChunk;  // 16 KiB
+constexpr int kStageBytes = 2 * kPanelStage;          // A + B images
+constexpr int kMaxRing = 5;                           // LDS stages (5 x 32 KiB = all 160 KiB)
 
 typedef __attribute__((ext_vector_type(2))) unsigned int u32x2;
+typedef __attribute__((ext_vector_type(8))) int i32x8;
 
 template <int EB>
 struct WideTraits;
 
 template <>
-struct WideTraits<16> {  // bf16
+struct WideTraits<16> {  // bf16: a stage = 32 rows = 2 k-steps of v_mfma_f32_32x32x16_bf16
+  static constexpr int kStagesPerSup = 2;
+  static constexpr int kSteps = 2;
   typedef bf16x8 frag;
-  static __device__ __forceinline__ frag read(const unsigned char* p) { return *reinterpret_cast<const frag*>(p); }
+  static __device__ __forceinline__ frag read(const unsigned char* tile, int kk, int lane) {
+    return *reinterpret_cast<const frag*>(tile + kk * 1024 + lane * 16);
+  }
   static __device__ __forceinline__ f32x16 mfma(frag a, frag b, f32x16 c) {
     return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+  }
+  // byte offset of the (stage st, tile T) image = sdelta(st, NT) + T * kTileStride
+  static constexpr int kTileStride = 4096;
+  static __device__ __forceinline__ int64_t sdelta(int64_t st, int NT) {
+    return (st >> 1) * (int64_t)NT * 4096 + (st & 1) * 2048;
   }
 };
 
 template <>
-struct WideTraits<8> {  // fp8 e4m3 (OCP)
-  typedef long frag;
-  static __device__ __forceinline__ frag read(const unsigned char* p) { return *reinterpret_cast<const long*>(p); }
-  static __device__ __forceinline__ f32x16 mfma(frag a, frag b, f32x16 c) {
-    return __builtin_amdgcn_mfma_f32_32x32x16_fp8_fp8(a, b, c, 0, 0, 0);
+struct WideTraits<8> {  // fp8 e4m3 (OCP): a stage = 64 rows = 1 block-scaled K=64 MFMA
+  static constexpr int kStagesPerSup = 1;
+  static constexpr int kSteps = 1;
+  typedef i32x8 frag;
+  static __device__ __forceinline__ frag read(const unsigned char* tile, int, int lane) {
+    const u32x4 lo = *reinterpret_cast<const u32x4*>(tile + lane * 16);
+    const u32x4 hi = *reinterpret_cast<const u32x4*>(tile + 1024 + lane * 16);
+    return i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
   }
+  static __device__ __forceinline__ f32x16 mfma(frag a, frag b, f32x16 c) {
+    // FMT 0/0 = e4m3 x e4m3, E8M0 scale 127 = 1.0 for both operands
+    return __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, b, c, 0, 0, 0, 127, 0, 127);
+  }
+  static constexpr int kTileStride = kChunk;
+  static __device__ __forceinline__ int64_t sdelta(int64_t st, int NT) { return st * (int64_t)NT * kChunk; }
 };
-
-// bytes of one (tile, k-step) chunk and of one panel per superstep
-template <int EB>
-constexpr int chunk_bytes() { return 64 * EB; }
-template <int EB>
-constexpr int panel_bytes() { return kTilesPerPanel * 4 * chunk_bytes<EB>(); }
 
 __device__ __forceinline__ void glds16(const void* g, void* l) {
   __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(g),
                                    (__attribute__((address_space(3))) void*)(l), 16, 0, 0);
 }
 
-template <int EB>
-__global__ __launch_bounds__(kWBlock, 1) void gram_wide_kernel(WideArgs a) {
+__device__ __forceinline__ int pair_index(int I, int J, int P) {
+  // pairs listed row-major over I <= J in [0, P] (P = augmentation panel)
+  return I * (P + 1) - I * (I - 1) / 2 + (J - I);
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <typename F, int WN>
+struct StageFrags {
+  F a[2][4];   // [k-step][A tile]
+  F b[2][WN];  // [k-step][B tile]
+};
+
+// One (pair, split) block's K loop + epilogue.  MODE 0: full panel pair; 1: (I, augmentation);
+// 2: (augmentation, augmentation).  Separate instantiations keep the accumulators in AGPRs with no
+// control-flow merge inside the loop (a merge there costs a full AGPR<->VGPR copy per stage).
+//
+// Schedule per stage i (fragments of stage i already in registers `cur`):
+//   MFMAs on A tiles 0-1 | wait stage i+1 (counted vmcnt) + s_barrier | ds_read stage i+1 -> `nxt`,
+//   glds stage i+4 into the buffer stage i vacated | MFMAs on A tiles 2-3 | lgkmcnt(0)
+// so the LDS reads and the barrier skew hide under half a stage of MFMAs, and three stages of
+// global_load_lds stay in flight across every barrier.
+template <int EB, int MODE, int RING, int WAVES>
+__device__ __forceinline__ void syrk_block(const WideArgs& a, unsigned char* smem, int I, int J, int pair, int split) {
   typedef WideTraits<EB> Tr;
-  constexpr int PB = panel_bytes<EB>();
-  constexpr int CB = chunk_bytes<EB>();
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  typedef typename Tr::frag F;
+  // WAVES 4: 2 x 2 waves of 128 x 128 (1 wave/SIMD); 8: 2 x 4 waves of 128 x 64 (2 waves/SIMD)
+  constexpr int kWBlock = 64 * WAVES;
+  constexpr int WN = WAVES == 4 ? 4 : 2;              // 32-col tiles per wave
+  constexpr int kLoadsPerPanel = kPanelStage / (kWBlock * 16);
+  constexpr int kLoadsPerStage = 2 * kLoadsPerPanel;
+  typedef StageFrags<F, WN> SF;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 2, wn = wave & 3;  // 2 x 4 waves
-  const int pair = blockIdx.x / a.splitk, split = blockIdx.x % a.splitk;
-  const int I = a.pairs[2 * pair], J = a.pairs[2 * pair + 1];
-  const bool diag = I == J;
-  const bool aug_a = I == a.npanels, aug_b = J == a.npanels;  // augmentation tile [1, y_hi, y_lo]
-  const int64_t s0 = a.nsup * split / a.splitk, s1 = a.nsup * (split + 1) / a.splitk;
+  const int wm = WAVES == 4 ? wave >> 1 : wave >> 2, wn = WAVES == 4 ? wave & 1 : wave & 3;
+  const int64_t nst = a.nsup * Tr::kStagesPerSup;
+  const int64_t st0 = nst * split / a.splitk, st1 = nst * (split + 1) / a.splitk;
+  const int64_t cnt = st1 - st0;
 
-  // LDS images: A[b] at (2b) * PB, B[b] at (2b + 1) * PB
-  auto bufA = [&](int b) { return smem + (size_t)(2 * b) * PB; };
-  auto bufB = [&](int b) { return smem + (size_t)(2 * b + 1) * PB; };
-
-  // stage loader: a data panel (8 tiles x 4 k-steps, contiguous) or the single augmentation tile
-  auto issue_panel = [&](unsigned char* dst, int pidx, int64_t s) {
-    if (pidx == a.npanels) {  // [1, y_hi, y_lo]: 1 tile x 4 k-steps; the other tiles stay zero
-      const unsigned char* g = a.Xaug + (s * 4) * CB;
-      if (tid * 16 < 4 * CB) glds16(g + tid * 16, dst + (wave * 64) * 16);
-      return;
-    }
-    const unsigned char* g = a.X + ((s * a.NT + (int64_t)pidx * kTilesPerPanel) * 4) * CB;
+  // per-thread global sources of its kLoadsPerPanel 16-byte pieces of each panel-stage image; a
+  // stage adds the wave-uniform Tr::sdelta (augmentation: only piece 0 of the first 128 threads is
+  // real data, the rest stream the zero page and never advance)
+  const unsigned char* srcA[kLoadsPerPanel];
+  const unsigned char* srcB[kLoadsPerPanel];
 #pragma unroll
-    for (int r = 0; r < PB / (kWBlock * 16); ++r) glds16(g + (r * kWBlock + tid) * 16, dst + (r * kWBlock + wave * 64) * 16);
+  for (int r = 0; r < kLoadsPerPanel; ++r) {
+    const int o = (r * kWBlock + tid) * 16;
+    const int64_t tile_off = (int64_t)(o >> 11) * Tr::kTileStride + (o & (kChunk - 1));
+    srcA[r] = MODE == 2 ? (o < kChunk ? a.Xaug + o : a.zeros + o)
+                        : a.X + (int64_t)I * kTilesPerPanel * Tr::kTileStride + tile_off;
+    srcB[r] = MODE >= 1 ? (o < kChunk ? a.Xaug + o : a.zeros + o)
+                        : a.X + (int64_t)J * kTilesPerPanel * Tr::kTileStride + tile_off;
+  }
+  // stages at or beyond cnt stream the zero page: the K loop then runs an even number of stages
+  // with no branch at all (a branch there lets the compiler sink MFMAs past the barrier) and
+  // every wait is the same counted vmcnt — the extra stage multiplies zeros
+  auto issue = [&](int64_t st, int buf) {
+    unsigned char* base = smem + buf * kStageBytes;
+    const bool live = st < cnt;
+    const int64_t dx = Tr::sdelta(st0 + st, a.NT), dg = Tr::sdelta(st0 + st, 1);
+#pragma unroll
+    for (int r = 0; r < kLoadsPerPanel; ++r) {
+      const int o = (r * kWBlock + tid) * 16;
+      const bool real = o < kChunk;
+      const unsigned char* s = MODE == 2 ? (real ? srcA[r] + dg : srcA[r]) : srcA[r] + dx;
+      glds16(live ? s : a.zeros + o, base + (r * kWBlock + wave * 64) * 16);
+    }
+#pragma unroll
+    for (int r = 0; r < kLoadsPerPanel; ++r) {
+      const int o = (r * kWBlock + tid) * 16;
+      const bool real = o < kChunk;
+      const unsigned char* s = MODE >= 1 ? (real ? srcB[r] + dg : srcB[r]) : srcB[r] + dx;
+      glds16(live ? s : a.zeros + o, base + kPanelStage + (r * kWBlock + wave * 64) * 16);
+    }
   };
-  auto issue = [&](int64_t s, int b) {
-    issue_panel(bufA(b), I, s);
-    if (!diag) issue_panel(bufB(b), J, s);
+  auto read = [&](SF& f, int buf) {
+    const unsigned char* A = smem + buf * kStageBytes;
+    const unsigned char* B = A + kPanelStage;
+#pragma unroll
+    for (int kk = 0; kk < Tr::kSteps; ++kk) {
+#pragma unroll
+      for (int x = 0; x < 4; ++x)
+        if (MODE != 2 || x == 0) f.a[kk][x] = Tr::read(A + (wm * 4 + x) * kChunk, kk, lane);
+#pragma unroll
+      for (int y = 0; y < WN; ++y)
+        if (MODE == 0 || y == 0) f.b[kk][y] = Tr::read(B + (wn * WN + y) * kChunk, kk, lane);
+    }
   };
 
-  f32x16 acc[4][2];
+  f32x16 acc[4][WN];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = f32x16{};
-
-  // augmentation images: only tile 0 is ever loaded, zero the rest once
-  for (int i = tid * 16; i < 2 * PB; i += kWBlock * 16) {
-    if (aug_a) *reinterpret_cast<u32x4*>(bufA(i / PB) + (i % PB)) = u32x4{0u, 0u, 0u, 0u};
-    if (aug_b && !diag) *reinterpret_cast<u32x4*>(bufB(i / PB) + (i % PB)) = u32x4{0u, 0u, 0u, 0u};
-  }
-  __syncthreads();
-  const bool wave_active = (!aug_a || wm == 0) && (!aug_b || wn == 0);
-
-  if (s0 < s1) {
-    issue(s0, 0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    int cur = 0;
-    for (int64_t s = s0; s < s1; ++s) {
-      if (s + 1 < s1) issue(s + 1, cur ^ 1);
-      const unsigned char* A = bufA(cur);
-      const unsigned char* B = diag ? bufA(cur) : bufB(cur);
-      if (wave_active) {
+    for (int j = 0; j < WN; ++j) acc[i][j] = f32x16{};
+  // (augmentation modes: waves whose B (or A) tiles come from the zero page multiply zeros —
+  // cheaper than a data-dependent branch around the accumulators)
+  auto mfmas = [&](const SF& f, int x0) {
 #pragma unroll
-        for (int ki = 0; ki < 4; ++ki) {
-          typename Tr::frag fa[4], fb[2];
+    for (int kk = 0; kk < Tr::kSteps; ++kk)
 #pragma unroll
-          for (int i = 0; i < 4; ++i) fa[i] = Tr::read(A + ((wm * 4 + i) * 4 + ki) * CB + lane * EB);
+      for (int x = x0; x < x0 + 2; ++x) {
+        if (MODE == 2 && x != 0) continue;
 #pragma unroll
-          for (int j = 0; j < 2; ++j) fb[j] = Tr::read(B + ((wn * 2 + j) * 4 + ki) * CB + lane * EB);
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int j = 0; j < 2; ++j) acc[i][j] = Tr::mfma(fa[i], fb[j], acc[i][j]);
+        for (int y = 0; y < WN; ++y) {
+          if (MODE != 0 && y != 0) continue;
+          acc[x][y] = Tr::mfma(f.a[kk][x], f.b[kk][y], acc[x][y]);
         }
       }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      cur ^= 1;
+  };
+  // one stage: MFMAs(A tiles 0-1 of cur) | vmcnt: stage i+1 landed | s_barrier | MFMAs(A tiles
+  // 2-3 of cur) interleaved with ds_read stage i+1 -> nxt and glds stage i+RING into the buffer
+  // stage i vacated (the issue slots ride in the MFMA shadow) | lgkmcnt(0)
+  int rb = 0;  // ring buffer of stage i
+  auto step = [&](SF& cur, SF& nxt, int64_t i) {
+    const int nb = rb + 1 == RING ? 0 : rb + 1;
+    mfmas(cur, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    wait_vm<(RING - 2) * kLoadsPerStage>();
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    mfmas(cur, 2);
+    read(nxt, nb);
+    issue(i + RING, rb);
+    if (MODE == 0) {
+#pragma unroll
+      for (int g = 0; g < 2 * WN; ++g) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                  // 1 MFMA
+        __builtin_amdgcn_sched_group_barrier(0x100, (4 + WN) * Tr::kSteps * (EB == 8 ? 2 : 1) / (2 * WN), 0);  // DS reads
+        __builtin_amdgcn_sched_group_barrier(0x020, kLoadsPerStage / (2 * WN), 0);  // glds (VMEM)
+        __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);                  // VALU address math
+      }
     }
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    rb = nb;
+  };
+
+  if (cnt > 0) {
+#pragma unroll
+    for (int p = 0; p < RING; ++p) issue(p, p);
+    wait_vm<(RING - 1) * kLoadsPerStage>();
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    SF f0, f1;
+    read(f0, 0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    for (int64_t i = 0; i < cnt; i += 2) {
+      step(f0, f1, i);
+      step(f1, f0, i + 1);
+    }
+    wait_vm<0>();  // drain the zero-page prefetches before the block can exit
   }
   // f32 partial tile [256][256] of this (pair, split)
-  float* out = a.part + (int64_t)blockIdx.x * kPanel * kPanel;
+  float* out = a.part + ((int64_t)pair_index(I, J, a.npanels) * a.splitk + split) * kPanel * kPanel;
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int x = 0; x < 4; ++x)
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int y = 0; y < WN; ++y)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int row = wm * 128 + i * 32 + mfma32_row(lane, r);
-        const int col = wn * 64 + j * 32 + mfma32_col(lane);
-        out[row * kPanel + col] = acc[i][j][r];
+        const int row = wm * 128 + x * 32 + mfma32_row(lane, r);
+        const int col = wn * 32 * WN + y * 32 + mfma32_col(lane);
+        out[row * kPanel + col] = acc[x][y][r];
       }
+}
+
+template <int EB, int RING, int WAVES>
+__global__ __launch_bounds__(64 * WAVES, 1) void gram_wide_kernel(WideArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  // XCD-aware bijective remap: dispatch puts block b on XCD b % 8; give each XCD a contiguous
+  // run of logical ids (split-major, pairs consecutive) so co-resident blocks share panels in L2
+  const int nwg = gridDim.x, orig = blockIdx.x, xcd = orig & 7, q = nwg >> 3, rem = nwg & 7;
+  const int L = (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + (orig >> 3);
+  const int npair = (a.npanels + 1) * (a.npanels + 2) / 2;
+  const int split = L / npair, pair = L - split * npair;
+  const int I = a.pairs[2 * pair], J = a.pairs[2 * pair + 1];
+  if (J != a.npanels) syrk_block<EB, 0, RING, WAVES>(a, smem, I, J, pair, split);
+  else if (I != a.npanels) syrk_block<EB, 1, RING, WAVES>(a, smem, I, J, pair, split);
+  else syrk_block<EB, 2, RING, WAVES>(a, smem, I, J, pair, split);
 }
 
 // f64 reduction of the split-K slabs, fp8 scales applied, straight into the flat WLS layout:
@@ -160,10 +279,6 @@ __device__ __forceinline__ double slab_sum(const WideArgs& a, int pair, int r, i
   return s;
 }
 
-__device__ __forceinline__ int pair_index(int I, int J, int P) {
-  // pairs listed row-major over I <= J in [0, P] (P = augmentation panel)
-  return I * (P + 1) - I * (I - 1) / 2 + (J - I);
-}
 
 __global__ __launch_bounds__(256) void gram_wide_reduce_kernel(WideArgs a, const float* __restrict__ scales,
                                                               double* __restrict__ out) {
@@ -264,13 +379,18 @@ __global__ __launch_bounds__(256) void pack_wide_kernel(const PackSrcW* __restri
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] = (__bf16)x[j];
       reinterpret_cast<u32x4*>(out)[c] = __builtin_bit_cast(u32x4, v);
-    } else {
+    } else {  // saturate to the e4m3 range (the conversion maps overflow to NaN)
       const float is = f < d ? inv_scale[f] : 0.0f;
-      int lo = __builtin_amdgcn_cvt_pk_fp8_f32(x[0] * is, x[1] * is, 0, false);
-      lo = __builtin_amdgcn_cvt_pk_fp8_f32(x[2] * is, x[3] * is, lo, true);
-      int hi = __builtin_amdgcn_cvt_pk_fp8_f32(x[4] * is, x[5] * is, 0, false);
-      hi = __builtin_amdgcn_cvt_pk_fp8_f32(x[6] * is, x[7] * is, hi, true);
-      reinterpret_cast<u32x2*>(out)[c] = u32x2{(unsigned)lo, (unsigned)hi};
+      float q[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) q[j] = fminf(fmaxf(x[j] * is, -448.0f), 448.0f);
+      int lo = __builtin_amdgcn_cvt_pk_fp8_f32(q[0], q[1], 0, false);
+      lo = __builtin_amdgcn_cvt_pk_fp8_f32(q[2], q[3], lo, true);
+      int hi = __builtin_amdgcn_cvt_pk_fp8_f32(q[4], q[5], 0, false);
+      hi = __builtin_amdgcn_cvt_pk_fp8_f32(q[6], q[7], hi, true);
+      // chunk (s, t) = [2 halves][64 lanes][16 B]; k-step ki -> half ki >> 1, byte 8 * (ki & 1)
+      const int64_t o = (s * NT + t) * 2048 + (((ki >> 1) * 64 + lane) << 4) + ((ki & 1) << 3);
+      *reinterpret_cast<u32x2*>(out + o) = u32x2{(unsigned)lo, (unsigned)hi};
     }
   }
 }
@@ -305,19 +425,31 @@ int64_t gram_wide_partials(int d, int splitk) {
   return (int64_t)npair * splitk * kPanel * kPanel;
 }
 
-void gram_wide(int eb, WideArgs a, const int* pairs_dev, const float* scales, double* out, hipStream_t st) {
+template <int EB, int RING, int WAVES>
+static void launch_wide(const WideArgs& a, int nblocks, hipStream_t st) {
+  const size_t lds = (size_t)RING * kStageBytes;
+  DQ_HIP_CHECK(hipFuncSetAttribute((const void*)gram_wide_kernel<EB, RING, WAVES>,
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  hipLaunchKernelGGL((gram_wide_kernel<EB, RING, WAVES>), dim3(nblocks), dim3(64 * WAVES), lds, st, a);
+  DQ_HIP_CHECK(hipGetLastError());
+}
+
+template <int EB>
+static void launch_wide_eb(const WideArgs& a, int nblocks, hipStream_t st, int ring, int waves) {
+  if (waves == 8) ring == 5 ? launch_wide<EB, 5, 8>(a, nblocks, st) : launch_wide<EB, 4, 8>(a, nblocks, st);
+  else ring == 5 ? launch_wide<EB, 5, 4>(a, nblocks, st) : launch_wide<EB, 4, 4>(a, nblocks, st);
+}
+
+void gram_wide(int eb, WideArgs a, const int* pairs_dev, const float* scales, double* out, hipStream_t st, int ring,
+               int waves) {
   a.pairs = pairs_dev;
   const int P = a.npanels;
   const int npair = (P + 1) * (P + 2) / 2;
-  const size_t lds = 4 * (size_t)(eb == 16 ? panel_bytes<16>() : panel_bytes<8>());
-  if (eb == 16) {
-    DQ_HIP_CHECK(hipFuncSetAttribute((const void*)gram_wide_kernel<16>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    hipLaunchKernelGGL(gram_wide_kernel<16>, dim3(npair * a.splitk), dim3(kWBlock), lds, st, a);
-  } else {
-    DQ_HIP_CHECK(hipFuncSetAttribute((const void*)gram_wide_kernel<8>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    hipLaunchKernelGGL(gram_wide_kernel<8>, dim3(npair * a.splitk), dim3(kWBlock), lds, st, a);
-  }
-  DQ_HIP_CHECK(hipGetLastError());
+  const int nb = npair * a.splitk;
+  if (ring != 4 && ring != 5) throw std::invalid_argument("gram_wide: ring must be 4 or 5");
+  if (waves != 4 && waves != 8) throw std::invalid_argument("gram_wide: waves must be 4 or 8");
+  if (eb == 16) launch_wide_eb<16>(a, nb, st, ring, waves);
+  else launch_wide_eb<8>(a, nb, st, ring, waves);
   const int64_t K = 5 + 2 * (int64_t)a.d + (int64_t)a.d * (a.d + 1) / 2;
   int64_t g = (K + 255) / 256;
   if (g > 8192) g = 8192;

@@ -64,6 +64,7 @@ PYBIND11_MODULE(_dq4ml_hip, m) {
     tile_bf16(P<const void>(X), xdt, ld, d, n, P<void>(out), as_stream(stream));
   });
   m.def("wide_tiled_bytes", &wide_tiled_bytes);
+  m.attr("WIDE_ZERO_BYTES") = kWideZeroBytes;
   m.def("gram_wide_partials", &gram_wide_partials);
   m.def("pack_wide", [](int eb, uintptr_t srcs_dev, int d, int64_t n, int nt, uintptr_t sel, uintptr_t inv_scale,
                         uintptr_t out, uintptr_t stream) {
@@ -73,12 +74,13 @@ PYBIND11_MODULE(_dq4ml_hip, m) {
   m.def("feature_amax", [](uintptr_t srcs_dev, int d, int64_t n, uintptr_t sel, uintptr_t amax, uintptr_t stream) {
     feature_amax(P<const PackSrcW>(srcs_dev), d, n, P<const uint8_t>(sel), P<float>(amax), as_stream(stream));
   });
-  m.def("gram_wide", [](int eb, uintptr_t X, uintptr_t Xaug, int nt, int npanels, int d, int64_t nsup, int splitk,
-                        uintptr_t pairs, uintptr_t part, double s1, double syh, double syl, uintptr_t scales,
-                        uintptr_t out, uintptr_t stream) {
+  m.def("gram_wide", [](int eb, uintptr_t X, uintptr_t Xaug, uintptr_t zeros, int nt, int npanels, int d,
+                        int64_t nsup, int splitk, uintptr_t pairs, uintptr_t part, double s1, double syh, double syl,
+                        uintptr_t scales, uintptr_t out, uintptr_t stream, int ring, int waves) {
     WideArgs a{};
     a.X = P<const unsigned char>(X);
     a.Xaug = P<const unsigned char>(Xaug);
+    a.zeros = P<const unsigned char>(zeros);
     a.NT = nt;
     a.npanels = npanels;
     a.d = d;
@@ -88,7 +90,7 @@ PYBIND11_MODULE(_dq4ml_hip, m) {
     a.aug_scale[0] = s1;
     a.aug_scale[1] = syh;
     a.aug_scale[2] = syl;
-    gram_wide(eb, a, P<const int>(pairs), P<const float>(scales), P<double>(out), as_stream(stream));
+    gram_wide(eb, a, P<const int>(pairs), P<const float>(scales), P<double>(out), as_stream(stream), ring, waves);
   });
 
   // ---- compaction (K3) -----------------------------------------------------------------------

@@ -142,6 +142,15 @@ __device__ __forceinline__ int64_t wide_offset(int f, int64_t r, int NT) {
   return ((((s * NT + t) * 4 + ki) * 64 + lane) << 3) + j;  // element index
 }
 
+// fp8 wide image: per (superstep, tile) a [2 halves][64 lanes][16 B] chunk; a lane's 32 bytes are
+// its k-steps 0..3 (8 rows each), halves = k-steps {0,1} / {2,3} (gram_wide.hip)
+__device__ __forceinline__ int64_t wide_offset_fp8(int f, int64_t r, int NT) {
+  const int64_t s = r >> 6;
+  const int ki = (int)((r >> 4) & 3), h = (int)((r >> 3) & 1), j = (int)(r & 7);
+  const int t = f >> 5, lane = 32 * h + (f & 31);
+  return (s * NT + t) * 2048 + (((ki >> 1) * 64 + lane) << 4) + ((ki & 1) << 3) + j;  // byte index
+}
+
 __device__ __forceinline__ float fp8_to_f32(uint8_t v) {
   return __builtin_amdgcn_cvt_f32_fp8((int)v, 0);
 }
@@ -152,9 +161,8 @@ __device__ __forceinline__ double predict_row(const void* X, int xdt, int64_t ld
   if (tiled == 2 || tiled == 3) {  // wide bf16 / wide fp8 (coef pre-multiplied by the fp8 scales)
     const int NT = ((d + 255) >> 8) * 8;
     for (int f = 0; f < d; ++f) {
-      const int64_t o = wide_offset(f, r, NT);
-      const float x = tiled == 2 ? bf16_bits_to_f32(reinterpret_cast<const uint16_t*>(X)[o])
-                                 : fp8_to_f32(reinterpret_cast<const uint8_t*>(X)[o]);
+      const float x = tiled == 2 ? bf16_bits_to_f32(reinterpret_cast<const uint16_t*>(X)[wide_offset(f, r, NT)])
+                                 : fp8_to_f32(reinterpret_cast<const uint8_t*>(X)[wide_offset_fp8(f, r, NT)]);
       acc += coef[f] * (double)x;
     }
     return acc;
@@ -381,7 +389,7 @@ __global__ __launch_bounds__(256) void xt_vec_kernel(const void* __restrict__ X,
     double x;
     if (tiled == 1) x = (double)bf16_bits_to_f32(reinterpret_cast<const uint16_t*>(X)[tiled_offset(j, r, NT)]);
     else if (tiled == 2) x = (double)bf16_bits_to_f32(reinterpret_cast<const uint16_t*>(X)[wide_offset(j, r, ((d + 255) >> 8) * 8)]);
-    else if (tiled == 3) x = (double)fp8_to_f32(reinterpret_cast<const uint8_t*>(X)[wide_offset(j, r, ((d + 255) >> 8) * 8)]);
+    else if (tiled == 3) x = (double)fp8_to_f32(reinterpret_cast<const uint8_t*>(X)[wide_offset_fp8(j, r, ((d + 255) >> 8) * 8)]);
     else x = ld_f64(X, xdt, (int64_t)j * ld + r);
     s += x * v[r];
   }

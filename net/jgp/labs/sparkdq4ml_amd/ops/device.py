@@ -6,6 +6,7 @@ launch path, so these ops compose with torch work and HIP-graph capture.  Shapes
 validated HERE, on the host, before any launch (a kernel's indexing assumes them)."""
 from __future__ import annotations
 
+import os
 from typing import List, Optional
 
 import numpy as np
@@ -440,11 +441,39 @@ def tile_wide(X: torch.Tensor, eb: int, sel: Optional[torch.Tensor] = None) -> T
     return pack_wide([X], eb, sel)
 
 
+_zero_pages = {}
+
+
+def _zero_page(h, dev):
+    z = _zero_pages.get(dev)
+    if z is None:
+        z = _zero_pages[dev] = torch.zeros(int(h.WIDE_ZERO_BYTES), dtype=torch.uint8, device=dev)
+    return z
+
+
+def _morton(i: int, j: int) -> int:
+    z = 0
+    for b in range(16):
+        z |= ((i >> b) & 1) << (2 * b + 1) | ((j >> b) & 1) << (2 * b)
+    return z
+
+
+def _wide_pairs(P: int, order: str = "morton"):
+    """Upper panel pairs (I <= J) over [0, P] (P = augmentation panel) in launch order.  Blocks
+    that one XCD runs together are consecutive in this list (the kernel's XCD remap), so a
+    Z-order walk makes them share few panels (~12 per 32 blocks instead of ~18 row-major) and
+    those hit that XCD's L2.  Partials are stored by row-major pair index, so order is free."""
+    pairs = [(i, j) for i in range(P + 1) for j in range(i, P + 1)]
+    if order == "morton":
+        pairs.sort(key=lambda p: _morton(*p))
+    return pairs
+
+
 def _wide_splitk(P: int, nsup: int, eb: int) -> int:
     """Split-K so the real (non-augmentation) panel-pair blocks fill whole waves of the 256 CUs
     (1 block/CU at bf16's 128 KiB LDS, 2 at fp8's 64 KiB)."""
-    npr = P * (P + 1) // 2
-    slots = 256 if eb == 16 else 512
+    npr = P * (P + 1) // 2 + 0.25 * (P + 1)  # augmentation blocks run at load speed
+    slots = 256  # 128 KiB LDS ring: one block per CU
     best, best_eff = 1, 0.0
     for k in range(1, 257):
         if k > nsup:
@@ -487,7 +516,7 @@ def _gram_wide(h, T: TiledWide, y, w, sel, x_zero_dead):
     cols = [live.to(torch.float32), (y_hi * live).to(torch.float32), (y_lo * live).to(torch.float32)]
     aug = pack_wide(cols, eb, None, nt=1, inv_scale=inv)
     P = (d + 255) // 256
-    pairs = [(i, j) for i in range(P + 1) for j in range(i, P + 1)]
+    pairs = _wide_pairs(P, os.environ.get("DQ4ML_WIDE_ORDER", "morton"))
     nsup = max(1, (n + 63) // 64)
     splitk = _wide_splitk(P, nsup, eb)
     # f32 MFMA accumulators count rows exactly only below 2^24 per split
@@ -495,6 +524,8 @@ def _gram_wide(h, T: TiledWide, y, w, sel, x_zero_dead):
     pairs_dev = torch.tensor(np.asarray(pairs, dtype=np.int32).reshape(-1), device=dev)
     part = torch.empty(int(h.gram_wide_partials(d, splitk)), dtype=torch.float32, device=dev)
     out = torch.empty(5 + 2 * d + d * (d + 1) // 2, dtype=torch.float64, device=dev)
-    h.gram_wide(eb, T.buf.data_ptr(), aug.buf.data_ptr(), T.nt, P, d, nsup, splitk, pairs_dev.data_ptr(),
-                part.data_ptr(), 1.0, float(s_h), float(s_l), _ptr(T.scales), out.data_ptr(), _stream())
+    h.gram_wide(eb, T.buf.data_ptr(), aug.buf.data_ptr(), _zero_page(h, dev).data_ptr(), T.nt, P, d, nsup, splitk,
+                pairs_dev.data_ptr(),
+                part.data_ptr(), 1.0, float(s_h), float(s_l), _ptr(T.scales), out.data_ptr(), _stream(),
+                int(os.environ.get("DQ4ML_WIDE_RING", "4")), int(os.environ.get("DQ4ML_WIDE_WAVES", "4")))
     return out

@@ -69,9 +69,11 @@ class TiledBF16:
         return f"TiledBF16(d={self.d}, n={self.n}, device={self.buf.device})"
 
 
-def wide_offsets(feats: torch.Tensor, rows: torch.Tensor, d: int) -> torch.Tensor:
-    """Element offsets in the wide (d > 64) fragment layout: k-step = 16 contiguous rows, tiles
-    padded to whole 256-feature panels (csrc/hip/gram_wide.hip)."""
+def wide_offsets(feats: torch.Tensor, rows: torch.Tensor, d: int, eb: int = 16) -> torch.Tensor:
+    """Element offsets in the wide (d > 64) fragment layout, tiles padded to whole 256-feature
+    panels (csrc/hip/gram_wide.hip).  Per (superstep s = 64 rows, 32-feature tile t) one chunk of
+    512 elements: bf16 ``[k-step][64 lanes][8]``; fp8 ``[half][64 lanes][16]`` where a lane's 32
+    bytes are its 4 k-steps (half = k-step >> 1) — one K=64 block-scaled MFMA operand."""
     NT = ((d + 255) // 256) * 8
     s = rows >> 6
     ki = (rows >> 4) & 3
@@ -79,6 +81,8 @@ def wide_offsets(feats: torch.Tensor, rows: torch.Tensor, d: int) -> torch.Tenso
     j = rows & 7
     t = feats >> 5
     lane = 32 * h + (feats & 31)
+    if eb == 8:
+        return (s * NT + t) * 2048 + (((ki >> 1) * 64 + lane) << 4) + ((ki & 1) << 3) + j
     return ((((s * NT + t) * 4 + ki) * 64 + lane) << 3) + j
 
 
@@ -115,7 +119,7 @@ class TiledWide:
     def gather_rows(self, rows: torch.Tensor) -> torch.Tensor:
         rows = rows.to(self.buf.device, torch.int64)
         f = torch.arange(self.d, device=self.buf.device, dtype=torch.int64).unsqueeze(1)
-        off = wide_offsets(f, rows.unsqueeze(0), self.d)
+        off = wide_offsets(f, rows.unsqueeze(0), self.d, self.eb)
         if self.eb == 16:
             return self.buf.view(torch.bfloat16)[off]
         q = self.buf.view(torch.float8_e4m3fn)[off].to(torch.float32)

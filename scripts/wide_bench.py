@@ -32,17 +32,32 @@ for r0 in range(0, n, chunk):
     del Xc
 T = TiledWide(buf, d, n, eb, scale if eb == 8 else None)
 y = torch.randn(n, generator=g, device="cuda")
-out = device.gram_stats(T, y, None, None, "fp8" if eb == 8 else "bf16", x_zero_dead=True)
-torch.cuda.synchronize()
+comp = "fp8" if eb == 8 else "bf16"
+# A/B variants interleaved in one process: "ring:order:waves" (env DQ4ML_WIDE_RING/_ORDER/_WAVES)
+variants = os.environ.get("VARIANTS", "4:morton:4").split(",")
 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-times = []
+res = {v: [] for v in variants}
+outs = {}
 for _ in range(reps):
-    e0.record()
-    out = device.gram_stats(T, y, None, None, "fp8" if eb == 8 else "bf16", x_zero_dead=True)
-    e1.record()
-    torch.cuda.synchronize()
-    times.append(e0.elapsed_time(e1))
-times.sort()
+    for v in variants:
+        ring, order, waves = (v.split(":") + ["4"])[:3]
+        os.environ["DQ4ML_WIDE_RING"], os.environ["DQ4ML_WIDE_ORDER"] = ring, order
+        os.environ["DQ4ML_WIDE_WAVES"] = waves
+        if v not in outs:  # warm-up + result
+            outs[v] = device.gram_stats(T, y, None, None, comp, x_zero_dead=True)
+        torch.cuda.synchronize()
+        e0.record()
+        out = device.gram_stats(T, y, None, None, comp, x_zero_dead=True)
+        e1.record()
+        torch.cuda.synchronize()
+        res[v].append(e0.elapsed_time(e1))
+base = outs[variants[0]]
+for v in variants:
+    t = sorted(res[v])
+    diff = float((outs[v] - base).abs().max() / base.abs().max())
+    print(json.dumps({"variant": v, "ms_median": t[len(t) // 2], "ms_min": t[0], "max_rel_diff_vs_first": diff}))
+times = sorted(res[variants[0]])
+out = outs[variants[0]]
 ms = times[len(times) // 2]
 P = (d + 255) // 256
 mfma_flops = 2.0 * n * 256 * 256 * (P * (P + 1) // 2)  # executed on the real panel pairs

@@ -7,19 +7,25 @@ import torch
 from net.jgp.labs.sparkdq4ml_amd.ops import layout
 
 
-def test_wide_offsets_is_a_bijection():
+@pytest.mark.parametrize("eb", [16, 8])
+def test_wide_offsets_is_a_bijection(eb):
     # host-only: every (feature, row) of a padded 2-panel, 3-superstep image maps to a distinct slot
     d, n = 300, 192
     nt = ((d + 255) // 256) * 8
     f = torch.arange(nt * 32).unsqueeze(1)
     r = torch.arange(n).unsqueeze(0)
-    off = layout.wide_offsets(f, r, d).reshape(-1)
+    off = layout.wide_offsets(f, r, d, eb).reshape(-1)
     assert off.numel() == nt * 32 * n
     assert torch.unique(off).numel() == off.numel()
     assert int(off.min()) == 0 and int(off.max()) == nt * 32 * n - 1
-    # a k-step (16 rows) of one 32-feature tile is one contiguous 512-element chunk
-    o = layout.wide_offsets(torch.arange(32).unsqueeze(1), torch.arange(16).unsqueeze(0), d)
-    assert sorted(o.reshape(-1).tolist()) == list(range(512))
+    # one superstep (64 rows) of one 32-feature tile is one contiguous 2048-element chunk
+    o = layout.wide_offsets(torch.arange(32).unsqueeze(1), torch.arange(64).unsqueeze(0), d, eb)
+    assert sorted(o.reshape(-1).tolist()) == list(range(2048))
+    if eb == 8:  # a lane's 32 bytes: rows {16 ki + 8 h + j} of one feature, halves 1 KiB apart
+        rows = torch.tensor([r for r in range(64) if not (r >> 3) & 1]).unsqueeze(0)  # lane-half 0
+        o = layout.wide_offsets(torch.tensor([[5]]), rows, d, eb).reshape(-1)
+        lane0 = [int(x) for x in o if int(x) < 1024]
+        assert sorted(lane0) == list(range(5 * 16, 5 * 16 + 16))
 
 
 gpu = pytest.mark.gpu
