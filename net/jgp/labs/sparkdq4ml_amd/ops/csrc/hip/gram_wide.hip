@@ -101,7 +101,8 @@ struct StageFrags {
   F b[2][WN];  // [k-step][B tile]
 };
 
-// One (pair, split) block's K loop + epilogue.  MODE 0: full panel pair; 1: (I, augmentation);
+// One (pair, split) block's K loop + epilogue.  MODE 0: off-diagonal panel pair; 3: diagonal pair
+// (one panel, loaded once); 1: (I, augmentation);
 // 2: (augmentation, augmentation).  Separate instantiations keep the accumulators in AGPRs with no
 // control-flow merge inside the loop (a merge there costs a full AGPR<->VGPR copy per stage).
 //
@@ -110,7 +111,14 @@ struct StageFrags {
 //   glds stage i+4 into the buffer stage i vacated | MFMAs on A tiles 2-3 | lgkmcnt(0)
 // so the LDS reads and the barrier skew hide under half a stage of MFMAs, and three stages of
 // global_load_lds stay in flight across every barrier.
-template <int EB, int MODE, int RING, int WAVES>
+template <typename V>
+__device__ __forceinline__ void keep_live(const V& v) {
+#pragma unroll
+  for (int e = 0; e < (int)(sizeof(V) / 4); ++e) asm volatile("" ::"v"(reinterpret_cast<const unsigned*>(&v)[e]));
+}
+
+// ABL (diagnostic builds only): 0 = real kernel, 1 = no MFMA (loads + LDS reads), 2 = no glds
+template <int EB, int MODE, int RING, int WAVES, int ABL = 0>
 __device__ __forceinline__ void syrk_block(const WideArgs& a, unsigned char* smem, int I, int J, int pair, int split) {
   typedef WideTraits<EB> Tr;
   typedef typename Tr::frag F;
@@ -118,7 +126,12 @@ __device__ __forceinline__ void syrk_block(const WideArgs& a, unsigned char* sme
   constexpr int kWBlock = 64 * WAVES;
   constexpr int WN = WAVES == 4 ? 4 : 2;              // 32-col tiles per wave
   constexpr int kLoadsPerPanel = kPanelStage / (kWBlock * 16);
-  constexpr int kLoadsPerStage = 2 * kLoadsPerPanel;
+  // loads per thread per stage: an augmentation side needs only piece 0 (tile 0 = [1, y_hi, y_lo]
+  // for threads < 128, the zero page into tile 1 for the rest — waves whose tiles are all zero
+  // read tile 1); a diagonal pair (MODE 3) loads its one panel once
+  constexpr int LA = MODE == 2 ? 1 : kLoadsPerPanel;
+  constexpr int LB = MODE == 3 ? 0 : (MODE >= 1 ? 1 : kLoadsPerPanel);
+  constexpr int kLoadsPerStage = LA + LB;
   typedef StageFrags<F, WN> SF;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = WAVES == 4 ? wave >> 1 : wave >> 2, wn = WAVES == 4 ? wave & 1 : wave & 3;
@@ -137,25 +150,26 @@ __device__ __forceinline__ void syrk_block(const WideArgs& a, unsigned char* sme
     const int64_t tile_off = (int64_t)(o >> 11) * Tr::kTileStride + (o & (kChunk - 1));
     srcA[r] = MODE == 2 ? (o < kChunk ? a.Xaug + o : a.zeros + o)
                         : a.X + (int64_t)I * kTilesPerPanel * Tr::kTileStride + tile_off;
-    srcB[r] = MODE >= 1 ? (o < kChunk ? a.Xaug + o : a.zeros + o)
-                        : a.X + (int64_t)J * kTilesPerPanel * Tr::kTileStride + tile_off;
+    srcB[r] = (MODE == 1 || MODE == 2) ? (o < kChunk ? a.Xaug + o : a.zeros + o)
+                                        : a.X + (int64_t)J * kTilesPerPanel * Tr::kTileStride + tile_off;
   }
   // stages at or beyond cnt stream the zero page: the K loop then runs an even number of stages
   // with no branch at all (a branch there lets the compiler sink MFMAs past the barrier) and
   // every wait is the same counted vmcnt — the extra stage multiplies zeros
   auto issue = [&](int64_t st, int buf) {
+    if (ABL == 2) return;
     unsigned char* base = smem + buf * kStageBytes;
     const bool live = st < cnt;
     const int64_t dx = Tr::sdelta(st0 + st, a.NT), dg = Tr::sdelta(st0 + st, 1);
 #pragma unroll
-    for (int r = 0; r < kLoadsPerPanel; ++r) {
+    for (int r = 0; r < LA; ++r) {
       const int o = (r * kWBlock + tid) * 16;
       const bool real = o < kChunk;
       const unsigned char* s = MODE == 2 ? (real ? srcA[r] + dg : srcA[r]) : srcA[r] + dx;
       glds16(live ? s : a.zeros + o, base + (r * kWBlock + wave * 64) * 16);
     }
 #pragma unroll
-    for (int r = 0; r < kLoadsPerPanel; ++r) {
+    for (int r = 0; r < LB; ++r) {
       const int o = (r * kWBlock + tid) * 16;
       const bool real = o < kChunk;
       const unsigned char* s = MODE >= 1 ? (real ? srcB[r] + dg : srcB[r]) : srcB[r] + dx;
@@ -164,15 +178,17 @@ __device__ __forceinline__ void syrk_block(const WideArgs& a, unsigned char* sme
   };
   auto read = [&](SF& f, int buf) {
     const unsigned char* A = smem + buf * kStageBytes;
-    const unsigned char* B = A + kPanelStage;
+    const unsigned char* B = MODE == 3 ? A : A + kPanelStage;
+    const int ta = MODE == 2 ? (wm == 0 ? 0 : 1) : wm * 4;                        // first A tile
+    const int tb = (MODE == 1 || MODE == 2) ? (wn == 0 ? 0 : 1) : wn * WN;       // first B tile
 #pragma unroll
     for (int kk = 0; kk < Tr::kSteps; ++kk) {
 #pragma unroll
       for (int x = 0; x < 4; ++x)
-        if (MODE != 2 || x == 0) f.a[kk][x] = Tr::read(A + (wm * 4 + x) * kChunk, kk, lane);
+        if (MODE != 2 || x == 0) f.a[kk][x] = Tr::read(A + (ta + x) * kChunk, kk, lane);
 #pragma unroll
       for (int y = 0; y < WN; ++y)
-        if (MODE == 0 || y == 0) f.b[kk][y] = Tr::read(B + (wn * WN + y) * kChunk, kk, lane);
+        if (MODE == 0 || MODE == 3 || y == 0) f.b[kk][y] = Tr::read(B + (tb + y) * kChunk, kk, lane);
     }
   };
 
@@ -184,6 +200,16 @@ __device__ __forceinline__ void syrk_block(const WideArgs& a, unsigned char* sme
   // (augmentation modes: waves whose B (or A) tiles come from the zero page multiply zeros —
   // cheaper than a data-dependent branch around the accumulators)
   auto mfmas = [&](const SF& f, int x0) {
+    if (ABL == 1) {
+#pragma unroll
+      for (int kk = 0; kk < Tr::kSteps; ++kk) {
+#pragma unroll
+        for (int x = x0; x < x0 + 2; ++x) keep_live(f.a[kk][x]);
+#pragma unroll
+        for (int y = 0; y < WN; ++y) keep_live(f.b[kk][y]);
+      }
+      return;
+    }
 #pragma unroll
     for (int kk = 0; kk < Tr::kSteps; ++kk)
 #pragma unroll
@@ -191,7 +217,7 @@ __device__ __forceinline__ void syrk_block(const WideArgs& a, unsigned char* sme
         if (MODE == 2 && x != 0) continue;
 #pragma unroll
         for (int y = 0; y < WN; ++y) {
-          if (MODE != 0 && y != 0) continue;
+          if ((MODE == 1 || MODE == 2) && y != 0) continue;
           acc[x][y] = Tr::mfma(f.a[kk][x], f.b[kk][y], acc[x][y]);
         }
       }
@@ -210,12 +236,12 @@ __device__ __forceinline__ void syrk_block(const WideArgs& a, unsigned char* sme
     mfmas(cur, 2);
     read(nxt, nb);
     issue(i + RING, rb);
-    if (MODE == 0) {
+    if (MODE == 0 || MODE == 3) {
 #pragma unroll
       for (int g = 0; g < 2 * WN; ++g) {
         __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                  // 1 MFMA
         __builtin_amdgcn_sched_group_barrier(0x100, (4 + WN) * Tr::kSteps * (EB == 8 ? 2 : 1) / (2 * WN), 0);  // DS reads
-        __builtin_amdgcn_sched_group_barrier(0x020, kLoadsPerStage / (2 * WN), 0);  // glds (VMEM)
+        __builtin_amdgcn_sched_group_barrier(0x020, (kLoadsPerStage + 2 * WN - 1) / (2 * WN), 0);  // glds
         __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);                  // VALU address math
       }
     }
@@ -255,7 +281,7 @@ __device__ __forceinline__ void syrk_block(const WideArgs& a, unsigned char* sme
       }
 }
 
-template <int EB, int RING, int WAVES>
+template <int EB, int RING, int WAVES, int ABL = 0>
 __global__ __launch_bounds__(64 * WAVES, 1) void gram_wide_kernel(WideArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   // XCD-aware bijective remap: dispatch puts block b on XCD b % 8; give each XCD a contiguous
@@ -265,55 +291,63 @@ __global__ __launch_bounds__(64 * WAVES, 1) void gram_wide_kernel(WideArgs a) {
   const int npair = (a.npanels + 1) * (a.npanels + 2) / 2;
   const int split = L / npair, pair = L - split * npair;
   const int I = a.pairs[2 * pair], J = a.pairs[2 * pair + 1];
-  if (J != a.npanels) syrk_block<EB, 0, RING, WAVES>(a, smem, I, J, pair, split);
-  else if (I != a.npanels) syrk_block<EB, 1, RING, WAVES>(a, smem, I, J, pair, split);
-  else syrk_block<EB, 2, RING, WAVES>(a, smem, I, J, pair, split);
+  if (I == J && J != a.npanels) syrk_block<EB, 3, RING, WAVES, ABL>(a, smem, I, J, pair, split);
+  else if (J != a.npanels) syrk_block<EB, 0, RING, WAVES, ABL>(a, smem, I, J, pair, split);
+  else if (I != a.npanels) syrk_block<EB, 1, RING, WAVES, ABL>(a, smem, I, J, pair, split);
+  else syrk_block<EB, 2, RING, WAVES, ABL>(a, smem, I, J, pair, split);
 }
 
 // f64 reduction of the split-K slabs, fp8 scales applied, straight into the flat WLS layout:
 // [count, wSum, wwSum, bSum, bbSum, aSum(d), abSum(d), aa packed-upper(d)]
-__device__ __forceinline__ double slab_sum(const WideArgs& a, int pair, int r, int c) {
-  double s = 0.0;
-  const float* p = a.part + (int64_t)pair * a.splitk * kPanel * kPanel + r * kPanel + c;
-  for (int k = 0; k < a.splitk; ++k) s += (double)p[(int64_t)k * kPanel * kPanel];
-  return s;
-}
 
 
+// Walks the partial tiles in STORAGE order (thread = one (pair, row, col) element; the split-K
+// slabs of consecutive threads are consecutive floats, so every read is coalesced) and scatters
+// the f64 sums into the flat WLS layout.  Augmentation columns [1, y_hi, y_lo] fold into
+// aSum / abSum / the five scalars.
 __global__ __launch_bounds__(256) void gram_wide_reduce_kernel(WideArgs a, const float* __restrict__ scales,
                                                               double* __restrict__ out) {
   const int d = a.d, P = a.npanels;
-  const int64_t K = 5 + 2 * (int64_t)d + (int64_t)d * (d + 1) / 2;
-  for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < K; k += (int64_t)gridDim.x * blockDim.x) {
-    const int pa = pair_index(P, P, P);
-    const double s1 = a.aug_scale[0], syh = a.aug_scale[1], syl = a.aug_scale[2];
-    double v;
-    if (k < 5) {
-      const double g11 = slab_sum(a, pa, 0, 0) * s1 * s1;
-      const double g1h = slab_sum(a, pa, 0, 1) * s1 * syh, g1l = slab_sum(a, pa, 0, 2) * s1 * syl;
-      const double ghh = slab_sum(a, pa, 1, 1) * syh * syh, ghl = slab_sum(a, pa, 1, 2) * syh * syl;
-      const double gll = slab_sum(a, pa, 2, 2) * syl * syl;
-      if (k <= 2) v = g11;                       // count, wSum, wwSum (unit weights; dead rows are zero)
-      else if (k == 3) v = g1h + g1l;            // Σy
-      else v = ghh + 2.0 * ghl + gll;            // Σy²
-    } else if (k < 5 + 2 * (int64_t)d) {
-      const int i = (int)((k - 5) % d);
-      const bool xy = (k - 5) >= d;
-      const int pi = pair_index(i / kPanel, P, P);
-      const double si = scales ? (double)scales[i] : 1.0;
-      if (!xy) v = slab_sum(a, pi, i % kPanel, 0) * si * s1;
-      else v = slab_sum(a, pi, i % kPanel, 1) * si * syh + slab_sum(a, pi, i % kPanel, 2) * si * syl;
-    } else {
-      const int64_t kk = k - (5 + 2 * (int64_t)d);
-      int64_t j = (int64_t)((sqrt(8.0 * (double)kk + 1.0) - 1.0) * 0.5);
-      while (j * (j + 1) / 2 > kk) --j;
-      while ((j + 1) * (j + 2) / 2 <= kk) ++j;
-      const int64_t i = kk - j * (j + 1) / 2;
-      const int pij = pair_index((int)(i / kPanel), (int)(j / kPanel), P);
-      const double sc = scales ? (double)scales[i] * (double)scales[j] : 1.0;
-      v = slab_sum(a, pij, (int)(i % kPanel), (int)(j % kPanel)) * sc;
+  const int npair = (P + 1) * (P + 2) / 2;
+  const int64_t tot = (int64_t)npair * kPanel * kPanel;
+  const double s1 = a.aug_scale[0], syh = a.aug_scale[1], syl = a.aug_scale[2];
+  const int64_t slab = (int64_t)kPanel * kPanel;
+  for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < tot; g += (int64_t)gridDim.x * blockDim.x) {
+    const int pr = (int)(g / slab);
+    const int e = (int)(g - (int64_t)pr * slab), r = e >> 8, c = e & (kPanel - 1);
+    int I = 0, rem = pr;  // row-major pair index -> (I, J)
+    while (rem >= P + 1 - I) { rem -= P + 1 - I; ++I; }
+    const int J = I + rem;
+    const float* base = a.part + (int64_t)pr * a.splitk * slab + e;
+    auto sum = [&](int off) {
+      double v = 0.0;
+      for (int k = 0; k < a.splitk; ++k) v += (double)base[(int64_t)k * slab + off];
+      return v;
+    };
+    const int i = I * kPanel + r;
+    if (J < P) {  // Gram block
+      const int j = J * kPanel + c;
+      if (i < d && j < d && i <= j) {
+        const double sc = scales ? (double)scales[i] * (double)scales[j] : 1.0;
+        out[5 + 2 * (int64_t)d + i + (int64_t)j * (j + 1) / 2] = sum(0) * sc;
+      }
+    } else if (I < P) {  // (X panel, augmentation): column 0 -> aSum, columns 1 + 2 -> abSum
+      if (i < d && c < 2) {
+        const double si = scales ? (double)scales[i] : 1.0;
+        if (c == 0) out[5 + i] = sum(0) * si * s1;
+        else out[5 + d + i] = (sum(0) * syh + sum(1) * syl) * si;
+      }
+    } else if (r == 0 && c == 0) {  // (augmentation, augmentation): the five scalars
+      const double g11 = sum(0) * s1 * s1;
+      const double g1h = sum(1) * s1 * syh, g1l = sum(2) * s1 * syl;
+      const double ghh = sum(kPanel + 1) * syh * syh, ghl = sum(kPanel + 2) * syh * syl;
+      const double gll = sum(2 * kPanel + 2) * syl * syl;
+      out[0] = g11;  // count, wSum, wwSum (unit weights; dead rows are zero)
+      out[1] = g11;
+      out[2] = g11;
+      out[3] = g1h + g1l;                // Σy
+      out[4] = ghh + 2.0 * ghl + gll;    // Σy²
     }
-    out[k] = v;
   }
 }
 
@@ -425,17 +459,20 @@ int64_t gram_wide_partials(int d, int splitk) {
   return (int64_t)npair * splitk * kPanel * kPanel;
 }
 
-template <int EB, int RING, int WAVES>
+template <int EB, int RING, int WAVES, int ABL = 0>
 static void launch_wide(const WideArgs& a, int nblocks, hipStream_t st) {
   const size_t lds = (size_t)RING * kStageBytes;
-  DQ_HIP_CHECK(hipFuncSetAttribute((const void*)gram_wide_kernel<EB, RING, WAVES>,
+  DQ_HIP_CHECK(hipFuncSetAttribute((const void*)gram_wide_kernel<EB, RING, WAVES, ABL>,
                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  hipLaunchKernelGGL((gram_wide_kernel<EB, RING, WAVES>), dim3(nblocks), dim3(64 * WAVES), lds, st, a);
+  hipLaunchKernelGGL((gram_wide_kernel<EB, RING, WAVES, ABL>), dim3(nblocks), dim3(64 * WAVES), lds, st, a);
   DQ_HIP_CHECK(hipGetLastError());
 }
 
 template <int EB>
 static void launch_wide_eb(const WideArgs& a, int nblocks, hipStream_t st, int ring, int waves) {
+  // diagnostic ablations (timing only, wrong results): waves 41 = no MFMA, 42 = no glds
+  if (waves == 41) return launch_wide<EB, 4, 4, 1>(a, nblocks, st);
+  if (waves == 42) return launch_wide<EB, 4, 4, 2>(a, nblocks, st);
   if (waves == 8) ring == 5 ? launch_wide<EB, 5, 8>(a, nblocks, st) : launch_wide<EB, 4, 8>(a, nblocks, st);
   else ring == 5 ? launch_wide<EB, 5, 4>(a, nblocks, st) : launch_wide<EB, 4, 4>(a, nblocks, st);
 }
@@ -447,12 +484,12 @@ void gram_wide(int eb, WideArgs a, const int* pairs_dev, const float* scales, do
   const int npair = (P + 1) * (P + 2) / 2;
   const int nb = npair * a.splitk;
   if (ring != 4 && ring != 5) throw std::invalid_argument("gram_wide: ring must be 4 or 5");
-  if (waves != 4 && waves != 8) throw std::invalid_argument("gram_wide: waves must be 4 or 8");
+  if (waves != 4 && waves != 8 && waves != 41 && waves != 42)
+    throw std::invalid_argument("gram_wide: waves must be 4 or 8");
   if (eb == 16) launch_wide_eb<16>(a, nb, st, ring, waves);
   else launch_wide_eb<8>(a, nb, st, ring, waves);
-  const int64_t K = 5 + 2 * (int64_t)a.d + (int64_t)a.d * (a.d + 1) / 2;
-  int64_t g = (K + 255) / 256;
-  if (g > 8192) g = 8192;
+  int64_t g = ((int64_t)npair * kPanel * kPanel + 255) / 256;
+  if (g > 16384) g = 16384;
   hipLaunchKernelGGL(gram_wide_reduce_kernel, dim3(g), dim3(256), 0, st, a, scales, out);
   DQ_HIP_CHECK(hipGetLastError());
 }

@@ -518,7 +518,7 @@ def _gram_wide(h, T: TiledWide, y, w, sel, x_zero_dead):
     P = (d + 255) // 256
     pairs = _wide_pairs(P, os.environ.get("DQ4ML_WIDE_ORDER", "morton"))
     nsup = max(1, (n + 63) // 64)
-    splitk = _wide_splitk(P, nsup, eb)
+    splitk = int(os.environ.get("DQ4ML_WIDE_SPLITK", "0")) or _wide_splitk(P, nsup, eb)
     # f32 MFMA accumulators count rows exactly only below 2^24 per split
     splitk = max(1, min(max(splitk, -(-nsup * 64 // (1 << 23))), nsup))
     pairs_dev = torch.tensor(np.asarray(pairs, dtype=np.int32).reshape(-1), device=dev)
@@ -527,5 +527,5 @@ def _gram_wide(h, T: TiledWide, y, w, sel, x_zero_dead):
     h.gram_wide(eb, T.buf.data_ptr(), aug.buf.data_ptr(), _zero_page(h, dev).data_ptr(), T.nt, P, d, nsup, splitk,
                 pairs_dev.data_ptr(),
                 part.data_ptr(), 1.0, float(s_h), float(s_l), _ptr(T.scales), out.data_ptr(), _stream(),
-                int(os.environ.get("DQ4ML_WIDE_RING", "4")), int(os.environ.get("DQ4ML_WIDE_WAVES", "4")))
+                int(os.environ.get("DQ4ML_WIDE_RING", "4")), int(os.environ.get("DQ4ML_WIDE_WAVES", "8")))
     return out

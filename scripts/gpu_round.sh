@@ -24,7 +24,7 @@ for s in $STEPS; do
     wide8) step wide8 900 env N=1e7 D=4096 EB=8 VARIANTS="${VARIANTS:-4:morton:4}" python scripts/wide_bench.py ;;
     wide16b) step wide16b 900 env N=4e6 D=4096 EB=16 VARIANTS="${VARIANTS:-4:morton:4}" python scripts/wide_bench.py ;;
     wideprof) (export TMPDIR=/tmp N=2e6 D=4096 EB=8 REPS=3; step wideprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/wideprof -o run --output-format csv -- python scripts/wide_bench.py) || exit $? ;;
-    widepmc) (export TMPDIR=/tmp N=1e6 D=4096 EB=${EB:-8} REPS=2
+    widepmc) (export TMPDIR=/tmp N=${N:-1e6} D=4096 EB=${EB:-8} REPS=${REPS:-2} VARIANTS="${VARIANTS:-4:morton:4}"
        step widepmc1 600 rocprofv3 --kernel-trace --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE -d gpurun_out/widepmc1 -o run --output-format csv -- python scripts/wide_bench.py &&
        step widepmc2 600 rocprofv3 --kernel-trace --pmc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum -d gpurun_out/widepmc2 -o run --output-format csv -- python scripts/wide_bench.py) || exit $? ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" ;;

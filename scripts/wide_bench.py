@@ -40,9 +40,9 @@ res = {v: [] for v in variants}
 outs = {}
 for _ in range(reps):
     for v in variants:
-        ring, order, waves = (v.split(":") + ["4"])[:3]
+        ring, order, waves, splitk = (v.split(":") + ["4", "0"][len(v.split(":")) - 2:])[:4]
         os.environ["DQ4ML_WIDE_RING"], os.environ["DQ4ML_WIDE_ORDER"] = ring, order
-        os.environ["DQ4ML_WIDE_WAVES"] = waves
+        os.environ["DQ4ML_WIDE_WAVES"], os.environ["DQ4ML_WIDE_SPLITK"] = waves, splitk
         if v not in outs:  # warm-up + result
             outs[v] = device.gram_stats(T, y, None, None, comp, x_zero_dead=True)
         torch.cuda.synchronize()
