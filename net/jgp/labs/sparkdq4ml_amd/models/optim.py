@@ -123,8 +123,7 @@ def _solve_cholesky(k, aa, ab):
     """-> (x, callable returning the packed inverse)."""
     h = native.host()
     if k >= DEVICE_SOLVE_MIN_K:
-        x, inv = _device_cholesky(k, aa, ab)
-        return x, (lambda: inv)
+        return _device_cholesky(k, aa, ab)
     try:
         x = h.cholesky_solve(k, aa, ab)
     except h.SingularMatrixError as e:
@@ -154,8 +153,8 @@ def _device_cholesky(k, aa, ab):
     if int(info.item()) != 0:
         raise SingularMatrixException("LAPACK.dppsv returned a non-positive pivot: A is not positive definite.")
     x = torch.cholesky_solve(torch.as_tensor(ab, dtype=torch.float64, device=dev).unsqueeze(1), L).squeeze(1)
-    inv = torch.cholesky_inverse(L)
-    return x.cpu().numpy(), inv[I, J].cpu().numpy()
+    # (AᵀA)⁻¹ only when the summary asks for standard errors (lazy diagInvAtWA)
+    return x.cpu().numpy(), (lambda: torch.cholesky_inverse(L)[I, J].cpu().numpy())
 
 
 def weighted_least_squares(stats: GramStats, fit_intercept: bool, reg_param: float, elastic_net: float,

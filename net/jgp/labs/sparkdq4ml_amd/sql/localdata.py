@@ -117,7 +117,15 @@ def table_from_data(data, schema, device) -> Table:
         n = None
         for k in names:
             v = data[k]
-            if torch.is_tensor(v) or isinstance(v, np.ndarray):
+            from ..ops.layout import TiledBF16, TiledWide
+
+            valid = None
+            if isinstance(v, tuple) and len(v) == 2 and torch.is_tensor(v[0]):  # (values, validity mask)
+                v, valid = v
+                valid = torch.as_tensor(valid, dtype=torch.bool).to(device)
+            if isinstance(v, (TiledBF16, TiledWide)):  # pre-tiled device feature matrix (zero copy)
+                c = ColumnData(VectorUDT(), v, None, {"ml_attr": {"num_attrs": int(v.d)}})
+            elif torch.is_tensor(v) or isinstance(v, np.ndarray):
                 t = torch.as_tensor(v).to(device)
                 if t.dim() == 2:
                     dt = VectorUDT()
@@ -132,7 +140,7 @@ def table_from_data(data, schema, device) -> Table:
                 else:
                     dt = {torch.float64: DoubleType(), torch.float32: FloatType(), torch.int32: IntegerType(),
                           torch.int64: LongType(), torch.bool: BooleanType()}.get(t.dtype, DoubleType())
-                    c = ColumnData(dt, t if t.dtype == dt.torch_dtype else t.to(dt.torch_dtype), None)
+                    c = ColumnData(dt, t if t.dtype == dt.torch_dtype else t.to(dt.torch_dtype), valid)
             else:
                 vals = list(v)
                 dt = NullType()

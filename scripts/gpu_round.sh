@@ -27,6 +27,9 @@ for s in $STEPS; do
     widepmc) (export TMPDIR=/tmp N=${N:-1e6} D=4096 EB=${EB:-8} REPS=${REPS:-2} VARIANTS="${VARIANTS:-4:morton:4}"
        step widepmc1 600 rocprofv3 --kernel-trace --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE -d gpurun_out/widepmc1 -o run --output-format csv -- python scripts/wide_bench.py &&
        step widepmc2 600 rocprofv3 --kernel-trace --pmc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum -d gpurun_out/widepmc2 -o run --output-format csv -- python scripts/wide_bench.py) || exit $? ;;
+    cfg4) step cfg4 900 python benchmarks/bench_dq_pipeline.py --steps 5 --warmup 2 --json-out gpurun_out/cfg4.json ;;
+    cfg5) step cfg5 900 python benchmarks/bench_wide.py --steps 3 --warmup 1 --json-out gpurun_out/cfg5.json ;;
+    cfg1) step cfg1 300 python benchmarks/bench_cpu_small.py --json-out gpurun_out/cfg1.json ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" ;;
     bench) step bench 600 python bench.py --steps 20 --warmup 3 ;;
     fitprof) step fitprof 300 env N=1.25e7 python scripts/fit_profile.py ;;
