@@ -53,8 +53,15 @@ class GramStats:
     def from_flat(cls, flat: np.ndarray, k: int) -> "GramStats":
         flat = np.asarray(flat, dtype=np.float64)
         assert flat.shape[0] == cls.layout_size(k), (flat.shape, k)
-        return cls(k, flat[0], flat[1], flat[2], flat[3], flat[4], flat[5:5 + k].copy(),
-                   flat[5 + k:5 + 2 * k].copy(), flat[5 + 2 * k:].copy())
+        # views, not copies: at k = 4096 the packed block alone is 67 MB
+        return cls(k, float(flat[0]), float(flat[1]), float(flat[2]), float(flat[3]), float(flat[4]),
+                   flat[5:5 + k], flat[5 + k:5 + 2 * k], flat[5 + 2 * k:])
+
+    @classmethod
+    def scalars_only(cls, head, k: int) -> "GramStats":
+        """Statistics whose vector parts stayed on the device (large-k device solve)."""
+        h = [float(v) for v in head[:5]]
+        return cls(k, h[0], h[1], h[2], h[3], h[4], None, None, None)
 
     # derived (Aggregator accessors)
     @property
@@ -157,10 +164,166 @@ def _device_cholesky(k, aa, ab):
     return x.cpu().numpy(), (lambda: torch.cholesky_inverse(L)[I, J].cpu().numpy())
 
 
+_SOLVER_CODES = {"auto": 0, "cholesky": 1, "quasi-newton": 2}
+
+
+def fit_wls_flat(flat, nf: int, fit_intercept: bool, reg_param: float, elastic_net: float,
+                 standardize_features: bool, standardize_label: bool, solver_type: str, max_iter: int,
+                 tol: float):
+    """``WeightedLeastSquares.fit`` straight from the (all-reduced) flat statistics.
+
+    Returns ``(WLSModel, GramStats)``.  k <= 1024 (or host statistics): one D2H of the flat vector
+    and the native driver ``_dq4ml_host.wls_fit`` (standardize -> Cholesky / OWLQN / L-BFGS ->
+    un-standardize in C++).  Larger k with the statistics on the device and no L1 term: the
+    standardized system is assembled and Cholesky-solved on the device (f64), only the
+    coefficients come back."""
+    import torch
+
+    k = nf + 1 if fit_intercept else nf
+    use_qn = (solver_type == "auto" and elastic_net != 0.0 and reg_param != 0.0) or solver_type == "quasi-newton"
+    if torch.is_tensor(flat) and flat.is_cuda and k >= DEVICE_SOLVE_MIN_K and not use_qn:
+        return _wls_device(flat, nf, fit_intercept, reg_param, elastic_net, standardize_features,
+                           standardize_label, solver_type, max_iter, tol)
+    host = flat.detach().cpu().numpy() if torch.is_tensor(flat) else np.asarray(flat, dtype=np.float64)
+    stats = GramStats.from_flat(host, nf)
+    return _wls_native(host, stats, fit_intercept, reg_param, elastic_net, standardize_features,
+                       standardize_label, solver_type, max_iter, tol), stats
+
+
+def _check_status(status: int, singular_fallback: bool = False):
+    if status == 1:
+        raise ValueError("Sum of weights cannot be zero.")
+    if status == 2:
+        raise ValueError("Training dataset is empty.")
+    if status == 3:
+        log.warning("The standard deviation of the label is zero, so the coefficients will be zeros and the "
+                    "intercept will be the mean of the label; as a result, training is not needed.")
+    elif status == 4:
+        log.warning("Mean and standard deviation of the label are zero, so the coefficients and the intercept "
+                    "will all be zero; as a result, training is not needed.")
+    elif status == 5:
+        raise ValueError("The standard deviation of the label is zero. Model cannot be regularized with "
+                         "standardization=true")
+    elif status == 6:
+        log.warning("The standard deviation of the label is zero. Consider setting fitIntercept=true.")
+    if singular_fallback:
+        log.warning("Cholesky solver failed due to singular covariance matrix. Retrying with Quasi-Newton solver.")
+
+
+def _wls_native(flat_np, stats, fit_intercept, reg_param, elastic_net, standardize_features, standardize_label,
+                solver_type, max_iter, tol) -> WLSModel:
+    if reg_param == 0.0:
+        log.warning("regParam is zero, which might cause numerical instability and overfitting.")
+    nf = stats.k
+    h = native.host()
+    try:
+        r = h.wls_fit(flat_np, nf, fit_intercept, float(reg_param), float(elastic_net), bool(standardize_features),
+                      bool(standardize_label), _SOLVER_CODES[solver_type], int(max_iter), float(tol), True)
+    except h.SingularMatrixError as e:
+        raise SingularMatrixException(str(e)) from None
+    _check_status(r["status"], r["singular_fallback"])
+    if r["status"] in (3, 4):
+        return WLSModel(np.zeros(nf), float(r["intercept"]), np.zeros(1), np.zeros(1), "none")
+    if r["converged_reason"]:
+        log.info("quasi-newton converged: %s after %d states", r["converged_reason"], len(r["objective_history"]))
+    diag_inv = np.zeros(1)
+    if r["solver"] == "cholesky":
+        ata, a_std, wsum = r["ata"], r["a_std"], float(r["w_sum"])
+        k = nf + 1 if fit_intercept else nf
+
+        def diag_inv():
+            inv = h.cholesky_inverse(k, ata)
+            mult = np.ones(k)
+            mult[:nf] = a_std * a_std
+            idx = np.arange(1, k + 1)
+            return inv[idx + (idx - 1) * idx // 2 - 1] / (wsum * mult)
+    return WLSModel(np.asarray(r["coefficients"]), float(r["intercept"]), diag_inv,
+                    np.asarray(r["objective_history"], dtype=np.float64), r["solver"])
+
+
+_dev_index_cache = {}
+
+
+def _wls_device(flat, nf, fit_intercept, reg_param, elastic_net, standardize_features, standardize_label,
+                solver_type, max_iter, tol):
+    """Large-k Cholesky branch of WLS on the device (f64; same algebra as ``wls.cpp``)."""
+    import torch
+
+    dev = flat.device
+    head = flat[:5].cpu().numpy()
+    stats = GramStats.scalars_only(head, nf)
+    count, wSum, _, bSum, bbSum = (float(v) for v in head)
+    rawBBar = bSum / wSum if wSum > 0 else 0.0
+    rawBStd = float(np.sqrt(max(bbSum / wSum - rawBBar * rawBBar, 0.0))) if wSum > 0 else 0.0
+    if wSum <= 0.0 or rawBStd == 0.0:  # rare short-circuits: the native driver owns their semantics
+        host = flat.cpu().numpy()
+        full = GramStats.from_flat(host, nf)
+        return _wls_native(host, full, fit_intercept, reg_param, elastic_net, standardize_features,
+                           standardize_label, solver_type, max_iter, tol), full
+    if reg_param == 0.0:
+        log.warning("regParam is zero, which might cause numerical instability and overfitting.")
+    bStd = rawBStd
+    key = (dev, nf)
+    if key not in _dev_index_cache:
+        I, J = packed_upper_indices(nf)
+        _dev_index_cache.clear()
+        _dev_index_cache[key] = (torch.as_tensor(I, device=dev), torch.as_tensor(J, device=dev),
+                                 torch.as_tensor(_packed_diag_index(nf), device=dev))
+    I, J, dj = _dev_index_cache[key]
+    aSum, abSum, aaP = flat[5:5 + nf], flat[5 + nf:5 + 2 * nf], flat[5 + 2 * nf:]
+    m = aSum / wSum
+    aStd = torch.sqrt(torch.clamp(aaP[dj] / wSum - m * m, min=0.0))
+    nz = aStd != 0.0
+    safe = torch.where(nz, aStd, torch.ones_like(aStd))
+    aBar = torch.where(nz, m / safe, torch.zeros_like(m))
+    abBar = torch.where(nz, abSum / wSum / (safe * bStd), torch.zeros_like(m))
+    den = aStd[I] * aStd[J]
+    vals = torch.where(den != 0.0, aaP / wSum / torch.where(den != 0.0, den, torch.ones_like(den)),
+                       torch.zeros_like(den))
+    k = nf + 1 if fit_intercept else nf
+    A = torch.zeros(k, k, dtype=torch.float64, device=dev)
+    A[I, J] = vals
+    A[J, I] = vals
+    eff_l2 = (1.0 - elastic_net) * reg_param / bStd
+    lam = torch.full((nf,), eff_l2, dtype=torch.float64, device=dev)
+    if not standardize_features:
+        lam = torch.where(nz, lam / (safe * safe), torch.zeros_like(lam))
+    if not standardize_label:
+        lam = lam * bStd
+    ar = torch.arange(nf, device=dev)
+    A[ar, ar] += lam
+    b = abBar
+    if fit_intercept:
+        A[:nf, nf] = aBar
+        A[nf, :nf] = aBar
+        A[nf, nf] = 1.0
+        b = torch.cat([abBar, torch.tensor([rawBBar / bStd], dtype=torch.float64, device=dev)])
+    L, info = torch.linalg.cholesky_ex(A)
+    if int(info.item()) != 0:
+        if solver_type != "auto":
+            raise SingularMatrixException("LAPACK.dppsv returned a non-positive pivot: A is not positive definite.")
+        host = flat.cpu().numpy()
+        full = GramStats.from_flat(host, nf)
+        return _wls_native(host, full, fit_intercept, reg_param, elastic_net, standardize_features,
+                           standardize_label, "quasi-newton", max_iter, tol), full
+    x = torch.cholesky_solve(b.unsqueeze(1), L).squeeze(1)
+    coef = torch.where(nz, x[:nf] * bStd / safe, torch.zeros_like(m)).cpu().numpy()
+    intercept = float(x[nf].item() * bStd) if fit_intercept else 0.0
+
+    def diag_inv():
+        inv = torch.cholesky_inverse(L).diagonal()
+        mult = torch.ones(k, dtype=torch.float64, device=dev)
+        mult[:nf] = aStd * aStd
+        return (inv / (wSum * mult)).cpu().numpy()
+    return WLSModel(coef, intercept, diag_inv, np.zeros(1), "cholesky"), stats
+
+
 def weighted_least_squares(stats: GramStats, fit_intercept: bool, reg_param: float, elastic_net: float,
                            standardize_features: bool, standardize_label: bool, solver_type: str,
                            max_iter: int, tol: float) -> WLSModel:
-    """``WeightedLeastSquares.fit`` on pre-aggregated statistics (solver_type: auto|cholesky|quasi-newton)."""
+    """``WeightedLeastSquares.fit`` on pre-aggregated statistics (solver_type: auto|cholesky|quasi-newton)
+    — the NumPy reference implementation of the native driver (``csrc/host/wls.cpp``), kept as the
+    test oracle for it."""
     if reg_param == 0.0:
         log.warning("regParam is zero, which might cause numerical instability and overfitting.")
     if stats.wSum <= 0.0:

@@ -31,7 +31,7 @@ from ..sql.table import ColumnData
 from ..sql.types import DoubleType, VectorUDT, is_numeric
 from ..utils.logging import get_logger
 from .linalg import DenseVector, Vector, Vectors
-from .optim import MAX_NUM_FEATURES, GramStats, weighted_least_squares
+from .optim import MAX_NUM_FEATURES, GramStats, fit_wls_flat
 from .param import Param, Params, param_accessors
 
 __all__ = ["LinearRegression", "LinearRegressionModel", "LinearRegressionTrainingSummary",
@@ -173,9 +173,8 @@ class LinearRegression(_LRParams):
         x_zero_dead = yvalid is None and (tbl.sel is None or (zd is not False and zd is tbl.sel))
         flat = kernels.gram_stats(X.values, yv, w, sel, self.getOrDefault("gramDtype"), x_zero_dead=x_zero_dead)
         flat = comm.all_reduce_sum(flat)  # X1: data-parallel Gram all-reduce (RCCL over xGMI)
-        stats = GramStats.from_flat(flat.cpu().numpy(), d)
-        wls = weighted_least_squares(
-            stats, self.getOrDefault("fitIntercept"), float(self.getOrDefault("regParam")),
+        wls, stats = fit_wls_flat(
+            flat, d, self.getOrDefault("fitIntercept"), float(self.getOrDefault("regParam")),
             float(self.getOrDefault("elasticNetParam")), bool(self.getOrDefault("standardization")), True,
             "auto", int(self.getOrDefault("maxIter")), float(self.getOrDefault("tol")))
         model = LinearRegressionModel(self.uid, DenseVector(wls.coefficients), float(wls.intercept))

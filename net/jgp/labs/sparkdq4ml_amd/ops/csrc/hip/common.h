@@ -31,6 +31,69 @@ enum DType : int { DT_F64 = 0, DT_F32 = 1, DT_BF16 = 2, DT_I32 = 3, DT_I64 = 4, 
 
 __device__ __forceinline__ float bf16_bits_to_f32(uint16_t b) { return __uint_as_float(uint32_t(b) << 16); }
 
+// 8 consecutive elements [r0, r0+8) of a typed column as f32 (zero past n); 16-byte vector loads
+// when the run is complete and aligned (r0 is a multiple of 8 in every caller)
+__device__ __forceinline__ void load8_f32(const void* p, int dt, int64_t r0, int64_t n, float x[8]) {
+  const bool full = r0 + 8 <= n && ((reinterpret_cast<uintptr_t>(p) & 15) == 0);
+  if (full && dt == DT_F32) {
+    const f32x4 a = *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(p) + r0);
+    const f32x4 b = *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(p) + r0 + 4);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) x[j] = a[j], x[4 + j] = b[j];
+    return;
+  }
+  if (full && dt == DT_F64) {
+    const double* q = reinterpret_cast<const double*>(p) + r0;
+#pragma unroll
+    for (int j = 0; j < 8; j += 2) {
+      const f64x2 v = *reinterpret_cast<const f64x2*>(q + j);
+      x[j] = (float)v[0], x[j + 1] = (float)v[1];
+    }
+    return;
+  }
+  if (full && dt == DT_BF16) {
+    const u32x4 v = *reinterpret_cast<const u32x4*>(reinterpret_cast<const uint16_t*>(p) + r0);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      x[2 * j] = __uint_as_float(v[j] << 16);
+      x[2 * j + 1] = __uint_as_float(v[j] & 0xffff0000u);
+    }
+    return;
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int64_t r = r0 + j;
+    float v = 0.0f;
+    if (r < n) {
+      switch (dt) {
+        case DT_F64: v = (float)reinterpret_cast<const double*>(p)[r]; break;
+        case DT_F32: v = reinterpret_cast<const float*>(p)[r]; break;
+        case DT_BF16: v = bf16_bits_to_f32(reinterpret_cast<const uint16_t*>(p)[r]); break;
+        case DT_I32: v = (float)reinterpret_cast<const int32_t*>(p)[r]; break;
+        case DT_I64: v = (float)reinterpret_cast<const int64_t*>(p)[r]; break;
+        case DT_U8: v = (float)reinterpret_cast<const uint8_t*>(p)[r]; break;
+        default: v = 0.0f;
+      }
+    }
+    x[j] = v;
+  }
+}
+
+// zero the elements of x whose row is dead in the 0/1 selection (one 8-byte load when possible)
+__device__ __forceinline__ void mask8(const uint8_t* sel, int64_t r0, int64_t n, float x[8]) {
+  if (sel == nullptr) return;
+  if (r0 + 8 <= n && ((reinterpret_cast<uintptr_t>(sel + r0) & 7) == 0)) {
+    const uint64_t m = *reinterpret_cast<const uint64_t*>(sel + r0);
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (((m >> (8 * j)) & 0xff) == 0) x[j] = 0.0f;
+    return;
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+    if (r0 + j >= n || sel[r0 + j] == 0) x[j] = 0.0f;
+}
+
 // 32x32 MFMA accumulator (f32, 16 regs): element reg of lane -> (row, col)
 __device__ __forceinline__ int mfma32_row(int lane, int reg) { return (reg & 3) + 8 * (reg >> 2) + 4 * (lane >> 5); }
 __device__ __forceinline__ int mfma32_col(int lane) { return lane & 31; }

@@ -376,54 +376,49 @@ __global__ __launch_bounds__(256) void amax_kernel(const PackSrcW* __restrict__ 
   if (threadIdx.x == 0) amax[blockIdx.x] = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
 }
 
-__device__ __forceinline__ float load_src(const PackSrcW& s, int64_t r) {
-  switch (s.dt) {
-    case DT_F64: return (float)reinterpret_cast<const double*>(s.ptr)[r];
-    case DT_F32: return reinterpret_cast<const float*>(s.ptr)[r];
-    case DT_BF16: return bf16_bits_to_f32(reinterpret_cast<const uint16_t*>(s.ptr)[r]);
-    case DT_I32: return (float)reinterpret_cast<const int32_t*>(s.ptr)[r];
-    case DT_I64: return (float)reinterpret_cast<const int64_t*>(s.ptr)[r];
-    default: return 0.0f;
-  }
-}
-
-// columns -> fragment-ordered tiles (EB = 16: bf16, EB = 8: fp8 with 1/scale pre-multiplied)
+// columns -> wide fragment-ordered tiles (EB = 16: bf16, EB = 8: fp8 with 1/scale pre-multiplied).
+// One block-iteration = one (superstep s, tile t) chunk: thread (f, q) vector-loads rows
+// [8q, 8q+8) of feature f (8 threads per feature: coalesced 256-B column runs); in the wide
+// layout that run is lane 32(q & 1) + f's fragment of k-step q >> 1 -> one 16-B (bf16) or 8-B
+// (fp8) store.
 template <int EB>
 __global__ __launch_bounds__(256) void pack_wide_kernel(const PackSrcW* __restrict__ srcs, int d, int64_t n, int NT,
                                                        int64_t nsup, const uint8_t* __restrict__ sel,
                                                        const float* __restrict__ inv_scale,
                                                        unsigned char* __restrict__ out) {
-  const int64_t nchunks = nsup * NT * 256;
-  for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < nchunks; c += (int64_t)gridDim.x * blockDim.x) {
-    const int lane = (int)(c & 63);
-    const int ki = (int)((c >> 6) & 3);
-    const int64_t st = c >> 8;
-    const int t = (int)(st % NT);
-    const int64_t s = st / NT;
-    const int f = t * 32 + (lane & 31);
-    const int64_t r = s * 64 + 16 * ki + 8 * (lane >> 5);
+  const int fl = threadIdx.x >> 3, q = threadIdx.x & 7;
+  const int ki = q >> 1, lane = 32 * (q & 1) + fl;
+  const int64_t nchunks = nsup * NT;
+  for (int64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
+    const int t = (int)(c % NT);
+    const int64_t s = c / NT;
+    const int f = t * 32 + fl;
+    const int64_t r0 = s * 64 + 8 * q;
     float x[8];
+    if (f < d) {
+      const PackSrcW src = srcs[f];
+      load8_f32(src.ptr, src.dt, r0, n, x);
+      mask8(sel, r0, n, x);
+    } else {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      x[j] = 0.0f;
-      if (f < d && r + j < n && (sel == nullptr || sel[r + j])) x[j] = load_src(srcs[f], r + j);
+      for (int j = 0; j < 8; ++j) x[j] = 0.0f;
     }
     if constexpr (EB == 16) {
       bf16x8 v;
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] = (__bf16)x[j];
-      reinterpret_cast<u32x4*>(out)[c] = __builtin_bit_cast(u32x4, v);
+      reinterpret_cast<u32x4*>(out)[c * 256 + ki * 64 + lane] = __builtin_bit_cast(u32x4, v);
     } else {  // saturate to the e4m3 range (the conversion maps overflow to NaN)
       const float is = f < d ? inv_scale[f] : 0.0f;
-      float q[8];
+      float qv[8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) q[j] = fminf(fmaxf(x[j] * is, -448.0f), 448.0f);
-      int lo = __builtin_amdgcn_cvt_pk_fp8_f32(q[0], q[1], 0, false);
-      lo = __builtin_amdgcn_cvt_pk_fp8_f32(q[2], q[3], lo, true);
-      int hi = __builtin_amdgcn_cvt_pk_fp8_f32(q[4], q[5], 0, false);
-      hi = __builtin_amdgcn_cvt_pk_fp8_f32(q[6], q[7], hi, true);
+      for (int j = 0; j < 8; ++j) qv[j] = fminf(fmaxf(x[j] * is, -448.0f), 448.0f);
+      int lo = __builtin_amdgcn_cvt_pk_fp8_f32(qv[0], qv[1], 0, false);
+      lo = __builtin_amdgcn_cvt_pk_fp8_f32(qv[2], qv[3], lo, true);
+      int hi = __builtin_amdgcn_cvt_pk_fp8_f32(qv[4], qv[5], 0, false);
+      hi = __builtin_amdgcn_cvt_pk_fp8_f32(qv[6], qv[7], hi, true);
       // chunk (s, t) = [2 halves][64 lanes][16 B]; k-step ki -> half ki >> 1, byte 8 * (ki & 1)
-      const int64_t o = (s * NT + t) * 2048 + (((ki >> 1) * 64 + lane) << 4) + ((ki & 1) << 3);
+      const int64_t o = c * 2048 + (((ki >> 1) * 64 + lane) << 4) + ((ki & 1) << 3);
       *reinterpret_cast<u32x2*>(out + o) = u32x2{(unsigned)lo, (unsigned)hi};
     }
   }
@@ -444,7 +439,7 @@ void feature_amax(const PackSrcW* srcs_dev, int d, int64_t n, const uint8_t* sel
 void pack_wide(int eb, const PackSrcW* srcs_dev, int d, int64_t n, int nt, const uint8_t* sel, const float* inv_scale,
                void* out, hipStream_t st) {
   const int64_t nsup = (n + 63) / 64;
-  int64_t g = (nsup * nt * 256 + 255) / 256;
+  int64_t g = nsup * nt;
   if (g > 16384) g = 16384;
   if (g < 1) g = 1;
   unsigned char* o = reinterpret_cast<unsigned char*>(out);

@@ -177,33 +177,36 @@ __device__ __forceinline__ double predict_row(const void* X, int xdt, int64_t ld
   return acc;
 }
 
-// columns (PackSrc per feature) -> tiled bf16, dead rows (sel == 0) written as zeros
+// columns (PackSrc per feature) -> tiled bf16, dead rows (sel == 0) written as zeros.
+// One block-iteration = one (superstep s, tile t) chunk (64 rows x 32 features, 4 KiB out):
+// thread (f, q) loads rows [8q, 8q+8) of feature f with 16-B vector loads (8 threads per feature
+// -> every wave reads 8 contiguous 256-B column runs) and that run is exactly one lane's
+// fragment of k-step q & 3 for lane half q >> 2 -> one 16-B store, no transpose.
 __global__ __launch_bounds__(256) void pack_tiled_kernel(const PackSrc* __restrict__ srcs, int d, int64_t n,
                                                         const uint8_t* __restrict__ sel, int NT, int64_t nsup,
                                                         uint16_t* __restrict__ out) {
-  const int64_t nchunks = nsup * NT * 256;
-  for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < nchunks; c += (int64_t)gridDim.x * blockDim.x) {
-    const int lane = (int)(c & 63);
-    const int i = (int)((c >> 6) & 3);
-    const int64_t st = c >> 8;
-    const int t = (int)(st % NT);
-    const int64_t s = st / NT;
-    const int f = t * 32 + (lane & 31);
-    const int64_t r = s * 64 + 32 * (lane >> 5) + 8 * i;
-    bf16x8 v;
+  const int fl = threadIdx.x >> 3, q = threadIdx.x & 7;
+  const int i = q & 3, h = q >> 2;
+  const int64_t nchunks = nsup * NT;
+  for (int64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
+    const int t = (int)(c % NT);
+    const int64_t s = c / NT;
+    const int f = t * 32 + fl;
+    const int64_t r0 = s * 64 + 8 * q;
+    float x[8];
     if (f < d) {
       const PackSrc src = srcs[f];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        float x = 0.0f;
-        if (r + j < n && (sel == nullptr || sel[r + j] != 0)) x = (float)ld_f64(src.ptr, src.dt, r + j);
-        v[j] = (__bf16)x;
-      }
+      load8_f32(src.ptr, src.dt, r0, n, x);
+      mask8(sel, r0, n, x);
     } else {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = (__bf16)0.0f;
+      for (int j = 0; j < 8; ++j) x[j] = 0.0f;
     }
-    reinterpret_cast<u32x4*>(out)[c] = __builtin_bit_cast(u32x4, v);
+    bf16x8 v;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = (__bf16)x[j];
+    // chunk c = [4 k-steps][64 lanes][8 bf16]; tall layout: lane 32h + f holds rows 32h + 8i + j
+    reinterpret_cast<u32x4*>(out)[c * 256 + i * 64 + h * 32 + fl] = __builtin_bit_cast(u32x4, v);
   }
 }
 
@@ -245,6 +248,94 @@ __global__ __launch_bounds__(256) void metrics_kernel(const void* __restrict__ X
   if (threadIdx.x < 8) {
     partials[(int64_t)blockIdx.x * 8 + threadIdx.x] =
         red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+  }
+}
+
+// ---- predict / metrics over the MFMA-fragment layouts (tiled codes 1 tall bf16, 2 wide bf16,
+// 3 wide fp8): block-iteration = one superstep (64 rows).  Thread (f, q) walks the tiles reading
+// its 16-B (8-B fp8) fragment = rows [8q, 8q+8) of feature t*32 + f in every layout, accumulates
+// coef * x for those 8 rows, and the 32 feature-threads of each row group are summed through LDS
+// — fragment-coalesced loads instead of per-row 2-byte gathers.
+template <int MODE>  // 0: predictions -> out, 1: the 8 metric sums -> partials
+__global__ __launch_bounds__(256) void tiled_rows_kernel(const unsigned char* __restrict__ X, int tiled, int d,
+                                                        int64_t n, const double* __restrict__ coef, double b,
+                                                        const void* __restrict__ y, int ydt,
+                                                        const uint8_t* __restrict__ sel, double shift,
+                                                        double* __restrict__ out) {
+  __shared__ double part[32][65];
+  __shared__ double red[4][8];
+  const int fl = threadIdx.x >> 3, q = threadIdx.x & 7;
+  const int NT = tiled == 1 ? (d + 31) >> 5 : ((d + 255) >> 8) * 8;
+  const int ntiles = (d + 31) >> 5;
+  const int64_t nsup = (n + 63) >> 6;
+  double m[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int64_t s = blockIdx.x; s < nsup; s += gridDim.x) {
+    double acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int t = 0; t < ntiles; ++t) {
+      const int f = t * 32 + fl;
+      if (f >= d) break;
+      const double c = coef[f];
+      const int64_t ch = s * NT + t;
+      float x[8];
+      if (tiled == 3) {
+        const int ki = q >> 1, lane = 32 * (q & 1) + fl;
+        const uint64_t v = *reinterpret_cast<const uint64_t*>(X + ch * 2048 + (((ki >> 1) * 64 + lane) << 4) +
+                                                              ((ki & 1) << 3));
+        const int lo = (int)(uint32_t)v, hi = (int)(uint32_t)(v >> 32);
+        x[0] = __builtin_amdgcn_cvt_f32_fp8(lo, 0);
+        x[1] = __builtin_amdgcn_cvt_f32_fp8(lo, 1);
+        x[2] = __builtin_amdgcn_cvt_f32_fp8(lo, 2);
+        x[3] = __builtin_amdgcn_cvt_f32_fp8(lo, 3);
+        x[4] = __builtin_amdgcn_cvt_f32_fp8(hi, 0);
+        x[5] = __builtin_amdgcn_cvt_f32_fp8(hi, 1);
+        x[6] = __builtin_amdgcn_cvt_f32_fp8(hi, 2);
+        x[7] = __builtin_amdgcn_cvt_f32_fp8(hi, 3);
+      } else {
+        const int64_t unit = tiled == 1 ? ch * 256 + (q & 3) * 64 + (q >> 2) * 32 + fl
+                                        : ch * 256 + (q >> 1) * 64 + 32 * (q & 1) + fl;
+        const u32x4 v = reinterpret_cast<const u32x4*>(X)[unit];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          x[2 * j] = __uint_as_float(v[j] << 16);
+          x[2 * j + 1] = __uint_as_float(v[j] & 0xffff0000u);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += c * (double)x[j];
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) part[fl][q * 8 + j] = acc[j];
+    __syncthreads();
+    if (threadIdx.x < 64) {
+      const int64_t r = s * 64 + threadIdx.x;
+      double p = b;
+      for (int k = 0; k < 32; ++k) p += part[k][threadIdx.x];
+      if (r < n) {
+        if (MODE == 0) {
+          out[r] = p;
+        } else if (sel == nullptr || sel[r] != 0) {
+          const double yy = ld_f64(y, ydt, r);
+          const double ys = yy - shift, ps = p - shift, res = yy - p;
+          m[0] += 1.0;
+          m[1] += ys;
+          m[2] += ys * ys;
+          m[3] += res;
+          m[4] += res * res;
+          m[5] += fabs(res);
+          m[6] += ps;
+          m[7] += ps * ps;
+        }
+      }
+    }
+    __syncthreads();
+  }
+  if (MODE == 1) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) m[k] = wave_sum_f64(m[k]);
+    if (threadIdx.x == 0) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) out[(int64_t)blockIdx.x * 8 + k] = m[k];
+    }
   }
 }
 
@@ -292,8 +383,8 @@ void pack_columns(const PackSrc* srcs_dev, int d, int64_t n, void* out, int odt,
 void pack_tiled(const PackSrc* srcs_dev, int d, int64_t n, const uint8_t* sel, void* out, hipStream_t st) {
   const int NT = (d + 31) / 32;
   const int64_t nsup = (n + 63) / 64;
-  int64_t g = (nsup * NT * 256 + 255) / 256;
-  if (g > 8192) g = 8192;
+  int64_t g = nsup * NT;
+  if (g > 16384) g = 16384;
   if (g < 1) g = 1;
   hipLaunchKernelGGL(pack_tiled_kernel, dim3(g), dim3(256), 0, st, srcs_dev, d, n, sel, NT, nsup,
                      reinterpret_cast<uint16_t*>(out));
@@ -303,6 +394,14 @@ void pack_tiled(const PackSrc* srcs_dev, int d, int64_t n, const uint8_t* sel, v
 void predict(const void* X, int xdt, int64_t ld, int d, int64_t n, const double* coef, double b, double* out,
              hipStream_t st, int tiled) {
   if (n <= 0) return;
+  if (tiled) {
+    int64_t g = (n + 63) / 64;
+    if (g > 8192) g = 8192;
+    hipLaunchKernelGGL(tiled_rows_kernel<0>, dim3(g), dim3(256), 0, st, reinterpret_cast<const unsigned char*>(X),
+                       tiled, d, n, coef, b, nullptr, 0, nullptr, 0.0, out);
+    DQ_HIP_CHECK(hipGetLastError());
+    return;
+  }
   int64_t g = (n + 255) / 256;
   if (g > 4096) g = 4096;
   hipLaunchKernelGGL(predict_kernel, dim3(g), dim3(256), 0, st, X, xdt, ld, d, n, coef, b, out, tiled);
@@ -320,8 +419,12 @@ void regression_metrics(const void* X, int xdt, int64_t ld, int d, int64_t n, co
                         const uint8_t* sel, const double* coef, double b, double shift, double* partials,
                         double* out, hipStream_t st, int tiled) {
   const int g = metrics_blocks(n);
-  hipLaunchKernelGGL(metrics_kernel, dim3(g), dim3(256), 0, st, X, xdt, ld, d, n, y, ydt, sel, coef, b, shift,
-                     partials, tiled);
+  if (tiled)
+    hipLaunchKernelGGL(tiled_rows_kernel<1>, dim3(g), dim3(256), 0, st, reinterpret_cast<const unsigned char*>(X),
+                       tiled, d, n, coef, b, y, ydt, sel, shift, partials);
+  else
+    hipLaunchKernelGGL(metrics_kernel, dim3(g), dim3(256), 0, st, X, xdt, ld, d, n, y, ydt, sel, coef, b, shift,
+                       partials, tiled);
   hipLaunchKernelGGL(sum_slabs_kernel, dim3(1), dim3(64), 0, st, partials, g, 8, out);
   DQ_HIP_CHECK(hipGetLastError());
 }

@@ -6,6 +6,7 @@
 
 #include "csv.h"
 #include "solvers.h"
+#include "wls.h"
 
 namespace py = pybind11;
 using namespace dq4ml;
@@ -24,6 +25,36 @@ PYBIND11_MODULE(_dq4ml_host, m) {
   m.doc() = "dq4ml host runtime: f64 normal-equation solvers (Breeze-compatible) and CSV scanner";
 
   py::register_exception<SingularMatrixError>(m, "SingularMatrixError");
+
+  m.def(
+      "wls_fit",
+      [](py::array_t<double, py::array::c_style | py::array::forcecast> flat, int nf, bool fit_intercept,
+         double reg_param, double elastic_net, bool standardize_features, bool standardize_label, int solver_type,
+         int max_iter, double tol, bool keep_system) {
+        const py::ssize_t need = 5 + 2 * (py::ssize_t)nf + (py::ssize_t)nf * (nf + 1) / 2;
+        if (flat.size() != need) throw std::invalid_argument("wls_fit: flat statistics have the wrong length");
+        WlsResult r;
+        {
+          py::gil_scoped_release nogil;
+          r = wls_fit(flat.data(), nf, fit_intercept, reg_param, elastic_net, standardize_features,
+                      standardize_label, solver_type, max_iter, tol, keep_system);
+        }
+        py::dict d;
+        d["status"] = r.status;
+        d["singular_fallback"] = r.singular_fallback;
+        d["solver"] = r.solver;
+        d["coefficients"] = to_np(r.coefficients);
+        d["intercept"] = r.intercept;
+        d["objective_history"] = to_np(r.objective_history);
+        d["converged_reason"] = r.converged_reason;
+        d["ata"] = to_np(r.ata);
+        d["a_std"] = to_np(r.a_std);
+        d["w_sum"] = r.w_sum;
+        return d;
+      },
+      py::arg("flat"), py::arg("nf"), py::arg("fit_intercept"), py::arg("reg_param"), py::arg("elastic_net"),
+      py::arg("standardize_features"), py::arg("standardize_label"), py::arg("solver_type"), py::arg("max_iter"),
+      py::arg("tol"), py::arg("keep_system") = true);
 
   m.def("dspmv", [](int k, py::array_t<double, py::array::c_style | py::array::forcecast> ap,
                     py::array_t<double, py::array::c_style | py::array::forcecast> x) {

@@ -30,6 +30,10 @@ for s in $STEPS; do
     cfg4) step cfg4 900 python benchmarks/bench_dq_pipeline.py --steps 5 --warmup 2 --json-out gpurun_out/cfg4.json ;;
     cfg5) step cfg5 900 python benchmarks/bench_wide.py --steps 3 --warmup 1 --json-out gpurun_out/cfg5.json ;;
     cfg1) step cfg1 300 python benchmarks/bench_cpu_small.py --json-out gpurun_out/cfg1.json ;;
+    prof4) step prof4 600 env WHICH=cfg4 python scripts/step_profile.py ;;
+    prof5) step prof5 600 env WHICH=cfg5 python scripts/step_profile.py ;;
+    kprof4) (export TMPDIR=/tmp; step kprof4 600 rocprofv3 --kernel-trace --stats -d gpurun_out/kprof4 -o run --output-format csv -- python benchmarks/bench_dq_pipeline.py --steps 2 --warmup 1) || exit $? ;;
+    kprof5) (export TMPDIR=/tmp; step kprof5 600 rocprofv3 --kernel-trace --stats -d gpurun_out/kprof5 -o run --output-format csv -- python benchmarks/bench_wide.py --steps 1 --warmup 1) || exit $? ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" ;;
     bench) step bench 600 python bench.py --steps 20 --warmup 3 ;;
     fitprof) step fitprof 300 env N=1.25e7 python scripts/fit_profile.py ;;

@@ -160,3 +160,22 @@ def test_assembler_fp8_wide_fit(gpu_session):
     # fp8 features: coefficients within a few % (quantization noise acts like errors-in-variables)
     assert np.abs(np.asarray(m.coefficients.toArray()) - beta).max() < 0.15
     assert m.summary.r2 > 0.95
+
+
+@gpu
+@pytest.mark.parametrize("wide", [False, True])
+def test_pack_mixed_dtypes_and_misaligned_columns(wide):
+    # f64 / f32 / bf16 / int32 columns, some starting at a non-16-byte-aligned offset (scalar path)
+    _hip()
+    from net.jgp.labs.sparkdq4ml_amd.ops import device
+
+    n = 10_007
+    g = torch.Generator(device="cuda").manual_seed(9)
+    base = torch.randn(4, n + 3, generator=g, device="cuda", dtype=torch.float64)
+    cols = [base[0, :n], base[1, 3:].float(), base[2, 1:n + 1].to(torch.bfloat16)[0:],
+            (base[3, :n] * 10).to(torch.int32), base[1, 1:n + 1]]  # last: f64 view at +8 bytes
+    cols = cols * (20 if wide else 4)  # d = 100 (wide) / 20 (tall)
+    sel = torch.rand(n, generator=g, device="cuda") > 0.3
+    dense = torch.stack([c.float() for c in cols]) * sel
+    T = device.pack_wide(cols, 16, sel) if wide else device.pack_tiled(cols, sel)
+    assert torch.equal(T.to_dense().float(), dense.to(torch.bfloat16).float())
