@@ -13,6 +13,7 @@ from typing import List
 
 import torch
 
+from ..utils import tracing
 from ..sql.dataframe import DataFrame
 from ..sql.expressions import (AnalysisException, ColRef, EvalContext, Expr, IsNotNull, BinOp,
                                SparkException)
@@ -97,17 +98,20 @@ class VectorAssembleExpr(Expr):
         on_dev = bool(parts) and parts[0].is_cuda
         if dt == torch.bfloat16 and on_dev and d <= 64:
             # MI355X-native storage: MFMA-fragment-ordered tiles, dead rows zeroed (no Gram mask)
-            mat = kernels.pack_tiled(parts, ctx.table.sel)
+            with tracing.span("pack"):
+                mat = kernels.pack_tiled(parts, ctx.table.sel)
             meta = {"ml_attr": {"num_attrs": d}, "zero_dead": ctx.table.sel}
         elif on_dev and (dt == torch.float8_e4m3fn or (dt == torch.bfloat16 and d > 64)):
             # wide fragment layout for the LDS-tiled MFMA SYRK (fp8: per-feature scales)
-            mat = kernels.pack_wide(parts, 8 if dt == torch.float8_e4m3fn else 16, ctx.table.sel)
+            with tracing.span("pack"):
+                mat = kernels.pack_wide(parts, 8 if dt == torch.float8_e4m3fn else 16, ctx.table.sel)
             meta = {"ml_attr": {"num_attrs": d}, "zero_dead": ctx.table.sel}
         elif dt == torch.float8_e4m3fn:  # host engine: fp8 storage is a device layout; keep fp32
             mat = kernels.pack_columns(parts, torch.float32)
             meta = {"ml_attr": {"num_attrs": int(mat.shape[0])}}
         else:
-            mat = kernels.pack_columns(parts, dt)
+            with tracing.span("pack"):
+                mat = kernels.pack_columns(parts, dt)
             meta = {"ml_attr": {"num_attrs": int(mat.shape[0])}}
         return ColumnData(VectorUDT(), mat, None, meta)
 

@@ -31,6 +31,7 @@ from ..sql.table import ColumnData
 from ..sql.types import DoubleType, VectorUDT, is_numeric
 from ..utils.logging import get_logger
 from .linalg import DenseVector, Vector, Vectors
+from ..utils import tracing
 from .optim import MAX_NUM_FEATURES, GramStats, fit_wls_flat
 from .param import Param, Params, param_accessors
 
@@ -119,6 +120,15 @@ def _features_label(params, df: DataFrame):
     return tbl, X, y
 
 
+
+def _gram_dtype(est, df) -> str:
+    """Explicit ``gramDtype`` param, else the session's ``dq4ml.gramDtype``, else fp64."""
+    if est.isSet("gramDtype"):
+        return est.getOrDefault("gramDtype")
+    sess = getattr(df, "sparkSession", None)
+    v = sess.conf.get("dq4ml.gramDtype", None) if sess is not None else None
+    return v if v in _GRAM_DTYPES else est.getOrDefault("gramDtype")
+
 @param_accessors
 class LinearRegression(_LRParams):
     uid_prefix = "linReg"
@@ -171,12 +181,16 @@ class LinearRegression(_LRParams):
             sel = yvalid if sel is None else (sel & yvalid)
         zd = X.meta.get("zero_dead", False)
         x_zero_dead = yvalid is None and (tbl.sel is None or (zd is not False and zd is tbl.sel))
-        flat = kernels.gram_stats(X.values, yv, w, sel, self.getOrDefault("gramDtype"), x_zero_dead=x_zero_dead)
-        flat = comm.all_reduce_sum(flat)  # X1: data-parallel Gram all-reduce (RCCL over xGMI)
-        wls, stats = fit_wls_flat(
-            flat, d, self.getOrDefault("fitIntercept"), float(self.getOrDefault("regParam")),
-            float(self.getOrDefault("elasticNetParam")), bool(self.getOrDefault("standardization")), True,
-            "auto", int(self.getOrDefault("maxIter")), float(self.getOrDefault("tol")))
+        with tracing.span("gram"):
+            flat = kernels.gram_stats(X.values, yv, w, sel, _gram_dtype(self, df), x_zero_dead=x_zero_dead)
+        tracing.add_rows("gram", tbl.nrows)
+        with tracing.span("allreduce"):
+            flat = comm.all_reduce_sum(flat)  # X1: data-parallel Gram all-reduce (RCCL over xGMI)
+        with tracing.span("solve"):
+            wls, stats = fit_wls_flat(
+                flat, d, self.getOrDefault("fitIntercept"), float(self.getOrDefault("regParam")),
+                float(self.getOrDefault("elasticNetParam")), bool(self.getOrDefault("standardization")), True,
+                "auto", int(self.getOrDefault("maxIter")), float(self.getOrDefault("tol")))
         model = LinearRegressionModel(self.uid, DenseVector(wls.coefficients), float(wls.intercept))
         self.copyValues(model)
         model._set_summary(LinearRegressionTrainingSummary(model, df, wls, wls.objectiveHistory,
@@ -204,7 +218,8 @@ class PredictExpr(Expr):
 
     def eval(self, ctx: EvalContext) -> ColumnData:
         X = ctx.table.column(self.features)
-        return ColumnData(DoubleType(), kernels.predict(X.values, self.coef, self.intercept), X.valid)
+        with tracing.span("predict"):
+            return ColumnData(DoubleType(), kernels.predict(X.values, self.coef, self.intercept), X.valid)
 
 
 @param_accessors
@@ -333,9 +348,10 @@ class LinearRegressionSummary:
             if y.valid is not None:
                 sel = y.valid if sel is None else (sel & y.valid)
             shift = float(self._stats.bBar) if self._stats is not None else 0.0
-            sums = kernels.regression_metrics(X.values, y.values, self._model._coefficients.toArray(),
-                                              float(self._model._intercept), sel, shift)
-            sums = comm.all_reduce_sum(sums)
+            with tracing.span("metrics"):
+                sums = kernels.regression_metrics(X.values, y.values, self._model._coefficients.toArray(),
+                                                  float(self._model._intercept), sel, shift)
+                sums = comm.all_reduce_sum(sums)
             self._m = _Metrics(sums.cpu().numpy(), shift, not self._model.getOrDefault("fitIntercept"))
         return self._m
 

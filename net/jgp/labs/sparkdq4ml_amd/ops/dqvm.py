@@ -425,7 +425,11 @@ def try_execute_fused(plan, session) -> Optional[Table]:
     ptrs = torch.from_numpy(np.asarray(g.ptrs, dtype=np.int64)).to(base.device)
     n = base.nrows
     grid = int(max(1, min((n + 255) // 256, 8192)))
-    h.rtc_launch(int(handle), grid, 256, ptrs.data_ptr(), int(n), torch.cuda.current_stream().cuda_stream)
+    from ..utils import tracing
+
+    with tracing.span("dq_fused"):
+        h.rtc_launch(int(handle), grid, 256, ptrs.data_ptr(), int(n), torch.cuda.current_stream().cuda_stream)
+    tracing.add_rows("dq_fused", n)
     STATS["fused_launches"] += 1
     if g.has_raise and int(err.item()) != 0:
         msg = "Failed to execute user defined function"

@@ -86,11 +86,21 @@ def _comm_tensor(t: torch.Tensor) -> torch.Tensor:
     return t
 
 
-def all_reduce_sum(t: torch.Tensor, bucket_bytes: int = DEFAULT_BUCKET_BYTES) -> torch.Tensor:
+_bucket_bytes = DEFAULT_BUCKET_BYTES
+
+
+def set_bucket_bytes(n: int):
+    """Bucket size of ``all_reduce_sum`` (session config ``dq4ml.bucketBytes``)."""
+    global _bucket_bytes
+    _bucket_bytes = max(1 << 16, int(n))
+
+
+def all_reduce_sum(t: torch.Tensor, bucket_bytes: Optional[int] = None) -> torch.Tensor:
     """Sum ``t`` over all ranks (returns a tensor on ``t``'s device).  Order of summation is fixed
     for a fixed world size, so repeated runs are bit-reproducible."""
     if world_size() == 1:
         return t
+    bucket_bytes = bucket_bytes or _bucket_bytes
     src_dev = t.device
     x = _comm_tensor(t.contiguous())
     nbytes = x.numel() * x.element_size()

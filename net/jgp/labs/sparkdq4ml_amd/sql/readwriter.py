@@ -21,6 +21,7 @@ from typing import Dict, List, Optional
 import numpy as np
 import torch
 
+from ..utils import tracing
 from ..utils.logging import get_logger
 from .localdata import column_from_numpy, column_from_pylist, table_from_data
 from .plan import LocalRelation
@@ -156,7 +157,8 @@ class DataFrameReader:
         if dev.type == "cuda" and len(data) >= thresh and not user_types and header is False:
             from ..ops import csvscan
 
-            t = csvscan.scan_device(data, sep=sep, infer=infer, device=dev)
+            with tracing.span("csv_scan"):
+                t = csvscan.scan_device(data, sep=sep, infer=infer, device=dev)
             if t is not None:
                 return t
         from ..ops import native

@@ -8,8 +8,10 @@
 * ``mi355x`` / ``mi355x[*]`` / ``gpu`` — require the GPU;
 * ``cpu`` / ``local-cpu[*]`` — force host execution (the unit-test configuration).
 
-Config keys (``.config(k, v)``): ``dq4ml.device``, ``dq4ml.gramDtype`` (fp64|fp32|bf16|fp8),
-``dq4ml.bucketBytes``, ``dq4ml.csv.deviceThresholdBytes``.
+Config keys (``.config(k, v)``): ``dq4ml.device``, ``dq4ml.gramDtype`` (fp64|fp32|bf16|fp8: the
+default Gram precision of estimators that do not set ``gramDtype``), ``dq4ml.bucketBytes`` (RCCL
+all-reduce bucket size), ``dq4ml.trace`` (per-stage tracing, ``utils.tracing``),
+``dq4ml.csv.deviceThresholdBytes`` (smallest file the device CSV scanner takes).
 """
 from __future__ import annotations
 
@@ -140,6 +142,14 @@ class SparkSession:
         self.master = conf.get("spark.master", "local[*]")
         self.appName = conf.get("spark.app.name", "dq4ml")
         self.device = _resolve_device(self.master, conf)
+        if str(conf.get("dq4ml.trace", "")).lower() in ("1", "true", "yes"):
+            from ..utils import tracing
+
+            tracing.enable(True)
+        if conf.get("dq4ml.bucketBytes"):
+            from ..parallel import comm
+
+            comm.set_bucket_bytes(int(conf["dq4ml.bucketBytes"]))
         self.udf = UDFRegistration(self)
         self.catalog = Catalog()
         self._stopped = False
