@@ -35,6 +35,7 @@ def _args(argv=None):
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32", "fp64"])
     ap.add_argument("--scaling", default="strong", choices=["strong", "weak"])
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--sync", action="store_true", help="synchronous fits (host waits for every solve)")
     return ap.parse_args(argv)
 
 
@@ -49,7 +50,10 @@ def main(argv=None):
     rank, world = comm.rank(), comm.world_size()
     if world != a.gpus and rank == 0:
         print(f"[bench] warning: --gpus {a.gpus} but WORLD_SIZE={world}", file=sys.stderr)
-    spark = SparkSession.builder().appName("bench").master("local[*]").getOrCreate()
+    # asynchronous fits: gram -> RCCL all-reduce -> device Cholesky enqueued back to back, the host
+    # never waits inside a step (the timed region still ends with barrier + synchronize)
+    spark = SparkSession.builder().appName("bench").master("local[*]") \
+        .config("dq4ml.fit.async", "false" if a.sync else "true").getOrCreate()
     dev = spark.device
     on_gpu = dev.type == "cuda"
 
@@ -111,7 +115,8 @@ def main(argv=None):
             "dtype": a.dtype, "data": "synthetic (random-init coefficients, N(0,1) features)",
             "config": {"model": f"LinearRegression(normal equations) d={d}", "global_batch": global_rows,
                        "seq_len": d, "parallelism": f"dp{world}", "rows_per_gpu": n,
-                       "device": str(dev), "coef_max_abs_err": err},
+                       "device": str(dev), "coef_max_abs_err": err,
+                       "fit_mode": "sync" if a.sync else "async"},
         }
         s = json.dumps(line)
         print(s, flush=True)

@@ -186,16 +186,68 @@ class LinearRegression(_LRParams):
         tracing.add_rows("gram", tbl.nrows)
         with tracing.span("allreduce"):
             flat = comm.all_reduce_sum(flat)  # X1: data-parallel Gram all-reduce (RCCL over xGMI)
-        with tracing.span("solve"):
-            wls, stats = fit_wls_flat(
-                flat, d, self.getOrDefault("fitIntercept"), float(self.getOrDefault("regParam")),
+        args = (flat, d, self.getOrDefault("fitIntercept"), float(self.getOrDefault("regParam")),
                 float(self.getOrDefault("elasticNetParam")), bool(self.getOrDefault("standardization")), True,
                 "auto", int(self.getOrDefault("maxIter")), float(self.getOrDefault("tol")))
+        if _async_fit(df, flat, d, args):
+            with tracing.span("solve"):
+                pending = _PendingWLS(args)  # device Cholesky enqueued; resolved on first read
+            model = LinearRegressionModel(self.uid, None, 0.0)
+            model._pending = pending
+            self.copyValues(model)
+            model._set_summary(LinearRegressionTrainingSummary(model, df, pending, None, stats=pending,
+                                                               solver=pending))
+            return model
+        with tracing.span("solve"):
+            wls, stats = fit_wls_flat(*args)
         model = LinearRegressionModel(self.uid, DenseVector(wls.coefficients), float(wls.intercept))
         self.copyValues(model)
         model._set_summary(LinearRegressionTrainingSummary(model, df, wls, wls.objectiveHistory,
                                                            stats=stats, solver=wls.solver))
         return model
+
+
+def _async_fit(df, flat, d, args) -> bool:
+    """Asynchronous normal-equation fit (session config ``dq4ml.fit.async``): device statistics,
+    <= 64 features, Cholesky branch (no L1) -> the solve is enqueued on the device and the host
+    does not wait for the fit; coefficients, summary and any Spark warning/exception materialize
+    on first read (edge cases re-solve on the host with identical semantics)."""
+    sess = getattr(df, "sparkSession", None)
+    if sess is None or str(sess.conf.get("dq4ml.fit.async", "false")).lower() not in ("1", "true", "yes"):
+        return False
+    if not (getattr(flat, "is_cuda", False) and 1 <= d <= 64):
+        return False
+    _, _, _, reg, enet = args[:5]
+    return not (enet != 0.0 and reg != 0.0)
+
+
+class _PendingWLS:
+    """A WLS solve enqueued on the device (``ops.device.wls_small``); ``resolve()`` syncs once."""
+
+    def __init__(self, args):
+        from ..ops import device
+
+        self.args = args
+        flat, d, fit_icpt, reg, enet, std_f, std_l = args[:7]
+        self.out = device.wls_small(flat, d, fit_icpt, reg, enet, std_f, std_l)
+        self._res = None
+
+    def resolve(self):
+        if self._res is None:
+            flat, d = self.args[0], self.args[1]
+            host = self.out.cpu().numpy()
+            if int(host[d + 1]) != 0:  # edge case: the host driver owns warnings/errors/fallbacks
+                self._res = fit_wls_flat(*self.args)
+            else:
+                from .optim import WLSModel
+
+                args = self.args
+
+                def diag_inv():
+                    return fit_wls_flat(*args)[0].diagInvAtWA
+                wls = WLSModel(host[:d].copy(), float(host[d]), diag_inv, np.zeros(1), "cholesky")
+                self._res = (wls, GramStats.scalars_only(host[d + 2:d + 7], d))
+        return self._res
 
 
 class PredictExpr(Expr):
@@ -228,10 +280,38 @@ class LinearRegressionModel(_LRParams):
 
     def __init__(self, uid: Optional[str], coefficients: Vector, intercept: float, scale: float = 1.0):
         super().__init__(uid)
-        self._coefficients = coefficients if isinstance(coefficients, Vector) else DenseVector(coefficients)
-        self._intercept = _JavaFloat(intercept)
+        self._pending = None  # _PendingWLS of an asynchronous fit
+        self._coef_v = None if coefficients is None else (
+            coefficients if isinstance(coefficients, Vector) else DenseVector(coefficients))
+        self._icpt_v = _JavaFloat(intercept)
         self.scale = scale
         self._summary = None
+
+    def _materialize(self):
+        if self._pending is not None:
+            wls, _ = self._pending.resolve()
+            self._coef_v = DenseVector(np.asarray(wls.coefficients, dtype=np.float64))
+            self._icpt_v = _JavaFloat(float(wls.intercept))
+            self._pending = None
+
+    @property
+    def _coefficients(self) -> Vector:
+        self._materialize()
+        return self._coef_v
+
+    @_coefficients.setter
+    def _coefficients(self, v):
+        self._pending, self._coef_v = None, v if isinstance(v, Vector) else DenseVector(v)
+
+    @property
+    def _intercept(self):
+        self._materialize()
+        return self._icpt_v
+
+    @_intercept.setter
+    def _intercept(self, v):
+        self._materialize()
+        self._icpt_v = _JavaFloat(v)
 
     # pyspark-style properties that are also callable (Java spelling) -----------------------------
     @property
@@ -339,8 +419,12 @@ class LinearRegressionSummary:
     def featuresCol(self):
         return self._model.getOrDefault("featuresCol")
 
+    def _resolve_fit(self):
+        pass
+
     def _metrics(self):
         if self._m is None:
+            self._resolve_fit()
             tbl = self._df._table()
             X = tbl.column(self.featuresCol)
             y = tbl.column(self.labelCol)
@@ -412,6 +496,7 @@ class LinearRegressionSummary:
 
     @property
     def _diag_inv(self):
+        self._resolve_fit()
         src = self._diag_src
         if src is None:
             return np.zeros(1)
@@ -450,9 +535,32 @@ class _CallableDF(DataFrame):
 
 class LinearRegressionTrainingSummary(LinearRegressionSummary):
     def __init__(self, model, df, diag_inv, objective_history, stats=None, solver="auto"):
+        if isinstance(diag_inv, _PendingWLS):  # asynchronous fit: everything resolves on first read
+            self._pending_fit = diag_inv
+            super().__init__(model, df, None, None)
+            self._hist_v, self._solver_v = None, None
+            return
+        self._pending_fit = None
         super().__init__(model, df, diag_inv, stats)
-        self._history = np.asarray(objective_history, dtype=np.float64)
-        self.solver = solver
+        self._hist_v = np.asarray(objective_history, dtype=np.float64)
+        self._solver_v = solver
+
+    def _resolve_fit(self):
+        if self._pending_fit is not None:
+            wls, stats = self._pending_fit.resolve()
+            self._diag_src, self._stats = wls, stats
+            self._hist_v, self._solver_v = np.asarray(wls.objectiveHistory, dtype=np.float64), wls.solver
+            self._pending_fit = None
+
+    @property
+    def _history(self):
+        self._resolve_fit()
+        return self._hist_v
+
+    @property
+    def solver(self):
+        self._resolve_fit()
+        return self._solver_v
 
     @property
     def objectiveHistory(self):

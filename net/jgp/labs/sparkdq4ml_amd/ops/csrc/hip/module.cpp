@@ -10,6 +10,7 @@
 #include "dqvm.h"
 #include "gram.h"
 #include "gram_wide.h"
+#include "wls_small.h"
 #include "rowops.h"
 
 namespace py = pybind11;
@@ -63,6 +64,11 @@ PYBIND11_MODULE(_dq4ml_hip, m) {
   m.def("tile_bf16", [](uintptr_t X, int xdt, int64_t ld, int d, int64_t n, uintptr_t out, uintptr_t stream) {
     tile_bf16(P<const void>(X), xdt, ld, d, n, P<void>(out), as_stream(stream));
   });
+  m.def("wls_small", [](uintptr_t flat, int nf, bool fit_intercept, double reg, double enet, bool std_f, bool std_l,
+                        uintptr_t out, uintptr_t stream) {
+    wls_small(P<const double>(flat), nf, fit_intercept, reg, enet, std_f, std_l, P<double>(out), as_stream(stream));
+  });
+  m.attr("WLS_SMALL_MAX_FEATURES") = kWlsSmallMaxFeatures;
   m.def("wide_tiled_bytes", &wide_tiled_bytes);
   m.attr("WIDE_ZERO_BYTES") = kWideZeroBytes;
   m.def("gram_wide_partials", &gram_wide_partials);

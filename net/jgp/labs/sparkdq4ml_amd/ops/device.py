@@ -379,6 +379,21 @@ def huber_pass(X, y, w, sel, ceff, icpt, sigma, eps):
 
 
 # ------------------------------------------------------------------------------------------
+def wls_small(flat: torch.Tensor, nf: int, fit_intercept: bool, reg: float, enet: float, std_f: bool,
+              std_l: bool) -> torch.Tensor:
+    """Device WLS Cholesky (k <= 65) from the flat statistics, enqueued on the current stream:
+    returns ``[coef(nf), intercept, status, count, wSum, wwSum, bSum, bbSum]`` (no host sync)."""
+    h = native.hip()
+    _check_dev(flat)
+    if flat.dtype != torch.float64 or flat.numel() != 5 + 2 * nf + nf * (nf + 1) // 2:
+        raise ValueError("wls_small: flat statistics have the wrong dtype/length")
+    out = torch.empty(nf + 7, dtype=torch.float64, device=flat.device)
+    h.wls_small(flat.data_ptr(), int(nf), bool(fit_intercept), float(reg), float(enet), bool(std_f), bool(std_l),
+                out.data_ptr(), _stream())
+    return out
+
+
+# ------------------------------------------------------------------------------------------
 # wide (d > 64) fragment layouts + LDS-tiled MFMA SYRK
 # ------------------------------------------------------------------------------------------
 def _srcw_desc(h, rows, dev):
