@@ -36,9 +36,9 @@ for s in $STEPS; do
     kprof5) (export TMPDIR=/tmp; step kprof5 600 rocprofv3 --kernel-trace --stats -d gpurun_out/kprof5 -o run --output-format csv -- python benchmarks/bench_wide.py --steps 1 --warmup 1) || exit $? ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" ;;
     bench) step bench 600 python bench.py --steps 20 --warmup 3 ;;
-    benchsync) step benchsync 600 python bench.py --steps 20 --warmup 3 --sync ;;
+    benchasync) step benchasync 600 python bench.py --steps 20 --warmup 3 --async ;;
     bench8th) step bench8th 600 python bench.py --steps 50 --warmup 5 --rows 1.25e7 ;;
-    bench8thsync) step bench8thsync 600 python bench.py --steps 50 --warmup 5 --rows 1.25e7 --sync ;;
+    bench8thasync) step bench8thasync 600 python bench.py --steps 50 --warmup 5 --rows 1.25e7 --async ;;
     asynctests) step asynctests 600 python -m pytest tests/test_gpu_async_fit.py -q -m gpu ;;
     fitprof) step fitprof 300 env N=1.25e7 python scripts/fit_profile.py ;;
     dist2) step dist2 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 scripts/dist_rehearsal.py ;;

@@ -47,7 +47,7 @@ def test_async_matches_sync(async_session, fit_intercept, std, reg):
                      fitIntercept=fit_intercept, standardization=std)
     np.testing.assert_allclose(a.coefficients.toArray(), s.coefficients.toArray(), rtol=1e-10, atol=1e-12)
     assert float(a.intercept) == pytest.approx(float(s.intercept), rel=1e-10, abs=1e-12)
-    assert list(a.summary.objectiveHistory.toArray()) == list(s.summary.objectiveHistory.toArray())
+    assert list(np.asarray(a.summary.objectiveHistory)) == list(np.asarray(s.summary.objectiveHistory))
     assert float(a.summary.r2) == pytest.approx(float(s.summary.r2), rel=1e-12)
     np.testing.assert_allclose(a.summary.coefficientStandardErrors, s.summary.coefficientStandardErrors, rtol=1e-8)
 
