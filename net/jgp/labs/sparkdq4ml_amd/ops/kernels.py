@@ -80,11 +80,21 @@ def gram_layout_size(d: int) -> int:
     return 5 + 2 * d + d * (d + 1) // 2
 
 
+_upper_idx = {}
+
+
 def packed_upper(aa: torch.Tensor) -> torch.Tensor:
+    """Packed upper (column-major) entries of a square matrix; index vectors cached per (d, device)."""
     d = aa.shape[0]
-    J = torch.repeat_interleave(torch.arange(d, device=aa.device), torch.arange(1, d + 1, device=aa.device))
-    I = torch.cat([torch.arange(j + 1, device=aa.device) for j in range(d)]) if d else J
-    return aa[I, J]
+    key = (d, aa.device)
+    idx = _upper_idx.get(key)
+    if idx is None:
+        J = torch.repeat_interleave(torch.arange(d, device=aa.device), torch.arange(1, d + 1, device=aa.device))
+        I = torch.cat([torch.arange(j + 1, device=aa.device) for j in range(d)]) if d else J
+        if len(_upper_idx) > 32:
+            _upper_idx.clear()
+        idx = _upper_idx[key] = (I, J)
+    return aa[idx[0], idx[1]]
 
 
 def gram_stats(X: torch.Tensor, y: torch.Tensor, w: Optional[torch.Tensor], sel: Optional[torch.Tensor],
