@@ -4,6 +4,8 @@ SQL clean-up -> label -> VectorAssembler -> LinearRegression(maxIter 40, regPara
 elasticNetParam 1) -> transform/show -> training summary -> predict(40 guests).
 
     python -m net.jgp.labs.sparkdq4ml_amd.apps.dq4ml_app [--data data/dataset-abstract.csv] [--master local[*]]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 \
+        -m net.jgp.labs.sparkdq4ml_amd.apps.dq4ml_app        (data-parallel: one rank per GPU)
 """
 from __future__ import annotations
 
@@ -13,6 +15,7 @@ import os
 from .. import (LinearRegression, SparkSession, VectorAssembler, Vectors, callUDF)
 from ..dq.rules import MinimumPriceDataQualityUdf, PriceCorrelationDataQualityUdf
 from ..sql.types import DataTypes
+from ..parallel import comm
 from ..utils.javafmt import java_str
 
 DEFAULT_DATA = "data/dataset-abstract.csv"
@@ -23,6 +26,9 @@ class DataQuality4MachineLearningApp:
         self.data, self.master, self.gram_dtype = data, master, gram_dtype
 
     def start(self):
+        # SPMD under torchrun: every rank runs the pipeline on its byte-range shard of the CSV,
+        # actions combine the shards, and only rank 0 writes the transcript
+        out = print if comm.rank() == 0 else (lambda *a, **k: None)
         spark = SparkSession.builder().appName("DQ4ML").master(self.master).getOrCreate()
 
         # DQ Section
@@ -33,33 +39,33 @@ class DataQuality4MachineLearningApp:
         df = df.withColumnRenamed("_c0", "guest")
         df = df.withColumnRenamed("_c1", "price")
 
-        print("----")
-        print("Load & Format")
+        out("----")
+        out("Load & Format")
         df.show()
-        print("----")
+        out("----")
 
         df = df.withColumn("price_no_min", callUDF("minimumPriceRule", df.col("price")))
-        print("----")
-        print("1st DQ rule")
+        out("----")
+        out("1st DQ rule")
         df.printSchema()
         df.show(50)
-        print("----")
+        out("----")
 
         df.createOrReplaceTempView("price")
         df = spark.sql("SELECT cast(guest as int) guest, price_no_min AS price FROM price WHERE price_no_min > 0")
-        print("----")
-        print("1st DQ rule - clean-up")
+        out("----")
+        out("1st DQ rule - clean-up")
         df.printSchema()
         df.show(50)
-        print("----")
+        out("----")
 
         df = df.withColumn("price_correct_correl", callUDF("priceCorrelationRule", df.col("price"), df.col("guest")))
         df.createOrReplaceTempView("price")
         df = spark.sql("SELECT guest, price_correct_correl AS price FROM price WHERE price_correct_correl > 0")
-        print("----")
-        print("2nd DQ rule")
+        out("----")
+        out("2nd DQ rule")
         df.show(50)
-        print("----")
+        out("----")
 
         # ML Section
         df = df.withColumn("label", df.col("price"))
@@ -73,20 +79,20 @@ class DataQuality4MachineLearningApp:
         model.transform(df).show()
 
         training_summary = model.summary()
-        print("numIterations: " + java_str(training_summary.totalIterations()))
-        print("objectiveHistory: " + str(Vectors.dense(training_summary.objectiveHistory())))
+        out("numIterations: " + java_str(training_summary.totalIterations()))
+        out("objectiveHistory: " + str(Vectors.dense(training_summary.objectiveHistory())))
         training_summary.residuals().show()
-        print("RMSE: " + java_str(training_summary.rootMeanSquaredError()))
-        print("r2: " + java_str(training_summary.r2()))
+        out("RMSE: " + java_str(training_summary.rootMeanSquaredError()))
+        out("r2: " + java_str(training_summary.r2()))
 
-        print("Intersection: " + java_str(model.intercept()))
-        print("Regression parameter: " + java_str(model.getRegParam()))
-        print("Tol: " + java_str(model.getTol()))
+        out("Intersection: " + java_str(model.intercept()))
+        out("Regression parameter: " + java_str(model.getRegParam()))
+        out("Tol: " + java_str(model.getTol()))
 
         feature = 40.0
         features = Vectors.dense(40.0)
         p = model.predict(features)
-        print("Prediction for " + java_str(feature) + " guests is " + java_str(p))
+        out("Prediction for " + java_str(feature) + " guests is " + java_str(p))
         return model
 
 
@@ -100,7 +106,11 @@ def main(argv=None):
     if not os.path.exists(data):
         here = os.path.join(os.path.dirname(__file__), "..", "..", "..", "..", "..", data)
         data = here if os.path.exists(here) else data
-    DataQuality4MachineLearningApp(data, a.master, a.gram_dtype).start()
+    comm.init()
+    try:
+        DataQuality4MachineLearningApp(data, a.master, a.gram_dtype).start()
+    finally:
+        comm.shutdown()
 
 
 if __name__ == "__main__":

@@ -14,11 +14,17 @@ import torch
 from ..utils.javafmt import java_str
 from .column import Column
 from .expressions import (Alias, AnalysisException, ColRef, Expr, to_expr)
-from .plan import Filter, Limit, LocalRelation, LogicalPlan, Project, Union, execute, output_name
+from .plan import Filter, Limit, LocalRelation, LogicalPlan, Project, Union, execute, is_sharded, output_name
 from .table import Table
 from .types import StructType, VectorUDT
 
 __all__ = ["DataFrame", "Row"]
+
+
+def _rank0() -> bool:
+    from ..parallel import comm
+
+    return comm.rank() == 0
 
 
 class Row(tuple):
@@ -182,7 +188,8 @@ class DataFrame:
         return [(f.name, f.dataType.simpleString()) for f in self.schema.fields]
 
     def printSchema(self):
-        print(self.schema.treeString())
+        if _rank0():
+            print(self.schema.treeString())
 
     def explain(self, extended=False):
         print("== Physical Plan ==\n" + self._plan.describe())
@@ -325,11 +332,29 @@ class DataFrame:
         return execute(self._plan, self.sparkSession)
 
     def count(self) -> int:
-        return self._table().count()
+        n = self._table().count()
+        if is_sharded(self._plan):  # X2-style: sum of the shards' counts
+            from ..parallel import comm
+
+            return int(sum(comm.all_gather_object(int(n))))
+        return n
 
     def _rows(self, t: Table) -> List[Row]:
         names = t.schema.names
-        return [Row._make(names, r) for r in t.to_rows()]
+        return [Row._make(names, r) for r in self._gather(t.to_rows())]
+
+    def _gather(self, local_rows, limit: Optional[int] = None):
+        """X5: rows of every shard in rank order (= global row order) on every rank."""
+        if not is_sharded(self._plan):
+            return local_rows
+        from ..parallel import comm
+
+        out = []
+        for part in comm.all_gather_object([tuple(r) for r in local_rows]):
+            out.extend(part)
+            if limit is not None and len(out) >= limit:
+                return out[:limit]
+        return out
 
     def collect(self) -> List[Row]:
         return self._rows(self._table())
@@ -337,7 +362,9 @@ class DataFrame:
     collectAsList = collect
 
     def take(self, n: int) -> List[Row]:
-        return self._rows(self._table().head_rows(n))
+        t = self._table().head_rows(n)
+        names = t.schema.names
+        return [Row._make(names, r) for r in self._gather(t.to_rows(), n)]
 
     def head(self, n: Optional[int] = None):
         if n is None:
@@ -354,18 +381,23 @@ class DataFrame:
     def showString(self, n: int = 20, truncate=True, vertical=False) -> str:
         tr = 20 if truncate is True else (0 if truncate is False else int(truncate))
         t = self._table().head_rows(n + 1)
-        rows = t.to_rows()
+        rows = self._gather(t.to_rows(), n + 1)
         has_more = len(rows) > n
         return show_string(t.schema.names, rows[:n], n, tr, vertical, has_more)
 
     def show(self, n: int = 20, truncate=True, vertical=False):
         if isinstance(n, bool):
             n, truncate = 20, n
-        print(self.showString(n, truncate, vertical))
+        s = self.showString(n, truncate, vertical)  # collective on sharded data: every rank joins
+        if _rank0():
+            print(s)
 
     def toPandas(self):
         import pandas as pd
 
+        if is_sharded(self._plan):
+            rows = self.collect()
+            return pd.DataFrame([tuple(r) for r in rows], columns=self.columns)
         t = self._table().compact()
         data = {}
         for f, c in zip(t.schema.fields, t.columns):

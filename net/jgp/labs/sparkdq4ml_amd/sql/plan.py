@@ -43,10 +43,18 @@ class LogicalPlan:
 
 
 class LocalRelation(LogicalPlan):
-    def __init__(self, table: Table, label: str = "LocalRelation"):
+    """A materialized relation.  ``sharded``: this process holds one data-parallel shard of it
+    (rank order = global row order); defaults to True whenever a multi-process group is up, which
+    is the SPMD contract of the engine: every source (reader byte range, ``createDataFrame``,
+    ``range``) contributes this rank's rows."""
+
+    def __init__(self, table: Table, label: str = "LocalRelation", sharded: Optional[bool] = None):
+        from ..parallel import comm
+
         self.table = table
         self._memo = table
         self.label = label
+        self.sharded = comm.world_size() > 1 if sharded is None else bool(sharded)
 
     def schema(self):
         return self.table.schema
@@ -56,6 +64,14 @@ class LocalRelation(LogicalPlan):
 
     def _label(self):
         return f"{self.label} [{', '.join(self.table.schema.names)}]"
+
+
+def is_sharded(plan) -> bool:
+    """True when any leaf relation of ``plan`` is a data-parallel shard (actions then combine
+    ranks: counts all-reduce, rows gather in rank order)."""
+    if isinstance(plan, LocalRelation):
+        return plan.sharded
+    return any(is_sharded(c) for c in plan.children())
 
 
 def output_name(e: Expr) -> str:
@@ -159,7 +175,15 @@ class Limit(LogicalPlan):
         return self.child.schema()
 
     def _compute(self, session):
-        return execute(self.child, session).head_rows(self.n)
+        t = execute(self.child, session)
+        if not is_sharded(self.child):
+            return t.head_rows(self.n)
+        # global LIMIT over shards: keep what is left of n after the ranks before this one
+        from ..parallel import comm
+
+        counts = comm.all_gather_object(int(t.count()))
+        before = sum(counts[:comm.rank()])
+        return t.head_rows(max(0, min(self.n - before, counts[comm.rank()])))
 
     def _label(self):
         return f"Limit {self.n}"

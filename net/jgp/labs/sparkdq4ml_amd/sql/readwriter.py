@@ -144,6 +144,12 @@ class DataFrameReader:
 
     # ---- csv -------------------------------------------------------------------------------
     def _read_csv(self, files: List[str]) -> Table:
+        """CSV -> columnar table.  In a multi-process group (``dq4ml.shardInput``, default on) each
+        rank parses only its byte range, moved to row boundaries (Hadoop split semantics), and the
+        inferred schema is merged across ranks (tightest common type; names from rank 0, whose
+        shard holds the header) — the shards then re-parse under the merged schema if it widened."""
+        from ..parallel import comm
+
         o = self._options
         dev = self._session.device
         data = b"".join(self._read_bytes(f) for f in files)
@@ -153,22 +159,44 @@ class DataFrameReader:
         sep = "\t" if sep == "\\t" else sep
         user_types = [_type_to_code(f.dataType) for f in self._schema.fields] if self._schema else []
         user_names = self._schema.names if self._schema else []
+        world, rank = comm.world_size(), comm.rank()
+        shard = world > 1 and _truthy(self._session.conf.get("dq4ml.shardInput", "true"))
+        if shard:
+            from ..ops.csvscan import shard_byte_range
+
+            lo, hi = shard_byte_range(data, rank, world)
+            data = data[lo:hi]
+            header = header and rank == 0
         thresh = int(self._session.conf.get("dq4ml.csv.deviceThresholdBytes", str(64 << 20)))
-        if dev.type == "cuda" and len(data) >= thresh and not user_types and header is False:
+        use_dev = dev.type == "cuda" and not user_types and not _truthy(o.get("header", "false"))
+        if shard:  # every rank must take the same (collective) path
+            use_dev = all(comm.all_gather_object(bool(use_dev and len(data) >= thresh)))
+        elif use_dev:
+            use_dev = len(data) >= thresh
+        if use_dev:
             from ..ops import csvscan
 
             with tracing.span("csv_scan"):
-                t = csvscan.scan_device(data, sep=sep, infer=infer, device=dev)
+                t = csvscan.scan_device(data, sep=sep, infer=infer, device=dev, sharded=shard)
             if t is not None:
                 return t
-        from ..ops import native
+        with tracing.span("csv_scan"):
+            nrows, cols = self._host_scan(data, header, infer, user_types, user_names, sep)
+            if shard and not user_types:
+                from ..ops import native
 
-        nrows, cols = native.host().csv_scan(
-            data, sep=sep, quote=o.get("quote", '"'), escape=o.get("escape", "\\"), header=header,
-            infer=infer, null_value=o.get("nullvalue", ""), comment=o.get("comment", ""),
-            ignore_leading_ws=_truthy(o.get("ignoreleadingwhitespace", "false")),
-            ignore_trailing_ws=_truthy(o.get("ignoretrailingwhitespace", "false")),
-            user_types=user_types, user_names=user_names)
+                h = native.host()
+                mine = ([c[0] for c in cols], [int(c[1]) for c in cols])
+                parts = comm.all_gather_object(mine)
+                names = parts[0][0] or max((p[0] for p in parts), key=len)
+                ncol = len(names)
+                codes = [0] * ncol
+                for _, cs in parts:
+                    for i in range(min(ncol, len(cs))):
+                        codes[i] = int(h.csv_merge_types(codes[i], cs[i]))
+                codes = [c if c else 6 for c in codes] if any(len(p[1]) for p in parts) else codes
+                if (list(names), codes) != (mine[0], mine[1]):
+                    nrows, cols = self._host_scan(data, header, False, codes, list(names), sep)
         fields, columns = [], []
         for (name, code, vals, valid) in cols:
             dt = self._schema[len(fields)].dataType if self._schema else csv_code_to_type(code)
@@ -179,6 +207,17 @@ class DataFrameReader:
             fields.append(StructField(name, dt, True))
             columns.append(c)
         return Table(StructType(fields), columns, nrows, None, dev)
+
+    def _host_scan(self, data, header, infer, user_types, user_names, sep):
+        from ..ops import native
+
+        o = self._options
+        return native.host().csv_scan(
+            data, sep=sep, quote=o.get("quote", '"'), escape=o.get("escape", "\\"), header=header,
+            infer=infer, null_value=o.get("nullvalue", ""), comment=o.get("comment", ""),
+            ignore_leading_ws=_truthy(o.get("ignoreleadingwhitespace", "false")),
+            ignore_trailing_ws=_truthy(o.get("ignoretrailingwhitespace", "false")),
+            user_types=user_types, user_names=user_names)
 
     @staticmethod
     def _read_bytes(path) -> bytes:
