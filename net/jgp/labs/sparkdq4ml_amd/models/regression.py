@@ -184,6 +184,7 @@ class LinearRegression(_LRParams):
         with tracing.span("gram"):
             flat = kernels.gram_stats(X.values, yv, w, sel, _gram_dtype(self, df), x_zero_dead=x_zero_dead)
         tracing.add_rows("gram", tbl.nrows)
+        _rank_health(df)
         with tracing.span("allreduce"):
             flat = comm.all_reduce_sum(flat)  # X1: data-parallel Gram all-reduce (RCCL over xGMI)
         args = (flat, d, self.getOrDefault("fitIntercept"), float(self.getOrDefault("regParam")),
@@ -205,6 +206,20 @@ class LinearRegression(_LRParams):
         model._set_summary(LinearRegressionTrainingSummary(model, df, wls, wls.objectiveHistory,
                                                            stats=stats, solver=wls.solver))
         return model
+
+
+def _rank_health(df):
+    """Rank-health barrier before the first distributed fit of a session (``dq4ml.healthCheck``:
+    ``once`` (default) | ``always`` | ``never``) — a dead rank surfaces as ``RankFailure``."""
+    if comm.world_size() == 1:
+        return
+    sess = getattr(df, "sparkSession", None)
+    mode = str(sess.conf.get("dq4ml.healthCheck", "once")).lower() if sess is not None else "once"
+    if mode == "never" or (mode == "once" and getattr(sess, "_health_checked", False)):
+        return
+    comm.health_check(float(sess.conf.get("dq4ml.healthCheckTimeout", "30")) if sess is not None else 30.0)
+    if sess is not None:
+        sess._health_checked = True
 
 
 def _async_fit(df, flat, d, args) -> bool:

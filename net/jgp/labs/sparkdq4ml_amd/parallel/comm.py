@@ -22,7 +22,8 @@ from typing import List, Optional
 import torch
 import torch.distributed as dist
 
-__all__ = ["init", "is_initialized", "rank", "world_size", "local_rank", "barrier", "all_reduce_sum",
+__all__ = ["init", "is_initialized", "rank", "world_size", "local_rank", "barrier", "health_check", "RankFailure",
+           "all_reduce_sum",
            "all_reduce_max", "broadcast", "all_gather_object", "gather_rows_to_root", "shutdown",
            "DEFAULT_BUCKET_BYTES"]
 
@@ -46,10 +47,21 @@ def local_rank() -> int:
     return int(os.environ.get("LOCAL_RANK", "0"))
 
 
-def init(backend: Optional[str] = None, timeout_s: float = 300.0):
-    """Initialise the process group from torchrun env vars (RANK/WORLD_SIZE/MASTER_ADDR/PORT)."""
+class RankFailure(RuntimeError):
+    """A peer rank did not answer a health check / collective in time."""
+
+
+def _timeout_s(default: float = 300.0) -> float:
+    return float(os.environ.get("DQ4ML_COMM_TIMEOUT", str(default)))
+
+
+def init(backend: Optional[str] = None, timeout_s: Optional[float] = None):
+    """Initialise the process group from torchrun env vars (RANK/WORLD_SIZE/MASTER_ADDR/PORT).
+    Collectives time out after ``timeout_s`` (env ``DQ4ML_COMM_TIMEOUT``, default 300 s) instead
+    of hanging on a dead peer."""
     if is_initialized():
         return
+    timeout_s = _timeout_s() if timeout_s is None else timeout_s
     if int(os.environ.get("WORLD_SIZE", "1")) <= 1 and "MASTER_ADDR" not in os.environ:
         return
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -65,6 +77,37 @@ def init(backend: Optional[str] = None, timeout_s: float = 300.0):
 def shutdown():
     if is_initialized():
         dist.destroy_process_group()
+
+
+def health_check(timeout_s: float = 30.0):
+    """Rank-health barrier: every rank contributes 1; raises :class:`RankFailure` (naming the
+    missing ranks where the backend can tell) instead of blocking forever on a dead peer."""
+    if world_size() == 1:
+        return
+    if dist.get_backend() == "gloo":
+        try:
+            dist.monitored_barrier(timeout=datetime.timedelta(seconds=timeout_s), wait_all_ranks=True)
+        except RuntimeError as e:
+            raise RankFailure(f"rank health check failed: {e}") from e
+        return
+    x = torch.ones(1, device=torch.device("cuda", torch.cuda.current_device()))
+    work = dist.all_reduce(x, async_op=True)
+    try:
+        ok = work.wait(timeout=datetime.timedelta(seconds=timeout_s))
+    except RuntimeError as e:
+        raise RankFailure(f"rank health check failed: {e}") from e
+    if ok is False or int(x.item()) != world_size():
+        raise RankFailure(f"rank health check: {int(x.item())} of {world_size()} ranks answered")
+
+
+def _fault(point: str):
+    """Fault injection for tests (env ``DQ4ML_FAULT=point:rank``): the named rank exits hard at
+    ``point`` so the survivors' error path can be exercised."""
+    spec = os.environ.get("DQ4ML_FAULT")
+    if spec:
+        p, _, r = spec.partition(":")
+        if p == point and (not r or int(r) == rank()):
+            os._exit(17)
 
 
 def barrier():
@@ -100,6 +143,7 @@ def all_reduce_sum(t: torch.Tensor, bucket_bytes: Optional[int] = None) -> torch
     for a fixed world size, so repeated runs are bit-reproducible."""
     if world_size() == 1:
         return t
+    _fault("before_allreduce")
     bucket_bytes = bucket_bytes or _bucket_bytes
     src_dev = t.device
     x = _comm_tensor(t.contiguous())
