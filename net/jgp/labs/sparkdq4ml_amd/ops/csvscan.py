@@ -18,7 +18,7 @@ from . import native
 __all__ = ["scan_device", "merge_type_mask", "shard_byte_range"]
 
 CT_NULL, CT_INT, CT_LONG, CT_DECIMAL, CT_DOUBLE, CT_BOOL, CT_STRING = range(7)
-STATS = {"device_scans": 0, "fallbacks": 0}
+STATS = {"device_scans": 0, "fallbacks": 0, "chunks": 0}
 
 
 def merge_type_mask(mask: int) -> int:
@@ -53,76 +53,161 @@ def shard_byte_range(data: bytes, rank: int, world: int) -> Tuple[int, int]:
     return align(n * rank // world), align(n * (rank + 1) // world)
 
 
-def scan_device(data: bytes, sep: str = ",", infer: bool = True, device=None, ncols: Optional[int] = None,
-                sharded: bool = False):
-    from ..sql.localdata import ColumnData
-    from ..sql.table import Table
-    from ..sql.types import (BooleanType, DoubleType, IntegerType, LongType, StructField, StructType)
+def _ncols_of(data: bytes, sep: str) -> int:
+    ends = [x for x in (data.find(b"\n"), data.find(b"\r")) if x >= 0]
+    return data.count(sep.encode(), 0, min(ends) if ends else len(data)) + 1
 
-    if not infer or len(sep) != 1 or data.find(b'"') >= 0 or data.find(b"\\") >= 0:
-        return None
-    h = native.hip()
-    dev = torch.device(device)
-    if ncols is None:
-        first = data.split(b"\n", 1)[0].split(b"\r", 1)[0]
-        ncols = first.count(sep.encode()) + 1
-    if ncols > 256:
-        return None
-    n = len(data)
+
+def _scan_chunk(h, buf, n: int, trailing: bool, ncols: int, sep: str, dev):
+    """K1 (line ends) + K2 (parse, type masks) over one device byte buffer; no host sync except
+    the line count."""
     stream = torch.cuda.current_stream(dev).cuda_stream
-    host = torch.frombuffer(bytearray(data), dtype=torch.uint8) if n else torch.zeros(0, dtype=torch.uint8)
-    buf = host.pin_memory().to(dev, non_blocking=True) if n else torch.zeros(1, dtype=torch.uint8, device=dev)
     nb = int(h.csv_count_blocks(n))
     counts = torch.empty(nb + 1, dtype=torch.int64, device=dev)
     h.csv_line_ends(buf.data_ptr(), n, counts.data_ptr(), 0, stream)
     nterm = int(counts[nb].item())
-    trailing = n > 0 and data[-1] not in (10, 13)
     nlines = nterm + (1 if trailing else 0)
     ends = torch.empty(max(nlines, 1), dtype=torch.int64, device=dev)
     if nterm:
         h.csv_line_ends(buf.data_ptr(), n, counts.data_ptr(), ends.data_ptr(), stream)
     if trailing:
         ends[nterm] = n
-    dvals = torch.empty(ncols, max(nlines, 1), dtype=torch.float64, device=dev)
-    ivals = torch.empty(ncols, max(nlines, 1), dtype=torch.int64, device=dev)
-    valid = torch.empty(ncols, max(nlines, 1), dtype=torch.bool, device=dev)
-    keep = torch.empty(max(nlines, 1), dtype=torch.bool, device=dev)
+    m = max(nlines, 1)
+    dvals = torch.empty(ncols, m, dtype=torch.float64, device=dev)
+    ivals = torch.empty(ncols, m, dtype=torch.int64, device=dev)
+    valid = torch.empty(ncols, m, dtype=torch.bool, device=dev)
+    keep = torch.empty(m, dtype=torch.bool, device=dev)
     masks = torch.zeros(ncols, dtype=torch.int32, device=dev)
     flags = torch.zeros(1, dtype=torch.int32, device=dev)
     h.csv_parse(buf.data_ptr(), n, ends.data_ptr(), nlines, ncols, ord(sep), dvals.data_ptr(), ivals.data_ptr(),
                 valid.data_ptr(), keep.data_ptr(), masks.data_ptr(), flags.data_ptr(), stream)
+    return nlines, dvals, ivals, valid, keep, masks, flags
+
+
+def _finish(parts, types, dev):
+    """Typed columns from per-chunk parse outputs under the merged types (int -> long -> double
+    widening is exact: the parser flags integers beyond 2^53 for the host path)."""
+    from ..sql.localdata import ColumnData
+    from ..sql.table import Table
+    from ..sql.types import (BooleanType, DoubleType, IntegerType, LongType, StructField, StructType)
+
+    fields, cols = [], []
+    total = sum(p[0] for p in parts)
+    for c, t in enumerate(types):
+        vals_l, valid_l = [], []
+        for nlines, dvals, ivals, valid, _, _, _ in parts:
+            if nlines == 0:
+                continue
+            valid_l.append(valid[c, :nlines])
+            if t == CT_INT:
+                vals_l.append(ivals[c, :nlines].to(torch.int32))
+            elif t == CT_LONG:
+                vals_l.append(ivals[c, :nlines])
+            elif t == CT_BOOL:
+                vals_l.append(ivals[c, :nlines] != 0)
+            else:
+                vals_l.append(dvals[c, :nlines])
+        dt = {CT_INT: IntegerType(), CT_LONG: LongType(), CT_BOOL: BooleanType()}.get(t, DoubleType())
+        if vals_l:
+            vals = torch.cat(vals_l) if len(vals_l) > 1 else vals_l[0].clone()
+            v = torch.cat(valid_l) if len(valid_l) > 1 else valid_l[0]
+        else:
+            vals = torch.empty(0, dtype=dt.torch_dtype, device=dev)
+            v = torch.ones(0, dtype=torch.bool, device=dev)
+        vv = None if bool(v.all()) else v.clone()
+        fields.append(StructField(f"_c{c}", dt, True))
+        cols.append(ColumnData(dt, vals, vv))
+    table = Table(StructType(fields), cols, total, None, dev)
+    keeps = [p[4][:p[0]] for p in parts if p[0]]
+    if total:
+        k = torch.cat(keeps) if len(keeps) > 1 else keeps[0]
+        if not bool(k.all()):  # empty lines are skipped
+            table = Table(table.schema, table.columns, total, k.clone(), dev).compact()
+    return table
+
+
+def _resolve_types(masks, flags, sharded):
     if sharded:
         masks = _or_reduce(masks)
         flags = comm.all_reduce_max(flags)
-    fl = int(flags.item())
-    mk = masks.cpu().numpy().astype(np.int64)
-    if fl:
-        STATS["fallbacks"] += 1
+    if int(flags.item()):
         return None
-    types = [merge_type_mask(m) for m in mk]
+    types = [merge_type_mask(m) for m in masks.cpu().numpy().astype(np.int64)]
     if any(t in (CT_STRING, CT_DECIMAL) for t in types):
+        return None
+    return types
+
+
+def scan_device(data: bytes, sep: str = ",", infer: bool = True, device=None, ncols: Optional[int] = None,
+                sharded: bool = False, chunk_bytes: Optional[int] = None):
+    """Parse ``data`` on the device.  Inputs larger than ``chunk_bytes`` stream through a
+    double-buffered pinned staging ring: chunk k+1's host->device copy runs on a side stream while
+    chunk k is parsed, chunks split on row boundaries, type masks OR-merged over
+    chunks (and ranks when ``sharded``)."""
+    if not infer or len(sep) != 1 or data.find(b'"') >= 0 or data.find(b"\\") >= 0:
+        return None
+    h = native.hip()
+    dev = torch.device(device)
+    if ncols is None:
+        ncols = _ncols_of(data, sep)
+    if ncols > 256:
+        return None
+    n = len(data)
+    if chunk_bytes is None or n <= chunk_bytes:
+        host = torch.frombuffer(bytearray(data), dtype=torch.uint8) if n else torch.zeros(0, dtype=torch.uint8)
+        buf = host.pin_memory().to(dev, non_blocking=True) if n else torch.zeros(1, dtype=torch.uint8, device=dev)
+        trailing = n > 0 and data[-1] not in (10, 13)
+        parts = [_scan_chunk(h, buf, n, trailing, ncols, sep, dev)]
+    else:
+        parts = _scan_chunked(h, data, ncols, sep, dev, int(chunk_bytes))
+    masks = parts[0][5]
+    flags = parts[0][6]
+    for p in parts[1:]:
+        masks = masks | p[5]
+        flags = torch.maximum(flags, p[6])
+    types = _resolve_types(masks, flags, sharded)
+    if types is None:
         STATS["fallbacks"] += 1
         return None
     STATS["device_scans"] += 1
-    fields, cols = [], []
-    for c, t in enumerate(types):
-        v = valid[c, :nlines]
-        vv = None if bool(v.all()) else v.clone()
-        if t == CT_INT:
-            vals, dt = ivals[c, :nlines].to(torch.int32), IntegerType()
-        elif t == CT_LONG:
-            vals, dt = ivals[c, :nlines].clone(), LongType()
-        elif t == CT_BOOL:
-            vals, dt = ivals[c, :nlines] != 0, BooleanType()
-        else:
-            vals, dt = dvals[c, :nlines].clone(), DoubleType()
-        fields.append(StructField(f"_c{c}", dt, True))
-        cols.append(ColumnData(dt, vals, vv))
-    table = Table(StructType(fields), cols, nlines, None, dev)
-    k = keep[:nlines]
-    if nlines and not bool(k.all()):  # empty lines are skipped
-        table = Table(table.schema, table.columns, nlines, k.clone(), dev).compact()
-    return table
+    STATS["chunks"] = STATS.get("chunks", 0) + len(parts)
+    return _finish(parts, types, dev)
+
+
+def chunk_bounds(data: bytes, chunk_bytes: int):
+    """Row-aligned chunk boundaries: each cut moves forward to just past a line terminator."""
+    n = len(data)
+    b = [0]
+    while b[-1] < n:
+        p = min(n, b[-1] + chunk_bytes)
+        if p < n:
+            q = p
+            while q < n and data[q - 1] not in (10, 13):
+                q += 1
+            if q < n and data[q - 1] == 13 and data[q] == 10:
+                q += 1
+            p = q
+        b.append(p)
+    return b
+
+
+def _scan_chunked(h, data: bytes, ncols: int, sep: str, dev, chunk_bytes: int):
+    from ..runtime.streams import StagingRing
+
+    bounds = chunk_bounds(data, chunk_bytes)
+    spans = [(bounds[i], bounds[i + 1]) for i in range(len(bounds) - 1)]
+    ring = StagingRing(max(e - s for s, e in spans), depth=2, device=dev)
+    mv = memoryview(data)
+    ring.put(0, mv[spans[0][0]:spans[0][1]])
+    parts = []
+    for i, (s, e) in enumerate(spans):
+        if i + 1 < len(spans):
+            ring.put(i + 1, mv[spans[i + 1][0]:spans[i + 1][1]])  # overlaps chunk i's parse
+        buf = ring.get(i)
+        trailing = data[e - 1] not in (10, 13)
+        parts.append(_scan_chunk(h, buf, e - s, trailing, ncols, sep, dev))
+        ring.release(i)
+    return parts
 
 
 def _or_reduce(masks: torch.Tensor) -> torch.Tensor:

@@ -1,0 +1,63 @@
+"""HIP stream helpers: a per-device side stream for copies/collectives that
+overlap compute on the current stream, and a double-buffered pinned staging ring for streamed
+host->device ingest (chunk k+1's H2D copy runs while chunk k is parsed)."""
+from __future__ import annotations
+
+from typing import Dict, List, Optional
+
+import numpy as np
+import torch
+
+__all__ = ["side_stream", "StagingRing"]
+
+_side: Dict[int, "torch.cuda.Stream"] = {}
+
+
+def side_stream(device: Optional[torch.device] = None) -> "torch.cuda.Stream":
+    idx = torch.cuda.current_device() if device is None or device.index is None else device.index
+    s = _side.get(idx)
+    if s is None:
+        s = _side[idx] = torch.cuda.Stream(device=idx)
+    return s
+
+
+class StagingRing:
+    """``depth`` pinned host buffers + device buffers of ``nbytes``; ``put(i, data)`` copies host
+    bytes into slot ``i % depth`` and enqueues its H2D on the side stream; ``get(i)`` makes the
+    current stream wait for that copy and returns the device view.  A slot is reused only after
+    the compute that consumed it has been recorded (event), so the ring never overwrites live data."""
+
+    def __init__(self, nbytes: int, depth: int = 2, device: Optional[torch.device] = None):
+        self.device = device or torch.device("cuda", torch.cuda.current_device())
+        self.host: List[torch.Tensor] = [torch.empty(nbytes, dtype=torch.uint8).pin_memory() for _ in range(depth)]
+        self.dev: List[torch.Tensor] = [torch.empty(nbytes, dtype=torch.uint8, device=self.device)
+                                        for _ in range(depth)]
+        self.copied = [torch.cuda.Event() for _ in range(depth)]
+        self.consumed = [None] * depth
+        self.sizes = [0] * depth
+        self.depth = depth
+        self.stream = side_stream(self.device)
+
+    def put(self, i: int, data) -> None:
+        k = i % self.depth
+        if self.consumed[k] is not None:
+            self.consumed[k].synchronize()  # host must not overwrite pinned memory still being copied/used
+        n = len(data)
+        if n > self.host[k].numel():
+            raise ValueError("StagingRing: chunk larger than the staging buffers")
+        self.host[k][:n].numpy()[:] = np.frombuffer(data, dtype=np.uint8, count=n)
+        self.sizes[k] = n
+        with torch.cuda.stream(self.stream):
+            self.dev[k][:n].copy_(self.host[k][:n], non_blocking=True)
+            self.copied[k].record(self.stream)
+
+    def get(self, i: int) -> torch.Tensor:
+        k = i % self.depth
+        torch.cuda.current_stream().wait_event(self.copied[k])
+        return self.dev[k][:self.sizes[k]]
+
+    def release(self, i: int) -> None:
+        k = i % self.depth
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream())
+        self.consumed[k] = ev

@@ -177,7 +177,8 @@ class DataFrameReader:
             from ..ops import csvscan
 
             with tracing.span("csv_scan"):
-                t = csvscan.scan_device(data, sep=sep, infer=infer, device=dev, sharded=shard)
+                t = csvscan.scan_device(data, sep=sep, infer=infer, device=dev, sharded=shard,
+                                        chunk_bytes=int(self._session.conf.get("dq4ml.chunkBytes", str(256 << 20))))
             if t is not None:
                 return t
         with tracing.span("csv_scan"):

@@ -11,7 +11,10 @@
 Config keys (``.config(k, v)``): ``dq4ml.device``, ``dq4ml.gramDtype`` (fp64|fp32|bf16|fp8: the
 default Gram precision of estimators that do not set ``gramDtype``), ``dq4ml.bucketBytes`` (RCCL
 all-reduce bucket size), ``dq4ml.trace`` (per-stage tracing, ``utils.tracing``),
-``dq4ml.csv.deviceThresholdBytes`` (smallest file the device CSV scanner takes).
+``dq4ml.csv.deviceThresholdBytes`` (smallest file the device CSV scanner takes),
+``dq4ml.chunkBytes`` (device CSV streaming chunk, default 256 MiB), ``dq4ml.shardInput`` (byte-range
+sharded reads across ranks, default true), ``dq4ml.fit.async`` (asynchronous normal-equation fits),
+``dq4ml.healthCheck`` (once|always|never rank-health barrier before distributed fits).
 """
 from __future__ import annotations
 

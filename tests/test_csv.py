@@ -126,3 +126,40 @@ def test_device_scan_through_reader(tmp_path):
     np.testing.assert_array_equal(t.columns[0].values.cpu().numpy(), a)
     np.testing.assert_array_equal(t.columns[1].values.cpu().numpy(), b)
     spark.stop()
+
+
+def test_chunk_bounds_are_row_aligned():
+    from net.jgp.labs.sparkdq4ml_amd.ops.csvscan import chunk_bounds
+
+    data = open(data_path("dataset-full.csv"), "rb").read() + b"\r\n1,2\n3,4.5"
+    for cb in (7, 100, 1000, len(data) + 5):
+        b = chunk_bounds(data, cb)
+        assert b[0] == 0 and b[-1] == len(data) and all(x < y for x, y in zip(b, b[1:]))
+        assert all(data[x - 1] in (10, 13) for x in b[1:-1])  # every cut follows a terminator
+        assert all(not (data[x - 1] == 13 and data[x] == 10) for x in b[1:-1])  # never inside CRLF
+        assert sum(_host(data[x:y])[0] for x, y in zip(b, b[1:])) == _host(data)[0]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("chunk", [997, 64 << 10])
+def test_device_chunked_scan_matches_one_shot(chunk):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from net.jgp.labs.sparkdq4ml_amd.ops import csvscan
+
+    rng = np.random.default_rng(1)
+    n = 50_000
+    lines = [f"{int(x)},{float(y)!r},{int(z)}" for x, y, z in
+             zip(rng.integers(-99, 99, n), np.round(rng.normal(size=n), 3), rng.integers(0, 2**40, n))]
+    lines[1234] = "7,,"  # nulls
+    lines[40000] = "3,2.5,12.75"  # widens the third column to double late in the file
+    data = ("\r\n".join(lines[:30000]) + "\n\n" + "\n".join(lines[30000:])).encode()
+    one = csvscan.scan_device(data, device="cuda")
+    before = csvscan.STATS["chunks"]
+    many = csvscan.scan_device(data, device="cuda", chunk_bytes=chunk)
+    assert csvscan.STATS["chunks"] - before > 1
+    assert one.nrows == many.nrows == n
+    assert [c.dtype.simpleString() for c in many.columns] == ["int", "double", "double"]
+    for a, b in zip(one.columns, many.columns):
+        assert torch.equal(a.values, b.values)
+        assert torch.equal(a.valid_mask(), b.valid_mask())
