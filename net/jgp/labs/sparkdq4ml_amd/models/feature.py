@@ -18,7 +18,7 @@ from ..sql.dataframe import DataFrame
 from ..sql.expressions import (AnalysisException, ColRef, EvalContext, Expr, IsNotNull, BinOp,
                                SparkException)
 from ..sql.plan import Filter, Project
-from ..sql.table import ColumnData
+from ..sql.table import ColumnData, LazyVectorColumn
 from ..sql.types import (BooleanType, DoubleType, VectorUDT, is_numeric)
 from .param import Param, Params, param_accessors
 
@@ -97,10 +97,17 @@ class VectorAssembleExpr(Expr):
         d = sum(1 if p.dim() == 1 else int(p.shape[0]) for p in parts)
         on_dev = bool(parts) and parts[0].is_cuda
         if dt == torch.bfloat16 and on_dev and d <= 64:
-            # MI355X-native storage: MFMA-fragment-ordered tiles, dead rows zeroed (no Gram mask)
-            with tracing.span("pack"):
-                mat = kernels.pack_tiled(parts, ctx.table.sel)
-            meta = {"ml_attr": {"num_attrs": d}, "zero_dead": ctx.table.sel}
+            # MI355X-native storage: MFMA-fragment-ordered tiles, dead rows zeroed (no Gram mask) —
+            # produced lazily: a normal-equation fit reads the source columns directly (fused
+            # assemble + Gram) and never pays for the pack
+            sel = ctx.table.sel
+
+            def _pack(parts=parts, sel=sel):
+                with tracing.span("pack"):
+                    return kernels.pack_tiled(parts, sel)
+            meta = {"ml_attr": {"num_attrs": d}, "zero_dead": sel}
+            n = int(parts[0].shape[-1])
+            return LazyVectorColumn(VectorUDT(), _pack, n, (parts, sel), meta)
         elif on_dev and (dt == torch.float8_e4m3fn or (dt == torch.bfloat16 and d > 64)):
             # wide fragment layout for the LDS-tiled MFMA SYRK (fp8: per-feature scales)
             with tracing.span("pack"):

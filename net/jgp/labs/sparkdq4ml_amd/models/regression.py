@@ -182,7 +182,12 @@ class LinearRegression(_LRParams):
         zd = X.meta.get("zero_dead", False)
         x_zero_dead = yvalid is None and (tbl.sel is None or (zd is not False and zd is tbl.sel))
         with tracing.span("gram"):
-            flat = kernels.gram_stats(X.values, yv, w, sel, _gram_dtype(self, df), x_zero_dead=x_zero_dead)
+            gd = _gram_dtype(self, df)
+            if _fusable_assembly(X, w, gd, yvalid):
+                parts, asel = X.sources  # fused VectorAssembler + Gram: the features are never packed
+                flat = kernels.gram_cols(parts, yv, sel if sel is not None else asel)
+            else:
+                flat = kernels.gram_stats(X.values, yv, w, sel, gd, x_zero_dead=x_zero_dead)
         tracing.add_rows("gram", tbl.nrows)
         _rank_health(df)
         with tracing.span("allreduce"):
@@ -206,6 +211,16 @@ class LinearRegression(_LRParams):
         model._set_summary(LinearRegressionTrainingSummary(model, df, wls, wls.objectiveHistory,
                                                            stats=stats, solver=wls.solver))
         return model
+
+
+def _fusable_assembly(X, w, gram_dtype, yvalid) -> bool:
+    from ..sql.table import LazyVectorColumn
+
+    if not isinstance(X, LazyVectorColumn) or X.materialized or w is not None or gram_dtype != "bf16":
+        return False
+    parts, _ = X.sources
+    return all(p.is_cuda and p.dtype in (torch.float32, torch.float64, torch.bfloat16, torch.int32, torch.int64,
+                                          torch.bool, torch.uint8) for p in parts)
 
 
 def _rank_health(df):

@@ -39,4 +39,13 @@ int gram_plan_blocks(int mode, int d, int64_t n, int xdt, int xmode);
 // xmode: 0 = X already zero on dead rows (or no sel/w), 1 = binary mask from sel, 2 = general weights
 void gram_tall(int mode, GramArgs a, int xmode, int blocks, double* out, hipStream_t st);
 
+// fused VectorAssembler + bf16 Gram over d <= 64 source columns (a.X unused; a.sel masks rows)
+struct PackSrcG {
+  const void* ptr;
+  int dt;
+  int pad;
+};
+int gram_cols_blocks(int d, int64_t n);
+void gram_cols(GramArgs a, const PackSrcG* srcs_dev, int blocks, double* out, hipStream_t st);
+
 }  // namespace dq4ml

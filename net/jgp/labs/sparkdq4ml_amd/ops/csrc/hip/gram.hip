@@ -379,6 +379,177 @@ __global__ __launch_bounds__((BF16Geom<NT, XMODE>::kBlock), 1) void gram_tall_bf
 }
 
 // =============================================================================================
+// Fused assemble + Gram over SOURCE COLUMNS (d <= 64): the VectorAssembler output is never
+// materialized.  Block-cooperative superstep: 256 threads vector-load 64 rows x 32*NT features
+// with 16-B loads (thread (f, q) = rows [8q, 8q+8) of feature f: coalesced 256-B column runs),
+// convert to bf16 (dead rows of the selection -> 0) and store them in MFMA-fragment order in LDS
+// (that octet IS one lane's fragment of k-step q & 3, half q >> 2); wave w then runs k-step w's
+// MFMAs for every tile pair.  Next superstep's global loads are in flight during the MFMAs;
+// double-buffered LDS, one barrier per superstep.  Partials use the bf16 kernel's slab layout.
+// =============================================================================================
+template <int NT>
+__global__ __launch_bounds__(256, (NT == 1 ? 3 : 2)) void gram_cols_kernel(GramArgs a, const PackSrcG* __restrict__ srcs) {
+  constexpr int NPAIR = NT * (NT + 1) / 2;
+  constexpr int FR = NT * 4 * 64 * 16;   // fragment bytes per superstep
+  constexpr int BUF = FR + 4 * 64 * 2;   // + W stripe [4 cols][64 rows] bf16
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int f = lane & 31, h = lane >> 5;
+  const int fl = tid >> 3, q = tid & 7;
+
+  f32x16 acc[NPAIR];
+  f32x16 accw[NT];
+#pragma unroll
+  for (int p = 0; p < NPAIR; ++p) acc[p] = f32x16{};
+#pragma unroll
+  for (int t = 0; t < NT; ++t) accw[t] = f32x16{};
+  RowAcc ra;
+
+  PackSrcG src[NT];
+  bool fv[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int feat = t * 32 + fl;
+    fv[t] = feat < a.d;
+    src[t] = fv[t] ? srcs[feat] : PackSrcG{nullptr, 0, 0};
+  }
+  const int64_t nsup = (a.n + 63) / 64;
+  const int64_t s0 = (int64_t)blockIdx.x * a.spw;
+  const int64_t s1 = s0 + a.spw < nsup ? s0 + a.spw : nsup;
+
+  float x[NT][8];
+  auto gload = [&](int64_t s) {
+    const int64_t r0 = s * 64 + 8 * q;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      if (fv[t]) {
+        load8_f32(src[t].ptr, src[t].dt, r0, a.n, x[t]);
+        mask8(a.sel, r0, a.n, x[t]);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) x[t][j] = 0.0f;
+      }
+    }
+  };
+  auto stage = [&](int buf, int64_t s) {
+    unsigned char* base = smem + buf * BUF;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      bf16x8 v;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = (__bf16)x[t][j];
+      *reinterpret_cast<u32x4*>(base + (((t * 4 + (q & 3)) * 64 + 32 * (q >> 2) + fl) << 4)) = __builtin_bit_cast(u32x4, v);
+    }
+    if (tid < 64) {
+      const RowVals rv = row_vals(a, s * 64 + tid);
+      ra.add(rv);
+      __bf16* wl = reinterpret_cast<__bf16*>(base + FR);
+      const float w_hi = (float)(__bf16)(float)rv.w;
+      const __bf16 wy_hi = (__bf16)(float)rv.wy;
+      wl[0 * 64 + tid] = (__bf16)(float)rv.w;
+      wl[1 * 64 + tid] = (__bf16)(float)(rv.w - (double)w_hi);
+      wl[2 * 64 + tid] = wy_hi;
+      wl[3 * 64 + tid] = (__bf16)(float)(rv.wy - (double)(float)wy_hi);
+    }
+  };
+  auto compute = [&](int buf) {
+    const unsigned char* base = smem + buf * BUF;
+    const int i = wave;  // this wave's k-step
+    bf16x8 fr[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) fr[t] = *reinterpret_cast<const bf16x8*>(base + (((t * 4 + i) * 64 + lane) << 4));
+    bf16x8 wf = bf16x8{};
+    if (f < 4) wf = *reinterpret_cast<const bf16x8*>(base + FR + (f * 64 + 32 * h + 8 * i) * 2);
+    int p = 0;
+#pragma unroll
+    for (int I = 0; I < NT; ++I)
+#pragma unroll
+      for (int J = I; J < NT; ++J, ++p) acc[p] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fr[I], fr[J], acc[p], 0, 0, 0);
+#pragma unroll
+    for (int t = 0; t < NT; ++t) accw[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fr[t], wf, accw[t], 0, 0, 0);
+  };
+
+  if (s0 < s1) gload(s0);
+  for (int64_t s = s0; s < s1; ++s) {
+    const int buf = (int)((s - s0) & 1);
+    stage(buf, s);
+    if (s + 1 < s1) gload(s + 1);
+    __syncthreads();
+    compute(buf);
+  }
+
+  // ---- block reduction over the 4 waves (two tree rounds) + partial slab -----------------------
+  constexpr int NV = (NPAIR + NT) * 16;
+  double sc[5] = {ra.cnt, ra.ws, ra.wws, ra.bs, ra.bbs};
+#pragma unroll
+  for (int k = 0; k < 5; ++k) sc[k] = wave_sum_f64(sc[k]);
+  __syncthreads();
+  float* tr = reinterpret_cast<float*>(smem);
+  double* scl = reinterpret_cast<double*>(smem + (size_t)2 * NV * 64 * sizeof(float));
+  if (lane == 0) {
+#pragma unroll
+    for (int k = 0; k < 5; ++k) scl[wave * 5 + k] = sc[k];
+  }
+#pragma unroll
+  for (int step = 2; step >= 1; step >>= 1) {
+    if (wave >= step && wave < 2 * step) {
+      float* dst = tr + (size_t)(wave - step) * NV * 64 + lane;
+      int v = 0;
+#pragma unroll
+      for (int p = 0; p < NPAIR; ++p)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) dst[(v++) * 64] = acc[p][r];
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) dst[(v++) * 64] = accw[t][r];
+    }
+    __syncthreads();
+    if (wave < step) {
+      const float* srcp = tr + (size_t)wave * NV * 64 + lane;
+      int v = 0;
+#pragma unroll
+      for (int p = 0; p < NPAIR; ++p)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[p][r] += srcp[(v++) * 64];
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) accw[t][r] += srcp[(v++) * 64];
+    }
+    __syncthreads();
+  }
+  if (wave == 0) {
+    const int d = a.d;
+    double* out = a.partials + (int64_t)blockIdx.x * a.P;
+    if (lane < 5) out[lane] = scl[lane] + scl[5 + lane] + scl[10 + lane] + scl[15 + lane];
+    const int col = mfma32_col(lane);
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float v = accw[t][r];
+        const float vn = __shfl_down(v, 1, 64);
+        const int feat = t * 32 + mfma32_row(lane, r);
+        if (feat < d) {
+          if (col == 0) out[5 + feat] = (double)v + (double)vn;
+          if (col == 2) out[5 + d + feat] = (double)v + (double)vn;
+        }
+      }
+    }
+    int p = 0;
+#pragma unroll
+    for (int I = 0; I < NT; ++I)
+#pragma unroll
+      for (int J = I; J < NT; ++J, ++p) {
+        double* tile = out + 5 + 2 * d + p * 1024;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) tile[mfma32_row(lane, r) * 32 + col] = (double)acc[p][r];
+      }
+  }
+}
+
+// =============================================================================================
 // f64 MFMA kernel (v_mfma_f64_16x16x4_f64): Spark-parity precision
 // =============================================================================================
 template <typename TX, int NT>
@@ -746,6 +917,42 @@ void gram_tall(int mode, GramArgs a, int xmode, int blocks, double* out, hipStre
   const int NT = (a.d + T - 1) / T;
   hipLaunchKernelGGL(gram_reduce_kernel, dim3(reduce_blocks(a.d)), dim3(1024), 0, st, a.partials, blocks, a.P, a.d,
                      T, NT, out);
+  DQ_HIP_CHECK(hipGetLastError());
+}
+
+static size_t cols_lds(int NT) {
+  const size_t bufs = 2 * ((size_t)NT * 4 * 64 * 16 + 4 * 64 * 2);
+  const size_t tree = (size_t)2 * ((NT * (NT + 1) / 2 + NT) * 16) * 64 * sizeof(float) + 4 * 5 * sizeof(double);
+  return bufs > tree ? bufs : tree;
+}
+
+int gram_cols_blocks(int d, int64_t n) {
+  const int NT = (d + 31) / 32;
+  int full = 1;
+  if (NT == 1) full = occupancy_blocks(gram_cols_kernel<1>, cols_lds(1), 256);
+  else full = occupancy_blocks(gram_cols_kernel<2>, cols_lds(2), 256);
+  const int64_t nsup = (n + 63) / 64;
+  int64_t want = (nsup + 3) / 4;  // >= 4 supersteps per block
+  if (want < 1) want = 1;
+  return (int)(want < full ? want : full);
+}
+
+void gram_cols(GramArgs a, const PackSrcG* srcs_dev, int blocks, double* out, hipStream_t st) {
+  if (a.d < 1 || a.d > 64) throw std::invalid_argument("gram_cols: d must be in [1, 64]");
+  if (a.w != nullptr) throw std::invalid_argument("gram_cols: instance weights need the materialized path");
+  if (blocks < 1) throw std::invalid_argument("gram_cols: blocks must be >= 1");
+  const int64_t nsup = (a.n + 63) / 64;
+  a.spw = (nsup + blocks - 1) / blocks;
+  if (a.spw < 1) a.spw = 1;
+  a.nsuper = nsup;
+  a.P = (int)gram_partial_stride(GRAM_BF16, a.d);
+  const int NT = (a.d + 31) / 32;
+  const size_t lds = cols_lds(NT);
+  if (NT == 1) hipLaunchKernelGGL(gram_cols_kernel<1>, dim3(blocks), dim3(256), lds, st, a, srcs_dev);
+  else hipLaunchKernelGGL(gram_cols_kernel<2>, dim3(blocks), dim3(256), lds, st, a, srcs_dev);
+  DQ_HIP_CHECK(hipGetLastError());
+  hipLaunchKernelGGL(gram_reduce_kernel, dim3(reduce_blocks(a.d)), dim3(1024), 0, st, a.partials, blocks, a.P, a.d,
+                     32, NT, out);
   DQ_HIP_CHECK(hipGetLastError());
 }
 

@@ -60,6 +60,19 @@ PYBIND11_MODULE(_dq4ml_hip, m) {
           a.partials = P<double>(partials);
           gram_tall(mode, a, xmode, blocks, P<double>(out), as_stream(stream));
         });
+  m.def("gram_cols_blocks", &gram_cols_blocks);
+  m.def("gram_cols", [](uintptr_t srcs, int d, int64_t n, uintptr_t y, int ydt, uintptr_t sel, uintptr_t partials,
+                        int blocks, uintptr_t out, uintptr_t stream) {
+    GramArgs a{};
+    a.d = d;
+    a.n = n;
+    a.xdt = DT_F32;
+    a.y = P<const void>(y);
+    a.ydt = ydt;
+    a.sel = P<const uint8_t>(sel);
+    a.partials = P<double>(partials);
+    gram_cols(a, P<const PackSrcG>(srcs), blocks, P<double>(out), as_stream(stream));
+  });
   m.def("tiled_elems", &tiled_elems);
   m.def("tile_bf16", [](uintptr_t X, int xdt, int64_t ld, int d, int64_t n, uintptr_t out, uintptr_t stream) {
     tile_bf16(P<const void>(X), xdt, ld, d, n, P<void>(out), as_stream(stream));

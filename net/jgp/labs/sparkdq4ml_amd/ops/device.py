@@ -142,6 +142,42 @@ def gram_stats(X, y, w, sel, compute: str = "fp64", x_zero_dead: bool = False, b
     return out
 
 
+def gram_cols(parts: List[torch.Tensor], y, sel, blocks: Optional[int] = None):
+    """Fused VectorAssembler + bf16 Gram over the SOURCE columns (d <= 64, unit weights): the
+    assembled matrix is never written (``gram.hip: gram_cols_kernel``)."""
+    h = native.hip()
+    rows = _rows_of(parts)
+    d, n = len(rows), rows[0].numel()
+    if not 1 <= d <= 64:
+        raise ValueError("gram_cols: 1 <= d <= 64")
+    for r in rows:
+        _check_dev(r)
+        if r.numel() != n:
+            raise ValueError("gram_cols: columns of different lengths")
+        dtype_code(r)
+    dev = rows[0].device
+    y, _, sel = _prep_rows(y, None, sel, n)
+    desc = _srcw_desc(h, rows, dev)
+    nb = int(blocks or _cols_blocks(h, d, n))
+    P = int(h.gram_partial_stride(2, d))
+    partials = torch.empty(nb * P, dtype=torch.float64, device=dev)
+    out = torch.empty(5 + 2 * d + d * (d + 1) // 2, dtype=torch.float64, device=dev)
+    h.gram_cols(desc.data_ptr(), d, n, y.data_ptr(), dtype_code(y), _ptr(sel), partials.data_ptr(), nb,
+                out.data_ptr(), _stream())
+    return out
+
+
+_cols_plan = {}
+
+
+def _cols_blocks(h, d, n):
+    key = (torch.cuda.current_device(), d, n)
+    nb = _cols_plan.get(key)
+    if nb is None:
+        nb = _cols_plan[key] = int(h.gram_cols_blocks(int(d), int(n)))
+    return nb
+
+
 def _prep_rows(y, w, sel, n):
     y = y.contiguous()
     if y.dtype not in (torch.float64, torch.float32):

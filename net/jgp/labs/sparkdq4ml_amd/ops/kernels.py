@@ -65,6 +65,13 @@ def pack_tiled(parts: Sequence[torch.Tensor], sel: Optional[torch.Tensor] = None
     return device.pack_tiled(list(parts), sel)
 
 
+def gram_cols(parts: Sequence[torch.Tensor], y: torch.Tensor, sel: Optional[torch.Tensor] = None):
+    """GPU only: fused VectorAssembler + bf16 Gram over the source columns (d <= 64)."""
+    from . import device
+
+    return device.gram_cols(list(parts), y, sel)
+
+
 def pack_wide(parts: Sequence[torch.Tensor], eb: int, sel: Optional[torch.Tensor] = None):
     """GPU only: columns -> wide (d > 64) fragment layout, bf16 (eb 16) or fp8 e4m3 with
     per-feature scales (eb 8) (``ops.layout.TiledWide``); rows outside ``sel`` become zeros."""

@@ -25,7 +25,7 @@ __all__ = ["ColumnData", "Table"]
 
 
 @dataclass
-class ColumnData:
+class ColumnData:  # noqa: D101 (dataclass below)
     dtype: DataType
     values: object  # torch.Tensor [n] | [d, n] (VectorUDT) | list (StringType)
     valid: Optional[torch.Tensor] = None  # bool [n]; None => no nulls
@@ -104,6 +104,39 @@ class ColumnData:
             vals = [v if ok else None for v, ok in zip(vals, m)]
         return vals
 
+
+
+class LazyVectorColumn(ColumnData):
+    """A vector column whose storage is produced on first use (the VectorAssembler's output):
+    consumers that can read the SOURCE columns directly (the fused assemble+Gram kernel) never
+    materialize it; everything else gets the packed matrix through ``values``."""
+
+    def __init__(self, dtype, materialize, n: int, sources, meta=None):  # noqa: D107
+        self.dtype = dtype
+        self.valid = None
+        self.meta = meta or {}
+        self._materialize = materialize
+        self._vals = None
+        self._n = int(n)
+        self.sources = sources  # (parts, sel)
+
+    @property
+    def values(self):
+        if self._vals is None:
+            self._vals = self._materialize()
+        return self._vals
+
+    @values.setter
+    def values(self, v):
+        self._vals = v
+
+    @property
+    def materialized(self) -> bool:
+        return self._vals is not None
+
+    @property
+    def n(self) -> int:
+        return self._n
 
 class Table:
     def __init__(self, schema: StructType, columns: List[ColumnData], nrows: int,

@@ -145,3 +145,47 @@ def test_tiled_layout_roundtrip_and_gram(d, n):
     m1 = device.regression_metrics(T, y, coef, 0.5, sel, 0.0)
     m2 = kernels.regression_metrics(X.float().cpu(), y.cpu(), coef, 0.5, sel.cpu(), 0.0)
     assert _rel(m1, m2) < 1e-10
+
+
+@pytest.mark.parametrize("d", [1, 20, 32, 33, 64])
+@pytest.mark.parametrize("n", [63, 4096 + 17, 300_001])
+def test_gram_cols_fused_matches_pack_then_gram(d, n):
+    # fused VectorAssembler + Gram over source columns == pack_tiled (dead rows zeroed) + tiled Gram
+    g = torch.Generator(device="cuda").manual_seed(d * 7 + n)
+    cols = [torch.randn(n, generator=g, device="cuda") * (1 + j % 3) for j in range(d)]
+    if d > 2:
+        cols[1] = cols[1].double()
+        cols[2] = (cols[2] * 10).to(torch.int32)
+    y = torch.randn(n, generator=g, device="cuda", dtype=torch.float64)
+    sel = torch.rand(n, generator=g, device="cuda") > 0.3
+    fused = device.gram_cols(cols, y, sel)
+    T = device.pack_tiled(cols, sel)
+    ref = device.gram_stats(T, y, None, sel, "bf16", x_zero_dead=True)
+    assert torch.equal(fused[:5], ref[:5])
+    assert _rel(fused[5:], ref[5:]) < 1e-6
+    fused_all = device.gram_cols(cols, y, None)
+    ref_all = device.gram_stats(device.pack_tiled(cols, None), y, None, None, "bf16", x_zero_dead=True)
+    assert _rel(fused_all, ref_all) < 1e-6
+
+
+def test_assembler_fit_uses_fused_gram(gpu_session):
+    from net.jgp.labs.sparkdq4ml_amd import LinearRegression, VectorAssembler, col
+    from net.jgp.labs.sparkdq4ml_amd.sql.table import LazyVectorColumn
+
+    n, d = 200_000, 12
+    g = torch.Generator(device="cuda").manual_seed(3)
+    data = {f"f{j}": torch.randn(n, generator=g, device="cuda") for j in range(d)}
+    beta = torch.linspace(-1, 1, d, device="cuda", dtype=torch.float64)
+    data["label"] = sum(beta[j] * data[f"f{j}"].double() for j in range(d)) + 2.0
+    df = gpu_session.createDataFrame(data).filter(col("f0") > -1.0)
+    out = VectorAssembler(inputCols=[f"f{j}" for j in range(d)], outputCol="features",
+                          outputDtype="bfloat16").transform(df)
+    m = LinearRegression(solver="normal", gramDtype="bf16").fit(out)
+    feats = out._table().column("features")
+    assert isinstance(feats, LazyVectorColumn) and not feats.materialized  # fit never packed the features
+    ref = LinearRegression(solver="normal", gramDtype="bf16").fit(
+        gpu_session.createDataFrame({"features": out._table().compact().column("features").dense(),
+                                     "label": out._table().compact().column("label").values}))
+    np.testing.assert_allclose(m.coefficients.toArray(), ref.coefficients.toArray(), rtol=1e-4, atol=1e-5)
+    assert float(m.summary.r2) > 0.999  # summary materializes the features lazily
+    assert feats.materialized
