@@ -159,7 +159,7 @@ class LinearRegression(_LRParams):
 
     def _train(self, df: DataFrame) -> "LinearRegressionModel":
         tbl, X, y = _features_label(self, df)
-        d = int(X.values.shape[0])
+        d = _num_features(X)
         if d <= 0:
             raise ValueError("requirement failed: The number of features must be positive.")
         loss, solver = self.getOrDefault("loss"), self.getOrDefault("solver")
@@ -211,6 +211,15 @@ class LinearRegression(_LRParams):
         model._set_summary(LinearRegressionTrainingSummary(model, df, wls, wls.objectiveHistory,
                                                            stats=stats, solver=wls.solver))
         return model
+
+
+def _num_features(X) -> int:
+    """Feature count without materializing a lazily assembled column."""
+    from ..sql.table import LazyVectorColumn
+
+    if isinstance(X, LazyVectorColumn) and not X.materialized:
+        return int(X.meta["ml_attr"]["num_attrs"])
+    return int(X.values.shape[0])
 
 
 def _fusable_assembly(X, w, gram_dtype, yvalid) -> bool:

@@ -161,7 +161,7 @@ def test_gram_cols_fused_matches_pack_then_gram(d, n):
     fused = device.gram_cols(cols, y, sel)
     T = device.pack_tiled(cols, sel)
     ref = device.gram_stats(T, y, None, sel, "bf16", x_zero_dead=True)
-    assert torch.equal(fused[:5], ref[:5])
+    assert _rel(fused[:5], ref[:5]) < 1e-12  # f64 scalars; summation order differs
     assert _rel(fused[5:], ref[5:]) < 1e-6
     fused_all = device.gram_cols(cols, y, None)
     ref_all = device.gram_stats(device.pack_tiled(cols, None), y, None, None, "bf16", x_zero_dead=True)
