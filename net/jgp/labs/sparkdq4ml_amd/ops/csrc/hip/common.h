@@ -31,13 +31,21 @@ enum DType : int { DT_F64 = 0, DT_F32 = 1, DT_BF16 = 2, DT_I32 = 3, DT_I64 = 4, 
 
 __device__ __forceinline__ float bf16_bits_to_f32(uint16_t b) { return __uint_as_float(uint32_t(b) << 16); }
 
+// Generic pointers that reach a kernel through a descriptor table compile to FLAT loads, which
+// count on lgkmcnt too — every LDS wait/barrier would then drain the prefetch.  All descriptor
+// pointers point at device global memory: load through the global address space.
+template <typename T>
+__device__ __forceinline__ const __attribute__((address_space(1))) T* gptr(const void* p) {
+  return (const __attribute__((address_space(1))) T*)(p);
+}
+
 // 8 consecutive elements [r0, r0+8) of a typed column as f32 (zero past n); 16-byte vector loads
 // when the run is complete and aligned (r0 is a multiple of 8 in every caller)
 __device__ __forceinline__ void load8_f32(const void* p, int dt, int64_t r0, int64_t n, float x[8]) {
   const bool full = r0 + 8 <= n && ((reinterpret_cast<uintptr_t>(p) & 15) == 0);
   if (full && dt == DT_F32) {
-    const f32x4 a = *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(p) + r0);
-    const f32x4 b = *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(p) + r0 + 4);
+    const f32x4 a = *gptr<f32x4>(reinterpret_cast<const float*>(p) + r0);
+    const f32x4 b = *gptr<f32x4>(reinterpret_cast<const float*>(p) + r0 + 4);
 #pragma unroll
     for (int j = 0; j < 4; ++j) x[j] = a[j], x[4 + j] = b[j];
     return;
@@ -46,13 +54,13 @@ __device__ __forceinline__ void load8_f32(const void* p, int dt, int64_t r0, int
     const double* q = reinterpret_cast<const double*>(p) + r0;
 #pragma unroll
     for (int j = 0; j < 8; j += 2) {
-      const f64x2 v = *reinterpret_cast<const f64x2*>(q + j);
+      const f64x2 v = *gptr<f64x2>(q + j);
       x[j] = (float)v[0], x[j + 1] = (float)v[1];
     }
     return;
   }
   if (full && dt == DT_BF16) {
-    const u32x4 v = *reinterpret_cast<const u32x4*>(reinterpret_cast<const uint16_t*>(p) + r0);
+    const u32x4 v = *gptr<u32x4>(reinterpret_cast<const uint16_t*>(p) + r0);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       x[2 * j] = __uint_as_float(v[j] << 16);
@@ -66,14 +74,54 @@ __device__ __forceinline__ void load8_f32(const void* p, int dt, int64_t r0, int
     float v = 0.0f;
     if (r < n) {
       switch (dt) {
-        case DT_F64: v = (float)reinterpret_cast<const double*>(p)[r]; break;
-        case DT_F32: v = reinterpret_cast<const float*>(p)[r]; break;
-        case DT_BF16: v = bf16_bits_to_f32(reinterpret_cast<const uint16_t*>(p)[r]); break;
-        case DT_I32: v = (float)reinterpret_cast<const int32_t*>(p)[r]; break;
-        case DT_I64: v = (float)reinterpret_cast<const int64_t*>(p)[r]; break;
-        case DT_U8: v = (float)reinterpret_cast<const uint8_t*>(p)[r]; break;
+        case DT_F64: v = (float)gptr<double>(p)[r]; break;
+        case DT_F32: v = gptr<float>(p)[r]; break;
+        case DT_BF16: v = bf16_bits_to_f32(gptr<uint16_t>(p)[r]); break;
+        case DT_I32: v = (float)gptr<int32_t>(p)[r]; break;
+        case DT_I64: v = (float)gptr<int64_t>(p)[r]; break;
+        case DT_U8: v = (float)gptr<uint8_t>(p)[r]; break;
         default: v = 0.0f;
       }
+    }
+    x[j] = v;
+  }
+}
+
+// Typed variant for kernels specialized on one source dtype (no per-element switch, no alignment
+// test: the host guarantees 16-byte aligned columns).  Only the ragged last 8 rows take the
+// guarded scalar path.
+template <int SDT, bool FULL = false>
+__device__ __forceinline__ void load8_typed(const void* p, int64_t r0, int64_t n, float x[8]) {
+  if (FULL || r0 + 8 <= n) {
+    if constexpr (SDT == DT_F32) {
+      const f32x4 a = *gptr<f32x4>(reinterpret_cast<const float*>(p) + r0);
+      const f32x4 b = *gptr<f32x4>(reinterpret_cast<const float*>(p) + r0 + 4);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) x[j] = a[j], x[4 + j] = b[j];
+    } else if constexpr (SDT == DT_F64) {
+#pragma unroll
+      for (int j = 0; j < 8; j += 2) {
+        const f64x2 v = *gptr<f64x2>(reinterpret_cast<const double*>(p) + r0 + j);
+        x[j] = (float)v[0], x[j + 1] = (float)v[1];
+      }
+    } else {
+      const u32x4 v = *gptr<u32x4>(reinterpret_cast<const uint16_t*>(p) + r0);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        x[2 * j] = __uint_as_float(v[j] << 16);
+        x[2 * j + 1] = __uint_as_float(v[j] & 0xffff0000u);
+      }
+    }
+    return;
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int64_t r = r0 + j;
+    float v = 0.0f;
+    if (r < n) {
+      if constexpr (SDT == DT_F32) v = gptr<float>(p)[r];
+      else if constexpr (SDT == DT_F64) v = (float)gptr<double>(p)[r];
+      else v = bf16_bits_to_f32(gptr<uint16_t>(p)[r]);
     }
     x[j] = v;
   }
@@ -83,7 +131,7 @@ __device__ __forceinline__ void load8_f32(const void* p, int dt, int64_t r0, int
 __device__ __forceinline__ void mask8(const uint8_t* sel, int64_t r0, int64_t n, float x[8]) {
   if (sel == nullptr) return;
   if (r0 + 8 <= n && ((reinterpret_cast<uintptr_t>(sel + r0) & 7) == 0)) {
-    const uint64_t m = *reinterpret_cast<const uint64_t*>(sel + r0);
+    const uint64_t m = *gptr<uint64_t>(sel + r0);
 #pragma unroll
     for (int j = 0; j < 8; ++j)
       if (((m >> (8 * j)) & 0xff) == 0) x[j] = 0.0f;
@@ -91,7 +139,7 @@ __device__ __forceinline__ void mask8(const uint8_t* sel, int64_t r0, int64_t n,
   }
 #pragma unroll
   for (int j = 0; j < 8; ++j)
-    if (r0 + j >= n || sel[r0 + j] == 0) x[j] = 0.0f;
+    if (r0 + j >= n || gptr<uint8_t>(sel)[r0 + j] == 0) x[j] = 0.0f;
 }
 
 // 32x32 MFMA accumulator (f32, 16 regs): element reg of lane -> (row, col)

@@ -46,6 +46,7 @@ struct PackSrcG {
   int pad;
 };
 int gram_cols_blocks(int d, int64_t n);
-void gram_cols(GramArgs a, const PackSrcG* srcs_dev, int blocks, double* out, hipStream_t st);
+// sdt: the common source dtype (DT_F32 / DT_F64 / DT_BF16, 16-byte aligned columns) or -1 (mixed)
+void gram_cols(GramArgs a, const PackSrcG* srcs_dev, int sdt, int blocks, double* out, hipStream_t st);
 
 }  // namespace dq4ml

@@ -387,7 +387,7 @@ __global__ __launch_bounds__((BF16Geom<NT, XMODE>::kBlock), 1) void gram_tall_bf
 // MFMAs for every tile pair.  Next superstep's global loads are in flight during the MFMAs;
 // double-buffered LDS, one barrier per superstep.  Partials use the bf16 kernel's slab layout.
 // =============================================================================================
-template <int NT>
+template <int NT, int SDT, int YDT>  // SDT: common source dtype (-1 mixed); YDT: label dtype (F32/F64)
 __global__ __launch_bounds__(256, (NT == 1 ? 3 : 2)) void gram_cols_kernel(GramArgs a, const PackSrcG* __restrict__ srcs) {
   constexpr int NPAIR = NT * (NT + 1) / 2;
   constexpr int FR = NT * 4 * 64 * 16;   // fragment bytes per superstep
@@ -411,45 +411,67 @@ __global__ __launch_bounds__(256, (NT == 1 ? 3 : 2)) void gram_cols_kernel(GramA
   for (int t = 0; t < NT; ++t) {
     const int feat = t * 32 + fl;
     fv[t] = feat < a.d;
-    src[t] = fv[t] ? srcs[feat] : PackSrcG{nullptr, 0, 0};
+    src[t] = srcs[fv[t] ? feat : 0];  // padding features load column 0 (branch-free) and stage zeros
   }
-  const int64_t nsup = (a.n + 63) / 64;
+  const int64_t nsup = (a.n + 63) / 64, nfull = a.n / 64;
   const int64_t s0 = (int64_t)blockIdx.x * a.spw;
   const int64_t s1 = s0 + a.spw < nsup ? s0 + a.spw : nsup;
+  const int64_t e1 = s1 < nfull ? s1 : nfull;  // full supersteps of this block: [s0, e1)
 
-  float x[NT][8];
-  auto gload = [&](int64_t s) {
+  // Everything a superstep needs is PREFETCHED into registers (features, selection bytes, the
+  // label of row tid for the 64 row-scalar threads) with branch-free typed loads, so the only
+  // vmcnt waits in the loop are the compiler's counted ones at first use — no scalar load in the
+  // loop can drain the prefetch.
+  struct Pref {
+    float x[NT][8];
+    uint64_t m;
+    double yv;
+    uint32_t live;
+  };
+  auto gload = [&](int64_t s, Pref& p) {
     const int64_t r0 = s * 64 + 8 * q;
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
-      if (fv[t]) {
-        load8_f32(src[t].ptr, src[t].dt, r0, a.n, x[t]);
-        mask8(a.sel, r0, a.n, x[t]);
-      } else {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) x[t][j] = 0.0f;
-      }
+      if constexpr (SDT >= 0) load8_typed<SDT, true>(src[t].ptr, r0, a.n, p.x[t]);
+      else load8_f32(src[t].ptr, src[t].dt, r0, a.n, p.x[t]);
     }
+    // branch-free: the host always passes a selection (all ones when there is none) and every
+    // wave loads the row scalars (only wave 0 uses them) so the compiler can count the loads
+    p.m = *gptr<uint64_t>(a.sel + r0);
+    const int64_t r = s * 64 + (tid & 63);
+    p.yv = YDT == DT_F64 ? gptr<double>(a.y)[r] : (double)gptr<float>(a.y)[r];
+    p.live = gptr<uint8_t>(a.sel)[r];
   };
-  auto stage = [&](int buf, int64_t s) {
-    unsigned char* base = smem + buf * BUF;
+  auto stage_w = [&](unsigned char* base, const RowVals& rv) {
+    __bf16* wl = reinterpret_cast<__bf16*>(base + FR);
+    const float w_hi = (float)(__bf16)(float)rv.w;
+    const __bf16 wy_hi = (__bf16)(float)rv.wy;
+    wl[0 * 64 + tid] = (__bf16)(float)rv.w;
+    wl[1 * 64 + tid] = (__bf16)(float)(rv.w - (double)w_hi);
+    wl[2 * 64 + tid] = wy_hi;
+    wl[3 * 64 + tid] = (__bf16)(float)(rv.wy - (double)(float)wy_hi);
+  };
+  auto stage_x = [&](unsigned char* base, float (&x)[NT][8], uint64_t m) {
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
       bf16x8 v;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = (__bf16)x[t][j];
+      for (int j = 0; j < 8; ++j) v[j] = (__bf16)(fv[t] && ((m >> (8 * j)) & 0xff) ? x[t][j] : 0.0f);
       *reinterpret_cast<u32x4*>(base + (((t * 4 + (q & 3)) * 64 + 32 * (q >> 2) + fl) << 4)) = __builtin_bit_cast(u32x4, v);
     }
+  };
+  auto stage = [&](int buf, Pref& p) {
+    unsigned char* base = smem + buf * BUF;
+    stage_x(base, p.x, p.m);
     if (tid < 64) {
-      const RowVals rv = row_vals(a, s * 64 + tid);
+      RowVals rv{p.live != 0, 0.0, 0.0, 0.0};
+      if (rv.live) {
+        rv.w = 1.0;
+        rv.y = p.yv;
+        rv.wy = p.yv;
+      }
       ra.add(rv);
-      __bf16* wl = reinterpret_cast<__bf16*>(base + FR);
-      const float w_hi = (float)(__bf16)(float)rv.w;
-      const __bf16 wy_hi = (__bf16)(float)rv.wy;
-      wl[0 * 64 + tid] = (__bf16)(float)rv.w;
-      wl[1 * 64 + tid] = (__bf16)(float)(rv.w - (double)w_hi);
-      wl[2 * 64 + tid] = wy_hi;
-      wl[3 * 64 + tid] = (__bf16)(float)(rv.wy - (double)(float)wy_hi);
+      stage_w(base, rv);
     }
   };
   auto compute = [&](int buf) {
@@ -469,13 +491,47 @@ __global__ __launch_bounds__(256, (NT == 1 ? 3 : 2)) void gram_cols_kernel(GramA
     for (int t = 0; t < NT; ++t) accw[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fr[t], wf, accw[t], 0, 0, 0);
   };
 
-  if (s0 < s1) gload(s0);
-  for (int64_t s = s0; s < s1; ++s) {
-    const int buf = (int)((s - s0) & 1);
-    stage(buf, s);
-    if (s + 1 < s1) gload(s + 1);
+  Pref pa, pb;
+  if (s0 < e1) gload(s0, pa);
+  if (s0 + 1 < e1) gload(s0 + 1, pb);
+  int64_t s = s0;
+  // unrolled by two so the register ring has static names; prefetches past the end re-load the
+  // last superstep (unconditional, so the compiler counts vmcnt instead of draining to 0)
+  for (; s + 1 < e1; s += 2) {
+    stage(0, pa);
+    gload(s + 2 < e1 ? s + 2 : e1 - 1, pa);
     __syncthreads();
-    compute(buf);
+    compute(0);
+    stage(1, pb);
+    gload(s + 3 < e1 ? s + 3 : e1 - 1, pb);
+    __syncthreads();
+    compute(1);
+  }
+  if (s < e1) {
+    stage(0, pa);
+    __syncthreads();
+    compute(0);
+    __syncthreads();
+  }
+  if (s1 > nfull && s0 <= nfull) {  // ragged last superstep: guarded loads (once in the grid)
+    const int64_t st = nfull, r0 = st * 64 + 8 * q;
+    float x[NT][8];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      if (fv[t]) load8_f32(src[t].ptr, src[t].dt, r0, a.n, x[t]);
+      else
+#pragma unroll
+        for (int j = 0; j < 8; ++j) x[t][j] = 0.0f;
+      mask8(a.sel, r0, a.n, x[t]);
+    }
+    stage_x(smem + BUF, x, ~0ull);
+    if (tid < 64) {
+      const RowVals rv = row_vals(a, st * 64 + tid);
+      ra.add(rv);
+      stage_w(smem + BUF, rv);
+    }
+    __syncthreads();
+    compute(1);
   }
 
   // ---- block reduction over the 4 waves (two tree rounds) + partial slab -----------------------
@@ -926,18 +982,34 @@ static size_t cols_lds(int NT) {
   return bufs > tree ? bufs : tree;
 }
 
+template <typename F>
+static void with_cols_kernel(int NT, int sdt, int ydt, F&& f) {
+#define DQ_COLS(NTV, YT)                                                 \
+  switch (sdt) {                                                         \
+    case DT_F32: return f(gram_cols_kernel<NTV, DT_F32, YT>);            \
+    case DT_F64: return f(gram_cols_kernel<NTV, DT_F64, YT>);            \
+    case DT_BF16: return f(gram_cols_kernel<NTV, DT_BF16, YT>);          \
+    default: return f(gram_cols_kernel<NTV, -1, YT>);                    \
+  }
+  if (ydt == DT_F64) {
+    if (NT == 1) { DQ_COLS(1, DT_F64) } else { DQ_COLS(2, DT_F64) }
+  }
+  if (NT == 1) { DQ_COLS(1, DT_F32) } else { DQ_COLS(2, DT_F32) }
+#undef DQ_COLS
+}
+
 int gram_cols_blocks(int d, int64_t n) {
   const int NT = (d + 31) / 32;
   int full = 1;
-  if (NT == 1) full = occupancy_blocks(gram_cols_kernel<1>, cols_lds(1), 256);
-  else full = occupancy_blocks(gram_cols_kernel<2>, cols_lds(2), 256);
+  with_cols_kernel(NT, DT_F32, DT_F64, [&](auto k) { full = occupancy_blocks(k, cols_lds(NT), 256); });
   const int64_t nsup = (n + 63) / 64;
   int64_t want = (nsup + 3) / 4;  // >= 4 supersteps per block
   if (want < 1) want = 1;
   return (int)(want < full ? want : full);
 }
 
-void gram_cols(GramArgs a, const PackSrcG* srcs_dev, int blocks, double* out, hipStream_t st) {
+void gram_cols(GramArgs a, const PackSrcG* srcs_dev, int sdt, int blocks, double* out, hipStream_t st) {
+  if (a.sel == nullptr) throw std::invalid_argument("gram_cols: pass an all-ones selection when there is none");
   if (a.d < 1 || a.d > 64) throw std::invalid_argument("gram_cols: d must be in [1, 64]");
   if (a.w != nullptr) throw std::invalid_argument("gram_cols: instance weights need the materialized path");
   if (blocks < 1) throw std::invalid_argument("gram_cols: blocks must be >= 1");
@@ -948,8 +1020,9 @@ void gram_cols(GramArgs a, const PackSrcG* srcs_dev, int blocks, double* out, hi
   a.P = (int)gram_partial_stride(GRAM_BF16, a.d);
   const int NT = (a.d + 31) / 32;
   const size_t lds = cols_lds(NT);
-  if (NT == 1) hipLaunchKernelGGL(gram_cols_kernel<1>, dim3(blocks), dim3(256), lds, st, a, srcs_dev);
-  else hipLaunchKernelGGL(gram_cols_kernel<2>, dim3(blocks), dim3(256), lds, st, a, srcs_dev);
+  if (a.ydt != DT_F64 && a.ydt != DT_F32) throw std::invalid_argument("gram_cols: label must be f32 or f64");
+  with_cols_kernel(NT, sdt, a.ydt,
+                   [&](auto k) { hipLaunchKernelGGL(k, dim3(blocks), dim3(256), lds, st, a, srcs_dev); });
   DQ_HIP_CHECK(hipGetLastError());
   hipLaunchKernelGGL(gram_reduce_kernel, dim3(reduce_blocks(a.d)), dim3(1024), 0, st, a.partials, blocks, a.P, a.d,
                      32, NT, out);

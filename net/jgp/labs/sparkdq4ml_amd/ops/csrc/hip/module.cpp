@@ -61,8 +61,8 @@ PYBIND11_MODULE(_dq4ml_hip, m) {
           gram_tall(mode, a, xmode, blocks, P<double>(out), as_stream(stream));
         });
   m.def("gram_cols_blocks", &gram_cols_blocks);
-  m.def("gram_cols", [](uintptr_t srcs, int d, int64_t n, uintptr_t y, int ydt, uintptr_t sel, uintptr_t partials,
-                        int blocks, uintptr_t out, uintptr_t stream) {
+  m.def("gram_cols", [](uintptr_t srcs, int sdt, int d, int64_t n, uintptr_t y, int ydt, uintptr_t sel,
+                        uintptr_t partials, int blocks, uintptr_t out, uintptr_t stream) {
     GramArgs a{};
     a.d = d;
     a.n = n;
@@ -71,7 +71,7 @@ PYBIND11_MODULE(_dq4ml_hip, m) {
     a.ydt = ydt;
     a.sel = P<const uint8_t>(sel);
     a.partials = P<double>(partials);
-    gram_cols(a, P<const PackSrcG>(srcs), blocks, P<double>(out), as_stream(stream));
+    gram_cols(a, P<const PackSrcG>(srcs), sdt, blocks, P<double>(out), as_stream(stream));
   });
   m.def("tiled_elems", &tiled_elems);
   m.def("tile_bf16", [](uintptr_t X, int xdt, int64_t ld, int d, int64_t n, uintptr_t out, uintptr_t stream) {

@@ -157,17 +157,31 @@ def gram_cols(parts: List[torch.Tensor], y, sel, blocks: Optional[int] = None):
         dtype_code(r)
     dev = rows[0].device
     y, _, sel = _prep_rows(y, None, sel, n)
+    if sel is None:  # the kernel's loads are branch-free: an all-ones selection
+        sel = _ones_sel(n, dev)
     desc = _srcw_desc(h, rows, dev)
     nb = int(blocks or _cols_blocks(h, d, n))
     P = int(h.gram_partial_stride(2, d))
     partials = torch.empty(nb * P, dtype=torch.float64, device=dev)
     out = torch.empty(5 + 2 * d + d * (d + 1) // 2, dtype=torch.float64, device=dev)
-    h.gram_cols(desc.data_ptr(), d, n, y.data_ptr(), dtype_code(y), _ptr(sel), partials.data_ptr(), nb,
+    codes = {dtype_code(r) for r in rows}
+    sdt = codes.pop() if len(codes) == 1 else -1
+    if sdt not in (0, 1, 2) or any(r.data_ptr() % 16 for r in rows):
+        sdt = -1  # mixed / unaligned columns: per-element typed loads
+    h.gram_cols(desc.data_ptr(), int(sdt), d, n, y.data_ptr(), dtype_code(y), _ptr(sel), partials.data_ptr(), nb,
                 out.data_ptr(), _stream())
     return out
 
 
 _cols_plan = {}
+_ones = {}
+
+
+def _ones_sel(n, dev):
+    t = _ones.get(dev)
+    if t is None or t.numel() < n:
+        t = _ones[dev] = torch.ones(max(n, 1 << 20) + 64, dtype=torch.bool, device=dev)
+    return t[:n]
 
 
 def _cols_blocks(h, d, n):
