@@ -107,6 +107,11 @@ class ColRef(Expr):
                 f"cannot resolve '`{self.name}`' given input columns: [{', '.join(schema.names)}]") from None
 
     def _resolve(self, schema):
+        if hasattr(schema, "resolve_ci"):
+            n = schema.resolve_ci(self.name)
+            if n is None:
+                raise KeyError(self.name)
+            return n
         names = schema.names
         if self.name in names:
             return self.name

@@ -157,8 +157,10 @@ class Filter(LogicalPlan):
 
 
 def _maybe_compact(t: Table, threshold: float = 0.25) -> Table:
-    """Keep the selection vector unless the live fraction got small (then compact)."""
-    if t.sel is None or t.nrows < 4096:
+    """Keep the selection vector unless the live fraction got small (then compact).  Device
+    tables keep it unconditionally: every device consumer (DQ VM, pack, Gram, metrics) reads the
+    selection natively, and deciding would cost a host sync per filter."""
+    if t.sel is None or t.nrows < 4096 or t.sel.is_cuda:
         return t
     live = int(t.sel.sum().item())
     return t.compact() if live < threshold * t.nrows else t

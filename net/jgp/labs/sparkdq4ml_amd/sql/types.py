@@ -132,25 +132,45 @@ class StructField:
 class StructType:
     def __init__(self, fields: Optional[List[StructField]] = None):
         self.fields: List[StructField] = list(fields or [])
+        self._index = None  # name -> field (first occurrence), built on demand
 
     def add(self, name, dataType, nullable=True, metadata=None):
         self.fields.append(StructField(name, dataType, nullable, metadata or {}))
+        self._index = None
         return self
+
+    def _idx(self):
+        if self._index is None or len(self._index[1]) != len(self.fields):
+            d = {}
+            for f in self.fields:
+                d.setdefault(f.name, f)
+            self._index = (d, [f.name for f in self.fields], {k.lower(): k for k in reversed(list(d))})
+        return self._index
 
     @property
     def names(self):
-        return [f.name for f in self.fields]
+        return list(self._idx()[1])
 
     def fieldNames(self):
         return self.names
 
+    def has(self, name) -> bool:
+        return name in self._idx()[0]
+
+    def resolve_ci(self, name):
+        """Exact name if present, else the case-insensitive match (first field), else None."""
+        d, _, lower = self._idx()
+        if name in d:
+            return name
+        return lower.get(name.lower())
+
     def __getitem__(self, key):
         if isinstance(key, int):
             return self.fields[key]
-        for f in self.fields:
-            if f.name == key:
-                return f
-        raise KeyError(key)
+        f = self._idx()[0].get(key)
+        if f is None:
+            raise KeyError(key)
+        return f
 
     def __iter__(self):
         return iter(self.fields)
