@@ -204,10 +204,13 @@ class LinearRegression(_LRParams):
             model._set_summary(LinearRegressionTrainingSummary(model, df, pending, None, stats=pending,
                                                                solver=pending))
             return model
+        # host bookkeeping first, while the Gram kernels run; the solve's D2H is the only sync
+        model = LinearRegressionModel(self.uid, None, 0.0)
+        self.copyValues(model)
         with tracing.span("solve"):
             wls, stats = fit_wls_flat(*args)
-        model = LinearRegressionModel(self.uid, DenseVector(wls.coefficients), float(wls.intercept))
-        self.copyValues(model)
+        model._coefficients = DenseVector(wls.coefficients)
+        model._intercept = float(wls.intercept)
         model._set_summary(LinearRegressionTrainingSummary(model, df, wls, wls.objectiveHistory,
                                                            stats=stats, solver=wls.solver))
         return model

@@ -586,6 +586,8 @@ def _gram_wide(h, T: TiledWide, y, w, sel, x_zero_dead):
     splitk = int(os.environ.get("DQ4ML_WIDE_SPLITK", "0")) or _wide_splitk(P, nsup, eb)
     # f32 MFMA accumulators count rows exactly only below 2^24 per split
     splitk = max(1, min(max(splitk, -(-nsup * 64 // (1 << 23))), nsup))
+    if os.environ.get("DQ4ML_WIDE_SAMEPAIR"):  # diagnostic only (wrong results): every block reads panels 0, 1
+        pairs = [(0, 1)] * len(pairs)
     pairs_dev = torch.tensor(np.asarray(pairs, dtype=np.int32).reshape(-1), device=dev)
     part = torch.empty(int(h.gram_wide_partials(d, splitk)), dtype=torch.float32, device=dev)
     out = torch.empty(5 + 2 * d + d * (d + 1) // 2, dtype=torch.float64, device=dev)

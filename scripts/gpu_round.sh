@@ -34,6 +34,7 @@ for s in $STEPS; do
     prof5) step prof5 600 env WHICH=cfg5 python scripts/step_profile.py ;;
     kprof4) (export TMPDIR=/tmp; step kprof4 600 rocprofv3 --kernel-trace --stats -d gpurun_out/kprof4 -o run --output-format csv -- python benchmarks/bench_dq_pipeline.py --steps 2 --warmup 1) || exit $? ;;
     kprof5) (export TMPDIR=/tmp; step kprof5 600 rocprofv3 --kernel-trace --stats -d gpurun_out/kprof5 -o run --output-format csv -- python benchmarks/bench_wide.py --steps 1 --warmup 1) || exit $? ;;
+    kprofasync) (export TMPDIR=/tmp; step kprofasync 600 rocprofv3 --kernel-trace --stats -d gpurun_out/kprofasync -o run --output-format csv -- python bench.py --steps 50 --warmup 5 --rows 1.25e7 --async) || exit $? ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" ;;
     bench) step bench 600 python bench.py --steps 20 --warmup 3 ;;
     benchasync) step benchasync 600 python bench.py --steps 20 --warmup 3 --async ;;

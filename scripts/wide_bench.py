@@ -40,7 +40,14 @@ res = {v: [] for v in variants}
 outs = {}
 for _ in range(reps):
     for v in variants:
-        ring, order, waves, splitk = (v.split(":") + ["4", "0"][len(v.split(":")) - 2:])[:4]
+        fields = v.split(":")
+        same = fields[-1] == "same"
+        if same:
+            fields = fields[:-1]
+        os.environ.pop("DQ4ML_WIDE_SAMEPAIR", None)
+        if same:
+            os.environ["DQ4ML_WIDE_SAMEPAIR"] = "1"
+        ring, order, waves, splitk = (fields + ["4", "0"][len(fields) - 2:])[:4]
         os.environ["DQ4ML_WIDE_RING"], os.environ["DQ4ML_WIDE_ORDER"] = ring, order
         os.environ["DQ4ML_WIDE_WAVES"], os.environ["DQ4ML_WIDE_SPLITK"] = waves, splitk
         if v not in outs:  # warm-up + result
