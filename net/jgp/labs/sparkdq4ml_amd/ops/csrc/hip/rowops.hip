@@ -253,68 +253,79 @@ __global__ __launch_bounds__(256) void metrics_kernel(const void* __restrict__ X
 
 // ---- predict / metrics over the MFMA-fragment layouts (tiled codes 1 tall bf16, 2 wide bf16,
 // 3 wide fp8): block-iteration = one superstep (64 rows).  Thread (f, q) walks the tiles reading
-// its 16-B (8-B fp8) fragment = rows [8q, 8q+8) of feature t*32 + f in every layout, accumulates
-// coef * x for those 8 rows, and the 32 feature-threads of each row group are summed through LDS
-// — fragment-coalesced loads instead of per-row 2-byte gathers.
-template <int MODE>  // 0: predictions -> out, 1: the 8 metric sums -> partials
+// its 16-B (8-B fp8) fragment = rows [8q, 8q+8) of feature t*32 + f in every layout and
+// accumulates coef * x (f64) for those 8 rows.  The 8 feature-threads of a wave fold with
+// shuffles, the 4 waves through a double-buffered 2 KiB LDS slab (one barrier per superstep),
+// and the next superstep's fragments are loaded before that barrier.
+__device__ __forceinline__ void frag8(const unsigned char* X, int tiled, int64_t ch, int q, int fl, float x[8]) {
+  if (tiled == 3) {
+    const int ki = q >> 1, lane = 32 * (q & 1) + fl;
+    const uint64_t v = *gptr<uint64_t>(X + ch * 2048 + (((ki >> 1) * 64 + lane) << 4) + ((ki & 1) << 3));
+    const int lo = (int)(uint32_t)v, hi = (int)(uint32_t)(v >> 32);
+    x[0] = __builtin_amdgcn_cvt_f32_fp8(lo, 0);
+    x[1] = __builtin_amdgcn_cvt_f32_fp8(lo, 1);
+    x[2] = __builtin_amdgcn_cvt_f32_fp8(lo, 2);
+    x[3] = __builtin_amdgcn_cvt_f32_fp8(lo, 3);
+    x[4] = __builtin_amdgcn_cvt_f32_fp8(hi, 0);
+    x[5] = __builtin_amdgcn_cvt_f32_fp8(hi, 1);
+    x[6] = __builtin_amdgcn_cvt_f32_fp8(hi, 2);
+    x[7] = __builtin_amdgcn_cvt_f32_fp8(hi, 3);
+    return;
+  }
+  const int64_t unit = tiled == 1 ? ch * 256 + (q & 3) * 64 + (q >> 2) * 32 + fl
+                                  : ch * 256 + (q >> 1) * 64 + 32 * (q & 1) + fl;
+  const u32x4 v = gptr<u32x4>(X)[unit];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    x[2 * j] = __uint_as_float(v[j] << 16);
+    x[2 * j + 1] = __uint_as_float(v[j] & 0xffff0000u);
+  }
+}
+
+template <int MODE, int YDT>  // MODE 0: predictions -> out, 1: the 8 metric sums -> partials
 __global__ __launch_bounds__(256) void tiled_rows_kernel(const unsigned char* __restrict__ X, int tiled, int d,
                                                         int64_t n, const double* __restrict__ coef, double b,
                                                         const void* __restrict__ y, int ydt,
                                                         const uint8_t* __restrict__ sel, double shift,
                                                         double* __restrict__ out) {
-  __shared__ double part[32][65];
-  __shared__ double red[4][8];
-  const int fl = threadIdx.x >> 3, q = threadIdx.x & 7;
+  __shared__ double part[2][4][64];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int fl = tid >> 3, q = tid & 7;
   const int NT = tiled == 1 ? (d + 31) >> 5 : ((d + 255) >> 8) * 8;
   const int ntiles = (d + 31) >> 5;
   const int64_t nsup = (n + 63) >> 6;
   double m[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  int buf = 0;
   for (int64_t s = blockIdx.x; s < nsup; s += gridDim.x) {
     double acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     for (int t = 0; t < ntiles; ++t) {
       const int f = t * 32 + fl;
-      if (f >= d) break;
-      const double c = coef[f];
-      const int64_t ch = s * NT + t;
       float x[8];
-      if (tiled == 3) {
-        const int ki = q >> 1, lane = 32 * (q & 1) + fl;
-        const uint64_t v = *reinterpret_cast<const uint64_t*>(X + ch * 2048 + (((ki >> 1) * 64 + lane) << 4) +
-                                                              ((ki & 1) << 3));
-        const int lo = (int)(uint32_t)v, hi = (int)(uint32_t)(v >> 32);
-        x[0] = __builtin_amdgcn_cvt_f32_fp8(lo, 0);
-        x[1] = __builtin_amdgcn_cvt_f32_fp8(lo, 1);
-        x[2] = __builtin_amdgcn_cvt_f32_fp8(lo, 2);
-        x[3] = __builtin_amdgcn_cvt_f32_fp8(lo, 3);
-        x[4] = __builtin_amdgcn_cvt_f32_fp8(hi, 0);
-        x[5] = __builtin_amdgcn_cvt_f32_fp8(hi, 1);
-        x[6] = __builtin_amdgcn_cvt_f32_fp8(hi, 2);
-        x[7] = __builtin_amdgcn_cvt_f32_fp8(hi, 3);
-      } else {
-        const int64_t unit = tiled == 1 ? ch * 256 + (q & 3) * 64 + (q >> 2) * 32 + fl
-                                        : ch * 256 + (q >> 1) * 64 + 32 * (q & 1) + fl;
-        const u32x4 v = reinterpret_cast<const u32x4*>(X)[unit];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          x[2 * j] = __uint_as_float(v[j] << 16);
-          x[2 * j + 1] = __uint_as_float(v[j] & 0xffff0000u);
-        }
-      }
+      frag8(X, tiled, s * NT + t, q, fl, x);
+      const double c = f < d ? coef[f] : 0.0;
 #pragma unroll
       for (int j = 0; j < 8; ++j) acc[j] += c * (double)x[j];
     }
 #pragma unroll
-    for (int j = 0; j < 8; ++j) part[fl][q * 8 + j] = acc[j];
+    for (int j = 0; j < 8; ++j) {  // fold the wave's 8 feature-threads (lane bits 3..5)
+      acc[j] += __shfl_xor(acc[j], 8, 64);
+      acc[j] += __shfl_xor(acc[j], 16, 64);
+      acc[j] += __shfl_xor(acc[j], 32, 64);
+    }
+    if (lane < 8) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) part[buf][wave][lane * 8 + j] = acc[j];
+    }
     __syncthreads();
-    if (threadIdx.x < 64) {
-      const int64_t r = s * 64 + threadIdx.x;
-      double p = b;
-      for (int k = 0; k < 32; ++k) p += part[k][threadIdx.x];
+    if (tid < 64) {
+      const int64_t r = s * 64 + tid;
+      const double p = b + part[buf][0][tid] + part[buf][1][tid] + part[buf][2][tid] + part[buf][3][tid];
       if (r < n) {
         if (MODE == 0) {
           out[r] = p;
         } else if (sel == nullptr || sel[r] != 0) {
-          const double yy = ld_f64(y, ydt, r);
+          const double yy = YDT == DT_F64 ? gptr<double>(y)[r] : YDT == DT_F32 ? (double)gptr<float>(y)[r]
+                                                                               : ld_f64(y, ydt, r);
           const double ys = yy - shift, ps = p - shift, res = yy - p;
           m[0] += 1.0;
           m[1] += ys;
@@ -327,12 +338,12 @@ __global__ __launch_bounds__(256) void tiled_rows_kernel(const unsigned char* __
         }
       }
     }
-    __syncthreads();
+    buf ^= 1;  // the other slab is free: its readers passed this superstep's barrier
   }
-  if (MODE == 1) {
+  if (MODE == 1) {  // only wave 0 accumulated metrics
 #pragma unroll
     for (int k = 0; k < 8; ++k) m[k] = wave_sum_f64(m[k]);
-    if (threadIdx.x == 0) {
+    if (tid == 0) {
 #pragma unroll
       for (int k = 0; k < 8; ++k) out[(int64_t)blockIdx.x * 8 + k] = m[k];
     }
@@ -397,7 +408,7 @@ void predict(const void* X, int xdt, int64_t ld, int d, int64_t n, const double*
   if (tiled) {
     int64_t g = (n + 63) / 64;
     if (g > 8192) g = 8192;
-    hipLaunchKernelGGL(tiled_rows_kernel<0>, dim3(g), dim3(256), 0, st, reinterpret_cast<const unsigned char*>(X),
+    hipLaunchKernelGGL((tiled_rows_kernel<0, DT_F64>), dim3(g), dim3(256), 0, st, reinterpret_cast<const unsigned char*>(X),
                        tiled, d, n, coef, b, nullptr, 0, nullptr, 0.0, out);
     DQ_HIP_CHECK(hipGetLastError());
     return;
@@ -420,8 +431,17 @@ void regression_metrics(const void* X, int xdt, int64_t ld, int d, int64_t n, co
                         double* out, hipStream_t st, int tiled) {
   const int g = metrics_blocks(n);
   if (tiled)
-    hipLaunchKernelGGL(tiled_rows_kernel<1>, dim3(g), dim3(256), 0, st, reinterpret_cast<const unsigned char*>(X),
-                       tiled, d, n, coef, b, y, ydt, sel, shift, partials);
+  {
+    if (ydt == DT_F64)
+      hipLaunchKernelGGL((tiled_rows_kernel<1, DT_F64>), dim3(g), dim3(256), 0, st,
+                         reinterpret_cast<const unsigned char*>(X), tiled, d, n, coef, b, y, ydt, sel, shift, partials);
+    else if (ydt == DT_F32)
+      hipLaunchKernelGGL((tiled_rows_kernel<1, DT_F32>), dim3(g), dim3(256), 0, st,
+                         reinterpret_cast<const unsigned char*>(X), tiled, d, n, coef, b, y, ydt, sel, shift, partials);
+    else
+      hipLaunchKernelGGL((tiled_rows_kernel<1, -1>), dim3(g), dim3(256), 0, st,
+                         reinterpret_cast<const unsigned char*>(X), tiled, d, n, coef, b, y, ydt, sel, shift, partials);
+  }
   else
     hipLaunchKernelGGL(metrics_kernel, dim3(g), dim3(256), 0, st, X, xdt, ld, d, n, y, ydt, sel, coef, b, shift,
                        partials, tiled);
