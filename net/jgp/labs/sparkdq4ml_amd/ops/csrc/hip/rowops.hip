@@ -257,8 +257,9 @@ __global__ __launch_bounds__(256) void metrics_kernel(const void* __restrict__ X
 // accumulates coef * x (f64) for those 8 rows.  The 8 feature-threads of a wave fold with
 // shuffles, the 4 waves through a double-buffered 2 KiB LDS slab (one barrier per superstep),
 // and the next superstep's fragments are loaded before that barrier.
-__device__ __forceinline__ void frag8(const unsigned char* X, int tiled, int64_t ch, int q, int fl, float x[8]) {
-  if (tiled == 3) {
+template <int TILED>
+__device__ __forceinline__ void frag8(const unsigned char* X, int64_t ch, int q, int fl, float x[8]) {
+  if constexpr (TILED == 3) {
     const int ki = q >> 1, lane = 32 * (q & 1) + fl;
     const uint64_t v = *gptr<uint64_t>(X + ch * 2048 + (((ki >> 1) * 64 + lane) << 4) + ((ki & 1) << 3));
     const int lo = (int)(uint32_t)v, hi = (int)(uint32_t)(v >> 32);
@@ -272,7 +273,7 @@ __device__ __forceinline__ void frag8(const unsigned char* X, int tiled, int64_t
     x[7] = __builtin_amdgcn_cvt_f32_fp8(hi, 3);
     return;
   }
-  const int64_t unit = tiled == 1 ? ch * 256 + (q & 3) * 64 + (q >> 2) * 32 + fl
+  const int64_t unit = TILED == 1 ? ch * 256 + (q & 3) * 64 + (q >> 2) * 32 + fl
                                   : ch * 256 + (q >> 1) * 64 + 32 * (q & 1) + fl;
   const u32x4 v = gptr<u32x4>(X)[unit];
 #pragma unroll
@@ -282,40 +283,64 @@ __device__ __forceinline__ void frag8(const unsigned char* X, int tiled, int64_t
   }
 }
 
-template <int MODE, int YDT>  // MODE 0: predictions -> out, 1: the 8 metric sums -> partials
+template <int MODE, int YDT, int TILED>  // MODE 0: predictions -> out, 1: the 8 metric sums -> partials
 __global__ __launch_bounds__(256) void tiled_rows_kernel(const unsigned char* __restrict__ X, int tiled, int d,
                                                         int64_t n, const double* __restrict__ coef, double b,
                                                         const void* __restrict__ y, int ydt,
                                                         const uint8_t* __restrict__ sel, double shift,
                                                         double* __restrict__ out) {
   __shared__ double part[2][4][64];
+  __shared__ double wpart[4][8][65];  // per wave: [feature-thread][row] (+1 pad)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int fl = tid >> 3, q = tid & 7;
-  const int NT = tiled == 1 ? (d + 31) >> 5 : ((d + 255) >> 8) * 8;
+  const int NT = TILED == 1 ? (d + 31) >> 5 : ((d + 255) >> 8) * 8;
+  // tall layouts (<= 2 tiles): the thread's coefficients live in registers
+  double c2[2] = {fl < d ? coef[fl] : 0.0, 32 + fl < d ? coef[32 + fl] : 0.0};
   const int ntiles = (d + 31) >> 5;
   const int64_t nsup = (n + 63) >> 6;
   double m[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   int buf = 0;
   for (int64_t s = blockIdx.x; s < nsup; s += gridDim.x) {
+    // the row scalars are requested together with the fragments: one memory round trip per superstep
+    double yy = 0.0;
+    bool live = false;
+    const int64_t rr = s * 64 + tid;
+    if (MODE == 1 && tid < 64 && rr < n) {
+      live = sel == nullptr || gptr<uint8_t>(sel)[rr] != 0;
+      yy = YDT == DT_F64 ? gptr<double>(y)[rr] : YDT == DT_F32 ? (double)gptr<float>(y)[rr] : ld_f64(y, ydt, rr);
+    }
     double acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    for (int t = 0; t < ntiles; ++t) {
-      const int f = t * 32 + fl;
-      float x[8];
-      frag8(X, tiled, s * NT + t, q, fl, x);
-      const double c = f < d ? coef[f] : 0.0;
+    if constexpr (TILED == 1) {  // tall: <= 2 tiles, both fragments requested before use
+      float x0[8], x1[8];
+      frag8<1>(X, s * NT, q, fl, x0);
+      if (ntiles > 1) frag8<1>(X, s * NT + 1, q, fl, x1);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) acc[j] += c * (double)x[j];
-    }
+      for (int j = 0; j < 8; ++j) acc[j] = c2[0] * (double)x0[j];
+      if (ntiles > 1) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {  // fold the wave's 8 feature-threads (lane bits 3..5)
-      acc[j] += __shfl_xor(acc[j], 8, 64);
-      acc[j] += __shfl_xor(acc[j], 16, 64);
-      acc[j] += __shfl_xor(acc[j], 32, 64);
-    }
-    if (lane < 8) {
+        for (int j = 0; j < 8; ++j) acc[j] += c2[1] * (double)x1[j];
+      }
+    } else {
+      for (int t = 0; t < ntiles; ++t) {
+        const int f = t * 32 + fl;
+        float x[8];
+        frag8<TILED>(X, s * NT + t, q, fl, x);
+        const double c = f < d ? coef[f] : 0.0;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) part[buf][wave][lane * 8 + j] = acc[j];
+        for (int j = 0; j < 8; ++j) acc[j] += c * (double)x[j];
+      }
     }
+    // fold the wave's 8 feature-threads through a per-wave LDS transpose (no cross-wave sync)
+    const int fw = lane >> 3;  // feature-thread within the wave
+#pragma unroll
+    for (int j = 0; j < 8; ++j) wpart[wave][fw][q * 8 + j] = acc[j];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    double rowp = 0.0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) rowp += wpart[wave][k][lane];
+    part[buf][wave][lane] = rowp;
     __syncthreads();
     if (tid < 64) {
       const int64_t r = s * 64 + tid;
@@ -323,9 +348,7 @@ __global__ __launch_bounds__(256) void tiled_rows_kernel(const unsigned char* __
       if (r < n) {
         if (MODE == 0) {
           out[r] = p;
-        } else if (sel == nullptr || sel[r] != 0) {
-          const double yy = YDT == DT_F64 ? gptr<double>(y)[r] : YDT == DT_F32 ? (double)gptr<float>(y)[r]
-                                                                               : ld_f64(y, ydt, r);
+        } else if (live) {
           const double ys = yy - shift, ps = p - shift, res = yy - p;
           m[0] += 1.0;
           m[1] += ys;
@@ -350,12 +373,19 @@ __global__ __launch_bounds__(256) void tiled_rows_kernel(const unsigned char* __
   }
 }
 
-__global__ __launch_bounds__(64) void sum_slabs_kernel(const double* __restrict__ partials, int nslab, int width,
-                                                      double* __restrict__ out) {
-  for (int k = threadIdx.x; k < width; k += blockDim.x) {
+__global__ __launch_bounds__(256) void sum_slabs_kernel(const double* __restrict__ partials, int nslab, int width,
+                                                       double* __restrict__ out) {
+  // fixed-order (deterministic) block reduction of nslab x width slabs: strided per-thread sums,
+  // wave shuffles, then 4 wave totals
+  __shared__ double wsum[4];
+  for (int k = 0; k < width; ++k) {
     double s = 0.0;
-    for (int b = 0; b < nslab; ++b) s += partials[(int64_t)b * width + k];
-    out[k] = s;
+    for (int b = threadIdx.x; b < nslab; b += blockDim.x) s += partials[(int64_t)b * width + k];
+    s = wave_sum_f64(s);
+    if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) out[k] = (wsum[0] + wsum[1]) + (wsum[2] + wsum[3]);
+    __syncthreads();
   }
 }
 
@@ -408,8 +438,10 @@ void predict(const void* X, int xdt, int64_t ld, int d, int64_t n, const double*
   if (tiled) {
     int64_t g = (n + 63) / 64;
     if (g > 8192) g = 8192;
-    hipLaunchKernelGGL((tiled_rows_kernel<0, DT_F64>), dim3(g), dim3(256), 0, st, reinterpret_cast<const unsigned char*>(X),
-                       tiled, d, n, coef, b, nullptr, 0, nullptr, 0.0, out);
+    auto xb = reinterpret_cast<const unsigned char*>(X);
+    if (tiled == 1) hipLaunchKernelGGL((tiled_rows_kernel<0, DT_F64, 1>), dim3(g), dim3(256), 0, st, xb, tiled, d, n, coef, b, nullptr, 0, nullptr, 0.0, out);
+    else if (tiled == 2) hipLaunchKernelGGL((tiled_rows_kernel<0, DT_F64, 2>), dim3(g), dim3(256), 0, st, xb, tiled, d, n, coef, b, nullptr, 0, nullptr, 0.0, out);
+    else hipLaunchKernelGGL((tiled_rows_kernel<0, DT_F64, 3>), dim3(g), dim3(256), 0, st, xb, tiled, d, n, coef, b, nullptr, 0, nullptr, 0.0, out);
     DQ_HIP_CHECK(hipGetLastError());
     return;
   }
@@ -421,7 +453,7 @@ void predict(const void* X, int xdt, int64_t ld, int d, int64_t n, const double*
 
 int metrics_blocks(int64_t n) {
   int64_t g = (n + 255) / 256;
-  if (g > 1024) g = 1024;
+  if (g > 4096) g = 4096;  // enough resident blocks to keep fragment loads in flight
   if (g < 1) g = 1;
   return (int)g;
 }
@@ -432,20 +464,21 @@ void regression_metrics(const void* X, int xdt, int64_t ld, int d, int64_t n, co
   const int g = metrics_blocks(n);
   if (tiled)
   {
-    if (ydt == DT_F64)
-      hipLaunchKernelGGL((tiled_rows_kernel<1, DT_F64>), dim3(g), dim3(256), 0, st,
-                         reinterpret_cast<const unsigned char*>(X), tiled, d, n, coef, b, y, ydt, sel, shift, partials);
-    else if (ydt == DT_F32)
-      hipLaunchKernelGGL((tiled_rows_kernel<1, DT_F32>), dim3(g), dim3(256), 0, st,
-                         reinterpret_cast<const unsigned char*>(X), tiled, d, n, coef, b, y, ydt, sel, shift, partials);
-    else
-      hipLaunchKernelGGL((tiled_rows_kernel<1, -1>), dim3(g), dim3(256), 0, st,
-                         reinterpret_cast<const unsigned char*>(X), tiled, d, n, coef, b, y, ydt, sel, shift, partials);
-  }
-  else
+    auto xb = reinterpret_cast<const unsigned char*>(X);
+#define DQ_TR(YT, TC)                                                                                      \
+  hipLaunchKernelGGL((tiled_rows_kernel<1, YT, TC>), dim3(g), dim3(256), 0, st, xb, tiled, d, n, coef, b, y, ydt, \
+                     sel, shift, partials)
+#define DQ_TRY(TC)                      \
+  if (ydt == DT_F64) DQ_TR(DT_F64, TC); \
+  else if (ydt == DT_F32) DQ_TR(DT_F32, TC); \
+  else DQ_TR(-1, TC);
+    if (tiled == 1) { DQ_TRY(1) } else if (tiled == 2) { DQ_TRY(2) } else { DQ_TRY(3) }
+#undef DQ_TRY
+#undef DQ_TR
+  }  else
     hipLaunchKernelGGL(metrics_kernel, dim3(g), dim3(256), 0, st, X, xdt, ld, d, n, y, ydt, sel, coef, b, shift,
                        partials, tiled);
-  hipLaunchKernelGGL(sum_slabs_kernel, dim3(1), dim3(64), 0, st, partials, g, 8, out);
+  hipLaunchKernelGGL(sum_slabs_kernel, dim3(1), dim3(256), 0, st, partials, g, 8, out);
   DQ_HIP_CHECK(hipGetLastError());
 }
 
@@ -531,7 +564,7 @@ void huber_pass(const void* X, int xdt, int64_t ld, int d, int64_t n, int tiled,
   const int g = metrics_blocks(n);
   hipLaunchKernelGGL(huber_rows_kernel, dim3(g), dim3(256), 0, st, X, xdt, ld, d, n, tiled, y, ydt, w, wdt, sel, ceff,
                      icpt, sigma, eps, mult, partials);
-  hipLaunchKernelGGL(sum_slabs_kernel, dim3(1), dim3(64), 0, st, partials, g, 4, out);
+  hipLaunchKernelGGL(sum_slabs_kernel, dim3(1), dim3(256), 0, st, partials, g, 4, out);
   hipLaunchKernelGGL(xt_vec_kernel, dim3(d), dim3(256), 0, st, X, xdt, ld, d, n, tiled, mult, out + 4);
   DQ_HIP_CHECK(hipGetLastError());
 }
