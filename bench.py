@@ -35,8 +35,11 @@ def _args(argv=None):
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32", "fp64"])
     ap.add_argument("--scaling", default="strong", choices=["strong", "weak"])
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--sync", dest="use_async", action="store_false",
+                    help="synchronous fits (host WLS solve after a D2H of the statistics, every step)")
     ap.add_argument("--async", dest="use_async", action="store_true",
-                    help="asynchronous fits (device WLS solve, no host wait per step)")
+                    help="asynchronous fits (device WLS solve, no host wait per step; the default)")
+    ap.set_defaults(use_async=True)
     return ap.parse_args(argv)
 
 
@@ -51,9 +54,11 @@ def main(argv=None):
     rank, world = comm.rank(), comm.world_size()
     if world != a.gpus and rank == 0:
         print(f"[bench] warning: --gpus {a.gpus} but WORLD_SIZE={world}", file=sys.stderr)
-    # --async: gram -> RCCL all-reduce -> device Cholesky enqueued back to back, the host never
-    # waits inside a step (measured no faster at d = 32: the one-workgroup solve costs what the
-    # host round trip does), so the default is the synchronous, Spark-faithful fit
+    # async (default): gram -> RCCL all-reduce -> device WLS solve (wls_small.hip) enqueued back
+    # to back, the host never waits inside a step; every fit's solve still runs inside the timed
+    # region (the closing synchronize), the model's coefficients materialize on first read.
+    # --sync: D2H of the statistics + host solve every step (Spark's driver-side solve).
+    # 1x MI355X, d = 32: 1e8 rows 1.043 (async) vs 1.075 (sync) ms; 1.25e7 rows 0.166 vs 0.201 ms.
     spark = SparkSession.builder().appName("bench").master("local[*]") \
         .config("dq4ml.fit.async", "true" if a.use_async else "false").getOrCreate()
     dev = spark.device
@@ -118,7 +123,7 @@ def main(argv=None):
             "config": {"model": f"LinearRegression(normal equations) d={d}", "global_batch": global_rows,
                        "seq_len": d, "parallelism": f"dp{world}", "rows_per_gpu": n,
                        "device": str(dev), "coef_max_abs_err": err,
-                       "fit_mode": "async" if a.use_async else "sync"},
+                       "fit_mode": "async" if (a.use_async and on_gpu) else "sync"},
         }
         s = json.dumps(line)
         print(s, flush=True)

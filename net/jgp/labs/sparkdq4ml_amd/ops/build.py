@@ -88,18 +88,43 @@ def _torch_lib():
     return os.path.join(os.path.dirname(torch.__file__), "lib")
 
 
+def _obj_stale(obj, src, headers):
+    if not os.path.exists(obj):
+        return True
+    t = os.path.getmtime(obj)
+    return any(os.path.getmtime(s) > t for s in [src, *headers])
+
+
 def build_hip(force: bool = False) -> str:
+    """One object per translation unit under ``ops/.obj/`` (compiled in parallel, only the stale
+    ones: a kernel edit recompiles one file, not the module), then one link."""
     srcs = _sources("hip", [".hip", ".cpp"])
+    headers = glob.glob(os.path.join(CSRC, "hip", "*.h"))
+    objdir = os.path.join(HERE, ".obj")
     with _Lock("hip"):
         if force or _stale(HIP_SO, srcs):
-            tmp = HIP_SO + f".tmp{os.getpid()}"
+            from concurrent.futures import ThreadPoolExecutor
+
+            os.makedirs(objdir, exist_ok=True)
             hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
             tl = _torch_lib()
-            cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-                   "-fvisibility=hidden", "-munsafe-fp-atomics", *_py_includes(),
-                   f"-I{os.path.join(CSRC, 'hip')}", *srcs,
-                   f"-L{tl}", "-lamdhip64", "-lhiprtc", f"-Wl,-rpath,{tl}", "-o", tmp]
-            _run(cmd)
+            flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-fvisibility=hidden",
+                     "-munsafe-fp-atomics", *_py_includes(), f"-I{os.path.join(CSRC, 'hip')}"]
+            objs = [os.path.join(objdir, os.path.basename(s) + ".o") for s in srcs]
+            todo = [(s, o) for s, o in zip(srcs, objs) if force or _obj_stale(o, s, headers)]
+
+            def cc(so):
+                s, o = so
+                tmp = o + f".tmp{os.getpid()}"
+                _run([hipcc, *flags, "-c", s, "-o", tmp])
+                os.replace(tmp, o)
+
+            jobs = max(1, min(len(todo), int(os.environ.get("MAX_JOBS", os.cpu_count() or 4)), 16))
+            with ThreadPoolExecutor(jobs) as ex:
+                list(ex.map(cc, todo))
+            tmp = HIP_SO + f".tmp{os.getpid()}"
+            _run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs,
+                  f"-L{tl}", "-lamdhip64", "-lhiprtc", f"-Wl,-rpath,{tl}", "-o", tmp])
             os.replace(tmp, HIP_SO)
     return HIP_SO
 

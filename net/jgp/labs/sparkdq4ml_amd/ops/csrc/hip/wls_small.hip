@@ -2,9 +2,28 @@
 // workgroup, on the device, straight from the all-reduced flat statistics — so a normal-equation
 // fit enqueues gram -> all-reduce -> solve with no host round trip (asynchronous fits).  Same
 // algebra as csrc/host/wls.cpp (standardize with population std, L2 on the standardized diagonal,
-// intercept column [aBar, 1], Cholesky, un-standardize); anything but the plain SPD case is
-// flagged in the status word and re-solved by the host driver (constant label, empty data,
-// non-positive pivot).
+// intercept column [aBar, 1], solve, un-standardize); anything but the plain SPD case is flagged
+// in the status word and re-solved by the host driver (constant label, empty data, non-positive
+// pivot).
+//
+// Latency design.  The solve sits on the critical path of every small-shard fit, and with one
+// wave per SIMD nothing hides latency: the cost is the instruction count per elimination step
+// times the dependent-issue latency.  So:
+//  * Gauss-Jordan on the full system [A | b] (no back substitution: x_r = b_r / D_r at the end,
+//    fully parallel).  Without pivoting it meets the same pivots as LDLᵀ / Cholesky; a pivot
+//    <= 0 = not SPD, the case in which dppsv fails too.
+//  * 256 threads; thread t OWNS elements e = t + 256 i of the (k x (k+1)) system and keeps them in
+//    registers for the whole solve; the slot count is a template parameter sized for the actual k.
+//  * ONE barrier per step and no branches in it: two parity copies of the system in LDS; step c
+//    reads the pivot, column c and row c of parity c & 1 and every slot writes its new value to
+//    the other parity (distinct addresses, coalesced).  The matrix stores 0 on its diagonal (the
+//    diagonal lives in a separate vector per parity), which makes the pivot row's update a no-op
+//    without a select.  Dead columns (< c) are not zeroed, so only each step's pivot is kept.
+//  History (k = 33): unrolled per-lane register rows + v_readlane: ~19k straight-line
+//  instructions, I-cache bound, 51 us; LDS read-modify-write LDLᵀ + back substitution: 34 us;
+//  register-owned LDLᵀ sized for k = 65 (9 slots / thread whatever k): 31 us; Gauss-Jordan with
+//  exec-masked publication of the next column / row: 29 us (every skipped masked store is a taken
+//  s_cbranch_execz).
 #include <hip/hip_runtime.h>
 
 #include "common.h"
@@ -15,21 +34,59 @@ namespace dq4ml {
 namespace {
 
 constexpr int kMaxK = kWlsSmallMaxFeatures + 1;
+constexpr int kThreads = 256;
+
+// scripts/wls_probe.hip builds this file with DQ4ML_WLS_PROBE: per-phase s_memtime stamps
+#ifdef DQ4ML_WLS_PROBE
+__device__ long long* g_wls_probe;
+#define WLS_STAMP(i) \
+  if (threadIdx.x == 0) g_wls_probe[i] = (long long)__builtin_amdgcn_s_memtime()
+#else
+#define WLS_STAMP(i)
+#endif
 
 __device__ __forceinline__ int64_t pku(int i, int j) { return i + (int64_t)j * (j + 1) / 2; }
 
-__global__ __launch_bounds__(64) void wls_small_kernel(const double* __restrict__ flat, int nf, int fit_intercept,
-                                                       double reg, double enet, int std_f, int std_l,
-                                                       double* __restrict__ out) {
-  __shared__ double A[kMaxK * kMaxK];
-  __shared__ double b[kMaxK], x[kMaxK], aStd[kMaxK], aBar[kMaxK];
+template <int KMAX>
+__global__ __launch_bounds__(kThreads) void wls_gj_kernel(const double* __restrict__ flat, int nf, int fit_intercept,
+                                                         double reg, double enet, int std_f, int std_l,
+                                                         double* __restrict__ out) {
+  constexpr int kW = KMAX + 1;                                 // row width incl. the RHS column
+  constexpr int kPer = (KMAX * kW + kThreads - 1) / kThreads;  // owned slots per thread
+  constexpr int kBuf = KMAX * kW + KMAX + kThreads;            // [matrix | diagonal | trash] per parity
+  __shared__ double M[2 * kBuf];
+  __shared__ double aStd[KMAX], aBar[KMAX], iStd[KMAX], pivots[KMAX];
   __shared__ int bad;
+  WLS_STAMP(0);
   const int t = threadIdx.x;
   const int k = fit_intercept ? nf + 1 : nf;
-  const double count = flat[0], wSum = flat[1], bSum = flat[3], bbSum = flat[4];
   const double* aSum = flat + 5;
   const double* abSum = flat + 5 + nf;
   const double* aa = flat + 5 + 2 * nf;
+  // owned slots (r, s) of the k x (k+1) system (row stride kW) and their raw statistics:
+  // branch-free clamped addresses, so every global load is in flight at once
+  int er[kPer], es[kPer], woff[kPer];
+  double a[kPer];
+  const int w = k + 1;
+#pragma unroll
+  for (int i = 0; i < kPer; ++i) {
+    const int e = t + kThreads * i;
+    const int r = e / w, s = e - (e / w) * w;
+    const bool live = r < k;
+    er[i] = live ? r : 0;
+    es[i] = live ? (s == k ? KMAX : s) : 0;  // the RHS lives in column KMAX
+    // write target: the diagonal goes to the parity's diagonal vector (the matrix keeps 0 there),
+    // dead slots to the thread's private trash double
+    woff[i] = !live ? KMAX * kW + KMAX + t : (r == s ? KMAX * kW + r : r * kW + es[i]);
+    const bool feat = live && r < nf && s < nf;
+    const int lo = s < r ? s : r, hi = s < r ? r : s;
+    const bool rhs = live && r < nf && s == k;
+    a[i] = feat ? aa[pku(lo, hi)] : (rhs ? abSum[r] : 0.0);
+    if (!live) er[i] = -1;
+  }
+  const int tf = t < nf ? t : 0;
+  const double my_sum = aSum[tf], my_diag = aa[pku(tf, tf)];
+  const double count = flat[0], wSum = flat[1], bSum = flat[3], bbSum = flat[4];
   // out = [coef(nf), intercept, status, count, wSum, wwSum, bSum, bbSum]
   if (t < 5) out[nf + 2 + t] = flat[t];
   const double rawBBar = wSum > 0.0 ? bSum / wSum : 0.0;
@@ -39,198 +96,104 @@ __global__ __launch_bounds__(64) void wls_small_kernel(const double* __restrict_
     return;
   }
   const double bStd = rawBStd;
-  for (int j = t; j < nf; j += blockDim.x) {
-    const double m = aSum[j] / wSum;
-    const double s = sqrt(fmax(aa[pku(j, j)] / wSum - m * m, 0.0));
-    aStd[j] = s;
-    aBar[j] = s == 0.0 ? 0.0 : m / s;
-    b[j] = s == 0.0 ? 0.0 : abSum[j] / wSum / (s * bStd);
+  // divisions (not reciprocal multiplies) exactly as wls.cpp / Spark: a constant feature must get
+  // an exactly-zero std, so the zero-pivot / singular fallback triggers identically
+  if (t < nf) {
+    const double m = my_sum / wSum;
+    const double sd = sqrt(fmax(my_diag / wSum - m * m, 0.0));
+    aStd[t] = sd;
+    aBar[t] = sd == 0.0 ? 0.0 : m / sd;
+    iStd[t] = sd == 0.0 ? 0.0 : 1.0 / (sd * sqrt(wSum));  // A_rs = aa_rs * iStd_r * iStd_s
   }
   if (t == 0) bad = 0;
   __syncthreads();
+  WLS_STAMP(1);
+  // standardized system into parity 0; the matrix diagonal is 0 in both parities
   const double eff_l2 = (1.0 - enet) * reg / bStd;
-  for (int e = t; e < nf * nf; e += blockDim.x) {
-    const int i = e / nf, j = e - (e / nf) * nf;
-    const int lo = i < j ? i : j, hi = i < j ? j : i;
-    const double den = aStd[i] * aStd[j];
-    double v = den == 0.0 ? 0.0 : aa[pku(lo, hi)] / wSum / den;
-    if (i == j) {
-      double lam = eff_l2;
-      if (!std_f) lam = aStd[j] != 0.0 ? lam / (aStd[j] * aStd[j]) : 0.0;
-      if (!std_l) lam *= bStd;
-      v += lam;
+#pragma unroll
+  for (int i = 0; i < kPer; ++i) {
+    const int r = er[i], s = es[i];
+    if (r < 0) continue;
+    double v;
+    if (s == KMAX) {  // RHS
+      v = r < nf ? (aStd[r] == 0.0 ? 0.0 : a[i] / wSum / (aStd[r] * bStd)) : rawBBar / bStd;
+    } else if (r < nf && s < nf) {
+      // aa / wSum / (std_r std_s) as two multiplies (within an ulp of wls.cpp; exact zeros kept)
+      v = a[i] * iStd[r] * iStd[s];
+      if (r == s) {
+        double lam = eff_l2;
+        if (!std_f) lam = aStd[s] != 0.0 ? lam / (aStd[s] * aStd[s]) : 0.0;
+        if (!std_l) lam *= bStd;
+        v += lam;
+      }
+    } else if (r == nf && s == nf) {  // intercept diagonal
+      v = 1.0;
+    } else {  // intercept row / column
+      v = aBar[r < nf ? r : s];
     }
-    A[i * kMaxK + j] = v;
-  }
-  if (fit_intercept) {
-    for (int i = t; i < nf; i += blockDim.x) {
-      A[i * kMaxK + nf] = aBar[i];
-      A[nf * kMaxK + i] = aBar[i];
-    }
-    if (t == 0) {
-      A[nf * kMaxK + nf] = 1.0;
-      b[nf] = rawBBar / bStd;
+    a[i] = v;
+    M[woff[i]] = v;
+    if (r == s) {
+      M[r * kW + r] = 0.0;
+      M[kBuf + r * kW + r] = 0.0;
     }
   }
   __syncthreads();
-  // right-looking Cholesky, lower factor in place
-  for (int c = 0; c < k; ++c) {
+  WLS_STAMP(2);
+  // Gauss-Jordan: step c reads parity c & 1 (pivot = diagonal vector[c], column c, row c) and
+  // writes every owned slot to the other parity.  With 0 stored on the matrix diagonal, the pivot
+  // row's update (uses M[c][c]) and the dead column's (uses M[c][c]) are no-ops — no selects, no
+  // branches, one barrier per step.
+  auto step = [&](const int c, const double* __restrict__ R, double* __restrict__ Wb) {
+    const double p = R[KMAX * kW + c];
+    double cv[kPer], rv[kPer];
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      cv[i] = R[(er[i] < 0 ? 0 : er[i]) * kW + c];
+      rv[i] = R[c * kW + es[i]];
+    }
+    // 1/p: v_rcp_f64 + two Newton steps (p is a normal positive number when it is used)
+    double ip = __builtin_amdgcn_rcp(p);
+    ip = ip * (2.0 - p * ip);
+    ip = ip * (2.0 - p * ip);
     if (t == 0) {
-      const double p = A[c * kMaxK + c];
       if (!(p > 0.0)) bad = 1;
-      A[c * kMaxK + c] = sqrt(fmax(p, 1e-300));
+      pivots[c] = p;  // the diagonal vector keeps drifting after its step (dead columns are not zeroed)
+    }
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+      a[i] -= cv[i] * ip * rv[i];
+      Wb[woff[i]] = a[i];
     }
     __syncthreads();
-    const double dc = A[c * kMaxK + c];
-    for (int r = c + 1 + t; r < k; r += blockDim.x) A[r * kMaxK + c] /= dc;
-    __syncthreads();
-    const int m = k - c - 1;
-    for (int e = t; e < m * m; e += blockDim.x) {
-      const int r = c + 1 + e / m, s = c + 1 + e % m;
-      if (s <= r) A[r * kMaxK + s] -= A[r * kMaxK + c] * A[s * kMaxK + c];
-    }
-    __syncthreads();
+  };
+  // unrolled by two: the parity buffers are compile-time bases (immediate LDS offsets)
+  int c = 0;
+  for (; c + 1 < k; c += 2) {
+    step(c, M, M + kBuf);
+    step(c + 1, M + kBuf, M);
   }
+  if (c < k) step(c, M, M + kBuf);
+  WLS_STAMP(3);
   if (bad) {
     if (t == 0) out[nf + 1] = 7.0;  // not positive definite: host falls back (L-BFGS in auto mode)
     return;
   }
-  // L y = b, then L^T x = y: wave 0 reduces each dot product, one barrier per row
-  for (int r = 0; r < k; ++r) {
-    if (t < 64) {
-      double s = 0.0;
-      for (int p = t; p < r; p += 64) s += A[r * kMaxK + p] * x[p];
-      s = wave_sum_f64(s);
-      if (t == 0) x[r] = (b[r] - s) / A[r * kMaxK + r];
+  // x_r = b_r / D_r (the RHS owners), un-standardized
+#pragma unroll
+  for (int i = 0; i < kPer; ++i) {
+    const int r = er[i];
+    if (r >= 0 && es[i] == KMAX) {
+      const double x = a[i] / pivots[r];
+      if (r < nf) out[r] = aStd[r] != 0.0 ? x * bStd / aStd[r] : 0.0;
+      else out[nf] = x * bStd;  // intercept (r == nf only when fitting it)
     }
-    __syncthreads();
   }
-  for (int r = k - 1; r >= 0; --r) {
-    if (t < 64) {
-      double s = 0.0;
-      for (int p = r + 1 + t; p < k; p += 64) s += A[p * kMaxK + r] * x[p];
-      s = wave_sum_f64(s);
-      if (t == 0) x[r] = (x[r] - s) / A[r * kMaxK + r];
-    }
-    __syncthreads();
-  }
-  for (int j = t; j < nf; j += blockDim.x) out[j] = aStd[j] != 0.0 ? x[j] * bStd / aStd[j] : 0.0;
   if (t == 0) {
-    out[nf] = fit_intercept ? x[nf] * bStd : 0.0;
+    if (!fit_intercept) out[nf] = 0.0;
     out[nf + 1] = 0.0;
   }
-}
-
-__device__ __forceinline__ double rl(double v, int l) {  // v_readlane x2: lane l's double, wave-uniform
-  const int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
-  const int hi = __builtin_amdgcn_readlane(__double2hiint(v), l);
-  return __hiloint2double(hi, lo);
-}
-
-// Register-resident variant for k <= KMAX <= 64 (one wave, no LDS, no barriers): lane r holds row r
-// of the standardized system in a fully unrolled register array; the right-looking Cholesky, the
-// forward substitution and the un-standardization exchange values with v_readlane (wave-uniform
-// lane index = unrolled loop counter).  ~k^2 readlanes instead of ~3k barrier-separated LDS steps.
-template <int KMAX>
-__global__ __launch_bounds__(64) void wls_reg_kernel(const double* __restrict__ flat, int nf, int fit_intercept,
-                                                    double reg, double enet, int std_f, int std_l,
-                                                    double* __restrict__ out) {
-  const int r = threadIdx.x;
-  const int k = fit_intercept ? nf + 1 : nf;
-  const double count = flat[0], wSum = flat[1], bSum = flat[3], bbSum = flat[4];
-  const double* aSum = flat + 5;
-  const double* abSum = flat + 5 + nf;
-  const double* aa = flat + 5 + 2 * nf;
-  if (r < 5) out[nf + 2 + r] = flat[r];
-  const double rawBBar = wSum > 0.0 ? bSum / wSum : 0.0;
-  const double rawBStd = wSum > 0.0 ? sqrt(fmax(bbSum / wSum - rawBBar * rawBBar, 0.0)) : 0.0;
-  if (wSum <= 0.0 || rawBStd == 0.0) {
-    if (r == 0) out[nf + 1] = wSum <= 0.0 ? (count > 0 ? 1.0 : 2.0) : 3.0;
-    return;
-  }
-  const double bStd = rawBStd;
-  // my feature's moments (lane r = feature r; the intercept lane r == nf has none)
-  double myStd = 0.0, myBar = 0.0, myB = 0.0;
-  if (r < nf) {
-    const double m = aSum[r] / wSum;
-    myStd = sqrt(fmax(aa[pku(r, r)] / wSum - m * m, 0.0));
-    myBar = myStd == 0.0 ? 0.0 : m / myStd;
-    myB = myStd == 0.0 ? 0.0 : abSum[r] / wSum / (myStd * bStd);
-  } else if (r == nf && fit_intercept) {
-    myB = rawBBar / bStd;
-  }
-  const double eff_l2 = (1.0 - enet) * reg / bStd;
-  double a[KMAX];
-#pragma unroll
-  for (int s = 0; s < KMAX; ++s) {
-    double v = 0.0;
-    if (s < k && r < k) {
-      const double sStd = rl(myStd, s), sBar = rl(myBar, s);
-      if (r < nf && s < nf) {
-        const int lo = r < s ? r : s, hi = r < s ? s : r;
-        const double den = myStd * sStd;
-        v = den == 0.0 ? 0.0 : aa[pku(lo, hi)] / wSum / den;
-        if (r == s) {
-          double lam = eff_l2;
-          if (!std_f) lam = myStd != 0.0 ? lam / (myStd * myStd) : 0.0;
-          if (!std_l) lam *= bStd;
-          v += lam;
-        }
-      } else if (r < nf) {  // s == nf: intercept column
-        v = myBar;
-      } else if (s < nf) {  // r == nf: intercept row
-        v = sBar;
-      } else {
-        v = 1.0;
-      }
-    }
-    a[s] = v;
-  }
-  // Cholesky: column c of L lives in a[c] of lanes r >= c
-  bool bad = false;
-#pragma unroll
-  for (int c = 0; c < KMAX; ++c) {
-    if (c < k) {
-      const double p = rl(a[c], c);
-      bad |= !(p > 0.0);
-      const double dc = sqrt(fmax(p, 1e-300));
-      const double l = r == c ? dc : a[c] / dc;
-      a[c] = l;
-#pragma unroll
-      for (int s = c + 1; s < KMAX; ++s)
-        if (s < k) a[s] -= (r > c ? l : 0.0) * rl(l, s);
-    }
-  }
-  if (bad) {
-    if (r == 0) out[nf + 1] = 7.0;
-    return;
-  }
-  // forward: L y = b (lane r keeps b_r, consumed column by column)
-  double y = myB;
-#pragma unroll
-  for (int c = 0; c < KMAX; ++c) {
-    if (c < k) {
-      const double yc = rl(y, c) / rl(a[c], c);
-      if (r == c) y = yc;
-      else if (r > c) y -= a[c] * yc;
-    }
-  }
-  // backward: L^T x = y; x_c = (y_c - sum_{r > c} L[r][c] x_r) / L[c][c]
-  double x = 0.0;
-#pragma unroll
-  for (int c = KMAX - 1; c >= 0; --c) {
-    if (c < k) {
-      const double t = wave_sum_f64(r > c && r < k ? a[c] * x : 0.0);
-      const double xc = (rl(y, c) - t) / rl(a[c], c);
-      if (r == c) x = xc;
-    }
-  }
-  if (r < nf) out[r] = myStd != 0.0 ? x * bStd / myStd : 0.0;
-  const double xi = rl(x, nf < 64 ? nf : 63);
-  if (r == 0) {
-    out[nf] = fit_intercept ? xi * bStd : 0.0;
-    out[nf + 1] = 0.0;
-  }
+  WLS_STAMP(4);
 }
 
 }  // namespace
@@ -239,20 +202,14 @@ void wls_small(const double* flat, int nf, int fit_intercept, double reg, double
                double* out, hipStream_t st) {
   if (nf < 1 || nf > kWlsSmallMaxFeatures) throw std::invalid_argument("wls_small: nf out of range");
   const int k = fit_intercept ? nf + 1 : nf;
-  if (k <= 16) {
-    hipLaunchKernelGGL(wls_reg_kernel<16>, dim3(1), dim3(64), 0, st, flat, nf, fit_intercept, reg, enet, std_f, std_l, out);
-  } else if (k <= 40) {
-    hipLaunchKernelGGL(wls_reg_kernel<40>, dim3(1), dim3(64), 0, st, flat, nf, fit_intercept, reg, enet, std_f, std_l, out);
-  } else if (k <= 64) {
-    hipLaunchKernelGGL(wls_reg_kernel<64>, dim3(1), dim3(64), 0, st, flat, nf, fit_intercept, reg, enet, std_f, std_l, out);
-  } else {  // k == 65: LDS variant (one wave: every __syncthreads is a single-wave barrier)
-    hipLaunchKernelGGL(wls_small_kernel, dim3(1), dim3(64), 0, st, flat, nf, fit_intercept, reg, enet, std_f, std_l,
-                       out);
-  }
-  DQ_HIP_CHECK(hipGetLastError());
-  return;
-  hipLaunchKernelGGL(wls_small_kernel, dim3(1), dim3(64), 0, st, flat, nf, fit_intercept, reg, enet, std_f, std_l,
-                     out);
+#define DQ_WLS_LAUNCH(KM)                                                                                     \
+  hipLaunchKernelGGL(wls_gj_kernel<KM>, dim3(1), dim3(kThreads), 0, st, flat, nf, fit_intercept, reg, enet, std_f, \
+                     std_l, out)
+  if (k <= 16) DQ_WLS_LAUNCH(16);
+  else if (k <= 33) DQ_WLS_LAUNCH(33);
+  else if (k <= 48) DQ_WLS_LAUNCH(48);
+  else DQ_WLS_LAUNCH(kMaxK);
+#undef DQ_WLS_LAUNCH
   DQ_HIP_CHECK(hipGetLastError());
 }
 
