@@ -190,20 +190,27 @@ class LinearRegression(_LRParams):
                 flat = kernels.gram_stats(X.values, yv, w, sel, gd, x_zero_dead=x_zero_dead)
         tracing.add_rows("gram", tbl.nrows)
         _rank_health(df)
-        with tracing.span("allreduce"):
-            flat = comm.all_reduce_sum(flat)  # X1: data-parallel Gram all-reduce (RCCL over xGMI)
         args = (flat, d, self.getOrDefault("fitIntercept"), float(self.getOrDefault("regParam")),
                 float(self.getOrDefault("elasticNetParam")), bool(self.getOrDefault("standardization")), True,
                 "auto", int(self.getOrDefault("maxIter")), float(self.getOrDefault("tol")))
         if _async_fit(df, flat, d, args):
+            # dq4ml.fit.overlapTail: fit tail (X1 all-reduce + device solve) on a side stream, so
+            # it overlaps whatever the caller enqueues next on the compute stream (the next fit's
+            # Gram pass) instead of following it (in-process A/B, 1x MI355X, d = 32: 159.3 -> 151.7 us
+            # per fit at 1.25e7 rows, 1033 -> 1025 us at 1e8; scripts/overlap_ab.py)
+            sess = getattr(df, "sparkSession", None)
+            ov = sess is not None and str(sess.conf.get("dq4ml.fit.overlapTail", "true")).lower() in ("1", "true")
             with tracing.span("solve"):
-                pending = _PendingWLS(args)  # device Cholesky enqueued; resolved on first read
+                pending = _PendingWLS(args, overlap=ov)  # resolved on first read
             model = LinearRegressionModel(self.uid, None, 0.0)
             model._pending = pending
             self.copyValues(model)
             model._set_summary(LinearRegressionTrainingSummary(model, df, pending, None, stats=pending,
                                                                solver=pending))
             return model
+        with tracing.span("allreduce"):
+            flat = comm.all_reduce_sum(flat)  # X1: data-parallel Gram all-reduce (RCCL over xGMI)
+        args = (flat,) + args[1:]
         # host bookkeeping first, while the Gram kernels run; the solve's D2H is the only sync
         model = LinearRegressionModel(self.uid, None, 0.0)
         self.copyValues(model)
@@ -263,20 +270,51 @@ def _async_fit(df, flat, d, args) -> bool:
     return not (enet != 0.0 and reg != 0.0)
 
 
-class _PendingWLS:
-    """A WLS solve enqueued on the device (``ops.device.wls_small``); ``resolve()`` syncs once."""
+_tail_streams = {}
 
-    def __init__(self, args):
+
+def _tail_stream(dev) -> "torch.cuda.Stream":
+    st = _tail_streams.get(dev)
+    if st is None:
+        st = _tail_streams[dev] = torch.cuda.Stream(device=dev)
+    return st
+
+
+class _PendingWLS:
+    """A WLS solve enqueued on the device (``ops.device.wls_small``); ``resolve()`` syncs once.
+
+    ``overlap=True``: the fit tail — X1 all-reduce of the flat statistics (RCCL) and the solve —
+    runs on a per-device side stream ordered after the Gram pass, so the compute stream is free
+    for the next launch at once (the Gram kernel leaves CU slots for the one-workgroup solve and
+    the RCCL kernel).  ``resolve()`` orders the caller's stream after the tail before reading."""
+
+    def __init__(self, args, overlap: bool = False):
         from ..ops import device
 
-        self.args = args
         flat, d, fit_icpt, reg, enet, std_f, std_l = args[:7]
-        self.out = device.wls_small(flat, d, fit_icpt, reg, enet, std_f, std_l)
+        self._done = None
+        if overlap:
+            cur = torch.cuda.current_stream(flat.device)
+            side = _tail_stream(flat.device)
+            side.wait_stream(cur)
+            with torch.cuda.stream(side):
+                flat.record_stream(side)  # produced on the compute stream, consumed here
+                with tracing.span("allreduce"):
+                    flat = comm.all_reduce_sum(flat)
+                self.out = device.wls_small(flat, d, fit_icpt, reg, enet, std_f, std_l)
+                self._done = torch.cuda.Event()
+                self._done.record(side)
+        else:
+            flat = comm.all_reduce_sum(flat)
+            self.out = device.wls_small(flat, d, fit_icpt, reg, enet, std_f, std_l)
+        self.args = (flat,) + tuple(args[1:])
         self._res = None
 
     def resolve(self):
         if self._res is None:
             flat, d = self.args[0], self.args[1]
+            if self._done is not None:
+                torch.cuda.current_stream(flat.device).wait_event(self._done)
             host = self.out.cpu().numpy()
             if int(host[d + 1]) != 0:  # edge case: the host driver owns warnings/errors/fallbacks
                 self._res = fit_wls_flat(*self.args)
