@@ -28,5 +28,15 @@ assert m.summary.numInstances == n, m.summary.numInstances
 err = float((coef - torch.linspace(-1, 1, d, dtype=torch.float64)).abs().max())
 print(f"rank {rank}: numInstances={m.summary.numInstances} max|coef-beta|={err:.3e} r2={m.summary.r2:.6f}")
 assert err < 5e-3
+# asynchronous fits with the overlapped tail (all-reduce + device solve on the side stream),
+# several in flight before the first read: must equal the synchronous model
+spark.conf.set("dq4ml.fit.async", "true")
+ms = [LinearRegression(solver="normal", gramDtype="bf16").fit(df) for _ in range(4)]
+for ma in ms:
+    ca = torch.tensor(ma.coefficients.toArray())
+    assert torch.allclose(ca, coef, rtol=1e-9, atol=1e-12), (ca - coef).abs().max()
+    assert ma.summary.numInstances == n
+spark.conf.set("dq4ml.fit.async", "false")
+print(f"rank {rank}: async overlapped fits match")
 comm.barrier()
 comm.shutdown()
