@@ -54,6 +54,9 @@ def main(argv=None):
     ap.add_argument("--rows-per-gpu", type=float, default=1.25e8)
     ap.add_argument("--features", type=int, default=64)
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--sync", dest="use_async", action="store_false",
+                    help="synchronous fits (host solve after a D2H every step); default: asynchronous "
+                         "device solve, the host builds the next step's plan while the GPU runs")
     a = ap.parse_args(argv)
     import numpy as np
 
@@ -65,7 +68,8 @@ def main(argv=None):
 
     comm.init()
     rank, world = comm.rank(), comm.world_size()
-    spark = SparkSession.builder().appName("bench-dq").master("local[*]").getOrCreate()
+    spark = SparkSession.builder().appName("bench-dq").master("local[*]") \
+        .config("dq4ml.fit.async", "true" if a.use_async else "false").getOrCreate()
     dev = spark.device
     n = int(a.rows_per_gpu) if dev.type == "cuda" else min(int(a.rows_per_gpu), 200_000)
     d = a.features
@@ -96,7 +100,8 @@ def main(argv=None):
           "config": {"model": f"DQ(range+notNull UDF filters) -> VectorAssembler -> LinearRegression d={d}",
                      "global_batch": total, "seq_len": d, "parallelism": f"dp{world}", "rows_per_gpu": n,
                      "rows_kept_global": int(kept), "coef_max_abs_err": err,
-                     "dq_vm": dict(dqvm.STATS)}}, a.json_out)
+                     "dq_vm": dict(dqvm.STATS),
+                     "fit_mode": "async" if (a.use_async and dev.type == "cuda") else "sync"}}, a.json_out)
     comm.shutdown()
 
 

@@ -31,6 +31,17 @@ def _plan_blocks(h, mode, d, n, xdt, xmode):
     return nb
 
 
+def _h2d(arr: np.ndarray, dev) -> torch.Tensor:
+    """Upload a small host table (kernel descriptors: source pointers + dtype codes, pair lists,
+    scales) WITHOUT a host-device sync: staged through torch's caching pinned-host allocator and
+    copied with ``non_blocking`` (a pageable H2D copy blocks the host until the stream drains,
+    which serialized the host's plan building with the GPU's previous step)."""
+    t = torch.from_numpy(np.ascontiguousarray(arr))
+    if torch.device(dev).type != "cuda":
+        return t.to(dev)
+    return t.pin_memory().to(dev, non_blocking=True)
+
+
 def dtype_code(t: torch.Tensor) -> int:
     try:
         return _DT[t.dtype]
@@ -293,7 +304,7 @@ def _pack_desc(h, parts, dev):
     for i, r in enumerate(rows):
         desc[i, 0] = r.data_ptr()
         desc[i, 1] = dtype_code(r)
-    desc_dev = torch.from_numpy(desc.reshape(-1).view(np.uint8).copy()).to(dev)
+    desc_dev = _h2d(desc.reshape(-1).view(np.uint8), dev)
     return rows, n, desc_dev
 
 
@@ -343,7 +354,7 @@ def pack_columns(parts: List[torch.Tensor], dtype: torch.dtype, sel: Optional[to
     for i, r in enumerate(rows):
         desc[i, 0] = r.data_ptr()
         desc[i, 1] = dtype_code(r)
-    desc_dev = torch.from_numpy(desc.reshape(-1).view(np.uint8).copy()).to(dev, non_blocking=False)
+    desc_dev = _h2d(desc.reshape(-1).view(np.uint8), dev)
     keep = rows  # keep sources alive until the kernel is enqueued
     if sel is not None:
         sel = sel.contiguous().to(torch.bool)
@@ -451,7 +462,7 @@ def _srcw_desc(h, rows, dev):
     for i, r in enumerate(rows):
         desc[i, 0] = r.data_ptr()
         desc[i, 1] = dtype_code(r)
-    return torch.from_numpy(desc.reshape(-1).view(np.uint8).copy()).to(dev)
+    return _h2d(desc.reshape(-1).view(np.uint8), dev)
 
 
 def _rows_of(parts):
@@ -577,7 +588,7 @@ def _gram_wide(h, T: TiledWide, y, w, sel, x_zero_dead):
     if eb == 8:
         amax_l = float((y_lo * live).abs().max()) if n else 0.0
         s_l = amax_l / FP8_MAX if amax_l > 0 else 1.0
-        inv = torch.tensor([1.0, 1.0 / s_h, 1.0 / s_l], dtype=torch.float32, device=dev)
+        inv = _h2d(np.asarray([1.0, 1.0 / s_h, 1.0 / s_l], dtype=np.float32), dev)
     cols = [live.to(torch.float32), (y_hi * live).to(torch.float32), (y_lo * live).to(torch.float32)]
     aug = pack_wide(cols, eb, None, nt=1, inv_scale=inv)
     P = (d + 255) // 256
@@ -588,7 +599,7 @@ def _gram_wide(h, T: TiledWide, y, w, sel, x_zero_dead):
     splitk = max(1, min(max(splitk, -(-nsup * 64 // (1 << 23))), nsup))
     if os.environ.get("DQ4ML_WIDE_SAMEPAIR"):  # diagnostic only (wrong results): every block reads panels 0, 1
         pairs = [(0, 1)] * len(pairs)
-    pairs_dev = torch.tensor(np.asarray(pairs, dtype=np.int32).reshape(-1), device=dev)
+    pairs_dev = _h2d(np.asarray(pairs, dtype=np.int32).reshape(-1), dev)
     part = torch.empty(int(h.gram_wide_partials(d, splitk)), dtype=torch.float32, device=dev)
     out = torch.empty(5 + 2 * d + d * (d + 1) // 2, dtype=torch.float64, device=dev)
     h.gram_wide(eb, T.buf.data_ptr(), aug.buf.data_ptr(), _zero_page(h, dev).data_ptr(), T.nt, P, d, nsup, splitk,

@@ -422,7 +422,9 @@ def try_execute_fused(plan, session) -> Optional[Table]:
     err = torch.zeros(1, dtype=torch.int32, device=base.device)
     g.ptrs[1] = err.data_ptr()
     handle, _log = h.rtc_compile(src, ENTRY)
-    ptrs = torch.from_numpy(np.asarray(g.ptrs, dtype=np.int64)).to(base.device)
+    from .device import _h2d
+
+    ptrs = _h2d(np.asarray(g.ptrs, dtype=np.int64), base.device)  # no host-device sync
     n = base.nrows
     grid = int(max(1, min((n + 255) // 256, 8192)))
     from ..utils import tracing

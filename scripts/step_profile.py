@@ -38,7 +38,7 @@ def grab(step, steps, warmup, dev):
     out = step()
     torch.cuda.synchronize()
     pr.disable()
-    pstats.Stats(pr).sort_stats("cumulative").print_stats(40)
+    pstats.Stats(pr).sort_stats(os.environ.get("SORT", "cumulative")).print_stats(int(os.environ.get("TOP", "40")))
     return 1.0, out
 
 
