@@ -298,24 +298,79 @@ def _wls_device(flat, nf, fit_intercept, reg_param, elastic_net, standardize_fea
         A[nf, :nf] = aBar
         A[nf, nf] = 1.0
         b = torch.cat([abBar, torch.tensor([rawBBar / bStd], dtype=torch.float64, device=dev)])
-    L, info = torch.linalg.cholesky_ex(A)
-    if int(info.item()) != 0:
-        if solver_type != "auto":
-            raise SingularMatrixException("LAPACK.dppsv returned a non-positive pivot: A is not positive definite.")
-        host = flat.cpu().numpy()
-        full = GramStats.from_flat(host, nf)
-        return _wls_native(host, full, fit_intercept, reg_param, elastic_net, standardize_features,
-                           standardize_label, "quasi-newton", max_iter, tol), full
-    x = torch.cholesky_solve(b.unsqueeze(1), L).squeeze(1)
+    x = _pcg(A, b) if solver_type == "auto" else None
+    L = None
+    if x is None:
+        L, info = torch.linalg.cholesky_ex(A)
+        if int(info.item()) != 0:
+            if solver_type != "auto":
+                raise SingularMatrixException("LAPACK.dppsv returned a non-positive pivot: A is not positive definite.")
+            host = flat.cpu().numpy()
+            full = GramStats.from_flat(host, nf)
+            return _wls_native(host, full, fit_intercept, reg_param, elastic_net, standardize_features,
+                               standardize_label, "quasi-newton", max_iter, tol), full
+        x = torch.cholesky_solve(b.unsqueeze(1), L).squeeze(1)
     coef = torch.where(nz, x[:nf] * bStd / safe, torch.zeros_like(m)).cpu().numpy()
     intercept = float(x[nf].item() * bStd) if fit_intercept else 0.0
 
     def diag_inv():
-        inv = torch.cholesky_inverse(L).diagonal()
+        Lf = L if L is not None else torch.linalg.cholesky(A)
+        inv = torch.cholesky_inverse(Lf).diagonal()
         mult = torch.ones(k, dtype=torch.float64, device=dev)
         mult[:nf] = aStd * aStd
         return (inv / (wSum * mult)).cpu().numpy()
     return WLSModel(coef, intercept, diag_inv, np.zeros(1), "cholesky"), stats
+
+
+PCG_RTOL = 1e-13
+
+
+def _pcg(A, b, rtol: float = PCG_RTOL, chunk: int = 8, max_iter: int = 96):
+    """Jacobi-preconditioned conjugate gradients on the standardized SPD system, on the device.
+
+    The large-k solve (k = 4097 in BASELINE config 5) through rocSOLVER potrf + potrs took ~15 ms,
+    latency bound (33 small diagonal-block kernels + sequential triangular solves); a standardized
+    Gram with a ridge term is usually well conditioned, where CG reaches a relative residual of
+    1e-13 in a dozen memory-bound GEMVs (134 MB each).  The recursion is checked once per
+    ``chunk`` iterations (one host sync), converged iterations are frozen by masks (no NaN from a
+    vanishing ``pAp``), and the final TRUE residual must pass too.  Returns None — the caller
+    falls back to the Cholesky factorization, with its exact non-SPD semantics — when a diagonal
+    entry is <= 0 or CG has not converged within ``max_iter``."""
+    import torch
+
+    dg = A.diagonal()
+    if bool((dg <= 0).any()):
+        return None
+    minv = 1.0 / dg
+    x = torch.zeros_like(b)
+    r = b.clone()
+    z = minv * r
+    p = z.clone()
+    rz = torch.dot(r, z)
+    thr = (rtol * rtol) * torch.dot(b, b)
+    zero = torch.zeros((), dtype=b.dtype, device=b.device)
+    done = False
+    for _ in range(0, max_iter, chunk):
+        for _ in range(chunk):
+            act = torch.dot(r, r) > thr
+            Ap = torch.mv(A, p)
+            alpha = torch.where(act, rz / torch.dot(p, Ap), zero)
+            x.add_(alpha * p)
+            r.sub_(alpha * Ap)
+            z = minv * r
+            rz_new = torch.dot(r, z)
+            beta = torch.where(act, rz_new / rz, zero)
+            p = z + beta * p
+            rz = torch.where(act, rz_new, rz)
+        if bool(torch.dot(r, r) <= thr):
+            done = True
+            break
+    if not done:
+        return None
+    res = b - torch.mv(A, x)
+    if not bool(torch.dot(res, res) <= 100.0 * thr):
+        return None
+    return x
 
 
 def weighted_least_squares(stats: GramStats, fit_intercept: bool, reg_param: float, elastic_net: float,

@@ -94,3 +94,27 @@ def test_device_large_k_matches_reference():
     np.testing.assert_allclose(got.coefficients, ref.coefficients, rtol=1e-8, atol=1e-10)
     assert got.intercept == pytest.approx(ref.intercept, rel=1e-8)
     np.testing.assert_allclose(got.diagInvAtWA, ref.diagInvAtWA, rtol=1e-7)
+
+
+def test_pcg_matches_direct_solve_and_declines_non_spd():
+    """Large-k device solve: Jacobi-PCG (optim._pcg) reaches the direct solution; a non-positive
+    diagonal or a non-converging (indefinite) system returns None -> Cholesky fallback path."""
+    import torch
+
+    from net.jgp.labs.sparkdq4ml_amd.models.optim import _pcg
+
+    g = torch.Generator().manual_seed(3)
+    X = torch.randn(3000, 300, generator=g, dtype=torch.float64)
+    X[:, 1] = X[:, 0] + 1e-3 * torch.randn(3000, generator=g, dtype=torch.float64)  # collinear pair
+    A = X.T @ X / 3000 + 1e-2 * torch.eye(300, dtype=torch.float64)
+    b = torch.randn(300, generator=g, dtype=torch.float64)
+    x = _pcg(A, b)
+    ref = torch.linalg.solve(A, b)
+    assert x is not None and float((x - ref).abs().max() / ref.abs().max()) < 1e-10
+    B = A.clone()
+    B[5, 5] = 0.0
+    assert _pcg(B, b) is None
+    C = torch.diag(torch.tensor([1.0, 2.0, 3.0], dtype=torch.float64))
+    C[0, 1] = C[1, 0] = 5.0  # indefinite with a positive diagonal
+    assert _pcg(C, torch.ones(3, dtype=torch.float64)) is None or torch.allclose(
+        C @ _pcg(C, torch.ones(3, dtype=torch.float64)), torch.ones(3, dtype=torch.float64))
