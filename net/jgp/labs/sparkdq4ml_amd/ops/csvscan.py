@@ -53,9 +53,16 @@ def shard_byte_range(data: bytes, rank: int, world: int) -> Tuple[int, int]:
     return align(n * rank // world), align(n * (rank + 1) // world)
 
 
-def _ncols_of(data: bytes, sep: str) -> int:
-    ends = [x for x in (data.find(b"\n"), data.find(b"\r")) if x >= 0]
-    return data.count(sep.encode(), 0, min(ends) if ends else len(data)) + 1
+def _ncols_of(data, sep: str) -> int:
+    """Column count from the first line (a bounded, growing head search: the input may be a
+    multi-GB map with no ``\n`` at all — the reference data is CR-only)."""
+    n, w = len(data), 1 << 16
+    while True:
+        head = bytes(data[:min(n, w)])
+        ends = [x for x in (head.find(b"\n"), head.find(b"\r")) if x >= 0]
+        if ends or w >= n:
+            return head.count(sep.encode(), 0, min(ends) if ends else len(head)) + 1
+        w *= 16
 
 
 def _scan_chunk(h, buf, n: int, trailing: bool, ncols: int, sep: str, dev):
@@ -138,13 +145,16 @@ def _resolve_types(masks, flags, sharded):
     return types
 
 
-def scan_device(data: bytes, sep: str = ",", infer: bool = True, device=None, ncols: Optional[int] = None,
+def scan_device(data, sep: str = ",", infer: bool = True, device=None, ncols: Optional[int] = None,
                 sharded: bool = False, chunk_bytes: Optional[int] = None):
     """Parse ``data`` on the device.  Inputs larger than ``chunk_bytes`` stream through a
     double-buffered pinned staging ring: chunk k+1's host->device copy runs on a side stream while
     chunk k is parsed, chunks split on row boundaries, type masks OR-merged over
     chunks (and ranks when ``sharded``)."""
-    if not infer or len(sep) != 1 or data.find(b'"') >= 0 or data.find(b"\\") >= 0:
+    # quotes / escapes need the host scanner: the parse kernel flags any field that starts with
+    # one (slow path) and a mid-field one makes the column a string — both fall back, so the
+    # input is never pre-scanned on the host
+    if not infer or len(sep) != 1:
         return None
     h = native.hip()
     dev = torch.device(device)

@@ -152,7 +152,26 @@ class DataFrameReader:
 
         o = self._options
         dev = self._session.device
-        data = b"".join(self._read_bytes(f) for f in files)
+        thresh = int(self._session.conf.get("dq4ml.csv.deviceThresholdBytes", str(64 << 20)))
+        mm = None
+        if len(files) == 1 and dev.type == "cuda" and os.path.getsize(files[0]) >= thresh:
+            # large single file: map it (page cache -> pinned staging ring directly, no read() copy)
+            mm = _map_file(files[0])
+            data = mm
+        else:
+            data = b"".join(self._read_bytes(f) for f in files)
+        try:
+            return self._read_csv_data(data, o, dev, thresh)
+        finally:
+            if mm is not None:
+                try:
+                    mm.close()
+                except BufferError:  # a view still alive (exception path): the GC unmaps it later
+                    pass
+
+    def _read_csv_data(self, data, o, dev, thresh) -> Table:
+        from ..parallel import comm
+
         header = _truthy(o.get("header", "false"))
         infer = _truthy(o.get("inferschema", "false"))
         sep = o.get("sep", o.get("delimiter", ","))
@@ -165,10 +184,14 @@ class DataFrameReader:
             from ..ops.csvscan import shard_byte_range
 
             lo, hi = shard_byte_range(data, rank, world)
-            data = data[lo:hi]
+            data = memoryview(data)[lo:hi] if not isinstance(data, bytes) else data[lo:hi]
             header = header and rank == 0
-        thresh = int(self._session.conf.get("dq4ml.csv.deviceThresholdBytes", str(64 << 20)))
-        use_dev = dev.type == "cuda" and not user_types and not _truthy(o.get("header", "false"))
+        # the device scanner implements the default dialect (the app's options, APP:53-55);
+        # any other option takes the host scanner
+        plain = (o.get("quote", '"') == '"' and o.get("escape", "\\") == "\\" and not o.get("nullvalue", "")
+                 and not o.get("comment", "") and not _truthy(o.get("ignoreleadingwhitespace", "false"))
+                 and not _truthy(o.get("ignoretrailingwhitespace", "false")))
+        use_dev = dev.type == "cuda" and not user_types and not _truthy(o.get("header", "false")) and plain
         if shard:  # every rank must take the same (collective) path
             use_dev = all(comm.all_gather_object(bool(use_dev and len(data) >= thresh)))
         elif use_dev:
@@ -181,6 +204,8 @@ class DataFrameReader:
                                         chunk_bytes=int(self._session.conf.get("dq4ml.chunkBytes", str(256 << 20))))
             if t is not None:
                 return t
+        if not isinstance(data, bytes):
+            data = bytes(data)  # host scanner path (small or fallback): a plain copy
         with tracing.span("csv_scan"):
             nrows, cols = self._host_scan(data, header, infer, user_types, user_names, sep)
             if shard and not user_types:
@@ -323,3 +348,12 @@ class DataFrameWriter:
 
 
 _ = (ColumnData, np, torch)
+
+
+def _map_file(path):
+    """Read-only map of a whole file, pre-faulted (MAP_POPULATE) so the staging copies stream."""
+    import mmap
+
+    with open(path, "rb") as f:
+        flags = mmap.MAP_SHARED | getattr(mmap, "MAP_POPULATE", 0)
+        return mmap.mmap(f.fileno(), 0, flags=flags, prot=mmap.PROT_READ)
