@@ -739,6 +739,88 @@ __global__ __launch_bounds__(kBlock) void gram_tall_f64_kernel(GramArgs a) {
 }
 
 // =============================================================================================
+// f64 "skinny" kernel, d <= 8 (the lab's own shape: d = 1): lane = row, every statistic a running
+// f64 register sum on the VALU.  The MFMA kernel maps 16 features to lanes, so at d = 1 15/16 of
+// its lanes idle and each load instruction fetches 4 x 8 B (0.9 TB/s measured); here every lane
+// streams its own rows' x / y / w / sel with branch-free selects (dead rows contribute exact
+// zeros, their garbage never enters a product), 4 rows in flight per thread.  Slab layout = the
+// f64 MFMA kernel's (16 x 16 tile), so gram_reduce_kernel is shared.
+// =============================================================================================
+template <typename TX, int D>
+__global__ __launch_bounds__(kBlock) void gram_skinny_f64_kernel(GramArgs a) {
+  constexpr int NA = D * (D + 1) / 2;
+  constexpr int NV = 5 + 2 * D + NA;
+  constexpr int UNR = 4;
+  __shared__ double red[kWavesPerBlock][NV];
+  double v[NV];
+#pragma unroll
+  for (int k = 0; k < NV; ++k) v[k] = 0.0;
+  const TX* X = reinterpret_cast<const TX*>(a.X);
+  const int64_t n = a.n;
+  const int64_t step = (int64_t)gridDim.x * kBlock * UNR;
+  for (int64_t r0 = (int64_t)blockIdx.x * kBlock * UNR + threadIdx.x; r0 < n; r0 += step) {
+    double x[UNR][D], yv[UNR], wv[UNR];
+    bool live[UNR];
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {  // loads of all UNR rows first (clamped, unconditional)
+      const int64_t r = r0 + (int64_t)u * kBlock;
+      const int64_t rc = r < n ? r : n - 1;
+      live[u] = r < n && (a.sel == nullptr || a.sel[rc] != 0);
+      yv[u] = load_as_f64(a.y, a.ydt, rc);
+      wv[u] = a.w ? load_as_f64(a.w, a.wdt, rc) : 1.0;
+#pragma unroll
+      for (int f = 0; f < D; ++f) x[u][f] = (double)X[(int64_t)f * a.ld + rc];
+    }
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      const double w = live[u] ? wv[u] : 0.0;
+      const double y = live[u] ? yv[u] : 0.0;
+      const double wy = w * y;
+      v[0] += live[u] ? 1.0 : 0.0;
+      v[1] += w;
+      v[2] += w * w;
+      v[3] += wy;
+      v[4] += wy * y;
+      int q = 0;
+#pragma unroll
+      for (int i = 0; i < D; ++i) {
+        const double xi = live[u] ? x[u][i] : 0.0;
+        v[5 + i] += w * xi;
+        v[5 + D + i] += wy * xi;
+        const double wxi = w * xi;
+#pragma unroll
+        for (int j = i; j < D; ++j, ++q) v[5 + 2 * D + q] += wxi * (live[u] ? x[u][j] : 0.0);
+      }
+    }
+  }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const double t = wave_sum_f64(v[k]);
+    if (lane == 0) red[wave][k] = t;
+  }
+  __syncthreads();
+  double* out = a.partials + (int64_t)blockIdx.x * a.P;
+  for (int k = threadIdx.x; k < NV; k += kBlock) {
+    double t = 0.0;
+#pragma unroll
+    for (int w = 0; w < kWavesPerBlock; ++w) t += red[w][k];
+    int64_t dst;
+    if (k < 5 + 2 * D) {
+      dst = k;  // scalars, Σw x (D), Σw x y (D): d == D
+    } else {
+      int q = k - 5 - 2 * D, i = 0;
+      while (q >= D - i) {
+        q -= D - i;
+        ++i;
+      }
+      dst = 5 + 2 * D + i * 16 + (i + q);  // (i, j = i + q) of the 16 x 16 f64 tile
+    }
+    out[dst] = t;
+  }
+}
+
+// =============================================================================================
 // slab reduction -> packed-upper flat layout
 // =============================================================================================
 __device__ __forceinline__ int64_t gram_src_index(int64_t k, int d, int T, int NT) {
@@ -942,7 +1024,40 @@ static void with_kernel(int mode, int xdt, int d, int xmode, bool tiled, F&& f) 
   throw std::invalid_argument("gram_tall: unsupported mode");
 }
 
+constexpr int kSkinnyMaxD = 8;
+
+template <typename F>
+static void with_skinny(int xdt, int d, F&& f) {
+#define DQ_SKINNY(TX)                                          \
+  switch (d) {                                                 \
+    case 1: return f(gram_skinny_f64_kernel<TX, 1>);           \
+    case 2: return f(gram_skinny_f64_kernel<TX, 2>);           \
+    case 3: return f(gram_skinny_f64_kernel<TX, 3>);           \
+    case 4: return f(gram_skinny_f64_kernel<TX, 4>);           \
+    case 5: return f(gram_skinny_f64_kernel<TX, 5>);           \
+    case 6: return f(gram_skinny_f64_kernel<TX, 6>);           \
+    case 7: return f(gram_skinny_f64_kernel<TX, 7>);           \
+    default: return f(gram_skinny_f64_kernel<TX, 8>);          \
+  }
+  if (xdt == DT_F64) { DQ_SKINNY(double) }
+  if (xdt == DT_F32) { DQ_SKINNY(float) }
+#undef DQ_SKINNY
+  throw std::invalid_argument("gram_skinny: unsupported feature dtype");
+}
+
+static bool use_skinny(int mode, int d, int xdt, int tiled) {
+  return mode == GRAM_F64 && !tiled && d <= kSkinnyMaxD && (xdt == DT_F64 || xdt == DT_F32);
+}
+
 int gram_plan_blocks(int mode, int d, int64_t n, int xdt, int xmode) {
+  if (use_skinny(mode, d, xdt, 0)) {
+    int full = 1;
+    with_skinny(xdt, d, [&](auto kern) { full = occupancy_blocks(kern, 0, kBlock); });
+    // >= 8 iterations of 4 rows per thread, at most one resident wave of blocks
+    int64_t want = (n + (int64_t)kBlock * 4 * 8 - 1) / ((int64_t)kBlock * 4 * 8);
+    if (want < 1) want = 1;
+    return (int)(want < full ? want : full);
+  }
   const size_t lds = mode == GRAM_BF16 ? bf16_lds(d, xmode) : f64_lds(d);
   int full = 1;
   const int block = mode == GRAM_BF16 ? bf16_block(d, xmode) : kBlock;
@@ -966,8 +1081,12 @@ void gram_tall(int mode, GramArgs a, int xmode, int blocks, double* out, hipStre
   a.P = (int)gram_partial_stride(mode, a.d);
   const size_t lds = mode == GRAM_BF16 ? bf16_lds(a.d, xmode) : f64_lds(a.d);
   if (a.tiled && mode != GRAM_BF16) throw std::invalid_argument("gram_tall: tiled storage needs bf16 mode");
-  with_kernel(mode, a.xdt, a.d, xmode, a.tiled != 0,
-              [&](auto kern) { hipLaunchKernelGGL(kern, dim3(blocks), dim3(block), lds, st, a); });
+  if (use_skinny(mode, a.d, a.xdt, a.tiled)) {
+    with_skinny(a.xdt, a.d, [&](auto kern) { hipLaunchKernelGGL(kern, dim3(blocks), dim3(kBlock), 0, st, a); });
+  } else {
+    with_kernel(mode, a.xdt, a.d, xmode, a.tiled != 0,
+                [&](auto kern) { hipLaunchKernelGGL(kern, dim3(blocks), dim3(block), lds, st, a); });
+  }
   DQ_HIP_CHECK(hipGetLastError());
   const int T = mode == GRAM_BF16 ? 32 : 16;
   const int NT = (a.d + T - 1) / T;

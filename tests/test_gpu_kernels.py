@@ -69,6 +69,30 @@ def test_gram_with_selection_and_weights(mode):
         assert _rel(out[5:], ref[5:]) < tol, (ww is None, ss is None)
 
 
+@pytest.mark.parametrize("d", [1, 2, 3, 8])
+@pytest.mark.parametrize("xdt", [torch.float64, torch.float32])
+def test_gram_f64_skinny_selection_weights_and_dead_nans(d, xdt):
+    """d <= 8 f64 statistics take the lane-per-row VALU kernel: selection, weights, f32 features,
+    and NaN / inf garbage in dead rows (null labels) must not leak into the sums."""
+    g = torch.Generator(device="cuda").manual_seed(40 + d)
+    n = 123_457
+    X = (torch.randn(d, n, generator=g, device="cuda", dtype=torch.float64) * 2 + 1).to(xdt)
+    y = torch.randn(n, generator=g, device="cuda", dtype=torch.float64)
+    sel = torch.rand(n, generator=g, device="cuda") > 0.25
+    w = torch.rand(n, generator=g, device="cuda", dtype=torch.float64) + 0.5
+    y_bad = y.clone()
+    y_bad[~sel] = float("nan")
+    Xb = X.clone()
+    Xb[:, (~sel).nonzero()[:5, 0]] = float("inf")
+    for ww in (None, w):
+        out = device.gram_stats(Xb, y_bad, ww, sel, "fp64")
+        ref = _ref_stats(X.double(), y, ww, sel)
+        assert torch.isfinite(out).all()
+        assert _rel(out, ref) < 1e-12
+    out = device.gram_stats(X, y, None, None, "fp64")
+    assert _rel(out, _ref_stats(X.double(), y, None, None)) < 1e-12
+
+
 def test_gram_deterministic():
     g = torch.Generator(device="cuda").manual_seed(11)
     X = torch.randn(32, 300_000, generator=g, device="cuda").to(torch.bfloat16)
