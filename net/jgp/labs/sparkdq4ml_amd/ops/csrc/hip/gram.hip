@@ -617,9 +617,14 @@ __global__ __launch_bounds__(kBlock) void gram_tall_f64_kernel(GramArgs a) {
   const int f = lane & 15, q = lane >> 4;
   double* lw = reinterpret_cast<double*>(smem) + wave * 128;  // [w(64), wy(64)]
 
-  f64x4 acc[NPAIR];
+  // kChains independent accumulators per tile pair: 16 back-to-back dependent f64 MFMAs per
+  // superstep otherwise serialize on the MFMA latency
+  constexpr int kChains = 4;
+  f64x4 acc[NPAIR][kChains];
 #pragma unroll
-  for (int p = 0; p < NPAIR; ++p) acc[p] = f64x4{};
+  for (int p = 0; p < NPAIR; ++p)
+#pragma unroll
+    for (int c = 0; c < kChains; ++c) acc[p][c] = f64x4{};
   double cs[NT], ab[NT];
 #pragma unroll
   for (int t = 0; t < NT; ++t) cs[t] = ab[t] = 0.0;
@@ -684,7 +689,7 @@ __global__ __launch_bounds__(kBlock) void gram_tall_f64_kernel(GramArgs a) {
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
           const double b = weighted ? x[J][e] * wv[e] : x[J][e];
-          acc[p] = __builtin_amdgcn_mfma_f64_16x16x4f64(x[I][e], b, acc[p], 0, 0, 0);
+          acc[p][e % kChains] = __builtin_amdgcn_mfma_f64_16x16x4f64(x[I][e], b, acc[p][e % kChains], 0, 0, 0);
         }
     __builtin_amdgcn_wave_barrier();
   }
@@ -729,7 +734,9 @@ __global__ __launch_bounds__(kBlock) void gram_tall_f64_kernel(GramArgs a) {
         for (int J = I; J < NT; ++J, ++p) {
           double* tile = red + 5 + 2 * d + p * 256;
 #pragma unroll
-          for (int r = 0; r < 4; ++r) tile[mfma16d_row(lane, r) * 16 + mfma16d_col(lane)] += acc[p][r];
+          for (int r = 0; r < 4; ++r)
+            tile[mfma16d_row(lane, r) * 16 + mfma16d_col(lane)] +=
+                (acc[p][0][r] + acc[p][1][r]) + (acc[p][2][r] + acc[p][3][r]);
         }
     }
     __syncthreads();
