@@ -146,7 +146,7 @@ def _resolve_types(masks, flags, sharded):
 
 
 def scan_device(data, sep: str = ",", infer: bool = True, device=None, ncols: Optional[int] = None,
-                sharded: bool = False, chunk_bytes: Optional[int] = None):
+                sharded: bool = False, chunk_bytes: Optional[int] = None, pinned: Optional[torch.Tensor] = None):
     """Parse ``data`` on the device.  Inputs larger than ``chunk_bytes`` stream through a
     double-buffered pinned staging ring: chunk k+1's host->device copy runs on a side stream while
     chunk k is parsed, chunks split on row boundaries, type masks OR-merged over
@@ -164,12 +164,15 @@ def scan_device(data, sep: str = ",", infer: bool = True, device=None, ncols: Op
         return None
     n = len(data)
     if chunk_bytes is None or n <= chunk_bytes:
-        host = torch.frombuffer(bytearray(data), dtype=torch.uint8) if n else torch.zeros(0, dtype=torch.uint8)
-        buf = host.pin_memory().to(dev, non_blocking=True) if n else torch.zeros(1, dtype=torch.uint8, device=dev)
+        if pinned is not None and n:
+            buf = pinned.to(dev, non_blocking=True)  # page-locked mapping: direct DMA
+        else:
+            host = torch.frombuffer(bytearray(data), dtype=torch.uint8) if n else torch.zeros(0, dtype=torch.uint8)
+            buf = host.pin_memory().to(dev, non_blocking=True) if n else torch.zeros(1, dtype=torch.uint8, device=dev)
         trailing = n > 0 and data[-1] not in (10, 13)
         parts = [_scan_chunk(h, buf, n, trailing, ncols, sep, dev)]
     else:
-        parts = _scan_chunked(h, data, ncols, sep, dev, int(chunk_bytes))
+        parts = _scan_chunked(h, data, ncols, sep, dev, int(chunk_bytes), pinned)
     masks = parts[0][5]
     flags = parts[0][6]
     for p in parts[1:]:
@@ -201,18 +204,23 @@ def chunk_bounds(data: bytes, chunk_bytes: int):
     return b
 
 
-def _scan_chunked(h, data: bytes, ncols: int, sep: str, dev, chunk_bytes: int):
+def _scan_chunked(h, data, ncols: int, sep: str, dev, chunk_bytes: int, pinned: Optional[torch.Tensor] = None):
     from ..runtime.streams import StagingRing
 
     bounds = chunk_bounds(data, chunk_bytes)
     spans = [(bounds[i], bounds[i + 1]) for i in range(len(bounds) - 1)]
-    ring = StagingRing(max(e - s for s, e in spans), depth=2, device=dev)
+    ring = StagingRing(max(e - s for s, e in spans), depth=2, device=dev, staging=pinned is None)
     mv = memoryview(data)
-    ring.put(0, mv[spans[0][0]:spans[0][1]])
+
+    def put(i):
+        s, e = spans[i]
+        ring.put(i, mv[s:e], pinned=None if pinned is None else pinned[s:e])
+
+    put(0)
     parts = []
     for i, (s, e) in enumerate(spans):
         if i + 1 < len(spans):
-            ring.put(i + 1, mv[spans[i + 1][0]:spans[i + 1][1]])  # overlaps chunk i's parse
+            put(i + 1)  # overlaps chunk i's parse
         buf = ring.get(i)
         trailing = data[e - 1] not in (10, 13)
         parts.append(_scan_chunk(h, buf, e - s, trailing, ncols, sep, dev))

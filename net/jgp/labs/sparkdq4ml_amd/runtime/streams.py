@@ -48,9 +48,12 @@ class StagingRing:
     current stream wait for that copy and returns the device view.  A slot is reused only after
     the compute that consumed it has been recorded (event), so the ring never overwrites live data."""
 
-    def __init__(self, nbytes: int, depth: int = 2, device: Optional[torch.device] = None):
+    def __init__(self, nbytes: int, depth: int = 2, device: Optional[torch.device] = None, staging: bool = True):
         self.device = device or torch.device("cuda", torch.cuda.current_device())
-        self.host: List[torch.Tensor] = [torch.empty(nbytes, dtype=torch.uint8).pin_memory() for _ in range(depth)]
+        # staging=False: every put() names an already page-locked source (runtime.hostmap), so no
+        # pinned bounce buffers are needed
+        self.host: List[torch.Tensor] = [torch.empty(nbytes if staging else 0, dtype=torch.uint8).pin_memory()
+                                         for _ in range(depth)]
         self.dev: List[torch.Tensor] = [torch.empty(nbytes, dtype=torch.uint8, device=self.device)
                                         for _ in range(depth)]
         self.copied = [torch.cuda.Event() for _ in range(depth)]
@@ -59,8 +62,22 @@ class StagingRing:
         self.depth = depth
         self.stream = side_stream(self.device)
 
-    def put(self, i: int, data) -> None:
+    def put(self, i: int, data, pinned: Optional[torch.Tensor] = None) -> None:
+        """Stage chunk ``i``.  ``pinned``: a page-locked host view of the same bytes — then the DMA
+        reads it directly (no host memcpy, and the slot's reuse is ordered on the device, not by a
+        host wait)."""
         k = i % self.depth
+        if pinned is not None:
+            n = pinned.numel()
+            if n > self.dev[k].numel():
+                raise ValueError("StagingRing: chunk larger than the device buffers")
+            self.sizes[k] = n
+            with torch.cuda.stream(self.stream):
+                if self.consumed[k] is not None:
+                    self.stream.wait_event(self.consumed[k])
+                self.dev[k][:n].copy_(pinned, non_blocking=True)
+                self.copied[k].record(self.stream)
+            return
         if self.consumed[k] is not None:
             self.consumed[k].synchronize()  # host must not overwrite pinned memory still being copied/used
         n = len(data)

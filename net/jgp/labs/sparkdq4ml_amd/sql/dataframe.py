@@ -283,6 +283,10 @@ class DataFrame:
 
     where = filter
 
+
+    def where(self, cond) -> "DataFrame":
+        """Alias of :meth:`filter` (Dataset.where)."""
+        return self.filter(cond)
     def limit(self, n: int) -> "DataFrame":
         return self._with(Limit(self._plan, n))
 

@@ -153,23 +153,19 @@ class DataFrameReader:
         o = self._options
         dev = self._session.device
         thresh = int(self._session.conf.get("dq4ml.csv.deviceThresholdBytes", str(64 << 20)))
-        mm = None
+        pinned = None
         if len(files) == 1 and dev.type == "cuda" and os.path.getsize(files[0]) >= thresh:
-            # large single file: map it (page cache -> pinned staging ring directly, no read() copy)
-            mm = _map_file(files[0])
-            data = mm
+            # large single file: cached read-only mapping, page-locked for direct DMA when the
+            # runtime allows it (runtime.hostmap) — no read() copy, no bounce buffer
+            from ..runtime import hostmap
+
+            mf = hostmap.open_mapped(files[0])
+            data, pinned = mf.mm, mf.host
         else:
             data = b"".join(self._read_bytes(f) for f in files)
-        try:
-            return self._read_csv_data(data, o, dev, thresh)
-        finally:
-            if mm is not None:
-                try:
-                    mm.close()
-                except BufferError:  # a view still alive (exception path): the GC unmaps it later
-                    pass
+        return self._read_csv_data(data, o, dev, thresh, pinned)
 
-    def _read_csv_data(self, data, o, dev, thresh) -> Table:
+    def _read_csv_data(self, data, o, dev, thresh, pinned=None) -> Table:
         from ..parallel import comm
 
         header = _truthy(o.get("header", "false"))
@@ -185,6 +181,7 @@ class DataFrameReader:
 
             lo, hi = shard_byte_range(data, rank, world)
             data = memoryview(data)[lo:hi] if not isinstance(data, bytes) else data[lo:hi]
+            pinned = None if pinned is None else pinned[lo:hi]
             header = header and rank == 0
         # the device scanner implements the default dialect (the app's options, APP:53-55);
         # any other option takes the host scanner
@@ -201,7 +198,8 @@ class DataFrameReader:
 
             with tracing.span("csv_scan"):
                 t = csvscan.scan_device(data, sep=sep, infer=infer, device=dev, sharded=shard,
-                                        chunk_bytes=int(self._session.conf.get("dq4ml.chunkBytes", str(256 << 20))))
+                                        chunk_bytes=int(self._session.conf.get("dq4ml.chunkBytes", str(256 << 20))),
+                                        pinned=pinned)
             if t is not None:
                 return t
         if not isinstance(data, bytes):
@@ -349,11 +347,3 @@ class DataFrameWriter:
 
 _ = (ColumnData, np, torch)
 
-
-def _map_file(path):
-    """Read-only map of a whole file, pre-faulted (MAP_POPULATE) so the staging copies stream."""
-    import mmap
-
-    with open(path, "rb") as f:
-        flags = mmap.MAP_SHARED | getattr(mmap, "MAP_POPULATE", 0)
-        return mmap.mmap(f.fileno(), 0, flags=flags, prot=mmap.PROT_READ)

@@ -1,0 +1,48 @@
+"""CPU checks of the benchmark entry points: the bench.py JSON contract and the synthetic CSV of
+the lab pipeline benchmark (reference data format: CR-only rows, no final terminator)."""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "benchmarks"))
+
+
+def test_synth_csv_matches_reference_format(tmp_path):
+    import bench_csv_pipeline as B
+
+    p = tmp_path / "s.csv"
+    B.synth_csv(str(p), 5000)
+    data = p.read_bytes()
+    assert b"\n" not in data and data[-1:] != b"\r" and data.count(b"\r") == 4999
+    rows = [r.split(b",") for r in data.split(b"\r")]
+    g = [int(r[0]) for r in rows]
+    pr = [float(r[1]) for r in rows]
+    assert min(g) >= 1 and max(g) <= 35 and all(1.0 <= x <= 999.99 for x in pr)
+    assert all(len(r[1].split(b".")[1]) in (1, 2) for r in rows)
+    assert sum(x < 20 for x in pr) > 0 and sum(a < 14 and x > 90 for a, x in zip(g, pr)) > 0
+
+
+def test_csv_pipeline_bench_on_host_engine(tmp_path):
+    env = dict(os.environ, TMPDIR=str(tmp_path))
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "benchmarks", "bench_csv_pipeline.py"), "--rows", "20000",
+                          "--steps", "1", "--warmup", "0"], capture_output=True, text=True, env=env, timeout=600)
+    assert out.returncode == 0, out.stderr[-2000:]
+    line = json.loads(out.stdout.strip().splitlines()[-1])
+    assert line["unit"] == "rows/s" and line["value"] > 0
+    assert 0 < line["config"]["rows_after_dq"] < 20000
+    assert abs(line["config"]["coefficients"][0] - 5.0) < 0.3
+
+
+def test_bench_py_json_contract():
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "2", "--warmup", "1",
+                          "--rows", "50000"], capture_output=True, text=True, timeout=600)
+    assert out.returncode == 0, out.stderr[-2000:]
+    line = json.loads(out.stdout.strip().splitlines()[-1])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+              "scaling", "vs_baseline", "dtype", "data", "config"):
+        assert k in line
+    assert line["n_gpus"] == 1 and line["steps"] == 2 and line["warmup"] == 1 and line["higher_is_better"] is True
+    assert line["metric"].startswith("rows/sec LinearRegression.fit")
+    assert line["config"]["coef_max_abs_err"] < 0.05

@@ -163,3 +163,39 @@ def test_device_chunked_scan_matches_one_shot(chunk):
     for a, b in zip(one.columns, many.columns):
         assert torch.equal(a.values, b.values)
         assert torch.equal(a.valid_mask(), b.valid_mask())
+
+
+@pytest.mark.gpu
+def test_mapped_zero_copy_chunked_reader_and_file_change(tmp_path):
+    """Large single files go through the cached, page-locked read-only mapping (runtime.hostmap)
+    and the chunked ring with direct DMA; a rewritten file must not be served from a stale map."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from net.jgp.labs.sparkdq4ml_amd import SparkSession
+    from net.jgp.labs.sparkdq4ml_amd.ops import csvscan
+    from net.jgp.labs.sparkdq4ml_amd.runtime import hostmap
+
+    s = SparkSession.getActiveSession()
+    if s is not None:
+        s.stop()
+    rng = np.random.default_rng(5)
+    n = 120_000
+    g = rng.integers(1, 36, n)
+    pr = np.round(rng.uniform(3, 199, n), 2)
+    p = tmp_path / "lab.csv"
+    p.write_bytes("\r".join(f"{int(x)},{float(y)!r}" for x, y in zip(g, pr)).encode())  # CR-only, no final CR
+    spark = SparkSession.builder().master("mi355x[*]").config("dq4ml.csv.deviceThresholdBytes", 0) \
+        .config("dq4ml.chunkBytes", 64 << 10).getOrCreate()
+    before = csvscan.STATS["chunks"]
+    for _ in range(2):  # second action: cached mapping
+        t = spark.read().option("inferSchema", "true").csv(str(p))._table()
+        np.testing.assert_array_equal(t.columns[0].values.cpu().numpy(), g)
+        np.testing.assert_array_equal(t.columns[1].values.cpu().numpy(), pr)
+    assert csvscan.STATS["chunks"] - before > 4
+    mf = hostmap.open_mapped(str(p))
+    assert mf.host is None or mf.host.is_pinned()
+    p.write_bytes(b"1,2.5\r3,4.25")
+    t = spark.read().option("inferSchema", "true").csv(str(p))._table()
+    assert t.nrows == 2 and t.columns[1].values.cpu().tolist() == [2.5, 4.25]
+    hostmap.clear()
+    spark.stop()
