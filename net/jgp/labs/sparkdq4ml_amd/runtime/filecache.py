@@ -1,0 +1,84 @@
+"""Pinned host cache of input files for CSV ingest.
+
+A large input file is read ONCE into page-locked host memory (parallel ``preadv`` into a pinned
+buffer) and kept, keyed by ``(path, size, mtime)``: every Spark action re-scans its input (S20),
+and each re-scan then streams the cached bytes to the device by direct DMA (~57 GB/s H2D on the
+MI355X box, 1 GB in 17 ms) with no host copy at all.  A rewritten file gets a new entry.
+
+Why a copy and not a registered file mapping: ``hipHostRegister`` of a read-only ``mmap`` works
+and avoids even the first copy, but the pinned pages still belong to the file — a truncating
+rewrite while registered left ``hipDeviceSynchronize`` hanging (round-1 test).  Our own pinned
+buffer cannot change underneath the device."""
+from __future__ import annotations
+
+import os
+import threading
+from collections import OrderedDict
+from concurrent.futures import ThreadPoolExecutor
+
+import torch
+
+__all__ = ["PinnedFile", "open_pinned", "clear"]
+
+MAX_FILES = int(os.environ.get("DQ4ML_FILECACHE_FILES", "2"))
+MAX_BYTES = int(float(os.environ.get("DQ4ML_FILECACHE_BYTES", str(32 << 30))))
+_SLICE = 64 << 20
+_cache: "OrderedDict[tuple, PinnedFile]" = OrderedDict()
+_lock = threading.Lock()
+_pool = None
+
+
+def _readers() -> ThreadPoolExecutor:
+    global _pool
+    if _pool is None:
+        _pool = ThreadPoolExecutor(max(1, min(8, os.cpu_count() or 4)))
+    return _pool
+
+
+class PinnedFile:
+    """``host``: pinned uint8 tensor with the file's bytes; ``data``: a numpy view of it (what the
+    scanner indexes/slices on the host)."""
+
+    def __init__(self, path: str, nbytes: int):
+        self.path = path
+        self.nbytes = nbytes
+        self.host = torch.empty(nbytes, dtype=torch.uint8).pin_memory()
+        self.data = self.host.numpy()
+        fd = os.open(path, os.O_RDONLY)
+        try:
+            mv = memoryview(self.data)
+
+            def read(off):
+                end = min(nbytes, off + _SLICE)
+                pos = off
+                while pos < end:
+                    got = os.preadv(fd, [mv[pos:end]], pos)
+                    if got <= 0:
+                        raise OSError(f"short read of {path} at {pos}")
+                    pos += got
+
+            list(_readers().map(read, range(0, nbytes, _SLICE)))
+        finally:
+            os.close(fd)
+
+
+def open_pinned(path: str) -> PinnedFile:
+    st = os.stat(path)
+    key = (os.path.realpath(path), st.st_size, st.st_mtime_ns)
+    with _lock:
+        pf = _cache.get(key)
+        if pf is not None:
+            _cache.move_to_end(key)
+            return pf
+        for k in [k for k in _cache if k[0] == key[0]]:  # the file changed: drop the stale copy
+            del _cache[k]
+        pf = PinnedFile(path, st.st_size)
+        _cache[key] = pf
+        while len(_cache) > MAX_FILES or (len(_cache) > 1 and sum(p.nbytes for p in _cache.values()) > MAX_BYTES):
+            _cache.popitem(last=False)
+        return pf
+
+
+def clear():
+    with _lock:
+        _cache.clear()

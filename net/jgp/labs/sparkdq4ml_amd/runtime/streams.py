@@ -50,7 +50,7 @@ class StagingRing:
 
     def __init__(self, nbytes: int, depth: int = 2, device: Optional[torch.device] = None, staging: bool = True):
         self.device = device or torch.device("cuda", torch.cuda.current_device())
-        # staging=False: every put() names an already page-locked source (runtime.hostmap), so no
+        # staging=False: every put() names an already page-locked source (runtime.filecache), so no
         # pinned bounce buffers are needed
         self.host: List[torch.Tensor] = [torch.empty(nbytes if staging else 0, dtype=torch.uint8).pin_memory()
                                          for _ in range(depth)]

@@ -155,12 +155,12 @@ class DataFrameReader:
         thresh = int(self._session.conf.get("dq4ml.csv.deviceThresholdBytes", str(64 << 20)))
         pinned = None
         if len(files) == 1 and dev.type == "cuda" and os.path.getsize(files[0]) >= thresh:
-            # large single file: cached read-only mapping, page-locked for direct DMA when the
-            # runtime allows it (runtime.hostmap) — no read() copy, no bounce buffer
-            from ..runtime import hostmap
+            # large single file: pinned host copy cached per (path, size, mtime) (runtime.filecache);
+            # every re-scan DMAs it straight to the device — no read(), no bounce buffer
+            from ..runtime import filecache
 
-            mf = hostmap.open_mapped(files[0])
-            data, pinned = mf.mm, mf.host
+            pf = filecache.open_pinned(files[0])
+            data, pinned = pf.data, pf.host
         else:
             data = b"".join(self._read_bytes(f) for f in files)
         return self._read_csv_data(data, o, dev, thresh, pinned)

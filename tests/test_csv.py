@@ -166,14 +166,14 @@ def test_device_chunked_scan_matches_one_shot(chunk):
 
 
 @pytest.mark.gpu
-def test_mapped_zero_copy_chunked_reader_and_file_change(tmp_path):
-    """Large single files go through the cached, page-locked read-only mapping (runtime.hostmap)
-    and the chunked ring with direct DMA; a rewritten file must not be served from a stale map."""
+def test_pinned_file_cache_chunked_reader_and_file_change(tmp_path):
+    """Large single files go through the pinned host file cache (runtime.filecache) and the
+    chunked ring with direct DMA; a rewritten file must not be served from a stale copy."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     from net.jgp.labs.sparkdq4ml_amd import SparkSession
     from net.jgp.labs.sparkdq4ml_amd.ops import csvscan
-    from net.jgp.labs.sparkdq4ml_amd.runtime import hostmap
+    from net.jgp.labs.sparkdq4ml_amd.runtime import filecache
 
     s = SparkSession.getActiveSession()
     if s is not None:
@@ -192,10 +192,15 @@ def test_mapped_zero_copy_chunked_reader_and_file_change(tmp_path):
         np.testing.assert_array_equal(t.columns[0].values.cpu().numpy(), g)
         np.testing.assert_array_equal(t.columns[1].values.cpu().numpy(), pr)
     assert csvscan.STATS["chunks"] - before > 4
-    mf = hostmap.open_mapped(str(p))
-    assert mf.host is None or mf.host.is_pinned()
+    pf = filecache.open_pinned(str(p))
+    assert pf.host.is_pinned() and pf is filecache.open_pinned(str(p))
+    import os
+    import time
+
+    time.sleep(0.01)
     p.write_bytes(b"1,2.5\r3,4.25")
+    os.utime(p, ns=(time.time_ns(), time.time_ns()))
     t = spark.read().option("inferSchema", "true").csv(str(p))._table()
     assert t.nrows == 2 and t.columns[1].values.cpu().tolist() == [2.5, 4.25]
-    hostmap.clear()
+    filecache.clear()
     spark.stop()
