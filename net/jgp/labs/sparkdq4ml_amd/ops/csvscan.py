@@ -146,7 +146,8 @@ def _resolve_types(masks, flags, sharded):
 
 
 def scan_device(data, sep: str = ",", infer: bool = True, device=None, ncols: Optional[int] = None,
-                sharded: bool = False, chunk_bytes: Optional[int] = None, pinned: Optional[torch.Tensor] = None):
+                sharded: bool = False, chunk_bytes: Optional[int] = None, pinned: Optional[torch.Tensor] = None,
+                device_data: Optional[torch.Tensor] = None):
     """Parse ``data`` on the device.  Inputs larger than ``chunk_bytes`` stream through a
     double-buffered pinned staging ring: chunk k+1's host->device copy runs on a side stream while
     chunk k is parsed, chunks split on row boundaries, type masks OR-merged over
@@ -163,7 +164,18 @@ def scan_device(data, sep: str = ",", infer: bool = True, device=None, ncols: Op
     if ncols > 256:
         return None
     n = len(data)
-    if chunk_bytes is None or n <= chunk_bytes:
+    if device_data is not None and n > 0:
+        # input bytes already resident in HBM (runtime.filecache): chunks are plain slices —
+        # no staging, no H2D; chunking only bounds the per-chunk parse outputs
+        if device_data.numel() != n:
+            raise ValueError("scan_device: device_data does not match data")
+        cb = max(int(chunk_bytes or n), 1 << 30)
+        bounds = chunk_bounds(data, cb) if n > cb else [0, n]
+        parts = []
+        for s, e in zip(bounds, bounds[1:]):
+            trailing = data[e - 1] not in (10, 13)
+            parts.append(_scan_chunk(h, device_data[s:e], e - s, trailing, ncols, sep, dev))
+    elif chunk_bytes is None or n <= chunk_bytes:
         if pinned is not None and n:
             buf = pinned.to(dev, non_blocking=True)  # page-locked mapping: direct DMA
         else:

@@ -162,10 +162,11 @@ class DataFrameReader:
             pf = filecache.open_pinned(files[0])
             data, pinned = pf.data, pf.host
         else:
+            pf = None
             data = b"".join(self._read_bytes(f) for f in files)
-        return self._read_csv_data(data, o, dev, thresh, pinned)
+        return self._read_csv_data(data, o, dev, thresh, pinned, pf)
 
-    def _read_csv_data(self, data, o, dev, thresh, pinned=None) -> Table:
+    def _read_csv_data(self, data, o, dev, thresh, pinned=None, pf=None) -> Table:
         from ..parallel import comm
 
         header = _truthy(o.get("header", "false"))
@@ -182,6 +183,8 @@ class DataFrameReader:
             lo, hi = shard_byte_range(data, rank, world)
             data = memoryview(data)[lo:hi] if not isinstance(data, bytes) else data[lo:hi]
             pinned = None if pinned is None else pinned[lo:hi]
+        else:
+            lo, hi = 0, len(data)
             header = header and rank == 0
         # the device scanner implements the default dialect (the app's options, APP:53-55);
         # any other option takes the host scanner
@@ -196,10 +199,16 @@ class DataFrameReader:
         if use_dev:
             from ..ops import csvscan
 
+            dbytes = None
+            if pf is not None and _truthy(self._session.conf.get("dq4ml.csv.deviceCache", "true")):
+                from ..runtime import filecache
+
+                if filecache.device_bytes_allowed(hi - lo):
+                    dbytes = pf.device_bytes(dev, lo, hi)  # HBM-resident input bytes
             with tracing.span("csv_scan"):
                 t = csvscan.scan_device(data, sep=sep, infer=infer, device=dev, sharded=shard,
                                         chunk_bytes=int(self._session.conf.get("dq4ml.chunkBytes", str(256 << 20))),
-                                        pinned=pinned)
+                                        pinned=pinned, device_data=dbytes)
             if t is not None:
                 return t
         if not isinstance(data, bytes):

@@ -185,13 +185,18 @@ def test_pinned_file_cache_chunked_reader_and_file_change(tmp_path):
     p = tmp_path / "lab.csv"
     p.write_bytes("\r".join(f"{int(x)},{float(y)!r}" for x, y in zip(g, pr)).encode())  # CR-only, no final CR
     spark = SparkSession.builder().master("mi355x[*]").config("dq4ml.csv.deviceThresholdBytes", 0) \
-        .config("dq4ml.chunkBytes", 64 << 10).getOrCreate()
+        .config("dq4ml.chunkBytes", 64 << 10).config("dq4ml.csv.deviceCache", "false").getOrCreate()
     before = csvscan.STATS["chunks"]
-    for _ in range(2):  # second action: cached mapping
+    for _ in range(2):  # second action: cached pinned copy, chunks DMA'd through the ring
         t = spark.read().option("inferSchema", "true").csv(str(p))._table()
         np.testing.assert_array_equal(t.columns[0].values.cpu().numpy(), g)
         np.testing.assert_array_equal(t.columns[1].values.cpu().numpy(), pr)
     assert csvscan.STATS["chunks"] - before > 4
+    spark.conf.set("dq4ml.csv.deviceCache", "true")
+    for _ in range(2):  # HBM-resident input bytes
+        t = spark.read().option("inferSchema", "true").csv(str(p))._table()
+        np.testing.assert_array_equal(t.columns[0].values.cpu().numpy(), g)
+        np.testing.assert_array_equal(t.columns[1].values.cpu().numpy(), pr)
     pf = filecache.open_pinned(str(p))
     assert pf.host.is_pinned() and pf is filecache.open_pinned(str(p))
     import os
