@@ -24,25 +24,55 @@ namespace dq4ml {
 
 namespace {
 
-constexpr int kChunk = 4096;  // bytes per block in the line-boundary passes
+// Line-boundary passes: a thread owns 64 contiguous bytes = four 16-byte granules (vector loads),
+// a block 256 threads = 16 KiB.  Granules are taken in ABSOLUTE 16-byte alignment (a chunk of a
+// larger buffer starts anywhere): the first / last granule may cover bytes outside [0, n), which
+// are masked — a 16-byte granule never crosses a page, so those loads cannot fault.  The
+// byte-per-thread first version (4 KiB blocks, two loads per byte for the CRLF rule) ran at
+// ~1 TB/s.
+constexpr int kBytesPerThread = 64;
+constexpr int kChunk = 256 * kBytesPerThread;  // bytes per block
 
-__device__ __forceinline__ bool is_term(const uint8_t* b, int64_t i) {
-  const uint8_t c = b[i];
-  return c == '\r' || (c == '\n' && (i == 0 || b[i - 1] != '\r'));
+// terminator bitmask of the thread's 64-byte window; window byte k <-> buffer index base + k
+__device__ __forceinline__ uint64_t term_mask(const uint8_t* __restrict__ b, int64_t n, int64_t base) {
+  const uint8_t* ab = b - (reinterpret_cast<uintptr_t>(b) & 15);  // granule-aligned view
+  const int64_t off = b - ab;                                    // 0..15
+  const int64_t g0 = base + off;                                  // aligned position of window byte 0
+  // the byte before the window (for CR LF)
+  uint32_t prev = (base >= 1 && base - 1 < n) ? b[base - 1] : 0u;
+  uint64_t m = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int64_t ga = g0 + 16 * j;  // aligned, multiple of 16
+    if (ga - off >= n || ga - off + 16 <= 0) {
+      prev = 0;
+      continue;
+    }
+    const u32x4 v = *reinterpret_cast<const u32x4*>(ab + ga);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const uint32_t c = (v[k >> 2] >> (8 * (k & 3))) & 0xffu;
+      const int64_t i = ga - off + k;
+      const bool inb = i >= 0 && i < n;
+      const bool t = inb && (c == '\r' || (c == '\n' && prev != '\r'));
+      m |= (uint64_t)t << (16 * j + k);
+      prev = inb ? c : 0u;
+    }
+  }
+  return m;
 }
 
 __global__ __launch_bounds__(256) void csv_count_kernel(const uint8_t* __restrict__ b, int64_t n,
                                                        int64_t* __restrict__ counts) {
-  __shared__ int64_t ws[4];
-  const int64_t base = (int64_t)blockIdx.x * kChunk;
-  int64_t c = 0;
-  for (int k = 0; k < kChunk / 256; ++k) {
-    const int64_t i = base + k * 256 + threadIdx.x;
-    c += __popcll(__ballot(i < n && is_term(b, i)));
-  }
+  __shared__ int ws[4];
+  const int64_t base = (int64_t)blockIdx.x * kChunk + (int64_t)threadIdx.x * kBytesPerThread -
+                       (int64_t)(reinterpret_cast<uintptr_t>(b) & 15);
+  int c = __popcll(term_mask(b, n, base));
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
   if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = c;
   __syncthreads();
-  if (threadIdx.x == 0) counts[blockIdx.x] = ws[0] + ws[1] + ws[2] + ws[3];
+  if (threadIdx.x == 0) counts[blockIdx.x] = (int64_t)ws[0] + ws[1] + ws[2] + ws[3];
 }
 
 __global__ __launch_bounds__(1024) void csv_scan_counts_kernel(int64_t* __restrict__ counts, int64_t nb) {
@@ -73,21 +103,28 @@ __global__ __launch_bounds__(1024) void csv_scan_counts_kernel(int64_t* __restri
 
 __global__ __launch_bounds__(256) void csv_ends_kernel(const uint8_t* __restrict__ b, int64_t n,
                                                       const int64_t* __restrict__ offsets, int64_t* __restrict__ ends) {
-  __shared__ int64_t woff[4];
+  __shared__ int wtot[4];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int64_t base = (int64_t)blockIdx.x * kChunk;
-  int64_t off = offsets[blockIdx.x];
-  for (int k = 0; k < kChunk / 256; ++k) {
-    const int64_t i = base + k * 256 + threadIdx.x;
-    const bool t = i < n && is_term(b, i);
-    const uint64_t m = __ballot(t);
-    if (lane == 0) woff[wave] = __popcll(m);
-    __syncthreads();
-    int64_t before = 0;
-    for (int w = 0; w < wave; ++w) before += woff[w];
-    if (t) ends[off + before + __popcll(m & ((1ull << lane) - 1ull))] = i;
-    off += woff[0] + woff[1] + woff[2] + woff[3];
-    __syncthreads();
+  const int64_t base = (int64_t)blockIdx.x * kChunk + (int64_t)threadIdx.x * kBytesPerThread -
+                       (int64_t)(reinterpret_cast<uintptr_t>(b) & 15);
+  uint64_t m = term_mask(b, n, base);
+  const int c = __popcll(m);
+  // exclusive prefix of the per-thread counts: wave scan (shfl_up) + wave totals in LDS
+  int inc = c;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int t = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += t;
+  }
+  if (lane == 63) wtot[wave] = inc;
+  __syncthreads();
+  int before = inc - c;
+  for (int w = 0; w < wave; ++w) before += wtot[w];
+  int64_t o = offsets[blockIdx.x] + before;
+  while (m) {
+    const int k = __builtin_ctzll(m);
+    ends[o++] = base + k;
+    m &= m - 1;
   }
 }
 
@@ -193,7 +230,60 @@ __device__ int parse_field(const uint8_t* p, int len, double& dv, int64_t& iv, b
 }
 
 constexpr int kMaxCols = 256;
+constexpr int kParseLds = 32768;  // staged bytes per 256-line group
 
+// Parse line li.  Bytes are read as B[i - bias] (global: B = b, bias = 0; LDS-staged: B = the
+// block's stage, bias = the buffer index of its first byte).
+// Called by EVERY lane of the wave (``active`` false past the last line) so the per-field type
+// bits can be OR-reduced across the wave with shuffles: one LDS atomic per wave and field instead
+// of 64 same-address atomics (which serialized the first version of this kernel).
+template <typename PB>
+__device__ __forceinline__ bool parse_line(PB B, int64_t bias, int64_t n, const int64_t* __restrict__ ends,
+                                           int64_t li, bool active, int64_t nlines, int ncols, uint8_t sep,
+                                           double* __restrict__ dvals, int64_t* __restrict__ ivals,
+                                           uint8_t* __restrict__ valid, uint8_t* __restrict__ keep,
+                                           uint32_t* smask) {
+  int64_t start = 0, end = 0;
+  if (active) {
+    if (li > 0) {
+      const int64_t pe = ends[li - 1];
+      start = pe + 1 + ((B[pe - bias] == '\r' && pe + 1 < n && B[pe + 1 - bias] == '\n') ? 1 : 0);
+    }
+    end = ends[li];  // exclusive (position of the terminator or n)
+    keep[li] = end > start;
+  }
+  int64_t pos = start;
+  bool slow = false;
+  for (int c = 0; c < ncols; ++c) {
+    double dv = 0.0;
+    int64_t iv = 0;
+    int ty = CT_NULL;
+    if (pos <= end && end > start) {
+      int64_t q = pos;
+      while (q < end && B[q - bias] != sep) ++q;
+      const int64_t flen = q - pos;
+      if (flen > 0 && (B[pos - bias] == '"' || B[pos - bias] == '\\')) slow = true;
+      ty = parse_field(&B[pos - bias], (int)(flen > 1 << 20 ? 1 << 20 : flen), dv, iv, slow);
+      pos = q + 1;
+    }
+    if (active) {
+      dvals[(int64_t)c * nlines + li] = dv;
+      ivals[(int64_t)c * nlines + li] = iv;
+      valid[(int64_t)c * nlines + li] = ty != CT_NULL && ty != CT_STRING;
+    }
+    uint32_t bit = (active && end > start) ? (1u << ty) : 0u;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) bit |= (uint32_t)__shfl_xor((int)bit, o, 64);
+    if ((threadIdx.x & 63) == 0 && bit) atomicOr(&smask[c], bit);
+  }
+  return slow;
+}
+
+// One thread per line, 256-line groups per block.  A group whose bytes fit kParseLds is first
+// staged into LDS by the whole block with 16-byte granule loads (coalesced; absolute alignment
+// as in the line-boundary passes), then every thread parses its line from LDS — the first
+// version walked each line with dependent byte loads from global memory (~180 GB/s).  Longer
+// groups (very wide rows) parse straight from global memory.
 __global__ __launch_bounds__(256) void csv_parse_kernel(const uint8_t* __restrict__ b, int64_t n,
                                                        const int64_t* __restrict__ ends, int64_t nlines, int ncols,
                                                        uint8_t sep, double* __restrict__ dvals,
@@ -202,38 +292,37 @@ __global__ __launch_bounds__(256) void csv_parse_kernel(const uint8_t* __restric
                                                        int* __restrict__ flags) {
   __shared__ uint32_t smask[kMaxCols];
   __shared__ int sflag;
+  __shared__ __attribute__((aligned(16))) uint8_t stage[kParseLds];
   for (int c = threadIdx.x; c < ncols; c += blockDim.x) smask[c] = 0;
   if (threadIdx.x == 0) sflag = 0;
-  __syncthreads();
-  for (int64_t li = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; li < nlines; li += (int64_t)gridDim.x * blockDim.x) {
-    int64_t start = 0;
-    if (li > 0) {
-      const int64_t pe = ends[li - 1];
-      start = pe + 1 + ((b[pe] == '\r' && pe + 1 < n && b[pe + 1] == '\n') ? 1 : 0);
-    }
-    const int64_t end = ends[li];  // exclusive (position of the terminator or n)
-    keep[li] = end > start;
-    int64_t pos = start;
-    bool slow = false;
-    for (int c = 0; c < ncols; ++c) {
-      double dv = 0.0;
-      int64_t iv = 0;
-      int ty = CT_NULL;
-      if (pos <= end && end > start) {
-        int64_t q = pos;
-        while (q < end && b[q] != sep) ++q;
-        const int64_t flen = q - pos;
-        if (flen > 0 && (b[pos] == '"' || b[pos] == '\\')) slow = true;
-        ty = parse_field(b + pos, (int)(flen > 1 << 20 ? 1 << 20 : flen), dv, iv, slow);
-        pos = q + 1;
+  const uint8_t* ab = b - (reinterpret_cast<uintptr_t>(b) & 15);
+  const int64_t off = b - ab;
+  bool slow = false;
+  const int64_t ngroups = (nlines + 255) / 256;
+  for (int64_t grp = blockIdx.x; grp < ngroups; grp += gridDim.x) {
+    const int64_t l0 = grp * 256;
+    const int64_t l1 = min(nlines, l0 + 256);
+    const int64_t li = l0 + threadIdx.x;
+    // bytes the group touches: [previous terminator, last line's end)
+    const int64_t lo = l0 > 0 ? ends[l0 - 1] : 0;
+    const int64_t hi = ends[l1 - 1];
+    const int64_t glo = (lo + off) & ~(int64_t)15;  // aligned-view granule bounds
+    const int64_t ghi = (hi + 1 + off + 15) & ~(int64_t)15;
+    __syncthreads();  // previous group's readers are done with the stage
+    if (ghi - glo <= kParseLds) {
+      for (int64_t g = glo + 16 * threadIdx.x; g < ghi; g += 16 * blockDim.x) {
+        u32x4 v = {0u, 0u, 0u, 0u};
+        if (g - off < n) v = *reinterpret_cast<const u32x4*>(ab + g);  // granule overlaps [0, n)
+        *reinterpret_cast<u32x4*>(stage + (g - glo)) = v;
       }
-      dvals[(int64_t)c * nlines + li] = dv;
-      ivals[(int64_t)c * nlines + li] = iv;
-      valid[(int64_t)c * nlines + li] = ty != CT_NULL && ty != CT_STRING;
-      if (end > start) atomicOr(&smask[c], 1u << ty);
+      __syncthreads();
+      slow |= parse_line(stage, glo - off, n, ends, li, li < l1, nlines, ncols, sep, dvals, ivals, valid, keep,
+                         smask);
+    } else {
+      slow |= parse_line(b, 0, n, ends, li, li < l1, nlines, ncols, sep, dvals, ivals, valid, keep, smask);
     }
-    if (slow) sflag = 1;
   }
+  if (slow) sflag = 1;
   __syncthreads();
   for (int c = threadIdx.x; c < ncols; c += blockDim.x)
     if (smask[c]) atomicOr(&masks[c], smask[c]);
@@ -242,7 +331,8 @@ __global__ __launch_bounds__(256) void csv_parse_kernel(const uint8_t* __restric
 
 }  // namespace
 
-int64_t csv_count_blocks(int64_t n) { return (n + kChunk - 1) / kChunk; }
+// + 1: the window grid starts at the granule boundary below the buffer start
+int64_t csv_count_blocks(int64_t n) { return (n + kChunk - 1) / kChunk + 1; }
 
 void csv_line_ends(const uint8_t* buf, int64_t n, int64_t* counts, int64_t* ends, hipStream_t st) {
   const int64_t nb = csv_count_blocks(n);
