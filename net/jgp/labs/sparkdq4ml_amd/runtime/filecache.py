@@ -23,7 +23,7 @@ from concurrent.futures import ThreadPoolExecutor
 
 import torch
 
-__all__ = ["PinnedFile", "open_pinned", "device_bytes_allowed", "clear"]
+__all__ = ["PinnedFile", "open_pinned", "shard_range", "device_bytes_allowed", "clear"]
 
 MAX_FILES = int(os.environ.get("DQ4ML_FILECACHE_FILES", "2"))
 MAX_BYTES = int(float(os.environ.get("DQ4ML_FILECACHE_BYTES", str(32 << 30))))
@@ -44,9 +44,11 @@ class PinnedFile:
     """``host``: pinned uint8 tensor with the file's bytes; ``data``: a numpy view of it (what the
     scanner indexes/slices on the host)."""
 
-    def __init__(self, path: str, nbytes: int):
+    def __init__(self, path: str, lo: int, hi: int):
+        """Bytes [lo, hi) of ``path`` (the whole file, or one rank's shard)."""
         self.path = path
-        self.nbytes = nbytes
+        self.lo = lo
+        self.nbytes = nbytes = hi - lo
         self._dev = {}  # (device, lo, hi) -> uint8 device tensor
         self.host = torch.empty(nbytes, dtype=torch.uint8).pin_memory()
         self.data = self.host.numpy()
@@ -58,9 +60,9 @@ class PinnedFile:
                 end = min(nbytes, off + _SLICE)
                 pos = off
                 while pos < end:
-                    got = os.preadv(fd, [mv[pos:end]], pos)
+                    got = os.preadv(fd, [mv[pos:end]], lo + pos)
                     if got <= 0:
-                        raise OSError(f"short read of {path} at {pos}")
+                        raise OSError(f"short read of {path} at {lo + pos}")
                     pos += got
 
             list(_readers().map(read, range(0, nbytes, _SLICE)))
@@ -87,9 +89,40 @@ def device_bytes_allowed(nbytes: int) -> bool:
     return used + nbytes <= MAX_DEVICE_BYTES
 
 
-def open_pinned(path: str) -> PinnedFile:
+def shard_range(path: str, rank: int, world: int):
+    """``ops.csvscan.shard_byte_range`` computed with small reads around the two cut points (a
+    row belongs to the shard holding its first byte) — a rank never reads the whole file."""
+    n = os.path.getsize(path)
+
+    def align(p, f):
+        if p <= 0:
+            return 0
+        if p >= n:
+            return n
+        # advance past the terminator that ends the row containing byte p - 1
+        pos = p - 1
+        while pos < n:
+            f.seek(pos)
+            win = f.read(1 << 16)
+            hits = [x for x in (win.find(b"\n"), win.find(b"\r")) if x >= 0]
+            if hits:
+                q = pos + min(hits) + 1  # just past the terminator
+                if q < n and win[q - 1 - pos:q - pos] == b"\r":
+                    f.seek(q)
+                    if f.read(1) == b"\n":
+                        q += 1
+                return min(q, n)
+            pos += len(win)
+        return n
+
+    with open(path, "rb") as f:
+        return align(n * rank // world, f), align(n * (rank + 1) // world, f)
+
+
+def open_pinned(path: str, lo: int = 0, hi: int = -1) -> PinnedFile:
     st = os.stat(path)
-    key = (os.path.realpath(path), st.st_size, st.st_mtime_ns)
+    hi = st.st_size if hi < 0 else hi
+    key = (os.path.realpath(path), st.st_size, st.st_mtime_ns, lo, hi)
     with _lock:
         pf = _cache.get(key)
         if pf is not None:
@@ -97,7 +130,7 @@ def open_pinned(path: str) -> PinnedFile:
             return pf
         for k in [k for k in _cache if k[0] == key[0]]:  # the file changed: drop the stale copy
             del _cache[k]
-        pf = PinnedFile(path, st.st_size)
+        pf = PinnedFile(path, lo, hi)
         _cache[key] = pf
         while len(_cache) > MAX_FILES or (len(_cache) > 1 and sum(p.nbytes for p in _cache.values()) > MAX_BYTES):
             _cache.popitem(last=False)

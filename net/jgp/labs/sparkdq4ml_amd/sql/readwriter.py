@@ -154,19 +154,28 @@ class DataFrameReader:
         dev = self._session.device
         thresh = int(self._session.conf.get("dq4ml.csv.deviceThresholdBytes", str(64 << 20)))
         pinned = None
+        world, rank = comm.world_size(), comm.rank()
+        shard = world > 1 and _truthy(self._session.conf.get("dq4ml.shardInput", "true"))
+        presharded = False
         if len(files) == 1 and dev.type == "cuda" and os.path.getsize(files[0]) >= thresh:
             # large single file: pinned host copy cached per (path, size, mtime) (runtime.filecache);
-            # every re-scan DMAs it straight to the device — no read(), no bounce buffer
+            # every re-scan DMAs it straight to the device — no read(), no bounce buffer.  A rank
+            # of a sharded read caches (and reads) only its own row-aligned byte range.
             from ..runtime import filecache
 
-            pf = filecache.open_pinned(files[0])
+            if shard:
+                lo, hi = filecache.shard_range(files[0], rank, world)
+                pf = filecache.open_pinned(files[0], lo, hi)
+                presharded = True
+            else:
+                pf = filecache.open_pinned(files[0])
             data, pinned = pf.data, pf.host
         else:
             pf = None
             data = b"".join(self._read_bytes(f) for f in files)
-        return self._read_csv_data(data, o, dev, thresh, pinned, pf)
+        return self._read_csv_data(data, o, dev, thresh, pinned, pf, presharded)
 
-    def _read_csv_data(self, data, o, dev, thresh, pinned=None, pf=None) -> Table:
+    def _read_csv_data(self, data, o, dev, thresh, pinned=None, pf=None, presharded=False) -> Table:
         from ..parallel import comm
 
         header = _truthy(o.get("header", "false"))
@@ -177,15 +186,17 @@ class DataFrameReader:
         user_names = self._schema.names if self._schema else []
         world, rank = comm.world_size(), comm.rank()
         shard = world > 1 and _truthy(self._session.conf.get("dq4ml.shardInput", "true"))
-        if shard:
+        lo, hi = 0, len(data)
+        if shard and not presharded:
             from ..ops.csvscan import shard_byte_range
 
             lo, hi = shard_byte_range(data, rank, world)
             data = memoryview(data)[lo:hi] if not isinstance(data, bytes) else data[lo:hi]
             pinned = None if pinned is None else pinned[lo:hi]
-        else:
-            lo, hi = 0, len(data)
+        if shard:
             header = header and rank == 0
+        if presharded:
+            lo, hi = 0, len(data)  # pf holds exactly this rank's bytes
         # the device scanner implements the default dialect (the app's options, APP:53-55);
         # any other option takes the host scanner
         plain = (o.get("quote", '"') == '"' and o.get("escape", "\\") == "\\" and not o.get("nullvalue", "")

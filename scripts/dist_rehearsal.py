@@ -38,5 +38,19 @@ for ma in ms:
     assert ma.summary.numInstances == n
 spark.conf.set("dq4ml.fit.async", "false")
 print(f"rank {rank}: async overlapped fits match")
+# sharded large-CSV read: each rank reads / pins / caches only its byte range (filecache.shard_range)
+import numpy as np  # noqa: E402
+
+path = os.path.join(os.environ.get("TMPDIR", "/tmp"), "dq4ml_rehearsal.csv")
+if rank == 0:
+    rng = np.random.default_rng(3)
+    gg = rng.integers(1, 36, 300_000)
+    open(path, "wb").write("\r".join(f"{int(a)},{5 * int(a) + 20}.5" for a in gg).encode())
+comm.barrier()
+spark.conf.set("dq4ml.csv.deviceThresholdBytes", "0")
+t = spark.read().option("inferSchema", "true").csv(path)._table()
+rows = comm.all_gather_object(int(t.nrows))
+assert sum(rows) == 300_000, rows
+print(f"rank {rank}: sharded device CSV rows {rows}")
 comm.barrier()
 comm.shutdown()

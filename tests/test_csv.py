@@ -209,3 +209,27 @@ def test_pinned_file_cache_chunked_reader_and_file_change(tmp_path):
     assert t.nrows == 2 and t.columns[1].values.cpu().tolist() == [2.5, 4.25]
     filecache.clear()
     spark.stop()
+
+
+def test_shard_range_matches_in_memory_sharding(tmp_path):
+    """runtime.filecache.shard_range (windowed reads around the cut points) must give exactly the
+    byte ranges of ops.csvscan.shard_byte_range (the whole-buffer Hadoop-split rule)."""
+    import random
+
+    from net.jgp.labs.sparkdq4ml_amd.ops.csvscan import shard_byte_range
+    from net.jgp.labs.sparkdq4ml_amd.runtime.filecache import shard_range
+
+    rnd = random.Random(7)
+    p = tmp_path / "s.csv"
+    for trial in range(25):
+        parts = []
+        for i in range(rnd.randint(1, 200)):
+            parts.append(b"%d,%d" % (rnd.randint(0, 10 ** rnd.randint(0, 8)), i))
+            parts.append(rnd.choice([b"\n", b"\r", b"\r\n"]))
+        if rnd.random() < 0.5:
+            parts.pop()
+        data = b"".join(parts)
+        p.write_bytes(data)
+        for world in (1, 2, 3, 8):
+            for r in range(world):
+                assert shard_range(str(p), r, world) == shard_byte_range(data, r, world), (trial, world, r)
