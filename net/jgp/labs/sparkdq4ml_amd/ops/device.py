@@ -117,8 +117,14 @@ def gram_stats(X, y, w, sel, compute: str = "fp64", x_zero_dead: bool = False, b
     if d > 64 and mode in (2, 3) and w is None:
         # ingest into the wide fragment layout once, then the LDS-tiled MFMA SYRK
         return _gram_wide(h, tile_wide(X, 16 if mode == 2 else 8, sel), y, None, sel, True)
-    if d > 64 or mode in (1, 3):
+    if d > 64 or mode == 3:
         return _gram_fallback_wide(X, y, w, sel, compute)
+    if mode == 1:
+        # "fp32" statistics: f32 (or f64) features through the f64 MFMA kernel — products of f32
+        # values are exact in f64, so this is at least the requested precision, at f32 bytes
+        mode = 0
+        if X.dtype not in (torch.float32, torch.float64):
+            X = X.to(torch.float32)
     if mode == 2 and X.dtype not in (torch.bfloat16, torch.float32, torch.float64):
         X = X.to(torch.float32)
     if mode == 0 and X.dtype not in (torch.float64, torch.float32):

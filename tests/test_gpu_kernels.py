@@ -93,6 +93,17 @@ def test_gram_f64_skinny_selection_weights_and_dead_nans(d, xdt):
     assert _rel(out, _ref_stats(X.double(), y, None, None)) < 1e-12
 
 
+@pytest.mark.parametrize("d", [3, 20, 32, 64])
+def test_gram_fp32_mode_uses_f64_kernel_on_f32_features(d):
+    """gramDtype fp32: f32 features through the f64 MFMA kernel (exact f32 products, f64 sums)."""
+    g = torch.Generator(device="cuda").manual_seed(90 + d)
+    n = 77_777
+    X = torch.randn(d, n, generator=g, device="cuda") + 0.3
+    y = torch.randn(n, generator=g, device="cuda") * 2
+    out = device.gram_stats(X, y, None, None, "fp32")
+    assert _rel(out, _ref_stats(X.double(), y.double(), None, None)) < 1e-12
+
+
 def test_gram_deterministic():
     g = torch.Generator(device="cuda").manual_seed(11)
     X = torch.randn(32, 300_000, generator=g, device="cuda").to(torch.bfloat16)
