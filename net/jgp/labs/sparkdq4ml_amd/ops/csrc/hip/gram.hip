@@ -605,6 +605,36 @@ __global__ __launch_bounds__(256, (NT == 1 ? 3 : 2)) void gram_cols_kernel(GramA
   }
 }
 
+constexpr int kStageLd = 66;  // f64 staging row stride (doubles): 2-double pad spreads the banks
+
+// Cooperative load of features [f0, f0 + 16) x rows [r0, r0 + 64) of a feature-major matrix into a
+// per-wave LDS tile xs[f][row] (f64), zeros for features >= d.  Chunk c = i * 64 + lane.
+template <typename TX>
+__device__ __forceinline__ void stage_tile(const TX* __restrict__ X, int64_t ld, int d, int f0, int64_t r0, int lane,
+                                           double* xs) {
+  constexpr int kPer = 16 / sizeof(TX);     // elements per 16-byte chunk
+  constexpr int kChunksPerRow = 64 / kPer;  // chunks per feature row segment
+  constexpr int kIters = 16 * kChunksPerRow / 64;
+  typedef __attribute__((ext_vector_type(kPer))) TX vec;
+  vec v[kIters];
+#pragma unroll
+  for (int i = 0; i < kIters; ++i) {  // all loads in flight first
+    const int c = i * 64 + lane;
+    const int fl = c / kChunksPerRow, k = c % kChunksPerRow;
+    const int feat = f0 + fl;
+    const TX* src = X + (int64_t)(feat < d ? feat : 0) * ld + r0 + k * kPer;
+    v[i] = feat < d ? __builtin_nontemporal_load(reinterpret_cast<const vec*>(src)) : vec{};
+  }
+#pragma unroll
+  for (int i = 0; i < kIters; ++i) {
+    const int c = i * 64 + lane;
+    const int fl = c / kChunksPerRow, k = c % kChunksPerRow;
+    double* dst = xs + fl * kStageLd + k * kPer;
+#pragma unroll
+    for (int j = 0; j < kPer; j += 2) *reinterpret_cast<f64x2*>(dst + j) = f64x2{(double)v[i][j], (double)v[i][j + 1]};
+  }
+}
+
 // =============================================================================================
 // f64 MFMA kernel (v_mfma_f64_16x16x4_f64): Spark-parity precision
 // =============================================================================================
@@ -616,10 +646,12 @@ __global__ __launch_bounds__(kBlock) void gram_tall_f64_kernel(GramArgs a) {
   const int wave = threadIdx.x >> 6;
   const int f = lane & 15, q = lane >> 4;
   double* lw = reinterpret_cast<double*>(smem) + wave * 128;  // [w(64), wy(64)]
+  // per-wave staging of one 16-feature x 64-row tile, rows padded to kStageLd doubles
+  double* xs = reinterpret_cast<double*>(smem) + kWavesPerBlock * 128 + wave * (16 * kStageLd);
 
   // kChains independent accumulators per tile pair: 16 back-to-back dependent f64 MFMAs per
   // superstep otherwise serialize on the MFMA latency
-  constexpr int kChains = 4;
+  constexpr int kChains = NT >= 2 ? 2 : 4;  // fewer for many pairs: VGPRs -> occupancy
   f64x4 acc[NPAIR][kChains];
 #pragma unroll
   for (int p = 0; p < NPAIR; ++p)
@@ -665,13 +697,33 @@ __global__ __launch_bounds__(kBlock) void gram_tall_f64_kernel(GramArgs a) {
       wyv[e] = lw[64 + 16 * q + e];
     }
     double x[NT][16];
+    if (s < a.nsuper) {
+      // full superstep: the wave loads each tile cooperatively — lane-contiguous 16-byte chunks,
+      // 512 B (f64) / 256 B (f32) runs per feature — and stages it in LDS, then every lane reads
+      // its 16 rows of its feature back (8 x ds_read_b128).  The per-lane strided scalar loads of
+      // the first version touched 64 cache lines per instruction (~3 TB/s at d = 16..32).
 #pragma unroll
-    for (int t = 0; t < NT; ++t) {
+      for (int t = 0; t < NT; ++t) {
+        stage_tile<TX>(X, a.ld, a.d, t * 16, r0, lane, xs);
+        __builtin_amdgcn_wave_barrier();
+        const f64x2* src = reinterpret_cast<const f64x2*>(xs + f * kStageLd + 16 * q);
 #pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        double v = 0.0;
-        if (fvalid[t] && e < rows_left) v = (double)fp[t][r0 + e];
-        x[t][e] = v;
+        for (int i = 0; i < 8; ++i) {
+          const f64x2 v = src[i];
+          x[t][2 * i] = v[0];
+          x[t][2 * i + 1] = v[1];
+        }
+        __builtin_amdgcn_wave_barrier();
+      }
+    } else {
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          double v = 0.0;
+          if (fvalid[t] && e < rows_left) v = (double)fp[t][r0 + e];
+          x[t][e] = v;
+        }
       }
     }
 #pragma unroll
@@ -734,9 +786,12 @@ __global__ __launch_bounds__(kBlock) void gram_tall_f64_kernel(GramArgs a) {
         for (int J = I; J < NT; ++J, ++p) {
           double* tile = red + 5 + 2 * d + p * 256;
 #pragma unroll
-          for (int r = 0; r < 4; ++r)
-            tile[mfma16d_row(lane, r) * 16 + mfma16d_col(lane)] +=
-                (acc[p][0][r] + acc[p][1][r]) + (acc[p][2][r] + acc[p][3][r]);
+          for (int r = 0; r < 4; ++r) {
+            double v = 0.0;
+#pragma unroll
+            for (int c = 0; c < kChains; ++c) v += acc[p][c][r];
+            tile[mfma16d_row(lane, r) * 16 + mfma16d_col(lane)] += v;
+          }
         }
     }
     __syncthreads();
@@ -992,7 +1047,7 @@ static size_t bf16_lds(int d, int xmode) {
 }
 
 static size_t f64_lds(int d) {
-  size_t lds = kWavesPerBlock * 128 * sizeof(double);
+  size_t lds = kWavesPerBlock * (128 + 16 * kStageLd) * sizeof(double);
   const size_t red = (size_t)gram_partial_stride(GRAM_F64, d) * sizeof(double);
   return red > lds ? red : lds;
 }
