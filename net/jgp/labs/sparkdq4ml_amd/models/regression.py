@@ -181,33 +181,37 @@ class LinearRegression(_LRParams):
             sel = yvalid if sel is None else (sel & yvalid)
         zd = X.meta.get("zero_dead", False)
         x_zero_dead = yvalid is None and (tbl.sel is None or (zd is not False and zd is tbl.sel))
+        sess = getattr(df, "sparkSession", None)
+        overlap = sess is not None and str(sess.conf.get("dq4ml.fit.overlapTail", "true")).lower() in ("1", "true")
         with tracing.span("gram"):
             gd = _gram_dtype(self, df)
             if _fusable_assembly(X, w, gd, yvalid):
                 parts, asel = X.sources  # fused VectorAssembler + Gram: the features are never packed
                 flat = kernels.gram_cols(parts, yv, sel if sel is not None else asel)
             else:
-                flat = kernels.gram_stats(X.values, yv, w, sel, gd, x_zero_dead=x_zero_dead)
+                # an overlapped asynchronous fit folds the Gram partials on its side stream too
+                defer = overlap and _async_conf(df) and d <= 64
+                flat = kernels.gram_stats(X.values, yv, w, sel, gd, x_zero_dead=x_zero_dead, defer=defer)
         tracing.add_rows("gram", tbl.nrows)
         _rank_health(df)
         args = (flat, d, self.getOrDefault("fitIntercept"), float(self.getOrDefault("regParam")),
                 float(self.getOrDefault("elasticNetParam")), bool(self.getOrDefault("standardization")), True,
                 "auto", int(self.getOrDefault("maxIter")), float(self.getOrDefault("tol")))
         if _async_fit(df, flat, d, args):
-            # dq4ml.fit.overlapTail: fit tail (X1 all-reduce + device solve) on a side stream, so
-            # it overlaps whatever the caller enqueues next on the compute stream (the next fit's
-            # Gram pass) instead of following it (in-process A/B, 1x MI355X, d = 32: 159.3 -> 151.7 us
-            # per fit at 1.25e7 rows, 1033 -> 1025 us at 1e8; scripts/overlap_ab.py)
-            sess = getattr(df, "sparkSession", None)
-            ov = sess is not None and str(sess.conf.get("dq4ml.fit.overlapTail", "true")).lower() in ("1", "true")
+            # dq4ml.fit.overlapTail: fit tail (Gram fold + X1 all-reduce + device solve) on a side
+            # stream, so it overlaps whatever the caller enqueues next on the compute stream (the
+            # next fit's Gram pass) instead of following it (in-process A/B, 1x MI355X, d = 32:
+            # 159.3 -> 151.7 us per fit at 1.25e7 rows, 1033 -> 1025 us at 1e8; scripts/overlap_ab.py)
             with tracing.span("solve"):
-                pending = _PendingWLS(args, overlap=ov)  # resolved on first read
+                pending = _PendingWLS(args, overlap=overlap)  # resolved on first read
             model = LinearRegressionModel(self.uid, None, 0.0)
             model._pending = pending
             self.copyValues(model)
             model._set_summary(LinearRegressionTrainingSummary(model, df, pending, None, stats=pending,
                                                                solver=pending))
             return model
+        if hasattr(flat, "finish"):
+            flat = flat.finish()
         with tracing.span("allreduce"):
             flat = comm.all_reduce_sum(flat)  # X1: data-parallel Gram all-reduce (RCCL over xGMI)
         args = (flat,) + args[1:]
@@ -256,6 +260,11 @@ def _rank_health(df):
         sess._health_checked = True
 
 
+def _async_conf(df) -> bool:
+    sess = getattr(df, "sparkSession", None)
+    return sess is not None and str(sess.conf.get("dq4ml.fit.async", "false")).lower() in ("1", "true", "yes")
+
+
 def _async_fit(df, flat, d, args) -> bool:
     """Asynchronous normal-equation fit (session config ``dq4ml.fit.async``): device statistics,
     <= 64 features, Cholesky branch (no L1) -> the solve is enqueued on the device and the host
@@ -293,11 +302,15 @@ class _PendingWLS:
 
         flat, d, fit_icpt, reg, enet, std_f, std_l = args[:7]
         self._done = None
+        if hasattr(flat, "finish") and not overlap:
+            flat = flat.finish()
         if overlap:
             cur = torch.cuda.current_stream(flat.device)
             side = _tail_stream(flat.device)
             side.wait_stream(cur)
             with torch.cuda.stream(side):
+                if hasattr(flat, "finish"):
+                    flat = flat.finish()  # Gram partial slabs -> flat statistics, on the side stream
                 flat.record_stream(side)  # produced on the compute stream, consumed here
                 with tracing.span("allreduce"):
                     flat = comm.all_reduce_sum(flat)

@@ -37,7 +37,10 @@ int gram_default_blocks(int64_t n);
 // grid that exactly fills the chip for the kernel instantiation (occupancy-sized, persistent-style)
 int gram_plan_blocks(int mode, int d, int64_t n, int xdt, int xmode);
 // xmode: 0 = X already zero on dead rows (or no sel/w), 1 = binary mask from sel, 2 = general weights
-void gram_tall(int mode, GramArgs a, int xmode, int blocks, double* out, hipStream_t st);
+// reduce = false: only the per-block partial slabs; gram_reduce (same mode/blocks/d) folds them
+// later, possibly on another stream
+void gram_tall(int mode, GramArgs a, int xmode, int blocks, double* out, hipStream_t st, bool reduce = true);
+void gram_reduce(int mode, const double* partials, int blocks, int d, double* out, hipStream_t st);
 
 // fused VectorAssembler + bf16 Gram over d <= 64 source columns (a.X unused; a.sel masks rows)
 struct PackSrcG {

@@ -1132,7 +1132,15 @@ int gram_plan_blocks(int mode, int d, int64_t n, int xdt, int xmode) {
   return (int)(want < full ? want : full);
 }
 
-void gram_tall(int mode, GramArgs a, int xmode, int blocks, double* out, hipStream_t st) {
+void gram_reduce(int mode, const double* partials, int blocks, int d, double* out, hipStream_t st) {
+  const int T = mode == GRAM_BF16 ? 32 : 16;
+  const int NT = (d + T - 1) / T;
+  hipLaunchKernelGGL(gram_reduce_kernel, dim3(reduce_blocks(d)), dim3(1024), 0, st, partials, blocks,
+                     (int)gram_partial_stride(mode, d), d, T, NT, out);
+  DQ_HIP_CHECK(hipGetLastError());
+}
+
+void gram_tall(int mode, GramArgs a, int xmode, int blocks, double* out, hipStream_t st, bool reduce) {
   if (a.d < 1 || a.d > 64) throw std::invalid_argument("gram_tall: d must be in [1, 64]");
   if (blocks < 1) throw std::invalid_argument("gram_tall: blocks must be >= 1");
   a.nsuper = a.n / 64;
@@ -1150,11 +1158,7 @@ void gram_tall(int mode, GramArgs a, int xmode, int blocks, double* out, hipStre
                 [&](auto kern) { hipLaunchKernelGGL(kern, dim3(blocks), dim3(block), lds, st, a); });
   }
   DQ_HIP_CHECK(hipGetLastError());
-  const int T = mode == GRAM_BF16 ? 32 : 16;
-  const int NT = (a.d + T - 1) / T;
-  hipLaunchKernelGGL(gram_reduce_kernel, dim3(reduce_blocks(a.d)), dim3(1024), 0, st, a.partials, blocks, a.P, a.d,
-                     T, NT, out);
-  DQ_HIP_CHECK(hipGetLastError());
+  if (reduce) gram_reduce(mode, a.partials, blocks, a.d, out, st);
 }
 
 static size_t cols_lds(int NT) {

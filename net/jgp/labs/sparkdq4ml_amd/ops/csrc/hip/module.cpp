@@ -44,7 +44,8 @@ PYBIND11_MODULE(_dq4ml_hip, m) {
   m.def("gram_plan_blocks", &gram_plan_blocks);
   m.def("gram_tall",
         [](int mode, uintptr_t X, int64_t ld, int d, int64_t n, int xdt, uintptr_t y, int ydt, uintptr_t w, int wdt,
-           uintptr_t sel, int xmode, uintptr_t partials, int blocks, uintptr_t out, uintptr_t stream, int tiled) {
+           uintptr_t sel, int xmode, uintptr_t partials, int blocks, uintptr_t out, uintptr_t stream, int tiled,
+           bool reduce) {
           GramArgs a{};
           a.tiled = tiled;
           a.X = P<const void>(X);
@@ -58,8 +59,11 @@ PYBIND11_MODULE(_dq4ml_hip, m) {
           a.wdt = wdt;
           a.sel = P<const uint8_t>(sel);
           a.partials = P<double>(partials);
-          gram_tall(mode, a, xmode, blocks, P<double>(out), as_stream(stream));
+          gram_tall(mode, a, xmode, blocks, P<double>(out), as_stream(stream), reduce);
         });
+  m.def("gram_reduce", [](int mode, uintptr_t partials, int blocks, int d, uintptr_t out, uintptr_t stream) {
+    gram_reduce(mode, P<const double>(partials), blocks, d, P<double>(out), as_stream(stream));
+  });
   m.def("gram_cols_blocks", &gram_cols_blocks);
   m.def("gram_cols", [](uintptr_t srcs, int sdt, int d, int64_t n, uintptr_t y, int ydt, uintptr_t sel,
                         uintptr_t partials, int blocks, uintptr_t out, uintptr_t stream) {

@@ -101,12 +101,36 @@ def tile_bf16(X: torch.Tensor) -> TiledBF16:
     return TiledBF16(buf, d, n)
 
 
-def gram_stats(X, y, w, sel, compute: str = "fp64", x_zero_dead: bool = False, blocks: Optional[int] = None):
+class DeferredGram:
+    """Gram partial slabs whose final fold (``gram_reduce``) has not been enqueued yet: the
+    asynchronous fit runs it on its side stream with the all-reduce and the solve, so the compute
+    stream moves on to the next launch right after the Gram kernel."""
+
+    is_cuda = True
+
+    def __init__(self, h, mode, partials, nb, d, out):
+        self._h, self.mode, self.partials, self.nb, self.d, self.out = h, mode, partials, nb, d, out
+        self.device = out.device
+
+    def finish(self) -> torch.Tensor:
+        """Enqueue the fold on the CURRENT stream (the caller orders it after the Gram kernel)."""
+        st = torch.cuda.current_stream(self.device)
+        self.partials.record_stream(st)
+        self.out.record_stream(st)
+        self._h.gram_reduce(self.mode, self.partials.data_ptr(), int(self.nb), int(self.d), self.out.data_ptr(),
+                            st.cuda_stream)
+        return self.out
+
+
+def gram_stats(X, y, w, sel, compute: str = "fp64", x_zero_dead: bool = False, blocks: Optional[int] = None,
+               defer: bool = False):
+    """WLS statistics.  ``defer``: the tiled bf16 path may return a :class:`DeferredGram` (call
+    ``finish()``); every other path returns the final tensor."""
     h = native.hip()
     if isinstance(X, TiledWide):
         return _gram_wide(h, X, y, w, sel, x_zero_dead)
     if isinstance(X, TiledBF16):
-        return _gram_tiled(h, X, y, w, sel, x_zero_dead, blocks)
+        return _gram_tiled(h, X, y, w, sel, x_zero_dead, blocks, defer)
     _check_dev(X, y, w, sel)
     d, n = X.shape
     mode = GRAM_MODES[compute]
@@ -155,7 +179,7 @@ def gram_stats(X, y, w, sel, compute: str = "fp64", x_zero_dead: bool = False, b
     partials = torch.empty(nb * P, dtype=torch.float64, device=X.device)
     h.gram_tall(mode, Xv.data_ptr(), int(ld), int(d), int(n), dtype_code(Xv), y.data_ptr(), dtype_code(y),
                 _ptr(w), dtype_code(w) if w is not None else 0, _ptr(sel), xmode, partials.data_ptr(), nb,
-                out.data_ptr(), _stream(), 0)
+                out.data_ptr(), _stream(), 0, True)
     return out
 
 
@@ -224,7 +248,7 @@ def _prep_rows(y, w, sel, n):
     return y, w, sel
 
 
-def _gram_tiled(h, T: "TiledBF16", y, w, sel, x_zero_dead, blocks):
+def _gram_tiled(h, T: "TiledBF16", y, w, sel, x_zero_dead, blocks, defer=False):
     d, n = T.d, T.n
     if d > 64:
         raise ValueError("tiled Gram supports d <= 64")
@@ -237,7 +261,9 @@ def _gram_tiled(h, T: "TiledBF16", y, w, sel, x_zero_dead, blocks):
     partials = torch.empty(nb * P, dtype=torch.float64, device=T.device)
     h.gram_tall(2, T.buf.data_ptr(), 0, int(d), int(n), 2, y.data_ptr(), dtype_code(y), _ptr(w),
                 dtype_code(w) if w is not None else 0, _ptr(sel), xmode, partials.data_ptr(), nb, out.data_ptr(),
-                _stream(), 1)
+                _stream(), 1, not defer)
+    if defer:
+        return DeferredGram(h, 2, partials, nb, d, out)
     return out
 
 

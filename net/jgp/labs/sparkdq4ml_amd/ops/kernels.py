@@ -105,7 +105,7 @@ def packed_upper(aa: torch.Tensor) -> torch.Tensor:
 
 
 def gram_stats(X: torch.Tensor, y: torch.Tensor, w: Optional[torch.Tensor], sel: Optional[torch.Tensor],
-               compute: str = "fp64", x_zero_dead: bool = False) -> torch.Tensor:
+               compute: str = "fp64", x_zero_dead: bool = False, defer: bool = False) -> torch.Tensor:
     """Flat f64 ``[count, wSum, wwSum, bSum, bbSum, aSum[d], abSum[d], aaSum packed-upper]`` over
     live rows (``sel``), with instance weights ``w`` (default 1) — Spark WLS ``Aggregator.add`` over
     every row, in one pass.  ``X`` is feature-major ``[d, n]``."""
@@ -115,7 +115,7 @@ def gram_stats(X: torch.Tensor, y: torch.Tensor, w: Optional[torch.Tensor], sel:
     if _on_gpu(X):
         from . import device
 
-        return device.gram_stats(X, y, w, sel, compute, x_zero_dead=x_zero_dead)
+        return device.gram_stats(X, y, w, sel, compute, x_zero_dead=x_zero_dead, defer=defer)
     Xd = (X.to_dense() if hasattr(X, "to_dense") else X).to(torch.float64)
     yd = y.to(torch.float64)
     wv = torch.ones(n, dtype=torch.float64) if w is None else w.to(torch.float64)
