@@ -189,8 +189,11 @@ class LinearRegression(_LRParams):
                 parts, asel = X.sources  # fused VectorAssembler + Gram: the features are never packed
                 flat = kernels.gram_cols(parts, yv, sel if sel is not None else asel)
             else:
-                # an overlapped asynchronous fit folds the Gram partials on its side stream too
-                defer = overlap and _async_conf(df) and d <= 64
+                # a single-GPU overlapped asynchronous fit folds the Gram partials on its side
+                # stream too.  Not with N > 1: co-running with the next Gram pass the fold's loads
+                # queue behind its HBM stream (8 us alone, ~100 us co-running), and the side stream
+                # must still fit the all-reduce and the solve into one Gram period
+                defer = overlap and _async_conf(df) and d <= 64 and comm.world_size() == 1
                 flat = kernels.gram_stats(X.values, yv, w, sel, gd, x_zero_dead=x_zero_dead, defer=defer)
         tracing.add_rows("gram", tbl.nrows)
         _rank_health(df)
