@@ -114,7 +114,13 @@ def _features_label(params, df: DataFrame):
     if not is_numeric(lt):
         raise ValueError(f"requirement failed: Column {lc} must be of type numeric but was actually of type "
                          f"{lt.simpleString()}.")
-    tbl = df._table()
+    # only (features, label, weight) are read: prune every other derived column (ColumnPruning)
+    need = {fc, lc}
+    if params.isSet("weightCol") and params.getOrDefault("weightCol"):
+        need.add(params.getOrDefault("weightCol"))
+    from ..sql.plan import execute, prune_columns
+
+    tbl = execute(prune_columns(df._plan, need), df.sparkSession)
     X = tbl.column(fc)
     y = tbl.column(lc)
     return tbl, X, y

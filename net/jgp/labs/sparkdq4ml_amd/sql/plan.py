@@ -17,7 +17,7 @@ from .expressions import (Alias, AnalysisException, ColRef, EvalContext, Expr, U
 from .table import ColumnData, Table
 from .types import BooleanType, StructField, StructType
 
-__all__ = ["LogicalPlan", "LocalRelation", "Project", "Filter", "Limit", "Union", "execute"]
+__all__ = ["LogicalPlan", "LocalRelation", "Project", "Filter", "Limit", "Union", "execute", "prune_columns"]
 
 
 class LogicalPlan:
@@ -218,6 +218,39 @@ class Union(LogicalPlan):
                 valid = torch.cat([ca.valid_mask(a.device), cb.valid_mask(b.device)])
             cols.append(ColumnData(ca.dtype, vals, valid, dict(ca.meta)))
         return Table(a.schema, cols, a.nrows + b.nrows, None, a.device)
+
+
+def prune_columns(plan: LogicalPlan, required) -> LogicalPlan:
+    """Catalyst-style ColumnPruning: a plan whose Projects compute only the output columns some
+    consumer needs (``required``: column names, case-insensitive; None = all).  Filters keep
+    what their condition references; leaves, Limit and Union are not pruned through.  Unchanged
+    subtrees are returned as-is, so their memoized tables are reused.
+
+    Spark's ``LinearRegression.train`` selects (label, features, weight) before aggregating and the
+    optimizer prunes every other derived column out of the whole-stage code — e.g. a DQ rule
+    output only used by a filter is evaluated in registers, never materialized."""
+    if required is None:
+        return plan
+    req = {r.lower() for r in required}
+    if isinstance(plan, Project):
+        keep = [e for e in plan.exprs if output_name(e).lower() in req]
+        child_req = set()
+        for e in keep:
+            child_req |= e.references()
+        child = prune_columns(plan.child, child_req)
+        if len(keep) == len(plan.exprs) and child is plan.child:
+            return plan
+        return Project(child, keep)
+    if isinstance(plan, Filter):
+        child = prune_columns(plan.child, req | {r.lower() for r in plan.cond.references()})
+        f = plan if child is plan.child else Filter(child, plan.cond)
+        names = f.schema().names
+        if any(n.lower() not in req for n in names):
+            # columns only the condition needs: drop them right above the filter, so a fused
+            # Project/Filter chain evaluates them in registers and never stores them
+            return Project(f, [ColRef(n) for n in names if n.lower() in req])
+        return f
+    return plan
 
 
 _exec_lock = threading.RLock()

@@ -132,3 +132,28 @@ def test_huber_robust_to_outliers(cpu_session):
     assert hub.scale > 0
     with pytest.raises(ValueError):
         LinearRegression(loss="huber", solver="normal").fit(df)
+
+
+def test_fit_prunes_unused_derived_columns(cpu_session):
+    """ColumnPruning: a fit reads only (features, label); a derived column only a filter uses is
+    not materialized by the pruned plan, and the model is unchanged."""
+    from net.jgp.labs.sparkdq4ml_amd import LinearRegression, VectorAssembler, col
+    from net.jgp.labs.sparkdq4ml_amd.sql.plan import Project, prune_columns
+
+    rows = [(float(i), float(2 * i + 1), float(i % 7)) for i in range(200)]
+    df = cpu_session.createDataFrame(rows, ["x", "y", "z"])
+    df = df.withColumn("z2", col("z") * 2).withColumn("unused", col("x") + col("z"))
+    df = df.filter(col("z2") > 1).withColumn("label", col("y"))
+    df = VectorAssembler().setInputCols(["x"]).setOutputCol("features").transform(df)
+    pruned = prune_columns(df._plan, {"features", "label"})
+    names = set()
+    p = pruned
+    while hasattr(p, "child"):
+        if isinstance(p, Project):
+            names |= {f.name for f in p.schema().fields}
+        p = p.child
+    assert "unused" not in names and "z2" in names  # z2 feeds the filter...
+    assert "z2" not in pruned.child.schema().names  # ...and is dropped right above it
+    m = LinearRegression().fit(df)
+    assert abs(m.coefficients[0] - 2.0) < 1e-9 and abs(m.intercept - 1.0) < 1e-9
+    assert "unused" in df.columns  # the user's DataFrame is untouched
