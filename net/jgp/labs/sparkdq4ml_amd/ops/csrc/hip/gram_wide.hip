@@ -117,7 +117,8 @@ __device__ __forceinline__ void keep_live(const V& v) {
   for (int e = 0; e < (int)(sizeof(V) / 4); ++e) asm volatile("" ::"v"(reinterpret_cast<const unsigned*>(&v)[e]));
 }
 
-// ABL (diagnostic builds only): 0 = real kernel, 1 = no MFMA (loads + LDS reads), 2 = no glds
+// ABL: 0 = real kernel, 3 = real kernel with s_setprio(1) around the MFMA clusters (A/B);
+// diagnostic builds only: 1 = no MFMA (loads + LDS reads), 2 = no glds
 template <int EB, int MODE, int RING, int WAVES, int ABL = 0>
 __device__ __forceinline__ void syrk_block(const WideArgs& a, unsigned char* smem, int I, int J, int pair, int split) {
   typedef WideTraits<EB> Tr;
@@ -228,11 +229,14 @@ __device__ __forceinline__ void syrk_block(const WideArgs& a, unsigned char* sme
   int rb = 0;  // ring buffer of stage i
   auto step = [&](SF& cur, SF& nxt, int64_t i) {
     const int nb = rb + 1 == RING ? 0 : rb + 1;
+    if constexpr (ABL == 3) __builtin_amdgcn_s_setprio(1);
     mfmas(cur, 0);
+    if constexpr (ABL == 3) __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_sched_barrier(0);
     wait_vm<(RING - 2) * kLoadsPerStage>();
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
+    if constexpr (ABL == 3) __builtin_amdgcn_s_setprio(1);
     mfmas(cur, 2);
     read(nxt, nb);
     issue(i + RING, rb);
@@ -246,6 +250,7 @@ __device__ __forceinline__ void syrk_block(const WideArgs& a, unsigned char* sme
       }
     }
     __builtin_amdgcn_sched_barrier(0);
+    if constexpr (ABL == 3) __builtin_amdgcn_s_setprio(0);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     rb = nb;
@@ -468,6 +473,9 @@ static void launch_wide_eb(const WideArgs& a, int nblocks, hipStream_t st, int r
   // diagnostic ablations (timing only, wrong results): waves 41 = no MFMA, 42 = no glds
   if (waves == 41) return launch_wide<EB, 4, 4, 1>(a, nblocks, st);
   if (waves == 42) return launch_wide<EB, 4, 4, 2>(a, nblocks, st);
+  // A/B: s_setprio(1) around the MFMA clusters (guide T5), 4 / 8 waves
+  if (waves == 43) return launch_wide<EB, 4, 4, 3>(a, nblocks, st);
+  if (waves == 83) return launch_wide<EB, 4, 8, 3>(a, nblocks, st);
   if (waves == 8) ring == 5 ? launch_wide<EB, 5, 8>(a, nblocks, st) : launch_wide<EB, 4, 8>(a, nblocks, st);
   else ring == 5 ? launch_wide<EB, 5, 4>(a, nblocks, st) : launch_wide<EB, 4, 4>(a, nblocks, st);
 }
@@ -479,7 +487,7 @@ void gram_wide(int eb, WideArgs a, const int* pairs_dev, const float* scales, do
   const int npair = (P + 1) * (P + 2) / 2;
   const int nb = npair * a.splitk;
   if (ring != 4 && ring != 5) throw std::invalid_argument("gram_wide: ring must be 4 or 5");
-  if (waves != 4 && waves != 8 && waves != 41 && waves != 42)
+  if (waves != 4 && waves != 8 && waves != 41 && waves != 42 && waves != 43 && waves != 83)
     throw std::invalid_argument("gram_wide: waves must be 4 or 8");
   if (eb == 16) launch_wide_eb<16>(a, nb, st, ring, waves);
   else launch_wide_eb<8>(a, nb, st, ring, waves);
