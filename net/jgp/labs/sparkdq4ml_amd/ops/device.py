@@ -141,6 +141,8 @@ def gram_stats(X, y, w, sel, compute: str = "fp64", x_zero_dead: bool = False, b
     if d > 64 and mode in (2, 3) and w is None:
         # ingest into the wide fragment layout once, then the LDS-tiled MFMA SYRK
         return _gram_wide(h, tile_wide(X, 16 if mode == 2 else 8, sel), y, None, sel, True)
+    if mode == 3 and d <= 64:
+        mode = 2  # tall fp8 request: the bf16 MFMA kernel is HBM-bound already and more precise
     if d > 64 or mode == 3:
         return _gram_fallback_wide(X, y, w, sel, compute)
     if mode == 1:

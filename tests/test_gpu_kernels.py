@@ -104,6 +104,16 @@ def test_gram_fp32_mode_uses_f64_kernel_on_f32_features(d):
     assert _rel(out, _ref_stats(X.double(), y.double(), None, None)) < 1e-12
 
 
+def test_gram_fp8_request_tall_uses_bf16_kernel():
+    """gramDtype fp8 with d <= 64: served by the bf16 MFMA kernel (HBM-bound either way)."""
+    g = torch.Generator(device="cuda").manual_seed(77)
+    X = (torch.randn(16, 50_000, generator=g, device="cuda") + 0.2).to(torch.bfloat16)
+    y = torch.randn(50_000, generator=g, device="cuda")
+    out = device.gram_stats(X, y, None, None, "fp8")
+    ref = device.gram_stats(X, y, None, None, "bf16")
+    assert torch.equal(out, ref)
+
+
 def test_gram_deterministic():
     g = torch.Generator(device="cuda").manual_seed(11)
     X = torch.randn(32, 300_000, generator=g, device="cuda").to(torch.bfloat16)
