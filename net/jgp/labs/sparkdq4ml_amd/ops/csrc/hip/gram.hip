@@ -806,7 +806,7 @@ __global__ __launch_bounds__(kBlock) void gram_tall_f64_kernel(GramArgs a) {
 // its lanes idle and each load instruction fetches 4 x 8 B (0.9 TB/s measured); here every lane
 // streams its own rows' x / y / w / sel with branch-free selects (dead rows contribute exact
 // zeros, their garbage never enters a product), 4 rows in flight per thread.  Slab layout = the
-// f64 MFMA kernel's (16 x 16 tile), so gram_reduce_kernel is shared.
+// f64 MFMA kernel's (16 x 16 tile), so the slab fold is shared.
 // =============================================================================================
 template <typename TX, int D>
 __global__ __launch_bounds__(kBlock) void gram_skinny_f64_kernel(GramArgs a) {
@@ -885,45 +885,48 @@ __global__ __launch_bounds__(kBlock) void gram_skinny_f64_kernel(GramArgs a) {
 // =============================================================================================
 // slab reduction -> packed-upper flat layout
 // =============================================================================================
-__device__ __forceinline__ int64_t gram_src_index(int64_t k, int d, int T, int NT) {
-  if (k < 5 + 2 * (int64_t)d) return k;
-  const int64_t kk = k - (5 + 2 * (int64_t)d);
-  int64_t j = (int64_t)((sqrt(8.0 * (double)kk + 1.0) - 1.0) * 0.5);
-  while (j * (j + 1) / 2 > kk) --j;
-  while ((j + 1) * (j + 2) / 2 <= kk) ++j;
-  const int64_t i = kk - j * (j + 1) / 2;  // i <= j
-  const int64_t I = i / T, J = j / T;
-  const int64_t p = I * NT - I * (I - 1) / 2 + (J - I);
-  return 5 + 2 * (int64_t)d + p * T * T + (i % T) * T + (j % T);
-}
 
-// 16 outputs per block (128-B coalesced row segments); 64 slab groups of 16 threads each load a
-// strided share of the slabs with independent loads (one latency round for <= 256 slabs), then a
-// fixed-order LDS combine: deterministic.
-__global__ __launch_bounds__(1024) void gram_reduce_kernel(const double* __restrict__ partials, int nslab, int P,
-                                                          int d, int T, int NT, double* __restrict__ out) {
-  __shared__ double part[64][17];
-  const int64_t K = 5 + 2 * (int64_t)d + (int64_t)d * (d + 1) / 2;
-  const int c = threadIdx.x & 15, g = threadIdx.x >> 4;
-  const int64_t k = (int64_t)blockIdx.x * 16 + c;
+// Storage-order fold: thread = one slab element (consecutive threads read consecutive doubles of
+// every slab: 512-B coalesced runs), 16 slab groups per block with independent loads, fixed-order
+// LDS combine (deterministic), then the element's packed-upper destination (lower halves of the
+// diagonal tiles and padding features are dropped).  The output-order first version gathered
+// each packed entry from 256-B-strided tile rows.
+__global__ __launch_bounds__(1024) void gram_fold_kernel(const double* __restrict__ partials, int nslab, int P, int d,
+                                                        int T, int NT, double* __restrict__ out) {
+  __shared__ double part[16][65];
+  const int c = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int o = blockIdx.x * 64 + c;
   double s = 0.0;
-  if (k < K) {
-    const int64_t src = gram_src_index(k, d, T, NT);
-    const double* p = partials + src;
+  if (o < P) {
+    const double* p = partials + o;
     int b = g;
-    for (; b + 192 < nslab; b += 256) {
-      const double v0 = p[(int64_t)b * P], v1 = p[(int64_t)(b + 64) * P];
-      const double v2 = p[(int64_t)(b + 128) * P], v3 = p[(int64_t)(b + 192) * P];
+    for (; b + 48 < nslab; b += 64) {
+      const double v0 = p[(int64_t)b * P], v1 = p[(int64_t)(b + 16) * P];
+      const double v2 = p[(int64_t)(b + 32) * P], v3 = p[(int64_t)(b + 48) * P];
       s += (v0 + v1) + (v2 + v3);
     }
-    for (; b < nslab; b += 64) s += p[(int64_t)b * P];
+    for (; b < nslab; b += 16) s += p[(int64_t)b * P];
   }
   part[g][c] = s;
   __syncthreads();
-  if (threadIdx.x < 16 && k < K) {
+  if (g == 0 && o < P) {
     double t = 0.0;
-    for (int i = 0; i < 64; ++i) t += part[i][c];
-    out[k] = t;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) t += part[i][c];
+    const int head = 5 + 2 * d;
+    if (o < head) {
+      out[o] = t;
+      return;
+    }
+    const int e = o - head, pr = e / (T * T), w = e - pr * T * T, r = w / T, cc = w - (w / T) * T;
+    int I = 0, rem = pr;  // row-major pair index over I <= J < NT
+    while (rem >= NT - I) {
+      rem -= NT - I;
+      ++I;
+    }
+    const int J = I + rem;
+    const int64_t i = (int64_t)I * T + r, j = (int64_t)J * T + cc;
+    if (i <= j && j < d) out[head + i + j * (j + 1) / 2] = t;
   }
 }
 
@@ -1012,11 +1015,6 @@ int64_t gram_partial_stride(int mode, int d) {
   }
   const int NT = (d + 31) / 32;
   return 5 + 2 * (int64_t)d + (int64_t)NT * (NT + 1) / 2 * 1024;
-}
-
-static int reduce_blocks(int d) {
-  const int64_t K = 5 + 2 * (int64_t)d + (int64_t)d * (d + 1) / 2;
-  return (int)((K + 15) / 16);
 }
 
 int gram_default_blocks(int64_t n) {
@@ -1135,8 +1133,9 @@ int gram_plan_blocks(int mode, int d, int64_t n, int xdt, int xmode) {
 void gram_reduce(int mode, const double* partials, int blocks, int d, double* out, hipStream_t st) {
   const int T = mode == GRAM_BF16 ? 32 : 16;
   const int NT = (d + T - 1) / T;
-  hipLaunchKernelGGL(gram_reduce_kernel, dim3(reduce_blocks(d)), dim3(1024), 0, st, partials, blocks,
-                     (int)gram_partial_stride(mode, d), d, T, NT, out);
+  const int P = (int)gram_partial_stride(mode, d);
+  // output-order gather (first version): 4.4 / 7.9 us at d = 32 / 64; storage order: 3.8 / 3.9 us
+  hipLaunchKernelGGL(gram_fold_kernel, dim3((P + 63) / 64), dim3(1024), 0, st, partials, blocks, P, d, T, NT, out);
   DQ_HIP_CHECK(hipGetLastError());
 }
 
@@ -1209,9 +1208,7 @@ void gram_cols(GramArgs a, const PackSrcG* srcs_dev, int sdt, int blocks, double
   with_cols_kernel(NT, sdt, a.ydt,
                    [&](auto k) { hipLaunchKernelGGL(k, dim3(blocks), dim3(256), lds, st, a, srcs_dev); });
   DQ_HIP_CHECK(hipGetLastError());
-  hipLaunchKernelGGL(gram_reduce_kernel, dim3(reduce_blocks(a.d)), dim3(1024), 0, st, a.partials, blocks, a.P, a.d,
-                     32, NT, out);
-  DQ_HIP_CHECK(hipGetLastError());
+  gram_reduce(GRAM_BF16, a.partials, blocks, a.d, out, st);
 }
 
 }  // namespace dq4ml
