@@ -119,7 +119,20 @@ def main(argv=None):
         df = VectorAssembler().setInputCols(["guest"]).setOutputCol("features").transform(df)
         return LinearRegression().setMaxIter(40).setRegParam(1).setElasticNetParam(1).fit(df)
 
-    elapsed, model = timed(step, a.steps, a.warmup, dev)
+    # the first action also reads the file into the pinned host cache and HBM (runtime.filecache):
+    # timed separately and reported, it is not part of the steady-state per-action number
+    import time
+
+    import torch
+
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    step()
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    first_ms = (time.perf_counter() - t0) * 1e3
+    elapsed, model = timed(step, a.steps, max(0, a.warmup - 1), dev)
     emit({"metric": "rows/sec lab pipeline CSV -> DQ rules -> VectorAssembler -> LinearRegression.fit",
           "value": rows * a.steps / elapsed, "unit": "rows/s", "n_gpus": world, "steps": a.steps,
           "warmup": a.warmup, "ms_per_step": elapsed / a.steps * 1e3, "higher_is_better": True,
@@ -130,6 +143,7 @@ def main(argv=None):
                      "rows_after_dq": int(model.summary.numInstances),
                      "coefficients": [float(v) for v in model.coefficients.toArray()],
                      "intercept": float(model.intercept), "parallelism": f"dp{world}",
+                     "first_action_ms": first_ms,
                      "device_scans": csvscan.STATS["device_scans"], "scan_fallbacks": csvscan.STATS["fallbacks"]}},
          a.json_out)
     comm.shutdown()
