@@ -639,5 +639,5 @@ def _gram_wide(h, T: TiledWide, y, w, sel, x_zero_dead):
     h.gram_wide(eb, T.buf.data_ptr(), aug.buf.data_ptr(), _zero_page(h, dev).data_ptr(), T.nt, P, d, nsup, splitk,
                 pairs_dev.data_ptr(),
                 part.data_ptr(), 1.0, float(s_h), float(s_l), _ptr(T.scales), out.data_ptr(), _stream(),
-                int(os.environ.get("DQ4ML_WIDE_RING", "4")), int(os.environ.get("DQ4ML_WIDE_WAVES", "8")))
+                int(os.environ.get("DQ4ML_WIDE_RING", "5")), int(os.environ.get("DQ4ML_WIDE_WAVES", "8")))
     return out
