@@ -23,7 +23,7 @@ from concurrent.futures import ThreadPoolExecutor
 
 import torch
 
-__all__ = ["PinnedFile", "open_pinned", "shard_range", "device_bytes_allowed", "clear"]
+__all__ = ["PinnedFile", "open_pinned", "shard_range", "map_readonly", "device_bytes_allowed", "clear"]
 
 MAX_FILES = int(os.environ.get("DQ4ML_FILECACHE_FILES", "2"))
 MAX_BYTES = int(float(os.environ.get("DQ4ML_FILECACHE_BYTES", str(32 << 30))))
@@ -87,6 +87,14 @@ def device_bytes_allowed(nbytes: int) -> bool:
     """Device residency within the cap, counting the cached entries."""
     used = sum(t.numel() for pf in _cache.values() for t in pf._dev.values())
     return used + nbytes <= MAX_DEVICE_BYTES
+
+
+def map_readonly(path: str):
+    """Read-only shared map of a whole file (for ranges larger than the pinned cache)."""
+    import mmap
+
+    with open(path, "rb") as f:
+        return mmap.mmap(f.fileno(), 0, flags=mmap.MAP_SHARED, prot=mmap.PROT_READ)
 
 
 def shard_range(path: str, rank: int, world: int):

@@ -163,13 +163,16 @@ class DataFrameReader:
             # of a sharded read caches (and reads) only its own row-aligned byte range.
             from ..runtime import filecache
 
-            if shard:
-                lo, hi = filecache.shard_range(files[0], rank, world)
+            lo, hi = filecache.shard_range(files[0], rank, world) if shard else (0, os.path.getsize(files[0]))
+            presharded = shard
+            if hi - lo <= filecache.MAX_BYTES:
                 pf = filecache.open_pinned(files[0], lo, hi)
-                presharded = True
+                data, pinned = pf.data, pf.host
             else:
-                pf = filecache.open_pinned(files[0])
-            data, pinned = pf.data, pf.host
+                # larger than the pinned cache may hold: a read-only map, streamed through the
+                # pinned staging ring chunk by chunk (no copy of the whole range is ever made)
+                pf = None
+                data = memoryview(filecache.map_readonly(files[0]))[lo:hi]
         else:
             pf = None
             data = b"".join(self._read_bytes(f) for f in files)

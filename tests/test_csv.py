@@ -211,6 +211,35 @@ def test_pinned_file_cache_chunked_reader_and_file_change(tmp_path):
     spark.stop()
 
 
+@pytest.mark.gpu
+def test_file_larger_than_pinned_cache_streams_from_a_map(tmp_path, monkeypatch):
+    """A file above filecache.MAX_BYTES is never copied whole: a read-only map is streamed
+    through the pinned staging ring, and nothing enters the pinned cache."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from net.jgp.labs.sparkdq4ml_amd import SparkSession
+    from net.jgp.labs.sparkdq4ml_amd.runtime import filecache
+
+    s = SparkSession.getActiveSession()
+    if s is not None:
+        s.stop()
+    filecache.clear()
+    rng = np.random.default_rng(9)
+    n = 50_000
+    g = rng.integers(1, 36, n)
+    pr = np.round(rng.uniform(3, 199, n), 2)
+    p = tmp_path / "big.csv"
+    p.write_bytes("\r".join(f"{int(x)},{float(y)!r}" for x, y in zip(g, pr)).encode())
+    monkeypatch.setattr(filecache, "MAX_BYTES", 1 << 16)
+    spark = SparkSession.builder().master("mi355x[*]").config("dq4ml.csv.deviceThresholdBytes", 0) \
+        .config("dq4ml.chunkBytes", 64 << 10).getOrCreate()
+    t = spark.read().option("inferSchema", "true").csv(str(p))._table()
+    np.testing.assert_array_equal(t.columns[0].values.cpu().numpy(), g)
+    np.testing.assert_array_equal(t.columns[1].values.cpu().numpy(), pr)
+    assert not filecache._cache
+    spark.stop()
+
+
 def test_shard_range_matches_in_memory_sharding(tmp_path):
     """runtime.filecache.shard_range (windowed reads around the cut points) must give exactly the
     byte ranges of ops.csvscan.shard_byte_range (the whole-buffer Hadoop-split rule)."""
