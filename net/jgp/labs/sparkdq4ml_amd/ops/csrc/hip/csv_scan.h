@@ -10,10 +10,12 @@ namespace dq4ml {
 enum CsvTypeCode : int { CT_NULL = 0, CT_INT = 1, CT_LONG = 2, CT_DECIMAL = 3, CT_DOUBLE = 4, CT_BOOL = 5, CT_STRING = 6 };
 
 int64_t csv_count_blocks(int64_t n);
-// counts: csv_count_blocks(n)+1 int64 (exclusive offsets, total at [nb]); ends: total int64 or null
+// Two calls: ends == null -> counts = csv_count_blocks(n)+1 int64 (exclusive per-block offsets,
+// total at [nb]); then ends (total int64) -> the ordered line-end offsets, reusing counts.
 void csv_line_ends(const uint8_t* buf, int64_t n, int64_t* counts, int64_t* ends, hipStream_t st);
+// dcols: ncols device pointers to nlines doubles each; valid: [ncols, nlines]; stats (zeroed):
+// [slow flag, empty lines, null fields per column (ncols), class masks per column (ncols)]
 void csv_parse(const uint8_t* buf, int64_t n, const int64_t* ends, int64_t nlines, int ncols, uint8_t sep,
-               double* dvals, int64_t* ivals, uint8_t* valid, uint8_t* keep, uint32_t* masks, int* flags,
-               hipStream_t st);
+               double* const* dcols, uint8_t* valid, uint8_t* keep, int64_t* stats, hipStream_t st);
 
 }  // namespace dq4ml

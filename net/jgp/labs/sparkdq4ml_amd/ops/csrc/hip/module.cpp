@@ -162,12 +162,10 @@ PYBIND11_MODULE(_dq4ml_hip, m) {
   m.def("csv_line_ends", [](uintptr_t buf, int64_t n, uintptr_t counts, uintptr_t ends, uintptr_t stream) {
     csv_line_ends(P<const uint8_t>(buf), n, P<int64_t>(counts), P<int64_t>(ends), as_stream(stream));
   });
-  m.def("csv_parse", [](uintptr_t buf, int64_t n, uintptr_t ends, int64_t nlines, int ncols, int sep, uintptr_t dvals,
-                        uintptr_t ivals, uintptr_t valid, uintptr_t keep, uintptr_t masks, uintptr_t flags,
-                        uintptr_t stream) {
-    csv_parse(P<const uint8_t>(buf), n, P<const int64_t>(ends), nlines, ncols, (uint8_t)sep, P<double>(dvals),
-              P<int64_t>(ivals), P<uint8_t>(valid), P<uint8_t>(keep), P<uint32_t>(masks), P<int>(flags),
-              as_stream(stream));
+  m.def("csv_parse", [](uintptr_t buf, int64_t n, uintptr_t ends, int64_t nlines, int ncols, int sep, uintptr_t dcols,
+                        uintptr_t valid, uintptr_t keep, uintptr_t stats, uintptr_t stream) {
+    csv_parse(P<const uint8_t>(buf), n, P<const int64_t>(ends), nlines, ncols, (uint8_t)sep, P<double* const>(dcols),
+              P<uint8_t>(valid), P<uint8_t>(keep), P<int64_t>(stats), as_stream(stream));
   });
 
   // ---- fused DQ chains: hipRTC whole-stage codegen ----------------------------------------------

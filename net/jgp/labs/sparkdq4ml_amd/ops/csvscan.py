@@ -66,8 +66,11 @@ def _ncols_of(data, sep: str) -> int:
 
 
 def _scan_chunk(h, buf, n: int, trailing: bool, ncols: int, sep: str, dev):
-    """K1 (line ends) + K2 (parse, type masks) over one device byte buffer; no host sync except
-    the line count."""
+    """K1 (line ends) + K2 (parse, type masks, null / empty-line counts) over one device byte
+    buffer; no host sync except the line count.  Returns (nlines, per-column f64 planes, valid
+    [ncols, m], keep [m], stats) — stats as documented at ``csv_parse`` (csv_scan.h)."""
+    from .device import _h2d
+
     stream = torch.cuda.current_stream(dev).cuda_stream
     nb = int(h.csv_count_blocks(n))
     counts = torch.empty(nb + 1, dtype=torch.int64, device=dev)
@@ -80,66 +83,66 @@ def _scan_chunk(h, buf, n: int, trailing: bool, ncols: int, sep: str, dev):
     if trailing:
         ends[nterm] = n
     m = max(nlines, 1)
-    dvals = torch.empty(ncols, m, dtype=torch.float64, device=dev)
-    ivals = torch.empty(ncols, m, dtype=torch.int64, device=dev)
+    # one exact-size allocation per column: a double column IS its plane (no copy, and no other
+    # column's storage kept alive by it)
+    dcols = [torch.empty(m, dtype=torch.float64, device=dev) for _ in range(ncols)]
+    ptrs = _h2d(np.array([t.data_ptr() for t in dcols], dtype=np.int64), dev)
     valid = torch.empty(ncols, m, dtype=torch.bool, device=dev)
     keep = torch.empty(m, dtype=torch.bool, device=dev)
-    masks = torch.zeros(ncols, dtype=torch.int32, device=dev)
-    flags = torch.zeros(1, dtype=torch.int32, device=dev)
-    h.csv_parse(buf.data_ptr(), n, ends.data_ptr(), nlines, ncols, ord(sep), dvals.data_ptr(), ivals.data_ptr(),
-                valid.data_ptr(), keep.data_ptr(), masks.data_ptr(), flags.data_ptr(), stream)
-    return nlines, dvals, ivals, valid, keep, masks, flags
+    stats = torch.zeros(2 + 2 * ncols, dtype=torch.int64, device=dev)
+    h.csv_parse(buf.data_ptr(), n, ends.data_ptr(), nlines, ncols, ord(sep), ptrs.data_ptr(), valid.data_ptr(),
+                keep.data_ptr(), stats.data_ptr(), stream)
+    return nlines, dcols, valid, keep, stats
 
 
-def _finish(parts, types, dev):
-    """Typed columns from per-chunk parse outputs under the merged types (int -> long -> double
-    widening is exact: the parser flags integers beyond 2^53 for the host path)."""
+def _finish(parts, types, st, dev):
+    """Typed columns from per-chunk parse outputs under the merged types.  ``st``: the chunks'
+    stats on the host.  Int / long / boolean values convert exactly from their f64 planes (the
+    parser flags integers beyond 2^53 for the host path)."""
     from ..sql.localdata import ColumnData
     from ..sql.table import Table
     from ..sql.types import (BooleanType, DoubleType, IntegerType, LongType, StructField, StructType)
 
     fields, cols = [], []
     total = sum(p[0] for p in parts)
+    live = [(k, p) for k, p in enumerate(parts) if p[0]]
     for c, t in enumerate(types):
-        vals_l, valid_l = [], []
-        for nlines, dvals, ivals, valid, _, _, _ in parts:
-            if nlines == 0:
-                continue
-            valid_l.append(valid[c, :nlines])
+        vals_l = []
+        for _, (nlines, dcols, _, _, _) in live:
+            d = dcols[c][:nlines]
             if t == CT_INT:
-                vals_l.append(ivals[c, :nlines].to(torch.int32))
+                d = d.to(torch.int32)
             elif t == CT_LONG:
-                vals_l.append(ivals[c, :nlines])
+                d = d.to(torch.int64)
             elif t == CT_BOOL:
-                vals_l.append(ivals[c, :nlines] != 0)
-            else:
-                vals_l.append(dvals[c, :nlines])
+                d = d != 0
+            vals_l.append(d)
         dt = {CT_INT: IntegerType(), CT_LONG: LongType(), CT_BOOL: BooleanType()}.get(t, DoubleType())
         if vals_l:
-            vals = torch.cat(vals_l) if len(vals_l) > 1 else vals_l[0].clone()
-            v = torch.cat(valid_l) if len(valid_l) > 1 else valid_l[0]
+            vals = torch.cat(vals_l) if len(vals_l) > 1 else vals_l[0]
         else:
             vals = torch.empty(0, dtype=dt.torch_dtype, device=dev)
-            v = torch.ones(0, dtype=torch.bool, device=dev)
-        vv = None if bool(v.all()) else v.clone()
+        vv = None
+        if int(st[:, 2 + c].sum()):  # null fields in this column: materialize its validity
+            valid_l = [p[2][c, :p[0]] for _, p in live]
+            vv = torch.cat(valid_l) if len(valid_l) > 1 else valid_l[0].clone()
         fields.append(StructField(f"_c{c}", dt, True))
         cols.append(ColumnData(dt, vals, vv))
     table = Table(StructType(fields), cols, total, None, dev)
-    keeps = [p[4][:p[0]] for p in parts if p[0]]
-    if total:
+    if total and int(st[:, 1].sum()):  # empty lines are skipped
+        keeps = [p[3][:p[0]] for _, p in live]
         k = torch.cat(keeps) if len(keeps) > 1 else keeps[0]
-        if not bool(k.all()):  # empty lines are skipped
-            table = Table(table.schema, table.columns, total, k.clone(), dev).compact()
+        table = Table(table.schema, table.columns, total, k.clone(), dev).compact()
     return table
 
 
-def _resolve_types(masks, flags, sharded):
+def _resolve_types(masks: np.ndarray, flag: int, sharded: bool):
     if sharded:
-        masks = _or_reduce(masks)
-        flags = comm.all_reduce_max(flags)
-    if int(flags.item()):
+        flag = int(comm.all_reduce_max(torch.tensor([flag], dtype=torch.int64))[0])
+        masks = _or_reduce(torch.from_numpy(masks)).numpy()
+    if flag:
         return None
-    types = [merge_type_mask(m) for m in masks.cpu().numpy().astype(np.int64)]
+    types = [merge_type_mask(int(m)) for m in masks]
     if any(t in (CT_STRING, CT_DECIMAL) for t in types):
         return None
     return types
@@ -185,18 +188,15 @@ def scan_device(data, sep: str = ",", infer: bool = True, device=None, ncols: Op
         parts = [_scan_chunk(h, buf, n, trailing, ncols, sep, dev)]
     else:
         parts = _scan_chunked(h, data, ncols, sep, dev, int(chunk_bytes), pinned)
-    masks = parts[0][5]
-    flags = parts[0][6]
-    for p in parts[1:]:
-        masks = masks | p[5]
-        flags = torch.maximum(flags, p[6])
-    types = _resolve_types(masks, flags, sharded)
+    st = torch.stack([p[4] for p in parts]).cpu().numpy()  # the one host read of the parse results
+    masks = np.bitwise_or.reduce(st[:, 2 + ncols:], axis=0)
+    types = _resolve_types(masks, int(st[:, 0].max()), sharded)
     if types is None:
         STATS["fallbacks"] += 1
         return None
     STATS["device_scans"] += 1
     STATS["chunks"] = STATS.get("chunks", 0) + len(parts)
-    return _finish(parts, types, dev)
+    return _finish(parts, types, st, dev)
 
 
 def chunk_bounds(data: bytes, chunk_bytes: int):
