@@ -279,11 +279,49 @@ __device__ __forceinline__ bool parse_line(PB B, int64_t bias, int64_t n, const 
     int64_t iv = 0;
     int ty = CT_NULL;
     if (pos <= end && line) {
+      // fast path, ONE walk over the bytes: [+-]digits[.digits] with at most 9 digits, ended by
+      // the separator or the line end — exact in 32-bit integer math, and the f64 value
+      // m / 10^frac is correctly rounded (Clinger).  Anything else re-walks the field in the
+      // general parser.
       int64_t q = pos;
-      while (q < end && B[q - bias] != sep) ++q;
-      const int64_t flen = q - pos;
-      if (flen > 0 && (B[pos - bias] == '"' || B[pos - bias] == '\\')) slow = true;
-      ty = parse_field(&B[pos - bias], (int)(flen > 1 << 20 ? 1 << 20 : flen), dv, iv, slow);
+      bool neg = false;
+      if (q < end) {
+        const int c0 = B[q - bias];
+        neg = c0 == '-';
+        q += (c0 == '-' || c0 == '+') ? 1 : 0;
+      }
+      uint32_t m = 0;
+      int nd = 0, fr = 0;
+      bool dot = false, bad = false;
+      for (; q < end; ++q) {
+        const int ch = B[q - bias];
+        const uint32_t d = (uint32_t)(ch - '0');
+        if (d < 10u) {
+          m = m * 10u + d;
+          ++nd;
+          fr += dot ? 1 : 0;
+        } else if (ch == '.' && !dot) {
+          dot = true;
+        } else {
+          bad = ch != sep;
+          break;
+        }
+      }
+      if (!bad && nd > 0 && nd <= 9) {
+        ty = dot ? CT_DOUBLE : CT_INT;
+        if (dot) {
+          dv = (double)m / kPow10[fr];
+          dv = neg ? -dv : dv;
+        } else {
+          dv = (double)(neg ? -(int64_t)m : (int64_t)m);  // -0 is +0.0 for integers
+        }
+      } else {
+        q = pos;
+        while (q < end && B[q - bias] != sep) ++q;
+        const int64_t flen = q - pos;
+        if (flen > 0 && (B[pos - bias] == '"' || B[pos - bias] == '\\')) slow = true;
+        ty = parse_field(&B[pos - bias], (int)(flen > 1 << 20 ? 1 << 20 : flen), dv, iv, slow);
+      }
       pos = q + 1;
     }
     const bool ok = ty != CT_NULL && ty != CT_STRING;

@@ -17,7 +17,37 @@ CASES = {
     "nulls": b"1,,3\n,2.5,\n",
     "bools": b"true,1\nFALSE,2\n",
     "special": b"NaN,1\n-Infinity,2\n1.5d,3\n",
+    # the parser's one-walk fast path ([+-]digits[.digits], <= 9 digits) and its edges
+    "fast_path_edges": b"-0,+5,007\n.5,5.,-.5\n123456789,1234567890,0.000000001\n-0.0,99999.9999,-123.456789\n",
+    "fast_path_strings": b"-,1\n+,2\n",
+    "fast_path_dots": b"1..2,3\n4,5\n",
 }
+
+
+def _fuzz_numeric(seed=11, rows=3000):
+    """Random numeric tokens around the fast path's limits (digit counts 1..15, signs, dots,
+    exponents, leading zeros) — all inside the device parser's exact range, so no host fallback —
+    checked against the host scanner."""
+    import random
+
+    rnd = random.Random(seed)
+
+    def tok():
+        nd = rnd.choice([1, 2, 3, 8, 9, 10, 12, 15])
+        digits = "".join(rnd.choice("0123456789") for _ in range(nd))
+        sign = rnd.choice(["", "", "-", "+"])
+        k = rnd.random()
+        if k < 0.35:
+            return sign + digits
+        if k < 0.85:
+            d = rnd.randint(0, nd)
+            return sign + digits[:d] + "." + digits[d:] if nd > 0 else sign + "0.5"
+        return sign + digits[:3] + "e" + str(rnd.randint(-7, 7))
+
+    return "\n".join(",".join(tok() for _ in range(3)) for _ in range(rows)).encode()
+
+
+CASES["fuzz_numeric"] = _fuzz_numeric()
 
 
 def _host(data, infer=True):
