@@ -36,33 +36,42 @@ namespace {
 constexpr int kBytesPerThread = 64;
 constexpr int kChunk = 256 * kBytesPerThread;  // bytes per block
 
-// terminator bitmask of the thread's 64-byte window; window byte k <-> buffer index base + k
+// 4-bit mask of the bytes of v equal to the byte in every lane of pat (SWAR: exact per byte —
+// no borrow crosses bytes — then the four 0x80 flags gathered to bits 0..3 by one multiply)
+__device__ __forceinline__ uint32_t byte_eq4(uint32_t v, uint32_t pat) {
+  const uint32_t x = v ^ pat;
+  const uint32_t z = ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x | 0x7F7F7F7Fu);
+  return (((z >> 7) * 0x00204081u) >> 21) & 0xFu;
+}
+
+// terminator bitmask of the thread's 64-byte window; window byte k <-> buffer index base + k.
+// Terminators: \r, and \n not preceded by \r (CR LF is one terminator, at the CR).
 __device__ __forceinline__ uint64_t term_mask(const uint8_t* __restrict__ b, int64_t n, int64_t base) {
   const uint8_t* ab = b - (reinterpret_cast<uintptr_t>(b) & 15);  // granule-aligned view
   const int64_t off = b - ab;                                    // 0..15
   const int64_t g0 = base + off;                                  // aligned position of window byte 0
-  // the byte before the window (for CR LF)
-  uint32_t prev = (base >= 1 && base - 1 < n) ? b[base - 1] : 0u;
-  uint64_t m = 0;
+  uint64_t cr = 0, lf = 0;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int64_t ga = g0 + 16 * j;  // aligned, multiple of 16
-    if (ga - off >= n || ga - off + 16 <= 0) {
-      prev = 0;
-      continue;
-    }
+    if (ga - off >= n || ga - off + 16 <= 0) continue;
     const u32x4 v = *reinterpret_cast<const u32x4*>(ab + ga);
 #pragma unroll
-    for (int k = 0; k < 16; ++k) {
-      const uint32_t c = (v[k >> 2] >> (8 * (k & 3))) & 0xffu;
-      const int64_t i = ga - off + k;
-      const bool inb = i >= 0 && i < n;
-      const bool t = inb && (c == '\r' || (c == '\n' && prev != '\r'));
-      m |= (uint64_t)t << (16 * j + k);
-      prev = inb ? c : 0u;
+    for (int w = 0; w < 4; ++w) {
+      cr |= (uint64_t)byte_eq4(v[w], 0x0D0D0D0Du) << (16 * j + 4 * w);
+      lf |= (uint64_t)byte_eq4(v[w], 0x0A0A0A0Au) << (16 * j + 4 * w);
     }
   }
-  return m;
+  // bytes outside [0, n) of the edge windows
+  const int64_t lo = base < 0 ? -base : 0, hi = n - base;
+  if (lo > 0 || hi < 64) {
+    const uint64_t keep_lo = lo >= 64 ? 0ull : (~0ull << lo);
+    const uint64_t keep_hi = hi <= 0 ? 0ull : (hi >= 64 ? ~0ull : ((1ull << hi) - 1));
+    cr &= keep_lo & keep_hi;
+    lf &= keep_lo & keep_hi;
+  }
+  const uint64_t prev_cr = (base >= 1 && base - 1 < n && b[base - 1] == '\r') ? 1ull : 0ull;
+  return cr | (lf & ~((cr << 1) | prev_cr));
 }
 
 __global__ __launch_bounds__(256) void csv_count_kernel(const uint8_t* __restrict__ b, int64_t n,
@@ -118,12 +127,18 @@ __global__ __launch_bounds__(1024) void csv_scan_counts_kernel(int64_t* __restri
   if (threadIdx.x == 0) counts[nb] = carry;
 }
 
+constexpr int kEndsStage = 8192;  // line ends per block staged in LDS (block-relative int32)
+
+// Each thread finds its window's line ends; a block with at most kEndsStage of them collects them
+// in LDS (in order) and writes them out as one coalesced run — per-thread direct stores put 64
+// lanes on 64 different cache lines per instruction.
 __global__ __launch_bounds__(256) void csv_ends_kernel(const uint8_t* __restrict__ b, int64_t n,
                                                       const int64_t* __restrict__ offsets, int64_t* __restrict__ ends) {
   __shared__ int wtot[4];
+  __shared__ int sends[kEndsStage];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int64_t base = (int64_t)blockIdx.x * kChunk + (int64_t)threadIdx.x * kBytesPerThread -
-                       (int64_t)(reinterpret_cast<uintptr_t>(b) & 15);
+  const int64_t bbase = (int64_t)blockIdx.x * kChunk - (int64_t)(reinterpret_cast<uintptr_t>(b) & 15);
+  const int64_t base = bbase + (int64_t)threadIdx.x * kBytesPerThread;
   uint64_t m = term_mask(b, n, base);
   const int c = __popcll(m);
   // exclusive prefix of the per-thread counts: wave scan (shfl_up) + wave totals in LDS
@@ -137,11 +152,23 @@ __global__ __launch_bounds__(256) void csv_ends_kernel(const uint8_t* __restrict
   __syncthreads();
   int before = inc - c;
   for (int w = 0; w < wave; ++w) before += wtot[w];
-  int64_t o = offsets[blockIdx.x] + before;
-  while (m) {
-    const int k = __builtin_ctzll(m);
-    ends[o++] = base + k;
-    m &= m - 1;
+  const int64_t o0 = offsets[blockIdx.x];
+  const int cnt = (int)(offsets[blockIdx.x + 1] - o0);  // offsets[nb] is the total
+  if (cnt <= kEndsStage) {
+    int o = before;
+    const int rel = threadIdx.x * kBytesPerThread;
+    while (m) {
+      sends[o++] = rel + __builtin_ctzll(m);
+      m &= m - 1;
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < cnt; i += blockDim.x) ends[o0 + i] = bbase + sends[i];
+  } else {
+    int64_t o = o0 + before;
+    while (m) {
+      ends[o++] = base + __builtin_ctzll(m);
+      m &= m - 1;
+    }
   }
 }
 
