@@ -113,6 +113,14 @@ class VectorAssembleExpr(Expr):
             with tracing.span("pack"):
                 mat = kernels.pack_wide(parts, 8 if dt == torch.float8_e4m3fn else 16, ctx.table.sel)
             meta = {"ml_attr": {"num_attrs": d}, "zero_dead": ctx.table.sel}
+        elif on_dev and dt == torch.float64 and d <= 8:
+            # narrow f64 assembly, produced lazily too: the f64 normal-equation statistics read
+            # the source columns directly (gram_skinny_cols); other consumers pack on first use
+            def _pack(parts=parts, dt=dt):
+                with tracing.span("pack"):
+                    return kernels.pack_columns(parts, dt)
+            return LazyVectorColumn(VectorUDT(), _pack, int(parts[0].shape[-1]), (parts, ctx.table.sel),
+                                    {"ml_attr": {"num_attrs": d}})
         elif dt == torch.float8_e4m3fn:  # host engine: fp8 storage is a device layout; keep fp32
             mat = kernels.pack_columns(parts, torch.float32)
             meta = {"ml_attr": {"num_attrs": int(mat.shape[0])}}

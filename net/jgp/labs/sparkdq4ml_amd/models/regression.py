@@ -194,6 +194,8 @@ class LinearRegression(_LRParams):
             if _fusable_assembly(X, w, gd, yvalid):
                 parts, asel = X.sources  # fused VectorAssembler + Gram: the features are never packed
                 flat = kernels.gram_cols(parts, yv, sel if sel is not None else asel)
+            elif _skinny_cols(X, gd):
+                flat = kernels.gram_skinny_cols(X.sources[0], yv, w, sel)  # f64, no pack
             else:
                 # a single-GPU overlapped asynchronous fit folds the Gram partials on its side
                 # stream too.  Not with N > 1: co-running with the next Gram pass the fold's loads
@@ -253,6 +255,18 @@ def _fusable_assembly(X, w, gram_dtype, yvalid) -> bool:
     parts, _ = X.sources
     return all(p.is_cuda and p.dtype in (torch.float32, torch.float64, torch.bfloat16, torch.int32, torch.int64,
                                           torch.bool, torch.uint8) for p in parts)
+
+
+def _skinny_cols(X, gram_dtype) -> bool:
+    """f64 statistics of a lazily assembled narrow vector, straight from its source columns."""
+    from ..sql.table import LazyVectorColumn
+
+    if not isinstance(X, LazyVectorColumn) or X.materialized or gram_dtype != "fp64":
+        return False
+    parts, _ = X.sources
+    d = sum(1 if p.dim() == 1 else int(p.shape[0]) for p in parts)
+    return 1 <= d <= 8 and all(p.is_cuda and p.dtype in (torch.float32, torch.float64, torch.bfloat16, torch.int32,
+                                                         torch.int64, torch.bool, torch.uint8) for p in parts)
 
 
 def _rank_health(df):

@@ -24,6 +24,11 @@ struct GramArgs {
   int64_t spw;         // supersteps (64 rows) per wave
   int64_t nsuper;      // n / 64
   int tiled;           // X is MFMA-fragment-ordered bf16 (tile_bf16 layout)
+  // columnar skinny f64 mode (cols = d <= 8, X unused): feature f is the source column colp[f]
+  // of DType coldt[f] — a VectorAssembler output read straight from its inputs, never packed
+  const void* colp[8];
+  int coldt[8];
+  int cols;
 };
 
 // MFMA-fragment-ordered bf16 feature storage ("tiled"): for superstep s (64 rows), 32-feature

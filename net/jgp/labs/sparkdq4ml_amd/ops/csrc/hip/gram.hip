@@ -808,7 +808,7 @@ __global__ __launch_bounds__(kBlock) void gram_tall_f64_kernel(GramArgs a) {
 // zeros, their garbage never enters a product), 4 rows in flight per thread.  Slab layout = the
 // f64 MFMA kernel's (16 x 16 tile), so the slab fold is shared.
 // =============================================================================================
-template <typename TX, int D>
+template <typename TX, int D, bool COLS = false>
 __global__ __launch_bounds__(kBlock) void gram_skinny_f64_kernel(GramArgs a) {
   constexpr int NA = D * (D + 1) / 2;
   constexpr int NV = 5 + 2 * D + NA;
@@ -831,7 +831,13 @@ __global__ __launch_bounds__(kBlock) void gram_skinny_f64_kernel(GramArgs a) {
       yv[u] = load_as_f64(a.y, a.ydt, rc);
       wv[u] = a.w ? load_as_f64(a.w, a.wdt, rc) : 1.0;
 #pragma unroll
-      for (int f = 0; f < D; ++f) x[u][f] = (double)X[(int64_t)f * a.ld + rc];
+      for (int f = 0; f < D; ++f) {
+        if constexpr (COLS) {
+          x[u][f] = load_as_f64(a.colp[f], a.coldt[f], rc);  // wave-uniform dtype switch
+        } else {
+          x[u][f] = (double)X[(int64_t)f * a.ld + rc];
+        }
+      }
     }
 #pragma unroll
     for (int u = 0; u < UNR; ++u) {
@@ -1105,6 +1111,20 @@ static void with_skinny(int xdt, int d, F&& f) {
   throw std::invalid_argument("gram_skinny: unsupported feature dtype");
 }
 
+template <typename F>
+static void with_skinny_cols(int d, F&& f) {
+  switch (d) {
+    case 1: return f(gram_skinny_f64_kernel<double, 1, true>);
+    case 2: return f(gram_skinny_f64_kernel<double, 2, true>);
+    case 3: return f(gram_skinny_f64_kernel<double, 3, true>);
+    case 4: return f(gram_skinny_f64_kernel<double, 4, true>);
+    case 5: return f(gram_skinny_f64_kernel<double, 5, true>);
+    case 6: return f(gram_skinny_f64_kernel<double, 6, true>);
+    case 7: return f(gram_skinny_f64_kernel<double, 7, true>);
+    default: return f(gram_skinny_f64_kernel<double, 8, true>);
+  }
+}
+
 static bool use_skinny(int mode, int d, int xdt, int tiled) {
   return mode == GRAM_F64 && !tiled && d <= kSkinnyMaxD && (xdt == DT_F64 || xdt == DT_F32);
 }
@@ -1150,7 +1170,11 @@ void gram_tall(int mode, GramArgs a, int xmode, int blocks, double* out, hipStre
   a.P = (int)gram_partial_stride(mode, a.d);
   const size_t lds = mode == GRAM_BF16 ? bf16_lds(a.d, xmode) : f64_lds(a.d);
   if (a.tiled && mode != GRAM_BF16) throw std::invalid_argument("gram_tall: tiled storage needs bf16 mode");
-  if (use_skinny(mode, a.d, a.xdt, a.tiled)) {
+  if (a.cols > 0) {
+    if (mode != GRAM_F64 || a.cols != a.d || a.d > kSkinnyMaxD || a.tiled)
+      throw std::invalid_argument("gram_tall: columnar sources need f64 mode and d <= 8");
+    with_skinny_cols(a.d, [&](auto kern) { hipLaunchKernelGGL(kern, dim3(blocks), dim3(kBlock), 0, st, a); });
+  } else if (use_skinny(mode, a.d, a.xdt, a.tiled)) {
     with_skinny(a.xdt, a.d, [&](auto kern) { hipLaunchKernelGGL(kern, dim3(blocks), dim3(kBlock), 0, st, a); });
   } else {
     with_kernel(mode, a.xdt, a.d, xmode, a.tiled != 0,

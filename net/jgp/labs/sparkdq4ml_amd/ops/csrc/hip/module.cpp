@@ -61,6 +61,28 @@ PYBIND11_MODULE(_dq4ml_hip, m) {
           a.partials = P<double>(partials);
           gram_tall(mode, a, xmode, blocks, P<double>(out), as_stream(stream), reduce);
         });
+  m.def("gram_skinny_cols",
+        [](const std::vector<uintptr_t>& cols, const std::vector<int>& dts, int64_t n, uintptr_t y, int ydt,
+           uintptr_t w, int wdt, uintptr_t sel, uintptr_t partials, int blocks, uintptr_t out, uintptr_t stream) {
+          const int d = (int)cols.size();
+          if (d < 1 || d > 8 || (int)dts.size() != d) throw std::invalid_argument("gram_skinny_cols: 1 <= d <= 8");
+          GramArgs a{};
+          for (int f = 0; f < d; ++f) {
+            a.colp[f] = P<const void>(cols[f]);
+            a.coldt[f] = dts[f];
+          }
+          a.cols = d;
+          a.d = d;
+          a.n = n;
+          a.xdt = DT_F64;
+          a.y = P<const void>(y);
+          a.ydt = ydt;
+          a.w = P<const void>(w);
+          a.wdt = wdt;
+          a.sel = P<const uint8_t>(sel);
+          a.partials = P<double>(partials);
+          gram_tall(GRAM_F64, a, w ? 2 : (sel ? 1 : 0), blocks, P<double>(out), as_stream(stream), true);
+        });
   m.def("gram_reduce", [](int mode, uintptr_t partials, int blocks, int d, uintptr_t out, uintptr_t stream) {
     gram_reduce(mode, P<const double>(partials), blocks, d, P<double>(out), as_stream(stream));
   });

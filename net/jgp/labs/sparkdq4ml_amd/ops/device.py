@@ -185,6 +185,36 @@ def gram_stats(X, y, w, sel, compute: str = "fp64", x_zero_dead: bool = False, b
     return out
 
 
+def gram_skinny_cols(parts: List[torch.Tensor], y, w, sel, blocks: Optional[int] = None):
+    """f64 WLS statistics of a narrow (d <= 8) VectorAssembler output straight from its SOURCE
+    columns (any of f64/f32/bf16/int32/int64/bool, mixed): the assembled [d, n] f64 matrix is
+    never written — for the lab's ``features = [guest]`` that is an int32 column read in place of
+    a 0.8 GB f64 pack (``gram.hip: gram_skinny_f64_kernel<.., COLS>``)."""
+    h = native.hip()
+    rows = _rows_of(parts)
+    d, n = len(rows), rows[0].numel()
+    if not 1 <= d <= 8:
+        raise ValueError("gram_skinny_cols: 1 <= d <= 8")
+    for r in rows:
+        _check_dev(r)
+        if r.numel() != n:
+            raise ValueError("gram_skinny_cols: columns of different lengths")
+    dev = rows[0].device
+    y, w, sel = _prep_rows(y, w, sel, n)
+    out = torch.empty(5 + 2 * d + d * (d + 1) // 2, dtype=torch.float64, device=dev)
+    if n == 0:
+        out.zero_()
+        return out
+    xmode = 2 if w is not None else (1 if sel is not None else 0)
+    nb = int(blocks or _plan_blocks(h, 0, d, n, 0, xmode))
+    P = int(h.gram_partial_stride(0, d))
+    partials = torch.empty(nb * P, dtype=torch.float64, device=dev)
+    h.gram_skinny_cols([r.data_ptr() for r in rows], [dtype_code(r) for r in rows], int(n), y.data_ptr(),
+                       dtype_code(y), _ptr(w), dtype_code(w) if w is not None else 0, _ptr(sel),
+                       partials.data_ptr(), nb, out.data_ptr(), _stream())
+    return out
+
+
 def gram_cols(parts: List[torch.Tensor], y, sel, blocks: Optional[int] = None):
     """Fused VectorAssembler + bf16 Gram over the SOURCE columns (d <= 64, unit weights): the
     assembled matrix is never written (``gram.hip: gram_cols_kernel``)."""

@@ -72,6 +72,14 @@ def gram_cols(parts: Sequence[torch.Tensor], y: torch.Tensor, sel: Optional[torc
     return device.gram_cols(list(parts), y, sel)
 
 
+def gram_skinny_cols(parts: Sequence[torch.Tensor], y: torch.Tensor, w: Optional[torch.Tensor] = None,
+                     sel: Optional[torch.Tensor] = None):
+    """GPU only: f64 statistics of a narrow (d <= 8) assembly read from its source columns."""
+    from . import device
+
+    return device.gram_skinny_cols(list(parts), y, w, sel)
+
+
 def pack_wide(parts: Sequence[torch.Tensor], eb: int, sel: Optional[torch.Tensor] = None):
     """GPU only: columns -> wide (d > 64) fragment layout, bf16 (eb 16) or fp8 e4m3 with
     per-feature scales (eb 8) (``ops.layout.TiledWide``); rows outside ``sel`` become zeros."""

@@ -93,6 +93,31 @@ def test_gram_f64_skinny_selection_weights_and_dead_nans(d, xdt):
     assert _rel(out, _ref_stats(X.double(), y, None, None)) < 1e-12
 
 
+@pytest.mark.parametrize("d", [1, 4, 8])
+def test_gram_skinny_cols_reads_mixed_source_columns(d):
+    """Narrow f64 statistics straight from the assembler's source columns (int32 / f32 / f64 /
+    bool / int64 mixed, one [2, n] vector part): equal to the stats of the packed f64 matrix."""
+    g = torch.Generator(device="cuda").manual_seed(300 + d)
+    n = 99_991
+    pool = [
+        lambda: torch.randint(1, 36, (n,), generator=g, device="cuda", dtype=torch.int32),
+        lambda: torch.randn(n, generator=g, device="cuda") * 3,
+        lambda: torch.randn(n, generator=g, device="cuda", dtype=torch.float64) + 1,
+        lambda: torch.rand(n, generator=g, device="cuda") > 0.5,
+        lambda: torch.randint(-9, 9, (n,), generator=g, device="cuda", dtype=torch.int64),
+    ]
+    parts = [pool[i % len(pool)]() for i in range(d)]
+    if d >= 4:  # a vector-valued part: two feature rows of one [2, n] tensor
+        parts = parts[:d - 2] + [torch.randn(2, n, generator=g, device="cuda", dtype=torch.float64)]
+    X = torch.cat([p.reshape(-1, n).double() for p in parts])
+    y = torch.randn(n, generator=g, device="cuda", dtype=torch.float64)
+    sel = torch.rand(n, generator=g, device="cuda") > 0.3
+    w = torch.rand(n, generator=g, device="cuda", dtype=torch.float64) + 0.5
+    for ww, ss in ((None, None), (None, sel), (w, sel)):
+        out = device.gram_skinny_cols(parts, y, ww, ss)
+        assert _rel(out, _ref_stats(X, y, ww, ss)) < 1e-12
+
+
 @pytest.mark.parametrize("d", [3, 20, 32, 64])
 def test_gram_fp32_mode_uses_f64_kernel_on_f32_features(d):
     """gramDtype fp32: f32 features through the f64 MFMA kernel (exact f32 products, f64 sums)."""
