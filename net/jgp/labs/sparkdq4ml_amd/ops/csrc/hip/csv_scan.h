@@ -13,9 +13,10 @@ int64_t csv_count_blocks(int64_t n);
 // Two calls: ends == null -> counts = csv_count_blocks(n)+1 int64 (exclusive per-block offsets,
 // total at [nb]); then ends (total int64) -> the ordered line-end offsets, reusing counts.
 void csv_line_ends(const uint8_t* buf, int64_t n, int64_t* counts, int64_t* ends, hipStream_t st);
-// dcols: ncols device pointers to nlines doubles each; valid: [ncols, nlines]; stats (zeroed):
+// dcols: [2 * ncols] int64 — ncols device pointers to nlines values each, then ncols storage
+// kinds (0 f64, 1 int32, 2 int64, 3 bool/uint8); valid: [ncols, nlines]; stats (zeroed):
 // [slow flag, empty lines, null fields per column (ncols), class masks per column (ncols)]
 void csv_parse(const uint8_t* buf, int64_t n, const int64_t* ends, int64_t nlines, int ncols, uint8_t sep,
-               double* const* dcols, uint8_t* valid, uint8_t* keep, int64_t* stats, hipStream_t st);
+               const int64_t* dcols, uint8_t* valid, uint8_t* keep, int64_t* stats, hipStream_t st);
 
 }  // namespace dq4ml

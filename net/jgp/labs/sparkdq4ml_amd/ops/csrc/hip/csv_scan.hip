@@ -284,7 +284,7 @@ constexpr int kParseLds = 32768;  // staged bytes per 256-line group
 template <typename PB>
 __device__ __forceinline__ bool parse_line(PB B, int64_t bias, int64_t n, const int64_t* __restrict__ ends,
                                            int64_t li, bool active, int64_t nlines, int ncols, uint8_t sep,
-                                           double* const* __restrict__ dcols, uint8_t* __restrict__ valid,
+                                           const int64_t* __restrict__ dcols, uint8_t* __restrict__ valid,
                                            uint8_t* __restrict__ keep, uint32_t* smask, int* snull, int* sempty) {
   const bool lane0 = (threadIdx.x & 63) == 0;
   int64_t start = 0, end = 0;
@@ -353,9 +353,17 @@ __device__ __forceinline__ bool parse_line(PB B, int64_t bias, int64_t n, const 
     }
     const bool ok = ty != CT_NULL && ty != CT_STRING;
     if (active) {
-      // ints / longs / booleans are stored as their (exact: |v| <= 2^53, else ``slow``) double
-      // value — one 8-byte plane per column; the host converts once the column type is known
-      dcols[c][li] = dv;
+      // one plane per column: f64 by default — ints / longs / booleans as their (exact:
+      // |v| <= 2^53, else ``slow``) double value, converted once the column type is known — or,
+      // when the host knows the type from an earlier scan of the same bytes, stored as that
+      // type directly (kind = dcols[ncols + c]; a mismatch is detected from the masks)
+      void* dst = reinterpret_cast<void*>(dcols[c]);
+      switch ((int)dcols[ncols + c]) {
+        case 1: reinterpret_cast<int32_t*>(dst)[li] = ok ? (int32_t)dv : 0; break;
+        case 2: reinterpret_cast<int64_t*>(dst)[li] = ok ? (int64_t)dv : 0; break;
+        case 3: reinterpret_cast<uint8_t*>(dst)[li] = dv != 0.0; break;
+        default: reinterpret_cast<double*>(dst)[li] = dv;
+      }
       valid[(int64_t)c * nlines + li] = ok;
     }
     uint32_t bit = line ? (1u << ty) : 0u;
@@ -377,7 +385,7 @@ __device__ __forceinline__ bool parse_line(PB B, int64_t bias, int64_t n, const 
 // groups (very wide rows) parse straight from global memory.
 __global__ __launch_bounds__(256) void csv_parse_kernel(const uint8_t* __restrict__ b, int64_t n,
                                                        const int64_t* __restrict__ ends, int64_t nlines, int ncols,
-                                                       uint8_t sep, double* const* __restrict__ dcols,
+                                                       uint8_t sep, const int64_t* __restrict__ dcols,
                                                        uint8_t* __restrict__ valid, uint8_t* __restrict__ keep,
                                                        unsigned long long* __restrict__ stats) {
   __shared__ uint32_t smask[kMaxCols];
@@ -449,7 +457,7 @@ void csv_line_ends(const uint8_t* buf, int64_t n, int64_t* counts, int64_t* ends
 }
 
 void csv_parse(const uint8_t* buf, int64_t n, const int64_t* ends, int64_t nlines, int ncols, uint8_t sep,
-               double* const* dcols, uint8_t* valid, uint8_t* keep, int64_t* stats, hipStream_t st) {
+               const int64_t* dcols, uint8_t* valid, uint8_t* keep, int64_t* stats, hipStream_t st) {
   if (ncols > kMaxCols) throw std::invalid_argument("csv_parse: too many columns for the device scanner");
   if (nlines <= 0) return;
   int64_t g = (nlines + 255) / 256;

@@ -186,7 +186,7 @@ PYBIND11_MODULE(_dq4ml_hip, m) {
   });
   m.def("csv_parse", [](uintptr_t buf, int64_t n, uintptr_t ends, int64_t nlines, int ncols, int sep, uintptr_t dcols,
                         uintptr_t valid, uintptr_t keep, uintptr_t stats, uintptr_t stream) {
-    csv_parse(P<const uint8_t>(buf), n, P<const int64_t>(ends), nlines, ncols, (uint8_t)sep, P<double* const>(dcols),
+    csv_parse(P<const uint8_t>(buf), n, P<const int64_t>(ends), nlines, ncols, (uint8_t)sep, P<const int64_t>(dcols),
               P<uint8_t>(valid), P<uint8_t>(keep), P<int64_t>(stats), as_stream(stream));
   });
 

@@ -65,7 +65,10 @@ def _ncols_of(data, sep: str) -> int:
         w *= 16
 
 
-def _scan_chunk(h, buf, n: int, trailing: bool, ncols: int, sep: str, dev):
+_KIND = {CT_INT: (1, torch.int32), CT_LONG: (2, torch.int64), CT_BOOL: (3, torch.bool)}
+
+
+def _scan_chunk(h, buf, n: int, trailing: bool, ncols: int, sep: str, dev, hint=None):
     """K1 (line ends) + K2 (parse, type masks, null / empty-line counts) over one device byte
     buffer; no host sync except the line count.  Returns (nlines, per-column f64 planes, valid
     [ncols, m], keep [m], stats) — stats as documented at ``csv_parse`` (csv_scan.h)."""
@@ -83,10 +86,11 @@ def _scan_chunk(h, buf, n: int, trailing: bool, ncols: int, sep: str, dev):
     if trailing:
         ends[nterm] = n
     m = max(nlines, 1)
-    # one exact-size allocation per column: a double column IS its plane (no copy, and no other
-    # column's storage kept alive by it)
-    dcols = [torch.empty(m, dtype=torch.float64, device=dev) for _ in range(ncols)]
-    ptrs = _h2d(np.array([t.data_ptr() for t in dcols], dtype=np.int64), dev)
+    # one exact-size allocation per column: a column IS its plane (no copy, and no other
+    # column's storage kept alive by it) — f64, or the hinted type (see scan_device)
+    kinds = [_KIND.get(t, (0, torch.float64)) for t in (hint or [CT_DOUBLE] * ncols)]
+    dcols = [torch.empty(m, dtype=dt, device=dev) for _, dt in kinds]
+    ptrs = _h2d(np.array([t.data_ptr() for t in dcols] + [k for k, _ in kinds], dtype=np.int64), dev)
     valid = torch.empty(ncols, m, dtype=torch.bool, device=dev)
     keep = torch.empty(m, dtype=torch.bool, device=dev)
     stats = torch.zeros(2 + 2 * ncols, dtype=torch.int64, device=dev)
@@ -95,7 +99,20 @@ def _scan_chunk(h, buf, n: int, trailing: bool, ncols: int, sep: str, dev):
     return nlines, dcols, valid, keep, stats
 
 
-def _finish(parts, types, st, dev):
+def type_code_of(dt) -> int:
+    """Lattice code of a device-scanned column's type (the reader's types_hint)."""
+    from ..sql.types import BooleanType, IntegerType, LongType
+
+    if isinstance(dt, IntegerType):
+        return CT_INT
+    if isinstance(dt, LongType):
+        return CT_LONG
+    if isinstance(dt, BooleanType):
+        return CT_BOOL
+    return CT_DOUBLE
+
+
+def _finish(parts, types, st, dev, hinted=False):
     """Typed columns from per-chunk parse outputs under the merged types.  ``st``: the chunks'
     stats on the host.  Int / long / boolean values convert exactly from their f64 planes (the
     parser flags integers beyond 2^53 for the host path)."""
@@ -110,7 +127,9 @@ def _finish(parts, types, st, dev):
         vals_l = []
         for _, (nlines, dcols, _, _, _) in live:
             d = dcols[c][:nlines]
-            if t == CT_INT:
+            if hinted:  # stored as the column's type already
+                pass
+            elif t == CT_INT:
                 d = d.to(torch.int32)
             elif t == CT_LONG:
                 d = d.to(torch.int64)
@@ -150,11 +169,15 @@ def _resolve_types(masks: np.ndarray, flag: int, sharded: bool):
 
 def scan_device(data, sep: str = ",", infer: bool = True, device=None, ncols: Optional[int] = None,
                 sharded: bool = False, chunk_bytes: Optional[int] = None, pinned: Optional[torch.Tensor] = None,
-                device_data: Optional[torch.Tensor] = None):
+                device_data: Optional[torch.Tensor] = None, types_hint: Optional[list] = None):
     """Parse ``data`` on the device.  Inputs larger than ``chunk_bytes`` stream through a
     double-buffered pinned staging ring: chunk k+1's host->device copy runs on a side stream while
     chunk k is parsed, chunks split on row boundaries, type masks OR-merged over
-    chunks (and ranks when ``sharded``)."""
+    chunks (and ranks when ``sharded``).
+
+    ``types_hint``: column type codes from an earlier scan of the same bytes (the reader keeps
+    them with its cached file): the parser then stores every column as its type directly — no
+    f64 plane to convert.  Inference still runs; a hint the masks contradict re-scans unhinted."""
     # quotes / escapes need the host scanner: the parse kernel flags any field that starts with
     # one (slow path) and a mid-field one makes the column a string — both fall back, so the
     # input is never pre-scanned on the host
@@ -166,6 +189,7 @@ def scan_device(data, sep: str = ",", infer: bool = True, device=None, ncols: Op
         ncols = _ncols_of(data, sep)
     if ncols > 256:
         return None
+    hint = list(types_hint) if types_hint is not None and len(types_hint) == ncols else None
     n = len(data)
     if device_data is not None and n > 0:
         # input bytes already resident in HBM (runtime.filecache): chunks are plain slices —
@@ -177,7 +201,7 @@ def scan_device(data, sep: str = ",", infer: bool = True, device=None, ncols: Op
         parts = []
         for s, e in zip(bounds, bounds[1:]):
             trailing = data[e - 1] not in (10, 13)
-            parts.append(_scan_chunk(h, device_data[s:e], e - s, trailing, ncols, sep, dev))
+            parts.append(_scan_chunk(h, device_data[s:e], e - s, trailing, ncols, sep, dev, hint))
     elif chunk_bytes is None or n <= chunk_bytes:
         if pinned is not None and n:
             buf = pinned.to(dev, non_blocking=True)  # page-locked mapping: direct DMA
@@ -185,18 +209,24 @@ def scan_device(data, sep: str = ",", infer: bool = True, device=None, ncols: Op
             host = torch.frombuffer(bytearray(data), dtype=torch.uint8) if n else torch.zeros(0, dtype=torch.uint8)
             buf = host.pin_memory().to(dev, non_blocking=True) if n else torch.zeros(1, dtype=torch.uint8, device=dev)
         trailing = n > 0 and data[-1] not in (10, 13)
-        parts = [_scan_chunk(h, buf, n, trailing, ncols, sep, dev)]
+        parts = [_scan_chunk(h, buf, n, trailing, ncols, sep, dev, hint)]
     else:
-        parts = _scan_chunked(h, data, ncols, sep, dev, int(chunk_bytes), pinned)
+        parts = _scan_chunked(h, data, ncols, sep, dev, int(chunk_bytes), pinned, hint)
     st = torch.stack([p[4] for p in parts]).cpu().numpy()  # the one host read of the parse results
     masks = np.bitwise_or.reduce(st[:, 2 + ncols:], axis=0)
     types = _resolve_types(masks, int(st[:, 0].max()), sharded)
     if types is None:
         STATS["fallbacks"] += 1
         return None
+    miss = hint is not None and [_KIND.get(t, (0,))[0] for t in types] != [_KIND.get(t, (0,))[0] for t in hint]
+    if sharded:  # every rank takes the same (collective) path
+        miss = bool(int(comm.all_reduce_max(torch.tensor([int(miss)], dtype=torch.int64))[0]))
+    if miss:
+        STATS["hint_misses"] = STATS.get("hint_misses", 0) + 1
+        return scan_device(data, sep, infer, device, ncols, sharded, chunk_bytes, pinned, device_data, None)
     STATS["device_scans"] += 1
     STATS["chunks"] = STATS.get("chunks", 0) + len(parts)
-    return _finish(parts, types, st, dev)
+    return _finish(parts, types, st, dev, hinted=hint is not None)
 
 
 def chunk_bounds(data: bytes, chunk_bytes: int):
@@ -216,7 +246,8 @@ def chunk_bounds(data: bytes, chunk_bytes: int):
     return b
 
 
-def _scan_chunked(h, data, ncols: int, sep: str, dev, chunk_bytes: int, pinned: Optional[torch.Tensor] = None):
+def _scan_chunked(h, data, ncols: int, sep: str, dev, chunk_bytes: int, pinned: Optional[torch.Tensor] = None,
+                  hint=None):
     from ..runtime.streams import StagingRing
 
     bounds = chunk_bounds(data, chunk_bytes)
@@ -235,7 +266,7 @@ def _scan_chunked(h, data, ncols: int, sep: str, dev, chunk_bytes: int, pinned: 
             put(i + 1)  # overlaps chunk i's parse
         buf = ring.get(i)
         trailing = data[e - 1] not in (10, 13)
-        parts.append(_scan_chunk(h, buf, e - s, trailing, ncols, sep, dev))
+        parts.append(_scan_chunk(h, buf, e - s, trailing, ncols, sep, dev, hint))
         ring.release(i)
     return parts
 

@@ -219,11 +219,15 @@ class DataFrameReader:
 
                 if filecache.device_bytes_allowed(hi - lo):
                     dbytes = pf.device_bytes(dev, lo, hi)  # HBM-resident input bytes
+            hkey = (lo, hi, sep)
             with tracing.span("csv_scan"):
                 t = csvscan.scan_device(data, sep=sep, infer=infer, device=dev, sharded=shard,
                                         chunk_bytes=int(self._session.conf.get("dq4ml.chunkBytes", str(256 << 20))),
-                                        pinned=pinned, device_data=dbytes)
+                                        pinned=pinned, device_data=dbytes,
+                                        types_hint=pf.type_hints.get(hkey) if pf is not None else None)
             if t is not None:
+                if pf is not None:  # the next action's scan of these bytes stores typed columns directly
+                    pf.type_hints[hkey] = [csvscan.type_code_of(f.dataType) for f in t.schema.fields]
                 return t
         if not isinstance(data, bytes):
             data = bytes(data)  # host scanner path (small or fallback): a plain copy

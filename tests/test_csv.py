@@ -131,6 +131,30 @@ def test_device_scan_matches_host(name):
 
 
 @pytest.mark.gpu
+def test_device_scan_types_hint():
+    """A correct types_hint stores typed columns directly (same table); a wrong one is caught by
+    the inference masks and the scan re-runs unhinted."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from net.jgp.labs.sparkdq4ml_amd.ops import csvscan
+
+    data = b"1,2.5,true\n-3,4,false\n\n5,,TRUE\n,1e3,false"
+    ref = csvscan.scan_device(data, device="cuda")
+    codes = [csvscan.type_code_of(f.dataType) for f in ref.schema.fields]
+    assert codes == [csvscan.CT_INT, csvscan.CT_DOUBLE, csvscan.CT_BOOL]
+    for hint in (codes, [csvscan.CT_INT, csvscan.CT_INT, csvscan.CT_BOOL]):
+        before = csvscan.STATS.get("hint_misses", 0)
+        t = csvscan.scan_device(data, device="cuda", types_hint=hint)
+        assert t.schema == ref.schema and t.nrows == ref.nrows == 4
+        for a, b in zip(t.columns, ref.columns):
+            assert a.values.dtype == b.values.dtype
+            assert torch.equal(a.valid_mask(), b.valid_mask())
+            m = a.valid_mask()
+            assert torch.equal(a.values[m], b.values[m])
+        assert csvscan.STATS.get("hint_misses", 0) - before == (0 if hint == codes else 1)
+
+
+@pytest.mark.gpu
 def test_device_scan_through_reader(tmp_path):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
