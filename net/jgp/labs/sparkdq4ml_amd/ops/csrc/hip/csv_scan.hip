@@ -20,6 +20,8 @@
 //      whole scan is re-done by the host scanner.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "common.h"
 #include "csv_scan.h"
 
@@ -274,7 +276,11 @@ __device__ int parse_field(const uint8_t* p, int len, double& dv, int64_t& iv, b
 }
 
 constexpr int kMaxCols = 256;
-constexpr int kParseLds = 32768;  // staged bytes per 256-line group
+// staged bytes per 256-line group: 8 KiB (short lines, <= ~24 B: 8 waves per SIMD — the byte
+// loops are latency-bound) or 32 KiB (wider rows; 4 waves per SIMD).  Chosen per launch from the
+// chunk's mean line length; a group that does not fit parses from global memory.
+constexpr int kParseLdsSmall = 8192;
+constexpr int kParseLdsLarge = 32768;
 
 // Parse line li.  Bytes are read as B[i - bias] (global: B = b, bias = 0; LDS-staged: B = the
 // block's stage, bias = the buffer index of its first byte).
@@ -320,19 +326,21 @@ __device__ __forceinline__ bool parse_line(PB B, int64_t bias, int64_t n, const 
       uint32_t m = 0;
       int nd = 0, fr = 0;
       bool dot = false, bad = false;
+      // branch-free body (selects): the loop exit is the only divergent branch — an if / else-if
+      // chain here cost two exec-mask updates per byte (SALU outnumbered VALU 1.8 : 1)
       for (; q < end; ++q) {
         const int ch = B[q - bias];
         const uint32_t d = (uint32_t)(ch - '0');
-        if (d < 10u) {
-          m = m * 10u + d;
-          ++nd;
-          fr += dot ? 1 : 0;
-        } else if (ch == '.' && !dot) {
-          dot = true;
-        } else {
+        const bool isd = d < 10u;
+        const bool isdot = ch == '.' && !dot;
+        if (!(isd || isdot)) {
           bad = ch != sep;
           break;
         }
+        m = isd ? m * 10u + d : m;
+        nd += isd ? 1 : 0;
+        fr += (isd && dot) ? 1 : 0;
+        dot = dot || isdot;
       }
       if (!bad && nd > 0 && nd <= 9) {
         ty = dot ? CT_DOUBLE : CT_INT;
@@ -383,15 +391,15 @@ __device__ __forceinline__ bool parse_line(PB B, int64_t bias, int64_t n, const 
 // as in the line-boundary passes), then every thread parses its line from LDS — the first
 // version walked each line with dependent byte loads from global memory (~180 GB/s).  Longer
 // groups (very wide rows) parse straight from global memory.
-__global__ __launch_bounds__(256) void csv_parse_kernel(const uint8_t* __restrict__ b, int64_t n,
-                                                       const int64_t* __restrict__ ends, int64_t nlines, int ncols,
-                                                       uint8_t sep, const int64_t* __restrict__ dcols,
-                                                       uint8_t* __restrict__ valid, uint8_t* __restrict__ keep,
-                                                       unsigned long long* __restrict__ stats) {
+template <int LDS, int WPE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void csv_parse_kernel(
+    const uint8_t* __restrict__ b, int64_t n, const int64_t* __restrict__ ends, int64_t nlines, int ncols, uint8_t sep,
+    const int64_t* __restrict__ dcols, uint8_t* __restrict__ valid, uint8_t* __restrict__ keep,
+    unsigned long long* __restrict__ stats) {
   __shared__ uint32_t smask[kMaxCols];
   __shared__ int snull[kMaxCols];
   __shared__ int sempty, sflag;
-  __shared__ __attribute__((aligned(16))) uint8_t stage[kParseLds];
+  __shared__ __attribute__((aligned(16))) uint8_t stage[LDS];
   for (int c = threadIdx.x; c < ncols; c += blockDim.x) {
     smask[c] = 0;
     snull[c] = 0;
@@ -414,7 +422,7 @@ __global__ __launch_bounds__(256) void csv_parse_kernel(const uint8_t* __restric
     const int64_t glo = (lo + off) & ~(int64_t)15;  // aligned-view granule bounds
     const int64_t ghi = (hi + 1 + off + 15) & ~(int64_t)15;
     __syncthreads();  // previous group's readers are done with the stage
-    if (ghi - glo <= kParseLds) {
+    if (ghi - glo <= LDS) {
       for (int64_t g = glo + 16 * threadIdx.x; g < ghi; g += 16 * blockDim.x) {
         u32x4 v = {0u, 0u, 0u, 0u};
         if (g - off < n) v = *reinterpret_cast<const u32x4*>(ab + g);  // granule overlaps [0, n)
@@ -462,8 +470,19 @@ void csv_parse(const uint8_t* buf, int64_t n, const int64_t* ends, int64_t nline
   if (nlines <= 0) return;
   int64_t g = (nlines + 255) / 256;
   if (g > 16384) g = 16384;
-  hipLaunchKernelGGL(csv_parse_kernel, dim3(g), dim3(256), 0, st, buf, n, ends, nlines, ncols, sep, dcols, valid,
-                     keep, reinterpret_cast<unsigned long long*>(stats));
+  // variant: DQ4ML_CSV_PARSE_LDS (8192 | 32768) forces one; default by mean line length
+  static const int forced = [] {
+    const char* e = getenv("DQ4ML_CSV_PARSE_LDS");
+    return e ? atoi(e) : 0;
+  }();
+  const bool small = forced ? forced == kParseLdsSmall : (n / nlines) * 256 * 5 / 4 <= kParseLdsSmall;
+  auto* stats64 = reinterpret_cast<unsigned long long*>(stats);
+  if (small)
+    hipLaunchKernelGGL((csv_parse_kernel<kParseLdsSmall, 8>), dim3(g), dim3(256), 0, st, buf, n, ends, nlines, ncols,
+                       sep, dcols, valid, keep, stats64);
+  else
+    hipLaunchKernelGGL((csv_parse_kernel<kParseLdsLarge, 4>), dim3(g), dim3(256), 0, st, buf, n, ends, nlines, ncols,
+                       sep, dcols, valid, keep, stats64);
   DQ_HIP_CHECK(hipGetLastError());
 }
 
