@@ -352,6 +352,9 @@ def compile_chain(nodes, base: Table, check_device: bool = True):
             syms = []
             for ex, f in zip(node.exprs, out_schema.fields):
                 base_e = ex.child if isinstance(ex, E.Alias) else ex
+                if isinstance(base_e, E.Cast) and isinstance(base_e.child, E.ColRef) and \
+                        base_e.child.data_type(schema).simpleString() == base_e.to.simpleString():
+                    base_e = base_e.child  # SimplifyCasts: a cast to the column's own type is the column
                 if isinstance(base_e, E.ColRef):
                     syms.append(chain.lookup(base_e.name))
                     continue
