@@ -27,11 +27,20 @@ def timed(step, steps: int, warmup: int, dev):
     comm.barrier()
     if on_gpu:
         torch.cuda.synchronize()
+    prof = None
+    if os.environ.get("DQ4ML_BENCH_CPROFILE"):  # host-side profile of the timed steps only
+        import cProfile
+
+        prof = cProfile.Profile()
+        prof.enable()
     t0 = time.perf_counter()
     for _ in range(steps):
         out = step()
     if on_gpu:
         torch.cuda.synchronize()
+    if prof is not None:
+        prof.disable()
+        prof.dump_stats(os.environ["DQ4ML_BENCH_CPROFILE"])
     comm.barrier()
     if on_gpu:
         torch.cuda.synchronize()

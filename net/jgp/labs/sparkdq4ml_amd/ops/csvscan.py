@@ -84,7 +84,7 @@ def _scan_chunk(h, buf, n: int, trailing: bool, ncols: int, sep: str, dev, hint=
     if nterm:
         h.csv_line_ends(buf.data_ptr(), n, counts.data_ptr(), ends.data_ptr(), stream)
     if trailing:
-        ends[nterm] = n
+        ends[nterm:].fill_(n)  # a fill kernel: ``ends[nterm] = n`` is a blocking pageable copy
     m = max(nlines, 1)
     # one exact-size allocation per column: a column IS its plane (no copy, and no other
     # column's storage kept alive by it) — f64, or the hinted type (see scan_device)

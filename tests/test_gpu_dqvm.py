@@ -72,3 +72,28 @@ def test_rule1_null_raises_on_gpu():
                 .withColumn("x", callUDF("minimumPriceRule", col("price"))))
     assert ok.count() == 8
     gpu.stop()
+
+
+def test_chain_cache_reuses_codegen_and_respects_structure(gpu_session):
+    """The structural chain cache: a re-built identical chain over a new relation reuses the
+    generated kernel; a different literal compiles anew; results match the plain computation."""
+    spark = gpu_session
+    rows = [(i % 7, float(i) * 0.5) for i in range(5000)]
+
+    def run(thresh):
+        df = spark.createDataFrame(rows, "g int, p double")
+        df = df.withColumn("q", col("p") * 2.0).where(col("q") > thresh)
+        got = df.collect()
+        return len(got), sum(r.q for r in got)
+
+    dqvm._CHAIN_CACHE.clear()
+    before = dqvm.STATS["fused_launches"]
+    a = run(10.0)
+    n1 = len(dqvm._CHAIN_CACHE)
+    b = run(10.0)
+    assert a == b and len(dqvm._CHAIN_CACHE) == n1  # same structure: cache hit
+    c = run(100.0)
+    assert len(dqvm._CHAIN_CACHE) > n1  # a different literal is a different kernel
+    assert dqvm.STATS["fused_launches"] - before >= 3
+    ref = [r for r in rows if r[1] * 2.0 > 100.0]
+    assert c[0] == len(ref) and abs(c[1] - sum(r[1] * 2.0 for r in ref)) < 1e-6
