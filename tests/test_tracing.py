@@ -67,3 +67,21 @@ def test_session_gram_dtype_default():
         assert _gram_dtype(LinearRegression(gramDtype="fp32"), df) == "fp32"
     finally:
         s.stop()
+
+
+def test_logging_levels_and_log4j_pattern():
+    """utils.logging mirrors log4j.properties (L4J:1-11): engine internals quiet, the app package
+    at DEBUG, and the `%d -%5p --- [%15.15t] %-40.40l: %m` console pattern."""
+    import logging
+    import re
+
+    from net.jgp.labs.sparkdq4ml_amd.utils import logging as dqlog
+
+    dqlog.configure_logging()
+    root = logging.getLogger(dqlog.ROOT)
+    assert root.level >= logging.WARNING
+    assert logging.getLogger(dqlog.ROOT + ".apps").level == logging.DEBUG
+    rec = logging.LogRecord(dqlog.ROOT + ".apps.x", logging.WARNING, "/a/b/app.py", 42, "hello %s", ("world",),
+                            None, func="start")
+    line = dqlog._Fmt().format(rec)
+    assert re.match(r"^\d{4}-\d\d-\d\d \d\d:\d\d:\d\d\.\d{3} - WARN --- \[.{15}\] .{40}: hello world$", line), line
