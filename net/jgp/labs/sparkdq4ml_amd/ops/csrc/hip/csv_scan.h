@@ -11,12 +11,14 @@ enum CsvTypeCode : int { CT_NULL = 0, CT_INT = 1, CT_LONG = 2, CT_DECIMAL = 3, C
 
 int64_t csv_count_blocks(int64_t n);
 // Two calls: ends == null -> counts = csv_count_blocks(n)+1 int64 (exclusive per-block offsets,
-// total at [nb]); then ends (total int64) -> the ordered line-end offsets, reusing counts.
-void csv_line_ends(const uint8_t* buf, int64_t n, int64_t* counts, int64_t* ends, hipStream_t st);
+// total at [nb]); then ends (total entries) -> the ordered line-end offsets, reusing counts.
+// ends are int32 when csv_ends_i32(n) (inputs below 2 GiB), else int64
+bool csv_ends_i32(int64_t n);
+void csv_line_ends(const uint8_t* buf, int64_t n, int64_t* counts, void* ends, hipStream_t st);
 // dcols: [2 * ncols] int64 — ncols device pointers to nlines values each, then ncols storage
 // kinds (0 f64, 1 int32, 2 int64, 3 bool/uint8); valid: [ncols, nlines]; stats (zeroed):
 // [slow flag, empty lines, null fields per column (ncols), class masks per column (ncols)]
-void csv_parse(const uint8_t* buf, int64_t n, const int64_t* ends, int64_t nlines, int ncols, uint8_t sep,
+void csv_parse(const uint8_t* buf, int64_t n, const void* ends, int64_t nlines, int ncols, uint8_t sep,
                const int64_t* dcols, uint8_t* valid, uint8_t* keep, int64_t* stats, hipStream_t st);
 
 }  // namespace dq4ml

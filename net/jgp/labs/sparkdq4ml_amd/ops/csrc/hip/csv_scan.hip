@@ -134,8 +134,9 @@ constexpr int kEndsStage = 8192;  // line ends per block staged in LDS (block-re
 // Each thread finds its window's line ends; a block with at most kEndsStage of them collects them
 // in LDS (in order) and writes them out as one coalesced run — per-thread direct stores put 64
 // lanes on 64 different cache lines per instruction.
+template <typename IT>
 __global__ __launch_bounds__(256) void csv_ends_kernel(const uint8_t* __restrict__ b, int64_t n,
-                                                      const int64_t* __restrict__ offsets, int64_t* __restrict__ ends) {
+                                                      const int64_t* __restrict__ offsets, IT* __restrict__ ends) {
   __shared__ int wtot[4];
   __shared__ int sends[kEndsStage];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -164,11 +165,11 @@ __global__ __launch_bounds__(256) void csv_ends_kernel(const uint8_t* __restrict
       m &= m - 1;
     }
     __syncthreads();
-    for (int i = threadIdx.x; i < cnt; i += blockDim.x) ends[o0 + i] = bbase + sends[i];
+    for (int i = threadIdx.x; i < cnt; i += blockDim.x) ends[o0 + i] = (IT)(bbase + sends[i]);
   } else {
     int64_t o = o0 + before;
     while (m) {
-      ends[o++] = base + __builtin_ctzll(m);
+      ends[o++] = (IT)(base + __builtin_ctzll(m));
       m &= m - 1;
     }
   }
@@ -287,8 +288,8 @@ constexpr int kParseLdsLarge = 32768;
 // Called by EVERY lane of the wave (``active`` false past the last line) so the per-field type
 // bits can be OR-reduced across the wave with shuffles: one LDS atomic per wave and field instead
 // of 64 same-address atomics (which serialized the first version of this kernel).
-template <typename PB>
-__device__ __forceinline__ bool parse_line(PB B, int64_t bias, int64_t n, const int64_t* __restrict__ ends,
+template <typename PB, typename IT>
+__device__ __forceinline__ bool parse_line(PB B, int64_t bias, int64_t n, const IT* __restrict__ ends,
                                            int64_t li, bool active, int64_t nlines, int ncols, uint8_t sep,
                                            const int64_t* __restrict__ dcols, uint8_t* __restrict__ valid,
                                            uint8_t* __restrict__ keep, uint32_t* smask, int* snull, int* sempty) {
@@ -391,9 +392,9 @@ __device__ __forceinline__ bool parse_line(PB B, int64_t bias, int64_t n, const 
 // as in the line-boundary passes), then every thread parses its line from LDS — the first
 // version walked each line with dependent byte loads from global memory (~180 GB/s).  Longer
 // groups (very wide rows) parse straight from global memory.
-template <int LDS, int WPE>
+template <int LDS, int WPE, typename IT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void csv_parse_kernel(
-    const uint8_t* __restrict__ b, int64_t n, const int64_t* __restrict__ ends, int64_t nlines, int ncols, uint8_t sep,
+    const uint8_t* __restrict__ b, int64_t n, const IT* __restrict__ ends, int64_t nlines, int ncols, uint8_t sep,
     const int64_t* __restrict__ dcols, uint8_t* __restrict__ valid, uint8_t* __restrict__ keep,
     unsigned long long* __restrict__ stats) {
   __shared__ uint32_t smask[kMaxCols];
@@ -453,18 +454,36 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
 // + 1: the window grid starts at the granule boundary below the buffer start
 int64_t csv_count_blocks(int64_t n) { return (n + kChunk - 1) / kChunk + 1; }
 
-void csv_line_ends(const uint8_t* buf, int64_t n, int64_t* counts, int64_t* ends, hipStream_t st) {
+bool csv_ends_i32(int64_t n) { return n < ((int64_t)1 << 31) - 1; }
+
+void csv_line_ends(const uint8_t* buf, int64_t n, int64_t* counts, void* ends, hipStream_t st) {
   const int64_t nb = csv_count_blocks(n);
   if (ends == nullptr) {  // pass 1: per-block counts -> exclusive offsets, total at counts[nb]
     hipLaunchKernelGGL(csv_count_kernel, dim3(nb), dim3(256), 0, st, buf, n, counts);
     hipLaunchKernelGGL(csv_scan_counts_kernel, dim3(1), dim3(1024), 0, st, counts, nb);
-  } else {  // pass 2 (the host sized ``ends`` from counts[nb]): the offsets are already there
-    hipLaunchKernelGGL(csv_ends_kernel, dim3(nb), dim3(256), 0, st, buf, n, counts, ends);
+  } else if (csv_ends_i32(n)) {  // pass 2 (ends sized from counts[nb]); int32 offsets below 2 GiB
+    hipLaunchKernelGGL((csv_ends_kernel<int32_t>), dim3(nb), dim3(256), 0, st, buf, n, counts,
+                       static_cast<int32_t*>(ends));
+  } else {
+    hipLaunchKernelGGL((csv_ends_kernel<int64_t>), dim3(nb), dim3(256), 0, st, buf, n, counts,
+                       static_cast<int64_t*>(ends));
   }
   DQ_HIP_CHECK(hipGetLastError());
 }
 
-void csv_parse(const uint8_t* buf, int64_t n, const int64_t* ends, int64_t nlines, int ncols, uint8_t sep,
+template <typename IT>
+static void launch_parse(bool small, int64_t g, hipStream_t st, const uint8_t* buf, int64_t n, const IT* ends,
+                         int64_t nlines, int ncols, uint8_t sep, const int64_t* dcols, uint8_t* valid, uint8_t* keep,
+                         unsigned long long* stats) {
+  if (small)
+    hipLaunchKernelGGL((csv_parse_kernel<kParseLdsSmall, 8, IT>), dim3(g), dim3(256), 0, st, buf, n, ends, nlines,
+                       ncols, sep, dcols, valid, keep, stats);
+  else
+    hipLaunchKernelGGL((csv_parse_kernel<kParseLdsLarge, 4, IT>), dim3(g), dim3(256), 0, st, buf, n, ends, nlines,
+                       ncols, sep, dcols, valid, keep, stats);
+}
+
+void csv_parse(const uint8_t* buf, int64_t n, const void* ends, int64_t nlines, int ncols, uint8_t sep,
                const int64_t* dcols, uint8_t* valid, uint8_t* keep, int64_t* stats, hipStream_t st) {
   if (ncols > kMaxCols) throw std::invalid_argument("csv_parse: too many columns for the device scanner");
   if (nlines <= 0) return;
@@ -477,12 +496,12 @@ void csv_parse(const uint8_t* buf, int64_t n, const int64_t* ends, int64_t nline
   }();
   const bool small = forced ? forced == kParseLdsSmall : (n / nlines) * 256 * 5 / 4 <= kParseLdsSmall;
   auto* stats64 = reinterpret_cast<unsigned long long*>(stats);
-  if (small)
-    hipLaunchKernelGGL((csv_parse_kernel<kParseLdsSmall, 8>), dim3(g), dim3(256), 0, st, buf, n, ends, nlines, ncols,
-                       sep, dcols, valid, keep, stats64);
+  if (csv_ends_i32(n))
+    launch_parse(small, g, st, buf, n, static_cast<const int32_t*>(ends), nlines, ncols, sep, dcols, valid, keep,
+                 stats64);
   else
-    hipLaunchKernelGGL((csv_parse_kernel<kParseLdsLarge, 4>), dim3(g), dim3(256), 0, st, buf, n, ends, nlines, ncols,
-                       sep, dcols, valid, keep, stats64);
+    launch_parse(small, g, st, buf, n, static_cast<const int64_t*>(ends), nlines, ncols, sep, dcols, valid, keep,
+                 stats64);
   DQ_HIP_CHECK(hipGetLastError());
 }
 

@@ -182,11 +182,12 @@ PYBIND11_MODULE(_dq4ml_hip, m) {
   // ---- CSV scan (K1/K2) ------------------------------------------------------------------------
   m.def("csv_count_blocks", &csv_count_blocks);
   m.def("csv_line_ends", [](uintptr_t buf, int64_t n, uintptr_t counts, uintptr_t ends, uintptr_t stream) {
-    csv_line_ends(P<const uint8_t>(buf), n, P<int64_t>(counts), P<int64_t>(ends), as_stream(stream));
+    csv_line_ends(P<const uint8_t>(buf), n, P<int64_t>(counts), P<void>(ends), as_stream(stream));
   });
+  m.def("csv_ends_i32", &csv_ends_i32);
   m.def("csv_parse", [](uintptr_t buf, int64_t n, uintptr_t ends, int64_t nlines, int ncols, int sep, uintptr_t dcols,
                         uintptr_t valid, uintptr_t keep, uintptr_t stats, uintptr_t stream) {
-    csv_parse(P<const uint8_t>(buf), n, P<const int64_t>(ends), nlines, ncols, (uint8_t)sep, P<const int64_t>(dcols),
+    csv_parse(P<const uint8_t>(buf), n, P<const void>(ends), nlines, ncols, (uint8_t)sep, P<const int64_t>(dcols),
               P<uint8_t>(valid), P<uint8_t>(keep), P<int64_t>(stats), as_stream(stream));
   });
 

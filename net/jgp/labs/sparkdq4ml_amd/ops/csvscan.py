@@ -80,7 +80,8 @@ def _scan_chunk(h, buf, n: int, trailing: bool, ncols: int, sep: str, dev, hint=
     h.csv_line_ends(buf.data_ptr(), n, counts.data_ptr(), 0, stream)
     nterm = int(counts[nb].item())
     nlines = nterm + (1 if trailing else 0)
-    ends = torch.empty(max(nlines, 1), dtype=torch.int64, device=dev)
+    # int32 line-end offsets below 2 GiB (half the bytes of the ends pass and of the parse's reads)
+    ends = torch.empty(max(nlines, 1), dtype=torch.int32 if h.csv_ends_i32(n) else torch.int64, device=dev)
     if nterm:
         h.csv_line_ends(buf.data_ptr(), n, counts.data_ptr(), ends.data_ptr(), stream)
     if trailing:

@@ -47,11 +47,11 @@ def main():
         nterm = int(counts[nb].item())
         t0 = t("sync count (.item)", t0)
         nlines = nterm + 1
-        ends = torch.empty(nlines, dtype=torch.int64, device=dev)
+        ends = torch.empty(nlines, dtype=torch.int32 if h.csv_ends_i32(n) else torch.int64, device=dev)
         t0 = t("alloc ends", t0)
         h.csv_line_ends(buf.data_ptr(), n, counts.data_ptr(), ends.data_ptr(), stream)
         t0 = t("launch ends", t0)
-        ends[nterm] = n
+        ends[nterm:].fill_(n)
         t0 = t("ends[nterm] = n", t0)
         dcols = [torch.empty(nlines, dtype=dt, device=dev) for dt in (torch.int32, torch.float64)]
         t0 = t("alloc cols", t0)
