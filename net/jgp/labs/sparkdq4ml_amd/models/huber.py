@@ -61,13 +61,24 @@ def train_huber(est, df, tbl, X, y, w, sel, d):
 
     lo = np.full(dim, -np.inf)
     lo[-1] = MIN_SIGMA
-    theta = np.ones(dim)
-    f, g = fg(theta)
-    hist = [f]
-    S, Y = [], []
     max_iter, tol = int(est.getOrDefault("maxIter")), float(est.getOrDefault("tol"))
-    f_hist = [np.inf]
-    for it in range(max_iter):
+    ck = _Checkpoint.of(df, flat, (d, dim, fit_icpt, eps, reg, std_flag, max_iter, tol))
+    state = ck.load() if ck is not None else None
+    if state is not None:  # resume: the exact optimizer state of the last checkpoint
+        start, theta, f, g, S, Y, hist, f_hist = state
+        log.info("resuming huber l-bfgs at iteration %d from %s", start, ck.path)
+    else:
+        start = 0
+        theta = np.ones(dim)
+        f, g = fg(theta)
+        hist = [f]
+        S, Y = [], []
+        f_hist = [np.inf]
+    for it in range(start, max_iter):
+        if ck is not None and it > start and it % ck.every == 0:
+            ck.save(it, theta, f, g, S, Y, hist, f_hist)
+        if _FAIL_AT_ITER is not None and it == _FAIL_AT_ITER:  # fault injection (tests)
+            raise RuntimeError(f"injected failure at huber iteration {it}")
         # projected gradient convergence
         pg = np.where((theta <= lo) & (g > 0), 0.0, g)
         if np.linalg.norm(pg) <= max(tol * abs(f), 1e-8):
@@ -109,9 +120,71 @@ def train_huber(est, df, tbl, X, y, w, sel, d):
         f_hist = f_hist[-20:]
         if len(f_hist) >= 2 and abs(f - max(f_hist)) <= tol * abs(hist[0]):
             break
+    if ck is not None:
+        ck.clear()
     coef = np.where(sx != 0.0, theta[:d] / safe, 0.0)
     icpt = float(theta[d]) if fit_icpt else 0.0
     model = LinearRegressionModel(est.uid, DenseVector(coef), icpt, float(theta[-1]))
     est.copyValues(model)
     model._set_summary(LinearRegressionTrainingSummary(model, df, None, np.array(hist), stats=stats, solver="l-bfgs-b"))
     return model
+
+
+_FAIL_AT_ITER = None  # tests: raise at this iteration (simulated crash between checkpoints)
+
+
+class _Checkpoint:
+    """Optimizer-state checkpoints of the iterative (data-pass per evaluation) Huber fit
+    (SURVEY.md §5d): with ``dq4ml.lbfgs.checkpointDir`` set, the complete L-BFGS state (iterate,
+    value, gradient, the s/y memory, objective histories, next iteration) is written every
+    ``dq4ml.lbfgs.checkpointInterval`` iterations (atomic rename; rank 0 writes, every rank
+    reads).  A re-run of the same fit — same parameters and the same data, fingerprinted by its
+    all-reduced Gram statistics — resumes from it and finishes exactly as the uninterrupted run
+    would have.  The file is removed when the fit completes."""
+
+    def __init__(self, path: str, every: int):
+        self.path, self.every = path, max(1, int(every))
+
+    @classmethod
+    def of(cls, df, flat, params):
+        import hashlib
+        import os
+
+        sess = getattr(df, "sparkSession", None)
+        root = sess.conf.get("dq4ml.lbfgs.checkpointDir", "") if sess is not None else ""
+        if not root:
+            return None
+        h = hashlib.sha1(repr(params).encode())
+        h.update(np.ascontiguousarray(flat.cpu().numpy()).tobytes())
+        os.makedirs(root, exist_ok=True)
+        return cls(os.path.join(root, f"huber-{h.hexdigest()[:20]}.npz"),
+                   int(sess.conf.get("dq4ml.lbfgs.checkpointInterval", "10")))
+
+    def save(self, it, theta, f, g, S, Y, hist, f_hist):
+        import os
+
+        if comm.rank() != 0:
+            return
+        dim = theta.shape[0]
+        tmp = self.path + ".tmp.npz"
+        np.savez(tmp, it=np.array(it), theta=theta, f=np.array(f), g=g,
+                 S=np.array(S).reshape(-1, dim), Y=np.array(Y).reshape(-1, dim),
+                 hist=np.array(hist), f_hist=np.array(f_hist))
+        os.replace(tmp, self.path)
+
+    def load(self):
+        import os
+
+        comm.barrier()  # a rank-0 write of an earlier attempt is complete before anyone reads
+        if not os.path.exists(self.path):
+            return None
+        z = np.load(self.path)  # allow_pickle=False: plain arrays only
+        return (int(z["it"]), z["theta"], float(z["f"]), z["g"], list(z["S"]), list(z["Y"]),
+                list(z["hist"]), list(z["f_hist"]))
+
+    def clear(self):
+        import os
+
+        comm.barrier()
+        if comm.rank() == 0 and os.path.exists(self.path):
+            os.remove(self.path)

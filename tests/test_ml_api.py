@@ -157,3 +157,32 @@ def test_fit_prunes_unused_derived_columns(cpu_session):
     m = LinearRegression().fit(df)
     assert abs(m.coefficients[0] - 2.0) < 1e-9 and abs(m.intercept - 1.0) < 1e-9
     assert "unused" in df.columns  # the user's DataFrame is untouched
+
+
+def test_huber_checkpoint_resume_is_exact(cpu_session, tmp_path):
+    """the iterative Huber fit checkpoints its L-BFGS state; a crash between
+    checkpoints followed by a re-run resumes and ends exactly where the uninterrupted fit does."""
+    import os
+
+    from net.jgp.labs.sparkdq4ml_amd.models import huber
+
+    df, X, y = _synth(cpu_session, outliers=True)
+    ref = LinearRegression(loss="huber", maxIter=60).fit(df)
+    assert ref.summary.totalIterations > 8
+    cpu_session.conf.set("dq4ml.lbfgs.checkpointDir", str(tmp_path))
+    cpu_session.conf.set("dq4ml.lbfgs.checkpointInterval", "3")
+    try:
+        huber._FAIL_AT_ITER = 7
+        with pytest.raises(RuntimeError, match="injected failure"):
+            LinearRegression(loss="huber", maxIter=60).fit(df)
+        files = [f for f in os.listdir(tmp_path) if f.endswith(".npz")]
+        assert len(files) == 1  # the iteration-6 state
+        huber._FAIL_AT_ITER = None
+        got = LinearRegression(loss="huber", maxIter=60).fit(df)
+    finally:
+        huber._FAIL_AT_ITER = None
+        cpu_session.conf.set("dq4ml.lbfgs.checkpointDir", "")
+    assert np.array_equal(got.coefficients.toArray(), ref.coefficients.toArray())
+    assert got.intercept == ref.intercept and got.scale == ref.scale
+    assert np.array_equal(got.summary.objectiveHistory, ref.summary.objectiveHistory)
+    assert not [f for f in os.listdir(tmp_path) if f.endswith(".npz")]  # removed on completion
