@@ -29,6 +29,7 @@ for s in $STEPS; do
        step widepmc2 600 rocprofv3 --kernel-trace --pmc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum -d gpurun_out/widepmc2 -o run --output-format csv -- python scripts/wide_bench.py) || exit $? ;;
     cfg4) step cfg4 900 python benchmarks/bench_dq_pipeline.py --steps 5 --warmup 2 --json-out gpurun_out/cfg4.json ;;
     cfg5) step cfg5 900 python benchmarks/bench_wide.py --steps 3 --warmup 1 --json-out gpurun_out/cfg5.json ;;
+    csv) step csv 600 python benchmarks/bench_csv_pipeline.py --steps 20 --warmup 3 --json-out gpurun_out/csv.json ;;
     cfg1) step cfg1 300 python benchmarks/bench_cpu_small.py --json-out gpurun_out/cfg1.json ;;
     prof4) step prof4 600 env WHICH=cfg4 python scripts/step_profile.py ;;
     prof5) step prof5 600 env WHICH=cfg5 python scripts/step_profile.py ;;
