@@ -36,17 +36,19 @@ def test_codegen_compiles(cpu_session, tmp_path):
         p = p.child
     nodes.reverse()
     base = execute(p, cpu_session)
-    src, g, outputs, sel_out = dqvm.compile_chain(nodes, base, check_device=False)
+    (src, src_vec), g, outputs, sel_out = dqvm.compile_chain(nodes, base, check_device=False)
     assert "atomicOr" not in src  # price has no nulls: rule 1 null check elided
     assert src.count("live = live &&") == 2
+    assert src_vec.count("live = live &&") == 4  # the 4-row body + the n % 4 tail body
     assert sel_out is not None
     kinds = [o[0] for o in outputs]
     assert kinds == ["col", "new", "new"]  # cast(guest as int) of an int column: the column itself
     hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
     if not os.path.exists(hipcc):
         pytest.skip("no hipcc")
-    f = tmp_path / "k.hip"
-    f.write_text("#include <hip/hip_runtime.h>\n" + src)
-    r = subprocess.run([hipcc, "--offload-arch=gfx950", "-O3", "-c", str(f), "-o", str(tmp_path / "k.o")],
-                       capture_output=True, text=True)
-    assert r.returncode == 0, r.stderr + "\n" + src
+    for i, code in enumerate((src, src_vec)):
+        f = tmp_path / f"k{i}.hip"
+        f.write_text("#include <hip/hip_runtime.h>\n" + code)
+        r = subprocess.run([hipcc, "--offload-arch=gfx950", "-O3", "-c", str(f), "-o", str(tmp_path / f"k{i}.o")],
+                           capture_output=True, text=True)
+        assert r.returncode == 0, r.stderr + "\n" + code
