@@ -808,7 +808,54 @@ __global__ __launch_bounds__(kBlock) void gram_tall_f64_kernel(GramArgs a) {
 // zeros, their garbage never enters a product), 4 rows in flight per thread.  Slab layout = the
 // f64 MFMA kernel's (16 x 16 tile), so the slab fold is shared.
 // =============================================================================================
-template <typename TX, int D, bool COLS = false>
+// 4 consecutive elements [r0, r0 + 4) of a typed column as f64, ONE vector load (the caller
+// guarantees 16-byte-aligned bases and r0 % 4 == 0; the switch is wave-uniform)
+__device__ __forceinline__ void load4_as_f64(const void* p, int dt, int64_t r0, double out[4]) {
+  typedef __attribute__((ext_vector_type(4))) int i32x4_t;
+  typedef __attribute__((ext_vector_type(2))) long long i64x2_t;
+  typedef __attribute__((ext_vector_type(4))) unsigned char u8x4_t;
+  typedef __attribute__((ext_vector_type(4))) unsigned short u16x4_t;
+  switch (dt) {
+    case DT_F64: {
+      const f64x2 a = reinterpret_cast<const f64x2*>(p)[r0 / 2], b = reinterpret_cast<const f64x2*>(p)[r0 / 2 + 1];
+      out[0] = a[0]; out[1] = a[1]; out[2] = b[0]; out[3] = b[1];
+      break;
+    }
+    case DT_F32: {
+      const f32x4 v = reinterpret_cast<const f32x4*>(p)[r0 / 4];
+      for (int u = 0; u < 4; ++u) out[u] = (double)v[u];
+      break;
+    }
+    case DT_I32: {
+      const i32x4_t v = reinterpret_cast<const i32x4_t*>(p)[r0 / 4];
+      for (int u = 0; u < 4; ++u) out[u] = (double)v[u];
+      break;
+    }
+    case DT_I64: {
+      const i64x2_t a = reinterpret_cast<const i64x2_t*>(p)[r0 / 2], b = reinterpret_cast<const i64x2_t*>(p)[r0 / 2 + 1];
+      out[0] = (double)a[0]; out[1] = (double)a[1]; out[2] = (double)b[0]; out[3] = (double)b[1];
+      break;
+    }
+    case DT_U8: {
+      const u8x4_t v = reinterpret_cast<const u8x4_t*>(p)[r0 / 4];
+      for (int u = 0; u < 4; ++u) out[u] = (double)v[u];
+      break;
+    }
+    case DT_BF16: {
+      const u16x4_t v = reinterpret_cast<const u16x4_t*>(p)[r0 / 4];
+      for (int u = 0; u < 4; ++u) out[u] = (double)bf16_bits_to_f32(v[u]);
+      break;
+    }
+    default:
+      for (int u = 0; u < 4; ++u) out[u] = 0.0;
+  }
+}
+
+// VEC (columnar sources only, host-checked 16-byte-aligned pointers): each lane owns 4
+// CONSECUTIVE rows and reads each column / the label / weights / selection with one vector load
+// (the row-strided form moves 1-8 bytes per lane per load); the partial last quad takes clamped
+// scalar loads.
+template <typename TX, int D, bool COLS = false, bool VEC = false>
 __global__ __launch_bounds__(kBlock) void gram_skinny_f64_kernel(GramArgs a) {
   constexpr int NA = D * (D + 1) / 2;
   constexpr int NV = 5 + 2 * D + NA;
@@ -820,22 +867,49 @@ __global__ __launch_bounds__(kBlock) void gram_skinny_f64_kernel(GramArgs a) {
   const TX* X = reinterpret_cast<const TX*>(a.X);
   const int64_t n = a.n;
   const int64_t step = (int64_t)gridDim.x * kBlock * UNR;
-  for (int64_t r0 = (int64_t)blockIdx.x * kBlock * UNR + threadIdx.x; r0 < n; r0 += step) {
+  const int64_t first = VEC ? ((int64_t)blockIdx.x * kBlock + threadIdx.x) * UNR
+                            : (int64_t)blockIdx.x * kBlock * UNR + threadIdx.x;
+  for (int64_t r0 = first; r0 < n; r0 += step) {
     double x[UNR][D], yv[UNR], wv[UNR];
     bool live[UNR];
+    if (VEC && r0 + UNR <= n) {
+      double t[UNR];
+      load4_as_f64(a.y, a.ydt, r0, yv);
+      if (a.w) {
+        load4_as_f64(a.w, a.wdt, r0, wv);
+      } else {
 #pragma unroll
-    for (int u = 0; u < UNR; ++u) {  // loads of all UNR rows first (clamped, unconditional)
-      const int64_t r = r0 + (int64_t)u * kBlock;
-      const int64_t rc = r < n ? r : n - 1;
-      live[u] = r < n && (a.sel == nullptr || a.sel[rc] != 0);
-      yv[u] = load_as_f64(a.y, a.ydt, rc);
-      wv[u] = a.w ? load_as_f64(a.w, a.wdt, rc) : 1.0;
+        for (int u = 0; u < UNR; ++u) wv[u] = 1.0;
+      }
+      if (a.sel) {
+        load4_as_f64(a.sel, DT_U8, r0, t);
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) live[u] = t[u] != 0.0;
+      } else {
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) live[u] = true;
+      }
 #pragma unroll
       for (int f = 0; f < D; ++f) {
-        if constexpr (COLS) {
-          x[u][f] = load_as_f64(a.colp[f], a.coldt[f], rc);  // wave-uniform dtype switch
-        } else {
-          x[u][f] = (double)X[(int64_t)f * a.ld + rc];
+        load4_as_f64(a.colp[f], a.coldt[f], r0, t);
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) x[u][f] = t[u];
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) {  // loads of all UNR rows first (clamped, unconditional)
+        const int64_t r = VEC ? r0 + u : r0 + (int64_t)u * kBlock;
+        const int64_t rc = r < n ? r : n - 1;
+        live[u] = r < n && (a.sel == nullptr || a.sel[rc] != 0);
+        yv[u] = load_as_f64(a.y, a.ydt, rc);
+        wv[u] = a.w ? load_as_f64(a.w, a.wdt, rc) : 1.0;
+#pragma unroll
+        for (int f = 0; f < D; ++f) {
+          if constexpr (COLS) {
+            x[u][f] = load_as_f64(a.colp[f], a.coldt[f], rc);  // wave-uniform dtype switch
+          } else {
+            x[u][f] = (double)X[(int64_t)f * a.ld + rc];
+          }
         }
       }
     }
@@ -1111,18 +1185,30 @@ static void with_skinny(int xdt, int d, F&& f) {
   throw std::invalid_argument("gram_skinny: unsupported feature dtype");
 }
 
-template <typename F>
-static void with_skinny_cols(int d, F&& f) {
+template <bool VEC, typename F>
+static void with_skinny_cols_t(int d, F&& f) {
   switch (d) {
-    case 1: return f(gram_skinny_f64_kernel<double, 1, true>);
-    case 2: return f(gram_skinny_f64_kernel<double, 2, true>);
-    case 3: return f(gram_skinny_f64_kernel<double, 3, true>);
-    case 4: return f(gram_skinny_f64_kernel<double, 4, true>);
-    case 5: return f(gram_skinny_f64_kernel<double, 5, true>);
-    case 6: return f(gram_skinny_f64_kernel<double, 6, true>);
-    case 7: return f(gram_skinny_f64_kernel<double, 7, true>);
-    default: return f(gram_skinny_f64_kernel<double, 8, true>);
+    case 1: return f(gram_skinny_f64_kernel<double, 1, true, VEC>);
+    case 2: return f(gram_skinny_f64_kernel<double, 2, true, VEC>);
+    case 3: return f(gram_skinny_f64_kernel<double, 3, true, VEC>);
+    case 4: return f(gram_skinny_f64_kernel<double, 4, true, VEC>);
+    case 5: return f(gram_skinny_f64_kernel<double, 5, true, VEC>);
+    case 6: return f(gram_skinny_f64_kernel<double, 6, true, VEC>);
+    case 7: return f(gram_skinny_f64_kernel<double, 7, true, VEC>);
+    default: return f(gram_skinny_f64_kernel<double, 8, true, VEC>);
   }
+}
+
+static bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+template <typename F>
+static void with_skinny_cols(const GramArgs& a, F&& f) {
+  bool vec = aligned16(a.y) && aligned16(a.w) && aligned16(a.sel);
+  for (int i = 0; i < a.cols; ++i) vec = vec && aligned16(a.colp[i]);
+  if (vec)
+    with_skinny_cols_t<true>(a.d, f);
+  else
+    with_skinny_cols_t<false>(a.d, f);
 }
 
 static bool use_skinny(int mode, int d, int xdt, int tiled) {
@@ -1173,7 +1259,7 @@ void gram_tall(int mode, GramArgs a, int xmode, int blocks, double* out, hipStre
   if (a.cols > 0) {
     if (mode != GRAM_F64 || a.cols != a.d || a.d > kSkinnyMaxD || a.tiled)
       throw std::invalid_argument("gram_tall: columnar sources need f64 mode and d <= 8");
-    with_skinny_cols(a.d, [&](auto kern) { hipLaunchKernelGGL(kern, dim3(blocks), dim3(kBlock), 0, st, a); });
+    with_skinny_cols(a, [&](auto kern) { hipLaunchKernelGGL(kern, dim3(blocks), dim3(kBlock), 0, st, a); });
   } else if (use_skinny(mode, a.d, a.xdt, a.tiled)) {
     with_skinny(a.xdt, a.d, [&](auto kern) { hipLaunchKernelGGL(kern, dim3(blocks), dim3(kBlock), 0, st, a); });
   } else {
