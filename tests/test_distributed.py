@@ -70,3 +70,6 @@ def test_dp_fit_matches_single_process(world, reg, cpu_session):
         assert rmse == pytest.approx(float(ref.summary.rootMeanSquaredError), rel=1e-9)
         assert r2 == pytest.approx(float(ref.summary.r2), rel=1e-9)
         assert nn == 5000
+    # X6: no coefficient broadcast — every rank solves the same all-reduced Gram, so the
+    # coefficients must agree bit for bit across ranks.
+    assert all(coef == res[0][1] and icpt == res[0][2] for _, coef, icpt, *_ in res)
