@@ -34,7 +34,9 @@ from ..sql.types import (BooleanType, DataType, DecimalType, DoubleType, FloatTy
 __all__ = ["try_execute_fused", "compile_chain", "Unfusable"]
 
 ENTRY = "dq_fused"
-STATS = {"fused_launches": 0, "unfusable": 0}
+# "vector_deferred": chains ending in VectorAssembler output — the assembler keeps them lazy and
+# fuses the pack into the Gram pass (models/feature.py), and the DQ sub-chain below is fused here.
+STATS = {"fused_launches": 0, "unfusable": 0, "vector_deferred": 0}
 
 
 class Unfusable(Exception):
@@ -587,13 +589,13 @@ def try_execute_fused(plan, session) -> Optional[Table]:
     else:
         try:
             cp = _ChainPlan(*compile_chain(nodes, base), refs)
-        except Unfusable:
-            cp = None
+        except Unfusable as e:
+            cp = "vector" if str(e) == "VectorAssembleExpr" else None
         if len(_CHAIN_CACHE) >= _CHAIN_CACHE_MAX:
             _CHAIN_CACHE.clear()
         _CHAIN_CACHE[key] = cp
-    if cp is None:
-        STATS["unfusable"] += 1
+    if cp is None or cp == "vector":
+        STATS["unfusable" if cp is None else "vector_deferred"] += 1
         return None
     from . import native
 
