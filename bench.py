@@ -43,17 +43,35 @@ def _args(argv=None):
     return ap.parse_args(argv)
 
 
+def _self_launch(a, argv) -> int:
+    """``--gpus N`` without a launcher: start N ranks (one process per GPU) through
+    ``parallel/launch.py`` BEFORE anything here touches the GPU, and return their exit code."""
+    from net.jgp.labs.sparkdq4ml_amd.parallel.launch import launch
+
+    args = list(sys.argv[1:] if argv is None else argv)
+    return launch(a.gpus, [os.path.abspath(__file__)] + args)
+
+
 def main(argv=None):
     a = _args(argv)
+    if a.gpus > 1 and int(os.environ.get("WORLD_SIZE", "1")) != a.gpus:
+        if "WORLD_SIZE" in os.environ:
+            print(f"[bench] --gpus {a.gpus} but WORLD_SIZE={os.environ['WORLD_SIZE']}", file=sys.stderr)
+            return 2
+        return _self_launch(a, argv)
     import torch
 
     from net.jgp.labs.sparkdq4ml_amd import LinearRegression, SparkSession
     from net.jgp.labs.sparkdq4ml_amd.parallel import comm
 
+    if torch.cuda.is_available() and a.gpus > torch.cuda.device_count():
+        print(f"[bench] --gpus {a.gpus} but only {torch.cuda.device_count()} visible GPU(s)", file=sys.stderr)
+        return 2
     comm.init()
     rank, world = comm.rank(), comm.world_size()
-    if world != a.gpus and rank == 0:
-        print(f"[bench] warning: --gpus {a.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    if world != a.gpus:
+        print(f"[bench] --gpus {a.gpus} but the process group has {world} rank(s)", file=sys.stderr)
+        return 2
     # async (default): gram -> RCCL all-reduce -> device WLS solve (wls_small.hip) enqueued back
     # to back, the host never waits inside a step; every fit's solve still runs inside the timed
     # region (the closing synchronize), the model's coefficients materialize on first read.
@@ -108,6 +126,8 @@ def main(argv=None):
     elapsed = time.perf_counter() - t0
     el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     elapsed = float(comm.all_reduce_max(el).item())
+    ranks = comm.all_gather_object({"rank": rank, "device": str(dev),
+                                    "device_index": dev.index if on_gpu else None})
 
     global_rows = total if a.scaling == "strong" else total * world
     ms = elapsed / a.steps * 1e3
@@ -124,6 +144,9 @@ def main(argv=None):
                        "seq_len": d, "parallelism": f"dp{world}", "rows_per_gpu": n,
                        "device": str(dev), "coef_max_abs_err": err,
                        "fit_mode": "async" if (a.use_async and on_gpu) else "sync"},
+            "world": world, "backend": comm.backend() or "none",
+            "rccl_version": comm.rccl_version() if on_gpu else None,
+            "rank_devices": [r["device"] for r in ranks],
         }
         s = json.dumps(line)
         print(s, flush=True)
@@ -131,7 +154,8 @@ def main(argv=None):
             with open(a.json_out, "w") as f:
                 f.write(s + "\n")
     comm.shutdown()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

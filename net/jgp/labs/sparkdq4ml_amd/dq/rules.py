@@ -50,7 +50,7 @@ class MinimumPriceDataQualityUdf(DQRule):
         p = RaiseIfNull(Cast(to_expr(price), "double"),
                         "Failed to execute user defined function(MinimumPriceDataQualityUdf: (double) => double)"
                         " caused by java.lang.NullPointerException")
-        return If(BinOp("<", p, Lit(float(services.MIN_PRICE))), Lit(-1.0), p)
+        return If(BinOp("<", p, Lit(float(services.MIN_PRICE)), ieee=True), Lit(-1.0), p)
 
 
 class PriceCorrelationDataQualityUdf(DQRule):
@@ -67,8 +67,8 @@ class PriceCorrelationDataQualityUdf(DQRule):
     def ir(self, price, guest):
         p = Cast(to_expr(price), "double")
         g = Cast(to_expr(guest), "int")
-        bad = BinOp("and", BinOp("<", g, Lit(services.CORRELATION_MAX_GUESTS)),
-                    BinOp(">", p, Lit(float(services.CORRELATION_MAX_PRICE))))
+        bad = BinOp("and", BinOp("<", g, Lit(services.CORRELATION_MAX_GUESTS), ieee=True),
+                    BinOp(">", p, Lit(float(services.CORRELATION_MAX_PRICE)), ieee=True))
         null = BinOp("or", IsNull(p), IsNull(g))
         return If(null, Lit(-1.0), If(bad, Lit(-1.0), p))
 
@@ -88,9 +88,9 @@ class RangeRule(DQRule):
         v = Cast(to_expr(x), "double")
         bad = IsNull(v)
         if self.lo is not None:
-            bad = BinOp("or", bad, BinOp("<", v, Lit(float(self.lo))))
+            bad = BinOp("or", bad, BinOp("<", v, Lit(float(self.lo)), ieee=True))
         if self.hi is not None:
-            bad = BinOp("or", bad, BinOp(">", v, Lit(float(self.hi))))
+            bad = BinOp("or", bad, BinOp(">", v, Lit(float(self.hi)), ieee=True))
         return If(bad, Lit(float(self.sentinel)), v)
 
 

@@ -13,6 +13,7 @@ from typing import List
 
 import torch
 
+from ..runtime.checks import defer
 from ..utils import tracing
 from ..sql.dataframe import DataFrame
 from ..sql.expressions import (AnalysisException, ColRef, EvalContext, Expr, IsNotNull, BinOp,
@@ -75,13 +76,18 @@ class VectorAssembleExpr(Expr):
 
         cols = [ctx.table.column(c) for c in self.inputs]
         live = ctx.table.sel_mask()
+        checks = [ck for c in cols for ck in c.checks]
         if self.handle_invalid == "error":
+            # a null input fails the job -- as a device flag read with the first host result
+            # (rows shown / fit coefficients), not a host sync here (runtime/checks.py)
             for name, c in zip(self.inputs, cols):
-                if c.valid is not None and bool((live & ~c.valid).any()):
-                    raise SparkException(
-                        f"Failed to execute user defined function(VectorAssembler$$Lambda: (struct<{name}:double>) "
-                        f"=> struct<type:tinyint,size:int,indices:array<int>,values:array<double>>) caused by "
-                        f"org.apache.spark.SparkException: Values to assemble cannot be null.")
+                if c.valid is not None:
+                    def exc(name=name):
+                        return SparkException(
+                            f"Failed to execute user defined function(VectorAssembler$$Lambda: (struct<{name}:double>)"
+                            f" => struct<type:tinyint,size:int,indices:array<int>,values:array<double>>) caused by "
+                            f"org.apache.spark.SparkException: Values to assemble cannot be null.")
+                    checks.append(defer((live & ~c.valid).any(), exc))
         parts = []
         for c in cols:
             if isinstance(c.dtype, VectorUDT):
@@ -107,7 +113,7 @@ class VectorAssembleExpr(Expr):
                     return kernels.pack_tiled(parts, sel)
             meta = {"ml_attr": {"num_attrs": d}, "zero_dead": sel}
             n = int(parts[0].shape[-1])
-            return LazyVectorColumn(VectorUDT(), _pack, n, (parts, sel), meta)
+            return _with_checks(LazyVectorColumn(VectorUDT(), _pack, n, (parts, sel), meta), checks)
         elif on_dev and (dt == torch.float8_e4m3fn or (dt == torch.bfloat16 and d > 64)):
             # wide fragment layout for the LDS-tiled MFMA SYRK (fp8: per-feature scales)
             with tracing.span("pack"):
@@ -119,8 +125,8 @@ class VectorAssembleExpr(Expr):
             def _pack(parts=parts, dt=dt):
                 with tracing.span("pack"):
                     return kernels.pack_columns(parts, dt)
-            return LazyVectorColumn(VectorUDT(), _pack, int(parts[0].shape[-1]), (parts, ctx.table.sel),
-                                    {"ml_attr": {"num_attrs": d}})
+            return _with_checks(LazyVectorColumn(VectorUDT(), _pack, int(parts[0].shape[-1]), (parts, ctx.table.sel),
+                                                 {"ml_attr": {"num_attrs": d}}), checks)
         elif dt == torch.float8_e4m3fn:  # host engine: fp8 storage is a device layout; keep fp32
             mat = kernels.pack_columns(parts, torch.float32)
             meta = {"ml_attr": {"num_attrs": int(mat.shape[0])}}
@@ -128,7 +134,12 @@ class VectorAssembleExpr(Expr):
             with tracing.span("pack"):
                 mat = kernels.pack_columns(parts, dt)
             meta = {"ml_attr": {"num_attrs": int(mat.shape[0])}}
-        return ColumnData(VectorUDT(), mat, None, meta)
+        return ColumnData(VectorUDT(), mat, None, meta, [c for c in checks if c is not None])
+
+
+def _with_checks(col, checks):
+    col.checks = [c for c in checks if c is not None]
+    return col
 
 
 @param_accessors

@@ -48,9 +48,11 @@ def _sample_moments(stats: GramStats):
 
 
 def train_lbfgs(est, df, tbl, X, y, d):
-    from .regression import (LinearRegressionModel, LinearRegressionTrainingSummary, _weight_of)
+    from ..runtime.checks import verify
+    from .regression import (LinearRegressionModel, LinearRegressionTrainingSummary, _fit_checks, _weight_of)
 
     loss = est.getOrDefault("loss")
+    verify(_fit_checks(est, tbl, X))  # the iterative path reads host statistics at once anyway
     w = _weight_of(est, tbl)
     sel = tbl.sel
     if y.valid is not None:

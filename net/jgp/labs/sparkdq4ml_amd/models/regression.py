@@ -25,7 +25,8 @@ import torch
 from ..ops import kernels
 from ..parallel import comm
 from ..sql.dataframe import DataFrame
-from ..sql.expressions import AnalysisException, ColRef, EvalContext, Expr
+from ..runtime.checks import defer, verify
+from ..sql.expressions import AnalysisException, ColRef, EvalContext, Expr, SparkException
 from ..sql.plan import Project, execute
 from ..sql.table import ColumnData
 from ..sql.types import DoubleType, VectorUDT, is_numeric
@@ -98,6 +99,28 @@ def _weight_of(params, tbl):
         w = tbl.column(params.getOrDefault("weightCol"))
         return w.values.to(torch.float64) if w.values.dtype != torch.float32 else w.values
     return None
+
+
+def _fit_checks(params, tbl, X) -> list:
+    """Data errors of a fit as pending device flags (``runtime/checks.py``; no host sync): the
+    features' own pending checks (``VectorAssembler`` nulls), a null feature vector, and a null
+    weight -- Spark 2.4 fails the job on the latter (``Row(label: Double, weight: Double, ...)``
+    pattern in ``LinearRegression.train`` -> ``scala.MatchError``)."""
+    checks = list(getattr(X, "checks", []))
+    live = None
+    if X.valid is not None:
+        live = tbl.sel_mask()
+        checks.append(defer((live & ~X.valid).any(), lambda: ValueError("features column contains nulls")))
+    if params.isSet("weightCol") and params.getOrDefault("weightCol"):
+        name = params.getOrDefault("weightCol")
+        wc = tbl.column(name)
+        if wc.valid is not None:
+            live = tbl.sel_mask() if live is None else live
+            checks.append(defer((live & ~wc.valid).any(), lambda: SparkException(
+                f"Job aborted due to stage failure: scala.MatchError: [null weight in column {name}] "
+                f"(of class org.apache.spark.sql.catalyst.expressions.GenericRowWithSchema)")))
+        checks.extend(wc.checks)
+    return [c for c in checks if c is not None]
 
 
 def _features_label(params, df: DataFrame):
@@ -178,8 +201,7 @@ class LinearRegression(_LRParams):
         return train_lbfgs(self, df, tbl, X, y, d)
 
     def _train_wls(self, df, tbl, X, y, d):
-        if X.valid is not None and bool((tbl.sel_mask() & ~X.valid).any()):
-            raise ValueError("features column contains nulls")
+        checks = _fit_checks(self, tbl, X)
         w = _weight_of(self, tbl)
         sel = tbl.sel
         yv, yvalid = y.values, y.valid
@@ -201,7 +223,7 @@ class LinearRegression(_LRParams):
                 # stream too.  Not with N > 1: co-running with the next Gram pass the fold's loads
                 # queue behind its HBM stream (8 us alone, ~100 us co-running), and the side stream
                 # must still fit the all-reduce and the solve into one Gram period
-                defer = overlap and _async_conf(df) and d <= 64 and comm.world_size() == 1
+                defer = overlap and _async_conf(df) and d <= 64 and not comm.collectives_active()
                 flat = kernels.gram_stats(X.values, yv, w, sel, gd, x_zero_dead=x_zero_dead, defer=defer)
         tracing.add_rows("gram", tbl.nrows)
         _rank_health(df)
@@ -214,7 +236,7 @@ class LinearRegression(_LRParams):
             # next fit's Gram pass) instead of following it (in-process A/B, 1x MI355X, d = 32:
             # 159.3 -> 151.7 us per fit at 1.25e7 rows, 1033 -> 1025 us at 1e8; scripts/overlap_ab.py)
             with tracing.span("solve"):
-                pending = _PendingWLS(args, overlap=overlap)  # resolved on first read
+                pending = _PendingWLS(args, overlap=overlap, checks=checks)  # resolved on first read
             model = LinearRegressionModel(self.uid, None, 0.0)
             model._pending = pending
             self.copyValues(model)
@@ -231,6 +253,7 @@ class LinearRegression(_LRParams):
         self.copyValues(model)
         with tracing.span("solve"):
             wls, stats = fit_wls_flat(*args)
+        verify(checks)  # the solve has synchronised: reading the flags costs one small copy
         model._coefficients = DenseVector(wls.coefficients)
         model._intercept = float(wls.intercept)
         model._set_summary(LinearRegressionTrainingSummary(model, df, wls, wls.objectiveHistory,
@@ -272,7 +295,7 @@ def _skinny_cols(X, gram_dtype) -> bool:
 def _rank_health(df):
     """Rank-health barrier before the first distributed fit of a session (``dq4ml.healthCheck``:
     ``once`` (default) | ``always`` | ``never``) — a dead rank surfaces as ``RankFailure``."""
-    if comm.world_size() == 1:
+    if not comm.collectives_active():
         return
     sess = getattr(df, "sparkSession", None)
     mode = str(sess.conf.get("dq4ml.healthCheck", "once")).lower() if sess is not None else "once"
@@ -320,11 +343,12 @@ class _PendingWLS:
     for the next launch at once (the Gram kernel leaves CU slots for the one-workgroup solve and
     the RCCL kernel).  ``resolve()`` orders the caller's stream after the tail before reading."""
 
-    def __init__(self, args, overlap: bool = False):
+    def __init__(self, args, overlap: bool = False, checks=None):
         from ..ops import device
 
         flat, d, fit_icpt, reg, enet, std_f, std_l = args[:7]
         self._done = None
+        self._checks = list(checks or [])
         if hasattr(flat, "finish") and not overlap:
             flat = flat.finish()
         if overlap:
@@ -352,6 +376,7 @@ class _PendingWLS:
             if self._done is not None:
                 torch.cuda.current_stream(flat.device).wait_event(self._done)
             host = self.out.cpu().numpy()
+            verify(self._checks)  # data errors of the fit surface here, on first read
             if int(host[d + 1]) != 0:  # edge case: the host driver owns warnings/errors/fallbacks
                 self._res = fit_wls_flat(*self.args)
             else:
@@ -387,7 +412,8 @@ class PredictExpr(Expr):
     def eval(self, ctx: EvalContext) -> ColumnData:
         X = ctx.table.column(self.features)
         with tracing.span("predict"):
-            return ColumnData(DoubleType(), kernels.predict(X.values, self.coef, self.intercept), X.valid)
+            return ColumnData(DoubleType(), kernels.predict(X.values, self.coef, self.intercept), X.valid,
+                              checks=list(X.checks))
 
 
 @param_accessors

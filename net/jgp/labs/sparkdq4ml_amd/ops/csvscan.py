@@ -274,7 +274,7 @@ def _scan_chunked(h, data, ncols: int, sep: str, dev, chunk_bytes: int, pinned: 
 
 def _or_reduce(masks: torch.Tensor) -> torch.Tensor:
     """Bitwise-OR all-reduce of the per-column class masks via MAX over bit planes."""
-    if comm.world_size() == 1:
+    if not comm.collectives_active():
         return masks
     bits = torch.stack([(masks >> i) & 1 for i in range(7)]).to(torch.int32)
     bits = comm.all_reduce_max(bits)

@@ -238,6 +238,19 @@ def _cast(g, v, m, src: DataType, to: DataType):
 _CMPS = {"<": "<", ">": ">", "<=": "<=", ">=": ">=", "=": "==", "==": "==", "!=": "!=", "<>": "!="}
 
 
+def _spark_cmp_c(op: str, a: str, b: str) -> str:
+    """C form of Spark SQL's NaN-aware float ordering (NaN = NaN, NaN above everything); the
+    torch form is ``sql.expressions._spark_cmp``."""
+    an, bn = f"__builtin_isnan({a})", f"__builtin_isnan({b})"
+    if op in ("=", "==", "!=", "<>"):
+        eq = f"(({a} == {b}) || ({an} && {bn}))"
+        return eq if op in ("=", "==") else f"(!{eq})"
+    return {"<": f"(!{an} && ({bn} || {a} < {b}))",
+            ">": f"(!{bn} && ({an} || {a} > {b}))",
+            "<=": f"({bn} || (!{an} && {a} <= {b}))",
+            ">=": f"({an} || (!{bn} && {a} >= {b}))"}[op]
+
+
 def _binop(g, e: E.BinOp, chain, schema, live):
     if e.op in ("and", "or"):
         av, am, _ = _compile(g, e.left, chain, schema, live)
@@ -259,11 +272,15 @@ def _binop(g, e: E.BinOp, chain, schema, live):
     a, b = f"(({oc})({av}))", f"(({oc})({bv}))"
     v, m = g.tmp("v"), g.tmp("m")
     if e.op in _CMPS:
-        g.emit(f"const bool {v} = {a} {_CMPS[e.op]} {b};")
+        if oc in ("double", "float") and not getattr(e, "ieee", False):
+            g.emit(f"const bool {v} = {_spark_cmp_c(e.op, a, b)};")
+        else:
+            g.emit(f"const bool {v} = {a} {_CMPS[e.op]} {b};")
         g.emit(f"const bool {m} = ({am}) && ({bm});")
         return v, m, BooleanType()
     if e.op == "<=>":
-        g.emit(f"const bool {v} = (({am}) && ({bm}) && ({a} == {b})) || (!({am}) && !({bm}));")
+        eq = _spark_cmp_c("=", a, b) if oc in ("double", "float") else f"({a} == {b})"
+        g.emit(f"const bool {v} = (({am}) && ({bm}) && {eq}) || (!({am}) && !({bm}));")
         return v, "true", BooleanType()
     if e.op in ("+", "-", "*"):
         g.emit(f"const {oc} {v} = {a} {e.op} {b};")

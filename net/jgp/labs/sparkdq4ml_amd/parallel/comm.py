@@ -23,12 +23,17 @@ import torch
 import torch.distributed as dist
 
 __all__ = ["init", "is_initialized", "rank", "world_size", "local_rank", "barrier", "health_check", "RankFailure",
-           "all_reduce_sum",
+           "collectives_active", "force_collectives", "backend", "rccl_version", "all_reduce_sum",
            "all_reduce_max", "broadcast", "all_gather_object", "gather_rows_to_root", "shutdown",
            "DEFAULT_BUCKET_BYTES"]
 
 DEFAULT_BUCKET_BYTES = int(os.environ.get("DQ4ML_BUCKET_BYTES", str(16 << 20)))
 _side_stream = None
+# DQ4ML_FORCE_COLLECTIVES=1: every collective goes through the process group even at world size 1
+# (a one-rank RCCL communicator on a one-GPU box), so the nccl code path -- device_id init,
+# bucketed side-stream all-reduce, async health check, the overlapped fit tail's RCCL call on
+# the side stream, record_stream lifetimes -- is exercised without an 8-GPU node.
+_force = os.environ.get("DQ4ML_FORCE_COLLECTIVES", "0").lower() in ("1", "true", "yes")
 
 
 def is_initialized() -> bool:
@@ -47,6 +52,31 @@ def local_rank() -> int:
     return int(os.environ.get("LOCAL_RANK", "0"))
 
 
+def force_collectives(on: bool = True):
+    """Route world-size-1 collectives through the process group too (see ``DQ4ML_FORCE_COLLECTIVES``)."""
+    global _force
+    _force = bool(on)
+
+
+def collectives_active() -> bool:
+    """True when collectives must be issued: a process group exists and either spans more than
+    one rank or the forced-collective mode is on."""
+    return is_initialized() and (dist.get_world_size() > 1 or _force)
+
+
+def backend() -> Optional[str]:
+    return dist.get_backend() if is_initialized() else None
+
+
+def rccl_version() -> Optional[str]:
+    """RCCL version torch links against (``torch.cuda.nccl.version()``; RCCL on ROCm)."""
+    try:
+        v = torch.cuda.nccl.version()
+    except Exception:  # noqa: BLE001 - CPU-only builds
+        return None
+    return ".".join(str(x) for x in v) if isinstance(v, tuple) else str(v)
+
+
 class RankFailure(RuntimeError):
     """A peer rank did not answer a health check / collective in time."""
 
@@ -63,7 +93,11 @@ def init(backend: Optional[str] = None, timeout_s: Optional[float] = None):
         return
     timeout_s = _timeout_s() if timeout_s is None else timeout_s
     if int(os.environ.get("WORLD_SIZE", "1")) <= 1 and "MASTER_ADDR" not in os.environ:
-        return
+        if not _force:
+            return
+        # forced collectives on a single process: a one-rank group on a private port
+        os.environ.update(RANK="0", WORLD_SIZE="1", LOCAL_RANK=os.environ.get("LOCAL_RANK", "0"),
+                          MASTER_PORT=os.environ.get("MASTER_PORT") or str(_free_port()))
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     if backend is None:
         backend = "nccl" if torch.cuda.is_available() else "gloo"
@@ -74,6 +108,16 @@ def init(backend: Optional[str] = None, timeout_s: Optional[float] = None):
     dist.init_process_group(backend=backend, timeout=datetime.timedelta(seconds=timeout_s), **kw)
 
 
+def _free_port() -> int:
+    import socket
+
+    sock = socket.socket()
+    sock.bind(("127.0.0.1", 0))
+    port = sock.getsockname()[1]
+    sock.close()
+    return port
+
+
 def shutdown():
     if is_initialized():
         dist.destroy_process_group()
@@ -82,7 +126,7 @@ def shutdown():
 def health_check(timeout_s: float = 30.0):
     """Rank-health barrier: every rank contributes 1; raises :class:`RankFailure` (naming the
     missing ranks where the backend can tell) instead of blocking forever on a dead peer."""
-    if world_size() == 1:
+    if not collectives_active():
         return
     if dist.get_backend() == "gloo":
         try:
@@ -141,7 +185,7 @@ def set_bucket_bytes(n: int):
 def all_reduce_sum(t: torch.Tensor, bucket_bytes: Optional[int] = None) -> torch.Tensor:
     """Sum ``t`` over all ranks (returns a tensor on ``t``'s device).  Order of summation is fixed
     for a fixed world size, so repeated runs are bit-reproducible."""
-    if world_size() == 1:
+    if not collectives_active():
         return t
     _fault("before_allreduce")
     bucket_bytes = bucket_bytes or _bucket_bytes
@@ -173,7 +217,7 @@ def _bucketed_all_reduce(x: torch.Tensor, bucket_bytes: int):
 
 
 def all_reduce_max(t: torch.Tensor) -> torch.Tensor:
-    if world_size() == 1:
+    if not collectives_active():
         return t
     x = _comm_tensor(t.contiguous())
     dist.all_reduce(x, op=dist.ReduceOp.MAX)
@@ -181,7 +225,7 @@ def all_reduce_max(t: torch.Tensor) -> torch.Tensor:
 
 
 def broadcast(t: torch.Tensor, src: int = 0) -> torch.Tensor:
-    if world_size() == 1:
+    if not collectives_active():
         return t
     x = _comm_tensor(t.contiguous())
     dist.broadcast(x, src=src)
@@ -189,7 +233,7 @@ def broadcast(t: torch.Tensor, src: int = 0) -> torch.Tensor:
 
 
 def all_gather_object(obj) -> List:
-    if world_size() == 1:
+    if not collectives_active():
         return [obj]
     out = [None] * world_size()
     dist.all_gather_object(out, obj)

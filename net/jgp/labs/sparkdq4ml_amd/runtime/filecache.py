@@ -137,7 +137,9 @@ def open_pinned(path: str, lo: int = 0, hi: int = -1) -> PinnedFile:
         if pf is not None:
             _cache.move_to_end(key)
             return pf
-        for k in [k for k in _cache if k[0] == key[0]]:  # the file changed: drop the stale copy
+        # the file changed (size or mtime differ): drop its stale copies; other byte ranges of
+        # an unchanged file stay cached
+        for k in [k for k in _cache if k[0] == key[0] and k[1:3] != key[1:3]]:
             del _cache[k]
         pf = PinnedFile(path, lo, hi)
         _cache[key] = pf

@@ -205,9 +205,34 @@ _CMP = {"<": torch.lt, ">": torch.gt, "<=": torch.le, ">=": torch.ge, "=": torch
 _ARITH = {"+": torch.add, "-": torch.sub, "*": torch.mul}
 
 
+def _spark_cmp(op: str, a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """Spark SQL's NaN-aware float/double ordering (``SQLOrderingUtil``/``NaN semantics``): NaN
+    equals NaN and sorts above every other value, including +Infinity.  Integral operands take
+    the plain comparison."""
+    if not (a.is_floating_point() or b.is_floating_point()):
+        return _CMP[op](a, b)
+    an, bn = torch.isnan(a), torch.isnan(b)
+    if op in ("=", "==", "!=", "<>"):
+        eq = torch.eq(a, b) | (an & bn)
+        return eq if op in ("=", "==") else ~eq
+    if op == "<":
+        return ~an & (bn | torch.lt(a, b))
+    if op == ">":
+        return ~bn & (an | torch.gt(a, b))
+    if op == "<=":
+        return bn | (~an & torch.le(a, b))
+    return an | (~bn & torch.ge(a, b))  # ">="
+
+
 class BinOp(Expr):
-    def __init__(self, op: str, left: Expr, right: Expr):
+    """Binary operator.  Comparisons follow Spark SQL (NaN = NaN, NaN above everything) unless
+    ``ieee=True``: the rule IR of a Java UDF body (``dq/rules.py``) compares primitive doubles
+    with Java's IEEE semantics (every comparison with NaN is false), exactly as the reference's
+    ``MinimumPriceDataQualityService.java:8`` / ``PriceCorrelationDataQualityService.java:6`` do."""
+
+    def __init__(self, op: str, left: Expr, right: Expr, ieee: bool = False):
         self.op, self.left, self.right = op, to_expr(left), to_expr(right)
+        self.ieee = bool(ieee)
 
     def children(self):
         return [self.left, self.right]
@@ -263,7 +288,7 @@ class BinOp(Expr):
         if self.op == "<=>":
             t = self.operand_type(schema)
             lm, rm = l.valid_mask(ctx.device), r.valid_mask(ctx.device)
-            eq = torch.eq(_num(l, t), _num(r, t))
+            eq = _spark_cmp("=", _num(l, t), _num(r, t))
             return ColumnData(BooleanType(), (lm & rm & eq) | (~lm & ~rm), None)
         if isinstance(l.dtype, StringType) and isinstance(r.dtype, StringType):
             if self.op not in _CMP:
@@ -283,7 +308,8 @@ class BinOp(Expr):
             valid = _and_valid(l, r)
         a, b = _num(l, t), _num(r, t)
         if self.op in _CMP:
-            return ColumnData(BooleanType(), _CMP[self.op](a, b), valid)
+            cmp = _CMP[self.op](a, b) if self.ieee else _spark_cmp(self.op, a, b)
+            return ColumnData(BooleanType(), cmp, valid)
         if self.op in _ARITH:
             return ColumnData(t, _ARITH[self.op](a, b).to(t.torch_dtype), valid)
         if self.op == "/":

@@ -30,6 +30,7 @@ class ColumnData:  # noqa: D101 (dataclass below)
     values: object  # torch.Tensor [n] | [d, n] (VectorUDT) | list (StringType)
     valid: Optional[torch.Tensor] = None  # bool [n]; None => no nulls
     meta: dict = field(default_factory=dict)
+    checks: list = field(default_factory=list)  # pending runtime.checks.DeviceCheck (data errors)
 
     @property
     def n(self) -> int:
@@ -66,7 +67,7 @@ class ColumnData:  # noqa: D101 (dataclass below)
         else:
             vals = self.values.index_select(0, idx.to(self.values.device))
         valid = None if self.valid is None else self.valid.index_select(0, idx.to(self.valid.device))
-        return ColumnData(self.dtype, vals, valid, dict(self.meta))
+        return ColumnData(self.dtype, vals, valid, dict(self.meta), list(self.checks))
 
     def slice(self, start: int, stop: int) -> "ColumnData":
         from ..ops.layout import TiledBF16, TiledWide
@@ -80,10 +81,15 @@ class ColumnData:  # noqa: D101 (dataclass below)
         else:
             vals = self.values[start:stop]
         valid = None if self.valid is None else self.valid[start:stop]
-        return ColumnData(self.dtype, vals, valid, dict(self.meta))
+        return ColumnData(self.dtype, vals, valid, dict(self.meta), list(self.checks))
 
     def to_pylist(self) -> list:
-        """Host python values (None for null) — used by show/collect."""
+        """Host python values (None for null) — used by show/collect.  Raises a pending data
+        error of the column (``runtime.checks``) first."""
+        if self.checks:
+            from ..runtime.checks import verify
+
+            verify(self.checks)
         if isinstance(self.values, list):
             vals = list(self.values)
         elif isinstance(self.dtype, VectorUDT):
@@ -119,6 +125,7 @@ class LazyVectorColumn(ColumnData):
         self._vals = None
         self._n = int(n)
         self.sources = sources  # (parts, sel)
+        self.checks = []
 
     @property
     def values(self):

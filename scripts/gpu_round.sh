@@ -18,7 +18,10 @@ STEPS=${STEPS:-"info tests bench prof"}
 for s in $STEPS; do
   case $s in
     info) step info 300 python -c "import torch,sys; sys.path.insert(0,'.'); from net.jgp.labs.sparkdq4ml_amd.ops import native; print(native.hip().device_info())" ;;
-    tests) step tests 900 python -m pytest tests -m gpu -q --maxfail=10 --ignore tests/test_gpu_wide.py ;;
+    tests) step tests 900 python -u -m pytest tests -m gpu -q --maxfail=10 --timeout 120 --timeout-method thread --ignore tests/test_gpu_wide.py ;;
+    alltests) step alltests 900 python -u -m pytest tests -m gpu -q --maxfail=10 --timeout 120 --timeout-method thread ;;
+    rccl) step rccl 300 python -u -m pytest tests/test_gpu_rccl.py -v --timeout 120 --timeout-method thread ;;
+    t) step t 600 python -u -m pytest ${TESTS} -m gpu -v --maxfail=5 --timeout 120 --timeout-method thread ;;
     widetests) step widetests 600 python -m pytest tests/test_gpu_wide.py -m gpu -q --maxfail=5 ;;
     wide16) step wide16 600 env N=2e6 D=1024 EB=16 python scripts/wide_bench.py ;;
     wide8) step wide8 900 env N=1e7 D=4096 EB=8 VARIANTS="${VARIANTS:-4:morton:4}" python scripts/wide_bench.py ;;

@@ -46,3 +46,26 @@ def test_bench_py_json_contract():
     assert line["n_gpus"] == 1 and line["steps"] == 2 and line["warmup"] == 1 and line["higher_is_better"] is True
     assert line["metric"].startswith("rows/sec LinearRegression.fit")
     assert line["config"]["coef_max_abs_err"] < 0.05
+
+
+def test_bench_py_self_launches_ranks():
+    """``bench.py --gpus 2`` with no launcher spawns its own two ranks (gloo on this CPU box) and
+    reports the two-rank run: n_gpus 2, dp2, one device per rank."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR",
+                                                             "MASTER_PORT")}
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2",
+                          "--warmup", "1", "--rows", "40000"], capture_output=True, text=True, timeout=600, env=env)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [ln for ln in out.stdout.strip().splitlines() if ln.startswith("{")]
+    assert len(lines) == 1  # rank 0 only
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["world"] == 2 and line["config"]["parallelism"] == "dp2"
+    assert line["backend"] == "gloo" and len(line["rank_devices"]) == 2
+    assert line["config"]["coef_max_abs_err"] < 0.05
+
+
+def test_bench_py_rejects_mismatched_world():
+    env = dict(os.environ, WORLD_SIZE="3")
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "1",
+                          "--warmup", "0", "--rows", "1000"], capture_output=True, text=True, timeout=300, env=env)
+    assert out.returncode == 2 and "WORLD_SIZE=3" in out.stderr

@@ -316,3 +316,27 @@ def test_shard_range_matches_in_memory_sharding(tmp_path):
         for world in (1, 2, 3, 8):
             for r in range(world):
                 assert shard_range(str(p), r, world) == shard_byte_range(data, r, world), (trial, world, r)
+
+
+def test_filecache_keeps_other_ranges_of_unchanged_file(tmp_path, monkeypatch):
+    """Two byte ranges of one unchanged file stay cached side by side; a rewrite evicts both."""
+    import os
+    import time
+
+    from net.jgp.labs.sparkdq4ml_amd.runtime import filecache
+
+    class _Dummy:
+        def __init__(self, path, lo, hi):
+            self.nbytes = hi - lo
+
+    monkeypatch.setattr(filecache, "PinnedFile", _Dummy)
+    filecache.clear()
+    p = tmp_path / "a.csv"
+    p.write_bytes(b"1,2\r3,4\r5,6")
+    a, b = filecache.open_pinned(str(p), 0, 4), filecache.open_pinned(str(p), 4, 11)
+    assert filecache.open_pinned(str(p), 0, 4) is a and filecache.open_pinned(str(p), 4, 11) is b
+    p.write_bytes(b"1,2\r3,4\r5,7")
+    os.utime(p, ns=(time.time_ns() + 10**9, time.time_ns() + 10**9))
+    a2 = filecache.open_pinned(str(p), 0, 4)
+    assert a2 is not a and len(filecache._cache) == 1
+    filecache.clear()
