@@ -34,8 +34,15 @@ void feature_amax(const PackSrcW* srcs_dev, int d, int64_t n, const uint8_t* sel
 // eb = 16 (bf16) or 8 (fp8 e4m3, values multiplied by inv_scale[f] before conversion)
 void pack_wide(int eb, const PackSrcW* srcs_dev, int d, int64_t n, int nt, const uint8_t* sel, const float* inv_scale,
                void* out, hipStream_t st);
+// zero the rows with sel[r] == 0 (and rows >= n) of a wide tiled matrix: in -> out (may alias)
+void wide_mask_rows(int eb, const void* in, void* out, int d, int64_t n, const uint8_t* sel, hipStream_t st);
 // out: flat WLS layout [count, wSum, wwSum, bSum, bbSum, aSum(d), abSum(d), aa packed-upper(d)]
 void gram_wide(int eb, WideArgs a, const int* pairs_dev, const float* scales, double* out, hipStream_t st,
                int ring = 4, int waves = 4);
+// persistent XCD-grouped schedule: grid blocks (one per CU, a multiple of 8), group b % 8 owns
+// splits [g*h, g*h+h) (a.splitk == 8*h) and dequeues (split, pair) units from heads[g] (8 ints,
+// zeroed here on the stream)
+void gram_wide_queue(int eb, WideArgs a, const int* pairs_dev, const float* scales, double* out, int* heads, int h,
+                     int grid, hipStream_t st, int waves = 8);
 
 }  // namespace dq4ml

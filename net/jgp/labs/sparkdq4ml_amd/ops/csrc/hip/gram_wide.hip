@@ -302,6 +302,39 @@ __global__ __launch_bounds__(64 * WAVES, 1) void gram_wide_kernel(WideArgs a) {
   else syrk_block<EB, 2, RING, WAVES, ABL>(a, smem, I, J, pair, split);
 }
 
+// Persistent, XCD-grouped schedule.  The grid is one block per CU; block b belongs to group
+// g = b % 8 (blocks dispatched round-robin over the 8 XCDs: a group shares one XCD's L2 -- for
+// speed only, any placement is correct).  Group g owns the row ranges (splits) g*h .. g*h+h-1 and
+// pulls (split, pair) work units from its own queue head in list order: the ~32 blocks of a group
+// always run a sliding window of consecutive units of the SAME row range whose panels overlap
+// (Z-order pair list), so each panel-stage is fetched from HBM about once per window and then
+// served from that XCD's L2 to every block of the window.  With the static one-pair-per-block
+// grid, co-resident blocks of an XCD mix row ranges and finish at different times (diagonal and
+// augmentation pairs are cheaper), which left the L2 hit rate at 54 % and the fabric reading each
+// input byte ~8x.  The dynamic queue also absorbs the unequal unit costs.
+template <int EB, int RING, int WAVES>
+__global__ __launch_bounds__(64 * WAVES, 1) void gram_wide_queue_kernel(WideArgs a, int* __restrict__ heads, int h) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  int* slot = reinterpret_cast<int*>(smem + RING * kStageBytes);  // same LDS array as the ring
+  const int g = blockIdx.x & 7;
+  const int npair = (a.npanels + 1) * (a.npanels + 2) / 2;
+  const int units = npair * h;
+  for (;;) {
+    if (threadIdx.x == 0) slot[0] = atomicAdd(&heads[g], 1);
+    __syncthreads();
+    const int u = slot[0];
+    __syncthreads();  // every wave has read the slot (and finished the previous unit's LDS reads)
+    if (u >= units) break;
+    const int k = u / npair, pos = u - k * npair;
+    const int split = g * h + k;
+    const int I = a.pairs[2 * pos], J = a.pairs[2 * pos + 1];
+    if (I == J && J != a.npanels) syrk_block<EB, 3, RING, WAVES>(a, smem, I, J, pos, split);
+    else if (J != a.npanels) syrk_block<EB, 0, RING, WAVES>(a, smem, I, J, pos, split);
+    else if (I != a.npanels) syrk_block<EB, 1, RING, WAVES>(a, smem, I, J, pos, split);
+    else syrk_block<EB, 2, RING, WAVES>(a, smem, I, J, pos, split);
+  }
+}
+
 // f64 reduction of the split-K slabs, fp8 scales applied, straight into the flat WLS layout:
 // [count, wSum, wwSum, bSum, bbSum, aSum(d), abSum(d), aa packed-upper(d)]
 
@@ -429,7 +462,64 @@ __global__ __launch_bounds__(256) void pack_wide_kernel(const PackSrcW* __restri
   }
 }
 
+// Zero the dead rows of a wide fragment-ordered matrix (a DQ selection applied AFTER the pack):
+// one pass over the storage, 16 B per thread, no dequantize / re-pack.  In both layouts a 16-B
+// unit holds 8-row runs of ONE feature: bf16 = rows s*64 + 16ki + 8h + [0, 8) (unit = (s, t, ki,
+// lane)), fp8 = two runs 16 rows apart, k-steps 2kh and 2kh + 1 (unit = (s, t, kh, lane));
+// lane = 32h + feature % 32.
+template <int EB>
+__global__ __launch_bounds__(256) void wide_mask_rows_kernel(const u32x4* __restrict__ in, u32x4* __restrict__ out,
+                                                            int64_t units, int NT, int64_t n,
+                                                            const uint8_t* __restrict__ sel) {
+  constexpr int kUnitsPerChunk = EB == 8 ? 128 : 256;
+  auto run_mask = [&](int64_t r0) -> uint64_t {  // 0x01 per live row byte, rows past n dead
+    if (r0 + 8 <= n) return *gptr<uint64_t>(sel + r0);
+    uint64_t m = 0;
+    for (int j = 0; j < 8; ++j)
+      if (r0 + j < n && sel[r0 + j]) m |= 1ull << (8 * j);
+    return m;
+  };
+  for (int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; u < units; u += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t c = u / kUnitsPerChunk;
+    const int q = (int)(u - c * kUnitsPerChunk);
+    const int64_t s = c / NT;
+    const int lane = q & 63, h = lane >> 5;
+    u32x4 v = in[u];
+    if constexpr (EB == 8) {
+      const int kh = q >> 6;
+      const int64_t base = s * 64 + 32 * kh + 8 * h;
+      const uint64_t m0 = run_mask(base) * 0xffull, m1 = run_mask(base + 16) * 0xffull;  // bytes 0x01 -> 0xff
+      v[0] &= (unsigned)m0, v[1] &= (unsigned)(m0 >> 32), v[2] &= (unsigned)m1, v[3] &= (unsigned)(m1 >> 32);
+    } else {
+      const int ki = q >> 6;
+      const uint64_t m = run_mask(s * 64 + 16 * ki + 8 * h);
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {  // dword w = rows 2w, 2w+1
+        const unsigned lo = (unsigned)((m >> (16 * w)) & 1) * 0xffffu;
+        const unsigned hi = (unsigned)((m >> (16 * w + 8)) & 1) * 0xffff0000u;
+        v[w] &= lo | hi;
+      }
+    }
+    out[u] = v;
+  }
+}
+
 }  // namespace
+
+void wide_mask_rows(int eb, const void* in, void* out, int d, int64_t n, const uint8_t* sel, hipStream_t st) {
+  const int NT = ((d + 255) / 256) * 8;
+  const int64_t units = wide_tiled_bytes(eb, d, n) / 16;
+  int64_t g = (units + 255) / 256;
+  if (g > 16384) g = 16384;
+  if (g < 1) g = 1;
+  if (eb == 8)
+    hipLaunchKernelGGL(wide_mask_rows_kernel<8>, dim3(g), dim3(256), 0, st, reinterpret_cast<const u32x4*>(in),
+                       reinterpret_cast<u32x4*>(out), units, NT, n, sel);
+  else
+    hipLaunchKernelGGL(wide_mask_rows_kernel<16>, dim3(g), dim3(256), 0, st, reinterpret_cast<const u32x4*>(in),
+                       reinterpret_cast<u32x4*>(out), units, NT, n, sel);
+  DQ_HIP_CHECK(hipGetLastError());
+}
 
 int64_t wide_tiled_bytes(int eb, int d, int64_t n) {
   const int NT = ((d + 255) / 256) * 8;
@@ -478,6 +568,31 @@ static void launch_wide_eb(const WideArgs& a, int nblocks, hipStream_t st, int r
   if (waves == 83) return launch_wide<EB, 4, 8, 3>(a, nblocks, st);
   if (waves == 8) ring == 5 ? launch_wide<EB, 5, 8>(a, nblocks, st) : launch_wide<EB, 4, 8>(a, nblocks, st);
   else ring == 5 ? launch_wide<EB, 5, 4>(a, nblocks, st) : launch_wide<EB, 4, 4>(a, nblocks, st);
+}
+
+template <int EB, int RING, int WAVES>
+static void launch_wide_queue(const WideArgs& a, int grid, int* heads, int h, hipStream_t st) {
+  const size_t lds = (size_t)RING * kStageBytes + 16;
+  DQ_HIP_CHECK(hipFuncSetAttribute((const void*)gram_wide_queue_kernel<EB, RING, WAVES>,
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  hipLaunchKernelGGL((gram_wide_queue_kernel<EB, RING, WAVES>), dim3(grid), dim3(64 * WAVES), lds, st, a, heads, h);
+  DQ_HIP_CHECK(hipGetLastError());
+}
+
+void gram_wide_queue(int eb, WideArgs a, const int* pairs_dev, const float* scales, double* out, int* heads, int h,
+                     int grid, hipStream_t st, int waves) {
+  a.pairs = pairs_dev;
+  if (a.splitk != 8 * h) throw std::invalid_argument("gram_wide_queue: splitk must be 8 * h");
+  if (grid < 8 || grid % 8) throw std::invalid_argument("gram_wide_queue: grid must be a positive multiple of 8");
+  if (waves != 4 && waves != 8) throw std::invalid_argument("gram_wide_queue: waves must be 4 or 8");
+  DQ_HIP_CHECK(hipMemsetAsync(heads, 0, 8 * sizeof(int), st));
+  if (eb == 16) waves == 8 ? launch_wide_queue<16, 4, 8>(a, grid, heads, h, st) : launch_wide_queue<16, 4, 4>(a, grid, heads, h, st);
+  else waves == 8 ? launch_wide_queue<8, 4, 8>(a, grid, heads, h, st) : launch_wide_queue<8, 4, 4>(a, grid, heads, h, st);
+  const int P = a.npanels;
+  int64_t g = ((int64_t)(P + 1) * (P + 2) / 2 * kPanel * kPanel + 255) / 256;
+  if (g > 16384) g = 16384;
+  hipLaunchKernelGGL(gram_wide_reduce_kernel, dim3(g), dim3(256), 0, st, a, scales, out);
+  DQ_HIP_CHECK(hipGetLastError());
 }
 
 void gram_wide(int eb, WideArgs a, const int* pairs_dev, const float* scales, double* out, hipStream_t st, int ring,

@@ -10,6 +10,7 @@
 #include "dqvm.h"
 #include "gram.h"
 #include "gram_wide.h"
+#include "gram_syrk.h"
 #include "wls_small.h"
 #include "rowops.h"
 
@@ -116,6 +117,9 @@ PYBIND11_MODULE(_dq4ml_hip, m) {
     pack_wide(eb, P<const PackSrcW>(srcs_dev), d, n, nt, P<const uint8_t>(sel), P<const float>(inv_scale), P<void>(out),
               as_stream(stream));
   });
+  m.def("wide_mask_rows", [](int eb, uintptr_t in, uintptr_t out, int d, int64_t n, uintptr_t sel, uintptr_t stream) {
+    wide_mask_rows(eb, P<const void>(in), P<void>(out), d, n, P<const uint8_t>(sel), as_stream(stream));
+  });
   m.def("feature_amax", [](uintptr_t srcs_dev, int d, int64_t n, uintptr_t sel, uintptr_t amax, uintptr_t stream) {
     feature_amax(P<const PackSrcW>(srcs_dev), d, n, P<const uint8_t>(sel), P<float>(amax), as_stream(stream));
   });
@@ -136,6 +140,45 @@ PYBIND11_MODULE(_dq4ml_hip, m) {
     a.aug_scale[1] = syh;
     a.aug_scale[2] = syl;
     gram_wide(eb, a, P<const int>(pairs), P<const float>(scales), P<double>(out), as_stream(stream), ring, waves);
+  });
+  m.def("gram_wide_queue", [](int eb, uintptr_t X, uintptr_t Xaug, uintptr_t zeros, int nt, int npanels, int d,
+                              int64_t nsup, int h, uintptr_t pairs, uintptr_t part, double s1, double syh, double syl,
+                              uintptr_t scales, uintptr_t out, uintptr_t heads, int grid, uintptr_t stream, int waves) {
+    WideArgs a{};
+    a.X = P<const unsigned char>(X);
+    a.Xaug = P<const unsigned char>(Xaug);
+    a.zeros = P<const unsigned char>(zeros);
+    a.NT = nt;
+    a.npanels = npanels;
+    a.d = d;
+    a.nsup = nsup;
+    a.splitk = 8 * h;
+    a.part = P<float>(part);
+    a.aug_scale[0] = s1;
+    a.aug_scale[1] = syh;
+    a.aug_scale[2] = syl;
+    gram_wide_queue(eb, a, P<const int>(pairs), P<const float>(scales), P<double>(out), P<int>(heads), h, grid,
+                    as_stream(stream), waves);
+  });
+
+  m.def("syrk_panels", &syrk_panels);
+  m.def("syrk_partials", &syrk_partials);
+  m.def("syrk_stages", &syrk_stages);
+  m.def("gram_syrk", [](int compute_f64, uintptr_t X, int64_t ld, int d, int64_t n, int xdt, uintptr_t y, uintptr_t w,
+                        uintptr_t pairs, int npair, int splitk, uintptr_t part, uintptr_t out, uintptr_t stream) {
+    SyrkArgs s{};
+    s.X = P<const void>(X);
+    s.ld = ld;
+    s.d = d;
+    s.n = n;
+    s.xdt = xdt;
+    s.y = P<const double>(y);
+    s.w = P<const double>(w);
+    s.pairs = P<const int>(pairs);
+    s.npair = npair;
+    s.splitk = splitk;
+    s.part = P<double>(part);
+    gram_syrk(compute_f64, s, P<double>(out), as_stream(stream));
   });
 
   // ---- compaction (K3) -----------------------------------------------------------------------

@@ -143,8 +143,10 @@ def gram_stats(X, y, w, sel, compute: str = "fp64", x_zero_dead: bool = False, b
         return _gram_wide(h, tile_wide(X, 16 if mode == 2 else 8, sel), y, None, sel, True)
     if mode == 3 and d <= 64:
         mode = 2  # tall fp8 request: the bf16 MFMA kernel is HBM-bound already and more precise
-    if d > 64 or mode == 3:
-        return _gram_fallback_wide(X, y, w, sel, compute)
+    if d > 64:
+        # fp64: f64 MFMA SYRK; fp32 and weighted bf16/fp8 requests: exact-f32 MFMA SYRK (at least
+        # the requested precision; the fragment kernels carry no per-row weights)
+        return _gram_syrk(h, X, y, w, sel, compute_f64=mode == 0)
     if mode == 1:
         # "fp32" statistics: f32 (or f64) features through the f64 MFMA kernel — products of f32
         # values are exact in f64, so this is at least the requested precision, at f32 bytes
@@ -299,31 +301,59 @@ def _gram_tiled(h, T: "TiledBF16", y, w, sel, x_zero_dead, blocks, defer=False):
     return out
 
 
-def _gram_fallback_wide(X, y, w, sel, compute):
-    """d > 64 (until the LDS-tiled MFMA SYRK lands) and fp32/fp8 requests: hipBLAS library GEMM in
-    the requested precision with f64 side sums."""
-    from . import kernels
+_syrk_pairs = {}
 
+
+def _syrk_pair_table(P: int, dev) -> torch.Tensor:
+    """Upper 128-panel pairs of the augmented matrix in Z-order (the blocks an XCD runs together
+    are consecutive in this list and share few panels), uploaded once per (P, device)."""
+    key = (P, str(dev))
+    t = _syrk_pairs.get(key)
+    if t is None:
+        pairs = sorted(((i, j) for i in range(P) for j in range(i, P)), key=lambda p: _morton(*p))
+        t = _syrk_pairs[key] = _h2d(np.asarray(pairs, dtype=np.int32).reshape(-1), dev)
+    return t
+
+
+def _gram_syrk(h, X, y, w, sel, compute_f64: bool):
+    """d > 64 at fp64 / exact-f32 precision, and weighted low-precision requests: the LDS-tiled
+    MFMA SYRK of ``gram_syrk.hip`` over the augmented [X | 1 | y] with the weight x selection
+    row factor applied in-kernel -- one pass, no library GEMM, no dense copies of X."""
     d, n = X.shape
-    dt = {"fp64": torch.float64, "fp32": torch.float32, "bf16": torch.bfloat16, "fp8": torch.bfloat16}[compute]
-    wv = torch.ones(n, dtype=torch.float64, device=X.device) if w is None else w.to(torch.float64)
-    if sel is not None:
-        wv = torch.where(sel, wv, torch.zeros_like(wv))
-    Xc = X.to(dt)
-    Xw = (X.to(torch.float64) * wv).to(dt)
-    aa = (Xw @ Xc.t()).to(torch.float64)
-    yd = y.to(torch.float64)
-    out = torch.empty(5 + 2 * d + d * (d + 1) // 2, dtype=torch.float64, device=X.device)
-    live = torch.ones(n, dtype=torch.bool, device=X.device) if sel is None else sel
-    out[0] = live.sum()
-    out[1] = wv.sum()
-    out[2] = (wv * wv).sum()
-    out[3] = (wv * yd).sum()
-    out[4] = (wv * yd * yd).sum()
-    Xd = X.to(torch.float64)
-    out[5:5 + d] = Xd @ wv
-    out[5 + d:5 + 2 * d] = Xd @ (wv * yd)
-    out[5 + 2 * d:] = kernels.packed_upper(aa)
+    dev = X.device
+    out = torch.empty(5 + 2 * d + d * (d + 1) // 2, dtype=torch.float64, device=dev)
+    if n == 0:
+        return out.zero_()
+    if X.dtype not in (torch.float64, torch.float32, torch.bfloat16):
+        X = X.to(torch.float64 if compute_f64 else torch.float32)
+    Xv, ld = _feature_view(X, 16 // X.element_size())
+    y, w, sel = _prep_rows(y, w, sel, n)
+    yd = y.to(torch.float64).contiguous()
+    weff = None
+    if w is not None:
+        weff = w.to(torch.float64)
+        if sel is not None:
+            weff = torch.where(sel, weff, torch.zeros_like(weff))
+    elif sel is not None:
+        weff = sel.to(torch.float64)
+    weff = None if weff is None else weff.contiguous()
+    P = int(h.syrk_panels(d))
+    npair = P * (P + 1) // 2
+    nst = int(h.syrk_stages(n))
+    target = 4 * _wide_grid(h)  # >= 4 blocks per CU slot wave (2 resident per CU at f64)
+    splitk = int(os.environ.get("DQ4ML_SYRK_SPLITK", "0")) or max(1, min(-(-target // npair), max(1, nst // 8)))
+    splitk = max(1, min(splitk, nst))
+    part = torch.empty(int(h.syrk_partials(d, splitk)), dtype=torch.float64, device=dev)
+    h.gram_syrk(1 if compute_f64 else 0, Xv.data_ptr(), int(ld), int(d), int(n), dtype_code(Xv), yd.data_ptr(),
+                _ptr(weff), _syrk_pair_table(P, dev).data_ptr(), npair, splitk, part.data_ptr(), out.data_ptr(),
+                _stream())
+    # the two non-Gram scalars (Spark's aggregator skips zero-weight rows: count = rows with w != 0)
+    if weff is None:
+        out[0:1].fill_(float(n))
+        out[2:3].fill_(float(n))
+    else:
+        out[0:1].copy_((weff != 0).sum().to(torch.float64).reshape(1))
+        out[2:3].copy_((weff * weff).sum().reshape(1))
     return out
 
 
@@ -577,6 +607,22 @@ def pack_wide(parts: List[torch.Tensor], eb: int, sel: Optional[torch.Tensor] = 
     return TiledWide(buf, d, n, eb, scales)
 
 
+def mask_wide_rows(T: TiledWide, sel: torch.Tensor) -> TiledWide:
+    """A copy of ``T`` whose rows with ``sel == False`` are zero (fp8 zero = 0x00, bf16 +0)."""
+    h = native.hip()
+    _check_dev(T.buf, sel)
+    if sel.numel() != T.n:
+        raise ValueError("mask_wide_rows: selection length != rows")
+    s = sel.contiguous().to(torch.bool)
+    if s.data_ptr() % 8:
+        s = s.clone()
+    out = torch.empty_like(T.buf)
+    if out.numel() != int(h.wide_tiled_bytes(T.eb, T.d, T.n)):
+        raise ValueError("mask_wide_rows: storage size does not match the wide layout")
+    h.wide_mask_rows(T.eb, T.buf.data_ptr(), out.data_ptr(), T.d, T.n, s.data_ptr(), _stream())
+    return TiledWide(out, T.d, T.n, T.eb, T.scales)
+
+
 def tile_wide(X: torch.Tensor, eb: int, sel: Optional[torch.Tensor] = None) -> TiledWide:
     return pack_wide([X], eb, sel)
 
@@ -627,12 +673,37 @@ def _wide_splitk(P: int, nsup: int, eb: int) -> int:
     return best
 
 
+def _wide_queue_h(nsup: int) -> int:
+    """Row ranges per XCD group of the persistent wide schedule (``DQ4ML_WIDE_H``, default 2:
+    ~10 units per block keeps the dynamic tail short); 0 = too few rows, use the static grid.
+    f32 accumulators count rows exactly only below 2^24 per split."""
+    hq = int(os.environ.get("DQ4ML_WIDE_H", "2"))
+    if nsup < 8 * 16:
+        return 0
+    hq = max(hq, -(-nsup * 64 // (8 << 23)))
+    return max(1, min(hq, nsup // 16))
+
+
+_wide_grids = {}
+
+
+def _wide_grid(h) -> int:
+    """One block per CU (the ring uses the whole LDS), rounded down to whole XCD groups."""
+    dev = torch.cuda.current_device()
+    if dev not in _wide_grids:
+        cus = int(h.device_info()["multiProcessorCount"])
+        _wide_grids[dev] = max(8, cus // 8 * 8)
+    return _wide_grids[dev]
+
+
 def _gram_wide(h, T: TiledWide, y, w, sel, x_zero_dead):
-    if w is not None:  # instance weights: hipBLASLt library GEMM on the dequantized matrix
-        return _gram_fallback_wide(T.to_dense(), y, w, sel, "bf16")
+    if w is not None:
+        # instance weights: the exact-f32 MFMA SYRK (per-row weight in-kernel) on the stored values
+        return _gram_syrk(h, T.to_dense(), y, w, sel, compute_f64=False)
     if sel is not None and not x_zero_dead:
-        # the stored tiles still hold the dead rows: re-pack once with the selection applied
-        T = pack_wide([T.to_dense()], T.eb, sel.contiguous().to(torch.bool))
+        # the stored tiles still hold the dead rows: zero them in one pass over the fragment
+        # storage (wide_mask_rows_kernel), no dequantize / re-pack
+        T = mask_wide_rows(T, sel)
     d, n = T.d, T.n
     dev = T.device
     _check_dev(T.buf, y, sel)
@@ -664,8 +735,19 @@ def _gram_wide(h, T: TiledWide, y, w, sel, x_zero_dead):
     if os.environ.get("DQ4ML_WIDE_SAMEPAIR"):  # diagnostic only (wrong results): every block reads panels 0, 1
         pairs = [(0, 1)] * len(pairs)
     pairs_dev = _h2d(np.asarray(pairs, dtype=np.int32).reshape(-1), dev)
-    part = torch.empty(int(h.gram_wide_partials(d, splitk)), dtype=torch.float32, device=dev)
     out = torch.empty(5 + 2 * d + d * (d + 1) // 2, dtype=torch.float64, device=dev)
+    sched = os.environ.get("DQ4ML_WIDE_SCHED", "queue")
+    hq = _wide_queue_h(nsup) if sched == "queue" else 0
+    if hq:
+        # persistent XCD-grouped schedule (gram_wide_queue_kernel): 8 groups x h row ranges
+        part = torch.empty(int(h.gram_wide_partials(d, 8 * hq)), dtype=torch.float32, device=dev)
+        heads = torch.empty(8, dtype=torch.int32, device=dev)
+        h.gram_wide_queue(eb, T.buf.data_ptr(), aug.buf.data_ptr(), _zero_page(h, dev).data_ptr(), T.nt, P, d, nsup,
+                          hq, pairs_dev.data_ptr(), part.data_ptr(), 1.0, float(s_h), float(s_l), _ptr(T.scales),
+                          out.data_ptr(), heads.data_ptr(), _wide_grid(h), _stream(),
+                          int(os.environ.get("DQ4ML_WIDE_WAVES", "8")))
+        return out
+    part = torch.empty(int(h.gram_wide_partials(d, splitk)), dtype=torch.float32, device=dev)
     h.gram_wide(eb, T.buf.data_ptr(), aug.buf.data_ptr(), _zero_page(h, dev).data_ptr(), T.nt, P, d, nsup, splitk,
                 pairs_dev.data_ptr(),
                 part.data_ptr(), 1.0, float(s_h), float(s_l), _ptr(T.scales), out.data_ptr(), _stream(),

@@ -47,6 +47,12 @@ for _ in range(reps):
         os.environ.pop("DQ4ML_WIDE_SAMEPAIR", None)
         if same:
             os.environ["DQ4ML_WIDE_SAMEPAIR"] = "1"
+        sched = "grid"
+        if fields[-1].startswith("q"):  # ...:q<h> = persistent XCD-grouped queue schedule, h row ranges/group
+            sched, hq = "queue", fields[-1][1:]
+            fields = fields[:-1]
+            os.environ["DQ4ML_WIDE_H"] = hq
+        os.environ["DQ4ML_WIDE_SCHED"] = sched
         ring, order, waves, splitk = (fields + ["4", "0"][len(fields) - 2:])[:4]
         os.environ["DQ4ML_WIDE_RING"], os.environ["DQ4ML_WIDE_ORDER"] = ring, order
         os.environ["DQ4ML_WIDE_WAVES"], os.environ["DQ4ML_WIDE_SPLITK"] = waves, splitk

@@ -49,11 +49,15 @@ def test_rccl_fit_paths_match_uncollective(rccl_run):
     assert rccl_run["coef_err"] < 5e-3
 
 
-def test_rccl_kernels_observed(rccl_run):
+def test_rccl_calls_observed(rccl_run):
+    """Only RCCL all-reduces are inside the profiled region.  A one-rank in-place all-reduce is
+    a no-op on the device (RCCL's one-rank path launches no ring kernel), so what is visible is
+    ProcessGroupNCCL's stream ordering around each call: an event on the caller's stream that
+    the communicator stream waits on.  With N ranks the same calls launch ``ncclDevKernel_*``."""
     if not rccl_run["kernels"]:
-        pytest.skip("torch profiler saw no device kernels on this box: " + rccl_run.get("profiler_error", ""))
-    # only all-reduce calls are inside the profiled region: the device work seen there is RCCL's
-    assert rccl_run["rccl_kernel_seen"] or rccl_run["rccl_copy_seen"], rccl_run["kernels"]
+        pytest.skip("torch profiler saw no HIP activity on this box: " + rccl_run.get("profiler_error", ""))
+    names = set(rccl_run["kernels"])
+    assert rccl_run["rccl_kernel_seen"] or {"hipEventRecord", "hipStreamWaitEvent"} <= names, names
 
 
 def test_bench_py_over_rccl():
