@@ -121,7 +121,7 @@ struct Staged {
   C a[8], b[8];
 };
 
-template <typename C, int SDT, bool HAS_W>
+template <typename C, int SDT, bool HAS_W, bool THIN>
 __device__ __forceinline__ void stage_load(const SyrkArgs& s, int I, int J, int64_t r0, Staged<C, SDT>& st) {
   const int fi = threadIdx.x >> 1;
   const int64_t row = r0 + (threadIdx.x & 1) * 8;
@@ -140,7 +140,7 @@ __device__ __forceinline__ void stage_load(const SyrkArgs& s, int I, int J, int6
     }
   };
   feat(I * kPanel + fi, st.a);
-  feat(J * kPanel + fi, st.b);
+  if (!THIN || fi < SyrkT<C>::kTile) feat(J * kPanel + fi, st.b);  // a thin panel: one MFMA tile of features
   if constexpr (HAS_W) {
     double w[8];
     load8_w(s.w, row, s.n, w);
@@ -153,34 +153,38 @@ __device__ __forceinline__ void stage_load(const SyrkArgs& s, int I, int J, int6
   }
 }
 
-template <typename C, int SDT>
+template <typename C, int SDT, bool THIN>
 __device__ __forceinline__ void stage_store(C* lds, const Staged<C, SDT>& st) {
   typedef SyrkT<C> T;
   const int fi = threadIdx.x >> 1, h = threadIdx.x & 1;
   C* A = lds + fi * T::kRS + h * 8;
   C* B = lds + kPanel * T::kRS + fi * T::kRS + h * 8;
+  const bool wb = !THIN || fi < T::kTile;
   if constexpr (sizeof(C) == 8) {  // 144-B feature rows: 16-B aligned runs
 #pragma unroll
     for (int j = 0; j < 8; j += 2) {
       *reinterpret_cast<f64x2*>(A + j) = f64x2{st.a[j], st.a[j + 1]};
-      *reinterpret_cast<f64x2*>(B + j) = f64x2{st.b[j], st.b[j + 1]};
+      if (wb) *reinterpret_cast<f64x2*>(B + j) = f64x2{st.b[j], st.b[j + 1]};
     }
   } else {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) A[j] = st.a[j], B[j] = st.b[j];
+    for (int j = 0; j < 8; ++j) {
+      A[j] = st.a[j];
+      if (wb) B[j] = st.b[j];
+    }
   }
 }
 
-template <typename C, int SDT, bool HAS_W>
-__global__ __launch_bounds__(kThreads, 2) void syrk_kernel(SyrkArgs s) {
+// THIN: panel J holds at most one MFMA tile of live features (the augmentation columns [1, y]
+// spilling past the last full data panel, e.g. d = 256 / 1024 / 4096): only the waves of the
+// first column half compute, one tile column each -- such pairs cost ~1/8 of a full one instead
+// of a full 128 x 128 tile of zeros.
+template <typename C, int SDT, bool HAS_W, bool THIN>
+__device__ __forceinline__ void syrk_body(const SyrkArgs& s, C* lds, int I, int J, int pair, int split) {
   typedef SyrkT<C> T;
   constexpr int TW = 64 / T::kTile;                   // MFMA tiles per wave edge
+  constexpr int TWN = THIN ? 1 : TW;                  // tile columns computed per wave
   constexpr int kBuf = 2 * kPanel * T::kRS;           // elements of one stage (A + B)
-  __shared__ __attribute__((aligned(16))) C lds[2 * kBuf];
-  const int nwg = gridDim.x, orig = blockIdx.x, xcd = orig & 7, q = nwg >> 3, rem = nwg & 7;
-  const int L = (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + (orig >> 3);
-  const int split = L / s.npair, pair = L - split * s.npair;
-  const int I = s.pairs[2 * pair], J = s.pairs[2 * pair + 1];
   const int64_t nst = (s.n + kSR - 1) / kSR;
   const int64_t st0 = nst * split / s.splitk, st1 = nst * (split + 1) / s.splitk;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, wm = wave >> 1, wn = wave & 1;
@@ -191,31 +195,34 @@ __global__ __launch_bounds__(kThreads, 2) void syrk_kernel(SyrkArgs s) {
 #pragma unroll
     for (int y = 0; y < TW; ++y) acc[x][y] = typename T::acc_t{};
 
+  const bool computes = !THIN || wn == 0;
   if (st0 < st1) {
     Staged<C, SDT> reg;
-    stage_load<C, SDT, HAS_W>(s, I, J, st0 * kSR, reg);
-    stage_store<C, SDT>(lds, reg);
+    stage_load<C, SDT, HAS_W, THIN>(s, I, J, st0 * kSR, reg);
+    stage_store<C, SDT, THIN>(lds, reg);
     __syncthreads();
     int cur = 0;
     const int fr = lane & (T::kTile - 1), kr = lane / T::kTile;
     for (int64_t st = st0; st < st1; ++st) {
       const bool more = st + 1 < st1;
-      if (more) stage_load<C, SDT, HAS_W>(s, I, J, (st + 1) * kSR, reg);  // in flight under the MFMAs
+      if (more) stage_load<C, SDT, HAS_W, THIN>(s, I, J, (st + 1) * kSR, reg);  // in flight under the MFMAs
       const C* A = lds + cur * kBuf + (wm * 64 + fr) * T::kRS + kr;
       const C* B = lds + cur * kBuf + kPanel * T::kRS + (wn * 64 + fr) * T::kRS + kr;
+      if (computes) {
 #pragma unroll
-      for (int k0 = 0; k0 < kSR; k0 += T::kK) {
-        C a[TW], b[TW];
+        for (int k0 = 0; k0 < kSR; k0 += T::kK) {
+          C a[TW], b[TWN];
 #pragma unroll
-        for (int x = 0; x < TW; ++x) a[x] = A[x * T::kTile * T::kRS + k0];
+          for (int x = 0; x < TW; ++x) a[x] = A[x * T::kTile * T::kRS + k0];
 #pragma unroll
-        for (int y = 0; y < TW; ++y) b[y] = B[y * T::kTile * T::kRS + k0];
+          for (int y = 0; y < TWN; ++y) b[y] = B[y * T::kTile * T::kRS + k0];
 #pragma unroll
-        for (int x = 0; x < TW; ++x)
+          for (int x = 0; x < TW; ++x)
 #pragma unroll
-          for (int y = 0; y < TW; ++y) acc[x][y] = T::mfma(a[x], b[y], acc[x][y]);
+            for (int y = 0; y < TWN; ++y) acc[x][y] = T::mfma(a[x], b[y], acc[x][y]);
+        }
       }
-      if (more) stage_store<C, SDT>(lds + (cur ^ 1) * kBuf, reg);
+      if (more) stage_store<C, SDT, THIN>(lds + (cur ^ 1) * kBuf, reg);
       __syncthreads();
       cur ^= 1;
     }
@@ -232,6 +239,18 @@ __global__ __launch_bounds__(kThreads, 2) void syrk_kernel(SyrkArgs s) {
         const int col = wn * 64 + y * T::kTile + T::ccol(lane);
         out[row * kPanel + col] = (double)acc[x][y][r];
       }
+}
+
+template <typename C, int SDT, bool HAS_W>
+__global__ __launch_bounds__(kThreads, 2) void syrk_kernel(SyrkArgs s) {
+  typedef SyrkT<C> T;
+  __shared__ __attribute__((aligned(16))) C lds[2 * 2 * kPanel * T::kRS];
+  const int nwg = gridDim.x, orig = blockIdx.x, xcd = orig & 7, q = nwg >> 3, rem = nwg & 7;
+  const int L = (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + (orig >> 3);
+  const int split = L / s.npair, pair = L - split * s.npair;
+  const int I = s.pairs[2 * pair], J = s.pairs[2 * pair + 1];
+  if (s.d + 2 - J * kPanel <= T::kTile) syrk_body<C, SDT, HAS_W, true>(s, lds, I, J, pair, split);
+  else syrk_body<C, SDT, HAS_W, false>(s, lds, I, J, pair, split);
 }
 
 // split-K fold + scatter of the augmented Gram into [count, wSum, wwSum, bSum, bbSum, aSum(d),
