@@ -181,6 +181,11 @@ def fit_wls_flat(flat, nf: int, fit_intercept: bool, reg_param: float, elastic_n
 
     k = nf + 1 if fit_intercept else nf
     use_qn = (solver_type == "auto" and elastic_net != 0.0 and reg_param != 0.0) or solver_type == "quasi-newton"
+    if torch.is_tensor(flat) and flat.is_cuda and use_qn and elastic_net != 0.0 and reg_param != 0.0:
+        res = wls_owlqn_device(flat, nf, fit_intercept, reg_param, elastic_net, standardize_features,
+                               standardize_label, max_iter, tol)
+        if res is not None:
+            return res
     if torch.is_tensor(flat) and flat.is_cuda and k >= DEVICE_SOLVE_MIN_K and not use_qn:
         return _wls_device(flat, nf, fit_intercept, reg_param, elastic_net, standardize_features,
                            standardize_label, solver_type, max_iter, tol)
@@ -188,6 +193,43 @@ def fit_wls_flat(flat, nf: int, fit_intercept: bool, reg_param: float, elastic_n
     stats = GramStats.from_flat(host, nf)
     return _wls_native(host, stats, fit_intercept, reg_param, elastic_net, standardize_features,
                        standardize_label, solver_type, max_iter, tol), stats
+
+
+def owlqn_result(host: np.ndarray, nf: int):
+    """(WLSModel, GramStats) from the host copy of a ``wls_qn_small`` output, or None when the
+    kernel handed the case back (status != 0: label / weight short-circuits, no L1 term)."""
+    if int(host[nf + 1]) != 0:
+        return None
+    H = int(host[nf + 7])
+    reason = ("max iterations", "function values converged", "gradient converged", "search failed")[int(host[nf + 8])]
+    log.info("quasi-newton converged: %s after %d states", reason, H)
+    wls = WLSModel(host[:nf].copy(), float(host[nf]), np.zeros(1), host[nf + 9:nf + 9 + H].copy(), "owlqn")
+    return wls, GramStats.scalars_only(host[nf + 2:nf + 7], nf)
+
+
+def wls_owlqn_device(flat, nf, fit_intercept, reg_param, elastic_net, standardize_features, standardize_label,
+                     max_iter, tol):
+    """The OWLQN branch with the statistics on the device: the one-wave HIP solver for k <= 128
+    (one D2H of its result), the device-resident torch OWLQN above (``models/owlqn_device.py``).
+    None = the native host driver owns the case."""
+    from ..ops import device
+    from .owlqn_device import QN_SMALL_MAX_K, QN_TORCH_MIN_K, solve_owlqn_device
+
+    k = nf + 1 if fit_intercept else nf
+    if k <= QN_SMALL_MAX_K:
+        out = device.wls_qn_small(flat, nf, fit_intercept, reg_param, elastic_net, standardize_features,
+                                  standardize_label, max_iter, tol)
+        return owlqn_result(out.cpu().numpy(), nf)
+    if k < QN_TORCH_MIN_K:
+        return None  # the host driver's packed dspmv is still cheaper than host-steered GEMVs here
+    r = solve_owlqn_device(flat, nf, fit_intercept, reg_param, elastic_net, standardize_features,
+                           standardize_label, max_iter, tol)
+    if r is None:
+        return None
+    coef, icpt, hist, reason = r
+    log.info("quasi-newton converged: %s after %d states", reason, len(hist))
+    head = flat[:5].cpu().numpy()
+    return WLSModel(coef, icpt, np.zeros(1), hist, "owlqn"), GramStats.scalars_only(head, nf)
 
 
 def _check_status(status: int, singular_fallback: bool = False):

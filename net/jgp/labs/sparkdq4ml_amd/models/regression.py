@@ -321,8 +321,10 @@ def _async_fit(df, flat, d, args) -> bool:
         return False
     if not (getattr(flat, "is_cuda", False) and 1 <= d <= 64):
         return False
-    _, _, _, reg, enet = args[:5]
-    return not (enet != 0.0 and reg != 0.0)
+    _, _, fit_icpt, reg, enet = args[:5]
+    # L1 (OWLQN, the lab's own regParam=1 / elasticNetParam=1) runs on the device too
+    # (wls_qn_kernel, k <= 128)
+    return not (enet != 0.0 and reg != 0.0) or d + (1 if fit_icpt else 0) <= 128
 
 
 _tail_streams = {}
@@ -347,8 +349,15 @@ class _PendingWLS:
         from ..ops import device
 
         flat, d, fit_icpt, reg, enet, std_f, std_l = args[:7]
+        max_iter, tol = args[8], args[9]
         self._done = None
         self._checks = list(checks or [])
+        self._qn = enet != 0.0 and reg != 0.0  # OWLQN branch (wls_qn_kernel) instead of Cholesky
+
+        def solve(flat):
+            if self._qn:
+                return device.wls_qn_small(flat, d, fit_icpt, reg, enet, std_f, std_l, max_iter, tol)
+            return device.wls_small(flat, d, fit_icpt, reg, enet, std_f, std_l)
         if hasattr(flat, "finish") and not overlap:
             flat = flat.finish()
         if overlap:
@@ -361,12 +370,12 @@ class _PendingWLS:
                 flat.record_stream(side)  # produced on the compute stream, consumed here
                 with tracing.span("allreduce"):
                     flat = comm.all_reduce_sum(flat)
-                self.out = device.wls_small(flat, d, fit_icpt, reg, enet, std_f, std_l)
+                self.out = solve(flat)
                 self._done = torch.cuda.Event()
                 self._done.record(side)
         else:
             flat = comm.all_reduce_sum(flat)
-            self.out = device.wls_small(flat, d, fit_icpt, reg, enet, std_f, std_l)
+            self.out = solve(flat)
         self.args = (flat,) + tuple(args[1:])
         self._res = None
 
@@ -377,6 +386,12 @@ class _PendingWLS:
                 torch.cuda.current_stream(flat.device).wait_event(self._done)
             host = self.out.cpu().numpy()
             verify(self._checks)  # data errors of the fit surface here, on first read
+            if self._qn:
+                from .optim import owlqn_result
+
+                r = owlqn_result(host, d)
+                self._res = r if r is not None else fit_wls_flat(*self.args)
+                return self._res
             if int(host[d + 1]) != 0:  # edge case: the host driver owns warnings/errors/fallbacks
                 self._res = fit_wls_flat(*self.args)
             else:

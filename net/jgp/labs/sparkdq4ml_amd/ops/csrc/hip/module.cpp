@@ -108,6 +108,12 @@ PYBIND11_MODULE(_dq4ml_hip, m) {
                         uintptr_t out, uintptr_t stream) {
     wls_small(P<const double>(flat), nf, fit_intercept, reg, enet, std_f, std_l, P<double>(out), as_stream(stream));
   });
+  m.def("wls_qn_small", [](uintptr_t flat, int nf, bool fit_intercept, double reg, double enet, bool std_f,
+                           bool std_l, int max_iter, double tol, int hist_cap, uintptr_t out, uintptr_t stream) {
+    wls_qn_small(P<const double>(flat), nf, fit_intercept, reg, enet, std_f, std_l, max_iter, tol, hist_cap,
+                 P<double>(out), as_stream(stream));
+  });
+  m.attr("WLS_QN_MAX_K") = kWlsQnMaxK;
   m.attr("WLS_SMALL_MAX_FEATURES") = kWlsSmallMaxFeatures;
   m.def("wide_tiled_bytes", &wide_tiled_bytes);
   m.attr("WIDE_ZERO_BYTES") = kWideZeroBytes;

@@ -11,4 +11,11 @@ constexpr int kWlsSmallMaxFeatures = 64;
 void wls_small(const double* flat, int nf, int fit_intercept, double reg, double enet, int std_f, int std_l,
                double* out, hipStream_t st);
 
+constexpr int kWlsQnMaxK = 128;
+// OWLQN branch (L1 > 0) for k <= 128, one wave: out = [coef(nf), intercept, status, count, wSum,
+// wwSum, bSum, bbSum, H, reason, history(hist_cap)]; status 0 solved, 1/2/3 as wls_small,
+// 8 history capacity exceeded, 9 no L1 term (host re-solves every non-zero status)
+void wls_qn_small(const double* flat, int nf, int fit_intercept, double reg, double enet, int std_f, int std_l,
+                  int max_iter, double tol, int hist_cap, double* out, hipStream_t st);
+
 }  // namespace dq4ml

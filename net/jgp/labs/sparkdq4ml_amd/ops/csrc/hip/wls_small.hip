@@ -196,7 +196,338 @@ __global__ __launch_bounds__(kThreads) void wls_gj_kernel(const double* __restri
   WLS_STAMP(4);
 }
 
+// ---- K6-small, L1 branch: OWLQN in one wave ---------------------------------------------------
+// The OWLQN branch of WeightedLeastSquares (regParam > 0, elasticNetParam > 0: the lab's own
+// LinearRegression at DataQuality4MachineLearningApp.java:120-126) for k <= 64 * SLOTS, entirely
+// on the device: standardize -> Breeze OWLQN (m = 10 two-loop on the pseudo-gradient, orthant
+// projection, backtracking line search, FunctionValuesConverged over 20 values, one history reset
+// on a failed search; csrc/host/solvers.cpp is the reference implementation) -> un-standardize.
+// One wave: lane l owns vector elements l + 64 s; dot products are wave reductions, every scalar
+// decision is computed redundantly by all lanes (uniform control flow, no barriers except around
+// the dspmv broadcast of x); the packed standardized system and the m = 10 history live in LDS.
+// out = [coef(nf), intercept, status, count, wSum, wwSum, bSum, bbSum, H, reason, history(H)]
+// status: 0 ok | 1, 2, 3 label / weight short-circuits (host owns them) | 8 history capacity
+// exceeded | 9 no L1 term (host: L-BFGS).  reason: 0 max iterations, 1 function values converged,
+// 2 gradient converged, 3 search failed.
+constexpr int kQnMem = 10;
+constexpr int kQnFvals = 20;
+
+template <int SLOTS>
+__global__ __launch_bounds__(64) void wls_qn_kernel(const double* __restrict__ flat, int nf, int fit_intercept,
+                                                    double reg, double enet, int std_f, int std_l, int max_iter,
+                                                    double tol, int hist_cap, double* __restrict__ out) {
+  constexpr int KMAX = 64 * SLOTS;
+  __shared__ double Ap[KMAX * (KMAX + 1) / 2];
+  __shared__ double xs[KMAX];
+  __shared__ double Sh[kQnMem][KMAX], Yh[kQnMem][KMAX];
+  __shared__ double sStd[KMAX], sBar[KMAX];
+  const int lane = threadIdx.x;
+  const int k = fit_intercept ? nf + 1 : nf;
+  const double* aSum = flat + 5;
+  const double* abSum = flat + 5 + nf;
+  const double* aa = flat + 5 + 2 * nf;
+  const double count = flat[0], wSum = flat[1], bSum = flat[3], bbSum = flat[4];
+  if (lane < 5) out[nf + 2 + lane] = flat[lane];
+  const double rawBBar = wSum > 0.0 ? bSum / wSum : 0.0;
+  const double rawBStd = wSum > 0.0 ? sqrt(fmax(bbSum / wSum - rawBBar * rawBBar, 0.0)) : 0.0;
+  if (wSum <= 0.0 || rawBStd == 0.0) {
+    if (lane == 0) out[nf + 1] = wSum <= 0.0 ? (count > 0 ? 1.0 : 2.0) : 3.0;
+    return;
+  }
+  const double bStd = rawBStd, bBar = rawBBar / bStd, bbBar = bbSum / wSum / (bStd * bStd);
+  const double eff_reg = reg / bStd, eff_l1 = enet * eff_reg, eff_l2 = (1.0 - enet) * eff_reg;
+  if (eff_l1 == 0.0) {
+    if (lane == 0) out[nf + 1] = 9.0;
+    return;
+  }
+  for (int i = lane; i < KMAX; i += 64) {
+    double sd = 0.0, bar = 0.0;
+    if (i < nf) {
+      const double m = aSum[i] / wSum;
+      sd = sqrt(fmax(aa[pku(i, i)] / wSum - m * m, 0.0));
+      bar = sd == 0.0 ? 0.0 : m / sd;
+    }
+    sStd[i] = sd;
+    sBar[i] = bar;
+  }
+  __syncthreads();
+  for (int j = 0; j < k; ++j)
+    for (int i = lane; i <= j; i += 64) {
+      double v;
+      if (j < nf) {
+        const double den = sStd[i] * sStd[j];
+        v = den == 0.0 ? 0.0 : aa[pku(i, j)] / wSum / den;
+        if (i == j) {
+          double lam = eff_l2;
+          if (!std_f) lam = sStd[j] != 0.0 ? lam / (sStd[j] * sStd[j]) : 0.0;
+          if (!std_l) lam *= bStd;
+          v += lam;
+        }
+      } else {
+        v = i < nf ? sBar[i] : 1.0;
+      }
+      Ap[pku(i, j)] = v;
+    }
+  double ab[SLOTS], l1[SLOTS], bar[SLOTS];
+#pragma unroll
+  for (int s = 0; s < SLOTS; ++s) {
+    const int i = lane + 64 * s;
+    const double sd = i < nf ? sStd[i] : 0.0;
+    ab[s] = i < nf ? (sd == 0.0 ? 0.0 : abSum[i] / wSum / (sd * bStd)) : (i == nf && fit_intercept ? bBar : 0.0);
+    l1[s] = i < k ? (std_f ? eff_l1 : (sd != 0.0 ? eff_l1 / sd : 0.0)) : 0.0;
+    if (fit_intercept && i == nf) l1[s] = 0.0;
+    bar[s] = i < nf ? sBar[i] : 0.0;
+  }
+  __syncthreads();
+
+  auto dot = [&](const double* a, const double* b) {
+    double v = 0.0;
+#pragma unroll
+    for (int s = 0; s < SLOTS; ++s) v += a[s] * b[s];
+    return wave_sum_f64(v);
+  };
+  auto sgn = [](double v) { return v > 0.0 ? 1.0 : (v < 0.0 ? -1.0 : 0.0); };
+  // f(x) = 1/2 bbBar - x.ab + 1/2 x^T A x, g = A x - ab; the intercept is re-set to
+  // bBar - coef.aBar first (in place, as the host cost function writes into the optimizer's x)
+  auto cost = [&](double* x, double* g) {
+    if (fit_intercept) {
+      double p = 0.0;
+#pragma unroll
+      for (int s = 0; s < SLOTS; ++s) p += x[s] * bar[s];
+      const double dp = wave_sum_f64(p);
+#pragma unroll
+      for (int s = 0; s < SLOTS; ++s)
+        if (lane + 64 * s == nf) x[s] = bBar - dp;
+    }
+#pragma unroll
+    for (int s = 0; s < SLOTS; ++s) xs[lane + 64 * s] = x[s];
+    __syncthreads();
+    double aax[SLOTS];
+#pragma unroll
+    for (int s = 0; s < SLOTS; ++s) {
+      const int i = lane + 64 * s;
+      double acc = 0.0;
+      if (i < k) {
+        for (int j = 0; j < i; ++j) acc += Ap[pku(j, i)] * xs[j];
+        for (int j = i; j < k; ++j) acc += Ap[pku(i, j)] * xs[j];
+      }
+      aax[s] = acc;
+    }
+    __syncthreads();
+    const double v = 0.5 * bbBar - dot(ab, x) + 0.5 * dot(x, aax);
+#pragma unroll
+    for (int s = 0; s < SLOTS; ++s) g[s] = aax[s] - ab[s];
+    return v;
+  };
+  auto adjust = [&](const double* x, const double* g, double v, double* ag) {
+    double p = 0.0;
+#pragma unroll
+    for (int s = 0; s < SLOTS; ++s) {
+      const double l = l1[s];
+      ag[s] = g[s];
+      if (l != 0.0) {
+        p += fabs(l * x[s]);
+        if (x[s] == 0.0) {
+          const double dp = g[s] + l, dm = g[s] - l;
+          ag[s] = dm > 0.0 ? dm : (dp < 0.0 ? dp : 0.0);
+        } else {
+          ag[s] = g[s] + sgn(x[s]) * l;
+        }
+      }
+    }
+    return v + wave_sum_f64(p);
+  };
+  double x[SLOTS], grad[SLOTS], agrad[SLOTS];
+#pragma unroll
+  for (int s = 0; s < SLOTS; ++s) x[s] = (fit_intercept && lane + 64 * s == k - 1) ? bBar : 0.0;
+  double value = cost(x, grad);
+  double adj = adjust(x, grad, value, agrad);
+  const double init_adj = adj;
+  double fv[kQnFvals];
+#pragma unroll
+  for (int i = 0; i < kQnFvals; ++i) fv[i] = 0.0;
+  int nfv = 1;
+  fv[kQnFvals - 1] = __builtin_inf();
+  int iter = 0, hh = 0, head = 0, H = 0;
+  bool search_failed = false, failed_once = false, overflow = false;
+  auto record = [&](double v) {
+    if (H >= hist_cap) {
+      overflow = true;
+      return;
+    }
+    if (lane == 0) out[nf + 9 + H] = v;
+    ++H;
+  };
+  auto converged = [&]() -> int {
+    if (max_iter >= 0 && iter >= max_iter) return 0;
+    if (nfv >= 2) {
+      double mx = -__builtin_inf();
+#pragma unroll
+      for (int i = 0; i < kQnFvals; ++i)
+        if (i >= kQnFvals - nfv) mx = fmax(mx, fv[i]);
+      if (fabs(adj - mx) <= tol * fabs(init_adj)) return 1;
+    }
+    if (sqrt(dot(agrad, agrad)) <= fmax(tol * fabs(value), 1e-8)) return 2;
+    if (search_failed) return 3;
+    return -1;
+  };
+  // projected step x + a d, then (adjusted value, adjusted directional derivative)
+  auto take_step = [&](const double* d, double a, double* nx) {
+#pragma unroll
+    for (int s = 0; s < SLOTS; ++s) {
+      nx[s] = x[s] + d[s] * a;
+      const double orth = x[s] != 0.0 ? sgn(x[s]) : sgn(-agrad[s]);
+      if (sgn(nx[s]) != orth) nx[s] = 0.0;
+    }
+  };
+  auto phi = [&](const double* d, double a, double& dd) {
+    double nx[SLOTS], g[SLOTS], ag[SLOTS];
+    take_step(d, a, nx);
+    const double v = cost(nx, g);
+    const double av = adjust(nx, g, v, ag);
+    dd = dot(ag, d);
+    return av;
+  };
+  record(adj);
+  int why = converged();
+  while (why < 0 && !overflow) {
+    bool fail = false;
+    double d[SLOTS];
+    // two-loop recursion on the pseudo-gradient (history in LDS, position i = (head + i) % m)
+    {
+      double diag = 1.0;
+      if (hh > 0) {
+        double sv[SLOTS], yv[SLOTS];
+#pragma unroll
+        for (int s = 0; s < SLOTS; ++s) sv[s] = Sh[head][lane + 64 * s], yv[s] = Yh[head][lane + 64 * s];
+        const double sy = dot(sv, yv), yy = dot(yv, yv);
+        if (sy < 0.0 || sy != sy) fail = true;
+        diag = sy / yy;
+      }
+#pragma unroll
+      for (int s = 0; s < SLOTS; ++s) d[s] = agrad[s];
+      double as_[kQnMem], rho[kQnMem];
+#pragma unroll
+      for (int i = 0; i < kQnMem; ++i) {
+        as_[i] = rho[i] = 0.0;
+        if (i < hh) {
+          const int p = (head + i) % kQnMem;
+          double sv[SLOTS], yv[SLOTS];
+#pragma unroll
+          for (int s = 0; s < SLOTS; ++s) sv[s] = Sh[p][lane + 64 * s], yv[s] = Yh[p][lane + 64 * s];
+          rho[i] = dot(sv, yv);
+          as_[i] = dot(sv, d) / rho[i];
+          if (as_[i] != as_[i]) fail = true;
+#pragma unroll
+          for (int s = 0; s < SLOTS; ++s) d[s] -= as_[i] * yv[s];
+        }
+      }
+#pragma unroll
+      for (int s = 0; s < SLOTS; ++s) d[s] *= diag;
+#pragma unroll
+      for (int i = kQnMem - 1; i >= 0; --i) {
+        if (i < hh) {
+          const int p = (head + i) % kQnMem;
+          double sv[SLOTS], yv[SLOTS];
+#pragma unroll
+          for (int s = 0; s < SLOTS; ++s) sv[s] = Sh[p][lane + 64 * s], yv[s] = Yh[p][lane + 64 * s];
+          const double beta = dot(yv, d) / rho[i];
+#pragma unroll
+          for (int s = 0; s < SLOTS; ++s) d[s] += (as_[i] - beta) * sv[s];
+        }
+      }
+#pragma unroll
+      for (int s = 0; s < SLOTS; ++s) {
+        d[s] = -d[s];
+        if (!(d[s] * agrad[s] < 0.0)) d[s] = 0.0;
+      }
+    }
+    double alpha = 0.0;
+    if (!fail) {  // backtracking line search (Breeze BacktrackingLineSearch as OWLQN configures it)
+      const double initfval = adj;
+      const double shrink = iter < 1 ? 0.1 : 0.5, grow = 2.1, c1 = 1e-4, c2 = 0.9;
+      double initd, fd;
+      phi(d, 0.0, initd);
+      alpha = iter < 1 ? 0.5 / sqrt(dot(grad, grad)) : 1.0;
+      double f = phi(d, alpha, fd);
+      for (int it = 0;; ++it) {
+        double mult;
+        if (f > initfval + alpha * initd * c1) mult = shrink;
+        else if (fd < c2 * initd) mult = grow;
+        else if (fd > -c2 * initd) mult = shrink;
+        else mult = 1.0;
+        if (mult == 1.0) break;
+        const double na = alpha * mult;
+        if (it >= 20 || na < 1e-10 || na > 1e10) {
+          fail = true;
+          break;
+        }
+        alpha = na;
+        f = phi(d, alpha, fd);
+        if (it + 1 >= 20) break;
+      }
+    }
+    if (!fail) {
+      double nx[SLOTS], g[SLOTS], ag[SLOTS];
+      take_step(d, alpha, nx);
+      const double v = cost(nx, g);
+      const double av = adjust(nx, g, v, ag);
+      head = (head + kQnMem - 1) % kQnMem;
+#pragma unroll
+      for (int s = 0; s < SLOTS; ++s) {
+        Sh[head][lane + 64 * s] = nx[s] - x[s];
+        Yh[head][lane + 64 * s] = g[s] - grad[s];
+        x[s] = nx[s], grad[s] = g[s], agrad[s] = ag[s];
+      }
+      hh = hh < kQnMem ? hh + 1 : kQnMem;
+#pragma unroll
+      for (int i = 0; i < kQnFvals - 1; ++i) fv[i] = fv[i + 1];
+      fv[kQnFvals - 1] = v;
+      nfv = nfv < kQnFvals ? nfv + 1 : kQnFvals;
+      value = v;
+      adj = av;
+      ++iter;
+      failed_once = false;
+    } else if (!failed_once) {
+      failed_once = true;
+      hh = 0;
+    } else {
+      search_failed = true;
+    }
+    record(adj);
+    why = converged();
+  }
+  if (overflow) {
+    if (lane == 0) out[nf + 1] = 8.0;
+    return;
+  }
+#pragma unroll
+  for (int s = 0; s < SLOTS; ++s) {
+    const int i = lane + 64 * s;
+    if (i < nf) out[i] = sStd[i] != 0.0 ? x[s] * bStd / sStd[i] : 0.0;
+    if (i == nf) out[nf] = fit_intercept ? x[s] * bStd : 0.0;
+  }
+  if (!fit_intercept && lane == 0) out[nf] = 0.0;
+  if (lane == 0) {
+    out[nf + 1] = 0.0;
+    out[nf + 7] = (double)H;
+    out[nf + 8] = (double)why;
+  }
+}
+
 }  // namespace
+
+void wls_qn_small(const double* flat, int nf, int fit_intercept, double reg, double enet, int std_f, int std_l,
+                  int max_iter, double tol, int hist_cap, double* out, hipStream_t st) {
+  const int k = fit_intercept ? nf + 1 : nf;
+  if (nf < 1 || k > kWlsQnMaxK) throw std::invalid_argument("wls_qn_small: k out of range");
+  if (hist_cap < 1) throw std::invalid_argument("wls_qn_small: hist_cap must be positive");
+  if (k <= 64) hipLaunchKernelGGL(wls_qn_kernel<1>, dim3(1), dim3(64), 0, st, flat, nf, fit_intercept, reg, enet,
+                                  std_f, std_l, max_iter, tol, hist_cap, out);
+  else hipLaunchKernelGGL(wls_qn_kernel<2>, dim3(1), dim3(64), 0, st, flat, nf, fit_intercept, reg, enet, std_f,
+                          std_l, max_iter, tol, hist_cap, out);
+  DQ_HIP_CHECK(hipGetLastError());
+}
 
 void wls_small(const double* flat, int nf, int fit_intercept, double reg, double enet, int std_f, int std_l,
                double* out, hipStream_t st) {

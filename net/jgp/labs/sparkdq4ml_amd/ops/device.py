@@ -548,6 +548,30 @@ def wls_small(flat: torch.Tensor, nf: int, fit_intercept: bool, reg: float, enet
     return out
 
 
+def wls_qn_cap(max_iter: int) -> int:
+    """objectiveHistory capacity of ``wls_qn_small``: one entry per loop pass (accepted steps plus
+    at most one failed search before each)."""
+    return 2 * max(int(max_iter), 0) + 8
+
+
+def wls_qn_small(flat: torch.Tensor, nf: int, fit_intercept: bool, reg: float, enet: float, std_f: bool,
+                 std_l: bool, max_iter: int, tol: float) -> torch.Tensor:
+    """Device OWLQN (L1 WLS, k <= 128) from the flat statistics, enqueued on the current stream:
+    ``[coef(nf), intercept, status, count, wSum, wwSum, bSum, bbSum, H, reason, history...]``."""
+    h = native.hip()
+    _check_dev(flat)
+    k = nf + 1 if fit_intercept else nf
+    if flat.dtype != torch.float64 or flat.numel() != 5 + 2 * nf + nf * (nf + 1) // 2:
+        raise ValueError("wls_qn_small: flat statistics have the wrong dtype/length")
+    if not 1 <= k <= int(h.WLS_QN_MAX_K):
+        raise ValueError(f"wls_qn_small: k = {k} out of range")
+    cap = wls_qn_cap(max_iter)
+    out = torch.empty(nf + 9 + cap, dtype=torch.float64, device=flat.device)
+    h.wls_qn_small(flat.data_ptr(), int(nf), bool(fit_intercept), float(reg), float(enet), bool(std_f), bool(std_l),
+                   int(max_iter), float(tol), cap, out.data_ptr(), _stream())
+    return out
+
+
 # ------------------------------------------------------------------------------------------
 # wide (d > 64) fragment layouts + LDS-tiled MFMA SYRK
 # ------------------------------------------------------------------------------------------

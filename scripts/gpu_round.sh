@@ -41,6 +41,7 @@ for s in $STEPS; do
     kprofasync) (export TMPDIR=/tmp; step kprofasync 600 rocprofv3 --kernel-trace --stats -d gpurun_out/kprofasync -o run --output-format csv -- python bench.py --steps 50 --warmup 5 --rows 1.25e7 --async) || exit $? ;;
     syrkbench) step syrkbench 600 python scripts/syrk_bench.py ;;
     kprofsyrk) (export TMPDIR=/tmp CASES="1024:2000000:f64:fp64" REPS=2; step kprofsyrk 600 rocprofv3 --kernel-trace --stats -d gpurun_out/kprofsyrk -o run --output-format csv -- python scripts/syrk_bench.py) || exit $? ;;
+    owlqn) step owlqn 600 python scripts/owlqn_bench.py ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" ;;
     bench) step bench 600 python bench.py --steps 20 --warmup 3 ;;
     benchasync) step benchasync 600 python bench.py --steps 20 --warmup 3 --async ;;
