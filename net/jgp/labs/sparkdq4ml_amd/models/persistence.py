@@ -11,6 +11,12 @@
                                   indices:array<int>,values:array<double>>, scale: double)
     path/data/_SUCCESS
 
+The target version is the reference's Spark 2.4.4 (``pom.xml``).  ``sparkVersion: "2.4.4"`` and
+the ``scale`` column agree: the Huber loss (and with it the model's ``scale``) arrived in Spark 2.3,
+whose ``LinearRegressionModelReader`` branches on the metadata version — "2.2 and before" reads
+``(intercept, coefficients)``, "2.3 and later" reads ``(intercept, coefficients, scale)``.  The
+reader below follows the same version split, so pre-2.3 directories still load (scale = 1.0).
+
 The parquet footer carries ``org.apache.spark.sql.parquet.row.metadata`` (Spark's JSON schema,
 including the VectorUDT annotation) so Spark itself can read the files back.  Params-only stages
 (``VectorAssembler``) write metadata only; ``Pipeline``/``PipelineModel`` write a stage list.
@@ -207,6 +213,13 @@ class LinearRegressionModelReader:
         data_dir = os.path.join(path, "data")
         files = sorted(f for f in os.listdir(data_dir) if f.endswith(".parquet"))
         row = pq.read_table(os.path.join(data_dir, files[0])).to_pylist()[0]
+        major, minor = (int(x) for x in str(meta.get("sparkVersion", SPARK_VERSION)).split(".")[:2])
+        if (major, minor) <= (2, 2):  # Spark 2.2 and before: (intercept, coefficients)
+            scale = 1.0
+        else:  # Spark 2.3 and later: (intercept, coefficients, scale)
+            if "scale" not in row:
+                raise ValueError(f"model data written by Spark {meta.get('sparkVersion')} lacks the scale column")
+            scale = float(row["scale"])
         m = LinearRegressionModel(meta["uid"], DenseVector(_vector_from_struct(row["coefficients"])),
-                                  float(row["intercept"]), float(row.get("scale", 1.0) or 1.0))
+                                  float(row["intercept"]), scale)
         return apply_metadata(m, meta)

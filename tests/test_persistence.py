@@ -53,6 +53,36 @@ def test_lr_model_roundtrip_and_layout(cpu_session, tmp_path):
     m.write().overwrite().save(path)
 
 
+def test_metadata_version_matches_data_layout(cpu_session, tmp_path):
+    """sparkVersion 2.4.4 goes with the 3-column (scale) layout; a pre-2.3 directory (2 columns,
+    sparkVersion 2.2.x) still loads with scale 1.0, as Spark's reader version split does."""
+    import pyarrow as pa
+
+    m, _ = _model(cpu_session)
+    path = str(tmp_path / "lrm")
+    m.write().save(path)
+    meta_file = os.path.join(path, "metadata", "part-00000")
+    meta = json.loads(open(meta_file).readline())
+    assert meta["sparkVersion"] == "2.4.4"
+    data_dir = os.path.join(path, "data")
+    fname = [f for f in os.listdir(data_dir) if f.endswith(".parquet")][0]
+    t = pq.read_table(os.path.join(data_dir, fname))
+    assert t.column_names[-1] == "scale" and t.column("scale").to_pylist() == [1.0]
+    # rewrite as a Spark 2.2 directory: drop the scale column, stamp 2.2.0
+    pq.write_table(pa.Table.from_arrays([t.column("intercept"), t.column("coefficients")],
+                                        names=["intercept", "coefficients"]), os.path.join(data_dir, fname))
+    meta["sparkVersion"] = "2.2.0"
+    open(meta_file, "w").write(json.dumps(meta) + "\n")
+    m2 = LinearRegressionModel.load(path)
+    np.testing.assert_array_equal(m2.coefficients.toArray(), m.coefficients.toArray())
+    assert m2.scale == 1.0
+    # a 2.3+ stamp on 2-column data is inconsistent and refused
+    meta["sparkVersion"] = "2.4.4"
+    open(meta_file, "w").write(json.dumps(meta) + "\n")
+    with pytest.raises(ValueError):
+        LinearRegressionModel.load(path)
+
+
 def test_params_only_stages(tmp_path):
     va = VectorAssembler().setInputCols(["a", "b"]).setOutputCol("features").setHandleInvalid("skip")
     p = str(tmp_path / "va")
