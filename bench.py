@@ -32,7 +32,13 @@ def _args(argv=None):
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--rows", type=float, default=1e8, help="global rows (strong scaling)")
     ap.add_argument("--features", type=int, default=32)
-    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32", "fp64"])
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32", "fp64"],
+                    help="compute precision of the Gram statistics (gramDtype)")
+    ap.add_argument("--storage", default=None, choices=["bf16", "fp32", "fp64", "f32cols"],
+                    help="feature storage: an assembled [d, n] matrix of that dtype (default: the "
+                         "--dtype; bf16 is ingested into the MFMA-fragment tiled layout), or "
+                         "f32cols = d separate f32 columns assembled by VectorAssembler inside "
+                         "every fit (fused assemble + Gram, gram_cols_kernel)")
     ap.add_argument("--scaling", default="strong", choices=["strong", "weak"])
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--sync", dest="use_async", action="store_false",
@@ -90,7 +96,9 @@ def main(argv=None):
     n = per_rank if (a.scaling == "weak" or rank < world - 1) else total - lo
     d = a.features
     gen = torch.Generator(device=dev).manual_seed(1234 + rank)
-    store = {"bf16": torch.bfloat16, "fp32": torch.float32, "fp64": torch.float64}[a.dtype]
+    storage = a.storage or a.dtype
+    store = {"bf16": torch.bfloat16, "fp32": torch.float32, "fp64": torch.float64,
+             "f32cols": torch.float32}[storage]
     ld = (n + 63) // 64 * 64
     Xbuf = torch.empty(d, ld, dtype=store, device=dev)
     beta = torch.linspace(-2.0, 2.0, d, device=dev, dtype=torch.float32)
@@ -102,7 +110,15 @@ def main(argv=None):
         Xbuf[:, s:e] = xc.to(store)
         y[s:e] = beta @ xc + 0.5 + 0.1 * torch.randn(e - s, generator=gen, device=dev, dtype=torch.float32)
     X = Xbuf[:, :n]
-    df = spark.createDataFrame({"features": X, "label": y})
+    if storage == "f32cols":
+        from net.jgp.labs.sparkdq4ml_amd import VectorAssembler
+
+        names = [f"x{i}" for i in range(d)]
+        cols = {nm: X[i] for i, nm in enumerate(names)}
+        cols["label"] = y
+        df = VectorAssembler().setInputCols(names).setOutputCol("features").transform(spark.createDataFrame(cols))
+    else:
+        df = spark.createDataFrame({"features": X, "label": y})
     lr = LinearRegression(solver="normal", gramDtype=a.dtype)
 
     def step():
@@ -142,7 +158,7 @@ def main(argv=None):
             "dtype": a.dtype, "data": "synthetic (random-init coefficients, N(0,1) features)",
             "config": {"model": f"LinearRegression(normal equations) d={d}", "global_batch": global_rows,
                        "seq_len": d, "parallelism": f"dp{world}", "rows_per_gpu": n,
-                       "device": str(dev), "coef_max_abs_err": err,
+                       "device": str(dev), "coef_max_abs_err": err, "storage": storage,
                        "fit_mode": "async" if (a.use_async and on_gpu) else "sync"},
             "world": world, "backend": comm.backend() or "none",
             "rccl_version": comm.rccl_version() if on_gpu else None,

@@ -119,9 +119,10 @@ class VectorAssembleExpr(Expr):
             with tracing.span("pack"):
                 mat = kernels.pack_wide(parts, 8 if dt == torch.float8_e4m3fn else 16, ctx.table.sel)
             meta = {"ml_attr": {"num_attrs": d}, "zero_dead": ctx.table.sel}
-        elif on_dev and dt == torch.float64 and d <= 8:
-            # narrow f64 assembly, produced lazily too: the f64 normal-equation statistics read
-            # the source columns directly (gram_skinny_cols); other consumers pack on first use
+        elif on_dev and dt in (torch.float64, torch.float32) and d <= 64:
+            # f64 / f32 assembly, produced lazily too: the normal-equation statistics read the
+            # source columns directly (gram_skinny_cols for d <= 8, the LDS-DMA stream kernels
+            # above); other consumers pack on first use
             def _pack(parts=parts, dt=dt):
                 with tracing.span("pack"):
                     return kernels.pack_columns(parts, dt)

@@ -213,12 +213,18 @@ class LinearRegression(_LRParams):
         overlap = sess is not None and str(sess.conf.get("dq4ml.fit.overlapTail", "true")).lower() in ("1", "true")
         with tracing.span("gram"):
             gd = _gram_dtype(self, df)
+            flat = None
             if _fusable_assembly(X, w, gd, yvalid):
                 parts, asel = X.sources  # fused VectorAssembler + Gram: the features are never packed
                 flat = kernels.gram_cols(parts, yv, sel if sel is not None else asel)
             elif _skinny_cols(X, gd):
                 flat = kernels.gram_skinny_cols(X.sources[0], yv, w, sel)  # f64, no pack
-            else:
+            elif _lazy_sources(X):
+                # f64 / f32 statistics of 9..64 same-dtype source columns: LDS-DMA stream kernel
+                # over the columns themselves (None: mixed / unaligned sources -> pack below)
+                parts, asel = X.sources
+                flat = kernels.gram_stream_cols(parts, yv, w, sel if sel is not None else asel, gd)
+            if flat is None:
                 # a single-GPU overlapped asynchronous fit folds the Gram partials on its side
                 # stream too.  Not with N > 1: co-running with the next Gram pass the fold's loads
                 # queue behind its HBM stream (8 us alone, ~100 us co-running), and the side stream
@@ -278,6 +284,12 @@ def _fusable_assembly(X, w, gram_dtype, yvalid) -> bool:
     parts, _ = X.sources
     return all(p.is_cuda and p.dtype in (torch.float32, torch.float64, torch.bfloat16, torch.int32, torch.int64,
                                           torch.bool, torch.uint8) for p in parts)
+
+
+def _lazy_sources(X) -> bool:
+    from ..sql.table import LazyVectorColumn
+
+    return isinstance(X, LazyVectorColumn) and not X.materialized
 
 
 def _skinny_cols(X, gram_dtype) -> bool:

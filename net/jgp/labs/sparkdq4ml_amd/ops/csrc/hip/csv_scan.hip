@@ -175,107 +175,6 @@ __global__ __launch_bounds__(256) void csv_ends_kernel(const uint8_t* __restrict
   }
 }
 
-__constant__ double kPow10[23] = {1e0,  1e1,  1e2,  1e3,  1e4,  1e5,  1e6,  1e7,  1e8,  1e9,  1e10, 1e11,
-                                  1e12, 1e13, 1e14, 1e15, 1e16, 1e17, 1e18, 1e19, 1e20, 1e21, 1e22};
-
-__device__ __forceinline__ int lower(int c) { return (c >= 'A' && c <= 'Z') ? c + 32 : c; }
-
-__device__ bool match_ci(const uint8_t* p, int len, const char* w, int wl) {
-  if (len != wl) return false;
-  for (int i = 0; i < wl; ++i)
-    if (lower(p[i]) != w[i]) return false;
-  return true;
-}
-
-// classify + parse one field; returns CSV type code, sets *slow when exactness cannot be guaranteed
-__device__ int parse_field(const uint8_t* p, int len, double& dv, int64_t& iv, bool& slow) {
-  dv = 0.0;
-  iv = 0;
-  if (len == 0) return CT_NULL;
-  if (match_ci(p, len, "true", 4)) { iv = 1; dv = 1.0; return CT_BOOL; }
-  if (match_ci(p, len, "false", 5)) return CT_BOOL;
-  int i = 0;
-  bool neg = false;
-  if (p[0] == '+' || p[0] == '-') {
-    neg = p[0] == '-';
-    i = 1;
-  }
-  const int rest = len - i;
-  if (rest == 3 && p[i] == 'N' && p[i + 1] == 'a' && p[i + 2] == 'N' && i == 0) { dv = __builtin_nan(""); return CT_DOUBLE; }
-  if (rest == 8 && p[i] == 'I') {
-    const char* inf = "Infinity";
-    bool ok = true;
-    for (int k = 0; k < 8; ++k) ok &= p[i + k] == (uint8_t)inf[k];
-    if (ok) { dv = neg ? -__builtin_inf() : __builtin_inf(); return CT_DOUBLE; }
-  }
-  uint64_t mant = 0;
-  int ndig = 0, dropped_nz = 0, frac = 0, dropped = 0;
-  bool seen_digit = false, dot = false, isint = true;
-  for (; i < len; ++i) {
-    const int c = p[i];
-    if (c >= '0' && c <= '9') {
-      seen_digit = true;
-      if (ndig < 19) {
-        if (mant != 0 || c != '0') ++ndig;
-        mant = mant * 10 + (c - '0');
-      } else {
-        ++dropped;
-        dropped_nz |= (c != '0');
-      }
-      if (dot) ++frac;
-    } else if (c == '.' && !dot) {
-      dot = true;
-      isint = false;
-    } else {
-      break;
-    }
-  }
-  if (!seen_digit) return CT_STRING;
-  int exp10 = 0;
-  if (i < len && (p[i] == 'e' || p[i] == 'E')) {
-    isint = false;
-    ++i;
-    bool eneg = false;
-    if (i < len && (p[i] == '+' || p[i] == '-')) {
-      eneg = p[i] == '-';
-      ++i;
-    }
-    int ed = 0, ev = 0;
-    for (; i < len && p[i] >= '0' && p[i] <= '9'; ++i, ++ed) ev = ev < 100000 ? ev * 10 + (p[i] - '0') : ev;
-    if (ed == 0) return CT_STRING;
-    exp10 = eneg ? -ev : ev;
-  }
-  if (i < len && (p[i] == 'd' || p[i] == 'D' || p[i] == 'f' || p[i] == 'F') && i == len - 1) {
-    isint = false;
-    ++i;
-  }
-  if (i != len) return CT_STRING;
-  if (isint) {
-    if (dropped) {  // > 19 digits: decimal(p,0) — exact value needs the host path
-      slow = true;
-      return CT_DECIMAL;
-    }
-    if (mant > (uint64_t)INT64_MAX + (neg ? 1u : 0u)) {
-      slow = true;
-      return CT_DECIMAL;
-    }
-    iv = neg ? (int64_t)(0 - mant) : (int64_t)mant;
-    dv = (double)iv;
-    if (mant > (1ull << 53)) slow = true;  // dv would round
-    return (iv >= INT32_MIN && iv <= INT32_MAX) ? CT_INT : CT_LONG;
-  }
-  // double: value = mant * 10^(exp10 - frac + dropped)
-  const int e = exp10 - frac + dropped;
-  if (dropped_nz || mant >= (1ull << 53) || e < -22 || e > 22) {
-    slow = true;
-    dv = (double)mant * (e >= 0 ? pow(10.0, (double)e) : 1.0 / pow(10.0, (double)-e));
-  } else {
-    dv = e >= 0 ? (double)mant * kPow10[e] : (double)mant / kPow10[-e];
-  }
-  if (neg) dv = -dv;
-  return CT_DOUBLE;
-}
-
 constexpr int kMaxCols = 256;
 // staged bytes per 256-line group: 8 KiB (short lines, <= ~24 B: 8 waves per SIMD — the byte
 // loops are latency-bound) or 32 KiB (wider rows; 4 waves per SIMD).  Chosen per launch from the
@@ -283,105 +182,81 @@ constexpr int kMaxCols = 256;
 constexpr int kParseLdsSmall = 8192;
 constexpr int kParseLdsLarge = 32768;
 
+using dq4ml_csv::CsvOpts;
+
 // Parse line li.  Bytes are read as B[i - bias] (global: B = b, bias = 0; LDS-staged: B = the
 // block's stage, bias = the buffer index of its first byte).
 // Called by EVERY lane of the wave (``active`` false past the last line) so the per-field type
 // bits can be OR-reduced across the wave with shuffles: one LDS atomic per wave and field instead
 // of 64 same-address atomics (which serialized the first version of this kernel).
+// Empty lines and comment lines are skipped (keep = 0).  A malformed record (see
+// csv_parse_dev.h; in strict mode also a field that does not convert to the user schema's type)
+// keeps its row with every field null, as Spark's PERMISSIVE mode.
 template <typename PB, typename IT>
 __device__ __forceinline__ bool parse_line(PB B, int64_t bias, int64_t n, const IT* __restrict__ ends,
-                                           int64_t li, bool active, int64_t nlines, int ncols, uint8_t sep,
+                                           int64_t li, bool active, int64_t nlines, int ncols, const CsvOpts& o,
                                            const int64_t* __restrict__ dcols, uint8_t* __restrict__ valid,
                                            uint8_t* __restrict__ keep, uint32_t* smask, int* snull, int* sempty) {
   const bool lane0 = (threadIdx.x & 63) == 0;
   int64_t start = 0, end = 0;
+  bool line = false;
   if (active) {
     if (li > 0) {
       const int64_t pe = ends[li - 1];
       start = pe + 1 + ((B[pe - bias] == '\r' && pe + 1 < n && B[pe + 1 - bias] == '\n') ? 1 : 0);
     }
     end = ends[li];  // exclusive (position of the terminator or n)
-    keep[li] = end > start;
+    line = end > start && !(o.comment && B[start - bias] == o.comment);
+    keep[li] = line;
   }
-  const bool line = active && end > start;
   const uint64_t empty = __ballot(active && !line);
   if (lane0 && empty) atomicAdd(sempty, (int)__popcll(empty));
-  int64_t pos = start;
-  bool slow = false;
+  long long pos = start;
+  bool slow = false, malformed = false;
   for (int c = 0; c < ncols; ++c) {
     double dv = 0.0;
-    int64_t iv = 0;
     int ty = CT_NULL;
-    if (pos <= end && line) {
-      // fast path, ONE walk over the bytes: [+-]digits[.digits] with at most 9 digits, ended by
-      // the separator or the line end — exact in 32-bit integer math, and the f64 value
-      // m / 10^frac is correctly rounded (Clinger).  Anything else re-walks the field in the
-      // general parser.
-      int64_t q = pos;
-      bool neg = false;
-      if (q < end) {
-        const int c0 = B[q - bias];
-        neg = c0 == '-';
-        q += (c0 == '-' || c0 == '+') ? 1 : 0;
-      }
-      uint32_t m = 0;
-      int nd = 0, fr = 0;
-      bool dot = false, bad = false;
-      // branch-free body (selects): the loop exit is the only divergent branch — an if / else-if
-      // chain here cost two exec-mask updates per byte (SALU outnumbered VALU 1.8 : 1)
-      for (; q < end; ++q) {
-        const int ch = B[q - bias];
-        const uint32_t d = (uint32_t)(ch - '0');
-        const bool isd = d < 10u;
-        const bool isdot = ch == '.' && !dot;
-        if (!(isd || isdot)) {
-          bad = ch != sep;
-          break;
-        }
-        m = isd ? m * 10u + d : m;
-        nd += isd ? 1 : 0;
-        fr += (isd && dot) ? 1 : 0;
-        dot = dot || isdot;
-      }
-      if (!bad && nd > 0 && nd <= 9) {
-        ty = dot ? CT_DOUBLE : CT_INT;
-        if (dot) {
-          dv = (double)m / kPow10[fr];
-          dv = neg ? -dv : dv;
-        } else {
-          dv = (double)(neg ? -(int64_t)m : (int64_t)m);  // -0 is +0.0 for integers
-        }
-      } else {
-        q = pos;
-        while (q < end && B[q - bias] != sep) ++q;
-        const int64_t flen = q - pos;
-        if (flen > 0 && (B[pos - bias] == '"' || B[pos - bias] == '\\')) slow = true;
-        ty = parse_field(&B[pos - bias], (int)(flen > 1 << 20 ? 1 << 20 : flen), dv, iv, slow);
-      }
-      pos = q + 1;
+    if (pos <= end && line) ty = dq4ml_csv::csv_field(B, (long long)bias, pos, (long long)end, o, dv, slow, malformed);
+    const int kind = (int)dcols[ncols + c];
+    bool ok = ty != CT_NULL && ty != CT_STRING;
+    if (o.strict && ty != CT_NULL && !dq4ml_csv::csv_conforms(ty, kind)) {
+      malformed = true;  // a value the user schema's type does not accept
+      ok = false;
     }
-    const bool ok = ty != CT_NULL && ty != CT_STRING;
     if (active) {
       // one plane per column: f64 by default — ints / longs / booleans as their (exact:
       // |v| <= 2^53, else ``slow``) double value, converted once the column type is known — or,
-      // when the host knows the type from an earlier scan of the same bytes, stored as that
-      // type directly (kind = dcols[ncols + c]; a mismatch is detected from the masks)
+      // when the type is known (an earlier scan of the same bytes, or the user schema), stored
+      // as that type directly (kind = dcols[ncols + c]; a hint mismatch shows in the masks)
       void* dst = reinterpret_cast<void*>(dcols[c]);
-      switch ((int)dcols[ncols + c]) {
+      switch (kind) {
         case 1: reinterpret_cast<int32_t*>(dst)[li] = ok ? (int32_t)dv : 0; break;
         case 2: reinterpret_cast<int64_t*>(dst)[li] = ok ? (int64_t)dv : 0; break;
-        case 3: reinterpret_cast<uint8_t*>(dst)[li] = dv != 0.0; break;
+        case 3: reinterpret_cast<uint8_t*>(dst)[li] = ok && dv != 0.0; break;
         default: reinterpret_cast<double*>(dst)[li] = dv;
       }
       valid[(int64_t)c * nlines + li] = ok;
     }
     uint32_t bit = line ? (1u << ty) : 0u;
 #pragma unroll
-    for (int o = 1; o < 64; o <<= 1) bit |= (uint32_t)__shfl_xor((int)bit, o, 64);
+    for (int oo = 1; oo < 64; oo <<= 1) bit |= (uint32_t)__shfl_xor((int)bit, oo, 64);
     const uint64_t nulls = __ballot(line && !ok);
     if (lane0) {
       if (bit) atomicOr(&smask[c], bit);
       if (nulls) atomicAdd(&snull[c], (int)__popcll(nulls));
+    }
+  }
+  // a malformed record: every field null (valid = 0) — the null counts above already cover the
+  // fields that failed; the rest are counted here
+  const uint64_t bad = __ballot(active && line && malformed);
+  if (bad) {
+    if (active && line && malformed) {
+      for (int c = 0; c < ncols; ++c) {
+        if (valid[(int64_t)c * nlines + li]) {
+          valid[(int64_t)c * nlines + li] = 0;
+          atomicAdd(&snull[c], 1);
+        }
+      }
     }
   }
   return slow;
@@ -394,7 +269,7 @@ __device__ __forceinline__ bool parse_line(PB B, int64_t bias, int64_t n, const 
 // groups (very wide rows) parse straight from global memory.
 template <int LDS, int WPE, typename IT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void csv_parse_kernel(
-    const uint8_t* __restrict__ b, int64_t n, const IT* __restrict__ ends, int64_t nlines, int ncols, uint8_t sep,
+    const uint8_t* __restrict__ b, int64_t n, const IT* __restrict__ ends, int64_t nlines, int ncols, CsvOpts o,
     const int64_t* __restrict__ dcols, uint8_t* __restrict__ valid, uint8_t* __restrict__ keep,
     unsigned long long* __restrict__ stats) {
   __shared__ uint32_t smask[kMaxCols];
@@ -430,10 +305,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
         *reinterpret_cast<u32x4*>(stage + (g - glo)) = v;
       }
       __syncthreads();
-      slow |= parse_line(stage, glo - off, n, ends, li, li < l1, nlines, ncols, sep, dcols, valid, keep, smask,
+      slow |= parse_line(stage, glo - off, n, ends, li, li < l1, nlines, ncols, o, dcols, valid, keep, smask,
                          snull, &sempty);
     } else {
-      slow |= parse_line(b, 0, n, ends, li, li < l1, nlines, ncols, sep, dcols, valid, keep, smask, snull, &sempty);
+      slow |= parse_line(b, 0, n, ends, li, li < l1, nlines, ncols, o, dcols, valid, keep, smask, snull, &sempty);
     }
   }
   if (slow) sflag = 1;
@@ -473,17 +348,17 @@ void csv_line_ends(const uint8_t* buf, int64_t n, int64_t* counts, void* ends, h
 
 template <typename IT>
 static void launch_parse(bool small, int64_t g, hipStream_t st, const uint8_t* buf, int64_t n, const IT* ends,
-                         int64_t nlines, int ncols, uint8_t sep, const int64_t* dcols, uint8_t* valid, uint8_t* keep,
-                         unsigned long long* stats) {
+                         int64_t nlines, int ncols, const CsvOpts& o, const int64_t* dcols, uint8_t* valid,
+                         uint8_t* keep, unsigned long long* stats) {
   if (small)
     hipLaunchKernelGGL((csv_parse_kernel<kParseLdsSmall, 8, IT>), dim3(g), dim3(256), 0, st, buf, n, ends, nlines,
-                       ncols, sep, dcols, valid, keep, stats);
+                       ncols, o, dcols, valid, keep, stats);
   else
     hipLaunchKernelGGL((csv_parse_kernel<kParseLdsLarge, 4, IT>), dim3(g), dim3(256), 0, st, buf, n, ends, nlines,
-                       ncols, sep, dcols, valid, keep, stats);
+                       ncols, o, dcols, valid, keep, stats);
 }
 
-void csv_parse(const uint8_t* buf, int64_t n, const void* ends, int64_t nlines, int ncols, uint8_t sep,
+void csv_parse(const uint8_t* buf, int64_t n, const void* ends, int64_t nlines, int ncols, const CsvOpts& o,
                const int64_t* dcols, uint8_t* valid, uint8_t* keep, int64_t* stats, hipStream_t st) {
   if (ncols > kMaxCols) throw std::invalid_argument("csv_parse: too many columns for the device scanner");
   if (nlines <= 0) return;
@@ -497,10 +372,10 @@ void csv_parse(const uint8_t* buf, int64_t n, const void* ends, int64_t nlines, 
   const bool small = forced ? forced == kParseLdsSmall : (n / nlines) * 256 * 5 / 4 <= kParseLdsSmall;
   auto* stats64 = reinterpret_cast<unsigned long long*>(stats);
   if (csv_ends_i32(n))
-    launch_parse(small, g, st, buf, n, static_cast<const int32_t*>(ends), nlines, ncols, sep, dcols, valid, keep,
+    launch_parse(small, g, st, buf, n, static_cast<const int32_t*>(ends), nlines, ncols, o, dcols, valid, keep,
                  stats64);
   else
-    launch_parse(small, g, st, buf, n, static_cast<const int64_t*>(ends), nlines, ncols, sep, dcols, valid, keep,
+    launch_parse(small, g, st, buf, n, static_cast<const int64_t*>(ends), nlines, ncols, o, dcols, valid, keep,
                  stats64);
   DQ_HIP_CHECK(hipGetLastError());
 }

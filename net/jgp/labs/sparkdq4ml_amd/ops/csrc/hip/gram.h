@@ -29,6 +29,9 @@ struct GramArgs {
   const void* colp[8];
   int coldt[8];
   int cols;
+  // stream kernels over source columns (gram_stream_cols): [2 * d] int64 device table of
+  // (column pointer, dtype) pairs — feature f is column srcs[2 f] (all of X's dtype xdt)
+  const int64_t* srcs;
 };
 
 // MFMA-fragment-ordered bf16 feature storage ("tiled"): for superstep s (64 rows), 32-feature
@@ -46,6 +49,14 @@ int gram_plan_blocks(int mode, int d, int64_t n, int xdt, int xmode);
 // later, possibly on another stream
 void gram_tall(int mode, GramArgs a, int xmode, int blocks, double* out, hipStream_t st, bool reduce = true);
 void gram_reduce(int mode, const double* partials, int blocks, int d, double* out, hipStream_t st);
+
+// LDS-DMA streamed tall kernels (gram_stream.hip): GRAM_F64 on f64/f32 features, GRAM_F32
+// (exact-f32 MFMA) on f32 features.  gram_stream_ok: operand dtypes/alignment the DMA path needs.
+bool gram_stream_ok(int mode, const GramArgs& a);
+int gram_stream_blocks(int mode, int d, int64_t n, int xdt);
+void gram_stream(int mode, GramArgs a, int xmode, int blocks, double* out, hipStream_t st, bool reduce = true);
+// GRAM_BF16 on f32 storage rides the same stream kernel (bf16 MFMA on converted LDS tiles); with
+// a.srcs set the features are d separate f32 columns (fused VectorAssembler + Gram)
 
 // fused VectorAssembler + bf16 Gram over d <= 64 source columns (a.X unused; a.sel masks rows)
 struct PackSrcG {

@@ -24,6 +24,8 @@
 //    atomics: bit-reproducible run to run).
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "common.h"
 #include "gram.h"
 
@@ -1215,7 +1217,20 @@ static bool use_skinny(int mode, int d, int xdt, int tiled) {
   return mode == GRAM_F64 && !tiled && d <= kSkinnyMaxD && (xdt == DT_F64 || xdt == DT_F32);
 }
 
+// DQ4ML_GRAM_STREAM=0 keeps the round-1 register-staged f64 kernel (A/B measurements only)
+static bool use_stream() {
+  static const bool on = [] {
+    const char* e = getenv("DQ4ML_GRAM_STREAM");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 int gram_plan_blocks(int mode, int d, int64_t n, int xdt, int xmode) {
+  if (mode == GRAM_F32 || (use_stream() && ((mode == GRAM_F64 && !use_skinny(mode, d, xdt, 0) &&
+                                              (xdt == DT_F64 || xdt == DT_F32)) ||
+                                             (mode == GRAM_BF16 && xdt == DT_F32))))
+    return gram_stream_blocks(mode, d, n, xdt);
   if (use_skinny(mode, d, xdt, 0)) {
     int full = 1;
     with_skinny(xdt, d, [&](auto kern) { full = occupancy_blocks(kern, 0, kBlock); });
@@ -1237,7 +1252,7 @@ int gram_plan_blocks(int mode, int d, int64_t n, int xdt, int xmode) {
 }
 
 void gram_reduce(int mode, const double* partials, int blocks, int d, double* out, hipStream_t st) {
-  const int T = mode == GRAM_BF16 ? 32 : 16;
+  const int T = mode == GRAM_F64 ? 16 : 32;
   const int NT = (d + T - 1) / T;
   const int P = (int)gram_partial_stride(mode, d);
   // output-order gather (first version): 4.4 / 7.9 us at d = 32 / 64; storage order: 3.8 / 3.9 us
@@ -1262,6 +1277,12 @@ void gram_tall(int mode, GramArgs a, int xmode, int blocks, double* out, hipStre
     with_skinny_cols(a, [&](auto kern) { hipLaunchKernelGGL(kern, dim3(blocks), dim3(kBlock), 0, st, a); });
   } else if (use_skinny(mode, a.d, a.xdt, a.tiled)) {
     with_skinny(a.xdt, a.d, [&](auto kern) { hipLaunchKernelGGL(kern, dim3(blocks), dim3(kBlock), 0, st, a); });
+  } else if ((mode == GRAM_F32 || (use_stream() && (mode == GRAM_F64 || (mode == GRAM_BF16 && a.xdt == DT_F32)))) &&
+             gram_stream_ok(mode, a)) {
+    gram_stream(mode, a, xmode, blocks, out, st, reduce);
+    return;
+  } else if (mode == GRAM_F32) {
+    throw std::invalid_argument("gram_tall(f32): needs 16-byte aligned f32 features and f32/f64 labels");
   } else {
     with_kernel(mode, a.xdt, a.d, xmode, a.tiled != 0,
                 [&](auto kern) { hipLaunchKernelGGL(kern, dim3(blocks), dim3(block), lds, st, a); });

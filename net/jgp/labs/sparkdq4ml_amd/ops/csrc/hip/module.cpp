@@ -62,6 +62,23 @@ PYBIND11_MODULE(_dq4ml_hip, m) {
           a.partials = P<double>(partials);
           gram_tall(mode, a, xmode, blocks, P<double>(out), as_stream(stream), reduce);
         });
+  m.def("gram_stream_cols",
+        [](int mode, uintptr_t srcs, int d, int64_t n, int xdt, uintptr_t y, int ydt, uintptr_t w, int wdt,
+           uintptr_t sel, uintptr_t partials, int blocks, uintptr_t out, uintptr_t stream) {
+          GramArgs a{};
+          a.srcs = P<const int64_t>(srcs);
+          a.d = d;
+          a.n = n;
+          a.xdt = xdt;
+          a.y = P<const void>(y);
+          a.ydt = ydt;
+          a.w = P<const void>(w);
+          a.wdt = wdt;
+          a.sel = P<const uint8_t>(sel);
+          a.partials = P<double>(partials);
+          gram_stream(mode, a, (w || sel) ? 1 : 0, blocks, P<double>(out), as_stream(stream), true);
+        });
+  m.def("gram_stream_blocks", &gram_stream_blocks);
   m.def("gram_skinny_cols",
         [](const std::vector<uintptr_t>& cols, const std::vector<int>& dts, int64_t n, uintptr_t y, int ydt,
            uintptr_t w, int wdt, uintptr_t sel, uintptr_t partials, int blocks, uintptr_t out, uintptr_t stream) {
@@ -235,10 +252,26 @@ PYBIND11_MODULE(_dq4ml_hip, m) {
   });
   m.def("csv_ends_i32", &csv_ends_i32);
   m.def("csv_parse", [](uintptr_t buf, int64_t n, uintptr_t ends, int64_t nlines, int ncols, int sep, uintptr_t dcols,
-                        uintptr_t valid, uintptr_t keep, uintptr_t stats, uintptr_t stream) {
-    csv_parse(P<const uint8_t>(buf), n, P<const void>(ends), nlines, ncols, (uint8_t)sep, P<const int64_t>(dcols),
+                        uintptr_t valid, uintptr_t keep, uintptr_t stats, uintptr_t stream, int quote, int escape,
+                        int comment, bool trim_lead, bool trim_trail, const std::string& null_value, bool strict) {
+    dq4ml_csv::CsvOpts o{};
+    if (null_value.size() > sizeof(o.null_val)) throw std::invalid_argument("csv_parse: nullValue longer than 16 bytes");
+    o.sep = (uint8_t)sep;
+    o.quote = (uint8_t)quote;
+    o.escape = (uint8_t)escape;
+    o.comment = (uint8_t)comment;
+    o.trim_lead = trim_lead;
+    o.trim_trail = trim_trail;
+    o.null_len = (uint8_t)null_value.size();
+    for (size_t i = 0; i < null_value.size(); ++i) o.null_val[i] = (uint8_t)null_value[i];
+    o.strict = strict;
+    csv_parse(P<const uint8_t>(buf), n, P<const void>(ends), nlines, ncols, o, P<const int64_t>(dcols),
               P<uint8_t>(valid), P<uint8_t>(keep), P<int64_t>(stats), as_stream(stream));
-  });
+  }, pybind11::arg("buf"), pybind11::arg("n"), pybind11::arg("ends"), pybind11::arg("nlines"), pybind11::arg("ncols"),
+     pybind11::arg("sep"), pybind11::arg("dcols"), pybind11::arg("valid"), pybind11::arg("keep"), pybind11::arg("stats"),
+     pybind11::arg("stream"), pybind11::arg("quote") = '"', pybind11::arg("escape") = '\\', pybind11::arg("comment") = 0,
+     pybind11::arg("trim_lead") = false, pybind11::arg("trim_trail") = false, pybind11::arg("null_value") = "",
+     pybind11::arg("strict") = false);
 
   // ---- fused DQ chains: hipRTC whole-stage codegen ----------------------------------------------
   m.def("rtc_compile", [](const std::string& src, const std::string& entry) {

@@ -68,7 +68,14 @@ def _ncols_of(data, sep: str) -> int:
 _KIND = {CT_INT: (1, torch.int32), CT_LONG: (2, torch.int64), CT_BOOL: (3, torch.bool)}
 
 
-def _scan_chunk(h, buf, n: int, trailing: bool, ncols: int, sep: str, dev, hint=None):
+def _opt_args(opts):
+    o = opts or {}
+    return dict(quote=ord(o.get("quote", '"')), escape=ord(o.get("escape", "\\")), comment=o.get("comment", 0),
+                trim_lead=bool(o.get("trim_lead", False)), trim_trail=bool(o.get("trim_trail", False)),
+                null_value=o.get("null_value", ""), strict=bool(o.get("strict", False)))
+
+
+def _scan_chunk(h, buf, n: int, trailing: bool, ncols: int, sep: str, dev, hint=None, opts=None):
     """K1 (line ends) + K2 (parse, type masks, null / empty-line counts) over one device byte
     buffer; no host sync except the line count.  Returns (nlines, per-column f64 planes, valid
     [ncols, m], keep [m], stats) — stats as documented at ``csv_parse`` (csv_scan.h)."""
@@ -96,7 +103,7 @@ def _scan_chunk(h, buf, n: int, trailing: bool, ncols: int, sep: str, dev, hint=
     keep = torch.empty(m, dtype=torch.bool, device=dev)
     stats = torch.zeros(2 + 2 * ncols, dtype=torch.int64, device=dev)
     h.csv_parse(buf.data_ptr(), n, ends.data_ptr(), nlines, ncols, ord(sep), ptrs.data_ptr(), valid.data_ptr(),
-                keep.data_ptr(), stats.data_ptr(), stream)
+                keep.data_ptr(), stats.data_ptr(), stream, **_opt_args(opts))
     return nlines, dcols, valid, keep, stats
 
 
@@ -168,9 +175,14 @@ def _resolve_types(masks: np.ndarray, flag: int, sharded: bool):
     return types
 
 
+# user-schema type codes the device parser converts (int, long, double, boolean)
+STRICT_CODES = (CT_INT, CT_LONG, CT_DOUBLE, CT_BOOL)
+
+
 def scan_device(data, sep: str = ",", infer: bool = True, device=None, ncols: Optional[int] = None,
                 sharded: bool = False, chunk_bytes: Optional[int] = None, pinned: Optional[torch.Tensor] = None,
-                device_data: Optional[torch.Tensor] = None, types_hint: Optional[list] = None):
+                device_data: Optional[torch.Tensor] = None, types_hint: Optional[list] = None,
+                opts: Optional[dict] = None, user_types: Optional[list] = None):
     """Parse ``data`` on the device.  Inputs larger than ``chunk_bytes`` stream through a
     double-buffered pinned staging ring: chunk k+1's host->device copy runs on a side stream while
     chunk k is parsed, chunks split on row boundaries, type masks OR-merged over
@@ -178,12 +190,23 @@ def scan_device(data, sep: str = ",", infer: bool = True, device=None, ncols: Op
 
     ``types_hint``: column type codes from an earlier scan of the same bytes (the reader keeps
     them with its cached file): the parser then stores every column as its type directly — no
-    f64 plane to convert.  Inference still runs; a hint the masks contradict re-scans unhinted."""
+    f64 plane to convert.  Inference still runs; a hint the masks contradict re-scans unhinted.
+
+    ``opts``: dialect (quote, escape, comment, trim_lead, trim_trail, null_value; see
+    ``csv_parse_dev.h``).  ``user_types``: a user schema (lattice codes in STRICT_CODES): the
+    columns are stored as those types, a field that does not convert nulls its record (Spark's
+    PERMISSIVE), no inference."""
     # quotes / escapes need the host scanner: the parse kernel flags any field that starts with
     # one (slow path) and a mid-field one makes the column a string — both fall back, so the
     # input is never pre-scanned on the host
-    if not infer or len(sep) != 1:
+    if len(sep) != 1 or not (infer or user_types):
         return None
+    if user_types:
+        if any(t not in STRICT_CODES for t in user_types):
+            return None
+        opts = dict(opts or {}, strict=True)
+        ncols = len(user_types)
+        types_hint = list(user_types)
     h = native.hip()
     dev = torch.device(device)
     if ncols is None:
@@ -202,7 +225,7 @@ def scan_device(data, sep: str = ",", infer: bool = True, device=None, ncols: Op
         parts = []
         for s, e in zip(bounds, bounds[1:]):
             trailing = data[e - 1] not in (10, 13)
-            parts.append(_scan_chunk(h, device_data[s:e], e - s, trailing, ncols, sep, dev, hint))
+            parts.append(_scan_chunk(h, device_data[s:e], e - s, trailing, ncols, sep, dev, hint, opts))
     elif chunk_bytes is None or n <= chunk_bytes:
         if pinned is not None and n:
             buf = pinned.to(dev, non_blocking=True)  # page-locked mapping: direct DMA
@@ -210,11 +233,20 @@ def scan_device(data, sep: str = ",", infer: bool = True, device=None, ncols: Op
             host = torch.frombuffer(bytearray(data), dtype=torch.uint8) if n else torch.zeros(0, dtype=torch.uint8)
             buf = host.pin_memory().to(dev, non_blocking=True) if n else torch.zeros(1, dtype=torch.uint8, device=dev)
         trailing = n > 0 and data[-1] not in (10, 13)
-        parts = [_scan_chunk(h, buf, n, trailing, ncols, sep, dev, hint)]
+        parts = [_scan_chunk(h, buf, n, trailing, ncols, sep, dev, hint, opts)]
     else:
-        parts = _scan_chunked(h, data, ncols, sep, dev, int(chunk_bytes), pinned, hint)
+        parts = _scan_chunked(h, data, ncols, sep, dev, int(chunk_bytes), pinned, hint, opts)
     st = torch.stack([p[4] for p in parts]).cpu().numpy()  # the one host read of the parse results
     masks = np.bitwise_or.reduce(st[:, 2 + ncols:], axis=0)
+    if user_types:
+        flag = int(st[:, 0].max())
+        if sharded:
+            flag = int(comm.all_reduce_max(torch.tensor([flag], dtype=torch.int64))[0])
+        if flag:
+            STATS["fallbacks"] += 1
+            return None
+        STATS["device_scans"] += 1
+        return _finish(parts, list(user_types), st, dev, hinted=True)
     types = _resolve_types(masks, int(st[:, 0].max()), sharded)
     if types is None:
         STATS["fallbacks"] += 1
@@ -224,7 +256,7 @@ def scan_device(data, sep: str = ",", infer: bool = True, device=None, ncols: Op
         miss = bool(int(comm.all_reduce_max(torch.tensor([int(miss)], dtype=torch.int64))[0]))
     if miss:
         STATS["hint_misses"] = STATS.get("hint_misses", 0) + 1
-        return scan_device(data, sep, infer, device, ncols, sharded, chunk_bytes, pinned, device_data, None)
+        return scan_device(data, sep, infer, device, ncols, sharded, chunk_bytes, pinned, device_data, None, opts)
     STATS["device_scans"] += 1
     STATS["chunks"] = STATS.get("chunks", 0) + len(parts)
     return _finish(parts, types, st, dev, hinted=hint is not None)
@@ -248,7 +280,7 @@ def chunk_bounds(data: bytes, chunk_bytes: int):
 
 
 def _scan_chunked(h, data, ncols: int, sep: str, dev, chunk_bytes: int, pinned: Optional[torch.Tensor] = None,
-                  hint=None):
+                  hint=None, opts=None):
     from ..runtime.streams import StagingRing
 
     bounds = chunk_bounds(data, chunk_bytes)
@@ -267,7 +299,7 @@ def _scan_chunked(h, data, ncols: int, sep: str, dev, chunk_bytes: int, pinned: 
             put(i + 1)  # overlaps chunk i's parse
         buf = ring.get(i)
         trailing = data[e - 1] not in (10, 13)
-        parts.append(_scan_chunk(h, buf, e - s, trailing, ncols, sep, dev, hint))
+        parts.append(_scan_chunk(h, buf, e - s, trailing, ncols, sep, dev, hint, opts))
         ring.release(i)
     return parts
 

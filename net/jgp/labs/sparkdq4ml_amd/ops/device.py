@@ -148,11 +148,12 @@ def gram_stats(X, y, w, sel, compute: str = "fp64", x_zero_dead: bool = False, b
         # the requested precision; the fragment kernels carry no per-row weights)
         return _gram_syrk(h, X, y, w, sel, compute_f64=mode == 0)
     if mode == 1:
-        # "fp32" statistics: f32 (or f64) features through the f64 MFMA kernel — products of f32
-        # values are exact in f64, so this is at least the requested precision, at f32 bytes
-        mode = 0
+        # "fp32" statistics: f32 features -> exact-f32 MFMA stream kernel (gram_stream.hip);
+        # anything else (f64 storage, unaligned views) -> the f64 kernel, at least as precise
         if X.dtype not in (torch.float32, torch.float64):
             X = X.to(torch.float32)
+        if X.dtype != torch.float32 or d <= 8:
+            mode = 0  # d <= 8: the f64 lane-per-row skinny kernel (exact, and HBM-bound already)
     if mode == 2 and X.dtype not in (torch.bfloat16, torch.float32, torch.float64):
         X = X.to(torch.float32)
     if mode == 0 and X.dtype not in (torch.float64, torch.float32):
@@ -172,6 +173,12 @@ def gram_stats(X, y, w, sel, compute: str = "fp64", x_zero_dead: bool = False, b
             sel = sel.to(torch.bool)
     if y.numel() != n or (w is not None and w.numel() != n) or (sel is not None and sel.numel() != n):
         raise ValueError("gram_stats: row-count mismatch")
+    if mode in (0, 1) or X.dtype == torch.float32:
+        # the LDS-DMA stream kernels (gram_stream.hip) read labels / weights as 16-B chunks and the
+        # selection as 4-B words: re-base unaligned views (an n-element copy, far below the pass)
+        y = y if y.data_ptr() % 16 == 0 else y.clone()
+        w = w if w is None or w.data_ptr() % 16 == 0 else w.clone()
+        sel = sel if sel is None or sel.data_ptr() % 4 == 0 else sel.clone()
     if w is not None:
         xmode = 2
     elif sel is not None and not x_zero_dead:
@@ -232,6 +239,9 @@ def gram_cols(parts: List[torch.Tensor], y, sel, blocks: Optional[int] = None):
         dtype_code(r)
     dev = rows[0].device
     y, _, sel = _prep_rows(y, None, sel, n)
+    out = gram_stream_cols(rows, y, None, sel, "bf16")
+    if out is not None:
+        return out
     if sel is None:  # the kernel's loads are branch-free: an all-ones selection
         sel = _ones_sel(n, dev)
     desc = _srcw_desc(h, rows, dev)
@@ -250,6 +260,50 @@ def gram_cols(parts: List[torch.Tensor], y, sel, blocks: Optional[int] = None):
 
 _cols_plan = {}
 _ones = {}
+
+
+def gram_stream_cols(parts, y, w, sel, compute: str):
+    """WLS statistics straight from the assembler's SOURCE columns through the LDS-DMA stream
+    kernels (gram_stream.hip): every column is DMA'd into the swizzled LDS tiles, the assembled
+    matrix is never written.  ``compute``: fp64 (f64 MFMA; all-f64 or all-f32 sources), fp32
+    (exact-f32 MFMA; f32 sources), bf16 (bf16 MFMA on converted tiles; f32 sources, unit weights).
+    Returns None when the sources do not qualify (mixed / unaligned / d outside 9..64): the caller
+    takes the packing or the typed-load kernels instead."""
+    rows = _rows_of(parts)
+    d = len(rows)
+    if not 9 <= d <= 64 or not rows[0].is_cuda:
+        return None
+    n = rows[0].numel()
+    dts = {r.dtype for r in rows}
+    if len(dts) != 1 or any(r.numel() != n or r.data_ptr() % 16 for r in rows):
+        return None
+    xdt = dts.pop()
+    mode = GRAM_MODES[compute]
+    if xdt not in (torch.float32, torch.float64) or (mode in (1, 2) and xdt != torch.float32):
+        return None
+    if mode == 3 or (mode == 2 and w is not None):
+        return None
+    h = native.hip()
+    dev = rows[0].device
+    y, w, sel = _prep_rows(y, w, sel, n)
+    y = y if y.data_ptr() % 16 == 0 else y.clone()
+    w = w if w is None or w.data_ptr() % 16 == 0 else w.clone()
+    sel = sel if sel is None or sel.data_ptr() % 4 == 0 else sel.clone()
+    out = torch.empty(5 + 2 * d + d * (d + 1) // 2, dtype=torch.float64, device=dev)
+    if n == 0:
+        return out.zero_()
+    desc = _srcw_desc(h, rows, dev)
+    xc = dtype_code(rows[0])
+    key = ("stream", torch.cuda.current_device(), mode, d, n, xc)
+    nb = _cols_plan.get(key)
+    if nb is None:
+        nb = _cols_plan[key] = int(h.gram_stream_blocks(mode, d, n, xc))
+    P = int(h.gram_partial_stride(mode, d))
+    partials = torch.empty(nb * P, dtype=torch.float64, device=dev)
+    h.gram_stream_cols(mode, desc.data_ptr(), d, n, xc, y.data_ptr(), dtype_code(y), _ptr(w),
+                       dtype_code(w) if w is not None else 0, _ptr(sel), partials.data_ptr(), nb, out.data_ptr(),
+                       _stream())
+    return out
 
 
 def _ones_sel(n, dev):

@@ -72,6 +72,15 @@ def gram_cols(parts: Sequence[torch.Tensor], y: torch.Tensor, sel: Optional[torc
     return device.gram_cols(list(parts), y, sel)
 
 
+def gram_stream_cols(parts: Sequence[torch.Tensor], y: torch.Tensor, w: Optional[torch.Tensor] = None,
+                     sel: Optional[torch.Tensor] = None, compute: str = "fp64"):
+    """GPU only: WLS statistics of 9..64 same-dtype source columns through the LDS-DMA stream
+    kernels (``gram_stream.hip``); None when the sources do not qualify."""
+    from . import device
+
+    return device.gram_stream_cols(list(parts), y, w, sel, compute)
+
+
 def gram_skinny_cols(parts: Sequence[torch.Tensor], y: torch.Tensor, w: Optional[torch.Tensor] = None,
                      sel: Optional[torch.Tensor] = None):
     """GPU only: f64 statistics of a narrow (d <= 8) assembly read from its source columns."""

@@ -55,6 +55,57 @@ def _type_to_code(t) -> int:
     return 6
 
 
+def _device_csv_opts(o) -> Optional[dict]:
+    """The reader options as the device parser's dialect, or None when only the host scanner
+    implements them (multi-byte quote / escape / comment, nullValue longer than 16 bytes)."""
+    quote, escape = o.get("quote", '"'), o.get("escape", "\\")
+    comment, null_value = o.get("comment", ""), o.get("nullvalue", "")
+    if len(quote) != 1 or len(escape) != 1 or len(comment) > 1 or len(null_value.encode()) > 16:
+        return None
+    return {"quote": quote, "escape": escape, "comment": ord(comment) if comment else 0,
+            "trim_lead": _truthy(o.get("ignoreleadingwhitespace", "false")),
+            "trim_trail": _truthy(o.get("ignoretrailingwhitespace", "false")),
+            "null_value": null_value}
+
+
+def _split_header(data, sep: str, opts: dict):
+    """(column names, byte offset of the first data line) of the header record — the first
+    non-empty, non-comment line, split the host scanner's way — or None when it needs the general
+    tokenizer (quotes / escapes in it) or the file has no data line.  A bounded head search: the
+    input may be a multi-GB map."""
+    n = len(data)
+    pos, w = 0, 1 << 16
+    comment = opts["comment"]
+    while pos < n:
+        head = bytes(data[pos:min(n, pos + w)])
+        cut = [x for x in (head.find(b"\n"), head.find(b"\r")) if x >= 0]
+        if not cut and pos + len(head) < n:
+            w *= 16
+            continue
+        e = min(cut) if cut else len(head)
+        line = head[:e]
+        nxt = pos + e + 1 if cut else n
+        if cut and head[e:e + 2] == b"\r\n":
+            nxt += 1
+        if line and not (comment and line[0] == comment):
+            text = line.decode("utf-8", "replace")
+            if opts["quote"] in text or opts["escape"] in text or nxt >= n:
+                return None
+            names = []
+            for i, f in enumerate(text.split(sep)):
+                if f == opts["null_value"]:
+                    names.append(f"_c{i}")
+                    continue
+                if opts["trim_lead"]:
+                    f = f.lstrip(" \t")
+                if opts["trim_trail"]:
+                    f = f.rstrip(" \t")
+                names.append(f)
+            return names, nxt
+        pos = nxt
+    return None
+
+
 def _truthy(v) -> bool:
     return str(v).lower() in ("true", "1", "yes")
 
@@ -200,12 +251,17 @@ class DataFrameReader:
             header = header and rank == 0
         if presharded:
             lo, hi = 0, len(data)  # pf holds exactly this rank's bytes
-        # the device scanner implements the default dialect (the app's options, APP:53-55);
-        # any other option takes the host scanner
-        plain = (o.get("quote", '"') == '"' and o.get("escape", "\\") == "\\" and not o.get("nullvalue", "")
-                 and not o.get("comment", "") and not _truthy(o.get("ignoreleadingwhitespace", "false"))
-                 and not _truthy(o.get("ignoretrailingwhitespace", "false")))
-        use_dev = dev.type == "cuda" and not user_types and not _truthy(o.get("header", "false")) and plain
+        # the device scanner takes the common dialect options (csv_parse_dev.h): header, a user
+        # schema of int / long / double / boolean columns, nullValue, comment, the whitespace
+        # trims, any single-byte quote / escape (fields starting with one -> host re-scan)
+        dopts = _device_csv_opts(o)
+        strict = [c for c in user_types] if user_types else None
+        use_dev = (dev.type == "cuda" and dopts is not None and len(sep) == 1 and (infer or strict)
+                   and (not strict or all(c in (1, 2, 4, 5) for c in strict)))
+        hdr = None
+        if use_dev and header:
+            hdr = _split_header(data, sep, dopts)
+            use_dev = hdr is not None
         if shard:  # every rank must take the same (collective) path
             use_dev = all(comm.all_gather_object(bool(use_dev and len(data) >= thresh)))
         elif use_dev:
@@ -213,21 +269,34 @@ class DataFrameReader:
         if use_dev:
             from ..ops import csvscan
 
+            off = hdr[1] if hdr is not None else 0
+            names = hdr[0] if hdr is not None else None
+            if shard and header is not None:
+                # names come from the rank whose shard holds the header (rank 0)
+                names = comm.all_gather_object(names)[0]
+            body = data[off:] if off else data
             dbytes = None
             if pf is not None and _truthy(self._session.conf.get("dq4ml.csv.deviceCache", "true")):
                 from ..runtime import filecache
 
                 if filecache.device_bytes_allowed(hi - lo):
                     dbytes = pf.device_bytes(dev, lo, hi)  # HBM-resident input bytes
-            hkey = (lo, hi, sep)
+                    dbytes = dbytes[off:] if off else dbytes
+            hkey = (lo + off, hi, sep, repr(sorted(dopts.items())))
+            ncols = len(strict) if strict else (len(names) if names else None)
             with tracing.span("csv_scan"):
-                t = csvscan.scan_device(data, sep=sep, infer=infer, device=dev, sharded=shard,
+                t = csvscan.scan_device(body, sep=sep, infer=infer, device=dev, sharded=shard, ncols=ncols,
                                         chunk_bytes=int(self._session.conf.get("dq4ml.chunkBytes", str(256 << 20))),
-                                        pinned=pinned, device_data=dbytes,
-                                        types_hint=pf.type_hints.get(hkey) if pf is not None else None)
+                                        pinned=None if pinned is None else pinned[off:], device_data=dbytes,
+                                        types_hint=(pf.type_hints.get(hkey) if pf is not None and not strict
+                                                    else None), opts=dopts, user_types=strict)
             if t is not None:
-                if pf is not None:  # the next action's scan of these bytes stores typed columns directly
+                if pf is not None and not strict:  # the next action's scan stores typed columns directly
                     pf.type_hints[hkey] = [csvscan.type_code_of(f.dataType) for f in t.schema.fields]
+                final = user_names if strict else names
+                if final:
+                    fields = [StructField(nm, f.dataType, True) for nm, f in zip(final, t.schema.fields)]
+                    t = Table(StructType(fields), t.columns, t.nrows, t.sel, t.device)
                 return t
         if not isinstance(data, bytes):
             data = bytes(data)  # host scanner path (small or fallback): a plain copy

@@ -51,6 +51,15 @@ for s in $STEPS; do
     fitprof) step fitprof 300 env N=1.25e7 python scripts/fit_profile.py ;;
     dist2) step dist2 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 scripts/dist_rehearsal.py ;;
     benchf32) step benchf32 600 python bench.py --steps 10 --warmup 2 --dtype fp32 ;;
+    benchf64) step benchf64 600 python bench.py --steps 10 --warmup 2 --dtype fp64 ;;
+    benchf64old) step benchf64old 600 env DQ4ML_GRAM_STREAM=0 python bench.py --steps 10 --warmup 2 --dtype fp64 ;;
+    benchf64s32) step benchf64s32 600 python bench.py --steps 10 --warmup 2 --dtype fp64 --storage fp32 ;;
+    benchs32) step benchs32 600 python bench.py --steps 10 --warmup 2 --dtype bf16 --storage fp32 ;;
+    benchcols) step benchcols 600 python bench.py --steps 10 --warmup 2 --dtype bf16 --storage f32cols ;;
+    benchring2) step benchring2 600 env DQ4ML_GRAM_STREAM_RING=2 python bench.py --steps 10 --warmup 2 --dtype fp32 ;;
+    benchring2f64) step benchring2f64 600 env DQ4ML_GRAM_STREAM_RING=2 python bench.py --steps 10 --warmup 2 --dtype fp64 ;;
+    benchring2cols) step benchring2cols 600 env DQ4ML_GRAM_STREAM_RING=2 python bench.py --steps 10 --warmup 2 --dtype bf16 --storage f32cols ;;
+    kprofcols) (export TMPDIR=/tmp; step kprofcols 600 rocprofv3 --kernel-trace --stats -d gpurun_out/kprofcols -o run --output-format csv -- python bench.py --steps 5 --warmup 1 --storage f32cols) || exit $? ;;
     prof) cd /tmp && export TMPDIR=/tmp && cd - >/dev/null; step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 5 --warmup 1 ;;
   esac
 done

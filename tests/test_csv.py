@@ -340,3 +340,99 @@ def test_filecache_keeps_other_ranges_of_unchanged_file(tmp_path, monkeypatch):
     a2 = filecache.open_pinned(str(p), 0, 4)
     assert a2 is not a and len(filecache._cache) == 1
     filecache.clear()
+
+
+def _fuzz_csv(rng, n, header, null_tok, spaces, comment):
+    lines = []
+    if comment:
+        lines.append("# a comment line before the header")
+    if header:
+        lines.append(" id , price,ok,big " if spaces else "id,price,ok,big")
+    for i in range(n):
+        r = rng.random()
+        if comment and r < 0.02:
+            lines.append("#" + "skip me,1,2")
+            continue
+        if r < 0.03:
+            lines.append("")
+            continue
+        f = [str(int(rng.integers(-10**6, 10**6))), repr(round(float(rng.normal()) * 100, 3)),
+             "true" if rng.random() < 0.5 else "FALSE", str(int(rng.integers(-2**40, 2**40)))]
+        for k in range(4):
+            u = rng.random()
+            if u < 0.05:
+                f[k] = null_tok
+            elif u < 0.07:
+                f[k] = ""
+        if spaces:
+            f = [(" " * int(rng.integers(0, 3))) + x + ("\t" if rng.random() < 0.3 else "") for x in f]
+        lines.append(",".join(f))
+    return "\n".join(lines).encode()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["header", "header_schema", "null_value", "whitespace", "comment", "schema_bad"])
+def test_device_reader_options_match_host(tmp_path, case):
+    """Reader options on the device scanner (header, user schema, nullValue, whitespace trims,
+    comment lines): same rows, types and names as the host scanner, and the device path is
+    actually taken."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from net.jgp.labs.sparkdq4ml_amd import SparkSession
+    from net.jgp.labs.sparkdq4ml_amd.ops import csvscan
+
+    rng = np.random.default_rng(hash(case) % 1000)
+    opts = {"inferSchema": "true"}
+    schema = None
+    header = case in ("header", "header_schema", "whitespace", "comment")
+    null_tok = "NA" if case == "null_value" else ""
+    data = _fuzz_csv(rng, 5000, header, null_tok, case == "whitespace", case == "comment")
+    if header:
+        opts["header"] = "true"
+    if case == "null_value":
+        opts["nullValue"] = "NA"
+    if case == "whitespace":
+        opts["ignoreLeadingWhiteSpace"] = "true"
+        opts["ignoreTrailingWhiteSpace"] = "true"
+    if case == "comment":
+        opts["comment"] = "#"
+    if case in ("header_schema", "schema_bad"):
+        schema = "a INT, b DOUBLE, c BOOLEAN, d LONG"
+        if case == "schema_bad":  # values the schema's types do not accept -> all-null records
+            data = data + b"\n1.5,2,true,3\nx,1,false,2\n7,8,maybe,9\n3,4,true,99999999999999999"
+    p = tmp_path / f"{case}.csv"
+    p.write_bytes(data)
+
+    def read(threshold):
+        s = SparkSession.getActiveSession()
+        if s is not None:
+            s.stop()
+        spark = SparkSession.builder().master("mi355x[*]").config("dq4ml.csv.deviceThresholdBytes",
+                                                                  threshold).getOrCreate()
+        r = spark.read()
+        for k, v in opts.items():
+            r = r.option(k, v)
+        if schema:
+            r = r.schema(schema)
+        before = csvscan.STATS["device_scans"]
+        df = r.csv(str(p))
+        took = csvscan.STATS["device_scans"] - before
+        out = (df.dtypes, [tuple(x) for x in df.collect()], took)
+        spark.stop()
+        return out
+
+    dev_types, dev_rows, took = read(0)
+    host_types, host_rows, _ = read(1 << 40)
+    assert took == 1, "the device scanner did not take the read"
+    assert dev_types == host_types
+    assert len(dev_rows) == len(host_rows)
+
+    def same(a, b):
+        if a is None or b is None:
+            return a is b
+        if isinstance(a, float) and a != a:
+            return b != b
+        return a == b
+
+    for ra, rb in zip(dev_rows, host_rows):
+        assert all(same(a, b) for a, b in zip(ra, rb)), (ra, rb)
