@@ -215,9 +215,13 @@ __device__ __forceinline__ bool parse_line(PB B, int64_t bias, int64_t n, const 
   bool slow = false, malformed = false;
   for (int c = 0; c < ncols; ++c) {
     double dv = 0.0;
+    long long lv = 0;
+    bool big = false;
     int ty = CT_NULL;
-    if (pos <= end && line) ty = dq4ml_csv::csv_field(B, (long long)bias, pos, (long long)end, o, dv, slow, malformed);
+    if (pos <= end && line)
+      ty = dq4ml_csv::csv_field(B, (long long)bias, pos, (long long)end, o, dv, lv, slow, big, malformed);
     const int kind = (int)dcols[ncols + c];
+    slow |= big && kind != 2;  // an f64 plane would round it; an int64 store of lv is exact
     bool ok = ty != CT_NULL && ty != CT_STRING;
     if (o.strict && ty != CT_NULL && !dq4ml_csv::csv_conforms(ty, kind)) {
       malformed = true;  // a value the user schema's type does not accept
@@ -231,7 +235,7 @@ __device__ __forceinline__ bool parse_line(PB B, int64_t bias, int64_t n, const 
       void* dst = reinterpret_cast<void*>(dcols[c]);
       switch (kind) {
         case 1: reinterpret_cast<int32_t*>(dst)[li] = ok ? (int32_t)dv : 0; break;
-        case 2: reinterpret_cast<int64_t*>(dst)[li] = ok ? (int64_t)dv : 0; break;
+        case 2: reinterpret_cast<int64_t*>(dst)[li] = ok ? (int64_t)lv : 0; break;
         case 3: reinterpret_cast<uint8_t*>(dst)[li] = ok && dv != 0.0; break;
         default: reinterpret_cast<double*>(dst)[li] = dv;
       }
