@@ -38,13 +38,7 @@ namespace {
 constexpr int kBytesPerThread = 64;
 constexpr int kChunk = 256 * kBytesPerThread;  // bytes per block
 
-// 4-bit mask of the bytes of v equal to the byte in every lane of pat (SWAR: exact per byte —
-// no borrow crosses bytes — then the four 0x80 flags gathered to bits 0..3 by one multiply)
-__device__ __forceinline__ uint32_t byte_eq4(uint32_t v, uint32_t pat) {
-  const uint32_t x = v ^ pat;
-  const uint32_t z = ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x | 0x7F7F7F7Fu);
-  return (((z >> 7) * 0x00204081u) >> 21) & 0xFu;
-}
+using dq4ml_csv::byte_eq4;
 
 // terminator bitmask of the thread's 64-byte window; window byte k <-> buffer index base + k.
 // Terminators: \r, and \n not preceded by \r (CR LF is one terminator, at the CR).

@@ -160,6 +160,9 @@ def _finish(parts, types, st, dev, hinted=False):
         keeps = [p[3][:p[0]] for _, p in live]
         k = torch.cat(keeps) if len(keeps) > 1 else keeps[0]
         table = Table(table.schema, table.columns, total, k.clone(), dev).compact()
+    # what a later fused scan of the same bytes relies on (ops/scanfuse.py): line count (empty
+    # lines included) and the columns holding nulls
+    table.scan_facts = {"nlines": int(total), "nullable": [bool(int(st[:, 2 + c].sum())) for c in range(len(types))]}
     return table
 
 

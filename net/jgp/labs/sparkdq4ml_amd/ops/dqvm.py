@@ -145,6 +145,15 @@ class _Chain:
         raise Unfusable(f"unresolved {name}")
 
 
+def _m_and(*ms: str) -> str:
+    """Validity conjunction, folded: constant-true operands drop out (a chain over null-free
+    columns then stores no validity at all)."""
+    if any(m == "false" for m in ms):
+        return "false"
+    rest = [m for m in ms if m != "true"]
+    return "true" if not rest else " && ".join(f"({m})" for m in rest)
+
+
 def _compile(g: _Gen, e: E.Expr, chain: _Chain, schema: StructType, live: str) -> Tuple[str, str, DataType]:
     """-> (value C expression/variable, valid C expression/variable, DataType)."""
     if isinstance(e, E.Alias):
@@ -195,9 +204,12 @@ def _compile(g: _Gen, e: E.Expr, chain: _Chain, schema: StructType, live: str) -
         t = wider_numeric(at, bt) if (is_numeric(at) or is_numeric(bt)) else at
         ct = _ctype(t)
         take = g.tmp("k")
-        g.emit(f"const bool {take} = ({cm}) && ({cv});")
-        v, m = g.tmp("v"), g.tmp("m")
+        g.emit(f"const bool {take} = {_m_and(cm, cv)};")
+        v = g.tmp("v")
         g.emit(f"const {ct} {v} = {take} ? ({ct})({av}) : ({ct})({bv});")
+        if am == bm:
+            return v, am, t
+        m = g.tmp("m")
         g.emit(f"const bool {m} = {take} ? ({am}) : ({bm});")
         return v, m, t
     if isinstance(e, E.CaseWhen):
@@ -258,9 +270,13 @@ def _binop(g, e: E.BinOp, chain, schema, live):
         v, m = g.tmp("v"), g.tmp("m")
         if e.op == "and":
             g.emit(f"const bool {v} = ({av}) && ({bv});")
+            if am == "true" and bm == "true":
+                return v, "true", BooleanType()
             g.emit(f"const bool {m} = (({am}) && ({bm})) || (({am}) && !({av})) || (({bm}) && !({bv}));")
         else:
             g.emit(f"const bool {v} = (({am}) && ({av})) || (({bm}) && ({bv}));")
+            if am == "true" and bm == "true":
+                return v, "true", BooleanType()
             g.emit(f"const bool {m} = (({am}) && ({bm})) || (({am}) && ({av})) || (({bm}) && ({bv}));")
         return v, m, BooleanType()
     av, am, at = _compile(g, e.left, chain, schema, live)
@@ -271,12 +287,16 @@ def _binop(g, e: E.BinOp, chain, schema, live):
     oc = _ctype(ot)
     a, b = f"(({oc})({av}))", f"(({oc})({bv}))"
     v, m = g.tmp("v"), g.tmp("m")
+    both = _m_and(am, bm)
+    if both in ("true", "false"):
+        m = both
     if e.op in _CMPS:
         if oc in ("double", "float") and not getattr(e, "ieee", False):
             g.emit(f"const bool {v} = {_spark_cmp_c(e.op, a, b)};")
         else:
             g.emit(f"const bool {v} = {a} {_CMPS[e.op]} {b};")
-        g.emit(f"const bool {m} = ({am}) && ({bm});")
+        if m not in ("true", "false"):
+            g.emit(f"const bool {m} = {both};")
         return v, m, BooleanType()
     if e.op == "<=>":
         eq = _spark_cmp_c("=", a, b) if oc in ("double", "float") else f"({a} == {b})"
@@ -284,8 +304,11 @@ def _binop(g, e: E.BinOp, chain, schema, live):
         return v, "true", BooleanType()
     if e.op in ("+", "-", "*"):
         g.emit(f"const {oc} {v} = {a} {e.op} {b};")
-        g.emit(f"const bool {m} = ({am}) && ({bm});")
+        if m not in ("true", "false"):
+            g.emit(f"const bool {m} = {both};")
         return v, m, ot
+    if e.op in ("/", "%"):
+        m = g.tmp("m")  # these add their own validity condition (no folding)
     if e.op == "/":
         g.emit(f"const double {v} = ((double)({bv})) == 0.0 ? 0.0 : ((double)({av})) / ((double)({bv}));")
         g.emit(f"const bool {m} = ({am}) && ({bm}) && ((double)({bv})) != 0.0;")
@@ -354,12 +377,16 @@ def _trivial(node) -> bool:
         isinstance(x, E.ColRef) or (isinstance(x, E.Alias) and isinstance(x.child, E.ColRef)) for x in node.exprs)
 
 
-def compile_chain(nodes, base: Table, check_device: bool = True):
+def compile_chain(nodes, base: Table, check_device: bool = True, gen: Optional[_Gen] = None):
     """nodes: bottom-up list of Project/Filter.  Returns (source, gen, outputs) where outputs[i] is
-    ('col', base_idx) or ('new', slot, valid_slot_or_None, tensor, valid_tensor, dtype)."""
+    ('col', base_idx) or ('new', slot, valid_slot_or_None, tensor, valid_tensor, dtype).
+
+    ``gen``: a generator whose base columns are not loaded from memory (the fused CSV scan,
+    ``ops/scanfuse.py``: they are parsed into registers): pass-through columns are then stored
+    like computed ones, the selection vector is always written and no source is generated here."""
     from ..sql.plan import Filter, Project
 
-    g = _Gen(base, check_device)
+    g = gen if gen is not None else _Gen(base, check_device)
     g.slot(base.sel, ("sel",))  # P[0] selection in
     g.slot(None, ("err",))  # P[1] error flag (filled by caller)
     live = "live"
@@ -393,9 +420,12 @@ def compile_chain(nodes, base: Table, check_device: bool = True):
     outputs = []
     for name, sym in zip(chain.names, chain.syms):
         if sym[0] == "col":
-            outputs.append(("col", sym[1]))
-            continue
-        _, v, m, t, _ = sym
+            if gen is None:  # zero-copy pass-through
+                outputs.append(("col", sym[1]))
+                continue
+            v, m, t = g.load_col(sym[1])
+        else:
+            _, v, m, t, _ = sym
         td = _TORCH[type(t)]
         out = torch.empty(n, dtype=td, device=dev)
         s = g.slot(out, ("out", len(outputs)))
@@ -407,11 +437,11 @@ def compile_chain(nodes, base: Table, check_device: bool = True):
             g.stores.append(("bool", m, sv))
         outputs.append(("new", out, vt, t))
     sel_out = None
-    if g.has_filter:
+    if g.has_filter or gen is not None:
         sel_out = torch.empty(n, dtype=torch.bool, device=dev)
         s = g.slot(sel_out, ("selout",))
         g.stores.append(("bool", "live", s))
-    src = (_kernel_source(g), _kernel_source_vec(g))
+    src = (_kernel_source(g), _kernel_source_vec(g)) if gen is None else None
     return src, g, outputs, sel_out
 
 
@@ -564,6 +594,14 @@ def _chain_key(nodes, base: Table):
     """Structural key of (chain, base layout): expression SQL text + output names per node, the
     resolved UDF objects (a re-registered name is a new object), base column types / storage
     dtypes / validity, selection presence."""
+    (parts, udfs), refs = nodes_key(nodes)
+    cols = tuple((f.name, f.dataType.simpleString(), str(c.values.dtype) if torch.is_tensor(c.values) else "-",
+                  c.valid is not None) for f, c in zip(base.schema.fields, base.columns))
+    return (parts, cols, base.sel is not None, udfs), refs
+
+
+def nodes_key(nodes):
+    """((per-node structure, UDF identities), resolved UDF objects) of a Project/Filter chain."""
     from ..sql.plan import Filter
 
     parts, refs = [], []
@@ -575,9 +613,7 @@ def _chain_key(nodes, base: Table):
             parts.append(("P", tuple(x.sql_name() for x in nd.exprs), tuple(nd.schema().names)))
             for x in nd.exprs:
                 _udfs_of(x, refs)
-    cols = tuple((f.name, f.dataType.simpleString(), str(c.values.dtype) if torch.is_tensor(c.values) else "-",
-                  c.valid is not None) for f, c in zip(base.schema.fields, base.columns))
-    return (tuple(parts), cols, base.sel is not None, tuple((id(r), b) for r, b in refs)), refs
+    return (tuple(parts), tuple((id(r), b) for r, b in refs)), refs
 
 
 def try_execute_fused(plan, session) -> Optional[Table]:
@@ -595,6 +631,19 @@ def try_execute_fused(plan, session) -> Optional[Table]:
     nodes.reverse()
     if all(_trivial(nd) for nd in nodes):
         return None
+    from ..sql.plan import CsvScanRelation
+
+    if isinstance(p, CsvScanRelation) and p._memo is None and p.fused is not None:
+        # the chain sits right on a not-yet-scanned CSV relation: scan + chain in one kernel
+        from . import scanfuse
+
+        r = scanfuse.try_fused_scan(nodes, p, plan, session)
+        if r == "vector":
+            STATS["vector_deferred"] += 1
+            return None
+        if r is not None:
+            STATS["fused_launches"] += 1
+            return _maybe_compact(r)
     base = execute(p, session)
     if base.nrows == 0 or base.device.type != "cuda":
         return None

@@ -1,0 +1,413 @@
+"""Fused CSV scan + DQ chain: K1 (line boundaries) + K2 (field parse) + K3 (DQ rules, filters,
+casts) in ONE hipRTC kernel per action.
+
+Spark re-reads ``dataset-abstract.csv`` on every action and runs the parsed rows through the
+rule UDFs and the clean-up filters in one whole-stage-codegen pipeline
+(``DataQuality4MachineLearningApp.java:53-55, 68-90``).  The unfused device path here took five
+kernels per action: terminator counts, their scan, a materialized ``[nlines]`` line-end array,
+the parse (one typed plane per column, validity, keep flags) and the ``dq_fused`` chain kernel
+re-reading those planes.  This module generates a kernel that
+
+* takes 16 KiB byte windows per block (the ``csv_count_kernel`` windows, so the exclusive scan of
+  the per-window terminator counts gives each block its first global line index — the only
+  global intermediate, ``nb`` int64s);
+* stages the window plus a head region (bytes of the line that straddles into the window) in
+  LDS with 16-byte granule loads, finds the terminators from the staged registers (SWAR), and
+  keeps their positions in LDS (uint16, 1024-line rounds) — no line-end array in HBM;
+* parses each line (one thread per line, ``csv_parse_dev.h`` field parser) into registers,
+  evaluates the DQ chain lowered by ``ops/dqvm.py`` on those registers, and stores only the
+  columns the consumer needs plus the selection vector.
+
+It runs only for a relation whose schema, null columns and line count are already known from an
+earlier device scan of the SAME cached bytes (``runtime.filecache``; Spark's own schema-inference
+job at ``load()`` is that earlier scan), so nothing has to be read back on the host: the action is
+asynchronous end to end.  The kernel still verifies every field against those facts and raises a
+deferred data error (``runtime/checks.py``) if one ever disagrees."""
+from __future__ import annotations
+
+import os
+from typing import Optional
+
+import numpy as np
+import torch
+
+__all__ = ["kernel_source", "ENTRY", "WINDOW", "head_bytes", "STATS"]
+
+ENTRY = "dq_scan_fused"
+WINDOW = 16384  # bytes per block: csv_count_kernel's window (256 threads x 64 bytes)
+CAP = 1024  # line ends per LDS round
+STATS = {"fused_scans": 0}
+
+_HDR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "csrc", "hip", "csv_parse_dev.h")
+_header_text: Optional[str] = None
+
+
+def header_text() -> str:
+    global _header_text
+    if _header_text is None:
+        with open(_HDR) as f:
+            _header_text = f.read().replace("#pragma once\n", "")
+    return _header_text
+
+
+def head_bytes(mean_line: float) -> int:
+    """LDS head region: the part of the line that straddles into the window — 4x the mean line
+    length, a power of two in [256, 2048].  A longer straddling line parses from global memory."""
+    h = 256
+    while h < 4 * mean_line and h < 2048:
+        h *= 2
+    return h
+
+
+def _wpe() -> str:
+    """Occupancy hint (``DQ4ML_SCAN_WPE`` waves per SIMD; default: the compiler's choice)."""
+    w = int(os.environ.get("DQ4ML_SCAN_WPE", "0"))
+    return f"__attribute__((amdgpu_waves_per_eu({w}))) " if w > 0 else ""
+
+
+_VALUE = {1: "(int)l{c}", 2: "l{c}", 0: "d{c}", 3: "(d{c} != 0.0)"}
+
+
+def _c_char(v: int) -> str:
+    return str(int(v))
+
+
+def kernel_source(g, kinds, nullable, used, opts: dict, strict: bool, head: int, slots: dict) -> str:
+    """Source of the fused kernel.
+
+    ``g``: the dqvm generator after lowering the chain (its ``lines`` use ``f<c>`` / ``m<c>`` for
+    base column ``c``; ``stores`` write row ``li``).  ``kinds``: storage kind per CSV column (0 f64,
+    1 int32, 2 int64, 3 bool).  ``nullable``: columns with nulls in the earlier scan (others are
+    verified null-free).  ``used``: columns the chain reads.  ``slots``: pointer-slot indices of
+    the scan inputs (buf, offs, nalloc, trailing, vflag)."""
+    ncols = len(kinds)
+    ns = len(g.ptrs)
+    nv = list(opts.get("null_value", "").encode())
+    o = (f"{{(unsigned char){_c_char(ord(opts.get('sep', ',')))}, (unsigned char){_c_char(opts['quote'])}, "
+         f"(unsigned char){_c_char(opts['escape'])}, (unsigned char){_c_char(opts['comment'])}, "
+         f"(unsigned char){int(bool(opts['trim_lead']))}, (unsigned char){int(bool(opts['trim_trail']))}, "
+         f"(unsigned char){len(nv)}, (unsigned char){int(strict)}, "
+         f"{{{', '.join(str(x) for x in (nv + [0] * (16 - len(nv))))}}}}}")
+    parse = []
+    for c in range(ncols):
+        k = int(kinds[c])
+        parse.append(f"    double d{c} = 0.0; long long l{c} = 0; bool g{c} = false; int y{c} = C_NULL;\n"
+                     f"    if (pos <= end && line) y{c} = csv_field(B, bias, pos, end, O, d{c}, l{c}, slow, g{c}, malformed);\n"
+                     f"    bool k{c} = y{c} != C_NULL && y{c} != C_STRING;\n")
+        if strict:
+            parse.append(f"    if (y{c} != C_NULL && !csv_conforms(y{c}, {k})) {{ malformed = true; k{c} = false; }}\n")
+        else:
+            parse.append(f"    bad |= line && y{c} != C_NULL && !csv_conforms(y{c}, {k});\n")
+        if k != 2:
+            parse.append(f"    slow |= g{c};\n")
+    parse.append("    if (malformed) {" + " ".join(f"k{c} = false;" for c in range(ncols)) + " }\n")
+    for c in range(ncols):
+        if not nullable[c]:
+            parse.append(f"    bad |= line && !k{c};\n")
+    for c in sorted(used):
+        ct = used[c]
+        val = _VALUE[int(kinds[c])].format(c=c)
+        parse.append(f"    const {ct} f{c} = k{c} ? ({ct})({val}) : ({ct})0;\n")
+        if nullable[c]:
+            parse.append(f"    const bool m{c} = k{c};\n")
+    body = "\n".join("    " + ln.strip() for ln in g.lines).replace("P[", "p[")
+    stores = "".join(f"    (({t}*)p[{s}])[li] = ({t})({v});\n" for t, v, s in g.stores)
+    comment = int(opts["comment"])
+    H, W = int(head), WINDOW
+    return (header_text() + f"""
+using namespace dq4ml_csv;
+typedef unsigned int csv_u32x4 __attribute__((ext_vector_type(4)));
+
+// one line: parse every field into registers, run the DQ chain, store the needed outputs at li
+template <typename PB>
+__device__ __forceinline__ void dq_row(PB B, long long bias, long long start, long long end, long long li,
+                                       void* const* p, unsigned int* vflag) {{
+    const CsvOpts O = {o};
+    const bool line = end > start && !({comment} && B[start - bias] == {comment});
+    long long pos = start;
+    bool slow = false, malformed = false, bad = false;
+{''.join(parse)}    bad |= slow;
+    if (bad) atomicOr(vflag, 1u);
+    bool live = line;
+{body}
+{stores}}}
+
+extern "C" __global__ __launch_bounds__(256) {_wpe()}void {ENTRY}(void* const* P, long long n) {{
+  void* p[{ns}];
+#pragma unroll
+  for (int i = 0; i < {ns}; ++i) p[i] = P[i];
+  const unsigned char* __restrict__ b = (const unsigned char*)p[{slots['buf']}];
+  const long long* __restrict__ offs = (const long long*)p[{slots['offs']}];
+  const long long nalloc = (long long)p[{slots['nalloc']}];
+  const bool trailing = (long long)p[{slots['trailing']}] != 0;
+  unsigned int* vflag = (unsigned int*)p[{slots['vflag']}];
+  __shared__ __attribute__((aligned(16))) unsigned char stage[{H} + {W} + 16];
+  __shared__ unsigned short lend[{CAP} + 1];
+  __shared__ int wtot[4];
+  __shared__ long long sprev0;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const long long a = (long long)(reinterpret_cast<unsigned long long>(b) & 15ull);
+  const unsigned char* ab = b - a;                         // 16-byte aligned view
+  const long long wbase = (long long)blockIdx.x * {W} - a;  // buffer index of window byte 0
+  const long long sbase = wbase - {H};                     // buffer index of stage[0]
+  const long long tb = wbase + 64 * tid;                    // this thread's 64 window bytes
+  if (wbase > n) return;  // past the end (block-uniform; the virtual terminator at n is in an earlier window)
+  unsigned long long cr = 0ull, lf = 0ull;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {{
+    const long long gi = tb + 16 * j;
+    csv_u32x4 v = {{0u, 0u, 0u, 0u}};
+    if (gi < n && gi + 16 > 0) v = *reinterpret_cast<const csv_u32x4*>(ab + gi + a);
+    *reinterpret_cast<csv_u32x4*>(stage + {H} + 64 * tid + 16 * j) = v;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {{
+      cr |= (unsigned long long)byte_eq4(v[w], 0x0D0D0D0Du) << (16 * j + 4 * w);
+      lf |= (unsigned long long)byte_eq4(v[w], 0x0A0A0A0Au) << (16 * j + 4 * w);
+    }}
+  }}
+  for (int gq = tid; gq < {H // 16} + 1; gq += 256) {{  // head granules + one tail granule
+    const long long gi = gq < {H // 16} ? sbase + 16 * gq : wbase + {W};
+    csv_u32x4 v = {{0u, 0u, 0u, 0u}};
+    if (gi < n && gi + 16 > 0) v = *reinterpret_cast<const csv_u32x4*>(ab + gi + a);
+    *reinterpret_cast<csv_u32x4*>(stage + (gq < {H // 16} ? 16 * gq : {H} + {W})) = v;
+  }}
+  {{
+    const long long lo = tb < 0 ? -tb : 0, hi = n - tb;
+    if (lo > 0 || hi < 64) {{
+      const unsigned long long keep_lo = lo >= 64 ? 0ull : (~0ull << lo);
+      const unsigned long long keep_hi = hi <= 0 ? 0ull : (hi >= 64 ? ~0ull : ((1ull << hi) - 1));
+      cr &= keep_lo & keep_hi;
+      lf &= keep_lo & keep_hi;
+    }}
+  }}
+  __syncthreads();
+  const unsigned long long prev_cr = (tb >= 1 && tb - 1 < n && stage[{H} + 64 * tid - 1] == '\\r') ? 1ull : 0ull;
+  unsigned long long m = cr | (lf & ~((cr << 1) | prev_cr));
+  if (trailing) {{  // the last line has no terminator: a virtual one at n
+    const long long r = n - tb;
+    if (r >= 0 && r < 64) m |= 1ull << r;
+  }}
+  const int c = __popcll(m);
+  int inc = c;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {{
+    const int t = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += t;
+  }}
+  if (lane == 63) wtot[wave] = inc;
+  if (wave == 0) {{
+    // the terminator before the window's first line: nearest first, through the staged head
+    long long found = -2;
+    for (int k0 = 0; k0 < {H} && found == -2; k0 += 64) {{
+      const long long q = wbase - 1 - k0 - lane;
+      bool t = q < 0;
+      if (q >= 0) {{
+        const int sq = {H} - 1 - k0 - lane;
+        const int ch = stage[sq];
+        const bool pcr = q >= 1 && (sq >= 1 ? stage[sq - 1] : b[q - 1]) == '\\r';
+        t = ch == '\\r' || (ch == '\\n' && !pcr);
+      }}
+      const unsigned long long bal = __ballot(t);
+      if (bal) found = wbase - 1 - k0 - (long long)__builtin_ctzll(bal);
+    }}
+    for (long long q0 = wbase - 1 - {H}; found == -2; q0 -= 64) {{  // a line longer than the head
+      const long long q = q0 - lane;
+      bool t = q < 0;
+      if (q >= 0) {{
+        const int ch = b[q];
+        t = ch == '\\r' || (ch == '\\n' && !(q >= 1 && b[q - 1] == '\\r'));
+      }}
+      const unsigned long long bal = __ballot(t);
+      if (bal) found = q0 - (long long)__builtin_ctzll(bal);
+    }}
+    if (lane == 0) sprev0 = found < -1 ? -1 : found;
+  }}
+  __syncthreads();
+  int before = inc - c;
+  for (int w = 0; w < wave; ++w) before += wtot[w];
+  const int cnt = wtot[0] + wtot[1] + wtot[2] + wtot[3];
+  if (cnt == 0) return;  // block-uniform
+  const long long gl0 = offs[blockIdx.x];
+  for (int R = 0; R < cnt; R += {CAP}) {{
+    if (before + c > R - 1 && before < R + {CAP}) {{
+      unsigned long long mm = m;
+      int o = before;
+      while (mm) {{
+        const int bit = __builtin_ctzll(mm);
+        mm &= mm - 1;
+        if (o >= R - 1 && o < R + {CAP}) lend[o - R + 1] = (unsigned short)({H} + 64 * tid + bit);
+        ++o;
+      }}
+    }}
+    __syncthreads();
+    const int nr = min(cnt - R, {CAP});
+    for (int j = tid; j < nr; j += 256) {{
+      const int jl = R + j;
+      const long long end = sbase + lend[j + 1];
+      const long long prev = jl == 0 ? sprev0 : sbase + lend[j];
+      long long start = prev + 1;
+      if (prev >= 0 && prev + 1 < n) {{
+        const bool ins = prev >= sbase;
+        const int c0 = ins ? stage[prev - sbase] : b[prev];
+        const int c1 = (ins && prev + 1 - sbase < {H} + {W} + 16) ? stage[prev + 1 - sbase] : b[prev + 1];
+        start += (c0 == '\\r' && c1 == '\\n') ? 1 : 0;
+      }}
+      const long long li = gl0 + jl;
+      if (li >= nalloc) {{
+        atomicOr(vflag, 2u);
+      }} else if (start >= sbase) {{
+        dq_row(stage, sbase, start, end, li, p, vflag);
+      }} else {{
+        dq_row(b, 0ll, start, end, li, p, vflag);
+      }}
+    }}
+    __syncthreads();
+  }}
+}}
+""")
+
+
+# ---------------------------------------------------------------------------------------------
+# chain lowering over a not-yet-scanned relation + execution
+
+
+class _ScanBase:
+    """What ``dqvm.compile_chain`` reads of a base table, for a relation not scanned yet."""
+
+    def __init__(self, schema, nrows: int, device):
+        self.schema = schema
+        self.columns = [None] * len(schema.fields)
+        self.nrows = int(nrows)
+        self.sel = None
+        self.device = device
+
+
+def _scan_gen(base: _ScanBase, nullable):
+    from . import dqvm
+
+    class _ScanGen(dqvm._Gen):
+        """Base column c is the register pair (f<c>, m<c>) the kernel's parse defines — or
+        (f<c>, true) for a column the earlier scan found null-free (verified in the kernel)."""
+
+        def __init__(self):
+            super().__init__(base, check_device=False)
+            self.used = {}
+
+        def load_col(self, idx: int):
+            if idx not in self.col_cache:
+                t = self.base.schema.fields[idx].dataType
+                self.used[idx] = dqvm._ctype(t)
+                self.col_cache[idx] = (f"f{idx}", f"m{idx}" if nullable[idx] else "true", t)
+            return self.col_cache[idx]
+
+    return _ScanGen()
+
+
+class _ScanPlan:
+    SCAN_SLOTS = ("buf", "offs", "nalloc", "trailing", "vflag")
+
+    def __init__(self, src: str, g, outputs, refs):
+        self.src = src
+        self.recipe = list(g.recipe)
+        self.has_raise = g.has_raise
+        self.outs = [("new", o[1].dtype, o[2] is not None, o[3]) for o in outputs]
+        self.refs = refs
+
+    def bind(self, nalloc: int, dev, scalars: dict, err: torch.Tensor):
+        outs = [(torch.empty(nalloc, dtype=o[1], device=dev),
+                 torch.empty(nalloc, dtype=torch.bool, device=dev) if o[2] else None) for o in self.outs]
+        sel_out = torch.empty(nalloc, dtype=torch.bool, device=dev)
+        ptrs = []
+        for tag in self.recipe:
+            k = tag[0]
+            if k == "sel":
+                v = 0
+            elif k == "err":
+                v = err.data_ptr()
+            elif k == "out":
+                v = outs[tag[1]][0].data_ptr()
+            elif k == "outvalid":
+                v = outs[tag[1]][1].data_ptr()
+            elif k == "selout":
+                v = sel_out.data_ptr()
+            elif k in scalars:
+                x = scalars[k]
+                v = x.data_ptr() if torch.is_tensor(x) else int(x)
+            else:
+                raise AssertionError(f"scan plan: unbound slot {tag}")
+            ptrs.append(v)
+        return ptrs, outs, sel_out
+
+
+_CACHE: dict = {}
+
+
+def try_fused_scan(nodes, rel, plan, session):
+    """Run the Project/Filter chain ``nodes`` (bottom-up) fused into the scan of ``rel``.
+    Returns the chain's Table, ``"vector"`` (the chain ends in a VectorAssembler: the assembler
+    consumes the sub-chain instead) or None (not fusable: the caller scans, then runs the chain)."""
+    from ..runtime.checks import defer
+    from ..sql.table import ColumnData, Table
+    from . import dqvm, native
+    from .device import _h2d
+
+    f = rel.fused
+    (parts, udfs), refs = dqvm.nodes_key(nodes)
+    head = head_bytes(f["mean_line"])
+    key = (parts, udfs, tuple(rel.schema().names), tuple(f["kinds"]), tuple(f["nullable"]),
+           repr(sorted(f["opts"].items())), f["strict"], head)
+    cp = _CACHE.get(key)
+    if cp is None and key not in _CACHE:
+        base = _ScanBase(rel.schema(), 0, f["device"])
+        g = _scan_gen(base, f["nullable"])
+        try:
+            _, g, outputs, _ = dqvm.compile_chain(nodes, base, False, gen=g)
+            slots = {k: g.slot(None, (k,)) for k in _ScanPlan.SCAN_SLOTS}
+            src = kernel_source(g, f["kinds"], f["nullable"], g.used, f["opts"], f["strict"], head, slots)
+            cp = _ScanPlan(src, g, outputs, refs)
+        except dqvm.Unfusable as e:
+            cp = "vector" if str(e) == "VectorAssembleExpr" else None
+        if len(_CACHE) >= 64:
+            _CACHE.clear()
+        _CACHE[key] = cp
+    if cp is None or cp == "vector":
+        return cp
+    h = native.hip()
+    dev = f["device"]
+    buf, n, nalloc = f["buf"], int(f["n"]), int(f["nlines"])
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    nb = int(h.csv_count_blocks(n))
+    offs = torch.empty(nb + 1, dtype=torch.int64, device=dev)
+    h.csv_line_ends(buf.data_ptr(), n, offs.data_ptr(), 0, stream)  # per-window counts -> offsets
+    err = torch.zeros(1, dtype=torch.int32, device=dev)
+    vflag = torch.zeros(1, dtype=torch.int32, device=dev)
+    ptr_list, outs, sel_out = cp.bind(nalloc, dev, {"buf": buf, "offs": offs, "nalloc": nalloc,
+                                                    "trailing": int(f["trailing"]), "vflag": vflag}, err)
+    handle, _log = h.rtc_compile(cp.src, ENTRY)
+    ptrs = _h2d(np.asarray(ptr_list, dtype=np.int64), dev)
+    from ..utils import tracing
+
+    with tracing.span("csv_scan_dq_fused"):
+        h.rtc_launch(int(handle), nb, 256, ptrs.data_ptr(), n, stream)
+    tracing.add_rows("csv_scan_dq_fused", nalloc)
+    STATS["fused_scans"] += 1
+    if cp.has_raise and int(err.item()) != 0:
+        from ..sql.expressions import SparkException
+
+        msg = "Failed to execute user defined function"
+        for nd in nodes:
+            for ex in getattr(nd, "exprs", []) + ([nd.cond] if hasattr(nd, "cond") else []):
+                r = dqvm._find_raise(ex)
+                if r is not None:
+                    msg = r.message
+        raise SparkException(msg)
+    # safety net: the earlier scan's facts (types, null-free columns, line count) are re-verified
+    # by the kernel; a disagreement surfaces with the first host read of any output
+    check = defer(vflag, lambda: RuntimeError(
+        f"fused CSV scan of {rel.label}: the input no longer matches the schema / line facts of its "
+        f"earlier device scan"))
+    schema = plan.schema()
+    cols = [ColumnData(fd.dataType, oo[0], oo[1], dict(fd.metadata), [check] if check is not None else [])
+            for fd, oo in zip(schema.fields, outs)]
+    keep = (offs, ptrs, buf)  # noqa: F841 (stream-ordered lifetimes: the caching allocator handles it)
+    return Table(schema, cols, nalloc, sel_out, dev)

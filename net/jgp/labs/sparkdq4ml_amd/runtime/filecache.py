@@ -51,6 +51,7 @@ class PinnedFile:
         self.nbytes = nbytes = hi - lo
         self._dev = {}  # (device, lo, hi) -> uint8 device tensor
         self.type_hints = {}  # (lo, hi, sep) -> column type codes of the last device scan
+        self.scan_facts = {}  # (lo, hi, sep, opts, user types) -> types / nulls / line count (ops/scanfuse)
         self.host = torch.empty(nbytes, dtype=torch.uint8).pin_memory()
         self.data = self.host.numpy()
         fd = os.open(path, os.O_RDONLY)

@@ -17,7 +17,7 @@ from .expressions import (Alias, AnalysisException, ColRef, EvalContext, Expr, U
 from .table import ColumnData, Table
 from .types import BooleanType, StructField, StructType
 
-__all__ = ["LogicalPlan", "LocalRelation", "Project", "Filter", "Limit", "Union", "execute", "prune_columns"]
+__all__ = ["LogicalPlan", "LocalRelation", "CsvScanRelation", "Project", "Filter", "Limit", "Union", "execute", "prune_columns"]
 
 
 class LogicalPlan:
@@ -64,6 +64,40 @@ class LocalRelation(LogicalPlan):
 
     def _label(self):
         return f"{self.label} [{', '.join(self.table.schema.names)}]"
+
+
+class CsvScanRelation(LocalRelation):
+    """A device CSV relation scanned lazily, at its first action (Spark also reads the file at
+    every action).  Created only when an earlier device scan of the same cached
+    bytes already fixed its schema, null columns and line count (``fused``: those facts plus the
+    HBM-resident bytes): a Project/Filter chain directly on top then runs fused INTO the scan
+    (``ops/scanfuse.py``); any other consumer gets the plain device scan (``scan()``)."""
+
+    def __init__(self, schema: StructType, scan, fused: Optional[dict], label: str = "CsvScan",
+                 sharded: Optional[bool] = None):
+        from ..parallel import comm
+
+        self._schema = schema
+        self._scan = scan
+        self.fused = fused
+        self.label = label
+        self.sharded = comm.world_size() > 1 if sharded is None else bool(sharded)
+        self._memo = None
+
+    @property
+    def table(self) -> Table:
+        if self._memo is None:
+            self._memo = self._scan()
+        return self._memo
+
+    def schema(self):
+        return self._schema
+
+    def _compute(self, session):
+        return self._scan()
+
+    def _label(self):
+        return f"{self.label} [{', '.join(self._schema.names)}]"
 
 
 def is_sharded(plan) -> bool:

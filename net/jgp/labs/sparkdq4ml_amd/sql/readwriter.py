@@ -171,6 +171,9 @@ class DataFrameReader:
         files = _expand(paths)
         if self._format == "csv":
             table = self._read_csv(files)
+            if not isinstance(table, Table):  # a lazily scanned relation (sql.plan.CsvScanRelation)
+                table.label = f"Relation[csv] {','.join(paths)}"
+                return DataFrame(table, self._session)
         elif self._format == "parquet":
             table = self._read_parquet(files)
         elif self._format == "json":
@@ -194,7 +197,7 @@ class DataFrameReader:
         return self.load(path, format="json")
 
     # ---- csv -------------------------------------------------------------------------------
-    def _read_csv(self, files: List[str]) -> Table:
+    def _read_csv(self, files: List[str]):
         """CSV -> columnar table.  In a multi-process group (``dq4ml.shardInput``, default on) each
         rank parses only its byte range, moved to row boundaries (Hadoop split semantics), and the
         inferred schema is merged across ranks (tightest common type; names from rank 0, whose
@@ -229,7 +232,9 @@ class DataFrameReader:
             data = b"".join(self._read_bytes(f) for f in files)
         return self._read_csv_data(data, o, dev, thresh, pinned, pf, presharded)
 
-    def _read_csv_data(self, data, o, dev, thresh, pinned=None, pf=None, presharded=False) -> Table:
+    def _read_csv_data(self, data, o, dev, thresh, pinned=None, pf=None, presharded=False):
+        """A Table, or a lazily scanned ``CsvScanRelation`` for bytes already typed by an earlier
+        device scan."""
         from ..parallel import comm
 
         header = _truthy(o.get("header", "false"))
@@ -266,6 +271,7 @@ class DataFrameReader:
             use_dev = all(comm.all_gather_object(bool(use_dev and len(data) >= thresh)))
         elif use_dev:
             use_dev = len(data) >= thresh
+        dev_scan = None
         if use_dev:
             from ..ops import csvscan
 
@@ -279,25 +285,72 @@ class DataFrameReader:
             if pf is not None and _truthy(self._session.conf.get("dq4ml.csv.deviceCache", "true")):
                 from ..runtime import filecache
 
-                if filecache.device_bytes_allowed(hi - lo):
+                if filecache.device_bytes_allowed(hi - lo) or (str(dev), lo, hi) in pf._dev:
                     dbytes = pf.device_bytes(dev, lo, hi)  # HBM-resident input bytes
                     dbytes = dbytes[off:] if off else dbytes
             hkey = (lo + off, hi, sep, repr(sorted(dopts.items())))
+            fkey = hkey + (tuple(strict) if strict else None,)
             ncols = len(strict) if strict else (len(names) if names else None)
-            with tracing.span("csv_scan"):
-                t = csvscan.scan_device(body, sep=sep, infer=infer, device=dev, sharded=shard, ncols=ncols,
-                                        chunk_bytes=int(self._session.conf.get("dq4ml.chunkBytes", str(256 << 20))),
-                                        pinned=None if pinned is None else pinned[off:], device_data=dbytes,
-                                        types_hint=(pf.type_hints.get(hkey) if pf is not None and not strict
-                                                    else None), opts=dopts, user_types=strict)
-            if t is not None:
-                if pf is not None and not strict:  # the next action's scan stores typed columns directly
-                    pf.type_hints[hkey] = [csvscan.type_code_of(f.dataType) for f in t.schema.fields]
-                final = user_names if strict else names
+            final = user_names if strict else names
+
+            def dev_scan():
+                with tracing.span("csv_scan"):
+                    t = csvscan.scan_device(body, sep=sep, infer=infer, device=dev, sharded=shard, ncols=ncols,
+                                            chunk_bytes=int(self._session.conf.get("dq4ml.chunkBytes", str(256 << 20))),
+                                            pinned=None if pinned is None else pinned[off:], device_data=dbytes,
+                                            types_hint=(pf.type_hints.get(hkey) if pf is not None and not strict
+                                                        else None), opts=dopts, user_types=strict)
+                if t is None:
+                    return None
+                codes = [csvscan.type_code_of(f.dataType) for f in t.schema.fields]
+                if pf is not None:
+                    if not strict:  # the next action's scan stores typed columns directly
+                        pf.type_hints[hkey] = codes
+                    facts = getattr(t, "scan_facts", None)
+                    if facts is not None and dbytes is not None:
+                        pf.scan_facts[fkey] = dict(facts, types=codes, nbytes=len(body))
                 if final:
                     fields = [StructField(nm, f.dataType, True) for nm, f in zip(final, t.schema.fields)]
                     t = Table(StructType(fields), t.columns, t.nrows, t.sel, t.device)
                 return t
+
+            # a re-read of bytes an earlier device scan already typed: lazy relation, scanned at
+            # the action — fused with the DQ chain on top of it when there is one (ops/scanfuse.py)
+            facts = pf.scan_facts.get(fkey) if (pf is not None and dbytes is not None) else None
+            lazy = (facts is not None and len(body) == facts["nbytes"]
+                    and _truthy(self._session.conf.get("dq4ml.csv.fuseScan", "true"))
+                    and len(facts["types"]) <= 64 and facts["nlines"] > 0
+                    and len(body) / facts["nlines"] <= 64)
+            if shard:  # every rank takes the same (collective) path
+                lazy = all(comm.all_gather_object(bool(lazy)))
+            if lazy:
+                from ..ops.csvscan import _KIND, _opt_args
+                from ..sql.plan import CsvScanRelation
+
+                codes = facts["types"]
+                fnames = final or [f"_c{i}" for i in range(len(codes))]
+                schema = StructType([StructField(nm, csv_code_to_type(c), True) for nm, c in zip(fnames, codes)])
+                n = len(body)
+                fused = {"buf": dbytes, "n": n, "nlines": facts["nlines"], "device": dev,
+                         "trailing": n > 0 and body[-1] not in (10, 13), "mean_line": n / facts["nlines"],
+                         "kinds": [_KIND.get(c, (0,))[0] for c in codes], "nullable": list(facts["nullable"]),
+                         "opts": dict(_opt_args(dopts), sep=sep, strict=bool(strict)), "strict": bool(strict)}
+                if fused["opts"]["null_value"] and len(fused["opts"]["null_value"].encode()) > 16:
+                    fused = None
+
+                def scan_or_host():
+                    t = dev_scan()
+                    return t if t is not None else self._host_table(data, header, infer, user_types, user_names,
+                                                                   sep, dev, shard)
+                return CsvScanRelation(schema, scan_or_host, fused, "Relation[csv]")
+            t = dev_scan()
+            if t is not None:
+                return t
+        return self._host_table(data, header, infer, user_types, user_names, sep, dev, shard)
+
+    def _host_table(self, data, header, infer, user_types, user_names, sep, dev, shard) -> Table:
+        from ..parallel import comm
+
         if not isinstance(data, bytes):
             data = bytes(data)  # host scanner path (small or fallback): a plain copy
         with tracing.span("csv_scan"):

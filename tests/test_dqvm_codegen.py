@@ -52,3 +52,55 @@ def test_codegen_compiles(cpu_session, tmp_path):
         r = subprocess.run([hipcc, "--offload-arch=gfx950", "-O3", "-c", str(f), "-o", str(tmp_path / f"k{i}.o")],
                            capture_output=True, text=True)
         assert r.returncode == 0, r.stderr + "\n" + code
+
+
+def test_scan_fused_codegen_compiles(cpu_session, tmp_path):
+    """The fused scan + DQ kernel (ops/scanfuse.py) of the lab chain over a CSV relation whose
+    facts say: int guest, double price, no nulls — compiles for gfx950, stores only the pruned
+    outputs (guest, label) and the selection, and carries no null checks."""
+    import torch
+
+    from net.jgp.labs.sparkdq4ml_amd import VectorAssembler
+    from net.jgp.labs.sparkdq4ml_amd.ops import scanfuse
+    from net.jgp.labs.sparkdq4ml_amd.ops.csvscan import _opt_args
+    from net.jgp.labs.sparkdq4ml_amd.sql.dataframe import DataFrame
+    from net.jgp.labs.sparkdq4ml_amd.sql.plan import CsvScanRelation, prune_columns
+    from net.jgp.labs.sparkdq4ml_amd.sql.types import DoubleType, IntegerType, StructField, StructType
+
+    spark = cpu_session
+    register_lab_rules(spark)
+    schema = StructType([StructField("_c0", IntegerType(), True), StructField("_c1", DoubleType(), True)])
+    fused = {"kinds": [1, 0], "nullable": [False, False], "strict": False,
+             "opts": dict(_opt_args({"comment": 0}), sep=",", strict=False)}
+    rel = CsvScanRelation(schema, lambda: None, fused, "Relation[csv]")
+    df = DataFrame(rel, spark).withColumnRenamed("_c0", "guest").withColumnRenamed("_c1", "price")
+    df = df.withColumn("price_no_min", callUDF("minimumPriceRule", df.col("price")))
+    df.createOrReplaceTempView("price")
+    df = spark.sql("SELECT cast(guest as int) guest, price_no_min AS price FROM price WHERE price_no_min > 0")
+    df = df.withColumn("price_correct_correl", callUDF("priceCorrelationRule", df.col("price"), df.col("guest")))
+    df.createOrReplaceTempView("price")
+    df = spark.sql("SELECT guest, price_correct_correl AS price FROM price WHERE price_correct_correl > 0")
+    df = df.withColumn("label", df.col("price"))
+    df = VectorAssembler().setInputCols(["guest"]).setOutputCol("features").transform(df)
+    plan = prune_columns(df._plan, {"label", "features"}).child  # the DQ chain below the assembler
+    nodes, p = [], plan
+    while isinstance(p, (Project, Filter)):
+        nodes.append(p)
+        p = p.child
+    nodes.reverse()
+    assert p is rel
+    base = scanfuse._ScanBase(rel.schema(), 0, torch.device("cpu"))
+    g = scanfuse._scan_gen(base, fused["nullable"])
+    _, g, outputs, _ = dqvm.compile_chain(nodes, base, False, gen=g)
+    slots = {k: g.slot(None, (k,)) for k in scanfuse._ScanPlan.SCAN_SLOTS}
+    src = scanfuse.kernel_source(g, fused["kinds"], fused["nullable"], g.used, fused["opts"], False, 256, slots)
+    assert [t for t in g.recipe if t[0] in ("out", "outvalid", "selout")] == [("out", 0), ("out", 1), ("selout",)]
+    assert "atomicOr((int*)" not in src  # no RaiseIfNull: price is null-free
+    hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+    if not os.path.exists(hipcc):
+        pytest.skip("no hipcc")
+    f = tmp_path / "scan.hip"
+    f.write_text("#include <hip/hip_runtime.h>\n" + src)
+    r = subprocess.run([hipcc, "--offload-arch=gfx950", "-O3", "-std=c++17", "-c", str(f), "-o", str(tmp_path / "scan.o")],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr

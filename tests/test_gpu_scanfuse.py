@@ -1,0 +1,161 @@
+"""Fused CSV scan + DQ chain (ops/scanfuse.py): the first read of a file is the eager device scan
+(it records the file's schema / null / line facts), a re-read is a lazy relation whose DQ chain
+runs fused into the scan.  Both must give the same rows, the same fit and the same errors; the
+second read must actually take the fused kernel."""
+import os
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "benchmarks"))
+
+from net.jgp.labs.sparkdq4ml_amd import LinearRegression, SparkSession, VectorAssembler, callUDF  # noqa: E402
+from net.jgp.labs.sparkdq4ml_amd.dq.rules import register_lab_rules  # noqa: E402
+from net.jgp.labs.sparkdq4ml_amd.ops import scanfuse  # noqa: E402
+from net.jgp.labs.sparkdq4ml_amd.runtime import filecache  # noqa: E402
+from net.jgp.labs.sparkdq4ml_amd.sql.plan import CsvScanRelation  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+
+def _session():
+    s = SparkSession.getActiveSession()
+    if s is not None:
+        s.stop()
+    filecache.clear()
+    spark = SparkSession.builder().master("mi355x[*]").config("dq4ml.csv.deviceThresholdBytes", "0").getOrCreate()
+    register_lab_rules(spark)
+    return spark
+
+
+def _chain(spark, path, opts=None):
+    r = spark.read().format("csv").option("inferSchema", "true")
+    for k, v in (opts or {}).items():
+        r = r.option(k, v)
+    raw = r.load(path)
+    df = raw.withColumnRenamed("_c0", "guest").withColumnRenamed("_c1", "price")
+    df = df.withColumn("price_no_min", callUDF("minimumPriceRule", df.col("price")))
+    df.createOrReplaceTempView("price")
+    df = spark.sql("SELECT cast(guest as int) guest, price_no_min AS price FROM price WHERE price_no_min > 0")
+    df = df.withColumn("price_correct_correl", callUDF("priceCorrelationRule", df.col("price"), df.col("guest")))
+    df.createOrReplaceTempView("price")
+    df = spark.sql("SELECT guest, price_correct_correl AS price FROM price WHERE price_correct_correl > 0")
+    return raw, df.withColumn("label", df.col("price"))
+
+
+def _rows(df):
+    return [tuple(r) for r in df.collect()]
+
+
+def _lab_csv(rng, n, term=b"\r", trailing=False, empty=0.0, long_comment=False):
+    g = rng.integers(1, 36, n)
+    price = np.round(5.0 * g + 20 + rng.normal(0, 3, n), 2)
+    low = rng.random(n) < 0.05
+    price[low] = rng.integers(3, 19, int(low.sum()))
+    hi = (rng.random(n) < 0.05) & (g < 14)
+    price[hi] = rng.integers(91, 199, int(hi.sum()))
+    lines = []
+    for i in range(n):
+        if empty and rng.random() < empty:
+            lines.append(b"")
+        if long_comment and i % 997 == 5:
+            lines.append(b"#" + b"x" * int(rng.integers(300, 5000)))
+        lines.append(b"%d,%s" % (g[i], repr(float(price[i])).encode()))
+    body = term.join(lines)
+    return body + (term if trailing else b"")
+
+
+@pytest.mark.parametrize("case", ["cr", "lf_trailing", "crlf_empty", "long_comment"])
+def test_fused_scan_matches_eager(tmp_path, case):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    rng = np.random.default_rng(len(case))
+    term = {"cr": b"\r", "lf_trailing": b"\n", "crlf_empty": b"\r\n", "long_comment": b"\n"}[case]
+    data = _lab_csv(rng, 60000, term, trailing=case == "lf_trailing", empty=0.01 if case == "crlf_empty" else 0.0,
+                    long_comment=case == "long_comment")
+    p = tmp_path / f"{case}.csv"
+    p.write_bytes(data)
+    opts = {"comment": "#"} if case == "long_comment" else None
+    spark = _session()
+    raw1, df1 = _chain(spark, str(p), opts)
+    assert not isinstance(raw1._plan, CsvScanRelation)  # first read: eager scan, facts recorded
+    eager = _rows(df1)
+    before = scanfuse.STATS["fused_scans"]
+    raw2, df2 = _chain(spark, str(p), opts)
+    assert isinstance(raw2._plan, CsvScanRelation)
+    assert raw2.schema == raw1.schema
+    fused = _rows(df2)
+    assert scanfuse.STATS["fused_scans"] == before + 1, "the re-read did not take the fused scan kernel"
+    assert len(fused) == len(eager) > 40000
+    assert fused == eager
+    # any other consumer of the lazy relation: the plain device scan, same rows
+    raw3, _ = _chain(spark, str(p), opts)
+    assert raw3.count() == raw1.count()
+    spark.stop()
+
+
+def test_fused_scan_fit_matches_eager(tmp_path):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from bench_csv_pipeline import synth_csv
+
+    p = str(tmp_path / "lab.csv")
+    synth_csv(p, 300000)
+    spark = _session()
+
+    def fit():
+        _, df = _chain(spark, p)
+        df = VectorAssembler().setInputCols(["guest"]).setOutputCol("features").transform(df)
+        m = LinearRegression().setMaxIter(40).setRegParam(1).setElasticNetParam(1).fit(df)
+        return m, df
+
+    m1, _ = fit()
+    before = scanfuse.STATS["fused_scans"]
+    m2, df2 = fit()
+    assert scanfuse.STATS["fused_scans"] == before + 1
+    assert m2.summary.numInstances == m1.summary.numInstances
+    assert float(m2.intercept) == pytest.approx(float(m1.intercept), rel=1e-12, abs=1e-12)
+    np.testing.assert_allclose(m2.coefficients.toArray(), m1.coefficients.toArray(), rtol=1e-12)
+    # async: the fused action issues no host sync before the fit result is read
+    spark.conf.set("dq4ml.fit.async", "true")
+    torch.cuda.synchronize()
+    torch.cuda.set_sync_debug_mode("error")
+    try:
+        _, df = _chain(spark, p)
+        df = VectorAssembler().setInputCols(["guest"]).setOutputCol("features").transform(df)
+        m3 = LinearRegression().setMaxIter(40).setRegParam(1).setElasticNetParam(1).fit(df)
+    finally:
+        torch.cuda.set_sync_debug_mode(0)
+    np.testing.assert_allclose(m3.coefficients.toArray(), m1.coefficients.toArray(), rtol=1e-12)
+    spark.stop()
+
+
+def test_fused_scan_nulls_and_raise(tmp_path):
+    """A null price: rule 1 raises (Java NPE) on the fused path exactly as on the eager one; null
+    guests flow through rule 2 (-> -1, filtered)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    rng = np.random.default_rng(3)
+    lines = _lab_csv(rng, 30000, b"\n").split(b"\n")
+    lines[100] = b"," + lines[100].split(b",")[1]  # null guest
+    p = tmp_path / "nullguest.csv"
+    p.write_bytes(b"\n".join(lines))
+    spark = _session()
+    _, d1 = _chain(spark, str(p))
+    eager = _rows(d1)
+    before = scanfuse.STATS["fused_scans"]
+    _, d2 = _chain(spark, str(p))
+    assert _rows(d2) == eager
+    assert scanfuse.STATS["fused_scans"] == before + 1
+    lines[200] = lines[200].split(b",")[0] + b","  # null price: minimumPriceRule throws
+    p2 = tmp_path / "nullprice.csv"
+    p2.write_bytes(b"\n".join(lines))
+    from net.jgp.labs.sparkdq4ml_amd.sql.expressions import SparkException
+
+    for _ in range(2):  # eager, then fused
+        _, d = _chain(spark, str(p2))
+        with pytest.raises(SparkException):
+            _rows(d)
+    spark.stop()
