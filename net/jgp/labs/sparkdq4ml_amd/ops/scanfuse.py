@@ -60,8 +60,10 @@ def head_bytes(mean_line: float) -> int:
 
 
 def _wpe() -> str:
-    """Occupancy hint (``DQ4ML_SCAN_WPE`` waves per SIMD; default: the compiler's choice)."""
-    w = int(os.environ.get("DQ4ML_SCAN_WPE", "0"))
+    """Occupancy hint (``DQ4ML_SCAN_WPE`` waves per SIMD; 0: the compiler's choice).  Default 8:
+    the byte walks are latency-bound, and 8 waves with a few spilled VGPRs beat 4 waves without
+    (lab CSV pipeline 2.16 / 1.94 / 1.91 ms per step at 4 / 6 / 8 waves, one run)."""
+    w = int(os.environ.get("DQ4ML_SCAN_WPE", "8"))
     return f"__attribute__((amdgpu_waves_per_eu({w}))) " if w > 0 else ""
 
 

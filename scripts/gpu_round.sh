@@ -60,6 +60,13 @@ for s in $STEPS; do
     benchring2f64) step benchring2f64 600 env DQ4ML_GRAM_STREAM_RING=2 python bench.py --steps 10 --warmup 2 --dtype fp64 ;;
     benchring2cols) step benchring2cols 600 env DQ4ML_GRAM_STREAM_RING=2 python bench.py --steps 10 --warmup 2 --dtype bf16 --storage f32cols ;;
     kprofcols) (export TMPDIR=/tmp; step kprofcols 600 rocprofv3 --kernel-trace --stats -d gpurun_out/kprofcols -o run --output-format csv -- python bench.py --steps 5 --warmup 1 --storage f32cols) || exit $? ;;
+    kprofcsv) (export TMPDIR=/tmp; step kprofcsv 600 rocprofv3 --kernel-trace --stats -d gpurun_out/kprofcsv -o run --output-format csv -- python benchmarks/bench_csv_pipeline.py --steps 5 --warmup 2) || exit $? ;;
+    csvwpe6) step csvwpe6 600 env DQ4ML_SCAN_WPE=6 python benchmarks/bench_csv_pipeline.py --steps 20 --warmup 3 ;;
+    csvwpe8) step csvwpe8 600 env DQ4ML_SCAN_WPE=8 python benchmarks/bench_csv_pipeline.py --steps 20 --warmup 3 ;;
+    csvpmc) (export TMPDIR=/tmp
+       step csvpmc1 300 timeout -s KILL 240 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_SALU GRBM_GUI_ACTIVE -d gpurun_out/csvpmc1 -o run --output-format csv -- python benchmarks/bench_csv_pipeline.py --steps 2 --warmup 1 --rows 2e7 &&
+       step csvpmc2 300 timeout -s KILL 240 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d gpurun_out/csvpmc2 -o run --output-format csv -- python benchmarks/bench_csv_pipeline.py --steps 2 --warmup 1 --rows 2e7 &&
+       step csvpmc3 300 timeout -s KILL 240 rocprofv3 --kernel-trace --pmc WRITE_SIZE TCC_HIT_sum -d gpurun_out/csvpmc3 -o run --output-format csv -- python benchmarks/bench_csv_pipeline.py --steps 2 --warmup 1 --rows 2e7) || exit $? ;;
     prof) cd /tmp && export TMPDIR=/tmp && cd - >/dev/null; step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 5 --warmup 1 ;;
   esac
 done
