@@ -37,12 +37,16 @@ void pack_wide(int eb, const PackSrcW* srcs_dev, int d, int64_t n, int nt, const
 // zero the rows with sel[r] == 0 (and rows >= n) of a wide tiled matrix: in -> out (may alias)
 void wide_mask_rows(int eb, const void* in, void* out, int d, int64_t n, const uint8_t* sel, hipStream_t st);
 // out: flat WLS layout [count, wSum, wwSum, bSum, bbSum, aSum(d), abSum(d), aa packed-upper(d)]
+// fold = false: partial tiles only (the caller folds them band by band with gram_wide_fold)
 void gram_wide(int eb, WideArgs a, const int* pairs_dev, const float* scales, double* out, hipStream_t st,
-               int ring = 4, int waves = 4);
+               int ring = 4, int waves = 4, bool fold = true);
 // persistent XCD-grouped schedule: grid blocks (one per CU, a multiple of 8), group b % 8 owns
 // splits [g*h, g*h+h) (a.splitk == 8*h) and dequeues (split, pair) units from heads[g] (8 ints,
 // zeroed here on the stream)
 void gram_wide_queue(int eb, WideArgs a, const int* pairs_dev, const float* scales, double* out, int* heads, int h,
-                     int grid, hipStream_t st, int waves = 8);
+                     int grid, hipStream_t st, int waves = 8, bool fold = true);
+// fold the pairs of panel columns [J0, J1) (J = npanels: the augmentation column -> the head of
+// the flat layout) into out (f64) or out32 (f32 wire buffer, same flat indexing)
+void gram_wide_fold(WideArgs a, const float* scales, double* out, float* out32, int J0, int J1, hipStream_t st);
 
 }  // namespace dq4ml

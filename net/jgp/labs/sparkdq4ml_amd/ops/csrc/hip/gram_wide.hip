@@ -343,19 +343,31 @@ __global__ __launch_bounds__(64 * WAVES, 1) void gram_wide_queue_kernel(WideArgs
 // slabs of consecutive threads are consecutive floats, so every read is coalesced) and scatters
 // the f64 sums into the flat WLS layout.  Augmentation columns [1, y_hi, y_lo] fold into
 // aSum / abSum / the five scalars.
+//
+// Banded form (data-parallel fits, X1): only the pairs of panel COLUMNS [J0, J1) — a contiguous
+// range of the packed-upper layout (J = npanels: the head [count .. abSum]) — and, with out32, the
+// values go to an f32 wire buffer (same flat indexing) that the bucketed RCCL all-reduce of that
+// band ships while the next band folds.
+__device__ __forceinline__ void wide_store(double* __restrict__ out, float* __restrict__ out32, int64_t idx, double v) {
+  if (out32) out32[idx] = (float)v;
+  else out[idx] = v;
+}
+
 __global__ __launch_bounds__(256) void gram_wide_reduce_kernel(WideArgs a, const float* __restrict__ scales,
-                                                              double* __restrict__ out) {
+                                                              double* __restrict__ out, float* __restrict__ out32,
+                                                              int J0, int J1) {
   const int d = a.d, P = a.npanels;
-  const int npair = (P + 1) * (P + 2) / 2;
-  const int64_t tot = (int64_t)npair * kPanel * kPanel;
+  int64_t npb = 0;  // pairs of the band's panel columns: column J holds pairs I = 0..J
+  for (int J = J0; J < J1; ++J) npb += J + 1;
+  const int64_t tot = npb * kPanel * kPanel;
   const double s1 = a.aug_scale[0], syh = a.aug_scale[1], syl = a.aug_scale[2];
   const int64_t slab = (int64_t)kPanel * kPanel;
   for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < tot; g += (int64_t)gridDim.x * blockDim.x) {
-    const int pr = (int)(g / slab);
-    const int e = (int)(g - (int64_t)pr * slab), r = e >> 8, c = e & (kPanel - 1);
-    int I = 0, rem = pr;  // row-major pair index -> (I, J)
-    while (rem >= P + 1 - I) { rem -= P + 1 - I; ++I; }
-    const int J = I + rem;
+    const int q = (int)(g / slab);
+    const int e = (int)(g - (int64_t)q * slab), r = e >> 8, c = e & (kPanel - 1);
+    int J = J0, I = q;  // band-local pair index (column-major) -> (I, J)
+    while (I >= J + 1) { I -= J + 1; ++J; }
+    const int pr = I * (P + 1) - I * (I - 1) / 2 + (J - I);  // row-major storage index of (I, J)
     const float* base = a.part + (int64_t)pr * a.splitk * slab + e;
     auto sum = [&](int off) {
       double v = 0.0;
@@ -367,24 +379,24 @@ __global__ __launch_bounds__(256) void gram_wide_reduce_kernel(WideArgs a, const
       const int j = J * kPanel + c;
       if (i < d && j < d && i <= j) {
         const double sc = scales ? (double)scales[i] * (double)scales[j] : 1.0;
-        out[5 + 2 * (int64_t)d + i + (int64_t)j * (j + 1) / 2] = sum(0) * sc;
+        wide_store(out, out32, 5 + 2 * (int64_t)d + i + (int64_t)j * (j + 1) / 2, sum(0) * sc);
       }
     } else if (I < P) {  // (X panel, augmentation): column 0 -> aSum, columns 1 + 2 -> abSum
       if (i < d && c < 2) {
         const double si = scales ? (double)scales[i] : 1.0;
-        if (c == 0) out[5 + i] = sum(0) * si * s1;
-        else out[5 + d + i] = (sum(0) * syh + sum(1) * syl) * si;
+        if (c == 0) wide_store(out, out32, 5 + i, sum(0) * si * s1);
+        else wide_store(out, out32, 5 + d + i, (sum(0) * syh + sum(1) * syl) * si);
       }
     } else if (r == 0 && c == 0) {  // (augmentation, augmentation): the five scalars
       const double g11 = sum(0) * s1 * s1;
       const double g1h = sum(1) * s1 * syh, g1l = sum(2) * s1 * syl;
       const double ghh = sum(kPanel + 1) * syh * syh, ghl = sum(kPanel + 2) * syh * syl;
       const double gll = sum(2 * kPanel + 2) * syl * syl;
-      out[0] = g11;  // count, wSum, wwSum (unit weights; dead rows are zero)
-      out[1] = g11;
-      out[2] = g11;
-      out[3] = g1h + g1l;                // Σy
-      out[4] = ghh + 2.0 * ghl + gll;    // Σy²
+      wide_store(out, out32, 0, g11);  // count, wSum, wwSum (unit weights; dead rows are zero)
+      wide_store(out, out32, 1, g11);
+      wide_store(out, out32, 2, g11);
+      wide_store(out, out32, 3, g1h + g1l);              // Σy
+      wide_store(out, out32, 4, ghh + 2.0 * ghl + gll);  // Σy²
     }
   }
 }
@@ -579,8 +591,24 @@ static void launch_wide_queue(const WideArgs& a, int grid, int* heads, int h, hi
   DQ_HIP_CHECK(hipGetLastError());
 }
 
+static void launch_fold(const WideArgs& a, const float* scales, double* out, float* out32, int J0, int J1,
+                        hipStream_t st) {
+  int64_t npb = 0;
+  for (int J = J0; J < J1; ++J) npb += J + 1;
+  int64_t g = (npb * kPanel * kPanel + 255) / 256;
+  if (g > 16384) g = 16384;
+  hipLaunchKernelGGL(gram_wide_reduce_kernel, dim3(g), dim3(256), 0, st, a, scales, out, out32, J0, J1);
+  DQ_HIP_CHECK(hipGetLastError());
+}
+
+void gram_wide_fold(WideArgs a, const float* scales, double* out, float* out32, int J0, int J1, hipStream_t st) {
+  if (J0 < 0 || J1 > a.npanels + 1 || J0 >= J1) throw std::invalid_argument("gram_wide_fold: bad panel-column band");
+  if ((out == nullptr) == (out32 == nullptr)) throw std::invalid_argument("gram_wide_fold: exactly one output");
+  launch_fold(a, scales, out, out32, J0, J1, st);
+}
+
 void gram_wide_queue(int eb, WideArgs a, const int* pairs_dev, const float* scales, double* out, int* heads, int h,
-                     int grid, hipStream_t st, int waves) {
+                     int grid, hipStream_t st, int waves, bool fold) {
   a.pairs = pairs_dev;
   if (a.splitk != 8 * h) throw std::invalid_argument("gram_wide_queue: splitk must be 8 * h");
   if (grid < 8 || grid % 8) throw std::invalid_argument("gram_wide_queue: grid must be a positive multiple of 8");
@@ -588,15 +616,11 @@ void gram_wide_queue(int eb, WideArgs a, const int* pairs_dev, const float* scal
   DQ_HIP_CHECK(hipMemsetAsync(heads, 0, 8 * sizeof(int), st));
   if (eb == 16) waves == 8 ? launch_wide_queue<16, 4, 8>(a, grid, heads, h, st) : launch_wide_queue<16, 4, 4>(a, grid, heads, h, st);
   else waves == 8 ? launch_wide_queue<8, 4, 8>(a, grid, heads, h, st) : launch_wide_queue<8, 4, 4>(a, grid, heads, h, st);
-  const int P = a.npanels;
-  int64_t g = ((int64_t)(P + 1) * (P + 2) / 2 * kPanel * kPanel + 255) / 256;
-  if (g > 16384) g = 16384;
-  hipLaunchKernelGGL(gram_wide_reduce_kernel, dim3(g), dim3(256), 0, st, a, scales, out);
-  DQ_HIP_CHECK(hipGetLastError());
+  if (fold) launch_fold(a, scales, out, nullptr, 0, a.npanels + 1, st);
 }
 
 void gram_wide(int eb, WideArgs a, const int* pairs_dev, const float* scales, double* out, hipStream_t st, int ring,
-               int waves) {
+               int waves, bool fold) {
   a.pairs = pairs_dev;
   const int P = a.npanels;
   const int npair = (P + 1) * (P + 2) / 2;
@@ -606,10 +630,7 @@ void gram_wide(int eb, WideArgs a, const int* pairs_dev, const float* scales, do
     throw std::invalid_argument("gram_wide: waves must be 4 or 8");
   if (eb == 16) launch_wide_eb<16>(a, nb, st, ring, waves);
   else launch_wide_eb<8>(a, nb, st, ring, waves);
-  int64_t g = ((int64_t)npair * kPanel * kPanel + 255) / 256;
-  if (g > 16384) g = 16384;
-  hipLaunchKernelGGL(gram_wide_reduce_kernel, dim3(g), dim3(256), 0, st, a, scales, out);
-  DQ_HIP_CHECK(hipGetLastError());
+  if (fold) launch_fold(a, scales, out, nullptr, 0, P + 1, st);
 }
 
 }  // namespace dq4ml

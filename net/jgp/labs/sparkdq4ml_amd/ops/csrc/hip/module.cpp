@@ -146,9 +146,8 @@ PYBIND11_MODULE(_dq4ml_hip, m) {
   m.def("feature_amax", [](uintptr_t srcs_dev, int d, int64_t n, uintptr_t sel, uintptr_t amax, uintptr_t stream) {
     feature_amax(P<const PackSrcW>(srcs_dev), d, n, P<const uint8_t>(sel), P<float>(amax), as_stream(stream));
   });
-  m.def("gram_wide", [](int eb, uintptr_t X, uintptr_t Xaug, uintptr_t zeros, int nt, int npanels, int d,
-                        int64_t nsup, int splitk, uintptr_t pairs, uintptr_t part, double s1, double syh, double syl,
-                        uintptr_t scales, uintptr_t out, uintptr_t stream, int ring, int waves) {
+  auto wide_args = [](uintptr_t X, uintptr_t Xaug, uintptr_t zeros, int nt, int npanels, int d, int64_t nsup,
+                      int splitk, uintptr_t part, double s1, double syh, double syl) {
     WideArgs a{};
     a.X = P<const unsigned char>(X);
     a.Xaug = P<const unsigned char>(Xaug);
@@ -162,26 +161,28 @@ PYBIND11_MODULE(_dq4ml_hip, m) {
     a.aug_scale[0] = s1;
     a.aug_scale[1] = syh;
     a.aug_scale[2] = syl;
-    gram_wide(eb, a, P<const int>(pairs), P<const float>(scales), P<double>(out), as_stream(stream), ring, waves);
+    return a;
+  };
+  m.def("gram_wide", [wide_args](int eb, uintptr_t X, uintptr_t Xaug, uintptr_t zeros, int nt, int npanels, int d,
+                                 int64_t nsup, int splitk, uintptr_t pairs, uintptr_t part, double s1, double syh,
+                                 double syl, uintptr_t scales, uintptr_t out, uintptr_t stream, int ring, int waves,
+                                 bool fold) {
+    WideArgs a = wide_args(X, Xaug, zeros, nt, npanels, d, nsup, splitk, part, s1, syh, syl);
+    gram_wide(eb, a, P<const int>(pairs), P<const float>(scales), P<double>(out), as_stream(stream), ring, waves, fold);
   });
-  m.def("gram_wide_queue", [](int eb, uintptr_t X, uintptr_t Xaug, uintptr_t zeros, int nt, int npanels, int d,
-                              int64_t nsup, int h, uintptr_t pairs, uintptr_t part, double s1, double syh, double syl,
-                              uintptr_t scales, uintptr_t out, uintptr_t heads, int grid, uintptr_t stream, int waves) {
-    WideArgs a{};
-    a.X = P<const unsigned char>(X);
-    a.Xaug = P<const unsigned char>(Xaug);
-    a.zeros = P<const unsigned char>(zeros);
-    a.NT = nt;
-    a.npanels = npanels;
-    a.d = d;
-    a.nsup = nsup;
-    a.splitk = 8 * h;
-    a.part = P<float>(part);
-    a.aug_scale[0] = s1;
-    a.aug_scale[1] = syh;
-    a.aug_scale[2] = syl;
+  m.def("gram_wide_queue", [wide_args](int eb, uintptr_t X, uintptr_t Xaug, uintptr_t zeros, int nt, int npanels,
+                                       int d, int64_t nsup, int h, uintptr_t pairs, uintptr_t part, double s1,
+                                       double syh, double syl, uintptr_t scales, uintptr_t out, uintptr_t heads,
+                                       int grid, uintptr_t stream, int waves, bool fold) {
+    WideArgs a = wide_args(X, Xaug, zeros, nt, npanels, d, nsup, 8 * h, part, s1, syh, syl);
     gram_wide_queue(eb, a, P<const int>(pairs), P<const float>(scales), P<double>(out), P<int>(heads), h, grid,
-                    as_stream(stream), waves);
+                    as_stream(stream), waves, fold);
+  });
+  m.def("gram_wide_fold", [wide_args](int npanels, int d, int splitk, uintptr_t part, double s1, double syh,
+                                      double syl, uintptr_t scales, uintptr_t out, uintptr_t out32, int J0, int J1,
+                                      uintptr_t stream) {
+    WideArgs a = wide_args(0, 0, 0, 0, npanels, d, 0, splitk, part, s1, syh, syl);
+    gram_wide_fold(a, P<const float>(scales), P<double>(out), P<float>(out32), J0, J1, as_stream(stream));
   });
 
   m.def("syrk_panels", &syrk_panels);

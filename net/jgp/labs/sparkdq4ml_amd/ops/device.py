@@ -6,12 +6,14 @@ launch path, so these ops compose with torch work and HIP-graph capture.  Shapes
 validated HERE, on the host, before any launch (a kernel's indexing assumes them)."""
 from __future__ import annotations
 
+import functools
 import os
 from typing import List, Optional
 
 import numpy as np
 import torch
 
+from ..parallel import comm
 from . import native
 
 __all__ = ["dtype_code", "gram_stats", "compact_indices", "pack_columns", "predict", "regression_metrics",
@@ -816,18 +818,66 @@ def _gram_wide(h, T: TiledWide, y, w, sel, x_zero_dead):
     out = torch.empty(5 + 2 * d + d * (d + 1) // 2, dtype=torch.float64, device=dev)
     sched = os.environ.get("DQ4ML_WIDE_SCHED", "queue")
     hq = _wide_queue_h(nsup) if sched == "queue" else 0
+    # data-parallel fit over RCCL: fold band by band and all-reduce each band while the next folds
+    banded = comm.collectives_active() and comm.backend() == "nccl"
     if hq:
         # persistent XCD-grouped schedule (gram_wide_queue_kernel): 8 groups x h row ranges
-        part = torch.empty(int(h.gram_wide_partials(d, 8 * hq)), dtype=torch.float32, device=dev)
+        splitk = 8 * hq
+        part = torch.empty(int(h.gram_wide_partials(d, splitk)), dtype=torch.float32, device=dev)
         heads = torch.empty(8, dtype=torch.int32, device=dev)
         h.gram_wide_queue(eb, T.buf.data_ptr(), aug.buf.data_ptr(), _zero_page(h, dev).data_ptr(), T.nt, P, d, nsup,
                           hq, pairs_dev.data_ptr(), part.data_ptr(), 1.0, float(s_h), float(s_l), _ptr(T.scales),
                           out.data_ptr(), heads.data_ptr(), _wide_grid(h), _stream(),
-                          int(os.environ.get("DQ4ML_WIDE_WAVES", "8")))
-        return out
-    part = torch.empty(int(h.gram_wide_partials(d, splitk)), dtype=torch.float32, device=dev)
-    h.gram_wide(eb, T.buf.data_ptr(), aug.buf.data_ptr(), _zero_page(h, dev).data_ptr(), T.nt, P, d, nsup, splitk,
-                pairs_dev.data_ptr(),
-                part.data_ptr(), 1.0, float(s_h), float(s_l), _ptr(T.scales), out.data_ptr(), _stream(),
-                int(os.environ.get("DQ4ML_WIDE_RING", "5")), int(os.environ.get("DQ4ML_WIDE_WAVES", "8")))
+                          int(os.environ.get("DQ4ML_WIDE_WAVES", "8")), not banded)
+    else:
+        part = torch.empty(int(h.gram_wide_partials(d, splitk)), dtype=torch.float32, device=dev)
+        h.gram_wide(eb, T.buf.data_ptr(), aug.buf.data_ptr(), _zero_page(h, dev).data_ptr(), T.nt, P, d, nsup,
+                    splitk, pairs_dev.data_ptr(), part.data_ptr(), 1.0, float(s_h), float(s_l), _ptr(T.scales),
+                    out.data_ptr(), _stream(), int(os.environ.get("DQ4ML_WIDE_RING", "5")),
+                    int(os.environ.get("DQ4ML_WIDE_WAVES", "8")), not banded)
+    if banded:
+        fold = functools.partial(h.gram_wide_fold, P, d, splitk, part.data_ptr(), 1.0, float(s_h), float(s_l),
+                                 _ptr(T.scales))
+        _fold_all_reduce(fold, out, P, d)
     return out
+
+
+def wide_bands(P: int, d: int, bucket_bytes: int, elt: int):
+    """Panel-column bands [J0, J1) of the wide fold, each a contiguous slice of the flat WLS layout
+    of about ``bucket_bytes`` on the wire: the augmentation column (the head: counts, Σy, aSum,
+    abSum) first, then runs of 256-wide Gram columns (column j holds j + 1 packed entries).
+    Returns [(J0, J1, flat_lo, flat_hi)]."""
+    base = 5 + 2 * d
+    bands = [(P, P + 1, 0, base)]
+    J0, acc = 0, 0
+    for J in range(P):
+        lo, hi = J * 256, min(d, (J + 1) * 256)
+        acc += (hi * (hi + 1) - lo * (lo + 1)) // 2 * elt
+        if acc >= bucket_bytes or J == P - 1:
+            a, b = J0 * 256, hi
+            bands.append((J0, J + 1, base + a * (a + 1) // 2, base + b * (b + 1) // 2))
+            J0, acc = J + 1, 0
+    return bands
+
+
+def _fold_all_reduce(fold, out: torch.Tensor, P: int, d: int):
+    """X1 for the wide Gram, overlapped with its own fold: band i's all-reduce is issued right
+    after band i's fold is enqueued, so RCCL (its own stream, ordered after the fold at issue
+    time) reduces band i over xGMI while the compute stream folds band i + 1.  Wire format
+    ``comm.wire_dtype()`` (default f32: the partials are f32 MFMA accumulators already, half the
+    bytes of f64 on every link); bands of ``comm.bucket_bytes()``."""
+    import torch.distributed as dist
+
+    wire = comm.wire_dtype()
+    f32 = wire == torch.float32
+    buf = torch.empty(out.numel(), dtype=torch.float32, device=out.device) if f32 else out
+    stream = _stream()
+    works = []
+    for J0, J1, lo, hi in wide_bands(P, d, comm.bucket_bytes(), buf.element_size()):
+        fold(0 if f32 else out.data_ptr(), buf.data_ptr() if f32 else 0, J0, J1, stream)
+        works.append(dist.all_reduce(buf[lo:hi], op=dist.ReduceOp.SUM, async_op=True))
+    for w in works:
+        w.wait()  # the compute stream waits for every band's collective
+    if f32:
+        out.copy_(buf)
+    comm.mark_reduced(out)

@@ -25,7 +25,8 @@ import torch.distributed as dist
 __all__ = ["init", "is_initialized", "rank", "world_size", "local_rank", "barrier", "health_check", "RankFailure",
            "collectives_active", "force_collectives", "backend", "rccl_version", "all_reduce_sum",
            "all_reduce_max", "broadcast", "all_gather_object", "gather_rows_to_root", "shutdown",
-           "DEFAULT_BUCKET_BYTES"]
+           "DEFAULT_BUCKET_BYTES", "set_bucket_bytes", "bucket_bytes", "set_wire_dtype", "wire_dtype",
+           "mark_reduced"]
 
 DEFAULT_BUCKET_BYTES = int(os.environ.get("DQ4ML_BUCKET_BYTES", str(16 << 20)))
 _side_stream = None
@@ -177,15 +178,43 @@ _bucket_bytes = DEFAULT_BUCKET_BYTES
 
 
 def set_bucket_bytes(n: int):
-    """Bucket size of ``all_reduce_sum`` (session config ``dq4ml.bucketBytes``)."""
+    """Bucket size of ``all_reduce_sum`` and of the wide Gram's banded fold (session config
+    ``dq4ml.bucketBytes``)."""
     global _bucket_bytes
     _bucket_bytes = max(1 << 16, int(n))
+
+
+def bucket_bytes() -> int:
+    return _bucket_bytes
+
+
+_wire = torch.float32 if os.environ.get("DQ4ML_ALLREDUCE_WIRE", "f32") == "f32" else torch.float64
+
+
+def set_wire_dtype(dt):
+    """Wire format of the wide Gram all-reduce (session config ``dq4ml.allreduceWire``: f32 | f64).
+    f32 halves the bytes on every xGMI link; the fp8/bf16 SYRK partials are f32 accumulators."""
+    global _wire
+    _wire = {"f32": torch.float32, "f64": torch.float64}.get(dt, dt)
+    if _wire not in (torch.float32, torch.float64):
+        raise ValueError(f"allreduce wire dtype: f32 or f64, not {dt!r}")
+
+
+def wire_dtype():
+    return _wire
+
+
+def mark_reduced(t: torch.Tensor) -> torch.Tensor:
+    """Flag a tensor whose cross-rank sum was already taken by its producer (the wide Gram's
+    banded fold + all-reduce): ``all_reduce_sum`` then passes it through."""
+    t._dq4ml_rank_reduced = True
+    return t
 
 
 def all_reduce_sum(t: torch.Tensor, bucket_bytes: Optional[int] = None) -> torch.Tensor:
     """Sum ``t`` over all ranks (returns a tensor on ``t``'s device).  Order of summation is fixed
     for a fixed world size, so repeated runs are bit-reproducible."""
-    if not collectives_active():
+    if not collectives_active() or getattr(t, "_dq4ml_rank_reduced", False):
         return t
     _fault("before_allreduce")
     bucket_bytes = bucket_bytes or _bucket_bytes

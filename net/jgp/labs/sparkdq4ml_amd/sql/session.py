@@ -153,6 +153,10 @@ class SparkSession:
             from ..parallel import comm
 
             comm.set_bucket_bytes(int(conf["dq4ml.bucketBytes"]))
+        if conf.get("dq4ml.allreduceWire"):
+            from ..parallel import comm
+
+            comm.set_wire_dtype(str(conf["dq4ml.allreduceWire"]).lower())
         self.udf = UDFRegistration(self)
         self.catalog = Catalog()
         self._stopped = False

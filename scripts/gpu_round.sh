@@ -67,6 +67,8 @@ for s in $STEPS; do
        step csvpmc1 300 timeout -s KILL 240 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_SALU GRBM_GUI_ACTIVE -d gpurun_out/csvpmc1 -o run --output-format csv -- python benchmarks/bench_csv_pipeline.py --steps 2 --warmup 1 --rows 2e7 &&
        step csvpmc2 300 timeout -s KILL 240 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d gpurun_out/csvpmc2 -o run --output-format csv -- python benchmarks/bench_csv_pipeline.py --steps 2 --warmup 1 --rows 2e7 &&
        step csvpmc3 300 timeout -s KILL 240 rocprofv3 --kernel-trace --pmc WRITE_SIZE TCC_HIT_sum -d gpurun_out/csvpmc3 -o run --output-format csv -- python benchmarks/bench_csv_pipeline.py --steps 2 --warmup 1 --rows 2e7) || exit $? ;;
+    sweep1) step sweep1 600 env DQ4ML_FORCE_COLLECTIVES=1 python scripts/bucket_sweep.py --rows 2e6 --buckets-mb 4,16,64 ;;
+    bandprof) (export TMPDIR=/tmp DQ4ML_FORCE_COLLECTIVES=1; step bandprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/bandprof -o run --output-format csv -- python scripts/bucket_sweep.py --rows 1e6 --buckets-mb 4 --wires f32 --reps 2) || exit $? ;;
     prof) cd /tmp && export TMPDIR=/tmp && cd - >/dev/null; step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 5 --warmup 1 ;;
   esac
 done

@@ -93,6 +93,26 @@ def main():
         wide[forced] = _fits(spark, X2, y2, solver="normal", gramDtype="fp64")
     comm.force_collectives(True)
     out["wide_eq"] = wide[True] == wide[False]
+
+    # wide bf16 fit (fragment-tiled MFMA SYRK): the Gram folds band by band, each band's RCCL
+    # all-reduce issued as soon as it is folded (ops/device.py _fold_all_reduce) — f64 wire: the
+    # same bits as the unbanded fold; f32 wire: within f32 rounding of it
+    from net.jgp.labs.sparkdq4ml_amd.ops import device as devops
+
+    d3, n3 = 1024, 100_000
+    X3 = torch.randn(d3, n3, generator=g, device=dev).to(torch.bfloat16)
+    y3 = torch.linspace(-1, 1, d3, device=dev) @ X3.float() + 0.5
+    res3 = {}
+    for wire in ("f64", "f32"):
+        comm.set_wire_dtype(wire)
+        for forced in (True, False):
+            comm.force_collectives(forced)
+            res3[(wire, forced)] = _fits(spark, X3, y3, solver="normal", gramDtype="bf16")
+    comm.set_wire_dtype("f32")
+    comm.force_collectives(True)
+    out["wide_bands"] = len(devops.wide_bands(4, d3, comm.bucket_bytes(), 4))
+    out["wide_banded_f64_eq"] = res3[("f64", True)] == res3[("f64", False)]
+    out["wide_banded_f32_diff"] = max(abs(a - b) for a, b in zip(res3[("f32", True)][0], res3[("f32", False)][0]))
     spark.stop()
 
     # --- evidence that RCCL kernels ran (torch profiler, when it sees device kernels at all) ---

@@ -49,6 +49,13 @@ def test_rccl_fit_paths_match_uncollective(rccl_run):
     assert rccl_run["coef_err"] < 5e-3
 
 
+def test_rccl_wide_banded_fold_all_reduce(rccl_run):
+    """Wide Gram X1: band-by-band fold with each band's all-reduce in flight during the next fold."""
+    assert rccl_run["wide_bands"] >= 3
+    assert rccl_run["wide_banded_f64_eq"]
+    assert rccl_run["wide_banded_f32_diff"] < 1e-4
+
+
 def test_rccl_calls_observed(rccl_run):
     """Only RCCL all-reduces are inside the profiled region.  A one-rank in-place all-reduce is
     a no-op on the device (RCCL's one-rank path launches no ring kernel), so what is visible is
