@@ -19,6 +19,7 @@ sharded reads across ranks, default true), ``dq4ml.fit.async`` (asynchronous nor
 from __future__ import annotations
 
 import os
+import re
 import threading
 from typing import Dict, Optional
 
@@ -69,6 +70,73 @@ class Catalog:
 
     def __call__(self):
         return self
+
+
+def master_width(master: str, device_type: str) -> int:
+    """Parallel width of a master URL: ``mi355x[N]`` / ``gpu[N]`` / ``local[N]`` ->
+    N; ``[*]`` -> every visible GPU on a GPU master, every core on a CPU one; no brackets -> 1."""
+    m = re.match(r"^[a-z0-9_-]+\[(\*|\d+)(?:\s*,\s*\d+)?\]$", (master or "local[*]").strip().lower())
+    if m is None:
+        return 1
+    if m.group(1) != "*":
+        n = int(m.group(1))
+        if n < 1:
+            raise ValueError(f"invalid master '{master}': width must be >= 1")
+        return n
+    if device_type == "cuda":
+        return max(1, torch.cuda.device_count())  # counting devices does not initialise HIP
+    return os.cpu_count() or 1
+
+
+def _spmd_width(master: str, conf: Dict[str, str], device: torch.device) -> int:
+    """Ranks the session runs as: a GPU master's (``mi355x`` / ``gpu`` / ``cuda``) width is one
+    process per GPU (RCCL over xGMI); ``local[N]`` and CPU masters keep Spark's meaning, N worker
+    threads (``dq4ml.spmd=true`` makes them N gloo / RCCL ranks instead)."""
+    width = master_width(master, device.type)
+    gpu_master = (master or "").strip().lower().startswith(("mi355x", "gpu", "cuda"))
+    spmd = str(conf.get("dq4ml.spmd", "true" if gpu_master else "false")).lower() in ("1", "true", "yes")
+    if not spmd:
+        if device.type == "cpu" and re.search(r"\[\d+", (master or "")):
+            torch.set_num_threads(width)  # local[N]: N worker threads
+        return 1
+    return width
+
+
+def _launch_width(master: str, width: int, explicit: bool) -> None:
+    """Match the process group to the master's width: inside a launcher the group must have
+    exactly ``width`` ranks; outside one an explicit ``[N]`` (N > 1) starts N ranks of THIS
+    program (``parallel/launch.py``: children, never an exec) and the parent exits with their
+    exit code — Spark's ``local[N]`` gives the app N workers the same way.  ``[*]`` outside a
+    launcher stays one process (it must not fork a script that merely wants "whatever is here")."""
+    import sys
+
+    from ..parallel import comm
+
+    world_env = int(os.environ.get("WORLD_SIZE", "0") or 0)
+    if world_env or comm.is_initialized():
+        world = comm.world_size() if comm.is_initialized() else world_env
+        if explicit and world != width:
+            raise ValueError(f"master '{master}' asks for {width} rank(s) but the process group has {world}")
+        if world > 1:
+            comm.init()
+        return
+    if width <= 1 or not explicit:
+        return
+    if torch.cuda.is_available() and torch.cuda.is_initialized():
+        raise RuntimeError(f"master '{master}': cannot start {width} ranks from a process that already "
+                           f"initialised the GPU; run it under parallel/launch.py or torchrun")
+    from ..parallel.launch import launch
+
+    main = sys.modules.get("__main__")
+    spec = getattr(main, "__spec__", None)
+    if spec is not None and spec.name:
+        argv, module = [spec.name] + sys.argv[1:], True
+    elif sys.argv and sys.argv[0] and os.path.exists(sys.argv[0]):
+        argv, module = [os.path.abspath(sys.argv[0])] + sys.argv[1:], False
+    else:
+        raise RuntimeError(f"master '{master}': no script to start {width} ranks of (interactive session); "
+                           f"use parallel/launch.py or torchrun")
+    raise SystemExit(launch(width, argv, module=module))
 
 
 def _resolve_device(master: str, conf: Dict[str, str]) -> torch.device:
@@ -132,7 +200,15 @@ class SparkSession:
                         if k not in ("spark.master",):
                             s.conf.set(k, v)
                     return s
-                s = SparkSession(dict(self._conf))
+                conf = dict(self._conf)
+                master = conf.get("spark.master", "local[*]")
+                want_cuda = not (str(conf.get("dq4ml.device") or os.environ.get("DQ4ML_DEVICE") or "").startswith("cpu")
+                                 or master.lower().startswith(("cpu", "local-cpu")))
+                dtype = "cuda" if want_cuda and torch.cuda.is_available() else "cpu"
+                width = _spmd_width(master, conf, torch.device(dtype))
+                _launch_width(master, width, bool(re.search(r"\[\d+", master)))
+                s = SparkSession(conf)
+                s.defaultParallelism = width
                 SparkSession._active = s
                 return s
 
