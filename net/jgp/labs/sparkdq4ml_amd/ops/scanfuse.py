@@ -59,6 +59,64 @@ def head_bytes(mean_line: float) -> int:
     return h
 
 
+def _ticket(lookback: bool) -> str:
+    if not lookback:
+        return "  const long long blk = blockIdx.x;"
+    return """  // window = dispatch-order ticket: every predecessor window's block is already resident, so
+  // the look-back below always makes progress
+  unsigned long long* status = (unsigned long long*)offs;
+  if (tid == 0) sblk = (long long)atomicAdd(status + gridDim.x, 1ull);
+  __syncthreads();
+  const long long blk = sblk;"""
+
+
+def _lookback(lookback: bool) -> str:
+    if not lookback:
+        return "  const long long gl0 = offs[blockIdx.x];"
+    return """  if (wave == 0) {
+    // decoupled look-back, one wave: publish this window's count (flag 1), then read the 64
+    // nearest predecessors at once; their values up to the nearest one carrying its inclusive
+    // prefix (flag 2) sum to ours.  Relaxed agent-scope atomics: the status words are
+    // self-contained (no other data to order), so no release/acquire cache maintenance.  Bounded
+    // spin: a predecessor that never publishes flags the scan (vflag 4) instead of hanging.
+    const unsigned long long kVal = (1ull << 62) - 1;
+    if (lane == 0)
+      __hip_atomic_store(status + blk, (1ull << 62) | (unsigned long long)cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    long long pre = 0;
+    long long j0 = blk - 1;
+    unsigned int spins = 0;
+    bool stuck = false;
+    while (j0 >= 0) {
+      const long long j = j0 - lane;
+      unsigned long long st = 2ull << 62;  // before window 0: an inclusive zero
+      if (j >= 0) st = __hip_atomic_load(status + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned int f = (unsigned int)(st >> 62);
+      const unsigned long long inv = __ballot(f == 0), incl = __ballot(f == 2);
+      const int k = incl ? (int)__builtin_ctzll(incl) : 64;
+      const unsigned long long upto = k >= 63 ? ~0ull : ((2ull << k) - 1);  // lanes 0..k
+      if (inv & upto) {
+        if (++spins > (1u << 20)) { stuck = true; break; }
+        __builtin_amdgcn_s_sleep(1);
+        continue;
+      }
+      long long v = lane <= k ? (long long)(st & kVal) : 0ll;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+      pre += v;
+      if (k < 64) break;
+      j0 -= 64;
+    }
+    if (lane == 0) {
+      if (stuck) atomicOr(vflag, 4u);
+      __hip_atomic_store(status + blk, (2ull << 62) | (unsigned long long)(pre + cnt), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+      sgl0 = pre;
+    }
+  }
+  __syncthreads();
+  const long long gl0 = sgl0;"""
+
+
 def _wpe() -> str:
     """Occupancy hint (``DQ4ML_SCAN_WPE`` waves per SIMD; 0: the compiler's choice).  Default 8:
     the byte walks are latency-bound, and 8 waves with a few spilled VGPRs beat 4 waves without
@@ -74,14 +132,21 @@ def _c_char(v: int) -> str:
     return str(int(v))
 
 
-def kernel_source(g, kinds, nullable, used, opts: dict, strict: bool, head: int, slots: dict) -> str:
+def kernel_source(g, kinds, nullable, used, opts: dict, strict: bool, head: int, slots: dict,
+                  lookback: bool = True) -> str:
     """Source of the fused kernel.
 
     ``g``: the dqvm generator after lowering the chain (its ``lines`` use ``f<c>`` / ``m<c>`` for
     base column ``c``; ``stores`` write row ``li``).  ``kinds``: storage kind per CSV column (0 f64,
     1 int32, 2 int64, 3 bool).  ``nullable``: columns with nulls in the earlier scan (others are
     verified null-free).  ``used``: columns the chain reads.  ``slots``: pointer-slot indices of
-    the scan inputs (buf, offs, nalloc, trailing, vflag)."""
+    the scan inputs (buf, offs, nalloc, trailing, vflag).
+
+    ``lookback``: single pass — each block takes a ticket (its window, in dispatch order),
+    publishes its line count and finds its first line index by decoupled look-back over its
+    predecessors' published counts (``offs`` is then the zeroed ``[nb + 1]`` status array, the
+    ticket counter last).  Otherwise ``offs`` holds the exclusive scan of ``csv_count_kernel``'s
+    per-window counts (two passes over the bytes)."""
     ncols = len(kinds)
     ns = len(g.ptrs)
     nv = list(opts.get("null_value", "").encode())
@@ -146,11 +211,12 @@ extern "C" __global__ __launch_bounds__(256) {_wpe()}void {ENTRY}(void* const* P
   __shared__ __attribute__((aligned(16))) unsigned char stage[{H} + {W} + 16];
   __shared__ unsigned short lend[{CAP} + 1];
   __shared__ int wtot[4];
-  __shared__ long long sprev0;
+  __shared__ long long sprev0, sblk, sgl0;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+{_ticket(lookback)}
   const long long a = (long long)(reinterpret_cast<unsigned long long>(b) & 15ull);
   const unsigned char* ab = b - a;                         // 16-byte aligned view
-  const long long wbase = (long long)blockIdx.x * {W} - a;  // buffer index of window byte 0
+  const long long wbase = blk * {W} - a;                    // buffer index of window byte 0
   const long long sbase = wbase - {H};                     // buffer index of stage[0]
   const long long tb = wbase + 64 * tid;                    // this thread's 64 window bytes
   if (wbase > n) return;  // past the end (block-uniform; the virtual terminator at n is in an earlier window)
@@ -228,8 +294,8 @@ extern "C" __global__ __launch_bounds__(256) {_wpe()}void {ENTRY}(void* const* P
   int before = inc - c;
   for (int w = 0; w < wave; ++w) before += wtot[w];
   const int cnt = wtot[0] + wtot[1] + wtot[2] + wtot[3];
+{_lookback(lookback)}
   if (cnt == 0) return;  // block-uniform
-  const long long gl0 = offs[blockIdx.x];
   for (int R = 0; R < cnt; R += {CAP}) {{
     if (before + c > R - 1 && before < R + {CAP}) {{
       unsigned long long mm = m;
@@ -342,6 +408,14 @@ class _ScanPlan:
 
 
 _CACHE: dict = {}
+_streams: dict = {}
+
+
+def _scan_stream(dev) -> torch.cuda.Stream:
+    s = _streams.get(str(dev))
+    if s is None:
+        s = _streams[str(dev)] = torch.cuda.Stream(device=dev)
+    return s
 
 
 def try_fused_scan(nodes, rel, plan, session):
@@ -356,8 +430,9 @@ def try_fused_scan(nodes, rel, plan, session):
     f = rel.fused
     (parts, udfs), refs = dqvm.nodes_key(nodes)
     head = head_bytes(f["mean_line"])
+    lookback = os.environ.get("DQ4ML_SCAN_LOOKBACK", "1") != "0"
     key = (parts, udfs, tuple(rel.schema().names), tuple(f["kinds"]), tuple(f["nullable"]),
-           repr(sorted(f["opts"].items())), f["strict"], head)
+           repr(sorted(f["opts"].items())), f["strict"], head, lookback, _wpe())
     cp = _CACHE.get(key)
     if cp is None and key not in _CACHE:
         base = _ScanBase(rel.schema(), 0, f["device"])
@@ -365,8 +440,9 @@ def try_fused_scan(nodes, rel, plan, session):
         try:
             _, g, outputs, _ = dqvm.compile_chain(nodes, base, False, gen=g)
             slots = {k: g.slot(None, (k,)) for k in _ScanPlan.SCAN_SLOTS}
-            src = kernel_source(g, f["kinds"], f["nullable"], g.used, f["opts"], f["strict"], head, slots)
+            src = kernel_source(g, f["kinds"], f["nullable"], g.used, f["opts"], f["strict"], head, slots, lookback)
             cp = _ScanPlan(src, g, outputs, refs)
+            cp.lookback = lookback
         except dqvm.Unfusable as e:
             cp = "vector" if str(e) == "VectorAssembleExpr" else None
         if len(_CACHE) >= 64:
@@ -377,20 +453,33 @@ def try_fused_scan(nodes, rel, plan, session):
     h = native.hip()
     dev = f["device"]
     buf, n, nalloc = f["buf"], int(f["n"]), int(f["nlines"])
-    stream = torch.cuda.current_stream(dev).cuda_stream
-    nb = int(h.csv_count_blocks(n))
-    offs = torch.empty(nb + 1, dtype=torch.int64, device=dev)
-    h.csv_line_ends(buf.data_ptr(), n, offs.data_ptr(), 0, stream)  # per-window counts -> offsets
-    err = torch.zeros(1, dtype=torch.int32, device=dev)
-    vflag = torch.zeros(1, dtype=torch.int32, device=dev)
-    ptr_list, outs, sel_out = cp.bind(nalloc, dev, {"buf": buf, "offs": offs, "nalloc": nalloc,
-                                                    "trailing": int(f["trailing"]), "vflag": vflag}, err)
-    handle, _log = h.rtc_compile(cp.src, ENTRY)
-    ptrs = _h2d(np.asarray(ptr_list, dtype=np.int64), dev)
-    from ..utils import tracing
+    # stage pipeline: the scan runs on its own stream and depends only on the
+    # HBM-resident input bytes, so action k+1's scan overlaps action k's Gram / fit tail on the
+    # compute stream; the compute stream waits for this scan's event before its consumers
+    cur = torch.cuda.current_stream(dev)
+    side = _scan_stream(dev) if os.environ.get("DQ4ML_SCAN_STREAM", "1") != "0" else cur
+    with torch.cuda.stream(side):
+        stream = side.cuda_stream
+        nb = int(h.csv_count_blocks(n))
+        if cp.lookback:  # single pass: zeroed look-back status + ticket counter
+            offs = torch.zeros(nb + 1, dtype=torch.int64, device=dev)
+        else:  # two passes: per-window terminator counts -> exclusive offsets
+            offs = torch.empty(nb + 1, dtype=torch.int64, device=dev)
+            h.csv_line_ends(buf.data_ptr(), n, offs.data_ptr(), 0, stream)
+        err = torch.zeros(1, dtype=torch.int32, device=dev)
+        vflag = torch.zeros(1, dtype=torch.int32, device=dev)
+        ptr_list, outs, sel_out = cp.bind(nalloc, dev, {"buf": buf, "offs": offs, "nalloc": nalloc,
+                                                        "trailing": int(f["trailing"]), "vflag": vflag}, err)
+        handle, _log = h.rtc_compile(cp.src, ENTRY)
+        ptrs = _h2d(np.asarray(ptr_list, dtype=np.int64), dev)
+        from ..utils import tracing
 
-    with tracing.span("csv_scan_dq_fused"):
-        h.rtc_launch(int(handle), nb, 256, ptrs.data_ptr(), n, stream)
+        with tracing.span("csv_scan_dq_fused"):
+            h.rtc_launch(int(handle), nb, 256, ptrs.data_ptr(), n, stream)
+    if side is not cur:
+        cur.wait_stream(side)
+        for t in [err, vflag, sel_out] + [x for o in outs for x in o if x is not None]:
+            t.record_stream(cur)  # produced on the scan stream, consumed on the compute stream
     tracing.add_rows("csv_scan_dq_fused", nalloc)
     STATS["fused_scans"] += 1
     if cp.has_raise and int(err.item()) != 0:
