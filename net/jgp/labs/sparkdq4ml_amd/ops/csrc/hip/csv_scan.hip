@@ -190,7 +190,8 @@ template <typename PB, typename IT>
 __device__ __forceinline__ bool parse_line(PB B, int64_t bias, int64_t n, const IT* __restrict__ ends,
                                            int64_t li, bool active, int64_t nlines, int ncols, const CsvOpts& o,
                                            const int64_t* __restrict__ dcols, uint8_t* __restrict__ valid,
-                                           uint8_t* __restrict__ keep, uint32_t* smask, int* snull, int* sempty) {
+                                           uint8_t* __restrict__ keep, uint32_t* smask, int* snull, int* sempty,
+                                           int* smiss) {
   const bool lane0 = (threadIdx.x & 63) == 0;
   int64_t start = 0, end = 0;
   bool line = false;
@@ -206,14 +207,20 @@ __device__ __forceinline__ bool parse_line(PB B, int64_t bias, int64_t n, const 
   const uint64_t empty = __ballot(active && !line);
   if (lane0 && empty) atomicAdd(sempty, (int)__popcll(empty));
   long long pos = start;
-  bool slow = false, malformed = false;
+  bool slow = false, malformed = false, miss = false;
+  const bool plain = o.null_len == 0 && !o.trim_lead && !o.trim_trail;
   for (int c = 0; c < ncols; ++c) {
     double dv = 0.0;
     long long lv = 0;
     bool big = false;
     int ty = CT_NULL;
-    if (pos <= end && line)
-      ty = dq4ml_csv::csv_field(B, (long long)bias, pos, (long long)end, o, dv, lv, slow, big, malformed);
+    if (pos <= end && line) {
+      const long long pb = (long long)bias, pe = (long long)end;
+      if (!(plain && dq4ml_csv::csv_field_fast(B, pb, pos, pe, o.sep, dv, lv, ty))) {
+        ty = dq4ml_csv::csv_field_general(B, pb, pos, pe, o, dv, lv, slow, big, malformed);
+        miss = true;  // a field outside the fast path (a later fused scan then keeps the general parser)
+      }
+    }
     const int kind = (int)dcols[ncols + c];
     slow |= big && kind != 2;  // an f64 plane would round it; an int64 store of lv is exact
     bool ok = ty != CT_NULL && ty != CT_STRING;
@@ -244,6 +251,8 @@ __device__ __forceinline__ bool parse_line(PB B, int64_t bias, int64_t n, const 
       if (nulls) atomicAdd(&snull[c], (int)__popcll(nulls));
     }
   }
+  const uint64_t misses = __ballot(active && line && miss);
+  if (lane0 && misses) atomicAdd(smiss, (int)__popcll(misses));
   // a malformed record: every field null (valid = 0) — the null counts above already cover the
   // fields that failed; the rest are counted here
   const uint64_t bad = __ballot(active && line && malformed);
@@ -272,7 +281,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     unsigned long long* __restrict__ stats) {
   __shared__ uint32_t smask[kMaxCols];
   __shared__ int snull[kMaxCols];
-  __shared__ int sempty, sflag;
+  __shared__ int sempty, sflag, smiss;
   __shared__ __attribute__((aligned(16))) uint8_t stage[LDS];
   for (int c = threadIdx.x; c < ncols; c += blockDim.x) {
     smask[c] = 0;
@@ -281,6 +290,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   if (threadIdx.x == 0) {
     sflag = 0;
     sempty = 0;
+    smiss = 0;
   }
   const uint8_t* ab = b - (reinterpret_cast<uintptr_t>(b) & 15);
   const int64_t off = b - ab;
@@ -304,14 +314,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
       }
       __syncthreads();
       slow |= parse_line(stage, glo - off, n, ends, li, li < l1, nlines, ncols, o, dcols, valid, keep, smask,
-                         snull, &sempty);
+                         snull, &sempty, &smiss);
     } else {
-      slow |= parse_line(b, 0, n, ends, li, li < l1, nlines, ncols, o, dcols, valid, keep, smask, snull, &sempty);
+      slow |= parse_line(b, 0, n, ends, li, li < l1, nlines, ncols, o, dcols, valid, keep, smask, snull, &sempty,
+                         &smiss);
     }
   }
   if (slow) sflag = 1;
   __syncthreads();
-  // stats: [0] slow flag, [1] empty lines, [2, 2+ncols) null fields, [2+ncols, 2+2*ncols) class masks
+  // stats: [0] slow flag, [1] empty lines, [2, 2+ncols) null fields, [2+ncols, 2+2*ncols) class masks,
+  // [2+2*ncols] lines with a field outside the numeric fast path
   for (int c = threadIdx.x; c < ncols; c += blockDim.x) {
     if (snull[c]) atomicAdd(&stats[2 + c], (unsigned long long)snull[c]);
     if (smask[c]) atomicOr(&stats[2 + ncols + c], (unsigned long long)smask[c]);
@@ -319,6 +331,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   if (threadIdx.x == 0) {
     if (sempty) atomicAdd(&stats[1], (unsigned long long)sempty);
     if (sflag) atomicOr(&stats[0], 1ull);
+    if (smiss) atomicAdd(&stats[2 + 2 * ncols], (unsigned long long)smiss);
   }
 }
 

@@ -101,7 +101,7 @@ def _scan_chunk(h, buf, n: int, trailing: bool, ncols: int, sep: str, dev, hint=
     ptrs = _h2d(np.array([t.data_ptr() for t in dcols] + [k for k, _ in kinds], dtype=np.int64), dev)
     valid = torch.empty(ncols, m, dtype=torch.bool, device=dev)
     keep = torch.empty(m, dtype=torch.bool, device=dev)
-    stats = torch.zeros(2 + 2 * ncols, dtype=torch.int64, device=dev)
+    stats = torch.zeros(3 + 2 * ncols, dtype=torch.int64, device=dev)
     h.csv_parse(buf.data_ptr(), n, ends.data_ptr(), nlines, ncols, ord(sep), ptrs.data_ptr(), valid.data_ptr(),
                 keep.data_ptr(), stats.data_ptr(), stream, **_opt_args(opts))
     return nlines, dcols, valid, keep, stats
@@ -162,7 +162,9 @@ def _finish(parts, types, st, dev, hinted=False):
         table = Table(table.schema, table.columns, total, k.clone(), dev).compact()
     # what a later fused scan of the same bytes relies on (ops/scanfuse.py): line count (empty
     # lines included) and the columns holding nulls
-    table.scan_facts = {"nlines": int(total), "nullable": [bool(int(st[:, 2 + c].sum())) for c in range(len(types))]}
+    nc = len(types)
+    table.scan_facts = {"nlines": int(total), "nullable": [bool(int(st[:, 2 + c].sum())) for c in range(nc)],
+                        "fast_only": int(st[:, 2 + 2 * nc].sum()) == 0}
     return table
 
 
@@ -240,7 +242,7 @@ def scan_device(data, sep: str = ",", infer: bool = True, device=None, ncols: Op
     else:
         parts = _scan_chunked(h, data, ncols, sep, dev, int(chunk_bytes), pinned, hint, opts)
     st = torch.stack([p[4] for p in parts]).cpu().numpy()  # the one host read of the parse results
-    masks = np.bitwise_or.reduce(st[:, 2 + ncols:], axis=0)
+    masks = np.bitwise_or.reduce(st[:, 2 + ncols:2 + 2 * ncols], axis=0)
     if user_types:
         flag = int(st[:, 0].max())
         if sharded:

@@ -117,7 +117,7 @@ def _lookback(lookback: bool) -> str:
   const long long gl0 = sgl0;"""
 
 
-def _wpe() -> str:
+def _wpe(fast_only: bool = False) -> str:
     """Occupancy hint (``DQ4ML_SCAN_WPE`` waves per SIMD; 0: the compiler's choice).  Default 8:
     the byte walks are latency-bound, and 8 waves with a few spilled VGPRs beat 4 waves without
     (lab CSV pipeline 2.16 / 1.94 / 1.91 ms per step at 4 / 6 / 8 waves, one run)."""
@@ -133,7 +133,7 @@ def _c_char(v: int) -> str:
 
 
 def kernel_source(g, kinds, nullable, used, opts: dict, strict: bool, head: int, slots: dict,
-                  lookback: bool = True) -> str:
+                  lookback: bool = True, fast_only: bool = False) -> str:
     """Source of the fused kernel.
 
     ``g``: the dqvm generator after lowering the chain (its ``lines`` use ``f<c>`` / ``m<c>`` for
@@ -146,7 +146,12 @@ def kernel_source(g, kinds, nullable, used, opts: dict, strict: bool, head: int,
     publishes its line count and finds its first line index by decoupled look-back over its
     predecessors' published counts (``offs`` is then the zeroed ``[nb + 1]`` status array, the
     ticket counter last).  Otherwise ``offs`` holds the exclusive scan of ``csv_count_kernel``'s
-    per-window counts (two passes over the bytes)."""
+    per-window counts (two passes over the bytes).
+
+    ``fast_only``: the earlier scan parsed every field on the numeric fast path (plain dialect):
+    only that path is compiled in — the general parser's registers (~60 VGPRs) leave the kernel
+    (40 VGPRs instead of 103, full occupancy without spills); a field it cannot take is a fact
+    violation (vflag), like a type or null mismatch."""
     ncols = len(kinds)
     ns = len(g.ptrs)
     nv = list(opts.get("null_value", "").encode())
@@ -158,9 +163,14 @@ def kernel_source(g, kinds, nullable, used, opts: dict, strict: bool, head: int,
     parse = []
     for c in range(ncols):
         k = int(kinds[c])
-        parse.append(f"    double d{c} = 0.0; long long l{c} = 0; bool g{c} = false; int y{c} = C_NULL;\n"
-                     f"    if (pos <= end && line) y{c} = csv_field(B, bias, pos, end, O, d{c}, l{c}, slow, g{c}, malformed);\n"
-                     f"    bool k{c} = y{c} != C_NULL && y{c} != C_STRING;\n")
+        if fast_only:
+            parse.append(f"    double d{c} = 0.0; long long l{c} = 0; bool g{c} = false; int y{c} = C_NULL;\n"
+                         f"    if (pos <= end && line && !csv_field_fast(B, bias, pos, end, O.sep, d{c}, l{c}, y{c})) bad = true;\n"
+                         f"    bool k{c} = y{c} != C_NULL && y{c} != C_STRING;\n")
+        else:
+            parse.append(f"    double d{c} = 0.0; long long l{c} = 0; bool g{c} = false; int y{c} = C_NULL;\n"
+                         f"    if (pos <= end && line) y{c} = csv_field(B, bias, pos, end, O, d{c}, l{c}, slow, g{c}, malformed);\n"
+                         f"    bool k{c} = y{c} != C_NULL && y{c} != C_STRING;\n")
         if strict:
             parse.append(f"    if (y{c} != C_NULL && !csv_conforms(y{c}, {k})) {{ malformed = true; k{c} = false; }}\n")
         else:
@@ -186,12 +196,12 @@ using namespace dq4ml_csv;
 typedef unsigned int csv_u32x4 __attribute__((ext_vector_type(4)));
 
 // one line: parse every field into registers, run the DQ chain, store the needed outputs at li
-template <typename PB>
-__device__ __forceinline__ void dq_row(PB B, long long bias, long long start, long long end, long long li,
+template <typename PB, typename IT>
+__device__ __forceinline__ void dq_row(PB B, IT bias, IT start, IT end, long long li,
                                        void* const* p, unsigned int* vflag) {{
     const CsvOpts O = {o};
     const bool line = end > start && !({comment} && B[start - bias] == {comment});
-    long long pos = start;
+    IT pos = start;
     bool slow = false, malformed = false, bad = false;
 {''.join(parse)}    bad |= slow;
     if (bad) atomicOr(vflag, 1u);
@@ -199,7 +209,7 @@ __device__ __forceinline__ void dq_row(PB B, long long bias, long long start, lo
 {body}
 {stores}}}
 
-extern "C" __global__ __launch_bounds__(256) {_wpe()}void {ENTRY}(void* const* P, long long n) {{
+extern "C" __global__ __launch_bounds__(256) {_wpe(fast_only)}void {ENTRY}(void* const* P, long long n) {{
   void* p[{ns}];
 #pragma unroll
   for (int i = 0; i < {ns}; ++i) p[i] = P[i];
@@ -324,7 +334,7 @@ extern "C" __global__ __launch_bounds__(256) {_wpe()}void {ENTRY}(void* const* P
       if (li >= nalloc) {{
         atomicOr(vflag, 2u);
       }} else if (start >= sbase) {{
-        dq_row(stage, sbase, start, end, li, p, vflag);
+        dq_row(stage, 0, (int)(start - sbase), (int)(end - sbase), li, p, vflag);  // 32-bit stage positions
       }} else {{
         dq_row(b, 0ll, start, end, li, p, vflag);
       }}
@@ -431,8 +441,11 @@ def try_fused_scan(nodes, rel, plan, session):
     (parts, udfs), refs = dqvm.nodes_key(nodes)
     head = head_bytes(f["mean_line"])
     lookback = os.environ.get("DQ4ML_SCAN_LOOKBACK", "1") != "0"
+    o = f["opts"]
+    fast_only = (bool(f.get("fast_only")) and not o["null_value"] and not o["trim_lead"] and not o["trim_trail"]
+                 and os.environ.get("DQ4ML_SCAN_FASTONLY", "1") != "0")
     key = (parts, udfs, tuple(rel.schema().names), tuple(f["kinds"]), tuple(f["nullable"]),
-           repr(sorted(f["opts"].items())), f["strict"], head, lookback, _wpe())
+           repr(sorted(f["opts"].items())), f["strict"], head, lookback, fast_only, _wpe(fast_only))
     cp = _CACHE.get(key)
     if cp is None and key not in _CACHE:
         base = _ScanBase(rel.schema(), 0, f["device"])
@@ -440,7 +453,8 @@ def try_fused_scan(nodes, rel, plan, session):
         try:
             _, g, outputs, _ = dqvm.compile_chain(nodes, base, False, gen=g)
             slots = {k: g.slot(None, (k,)) for k in _ScanPlan.SCAN_SLOTS}
-            src = kernel_source(g, f["kinds"], f["nullable"], g.used, f["opts"], f["strict"], head, slots, lookback)
+            src = kernel_source(g, f["kinds"], f["nullable"], g.used, f["opts"], f["strict"], head, slots, lookback,
+                                fast_only)
             cp = _ScanPlan(src, g, outputs, refs)
             cp.lookback = lookback
         except dqvm.Unfusable as e:

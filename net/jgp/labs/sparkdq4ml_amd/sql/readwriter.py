@@ -334,6 +334,7 @@ class DataFrameReader:
                 fused = {"buf": dbytes, "n": n, "nlines": facts["nlines"], "device": dev,
                          "trailing": n > 0 and body[-1] not in (10, 13), "mean_line": n / facts["nlines"],
                          "kinds": [_KIND.get(c, (0,))[0] for c in codes], "nullable": list(facts["nullable"]),
+                         "fast_only": bool(facts.get("fast_only")),
                          "opts": dict(_opt_args(dopts), sep=sep, strict=bool(strict)), "strict": bool(strict)}
                 if fused["opts"]["null_value"] and len(fused["opts"]["null_value"].encode()) > 16:
                     fused = None

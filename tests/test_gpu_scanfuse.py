@@ -49,7 +49,7 @@ def _rows(df):
     return [tuple(r) for r in df.collect()]
 
 
-def _lab_csv(rng, n, term=b"\r", trailing=False, empty=0.0, long_comment=False):
+def _lab_csv(rng, n, term=b"\r", trailing=False, empty=0.0, long_comment=False, general=False):
     g = rng.integers(1, 36, n)
     price = np.round(5.0 * g + 20 + rng.normal(0, 3, n), 2)
     low = rng.random(n) < 0.05
@@ -62,19 +62,22 @@ def _lab_csv(rng, n, term=b"\r", trailing=False, empty=0.0, long_comment=False):
             lines.append(b"")
         if long_comment and i % 997 == 5:
             lines.append(b"#" + b"x" * int(rng.integers(300, 5000)))
-        lines.append(b"%d,%s" % (g[i], repr(float(price[i])).encode()))
+        p = repr(float(price[i])).encode()
+        if general and i % 7 == 3:  # outside the numeric fast path: exponent / > 9 digits
+            p = b"%.6e" % price[i] if i % 2 else b"%.9f" % price[i]
+        lines.append(b"%d,%s" % (g[i], p))
     body = term.join(lines)
     return body + (term if trailing else b"")
 
 
-@pytest.mark.parametrize("case", ["cr", "lf_trailing", "crlf_empty", "long_comment"])
+@pytest.mark.parametrize("case", ["cr", "lf_trailing", "crlf_empty", "long_comment", "general"])
 def test_fused_scan_matches_eager(tmp_path, case):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     rng = np.random.default_rng(len(case))
-    term = {"cr": b"\r", "lf_trailing": b"\n", "crlf_empty": b"\r\n", "long_comment": b"\n"}[case]
+    term = {"cr": b"\r", "lf_trailing": b"\n", "crlf_empty": b"\r\n", "long_comment": b"\n", "general": b"\r"}[case]
     data = _lab_csv(rng, 60000, term, trailing=case == "lf_trailing", empty=0.01 if case == "crlf_empty" else 0.0,
-                    long_comment=case == "long_comment")
+                    long_comment=case == "long_comment", general=case == "general")
     p = tmp_path / f"{case}.csv"
     p.write_bytes(data)
     opts = {"comment": "#"} if case == "long_comment" else None
@@ -90,6 +93,8 @@ def test_fused_scan_matches_eager(tmp_path, case):
     assert scanfuse.STATS["fused_scans"] == before + 1, "the re-read did not take the fused scan kernel"
     assert len(fused) == len(eager) > 40000
     assert fused == eager
+    f = raw2._plan.fused
+    assert f["fast_only"] == (case != "general")  # the general-parser build is exercised too
     # any other consumer of the lazy relation: the plain device scan, same rows
     raw3, _ = _chain(spark, str(p), opts)
     assert raw3.count() == raw1.count()
