@@ -164,3 +164,61 @@ def test_fused_scan_nulls_and_raise(tmp_path):
         with pytest.raises(SparkException):
             _rows(d)
     spark.stop()
+
+
+@pytest.mark.parametrize("case", ["header", "user_schema", "null_value", "whitespace", "nulls_fast"])
+def test_fused_scan_reader_options(tmp_path, case):
+    """Every reader option the device scanner takes also holds on the fused path: the eager read
+    and the fused re-read of the same file give the same rows through a DQ chain (a cast, a
+    filter over a nullable column, a computed column)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    rng = np.random.default_rng(11)
+    n = 40000
+    a = rng.integers(-1000, 1000, n)
+    b = np.round(rng.normal(0, 50, n), 3)
+    rows = []
+    for i in range(n):
+        fa, fb = str(a[i]), repr(float(b[i]))
+        if case in ("null_value", "nulls_fast") and i % 37 == 5:
+            fb = "NA" if case == "null_value" else ""
+        if case == "whitespace":
+            fa, fb = " " + fa, fb + "\t"
+        rows.append(f"{fa},{fb}")
+    text = ("x,y\n" if case == "header" else "") + "\n".join(rows)
+    p = tmp_path / f"{case}.csv"
+    p.write_bytes(text.encode())
+    opts = {"header": "true"} if case == "header" else {}
+    if case == "null_value":
+        opts["nullValue"] = "NA"
+    if case == "whitespace":
+        opts.update(ignoreLeadingWhiteSpace="true", ignoreTrailingWhiteSpace="true")
+    spark = _session()
+
+    def run():
+        r = spark.read().format("csv").option("inferSchema", "true")
+        for k, v in opts.items():
+            r = r.option(k, v)
+        if case == "user_schema":
+            r = r.schema("x LONG, y DOUBLE")
+        df = r.load(str(p))
+        c0, c1 = df.columns
+        df.createOrReplaceTempView("t")
+        out = spark.sql(f"SELECT cast({c0} as double) * 2 AS a2, {c1} AS yy FROM t WHERE {c1} > -20 OR {c1} IS NULL")
+        return df, [tuple(r) for r in out.collect()]
+
+    d1, eager = run()
+    before = scanfuse.STATS["fused_scans"]
+    d2, fused = run()
+    assert isinstance(d2._plan, CsvScanRelation)
+    assert scanfuse.STATS["fused_scans"] == before + 1
+    assert d2.schema == d1.schema
+    assert len(fused) == len(eager) > 1000
+
+    def same(x, y):
+        return (x is None and y is None) or x == y
+
+    assert all(same(u, v) for ra, rb in zip(fused, eager) for u, v in zip(ra, rb))
+    fast = d2._plan.fused["fast_only"]
+    assert fast == (case in ("header", "user_schema", "nulls_fast"))
+    spark.stop()
