@@ -19,6 +19,7 @@ expressions are not fused and fall back to the per-node vectorized evaluator.
 from __future__ import annotations
 
 import itertools
+import os
 from typing import Dict, List, Optional, Tuple
 
 import numpy as np
@@ -485,53 +486,59 @@ def _kernel_source(g: _Gen) -> str:
             f"  }}\n}}\n")
 
 
-_VEC = {"double": "dq_f64x4", "float": "dq_f32x4", "int": "dq_i32x4", "long long": "dq_i64x4",
-        "bool": "dq_u8x4", "unsigned char": "dq_u8x4"}
-_VEC_TYPES = ("typedef double dq_f64x4 __attribute__((ext_vector_type(4)));\n"
-              "typedef float dq_f32x4 __attribute__((ext_vector_type(4)));\n"
-              "typedef int dq_i32x4 __attribute__((ext_vector_type(4)));\n"
-              "typedef long long dq_i64x4 __attribute__((ext_vector_type(4)));\n"
-              "typedef unsigned char dq_u8x4 __attribute__((ext_vector_type(4)));\n")
+VEC_ROWS = int(os.environ.get("DQ4ML_DQ_ROWS", "4"))  # consecutive rows per thread, vector form
+_VEC_BASE = {"double": "double", "float": "float", "int": "int", "long long": "long long", "bool": "unsigned char",
+             "unsigned char": "unsigned char"}
+_VEC_NAME = {"double": "f64", "float": "f32", "int": "i32", "long long": "i64", "bool": "u8", "unsigned char": "u8"}
 
 
-def _kernel_source_vec(g: _Gen) -> str:
-    """The same chain for 32-byte-aligned slots (the usual case: whole device allocations): each
-    thread owns 4 CONSECUTIVE rows, so every column is read and every output written with one
-    4-wide vector access per thread (the strided form moves 1-8 bytes per lane per instruction);
-    the n % 4 tail rows run the scalar body."""
+def _vec_t(ct: str, v: int) -> str:
+    return f"dq_{_VEC_NAME[ct]}x{v}"
+
+
+def _vec_types(v: int) -> str:
+    return "".join(f"typedef {b} dq_{nm}x{v} __attribute__((ext_vector_type({v})));\n"
+                   for b, nm in (("double", "f64"), ("float", "f32"), ("int", "i32"), ("long long", "i64"),
+                                 ("unsigned char", "u8")))
+
+
+def _kernel_source_vec(g: _Gen, V: int = VEC_ROWS) -> str:
+    """The same chain for aligned slots (the usual case: whole device allocations): each thread
+    owns V CONSECUTIVE rows, so every column is read and every output written with one V-wide
+    vector access per thread (the strided form moves 1-8 bytes per lane per instruction); the
+    n % V tail rows run the scalar body."""
     ns = len(g.ptrs)
-    decl = "".join(f"    {ct} {v}_a[4];\n" for ct, v, _, _ in g.loads)
-    ld = "".join(f"    {{ const {_VEC[st]} q = *(const {_VEC[st]}*)((const {'unsigned char' if st == 'bool' else st}*)p[{s}] + r0);\n"
-                 f"      for (int u = 0; u < 4; ++u) {v}_a[u] = ({ct})q[u]; }}\n" for ct, v, st, s in g.loads)
+    decl = "".join(f"    {ct} {v}_a[{V}];\n" for ct, v, _, _ in g.loads)
+    ld = "".join(f"    {{ const {_vec_t(st, V)} q = *(const {_vec_t(st, V)}*)((const {_VEC_BASE[st]}*)p[{s}] + r0);\n"
+                 f"      for (int u = 0; u < {V}; ++u) {v}_a[u] = ({ct})q[u]; }}\n" for ct, v, st, s in g.loads)
     use = "".join(f"      const {ct} {v} = {v}_a[u];\n" for ct, v, _, _ in g.loads)
     body = "\n".join("  " + ln for ln in g.lines).replace("P[", "p[")
-    odecl = "".join(f"    {_VEC[t]} o{s};\n" for t, _, s in g.stores)
-    oset = "".join(f"      o{s}[u] = ({'unsigned char' if t == 'bool' else t})({v});\n" for t, v, s in g.stores)
-    ost = "".join(f"    *({_VEC[t]}*)(({'unsigned char' if t == 'bool' else t}*)p[{s}] + r0) = o{s};\n"
-                  for t, _, s in g.stores)
+    odecl = "".join(f"    {_vec_t(t, V)} o{s};\n" for t, _, s in g.stores)
+    oset = "".join(f"      o{s}[u] = ({_VEC_BASE[t]})({v});\n" for t, v, s in g.stores)
+    ost = "".join(f"    *({_vec_t(t, V)}*)(({_VEC_BASE[t]}*)p[{s}] + r0) = o{s};\n" for t, _, s in g.stores)
     tail_ld = "".join(f"    const {ct} {v} = ({ct})((const {st}*)p[{s}])[r];\n" for ct, v, st, s in g.loads)
     tail_st = "".join(f"    (({t}*)p[{s}])[r] = ({t})({v});\n" for t, v, s in g.stores)
-    return (_VEC_TYPES +
+    return (_vec_types(V) +
             f'extern "C" __global__ __launch_bounds__(256) void {ENTRY}(void* const* P, long long n) {{\n'
             f"  void* p[{ns}];\n"
             f"#pragma unroll\n"
             f"  for (int i = 0; i < {ns}; ++i) p[i] = P[i];\n"
             f"  const long long stride = (long long)gridDim.x * blockDim.x;\n"
             f"  const long long gt = (long long)blockIdx.x * blockDim.x + threadIdx.x;\n"
-            f"  const long long nq = n / 4;\n"
+            f"  const long long nq = n / {V};\n"
             f"  for (long long t = gt; t < nq; t += stride) {{\n"
-            f"    const long long r0 = 4 * t;\n"
-            f"    bool live_a[4];\n{decl}"
-            f"    if (p[0]) {{ const dq_u8x4 q = *(const dq_u8x4*)((const unsigned char*)p[0] + r0);\n"
-            f"      for (int u = 0; u < 4; ++u) live_a[u] = q[u] != 0; }}\n"
-            f"    else {{ for (int u = 0; u < 4; ++u) live_a[u] = true; }}\n{ld}{odecl}"
+            f"    const long long r0 = {V} * t;\n"
+            f"    bool live_a[{V}];\n{decl}"
+            f"    if (p[0]) {{ const dq_u8x{V} q = *(const dq_u8x{V}*)((const unsigned char*)p[0] + r0);\n"
+            f"      for (int u = 0; u < {V}; ++u) live_a[u] = q[u] != 0; }}\n"
+            f"    else {{ for (int u = 0; u < {V}; ++u) live_a[u] = true; }}\n{ld}{odecl}"
             f"#pragma unroll\n"
-            f"    for (int u = 0; u < 4; ++u) {{\n"
+            f"    for (int u = 0; u < {V}; ++u) {{\n"
             f"      bool live = live_a[u];\n{use}{body}\n{oset}"
             f"    }}\n{ost}"
             f"  }}\n"
-            f"  if (gt < n - 4 * nq) {{\n"
-            f"    const long long r = 4 * nq + gt;\n"
+            f"  if (gt < n - {V} * nq) {{\n"
+            f"    const long long r = {V} * nq + gt;\n"
             f"    bool live = p[0] ? ((const bool*)p[0])[r] : true;\n{tail_ld}{body}\n{tail_st}"
             f"  }}\n}}\n")
 
@@ -668,13 +675,13 @@ def try_execute_fused(plan, session) -> Optional[Table]:
     h = native.hip()
     err = torch.zeros(1, dtype=torch.int32, device=base.device)
     ptr_list, outs, sel_out, keep = cp.bind(base, err)
-    vec = all(q % 32 == 0 for q in ptr_list)  # whole allocations: the 4-consecutive-rows form
+    vec = all(q % (8 * VEC_ROWS) == 0 for q in ptr_list)  # whole allocations: the V-consecutive-rows form
     handle, _log = h.rtc_compile(cp.src[1] if vec else cp.src[0], ENTRY)
     from .device import _h2d
 
     ptrs = _h2d(np.asarray(ptr_list, dtype=np.int64), base.device)  # no host-device sync
     n = base.nrows
-    grid = int(max(1, min((n + 1023) // 1024 if vec else (n + 255) // 256, 8192)))
+    grid = int(max(1, min((n + 256 * VEC_ROWS - 1) // (256 * VEC_ROWS) if vec else (n + 255) // 256, 8192)))
     from ..utils import tracing
 
     with tracing.span("dq_fused"):

@@ -125,7 +125,7 @@ def _wpe(fast_only: bool = False) -> str:
     return f"__attribute__((amdgpu_waves_per_eu({w}))) " if w > 0 else ""
 
 
-_VALUE = {1: "(int)l{c}", 2: "l{c}", 0: "d{c}", 3: "(d{c} != 0.0)"}
+_VALUE = {1: "(int)fzl{c}", 2: "fzl{c}", 0: "fzd{c}", 3: "(fzd{c} != 0.0)"}
 
 
 def _c_char(v: int) -> str:
@@ -164,29 +164,29 @@ def kernel_source(g, kinds, nullable, used, opts: dict, strict: bool, head: int,
     for c in range(ncols):
         k = int(kinds[c])
         if fast_only:
-            parse.append(f"    double d{c} = 0.0; long long l{c} = 0; bool g{c} = false; int y{c} = C_NULL;\n"
-                         f"    if (pos <= end && line && !csv_field_fast(B, bias, pos, end, O.sep, d{c}, l{c}, y{c})) bad = true;\n"
-                         f"    bool k{c} = y{c} != C_NULL && y{c} != C_STRING;\n")
+            parse.append(f"    double fzd{c} = 0.0; long long fzl{c} = 0; bool fzg{c} = false; int fzy{c} = C_NULL;\n"
+                         f"    if (pos <= end && line && !csv_field_fast(B, bias, pos, end, O.sep, fzd{c}, fzl{c}, fzy{c})) bad = true;\n"
+                         f"    bool fzk{c} = fzy{c} != C_NULL && fzy{c} != C_STRING;\n")
         else:
-            parse.append(f"    double d{c} = 0.0; long long l{c} = 0; bool g{c} = false; int y{c} = C_NULL;\n"
-                         f"    if (pos <= end && line) y{c} = csv_field(B, bias, pos, end, O, d{c}, l{c}, slow, g{c}, malformed);\n"
-                         f"    bool k{c} = y{c} != C_NULL && y{c} != C_STRING;\n")
+            parse.append(f"    double fzd{c} = 0.0; long long fzl{c} = 0; bool fzg{c} = false; int fzy{c} = C_NULL;\n"
+                         f"    if (pos <= end && line) fzy{c} = csv_field(B, bias, pos, end, O, fzd{c}, fzl{c}, slow, fzg{c}, malformed);\n"
+                         f"    bool fzk{c} = fzy{c} != C_NULL && fzy{c} != C_STRING;\n")
         if strict:
-            parse.append(f"    if (y{c} != C_NULL && !csv_conforms(y{c}, {k})) {{ malformed = true; k{c} = false; }}\n")
+            parse.append(f"    if (fzy{c} != C_NULL && !csv_conforms(fzy{c}, {k})) {{ malformed = true; fzk{c} = false; }}\n")
         else:
-            parse.append(f"    bad |= line && y{c} != C_NULL && !csv_conforms(y{c}, {k});\n")
+            parse.append(f"    bad |= line && fzy{c} != C_NULL && !csv_conforms(fzy{c}, {k});\n")
         if k != 2:
-            parse.append(f"    slow |= g{c};\n")
-    parse.append("    if (malformed) {" + " ".join(f"k{c} = false;" for c in range(ncols)) + " }\n")
+            parse.append(f"    slow |= fzg{c};\n")
+    parse.append("    if (malformed) {" + " ".join(f"fzk{c} = false;" for c in range(ncols)) + " }\n")
     for c in range(ncols):
         if not nullable[c]:
-            parse.append(f"    bad |= line && !k{c};\n")
+            parse.append(f"    bad |= line && !fzk{c};\n")
     for c in sorted(used):
         ct = used[c]
         val = _VALUE[int(kinds[c])].format(c=c)
-        parse.append(f"    const {ct} f{c} = k{c} ? ({ct})({val}) : ({ct})0;\n")
+        parse.append(f"    const {ct} fzf{c} = fzk{c} ? ({ct})({val}) : ({ct})0;\n")
         if nullable[c]:
-            parse.append(f"    const bool m{c} = k{c};\n")
+            parse.append(f"    const bool fzm{c} = fzk{c};\n")
     body = "\n".join("    " + ln.strip() for ln in g.lines).replace("P[", "p[")
     stores = "".join(f"    (({t}*)p[{s}])[li] = ({t})({v});\n" for t, v, s in g.stores)
     comment = int(opts["comment"])
@@ -364,8 +364,9 @@ def _scan_gen(base: _ScanBase, nullable):
     from . import dqvm
 
     class _ScanGen(dqvm._Gen):
-        """Base column c is the register pair (f<c>, m<c>) the kernel's parse defines — or
-        (f<c>, true) for a column the earlier scan found null-free (verified in the kernel)."""
+        """Base column c is the register pair (fzf<c>, fzm<c>) the kernel's parse defines — or
+        (fzf<c>, true) for a column the earlier scan found null-free (verified in the kernel).
+        The ``fz`` prefix keeps them apart from the generator's own temporaries (k<n>, m<n>, ...)."""
 
         def __init__(self):
             super().__init__(base, check_device=False)
@@ -375,7 +376,7 @@ def _scan_gen(base: _ScanBase, nullable):
             if idx not in self.col_cache:
                 t = self.base.schema.fields[idx].dataType
                 self.used[idx] = dqvm._ctype(t)
-                self.col_cache[idx] = (f"f{idx}", f"m{idx}" if nullable[idx] else "true", t)
+                self.col_cache[idx] = (f"fzf{idx}", f"fzm{idx}" if nullable[idx] else "true", t)
             return self.col_cache[idx]
 
     return _ScanGen()

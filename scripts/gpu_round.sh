@@ -31,6 +31,8 @@ for s in $STEPS; do
        step widepmc1 600 rocprofv3 --kernel-trace --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE -d gpurun_out/widepmc1 -o run --output-format csv -- python scripts/wide_bench.py &&
        step widepmc2 600 rocprofv3 --kernel-trace --pmc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum -d gpurun_out/widepmc2 -o run --output-format csv -- python scripts/wide_bench.py) || exit $? ;;
     cfg4) step cfg4 900 python benchmarks/bench_dq_pipeline.py --steps 5 --warmup 2 --json-out gpurun_out/cfg4.json ;;
+    cfg4r8) step cfg4r8 900 env DQ4ML_DQ_ROWS=8 python benchmarks/bench_dq_pipeline.py --steps 5 --warmup 2 ;;
+    cfg4r16) step cfg4r16 900 env DQ4ML_DQ_ROWS=16 python benchmarks/bench_dq_pipeline.py --steps 5 --warmup 2 ;;
     cfg5) step cfg5 900 python benchmarks/bench_wide.py --steps 3 --warmup 1 --json-out gpurun_out/cfg5.json ;;
     csv) step csv 600 python benchmarks/bench_csv_pipeline.py --steps 20 --warmup 3 --json-out gpurun_out/csv.json ;;
     cfg1) step cfg1 300 python benchmarks/bench_cpu_small.py --json-out gpurun_out/cfg1.json ;;
@@ -47,6 +49,8 @@ for s in $STEPS; do
     benchasync) step benchasync 600 python bench.py --steps 20 --warmup 3 --async ;;
     bench8th) step bench8th 600 python bench.py --steps 50 --warmup 5 --rows 1.25e7 ;;
     bench8thasync) step bench8thasync 600 python bench.py --steps 50 --warmup 5 --rows 1.25e7 --async ;;
+    bench8thrccl) step bench8thrccl 600 env DQ4ML_FORCE_COLLECTIVES=1 python bench.py --steps 50 --warmup 5 --rows 1.25e7 --async ;;
+    kprof8thrccl) (export TMPDIR=/tmp DQ4ML_FORCE_COLLECTIVES=1; step kprof8thrccl 600 rocprofv3 --kernel-trace --stats -d gpurun_out/kprof8thrccl -o run --output-format csv -- python bench.py --steps 20 --warmup 5 --rows 1.25e7 --async) || exit $? ;;
     asynctests) step asynctests 600 python -m pytest tests/test_gpu_async_fit.py -q -m gpu ;;
     fitprof) step fitprof 300 env N=1.25e7 python scripts/fit_profile.py ;;
     dist2) step dist2 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 scripts/dist_rehearsal.py ;;

@@ -54,7 +54,8 @@ def test_codegen_compiles(cpu_session, tmp_path):
         assert r.returncode == 0, r.stderr + "\n" + code
 
 
-def test_scan_fused_codegen_compiles(cpu_session, tmp_path):
+@pytest.mark.parametrize("nullable,fast", [((False, False), True), ((True, True), False), ((True, False), True)])
+def test_scan_fused_codegen_compiles(cpu_session, tmp_path, nullable, fast):
     """The fused scan + DQ kernel (ops/scanfuse.py) of the lab chain over a CSV relation whose
     facts say: int guest, double price, no nulls — compiles for gfx950, stores only the pruned
     outputs (guest, label) and the selection, and carries no null checks."""
@@ -70,7 +71,7 @@ def test_scan_fused_codegen_compiles(cpu_session, tmp_path):
     spark = cpu_session
     register_lab_rules(spark)
     schema = StructType([StructField("_c0", IntegerType(), True), StructField("_c1", DoubleType(), True)])
-    fused = {"kinds": [1, 0], "nullable": [False, False], "strict": False,
+    fused = {"kinds": [1, 0], "nullable": list(nullable), "strict": False,
              "opts": dict(_opt_args({"comment": 0}), sep=",", strict=False)}
     rel = CsvScanRelation(schema, lambda: None, fused, "Relation[csv]")
     df = DataFrame(rel, spark).withColumnRenamed("_c0", "guest").withColumnRenamed("_c1", "price")
@@ -93,9 +94,11 @@ def test_scan_fused_codegen_compiles(cpu_session, tmp_path):
     g = scanfuse._scan_gen(base, fused["nullable"])
     _, g, outputs, _ = dqvm.compile_chain(nodes, base, False, gen=g)
     slots = {k: g.slot(None, (k,)) for k in scanfuse._ScanPlan.SCAN_SLOTS}
-    src = scanfuse.kernel_source(g, fused["kinds"], fused["nullable"], g.used, fused["opts"], False, 256, slots)
-    assert [t for t in g.recipe if t[0] in ("out", "outvalid", "selout")] == [("out", 0), ("out", 1), ("selout",)]
-    assert "atomicOr((int*)" not in src  # no RaiseIfNull: price is null-free
+    src = scanfuse.kernel_source(g, fused["kinds"], fused["nullable"], g.used, fused["opts"], False, 256, slots,
+                                 True, fast)
+    if not any(nullable):
+        assert [t for t in g.recipe if t[0] in ("out", "outvalid", "selout")] == [("out", 0), ("out", 1), ("selout",)]
+    assert ("atomicOr((int*)" in src) == nullable[1]  # RaiseIfNull only when price may be null
     hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
     if not os.path.exists(hipcc):
         pytest.skip("no hipcc")
