@@ -89,13 +89,20 @@ struct SGeom {
 // bit that separates them.
 template <int CPL>
 __device__ __forceinline__ int swz16(int f) { return f ^ ((f >= 4 && f <= 11) ? CPL : 0); }
-// f32-storage kernel, lane (f = l & 31, h = l >> 5): every 16-lane group is one h, 16 distinct f&15
-__device__ __forceinline__ int swz32(int f) { return f & 15; }
+// f32-storage kernel, lane (f = l & 31, h = l >> 5): every 16-lane group is one h, 16 distinct f&15.
+// 64-row stages (CPL = 4, 256-B feature rows): slot = chunk ^ (f & 15); 32-row stages (CPL = 2,
+// 128-B feature rows, two features per 256-B bank row): slot = chunk ^ ((f >> 1) & 7), so the 16
+// lanes of a read group hit 16 distinct (f & 1, slot) 16-B bank slots.
+template <int CPL>
+__device__ __forceinline__ int swz32(int f) {
+  if constexpr (CPL == 4) return f & 15;
+  else return (f >> 1) & 7;
+}
 
 template <int TF, int CPL>
 __device__ __forceinline__ int swz(int f) {
   if constexpr (TF == 16) return swz16<CPL>(f);
-  else return swz32(f);
+  else return swz32<CPL>(f);
 }
 
 // Per-lane DMA source of every (tile, piece): the lane's feature (clamped into [0, d): padding
@@ -388,10 +395,11 @@ __global__ __launch_bounds__(kSB) void gram_stream_f64_kernel(GramArgs a) {
 // "32 float features" storage of the headline config).  Side sums Σw·x, Σw·x·y on the f32 VALU
 // from the unrounded features in both.
 // =============================================================================================
-template <int NT, int RING, int CMP, int XM>
+template <int NT, int RING, int CMP, int XM, int RS = 64>
 __global__ __launch_bounds__(kSB) void gram_stream_f32_kernel(GramArgs a) {
-  constexpr int RS = 64;
+  static_assert(RS == 64 || RS == 32, "f32 stream kernel: 64- or 32-row stages");
   typedef SGeom<float, 32, NT, RS, RING> G;
+  constexpr int HC = G::kCPF / 2;  // chunks per half stage: lane h reads rows [h * RS / 2, (h + 1) * RS / 2)
   constexpr int NPAIR = NT * (NT + 1) / 2;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -436,20 +444,20 @@ __global__ __launch_bounds__(kSB) void gram_stream_f32_kernel(GramArgs a) {
     for (int t = 0; t < NT; ++t) c32[t] = a32[t] = 0.0f;
     constexpr int RPS = CMP == 0 ? 4 : 8;  // rows per step: one f32x4 chunk / one bf16x8 fragment
 #pragma unroll
-    for (int i = 0; i < 32 / RPS; ++i) {
+    for (int i = 0; i < (RS / 2) / RPS; ++i) {
       float x[NT][RPS], w8[RPS], wy8[RPS];
 #pragma unroll
       for (int u = 0; u < RPS / 4; ++u) {
-        const int c = 8 * h + (RPS / 4) * i + u;
-        const int p = c ^ swz32(f);
+        const int c = HC * h + (RPS / 4) * i + u;
+        const int p = c ^ swz32<G::kCPF / 4>(f);
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
           const f32x4 v = *reinterpret_cast<const f32x4*>(st + t * G::kTileBytes + f * G::kFeatBytes + p * 16);
 #pragma unroll
           for (int j = 0; j < 4; ++j) x[t][4 * u + j] = fvalid[t] ? v[j] : 0.0f;
         }
-        const f32x4 w4 = *reinterpret_cast<const f32x4*>(stripe + 32 * h + RPS * i + 4 * u);
-        const f32x4 wy4 = *reinterpret_cast<const f32x4*>(stripe + 64 + 32 * h + RPS * i + 4 * u);
+        const f32x4 w4 = *reinterpret_cast<const f32x4*>(stripe + (RS / 2) * h + RPS * i + 4 * u);
+        const f32x4 wy4 = *reinterpret_cast<const f32x4*>(stripe + 64 + (RS / 2) * h + RPS * i + 4 * u);
 #pragma unroll
         for (int j = 0; j < 4; ++j) w8[4 * u + j] = w4[j], wy8[4 * u + j] = wy4[j];
       }
@@ -491,7 +499,7 @@ __global__ __launch_bounds__(kSB) void gram_stream_f32_kernel(GramArgs a) {
 #pragma unroll
     for (int t = 0; t < NT; ++t) cs[t] += (double)c32[t], ab[t] += (double)a32[t];
     wait_lgkm0();
-    if (++chunk == kFlush) {
+    if (++chunk == kFlush * 64 / RS) {  // f32 accumulation chunks of 1024 rows
       flush();
       chunk = 0;
     }
@@ -566,11 +574,37 @@ static void pick_ring(F&& f, K2 k2, int wb2, K3 k3, bool mfma_heavy = false) {
   return f(k2, wb2);
 }
 
+// f32 storage, 64 features (NT = 2): DQ4ML_GRAM_STREAM_F32RS=32 takes 32-row stages, so a deeper
+// DMA ring fits four waves per CU (ring 4: 3 stages, 28 KiB, in flight per wave instead of one
+// 17 KiB stage at ring 2).  Measured and kept off: config 4 (1.25e8 x 64, one box, one run)
+// 6.18 ms at 64 rows / ring 2, 6.45 at 32 / ring 3, 6.53 at 32 / ring 4 — the per-stage fixed
+// work (row scalars, waits) doubles and the extra bytes in flight buy nothing.
+static int f32_rs(int d) {
+  static const int rs = [] {
+    const char* e = getenv("DQ4ML_GRAM_STREAM_F32RS");
+    return e ? atoi(e) : 64;
+  }();
+  return (d > 32 && rs == 32) ? 32 : 64;
+}
+
+template <int NT, int CMP, int XM, typename F>
+static void f32_rs32(F&& f) {
+  const char* e = getenv("DQ4ML_GRAM_STREAM_RING");
+  const int want = e ? atoi(e) : 4;
+  if (want >= 4 && kSW * SGeom<float, 32, NT, 32, 4>::kWaveBytes <= kLdsMax)
+    return f(gram_stream_f32_kernel<NT, 4, CMP, XM, 32>, SGeom<float, 32, NT, 32, 4>::kWaveBytes);
+  return f(gram_stream_f32_kernel<NT, 3, CMP, XM, 32>, SGeom<float, 32, NT, 32, 3>::kWaveBytes);
+}
+
 template <typename F>
 static void with_stream_kernel(int mode, int xdt, int d, int xm, F&& f) {
   if (mode == GRAM_F32 || mode == GRAM_BF16) {
     if (xdt != DT_F32) throw std::invalid_argument("gram_stream(f32/bf16): needs f32 features");
     const int NT = (d + 31) / 32;
+    if (NT == 2 && f32_rs(d) == 32) {
+      if (mode == GRAM_F32) return xm ? f32_rs32<2, 0, 1>(f) : f32_rs32<2, 0, 0>(f);
+      return xm ? f32_rs32<2, 1, 1>(f) : f32_rs32<2, 1, 0>(f);
+    }
 #define DQ_SF32(NTV, CMPV, XMV)                                                                        \
   return pick_ring<SGeom<float, 32, NTV, 64, 3>>(f, gram_stream_f32_kernel<NTV, 2, CMPV, XMV>,         \
                                                  SGeom<float, 32, NTV, 64, 2>::kWaveBytes,              \
@@ -613,6 +647,7 @@ static void with_stream_kernel(int mode, int xdt, int d, int xm, F&& f) {
 }
 
 static int stream_rs(int mode, int xdt, int d) {
+  if (mode == GRAM_F32 || mode == GRAM_BF16) return f32_rs(d);
   return (mode == GRAM_F64 && xdt == DT_F64 && d > 32) ? 32 : 64;
 }
 

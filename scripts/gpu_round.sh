@@ -31,6 +31,8 @@ for s in $STEPS; do
        step widepmc1 600 rocprofv3 --kernel-trace --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE -d gpurun_out/widepmc1 -o run --output-format csv -- python scripts/wide_bench.py &&
        step widepmc2 600 rocprofv3 --kernel-trace --pmc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum -d gpurun_out/widepmc2 -o run --output-format csv -- python scripts/wide_bench.py) || exit $? ;;
     cfg4) step cfg4 900 python benchmarks/bench_dq_pipeline.py --steps 5 --warmup 2 --json-out gpurun_out/cfg4.json ;;
+    cfg4rs64) step cfg4rs64 900 env DQ4ML_GRAM_STREAM_F32RS=64 python benchmarks/bench_dq_pipeline.py --steps 5 --warmup 2 ;;
+    cfg4ring3) step cfg4ring3 900 env DQ4ML_GRAM_STREAM_RING=3 python benchmarks/bench_dq_pipeline.py --steps 5 --warmup 2 ;;
     cfg4r8) step cfg4r8 900 env DQ4ML_DQ_ROWS=8 python benchmarks/bench_dq_pipeline.py --steps 5 --warmup 2 ;;
     cfg4r16) step cfg4r16 900 env DQ4ML_DQ_ROWS=16 python benchmarks/bench_dq_pipeline.py --steps 5 --warmup 2 ;;
     cfg5) step cfg5 900 python benchmarks/bench_wide.py --steps 3 --warmup 1 --json-out gpurun_out/cfg5.json ;;
@@ -51,6 +53,10 @@ for s in $STEPS; do
     bench8thasync) step bench8thasync 600 python bench.py --steps 50 --warmup 5 --rows 1.25e7 --async ;;
     bench8thrccl) step bench8thrccl 600 env DQ4ML_FORCE_COLLECTIVES=1 python bench.py --steps 50 --warmup 5 --rows 1.25e7 --async ;;
     kprof8thrccl) (export TMPDIR=/tmp DQ4ML_FORCE_COLLECTIVES=1; step kprof8thrccl 600 rocprofv3 --kernel-trace --stats -d gpurun_out/kprof8thrccl -o run --output-format csv -- python bench.py --steps 20 --warmup 5 --rows 1.25e7 --async) || exit $? ;;
+    hostov) step hostov 300 python scripts/host_overhead.py && step hostovrccl 300 env DQ4ML_FORCE_COLLECTIVES=1 python scripts/host_overhead.py ;;
+    f32pmc) (export TMPDIR=/tmp
+       step f32pmc1 300 timeout -s KILL 240 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_SALU GRBM_GUI_ACTIVE -d gpurun_out/f32pmc1 -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --dtype fp32 &&
+       step f32pmc2 300 timeout -s KILL 240 rocprofv3 --kernel-trace --pmc SQ_WAIT_INST_LDS SQ_INSTS_MFMA SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_MISC GRBM_GUI_ACTIVE -d gpurun_out/f32pmc2 -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --dtype fp32) || exit $? ;;
     asynctests) step asynctests 600 python -m pytest tests/test_gpu_async_fit.py -q -m gpu ;;
     fitprof) step fitprof 300 env N=1.25e7 python scripts/fit_profile.py ;;
     dist2) step dist2 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 scripts/dist_rehearsal.py ;;

@@ -22,13 +22,14 @@ def swz16(f, cpl):  # f64 kernel (16-feature tiles), gram_stream.hip swz16<CPL>
     return f ^ (cpl if 4 <= f <= 11 else 0)
 
 
-def swz32(f):  # exact-f32 kernel (32-feature tiles), gram_stream.hip swz32
-    return f & 15
+def swz32(f, cpl=4):  # f32-storage kernels (32-feature tiles), gram_stream.hip swz32<CPL>
+    return f & 15 if cpl == 4 else (f >> 1) & 7
 
 
 # (name, element bytes, tile features TF, stage rows RS)
 VARIANTS = [("f64 storage, d<=32", 8, 16, 64), ("f64 storage, d>32", 8, 16, 32),
-            ("f32 storage, f64 stats", 4, 16, 64), ("f32 storage, exact-f32 stats", 4, 32, 64)]
+            ("f32 storage, f64 stats", 4, 16, 64), ("f32 storage, exact-f32 stats", 4, 32, 64),
+            ("f32 storage, 64 features, 32-row stages", 4, 32, 32)]
 
 
 def _geom(esz, tf, rs):
@@ -38,7 +39,8 @@ def _geom(esz, tf, rs):
 
 
 def _g(tf, cpl):
-    return (lambda f: swz16(f, cpl)) if tf == 16 else swz32
+    # f32 kernels: the swizzle is keyed by chunks-per-feature / 4 (4 at 64 rows, 2 at 32 rows)
+    return (lambda f: swz16(f, cpl)) if tf == 16 else (lambda f: swz32(f, cpl // 2))
 
 
 def _lane_chunks(lane, tf, cpl):
