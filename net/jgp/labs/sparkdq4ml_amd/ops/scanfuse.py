@@ -160,37 +160,78 @@ def kernel_source(g, kinds, nullable, used, opts: dict, strict: bool, head: int,
          f"(unsigned char){int(bool(opts['trim_lead']))}, (unsigned char){int(bool(opts['trim_trail']))}, "
          f"(unsigned char){len(nv)}, (unsigned char){int(strict)}, "
          f"{{{', '.join(str(x) for x in (nv + [0] * (16 - len(nv))))}}}}}")
-    parse = []
-    for c in range(ncols):
-        k = int(kinds[c])
+    def field_code(c: int, swar: bool) -> str:
+        if swar:  # short line in registers (csv_line16 / csv_swar_field); > 8-byte fields walk the stage
+            return (f"    double fzd{c} = 0.0; long long fzl{c} = 0; bool fzg{c} = false; int fzy{c} = C_NULL;\n"
+                    f"    if (pos <= len && line) {{\n"
+                    f"      const unsigned int rest = sepm >> pos;\n"
+                    f"      const int q = rest ? pos + (int)__builtin_ctz(rest) : len;\n"
+                    f"      if (q - pos <= 8) {{\n"
+                    f"        if (!csv_swar_field(csv_bytes8(lo, hi, pos), q - pos, fzd{c}, fzl{c}, fzy{c})) bad = true;\n"
+                    f"      }} else {{\n"
+                    f"        int ps = start + pos;\n"
+                    f"        if (!csv_field_fast(B, 0, ps, end, O.sep, fzd{c}, fzl{c}, fzy{c})) bad = true;\n"
+                    f"      }}\n"
+                    f"      pos = q + 1;\n"
+                    f"    }}\n"
+                    f"    bool fzk{c} = fzy{c} != C_NULL && fzy{c} != C_STRING;\n")
         if fast_only:
-            parse.append(f"    double fzd{c} = 0.0; long long fzl{c} = 0; bool fzg{c} = false; int fzy{c} = C_NULL;\n"
-                         f"    if (pos <= end && line && !csv_field_fast(B, bias, pos, end, O.sep, fzd{c}, fzl{c}, fzy{c})) bad = true;\n"
-                         f"    bool fzk{c} = fzy{c} != C_NULL && fzy{c} != C_STRING;\n")
-        else:
-            parse.append(f"    double fzd{c} = 0.0; long long fzl{c} = 0; bool fzg{c} = false; int fzy{c} = C_NULL;\n"
-                         f"    if (pos <= end && line) fzy{c} = csv_field(B, bias, pos, end, O, fzd{c}, fzl{c}, slow, fzg{c}, malformed);\n"
-                         f"    bool fzk{c} = fzy{c} != C_NULL && fzy{c} != C_STRING;\n")
-        if strict:
-            parse.append(f"    if (fzy{c} != C_NULL && !csv_conforms(fzy{c}, {k})) {{ malformed = true; fzk{c} = false; }}\n")
-        else:
-            parse.append(f"    bad |= line && fzy{c} != C_NULL && !csv_conforms(fzy{c}, {k});\n")
-        if k != 2:
-            parse.append(f"    slow |= fzg{c};\n")
-    parse.append("    if (malformed) {" + " ".join(f"fzk{c} = false;" for c in range(ncols)) + " }\n")
-    for c in range(ncols):
-        if not nullable[c]:
-            parse.append(f"    bad |= line && !fzk{c};\n")
-    for c in sorted(used):
-        ct = used[c]
-        val = _VALUE[int(kinds[c])].format(c=c)
-        parse.append(f"    const {ct} fzf{c} = fzk{c} ? ({ct})({val}) : ({ct})0;\n")
-        if nullable[c]:
-            parse.append(f"    const bool fzm{c} = fzk{c};\n")
+            return (f"    double fzd{c} = 0.0; long long fzl{c} = 0; bool fzg{c} = false; int fzy{c} = C_NULL;\n"
+                    f"    if (pos <= end && line && !csv_field_fast(B, bias, pos, end, O.sep, fzd{c}, fzl{c}, fzy{c})) bad = true;\n"
+                    f"    bool fzk{c} = fzy{c} != C_NULL && fzy{c} != C_STRING;\n")
+        return (f"    double fzd{c} = 0.0; long long fzl{c} = 0; bool fzg{c} = false; int fzy{c} = C_NULL;\n"
+                f"    if (pos <= end && line) fzy{c} = csv_field(B, bias, pos, end, O, fzd{c}, fzl{c}, slow, fzg{c}, malformed);\n"
+                f"    bool fzk{c} = fzy{c} != C_NULL && fzy{c} != C_STRING;\n")
+
+    def parse_code(swar: bool) -> str:
+        parse = []
+        for c in range(ncols):
+            k = int(kinds[c])
+            parse.append(field_code(c, swar))
+            if strict:
+                parse.append(f"    if (fzy{c} != C_NULL && !csv_conforms(fzy{c}, {k})) {{ malformed = true; fzk{c} = false; }}\n")
+            else:
+                parse.append(f"    bad |= line && fzy{c} != C_NULL && !csv_conforms(fzy{c}, {k});\n")
+            if k != 2:
+                parse.append(f"    slow |= fzg{c};\n")
+        parse.append("    if (malformed) {" + " ".join(f"fzk{c} = false;" for c in range(ncols)) + " }\n")
+        for c in range(ncols):
+            if not nullable[c]:
+                parse.append(f"    bad |= line && !fzk{c};\n")
+        for c in sorted(used):
+            ct = used[c]
+            val = _VALUE[int(kinds[c])].format(c=c)
+            parse.append(f"    const {ct} fzf{c} = fzk{c} ? ({ct})({val}) : ({ct})0;\n")
+            if nullable[c]:
+                parse.append(f"    const bool fzm{c} = fzk{c};\n")
+        return "".join(parse)
+
+    # SWAR rows: fast-only files whose separator cannot be part of a number
+    sep_c = opts.get("sep", ",")
+    swar = fast_only and sep_c not in "0123456789.+-" and os.environ.get("DQ4ML_SCAN_SWAR", "1") != "0"
     body = "\n".join("    " + ln.strip() for ln in g.lines).replace("P[", "p[")
     stores = "".join(f"    (({t}*)p[{s}])[li] = ({t})({v});\n" for t, v, s in g.stores)
     comment = int(opts["comment"])
     H, W = int(head), WINDOW
+    swar_row = "" if not swar else f"""
+// a line of at most 16 bytes in the LDS stage: held in two 64-bit registers, fields cut by the
+// separator bitmask, numeric fields converted SWAR (csv_parse_dev.h) — no per-byte loop
+__device__ __forceinline__ void dq_row_swar(const unsigned char* B, int start, int end, long long li,
+                                            void* const* p, unsigned int* vflag) {{
+    const CsvOpts O = {o};
+    const int len = end - start;
+    const bool line = len > 0 && !({comment} && B[start] == {comment});
+    unsigned long long lo, hi;
+    csv_line16(B, start, lo, hi);
+    const unsigned int sepm = csv_eq16(lo, hi, O.sep) & ((1u << len) - 1u);
+    int pos = 0;
+    bool slow = false, malformed = false, bad = false;
+{parse_code(True)}    bad |= slow;
+    if (bad) atomicOr(vflag, 1u);
+    bool live = line;
+{body}
+{stores}}}
+"""
     return (header_text() + f"""
 using namespace dq4ml_csv;
 typedef unsigned int csv_u32x4 __attribute__((ext_vector_type(4)));
@@ -203,12 +244,12 @@ __device__ __forceinline__ void dq_row(PB B, IT bias, IT start, IT end, long lon
     const bool line = end > start && !({comment} && B[start - bias] == {comment});
     IT pos = start;
     bool slow = false, malformed = false, bad = false;
-{''.join(parse)}    bad |= slow;
+{parse_code(False)}    bad |= slow;
     if (bad) atomicOr(vflag, 1u);
     bool live = line;
 {body}
 {stores}}}
-
+{swar_row}
 extern "C" __global__ __launch_bounds__(256) {_wpe(fast_only)}void {ENTRY}(void* const* P, long long n) {{
   void* p[{ns}];
 #pragma unroll
@@ -334,7 +375,8 @@ extern "C" __global__ __launch_bounds__(256) {_wpe(fast_only)}void {ENTRY}(void*
       if (li >= nalloc) {{
         atomicOr(vflag, 2u);
       }} else if (start >= sbase) {{
-        dq_row(stage, 0, (int)(start - sbase), (int)(end - sbase), li, p, vflag);  // 32-bit stage positions
+        const int s0 = (int)(start - sbase), e0 = (int)(end - sbase);  // 32-bit stage positions
+        {"if (e0 - s0 <= 16) dq_row_swar(stage, s0, e0, li, p, vflag); else " if swar else ""}dq_row(stage, 0, s0, e0, li, p, vflag);
       }} else {{
         dq_row(b, 0ll, start, end, li, p, vflag);
       }}
