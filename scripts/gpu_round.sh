@@ -57,10 +57,13 @@ for s in $STEPS; do
     f32pmc) (export TMPDIR=/tmp
        step f32pmc1 300 timeout -s KILL 240 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_SALU GRBM_GUI_ACTIVE -d gpurun_out/f32pmc1 -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --dtype fp32 &&
        step f32pmc2 300 timeout -s KILL 240 rocprofv3 --kernel-trace --pmc SQ_WAIT_INST_LDS SQ_INSTS_MFMA SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_MISC GRBM_GUI_ACTIVE -d gpurun_out/f32pmc2 -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --dtype fp32) || exit $? ;;
+    reserveab) for r in 0 1 8 0 1 8; do step res$r 300 env DQ4ML_GRAM_RESERVE=$r python bench.py --steps 50 --warmup 5 --rows 1.25e7 --async; done
+       for r in 0 1 8; do step resbig$r 300 env DQ4ML_GRAM_RESERVE=$r python bench.py --steps 20 --warmup 3; done ;;
     asynctests) step asynctests 600 python -m pytest tests/test_gpu_async_fit.py -q -m gpu ;;
     fitprof) step fitprof 300 env N=1.25e7 python scripts/fit_profile.py ;;
     dist2) step dist2 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 scripts/dist_rehearsal.py ;;
     benchf32) step benchf32 600 python bench.py --steps 10 --warmup 2 --dtype fp32 ;;
+    benchf32r3) step benchf32r3 600 env DQ4ML_GRAM_STREAM_RING=3 python bench.py --steps 10 --warmup 2 --dtype fp32 ;;
     benchf64) step benchf64 600 python bench.py --steps 10 --warmup 2 --dtype fp64 ;;
     benchf64old) step benchf64old 600 env DQ4ML_GRAM_STREAM=0 python bench.py --steps 10 --warmup 2 --dtype fp64 ;;
     benchf64s32) step benchf64s32 600 python bench.py --steps 10 --warmup 2 --dtype fp64 --storage fp32 ;;
