@@ -584,16 +584,18 @@ static int f32_rs(int d) {
     const char* e = getenv("DQ4ML_GRAM_STREAM_F32RS");
     return e ? atoi(e) : 64;
   }();
-  return (d > 32 && rs == 32) ? 32 : 64;
+  (void)d;
+  return rs == 32 ? 32 : 64;
 }
 
 template <int NT, int CMP, int XM, typename F>
 static void f32_rs32(F&& f) {
   const char* e = getenv("DQ4ML_GRAM_STREAM_RING");
-  const int want = e ? atoi(e) : 4;
+  const int want = e ? atoi(e) : (CMP == 0 ? 2 : 4);
   if (want >= 4 && kSW * SGeom<float, 32, NT, 32, 4>::kWaveBytes <= kLdsMax)
     return f(gram_stream_f32_kernel<NT, 4, CMP, XM, 32>, SGeom<float, 32, NT, 32, 4>::kWaveBytes);
-  return f(gram_stream_f32_kernel<NT, 3, CMP, XM, 32>, SGeom<float, 32, NT, 32, 3>::kWaveBytes);
+  if (want == 3) return f(gram_stream_f32_kernel<NT, 3, CMP, XM, 32>, SGeom<float, 32, NT, 32, 3>::kWaveBytes);
+  return f(gram_stream_f32_kernel<NT, 2, CMP, XM, 32>, SGeom<float, 32, NT, 32, 2>::kWaveBytes);
 }
 
 template <typename F>
@@ -601,7 +603,11 @@ static void with_stream_kernel(int mode, int xdt, int d, int xm, F&& f) {
   if (mode == GRAM_F32 || mode == GRAM_BF16) {
     if (xdt != DT_F32) throw std::invalid_argument("gram_stream(f32/bf16): needs f32 features");
     const int NT = (d + 31) / 32;
-    if (NT == 2 && f32_rs(d) == 32) {
+    if (f32_rs(d) == 32) {
+      if (NT == 1) {
+        if (mode == GRAM_F32) return xm ? f32_rs32<1, 0, 1>(f) : f32_rs32<1, 0, 0>(f);
+        return xm ? f32_rs32<1, 1, 1>(f) : f32_rs32<1, 1, 0>(f);
+      }
       if (mode == GRAM_F32) return xm ? f32_rs32<2, 0, 1>(f) : f32_rs32<2, 0, 0>(f);
       return xm ? f32_rs32<2, 1, 1>(f) : f32_rs32<2, 1, 0>(f);
     }

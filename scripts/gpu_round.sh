@@ -65,6 +65,8 @@ for s in $STEPS; do
     dist2) step dist2 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 scripts/dist_rehearsal.py ;;
     benchf32) step benchf32 600 python bench.py --steps 10 --warmup 2 --dtype fp32 ;;
     benchf32r3) step benchf32r3 600 env DQ4ML_GRAM_STREAM_RING=3 python bench.py --steps 10 --warmup 2 --dtype fp32 ;;
+    benchf32rs) for r in 2 3 4; do step benchf32rs32r$r 600 env DQ4ML_GRAM_STREAM_F32RS=32 DQ4ML_GRAM_STREAM_RING=$r python bench.py --steps 10 --warmup 2 --dtype fp32; done
+       step benchs32rs32 600 env DQ4ML_GRAM_STREAM_F32RS=32 python bench.py --steps 10 --warmup 2 --dtype bf16 --storage fp32 ;;
     benchf64) step benchf64 600 python bench.py --steps 10 --warmup 2 --dtype fp64 ;;
     benchf64old) step benchf64old 600 env DQ4ML_GRAM_STREAM=0 python bench.py --steps 10 --warmup 2 --dtype fp64 ;;
     benchf64s32) step benchf64s32 600 python bench.py --steps 10 --warmup 2 --dtype fp64 --storage fp32 ;;
