@@ -60,6 +60,8 @@ for s in $STEPS; do
        step f32pmc2 300 timeout -s KILL 240 rocprofv3 --kernel-trace --pmc SQ_WAIT_INST_LDS SQ_INSTS_MFMA SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_MISC GRBM_GUI_ACTIVE -d gpurun_out/f32pmc2 -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --dtype fp32) || exit $? ;;
     reserveab) for r in 0 1 8 0 1 8; do step res$r 300 env DQ4ML_GRAM_RESERVE=$r python bench.py --steps 50 --warmup 5 --rows 1.25e7 --async; done
        for r in 0 1 8; do step resbig$r 300 env DQ4ML_GRAM_RESERVE=$r python bench.py --steps 20 --warmup 3; done ;;
+    mfmapeak) step mfmapeak 120 ./scripts/mfma_peak &&
+       (export TMPDIR=/tmp; step mfmapeakpmc 120 timeout -s KILL 100 rocprofv3 --kernel-trace --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_BUSY_CYCLES -d gpurun_out/mfmapeakpmc -o run --output-format csv -- ./scripts/mfma_peak) || exit $? ;;
     asynctests) step asynctests 600 python -m pytest tests/test_gpu_async_fit.py -q -m gpu ;;
     fitprof) step fitprof 300 env N=1.25e7 python scripts/fit_profile.py ;;
     dist2) step dist2 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 scripts/dist_rehearsal.py ;;
