@@ -128,10 +128,6 @@ def _wpe(fast_only: bool = False) -> str:
 _VALUE = {1: "(int)fzl{c}", 2: "fzl{c}", 0: "fzd{c}", 3: "(fzd{c} != 0.0)"}
 
 
-def _c_char(v: int) -> str:
-    return str(int(v))
-
-
 def kernel_source(g, kinds, nullable, used, opts: dict, strict: bool, head: int, slots: dict,
                   lookback: bool = True, fast_only: bool = False) -> str:
     """Source of the fused kernel.
@@ -155,8 +151,8 @@ def kernel_source(g, kinds, nullable, used, opts: dict, strict: bool, head: int,
     ncols = len(kinds)
     ns = len(g.ptrs)
     nv = list(opts.get("null_value", "").encode())
-    o = (f"{{(unsigned char){_c_char(ord(opts.get('sep', ',')))}, (unsigned char){_c_char(opts['quote'])}, "
-         f"(unsigned char){_c_char(opts['escape'])}, (unsigned char){_c_char(opts['comment'])}, "
+    o = (f"{{(unsigned char){ord(opts.get('sep', ','))}, (unsigned char){int(opts['quote'])}, "
+         f"(unsigned char){int(opts['escape'])}, (unsigned char){int(opts['comment'])}, "
          f"(unsigned char){int(bool(opts['trim_lead']))}, (unsigned char){int(bool(opts['trim_trail']))}, "
          f"(unsigned char){len(nv)}, (unsigned char){int(strict)}, "
          f"{{{', '.join(str(x) for x in (nv + [0] * (16 - len(nv))))}}}}}")
@@ -557,5 +553,4 @@ def try_fused_scan(nodes, rel, plan, session):
     schema = plan.schema()
     cols = [ColumnData(fd.dataType, oo[0], oo[1], dict(fd.metadata), [check] if check is not None else [])
             for fd, oo in zip(schema.fields, outs)]
-    keep = (offs, ptrs, buf)  # noqa: F841 (stream-ordered lifetimes: the caching allocator handles it)
     return Table(schema, cols, nalloc, sel_out, dev)
