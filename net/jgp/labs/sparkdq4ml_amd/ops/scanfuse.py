@@ -59,13 +59,50 @@ def head_bytes(mean_line: float) -> int:
     return h
 
 
-def _ticket(lookback: bool) -> str:
+def ticket_mode() -> str:
+    """How a look-back block picks its window (``DQ4ML_SCAN_TICKET``):
+
+    * ``xcd`` (default): one dispatch-order ticket counter per ``blockIdx.x % 8`` class (the
+      8 XCDs take workgroups round-robin), on separate cache lines; window = ticket * 8 + class.
+    * ``global``: one counter for the grid — strict dispatch order, but every block's ticket
+      is an atomic on ONE address, serialised at the memory side: 0.48 of 0.75 ms in a
+      1e8-line scan with the per-line work ablated (``scripts/scan_ablation.py``).
+    * ``none``: window = ``blockIdx.x`` (relies on in-order dispatch per XCD).
+
+    Either way a predecessor that never publishes ends in the bounded spin (vflag 4, a loud
+    fact-check failure), never a hang."""
+    m = os.environ.get("DQ4ML_SCAN_TICKET", "xcd")
+    if m not in ("xcd", "global", "none"):
+        raise ValueError(f"DQ4ML_SCAN_TICKET={m!r}: expected xcd, global or none")
+    return m
+
+
+# status words after the per-window ones: the global ticket, then 8 per-class tickets 128 B apart
+TICKET_WORDS = 1 + 8 * 16
+
+
+def _ticket(lookback: bool, mode: str = "xcd") -> str:
     if not lookback:
         return "  const long long blk = blockIdx.x;"
-    return """  // window = dispatch-order ticket: every predecessor window's block is already resident, so
+    if mode == "none":
+        return """  DQG unsigned long long* status = (DQG unsigned long long*)offs;
+  const long long blk = blockIdx.x;"""
+    if mode == "global":
+        return """  // window = dispatch-order ticket: every predecessor window's block is already resident, so
   // the look-back below always makes progress
-  unsigned long long* status = (unsigned long long*)offs;
-  if (tid == 0) sblk = (long long)atomicAdd(status + gridDim.x, 1ull);
+  DQG unsigned long long* status = (DQG unsigned long long*)offs;
+  if (tid == 0)
+    sblk = (long long)__hip_atomic_fetch_add(status + gridDim.x, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  const long long blk = sblk;"""
+    return """  // window = per-XCD dispatch-order ticket * 8 + class: one counter per blockIdx.x % 8 class
+  // (the XCD round-robin), so no single address serialises every block's ticket
+  DQG unsigned long long* status = (DQG unsigned long long*)offs;
+  if (tid == 0) {
+    const unsigned int x = blockIdx.x & 7u;
+    sblk = (long long)__hip_atomic_fetch_add(status + gridDim.x + 1 + 16 * x, 1ull, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT) * 8 + x;
+  }
   __syncthreads();
   const long long blk = sblk;"""
 
@@ -107,7 +144,7 @@ def _lookback(lookback: bool) -> str:
       j0 -= 64;
     }
     if (lane == 0) {
-      if (stuck) atomicOr(vflag, 4u);
+      if (stuck) dq_flag(vflag, 4u);
       __hip_atomic_store(status + blk, (2ull << 62) | (unsigned long long)(pre + cnt), __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_AGENT);
       sgl0 = pre;
@@ -129,7 +166,7 @@ _VALUE = {1: "(int)fzl{c}", 2: "fzl{c}", 0: "fzd{c}", 3: "(fzd{c} != 0.0)"}
 
 
 def kernel_source(g, kinds, nullable, used, opts: dict, strict: bool, head: int, slots: dict,
-                  lookback: bool = True, fast_only: bool = False) -> str:
+                  lookback: bool = True, fast_only: bool = False, ticket: str = "xcd") -> str:
     """Source of the fused kernel.
 
     ``g``: the dqvm generator after lowering the chain (its ``lines`` use ``f<c>`` / ``m<c>`` for
@@ -140,9 +177,9 @@ def kernel_source(g, kinds, nullable, used, opts: dict, strict: bool, head: int,
 
     ``lookback``: single pass — each block takes a ticket (its window, in dispatch order),
     publishes its line count and finds its first line index by decoupled look-back over its
-    predecessors' published counts (``offs`` is then the zeroed ``[nb + 1]`` status array, the
-    ticket counter last).  Otherwise ``offs`` holds the exclusive scan of ``csv_count_kernel``'s
-    per-window counts (two passes over the bytes).
+    predecessors' published counts (``offs`` is then the zeroed ``[nb + TICKET_WORDS]`` status
+    array, the ticket counters last; ``ticket``: see ``ticket_mode``).  Otherwise ``offs`` holds
+    the exclusive scan of ``csv_count_kernel``'s per-window counts (two passes over the bytes).
 
     ``fast_only``: the earlier scan parsed every field on the numeric fast path (plain dialect):
     only that path is compiled in — the general parser's registers (~60 VGPRs) leave the kernel
@@ -205,8 +242,15 @@ def kernel_source(g, kinds, nullable, used, opts: dict, strict: bool, head: int,
     # SWAR rows: fast-only files whose separator cannot be part of a number
     sep_c = opts.get("sep", ",")
     swar = fast_only and sep_c not in "0123456789.+-" and os.environ.get("DQ4ML_SCAN_SWAR", "1") != "0"
-    body = "\n".join("    " + ln.strip() for ln in g.lines).replace("P[", "p[")
-    stores = "".join(f"    (({t}*)p[{s}])[li] = ({t})({v});\n" for t, v, s in g.stores)
+    body = ("\n".join("    " + ln.strip() for ln in g.lines).replace("P[", "p[")
+            .replace("atomicOr((int*)p[", "dq_flag((unsigned int*)p["))
+    stores = "".join(f"    ((DQG {t}*)p[{s}])[li] = ({t})({v});\n" for t, v, s in g.stores)
+    # diagnostic ablation builds (wrong results; scripts/scan_ablation.py), bit flags: 1 no per-line
+    # work, 2 no stores, 4 no look-back, 8 no line-end scatter / line loop, 16 no ticket, 32 no LDS
+    # staging stores
+    abl = int(os.environ.get("DQ4ML_SCAN_ABL", "0"))
+    if abl & 2:
+        stores = "".join(f"    if (li == -7) ((DQG {t}*)p[{s}])[0] = ({t})({v});\n" for t, v, s in g.stores)
     comment = int(opts["comment"])
     H, W = int(head), WINDOW
     swar_row = "" if not swar else f"""
@@ -223,7 +267,7 @@ __device__ __forceinline__ void dq_row_swar(const unsigned char* B, int start, i
     int pos = 0;
     bool slow = false, malformed = false, bad = false;
 {parse_code(True)}    bad |= slow;
-    if (bad) atomicOr(vflag, 1u);
+    if (bad) dq_flag(vflag, 1u);
     bool live = line;
 {body}
 {stores}}}
@@ -231,6 +275,13 @@ __device__ __forceinline__ void dq_row_swar(const unsigned char* B, int start, i
     return (header_text() + f"""
 using namespace dq4ml_csv;
 typedef unsigned int csv_u32x4 __attribute__((ext_vector_type(4)));
+// every global access names the global address space: generic (flat) accesses count in both
+// the VM and the LDS wait counters, so each LDS read after a flat store would wait for that store
+#define DQG __attribute__((address_space(1)))
+
+__device__ __forceinline__ void dq_flag(unsigned int* f, unsigned int v) {{
+  __hip_atomic_fetch_or((DQG unsigned int*)f, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}}
 
 // one line: parse every field into registers, run the DQ chain, store the needed outputs at li
 template <typename PB, typename IT>
@@ -241,7 +292,7 @@ __device__ __forceinline__ void dq_row(PB B, IT bias, IT start, IT end, long lon
     IT pos = start;
     bool slow = false, malformed = false, bad = false;
 {parse_code(False)}    bad |= slow;
-    if (bad) atomicOr(vflag, 1u);
+    if (bad) dq_flag(vflag, 1u);
     bool live = line;
 {body}
 {stores}}}
@@ -250,19 +301,19 @@ extern "C" __global__ __launch_bounds__(256) {_wpe(fast_only)}void {ENTRY}(void*
   void* p[{ns}];
 #pragma unroll
   for (int i = 0; i < {ns}; ++i) p[i] = P[i];
-  const unsigned char* __restrict__ b = (const unsigned char*)p[{slots['buf']}];
-  const long long* __restrict__ offs = (const long long*)p[{slots['offs']}];
+  const DQG unsigned char* __restrict__ b = (const DQG unsigned char*)p[{slots['buf']}];
+  const DQG long long* __restrict__ offs = (const DQG long long*)p[{slots['offs']}];
   const long long nalloc = (long long)p[{slots['nalloc']}];
   const bool trailing = (long long)p[{slots['trailing']}] != 0;
   unsigned int* vflag = (unsigned int*)p[{slots['vflag']}];
   __shared__ __attribute__((aligned(16))) unsigned char stage[{H} + {W} + 16];
   __shared__ unsigned short lend[{CAP} + 1];
   __shared__ int wtot[4];
-  __shared__ long long sprev0, sblk, sgl0;
+  __shared__ long long sstart0, sblk, sgl0;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-{_ticket(lookback)}
+{_ticket(lookback, ticket if not abl & 16 else "none")}
   const long long a = (long long)(reinterpret_cast<unsigned long long>(b) & 15ull);
-  const unsigned char* ab = b - a;                         // 16-byte aligned view
+  const DQG unsigned char* ab = b - a;                     // 16-byte aligned view
   const long long wbase = blk * {W} - a;                    // buffer index of window byte 0
   const long long sbase = wbase - {H};                     // buffer index of stage[0]
   const long long tb = wbase + 64 * tid;                    // this thread's 64 window bytes
@@ -272,8 +323,8 @@ extern "C" __global__ __launch_bounds__(256) {_wpe(fast_only)}void {ENTRY}(void*
   for (int j = 0; j < 4; ++j) {{
     const long long gi = tb + 16 * j;
     csv_u32x4 v = {{0u, 0u, 0u, 0u}};
-    if (gi < n && gi + 16 > 0) v = *reinterpret_cast<const csv_u32x4*>(ab + gi + a);
-    *reinterpret_cast<csv_u32x4*>(stage + {H} + 64 * tid + 16 * j) = v;
+    if (gi < n && gi + 16 > 0) v = *reinterpret_cast<const DQG csv_u32x4*>(ab + gi + a);
+    {"if (v[0] == 0x7F7F7F7Fu && v[1] == 3u) " if abl & 32 else ""}*reinterpret_cast<csv_u32x4*>(stage + {H} + 64 * tid + 16 * j) = v;
 #pragma unroll
     for (int w = 0; w < 4; ++w) {{
       cr |= (unsigned long long)byte_eq4(v[w], 0x0D0D0D0Du) << (16 * j + 4 * w);
@@ -283,7 +334,7 @@ extern "C" __global__ __launch_bounds__(256) {_wpe(fast_only)}void {ENTRY}(void*
   for (int gq = tid; gq < {H // 16} + 1; gq += 256) {{  // head granules + one tail granule
     const long long gi = gq < {H // 16} ? sbase + 16 * gq : wbase + {W};
     csv_u32x4 v = {{0u, 0u, 0u, 0u}};
-    if (gi < n && gi + 16 > 0) v = *reinterpret_cast<const csv_u32x4*>(ab + gi + a);
+    if (gi < n && gi + 16 > 0) v = *reinterpret_cast<const DQG csv_u32x4*>(ab + gi + a);
     *reinterpret_cast<csv_u32x4*>(stage + (gq < {H // 16} ? 16 * gq : {H} + {W})) = v;
   }}
   {{
@@ -298,6 +349,9 @@ extern "C" __global__ __launch_bounds__(256) {_wpe(fast_only)}void {ENTRY}(void*
   __syncthreads();
   const unsigned long long prev_cr = (tb >= 1 && tb - 1 < n && stage[{H} + 64 * tid - 1] == '\\r') ? 1ull : 0ull;
   unsigned long long m = cr | (lf & ~((cr << 1) | prev_cr));
+  // terminators that are the CR of a CR LF: the next line starts one byte later (bit 15 of the
+  // LDS line-end word), so no line reads stage bytes to find its start
+  const unsigned long long crlf = cr & ((lf >> 1) | ((unsigned long long)(stage[{H} + 64 * tid + 64] == '\\n') << 63));
   if (trailing) {{  // the last line has no terminator: a virtual one at n
     const long long r = n - tb;
     if (r >= 0 && r < 64) m |= 1ull << r;
@@ -335,13 +389,26 @@ extern "C" __global__ __launch_bounds__(256) {_wpe(fast_only)}void {ENTRY}(void*
       const unsigned long long bal = __ballot(t);
       if (bal) found = q0 - (long long)__builtin_ctzll(bal);
     }}
-    if (lane == 0) sprev0 = found < -1 ? -1 : found;
+    if (lane == 0) {{  // the window's first line starts after that terminator (and its LF)
+      long long st0 = 0;
+      if (found >= 0) {{
+        st0 = found + 1;
+        if (found + 1 < n) {{
+          const bool ins = found >= sbase;
+          const int c0 = ins ? stage[found - sbase] : b[found];
+          const int c1 = ins ? stage[found + 1 - sbase] : b[found + 1];
+          st0 += (c0 == '\\r' && c1 == '\\n') ? 1 : 0;
+        }}
+      }}
+      sstart0 = st0;
+    }}
   }}
   __syncthreads();
   int before = inc - c;
   for (int w = 0; w < wave; ++w) before += wtot[w];
   const int cnt = wtot[0] + wtot[1] + wtot[2] + wtot[3];
-{_lookback(lookback)}
+{_lookback(lookback) if not abl & 4 else "  const long long gl0 = 0;"}
+{"  if (cnt + m == 7777777) dq_flag(vflag, (unsigned int)gl0 + (unsigned int)sstart0); return;" if abl & 8 else ""}
   if (cnt == 0) return;  // block-uniform
   for (int R = 0; R < cnt; R += {CAP}) {{
     if (before + c > R - 1 && before < R + {CAP}) {{
@@ -350,7 +417,8 @@ extern "C" __global__ __launch_bounds__(256) {_wpe(fast_only)}void {ENTRY}(void*
       while (mm) {{
         const int bit = __builtin_ctzll(mm);
         mm &= mm - 1;
-        if (o >= R - 1 && o < R + {CAP}) lend[o - R + 1] = (unsigned short)({H} + 64 * tid + bit);
+        if (o >= R - 1 && o < R + {CAP})
+          lend[o - R + 1] = (unsigned short)(({H} + 64 * tid + bit) | ((unsigned int)((crlf >> bit) & 1ull) << 15));
         ++o;
       }}
     }}
@@ -358,18 +426,17 @@ extern "C" __global__ __launch_bounds__(256) {_wpe(fast_only)}void {ENTRY}(void*
     const int nr = min(cnt - R, {CAP});
     for (int j = tid; j < nr; j += 256) {{
       const int jl = R + j;
-      const long long end = sbase + lend[j + 1];
-      const long long prev = jl == 0 ? sprev0 : sbase + lend[j];
-      long long start = prev + 1;
-      if (prev >= 0 && prev + 1 < n) {{
-        const bool ins = prev >= sbase;
-        const int c0 = ins ? stage[prev - sbase] : b[prev];
-        const int c1 = (ins && prev + 1 - sbase < {H} + {W} + 16) ? stage[prev + 1 - sbase] : b[prev + 1];
-        start += (c0 == '\\r' && c1 == '\\n') ? 1 : 0;
+      const long long end = sbase + (lend[j + 1] & 0x7FFFu);
+      long long start = sstart0;
+      if (jl != 0) {{
+        const unsigned int w = lend[j];
+        start = sbase + (w & 0x7FFFu) + 1 + (w >> 15);
       }}
       const long long li = gl0 + jl;
-      if (li >= nalloc) {{
-        atomicOr(vflag, 2u);
+      if ({int(abl & 1)}) {{
+        if (li == -7) dq_flag(vflag, (unsigned int)start);
+      }} else if (li >= nalloc) {{
+        dq_flag(vflag, 2u);
       }} else if (start >= sbase) {{
         const int s0 = (int)(start - sbase), e0 = (int)(end - sbase);  // 32-bit stage positions
         {"if (e0 - s0 <= 16) dq_row_swar(stage, s0, e0, li, p, vflag); else " if swar else ""}dq_row(stage, 0, s0, e0, li, p, vflag);
@@ -480,11 +547,13 @@ def try_fused_scan(nodes, rel, plan, session):
     (parts, udfs), refs = dqvm.nodes_key(nodes)
     head = head_bytes(f["mean_line"])
     lookback = os.environ.get("DQ4ML_SCAN_LOOKBACK", "1") != "0"
+    ticket = ticket_mode()
     o = f["opts"]
     fast_only = (bool(f.get("fast_only")) and not o["null_value"] and not o["trim_lead"] and not o["trim_trail"]
                  and os.environ.get("DQ4ML_SCAN_FASTONLY", "1") != "0")
     key = (parts, udfs, tuple(rel.schema().names), tuple(f["kinds"]), tuple(f["nullable"]),
-           repr(sorted(f["opts"].items())), f["strict"], head, lookback, fast_only, _wpe(fast_only))
+           repr(sorted(f["opts"].items())), f["strict"], head, lookback, fast_only, _wpe(fast_only),
+           ticket, os.environ.get("DQ4ML_SCAN_ABL", "0"))
     cp = _CACHE.get(key)
     if cp is None and key not in _CACHE:
         base = _ScanBase(rel.schema(), 0, f["device"])
@@ -493,7 +562,7 @@ def try_fused_scan(nodes, rel, plan, session):
             _, g, outputs, _ = dqvm.compile_chain(nodes, base, False, gen=g)
             slots = {k: g.slot(None, (k,)) for k in _ScanPlan.SCAN_SLOTS}
             src = kernel_source(g, f["kinds"], f["nullable"], g.used, f["opts"], f["strict"], head, slots, lookback,
-                                fast_only)
+                                fast_only, ticket)
             cp = _ScanPlan(src, g, outputs, refs)
             cp.lookback = lookback
         except dqvm.Unfusable as e:
@@ -514,8 +583,8 @@ def try_fused_scan(nodes, rel, plan, session):
     with torch.cuda.stream(side):
         stream = side.cuda_stream
         nb = int(h.csv_count_blocks(n))
-        if cp.lookback:  # single pass: zeroed look-back status + ticket counter
-            offs = torch.zeros(nb + 1, dtype=torch.int64, device=dev)
+        if cp.lookback:  # single pass: zeroed look-back status + ticket counters
+            offs = torch.zeros(nb + TICKET_WORDS, dtype=torch.int64, device=dev)
         else:  # two passes: per-window terminator counts -> exclusive offsets
             offs = torch.empty(nb + 1, dtype=torch.int64, device=dev)
             h.csv_line_ends(buf.data_ptr(), n, offs.data_ptr(), 0, stream)

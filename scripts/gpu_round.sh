@@ -66,6 +66,7 @@ for s in $STEPS; do
        step syrkpmc1 300 timeout -s KILL 240 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE -d gpurun_out/syrkpmc1 -o run --output-format csv -- python scripts/syrk_bench.py &&
        step syrkpmc2 300 timeout -s KILL 240 rocprofv3 --kernel-trace --pmc SQ_WAIT_ANY SQ_INSTS_VMEM SQ_INSTS_MFMA SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE -d gpurun_out/syrkpmc2 -o run --output-format csv -- python scripts/syrk_bench.py) || exit $? ;;
     cpubase) step cpubase 600 python scripts/cpu_baseline.py --rows 2e7 --threads 16 ;;
+    scanabl) for v in ${SCANABL:-0 1 5 9 13 0}; do step scanabl${DQ4ML_SCAN_TICKET:-xcd}$v 300 env DQ4ML_SCAN_ABL=$v python scripts/scan_ablation.py; done ;;
     asynctests) step asynctests 600 python -m pytest tests/test_gpu_async_fit.py -q -m gpu ;;
     fitprof) step fitprof 300 env N=1.25e7 python scripts/fit_profile.py ;;
     dist2) step dist2 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 scripts/dist_rehearsal.py ;;

@@ -54,8 +54,9 @@ def test_codegen_compiles(cpu_session, tmp_path):
         assert r.returncode == 0, r.stderr + "\n" + code
 
 
-@pytest.mark.parametrize("nullable,fast", [((False, False), True), ((True, True), False), ((True, False), True)])
-def test_scan_fused_codegen_compiles(cpu_session, tmp_path, nullable, fast):
+@pytest.mark.parametrize("nullable,fast,ticket", [((False, False), True, "xcd"), ((True, True), False, "global"),
+                                                   ((True, False), True, "none")])
+def test_scan_fused_codegen_compiles(cpu_session, tmp_path, nullable, fast, ticket):
     """The fused scan + DQ kernel (ops/scanfuse.py) of the lab chain over a CSV relation whose
     facts say: int guest, double price, no nulls — compiles for gfx950, stores only the pruned
     outputs (guest, label) and the selection, and carries no null checks."""
@@ -95,10 +96,10 @@ def test_scan_fused_codegen_compiles(cpu_session, tmp_path, nullable, fast):
     _, g, outputs, _ = dqvm.compile_chain(nodes, base, False, gen=g)
     slots = {k: g.slot(None, (k,)) for k in scanfuse._ScanPlan.SCAN_SLOTS}
     src = scanfuse.kernel_source(g, fused["kinds"], fused["nullable"], g.used, fused["opts"], False, 256, slots,
-                                 True, fast)
+                                 True, fast, ticket)
     if not any(nullable):
         assert [t for t in g.recipe if t[0] in ("out", "outvalid", "selout")] == [("out", 0), ("out", 1), ("selout",)]
-    assert ("atomicOr((int*)" in src) == nullable[1]  # RaiseIfNull only when price may be null
+    assert ("dq_flag((unsigned int*)p[" in src) == nullable[1]  # RaiseIfNull only when price may be null
     hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
     if not os.path.exists(hipcc):
         pytest.skip("no hipcc")
