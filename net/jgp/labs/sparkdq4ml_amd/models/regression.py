@@ -123,7 +123,7 @@ def _fit_checks(params, tbl, X) -> list:
     return [c for c in checks if c is not None]
 
 
-def _features_label(params, df: DataFrame):
+def _check_features_label(params, df: DataFrame):
     schema = df.schema
     fc, lc = params.getOrDefault("featuresCol"), params.getOrDefault("labelCol")
     try:
@@ -137,6 +137,31 @@ def _features_label(params, df: DataFrame):
     if not is_numeric(lt):
         raise ValueError(f"requirement failed: Column {lc} must be of type numeric but was actually of type "
                          f"{lt.simpleString()}.")
+    return fc, lc
+
+
+def _fused_scan_stats(params, df: DataFrame):
+    """The fit's f64 statistics computed inside the CSV scan kernel itself (``scanfuse.try_fused_gram``:
+    scan + DQ chain + VectorAssembler + Gram, no row ever stored) when the DataFrame is that shape
+    and the fit is the default-precision, unweighted normal-equation one; else None."""
+    if params.getOrDefault("loss") != "squaredError" or params.getOrDefault("solver") not in ("auto", "normal"):
+        return None
+    if params.isSet("weightCol") and params.getOrDefault("weightCol"):
+        return None
+    if _gram_dtype(params, df) != "fp64":
+        return None
+    sess = getattr(df, "sparkSession", None)
+    if sess is None or getattr(sess, "device", None) is None or sess.device.type != "cuda":
+        return None
+    fc, lc = _check_features_label(params, df)
+    from ..ops import scanfuse
+    from ..sql.plan import prune_columns
+
+    return scanfuse.try_fused_gram(prune_columns(df._plan, {fc, lc}), fc, lc, sess)
+
+
+def _features_label(params, df: DataFrame):
+    fc, lc = _check_features_label(params, df)
     # only (features, label, weight) are read: prune every other derived column (ColumnPruning)
     need = {fc, lc}
     if params.isSet("weightCol") and params.getOrDefault("weightCol"):
@@ -187,6 +212,9 @@ class LinearRegression(_LRParams):
         return load_params_only(cls, path)
 
     def _train(self, df: DataFrame) -> "LinearRegressionModel":
+        fused = _fused_scan_stats(self, df)
+        if fused is not None:
+            return self._train_wls(df, None, None, None, fused.d, fused)
         tbl, X, y = _features_label(self, df)
         d = _num_features(X)
         if d <= 0:
@@ -200,7 +228,21 @@ class LinearRegression(_LRParams):
 
         return train_lbfgs(self, df, tbl, X, y, d)
 
-    def _train_wls(self, df, tbl, X, y, d):
+    def _train_wls(self, df, tbl, X, y, d, fused=None):
+        sess = getattr(df, "sparkSession", None)
+        overlap = sess is not None and str(sess.conf.get("dq4ml.fit.overlapTail", "true")).lower() in ("1", "true")
+        if fused is not None:  # statistics already reduced by the fused CSV scan kernel
+            flat, checks = fused.flat, list(fused.checks)
+            tracing.add_rows("gram", fused.nrows)
+            # no side-stream tail: nothing is left to overlap with (the next action's scan waits
+            # for this solve, see scanfuse.try_fused_gram)
+            overlap = False
+        else:
+            flat, checks = self._wls_stats(df, tbl, X, y, d, overlap)
+        _rank_health(df)
+        return self._wls_finish(df, flat, d, checks, overlap)
+
+    def _wls_stats(self, df, tbl, X, y, d, overlap):
         checks = _fit_checks(self, tbl, X)
         w = _weight_of(self, tbl)
         sel = tbl.sel
@@ -209,8 +251,6 @@ class LinearRegression(_LRParams):
             sel = yvalid if sel is None else (sel & yvalid)
         zd = X.meta.get("zero_dead", False)
         x_zero_dead = yvalid is None and (tbl.sel is None or (zd is not False and zd is tbl.sel))
-        sess = getattr(df, "sparkSession", None)
-        overlap = sess is not None and str(sess.conf.get("dq4ml.fit.overlapTail", "true")).lower() in ("1", "true")
         with tracing.span("gram"):
             gd = _gram_dtype(self, df)
             flat = None
@@ -232,7 +272,9 @@ class LinearRegression(_LRParams):
                 defer = overlap and _async_conf(df) and d <= 64 and not comm.collectives_active()
                 flat = kernels.gram_stats(X.values, yv, w, sel, gd, x_zero_dead=x_zero_dead, defer=defer)
         tracing.add_rows("gram", tbl.nrows)
-        _rank_health(df)
+        return flat, checks
+
+    def _wls_finish(self, df, flat, d, checks, overlap):
         args = (flat, d, self.getOrDefault("fitIntercept"), float(self.getOrDefault("regParam")),
                 float(self.getOrDefault("elasticNetParam")), bool(self.getOrDefault("standardization")), True,
                 "auto", int(self.getOrDefault("maxIter")), float(self.getOrDefault("tol")))

@@ -36,7 +36,7 @@ __all__ = ["kernel_source", "ENTRY", "WINDOW", "head_bytes", "STATS"]
 ENTRY = "dq_scan_fused"
 WINDOW = 16384  # bytes per block: csv_count_kernel's window (256 threads x 64 bytes)
 CAP = 1024  # line ends per LDS round
-STATS = {"fused_scans": 0}
+STATS = {"fused_scans": 0, "fused_grams": 0}
 
 _HDR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "csrc", "hip", "csv_parse_dev.h")
 _header_text: Optional[str] = None
@@ -165,8 +165,31 @@ def _wpe(fast_only: bool = False) -> str:
 _VALUE = {1: "(int)fzl{c}", 2: "fzl{c}", 0: "fzd{c}", 3: "(fzd{c} != 0.0)"}
 
 
+def gram_width(d: int) -> int:
+    """Statistics per block in Gram mode: live count, Σy, Σy², Σx (d), Σxy (d), packed-upper Σxx."""
+    return 3 + 2 * d + d * (d + 1) // 2
+
+
+def _gram_code(xs, yv) -> str:
+    """Per-line accumulation of the Gram statistics (``gram_width`` order) for a live row."""
+    d = len(xs)
+    lines = ["    if (live) {\n"]
+    lines += [f"      const double gx{i} = (double)({v});\n" for i, v in enumerate(xs)]
+    lines.append(f"      const double gy = (double)({yv});\n")
+    lines.append("      acc[0] += 1.0; acc[1] += gy; acc[2] += gy * gy;\n")
+    for i in range(d):
+        lines.append(f"      acc[{3 + i}] += gx{i}; acc[{3 + d + i}] += gx{i} * gy;\n")
+    q = 3 + 2 * d
+    for i in range(d):
+        for j in range(i, d):
+            lines.append(f"      acc[{q}] += gx{i} * gx{j};\n")
+            q += 1
+    lines.append("    }\n")
+    return "".join(lines)
+
+
 def kernel_source(g, kinds, nullable, used, opts: dict, strict: bool, head: int, slots: dict,
-                  lookback: bool = True, fast_only: bool = False, ticket: str = "xcd") -> str:
+                  lookback: bool = True, fast_only: bool = False, ticket: str = "xcd", gram: int = 0) -> str:
     """Source of the fused kernel.
 
     ``g``: the dqvm generator after lowering the chain (its ``lines`` use ``f<c>`` / ``m<c>`` for
@@ -184,7 +207,13 @@ def kernel_source(g, kinds, nullable, used, opts: dict, strict: bool, head: int,
     ``fast_only``: the earlier scan parsed every field on the numeric fast path (plain dialect):
     only that path is compiled in — the general parser's registers (~60 VGPRs) leave the kernel
     (40 VGPRs instead of 103, full occupancy without spills); a field it cannot take is a fact
-    violation (vflag), like a type or null mismatch."""
+    violation (vflag), like a type or null mismatch.
+
+    ``gram`` = d > 0: the chain's outputs are d features and a label (a ``VectorAssembler`` +
+    ``LinearRegression`` consumer, ``try_fused_gram``): no row is stored — every live row adds
+    to register sums of the f64 normal-equation statistics, and each block writes its
+    ``gram_width(d)`` sums (wave shuffles + LDS, fixed order) to ``p[slots['gpart']]`` at its
+    window index."""
     ncols = len(kinds)
     ns = len(g.ptrs)
     nv = list(opts.get("null_value", "").encode())
@@ -193,7 +222,21 @@ def kernel_source(g, kinds, nullable, used, opts: dict, strict: bool, head: int,
          f"(unsigned char){int(bool(opts['trim_lead']))}, (unsigned char){int(bool(opts['trim_trail']))}, "
          f"(unsigned char){len(nv)}, (unsigned char){int(strict)}, "
          f"{{{', '.join(str(x) for x in (nv + [0] * (16 - len(nv))))}}}}}")
+    # diagnostic ablation builds (wrong results; scripts/scan_ablation.py), bit flags: 1 no per-line
+    # work, 2 no stores, 4 no look-back, 8 no line-end scatter / line loop, 16 no ticket, 32 no LDS
+    # staging stores, 64 no SWAR field conversion, 128 no Gram accumulation, 256 no Gram epilogue
+    abl = int(os.environ.get("DQ4ML_SCAN_ABL", "0"))
+
     def field_code(c: int, swar: bool) -> str:
+        if swar and abl & 64:
+            return (f"    double fzd{c} = 0.0; long long fzl{c} = 0; bool fzg{c} = false; int fzy{c} = C_NULL;\n"
+                    f"    if (pos <= len && line) {{\n"
+                    f"      const unsigned int rest = sepm >> pos;\n"
+                    f"      const int q = rest ? pos + (int)__builtin_ctz(rest) : len;\n"
+                    f"      fzl{c} = (long long)(csv_bytes8(lo, hi, pos) & 0xFFull) + (q - pos); fzd{c} = (double)fzl{c};\n"
+                    f"      fzy{c} = C_INT; pos = q + 1;\n"
+                    f"    }}\n"
+                    f"    bool fzk{c} = fzy{c} != C_NULL && fzy{c} != C_STRING;\n")
         if swar:  # short line in registers (csv_line16 / csv_swar_field); > 8-byte fields walk the stage
             return (f"    double fzd{c} = 0.0; long long fzl{c} = 0; bool fzg{c} = false; int fzy{c} = C_NULL;\n"
                     f"    if (pos <= len && line) {{\n"
@@ -245,11 +288,16 @@ def kernel_source(g, kinds, nullable, used, opts: dict, strict: bool, head: int,
     body = ("\n".join("    " + ln.strip() for ln in g.lines).replace("P[", "p[")
             .replace("atomicOr((int*)p[", "dq_flag((unsigned int*)p["))
     stores = "".join(f"    ((DQG {t}*)p[{s}])[li] = ({t})({v});\n" for t, v, s in g.stores)
-    # diagnostic ablation builds (wrong results; scripts/scan_ablation.py), bit flags: 1 no per-line
-    # work, 2 no stores, 4 no look-back, 8 no line-end scatter / line loop, 16 no ticket, 32 no LDS
-    # staging stores
-    abl = int(os.environ.get("DQ4ML_SCAN_ABL", "0"))
-    if abl & 2:
+    if gram:
+        vals = {}
+        for t, v, s in g.stores:
+            tag = g.recipe[s]
+            if tag[0] == "outvalid":
+                raise ValueError("gram mode: nullable outputs")
+            if tag[0] == "out":
+                vals[tag[1]] = v
+        stores = _gram_code([vals[i] for i in range(gram)], vals[gram]) if not abl & 128 else ""
+    elif abl & 2:
         stores = "".join(f"    if (li == -7) ((DQG {t}*)p[{s}])[0] = ({t})({v});\n" for t, v, s in g.stores)
     comment = int(opts["comment"])
     H, W = int(head), WINDOW
@@ -257,7 +305,7 @@ def kernel_source(g, kinds, nullable, used, opts: dict, strict: bool, head: int,
 // a line of at most 16 bytes in the LDS stage: held in two 64-bit registers, fields cut by the
 // separator bitmask, numeric fields converted SWAR (csv_parse_dev.h) — no per-byte loop
 __device__ __forceinline__ void dq_row_swar(const unsigned char* B, int start, int end, long long li,
-                                            void* const* p, unsigned int* vflag) {{
+                                            void* const* p, unsigned int* vflag, double* acc) {{
     const CsvOpts O = {o};
     const int len = end - start;
     const bool line = len > 0 && !({comment} && B[start] == {comment});
@@ -286,7 +334,7 @@ __device__ __forceinline__ void dq_flag(unsigned int* f, unsigned int v) {{
 // one line: parse every field into registers, run the DQ chain, store the needed outputs at li
 template <typename PB, typename IT>
 __device__ __forceinline__ void dq_row(PB B, IT bias, IT start, IT end, long long li,
-                                       void* const* p, unsigned int* vflag) {{
+                                       void* const* p, unsigned int* vflag, double* acc) {{
     const CsvOpts O = {o};
     const bool line = end > start && !({comment} && B[start - bias] == {comment});
     IT pos = start;
@@ -410,6 +458,7 @@ extern "C" __global__ __launch_bounds__(256) {_wpe(fast_only)}void {ENTRY}(void*
 {_lookback(lookback) if not abl & 4 else "  const long long gl0 = 0;"}
 {"  if (cnt + m == 7777777) dq_flag(vflag, (unsigned int)gl0 + (unsigned int)sstart0); return;" if abl & 8 else ""}
   if (cnt == 0) return;  // block-uniform
+  double acc[{max(1, gram_width(gram) if gram else 1)}] = {{}};
   for (int R = 0; R < cnt; R += {CAP}) {{
     if (before + c > R - 1 && before < R + {CAP}) {{
       unsigned long long mm = m;
@@ -439,15 +488,32 @@ extern "C" __global__ __launch_bounds__(256) {_wpe(fast_only)}void {ENTRY}(void*
         dq_flag(vflag, 2u);
       }} else if (start >= sbase) {{
         const int s0 = (int)(start - sbase), e0 = (int)(end - sbase);  // 32-bit stage positions
-        {"if (e0 - s0 <= 16) dq_row_swar(stage, s0, e0, li, p, vflag); else " if swar else ""}dq_row(stage, 0, s0, e0, li, p, vflag);
+        {"if (e0 - s0 <= 16) dq_row_swar(stage, s0, e0, li, p, vflag, acc); else " if swar else ""}dq_row(stage, 0, s0, e0, li, p, vflag, acc);
       }} else {{
-        dq_row(b, 0ll, start, end, li, p, vflag);
+        dq_row(b, 0ll, start, end, li, p, vflag, acc);
       }}
     }}
     __syncthreads();
   }}
-}}
+{_gram_epilogue(gram, slots) if gram and not abl & 256 else ""}}}
 """)
+
+
+def _gram_epilogue(d: int, slots: dict) -> str:
+    nv = gram_width(d)
+    red = "".join(f"""  {{
+    double t = acc[{k}];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o, 64);
+    if (lane == 0) gred[wave][{k}] = t;
+  }}
+""" for k in range(nv))
+    return f"""  // this window's statistics: wave sums, then the 4 waves in a fixed order (deterministic)
+  __shared__ double gred[4][{nv}];
+{red}  __syncthreads();
+  if (tid < {nv})
+    ((DQG double*)p[{slots['gpart']}])[blk * {nv} + tid] = gred[0][tid] + gred[1][tid] + gred[2][tid] + gred[3][tid];
+"""
 
 
 # ---------------------------------------------------------------------------------------------
@@ -490,17 +556,20 @@ def _scan_gen(base: _ScanBase, nullable):
 class _ScanPlan:
     SCAN_SLOTS = ("buf", "offs", "nalloc", "trailing", "vflag")
 
-    def __init__(self, src: str, g, outputs, refs):
+    def __init__(self, src: str, g, outputs, refs, gram: int = 0):
         self.src = src
         self.recipe = list(g.recipe)
         self.has_raise = g.has_raise
         self.outs = [("new", o[1].dtype, o[2] is not None, o[3]) for o in outputs]
         self.refs = refs
+        self.gram = gram
 
     def bind(self, nalloc: int, dev, scalars: dict, err: torch.Tensor):
-        outs = [(torch.empty(nalloc, dtype=o[1], device=dev),
-                 torch.empty(nalloc, dtype=torch.bool, device=dev) if o[2] else None) for o in self.outs]
-        sel_out = torch.empty(nalloc, dtype=torch.bool, device=dev)
+        """Pointer slots; Gram mode allocates no row outputs (their slots are never stored to)."""
+        g = self.gram
+        outs = [(None if g else torch.empty(nalloc, dtype=o[1], device=dev),
+                 torch.empty(nalloc, dtype=torch.bool, device=dev) if o[2] and not g else None) for o in self.outs]
+        sel_out = None if g else torch.empty(nalloc, dtype=torch.bool, device=dev)
         ptrs = []
         for tag in self.recipe:
             k = tag[0]
@@ -508,6 +577,8 @@ class _ScanPlan:
                 v = 0
             elif k == "err":
                 v = err.data_ptr()
+            elif k in ("out", "outvalid", "selout") and g:
+                v = 0
             elif k == "out":
                 v = outs[tag[1]][0].data_ptr()
             elif k == "outvalid":
@@ -534,14 +605,10 @@ def _scan_stream(dev) -> torch.cuda.Stream:
     return s
 
 
-def try_fused_scan(nodes, rel, plan, session):
-    """Run the Project/Filter chain ``nodes`` (bottom-up) fused into the scan of ``rel``.
-    Returns the chain's Table, ``"vector"`` (the chain ends in a VectorAssembler: the assembler
-    consumes the sub-chain instead) or None (not fusable: the caller scans, then runs the chain)."""
-    from ..runtime.checks import defer
-    from ..sql.table import ColumnData, Table
-    from . import dqvm, native
-    from .device import _h2d
+def _compile(nodes, rel, gram: int = 0):
+    """The cached kernel plan of ``nodes`` fused into the scan of ``rel`` (None: not fusable,
+    ``"vector"``: the chain ends in a VectorAssembler)."""
+    from . import dqvm
 
     f = rel.fused
     (parts, udfs), refs = dqvm.nodes_key(nodes)
@@ -553,25 +620,37 @@ def try_fused_scan(nodes, rel, plan, session):
                  and os.environ.get("DQ4ML_SCAN_FASTONLY", "1") != "0")
     key = (parts, udfs, tuple(rel.schema().names), tuple(f["kinds"]), tuple(f["nullable"]),
            repr(sorted(f["opts"].items())), f["strict"], head, lookback, fast_only, _wpe(fast_only),
-           ticket, os.environ.get("DQ4ML_SCAN_ABL", "0"))
+           ticket, os.environ.get("DQ4ML_SCAN_ABL", "0"), gram)
     cp = _CACHE.get(key)
     if cp is None and key not in _CACHE:
         base = _ScanBase(rel.schema(), 0, f["device"])
         g = _scan_gen(base, f["nullable"])
         try:
             _, g, outputs, _ = dqvm.compile_chain(nodes, base, False, gen=g)
-            slots = {k: g.slot(None, (k,)) for k in _ScanPlan.SCAN_SLOTS}
+            names = _ScanPlan.SCAN_SLOTS + (("gpart",) if gram else ())
+            slots = {k: g.slot(None, (k,)) for k in names}
             src = kernel_source(g, f["kinds"], f["nullable"], g.used, f["opts"], f["strict"], head, slots, lookback,
-                                fast_only, ticket)
-            cp = _ScanPlan(src, g, outputs, refs)
+                                fast_only, ticket, gram)
+            cp = _ScanPlan(src, g, outputs, refs, gram)
             cp.lookback = lookback
         except dqvm.Unfusable as e:
             cp = "vector" if str(e) == "VectorAssembleExpr" else None
+        except ValueError:  # Gram mode over nullable outputs
+            cp = None
         if len(_CACHE) >= 64:
             _CACHE.clear()
         _CACHE[key] = cp
-    if cp is None or cp == "vector":
-        return cp
+    return cp
+
+
+def _launch(cp, nodes, rel, extra: dict, own_stream: bool = True):
+    """One launch of ``cp`` over ``rel``'s cached bytes; returns (outs, sel_out, err, vflag,
+    scan stream, compute stream) after checking a raised UDF error.  ``own_stream``: on the
+    scan side stream (else on the compute stream, in order with the caller's work)."""
+    from . import dqvm, native
+    from .device import _h2d
+
+    f = rel.fused
     h = native.hip()
     dev = f["device"]
     buf, n, nalloc = f["buf"], int(f["n"]), int(f["nlines"])
@@ -579,7 +658,7 @@ def try_fused_scan(nodes, rel, plan, session):
     # HBM-resident input bytes, so action k+1's scan overlaps action k's Gram / fit tail on the
     # compute stream; the compute stream waits for this scan's event before its consumers
     cur = torch.cuda.current_stream(dev)
-    side = _scan_stream(dev) if os.environ.get("DQ4ML_SCAN_STREAM", "1") != "0" else cur
+    side = _scan_stream(dev) if own_stream and os.environ.get("DQ4ML_SCAN_STREAM", "1") != "0" else cur
     with torch.cuda.stream(side):
         stream = side.cuda_stream
         nb = int(h.csv_count_blocks(n))
@@ -590,18 +669,16 @@ def try_fused_scan(nodes, rel, plan, session):
             h.csv_line_ends(buf.data_ptr(), n, offs.data_ptr(), 0, stream)
         err = torch.zeros(1, dtype=torch.int32, device=dev)
         vflag = torch.zeros(1, dtype=torch.int32, device=dev)
-        ptr_list, outs, sel_out = cp.bind(nalloc, dev, {"buf": buf, "offs": offs, "nalloc": nalloc,
-                                                        "trailing": int(f["trailing"]), "vflag": vflag}, err)
+        scalars = {"buf": buf, "offs": offs, "nalloc": nalloc, "trailing": int(f["trailing"]), "vflag": vflag}
+        if cp.gram:
+            extra["gpart"] = scalars["gpart"] = torch.zeros(nb, gram_width(cp.gram), dtype=torch.float64, device=dev)
+        ptr_list, outs, sel_out = cp.bind(nalloc, dev, scalars, err)
         handle, _log = h.rtc_compile(cp.src, ENTRY)
         ptrs = _h2d(np.asarray(ptr_list, dtype=np.int64), dev)
         from ..utils import tracing
 
         with tracing.span("csv_scan_dq_fused"):
             h.rtc_launch(int(handle), nb, 256, ptrs.data_ptr(), n, stream)
-    if side is not cur:
-        cur.wait_stream(side)
-        for t in [err, vflag, sel_out] + [x for o in outs for x in o if x is not None]:
-            t.record_stream(cur)  # produced on the scan stream, consumed on the compute stream
     tracing.add_rows("csv_scan_dq_fused", nalloc)
     STATS["fused_scans"] += 1
     if cp.has_raise and int(err.item()) != 0:
@@ -614,12 +691,114 @@ def try_fused_scan(nodes, rel, plan, session):
                 if r is not None:
                     msg = r.message
         raise SparkException(msg)
+    return outs, sel_out, err, vflag, side, cur
+
+
+def _fact_check(rel, vflag):
+    from ..runtime.checks import defer
+
     # safety net: the earlier scan's facts (types, null-free columns, line count) are re-verified
     # by the kernel; a disagreement surfaces with the first host read of any output
-    check = defer(vflag, lambda: RuntimeError(
+    return defer(vflag, lambda: RuntimeError(
         f"fused CSV scan of {rel.label}: the input no longer matches the schema / line facts of its "
         f"earlier device scan"))
+
+
+def try_fused_scan(nodes, rel, plan, session):
+    """Run the Project/Filter chain ``nodes`` (bottom-up) fused into the scan of ``rel``.
+    Returns the chain's Table, ``"vector"`` (the chain ends in a VectorAssembler: the assembler
+    consumes the sub-chain instead) or None (not fusable: the caller scans, then runs the chain)."""
+    from ..sql.table import ColumnData, Table
+
+    cp = _compile(nodes, rel)
+    if cp is None or cp == "vector":
+        return cp
+    outs, sel_out, err, vflag, side, cur = _launch(cp, nodes, rel, {})
+    if side is not cur:
+        cur.wait_stream(side)
+        for t in [err, vflag, sel_out] + [x for o in outs for x in o if x is not None]:
+            t.record_stream(cur)  # produced on the scan stream, consumed on the compute stream
+    check = _fact_check(rel, vflag)
     schema = plan.schema()
     cols = [ColumnData(fd.dataType, oo[0], oo[1], dict(fd.metadata), [check] if check is not None else [])
             for fd, oo in zip(schema.fields, outs)]
-    return Table(schema, cols, nalloc, sel_out, dev)
+    return Table(schema, cols, int(rel.fused["nlines"]), sel_out, rel.fused["device"])
+
+
+class FusedGram:
+    """``try_fused_gram``'s result: the f64 WLS statistics (``ops.device.gram_stats`` layout),
+    the feature count, the pending fact check and the scanned line count."""
+
+    def __init__(self, flat, d: int, checks: list, nrows: int):
+        self.flat, self.d, self.checks, self.nrows = flat, d, checks, nrows
+
+
+def try_fused_gram(plan, features_col: str, label_col: str, session) -> Optional[FusedGram]:
+    """K1 + K3 + the VectorAssembler + the normal-equation Gram pass in ONE kernel: ``plan`` (pruned
+    to the features and label) must be ``Project[VectorAssembler(inputs) AS features, label]`` over
+    a Project/Filter chain over a not-yet-scanned CSV relation, with at most 8 numeric inputs, no
+    weights and no nullable output.  The parsed rows never reach HBM: each block reduces the
+    statistics of its live rows (``kernel_source(gram=d)``), a fixed-order column sum folds the
+    per-window partials.  Spark runs this as one stage too — the assembler and the
+    ``treeAggregate`` seqOp inside the scan's whole-stage-codegen pipeline
+    (``DataQuality4MachineLearningApp.java:53-55, 68-90, 117-126``).  None: not this shape."""
+    from ..models.feature import VectorAssembleExpr
+    from ..sql.expressions import Alias, ColRef
+    from ..sql.plan import CsvScanRelation, Filter, Project, output_name
+    from ..sql.types import BooleanType, VectorUDT, is_numeric
+
+    if os.environ.get("DQ4ML_SCAN_GRAM", "1") == "0" or session is None:
+        return None
+    if str(session.conf.get("dq4ml.fit.fuseScan", "true")).lower() not in ("1", "true", "yes"):
+        return None
+    if getattr(session, "device", None) is None or session.device.type != "cuda":
+        return None
+    nodes, p = [], plan
+    while isinstance(p, (Project, Filter)) and p._memo is None:
+        nodes.append(p)
+        p = p.child
+    if not nodes or not isinstance(nodes[0], Project):
+        return None
+    if not (isinstance(p, CsvScanRelation) and p._memo is None and p.fused is not None):
+        return None
+    top = nodes[0]
+    by_name = {output_name(e): e for e in top.exprs}
+    fe, le = by_name.get(features_col), by_name.get(label_col)
+    if fe is None or le is None or not isinstance(fe, Alias) or not isinstance(fe.child, VectorAssembleExpr):
+        return None
+    va = fe.child
+    cs = top.child.schema()
+    d = len(va.inputs)
+    if not 1 <= d <= 8:
+        return None
+    for c in va.inputs:
+        t = ColRef(c).data_type(cs)
+        if isinstance(t, VectorUDT) or not (is_numeric(t) or isinstance(t, BooleanType)):
+            return None
+    lexpr = le.child if isinstance(le, Alias) else le
+    if not is_numeric(lexpr.data_type(cs)):
+        return None
+    gtop = Project(top.child, [Alias(ColRef(c), f"__gx{i}") for i, c in enumerate(va.inputs)] + [Alias(lexpr, "__gy")])
+    chain = list(reversed(nodes[1:])) + [gtop]
+    cp = _compile(chain, p, gram=d)
+    if cp is None or cp == "vector":
+        return None
+    extra = {}
+    # on the compute stream, after the previous action's fit tail: the one-workgroup solve
+    # kernel co-running with a whole-GPU scan gets ~1/8 of a CU's issue slots (22 -> 727 us,
+    # kernel trace) and holds the pipeline longer than running alone between two scans; with
+    # nothing left to overlap, a side stream would only add cross-queue waits
+    _, _, err, vflag, side, cur = _launch(cp, chain, p, extra, own_stream=False)
+    gpart = extra["gpart"]
+    with torch.cuda.stream(side):
+        # fixed-order column sums of the per-window partials -> the gram_stats layout
+        # [n, Σw, Σw², Σwy, Σwy², Σwx, Σwxy, packed-upper Σwxx] (unit weights: Σw = Σw² = n)
+        tot = gpart.sum(0)
+        flat = torch.cat([tot[:1].expand(3), tot[1:]])
+    if side is not cur:
+        cur.wait_stream(side)
+        for t in (err, vflag, gpart, tot, flat):
+            t.record_stream(cur)
+    check = _fact_check(p, vflag)
+    STATS["fused_grams"] += 1
+    return FusedGram(flat, d, [check] if check is not None else [], int(p.fused["nlines"]))

@@ -38,6 +38,7 @@ for s in $STEPS; do
     cfg4r16) step cfg4r16 900 env DQ4ML_DQ_ROWS=16 python benchmarks/bench_dq_pipeline.py --steps 5 --warmup 2 ;;
     cfg5) step cfg5 900 python benchmarks/bench_wide.py --steps 3 --warmup 1 --json-out gpurun_out/cfg5.json ;;
     csv) step csv 600 python benchmarks/bench_csv_pipeline.py --steps 20 --warmup 3 --json-out gpurun_out/csv.json ;;
+    csvnogram) step csvnogram 600 env DQ4ML_SCAN_GRAM=0 python benchmarks/bench_csv_pipeline.py --steps 20 --warmup 3 ;;
     cfg1) step cfg1 300 python benchmarks/bench_cpu_small.py --json-out gpurun_out/cfg1.json ;;
     prof4) step prof4 600 env WHICH=cfg4 python scripts/step_profile.py ;;
     prof5) step prof5 600 env WHICH=cfg5 python scripts/step_profile.py ;;
@@ -66,6 +67,7 @@ for s in $STEPS; do
        step syrkpmc1 300 timeout -s KILL 240 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE -d gpurun_out/syrkpmc1 -o run --output-format csv -- python scripts/syrk_bench.py &&
        step syrkpmc2 300 timeout -s KILL 240 rocprofv3 --kernel-trace --pmc SQ_WAIT_ANY SQ_INSTS_VMEM SQ_INSTS_MFMA SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE -d gpurun_out/syrkpmc2 -o run --output-format csv -- python scripts/syrk_bench.py) || exit $? ;;
     cpubase) step cpubase 600 python scripts/cpu_baseline.py --rows 2e7 --threads 16 ;;
+    scangram) for v in ${SCANABL:-0}; do step scangram$v 300 env DQ4ML_SCAN_ABL=$v python scripts/scan_ablation.py --gram; done && step scantable 300 python scripts/scan_ablation.py ;;
     scanabl) for v in ${SCANABL:-0 1 5 9 13 0}; do step scanabl${DQ4ML_SCAN_TICKET:-xcd}$v 300 env DQ4ML_SCAN_ABL=$v python scripts/scan_ablation.py; done ;;
     asynctests) step asynctests 600 python -m pytest tests/test_gpu_async_fit.py -q -m gpu ;;
     fitprof) step fitprof 300 env N=1.25e7 python scripts/fit_profile.py ;;

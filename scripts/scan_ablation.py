@@ -21,11 +21,12 @@ def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--rows", type=float, default=1e8)
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--gram", action="store_true", help="Gram mode (scanfuse.try_fused_gram) instead of table mode")
     a = ap.parse_args(argv)
     import torch
 
     from bench_csv_pipeline import synth_csv
-    from net.jgp.labs.sparkdq4ml_amd import SparkSession, callUDF
+    from net.jgp.labs.sparkdq4ml_amd import SparkSession, VectorAssembler, callUDF
     from net.jgp.labs.sparkdq4ml_amd.dq.rules import register_lab_rules
     from net.jgp.labs.sparkdq4ml_amd.ops import scanfuse
     from net.jgp.labs.sparkdq4ml_amd.sql.plan import CsvScanRelation, Filter, Project, prune_columns
@@ -48,28 +49,38 @@ def main(argv=None):
         df = df.withColumn("price_correct_correl", callUDF("priceCorrelationRule", df.col("price"), df.col("guest")))
         df.createOrReplaceTempView("price")
         df = spark.sql("SELECT guest, price_correct_correl AS price FROM price WHERE price_correct_correl > 0")
-        return raw, df.withColumn("label", df.col("price"))
+        df = df.withColumn("label", df.col("price"))
+        return raw, VectorAssembler().setInputCols(["guest"]).setOutputCol("features").transform(df)
 
     chain()  # eager scan: records the file's facts
     raw, df = chain()
     assert isinstance(raw._plan, CsvScanRelation)
-    plan = prune_columns(df._plan, {"guest", "label"})
-    nodes, p = [], plan
-    while isinstance(p, (Project, Filter)):
-        nodes.append(p)
-        p = p.child
-    nodes.reverse()
+    plan = prune_columns(df._plan, {"features", "label"})
+    if a.gram:
+        def once():
+            assert scanfuse.try_fused_gram(plan, "features", "label", spark) is not None
+    else:
+        plan = plan.child  # the chain below the assembler
+        nodes, p = [], plan
+        while isinstance(p, (Project, Filter)):
+            nodes.append(p)
+            p = p.child
+        nodes.reverse()
+
+        def once():
+            scanfuse.try_fused_scan(nodes, p, plan, spark)
     for _ in range(3):
-        scanfuse.try_fused_scan(nodes, p, plan, spark)
+        once()
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    side = scanfuse._scan_stream(torch.device("cuda", torch.cuda.current_device()))
+    # Gram mode runs on the compute stream, table mode on the scan side stream
+    side = torch.cuda.current_stream() if a.gram else scanfuse._scan_stream(torch.device("cuda", torch.cuda.current_device()))
     e0.record(side)
     for _ in range(a.reps):
-        scanfuse.try_fused_scan(nodes, p, plan, spark)
+        once()
     e1.record(side)
     torch.cuda.synchronize()
-    print(json.dumps({"abl": int(os.environ.get("DQ4ML_SCAN_ABL", "0")), "rows": rows,
+    print(json.dumps({"abl": int(os.environ.get("DQ4ML_SCAN_ABL", "0")), "gram": a.gram, "rows": rows,
                       "ms_per_scan": e0.elapsed_time(e1) / a.reps}), flush=True)
 
 

@@ -108,3 +108,56 @@ def test_scan_fused_codegen_compiles(cpu_session, tmp_path, nullable, fast, tick
     r = subprocess.run([hipcc, "--offload-arch=gfx950", "-O3", "-std=c++17", "-c", str(f), "-o", str(tmp_path / "scan.o")],
                        capture_output=True, text=True)
     assert r.returncode == 0, r.stderr
+
+
+def test_scan_fused_gram_codegen_compiles(cpu_session, tmp_path):
+    """Gram mode of the fused scan kernel (``scanfuse.try_fused_gram``'s shape): the lab chain,
+    then ``VectorAssembler([guest])`` + label as the kernel's d = 1 feature / label outputs —
+    no row store, per-window f64 statistics in the ``gram_width`` layout; compiles for gfx950."""
+    import torch
+
+    from net.jgp.labs.sparkdq4ml_amd import VectorAssembler
+    from net.jgp.labs.sparkdq4ml_amd.ops import scanfuse
+    from net.jgp.labs.sparkdq4ml_amd.ops.csvscan import _opt_args
+    from net.jgp.labs.sparkdq4ml_amd.sql.dataframe import DataFrame
+    from net.jgp.labs.sparkdq4ml_amd.sql.expressions import Alias, ColRef
+    from net.jgp.labs.sparkdq4ml_amd.sql.plan import CsvScanRelation, prune_columns
+    from net.jgp.labs.sparkdq4ml_amd.sql.types import DoubleType, IntegerType, StructField, StructType
+
+    spark = cpu_session
+    register_lab_rules(spark)
+    schema = StructType([StructField("_c0", IntegerType(), True), StructField("_c1", DoubleType(), True)])
+    fused = {"kinds": [1, 0], "nullable": [False, False], "strict": False,
+             "opts": dict(_opt_args({"comment": 0}), sep=",", strict=False)}
+    rel = CsvScanRelation(schema, lambda: None, fused, "Relation[csv]")
+    df = DataFrame(rel, spark).withColumnRenamed("_c0", "guest").withColumnRenamed("_c1", "price")
+    df = df.withColumn("price_no_min", callUDF("minimumPriceRule", df.col("price")))
+    df.createOrReplaceTempView("price")
+    df = spark.sql("SELECT cast(guest as int) guest, price_no_min AS price FROM price WHERE price_no_min > 0")
+    df = df.withColumn("label", df.col("price"))
+    df = VectorAssembler().setInputCols(["guest"]).setOutputCol("features").transform(df)
+    plan = prune_columns(df._plan, {"label", "features"})
+    nodes, p = [], plan
+    while isinstance(p, (Project, Filter)):
+        nodes.append(p)
+        p = p.child
+    assert p is rel
+    top = nodes[0]
+    gtop = Project(top.child, [Alias(ColRef("guest"), "__gx0"), Alias(ColRef("label"), "__gy")])
+    chain = list(reversed(nodes[1:])) + [gtop]
+    base = scanfuse._ScanBase(rel.schema(), 0, torch.device("cpu"))
+    g = scanfuse._scan_gen(base, fused["nullable"])
+    _, g, outputs, _ = dqvm.compile_chain(chain, base, False, gen=g)
+    slots = {k: g.slot(None, (k,)) for k in scanfuse._ScanPlan.SCAN_SLOTS + ("gpart",)}
+    src = scanfuse.kernel_source(g, fused["kinds"], fused["nullable"], g.used, fused["opts"], False, 256, slots,
+                                 True, True, "xcd", 1)
+    assert scanfuse.gram_width(1) == 6 and "gred[4][6]" in src
+    assert "[li] =" not in src  # no row is stored
+    hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+    if not os.path.exists(hipcc):
+        pytest.skip("no hipcc")
+    f = tmp_path / "scan_gram.hip"
+    f.write_text("#include <hip/hip_runtime.h>\n" + src)
+    r = subprocess.run([hipcc, "--offload-arch=gfx950", "-O3", "-std=c++17", "-c", str(f), "-o", str(tmp_path / "g.o")],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
