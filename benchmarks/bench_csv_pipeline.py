@@ -26,6 +26,7 @@ import sys
 import tempfile
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import harness  # noqa: E402
 from harness import emit, timed  # noqa: E402
 
 
@@ -143,7 +144,7 @@ def main(argv=None):
                      "rows_after_dq": int(model.summary.numInstances),
                      "coefficients": [float(v) for v in model.coefficients.toArray()],
                      "intercept": float(model.intercept), "parallelism": f"dp{world}",
-                     "first_action_ms": first_ms,
+                     "first_action_ms": first_ms, "host_issue_ms_per_step": harness.LAST_ISSUE_S / a.steps * 1e3,
                      "device_scans": csvscan.STATS["device_scans"], "scan_fallbacks": csvscan.STATS["fallbacks"]}},
          a.json_out)
     comm.shutdown()

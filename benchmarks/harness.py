@@ -13,6 +13,9 @@ if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
 
+LAST_ISSUE_S = 0.0
+
+
 def timed(step, steps: int, warmup: int, dev):
     import torch
 
@@ -36,6 +39,8 @@ def timed(step, steps: int, warmup: int, dev):
     t0 = time.perf_counter()
     for _ in range(steps):
         out = step()
+    global LAST_ISSUE_S  # host time to issue the timed steps (async device work: < el unless host-bound)
+    LAST_ISSUE_S = time.perf_counter() - t0
     if on_gpu:
         torch.cuda.synchronize()
     if prof is not None:
