@@ -283,15 +283,18 @@ def _wls_native(flat_np, stats, fit_intercept, reg_param, elastic_net, standardi
                     np.asarray(r["objective_history"], dtype=np.float64), r["solver"])
 
 
-_dev_index_cache = {}
-
-
 def _wls_device(flat, nf, fit_intercept, reg_param, elastic_net, standardize_features, standardize_label,
                 solver_type, max_iter, tol):
-    """Large-k Cholesky branch of WLS on the device (f64; same algebra as ``wls.cpp``)."""
+    """Large-k Cholesky branch of WLS on the device (f64; same algebra as ``wls.cpp``).
+
+    The standardized dense system is assembled by ``wls_large.hip`` (one prep + one tiled kernel,
+    no index scatter) and solved by the device Jacobi-PCG (two kernels per iteration, one host
+    read of the control block per chunk); rocSOLVER Cholesky is the fallback with dppsv's exact
+    non-SPD semantics."""
     import torch
 
-    dev = flat.device
+    from ..ops import device
+
     head = flat[:5].cpu().numpy()
     stats = GramStats.scalars_only(head, nf)
     count, wSum, _, bSum, bbSum = (float(v) for v in head)
@@ -305,44 +308,19 @@ def _wls_device(flat, nf, fit_intercept, reg_param, elastic_net, standardize_fea
     if reg_param == 0.0:
         log.warning("regParam is zero, which might cause numerical instability and overfitting.")
     bStd = rawBStd
-    key = (dev, nf)
-    if key not in _dev_index_cache:
-        I, J = packed_upper_indices(nf)
-        _dev_index_cache.clear()
-        _dev_index_cache[key] = (torch.as_tensor(I, device=dev), torch.as_tensor(J, device=dev),
-                                 torch.as_tensor(_packed_diag_index(nf), device=dev))
-    I, J, dj = _dev_index_cache[key]
-    aSum, abSum, aaP = flat[5:5 + nf], flat[5 + nf:5 + 2 * nf], flat[5 + 2 * nf:]
-    m = aSum / wSum
-    aStd = torch.sqrt(torch.clamp(aaP[dj] / wSum - m * m, min=0.0))
-    nz = aStd != 0.0
-    safe = torch.where(nz, aStd, torch.ones_like(aStd))
-    aBar = torch.where(nz, m / safe, torch.zeros_like(m))
-    abBar = torch.where(nz, abSum / wSum / (safe * bStd), torch.zeros_like(m))
-    den = aStd[I] * aStd[J]
-    vals = torch.where(den != 0.0, aaP / wSum / torch.where(den != 0.0, den, torch.ones_like(den)),
-                       torch.zeros_like(den))
     k = nf + 1 if fit_intercept else nf
-    A = torch.zeros(k, k, dtype=torch.float64, device=dev)
-    A[I, J] = vals
-    A[J, I] = vals
     eff_l2 = (1.0 - elastic_net) * reg_param / bStd
-    lam = torch.full((nf,), eff_l2, dtype=torch.float64, device=dev)
-    if not standardize_features:
-        lam = torch.where(nz, lam / (safe * safe), torch.zeros_like(lam))
-    if not standardize_label:
-        lam = lam * bStd
-    ar = torch.arange(nf, device=dev)
-    A[ar, ar] += lam
-    b = abBar
-    if fit_intercept:
-        A[:nf, nf] = aBar
-        A[nf, :nf] = aBar
-        A[nf, nf] = 1.0
-        b = torch.cat([abBar, torch.tensor([rawBBar / bStd], dtype=torch.float64, device=dev)])
-    x = _pcg(A, b) if solver_type == "auto" else None
+    sysm = device.wls_assemble(flat, nf, fit_intercept, wSum, bStd, rawBBar, eff_l2, standardize_features,
+                               standardize_label)
+    A, b, aStd = sysm.A, sysm.b, sysm.aStd
+    o = device.wls_pcg(sysm, nf, bStd, PCG_RTOL) if solver_type == "auto" else None
     L = None
-    if x is None:
+    if o is not None:
+        w = device.PCG_STATE_WORDS
+        x = o[w:w + k]
+        coef = o[w + k:w + k + nf].copy()
+        intercept = float(x[nf] * bStd) if fit_intercept else 0.0
+    else:
         L, info = torch.linalg.cholesky_ex(A)
         if int(info.item()) != 0:
             if solver_type != "auto":
@@ -351,14 +329,16 @@ def _wls_device(flat, nf, fit_intercept, reg_param, elastic_net, standardize_fea
             full = GramStats.from_flat(host, nf)
             return _wls_native(host, full, fit_intercept, reg_param, elastic_net, standardize_features,
                                standardize_label, "quasi-newton", max_iter, tol), full
-        x = torch.cholesky_solve(b.unsqueeze(1), L).squeeze(1)
-    coef = torch.where(nz, x[:nf] * bStd / safe, torch.zeros_like(m)).cpu().numpy()
-    intercept = float(x[nf].item() * bStd) if fit_intercept else 0.0
+        xt = torch.cholesky_solve(b.unsqueeze(1), L).squeeze(1)
+        nz = aStd != 0.0
+        safe = torch.where(nz, aStd, torch.ones_like(aStd))
+        coef = torch.where(nz, xt[:nf] * bStd / safe, torch.zeros_like(aStd)).cpu().numpy()
+        intercept = float(xt[nf].item() * bStd) if fit_intercept else 0.0
 
     def diag_inv():
         Lf = L if L is not None else torch.linalg.cholesky(A)
         inv = torch.cholesky_inverse(Lf).diagonal()
-        mult = torch.ones(k, dtype=torch.float64, device=dev)
+        mult = torch.ones(k, dtype=torch.float64, device=A.device)
         mult[:nf] = aStd * aStd
         return (inv / (wSum * mult)).cpu().numpy()
     return WLSModel(coef, intercept, diag_inv, np.zeros(1), "cholesky"), stats

@@ -12,6 +12,7 @@
 #include "gram_wide.h"
 #include "gram_syrk.h"
 #include "wls_small.h"
+#include "wls_large.h"
 #include "rowops.h"
 
 namespace py = pybind11;
@@ -125,6 +126,24 @@ PYBIND11_MODULE(_dq4ml_hip, m) {
                         uintptr_t out, uintptr_t stream) {
     wls_small(P<const double>(flat), nf, fit_intercept, reg, enet, std_f, std_l, P<double>(out), as_stream(stream));
   });
+  m.def("wls_assemble", [](uintptr_t flat, int nf, bool fit_intercept, double wSum, double bStd, double rawBBar,
+                           double eff_l2, bool std_f, bool std_l, uintptr_t A, uintptr_t b, uintptr_t minv,
+                           uintptr_t aStd, uintptr_t aBar, uintptr_t lam, uintptr_t o, uintptr_t stream) {
+    wls_assemble(P<const double>(flat), nf, fit_intercept, wSum, bStd, rawBBar, eff_l2, std_f, std_l, P<double>(A),
+                 P<double>(b), P<double>(minv), P<double>(aStd), P<double>(aBar), P<double>(lam), P<double>(o),
+                 as_stream(stream));
+  });
+  m.def("wls_pcg_init", [](uintptr_t b, uintptr_t minv, int k, double rtol, uintptr_t o, uintptr_t r, uintptr_t p,
+                           uintptr_t stream) {
+    wls_pcg_init(P<const double>(b), P<const double>(minv), k, rtol, P<double>(o), P<double>(r), P<double>(p),
+                 as_stream(stream));
+  });
+  m.def("wls_pcg_chunk", [](uintptr_t A, uintptr_t b, uintptr_t minv, uintptr_t aStd, int k, int nf, double bStd,
+                            int iters, uintptr_t o, uintptr_t r, uintptr_t p, uintptr_t Ap, uintptr_t stream) {
+    wls_pcg_chunk(P<const double>(A), P<const double>(b), P<const double>(minv), P<const double>(aStd), k, nf, bStd,
+                  iters, P<double>(o), P<double>(r), P<double>(p), P<double>(Ap), as_stream(stream));
+  });
+  m.attr("PCG_STATE_WORDS") = (int)PCG_STATE_WORDS;
   m.def("wls_qn_small", [](uintptr_t flat, int nf, bool fit_intercept, double reg, double enet, bool std_f,
                            bool std_l, int max_iter, double tol, int hist_cap, uintptr_t out, uintptr_t stream) {
     wls_qn_small(P<const double>(flat), nf, fit_intercept, reg, enet, std_f, std_l, max_iter, tol, hist_cap,

@@ -7,6 +7,7 @@ validated HERE, on the host, before any launch (a kernel's indexing assumes them
 from __future__ import annotations
 
 import functools
+from dataclasses import dataclass
 import os
 from typing import List, Optional
 
@@ -626,6 +627,68 @@ def wls_qn_small(flat: torch.Tensor, nf: int, fit_intercept: bool, reg: float, e
     h.wls_qn_small(flat.data_ptr(), int(nf), bool(fit_intercept), float(reg), float(enet), bool(std_f), bool(std_l),
                    int(max_iter), float(tol), cap, out.data_ptr(), _stream())
     return out
+
+
+PCG_STATE_WORDS = 8  # == WlsPcgState::PCG_STATE_WORDS (wls_large.h); checked against the module
+
+
+@dataclass
+class WlsSystem:
+    """The standardized dense WLS system on the device (``wls_large.hip``) and its PCG workspace."""
+    A: torch.Tensor      # [k, k] f64 row-major (symmetric)
+    b: torch.Tensor      # [k]
+    minv: torch.Tensor   # [k] Jacobi preconditioner
+    aStd: torch.Tensor   # [nf] population std of every feature
+    o: torch.Tensor      # control block [state(8) | x(k) | coef(nf)]
+    k: int
+
+
+def wls_assemble(flat: torch.Tensor, nf: int, fit_intercept: bool, wSum: float, bStd: float, rawBBar: float,
+                 eff_l2: float, std_f: bool, std_l: bool) -> WlsSystem:
+    """Standardized dense system of the large-k WLS branch from the flat statistics (no host sync)."""
+    h = native.hip()
+    _check_dev(flat)
+    if int(h.PCG_STATE_WORDS) != PCG_STATE_WORDS:
+        raise RuntimeError("wls_large: control-block layout mismatch between device.py and the HIP module")
+    if flat.dtype != torch.float64 or flat.numel() != 5 + 2 * nf + nf * (nf + 1) // 2:
+        raise ValueError("wls_assemble: flat statistics have the wrong dtype/length")
+    k = nf + 1 if fit_intercept else nf
+    dev = flat.device
+    A = torch.empty(k, k, dtype=torch.float64, device=dev)
+    vec = torch.empty(2 * k + 3 * nf, dtype=torch.float64, device=dev)
+    b, minv = vec[:k], vec[k:2 * k]
+    aStd, aBar, lam = vec[2 * k:2 * k + nf], vec[2 * k + nf:2 * k + 2 * nf], vec[2 * k + 2 * nf:]
+    o = torch.zeros(PCG_STATE_WORDS + k + nf, dtype=torch.float64, device=dev)
+    h.wls_assemble(flat.data_ptr(), int(nf), bool(fit_intercept), float(wSum), float(bStd), float(rawBBar),
+                   float(eff_l2), bool(std_f), bool(std_l), A.data_ptr(), b.data_ptr(), minv.data_ptr(),
+                   aStd.data_ptr(), aBar.data_ptr(), lam.data_ptr(), o.data_ptr(), _stream())
+    return WlsSystem(A, b, minv, aStd, o, k)
+
+
+def wls_pcg(sysm: WlsSystem, nf: int, bStd: float, rtol: float, chunk: int = 8,
+            max_iter: int = 96) -> Optional[np.ndarray]:
+    """Jacobi-PCG on the assembled system: ``chunk`` iterations per host check (one D2H of the
+    control block).  Returns the host control block ``[state | x | coef]`` once CG has converged
+    AND the true residual passes, None when a diagonal entry is not > 0 or CG has not converged
+    within ``max_iter`` (the caller falls back to Cholesky)."""
+    h = native.hip()
+    k, dev = sysm.k, sysm.A.device
+    r = torch.empty(k, dtype=torch.float64, device=dev)
+    p = torch.empty_like(r)
+    Ap = torch.empty_like(r)
+    st = _stream()
+    h.wls_pcg_init(sysm.b.data_ptr(), sysm.minv.data_ptr(), k, float(rtol), sysm.o.data_ptr(), r.data_ptr(),
+                   p.data_ptr(), st)
+    for _ in range(0, max_iter, chunk):
+        h.wls_pcg_chunk(sysm.A.data_ptr(), sysm.b.data_ptr(), sysm.minv.data_ptr(), sysm.aStd.data_ptr(), k,
+                        int(nf), float(bStd), int(chunk), sysm.o.data_ptr(), r.data_ptr(), p.data_ptr(),
+                        Ap.data_ptr(), st)
+        o = sysm.o.cpu().numpy()
+        if o[4] != 0.0:  # PCG_BAD: a diagonal entry <= 0 (or NaN)
+            return None
+        if o[3] != 0.0:  # PCG_CONV
+            return o if o[5] != 0.0 else None  # PCG_OK: the true residual check
+    return None
 
 
 # ------------------------------------------------------------------------------------------
