@@ -109,7 +109,8 @@ def build_hip(force: bool = False) -> str:
             hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
             tl = _torch_lib()
             flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-fvisibility=hidden",
-                     "-munsafe-fp-atomics", *_py_includes(), f"-I{os.path.join(CSRC, 'hip')}"]
+                     "-munsafe-fp-atomics", *_py_includes(), f"-I{os.path.join(CSRC, 'hip')}",
+                     *os.environ.get("DQ4ML_HIPCC_EXTRA", "").split()]  # A/B builds (-D knobs)
             objs = [os.path.join(objdir, os.path.basename(s) + ".o") for s in srcs]
             todo = [(s, o) for s, o in zip(srcs, objs) if force or _obj_stale(o, s, headers)]
 

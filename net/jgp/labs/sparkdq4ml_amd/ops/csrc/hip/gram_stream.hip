@@ -37,13 +37,18 @@ constexpr int kSB = kSW * kWave;
 constexpr int kRawBytes = 1280;  // [y | w]: 1 KiB (lanes 0-31 | 32-63 x 16 B); sel: 64 x 4 B
 constexpr int kFlush = 16;       // exact-f32 kernel: stages per f32 accumulation chunk
 
+// cache policy of the stream's DMA loads: every byte is read once per pass (the rows stream
+// through, nothing is re-read from L2 / MALL), so non-temporal (aux 2 = nt) by default
+#ifndef DQ4ML_GLDS_AUX
+#define DQ4ML_GLDS_AUX 2
+#endif
 __device__ __forceinline__ void glds16(const void* g, void* l) {
   __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(g),
-                                   (__attribute__((address_space(3))) void*)(l), 16, 0, 0);
+                                   (__attribute__((address_space(3))) void*)(l), 16, 0, DQ4ML_GLDS_AUX);
 }
 __device__ __forceinline__ void glds4(const void* g, void* l) {
   __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(g),
-                                   (__attribute__((address_space(3))) void*)(l), 4, 0, 0);
+                                   (__attribute__((address_space(3))) void*)(l), 4, 0, DQ4ML_GLDS_AUX);
 }
 template <int N>
 __device__ __forceinline__ void wait_vm() {
