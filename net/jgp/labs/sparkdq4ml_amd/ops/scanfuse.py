@@ -165,6 +165,11 @@ def _wpe(fast_only: bool = False) -> str:
 _VALUE = {1: "(int)fzl{c}", 2: "fzl{c}", 0: "fzd{c}", 3: "(fzd{c} != 0.0)"}
 
 
+def _scan_nt() -> bool:
+    """Window loads with the non-temporal hint (DQ4ML_SCAN_NT=1; A/B knob)."""
+    return os.environ.get("DQ4ML_SCAN_NT", "0") != "0"
+
+
 def gram_width(d: int) -> int:
     """Statistics per block in Gram mode: live count, Σy, Σy², Σx (d), Σxy (d), packed-upper Σxx."""
     return 3 + 2 * d + d * (d + 1) // 2
@@ -371,7 +376,7 @@ extern "C" __global__ __launch_bounds__(256) {_wpe(fast_only)}void {ENTRY}(void*
   for (int j = 0; j < 4; ++j) {{
     const long long gi = tb + 16 * j;
     csv_u32x4 v = {{0u, 0u, 0u, 0u}};
-    if (gi < n && gi + 16 > 0) v = *reinterpret_cast<const DQG csv_u32x4*>(ab + gi + a);
+    if (gi < n && gi + 16 > 0) v = {"__builtin_nontemporal_load(" if _scan_nt() else "*("}reinterpret_cast<const DQG csv_u32x4*>(ab + gi + a));
     {"if (v[0] == 0x7F7F7F7Fu && v[1] == 3u) " if abl & 32 else ""}*reinterpret_cast<csv_u32x4*>(stage + {H} + 64 * tid + 16 * j) = v;
 #pragma unroll
     for (int w = 0; w < 4; ++w) {{
@@ -620,7 +625,7 @@ def _compile(nodes, rel, gram: int = 0):
                  and os.environ.get("DQ4ML_SCAN_FASTONLY", "1") != "0")
     key = (parts, udfs, tuple(rel.schema().names), tuple(f["kinds"]), tuple(f["nullable"]),
            repr(sorted(f["opts"].items())), f["strict"], head, lookback, fast_only, _wpe(fast_only),
-           ticket, os.environ.get("DQ4ML_SCAN_ABL", "0"), gram)
+           ticket, os.environ.get("DQ4ML_SCAN_ABL", "0"), gram, _scan_nt())
     cp = _CACHE.get(key)
     if cp is None and key not in _CACHE:
         base = _ScanBase(rel.schema(), 0, f["device"])

@@ -88,6 +88,8 @@ for s in $STEPS; do
     kprofcsv) (export TMPDIR=/tmp; step kprofcsv 600 rocprofv3 --kernel-trace --stats -d gpurun_out/kprofcsv -o run --output-format csv -- python benchmarks/bench_csv_pipeline.py --steps 5 --warmup 2) || exit $? ;;
     csvtwopass) step csvtwopass 600 env DQ4ML_SCAN_LOOKBACK=0 python benchmarks/bench_csv_pipeline.py --steps 20 --warmup 3 ;;
     csvnostream) step csvnostream 600 env DQ4ML_SCAN_STREAM=0 python benchmarks/bench_csv_pipeline.py --steps 20 --warmup 3 ;;
+    csvnt) step csvnt 600 env DQ4ML_SCAN_NT=1 python benchmarks/bench_csv_pipeline.py --steps 20 --warmup 3 ;;
+    csvntt) step csvntt 600 env DQ4ML_SCAN_NT=1 python -u -m pytest tests/test_gpu_scanfuse.py -q -m gpu --timeout 120 --timeout-method thread ;;
     csvnoswar) step csvnoswar 600 env DQ4ML_SCAN_SWAR=0 python benchmarks/bench_csv_pipeline.py --steps 20 --warmup 3 ;;
     csvwpe6) step csvwpe6 600 env DQ4ML_SCAN_WPE=6 python benchmarks/bench_csv_pipeline.py --steps 20 --warmup 3 ;;
     csvwpe8) step csvwpe8 600 env DQ4ML_SCAN_WPE=8 python benchmarks/bench_csv_pipeline.py --steps 20 --warmup 3 ;;
