@@ -194,7 +194,8 @@ def _gram_code(xs, yv) -> str:
 
 
 def kernel_source(g, kinds, nullable, used, opts: dict, strict: bool, head: int, slots: dict,
-                  lookback: bool = True, fast_only: bool = False, ticket: str = "xcd", gram: int = 0) -> str:
+                  lookback: bool = True, fast_only: bool = False, ticket: str = "xcd", gram: int = 0,
+                  nolb: bool = False) -> str:
     """Source of the fused kernel.
 
     ``g``: the dqvm generator after lowering the chain (its ``lines`` use ``f<c>`` / ``m<c>`` for
@@ -364,7 +365,7 @@ extern "C" __global__ __launch_bounds__(256) {_wpe(fast_only)}void {ENTRY}(void*
   __shared__ int wtot[4];
   __shared__ long long sstart0, sblk, sgl0;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-{_ticket(lookback, ticket if not abl & 16 else "none")}
+{"  const long long blk = blockIdx.x;  // Gram mode: no global line numbering needed" if nolb else _ticket(lookback, ticket if not abl & 16 else "none")}
   const long long a = (long long)(reinterpret_cast<unsigned long long>(b) & 15ull);
   const DQG unsigned char* ab = b - a;                     // 16-byte aligned view
   const long long wbase = blk * {W} - a;                    // buffer index of window byte 0
@@ -460,7 +461,7 @@ extern "C" __global__ __launch_bounds__(256) {_wpe(fast_only)}void {ENTRY}(void*
   int before = inc - c;
   for (int w = 0; w < wave; ++w) before += wtot[w];
   const int cnt = wtot[0] + wtot[1] + wtot[2] + wtot[3];
-{_lookback(lookback) if not abl & 4 else "  const long long gl0 = 0;"}
+{_lookback(lookback) if not (abl & 4 or nolb) else "  const long long gl0 = 0;"}
 {"  if (cnt + m == 7777777) dq_flag(vflag, (unsigned int)gl0 + (unsigned int)sstart0); return;" if abl & 8 else ""}
   if (cnt == 0) return;  // block-uniform
   double acc[{max(1, gram_width(gram) if gram else 1)}] = {{}};
@@ -489,7 +490,7 @@ extern "C" __global__ __launch_bounds__(256) {_wpe(fast_only)}void {ENTRY}(void*
       const long long li = gl0 + jl;
       if ({int(abl & 1)}) {{
         if (li == -7) dq_flag(vflag, (unsigned int)start);
-      }} else if (li >= nalloc) {{
+      }} else if ({"false" if nolb else "li >= nalloc"}) {{
         dq_flag(vflag, 2u);
       }} else if (start >= sbase) {{
         const int s0 = (int)(start - sbase), e0 = (int)(end - sbase);  // 32-bit stage positions
@@ -619,13 +620,16 @@ def _compile(nodes, rel, gram: int = 0):
     (parts, udfs), refs = dqvm.nodes_key(nodes)
     head = head_bytes(f["mean_line"])
     lookback = os.environ.get("DQ4ML_SCAN_LOOKBACK", "1") != "0"
+    # Gram mode stores no row, so it needs no global line numbering: no ticket, no look-back,
+    # window = blockIdx.x (the line-count fact is a property of the same cached bytes)
+    nolb = bool(gram) and lookback and os.environ.get("DQ4ML_SCAN_GRAM_NOLB", "1") != "0"
     ticket = ticket_mode()
     o = f["opts"]
     fast_only = (bool(f.get("fast_only")) and not o["null_value"] and not o["trim_lead"] and not o["trim_trail"]
                  and os.environ.get("DQ4ML_SCAN_FASTONLY", "1") != "0")
     key = (parts, udfs, tuple(rel.schema().names), tuple(f["kinds"]), tuple(f["nullable"]),
            repr(sorted(f["opts"].items())), f["strict"], head, lookback, fast_only, _wpe(fast_only),
-           ticket, os.environ.get("DQ4ML_SCAN_ABL", "0"), gram, _scan_nt())
+           ticket, os.environ.get("DQ4ML_SCAN_ABL", "0"), gram, _scan_nt(), nolb)
     cp = _CACHE.get(key)
     if cp is None and key not in _CACHE:
         base = _ScanBase(rel.schema(), 0, f["device"])
@@ -635,7 +639,7 @@ def _compile(nodes, rel, gram: int = 0):
             names = _ScanPlan.SCAN_SLOTS + (("gpart",) if gram else ())
             slots = {k: g.slot(None, (k,)) for k in names}
             src = kernel_source(g, f["kinds"], f["nullable"], g.used, f["opts"], f["strict"], head, slots, lookback,
-                                fast_only, ticket, gram)
+                                fast_only, ticket, gram, nolb)
             cp = _ScanPlan(src, g, outputs, refs, gram)
             cp.lookback = lookback
         except dqvm.Unfusable as e:

@@ -90,6 +90,7 @@ for s in $STEPS; do
     csvnostream) step csvnostream 600 env DQ4ML_SCAN_STREAM=0 python benchmarks/bench_csv_pipeline.py --steps 20 --warmup 3 ;;
     csvnt) step csvnt 600 env DQ4ML_SCAN_NT=1 python benchmarks/bench_csv_pipeline.py --steps 20 --warmup 3 ;;
     csvntt) step csvntt 600 env DQ4ML_SCAN_NT=1 python -u -m pytest tests/test_gpu_scanfuse.py -q -m gpu --timeout 120 --timeout-method thread ;;
+    csvlb) step csvlb 600 env DQ4ML_SCAN_GRAM_NOLB=0 python benchmarks/bench_csv_pipeline.py --steps 20 --warmup 3 ;;
     csvnoswar) step csvnoswar 600 env DQ4ML_SCAN_SWAR=0 python benchmarks/bench_csv_pipeline.py --steps 20 --warmup 3 ;;
     csvwpe6) step csvwpe6 600 env DQ4ML_SCAN_WPE=6 python benchmarks/bench_csv_pipeline.py --steps 20 --warmup 3 ;;
     csvwpe8) step csvwpe8 600 env DQ4ML_SCAN_WPE=8 python benchmarks/bench_csv_pipeline.py --steps 20 --warmup 3 ;;
