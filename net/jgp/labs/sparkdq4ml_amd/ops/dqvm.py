@@ -487,6 +487,8 @@ def _kernel_source(g: _Gen) -> str:
 
 
 VEC_ROWS = int(os.environ.get("DQ4ML_DQ_ROWS", "4"))  # consecutive rows per thread, vector form
+VEC_NT = os.environ.get("DQ4ML_DQ_NT", "0") != "0"  # non-temporal column loads (A/B knob)
+GRID_CAP = int(os.environ.get("DQ4ML_DQ_GRID", "8192"))  # grid-stride cap (blocks)
 _VEC_BASE = {"double": "double", "float": "float", "int": "int", "long long": "long long", "bool": "unsigned char",
              "unsigned char": "unsigned char"}
 _VEC_NAME = {"double": "f64", "float": "f32", "int": "i32", "long long": "i64", "bool": "u8", "unsigned char": "u8"}
@@ -509,7 +511,8 @@ def _kernel_source_vec(g: _Gen, V: int = VEC_ROWS) -> str:
     n % V tail rows run the scalar body."""
     ns = len(g.ptrs)
     decl = "".join(f"    {ct} {v}_a[{V}];\n" for ct, v, _, _ in g.loads)
-    ld = "".join(f"    {{ const {_vec_t(st, V)} q = *(const {_vec_t(st, V)}*)((const {_VEC_BASE[st]}*)p[{s}] + r0);\n"
+    ldf = "__builtin_nontemporal_load(" if VEC_NT else "*("
+    ld = "".join(f"    {{ const {_vec_t(st, V)} q = {ldf}(const {_vec_t(st, V)}*)((const {_VEC_BASE[st]}*)p[{s}] + r0));\n"
                  f"      for (int u = 0; u < {V}; ++u) {v}_a[u] = ({ct})q[u]; }}\n" for ct, v, st, s in g.loads)
     use = "".join(f"      const {ct} {v} = {v}_a[u];\n" for ct, v, _, _ in g.loads)
     body = "\n".join("  " + ln for ln in g.lines).replace("P[", "p[")
@@ -681,7 +684,7 @@ def try_execute_fused(plan, session) -> Optional[Table]:
 
     ptrs = _h2d(np.asarray(ptr_list, dtype=np.int64), base.device)  # no host-device sync
     n = base.nrows
-    grid = int(max(1, min((n + 256 * VEC_ROWS - 1) // (256 * VEC_ROWS) if vec else (n + 255) // 256, 8192)))
+    grid = int(max(1, min((n + 256 * VEC_ROWS - 1) // (256 * VEC_ROWS) if vec else (n + 255) // 256, GRID_CAP)))
     from ..utils import tracing
 
     with tracing.span("dq_fused"):

@@ -34,6 +34,9 @@ for s in $STEPS; do
     cfg4rs64) step cfg4rs64 900 env DQ4ML_GRAM_STREAM_F32RS=64 python benchmarks/bench_dq_pipeline.py --steps 5 --warmup 2 ;;
     cfg4ring3) step cfg4ring3 900 env DQ4ML_GRAM_STREAM_RING=3 python benchmarks/bench_dq_pipeline.py --steps 5 --warmup 2 ;;
     cfg4nodqs) step cfg4nodqs 900 env DQ4ML_DQ_STREAM=0 python benchmarks/bench_dq_pipeline.py --steps 5 --warmup 2 ;;
+    cfg4nt) step cfg4nt 900 env DQ4ML_DQ_NT=1 python benchmarks/bench_dq_pipeline.py --steps 5 --warmup 2 ;;
+    cfg4g32) step cfg4g32 900 env DQ4ML_DQ_GRID=32768 python benchmarks/bench_dq_pipeline.py --steps 5 --warmup 2 ;;
+    cfg4g2) step cfg4g2 900 env DQ4ML_DQ_GRID=2048 python benchmarks/bench_dq_pipeline.py --steps 5 --warmup 2 ;;
     cfg4r8) step cfg4r8 900 env DQ4ML_DQ_ROWS=8 python benchmarks/bench_dq_pipeline.py --steps 5 --warmup 2 ;;
     cfg4r16) step cfg4r16 900 env DQ4ML_DQ_ROWS=16 python benchmarks/bench_dq_pipeline.py --steps 5 --warmup 2 ;;
     cfg5) step cfg5 900 python benchmarks/bench_wide.py --steps 3 --warmup 1 --json-out gpurun_out/cfg5.json ;;
