@@ -69,3 +69,27 @@ def test_bench_py_rejects_mismatched_world():
     out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "1",
                           "--warmup", "0", "--rows", "1000"], capture_output=True, text=True, timeout=300, env=env)
     assert out.returncode == 2 and "WORLD_SIZE=3" in out.stderr
+
+
+def test_bench_py_under_the_drivers_launcher_four_ranks():
+    """The driver's exact multi-GPU command shape (``torch.distributed.run --nnodes=1
+    --nproc-per-node N --master-addr 127.0.0.1``), rehearsed with 4 gloo ranks on this CPU box:
+    one JSON line from rank 0, strong scaling (global rows fixed, an uneven last shard)."""
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR",
+                                                             "MASTER_PORT")}
+    out = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "4",
+                          "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
+                          "--gpus", "4", "--steps", "2", "--warmup", "1", "--rows", "40002"],
+                         capture_output=True, text=True, timeout=600, env=env)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [ln for ln in out.stdout.strip().splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 4 and line["world"] == 4 and line["config"]["parallelism"] == "dp4"
+    assert line["scaling"] == "strong" and line["config"]["global_batch"] == 40002
+    assert line["config"]["coef_max_abs_err"] < 0.05
