@@ -96,6 +96,7 @@ for s in $STEPS; do
     csvlb) step csvlb 600 env DQ4ML_SCAN_GRAM_NOLB=0 python benchmarks/bench_csv_pipeline.py --steps 20 --warmup 3 ;;
     csvnoswar) step csvnoswar 600 env DQ4ML_SCAN_SWAR=0 python benchmarks/bench_csv_pipeline.py --steps 20 --warmup 3 ;;
     csvwpe6) step csvwpe6 600 env DQ4ML_SCAN_WPE=6 python benchmarks/bench_csv_pipeline.py --steps 20 --warmup 3 ;;
+    csvwpe0) step csvwpe0 600 env DQ4ML_SCAN_WPE=0 python benchmarks/bench_csv_pipeline.py --steps 20 --warmup 3 ;;
     csvwpe8) step csvwpe8 600 env DQ4ML_SCAN_WPE=8 python benchmarks/bench_csv_pipeline.py --steps 20 --warmup 3 ;;
     csvpmc) (export TMPDIR=/tmp
        step csvpmc1 300 timeout -s KILL 240 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_SALU GRBM_GUI_ACTIVE -d gpurun_out/csvpmc1 -o run --output-format csv -- python benchmarks/bench_csv_pipeline.py --steps 2 --warmup 1 --rows 2e7 &&
