@@ -161,3 +161,13 @@ def test_scan_fused_gram_codegen_compiles(cpu_session, tmp_path):
     r = subprocess.run([hipcc, "--offload-arch=gfx950", "-O3", "-std=c++17", "-c", str(f), "-o", str(tmp_path / "g.o")],
                        capture_output=True, text=True)
     assert r.returncode == 0, r.stderr
+    # the default Gram-mode build: no global line numbering (no ticket, no look-back, no nalloc check)
+    src2 = scanfuse.kernel_source(g, fused["kinds"], fused["nullable"], g.used, fused["opts"], False, 256, slots,
+                                  True, True, "xcd", 1, nolb=True)
+    assert "__hip_atomic_fetch_add" not in src2 and "sgl0 = pre" not in src2 and "li >= nalloc" not in src2
+    assert "const long long blk = blockIdx.x;" in src2 and "sgl0 = pre" in src
+    f2 = tmp_path / "scan_gram_nolb.hip"
+    f2.write_text("#include <hip/hip_runtime.h>\n" + src2)
+    r = subprocess.run([hipcc, "--offload-arch=gfx950", "-O3", "-std=c++17", "-c", str(f2), "-o", str(tmp_path / "g2.o")],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
