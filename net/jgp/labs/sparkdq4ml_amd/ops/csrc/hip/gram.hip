@@ -283,7 +283,20 @@ __global__ __launch_bounds__((BF16Geom<NT, XMODE>::kBlock), 1) void gram_tall_bf
   };
 
   // full supersteps: register double buffer (loads of s+1 in flight while s computes)
-  if (s0 < s1) {
+  if (a.interleave) {
+    if (gw < a.nsuper) {
+      bf16x8 cur[NT][4], nxt[NT][4];
+      load(gw * 64, 64, cur);
+      for (int64_t s = gw; s < a.nsuper; s += total_waves) {
+        if (s + total_waves < a.nsuper) load((s + total_waves) * 64, 64, nxt);
+        compute(s * 64, cur);
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) cur[t][i] = nxt[t][i];
+      }
+    }
+  } else if (s0 < s1) {
     bf16x8 cur[NT][4], nxt[NT][4];
     load(s0 * 64, 64, cur);
     for (int64_t s = s0; s < s1; ++s) {
@@ -1268,6 +1281,15 @@ void gram_tall(int mode, GramArgs a, int xmode, int blocks, double* out, hipStre
   const int64_t total_waves = (int64_t)blocks * (block / kWave);
   a.spw = (a.nsuper + total_waves - 1) / total_waves;
   if (a.spw < 1) a.spw = 1;
+  {
+    static const int interleave = [] {
+      // default on: same-box A/B (scripts/interleave_ab.sh, 5 alternations) 1e8 rows 1.011-1.015 vs
+      // 1.020-1.026 ms, 1.25e7 rows 0.1426-0.1441 vs 0.1471-0.1476 ms per fit
+      const char* e = getenv("DQ4ML_GRAM_INTERLEAVE");
+      return e && e[0] == '0' ? 0 : 1;
+    }();
+    a.interleave = interleave;
+  }
   a.P = (int)gram_partial_stride(mode, a.d);
   const size_t lds = mode == GRAM_BF16 ? bf16_lds(a.d, xmode) : f64_lds(a.d);
   if (a.tiled && mode != GRAM_BF16) throw std::invalid_argument("gram_tall: tiled storage needs bf16 mode");
