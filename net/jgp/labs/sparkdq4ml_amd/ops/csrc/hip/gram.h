@@ -32,7 +32,7 @@ struct GramArgs {
   // stream kernels over source columns (gram_stream_cols): [2 * d] int64 device table of
   // (column pointer, dtype) pairs — feature f is column srcs[2 f] (all of X's dtype xdt)
   const int64_t* srcs;
-  // bf16 kernel: 1 = wave w takes supersteps w, w + W, w + 2W, ... (W = total waves) instead of
+  // bf16 + stream kernels: 1 = wave w takes supersteps (stages) w, w + W, w + 2W, ... (W = total waves) instead of
   // one contiguous range (default; DQ4ML_GRAM_INTERLEAVE=0 restores the contiguous ranges; both orders are fixed, so run-to-run
   // deterministic).  Every wave sweeps the whole row range in step with the others: measured ~1 % faster
   // at 1e8 rows and ~2.5 % at the 1.25e7-row 8-GPU shard (the waves' drain is more even)
@@ -43,6 +43,10 @@ struct GramArgs {
 // tile t, k-step i: 64 lanes x 16 B contiguous, lane l = 32h + f holding rows s*64+32h+8i..+8 of
 // feature 32t+f.  One wave load instruction = 1 KiB contiguous; zero padded to whole supersteps.
 int64_t tiled_elems(int d, int64_t n);
+
+// GramArgs::interleave for the tall bf16 kernel (1 unless DQ4ML_GRAM_INTERLEAVE=0); the stream
+// kernels keep contiguous ranges (DQ4ML_GRAM_STREAM_INTERLEAVE=1 for A/B)
+int gram_interleave();
 void tile_bf16(const void* X, int xdt, int64_t ld, int d, int64_t n, void* out, hipStream_t st);
 
 int64_t gram_partial_stride(int mode, int d);

@@ -1273,6 +1273,16 @@ void gram_reduce(int mode, const double* partials, int blocks, int d, double* ou
   DQ_HIP_CHECK(hipGetLastError());
 }
 
+int gram_interleave() {
+  // default on: same-box A/B (scripts/interleave_ab.sh, 5 alternations) 1e8 rows 1.011-1.015 vs
+  // 1.020-1.026 ms, 1.25e7 rows 0.1426-0.1441 vs 0.1471-0.1476 ms per fit (tall bf16 kernel)
+  static const int interleave = [] {
+    const char* e = getenv("DQ4ML_GRAM_INTERLEAVE");
+    return e && e[0] == '0' ? 0 : 1;
+  }();
+  return interleave;
+}
+
 void gram_tall(int mode, GramArgs a, int xmode, int blocks, double* out, hipStream_t st, bool reduce) {
   if (a.d < 1 || a.d > 64) throw std::invalid_argument("gram_tall: d must be in [1, 64]");
   if (blocks < 1) throw std::invalid_argument("gram_tall: blocks must be >= 1");
@@ -1281,15 +1291,7 @@ void gram_tall(int mode, GramArgs a, int xmode, int blocks, double* out, hipStre
   const int64_t total_waves = (int64_t)blocks * (block / kWave);
   a.spw = (a.nsuper + total_waves - 1) / total_waves;
   if (a.spw < 1) a.spw = 1;
-  {
-    static const int interleave = [] {
-      // default on: same-box A/B (scripts/interleave_ab.sh, 5 alternations) 1e8 rows 1.011-1.015 vs
-      // 1.020-1.026 ms, 1.25e7 rows 0.1426-0.1441 vs 0.1471-0.1476 ms per fit
-      const char* e = getenv("DQ4ML_GRAM_INTERLEAVE");
-      return e && e[0] == '0' ? 0 : 1;
-    }();
-    a.interleave = interleave;
-  }
+  a.interleave = gram_interleave();
   a.P = (int)gram_partial_stride(mode, a.d);
   const size_t lds = mode == GRAM_BF16 ? bf16_lds(a.d, xmode) : f64_lds(a.d);
   if (a.tiled && mode != GRAM_BF16) throw std::invalid_argument("gram_tall: tiled storage needs bf16 mode");
