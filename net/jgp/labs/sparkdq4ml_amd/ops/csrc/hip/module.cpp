@@ -144,6 +144,9 @@ PYBIND11_MODULE(_dq4ml_hip, m) {
                   iters, P<double>(o), P<double>(r), P<double>(p), P<double>(Ap), as_stream(stream));
   });
   m.attr("PCG_STATE_WORDS") = (int)PCG_STATE_WORDS;
+  m.attr("PCG_CONV") = (int)PCG_CONV;
+  m.attr("PCG_BAD") = (int)PCG_BAD;
+  m.attr("PCG_OK") = (int)PCG_OK;
   m.def("wls_qn_small", [](uintptr_t flat, int nf, bool fit_intercept, double reg, double enet, bool std_f,
                            bool std_l, int max_iter, double tol, int hist_cap, uintptr_t out, uintptr_t stream) {
     wls_qn_small(P<const double>(flat), nf, fit_intercept, reg, enet, std_f, std_l, max_iter, tol, hist_cap,

@@ -629,7 +629,8 @@ def wls_qn_small(flat: torch.Tensor, nf: int, fit_intercept: bool, reg: float, e
     return out
 
 
-PCG_STATE_WORDS = 8  # == WlsPcgState::PCG_STATE_WORDS (wls_large.h); checked against the module
+# control-block layout of wls_large.h (WlsPcgState), checked against the module on first use
+PCG_STATE_WORDS, PCG_CONV, PCG_BAD, PCG_OK = 8, 3, 4, 5
 
 
 @dataclass
@@ -648,7 +649,8 @@ def wls_assemble(flat: torch.Tensor, nf: int, fit_intercept: bool, wSum: float, 
     """Standardized dense system of the large-k WLS branch from the flat statistics (no host sync)."""
     h = native.hip()
     _check_dev(flat)
-    if int(h.PCG_STATE_WORDS) != PCG_STATE_WORDS:
+    if (int(h.PCG_STATE_WORDS), int(h.PCG_CONV), int(h.PCG_BAD), int(h.PCG_OK)) != (
+            PCG_STATE_WORDS, PCG_CONV, PCG_BAD, PCG_OK):
         raise RuntimeError("wls_large: control-block layout mismatch between device.py and the HIP module")
     if flat.dtype != torch.float64 or flat.numel() != 5 + 2 * nf + nf * (nf + 1) // 2:
         raise ValueError("wls_assemble: flat statistics have the wrong dtype/length")
@@ -684,10 +686,10 @@ def wls_pcg(sysm: WlsSystem, nf: int, bStd: float, rtol: float, chunk: int = 8,
                         int(nf), float(bStd), int(chunk), sysm.o.data_ptr(), r.data_ptr(), p.data_ptr(),
                         Ap.data_ptr(), st)
         o = sysm.o.cpu().numpy()
-        if o[4] != 0.0:  # PCG_BAD: a diagonal entry <= 0 (or NaN)
+        if o[PCG_BAD] != 0.0:  # a diagonal entry <= 0 (or NaN)
             return None
-        if o[3] != 0.0:  # PCG_CONV
-            return o if o[5] != 0.0 else None  # PCG_OK: the true residual check
+        if o[PCG_CONV] != 0.0:
+            return o if o[PCG_OK] != 0.0 else None  # the true residual check
     return None
 
 
