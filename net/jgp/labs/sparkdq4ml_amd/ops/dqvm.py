@@ -488,7 +488,7 @@ def _kernel_source(g: _Gen) -> str:
 
 VEC_ROWS = int(os.environ.get("DQ4ML_DQ_ROWS", "4"))  # consecutive rows per thread, vector form
 VEC_NT = os.environ.get("DQ4ML_DQ_NT", "0") != "0"  # non-temporal column loads (A/B knob)
-GRID_CAP = int(os.environ.get("DQ4ML_DQ_GRID", "8192"))  # grid-stride cap (blocks)
+GRID_CAP = int(os.environ.get("DQ4ML_DQ_GRID", "131072"))  # grid-stride cap (blocks); config 4 A/B 2x: 8192 5.997 / 5.925, 32768 5.894 / 5.910, 131072 5.872 / 5.859 ms
 _VEC_BASE = {"double": "double", "float": "float", "int": "int", "long long": "long long", "bool": "unsigned char",
              "unsigned char": "unsigned char"}
 _VEC_NAME = {"double": "f64", "float": "f32", "int": "i32", "long long": "i64", "bool": "u8", "unsigned char": "u8"}
