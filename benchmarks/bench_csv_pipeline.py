@@ -27,7 +27,7 @@ import tempfile
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 import harness  # noqa: E402
-from harness import emit, timed  # noqa: E402
+from harness import check_world, emit, self_launch, timed, world_info  # noqa: E402
 
 
 def synth_csv(path: str, rows: int, seed: int = 7) -> int:
@@ -85,6 +85,9 @@ def main(argv=None):
     ap.add_argument("--path", default=None, help="CSV to use (default: synthesize under $TMPDIR)")
     ap.add_argument("--json-out", default=None)
     a = ap.parse_args(argv)
+    rc = self_launch(a.gpus, __file__, argv)  # --gpus N: one process per GPU, before any GPU call
+    if rc is not None:
+        return rc
 
     from net.jgp.labs.sparkdq4ml_amd import LinearRegression, SparkSession, VectorAssembler, callUDF
     from net.jgp.labs.sparkdq4ml_amd.dq.rules import register_lab_rules
@@ -92,6 +95,8 @@ def main(argv=None):
     from net.jgp.labs.sparkdq4ml_amd.parallel import comm
 
     comm.init()
+    if not check_world(a.gpus):
+        return 2
     rank, world = comm.rank(), comm.world_size()
     spark = SparkSession.builder().appName("bench-csv").master("local[*]") \
         .config("dq4ml.fit.async", "true").getOrCreate()
@@ -134,6 +139,7 @@ def main(argv=None):
         torch.cuda.synchronize()
     first_ms = (time.perf_counter() - t0) * 1e3
     elapsed, model = timed(step, a.steps, max(0, a.warmup - 1), dev)
+    info = world_info(dev)
     emit({"metric": "rows/sec lab pipeline CSV -> DQ rules -> VectorAssembler -> LinearRegression.fit",
           "value": rows * a.steps / elapsed, "unit": "rows/s", "n_gpus": world, "steps": a.steps,
           "warmup": a.warmup, "ms_per_step": elapsed / a.steps * 1e3, "higher_is_better": True,
@@ -145,10 +151,11 @@ def main(argv=None):
                      "coefficients": [float(v) for v in model.coefficients.toArray()],
                      "intercept": float(model.intercept), "parallelism": f"dp{world}",
                      "first_action_ms": first_ms, "host_issue_ms_per_step": harness.LAST_ISSUE_S / a.steps * 1e3,
-                     "device_scans": csvscan.STATS["device_scans"], "scan_fallbacks": csvscan.STATS["fallbacks"]}},
-         a.json_out)
+                     "device_scans": csvscan.STATS["device_scans"], "scan_fallbacks": csvscan.STATS["fallbacks"]},
+          **info}, a.json_out)
     comm.shutdown()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

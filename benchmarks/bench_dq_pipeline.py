@@ -23,7 +23,7 @@ import os
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-from harness import emit, timed  # noqa: E402
+from harness import check_world, emit, self_launch, timed, world_info  # noqa: E402
 
 
 def build(spark, n, d, seed, dev):
@@ -58,6 +58,9 @@ def main(argv=None):
                     help="synchronous fits (host solve after a D2H every step); default: asynchronous "
                          "device solve, the host builds the next step's plan while the GPU runs")
     a = ap.parse_args(argv)
+    rc = self_launch(a.gpus, __file__, argv)  # --gpus N: one process per GPU, before any GPU call
+    if rc is not None:
+        return rc
     import numpy as np
 
     from net.jgp.labs.sparkdq4ml_amd import LinearRegression, SparkSession, VectorAssembler, callUDF, col
@@ -67,6 +70,8 @@ def main(argv=None):
     from net.jgp.labs.sparkdq4ml_amd.sql.types import DataTypes
 
     comm.init()
+    if not check_world(a.gpus):
+        return 2
     rank, world = comm.rank(), comm.world_size()
     spark = SparkSession.builder().appName("bench-dq").master("local[*]") \
         .config("dq4ml.fit.async", "true" if a.use_async else "false").getOrCreate()
@@ -92,6 +97,7 @@ def main(argv=None):
     err = float(np.abs(coef - beta.cpu().numpy()).max())
     total = n * world
     kept = model.summary.numInstances
+    info = world_info(dev)
     emit({"metric": "rows/sec DQ filters + VectorAssembler + LinearRegression.fit, 1e9x64 (BASELINE config 4)",
           "value": total * a.steps / elapsed, "unit": "rows/s", "n_gpus": world, "steps": a.steps,
           "warmup": a.warmup, "ms_per_step": elapsed / a.steps * 1e3, "higher_is_better": True,
@@ -101,9 +107,10 @@ def main(argv=None):
                      "global_batch": total, "seq_len": d, "parallelism": f"dp{world}", "rows_per_gpu": n,
                      "rows_kept_global": int(kept), "coef_max_abs_err": err,
                      "dq_vm": dict(dqvm.STATS),
-                     "fit_mode": "async" if (a.use_async and dev.type == "cuda") else "sync"}}, a.json_out)
+                     "fit_mode": "async" if (a.use_async and dev.type == "cuda") else "sync"}, **info}, a.json_out)
     comm.shutdown()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -1,10 +1,11 @@
 #!/usr/bin/env python3
 """BASELINE.json config #5: wide regression, 1e7 rows x 4096 features, fp8 (MFMA-bound LDS-tiled
 XᵀX).  One step = one ``LinearRegression.fit`` (normal equations): fp8 wide SYRK
-(``gram_wide.hip``, block-scaled K=64 MFMA) over the rank's rows + split-K f64 reduction -> RCCL
-all-reduce of the 8.4 M-entry f64 statistics -> standardization + f64 Cholesky of the 4097-order
-system on the device -> model.  regParam 0.01 / elasticNet 0 (L2 -> Cholesky; an L1 penalty
-would run OWLQN over the 4096² packed matrix on the host).
+(``gram_wide.hip``, block-scaled K=64 MFMA) over the rank's rows + split-K reduction folded band
+by band, each band's RCCL all-reduce in flight while the next folds -> standardization + the
+4097-order solve on the device (``wls_large.hip``: assembly + Jacobi-PCG) -> model.  regParam 0.01
+/ elasticNet 0 (L2; an L1 penalty runs the device OWLQN over the dense standardized system,
+``models/owlqn_device.py``).
 
 Features are stream-ingested straight into the fp8 fragment layout (64-row-aligned chunks, one
 global per-feature scale) — the 41 GB matrix never exists in a wider dtype.
@@ -18,7 +19,7 @@ import os
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-from harness import emit, timed  # noqa: E402
+from harness import check_world, emit, self_launch, timed, world_info  # noqa: E402
 
 
 def main(argv=None):
@@ -31,6 +32,9 @@ def main(argv=None):
     ap.add_argument("--dtype", default="fp8", choices=["fp8", "bf16"])
     ap.add_argument("--json-out", default=None)
     a = ap.parse_args(argv)
+    rc = self_launch(a.gpus, __file__, argv)  # --gpus N: one process per GPU, before any GPU call
+    if rc is not None:
+        return rc
     import numpy as np
     import torch
 
@@ -40,14 +44,24 @@ def main(argv=None):
     from net.jgp.labs.sparkdq4ml_amd.parallel import comm
 
     comm.init()
+    if not check_world(a.gpus):
+        return 2
     rank, world = comm.rank(), comm.world_size()
     spark = SparkSession.builder().appName("bench-wide").master("local[*]").getOrCreate()
     dev = spark.device
-    if dev.type != "cuda":
-        raise SystemExit("bench_wide needs an MI355X (the wide fp8 layout is a device format)")
     d, total = a.features, int(a.rows)
+    if dev.type != "cuda":  # host-engine rehearsal of the launcher / JSON contract: small dense shape
+        d, total = min(d, 96), min(total, 20_000 * world)
     n = total // world if rank < world - 1 else total - (world - 1) * (total // world)
     eb = 8 if a.dtype == "fp8" else 16
+    if dev.type != "cuda":
+        g = torch.Generator().manual_seed(4321 + rank)
+        beta = torch.linspace(-1.0, 1.0, d)
+        X = torch.randn(d, n, generator=g)
+        y = beta @ X + 0.5 + 0.1 * torch.randn(n, generator=g)
+        df = spark.createDataFrame({"features": X, "label": y})
+        lr = LinearRegression(solver="normal", regParam=0.01, elasticNetParam=0.0)
+        return _report(a, lr, df, beta, total, world, d, n, dev, timed, emit, world_info, comm)
     h = native.hip()
     buf = torch.empty(int(h.wide_tiled_bytes(eb, d, n)), dtype=torch.uint8, device=dev)
     per_row = buf.numel() // (((n + 63) // 64) * 64)
@@ -67,20 +81,29 @@ def main(argv=None):
     X = TiledWide(buf, d, n, eb, scale if eb == 8 else None)
     df = spark.createDataFrame({"features": X, "label": y})
     lr = LinearRegression(solver="normal", gramDtype=a.dtype, regParam=0.01, elasticNetParam=0.0)
+    return _report(a, lr, df, beta, total, world, d, n, dev, timed, emit, world_info, comm)
+
+
+def _report(a, lr, df, beta, total, world, d, n, dev, timed, emit, world_info, comm):
+    import numpy as np
+
     elapsed, model = timed(lambda: lr.fit(df), a.steps, a.warmup, dev)
     coef = np.asarray(model.coefficients.toArray())
     err = float(np.abs(coef - beta.double().cpu().numpy()).max())
     ms = elapsed / a.steps * 1e3
+    info = world_info(dev)
     emit({"metric": "rows/sec LinearRegression.fit, wide 1e7x4096 fp8 (BASELINE config 5)",
           "value": total * a.steps / elapsed, "unit": "rows/s", "n_gpus": world, "steps": a.steps,
           "warmup": a.warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": "strong",
-          "vs_baseline": None, "dtype": a.dtype, "data": "synthetic (N(0,1) features, random-init coefficients)",
+          "vs_baseline": None, "dtype": a.dtype if dev.type == "cuda" else "fp64",
+          "data": "synthetic (N(0,1) features, random-init coefficients)",
           "config": {"model": f"LinearRegression(normal equations, L2 0.01) d={d}", "global_batch": total,
                      "seq_len": d, "parallelism": f"dp{world}", "rows_per_gpu": n,
-                     "useful_tflops": total * d * (d + 1) / (ms * 1e-3) / 1e12, "coef_max_abs_err": err}},
-         a.json_out)
+                     "useful_tflops": total * d * (d + 1) / (ms * 1e-3) / 1e12, "coef_max_abs_err": err},
+          **info}, a.json_out)
     comm.shutdown()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

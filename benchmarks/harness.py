@@ -16,6 +16,45 @@ if ROOT not in sys.path:
 LAST_ISSUE_S = 0.0
 
 
+def self_launch(gpus: int, script: str, argv=None):
+    """``bench.py``'s ``--gpus`` contract for the config benchmarks.  Returns an exit code the
+    caller returns at once -- N ranks were started through ``parallel/launch.py`` (one process per
+    GPU, BEFORE this process touches the GPU) or the launcher's world size disagrees (2) -- or None
+    when this process is a rank and runs the benchmark."""
+    if gpus > 1 and int(os.environ.get("WORLD_SIZE", "1")) != gpus:
+        if "WORLD_SIZE" in os.environ:
+            print(f"[bench] --gpus {gpus} but WORLD_SIZE={os.environ['WORLD_SIZE']}", file=sys.stderr)
+            return 2
+        from net.jgp.labs.sparkdq4ml_amd.parallel.launch import launch
+
+        return launch(gpus, [os.path.abspath(script)] + list(sys.argv[1:] if argv is None else argv))
+    return None
+
+
+def check_world(gpus: int) -> bool:
+    """After ``comm.init()``: the process group has exactly ``--gpus`` ranks (and GPUs exist)."""
+    import torch
+
+    from net.jgp.labs.sparkdq4ml_amd.parallel import comm
+
+    if torch.cuda.is_available() and gpus > torch.cuda.device_count():
+        print(f"[bench] --gpus {gpus} but only {torch.cuda.device_count()} visible GPU(s)", file=sys.stderr)
+        return False
+    if comm.world_size() != gpus:
+        print(f"[bench] --gpus {gpus} but the process group has {comm.world_size()} rank(s)", file=sys.stderr)
+        return False
+    return True
+
+
+def world_info(dev) -> dict:
+    """``world`` / ``backend`` / ``rank_devices`` keys of the JSON line (collective: every rank calls)."""
+    from net.jgp.labs.sparkdq4ml_amd.parallel import comm
+
+    ranks = comm.all_gather_object({"rank": comm.rank(), "device": str(dev)})
+    return {"world": comm.world_size(), "backend": comm.backend() or "none",
+            "rank_devices": [r["device"] for r in ranks]}
+
+
 def timed(step, steps: int, warmup: int, dev):
     import torch
 

@@ -8,13 +8,17 @@
   afterwards (GLMNET style);
 * huber: L-BFGS-B over (coefficients, intercept, σ) with σ > 0 (see :func:`_train_huber`).
 
-MI355X design: Spark re-scans the data every iteration (``LeastSquaresAggregator`` inside a
-``treeAggregate``).  For squared error that loss is a quadratic form in the
-sufficient statistics, so ONE fused MFMA Gram pass (the same kernel as the normal-equation path)
-plus an O(d^2) f64 iteration replaces maxIter data passes — identical objective, identical
-optimizer, no per-iteration all-reduce; with 288 GB of HBM the d x d Gram fits for any d this path
-targets.  Huber is not quadratic and keeps per-iteration device passes (``kernels.huber_loss_grad``)
-with one all-reduce of (d+3) f64 per evaluation.
+MI355X design: Spark re-scans the data for every cost evaluation
+(``LeastSquaresAggregator`` inside a ``treeAggregate``).  Here too, by default
+(``dq4ml.lbfgs.mode = passes``): one summarizer pass for the feature moments, then per evaluation
+two streaming HIP passes over the HBM-resident shard (``ops/csrc/hip/lsq.hip``: margins, then
+Σ w·diff·x) and ONE RCCL all-reduce of (d + 1) f64 — O(n·d) device work per evaluation, never the
+d x d Gram.  The Breeze optimizer state lives on the device (``models/qn_device.py``).
+
+``dq4ml.lbfgs.mode = gram``: squared error is a quadratic form in the sufficient statistics, so ONE
+fused MFMA Gram pass plus an O(d^2) host iteration gives the same optimum (the same optimizer on the
+same objective) — cheaper when n·d^2 of MFMA work beats maxIter data passes.  Huber is not quadratic
+and keeps per-iteration device passes (``kernels.huber_pass``).
 """
 from __future__ import annotations
 
@@ -23,6 +27,7 @@ import torch
 
 from ..ops import kernels, native
 from ..parallel import comm
+from ..utils import tracing
 from ..utils.logging import get_logger
 from .linalg import DenseVector
 from .optim import GramStats, packed_upper_indices
@@ -59,6 +64,10 @@ def train_lbfgs(est, df, tbl, X, y, d):
         sel = y.valid if sel is None else (sel & y.valid)
     if loss == "huber":
         return _train_huber(est, df, tbl, X, y, w, sel, d)
+    sess = getattr(df, "sparkSession", None)
+    mode = str(sess.conf.get("dq4ml.lbfgs.mode", "passes")).lower() if sess is not None else "passes"
+    if mode != "gram":
+        return _train_passes(est, df, X, y, w, sel, d)
     flat = kernels.gram_stats(X.values, y.values, w, sel, est.getOrDefault("gramDtype"))
     flat = comm.all_reduce_sum(flat)
     stats = GramStats.from_flat(flat.cpu().numpy(), d)
@@ -107,6 +116,155 @@ def train_lbfgs(est, df, tbl, X, y, d):
     coef = np.where(zero, 0.0, np.asarray(x) * ys / safe)
     icpt = my - float(np.dot(coef, mx)) if fit_icpt else 0.0
     return finish(coef, icpt, hist, "owlqn" if l1vec is not None else "l-bfgs")
+
+
+def _train_passes(est, df, X, y, w, sel, d):
+    """Spark 2.4 ``LinearRegression.train`` l-bfgs branch with squared error, data pass per
+    evaluation: summarizer moments -> standardization / regularization constants -> Breeze
+    L-BFGS (L2) or OWLQN (L1 > 0) over ``LeastSquaresCostFun`` -> un-standardize."""
+    from .qn_device import minimize
+    from .regression import LinearRegressionModel, LinearRegressionTrainingSummary
+
+    P = kernels.lsq_passes(X.values, y.values, w, sel)
+    dev = P.device
+    with tracing.span("gram"):  # the summarizer pass (feature moments), one all-reduce with the scalars
+        head = comm.all_reduce_sum(torch.cat([P.scalars(), P.moments()]))
+    host = head.cpu().numpy()
+    count, W, W2, bsum, bbsum = (float(v) for v in host[:5])
+    sx_sum, sxx_sum = host[5:5 + d], host[5 + d:5 + 2 * d]
+    stats = GramStats.scalars_only(host[:5], d)
+    fit_icpt = bool(est.getOrDefault("fitIntercept"))
+    std_flag = bool(est.getOrDefault("standardization"))
+    reg, enet = float(est.getOrDefault("regParam")), float(est.getOrDefault("elasticNetParam"))
+    max_iter, tol = int(est.getOrDefault("maxIter")), float(est.getOrDefault("tol"))
+    if W <= 0.0:
+        raise ValueError("requirement failed: The training dataset is empty (weight sum is 0).")
+    denom = W - W2 / W
+    mx = sx_sum / W
+    my = bsum / W
+    var_x = np.maximum(sxx_sum - W * mx * mx, 0.0) / denom if denom > 0 else np.zeros(d)
+    var_y = max(bbsum - W * my * my, 0.0) / denom if denom > 0 else 0.0
+    sx, raw_ys = np.sqrt(var_x), float(np.sqrt(var_y))
+
+    def finish(coef, icpt, hist, solver):
+        model = LinearRegressionModel(est.uid, DenseVector(coef), float(icpt))
+        est.copyValues(model)
+        model._set_summary(LinearRegressionTrainingSummary(model, df, None, hist, stats=stats, solver=solver))
+        return model
+
+    if raw_ys == 0.0 and (fit_icpt or my == 0.0):
+        log.warning("The standard deviation of the label is zero, so the coefficients will be zeros and the "
+                    "intercept will be the mean of the label; as a result, training is not needed.")
+        return finish(np.zeros(d), my if fit_icpt else 0.0, np.zeros(1), "none")
+    ys = raw_ys if raw_ys > 0 else abs(my)
+    eff_reg = reg / ys
+    l1, l2 = enet * eff_reg, (1.0 - enet) * eff_reg
+    nz = sx != 0.0
+    safe = np.where(nz, sx, 1.0)
+    t = lambda a: torch.as_tensor(np.ascontiguousarray(a, dtype=np.float64), device=dev)  # noqa: E731
+    inv_sx, mx_t = t(np.where(nz, 1.0 / safe, 0.0)), t(mx)
+    reg_w = None  # L2 weights per coordinate (standardization=false: 1 / sigma^2)
+    if l2 != 0.0:
+        reg_w = torch.ones(d, dtype=torch.float64, device=dev) if std_flag else t(np.where(nz, 1.0 / (safe * safe), 0.0))
+    icpt0 = torch.tensor(my / ys if fit_icpt else 0.0, dtype=torch.float64, device=dev)
+    inv_ys, inv_w = 1.0 / ys, 1.0 / W
+
+    def fg(x):
+        cf = x * inv_sx
+        offset = icpt0 - torch.dot(cf, mx_t) if fit_icpt else icpt0
+        with tracing.span("lsq_pass"):
+            out = P.evaluate(cf, offset, inv_ys)
+        with tracing.span("allreduce"):
+            out = comm.all_reduce_sum(out)  # X4: (d + 1) f64 per evaluation
+        tracing.add_rows("lsq_pass", P.n)
+        loss = out[0] * inv_w
+        g = out[1:] * inv_sx * inv_w
+        if reg_w is not None:
+            rx = reg_w * x
+            loss = loss + 0.5 * l2 * torch.dot(x, rx)
+            g = g + l2 * rx
+        return loss, g
+
+    l1vec = None
+    if enet != 0.0 and eff_reg != 0.0:
+        l1vec = torch.full((d,), l1, dtype=torch.float64, device=dev) if std_flag else t(np.where(nz, l1 / safe, 0.0))
+    ck = _QNCheckpoint.of(df, head, (d, fit_icpt, reg, enet, std_flag, max_iter, tol))
+    resume = ck.load() if ck is not None else None
+    if resume is not None:
+        log.info("resuming l-bfgs at iteration %d from %s", int(resume["iter"]), ck.path)
+    x, hist, reason = minimize(fg, torch.zeros(d, dtype=torch.float64, device=dev), max_iter, tol, l1vec,
+                               resume=resume, on_iteration=ck.maybe_save if ck is not None else None)
+    if ck is not None:
+        ck.clear()
+    log.info("l-bfgs path (data passes): %s after %d states", reason, len(hist))
+    coef = np.where(nz, x.cpu().numpy() * ys / safe, 0.0)
+    icpt = my - float(np.dot(coef, mx)) if fit_icpt else 0.0
+    return finish(coef, icpt, np.asarray(hist, dtype=np.float64), "owlqn" if l1vec is not None else "l-bfgs")
+
+
+_QN_FAIL_AT_ITER = None  # tests: raise after this iteration's checkpoint (simulated crash)
+
+
+class _QNCheckpoint:
+    """Optimizer-state checkpoints of the squared-loss l-bfgs path, the counterpart
+    of the Huber fit's ``_Checkpoint``: with ``dq4ml.lbfgs.checkpointDir`` set, the complete Breeze
+    state (iterate, gradients, s/y history, function-value window, objective history, failure
+    flags) is written every ``dq4ml.lbfgs.checkpointInterval`` iterations; a re-run of the same fit
+    on the same data (fingerprinted by its all-reduced moments) resumes from it and ends exactly as
+    the uninterrupted run."""
+
+    def __init__(self, path: str, every: int):
+        self.path, self.every = path, max(1, int(every))
+
+    @classmethod
+    def of(cls, df, head, params):
+        import hashlib
+        import os
+
+        sess = getattr(df, "sparkSession", None)
+        root = sess.conf.get("dq4ml.lbfgs.checkpointDir", "") if sess is not None else ""
+        if not root:
+            return None
+        h = hashlib.sha1(repr(params).encode())
+        h.update(np.ascontiguousarray(head.cpu().numpy()).tobytes())
+        os.makedirs(root, exist_ok=True)
+        return cls(os.path.join(root, f"lsq-{h.hexdigest()[:20]}.npz"),
+                   int(sess.conf.get("dq4ml.lbfgs.checkpointInterval", "10")))
+
+    def maybe_save(self, state):
+        import os
+
+        it = int(state["iter"])
+        if it % self.every == 0 and comm.rank() == 0:
+            host = {k: (v.cpu().numpy() if torch.is_tensor(v) else v) for k, v in state.items() if k not in ("S", "Y")}
+            S = np.stack([s.cpu().numpy() for s in state["S"]]) if state["S"] else np.zeros((0, 0))
+            Y = np.stack([y.cpu().numpy() for y in state["Y"]]) if state["Y"] else np.zeros((0, 0))
+            tmp = self.path + ".tmp.npz"
+            np.savez(tmp, S=S, Y=Y, **{k: np.asarray(v) for k, v in host.items()})
+            os.replace(tmp, self.path)
+        if _QN_FAIL_AT_ITER is not None and it == _QN_FAIL_AT_ITER:
+            raise RuntimeError(f"injected failure after l-bfgs iteration {it}")
+
+    def load(self):
+        import os
+
+        comm.barrier()
+        if not os.path.exists(self.path):
+            return None
+        z = np.load(self.path)  # allow_pickle=False: plain arrays only
+        st = {k: z[k] for k in z.files}
+        st["S"] = list(st["S"]) if st["S"].size else []
+        st["Y"] = list(st["Y"]) if st["Y"].size else []
+        st["fvals"] = [float(v) for v in st["fvals"]]
+        st["history"] = [float(v) for v in st["history"]]
+        return st
+
+    def clear(self):
+        import os
+
+        comm.barrier()
+        if comm.rank() == 0 and os.path.exists(self.path):
+            os.remove(self.path)
 
 
 def _train_huber(est, df, tbl, X, y, w, sel, d):

@@ -169,17 +169,23 @@ _SOLVER_CODES = {"auto": 0, "cholesky": 1, "quasi-newton": 2}
 
 def fit_wls_flat(flat, nf: int, fit_intercept: bool, reg_param: float, elastic_net: float,
                  standardize_features: bool, standardize_label: bool, solver_type: str, max_iter: int,
-                 tol: float):
+                 tol: float, host_only: bool = False):
     """``WeightedLeastSquares.fit`` straight from the (all-reduced) flat statistics.
 
     Returns ``(WLSModel, GramStats)``.  k <= 1024 (or host statistics): one D2H of the flat vector
     and the native driver ``_dq4ml_host.wls_fit`` (standardize -> Cholesky / OWLQN / L-BFGS ->
     un-standardize in C++).  Larger k with the statistics on the device and no L1 term: the
     standardized system is assembled and Cholesky-solved on the device (f64), only the
-    coefficients come back."""
+    coefficients come back.  ``host_only``: straight to the native driver (the cases a device
+    solver handed back: running the device solve again would only repeat its answer)."""
     import torch
 
     k = nf + 1 if fit_intercept else nf
+    if host_only:
+        host = flat.detach().cpu().numpy() if torch.is_tensor(flat) else np.asarray(flat, dtype=np.float64)
+        stats = GramStats.from_flat(host, nf)
+        return _wls_native(host, stats, fit_intercept, reg_param, elastic_net, standardize_features,
+                           standardize_label, solver_type, max_iter, tol), stats
     use_qn = (solver_type == "auto" and elastic_net != 0.0 and reg_param != 0.0) or solver_type == "quasi-newton"
     if torch.is_tensor(flat) and flat.is_cuda and use_qn and elastic_net != 0.0 and reg_param != 0.0:
         res = wls_owlqn_device(flat, nf, fit_intercept, reg_param, elastic_net, standardize_features,

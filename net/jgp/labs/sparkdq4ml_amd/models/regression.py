@@ -444,10 +444,12 @@ class _PendingWLS:
                 from .optim import owlqn_result
 
                 r = owlqn_result(host, d)
-                self._res = r if r is not None else fit_wls_flat(*self.args)
+                # handed back (label / weight short-circuits, history capacity): the native driver,
+                # not a second device solve
+                self._res = r if r is not None else fit_wls_flat(*self.args, host_only=True)
                 return self._res
             if int(host[d + 1]) != 0:  # edge case: the host driver owns warnings/errors/fallbacks
-                self._res = fit_wls_flat(*self.args)
+                self._res = fit_wls_flat(*self.args, host_only=True)
             else:
                 from .optim import WLSModel
 

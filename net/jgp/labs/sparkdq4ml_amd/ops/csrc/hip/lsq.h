@@ -1,0 +1,35 @@
+// K9: per-evaluation data passes of the squared-loss l-bfgs / OWLQN path (lsq.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace dq4ml {
+
+// Feature-matrix layouts (the ``tiled`` codes of rowops): 0 plain feature-major [d][ld] of xdt
+// (f64 / f32 / bf16), 1 tall bf16 tiles (TiledBF16), 2 wide bf16 tiles, 3 wide fp8 tiles (TiledWide).
+struct LsqX {
+  const void* X;
+  int layout;
+  int xdt;      // layout 0 only
+  int64_t ld;   // layout 0 only
+  int d;
+  int64_t n;
+};
+
+// workspace sizes (doubles) of one evaluation / one moments pass
+int64_t lsq_part_doubles(const LsqX& x, int mode);
+int lsq_margin_blocks(const LsqX& x);
+
+// Margin pass: v[r] = w[r] * (x_r . cf + *offset - y[r] * inv_ystd), loss partial sum of 1/2 w diff^2 per
+// block (lpart[lsq_margin_blocks]).  cf: effective coefficients (f32 for the tile layouts, f64 plain).
+void lsq_margin(const LsqX& x, const void* cf, const double* offset, double inv_ystd, const double* y, const double* w,
+                double* v, double* lpart, hipStream_t st);
+
+// Column pass: mode 0 -> out[1 + j] = sum_r v[r] x[r][j] and out[0] = sum(lpart) (the evaluation);
+// mode 1 -> out[j] = sum_r v[r] x[r][j], out[d + j] = sum_r v[r] x[r][j]^2 (feature moments, v = w).
+// part: lsq_part_doubles(x, mode) doubles of workspace.  Fixed-order reductions (deterministic).
+void lsq_columns(const LsqX& x, int mode, const double* v, const double* lpart, int nl, double* part, double* out,
+                 hipStream_t st);
+
+}  // namespace dq4ml

@@ -14,6 +14,7 @@
 #include "wls_small.h"
 #include "wls_large.h"
 #include "rowops.h"
+#include "lsq.h"
 
 namespace py = pybind11;
 using namespace dq4ml;
@@ -259,6 +260,34 @@ PYBIND11_MODULE(_dq4ml_hip, m) {
     huber_pass(P<const void>(X), xdt, ld, d, n, tiled, P<const void>(y), ydt, P<const void>(w), wdt,
                P<const uint8_t>(sel), P<const double>(ceff), icpt, sigma, eps, P<double>(mult), P<double>(partials),
                P<double>(out), as_stream(stream));
+  });
+  // ---- K9: squared-loss l-bfgs evaluation passes ----------------------------------------------
+  auto lsqx = [](uintptr_t X, int layout, int xdt, int64_t ld, int d, int64_t n) {
+    LsqX x{};
+    x.X = P<const void>(X);
+    x.layout = layout;
+    x.xdt = xdt;
+    x.ld = ld;
+    x.d = d;
+    x.n = n;
+    return x;
+  };
+  m.def("lsq_margin_blocks", [lsqx](uintptr_t X, int layout, int xdt, int64_t ld, int d, int64_t n) {
+    return lsq_margin_blocks(lsqx(X, layout, xdt, ld, d, n));
+  });
+  m.def("lsq_part_doubles", [lsqx](uintptr_t X, int layout, int xdt, int64_t ld, int d, int64_t n, int mode) {
+    return lsq_part_doubles(lsqx(X, layout, xdt, ld, d, n), mode);
+  });
+  m.def("lsq_margin", [lsqx](uintptr_t X, int layout, int xdt, int64_t ld, int d, int64_t n, uintptr_t cf,
+                             uintptr_t offset, double inv_ystd, uintptr_t y, uintptr_t w, uintptr_t v, uintptr_t lpart,
+                             uintptr_t stream) {
+    lsq_margin(lsqx(X, layout, xdt, ld, d, n), P<const void>(cf), P<const double>(offset), inv_ystd, P<const double>(y),
+               P<const double>(w), P<double>(v), P<double>(lpart), as_stream(stream));
+  });
+  m.def("lsq_columns", [lsqx](uintptr_t X, int layout, int xdt, int64_t ld, int d, int64_t n, int mode, uintptr_t v,
+                              uintptr_t lpart, int nl, uintptr_t part, uintptr_t out, uintptr_t stream) {
+    lsq_columns(lsqx(X, layout, xdt, ld, d, n), mode, P<const double>(v), P<const double>(lpart), nl, P<double>(part),
+                P<double>(out), as_stream(stream));
   });
   m.def("regression_metrics",
         [](uintptr_t X, int xdt, int64_t ld, int d, int64_t n, uintptr_t y, int ydt, uintptr_t sel, uintptr_t coef,

@@ -591,6 +591,81 @@ def huber_pass(X, y, w, sel, ceff, icpt, sigma, eps):
 
 
 # ------------------------------------------------------------------------------------------
+# K9 -- squared-loss l-bfgs evaluation passes (lsq.hip)
+class LsqPasses:
+    """Device state of one squared-loss l-bfgs / OWLQN fit (Spark ``LeastSquaresAggregator``): the
+    feature matrix as the kernels read it, the label and the effective row weights (selection and
+    label nulls folded in: w = 0) as f64 rows, and the per-evaluation workspaces.  Every method
+    enqueues on the current stream and returns device tensors (no host sync)."""
+
+    def __init__(self, X, y, w, sel):
+        h = self._h = native.hip()
+        d, n = X.shape
+        self.d, self.n = int(d), int(n)
+        self.scales = None
+        if isinstance(X, TiledWide):
+            self._xb, self.layout, self.xdt, self.ld = X.buf, (2 if X.eb == 16 else 3), 2, 0
+            if X.eb == 8:
+                self.scales = X.scales.to(torch.float64)
+        elif isinstance(X, TiledBF16):
+            self._xb, self.layout, self.xdt, self.ld = X.buf, 1, 2, 0
+        else:
+            if X.dtype not in (torch.float64, torch.float32, torch.bfloat16):
+                X = X.to(torch.float64)
+            Xv, ld = _feature_view(X, 4)
+            self._xb, self.layout, self.xdt, self.ld = Xv, 0, dtype_code(Xv), int(ld)
+        _check_dev(self._xb, y, w, sel)
+        dev = self.device = self._xb.device
+        if y.numel() != n or (w is not None and w.numel() != n) or (sel is not None and sel.numel() != n):
+            raise ValueError("lsq: row-count mismatch between features, label, weight and selection")
+        wt = torch.ones(n, dtype=torch.float64, device=dev) if w is None else w.to(torch.float64)
+        if sel is not None:
+            wt = torch.where(sel.to(torch.bool), wt, torch.zeros_like(wt))
+        self.w = wt.contiguous()
+        self.y = torch.where(self.w != 0, y.to(torch.float64), torch.zeros_like(self.w)).contiguous()
+        self._desc = (self._xb.data_ptr(), self.layout, self.xdt, self.ld, self.d, self.n)
+        self.nl = int(h.lsq_margin_blocks(*self._desc))
+        self._v = torch.empty(max(self.n, 1), dtype=torch.float64, device=dev)
+        self._lpart = torch.empty(self.nl, dtype=torch.float64, device=dev)
+        self._part = {m: torch.empty(max(int(h.lsq_part_doubles(*self._desc, m)), 1), dtype=torch.float64,
+                                     device=dev) for m in (0, 1)}
+
+    def scalars(self) -> torch.Tensor:
+        """[count, wSum, wwSum, Σ w y, Σ w y²] over the live rows."""
+        w, y = self.w, self.y
+        return torch.stack([(w != 0).sum().to(torch.float64), w.sum(), (w * w).sum(), (w * y).sum(),
+                            (w * y * y).sum()])
+
+    def moments(self) -> torch.Tensor:
+        """[Σ w x_j (d), Σ w x_j² (d)] (f64; the summarizer pass of the l-bfgs path)."""
+        out = torch.empty(2 * self.d, dtype=torch.float64, device=self.device)
+        self._h.lsq_columns(*self._desc, 1, self.w.data_ptr(), 0, 0, self._part[1].data_ptr(), out.data_ptr(),
+                            _stream())
+        if self.scales is not None:  # the pass saw q = x / scale
+            out[:self.d] *= self.scales
+            out[self.d:] *= self.scales * self.scales
+        return out
+
+    def evaluate(self, cf: torch.Tensor, offset: torch.Tensor, inv_ystd: float) -> torch.Tensor:
+        """[Σ ½ w diff², Σ w diff x_j (d)] with diff = x . cf + offset - y * inv_ystd (f64; ``offset``
+        a one-element device tensor, read by the kernel: launching a pass needs no host sync)."""
+        c = cf.to(torch.float64)
+        off = offset.to(torch.float64).reshape(1).contiguous()
+        if self.scales is not None:
+            c = c * self.scales
+        c = c.contiguous() if self.layout == 0 else c.to(torch.float32).contiguous()
+        out = torch.empty(1 + self.d, dtype=torch.float64, device=self.device)
+        st = _stream()
+        self._h.lsq_margin(*self._desc, c.data_ptr(), off.data_ptr(), float(inv_ystd), self.y.data_ptr(),
+                           self.w.data_ptr(), self._v.data_ptr(), self._lpart.data_ptr(), st)
+        self._h.lsq_columns(*self._desc, 0, self._v.data_ptr(), self._lpart.data_ptr(), self.nl,
+                            self._part[0].data_ptr(), out.data_ptr(), st)
+        if self.scales is not None:
+            out[1:] *= self.scales
+        return out
+
+
+# ------------------------------------------------------------------------------------------
 def wls_small(flat: torch.Tensor, nf: int, fit_intercept: bool, reg: float, enet: float, std_f: bool,
               std_l: bool) -> torch.Tensor:
     """Device WLS Cholesky (k <= 65) from the flat statistics, enqueued on the current stream:
@@ -935,14 +1010,22 @@ def _fold_all_reduce(fold, out: torch.Tensor, P: int, d: int):
 
     wire = comm.wire_dtype()
     f32 = wire == torch.float32
+    base = 5 + 2 * d
     buf = torch.empty(out.numel(), dtype=torch.float32, device=out.device) if f32 else out
     stream = _stream()
     works = []
     for J0, J1, lo, hi in wide_bands(P, d, comm.bucket_bytes(), buf.element_size()):
-        fold(0 if f32 else out.data_ptr(), buf.data_ptr() if f32 else 0, J0, J1, stream)
-        works.append(dist.all_reduce(buf[lo:hi], op=dist.ReduceOp.SUM, async_op=True))
+        if f32 and J0 != P:
+            fold(0, buf.data_ptr(), J0, J1, stream)
+            works.append(dist.all_reduce(buf[lo:hi], op=dist.ReduceOp.SUM, async_op=True))
+        else:
+            # the head band (count, wSum, wwSum, Σy, Σy², aSum, abSum: 5 + 2d values) is always
+            # reduced in f64: counts above 2^24 stay exact and the variances E[x²] - E[x]² keep
+            # their digits; only the packed Σxx bands may take the f32 wire
+            fold(out.data_ptr(), 0, J0, J1, stream)
+            works.append(dist.all_reduce(out[lo:hi], op=dist.ReduceOp.SUM, async_op=True))
     for w in works:
         w.wait()  # the compute stream waits for every band's collective
     if f32:
-        out.copy_(buf)
+        out[base:].copy_(buf[base:])
     comm.mark_reduced(out)

@@ -217,4 +217,51 @@ def huber_pass(X, y, w, sel, ceff: np.ndarray, icpt: float, sigma: float, eps: f
     return out
 
 
+# ------------------------------------------------------------------------------------------
+# K9 — squared-loss l-bfgs evaluation passes
+# ------------------------------------------------------------------------------------------
+class _HostLsq:
+    """fp64 host implementation of :class:`ops.device.LsqPasses` (CPU engine; the kernel tests'
+    oracle)."""
+
+    def __init__(self, X, y, w, sel):
+        self.X = (X.to_dense() if hasattr(X, "to_dense") else X).to(torch.float64)
+        self.d, self.n = int(self.X.shape[0]), int(self.X.shape[1])
+        wt = torch.ones(self.n, dtype=torch.float64) if w is None else w.to(torch.float64)
+        if sel is not None:
+            wt = torch.where(sel.to(torch.bool), wt, torch.zeros_like(wt))
+        self.w = wt
+        self.y = torch.where(wt != 0, y.to(torch.float64), torch.zeros_like(wt))
+        self.device = self.X.device
+        self._Xz = torch.where(wt.unsqueeze(0) != 0, self.X, torch.zeros_like(self.X))  # dead rows: no NaN
+
+    def scalars(self):
+        w, y = self.w, self.y
+        return torch.stack([(w != 0).sum().to(torch.float64), w.sum(), (w * w).sum(), (w * y).sum(),
+                            (w * y * y).sum()])
+
+    def moments(self):
+        return torch.cat([self._Xz @ self.w, (self._Xz * self._Xz) @ self.w])
+
+    def evaluate(self, cf, offset, inv_ystd):
+        cf = cf.to(torch.float64)
+        diff = cf @ self._Xz + torch.as_tensor(offset, dtype=torch.float64).reshape(()) - self.y * inv_ystd
+        v = torch.where(self.w != 0, self.w * diff, torch.zeros_like(diff))
+        out = torch.empty(1 + self.d, dtype=torch.float64)
+        out[0] = (0.5 * v * diff).sum()
+        out[1:] = self._Xz @ v
+        return out
+
+
+def lsq_passes(X, y: torch.Tensor, w: Optional[torch.Tensor], sel: Optional[torch.Tensor]):
+    """Per-fit state of the squared-loss l-bfgs path: ``.scalars()``,
+    ``.moments()`` (summarizer pass) and ``.evaluate(cf, offset, inv_ystd)`` (one
+    ``LeastSquaresAggregator`` pass) — device kernels for device data, fp64 torch on the host."""
+    if _on_gpu(X if torch.is_tensor(X) else X.buf):
+        from . import device
+
+        return device.LsqPasses(X, y, w, sel)
+    return _HostLsq(X, y, w, sel)
+
+
 _ = (List, native)

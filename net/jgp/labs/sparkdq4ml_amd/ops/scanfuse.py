@@ -42,6 +42,11 @@ _HDR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "csrc", "hip", "
 _header_text: Optional[str] = None
 
 
+
+class _GramNullable(ValueError):
+    """The in-scan Gram epilogue cannot take a chain whose feature / label outputs are nullable;
+    only this rejection is cached as "no fused plan" (any other codegen error propagates)."""
+
 def header_text() -> str:
     global _header_text
     if _header_text is None:
@@ -299,7 +304,7 @@ def kernel_source(g, kinds, nullable, used, opts: dict, strict: bool, head: int,
         for t, v, s in g.stores:
             tag = g.recipe[s]
             if tag[0] == "outvalid":
-                raise ValueError("gram mode: nullable outputs")
+                raise _GramNullable("gram mode: nullable outputs")
             if tag[0] == "out":
                 vals[tag[1]] = v
         stores = _gram_code([vals[i] for i in range(gram)], vals[gram]) if not abl & 128 else ""
@@ -644,7 +649,7 @@ def _compile(nodes, rel, gram: int = 0):
             cp.lookback = lookback
         except dqvm.Unfusable as e:
             cp = "vector" if str(e) == "VectorAssembleExpr" else None
-        except ValueError:  # Gram mode over nullable outputs
+        except _GramNullable:  # Gram mode over nullable outputs: the row-storing scan instead
             cp = None
         if len(_CACHE) >= 64:
             _CACHE.clear()

@@ -5,7 +5,10 @@ Result: a string-typed DataFrame ``summary | <col>...`` with the rows ``count``,
 rendered as Spark casts the aggregate to string (``Double.toString`` for doubles, the column's
 own type for min/max).  Numeric columns are reduced on the table's device in ONE pass of
 masked reductions (no row compaction); string columns take the host path (mean/stddev of the
-strings cast to double, min/max lexicographic).  Vector columns are not describable, as in Spark.
+strings cast to double, min/max lexicographic).  As in Spark's ``StatFunctions.summary`` only
+numeric and string columns are summarized: any other column (boolean, vector, ...) is dropped
+silently, named or not.  Floating min/max order NaN above every number (Spark's ordering): ``min``
+skips NaN unless every value is NaN, ``max`` is NaN as soon as one value is.
 """
 from __future__ import annotations
 
@@ -15,8 +18,7 @@ import torch
 
 from ..utils.javafmt import java_str
 from .table import ColumnData
-from .types import (BooleanType, IntegerType, LongType, StringType, StructField, StructType,
-                    VectorUDT, is_numeric)
+from .types import IntegerType, LongType, StringType, StructField, StructType, is_numeric
 
 __all__ = ["describe"]
 
@@ -40,7 +42,12 @@ def _numeric(c: ColumnData, live: torch.Tensor, integral: bool) -> List:
     xs = x[m]
     mean = float(xs.mean().item())
     sd = float(xs.std(unbiased=True).item()) if n > 1 else float("nan")
-    mn, mx = xs.min().item(), xs.max().item()
+    nan = torch.isnan(xs)
+    if bool(nan.any()):  # NaN is the largest double in Spark's ordering
+        mx = float("nan")
+        mn = float("nan") if bool(nan.all()) else xs[~nan].min().item()
+    else:
+        mn, mx = xs.min().item(), xs.max().item()
     if integral:
         raw = c.values[m]
         mn, mx = int(raw.min().item()), int(raw.max().item())
@@ -70,9 +77,9 @@ def describe(df, cols: List[str]):
 
     t = df._table()
     fields = [t.schema[t.index_of(c)] for c in cols]
-    for f in fields:
-        if isinstance(f.dataType, VectorUDT):
-            raise ValueError(f"describe() does not support vector column {f.name}")
+    # StatFunctions.summary: numeric and string columns only, the rest dropped without an error
+    fields = [f for f in fields if is_numeric(f.dataType) or isinstance(f.dataType, StringType)]
+    cols = [f.name for f in fields]
     stats = []
     from .plan import is_sharded
 
@@ -96,10 +103,8 @@ def describe(df, cols: List[str]):
             if isinstance(f.dataType, StringType):
                 keep = live.cpu().tolist()
                 stats.append(_strings([v for v, k in zip(c.values, keep) if k]))
-            elif is_numeric(f.dataType) or isinstance(f.dataType, BooleanType):
-                stats.append(_numeric(c, live, _integral(f)))
             else:
-                stats.append(["0", None, None, None, None])
+                stats.append(_numeric(c, live, _integral(f)))
     rows = [tuple([s] + [st[i] for st in stats]) for i, s in enumerate(_STATS)]
     schema = StructType([StructField("summary", StringType(), True)] +
                         [StructField(f.name, StringType(), True) for f in fields])
@@ -107,4 +112,4 @@ def describe(df, cols: List[str]):
 
 
 def _integral(f) -> bool:
-    return isinstance(f.dataType, (IntegerType, LongType, BooleanType))
+    return isinstance(f.dataType, (IntegerType, LongType))

@@ -94,6 +94,30 @@ def main():
     comm.force_collectives(True)
     out["wide_eq"] = wide[True] == wide[False]
 
+    # squared-loss l-bfgs / OWLQN (K9 + X4): one (d + 1)-f64 all-reduce per cost evaluation
+    from net.jgp.labs.sparkdq4ml_amd.parallel import comm as _c
+
+    calls = {"n": 0}
+    real = _c.all_reduce_sum
+
+    def counting(t, *a, **k):
+        calls["n"] += 1
+        return real(t, *a, **k)
+    lb = {}
+    for forced in (True, False):
+        comm.force_collectives(forced)
+        _c.all_reduce_sum = counting
+        try:
+            calls["n"] = 0
+            lb[forced] = _fits(spark, X2[:48].contiguous(), y2, solver="l-bfgs", regParam=0.01, elasticNetParam=0.5,
+                               tol=1e-10, maxIter=100)
+            lb[(forced, "calls")] = calls["n"]
+        finally:
+            _c.all_reduce_sum = real
+    comm.force_collectives(True)
+    out["lbfgs_eq"] = lb[True] == lb[False]
+    out["lbfgs_allreduce_calls"] = lb[(True, "calls")]
+
     # wide bf16 fit (fragment-tiled MFMA SYRK): the Gram folds band by band, each band's RCCL
     # all-reduce issued as soon as it is folded (ops/device.py _fold_all_reduce) — f64 wire: the
     # same bits as the unbanded fold; f32 wire: within f32 rounding of it
@@ -111,6 +135,28 @@ def main():
     comm.set_wire_dtype("f32")
     comm.force_collectives(True)
     out["wide_bands"] = len(devops.wide_bands(4, d3, comm.bucket_bytes(), 4))
+
+    # the head band (counts, Σy, aSum, abSum) crosses the wire in f64 even with the f32 wire: a row
+    # count above 2^24 (odd, so not an f32 value) survives the banded all-reduce exactly
+    from net.jgp.labs.sparkdq4ml_amd.ops import native as _native
+    from net.jgp.labs.sparkdq4ml_amd.ops.layout import TiledWide
+
+    d4, n4 = 256, (1 << 24) + 777
+    hh = _native.hip()
+    buf4 = torch.empty(int(hh.wide_tiled_bytes(16, d4, n4)), dtype=torch.uint8, device=dev)
+    per_row = buf4.numel() // (((n4 + 63) // 64) * 64)
+    y4 = torch.empty(n4, dtype=torch.float32, device=dev)
+    ch = 1 << 21
+    for r0 in range(0, n4, ch):
+        r1 = min(n4, r0 + ch)
+        xc = torch.randn(d4, r1 - r0, generator=g, device=dev)
+        y4[r0:r1] = xc[0] + 1.0
+        devops.pack_wide([xc], 16, None, out=buf4[r0 * per_row:r0 * per_row + ((r1 - r0 + 63) // 64) * 64 * per_row])
+    T4 = TiledWide(buf4, d4, n4, 16)
+    flat4 = devops.gram_stats(T4, y4, None, None, "bf16")
+    head4 = flat4[:2].tolist()
+    out["head_band_count_exact"] = head4 == [float(n4), float(n4)]
+    del buf4, T4, flat4
     out["wide_banded_f64_eq"] = res3[("f64", True)] == res3[("f64", False)]
     out["wide_banded_f32_diff"] = max(abs(a - b) for a, b in zip(res3[("f32", True)][0], res3[("f32", False)][0]))
     spark.stop()

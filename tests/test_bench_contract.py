@@ -5,6 +5,8 @@ import os
 import subprocess
 import sys
 
+import pytest
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "benchmarks"))
 
@@ -93,3 +95,50 @@ def test_bench_py_under_the_drivers_launcher_four_ranks():
     assert line["n_gpus"] == 4 and line["world"] == 4 and line["config"]["parallelism"] == "dp4"
     assert line["scaling"] == "strong" and line["config"]["global_batch"] == 40002
     assert line["config"]["coef_max_abs_err"] < 0.05
+
+
+def _launcher_run(script, args, nproc=4, timeout=900):
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR",
+                                                             "MASTER_PORT")}
+    out = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nproc),
+                          "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, script),
+                          "--gpus", str(nproc), *args], capture_output=True, text=True, timeout=timeout, env=env)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [ln for ln in out.stdout.strip().splitlines() if ln.startswith("{")]
+    assert len(lines) == 1  # rank 0 only
+    return json.loads(lines[0])
+
+
+@pytest.mark.parametrize("script,args", [
+    ("benchmarks/bench_dq_pipeline.py", ["--rows-per-gpu", "20000", "--features", "16", "--steps", "1", "--warmup", "1"]),
+    ("benchmarks/bench_csv_pipeline.py", ["--rows", "40000", "--steps", "1", "--warmup", "1"]),
+    ("benchmarks/bench_wide.py", ["--steps", "1", "--warmup", "1"]),
+    ("benchmarks/bench_lbfgs.py", ["--features", "4100", "--rows", "4000", "--max-iter", "15", "--steps", "1",
+                                   "--warmup", "0"]),
+])
+def test_config_benches_under_the_drivers_launcher_four_ranks(script, args, tmp_path, monkeypatch):
+    """every config benchmark honours ``--gpus N`` under the driver's launcher shape
+    (4 gloo ranks on this CPU box): one JSON line, n_gpus / world 4, one device per rank."""
+    monkeypatch.setenv("TMPDIR", str(tmp_path))  # the CSV bench synthesizes its file there
+    line = _launcher_run(script, args)
+    assert line["n_gpus"] == 4 and line["world"] == 4 and line["backend"] == "gloo"
+    assert len(line["rank_devices"]) == 4 and line["config"]["parallelism"] == "dp4"
+
+
+def test_config_bench_self_launches_and_rejects_mismatch():
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR",
+                                                             "MASTER_PORT")}
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "benchmarks", "bench_wide.py"), "--gpus", "2",
+                          "--steps", "1", "--warmup", "0"], capture_output=True, text=True, timeout=600, env=env)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [ln for ln in out.stdout.strip().splitlines() if ln.startswith("{")]
+    assert len(lines) == 1 and json.loads(lines[0])["n_gpus"] == 2
+    bad = subprocess.run([sys.executable, os.path.join(ROOT, "benchmarks", "bench_dq_pipeline.py"), "--gpus", "2",
+                          "--steps", "1", "--warmup", "0"], capture_output=True, text=True, timeout=300,
+                         env=dict(env, WORLD_SIZE="3"))
+    assert bad.returncode == 2 and "WORLD_SIZE=3" in bad.stderr

@@ -49,11 +49,20 @@ def test_rccl_fit_paths_match_uncollective(rccl_run):
     assert rccl_run["coef_err"] < 5e-3
 
 
+def test_rccl_lbfgs_per_evaluation_all_reduce(rccl_run):
+    """K9 + X4: the squared-loss l-bfgs path all-reduces its (d + 1)-f64 evaluation once per cost
+    evaluation over RCCL and ends with the same model as the collective-free run."""
+    assert rccl_run["lbfgs_eq"]
+    assert rccl_run["lbfgs_allreduce_calls"] >= 5
+
+
 def test_rccl_wide_banded_fold_all_reduce(rccl_run):
     """Wide Gram X1: band-by-band fold with each band's all-reduce in flight during the next fold."""
     assert rccl_run["wide_bands"] >= 3
     assert rccl_run["wide_banded_f64_eq"]
     assert rccl_run["wide_banded_f32_diff"] < 1e-4
+    # ADVICE r2: the head band stays f64 on the wire (a count above 2^24 is exact)
+    assert rccl_run["head_band_count_exact"]
 
 
 def test_rccl_calls_observed(rccl_run):

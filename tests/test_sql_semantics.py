@@ -62,6 +62,23 @@ def test_describe_matches_spark_stats(cpu_session):
     assert one[2][1] == "NaN"  # stddev_samp of one value
 
 
+def test_describe_drops_non_numeric_and_orders_nan_last(cpu_session):
+    """StatFunctions.summary keeps numeric / string columns only (booleans and vectors
+    vanish, even when named) and orders NaN above every double (min skips it, max returns it)."""
+    df = cpu_session.createDataFrame({"x": torch.tensor([1.0, float("nan"), -2.0], dtype=torch.float64),
+                                      "b": torch.tensor([True, False, True]),
+                                      "v": torch.ones(2, 3, dtype=torch.float64)})
+    from net.jgp.labs.sparkdq4ml_amd import VectorAssembler
+
+    df = VectorAssembler().setInputCols(["x"]).setOutputCol("vec").transform(df.select("x", "b"))
+    out = df.describe("x", "b", "vec")
+    assert out.columns == ["summary", "x"]
+    rows = {r[0]: r[1] for r in out.collect()}
+    assert rows["min"] == "-2.0" and rows["max"] == "NaN" and rows["mean"] == "NaN"
+    allnan = cpu_session.createDataFrame({"x": torch.tensor([float("nan")] * 2, dtype=torch.float64)}).describe()
+    assert {r[0]: r[1] for r in allnan.collect()}["min"] == "NaN"
+
+
 def test_null_weight_fails_fit(cpu_session):
     X = torch.arange(5, dtype=torch.float64).unsqueeze(0)
     y = 2 * X[0] + 1
