@@ -83,6 +83,10 @@ def main(argv=None):
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--rows", type=float, default=1e8, help="rows of the synthetic CSV (all ranks)")
     ap.add_argument("--path", default=None, help="CSV to use (default: synthesize under $TMPDIR)")
+    ap.add_argument("--features", type=int, default=1,
+                    help="1: the lab's guest,price CSV and DQ chain; d > 1: BASELINE-shape rows of d float "
+                         "features + a label (range-rule DQ filter on the label, VectorAssembler of the d "
+                         "columns, normal-equation fit)")
     ap.add_argument("--json-out", default=None)
     a = ap.parse_args(argv)
     rc = self_launch(a.gpus, __file__, argv)  # --gpus N: one process per GPU, before any GPU call
@@ -102,17 +106,40 @@ def main(argv=None):
         .config("dq4ml.fit.async", "true").getOrCreate()
     dev = spark.device
     rows = int(a.rows) if dev.type == "cuda" else min(int(a.rows), 200_000)
+    d = a.features
     path = a.path
     if path is None:
-        path = os.path.join(os.environ.get("TMPDIR", tempfile.gettempdir()), f"dq4ml_synth_{rows}.csv")
-        if rank == 0 and not os.path.exists(path):
-            synth_csv(path + ".tmp", rows)
-            os.replace(path + ".tmp", path)
+        if d > 1:
+            import csv_synth
+
+            path = os.path.join(csv_synth.scratch_dir(int(rows * (9.6 * d + 9))), f"dq4ml_wide_{rows}x{d}.csv")
+            if rank == 0 and not os.path.exists(path):
+                csv_synth.write_wide_csv(path, rows, d, device=dev, y0=60.0)
+        else:
+            path = os.path.join(os.environ.get("TMPDIR", tempfile.gettempdir()), f"dq4ml_synth_{rows}.csv")
+            if rank == 0 and not os.path.exists(path):
+                synth_csv(path + ".tmp", rows)
+                os.replace(path + ".tmp", path)
         comm.barrier()
     nbytes = os.path.getsize(path)
     register_lab_rules(spark)
+    if d > 1:
+        from net.jgp.labs.sparkdq4ml_amd import col
+        from net.jgp.labs.sparkdq4ml_amd.dq.rules import RangeRule
+        from net.jgp.labs.sparkdq4ml_amd.sql.types import DataTypes
+
+        spark.udf().register("rangeRule", RangeRule(0.0, 150.0, name="rangeRule"), DataTypes.DoubleType)
+
+    def step_wide():
+        df = spark.read().format("csv").option("inferSchema", "true").option("header", "false").load(path)
+        df = df.withColumn("y_ok", callUDF("rangeRule", col(f"_c{d}"))).filter(col("y_ok") > 0)
+        df = df.withColumn("label", col("y_ok"))
+        df = VectorAssembler().setInputCols([f"_c{i}" for i in range(d)]).setOutputCol("features").transform(df)
+        return LinearRegression(solver="normal", regParam=1e-3).fit(df)
 
     def step():
+        if d > 1:
+            return step_wide()
         df = spark.read().format("csv").option("inferSchema", "true").option("header", "false").load(path)
         df = df.withColumnRenamed("_c0", "guest").withColumnRenamed("_c1", "price")
         df = df.withColumn("price_no_min", callUDF("minimumPriceRule", df.col("price")))
@@ -140,7 +167,10 @@ def main(argv=None):
     first_ms = (time.perf_counter() - t0) * 1e3
     elapsed, model = timed(step, a.steps, max(0, a.warmup - 1), dev)
     info = world_info(dev)
-    emit({"metric": "rows/sec lab pipeline CSV -> DQ rules -> VectorAssembler -> LinearRegression.fit",
+    from net.jgp.labs.sparkdq4ml_amd.ops import scancut
+
+    emit({"metric": "rows/sec lab pipeline CSV -> DQ rules -> VectorAssembler -> LinearRegression.fit"
+                    + ("" if d == 1 else f" ({d} float features per row)"),
           "value": rows * a.steps / elapsed, "unit": "rows/s", "n_gpus": world, "steps": a.steps,
           "warmup": a.warmup, "ms_per_step": elapsed / a.steps * 1e3, "higher_is_better": True,
           "scaling": "strong", "vs_baseline": None, "dtype": "fp64",
@@ -151,7 +181,8 @@ def main(argv=None):
                      "coefficients": [float(v) for v in model.coefficients.toArray()],
                      "intercept": float(model.intercept), "parallelism": f"dp{world}",
                      "first_action_ms": first_ms, "host_issue_ms_per_step": harness.LAST_ISSUE_S / a.steps * 1e3,
-                     "device_scans": csvscan.STATS["device_scans"], "scan_fallbacks": csvscan.STATS["fallbacks"]},
+                     "device_scans": csvscan.STATS["device_scans"], "scan_fallbacks": csvscan.STATS["fallbacks"],
+                     "features": d, "csv_bytes": nbytes, "cut_grams": scancut.STATS["cut_grams"]},
           **info}, a.json_out)
     comm.shutdown()
     return 0

@@ -104,6 +104,29 @@ def _scan_chunk(h, buf, n: int, trailing: bool, ncols: int, sep: str, dev, hint=
     stats = torch.zeros(3 + 2 * ncols, dtype=torch.int64, device=dev)
     h.csv_parse(buf.data_ptr(), n, ends.data_ptr(), nlines, ncols, ord(sep), ptrs.data_ptr(), valid.data_ptr(),
                 keep.data_ptr(), stats.data_ptr(), stream, **_opt_args(opts))
+    # facts for the byte-parallel cutter (ops/scancut.py), read with the stats: the longest line
+    # (terminator included) and the separator count (= nlines * (ncols - 1) when every line has
+    # exactly ncols fields, given that no column holds nulls)
+    # plus the shortest line and the terminator kinds (line ends are the CR of a CR LF pair):
+    # [longest, separators, shortest, CR ends, LF ends, CR LF ends]
+    z = torch.zeros(1, dtype=torch.int64, device=dev)
+    if nlines:
+        e = ends[:nlines].to(torch.int64)
+        d1 = e[1:] - e[:-1] if nlines > 1 else e[:1] + 1
+        maxl = torch.maximum(e[:1] + 1, d1.max()).reshape(1)
+        minl = torch.minimum(e[:1] + 1, d1.min()).reshape(1)
+    else:
+        maxl, minl = z, torch.full_like(z, 1 << 30)
+    nsep = (buf[:n] == ord(sep)).sum().reshape(1) if n else z
+    if nterm:
+        te = ends[:nterm].to(torch.int64)
+        tb = buf[te]
+        nx = buf[(te + 1).clamp(max=max(n - 1, 0))]
+        cr = tb == 13
+        kinds = torch.stack([cr.sum(), (tb == 10).sum(), (cr & (nx == 10) & (te + 1 < n)).sum()])
+    else:
+        kinds = torch.zeros(3, dtype=torch.int64, device=dev)
+    stats = torch.cat([stats, maxl, nsep.to(torch.int64), minl, kinds.to(torch.int64)])
     return nlines, dcols, valid, keep, stats
 
 
@@ -163,8 +186,13 @@ def _finish(parts, types, st, dev, hinted=False):
     # what a later fused scan of the same bytes relies on (ops/scanfuse.py): line count (empty
     # lines included) and the columns holding nulls
     nc = len(types)
+    nonempty = int(total) - int(st[:, 1].sum())
     table.scan_facts = {"nlines": int(total), "nullable": [bool(int(st[:, 2 + c].sum())) for c in range(nc)],
-                        "fast_only": int(st[:, 2 + 2 * nc].sum()) == 0}
+                        "fast_only": int(st[:, 2 + 2 * nc].sum()) == 0,
+                        "empty_lines": int(st[:, 1].sum()), "max_line": int(st[:, 3 + 2 * nc].max()),
+                        "uniform_fields": int(st[:, 4 + 2 * nc].sum()) == nonempty * (nc - 1),
+                        "min_line": max(1, int(st[:, 5 + 2 * nc].min())) if len(st) else 1,
+                        "term_kinds": [int(st[:, 6 + 2 * nc + k].sum()) for k in range(3)]}
     return table
 
 

@@ -691,22 +691,21 @@ def try_execute_fused(plan, session) -> Optional[Table]:
         h.rtc_launch(int(handle), grid, 256, ptrs.data_ptr(), int(n), torch.cuda.current_stream().cuda_stream)
     tracing.add_rows("dq_fused", n)
     STATS["fused_launches"] += 1
-    if cp.has_raise and int(err.item()) != 0:
-        msg = "Failed to execute user defined function"
-        for nd in nodes:
-            for ex in getattr(nd, "exprs", []) + ([nd.cond] if hasattr(nd, "cond") else []):
-                r = _find_raise(ex)
-                if r is not None:
-                    msg = r.message
-        raise E.SparkException(msg)
+    checks = []
+    if cp.has_raise:
+        # a raising rule (RaiseIfNull, MinimumPriceDataQualityUdf.java:11-13) fails the job on the
+        # first host read of the action's results (runtime/checks.py): no sync per action
+        from .scanfuse import _udf_error_check
+
+        checks = [c for c in (_udf_error_check(nodes, err),) if c is not None]
     schema = plan.schema()
     cols = []
     for o, f, oo in zip(cp.outs, schema.fields, outs):
         if o[0] == "col":
             c = base.columns[o[1]]
-            cols.append(ColumnData(c.dtype, c.values, c.valid, dict(c.meta)))
+            cols.append(ColumnData(c.dtype, c.values, c.valid, dict(c.meta), list(c.checks) + checks))
         else:
-            cols.append(ColumnData(f.dataType, oo[0], oo[1], dict(f.metadata)))
+            cols.append(ColumnData(f.dataType, oo[0], oo[1], dict(f.metadata), list(checks)))
     sel = sel_out if sel_out is not None else base.sel
     del keep
     return _maybe_compact(Table(schema, cols, n, sel, base.device))

@@ -1,0 +1,610 @@
+"""Byte-parallel CSV field cutter with the DQ chain, the VectorAssembler and the normal-equation
+Gram in ONE persistent hipRTC kernel per action (SURVEY.md K1 + K3 + K4 + K5).
+
+The action is ``LinearRegression.fit`` over ``VectorAssembler`` over a DQ chain over a CSV re-read
+(``DataQuality4MachineLearningApp.java:53-55, 68-90, 110-126``; Spark re-scans the file on every
+action, S20).  ``scanfuse.py``'s per-line kernel gives each LINE to one lane, which then walks
+its bytes serially: fine for the lab's 8-byte rows, latency-bound for a 300-byte row of 33
+numeric fields.  Here the unit of parallel work is the FIELD:
+
+1. a block stages a 16 KiB window plus a head (the row that straddles into it) in LDS with
+   16-byte granule loads, and every lane builds the terminator and separator bitmasks of its 64
+   window bytes with SWAR compares (4 bytes per 32-bit op);
+2. the delimiter counts are prefix-summed across the block (wave ``shfl_up`` scans + one LDS
+   word per wave) and each lane scatters its delimiter positions into an LDS position array —
+   the cut: field f of the window spans (pos[f-1], pos[f]);
+3. every lane converts its own field: one 16-byte funnel-shifted LDS read and the 16-byte SWAR
+   converter (``csv_swar_field16``, exact and bit-identical to the byte-walking fast path), the
+   value lands in an LDS row tile [row][column] (f64);
+4. one thread per row runs the DQ chain (``ops/dqvm.py`` lowering, rule bodies and filters in
+   registers) on its row of the tile, which gives the features, the label and the live flag;
+5. the normal-equation statistics: for d <= 8 every row thread adds to f64 register sums (the
+   per-line kernel's scheme); for wider rows the live rows' augmented vectors ``[x | 1 | y]`` go
+   to a second LDS tile and 4 x 4 register blocks of the upper Gram accumulate over them (f64,
+   every statistic exact to the input doubles).
+
+Blocks are persistent (one per CU slot, windows ``blockIdx.x + k * gridDim.x``) and keep their
+sums in registers across windows; one partial per block (and row group) is folded at the end in
+a fixed order, so repeated actions are bitwise identical.  Nothing is stored per row.
+
+Preconditions, all facts of the earlier device scan of the same cached bytes (Spark's schema
+inference job at ``load()``): every field took the numeric fast path, no column holds nulls, no
+empty line, every line has exactly the column count (separator count = lines x (columns - 1)),
+int32 / double columns only, and the longest line fits the staged head.  The kernel re-verifies
+the facts it relies on (field count per row, field classes) and raises the deferred data error
+of ``runtime/checks.py`` if the bytes ever disagree.
+"""
+from __future__ import annotations
+
+import os
+from typing import Optional
+
+import numpy as np
+import torch
+
+__all__ = ["applicable", "kernel_source", "try_cut_gram", "STATS", "ENTRY"]
+
+ENTRY = "dq_scan_cut"
+WINDOW = 16384
+TILE_BYTES = 18432  # LDS of the row tiles (chain inputs + Gram rows) per round
+STATS = {"cut_grams": 0}
+
+
+def head_for(max_line: int) -> int:
+    """Staged head: a power of two >= the longest line + 32 bytes, in [256, 4096] (None above)."""
+    h = 256
+    while h < max_line + 32:
+        h *= 2
+    return h if h <= 4096 else None
+
+
+def applicable(f: dict) -> Optional[int]:
+    """The head size when the cached relation's facts allow the cutter, else None."""
+    if os.environ.get("DQ4ML_SCAN_CUT", "1") == "0":
+        return None
+    o = f["opts"]
+    sep = o.get("sep", ",")
+    if not f.get("fast_only") or f.get("strict") or any(f["nullable"]) or f.get("empty_lines", 1) != 0:
+        return None
+    if not f.get("uniform_fields") or len(f["kinds"]) < 1 or any(int(k) not in (0, 1) for k in f["kinds"]):
+        return None
+    if o["null_value"] or o["trim_lead"] or o["trim_trail"] or int(o["comment"]) or len(sep) != 1:
+        return None
+    if sep in "0123456789.+-\r\n" or term_of(f) is None:
+        return None
+    return head_for(int(f.get("max_line", 1 << 30)))
+
+
+def term_of(f: dict):
+    """(terminator byte, CR LF) when every line of the cached bytes ends the same way — CR only
+    (the reference data), LF only, or CR LF only — else None (mixed endings keep
+    the per-line kernel)."""
+    cr, lf, crlf = (list(f.get("term_kinds") or (1, 1, 0)) + [0, 0, 0])[:3]
+    if lf == 0 and crlf == 0:
+        return 13, False
+    if cr == 0:
+        return 10, False
+    if lf == 0 and crlf == cr:
+        return 13, True
+    return None
+
+
+def gram_width(d: int) -> int:
+    return 3 + 2 * d + d * (d + 1) // 2
+
+
+def _gram_index(i: int, j: int, d: int) -> Optional[int]:
+    """Slot of augmented Gram entry (i <= j) of [x_0..x_{d-1}, 1, y] in the gram_width layout
+    [count, Σy, Σy², Σx (d), Σxy (d), packed-upper Σxx]; None for padding."""
+    if j >= d + 2:
+        return None
+    if j < d:
+        return 3 + 2 * d + j * (j + 1) // 2 + i
+    if j == d:
+        return 3 + i if i < d else 0
+    if i < d:
+        return 3 + d + i
+    return 1 if i == d else 2
+
+
+def _passthrough(xs, used, d):
+    """Feature columns when every feature is a bare column read (``fzf<c>``, each column at most
+    once), else None."""
+    import re
+
+    cols = []
+    for v in xs:
+        m = re.fullmatch(r"\(*(?:\(double\))?\(*fzf(\d+)\)*", v.replace(" ", ""))
+        if m is None:
+            return None
+        cols.append(int(m.group(1)))
+    return cols if len(set(cols)) == len(cols) else None
+
+
+class _Shape:
+    """Compile-time sizes of one cutter kernel (shared by the codegen and the launcher)."""
+
+    def __init__(self, C, d, H, min_line, ucols, feat):
+        self.C, self.d, self.H = C, d, H
+        self.W = WINDOW
+        self.HG = (H // 16 + 2 + 255) // 256          # head + tail granules per thread
+        rows_max = (H + self.W) // max(1, min_line) + 2  # rows that can end in one window
+        self.DCAP = min((H + self.W) // 2 + 64, rows_max * C + 64)
+        self.blocked = d > 8
+        self.PP = (d + 2 + 3) // 4 * 4
+        self.NB = self.PP // 4
+        self.U = self.NB * (self.NB + 1) // 2
+        self.RG = max(1, 256 // self.U) if self.blocked else 1
+        self.ucols = ucols                              # columns the chain reads, in vt order
+        self.CU = max(1, len(ucols))
+        self.feat = feat                                # passthrough feature columns (blocked only)
+        per_row = 8 * (self.CU + (self.PP if self.blocked else 0))
+        self.gw = gram_width(d)
+        fixed = (16 + H + self.W + 32) + 2 * self.DCAP + 4 * C + 128 + (0 if self.blocked else 32 * self.gw)
+        # the row tiles take what keeps 4 blocks resident per CU (40 KiB each), within
+        # [4 KiB, TILE_BYTES]: more rounds per window beat fewer resident blocks
+        tile = max(4096, min(TILE_BYTES, 40960 - fixed))
+        self.RR = int(max(1, min(rows_max, tile // per_row)))
+        self.lds = fixed + 8 * self.RR * self.CU + (8 * self.RR * self.PP if self.blocked else 0)
+        self.gw = gram_width(d)
+
+
+def kernel_source(g, kinds, used, opts: dict, H: int, slots: dict, d: int, term: int = 13, crlf: bool = False,
+                  min_line: int = 1, waves_per_simd: int = 0):
+    """Source of the cutter kernel and its ``_Shape``.  ``term``: the file's one terminator byte
+    (13 CR, 10 LF; ``crlf``: every CR is followed by LF, which then opens the next row and is
+    skipped); ``min_line``: the shortest line, sizing the delimiter array and the row tile."""
+    from .scanfuse import _gram_code, header_text
+
+    C = len(kinds)
+    NS = len(g.ptrs)
+    vals = {}
+    for t, v, s in g.stores:
+        tag = g.recipe[s]
+        if tag[0] == "outvalid":
+            from .scanfuse import _GramNullable
+
+            raise _GramNullable("gram mode: nullable outputs")
+        if tag[0] == "out":
+            vals[tag[1]] = v
+    xs, yv = [vals[i] for i in range(d)], vals[d]
+    feat = _passthrough(xs, used, d) if d > 8 else None
+    ucols = sorted(used)
+    if feat is not None:  # features go straight from the converter to the Gram tile
+        body_text = "\n".join(g.lines) + "\n" + yv
+        import re
+
+        ucols = [c for c in ucols if re.search(rf"\bfzf{c}\b", body_text)]
+    sh = _Shape(C, d, H, min_line, ucols, feat)
+    W, HG, DCAP, RR, CU, PP, NB, U, RG, GW = sh.W, sh.HG, sh.DCAP, sh.RR, sh.CU, sh.PP, sh.NB, sh.U, sh.RG, sh.gw
+    usl = {c: i for i, c in enumerate(ucols)}
+    sep = ord(opts.get("sep", ","))
+    sep4 = f"0x{sep:02X}{sep:02X}{sep:02X}{sep:02X}u"
+    term4 = f"0x{term:02X}{term:02X}{term:02X}{term:02X}u"
+    o = (f"{{(unsigned char){sep}, (unsigned char){int(opts['quote'])}, (unsigned char){int(opts['escape'])}, "
+         f"(unsigned char)0, (unsigned char)0, (unsigned char)0, (unsigned char)0, (unsigned char)0, "
+         f"{{{', '.join('0' for _ in range(16))}}}}}")
+    body = ("\n".join("      " + ln.strip() for ln in g.lines).replace("P[", "p[")
+            .replace("atomicOr((int*)p[", "dq_flag((unsigned int*)p["))
+    loads = "".join(f"      const {ct} fzf{c} = ({ct})(vt[rb + {usl[c]}]);\n"
+                    for c, ct in sorted(used.items()) if c in usl)
+    # per column: its vt slot (-1: the chain does not read it) and its feature slot in the Gram
+    # tile (-1: not a passthrough feature)
+    ctab = []
+    for c in range(C):
+        ctab.append(usl.get(c, -1))
+        ctab.append(feat.index(c) if feat is not None and c in feat else -1)
+    if sh.blocked:
+        outs = f"      double* __restrict__ gr = gt + r * {PP};\n"
+        if feat is None:
+            outs += "".join(f"      gr[{i}] = live ? (double)({v}) : 0.0;\n" for i, v in enumerate(xs))
+        else:
+            outs += f"      if (!live) {{\n#pragma unroll\n        for (int i = 0; i < {d}; ++i) gr[i] = 0.0;\n      }}\n"
+        outs += f"      gr[{d}] = live ? 1.0 : 0.0;\n      gr[{d + 1}] = live ? (double)({yv}) : 0.0;\n"
+        outs += "".join(f"      gr[{i}] = 0.0;\n" for i in range(d + 2, PP))
+        acc_decl = "  double acc[16];\n#pragma unroll\n  for (int k = 0; k < 16; ++k) acc[k] = 0.0;\n"
+        acc_decl += f"""  const int gu = tid % {U}, grg = tid / {U};
+  const bool gact = tid < {U * RG};
+  int bi = 0, brem = gu;
+  while (brem >= {NB} - bi) {{ brem -= {NB} - bi; ++bi; }}
+  const int bj = bi + brem;
+"""
+        gram_phase = f"""      if (gact) {{
+        for (int r = grg; r < nr; r += {RG}) {{
+          const double* __restrict__ gr = gt + r * {PP};
+          const f64x2 a01 = *reinterpret_cast<const f64x2*>(gr + 4 * bi), a23 = *reinterpret_cast<const f64x2*>(gr + 4 * bi + 2);
+          const f64x2 b01 = *reinterpret_cast<const f64x2*>(gr + 4 * bj), b23 = *reinterpret_cast<const f64x2*>(gr + 4 * bj + 2);
+          const double av[4] = {{a01[0], a01[1], a23[0], a23[1]}}, bv[4] = {{b01[0], b01[1], b23[0], b23[1]}};
+#pragma unroll
+          for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int v = 0; v < 4; ++v) acc[4 * u + v] = __builtin_fma(av[u], bv[v], acc[4 * u + v]);
+        }}
+      }}
+"""
+        # every (i <= j) entry of the augmented upper triangle sits in exactly one 4 x 4 block:
+        # each row group writes a complete gram_width slab (no zero fill needed)
+        idx_tab = []
+        for bI in range(NB):
+            for bJ in range(bI, NB):
+                for u in range(4):
+                    for v in range(4):
+                        i, j = 4 * bI + u, 4 * bJ + v
+                        k = _gram_index(i, j, d) if i <= j else None
+                        idx_tab.append(-1 if k is None else k)
+        epilogue = f"""  if (gact) {{
+    DQG double* __restrict__ gp = (DQG double*)p[{slots['gpart']}] + ((long long)blockIdx.x * {RG} + grg) * {GW};
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {{
+      const int slot = DQ_GIDX[gu * 16 + k];
+      if (slot >= 0) gp[slot] = acc[k];
+    }}
+  }}
+"""
+        tables = f"__device__ const short DQ_GIDX[{U * 16}] = {{{', '.join(str(x) for x in idx_tab)}}};\n"
+        gt_decl = f"  __shared__ __attribute__((aligned(16))) double gt[{RR * PP}];\n"
+    else:
+        outs = _gram_code(xs, yv).replace("    if (live)", "      if (live)")
+        acc_decl = f"  double acc[{GW}];\n#pragma unroll\n  for (int k = 0; k < {GW}; ++k) acc[k] = 0.0;\n"
+        gram_phase = ""
+        red = "".join(f"""  {{
+    double t = acc[{k}];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o, 64);
+    if (lane == 0) gred[wave][{k}] = t;
+  }}
+""" for k in range(GW))
+        epilogue = f"""  __shared__ double gred[4][{GW}];
+{red}  __syncthreads();
+  if (tid < {GW})
+    ((DQG double*)p[{slots['gpart']}])[(long long)blockIdx.x * {GW} + tid] =
+        (gred[0][tid] + gred[1][tid]) + (gred[2][tid] + gred[3][tid]);
+"""
+        tables = ""
+        gt_decl = ""
+    feat_store = ("          const int fs = ctab[2 * col + 1];\n"
+                  f"          if (fs >= 0) gt[rr * {PP} + fs] = dv;\n") if (sh.blocked and feat is not None) else ""
+    kind_tab = ", ".join(str(int(k)) for k in kinds)
+    lb = f"__launch_bounds__(256, {waves_per_simd})" if waves_per_simd else "__launch_bounds__(256)"
+    src = header_text() + f"""
+using namespace dq4ml_csv;
+typedef unsigned int csv_u32x4 __attribute__((ext_vector_type(4)));
+typedef double f64x2 __attribute__((ext_vector_type(2)));
+#define DQG __attribute__((address_space(1)))
+
+__device__ __forceinline__ void dq_flag(unsigned int* f, unsigned int v) {{
+  __hip_atomic_fetch_or((DQG unsigned int*)f, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}}
+__device__ const unsigned char DQ_KIND[{C}] = {{{kind_tab}}};
+__device__ const short DQ_CTAB[{2 * C}] = {{{', '.join(str(x) for x in ctab)}}};
+{tables}
+// 0x80 in every byte of v equal to the byte of pat
+__device__ __forceinline__ unsigned int dq_eq80(unsigned int v, unsigned int pat) {{
+  const unsigned int x = v ^ pat;
+  return ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x | 0x7F7F7F7Fu);
+}}
+// the four 0x80 flags of z gathered to bits 0..3
+__device__ __forceinline__ unsigned int dq_gather4(unsigned int z) {{
+  return (((z >> 7) * 0x00204081u) >> 21) & 0xFu;
+}}
+// one window's granules: 64 bytes per lane, then the head (the row straddling into the window)
+// and two tail granules; zero outside [0, n)
+__device__ __forceinline__ void dq_fetch(const DQG unsigned char* ab, long long a, long long n, long long blk, int tid,
+                                         csv_u32x4 (&pg)[4], csv_u32x4 (&ph)[{HG}]) {{
+  const long long wbase = blk * {W} - a, sbase = wbase - {H}, tb = wbase + 64 * tid;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {{
+    const long long gi = tb + 16 * j;
+    pg[j] = (gi < n && gi + 16 > 0) ? *reinterpret_cast<const DQG csv_u32x4*>(ab + gi + a) : csv_u32x4{{0u, 0u, 0u, 0u}};
+  }}
+#pragma unroll
+  for (int i = 0; i < {HG}; ++i) {{
+    const int gq = tid + 256 * i;
+    const long long gi = gq < {H // 16} ? sbase + 16 * gq : wbase + {W} + 16 * (gq - {H // 16});
+    ph[i] = (gq < {H // 16} + 2 && gi < n && gi + 16 > 0) ? *reinterpret_cast<const DQG csv_u32x4*>(ab + gi + a)
+                                                          : csv_u32x4{{0u, 0u, 0u, 0u}};
+  }}
+}}
+
+extern "C" __global__ {lb} void {ENTRY}(void* const* P, long long n) {{
+  void* p[{NS}];
+#pragma unroll
+  for (int i = 0; i < {NS}; ++i) p[i] = P[i];
+  const DQG unsigned char* __restrict__ b = (const DQG unsigned char*)p[{slots['buf']}];
+  const long long nwin = (long long)p[{slots['nwin']}];
+  const bool trailing = (long long)p[{slots['trailing']}] != 0;
+  unsigned int* vflag = (unsigned int*)p[{slots['vflag']}];
+  __shared__ __attribute__((aligned(16))) unsigned char stage_raw[16 + {H} + {W} + 32];
+  unsigned char* const stage = stage_raw + 16;  // 16 readable bytes below stage[0] (right-aligned reads)
+  __shared__ unsigned short dpos[{DCAP}];
+  __shared__ __attribute__((aligned(16))) double vt[{RR * CU}];
+{gt_decl}  __shared__ short ctab[{2 * C}];
+  __shared__ int wtot[4], shtot, sst0;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const long long a = (long long)(reinterpret_cast<unsigned long long>(b) & 15ull);
+  const DQG unsigned char* ab = b - a;  // 16-byte aligned view
+  const CsvOpts O = {o};
+  bool bad = false;
+  for (int i = tid; i < {2 * C}; i += 256) ctab[i] = DQ_CTAB[i];
+{acc_decl}
+  // a CONTIGUOUS run of windows per block: the row start of window k+1 is carried from the cut
+  // of window k (only the first window searches back for it), and window k+1's bytes are in
+  // flight (registers) while window k is cut
+  const long long w0 = nwin * blockIdx.x / gridDim.x, w1 = nwin * (blockIdx.x + 1) / gridDim.x;
+  csv_u32x4 pg[4], ph[{HG}];
+  if (w0 < w1) dq_fetch(ab, a, n, w0, tid, pg, ph);
+  int st0 = -1;  // stage index of the window's first row (block-uniform; -1: search)
+  for (long long blk = w0; blk < w1; ++blk) {{
+    const long long wbase = blk * {W} - a;  // buffer index of window byte 0
+    const long long sbase = wbase - {H};    // buffer index of stage[0]
+    const long long tb = wbase + 64 * tid;  // this lane's 64 window bytes
+    __syncthreads();  // the previous window's readers are done with every LDS array
+    unsigned int dlo = 0u, dhi = 0u;  // delimiter (separator or terminator) bits of the 64 bytes
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {{
+      const csv_u32x4 v = pg[j];
+      *reinterpret_cast<csv_u32x4*>(stage + {H} + 64 * tid + 16 * j) = v;
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {{
+        const unsigned int g4 = dq_gather4(dq_eq80(v[w], {sep4}) | dq_eq80(v[w], {term4}));
+        if (j < 2) dlo |= g4 << (16 * j + 4 * w);
+        else dhi |= g4 << (16 * (j - 2) + 4 * w);
+      }}
+    }}
+#pragma unroll
+    for (int i = 0; i < {HG}; ++i) {{  // head granules + two tail granules
+      const int gq = tid + 256 * i;
+      if (gq < {H // 16} + 2)
+        *reinterpret_cast<csv_u32x4*>(stage + (gq < {H // 16} ? 16 * gq : {H} + {W} + 16 * (gq - {H // 16}))) = ph[i];
+    }}
+    if (blk + 1 < w1) dq_fetch(ab, a, n, blk + 1, tid, pg, ph);
+    unsigned long long dm = ((unsigned long long)dhi << 32) | dlo;
+    {{
+      const long long lo = tb < 0 ? -tb : 0, hi = n - tb;
+      if (lo > 0 || hi < 64) {{  // bytes before the buffer (aligned granule) or past its end
+        const unsigned long long keep_lo = lo >= 64 ? 0ull : (~0ull << lo);
+        const unsigned long long keep_hi = hi <= 0 ? 0ull : (hi >= 64 ? ~0ull : ((1ull << hi) - 1));
+        dm &= keep_lo & keep_hi;
+      }}
+      if (trailing && hi >= 0 && hi < 64) dm |= 1ull << hi;  // the last line's virtual terminator at n
+    }}
+    const int cd = __popcll(dm);
+    int inc = cd;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {{
+      const int t = __shfl_up(inc, o, 64);
+      if (lane >= o) inc += t;
+    }}
+    if (lane == 63) wtot[wave] = inc;
+    if (st0 < 0) __syncthreads();  // (block-uniform) wave 0 reads the other waves' head stores below
+    if (st0 < 0 && wave == 0) {{
+      // the first window of the run: the terminator before its first row, through the staged head
+      long long found = -2;
+      for (int k0 = 0; k0 < {H} && found == -2; k0 += 64) {{
+        const long long q = wbase - 1 - k0 - lane;
+        const bool t = q < 0 || stage[{H} - 1 - k0 - lane] == {term};
+        const unsigned long long bal = __ballot(t);
+        if (bal) found = wbase - 1 - k0 - (long long)__builtin_ctzll(bal);
+      }}
+      for (long long q0 = wbase - 1 - {H}; found == -2; q0 -= 64) {{  // longer than the head (fact violation)
+        const long long q = q0 - lane;
+        const bool t = q < 0 || b[q] == {term};
+        const unsigned long long bal = __ballot(t);
+        if (bal) found = q0 - (long long)__builtin_ctzll(bal);
+      }}
+      if (lane == 0) sst0 = (int)(found < 0 ? -sbase : found + 1 + {1 if crlf else 0} - sbase);
+    }}
+    __syncthreads();
+    if (st0 < 0) st0 = sst0;
+    if (st0 < 0 || st0 > {H} + 1) {{  // a row longer than the head: the max-line fact is wrong
+      bad = true;
+      break;  // block-uniform
+    }}
+    int before = inc - cd;
+    for (int w = 0; w < wave; ++w) before += wtot[w];
+    const int dwin = (wtot[0] + wtot[1]) + (wtot[2] + wtot[3]);
+    // separators of the first row's head part [st0, H) (no terminator can be there)
+    unsigned long long hm = 0ull;
+    if (tid < {H // 64}) {{
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {{
+        const csv_u32x4 v = *reinterpret_cast<const csv_u32x4*>(stage + 64 * tid + 16 * j);
+#pragma unroll
+        for (int w = 0; w < 4; ++w) hm |= (unsigned long long)dq_gather4(dq_eq80(v[w], {sep4})) << (16 * j + 4 * w);
+      }}
+      const int lo = st0 - 64 * tid;
+      hm = lo >= 64 ? 0ull : (lo > 0 ? (hm & (~0ull << lo)) : hm);
+    }}
+    int hinc = __popcll(hm);
+    if (wave == 0) {{
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {{
+        const int t = __shfl_up(hinc, o, 64);
+        if (lane >= o) hinc += t;
+      }}
+      if (lane == 63) shtot = hinc;
+    }}
+    __syncthreads();
+    const int htot = shtot;
+    const int ftot = htot + dwin;      // delimiters from the first row's start on
+    const int cnt = ftot / {C};        // complete rows (every row holds exactly {C} fields)
+    if (ftot > {DCAP}) {{  // more delimiters than any window of valid lines holds
+      bad = true;
+      break;  // block-uniform
+    }}
+    // the cut: every delimiter's stage position, in byte order
+    if (hm) {{
+      int idx = hinc - __popcll(hm);
+      unsigned long long mm = hm;
+      while (mm) {{
+        const int bit = __builtin_ctzll(mm);
+        mm &= mm - 1;
+        dpos[idx++] = (unsigned short)(64 * tid + bit);
+      }}
+    }}
+    {{
+      int idx = htot + before;
+      unsigned long long mm = dm;
+      while (mm) {{
+        const int bit = __builtin_ctzll(mm);
+        mm &= mm - 1;
+        dpos[idx++] = (unsigned short)({H} + 64 * tid + bit);
+      }}
+    }}
+    __syncthreads();
+    // the next window's first row starts after this window's last complete row
+    const int nst0 = cnt > 0 ? (int)dpos[cnt * {C} - 1] + 1 + {1 if crlf else 0} - {W} : st0 - {W};
+    for (int R0 = 0; R0 < cnt; R0 += {RR}) {{
+      const int nr = min({RR}, cnt - R0), f0 = R0 * {C}, f1 = f0 + nr * {C};
+      if (R0 > 0) __syncthreads();  // the previous round's Gram readers are done with the tiles
+      // one field per lane: the right-aligned 16-byte converter straight out of the stage
+      for (int f = f0 + tid; f < f1; f += 256) {{
+        const int end = dpos[f];
+        const int rw = f / {C}, col = f - rw * {C};
+        const int start = f == 0 ? st0 : (int)dpos[f - 1] + 1 + ({1 if crlf else 0} && col == 0 ? 1 : 0);
+        const int len = end - start;
+        double dv = 0.0;
+        long long lv = 0;
+        int ty = C_NULL;
+        bool ok = false;
+        if (len >= 0 && len <= 16) {{
+          ok = csv_field_r16(stage, end, len, dv, lv, ty);
+        }} else if (len > 16) {{
+          int ps = start;
+          ok = csv_field_fast(stage, 0, ps, end, O.sep, dv, lv, ty);
+        }}
+        bad |= !ok || ty == C_NULL || !csv_conforms(ty, DQ_KIND[col]);
+        {{
+          const int rr = rw - R0;
+          const int us = ctab[2 * col];
+          if (us >= 0) vt[rr * {CU} + us] = dv;
+{feat_store}        }}
+      }}
+      __syncthreads();
+      for (int r = tid; r < nr; r += 256) {{  // one row per thread: the DQ chain and the assembler
+        const int rb = r * {CU};
+{loads}        const bool line = true;
+        bool live = line;
+{body}
+{outs}      }}
+      __syncthreads();
+{gram_phase}    }}
+    st0 = nst0;
+  }}
+  if (bad) dq_flag(vflag, 1u);
+{epilogue}}}
+"""
+    return src, sh
+
+
+# ---------------------------------------------------------------------------------------------
+_CACHE: dict = {}
+
+
+class _CutPlan:
+    def __init__(self, src, g, refs, sh, per_cu):
+        self.src, self.recipe, self.has_raise, self.refs = src, list(g.recipe), g.has_raise, refs
+        self.sh, self.per_cu = sh, per_cu
+        self.rg = sh.RG
+
+
+def blocks_per_cu(lds: int) -> int:
+    """Resident 256-thread blocks per CU the cutter is built for (160 KiB LDS, at most 4)."""
+    return int(max(1, min(4, (160 * 1024) // max(lds, 1))))
+
+
+def _compile(nodes, rel, d: int):
+    from . import dqvm
+    from .scanfuse import _GramNullable, _ScanBase, _scan_gen
+
+    f = rel.fused
+    H = applicable(f)
+    if H is None:
+        return None
+    term, crlf = term_of(f)
+    min_line = int(f.get("min_line", 1))
+    (parts, udfs), refs = dqvm.nodes_key(nodes)
+    key = (parts, udfs, tuple(rel.schema().names), tuple(f["kinds"]), repr(sorted(f["opts"].items())), H, d, term,
+           crlf, min_line)
+    if key in _CACHE:
+        return _CACHE[key]
+    base = _ScanBase(rel.schema(), 0, f["device"])
+    g = _scan_gen(base, f["nullable"])
+    cp = None
+    try:
+        _, g, outputs, _ = dqvm.compile_chain(nodes, base, False, gen=g)
+        slots = {k: g.slot(None, (k,)) for k in ("buf", "nwin", "trailing", "vflag", "gpart")}
+        _, sh = kernel_source(g, f["kinds"], g.used, f["opts"], H, slots, d, term, crlf, min_line)
+        per_cu = blocks_per_cu(sh.lds)
+        src, sh = kernel_source(g, f["kinds"], g.used, f["opts"], H, slots, d, term, crlf, min_line, per_cu)
+        cp = _CutPlan(src, g, refs, sh, per_cu)
+    except (dqvm.Unfusable, _GramNullable):
+        cp = None
+    if len(_CACHE) >= 64:
+        _CACHE.clear()
+    _CACHE[key] = cp
+    return cp
+
+
+_grid_cache: dict = {}
+
+
+def _grid(h, per_cu: int, nwin: int) -> int:
+    dev = torch.cuda.current_device()
+    cus = _grid_cache.get(dev)
+    if cus is None:
+        cus = _grid_cache[dev] = int(h.device_info()["multiProcessorCount"])
+    return int(max(1, min(nwin, cus * per_cu)))
+
+
+def n_windows(buf_ptr: int, n: int) -> int:
+    """Windows covering buffer bytes [0, n] (byte n: the last line's virtual terminator); window
+    k spans [k W - a, (k + 1) W - a) with a = the buffer's misalignment to 16 bytes."""
+    return (n + (buf_ptr & 15)) // WINDOW + 1
+
+
+def try_cut_gram(chain, rel, d: int):
+    """Launch the cutter for the Gram action (``scanfuse.try_fused_gram``'s chain with the
+    features as ``__gx<i>`` and the label as ``__gy``).  Returns (flat statistics, err, vflag,
+    stream) or None when the facts / chain do not allow it."""
+    from . import native
+    from .device import _h2d
+    from .scanfuse import _scan_stream  # noqa: F401 - same stream policy as the per-line kernel
+    from ..utils import tracing
+
+    cp = _compile(chain, rel, d)
+    if cp is None:
+        return None
+    f = rel.fused
+    h = native.hip()
+    dev = f["device"]
+    buf, n = f["buf"], int(f["n"])
+    nwin = n_windows(buf.data_ptr(), n)
+    grid = _grid(h, cp.per_cu, nwin)
+    err = torch.zeros(1, dtype=torch.int32, device=dev)
+    vflag = torch.zeros(1, dtype=torch.int32, device=dev)
+    gw = gram_width(d)
+    gpart = torch.empty(grid * cp.rg, gw, dtype=torch.float64, device=dev)
+    scalars = {"buf": buf, "nwin": nwin, "trailing": int(f["trailing"]), "vflag": vflag, "gpart": gpart}
+    ptrs = []
+    for tag in cp.recipe:
+        k = tag[0]
+        if k == "err":
+            ptrs.append(err.data_ptr())
+        elif k in ("sel", "out", "outvalid", "selout"):
+            ptrs.append(0)
+        elif k in scalars:
+            x = scalars[k]
+            ptrs.append(x.data_ptr() if torch.is_tensor(x) else int(x))
+        else:
+            raise AssertionError(f"cut plan: unbound slot {tag}")
+    handle, _log = h.rtc_compile(cp.src, ENTRY)
+    pt = _h2d(np.asarray(ptrs, dtype=np.int64), dev)
+    stream = torch.cuda.current_stream(dev)
+    with tracing.span("csv_cut_gram"):
+        h.rtc_launch(int(handle), grid, 256, pt.data_ptr(), n, stream.cuda_stream)
+        tot = gpart.sum(0)
+        flat = torch.cat([tot[:1].expand(3), tot[1:]])
+    tracing.add_rows("csv_cut_gram", int(f["nlines"]))
+    STATS["cut_grams"] += 1
+    return flat, err, vflag, cp

@@ -190,8 +190,8 @@ def _gram_code(xs, yv) -> str:
     for i in range(d):
         lines.append(f"      acc[{3 + i}] += gx{i}; acc[{3 + d + i}] += gx{i} * gy;\n")
     q = 3 + 2 * d
-    for i in range(d):
-        for j in range(i, d):
+    for j in range(d):  # packed upper, column by column: slot j(j+1)/2 + i (the WLS flat layout)
+        for i in range(j + 1):
             lines.append(f"      acc[{q}] += gx{i} * gx{j};\n")
             q += 1
     lines.append("    }\n")
@@ -622,6 +622,8 @@ def _compile(nodes, rel, gram: int = 0):
     from . import dqvm
 
     f = rel.fused
+    if len(f["kinds"]) > 64 or f["mean_line"] > 64:
+        return None  # one thread per line: wide rows take the cutter (ops/scancut.py) or scan eagerly
     (parts, udfs), refs = dqvm.nodes_key(nodes)
     head = head_bytes(f["mean_line"])
     lookback = os.environ.get("DQ4ML_SCAN_LOOKBACK", "1") != "0"
@@ -695,17 +697,25 @@ def _launch(cp, nodes, rel, extra: dict, own_stream: bool = True):
             h.rtc_launch(int(handle), nb, 256, ptrs.data_ptr(), n, stream)
     tracing.add_rows("csv_scan_dq_fused", nalloc)
     STATS["fused_scans"] += 1
-    if cp.has_raise and int(err.item()) != 0:
-        from ..sql.expressions import SparkException
-
-        msg = "Failed to execute user defined function"
-        for nd in nodes:
-            for ex in getattr(nd, "exprs", []) + ([nd.cond] if hasattr(nd, "cond") else []):
-                r = dqvm._find_raise(ex)
-                if r is not None:
-                    msg = r.message
-        raise SparkException(msg)
     return outs, sel_out, err, vflag, side, cur
+
+
+def _udf_error_check(nodes, err):
+    """A raising rule (``RaiseIfNull``: ``MinimumPriceDataQualityUdf``'s NPE on a null price,
+    ``MinimumPriceDataQualityUdf.java:11-13``) as a deferred device check (``runtime/checks.py``):
+    the action stays asynchronous and the SparkException surfaces with the first host read of
+    its results — the job fails exactly as Spark's does, without a sync per action."""
+    from ..runtime.checks import defer
+    from ..sql.expressions import SparkException
+    from . import dqvm
+
+    msg = "Failed to execute user defined function"
+    for nd in nodes:
+        for ex in getattr(nd, "exprs", []) + ([nd.cond] if hasattr(nd, "cond") else []):
+            r = dqvm._find_raise(ex)
+            if r is not None:
+                msg = r.message
+    return defer(err, lambda: SparkException(msg))
 
 
 def _fact_check(rel, vflag):
@@ -732,9 +742,10 @@ def try_fused_scan(nodes, rel, plan, session):
         cur.wait_stream(side)
         for t in [err, vflag, sel_out] + [x for o in outs for x in o if x is not None]:
             t.record_stream(cur)  # produced on the scan stream, consumed on the compute stream
-    check = _fact_check(rel, vflag)
+    checks = [_fact_check(rel, vflag)] + ([_udf_error_check(nodes, err)] if cp.has_raise else [])
+    checks = [c for c in checks if c is not None]
     schema = plan.schema()
-    cols = [ColumnData(fd.dataType, oo[0], oo[1], dict(fd.metadata), [check] if check is not None else [])
+    cols = [ColumnData(fd.dataType, oo[0], oo[1], dict(fd.metadata), list(checks))
             for fd, oo in zip(schema.fields, outs)]
     return Table(schema, cols, int(rel.fused["nlines"]), sel_out, rel.fused["device"])
 
@@ -783,7 +794,7 @@ def try_fused_gram(plan, features_col: str, label_col: str, session) -> Optional
     va = fe.child
     cs = top.child.schema()
     d = len(va.inputs)
-    if not 1 <= d <= 8:
+    if not 1 <= d <= 128:
         return None
     for c in va.inputs:
         t = ColRef(c).data_type(cs)
@@ -794,6 +805,18 @@ def try_fused_gram(plan, features_col: str, label_col: str, session) -> Optional
         return None
     gtop = Project(top.child, [Alias(ColRef(c), f"__gx{i}") for i, c in enumerate(va.inputs)] + [Alias(lexpr, "__gy")])
     chain = list(reversed(nodes[1:])) + [gtop]
+    from . import scancut
+
+    cut = scancut.try_cut_gram(chain, p, d)  # the byte-parallel field cutter (wide rows, any d <= 128)
+    if cut is not None:
+        flat, err, vflag, ccp = cut
+        checks = [_fact_check(p, vflag)]
+        if ccp.has_raise:
+            checks.append(_udf_error_check(chain, err))
+        STATS["fused_grams"] += 1
+        return FusedGram(flat, d, [c for c in checks if c is not None], int(p.fused["nlines"]))
+    if d > 8:
+        return None
     cp = _compile(chain, p, gram=d)
     if cp is None or cp == "vector":
         return None
@@ -813,6 +836,6 @@ def try_fused_gram(plan, features_col: str, label_col: str, session) -> Optional
         cur.wait_stream(side)
         for t in (err, vflag, gpart, tot, flat):
             t.record_stream(cur)
-    check = _fact_check(p, vflag)
+    checks = [_fact_check(p, vflag)] + ([_udf_error_check(chain, err)] if cp.has_raise else [])
     STATS["fused_grams"] += 1
-    return FusedGram(flat, d, [check] if check is not None else [], int(p.fused["nlines"]))
+    return FusedGram(flat, d, [c for c in checks if c is not None], int(p.fused["nlines"]))

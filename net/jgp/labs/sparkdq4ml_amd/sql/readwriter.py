@@ -317,10 +317,12 @@ class DataFrameReader:
             # a re-read of bytes an earlier device scan already typed: lazy relation, scanned at
             # the action — fused with the DQ chain on top of it when there is one (ops/scanfuse.py)
             facts = pf.scan_facts.get(fkey) if (pf is not None and dbytes is not None) else None
+            # (the per-line fused kernel takes <= 64 columns of lines <= 64 bytes on average; wider
+            # rows go through the byte-parallel cutter, ops/scancut.py, or scan eagerly)
             lazy = (facts is not None and len(body) == facts["nbytes"]
                     and _truthy(self._session.conf.get("dq4ml.csv.fuseScan", "true"))
-                    and len(facts["types"]) <= 64 and facts["nlines"] > 0
-                    and len(body) / facts["nlines"] <= 64)
+                    and len(facts["types"]) <= 256 and facts["nlines"] > 0
+                    and len(body) / facts["nlines"] <= 4096)
             if shard:  # every rank takes the same (collective) path
                 lazy = all(comm.all_gather_object(bool(lazy)))
             if lazy:
@@ -335,6 +337,11 @@ class DataFrameReader:
                          "trailing": n > 0 and body[-1] not in (10, 13), "mean_line": n / facts["nlines"],
                          "kinds": [_KIND.get(c, (0,))[0] for c in codes], "nullable": list(facts["nullable"]),
                          "fast_only": bool(facts.get("fast_only")),
+                         "max_line": int(facts.get("max_line", 1 << 30)),
+                         "uniform_fields": bool(facts.get("uniform_fields")),
+                         "empty_lines": int(facts.get("empty_lines", 1)),
+                         "min_line": int(facts.get("min_line", 1)),
+                         "term_kinds": list(facts.get("term_kinds") or (1, 1, 0)),
                          "opts": dict(_opt_args(dopts), sep=sep, strict=bool(strict)), "strict": bool(strict)}
                 if fused["opts"]["null_value"] and len(fused["opts"]["null_value"].encode()) > 16:
                     fused = None

@@ -183,9 +183,16 @@ class Table:
         return self.sel
 
     def count(self) -> int:
-        if self.sel is None:
-            return self.nrows
-        return int(self.sel.sum().item())
+        """Live rows.  The chain that produced the table ran over every column, so a pending data
+        error of ANY column (a raising rule, ``runtime/checks.py``) fails the count too — read
+        after the count's own device read, so no extra sync."""
+        n = self.nrows if self.sel is None else int(self.sel.sum().item())
+        pending = [ck for c in self.columns for ck in getattr(c, "checks", ())]
+        if pending:
+            from ..runtime.checks import verify
+
+            verify(pending)
+        return n
 
     def compact(self) -> "Table":
         """Materialize the selection vector (stream compaction)."""

@@ -109,6 +109,14 @@ for s in $STEPS; do
     lbfgs) step lbfgs 900 python benchmarks/bench_lbfgs.py --steps 2 --warmup 1 --json-out gpurun_out/lbfgs.json ;;
     lbfgs8) step lbfgs8 900 python benchmarks/bench_lbfgs.py --steps 2 --warmup 1 --dtype fp8 --json-out gpurun_out/lbfgs8.json ;;
     kproflbfgs) (export TMPDIR=/tmp; step kproflbfgs 600 rocprofv3 --kernel-trace --stats -d gpurun_out/kproflbfgs -o run --output-format csv -- python benchmarks/bench_lbfgs.py --steps 1 --warmup 0) || exit $? ;;
+    cut) step cut 600 python -u -m pytest tests/test_gpu_scancut.py tests/test_gpu_scanfuse.py tests/test_gpu_dqvm.py tests/test_gpu_semantics.py -m gpu -v --maxfail=5 --timeout 120 --timeout-method thread ;;
+    cutpmc) (export TMPDIR=/tmp
+       step cutpmc1 300 timeout -s KILL 240 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS GRBM_GUI_ACTIVE -d gpurun_out/cutpmc1 -o run --output-format csv -- python benchmarks/bench_csv_pipeline.py --features 32 --rows 2e7 --steps 2 --warmup 1 &&
+       step cutpmc2 300 timeout -s KILL 240 rocprofv3 --kernel-trace --pmc SQ_INSTS_SALU SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_VMEM SQ_ACTIVE_INST_MISC GRBM_GUI_ACTIVE -d gpurun_out/cutpmc2 -o run --output-format csv -- python benchmarks/bench_csv_pipeline.py --features 32 --rows 2e7 --steps 2 --warmup 1) || exit $? ;;
+    csv32s) step csv32s 600 python benchmarks/bench_csv_pipeline.py --features 32 --rows 2e7 --steps 10 --warmup 2 ;;
+    csv32) step csv32 900 python benchmarks/bench_csv_pipeline.py --features 32 --rows 1e8 --steps 10 --warmup 2 --json-out gpurun_out/csv32.json ;;
+    csv64) step csv64 900 python benchmarks/bench_csv_pipeline.py --features 64 --rows ${CSV64_ROWS:-5e7} --steps 10 --warmup 2 --json-out gpurun_out/csv64.json ;;
+    kprofcsv32) (export TMPDIR=/tmp; step kprofcsv32 600 rocprofv3 --kernel-trace --stats -d gpurun_out/kprofcsv32 -o run --output-format csv -- python benchmarks/bench_csv_pipeline.py --features 32 --rows 2e7 --steps 5 --warmup 2) || exit $? ;;
     prof) cd /tmp && export TMPDIR=/tmp && cd - >/dev/null; step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 5 --warmup 1 ;;
   esac
 done

@@ -1,0 +1,101 @@
+// Host check of the device field converters (csv_parse_dev.h): csv_swar_field16 and csv_field_r16 must accept
+// exactly what the byte-walking fast path csv_field_fast accepts and return the same bits, over
+// every field shape the cutter hands it (1..16 bytes: signs, dots, digits, junk).  Compiled with
+// g++ (the header is plain C++ once the HIP qualifiers are defined away).
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <random>
+#include <string>
+
+#define __device__
+#define __forceinline__ inline
+static inline int __popcll(unsigned long long x) { return __builtin_popcountll(x); }
+#include "csv_parse_dev.h"
+
+using namespace dq4ml_csv;
+
+static bool fast(const std::string& f, double& dv, long long& lv, int& ty) {
+  std::string s = f + ",";
+  int pos = 0;
+  const int end = (int)f.size();
+  return csv_field_fast((const unsigned char*)s.data(), 0, pos, end, (unsigned char)',', dv, lv, ty);
+}
+
+static std::mt19937 junk(7);
+
+// the right-aligned converter: the field at a varying offset in a dword-aligned stage, junk bytes
+// before it (they must be masked off) and after it
+static bool r16(const std::string& f, double& dv, long long& lv, int& ty) {
+  alignas(16) unsigned char buf[64];
+  const char pool[] = "0123456789.-+,\r\n x";
+  for (auto& c : buf) c = (unsigned char)pool[junk() % (sizeof(pool) - 1)];
+  const int off = 16 + (int)(junk() % 16);
+  memcpy(buf + off, f.data(), f.size());
+  return csv_field_r16(buf, off + (int)f.size(), (int)f.size(), dv, lv, ty);
+}
+
+static bool swar(const std::string& f, double& dv, long long& lv, int& ty) {
+  unsigned char buf[48] = {0};
+  const int off = 5;  // an unaligned start, like a field inside an LDS stage
+  memcpy(buf + off, f.data(), f.size());
+  unsigned long long lo, hi;
+  csv_line16(buf, off, lo, hi);
+  return csv_swar_field16(lo, hi, (int)f.size(), dv, lv, ty);
+}
+
+int main() {
+  std::mt19937_64 rng(12345);
+  const char alpha[] = "0123456789.-+e,x ";
+  long checked = 0, accepted = 0;
+  auto check = [&](const std::string& f) {
+    double d1 = 0, d2 = 0;
+    long long l1 = 0, l2 = 0;
+    int t1 = -1, t2 = -1;
+    const bool a = fast(f, d1, l1, t1), b = swar(f, d2, l2, t2);
+    ++checked;
+    if (a != b || (a && (t1 != t2 || l1 != l2 || memcmp(&d1, &d2, sizeof d1) != 0))) {
+      printf("MISMATCH field '%s': fast %d ty %d %.17g %lld | swar16 %d ty %d %.17g %lld\n", f.c_str(), a, t1, d1,
+             l1, b, t2, d2, l2);
+      return false;
+    }
+    double d3 = 0;
+    long long l3 = 0;
+    int t3 = -1;
+    const bool c = r16(f, d3, l3, t3);
+    if (a != c || (a && (t1 != t3 || l1 != l3 || memcmp(&d1, &d3, sizeof d1) != 0))) {
+      printf("MISMATCH field '%s': fast %d ty %d %.17g %lld | r16 %d ty %d %.17g %lld\n", f.c_str(), a, t1, d1, l1,
+             c, t3, d3, l3);
+      return false;
+    }
+    accepted += a;
+    return true;
+  };
+  // numeric shapes: [sign] digits [. digits], 1..16 bytes
+  for (int it = 0; it < 3000000; ++it) {
+    std::string f;
+    const int sg = (int)(rng() % 4);
+    if (sg == 1) f += '-';
+    if (sg == 2) f += '+';
+    const int nd = 1 + (int)(rng() % 12);
+    const int dp = (rng() % 3) ? (int)(rng() % (nd + 1)) : -1;
+    for (int k = 0; k < nd; ++k) {
+      if (k == dp) f += '.';
+      f += (char)('0' + rng() % 10);
+    }
+    if (dp == nd) f += '.';
+    if (f.size() > 16) continue;
+    if (!check(f)) return 1;
+  }
+  if (!check("")) return 1;  // the empty field: null
+  // arbitrary bytes from a small alphabet (junk, double dots, stray signs)
+  for (int it = 0; it < 2000000; ++it) {
+    const int len = 1 + (int)(rng() % 16);
+    std::string f;
+    for (int k = 0; k < len; ++k) f += alpha[rng() % (sizeof(alpha) - 1)];
+    if (f.find(',') != std::string::npos) continue;  // the cutter never hands over a separator
+    if (!check(f)) return 1;
+  }
+  printf("swar16 ok: %ld fields, %ld accepted\n", checked, accepted);
+  return 0;
+}
