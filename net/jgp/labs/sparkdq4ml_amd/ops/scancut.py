@@ -47,6 +47,7 @@ __all__ = ["applicable", "kernel_source", "try_cut_gram", "STATS", "ENTRY"]
 ENTRY = "dq_scan_cut"
 WINDOW = 16384
 TILE_BYTES = 18432  # LDS of the row tiles (chain inputs + Gram rows) per round
+TARGET_PER_CU = 4   # resident blocks per CU the LDS budget aims at
 STATS = {"cut_grams": 0}
 
 
@@ -140,17 +141,19 @@ class _Shape:
         self.feat = feat                                # passthrough feature columns (blocked only)
         per_row = 8 * (self.CU + (self.PP if self.blocked else 0))
         self.gw = gram_width(d)
-        fixed = (16 + H + self.W + 32) + 2 * self.DCAP + 4 * C + 128 + (0 if self.blocked else 32 * self.gw)
-        # the row tiles take what keeps 4 blocks resident per CU (40 KiB each), within
-        # [4 KiB, TILE_BYTES]: more rounds per window beat fewer resident blocks
-        tile = max(4096, min(TILE_BYTES, 40960 - fixed))
+        fixed = (16 + H + self.W + 32) + 2 * self.DCAP + 4 * C + 384 + (0 if self.blocked else 32 * self.gw)
+        # the row tiles take what keeps TARGET_PER_CU blocks resident per CU (40 KiB each at 4),
+        # within [4 KiB, TILE_BYTES]: more rounds per window beat fewer resident blocks
+        per_cu = int(os.environ.get("DQ4ML_CUT_PER_CU", TARGET_PER_CU))
+        cap = int(os.environ.get("DQ4ML_CUT_TILE", TILE_BYTES))
+        tile = max(4096, min(cap, (160 * 1024) // per_cu - fixed))
         self.RR = int(max(1, min(rows_max, tile // per_row)))
         self.lds = fixed + 8 * self.RR * self.CU + (8 * self.RR * self.PP if self.blocked else 0)
         self.gw = gram_width(d)
 
 
 def kernel_source(g, kinds, used, opts: dict, H: int, slots: dict, d: int, term: int = 13, crlf: bool = False,
-                  min_line: int = 1, waves_per_simd: int = 0):
+                  min_line: int = 1, waves_per_simd: int = 0, max_line: int = 1 << 30):
     """Source of the cutter kernel and its ``_Shape``.  ``term``: the file's one terminator byte
     (13 CR, 10 LF; ``crlf``: every CR is followed by LF, which then opens the next row and is
     skipped); ``min_line``: the shortest line, sizing the delimiter array and the row tile."""
@@ -176,6 +179,18 @@ def kernel_source(g, kinds, used, opts: dict, H: int, slots: dict, d: int, term:
 
         ucols = [c for c in ucols if re.search(rf"\bfzf{c}\b", body_text)]
     sh = _Shape(C, d, H, min_line, ucols, feat)
+    # the converter's frame: 8 bytes when no field can be longer (line minus terminator and the
+    # other fields' >= 2 bytes each), else 16 (longer fields take the byte-walking fast path)
+    FW = 8 if max_line - 1 - 2 * (C - 1) <= 8 else 16
+    # diagnostic ablations (timing only, results are wrong): 1 no field conversion, 2 no Gram
+    # phase, 4 no row phase
+    abl = int(os.environ.get("DQ4ML_CUT_ABLATE", "0"))
+    conv_call = ("ok = true; m = (unsigned)len;" if abl & 1 else
+                 f"""if (__ballot(fl > 8) == 0ull) {{
+          ok = csv_num_r8s(stage, end, fl, m, fr, dot);
+        }} else {{
+          ok = csv_num_r<{FW // 4}>(stage, end, len < {FW} ? len : {FW}, m, fr, neg, dot);
+        }}""")
     W, HG, DCAP, RR, CU, PP, NB, U, RG, GW = sh.W, sh.HG, sh.DCAP, sh.RR, sh.CU, sh.PP, sh.NB, sh.U, sh.RG, sh.gw
     usl = {c: i for i, c in enumerate(ucols)}
     sep = ord(opts.get("sep", ","))
@@ -262,11 +277,23 @@ def kernel_source(g, kinds, used, opts: dict, H: int, slots: dict, d: int, term:
 """
         tables = ""
         gt_decl = ""
-    feat_store = ("          const int fs = ctab[2 * col + 1];\n"
-                  f"          if (fs >= 0) gt[rr * {PP} + fs] = dv;\n") if (sh.blocked and feat is not None) else ""
+    # column -> vt slot / Gram-tile feature slot: VALU selects for the common shapes, else the
+    # LDS table
+    if len(ucols) <= 6:
+        us_expr = "".join(f"c == {cc} ? {i} : " for i, cc in enumerate(ucols)) + "-1"
+    else:
+        us_expr = "ctab[2 * c]"
+    feat_store = ""
+    if sh.blocked and feat is not None:
+        if feat == list(range(feat[0], feat[0] + d)):
+            fs_expr = f"(c >= {feat[0]} && c < {feat[0] + d}) ? c - {feat[0]} : -1"
+        else:
+            fs_expr = "ctab[2 * c + 1]"
+        feat_store = (f"        const int fs = {fs_expr};\n"
+                      f"        if (fs >= 0) gt[rr * {PP} + fs] = dv;\n")
     kind_tab = ", ".join(str(int(k)) for k in kinds)
     lb = f"__launch_bounds__(256, {waves_per_simd})" if waves_per_simd else "__launch_bounds__(256)"
-    src = header_text() + f"""
+    src = "#define CSV_UDOT4(a, b, c) __builtin_amdgcn_udot4((a), (b), (c), false)\n" + header_text() + f"""
 using namespace dq4ml_csv;
 typedef unsigned int csv_u32x4 __attribute__((ext_vector_type(4)));
 typedef double f64x2 __attribute__((ext_vector_type(2)));
@@ -316,7 +343,9 @@ extern "C" __global__ {lb} void {ENTRY}(void* const* P, long long n) {{
   unsigned int* vflag = (unsigned int*)p[{slots['vflag']}];
   __shared__ __attribute__((aligned(16))) unsigned char stage_raw[16 + {H} + {W} + 32];
   unsigned char* const stage = stage_raw + 16;  // 16 readable bytes below stage[0] (right-aligned reads)
-  __shared__ unsigned short dpos[{DCAP}];
+  __shared__ unsigned short dpos[{DCAP} + 1];
+  unsigned short* const dposx = dpos;  // dposx[0]: the delimiter before the window's first field
+  unsigned short* const dcut = dpos + 1;  // the window's delimiters
   __shared__ __attribute__((aligned(16))) double vt[{RR * CU}];
 {gt_decl}  __shared__ short ctab[{2 * C}];
   __shared__ int wtot[4], shtot, sst0;
@@ -326,6 +355,11 @@ extern "C" __global__ {lb} void {ENTRY}(void* const* P, long long n) {{
   const CsvOpts O = {o};
   bool bad = false;
   for (int i = tid; i < {2 * C}; i += 256) ctab[i] = DQ_CTAB[i];
+  __shared__ double p10t[16], ip10t[16];  // 10^k and RN(10^-k) for the converter (k > 9: unused)
+  if (tid < 16) {{
+    p10t[tid] = tid <= 9 ? csv_pow10(tid) : 1.0;
+    ip10t[tid] = tid <= 9 ? csv_inv_pow10(tid) : 1.0;
+  }}
 {acc_decl}
   // a CONTIGUOUS run of windows per block: the row start of window k+1 is carried from the cut
   // of window k (only the first window searches back for it), and window k+1's bytes are in
@@ -432,14 +466,16 @@ extern "C" __global__ {lb} void {ENTRY}(void* const* P, long long n) {{
       bad = true;
       break;  // block-uniform
     }}
-    // the cut: every delimiter's stage position, in byte order
+    // the cut: every delimiter's stage position, in byte order, after the sentinel (the
+    // delimiter "before" the first field: its start minus one, minus the LF of a CR LF)
+    if (tid == 0) dposx[0] = (unsigned short)(st0 - 1 - {1 if crlf else 0});
     if (hm) {{
       int idx = hinc - __popcll(hm);
       unsigned long long mm = hm;
       while (mm) {{
         const int bit = __builtin_ctzll(mm);
         mm &= mm - 1;
-        dpos[idx++] = (unsigned short)(64 * tid + bit);
+        dcut[idx++] = (unsigned short)(64 * tid + bit);
       }}
     }}
     {{
@@ -448,47 +484,53 @@ extern "C" __global__ {lb} void {ENTRY}(void* const* P, long long n) {{
       while (mm) {{
         const int bit = __builtin_ctzll(mm);
         mm &= mm - 1;
-        dpos[idx++] = (unsigned short)({H} + 64 * tid + bit);
+        dcut[idx++] = (unsigned short)({H} + 64 * tid + bit);
       }}
     }}
     __syncthreads();
     // the next window's first row starts after this window's last complete row
-    const int nst0 = cnt > 0 ? (int)dpos[cnt * {C} - 1] + 1 + {1 if crlf else 0} - {W} : st0 - {W};
+    const int nst0 = cnt > 0 ? (int)dcut[cnt * {C} - 1] + 1 + {1 if crlf else 0} - {W} : st0 - {W};
     for (int R0 = 0; R0 < cnt; R0 += {RR}) {{
       const int nr = min({RR}, cnt - R0), f0 = R0 * {C}, f1 = f0 + nr * {C};
       if (R0 > 0) __syncthreads();  // the previous round's Gram readers are done with the tiles
-      // one field per lane: the right-aligned 16-byte converter straight out of the stage
+      // one field per lane: the sign byte, then the unsigned part through the 8-byte 64-bit SWAR
+      // frame when every field of the wave fits it (wave-uniform branch), else the 16-byte frame;
+      // fields longer than that take the byte-walking fast path (rare, divergent)
       for (int f = f0 + tid; f < f1; f += 256) {{
-        const int end = dpos[f];
-        const int rw = f / {C}, col = f - rw * {C};
-        const int start = f == 0 ? st0 : (int)dpos[f - 1] + 1 + ({1 if crlf else 0} && col == 0 ? 1 : 0);
+        const int end = dposx[f + 1];
+        const int rw = f / {C}, c = f - rw * {C};
+        const int start = dposx[f] + 1 + ({1 if crlf else 0} && c == 0 ? 1 : 0);
         const int len = end - start;
-        double dv = 0.0;
-        long long lv = 0;
-        int ty = C_NULL;
-        bool ok = false;
-        if (len >= 0 && len <= 16) {{
-          ok = csv_field_r16(stage, end, len, dv, lv, ty);
-        }} else if (len > 16) {{
+        const int c0 = stage[start];
+        const bool neg0 = c0 == '-';
+        const int fl = len - ((c0 == '-' || c0 == '+') ? 1 : 0);
+        unsigned m = 0u;
+        int fr = 0;
+        bool neg = neg0, dot = false, ok;
+        {conv_call}
+        const double v = dot ? csv_div_pow10_fma((double)m, p10t[fr & 15], ip10t[fr & 15]) : (double)m;
+        double dv = neg ? -v : v;
+        ok = ok && csv_conforms(dot ? C_DOUBLE : C_INT, DQ_KIND[c]);
+        if (len > {FW}) {{
           int ps = start;
-          ok = csv_field_fast(stage, 0, ps, end, O.sep, dv, lv, ty);
+          long long lv = 0;
+          int ty = C_NULL;
+          ok = csv_field_fast(stage, 0, ps, end, O.sep, dv, lv, ty) && ty != C_NULL && csv_conforms(ty, DQ_KIND[c]);
         }}
-        bad |= !ok || ty == C_NULL || !csv_conforms(ty, DQ_KIND[col]);
-        {{
-          const int rr = rw - R0;
-          const int us = ctab[2 * col];
-          if (us >= 0) vt[rr * {CU} + us] = dv;
-{feat_store}        }}
-      }}
+        bad |= !ok;
+        const int rr = rw - R0;
+        const int us = {us_expr};
+        if (us >= 0) vt[rr * {CU} + us] = dv;
+{feat_store}      }}
       __syncthreads();
       for (int r = tid; r < nr; r += 256) {{  // one row per thread: the DQ chain and the assembler
         const int rb = r * {CU};
 {loads}        const bool line = true;
         bool live = line;
-{body}
-{outs}      }}
+{body if not abl & 4 else ""}
+{outs if not abl & 4 else ""}      }}
       __syncthreads();
-{gram_phase}    }}
+{gram_phase if not abl & 2 else ""}    }}
     st0 = nst0;
   }}
   if (bad) dq_flag(vflag, 1u);
@@ -525,7 +567,8 @@ def _compile(nodes, rel, d: int):
     min_line = int(f.get("min_line", 1))
     (parts, udfs), refs = dqvm.nodes_key(nodes)
     key = (parts, udfs, tuple(rel.schema().names), tuple(f["kinds"]), repr(sorted(f["opts"].items())), H, d, term,
-           crlf, min_line)
+           crlf, min_line, int(f.get("max_line", 1 << 30)), os.environ.get("DQ4ML_CUT_PER_CU"),
+           os.environ.get("DQ4ML_CUT_TILE"), os.environ.get("DQ4ML_CUT_ABLATE"))
     if key in _CACHE:
         return _CACHE[key]
     base = _ScanBase(rel.schema(), 0, f["device"])
@@ -534,9 +577,10 @@ def _compile(nodes, rel, d: int):
     try:
         _, g, outputs, _ = dqvm.compile_chain(nodes, base, False, gen=g)
         slots = {k: g.slot(None, (k,)) for k in ("buf", "nwin", "trailing", "vflag", "gpart")}
-        _, sh = kernel_source(g, f["kinds"], g.used, f["opts"], H, slots, d, term, crlf, min_line)
+        ml = int(f.get("max_line", 1 << 30))
+        _, sh = kernel_source(g, f["kinds"], g.used, f["opts"], H, slots, d, term, crlf, min_line, 0, ml)
         per_cu = blocks_per_cu(sh.lds)
-        src, sh = kernel_source(g, f["kinds"], g.used, f["opts"], H, slots, d, term, crlf, min_line, per_cu)
+        src, sh = kernel_source(g, f["kinds"], g.used, f["opts"], H, slots, d, term, crlf, min_line, per_cu, ml)
         cp = _CutPlan(src, g, refs, sh, per_cu)
     except (dqvm.Unfusable, _GramNullable):
         cp = None

@@ -113,6 +113,21 @@ for s in $STEPS; do
     cutpmc) (export TMPDIR=/tmp
        step cutpmc1 300 timeout -s KILL 240 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS GRBM_GUI_ACTIVE -d gpurun_out/cutpmc1 -o run --output-format csv -- python benchmarks/bench_csv_pipeline.py --features 32 --rows 2e7 --steps 2 --warmup 1 &&
        step cutpmc2 300 timeout -s KILL 240 rocprofv3 --kernel-trace --pmc SQ_INSTS_SALU SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_VMEM SQ_ACTIVE_INST_MISC GRBM_GUI_ACTIVE -d gpurun_out/cutpmc2 -o run --output-format csv -- python benchmarks/bench_csv_pipeline.py --features 32 --rows 2e7 --steps 2 --warmup 1) || exit $? ;;
+    cutsweep) for pc in 3 4; do for tl in 18432 36864; do
+         step cutsweep_lab_${pc}_${tl} 300 env DQ4ML_CUT_PER_CU=$pc DQ4ML_CUT_TILE=$tl python benchmarks/bench_csv_pipeline.py --steps 10 --warmup 2 &&
+         step cutsweep_w32_${pc}_${tl} 300 env DQ4ML_CUT_PER_CU=$pc DQ4ML_CUT_TILE=$tl python benchmarks/bench_csv_pipeline.py --features 32 --rows 2e7 --steps 10 --warmup 2 || exit $?
+       done; done ;;
+    cutpmclab) (export TMPDIR=/tmp
+       step cutpmclab1 300 timeout -s KILL 240 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS GRBM_GUI_ACTIVE -d gpurun_out/cutpmclab1 -o run --output-format csv -- python benchmarks/bench_csv_pipeline.py --steps 2 --warmup 1 &&
+       step cutpmclab2 300 timeout -s KILL 240 rocprofv3 --kernel-trace --pmc SQ_INSTS_SALU SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_VMEM SQ_ACTIVE_INST_MISC GRBM_GUI_ACTIVE -d gpurun_out/cutpmclab2 -o run --output-format csv -- python benchmarks/bench_csv_pipeline.py --steps 2 --warmup 1) || exit $? ;;
+    cutabl) for ab in 0 1 2 4 7; do
+         step cutabl_lab_$ab 300 env DQ4ML_CUT_ABLATE=$ab python benchmarks/bench_csv_pipeline.py --steps 10 --warmup 2 &&
+         step cutabl_w32_$ab 300 env DQ4ML_CUT_ABLATE=$ab python benchmarks/bench_csv_pipeline.py --features 32 --rows 2e7 --steps 10 --warmup 2 || exit $?
+       done ;;
+    cutnf) for nf in 1 2; do for pc in 3 4; do
+         step cutnf_lab_${nf}_${pc} 300 env DQ4ML_CUT_NF=$nf DQ4ML_CUT_PER_CU=$pc python benchmarks/bench_csv_pipeline.py --steps 10 --warmup 2 &&
+         step cutnf_w32_${nf}_${pc} 300 env DQ4ML_CUT_NF=$nf DQ4ML_CUT_PER_CU=$pc python benchmarks/bench_csv_pipeline.py --features 32 --rows 2e7 --steps 10 --warmup 2 || exit $?
+       done; done ;;
     csv32s) step csv32s 600 python benchmarks/bench_csv_pipeline.py --features 32 --rows 2e7 --steps 10 --warmup 2 ;;
     csv32) step csv32 900 python benchmarks/bench_csv_pipeline.py --features 32 --rows 1e8 --steps 10 --warmup 2 --json-out gpurun_out/csv32.json ;;
     csv64) step csv64 900 python benchmarks/bench_csv_pipeline.py --features 64 --rows ${CSV64_ROWS:-5e7} --steps 10 --warmup 2 --json-out gpurun_out/csv64.json ;;

@@ -1,4 +1,4 @@
-// Host check of the device field converters (csv_parse_dev.h): csv_swar_field16 and csv_field_r16 must accept
+// Host check of the device field converters (csv_parse_dev.h): csv_swar_field16, csv_field_r16 and csv_field_r8 must accept
 // exactly what the byte-walking fast path csv_field_fast accepts and return the same bits, over
 // every field shape the cutter hands it (1..16 bytes: signs, dots, digits, junk).  Compiled with
 // g++ (the header is plain C++ once the HIP qualifiers are defined away).
@@ -35,6 +35,38 @@ static bool r16(const std::string& f, double& dv, long long& lv, int& ty) {
   return csv_field_r16(buf, off + (int)f.size(), (int)f.size(), dv, lv, ty);
 }
 
+static bool r8(const std::string& f, double& dv, long long& lv, int& ty) {
+  alignas(16) unsigned char buf[64];
+  const char pool[] = "0123456789.-+,\r\n x";
+  for (auto& c : buf) c = (unsigned char)pool[junk() % (sizeof(pool) - 1)];
+  const int off = 16 + (int)(junk() % 16);
+  memcpy(buf + off, f.data(), f.size());
+  return csv_field_r8(buf, off + (int)f.size(), (int)f.size(), dv, lv, ty);
+}
+
+// the cutter's sign-stripped 8-byte path (csv_num_r8s + the caller's sign handling)
+static bool r8s(const std::string& f, double& dv, long long& lv, int& ty, bool& fits) {
+  alignas(16) unsigned char buf[64];
+  const char pool[] = "0123456789.-+,\r\n x";
+  for (auto& c : buf) c = (unsigned char)pool[junk() % (sizeof(pool) - 1)];
+  const int off = 16 + (int)(junk() % 16);
+  memcpy(buf + off, f.data(), f.size());
+  const int len = (int)f.size();
+  const unsigned char c0 = len ? buf[off] : 0;
+  const int sg = (c0 == '-' || c0 == '+') ? 1 : 0;
+  fits = len - sg <= 8;
+  if (!fits) return false;
+  unsigned m;
+  int fr;
+  bool dot;
+  const bool ok = csv_num_r8s(buf, off + len, len - sg, m, fr, dot);
+  const double v = dot ? csv_div_pow10((double)m, fr) : (double)m;
+  dv = ok ? (c0 == '-' ? -v : v) : 0.0;
+  lv = ok && !dot ? (c0 == '-' ? -(long long)m : (long long)m) : 0;
+  ty = len == 0 ? C_NULL : (dot ? C_DOUBLE : C_INT);
+  return len == 0 || ok;
+}
+
 static bool swar(const std::string& f, double& dv, long long& lv, int& ty) {
   unsigned char buf[48] = {0};
   const int off = 5;  // an unaligned start, like a field inside an LDS stage
@@ -67,6 +99,29 @@ int main() {
       printf("MISMATCH field '%s': fast %d ty %d %.17g %lld | r16 %d ty %d %.17g %lld\n", f.c_str(), a, t1, d1, l1,
              c, t3, d3, l3);
       return false;
+    }
+    {
+      double d5 = 0;
+      long long l5 = 0;
+      int t5 = -1;
+      bool fits = false;
+      const bool g = r8s(f, d5, l5, t5, fits);
+      if (fits && (a != g || (a && (t1 != t5 || l1 != l5 || memcmp(&d1, &d5, sizeof d1) != 0)))) {
+        printf("MISMATCH field '%s': fast %d ty %d %.17g %lld | r8s %d ty %d %.17g %lld\n", f.c_str(), a, t1, d1,
+               l1, g, t5, d5, l5);
+        return false;
+      }
+    }
+    if (f.size() <= 8) {
+      double d4 = 0;
+      long long l4 = 0;
+      int t4 = -1;
+      const bool e = r8(f, d4, l4, t4);
+      if (a != e || (a && (t1 != t4 || l1 != l4 || memcmp(&d1, &d4, sizeof d1) != 0))) {
+        printf("MISMATCH field '%s': fast %d ty %d %.17g %lld | r8 %d ty %d %.17g %lld\n", f.c_str(), a, t1, d1, l1,
+               e, t4, d4, l4);
+        return false;
+      }
     }
     accepted += a;
     return true;

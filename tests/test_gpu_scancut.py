@@ -156,3 +156,56 @@ def test_cutter_on_reference_dataset_matches_golden(spark, tmp_path):
     keep = raw[:, 1] >= 20
     ref = _oracle(raw[:, :1].T, raw[:, 1], keep)
     np.testing.assert_allclose(fused.flat.cpu().numpy(), ref, rtol=1e-13)
+
+
+def _lab_df(spark, path):
+    from net.jgp.labs.sparkdq4ml_amd import VectorAssembler, callUDF
+
+    df = spark.read().format("csv").option("inferSchema", "true").load(path)
+    df = df.withColumnRenamed("_c0", "guest").withColumnRenamed("_c1", "price")
+    df = df.withColumn("price_no_min", callUDF("minimumPriceRule", df.col("price")))
+    df.createOrReplaceTempView("price")
+    df = spark.sql("SELECT cast(guest as int) guest, price_no_min AS price FROM price WHERE price_no_min > 0")
+    df = df.withColumn("price_correct_correl", callUDF("priceCorrelationRule", df.col("price"), df.col("guest")))
+    df.createOrReplaceTempView("price")
+    df = spark.sql("SELECT guest, price_correct_correl AS price FROM price WHERE price_correct_correl > 0")
+    df = df.withColumn("label", df.col("price"))
+    return VectorAssembler().setInputCols(["guest"]).setOutputCol("features").transform(df)
+
+
+def test_lab_pipeline_on_csv_has_no_host_sync_and_defers_the_npe(spark, tmp_path):
+    """the lab's CSV -> rules -> fit action issues no device->host sync (async fit,
+    ``set_sync_debug_mode("error")``), and a null price still fails the job with the rule's NPE
+    (``MinimumPriceDataQualityUdf.java:11-13``) — raised on the first host read of the model."""
+    import bench_csv_pipeline as B
+
+    from net.jgp.labs.sparkdq4ml_amd import LinearRegression
+    from net.jgp.labs.sparkdq4ml_amd.dq.rules import register_lab_rules
+    from net.jgp.labs.sparkdq4ml_amd.sql.expressions import SparkException
+
+    spark.conf.set("dq4ml.fit.async", "true")
+    register_lab_rules(spark)
+    p = str(tmp_path / "lab.csv")
+    B.synth_csv(p, 200_000)
+    spark.read().format("csv").option("inferSchema", "true").load(p).count()  # the eager scan: facts
+    lr = LinearRegression().setMaxIter(40).setRegParam(1).setElasticNetParam(1)
+    ref = lr.fit(_lab_df(spark, p)).coefficients[0]  # warm-up: kernels compiled, plans cached
+    torch.cuda.synchronize()
+    torch.cuda.set_sync_debug_mode("error")
+    try:
+        models = [lr.fit(_lab_df(spark, p)) for _ in range(2)]
+    finally:
+        torch.cuda.set_sync_debug_mode("default")
+    assert all(m.coefficients[0] == ref for m in models)
+    # a null price (an empty field) in the middle of the file
+    data = bytearray(open(p, "rb").read())
+    cut = data.index(b"\r", len(data) // 2) + 1
+    comma = data.index(b",", cut)
+    end = data.index(b"\r", comma)
+    q = str(tmp_path / "lab_null.csv")
+    open(q, "wb").write(bytes(data[:comma + 1] + data[end:]))
+    spark.read().format("csv").option("inferSchema", "true").load(q).count()
+    m = lr.fit(_lab_df(spark, q))
+    with pytest.raises(SparkException, match="NullPointerException"):
+        m.coefficients
+    spark.conf.set("dq4ml.fit.async", "false")

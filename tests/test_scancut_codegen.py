@@ -47,7 +47,7 @@ def _cut_source(spark, d, lab):
     schema = StructType([StructField(f"_c{i}", IntegerType() if k == 1 else DoubleType(), True)
                          for i, k in enumerate(kinds)])
     fused = {"kinds": kinds, "nullable": [False] * ncol, "strict": False, "fast_only": True, "empty_lines": 0,
-             "uniform_fields": True, "max_line": 12 if lab else 11 * ncol, "device": torch.device("cpu"),
+             "uniform_fields": True, "max_line": 10 if lab else 11 * ncol, "device": torch.device("cpu"),
              "min_line": 6 if lab else 9 * ncol, "term_kinds": [100, 0, 0],
              "opts": dict(_opt_args({"comment": 0}), sep=",", strict=False)}
     rel = CsvScanRelation(schema, lambda: None, fused, "Relation[csv]")
@@ -84,10 +84,11 @@ def _cut_source(spark, d, lab):
     g = scanfuse._scan_gen(base, fused["nullable"])
     _, g, _, _ = dqvm.compile_chain(chain, base, False, gen=g)
     slots = {k: g.slot(None, (k,)) for k in ("buf", "nwin", "trailing", "vflag", "gpart")}
+    ml = fused["max_line"]
     src, sh = scancut.kernel_source(g, kinds, g.used, fused["opts"], H, slots, d, 13, False, fused["min_line"],
                                     scancut.blocks_per_cu(scancut.kernel_source(g, kinds, g.used, fused["opts"], H,
                                                                                 slots, d, 13, False,
-                                                                                fused["min_line"])[1].lds))
+                                                                                fused["min_line"], 0, ml)[1].lds), ml)
     return src
 
 
@@ -97,6 +98,7 @@ def test_cut_kernel_compiles_for_gfx950(cpu_session, tmp_path, d, lab):
     assert f"void {scancut.ENTRY}(" in src
     assert "for (int r = tid; r < nr; r += 256)" in src  # a row tile larger than the block is covered
     assert ("DQ_GIDX" in src) == (d > 8)
+    assert ("csv_num_r<2>(stage, end" in src) == lab  # 8-byte converter frame for the lab's short fields
     hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
     if not os.path.exists(hipcc):
         pytest.skip("no hipcc")
