@@ -49,6 +49,7 @@ WINDOW = 16384
 TILE_BYTES = 18432  # LDS of the row tiles (chain inputs + Gram rows) per round
 TARGET_PER_CU = 4   # resident blocks per CU the LDS budget aims at
 STATS = {"cut_grams": 0}
+LAST_STAMPS: dict = {}  # diagnostic phase clocks of the last launch (DQ4ML_CUT_STAMPS=1)
 
 
 def head_for(max_line: int) -> int:
@@ -136,20 +137,194 @@ class _Shape:
         self.NB = self.PP // 4
         self.U = self.NB * (self.NB + 1) // 2
         self.RG = max(1, 256 // self.U) if self.blocked else 1
+        # the MFMA Gram (v_mfma_f64_16x16x4_f64 over 16-feature tiles of the row tile): d + 2 <= 80;
+        # waves split into G tile groups x (4 / G) row groups, <= 32 accumulator VGPRs per wave
+        self.NT16 = (d + 2 + 15) // 16
+        self.tiles = [(I, J) for I in range(self.NT16) for J in range(I, self.NT16)]
+        self.mfma = self.blocked and d + 2 <= 80 and os.environ.get("DQ4ML_CUT_MFMA", "1") != "0"
+        if self.mfma:
+            self.G = next((g for g in (1, 2, 4) if -(-len(self.tiles) // g) * 8 <= 32), 4)
+            self.RG = 4 // self.G
         self.ucols = ucols                              # columns the chain reads, in vt order
         self.CU = max(1, len(ucols))
         self.feat = feat                                # passthrough feature columns (blocked only)
         per_row = 8 * (self.CU + (self.PP if self.blocked else 0))
         self.gw = gram_width(d)
-        fixed = (16 + H + self.W + 32) + 2 * self.DCAP + 4 * C + 384 + (0 if self.blocked else 32 * self.gw)
+        fixed = (16 + H + self.W + 32) + 2 * self.DCAP + 4 * C + 384 + (
+            8 * (3 * self.PP + 16) if self.blocked else 32 * self.gw)
         # the row tiles take what keeps TARGET_PER_CU blocks resident per CU (40 KiB each at 4),
         # within [4 KiB, TILE_BYTES]: more rounds per window beat fewer resident blocks
         per_cu = int(os.environ.get("DQ4ML_CUT_PER_CU", TARGET_PER_CU))
         cap = int(os.environ.get("DQ4ML_CUT_TILE", TILE_BYTES))
         tile = max(4096, min(cap, (160 * 1024) // per_cu - fixed))
         self.RR = int(max(1, min(rows_max, tile // per_row)))
-        self.lds = fixed + 8 * self.RR * self.CU + (8 * self.RR * self.PP if self.blocked else 0)
+        self.lds = fixed + 8 * self.RR * self.CU + (8 * ((self.RR + 3) * self.PP + 16) if self.blocked else 0)
         self.gw = gram_width(d)
+
+
+def _valu_gram(sh, slots):
+    """4 x 4 f64 register blocks of the upper augmented Gram per thread, rows of the tile in
+    row groups (VALU FMAs; any d)."""
+    d, PP, NB, U, RG, GW = sh.d, sh.PP, sh.NB, sh.U, sh.RG, sh.gw
+    acc_decl = "  double acc[16];\n#pragma unroll\n  for (int k = 0; k < 16; ++k) acc[k] = 0.0;\n"
+    acc_decl += f"""  const int gu = tid % {U}, grg = tid / {U};
+  const bool gact = tid < {U * RG};
+  int bi = 0, brem = gu;
+  while (brem >= {NB} - bi) {{ brem -= {NB} - bi; ++bi; }}
+  const int bj = bi + brem;
+"""
+    gram_phase = f"""      if (gact) {{
+    for (int r = grg; r < nr; r += {RG}) {{
+      const double* __restrict__ gr = gt + r * {PP};
+      const f64x2 a01 = *reinterpret_cast<const f64x2*>(gr + 4 * bi), a23 = *reinterpret_cast<const f64x2*>(gr + 4 * bi + 2);
+      const f64x2 b01 = *reinterpret_cast<const f64x2*>(gr + 4 * bj), b23 = *reinterpret_cast<const f64x2*>(gr + 4 * bj + 2);
+      const double av[4] = {{a01[0], a01[1], a23[0], a23[1]}}, bv[4] = {{b01[0], b01[1], b23[0], b23[1]}};
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) acc[4 * u + v] = __builtin_fma(av[u], bv[v], acc[4 * u + v]);
+    }}
+  }}
+"""
+    # every (i <= j) entry of the augmented upper triangle sits in exactly one 4 x 4 block:
+    # each row group writes a complete gram_width slab (no zero fill needed)
+    idx_tab = []
+    for bI in range(NB):
+        for bJ in range(bI, NB):
+            for u in range(4):
+                for v in range(4):
+                    i, j = 4 * bI + u, 4 * bJ + v
+                    k = _gram_index(i, j, d) if i <= j else None
+                    idx_tab.append(-1 if k is None else k)
+    epilogue = f"""  if (gact) {{
+DQG double* __restrict__ gp = (DQG double*)p[{slots['gpart']}] + ((long long)blockIdx.x * {RG} + grg) * {GW};
+#pragma unroll
+for (int k = 0; k < 16; ++k) {{
+  const int slot = DQ_GIDX[gu * 16 + k];
+  if (slot >= 0) gp[slot] = acc[k];
+}}
+  }}
+"""
+    tables = f"__device__ const short DQ_GIDX[{U * 16}] = {{{', '.join(str(x) for x in idx_tab)}}};\n"
+    return acc_decl, gram_phase, epilogue, tables
+
+
+def _mfma_gram(sh, slots):
+    """The augmented Gram of the row tile on the matrix cores: v_mfma_f64_16x16x4_f64 per upper
+    16 x 16 feature tile, 4 rows per k-step.  Lane l holds row (l >> 4) of the k-step and feature
+    16 X + (l & 15) of panel X — one conflict-free ds_read_b64 per panel — for both operands
+    (A = tile rows, B = tile columns), and accumulates D[(l >> 4) + 4 e][l & 15] in f64.  Rows past
+    the tile are zeroed by a select (stale LDS never enters); feature columns past d + 2 read the
+    next row's bytes and only reach discarded (padding) entries.  Waves split into G tile groups x
+    4/G row groups; each row group writes a complete gram_width slab."""
+    d, PP, GW, G, RG = sh.d, sh.PP, sh.gw, sh.G, sh.RG
+    tiles = sh.tiles
+    groups = [tiles[g::G] for g in range(G)]
+    TW = max(len(t) for t in groups)
+    acc_decl = (f"  typedef double f64x4 __attribute__((ext_vector_type(4)));\n"
+                f"  f64x4 gacc[{TW}];\n#pragma unroll\n  for (int t = 0; t < {TW}; ++t) gacc[t] = f64x4{{0.0, 0.0, 0.0, 0.0}};\n"
+                f"  const int gtg = wave % {G}, grg = wave / {G};\n")
+    bodies = []
+    for g, tl in enumerate(groups):
+        panels = sorted({x for t in tl for x in t})
+        reads = "".join(f"          const double pv{x} = rv ? gr[{16 * x}] : 0.0;\n" for x in panels)
+        mf = "".join(f"          gacc[{k}] = __builtin_amdgcn_mfma_f64_16x16x4f64(pv{I}, pv{J}, gacc[{k}], 0, 0, 0);\n"
+                     for k, (I, J) in enumerate(tl))
+        bodies.append(f"""        if (gtg == {g}) {{{{
+          for (int k0 = 4 * grg; k0 < nr; k0 += {4 * RG}) {{{{
+            const int r = k0 + (lane >> 4);
+            const bool rv = r < nr;
+            const double* __restrict__ gr = gt + r * {PP} + (lane & 15);
+{reads}{mf}          }}}}
+        }}}}
+""")
+    gram_phase = "".join(bodies).replace("{{", "{").replace("}}", "}")
+    # (lane, e) -> gram_width slot of each tile (-1: lower half of a diagonal tile or padding)
+    tabs = []
+    for I, J in tiles:
+        for lane in range(64):
+            for e in range(4):
+                i, j = 16 * I + (lane >> 4) + 4 * e, 16 * J + (lane & 15)
+                k = _gram_index(i, j, d) if i <= j else None
+                tabs.append(-1 if k is None else k)
+    tables = f"__device__ const short DQ_TIDX[{len(tiles) * 256}] = {{{', '.join(str(x) for x in tabs)}}};\n"
+    ep = []
+    for g, tl in enumerate(groups):
+        wr = "".join(f"""      for (int e = 0; e < 4; ++e) {{
+        const int slot = DQ_TIDX[{tiles.index(t) * 256} + lane * 4 + e];
+        if (slot >= 0) gp[slot] = gacc[{k}][e];
+      }}
+""" for k, t in enumerate(tl))
+        ep.append(f"    if (gtg == {g}) {{\n{wr}    }}\n")
+    epilogue = (f"  {{\n    DQG double* __restrict__ gp = (DQG double*)p[{slots['gpart']}] + "
+                f"((long long)blockIdx.x * {RG} + grg) * {GW};\n" + "".join(ep) + "  }\n")
+    return acc_decl, gram_phase, epilogue, tables
+
+
+def _conv_loop(NF, C, CU, PP, FW, crlf, conv_call, frame_load, div_expr, int_ok, us_expr, feat_store):
+    """The field-conversion loop: NF fields per lane per iteration (fb + 256 h), their positions
+    prefetched one iteration ahead, every field's frame + sign loads issued before any wait."""
+    cr = 1 if crlf else 0
+    L = ["      // (the next iteration's positions are loaded while this one converts)"]
+    for h in range(NF):
+        L.append(f"      int q{h}_p = 0, q{h}_e = 0;")
+        L.append(f"      if (f0 + tid + {256 * h} < f1) {{ q{h}_p = dposx[f0 + tid + {256 * h}]; "
+                 f"q{h}_e = dposx[f0 + tid + {256 * h} + 1]; }}")
+    L.append(f"      for (int fb = f0 + tid; fb < f1; fb += {256 * NF}) {{")
+    for h in range(NF):
+        L.append(f"        const bool q{h}_act = fb + {256 * h} < f1;")
+        L.append(f"        const int q{h}_f = q{h}_act ? fb + {256 * h} : fb;  // (a spare lane repeats fb)")
+        L.append(f"        const int q{h}_fn = fb + {256 * (NF + h)} < f1 ? fb + {256 * (NF + h)} : fb;")
+        L.append(f"        const int q{h}_pn = dposx[q{h}_fn], q{h}_en = dposx[q{h}_fn + 1];")
+    for h in range(NF):
+        fl_ = (frame_load.replace("fw0", f"q{h}_w0").replace("fw1", f"q{h}_w1").replace("fw2", f"q{h}_w2")
+               .replace("const int c0 =", f"const int q{h}_c0 =").replace("stage[start]", f"stage[q{h}_start]")
+               .replace("fwp", f"q{h}_wp").replace("+ end", f"+ q{h}_end").replace("^ start", f"^ q{h}_start")
+               .replace("+ f;", f"+ q{h}_f;").replace("(f & 1)", f"(q{h}_f & 1)"))
+        L.append(f"        const int q{h}_end = q{h}_e;")
+        L.append(f"        const int q{h}_rw = q{h}_f / {C}, q{h}_c = q{h}_f - q{h}_rw * {C};")
+        L.append(f"        const int q{h}_start = q{h}_p + 1 + ({cr} && q{h}_c == 0 ? 1 : 0);")
+        L.append(f"        q{h}_p = q{h}_pn;")
+        L.append(f"        q{h}_e = q{h}_en;")
+        L.append(f"        const int q{h}_fsh = (q{h}_end - 8) & 3;")
+        L.append(f"        const unsigned* q{h}_wp = reinterpret_cast<const unsigned*>(stage + (q{h}_end - 8 - q{h}_fsh));")
+        L.append("        " + fl_)
+    keep = ", ".join(f'"v"(q{h}_w0), "v"(q{h}_w1), "v"(q{h}_w2), "v"(q{h}_c0)' for h in range(NF))
+    L.append(f"        asm volatile(\"\" ::{keep});  // one wait for every frame (else they sink past the branch)")
+    cc = conv_call.replace(chr(10) + "        ", chr(10) + "          ")
+    fs = feat_store.replace("        const int fs", "            const int fs").replace(
+        "        if (fs >= 0)", "            if (fs >= 0)")
+    for h in range(NF):
+        L.append(f"""        {{
+          const int f = q{h}_f, end = q{h}_end, start = q{h}_start, len = end - start, c = q{h}_c, rw = q{h}_rw;
+          const int fsh = q{h}_fsh;
+          const unsigned fw0 = q{h}_w0, fw1 = q{h}_w1, fw2 = q{h}_w2;
+          const int c0 = q{h}_c0;
+          const bool neg0 = c0 == '-';
+          const int fl = len - ((c0 == '-' || c0 == '+') ? 1 : 0);
+          unsigned m = 0u;
+          int fr = 0;
+          bool neg = neg0, dot = false, ok;
+          {cc}
+          const double v = {div_expr};  // fr = 0 without a dot: 10^0 = 1, exact
+          double dv = neg ? -v : v;
+          ok = ok && {int_ok};
+          if (len > {FW}) {{
+            int ps = start;
+            long long lv = 0;
+            int ty = C_NULL;
+            ok = csv_field_fast(stage, 0, ps, end, O.sep, dv, lv, ty) && ty != C_NULL && csv_conforms(ty, DQ_KIND[c]);
+          }}
+          if (q{h}_act) {{
+            bad |= !ok;
+            const int rr = rw - R0;
+            const int us = {us_expr};
+            if (us >= 0) vt[rr * {CU} + us] = dv;
+{fs}          }}
+          (void)f;
+        }}""")
+    L.append("      }")
+    return "\n".join(L) + "\n"
 
 
 def kernel_source(g, kinds, used, opts: dict, H: int, slots: dict, d: int, term: int = 13, crlf: bool = False,
@@ -183,12 +358,47 @@ def kernel_source(g, kinds, used, opts: dict, H: int, slots: dict, d: int, term:
     # other fields' >= 2 bytes each), else 16 (longer fields take the byte-walking fast path)
     FW = 8 if max_line - 1 - 2 * (C - 1) <= 8 else 16
     # diagnostic ablations (timing only, results are wrong): 1 no field conversion, 2 no Gram
-    # phase, 4 no row phase
+    # phase (the compiler then also drops the feature conversions: nothing reads the tile), 4 no
+    # row phase, 8 nothing after the cut (stage, masks, scans, scatter only)
     abl = int(os.environ.get("DQ4ML_CUT_ABLATE", "0"))
+    # diagnostic phase clocks (DQ4ML_CUT_STAMPS=1): s_memtime after each block barrier, per-phase
+    # sums of wave 0 of every block -> the dbg slot ([grid][8] u64: phases 0-5, windows)
+    stamps = os.environ.get("DQ4ML_CUT_STAMPS", "0") == "1" and "dbg" in slots
+    if stamps:
+        stamp_decl = ("  unsigned long long dq_ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};\n"
+                      "  unsigned long long dq_t = __builtin_amdgcn_s_memtime();\n"
+                      "#define DQ_STAMP(k) do { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); "
+                      "dq_ph[k] += t_ - dq_t; dq_t = t_; } while (0)\n")
+        stamp_out = (f"  if (tid == 0) {{\n    dq_ph[6] = (unsigned long long)(w1 - w0);\n"
+                     f"    unsigned long long* dg = (unsigned long long*)p[{slots.get('dbg', 0)}] + blockIdx.x * 8;\n"
+                     "#pragma unroll\n    for (int k = 0; k < 8; ++k) dg[k] = dq_ph[k];\n  }\n")
+    else:
+        stamp_decl, stamp_out = "#define DQ_STAMP(k) do { } while (0)\n", ""
+    # an int32 column must hold no dot (a double column takes both classes): VALU, no table load
+    ints = [c for c, k in enumerate(kinds) if int(k) == 1]
+    int_ok = "(" + " || ".join(f"c == {c}" for c in ints) + ") ? !dot : true" if 0 < len(ints) <= 8 else (
+        "true" if not ints else "csv_conforms(dot ? C_DOUBLE : C_INT, DQ_KIND[c])")
+    div_expr = ("csv_div_pow10_fma((double)m, csv_pow10(fr), csv_inv_pow10(fr))"
+                if os.environ.get("DQ4ML_CUT_P10", "lds") == "valu" else
+                "csv_div_pow10_fma((double)m, p10t[fr & 15], ip10t[fr & 15])")
+    if abl & 16:  # (diagnostic) no table read: the quotient's LDS round trip
+        div_expr = "csv_div_pow10_fma((double)m, 1.0 + fr, 1.0)"
+    frame_load = ("const unsigned fw0 = fwp[0], fw1 = fwp[1], fw2 = fwp[2];\n        const int c0 = stage[start];"
+                  if not abl & 32 else  # (diagnostic) no frame / sign reads
+                  "const unsigned fw0 = 0x31323334u + end, fw1 = 0x2E353637u ^ start, fw2 = 0x38393031u + f;\n"
+                  "        const int c0 = 0x30 + (f & 1);")
+    # the next window's prefetch: right after this window's bytes are staged ("early"), or after
+    # the field conversion of its first tile round ("late": the 20 prefetch VGPRs are not live
+    # across the converter, and the loads still have the row, Gram and stage phases to land)
+    late = os.environ.get("DQ4ML_CUT_PF", "late") == "late"
+    pf_early = "" if late else "    if (blk + 1 < w1) dq_fetch(ab, a, n, blk + 1, tid, pg, ph);\n"
+    pf_late = "      if (R0 == 0 && blk + 1 < w1) dq_fetch(ab, a, n, blk + 1, tid, pg, ph);\n" if late else ""
+    pf_tail = ("    if ((cnt == 0 || " + ("true" if abl & 8 else "false") + ") && blk + 1 < w1) "
+               "dq_fetch(ab, a, n, blk + 1, tid, pg, ph);  // no tile round ran\n") if late else ""
     conv_call = ("ok = true; m = (unsigned)len;" if abl & 1 else
                  f"""if (__ballot(fl > 8) == 0ull) {{
-          ok = csv_num_r8s(stage, end, fl, m, fr, dot);
-        }} else {{
+          ok = csv_num_r8s_w(fw0, fw1, fw2, fsh, fl, m, fr, dot);
+        }} else {{  // (re-reads its frame: no register array lives across the branch)
           ok = csv_num_r<{FW // 4}>(stage, end, len < {FW} ? len : {FW}, m, fr, neg, dot);
         }}""")
     W, HG, DCAP, RR, CU, PP, NB, U, RG, GW = sh.W, sh.HG, sh.DCAP, sh.RR, sh.CU, sh.PP, sh.NB, sh.U, sh.RG, sh.gw
@@ -196,6 +406,34 @@ def kernel_source(g, kinds, used, opts: dict, H: int, slots: dict, d: int, term:
     sep = ord(opts.get("sep", ","))
     sep4 = f"0x{sep:02X}{sep:02X}{sep:02X}{sep:02X}u"
     term4 = f"0x{term:02X}{term:02X}{term:02X}{term:02X}u"
+    # carried row starts (every window but a run's first) count the head's separators in phase 0
+    # from the head granule registers — one barrier and phase less per window — when the head's
+    # granules all sit in wave 0 (H <= 1024)
+    hf = H <= 1024 and os.environ.get("DQ4ML_CUT_HFAST", "1") != "0"
+    if hf:
+        hraw_code = f"""    unsigned int hraw16 = 0u;  // separators of this lane's head granule (wave 0, lanes < {H // 16})
+    if (tid < {H // 16}) {{
+      const csv_u32x4 v = ph[0];
+#pragma unroll
+      for (int w = 0; w < 4; ++w) hraw16 |= dq_gather4(dq_eq80(v[w], {sep4})) << (4 * w);
+    }}
+"""
+        hscan_code = f"""    const bool hfast = st0 >= 0;  // a carried row start (block-uniform)
+    unsigned int hm16 = 0u;
+    int hinc = 0;
+    if (hfast && wave == 0) {{
+      if (lane < {H // 16}) {{
+        const int lo = st0 - 16 * lane;
+        hm16 = lo >= 16 ? 0u : (lo > 0 ? (hraw16 & (0xFFFFu << lo)) : hraw16);
+      }}
+      int hsum;
+      hinc = dq_wave_prefix<5>(__popc(hm16), hsum) + __popc(hm16);
+      if (lane == 0) shtot = hsum;
+    }}
+"""
+    else:
+        hraw_code = ""
+        hscan_code = "    const bool hfast = false;\n    unsigned int hm16 = 0u;\n    int hinc = 0;\n"
     o = (f"{{(unsigned char){sep}, (unsigned char){int(opts['quote'])}, (unsigned char){int(opts['escape'])}, "
          f"(unsigned char)0, (unsigned char)0, (unsigned char)0, (unsigned char)0, (unsigned char)0, "
          f"{{{', '.join('0' for _ in range(16))}}}}}")
@@ -217,47 +455,12 @@ def kernel_source(g, kinds, used, opts: dict, H: int, slots: dict, d: int, term:
             outs += f"      if (!live) {{\n#pragma unroll\n        for (int i = 0; i < {d}; ++i) gr[i] = 0.0;\n      }}\n"
         outs += f"      gr[{d}] = live ? 1.0 : 0.0;\n      gr[{d + 1}] = live ? (double)({yv}) : 0.0;\n"
         outs += "".join(f"      gr[{i}] = 0.0;\n" for i in range(d + 2, PP))
-        acc_decl = "  double acc[16];\n#pragma unroll\n  for (int k = 0; k < 16; ++k) acc[k] = 0.0;\n"
-        acc_decl += f"""  const int gu = tid % {U}, grg = tid / {U};
-  const bool gact = tid < {U * RG};
-  int bi = 0, brem = gu;
-  while (brem >= {NB} - bi) {{ brem -= {NB} - bi; ++bi; }}
-  const int bj = bi + brem;
-"""
-        gram_phase = f"""      if (gact) {{
-        for (int r = grg; r < nr; r += {RG}) {{
-          const double* __restrict__ gr = gt + r * {PP};
-          const f64x2 a01 = *reinterpret_cast<const f64x2*>(gr + 4 * bi), a23 = *reinterpret_cast<const f64x2*>(gr + 4 * bi + 2);
-          const f64x2 b01 = *reinterpret_cast<const f64x2*>(gr + 4 * bj), b23 = *reinterpret_cast<const f64x2*>(gr + 4 * bj + 2);
-          const double av[4] = {{a01[0], a01[1], a23[0], a23[1]}}, bv[4] = {{b01[0], b01[1], b23[0], b23[1]}};
-#pragma unroll
-          for (int u = 0; u < 4; ++u)
-#pragma unroll
-            for (int v = 0; v < 4; ++v) acc[4 * u + v] = __builtin_fma(av[u], bv[v], acc[4 * u + v]);
-        }}
-      }}
-"""
-        # every (i <= j) entry of the augmented upper triangle sits in exactly one 4 x 4 block:
-        # each row group writes a complete gram_width slab (no zero fill needed)
-        idx_tab = []
-        for bI in range(NB):
-            for bJ in range(bI, NB):
-                for u in range(4):
-                    for v in range(4):
-                        i, j = 4 * bI + u, 4 * bJ + v
-                        k = _gram_index(i, j, d) if i <= j else None
-                        idx_tab.append(-1 if k is None else k)
-        epilogue = f"""  if (gact) {{
-    DQG double* __restrict__ gp = (DQG double*)p[{slots['gpart']}] + ((long long)blockIdx.x * {RG} + grg) * {GW};
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {{
-      const int slot = DQ_GIDX[gu * 16 + k];
-      if (slot >= 0) gp[slot] = acc[k];
-    }}
-  }}
-"""
-        tables = f"__device__ const short DQ_GIDX[{U * 16}] = {{{', '.join(str(x) for x in idx_tab)}}};\n"
-        gt_decl = f"  __shared__ __attribute__((aligned(16))) double gt[{RR * PP}];\n"
+        if sh.mfma:
+            acc_decl, gram_phase, epilogue, tables = _mfma_gram(sh, slots)
+        else:
+            acc_decl, gram_phase, epilogue, tables = _valu_gram(sh, slots)
+        # (+3 rows + 16: the MFMA Gram's k-step and padding-column reads stay inside the array)
+        gt_decl = f"  __shared__ __attribute__((aligned(16))) double gt[{(RR + 3) * PP + 16}];\n"
     else:
         outs = _gram_code(xs, yv).replace("    if (live)", "      if (live)")
         acc_decl = f"  double acc[{GW}];\n#pragma unroll\n  for (int k = 0; k < {GW}; ++k) acc[k] = 0.0;\n"
@@ -291,9 +494,18 @@ def kernel_source(g, kinds, used, opts: dict, H: int, slots: dict, d: int, term:
             fs_expr = "ctab[2 * c + 1]"
         feat_store = (f"        const int fs = {fs_expr};\n"
                       f"        if (fs >= 0) gt[rr * {PP} + fs] = dv;\n")
+    NF = int(os.environ.get("DQ4ML_CUT_NF", "1"))
+    # no barrier at the window top: phase 0 writes only the stage, the cut and the scan words,
+    # which the previous window finished reading before its row-phase barrier, so the previous
+    # window's Gram (reading the row tile, written again only after this window's cut barrier)
+    # overlaps this window's staging
+    top_sync = ("    __syncthreads();  // the previous window's readers are done with every LDS array\n"
+                if os.environ.get("DQ4ML_CUT_TOPSYNC", "0") == "1" else "")
+    conv_loop = _conv_loop(NF, C, CU, PP, FW, crlf, conv_call, frame_load, div_expr, int_ok, us_expr, feat_store)
     kind_tab = ", ".join(str(int(k)) for k in kinds)
     lb = f"__launch_bounds__(256, {waves_per_simd})" if waves_per_simd else "__launch_bounds__(256)"
-    src = "#define CSV_UDOT4(a, b, c) __builtin_amdgcn_udot4((a), (b), (c), false)\n" + header_text() + f"""
+    src = ("#define CSV_UDOT4(a, b, c) __builtin_amdgcn_udot4((a), (b), (c), false)\n"
+           "#define CSV_MUL24(a, b) __umul24((a), (b))\n") + header_text() + f"""
 using namespace dq4ml_csv;
 typedef unsigned int csv_u32x4 __attribute__((ext_vector_type(4)));
 typedef double f64x2 __attribute__((ext_vector_type(2)));
@@ -309,6 +521,21 @@ __device__ const short DQ_CTAB[{2 * C}] = {{{', '.join(str(x) for x in ctab)}}};
 __device__ __forceinline__ unsigned int dq_eq80(unsigned int v, unsigned int pat) {{
   const unsigned int x = v ^ pat;
   return ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x | 0x7F7F7F7Fu);
+}}
+// exclusive prefix sum of c (0 <= c < 2^B) over the wave's 64 lanes, and the wave total, with
+// no cross-lane data movement: c's bit planes are ballots, and mbcnt counts the set lanes below
+// (a __shfl_up scan is six dependent ds_bpermute round trips)
+template <int B>
+__device__ __forceinline__ int dq_wave_prefix(int c, int& total) {{
+  int pre = 0, tot = 0;
+#pragma unroll
+  for (int b = 0; b < B; ++b) {{
+    const unsigned long long bal = __ballot((c >> b) & 1);
+    pre += (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bal, 0u)) << b;
+    tot += __popcll(bal) << b;
+  }}
+  total = tot;
+  return pre;
 }}
 // the four 0x80 flags of z gathered to bits 0..3
 __device__ __forceinline__ unsigned int dq_gather4(unsigned int z) {{
@@ -354,7 +581,7 @@ extern "C" __global__ {lb} void {ENTRY}(void* const* P, long long n) {{
   const DQG unsigned char* ab = b - a;  // 16-byte aligned view
   const CsvOpts O = {o};
   bool bad = false;
-  for (int i = tid; i < {2 * C}; i += 256) ctab[i] = DQ_CTAB[i];
+{stamp_decl}  for (int i = tid; i < {2 * C}; i += 256) ctab[i] = DQ_CTAB[i];
   __shared__ double p10t[16], ip10t[16];  // 10^k and RN(10^-k) for the converter (k > 9: unused)
   if (tid < 16) {{
     p10t[tid] = tid <= 9 ? csv_pow10(tid) : 1.0;
@@ -372,7 +599,7 @@ extern "C" __global__ {lb} void {ENTRY}(void* const* P, long long n) {{
     const long long wbase = blk * {W} - a;  // buffer index of window byte 0
     const long long sbase = wbase - {H};    // buffer index of stage[0]
     const long long tb = wbase + 64 * tid;  // this lane's 64 window bytes
-    __syncthreads();  // the previous window's readers are done with every LDS array
+{top_sync}    DQ_STAMP(5);
     unsigned int dlo = 0u, dhi = 0u;  // delimiter (separator or terminator) bits of the 64 bytes
 #pragma unroll
     for (int j = 0; j < 4; ++j) {{
@@ -391,7 +618,7 @@ extern "C" __global__ {lb} void {ENTRY}(void* const* P, long long n) {{
       if (gq < {H // 16} + 2)
         *reinterpret_cast<csv_u32x4*>(stage + (gq < {H // 16} ? 16 * gq : {H} + {W} + 16 * (gq - {H // 16}))) = ph[i];
     }}
-    if (blk + 1 < w1) dq_fetch(ab, a, n, blk + 1, tid, pg, ph);
+{hraw_code}{pf_early}
     unsigned long long dm = ((unsigned long long)dhi << 32) | dlo;
     {{
       const long long lo = tb < 0 ? -tb : 0, hi = n - tb;
@@ -403,13 +630,10 @@ extern "C" __global__ {lb} void {ENTRY}(void* const* P, long long n) {{
       if (trailing && hi >= 0 && hi < 64) dm |= 1ull << hi;  // the last line's virtual terminator at n
     }}
     const int cd = __popcll(dm);
-    int inc = cd;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {{
-      const int t = __shfl_up(inc, o, 64);
-      if (lane >= o) inc += t;
-    }}
-    if (lane == 63) wtot[wave] = inc;
+    int wsum;
+    const int inc = dq_wave_prefix<7>(cd, wsum) + cd;
+    if (lane == 0) wtot[wave] = wsum;
+{hscan_code}
     if (st0 < 0) __syncthreads();  // (block-uniform) wave 0 reads the other waves' head stores below
     if (st0 < 0 && wave == 0) {{
       // the first window of the run: the terminator before its first row, through the staged head
@@ -429,6 +653,7 @@ extern "C" __global__ {lb} void {ENTRY}(void* const* P, long long n) {{
       if (lane == 0) sst0 = (int)(found < 0 ? -sbase : found + 1 + {1 if crlf else 0} - sbase);
     }}
     __syncthreads();
+    DQ_STAMP(0);
     if (st0 < 0) st0 = sst0;
     if (st0 < 0 || st0 > {H} + 1) {{  // a row longer than the head: the max-line fact is wrong
       bad = true;
@@ -437,9 +662,10 @@ extern "C" __global__ {lb} void {ENTRY}(void* const* P, long long n) {{
     int before = inc - cd;
     for (int w = 0; w < wave; ++w) before += wtot[w];
     const int dwin = (wtot[0] + wtot[1]) + (wtot[2] + wtot[3]);
-    // separators of the first row's head part [st0, H) (no terminator can be there)
+    // separators of the first row's head part [st0, H) (no terminator can be there): for a
+    // carried row start they were counted above from the head granule registers (H <= 1024)
     unsigned long long hm = 0ull;
-    if (tid < {H // 64}) {{
+    if (!hfast && tid < {H // 64}) {{
 #pragma unroll
       for (int j = 0; j < 4; ++j) {{
         const csv_u32x4 v = *reinterpret_cast<const csv_u32x4*>(stage + 64 * tid + 16 * j);
@@ -449,16 +675,16 @@ extern "C" __global__ {lb} void {ENTRY}(void* const* P, long long n) {{
       const int lo = st0 - 64 * tid;
       hm = lo >= 64 ? 0ull : (lo > 0 ? (hm & (~0ull << lo)) : hm);
     }}
-    int hinc = __popcll(hm);
-    if (wave == 0) {{
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {{
-        const int t = __shfl_up(hinc, o, 64);
-        if (lane >= o) hinc += t;
+    if (!hfast) {{  // (block-uniform) the first window of the run
+      hinc = __popcll(hm);
+      if (wave == 0) {{
+        int hsum;
+        hinc += dq_wave_prefix<7>(hinc, hsum);
+        if (lane == 0) shtot = hsum;
       }}
-      if (lane == 63) shtot = hinc;
+      __syncthreads();
     }}
-    __syncthreads();
+    DQ_STAMP(1);
     const int htot = shtot;
     const int ftot = htot + dwin;      // delimiters from the first row's start on
     const int cnt = ftot / {C};        // complete rows (every row holds exactly {C} fields)
@@ -478,6 +704,15 @@ extern "C" __global__ {lb} void {ENTRY}(void* const* P, long long n) {{
         dcut[idx++] = (unsigned short)(64 * tid + bit);
       }}
     }}
+    if (hfast && hm16) {{
+      int idx = hinc - __popc(hm16);
+      unsigned int mm = hm16;
+      while (mm) {{
+        const int bit = __builtin_ctz(mm);
+        mm &= mm - 1;
+        dcut[idx++] = (unsigned short)(16 * tid + bit);
+      }}
+    }}
     {{
       int idx = htot + before;
       unsigned long long mm = dm;
@@ -488,41 +723,18 @@ extern "C" __global__ {lb} void {ENTRY}(void* const* P, long long n) {{
       }}
     }}
     __syncthreads();
+    DQ_STAMP(2);
     // the next window's first row starts after this window's last complete row
     const int nst0 = cnt > 0 ? (int)dcut[cnt * {C} - 1] + 1 + {1 if crlf else 0} - {W} : st0 - {W};
-    for (int R0 = 0; R0 < cnt; R0 += {RR}) {{
+    for (int R0 = 0; R0 < {"0" if abl & 8 else "cnt"}; R0 += {RR}) {{
       const int nr = min({RR}, cnt - R0), f0 = R0 * {C}, f1 = f0 + nr * {C};
       if (R0 > 0) __syncthreads();  // the previous round's Gram readers are done with the tiles
       // one field per lane: the sign byte, then the unsigned part through the 8-byte 64-bit SWAR
       // frame when every field of the wave fits it (wave-uniform branch), else the 16-byte frame;
       // fields longer than that take the byte-walking fast path (rare, divergent)
-      for (int f = f0 + tid; f < f1; f += 256) {{
-        const int end = dposx[f + 1];
-        const int rw = f / {C}, c = f - rw * {C};
-        const int start = dposx[f] + 1 + ({1 if crlf else 0} && c == 0 ? 1 : 0);
-        const int len = end - start;
-        const int c0 = stage[start];
-        const bool neg0 = c0 == '-';
-        const int fl = len - ((c0 == '-' || c0 == '+') ? 1 : 0);
-        unsigned m = 0u;
-        int fr = 0;
-        bool neg = neg0, dot = false, ok;
-        {conv_call}
-        const double v = dot ? csv_div_pow10_fma((double)m, p10t[fr & 15], ip10t[fr & 15]) : (double)m;
-        double dv = neg ? -v : v;
-        ok = ok && csv_conforms(dot ? C_DOUBLE : C_INT, DQ_KIND[c]);
-        if (len > {FW}) {{
-          int ps = start;
-          long long lv = 0;
-          int ty = C_NULL;
-          ok = csv_field_fast(stage, 0, ps, end, O.sep, dv, lv, ty) && ty != C_NULL && csv_conforms(ty, DQ_KIND[c]);
-        }}
-        bad |= !ok;
-        const int rr = rw - R0;
-        const int us = {us_expr};
-        if (us >= 0) vt[rr * {CU} + us] = dv;
-{feat_store}      }}
-      __syncthreads();
+{conv_loop}
+{pf_late}      __syncthreads();
+      DQ_STAMP(3);
       for (int r = tid; r < nr; r += 256) {{  // one row per thread: the DQ chain and the assembler
         const int rb = r * {CU};
 {loads}        const bool line = true;
@@ -530,10 +742,12 @@ extern "C" __global__ {lb} void {ENTRY}(void* const* P, long long n) {{
 {body if not abl & 4 else ""}
 {outs if not abl & 4 else ""}      }}
       __syncthreads();
+      DQ_STAMP(4);
 {gram_phase if not abl & 2 else ""}    }}
-    st0 = nst0;
+{pf_tail}    st0 = nst0;
   }}
   if (bad) dq_flag(vflag, 1u);
+{stamp_out}
 {epilogue}}}
 """
     return src, sh
@@ -555,6 +769,12 @@ def blocks_per_cu(lds: int) -> int:
     return int(max(1, min(4, (160 * 1024) // max(lds, 1))))
 
 
+# Below this mean line length (bytes) the per-line kernel (scanfuse.py) wins for d <= 8: a short
+# row is one lane's few SWAR steps there, while the cutter pays its per-field cut and row-tile
+# round trip (lab CSV, 9.2-byte rows: 1.60 vs 1.75 ms per action, same box).
+MIN_MEAN_LINE = 24
+
+
 def _compile(nodes, rel, d: int):
     from . import dqvm
     from .scanfuse import _GramNullable, _ScanBase, _scan_gen
@@ -563,12 +783,17 @@ def _compile(nodes, rel, d: int):
     H = applicable(f)
     if H is None:
         return None
+    if d <= 8 and float(f.get("mean_line", 0.0)) < float(os.environ.get("DQ4ML_CUT_MIN_LINE", MIN_MEAN_LINE)):
+        return None
     term, crlf = term_of(f)
     min_line = int(f.get("min_line", 1))
     (parts, udfs), refs = dqvm.nodes_key(nodes)
     key = (parts, udfs, tuple(rel.schema().names), tuple(f["kinds"]), repr(sorted(f["opts"].items())), H, d, term,
            crlf, min_line, int(f.get("max_line", 1 << 30)), os.environ.get("DQ4ML_CUT_PER_CU"),
-           os.environ.get("DQ4ML_CUT_TILE"), os.environ.get("DQ4ML_CUT_ABLATE"))
+           os.environ.get("DQ4ML_CUT_TILE"), os.environ.get("DQ4ML_CUT_ABLATE"),
+           os.environ.get("DQ4ML_CUT_STAMPS"), os.environ.get("DQ4ML_CUT_P10"), os.environ.get("DQ4ML_CUT_HFAST"),
+           os.environ.get("DQ4ML_CUT_PF"), os.environ.get("DQ4ML_CUT_NF"),
+           os.environ.get("DQ4ML_CUT_TOPSYNC"))
     if key in _CACHE:
         return _CACHE[key]
     base = _ScanBase(rel.schema(), 0, f["device"])
@@ -576,7 +801,9 @@ def _compile(nodes, rel, d: int):
     cp = None
     try:
         _, g, outputs, _ = dqvm.compile_chain(nodes, base, False, gen=g)
-        slots = {k: g.slot(None, (k,)) for k in ("buf", "nwin", "trailing", "vflag", "gpart")}
+        names = ("buf", "nwin", "trailing", "vflag", "gpart") + (
+            ("dbg",) if os.environ.get("DQ4ML_CUT_STAMPS", "0") == "1" else ())
+        slots = {k: g.slot(None, (k,)) for k in names}
         ml = int(f.get("max_line", 1 << 30))
         _, sh = kernel_source(g, f["kinds"], g.used, f["opts"], H, slots, d, term, crlf, min_line, 0, ml)
         per_cu = blocks_per_cu(sh.lds)
@@ -630,6 +857,8 @@ def try_cut_gram(chain, rel, d: int):
     gw = gram_width(d)
     gpart = torch.empty(grid * cp.rg, gw, dtype=torch.float64, device=dev)
     scalars = {"buf": buf, "nwin": nwin, "trailing": int(f["trailing"]), "vflag": vflag, "gpart": gpart}
+    if any(t[0] == "dbg" for t in cp.recipe):
+        LAST_STAMPS["buf"] = scalars["dbg"] = torch.zeros(grid, 8, dtype=torch.int64, device=dev)
     ptrs = []
     for tag in cp.recipe:
         k = tag[0]

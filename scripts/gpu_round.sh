@@ -128,6 +128,15 @@ for s in $STEPS; do
          step cutnf_lab_${nf}_${pc} 300 env DQ4ML_CUT_NF=$nf DQ4ML_CUT_PER_CU=$pc python benchmarks/bench_csv_pipeline.py --steps 10 --warmup 2 &&
          step cutnf_w32_${nf}_${pc} 300 env DQ4ML_CUT_NF=$nf DQ4ML_CUT_PER_CU=$pc python benchmarks/bench_csv_pipeline.py --features 32 --rows 2e7 --steps 10 --warmup 2 || exit $?
        done; done ;;
+    cutb) (export TMPDIR=/tmp
+       step cutb_lab 300 env VARIANTS="${LABV:-base;DQ4ML_SCAN_CUT=0;DQ4ML_CUT_ABLATE=1;DQ4ML_CUT_ABLATE=4;DQ4ML_CUT_ABLATE=5}" python scripts/cut_bench.py --rows 1e8 &&
+       step cutb_w32 300 env VARIANTS="${W32V:-base;DQ4ML_CUT_ABLATE=1;DQ4ML_CUT_ABLATE=2;DQ4ML_CUT_ABLATE=4;DQ4ML_CUT_ABLATE=7}" python scripts/cut_bench.py --features 32 --rows 2e7) || exit $? ;;
+    cutb64) (export TMPDIR=/tmp
+       step cutb_w64 300 env VARIANTS="${W64V:-base;DQ4ML_CUT_MFMA=0}" python scripts/cut_bench.py --features 64 --rows 1e7) || exit $? ;;
+    cutpmcb) (export TMPDIR=/tmp VARIANTS=base
+       step cutpmcb1 300 timeout -s KILL 240 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS GRBM_GUI_ACTIVE -d gpurun_out/cutpmcb1 -o run --output-format csv -- python scripts/cut_bench.py --features 32 --rows 2e7 --reps 3 &&
+       step cutpmcb2 300 timeout -s KILL 240 rocprofv3 --kernel-trace --pmc SQ_INSTS_SALU SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_VMEM SQ_ACTIVE_INST_MISC GRBM_GUI_ACTIVE -d gpurun_out/cutpmcb2 -o run --output-format csv -- python scripts/cut_bench.py --features 32 --rows 2e7 --reps 3 &&
+       step cutpmcb3 300 timeout -s KILL 240 rocprofv3 --kernel-trace --pmc SQ_INST_CYCLES_VMEM SQ_ACTIVE_INST_SCA SQ_INSTS_SMEM SQ_INST_LEVEL_LDS SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA GRBM_GUI_ACTIVE -d gpurun_out/cutpmcb3 -o run --output-format csv -- python scripts/cut_bench.py --features 32 --rows 2e7 --reps 3) || exit $? ;;
     csv32s) step csv32s 600 python benchmarks/bench_csv_pipeline.py --features 32 --rows 2e7 --steps 10 --warmup 2 ;;
     csv32) step csv32 900 python benchmarks/bench_csv_pipeline.py --features 32 --rows 1e8 --steps 10 --warmup 2 --json-out gpurun_out/csv32.json ;;
     csv64) step csv64 900 python benchmarks/bench_csv_pipeline.py --features 64 --rows ${CSV64_ROWS:-5e7} --steps 10 --warmup 2 --json-out gpurun_out/csv64.json ;;

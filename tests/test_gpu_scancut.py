@@ -26,7 +26,9 @@ def spark():
         s.stop()
     filecache.clear()
     s = SparkSession.builder().master("mi355x[*]").config("dq4ml.csv.deviceThresholdBytes", "0").getOrCreate()
+    os.environ["DQ4ML_CUT_MIN_LINE"] = "0"  # the cutter on short rows too (routing is tested below)
     yield s
+    os.environ.pop("DQ4ML_CUT_MIN_LINE", None)
     s.stop()
 
 
@@ -209,3 +211,22 @@ def test_lab_pipeline_on_csv_has_no_host_sync_and_defers_the_npe(spark, tmp_path
     with pytest.raises(SparkException, match="NullPointerException"):
         m.coefficients
     spark.conf.set("dq4ml.fit.async", "false")
+
+
+def test_short_rows_route_to_the_per_line_kernel(spark, tmp_path, monkeypatch):
+    """Below MIN_MEAN_LINE bytes per line (d <= 8) the per-line fused scan runs, not the cutter."""
+    import bench_csv_pipeline as B
+
+    from net.jgp.labs.sparkdq4ml_amd import LinearRegression
+    from net.jgp.labs.sparkdq4ml_amd.dq.rules import register_lab_rules
+    from net.jgp.labs.sparkdq4ml_amd.models import regression
+    from net.jgp.labs.sparkdq4ml_amd.ops import scancut
+
+    monkeypatch.delenv("DQ4ML_CUT_MIN_LINE")
+    register_lab_rules(spark)
+    p = str(tmp_path / "lab.csv")
+    B.synth_csv(p, 100_000)
+    spark.read().format("csv").option("inferSchema", "true").load(p).count()
+    before = scancut.STATS["cut_grams"]
+    fused = regression._fused_scan_stats(LinearRegression(), _lab_df(spark, p))
+    assert fused is not None and scancut.STATS["cut_grams"] == before

@@ -33,7 +33,7 @@ def test_gram_index_covers_layout_once(d):
             assert f"acc[{scancut._gram_index(i, j, d)}] += gx{i} * gx{j};" in code
 
 
-def _cut_source(spark, d, lab):
+def _cut_source(spark, d, lab, stamps=False):
     import torch
 
     from net.jgp.labs.sparkdq4ml_amd.ops.csvscan import _opt_args
@@ -83,7 +83,7 @@ def _cut_source(spark, d, lab):
     base = scanfuse._ScanBase(rel.schema(), 0, torch.device("cpu"))
     g = scanfuse._scan_gen(base, fused["nullable"])
     _, g, _, _ = dqvm.compile_chain(chain, base, False, gen=g)
-    slots = {k: g.slot(None, (k,)) for k in ("buf", "nwin", "trailing", "vflag", "gpart")}
+    slots = {k: g.slot(None, (k,)) for k in ("buf", "nwin", "trailing", "vflag", "gpart") + (("dbg",) if stamps else ())}
     ml = fused["max_line"]
     src, sh = scancut.kernel_source(g, kinds, g.used, fused["opts"], H, slots, d, 13, False, fused["min_line"],
                                     scancut.blocks_per_cu(scancut.kernel_source(g, kinds, g.used, fused["opts"], H,
@@ -92,12 +92,15 @@ def _cut_source(spark, d, lab):
     return src
 
 
-@pytest.mark.parametrize("d,lab", [(1, True), (12, False)])
-def test_cut_kernel_compiles_for_gfx950(cpu_session, tmp_path, d, lab):
-    src = _cut_source(cpu_session, d, lab)
+@pytest.mark.parametrize("d,lab,stamps", [(1, True, False), (12, False, False), (40, False, True)])
+def test_cut_kernel_compiles_for_gfx950(cpu_session, tmp_path, monkeypatch, d, lab, stamps):
+    if stamps:  # the diagnostic phase-clock build
+        monkeypatch.setenv("DQ4ML_CUT_STAMPS", "1")
+    src = _cut_source(cpu_session, d, lab, stamps)
+    assert ("s_memtime" in src) == stamps
     assert f"void {scancut.ENTRY}(" in src
     assert "for (int r = tid; r < nr; r += 256)" in src  # a row tile larger than the block is covered
-    assert ("DQ_GIDX" in src) == (d > 8)
+    assert ("DQ_TIDX" in src) == (d > 8)  # the MFMA Gram of the row tile
     assert ("csv_num_r<2>(stage, end" in src) == lab  # 8-byte converter frame for the lab's short fields
     hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
     if not os.path.exists(hipcc):
