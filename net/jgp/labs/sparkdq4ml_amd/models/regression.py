@@ -141,23 +141,30 @@ def _check_features_label(params, df: DataFrame):
 
 
 def _fused_scan_stats(params, df: DataFrame):
-    """The fit's f64 statistics computed inside the CSV scan kernel itself (``scanfuse.try_fused_gram``:
-    scan + DQ chain + VectorAssembler + Gram, no row ever stored) when the DataFrame is that shape
-    and the fit is the default-precision, unweighted normal-equation one; else None."""
+    """The fit's statistics computed inside ONE pass over the source with the DQ chain fused in:
+    the CSV scan kernel itself for f64 statistics (``scanfuse.try_fused_gram`` / the cutter:
+    scan + DQ chain + VectorAssembler + Gram, no row ever stored), or the stream Gram with the
+    chain in its stage prologue for bf16 / f32 statistics over in-memory columns
+    (``streamfuse.try_fused_stream``), when the DataFrame is that shape and the fit is an
+    unweighted normal-equation one; else None."""
     if params.getOrDefault("loss") != "squaredError" or params.getOrDefault("solver") not in ("auto", "normal"):
         return None
     if params.isSet("weightCol") and params.getOrDefault("weightCol"):
         return None
-    if _gram_dtype(params, df) != "fp64":
-        return None
+    gd = _gram_dtype(params, df)
     sess = getattr(df, "sparkSession", None)
     if sess is None or getattr(sess, "device", None) is None or sess.device.type != "cuda":
         return None
     fc, lc = _check_features_label(params, df)
-    from ..ops import scanfuse
+    from ..ops import scanfuse, streamfuse
     from ..sql.plan import prune_columns
 
-    return scanfuse.try_fused_gram(prune_columns(df._plan, {fc, lc}), fc, lc, sess)
+    plan = prune_columns(df._plan, {fc, lc})
+    if gd == "fp64":
+        return scanfuse.try_fused_gram(plan, fc, lc, sess)
+    # bf16 / exact-f32 statistics over in-memory columns: the DQ chain in the stream Gram's
+    # stage prologue, one HBM pass (ops/streamfuse.py)
+    return streamfuse.try_fused_stream(plan, fc, lc, sess, gd)
 
 
 def _features_label(params, df: DataFrame):

@@ -1,10 +1,12 @@
 // Shared helpers for the dq4ml gfx950 kernels.
 #pragma once
+#ifndef __HIPCC_RTC__  // (hipRTC builds of the kernels take only the device parts below)
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
 #include <stdexcept>
 #include <string>
+#endif
 
 namespace dq4ml {
 
@@ -17,6 +19,7 @@ typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
 
 constexpr int kWave = 64;  // CDNA wavefront
 
+#ifndef __HIPCC_RTC__
 #define DQ_HIP_CHECK(expr)                                                                          \
   do {                                                                                              \
     hipError_t _e = (expr);                                                                         \
@@ -25,6 +28,7 @@ constexpr int kWave = 64;  // CDNA wavefront
   } while (0)
 
 inline hipStream_t as_stream(uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }
+#endif
 
 // dtype codes shared with the python side (ops/device.py)
 enum DType : int { DT_F64 = 0, DT_F32 = 1, DT_BF16 = 2, DT_I32 = 3, DT_I64 = 4, DT_U8 = 5, DT_F16 = 6, DT_FP8 = 7 };

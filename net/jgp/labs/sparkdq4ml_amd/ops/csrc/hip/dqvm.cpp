@@ -70,6 +70,12 @@ int64_t rtc_compile(const std::string& src, const std::string& entry, std::strin
   return h;
 }
 
+void* rtc_function(int64_t handle) {
+  std::lock_guard<std::mutex> g(g_mu);
+  if (handle < 0 || handle >= (int64_t)g_mods.size()) throw std::invalid_argument("rtc_function: bad handle");
+  return reinterpret_cast<void*>(g_mods[handle].fn);
+}
+
 void rtc_launch(int64_t handle, int grid, int block, void* const* ptrs_dev, int64_t n, hipStream_t st) {
   hipFunction_t fn;
   {

@@ -11,6 +11,8 @@ namespace dq4ml {
 // (void* const* ptrs, long long n)) for gfx950 with hipRTC; returns an opaque handle.  Compiled
 // code objects are cached by source text for the life of the process.
 int64_t rtc_compile(const std::string& src, const std::string& entry, std::string* log);
+// the module function of a compiled handle (launched by a typed host wrapper, e.g. gram_stream_rtc)
+void* rtc_function(int64_t handle);
 void rtc_launch(int64_t handle, int grid, int block, void* const* ptrs_dev, int64_t n, hipStream_t st);
 
 }  // namespace dq4ml

@@ -1,8 +1,10 @@
 // K5 Gram / WLS-statistics kernels (see gram.hip).
 #pragma once
+#ifndef __HIPCC_RTC__
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#endif
 
 namespace dq4ml {
 
@@ -37,8 +39,13 @@ struct GramArgs {
   // deterministic).  Every wave sweeps the whole row range in step with the others: measured ~1 % faster
   // at 1e8 rows and ~2.5 % at the 1.25e7-row 8-GPU shard (the waves' drain is more even)
   int interleave;
+  // stream kernels compiled with a DQ row predicate (ops/streamfuse.py, hipRTC): per-lane DMA
+  // sources of the stage's row-scalar area — [64 lanes][(base, bytes per row) x 2 instructions]
+  // int64 pairs, then the region pointers the guarded tail stage copies from
+  const int64_t* rawtab;
 };
 
+#ifndef __HIPCC_RTC__
 // MFMA-fragment-ordered bf16 feature storage ("tiled"): for superstep s (64 rows), 32-feature
 // tile t, k-step i: 64 lanes x 16 B contiguous, lane l = 32h + f holding rows s*64+32h+8i..+8 of
 // feature 32t+f.  One wave load instruction = 1 KiB contiguous; zero padded to whole supersteps.
@@ -76,5 +83,11 @@ struct PackSrcG {
 int gram_cols_blocks(int d, int64_t n);
 // sdt: the common source dtype (DT_F32 / DT_F64 / DT_BF16, 16-byte aligned columns) or -1 (mixed)
 void gram_cols(GramArgs a, const PackSrcG* srcs_dev, int sdt, int blocks, double* out, hipStream_t st);
+
+// a stream kernel compiled by hipRTC with a DQ row predicate (ops/streamfuse.py): the same
+// argument setup as gram_stream (mode GRAM_F32 / GRAM_BF16, binary row mask), launched through
+// the module function ``fn`` with ``lds`` bytes of dynamic LDS
+void gram_stream_rtc(void* fn, int mode, GramArgs a, int blocks, size_t lds, double* out, hipStream_t st);
+#endif
 
 }  // namespace dq4ml

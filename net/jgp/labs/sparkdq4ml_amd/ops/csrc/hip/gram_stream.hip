@@ -23,12 +23,14 @@
 //
 // Stage = RS rows (64; 32 for f64 storage at d > 32 to keep four waves per CU).  Per-wave LDS:
 // 2 x (NT tiles of TF features x RS rows + 1.25 KiB row scalars) + the (w, wy) stripe.
+#ifndef __HIPCC_RTC__  // (ops/streamfuse.py compiles the device part below with hipRTC too)
 #include <hip/hip_runtime.h>
 
 #include <cstdlib>
 
 #include "common.h"
 #include "gram.h"
+#endif
 
 namespace dq4ml {
 
@@ -119,8 +121,21 @@ __device__ __forceinline__ int swz(int f) {
 template <typename TX, int TF, int NT, int RS, int RING>
 struct SrcBases {
   const TX* p[NT][SGeom<TX, TF, NT, RS, RING>::kPieces];
+#ifdef DQ4ML_ROW_PRED
+  // the row-scalar area's two DMA instructions: per-lane source base and bytes per row (the DQ
+  // predicate's input columns, laid out by ops/streamfuse.py)
+  const unsigned char* rb1;
+  const unsigned char* rb2;
+  int64_t rs1, rs2;
+#endif
   __device__ __forceinline__ void init(const GramArgs& a, int lane) {
     typedef SGeom<TX, TF, NT, RS, RING> G;
+#ifdef DQ4ML_ROW_PRED
+    rb1 = reinterpret_cast<const unsigned char*>(a.rawtab[lane * 4 + 0]);
+    rs1 = a.rawtab[lane * 4 + 1];
+    rb2 = reinterpret_cast<const unsigned char*>(a.rawtab[lane * 4 + 2]);
+    rs2 = a.rawtab[lane * 4 + 3];
+#endif
 #pragma unroll
     for (int t = 0; t < NT; ++t)
 #pragma unroll
@@ -148,6 +163,11 @@ __device__ __forceinline__ void issue_stage(const GramArgs& a, const SrcBases<TX
   for (int t = 0; t < NT; ++t)
 #pragma unroll
     for (int k = 0; k < G::kPieces; ++k) glds16(sb.p[t][k] + r0, st + t * G::kTileBytes + k * 1024);
+#ifdef DQ4ML_ROW_PRED
+  glds16(sb.rb1 + r0 * sb.rs1, st + G::kStageX);
+  glds4(sb.rb2 + r0 * sb.rs2, st + G::kStageX + 1024);
+  return;
+#endif
   const int ysz = a.ydt == DT_F64 ? 8 : 4;
   const unsigned char* yb = reinterpret_cast<const unsigned char*>(a.y) + r0 * ysz;
   const void* src;
@@ -193,6 +213,10 @@ __device__ __forceinline__ void fill_stage_guarded(const GramArgs& a, const SrcB
       *reinterpret_cast<vec*>(st + t * G::kTileBytes + k * 1024 + lane * 16) = v;
     }
   unsigned char* raw = st + G::kStageX;
+#ifdef DQ4ML_ROW_PRED
+  dq_fill_raw(a, raw, lane, r0);  // the predicate's columns, rows >= n zero
+  return;
+#endif
   if (lane < RS) {
     const int64_t r = r0 + lane;
     const bool in = r < a.n;
@@ -211,6 +235,19 @@ __device__ __forceinline__ void fill_stage_guarded(const GramArgs& a, const SrcB
 // (a selection exists, or this is a guarded tail stage whose bytes mark the rows < n).
 __device__ __forceinline__ void stage_rows(const GramArgs& a, const unsigned char* raw, int lane, int rows_valid,
                                            bool sel_any, RowAcc& ra, double& w_eff, double& wy_eff) {
+#ifdef DQ4ML_ROW_PRED
+  {  // the DQ chain on the row's staged columns gives liveness and the label (unit weights)
+    double yv = 0.0;
+    const bool keep = dq_row_pred(raw, lane, yv);
+    const bool lv = lane < rows_valid && keep;
+    RowVals rv{lv, lv ? 1.0 : 0.0, lv ? yv : 0.0, lv ? yv : 0.0};
+    ra.add(rv);
+    w_eff = rv.w;
+    wy_eff = rv.wy;
+    (void)sel_any;
+    return;
+  }
+#endif
   bool live = lane < rows_valid;
   if (sel_any) live = live && raw[1024 + lane] != 0;
   const double y = a.ydt == DT_F64 ? reinterpret_cast<const double*>(raw)[lane]
@@ -411,7 +448,7 @@ __global__ __launch_bounds__(kSB) void gram_stream_f64_kernel(GramArgs a) {
 // from the unrounded features in both.
 // =============================================================================================
 template <int NT, int RING, int CMP, int XM, int RS = 64>
-__global__ __launch_bounds__(kSB) void gram_stream_f32_kernel(GramArgs a) {
+__device__ __forceinline__ void gram_stream_f32_body(const GramArgs& a) {
   static_assert(RS == 64 || RS == 32, "f32 stream kernel: 64- or 32-row stages");
   typedef SGeom<float, 32, NT, RS, RING> G;
   constexpr int HC = G::kCPF / 2;  // chunks per half stage: lane h reads rows [h * RS / 2, (h + 1) * RS / 2)
@@ -568,7 +605,13 @@ __global__ __launch_bounds__(kSB) void gram_stream_f32_kernel(GramArgs a) {
   for (int i = threadIdx.x; i < P; i += kSB) out[i] = red[i];
 }
 
+template <int NT, int RING, int CMP, int XM, int RS = 64>
+__global__ __launch_bounds__(kSB) void gram_stream_f32_kernel(GramArgs a) {
+  gram_stream_f32_body<NT, RING, CMP, XM, RS>(a);
+}
+
 // ---- dispatch --------------------------------------------------------------------------------
+#ifndef __HIPCC_RTC__
 constexpr int kLdsMax = 160 * 1024;
 
 // DQ4ML_GRAM_STREAM_RING=2|3 (A/B): ring depth where a 3-deep ring still fits four waves per CU
@@ -740,4 +783,26 @@ void gram_stream(int mode, GramArgs a, int xmode, int blocks, double* out, hipSt
   if (reduce) gram_reduce(mode, a.partials, blocks, a.d, out, st);
 }
 
+void gram_stream_rtc(void* fn, int mode, GramArgs a, int blocks, size_t lds, double* out, hipStream_t st) {
+  if (mode != GRAM_F32 && mode != GRAM_BF16) throw std::invalid_argument("gram_stream_rtc: f32 / bf16 modes");
+  if (a.xdt != DT_F32 || a.srcs == nullptr || a.rawtab == nullptr || a.d < 1 || a.d > 64 || a.n < 1)
+    throw std::invalid_argument("gram_stream_rtc: f32 source columns and a row-scalar table");
+  if (blocks < 1 || lds > (size_t)kLdsMax) throw std::invalid_argument("gram_stream_rtc: blocks / lds");
+  const int64_t nstage = a.n / 64;
+  const int64_t total_waves = (int64_t)blocks * kSW;
+  a.spw = (nstage + total_waves - 1) / total_waves;
+  if (a.spw < 1) a.spw = 1;
+  a.nsuper = nstage;
+  a.interleave = 0;
+  a.P = (int)gram_partial_stride(mode, a.d);
+  void* args[] = {&a};
+  DQ_HIP_CHECK(hipModuleLaunchKernel(reinterpret_cast<hipFunction_t>(fn), blocks, 1, 1, kSB, 1, 1, (unsigned)lds, st,
+                                     args, nullptr));
+  gram_reduce(mode, a.partials, blocks, a.d, out, st);
+}
+
 }  // namespace dq4ml
+#else
+}  // namespace
+}  // namespace dq4ml
+#endif

@@ -81,6 +81,19 @@ PYBIND11_MODULE(_dq4ml_hip, m) {
           gram_stream(mode, a, (w || sel) ? 1 : 0, blocks, P<double>(out), as_stream(stream), true);
         });
   m.def("gram_stream_blocks", &gram_stream_blocks);
+  m.def("gram_stream_rtc",
+        [](int64_t handle, int mode, uintptr_t srcs, int d, int64_t n, uintptr_t rawtab, uintptr_t partials, int blocks,
+           int64_t lds, uintptr_t out, uintptr_t stream) {
+          GramArgs a{};
+          a.srcs = P<const int64_t>(srcs);
+          a.d = d;
+          a.n = n;
+          a.xdt = DT_F32;
+          a.ydt = DT_F64;
+          a.rawtab = P<const int64_t>(rawtab);
+          a.partials = P<double>(partials);
+          gram_stream_rtc(rtc_function(handle), mode, a, blocks, (size_t)lds, P<double>(out), as_stream(stream));
+        });
   m.def("gram_skinny_cols",
         [](const std::vector<uintptr_t>& cols, const std::vector<int>& dts, int64_t n, uintptr_t y, int ydt,
            uintptr_t w, int wdt, uintptr_t sel, uintptr_t partials, int blocks, uintptr_t out, uintptr_t stream) {
