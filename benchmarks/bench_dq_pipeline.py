@@ -65,7 +65,8 @@ def main(argv=None):
 
     from net.jgp.labs.sparkdq4ml_amd import LinearRegression, SparkSession, VectorAssembler, callUDF, col
     from net.jgp.labs.sparkdq4ml_amd.dq.rules import NotNullRule, RangeRule
-    from net.jgp.labs.sparkdq4ml_amd.ops import dqvm
+    import harness
+    from net.jgp.labs.sparkdq4ml_amd.ops import dqvm, streamfuse
     from net.jgp.labs.sparkdq4ml_amd.parallel import comm
     from net.jgp.labs.sparkdq4ml_amd.sql.types import DataTypes
 
@@ -106,7 +107,8 @@ def main(argv=None):
           "config": {"model": f"DQ(range+notNull UDF filters) -> VectorAssembler -> LinearRegression d={d}",
                      "global_batch": total, "seq_len": d, "parallelism": f"dp{world}", "rows_per_gpu": n,
                      "rows_kept_global": int(kept), "coef_max_abs_err": err,
-                     "dq_vm": dict(dqvm.STATS),
+                     "dq_vm": dict(dqvm.STATS), "stream_dq_grams": dict(streamfuse.STATS),
+                     "host_issue_ms_per_step": harness.LAST_ISSUE_S / a.steps * 1e3,
                      "fit_mode": "async" if (a.use_async and dev.type == "cuda") else "sync"}, **info}, a.json_out)
     comm.shutdown()
     return 0

@@ -38,6 +38,7 @@ _HERE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "csrc", "hip")
 _text: Optional[str] = None
 _CACHE: dict = {}
 _TABS: dict = {}
+_CUS: dict = {}
 
 # the stage's row-scalar area: a 16-B-per-lane DMA instruction (1024 B) and a 4-B one (256 B)
 RAW16, RAW4 = 1024, 256
@@ -299,7 +300,9 @@ def try_fused_stream(plan, features_col: str, label_col: str, session, gram_dtyp
     handle, _log = h.rtc_compile(cp.src, ENTRY)
     P = int(h.gram_partial_stride(cp.mode, d))
     lds = max(4 * _wave_bytes(cp.NT, cp.RING), 8 * P)
-    cus = int(h.device_info()["multiProcessorCount"])
+    cus = _CUS.get(dev.index)
+    if cus is None:  # (device properties: a slow query, once per device)
+        cus = _CUS[dev.index] = int(h.device_info()["multiProcessorCount"])
     nstage = n // 64
     blocks = int(max(1, min(cus * max(1, (160 * 1024) // lds), (nstage + 15) // 16)))
     partials = torch.empty(blocks * P, dtype=torch.float64, device=dev)

@@ -30,7 +30,11 @@ for s in $STEPS; do
     widepmc) (export TMPDIR=/tmp N=${N:-1e6} D=4096 EB=${EB:-8} REPS=${REPS:-2} VARIANTS="${VARIANTS:-4:morton:4}"
        step widepmc1 600 rocprofv3 --kernel-trace --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE -d gpurun_out/widepmc1 -o run --output-format csv -- python scripts/wide_bench.py &&
        step widepmc2 600 rocprofv3 --kernel-trace --pmc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum -d gpurun_out/widepmc2 -o run --output-format csv -- python scripts/wide_bench.py) || exit $? ;;
-    cfg4) step cfg4 900 python benchmarks/bench_dq_pipeline.py --steps 5 --warmup 2 --json-out gpurun_out/cfg4.json ;;
+    cfg4) step cfg4 900 python benchmarks/bench_dq_pipeline.py --steps ${CFG4_STEPS:-5} --warmup 2 --json-out gpurun_out/cfg4.json ;;
+    cfg4prof) step cfg4prof 900 env DQ4ML_BENCH_CPROFILE=gpurun_out/cfg4.prof python benchmarks/bench_dq_pipeline.py --steps 10 --warmup 2 ;;
+    cfg4two) step cfg4two 900 env DQ4ML_STREAM_DQ=0 python benchmarks/bench_dq_pipeline.py --steps 5 --warmup 2 --json-out gpurun_out/cfg4two.json ;;
+    kprof4sf) (export TMPDIR=/tmp; step kprof4sf 600 rocprofv3 --kernel-trace --stats -d gpurun_out/kprof4sf -o run --output-format csv -- python benchmarks/bench_dq_pipeline.py --steps 3 --warmup 1) || exit $? ;;
+    sf) step sf 600 python -u -m pytest tests/test_gpu_streamfuse.py -m gpu -v --maxfail=3 --timeout 120 --timeout-method thread ;;
     cfg4rs64) step cfg4rs64 900 env DQ4ML_GRAM_STREAM_F32RS=64 python benchmarks/bench_dq_pipeline.py --steps 5 --warmup 2 ;;
     cfg4ring3) step cfg4ring3 900 env DQ4ML_GRAM_STREAM_RING=3 python benchmarks/bench_dq_pipeline.py --steps 5 --warmup 2 ;;
     cfg4nodqs) step cfg4nodqs 900 env DQ4ML_DQ_STREAM=0 python benchmarks/bench_dq_pipeline.py --steps 5 --warmup 2 ;;
