@@ -32,8 +32,9 @@ def _args(argv=None):
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--rows", type=float, default=1e8, help="global rows (strong scaling)")
     ap.add_argument("--features", type=int, default=32)
-    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32", "fp64"],
-                    help="compute precision of the Gram statistics (gramDtype)")
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32", "fp32split", "fp64"],
+                    help="compute precision of the Gram statistics (gramDtype; fp32split: f32 statistics "
+                         "from split-bf16 products on f32 storage)")
     ap.add_argument("--storage", default=None, choices=["bf16", "fp32", "fp64", "f32cols"],
                     help="feature storage: an assembled [d, n] matrix of that dtype (default: the "
                          "--dtype; bf16 is ingested into the MFMA-fragment tiled layout), or "
@@ -96,7 +97,7 @@ def main(argv=None):
     n = per_rank if (a.scaling == "weak" or rank < world - 1) else total - lo
     d = a.features
     gen = torch.Generator(device=dev).manual_seed(1234 + rank)
-    storage = a.storage or a.dtype
+    storage = a.storage or ("fp32" if a.dtype == "fp32split" else a.dtype)
     store = {"bf16": torch.bfloat16, "fp32": torch.float32, "fp64": torch.float64,
              "f32cols": torch.float32}[storage]
     ld = (n + 63) // 64 * 64

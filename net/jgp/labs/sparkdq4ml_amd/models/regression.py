@@ -64,7 +64,7 @@ def _jarr(a):
     return np.asarray(a, dtype=np.float64).view(_JavaArray)
 
 
-_GRAM_DTYPES = ("fp64", "fp32", "bf16", "fp8")
+_GRAM_DTYPES = ("fp64", "fp32", "fp32split", "bf16", "fp8")
 
 
 class _LRParams(Params):
@@ -90,7 +90,9 @@ class _LRParams(Params):
         "epsilon": Param("epsilon", "The shape parameter to control the amount of robustness. Must be > 1.0.", 1.35,
                          lambda v: v > 1.0, converter=float),
         "gramDtype": Param("gramDtype", "device compute precision of the normal-equation Gram pass "
-                                        "(fp64 | fp32 | bf16 | fp8)", "fp64", lambda v: v in _GRAM_DTYPES),
+                                        "(fp64 | fp32 | fp32split | bf16 | fp8; fp32split: f32 statistics "
+                                        "from split-bf16 products, exact-f32-class error at the bf16 MFMA "
+                                        "rate)", "fp64", lambda v: v in _GRAM_DTYPES),
     }
 
 

@@ -16,6 +16,8 @@ typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(4))) double f64x4;
 typedef __attribute__((ext_vector_type(2))) double f64x2;
 typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
+typedef __attribute__((ext_vector_type(2))) unsigned int u32x2;
+typedef __attribute__((ext_vector_type(2))) float f32x2;
 
 constexpr int kWave = 64;  // CDNA wavefront
 

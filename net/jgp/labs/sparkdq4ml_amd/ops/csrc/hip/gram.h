@@ -8,7 +8,10 @@
 
 namespace dq4ml {
 
-enum GramMode : int { GRAM_F64 = 0, GRAM_F32 = 1, GRAM_BF16 = 2, GRAM_FP8 = 3 };
+// GRAM_F32S: f32 statistics from split-bf16 products (each f32 = hi + mid + lo bf16, the six
+// leading cross products on the bf16 MFMA; f32 accumulation) — exact-f32-class error at the bf16
+// MFMA rate (gram_stream.hip)
+enum GramMode : int { GRAM_F64 = 0, GRAM_F32 = 1, GRAM_BF16 = 2, GRAM_FP8 = 3, GRAM_F32S = 4 };
 
 struct GramArgs {
   const void* X;       // feature-major [d, ld]

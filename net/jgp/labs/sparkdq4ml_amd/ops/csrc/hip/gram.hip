@@ -1240,7 +1240,7 @@ static bool use_stream() {
 }
 
 int gram_plan_blocks(int mode, int d, int64_t n, int xdt, int xmode) {
-  if (mode == GRAM_F32 || (use_stream() && ((mode == GRAM_F64 && !use_skinny(mode, d, xdt, 0) &&
+  if (mode == GRAM_F32 || mode == GRAM_F32S || (use_stream() && ((mode == GRAM_F64 && !use_skinny(mode, d, xdt, 0) &&
                                               (xdt == DT_F64 || xdt == DT_F32)) ||
                                              (mode == GRAM_BF16 && xdt == DT_F32))))
     return gram_stream_blocks(mode, d, n, xdt);
@@ -1301,11 +1301,12 @@ void gram_tall(int mode, GramArgs a, int xmode, int blocks, double* out, hipStre
     with_skinny_cols(a, [&](auto kern) { hipLaunchKernelGGL(kern, dim3(blocks), dim3(kBlock), 0, st, a); });
   } else if (use_skinny(mode, a.d, a.xdt, a.tiled)) {
     with_skinny(a.xdt, a.d, [&](auto kern) { hipLaunchKernelGGL(kern, dim3(blocks), dim3(kBlock), 0, st, a); });
-  } else if ((mode == GRAM_F32 || (use_stream() && (mode == GRAM_F64 || (mode == GRAM_BF16 && a.xdt == DT_F32)))) &&
+  } else if ((mode == GRAM_F32 || mode == GRAM_F32S ||
+              (use_stream() && (mode == GRAM_F64 || (mode == GRAM_BF16 && a.xdt == DT_F32)))) &&
              gram_stream_ok(mode, a)) {
     gram_stream(mode, a, xmode, blocks, out, st, reduce);
     return;
-  } else if (mode == GRAM_F32) {
+  } else if (mode == GRAM_F32 || mode == GRAM_F32S) {
     throw std::invalid_argument("gram_tall(f32): needs 16-byte aligned f32 features and f32/f64 labels");
   } else {
     with_kernel(mode, a.xdt, a.d, xmode, a.tiled != 0,

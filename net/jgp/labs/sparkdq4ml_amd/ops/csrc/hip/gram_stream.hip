@@ -513,13 +513,28 @@ __device__ __forceinline__ void gram_stream_f32_body(const GramArgs& a) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) w8[4 * u + j] = w4[j], wy8[4 * u + j] = wy4[j];
       }
-#pragma unroll
-      for (int j = 0; j < RPS; ++j)
+      if constexpr (CMP == 2) {  // even / odd rows in the two halves of packed FMAs
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
-          c32[t] = __builtin_fmaf(x[t][j], w8[j], c32[t]);
-          a32[t] = __builtin_fmaf(x[t][j], wy8[j], a32[t]);
+          f32x2 c2 = {c32[t], 0.0f}, a2 = {a32[t], 0.0f};
+#pragma unroll
+          for (int j = 0; j < RPS; j += 2) {
+            const f32x2 xv = {x[t][j], x[t][j + 1]};
+            c2 = __builtin_elementwise_fma(xv, f32x2{w8[j], w8[j + 1]}, c2);
+            a2 = __builtin_elementwise_fma(xv, f32x2{wy8[j], wy8[j + 1]}, a2);
+          }
+          c32[t] = c2.x + c2.y;
+          a32[t] = a2.x + a2.y;
         }
+      } else {
+#pragma unroll
+        for (int j = 0; j < RPS; ++j)
+#pragma unroll
+          for (int t = 0; t < NT; ++t) {
+            c32[t] = __builtin_fmaf(x[t][j], w8[j], c32[t]);
+            a32[t] = __builtin_fmaf(x[t][j], wy8[j], a32[t]);
+          }
+      }
       if constexpr (CMP == 0) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -532,7 +547,7 @@ __device__ __forceinline__ void gram_stream_f32_body(const GramArgs& a) {
               acc[pp] = __builtin_amdgcn_mfma_f32_32x32x2f32(x[I][j], b, acc[pp], 0, 0, 0);
             }
         }
-      } else {
+      } else if constexpr (CMP == 1) {
         bf16x8 fa[NT], fb[NT];
 #pragma unroll
         for (int t = 0; t < NT; ++t)
@@ -546,6 +561,57 @@ __device__ __forceinline__ void gram_stream_f32_body(const GramArgs& a) {
         for (int I = 0; I < NT; ++I)
 #pragma unroll
           for (int J = I; J < NT; ++J, ++pp) acc[pp] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[I], fb[J], acc[pp], 0, 0, 0);
+      } else {
+        // CMP 2 (GRAM_F32S): x = hi + mid + lo exactly, by truncation: hi = the top 16 bits of
+        // x (sign, exponent, 7 mantissa bits), mid = the top 16 bits of r = x - hi (<= 16
+        // significant bits, exact), lo = r - mid (<= 8 significant bits: its top 16 bits ARE it).
+        // x·z ~ hi·hi' + hi·mid' + mid·hi' + mid·mid' + hi·lo' + lo·hi' (the dropped terms are
+        // below 2^-24 relative), every bf16 product exact in the f32 accumulator — exact-f32-class
+        // error on six bf16 MFMAs per pair and k-step.  VALU: two masks and one packed subtract
+        // per residual and element pair, one byte permute per packed bf16 pair (no conversions)
+        bf16x8 ah[NT], am[NT], al[NT], bh[NT], bm[NT], bl[NT];
+        auto split = [&](const float (&v)[8], bf16x8& h8, bf16x8& m8, bf16x8& l8) {
+          u32x4 hw, mw, lw;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const f32x2 xv = {v[2 * q], v[2 * q + 1]};
+            const u32x2 xu = __builtin_bit_cast(u32x2, xv);
+            const f32x2 r = xv - __builtin_bit_cast(f32x2, xu & 0xFFFF0000u);
+            const u32x2 ru = __builtin_bit_cast(u32x2, r);
+            const u32x2 lu = __builtin_bit_cast(u32x2, r - __builtin_bit_cast(f32x2, ru & 0xFFFF0000u));
+            hw[q] = __builtin_amdgcn_perm(xu.y, xu.x, 0x07060302u);
+            mw[q] = __builtin_amdgcn_perm(ru.y, ru.x, 0x07060302u);
+            lw[q] = __builtin_amdgcn_perm(lu.y, lu.x, 0x07060302u);
+          }
+          h8 = __builtin_bit_cast(bf16x8, hw);
+          m8 = __builtin_bit_cast(bf16x8, mw);
+          l8 = __builtin_bit_cast(bf16x8, lw);
+        };
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+          split(x[t], ah[t], am[t], al[t]);
+          if constexpr (XM) {
+            float xb[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) xb[j] = x[t][j] * w8[j];
+            split(xb, bh[t], bm[t], bl[t]);
+          } else {
+            bh[t] = ah[t], bm[t] = am[t], bl[t] = al[t];
+          }
+        }
+        int pp = 0;
+#pragma unroll
+        for (int I = 0; I < NT; ++I)
+#pragma unroll
+          for (int J = I; J < NT; ++J, ++pp) {
+            // smallest terms first into the running f32 sum
+            acc[pp] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[I], bh[J], acc[pp], 0, 0, 0);
+            acc[pp] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[I], bl[J], acc[pp], 0, 0, 0);
+            acc[pp] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am[I], bm[J], acc[pp], 0, 0, 0);
+            acc[pp] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am[I], bh[J], acc[pp], 0, 0, 0);
+            acc[pp] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[I], bm[J], acc[pp], 0, 0, 0);
+            acc[pp] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[I], bh[J], acc[pp], 0, 0, 0);
+          }
       }
     }
 #pragma unroll
@@ -658,6 +724,18 @@ static void f32_rs32(F&& f) {
 
 template <typename F>
 static void with_stream_kernel(int mode, int xdt, int d, int xm, F&& f) {
+  // split-bf16 f32 statistics: 64-row stages, ring 2 (two blocks per CU: one wave's split VALU
+  // overlaps the other's MFMAs; 1e8 x 32 same box 2.55 vs 2.81 ms at ring 3)
+  if (mode == GRAM_F32S) {
+    if (xdt != DT_F32) throw std::invalid_argument("gram_stream(f32s): needs f32 features");
+#define DQ_SF32S(NTV, XMV)                                                                             \
+  return pick_ring<SGeom<float, 32, NTV, 64, 3>>(f, gram_stream_f32_kernel<NTV, 2, 2, XMV>,            \
+                                                 SGeom<float, 32, NTV, 64, 2>::kWaveBytes,              \
+                                                 gram_stream_f32_kernel<NTV, 3, 2, XMV>, true);
+    if ((d + 31) / 32 == 1) { if (xm) { DQ_SF32S(1, 1) } else { DQ_SF32S(1, 0) } }
+    if (xm) { DQ_SF32S(2, 1) } else { DQ_SF32S(2, 0) }
+#undef DQ_SF32S
+  }
   if (mode == GRAM_F32 || mode == GRAM_BF16) {
     if (xdt != DT_F32) throw std::invalid_argument("gram_stream(f32/bf16): needs f32 features");
     const int NT = (d + 31) / 32;
@@ -711,6 +789,7 @@ static void with_stream_kernel(int mode, int xdt, int d, int xm, F&& f) {
 }
 
 static int stream_rs(int mode, int xdt, int d) {
+  if (mode == GRAM_F32S) return 64;
   if (mode == GRAM_F32 || mode == GRAM_BF16) return f32_rs(d);
   return (mode == GRAM_F64 && xdt == DT_F64 && d > 32) ? 32 : 64;
 }
@@ -727,8 +806,8 @@ static bool al(const void* p, uintptr_t m) { return (reinterpret_cast<uintptr_t>
 
 bool gram_stream_ok(int mode, const GramArgs& a) {
   if (a.tiled || a.cols > 0 || a.d < 1 || a.d > 64 || a.n < 1) return false;
-  if ((mode == GRAM_F32 || mode == GRAM_BF16) && a.xdt != DT_F32) return false;
-  if (mode != GRAM_F32 && mode != GRAM_F64 && mode != GRAM_BF16) return false;
+  if ((mode == GRAM_F32 || mode == GRAM_BF16 || mode == GRAM_F32S) && a.xdt != DT_F32) return false;
+  if (mode != GRAM_F32 && mode != GRAM_F64 && mode != GRAM_BF16 && mode != GRAM_F32S) return false;
   if (a.xdt != DT_F32 && a.xdt != DT_F64) return false;
   const int xs = a.xdt == DT_F64 ? 8 : 4;
   if (a.srcs == nullptr && (!al(a.X, 16) || (a.d > 1 && ((a.ld * xs) & 15) != 0))) return false;
@@ -784,7 +863,8 @@ void gram_stream(int mode, GramArgs a, int xmode, int blocks, double* out, hipSt
 }
 
 void gram_stream_rtc(void* fn, int mode, GramArgs a, int blocks, size_t lds, double* out, hipStream_t st) {
-  if (mode != GRAM_F32 && mode != GRAM_BF16) throw std::invalid_argument("gram_stream_rtc: f32 / bf16 modes");
+  if (mode != GRAM_F32 && mode != GRAM_BF16 && mode != GRAM_F32S)
+    throw std::invalid_argument("gram_stream_rtc: f32 / bf16 / split-f32 modes");
   if (a.xdt != DT_F32 || a.srcs == nullptr || a.rawtab == nullptr || a.d < 1 || a.d > 64 || a.n < 1)
     throw std::invalid_argument("gram_stream_rtc: f32 source columns and a row-scalar table");
   if (blocks < 1 || lds > (size_t)kLdsMax) throw std::invalid_argument("gram_stream_rtc: blocks / lds");

@@ -22,7 +22,7 @@ __all__ = ["dtype_code", "gram_stats", "compact_indices", "pack_columns", "predi
 
 _DT = {torch.float64: 0, torch.float32: 1, torch.bfloat16: 2, torch.int32: 3, torch.int64: 4, torch.uint8: 5,
        torch.bool: 5, torch.float16: 6}
-GRAM_MODES = {"fp64": 0, "fp32": 1, "bf16": 2, "fp8": 3}
+GRAM_MODES = {"fp64": 0, "fp32": 1, "bf16": 2, "fp8": 3, "fp32split": 4}
 _plan_cache = {}
 
 
@@ -150,9 +150,10 @@ def gram_stats(X, y, w, sel, compute: str = "fp64", x_zero_dead: bool = False, b
         # fp64: f64 MFMA SYRK; fp32 and weighted bf16/fp8 requests: exact-f32 MFMA SYRK (at least
         # the requested precision; the fragment kernels carry no per-row weights)
         return _gram_syrk(h, X, y, w, sel, compute_f64=mode == 0)
-    if mode == 1:
+    if mode in (1, 4):
         # "fp32" statistics: f32 features -> exact-f32 MFMA stream kernel (gram_stream.hip);
-        # anything else (f64 storage, unaligned views) -> the f64 kernel, at least as precise
+        # "fp32split": the same statistics from split-bf16 products on the bf16 MFMA; anything
+        # else (f64 storage, unaligned views) -> the f64 kernel, at least as precise
         if X.dtype not in (torch.float32, torch.float64):
             X = X.to(torch.float32)
         if X.dtype != torch.float32 or d <= 8:
@@ -176,7 +177,7 @@ def gram_stats(X, y, w, sel, compute: str = "fp64", x_zero_dead: bool = False, b
             sel = sel.to(torch.bool)
     if y.numel() != n or (w is not None and w.numel() != n) or (sel is not None and sel.numel() != n):
         raise ValueError("gram_stats: row-count mismatch")
-    if mode in (0, 1) or X.dtype == torch.float32:
+    if mode in (0, 1, 4) or X.dtype == torch.float32:
         # the LDS-DMA stream kernels (gram_stream.hip) read labels / weights as 16-B chunks and the
         # selection as 4-B words: re-base unaligned views (an n-element copy, far below the pass)
         y = y if y.data_ptr() % 16 == 0 else y.clone()
@@ -282,7 +283,7 @@ def gram_stream_cols(parts, y, w, sel, compute: str):
         return None
     xdt = dts.pop()
     mode = GRAM_MODES[compute]
-    if xdt not in (torch.float32, torch.float64) or (mode in (1, 2) and xdt != torch.float32):
+    if xdt not in (torch.float32, torch.float64) or (mode in (1, 2, 4) and xdt != torch.float32):
         return None
     if mode == 3 or (mode == 2 and w is not None):
         return None

@@ -17,7 +17,7 @@ compiled by hipRTC with the chain lowered into its per-stage row prologue:
 * the features stream as before (f32 source columns DMA'd into swizzled LDS tiles, bf16 or
   exact-f32 MFMA).
 
-Applies when: gramDtype bf16 / fp32, no weights, 9 <= d <= 64 non-null 16-byte-aligned f32
+Applies when: gramDtype bf16 / fp32 / fp32split, no weights, 9 <= d <= 64 non-null 16-byte-aligned f32
 feature columns passed through unchanged by the chain, a chain that ``dqvm`` can fuse without a
 raising rule, and its input columns fit the 1280-byte row-scalar area (<= 20 bytes per row).
 """
@@ -39,6 +39,7 @@ _text: Optional[str] = None
 _CACHE: dict = {}
 _TABS: dict = {}
 _CUS: dict = {}
+_MODES = {"bf16": 2, "fp32": 1, "fp32split": 4}  # gramDtype -> GramMode (its kernel: CMP 1 / 0 / 2)
 
 # the stage's row-scalar area: a 16-B-per-lane DMA instruction (1024 B) and a 4-B one (256 B)
 RAW16, RAW4 = 1024, 256
@@ -209,7 +210,7 @@ def _compile(chain, rel, feat_cols, mode):
         NT = (d + 31) // 32
         RING = 3 if 4 * _wave_bytes(NT, 3) <= 160 * 1024 else 2
         ctypes = {c: dqvm._ctype(schema.fields[c].dataType) for c in used}
-        src = kernel_source(g, layout, ctypes, yv, NT, RING, 1 if mode == 2 else 0, yvalid)
+        src = kernel_source(g, layout, ctypes, yv, NT, RING, {2: 1, 1: 0, 4: 2}[mode], yvalid)
         plan = _Plan(src, layout, d, NT, RING, mode)
     except (dqvm.Unfusable, _GramNullable, KeyError) as e:
         if os.environ.get("DQ4ML_STREAM_DQ_DEBUG"):
@@ -229,7 +230,7 @@ def try_fused_stream(plan, features_col: str, label_col: str, session, gram_dtyp
     from ..sql.plan import Filter, LocalRelation, Project, output_name
     from .scanfuse import FusedGram
 
-    if os.environ.get("DQ4ML_STREAM_DQ", "1") == "0" or gram_dtype not in ("bf16", "fp32"):
+    if os.environ.get("DQ4ML_STREAM_DQ", "1") == "0" or gram_dtype not in _MODES:
         return None
     if getattr(session, "device", None) is None or session.device.type != "cuda":
         return None
@@ -271,7 +272,7 @@ def try_fused_stream(plan, features_col: str, label_col: str, session, gram_dtyp
     lexpr = le.child if isinstance(le, Alias) else le
     gtop = Project(top.child, [Alias(ColRef(c), f"__gx{i}") for i, c in enumerate(va.inputs)] + [Alias(lexpr, "__gy")])
     chain = list(reversed(nodes[1:])) + [gtop]
-    mode = 2 if gram_dtype == "bf16" else 1
+    mode = _MODES[gram_dtype]
     cp = _compile(chain, p, feat_cols, mode)
     if cp is None:
         return None

@@ -35,6 +35,23 @@ for s in $STEPS; do
     cfg4two) step cfg4two 900 env DQ4ML_STREAM_DQ=0 python benchmarks/bench_dq_pipeline.py --steps 5 --warmup 2 --json-out gpurun_out/cfg4two.json ;;
     kprof4sf) (export TMPDIR=/tmp; step kprof4sf 600 rocprofv3 --kernel-trace --stats -d gpurun_out/kprof4sf -o run --output-format csv -- python benchmarks/bench_dq_pipeline.py --steps 3 --warmup 1) || exit $? ;;
     sf) step sf 600 python -u -m pytest tests/test_gpu_streamfuse.py -m gpu -v --maxfail=3 --timeout 120 --timeout-method thread ;;
+    f32s) step f32s_t 600 python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_streamfuse.py -m gpu -q -k "fp32 or one_pass" --timeout 120 --timeout-method thread &&
+          step f32s_b1 300 python bench.py --steps 20 --warmup 3 --dtype fp32 &&
+          step f32s_b2 300 python bench.py --steps 20 --warmup 3 --dtype fp32split &&
+          step f32s_b3 300 python bench.py --steps 20 --warmup 3 --dtype fp32 &&
+          step f32s_b4 300 python bench.py --steps 20 --warmup 3 --dtype fp32split &&
+          (export TMPDIR=/tmp; step f32spmc 300 timeout -s KILL 240 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_SALU GRBM_GUI_ACTIVE -d gpurun_out/f32spmc -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --dtype fp32split) || exit $? ;;
+    f32sr) step f32sr_a 300 env DQ4ML_GRAM_STREAM_RING=2 python bench.py --steps 20 --warmup 3 --dtype fp32split &&
+           step f32sr_b 300 env DQ4ML_GRAM_STREAM_RING=3 python bench.py --steps 20 --warmup 3 --dtype fp32split &&
+           step f32sr_c 300 env DQ4ML_GRAM_STREAM_RING=2 python bench.py --steps 20 --warmup 3 --dtype fp32split &&
+           step f32sr_d 300 env DQ4ML_GRAM_STREAM_RING=3 python bench.py --steps 20 --warmup 3 --dtype fp32split &&
+           step f32sr_e 300 env DQ4ML_GRAM_STREAM_RING=2 python bench.py --steps 20 --warmup 3 --dtype fp32 || exit $? ;;
+    f32s2) step f32s2_t 600 python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_streamfuse.py tests/test_gpu_determinism.py -m gpu -q --timeout 120 --timeout-method thread &&
+           step f32s2_a 300 python bench.py --steps 20 --warmup 3 --dtype fp32split &&
+           step f32s2_b 300 python bench.py --steps 20 --warmup 3 --dtype bf16 --storage fp32 &&
+           step f32s2_c 300 python bench.py --steps 20 --warmup 3 --dtype fp32split &&
+           step f32s2_d 300 python bench.py --steps 20 --warmup 3 --dtype bf16 --storage fp32 &&
+           (export TMPDIR=/tmp; step f32s2pmc 300 timeout -s KILL 240 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_SALU GRBM_GUI_ACTIVE -d gpurun_out/f32s2pmc -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --dtype fp32split) || exit $? ;;
     cfg4rs64) step cfg4rs64 900 env DQ4ML_GRAM_STREAM_F32RS=64 python benchmarks/bench_dq_pipeline.py --steps 5 --warmup 2 ;;
     cfg4ring3) step cfg4ring3 900 env DQ4ML_GRAM_STREAM_RING=3 python benchmarks/bench_dq_pipeline.py --steps 5 --warmup 2 ;;
     cfg4nodqs) step cfg4nodqs 900 env DQ4ML_DQ_STREAM=0 python benchmarks/bench_dq_pipeline.py --steps 5 --warmup 2 ;;

@@ -124,16 +124,18 @@ def test_gram_skinny_cols_reads_mixed_source_columns(d):
         assert _rel(out, _ref_stats(X, y, ww, ss)) < 1e-12
 
 
+@pytest.mark.parametrize("mode", ["fp32", "fp32split"])
 @pytest.mark.parametrize("d", [3, 20, 32, 33, 64])
 @pytest.mark.parametrize("n", [1, 65, 77_777])
-def test_gram_fp32_mode_exact_f32_kernel(d, n):
+def test_gram_fp32_mode_exact_f32_kernel(d, n, mode):
     """gramDtype fp32 on f32 features: the exact-f32 MFMA stream kernel (gram_stream.hip) for
     d > 8 — f32 products and 1024-row f32 partial sums flushed to f64; d <= 8 keeps the f64
-    skinny kernel.  Scalars (count, Σw, Σy...) stay f64."""
+    skinny kernel.  Scalars (count, Σw, Σy...) stay f64.  fp32split: the same statistics from
+    split-bf16 products (x = hi + mid + lo, six bf16 MFMAs per pair) at the same tolerance."""
     g = torch.Generator(device="cuda").manual_seed(90 + d + n)
     X = torch.randn(d, n, generator=g, device="cuda") + 0.3
     y = torch.randn(n, generator=g, device="cuda") * 2
-    out = device.gram_stats(X, y, None, None, "fp32")
+    out = device.gram_stats(X, y, None, None, mode)
     ref = _ref_stats(X.double(), y.double(), None, None)
     assert _rel(out[:5], ref[:5]) < 1e-12
     assert _rel(out, ref) < (1e-12 if d <= 8 else 2e-6)

@@ -48,7 +48,7 @@ def _df(spark, n, d, seed=3):
 
 
 @pytest.mark.parametrize("d,n,gd", [(64, 300_007, "bf16"), (20, 200_000, "bf16"), (64, 150_000, "fp32"),
-                                    (33, 100_050, "fp32")])
+                                    (33, 100_050, "fp32"), (40, 120_000, "fp32split")])
 def test_one_pass_equals_two_pass(spark, monkeypatch, d, n, gd):
     from net.jgp.labs.sparkdq4ml_amd import LinearRegression
     from net.jgp.labs.sparkdq4ml_amd.models import regression
