@@ -215,14 +215,15 @@ def owlqn_result(host: np.ndarray, nf: int):
 
 def wls_owlqn_device(flat, nf, fit_intercept, reg_param, elastic_net, standardize_features, standardize_label,
                      max_iter, tol):
-    """The OWLQN branch with the statistics on the device: the one-wave HIP solver for k <= 128
-    (one D2H of its result), the device-resident torch OWLQN above (``models/owlqn_device.py``).
+    """The OWLQN branch with the statistics on the device: the HIP solvers (one wave for
+    k <= 128, one cooperative grid launch up to ``QN_DEVICE_MAX_K``; one D2H of the result), the
+    host-steered torch OWLQN only when forced (``DQ4ML_QN_ENGINE=torch``, A/B) or beyond.
     None = the native host driver owns the case."""
     from ..ops import device
-    from .owlqn_device import QN_SMALL_MAX_K, QN_TORCH_MIN_K, solve_owlqn_device
+    from .owlqn_device import QN_DEVICE_MAX_K, QN_TORCH_MIN_K, qn_engine, solve_owlqn_device
 
     k = nf + 1 if fit_intercept else nf
-    if k <= QN_SMALL_MAX_K:
+    if k <= QN_DEVICE_MAX_K and qn_engine() == "hip":
         out = device.wls_qn_small(flat, nf, fit_intercept, reg_param, elastic_net, standardize_features,
                                   standardize_label, max_iter, tol)
         return owlqn_result(out.cpu().numpy(), nf)

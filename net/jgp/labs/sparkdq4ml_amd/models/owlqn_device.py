@@ -7,12 +7,15 @@ driver implements it (``ops/csrc/host/solvers.cpp``: L-BFGS two-loop on the pseu
 orthant projection, backtracking line search seeded with 0.5/|g| on the first iteration,
 FunctionValuesConverged over the last 20 values, one history reset on a failed search):
 
-* ``k <= 128``: ONE workgroup runs the whole solve (``ops/csrc/hip/wls_small.hip``,
+* ``k <= 128``: ONE wave runs the whole solve (``ops/csrc/hip/wls_small.hip``,
   ``wls_qn_kernel``) -- no host round trip, so an L1 fit can be asynchronous;
-* larger k (up to 4097): this module's torch version: vectors and the dense k x k system stay in
-  HBM, every cost evaluation is one f64 GEMV there, and only the scalars that steer the line
-  search cross to the host (the host driver would run an O(k^2) packed ``dspmv`` per evaluation
-  on one CPU core: 8.4 M entries at k = 4097).
+* ``128 < k <= QN_DEVICE_MAX_K`` (4608): ONE cooperative grid launch, one block per CU
+  (``ops/csrc/hip/wls_qn_grid.hip``): the dense standardized system in HBM, row panels per block,
+  one grid barrier per cost evaluation with every block taking the same line-search decisions --
+  no host round trip either, so these fits are asynchronous too;
+* this module's torch version (``DQ4ML_QN_ENGINE=torch``, kept for A/B): vectors and the dense
+  k x k system stay in HBM, every cost evaluation is one f64 GEMV there, and the scalars that
+  steer the line search cross to the host on every evaluation.
 """
 from __future__ import annotations
 
@@ -21,9 +24,18 @@ from typing import Optional, Tuple
 import numpy as np
 import torch
 
-__all__ = ["standardized_system", "owlqn_torch", "solve_owlqn_device", "QN_SMALL_MAX_K", "QN_TORCH_MIN_K"]
+__all__ = ["standardized_system", "owlqn_torch", "solve_owlqn_device", "QN_SMALL_MAX_K", "QN_DEVICE_MAX_K",
+           "QN_TORCH_MIN_K", "qn_engine"]
 
 QN_SMALL_MAX_K = 128
+QN_DEVICE_MAX_K = 4608  # kWlsQnGridMaxK (wls_small.h)
+
+
+def qn_engine() -> str:
+    """``hip`` (default: the one-wave / grid HIP solvers) or ``torch`` (host-steered, A/B)."""
+    import os
+
+    return "torch" if os.environ.get("DQ4ML_QN_ENGINE", "hip") == "torch" else "hip"
 # device-resident torch engine from this k on (scripts/owlqn_bench.py, 1x MI355X, L1 = 0.01:
 # k = 1025 device 12.1 ms vs host 6.3 ms; k = 4097 device 22.4 ms vs host 267 ms)
 QN_TORCH_MIN_K = 2048

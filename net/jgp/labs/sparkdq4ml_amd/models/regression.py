@@ -375,19 +375,24 @@ def _async_conf(df) -> bool:
 
 
 def _async_fit(df, flat, d, args) -> bool:
-    """Asynchronous normal-equation fit (session config ``dq4ml.fit.async``): device statistics,
-    <= 64 features, Cholesky branch (no L1) -> the solve is enqueued on the device and the host
-    does not wait for the fit; coefficients, summary and any Spark warning/exception materialize
-    on first read (edge cases re-solve on the host with identical semantics)."""
+    """Asynchronous normal-equation fit (session config ``dq4ml.fit.async``): device statistics
+    and a device solver for the branch -- Cholesky (no L1) for <= 64 features, OWLQN (L1) up to
+    k = QN_DEVICE_MAX_K -> the solve is enqueued on the device and the host does not wait for the
+    fit; coefficients, summary and any Spark warning/exception materialize on first read (edge
+    cases re-solve on the host with identical semantics)."""
     sess = getattr(df, "sparkSession", None)
     if sess is None or str(sess.conf.get("dq4ml.fit.async", "false")).lower() not in ("1", "true", "yes"):
         return False
-    if not (getattr(flat, "is_cuda", False) and 1 <= d <= 64):
+    if not (getattr(flat, "is_cuda", False) and d >= 1):
         return False
     _, _, fit_icpt, reg, enet = args[:5]
-    # L1 (OWLQN, the lab's own regParam=1 / elasticNetParam=1) runs on the device too
-    # (wls_qn_kernel, k <= 128)
-    return not (enet != 0.0 and reg != 0.0) or d + (1 if fit_icpt else 0) <= 128
+    # L1 (OWLQN, the lab's own regParam=1 / elasticNetParam=1) runs on the device too: one wave
+    # for k <= 128, one cooperative grid launch up to QN_DEVICE_MAX_K (wls_qn_grid.hip)
+    from .owlqn_device import QN_DEVICE_MAX_K, qn_engine
+
+    if enet != 0.0 and reg != 0.0:
+        return qn_engine() == "hip" and d + (1 if fit_icpt else 0) <= QN_DEVICE_MAX_K
+    return d <= 64
 
 
 _tail_streams = {}

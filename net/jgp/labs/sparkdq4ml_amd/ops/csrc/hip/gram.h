@@ -46,7 +46,14 @@ struct GramArgs {
   // sources of the stage's row-scalar area — [64 lanes][(base, bytes per row) x 2 instructions]
   // int64 pairs, then the region pointers the guarded tail stage copies from
   const int64_t* rawtab;
+  // in-kernel fold (tall bf16 kernel): kFoldTickets zeroed counters owned by the launching stream
+  // (the last block resets them) and the packed output; partials then holds blocks + kFoldGroups
+  // slabs.  Null: the slabs are folded by gram_reduce (a separate kernel)
+  unsigned int* ticket;
+  double* fold_out;
 };
+constexpr int kFoldGroups = 8;               // one group per XCD (blocks are dealt round-robin)
+constexpr int kFoldTickets = kFoldGroups + 1;
 
 #ifndef __HIPCC_RTC__
 // MFMA-fragment-ordered bf16 feature storage ("tiled"): for superstep s (64 rows), 32-feature

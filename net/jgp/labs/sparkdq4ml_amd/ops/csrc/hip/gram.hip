@@ -169,6 +169,89 @@ __device__ __forceinline__ void weight_frags(bf16x8 (&fr)[4], const float* wl /*
     for (int j = 0; j < 8; ++j) fr[i][j] = (__bf16)((float)fr[i][j] * wl[8 * i + j]);
 }
 
+// slab element o (storage order: head, then T x T tiles of the row-major upper pairs I <= J < NT)
+// -> its packed-upper destination; lower halves of the diagonal tiles and padding features drop
+__device__ __forceinline__ void fold_store(int o, double t, int d, int T, int NT, double* __restrict__ out) {
+  const int head = 5 + 2 * d;
+  if (o < head) {
+    out[o] = t;
+    return;
+  }
+  const int e = o - head, pr = e / (T * T), w = e - pr * T * T, r = w / T, cc = w - (w / T) * T;
+  int I = 0, rem = pr;
+  while (rem >= NT - I) {
+    rem -= NT - I;
+    ++I;
+  }
+  const int J = I + rem;
+  const int64_t i = (int64_t)I * T + r, j = (int64_t)J * T + cc;
+  if (i <= j && j < d) out[head + i + j * (j + 1) / 2] = t;
+}
+
+// Fold of the blocks' slabs inside the Gram kernel (replaces gram_reduce's kernel and its kernel
+// boundary): the last block of each XCD group (block b is in group b % G) sums the group's slabs
+// in ascending block order into a group slab, and the last group folds the G group slabs in
+// ascending order into the packed output.  Both orders are fixed, so the result does not depend
+// on which block arrives last (run-to-run bitwise deterministic).
+// Visibility without cache maintenance: the slabs are written and read with relaxed agent-scope
+// atomic stores / loads (coherent across the XCDs' L2s), the writer waits for its stores
+// (vmcnt(0)) before its relaxed counter increment.  An agent-scope release / acquire fence instead
+// (L2 write-back + invalidate in every block) cost ~85 us per pass (measured, 1.25e7 x 32).
+constexpr int kFoldBatch = 32;  // slabs per group in flight at once (256 blocks / 8 groups)
+__device__ __forceinline__ void slab_put(double* p, double v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double slab_get(const double* p) {
+  return __hip_atomic_load(const_cast<double*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void slab_fold_tail(const GramArgs& a, int T, int NT) {
+  __shared__ unsigned int s_last;
+  const int P = a.P, nb = gridDim.x, G = nb < kFoldGroups ? nb : kFoldGroups, g = blockIdx.x % G;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned int mine = (unsigned int)((nb - 1 - g) / G);  // this group's block count - 1
+    s_last = __hip_atomic_fetch_add(a.ticket + g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == mine;
+  }
+  __syncthreads();
+  if (!s_last) return;
+  const double* src = a.partials;
+  double* gs = a.partials + (int64_t)nb * P;
+  for (int o = threadIdx.x; o < P; o += blockDim.x) {
+    // every slab of the group in flight at once (the coherent loads miss L2: one round trip,
+    // not one per slab), then summed in ascending block order
+    double s = 0.0;
+    for (int b0 = g; b0 < nb; b0 += kFoldBatch * G) {
+      double v[kFoldBatch];
+#pragma unroll
+      for (int i = 0; i < kFoldBatch; ++i) {
+        const int b = b0 + i * G;
+        v[i] = b < nb ? slab_get(src + (int64_t)b * P + o) : 0.0;
+      }
+#pragma unroll
+      for (int i = 0; i < kFoldBatch; ++i) s += v[i];
+    }
+    slab_put(gs + (int64_t)g * P + o, s);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0)
+    s_last = __hip_atomic_fetch_add(a.ticket + kFoldGroups, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+             (unsigned int)(G - 1);
+  __syncthreads();
+  if (!s_last) return;
+  for (int o = threadIdx.x; o < P; o += blockDim.x) {
+    double v[kFoldGroups];
+#pragma unroll
+    for (int k = 0; k < kFoldGroups; ++k) v[k] = k < G ? slab_get(gs + (int64_t)k * P + o) : 0.0;
+    double s = 0.0;
+#pragma unroll
+    for (int k = 0; k < kFoldGroups; ++k) s += v[k];
+    fold_store(o, s, a.d, T, NT, a.fold_out);
+  }
+  if (threadIdx.x < kFoldTickets) a.ticket[threadIdx.x] = 0u;
+}
+
 // =============================================================================================
 // bf16 MFMA kernel
 // =============================================================================================
@@ -364,7 +447,7 @@ __global__ __launch_bounds__((BF16Geom<NT, XMODE>::kBlock), 1) void gram_tall_bf
     if (lane < 5) {
       double t = 0.0;
       for (int w = 0; w < W; ++w) t += scl[w * 5 + lane];
-      out[lane] = t;
+      slab_put(out + lane, t);
     }
     const int col = mfma32_col(lane);
 #pragma unroll
@@ -376,8 +459,8 @@ __global__ __launch_bounds__((BF16Geom<NT, XMODE>::kBlock), 1) void gram_tall_bf
         const float vn = __shfl_down(v, 1, 64);  // col+1 (same row)
         const int feat = t * 32 + mfma32_row(lane, r);
         if (feat < d) {
-          if (col == 0) out[5 + feat] = (double)v + (double)vn;
-          if (col == 2) out[5 + d + feat] = (double)v + (double)vn;
+          if (col == 0) slab_put(out + 5 + feat, (double)v + (double)vn);
+          if (col == 2) slab_put(out + 5 + d + feat, (double)v + (double)vn);
         }
       }
     }
@@ -388,9 +471,10 @@ __global__ __launch_bounds__((BF16Geom<NT, XMODE>::kBlock), 1) void gram_tall_bf
       for (int J = I; J < NT; ++J, ++p) {
         double* tile = out + 5 + 2 * d + p * 1024;
 #pragma unroll
-        for (int r = 0; r < 16; ++r) tile[mfma32_row(lane, r) * 32 + col] = (double)acc[p][r];
+        for (int r = 0; r < 16; ++r) slab_put(tile + mfma32_row(lane, r) * 32 + col, (double)acc[p][r]);
       }
   }
+  if (a.ticket) slab_fold_tail(a, 32, NT);
 }
 
 // =============================================================================================
@@ -593,7 +677,7 @@ __global__ __launch_bounds__(256, (NT == 1 ? 3 : 2)) void gram_cols_kernel(GramA
   if (wave == 0) {
     const int d = a.d;
     double* out = a.partials + (int64_t)blockIdx.x * a.P;
-    if (lane < 5) out[lane] = scl[lane] + scl[5 + lane] + scl[10 + lane] + scl[15 + lane];
+    if (lane < 5) slab_put(out + lane, scl[lane] + scl[5 + lane] + scl[10 + lane] + scl[15 + lane]);
     const int col = mfma32_col(lane);
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
@@ -603,8 +687,8 @@ __global__ __launch_bounds__(256, (NT == 1 ? 3 : 2)) void gram_cols_kernel(GramA
         const float vn = __shfl_down(v, 1, 64);
         const int feat = t * 32 + mfma32_row(lane, r);
         if (feat < d) {
-          if (col == 0) out[5 + feat] = (double)v + (double)vn;
-          if (col == 2) out[5 + d + feat] = (double)v + (double)vn;
+          if (col == 0) slab_put(out + 5 + feat, (double)v + (double)vn);
+          if (col == 2) slab_put(out + 5 + d + feat, (double)v + (double)vn);
         }
       }
     }
@@ -615,9 +699,10 @@ __global__ __launch_bounds__(256, (NT == 1 ? 3 : 2)) void gram_cols_kernel(GramA
       for (int J = I; J < NT; ++J, ++p) {
         double* tile = out + 5 + 2 * d + p * 1024;
 #pragma unroll
-        for (int r = 0; r < 16; ++r) tile[mfma32_row(lane, r) * 32 + col] = (double)acc[p][r];
+        for (int r = 0; r < 16; ++r) slab_put(tile + mfma32_row(lane, r) * 32 + col, (double)acc[p][r]);
       }
   }
+  if (a.ticket) slab_fold_tail(a, 32, NT);
 }
 
 constexpr int kStageLd = 66;  // f64 staging row stride (doubles): 2-double pad spreads the banks
@@ -1008,20 +1093,7 @@ __global__ __launch_bounds__(1024) void gram_fold_kernel(const double* __restric
     double t = 0.0;
 #pragma unroll
     for (int i = 0; i < 16; ++i) t += part[i][c];
-    const int head = 5 + 2 * d;
-    if (o < head) {
-      out[o] = t;
-      return;
-    }
-    const int e = o - head, pr = e / (T * T), w = e - pr * T * T, r = w / T, cc = w - (w / T) * T;
-    int I = 0, rem = pr;  // row-major pair index over I <= J < NT
-    while (rem >= NT - I) {
-      rem -= NT - I;
-      ++I;
-    }
-    const int J = I + rem;
-    const int64_t i = (int64_t)I * T + r, j = (int64_t)J * T + cc;
-    if (i <= j && j < d) out[head + i + j * (j + 1) / 2] = t;
+    fold_store(o, t, d, T, NT, out);
   }
 }
 
@@ -1295,6 +1367,11 @@ void gram_tall(int mode, GramArgs a, int xmode, int blocks, double* out, hipStre
   a.P = (int)gram_partial_stride(mode, a.d);
   const size_t lds = mode == GRAM_BF16 ? bf16_lds(a.d, xmode) : f64_lds(a.d);
   if (a.tiled && mode != GRAM_BF16) throw std::invalid_argument("gram_tall: tiled storage needs bf16 mode");
+  // in-kernel fold: tall bf16 kernel only (the caller sized partials for blocks + kFoldGroups slabs)
+  const bool fold_in = reduce && a.ticket != nullptr && mode == GRAM_BF16 && a.cols == 0 &&
+                       !(a.xdt == DT_F32 && use_stream() && gram_stream_ok(mode, a));
+  if (!fold_in) a.ticket = nullptr;
+  a.fold_out = fold_in ? out : nullptr;
   if (a.cols > 0) {
     if (mode != GRAM_F64 || a.cols != a.d || a.d > kSkinnyMaxD || a.tiled)
       throw std::invalid_argument("gram_tall: columnar sources need f64 mode and d <= 8");
@@ -1313,7 +1390,7 @@ void gram_tall(int mode, GramArgs a, int xmode, int blocks, double* out, hipStre
                 [&](auto kern) { hipLaunchKernelGGL(kern, dim3(blocks), dim3(block), lds, st, a); });
   }
   DQ_HIP_CHECK(hipGetLastError());
-  if (reduce) gram_reduce(mode, a.partials, blocks, a.d, out, st);
+  if (reduce && !fold_in) gram_reduce(mode, a.partials, blocks, a.d, out, st);
 }
 
 static size_t cols_lds(int NT) {
@@ -1361,10 +1438,11 @@ void gram_cols(GramArgs a, const PackSrcG* srcs_dev, int sdt, int blocks, double
   const int NT = (a.d + 31) / 32;
   const size_t lds = cols_lds(NT);
   if (a.ydt != DT_F64 && a.ydt != DT_F32) throw std::invalid_argument("gram_cols: label must be f32 or f64");
+  a.fold_out = a.ticket ? out : nullptr;  // in-kernel fold when the caller passed counters
   with_cols_kernel(NT, sdt, a.ydt,
                    [&](auto k) { hipLaunchKernelGGL(k, dim3(blocks), dim3(256), lds, st, a, srcs_dev); });
   DQ_HIP_CHECK(hipGetLastError());
-  gram_reduce(GRAM_BF16, a.partials, blocks, a.d, out, st);
+  if (!a.ticket) gram_reduce(GRAM_BF16, a.partials, blocks, a.d, out, st);
 }
 
 }  // namespace dq4ml

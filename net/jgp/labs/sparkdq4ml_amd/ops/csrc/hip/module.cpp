@@ -43,14 +43,17 @@ PYBIND11_MODULE(_dq4ml_hip, m) {
 
   // ---- Gram (K5) ---------------------------------------------------------------------------
   m.def("gram_partial_stride", &gram_partial_stride);
+  m.def("gram_fold_groups", [] { return kFoldGroups; });
+  m.def("gram_fold_tickets", [] { return kFoldTickets; });
   m.def("gram_default_blocks", &gram_default_blocks);
   m.def("gram_plan_blocks", &gram_plan_blocks);
   m.def("gram_tall",
         [](int mode, uintptr_t X, int64_t ld, int d, int64_t n, int xdt, uintptr_t y, int ydt, uintptr_t w, int wdt,
            uintptr_t sel, int xmode, uintptr_t partials, int blocks, uintptr_t out, uintptr_t stream, int tiled,
-           bool reduce) {
+           bool reduce, uintptr_t ticket) {
           GramArgs a{};
           a.tiled = tiled;
+          a.ticket = P<unsigned int>(ticket);
           a.X = P<const void>(X);
           a.ld = ld;
           a.d = d;
@@ -121,8 +124,9 @@ PYBIND11_MODULE(_dq4ml_hip, m) {
   });
   m.def("gram_cols_blocks", &gram_cols_blocks);
   m.def("gram_cols", [](uintptr_t srcs, int sdt, int d, int64_t n, uintptr_t y, int ydt, uintptr_t sel,
-                        uintptr_t partials, int blocks, uintptr_t out, uintptr_t stream) {
+                        uintptr_t partials, int blocks, uintptr_t out, uintptr_t stream, uintptr_t ticket) {
     GramArgs a{};
+    a.ticket = P<unsigned int>(ticket);
     a.d = d;
     a.n = n;
     a.xdt = DT_F32;
@@ -167,6 +171,15 @@ PYBIND11_MODULE(_dq4ml_hip, m) {
                  P<double>(out), as_stream(stream));
   });
   m.attr("WLS_QN_MAX_K") = kWlsQnMaxK;
+  m.attr("WLS_QN_GRID_MAX_K") = kWlsQnGridMaxK;
+  m.def("wls_qn_grid_work", &wls_qn_grid_work);
+  m.def("wls_qn_grid_blocks", &wls_qn_grid_blocks);
+  m.def("wls_qn_grid", [](uintptr_t flat, int nf, bool fit_intercept, double reg, double enet, bool std_f, bool std_l,
+                          int max_iter, double tol, int hist_cap, uintptr_t work, int blocks, uintptr_t out,
+                          uintptr_t stream) {
+    wls_qn_grid(P<const double>(flat), nf, fit_intercept, reg, enet, std_f, std_l, max_iter, tol, hist_cap,
+                P<double>(work), blocks, P<double>(out), as_stream(stream));
+  });
   m.attr("WLS_SMALL_MAX_FEATURES") = kWlsSmallMaxFeatures;
   m.def("wide_tiled_bytes", &wide_tiled_bytes);
   m.attr("WIDE_ZERO_BYTES") = kWideZeroBytes;

@@ -18,4 +18,16 @@ constexpr int kWlsQnMaxK = 128;
 void wls_qn_small(const double* flat, int nf, int fit_intercept, double reg, double enet, int std_f, int std_l,
                   int max_iter, double tol, int hist_cap, double* out, hipStream_t st);
 
+// OWLQN branch for 128 < k <= kWlsQnGridMaxK (wls_qn_grid.hip): one cooperative launch of
+// wls_qn_grid_blocks(k) blocks, same out layout as wls_qn_small; work = wls_qn_grid_work(k, blocks)
+// doubles of device scratch (the dense standardized system, vectors, history, partial sums)
+constexpr int kWlsQnGridMaxK = 4608;
+struct WlsQnWork {
+  double *A, *ab, *l1, *bar, *sstd, *x, *g, *ag, *d, *cx, *cg, *cag, *S, *Y, *part, *scal;
+};
+int64_t wls_qn_grid_work(int k, int blocks);
+int wls_qn_grid_blocks(int k);
+void wls_qn_grid(const double* flat, int nf, int fit_intercept, double reg, double enet, int std_f, int std_l,
+                 int max_iter, double tol, int hist_cap, double* work, int blocks, double* out, hipStream_t st);
+
 }  // namespace dq4ml

@@ -104,6 +104,24 @@ def tile_bf16(X: torch.Tensor) -> TiledBF16:
     return TiledBF16(buf, d, n)
 
 
+_tickets = {}
+
+
+def _fold_ticket(h, dev):
+    """Counters of the Gram kernels' in-kernel slab fold (``slab_fold_tail`` in gram.hip), one
+    zeroed set per (device, stream): launches on one stream run in order and each leaves them
+    zeroed.  Opt-in (``DQ4ML_GRAM_FOLD=kernel``): same-box A/B at the 8-GPU shard (1.25e7 x 32)
+    155 us per fit vs 142-148 us with the separate ``gram_reduce`` kernel (profiles/r3_fold_ab.md)"""
+    if os.environ.get("DQ4ML_GRAM_FOLD", "separate") != "kernel":
+        return 0
+    st = torch.cuda.current_stream(dev)
+    key = (st.device.index, st.cuda_stream)
+    t = _tickets.get(key)
+    if t is None:
+        t = _tickets[key] = torch.zeros(int(h.gram_fold_tickets()), dtype=torch.int32, device=dev)
+    return t.data_ptr()
+
+
 class DeferredGram:
     """Gram partial slabs whose final fold (``gram_reduce``) has not been enqueued yet: the
     asynchronous fit runs it on its side stream with the all-reduce and the solve, so the compute
@@ -191,10 +209,11 @@ def gram_stats(X, y, w, sel, compute: str = "fp64", x_zero_dead: bool = False, b
         xmode = 0
     nb = int(blocks or _plan_blocks(h, mode, d, n, dtype_code(Xv), xmode))
     P = int(h.gram_partial_stride(mode, d))
-    partials = torch.empty(nb * P, dtype=torch.float64, device=X.device)
+    tk = _fold_ticket(h, X.device) if mode == 2 else 0
+    partials = torch.empty((nb + (h.gram_fold_groups() if tk else 0)) * P, dtype=torch.float64, device=X.device)
     h.gram_tall(mode, Xv.data_ptr(), int(ld), int(d), int(n), dtype_code(Xv), y.data_ptr(), dtype_code(y),
                 _ptr(w), dtype_code(w) if w is not None else 0, _ptr(sel), xmode, partials.data_ptr(), nb,
-                out.data_ptr(), _stream(), 0, True)
+                out.data_ptr(), _stream(), 0, True, tk)
     return out
 
 
@@ -251,14 +270,15 @@ def gram_cols(parts: List[torch.Tensor], y, sel, blocks: Optional[int] = None):
     desc = _srcw_desc(h, rows, dev)
     nb = int(blocks or _cols_blocks(h, d, n))
     P = int(h.gram_partial_stride(2, d))
-    partials = torch.empty(nb * P, dtype=torch.float64, device=dev)
+    tk = _fold_ticket(h, dev)
+    partials = torch.empty((nb + (h.gram_fold_groups() if tk else 0)) * P, dtype=torch.float64, device=dev)
     out = torch.empty(5 + 2 * d + d * (d + 1) // 2, dtype=torch.float64, device=dev)
     codes = {dtype_code(r) for r in rows}
     sdt = codes.pop() if len(codes) == 1 else -1
     if sdt not in (0, 1, 2) or any(r.data_ptr() % 16 for r in rows):
         sdt = -1  # mixed / unaligned columns: per-element typed loads
     h.gram_cols(desc.data_ptr(), int(sdt), d, n, y.data_ptr(), dtype_code(y), _ptr(sel), partials.data_ptr(), nb,
-                out.data_ptr(), _stream())
+                out.data_ptr(), _stream(), tk)
     return out
 
 
@@ -350,10 +370,14 @@ def _gram_tiled(h, T: "TiledBF16", y, w, sel, x_zero_dead, blocks, defer=False):
     xmode = 2 if w is not None else (1 if (sel is not None and not x_zero_dead) else 0)
     nb = int(blocks or _plan_blocks(h, 2, d, n, 2, xmode))
     P = int(h.gram_partial_stride(2, d))
-    partials = torch.empty(nb * P, dtype=torch.float64, device=T.device)
+    # in-kernel fold (default): the kernel's last block writes the packed statistics, so there is
+    # nothing left to defer to the fit's side stream
+    tk = _fold_ticket(h, T.device)
+    defer = defer and not tk
+    partials = torch.empty((nb + (h.gram_fold_groups() if tk else 0)) * P, dtype=torch.float64, device=T.device)
     h.gram_tall(2, T.buf.data_ptr(), 0, int(d), int(n), 2, y.data_ptr(), dtype_code(y), _ptr(w),
                 dtype_code(w) if w is not None else 0, _ptr(sel), xmode, partials.data_ptr(), nb, out.data_ptr(),
-                _stream(), 1, not defer)
+                _stream(), 1, not defer, tk)
     if defer:
         return DeferredGram(h, 2, partials, nb, d, out)
     return out
@@ -689,20 +713,39 @@ def wls_qn_cap(max_iter: int) -> int:
 
 def wls_qn_small(flat: torch.Tensor, nf: int, fit_intercept: bool, reg: float, enet: float, std_f: bool,
                  std_l: bool, max_iter: int, tol: float) -> torch.Tensor:
-    """Device OWLQN (L1 WLS, k <= 128) from the flat statistics, enqueued on the current stream:
-    ``[coef(nf), intercept, status, count, wSum, wwSum, bSum, bbSum, H, reason, history...]``."""
+    """Device OWLQN (L1 WLS) from the flat statistics, enqueued on the current stream, no host
+    round trip: ``[coef(nf), intercept, status, count, wSum, wwSum, bSum, bbSum, H, reason,
+    history...]``.  k <= 128: one wave (``wls_qn_kernel``); up to ``WLS_QN_GRID_MAX_K``: one
+    cooperative grid launch (``wls_qn_grid.hip``) with its scratch allocated here."""
     h = native.hip()
     _check_dev(flat)
     k = nf + 1 if fit_intercept else nf
     if flat.dtype != torch.float64 or flat.numel() != 5 + 2 * nf + nf * (nf + 1) // 2:
         raise ValueError("wls_qn_small: flat statistics have the wrong dtype/length")
-    if not 1 <= k <= int(h.WLS_QN_MAX_K):
+    if not 1 <= k <= int(h.WLS_QN_GRID_MAX_K):
         raise ValueError(f"wls_qn_small: k = {k} out of range")
     cap = wls_qn_cap(max_iter)
     out = torch.empty(nf + 9 + cap, dtype=torch.float64, device=flat.device)
-    h.wls_qn_small(flat.data_ptr(), int(nf), bool(fit_intercept), float(reg), float(enet), bool(std_f), bool(std_l),
-                   int(max_iter), float(tol), cap, out.data_ptr(), _stream())
+    if k <= int(h.WLS_QN_MAX_K):
+        h.wls_qn_small(flat.data_ptr(), int(nf), bool(fit_intercept), float(reg), float(enet), bool(std_f),
+                       bool(std_l), int(max_iter), float(tol), cap, out.data_ptr(), _stream())
+        return out
+    nb = _qn_grid_blocks(h, k)
+    work = torch.empty(int(h.wls_qn_grid_work(k, nb)), dtype=torch.float64, device=flat.device)
+    h.wls_qn_grid(flat.data_ptr(), int(nf), bool(fit_intercept), float(reg), float(enet), bool(std_f), bool(std_l),
+                  int(max_iter), float(tol), cap, work.data_ptr(), nb, out.data_ptr(), _stream())
     return out
+
+
+_qn_grid_plan = {}
+
+
+def _qn_grid_blocks(h, k):
+    key = (torch.cuda.current_device(), k)
+    nb = _qn_grid_plan.get(key)
+    if nb is None:
+        nb = _qn_grid_plan[key] = int(h.wls_qn_grid_blocks(int(k)))
+    return nb
 
 
 # control-block layout of wls_large.h (WlsPcgState), checked against the module on first use

@@ -131,3 +131,76 @@ def test_wide_l1_fit_uses_device_owlqn(gpu_session):
     np.testing.assert_allclose(coef, r["coefficients"], rtol=1e-6, atol=1e-8)
     assert icpt == pytest.approx(r["intercept"], rel=1e-7, abs=1e-9)
     assert hist[0] == r["objective_history"][0]
+
+
+def _wide_flat(d, n, seed):
+    from net.jgp.labs.sparkdq4ml_amd.ops import device
+
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    X = torch.randn(d, n, generator=g, device="cuda", dtype=torch.float64)
+    X = X * (0.5 + torch.rand(d, 1, generator=g, device="cuda", dtype=torch.float64) * 2)
+    beta = torch.randn(d, generator=g, device="cuda", dtype=torch.float64) * \
+        (torch.rand(d, generator=g, device="cuda") > 0.5)
+    y = beta @ X + 1.0 + 0.1 * torch.randn(n, generator=g, device="cuda", dtype=torch.float64)
+    return device.gram_stats(X, y, None, None, "fp64")
+
+
+@pytest.mark.parametrize("d,reg,enet,icpt,stdf", [(128, 0.01, 1.0, True, True), (256, 0.02, 1.0, True, True),
+                                                  (300, 0.05, 0.5, False, False), (1024, 0.01, 1.0, True, True)])
+def test_qn_grid_kernel_matches_native(d, reg, enet, icpt, stdf):
+    """k > 128: the cooperative grid OWLQN (wls_qn_grid.hip) vs the native host driver."""
+    from net.jgp.labs.sparkdq4ml_amd.models.optim import owlqn_result
+    from net.jgp.labs.sparkdq4ml_amd.ops import device
+
+    flat = _wide_flat(d, max(4 * d, 20_000), d)
+    out = device.wls_qn_small(flat, d, icpt, reg, enet, stdf, True, 100, 1e-6)
+    out2 = device.wls_qn_small(flat, d, icpt, reg, enet, stdf, True, 100, 1e-6)
+    used = d + 9 + int(out[d + 7])  # coefficients, status, scalars, H, reason, history (the rest is scratch)
+    assert torch.equal(out[:used], out2[:used])  # fixed-order reductions: bitwise run to run
+    wls, _ = owlqn_result(out.cpu().numpy(), d)
+    r = _host(flat.cpu().numpy(), d, icpt, reg, enet, stdf)
+    np.testing.assert_allclose(wls.coefficients, r["coefficients"], rtol=1e-6, atol=1e-8)
+    assert wls.intercept == pytest.approx(r["intercept"], rel=1e-7, abs=1e-9)
+    hist, ref = wls.objectiveHistory, np.asarray(r["objective_history"])
+    assert hist[0] == pytest.approx(ref[0], rel=1e-12)
+    assert abs(len(hist) - len(ref)) <= 3
+    assert hist[-1] == pytest.approx(ref[-1], rel=1e-8)
+
+
+def test_qn_grid_kernel_short_circuits_and_no_l1():
+    from net.jgp.labs.sparkdq4ml_amd.ops import device
+
+    nf = 200
+    flat = np.zeros(5 + 2 * nf + nf * (nf + 1) // 2)
+    flat[:5] = [10, 10, 10, 20, 40]  # constant label: std 0 -> the host owns it
+    out = device.wls_qn_small(torch.tensor(flat, device="cuda"), nf, True, 1.0, 1.0, True, True, 40, 1e-6).cpu()
+    assert int(out[nf + 1]) == 3
+    flat = _wide_flat(nf, 5000, 3)
+    out = device.wls_qn_small(flat, nf, True, 1.0, 0.0, True, True, 40, 1e-6).cpu()
+    assert int(out[nf + 1]) == 9  # no L1 term
+
+
+def test_wide_async_l1_fit_has_no_host_sync(gpu_session):
+    """An L1 fit at d = 257 is enqueued (wide Gram -> grid OWLQN) with no host sync, and equals the
+    synchronous fit."""
+    from net.jgp.labs.sparkdq4ml_amd import LinearRegression
+
+    gpu_session.conf.set("dq4ml.fit.async", "true")
+    n, d = 30_000, 257
+    g = torch.Generator(device="cuda").manual_seed(5)
+    X = torch.randn(d, n, generator=g, device="cuda", dtype=torch.float64)
+    beta = torch.randn(d, generator=g, device="cuda", dtype=torch.float64) * (torch.rand(d, generator=g, device="cuda") > 0.6)
+    y = beta @ X + 2.0 + 0.05 * torch.randn(n, generator=g, device="cuda", dtype=torch.float64)
+    df = gpu_session.createDataFrame({"features": X, "label": y})
+    lr = LinearRegression(regParam=0.01, elasticNetParam=1.0)
+    lr.fit(df).coefficients  # warm-up
+    torch.cuda.synchronize()
+    torch.cuda.set_sync_debug_mode("error")
+    try:
+        m = lr.fit(df)
+        assert m._pending is not None and m._pending._qn
+    finally:
+        torch.cuda.set_sync_debug_mode("default")
+    gpu_session.conf.set("dq4ml.fit.async", "false")
+    ref = lr.fit(df)
+    np.testing.assert_allclose(m.coefficients.toArray(), ref.coefficients.toArray(), rtol=1e-10, atol=1e-13)
