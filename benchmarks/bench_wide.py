@@ -4,8 +4,8 @@ XᵀX).  One step = one ``LinearRegression.fit`` (normal equations): fp8 wide SY
 (``gram_wide.hip``, block-scaled K=64 MFMA) over the rank's rows + split-K reduction folded band
 by band, each band's RCCL all-reduce in flight while the next folds -> standardization + the
 4097-order solve on the device (``wls_large.hip``: assembly + Jacobi-PCG) -> model.  regParam 0.01
-/ elasticNet 0 (L2; an L1 penalty runs the device OWLQN over the dense standardized system,
-``models/owlqn_device.py``).
+/ elasticNet 0 (L2; an L1 penalty runs the cooperative-grid device OWLQN over the dense
+standardized system, ``ops/csrc/hip/wls_qn_grid.hip``, asynchronously).
 
 Features are stream-ingested straight into the fp8 fragment layout (64-row-aligned chunks, one
 global per-feature scale) — the 41 GB matrix never exists in a wider dtype.

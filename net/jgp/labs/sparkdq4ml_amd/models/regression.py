@@ -19,6 +19,8 @@ from __future__ import annotations
 
 from typing import Optional
 
+import os
+
 import numpy as np
 import torch
 
@@ -247,6 +249,12 @@ class LinearRegression(_LRParams):
             # for this solve, see scanfuse.try_fused_gram)
             overlap = False
         else:
+            pipe = _pipe_stream(df, tbl) if overlap else None
+            if pipe is not None:
+                with torch.cuda.stream(pipe):
+                    flat, checks = self._wls_stats(df, tbl, X, y, d, overlap)
+                    _rank_health(df)
+                    return self._wls_finish(df, flat, d, checks, overlap)
             flat, checks = self._wls_stats(df, tbl, X, y, d, overlap)
         _rank_health(df)
         return self._wls_finish(df, flat, d, checks, overlap)
@@ -396,6 +404,29 @@ def _async_fit(df, flat, d, args) -> bool:
 
 
 _tail_streams = {}
+_pipe_streams = {}
+
+
+def _pipe_stream(df, tbl):
+    """Compute stream for this asynchronous fit's statistics pass (``dq4ml.fit.pipeline``, default
+    2): consecutive fits alternate over that many streams, each ordered after the caller's stream,
+    so fit k+1's Gram blocks start on the CUs that fit k's drain frees instead of waiting for
+    fit k's last block (the drain and launch are most of the ~25 us fixed cost of a pass).  Every
+    fit still runs its whole pass; results are per fit and unchanged.  None: the caller's stream."""
+    if not _async_conf(df):
+        return None
+    sess = df.sparkSession
+    depth = int(os.environ.get("DQ4ML_FIT_PIPELINE") or sess.conf.get("dq4ml.fit.pipeline", "2"))
+    dev = getattr(sess, "device", None)
+    if depth < 2 or dev is None or dev.type != "cuda":
+        return None
+    ring = _pipe_streams.get(dev)
+    if ring is None or len(ring[1]) != depth:
+        ring = _pipe_streams[dev] = [0, [torch.cuda.Stream(device=dev) for _ in range(depth)]]
+    st = ring[1][ring[0] % depth]
+    ring[0] += 1
+    st.wait_stream(torch.cuda.current_stream(dev))
+    return st
 
 
 def _tail_stream(dev) -> "torch.cuda.Stream":

@@ -60,6 +60,12 @@ for s in $STEPS; do
     qn) step qn_t 600 python -u -m pytest tests/test_gpu_owlqn.py -m gpu -v --timeout 120 --timeout-method thread &&
         step qn_b 600 python scripts/owlqn_bench.py &&
         step qn_bt 600 env DQ4ML_QN_ENGINE=torch CASES=4096:0.01 python scripts/owlqn_bench.py || exit $? ;;
+    pipe) step pipe_t 600 python -u -m pytest tests/test_gpu_fit_pipeline.py tests/test_gpu_pipeline.py tests/test_gpu_determinism.py tests/test_gpu_owlqn.py -m gpu -q --timeout 120 --timeout-method thread &&
+          for r in 1 2; do for m in 1 2; do
+            step pipe_${m}_s${r} 300 env DQ4ML_FIT_PIPELINE=$m python bench.py --steps 200 --warmup 20 --rows 1.25e7 &&
+            step pipe_${m}_f${r} 300 env DQ4ML_FIT_PIPELINE=$m DQ4ML_FORCE_COLLECTIVES=1 python bench.py --steps 200 --warmup 20 --rows 1.25e7 &&
+            step pipe_${m}_q${r} 300 env DQ4ML_FIT_PIPELINE=$m python bench.py --steps 100 --warmup 10 --rows 2.5e7 &&
+            step pipe_${m}_h${r} 300 env DQ4ML_FIT_PIPELINE=$m python bench.py --steps 30 --warmup 5 || exit $?; done; done ;;
     cfg4rs64) step cfg4rs64 900 env DQ4ML_GRAM_STREAM_F32RS=64 python benchmarks/bench_dq_pipeline.py --steps 5 --warmup 2 ;;
     cfg4ring3) step cfg4ring3 900 env DQ4ML_GRAM_STREAM_RING=3 python benchmarks/bench_dq_pipeline.py --steps 5 --warmup 2 ;;
     cfg4nodqs) step cfg4nodqs 900 env DQ4ML_DQ_STREAM=0 python benchmarks/bench_dq_pipeline.py --steps 5 --warmup 2 ;;
