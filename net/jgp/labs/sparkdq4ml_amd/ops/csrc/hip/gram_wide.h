@@ -45,6 +45,11 @@ void gram_wide(int eb, WideArgs a, const int* pairs_dev, const float* scales, do
 // zeroed here on the stream)
 void gram_wide_queue(int eb, WideArgs a, const int* pairs_dev, const float* scales, double* out, int* heads, int h,
                      int grid, hipStream_t st, int waves = 8, bool fold = true);
+// gang schedule: grid blocks (one per CU, a multiple of 8) of 8 waves; group b % 8 owns splits
+// [g*S, g*S+S) (a.splitk == 8*S); pairs_dev lists the P(P+1)/2 pairs I <= J < npanels (diagonal
+// units also write the augmentation tiles)
+void gram_wide_gang(int eb, WideArgs a, const int* pairs_dev, const float* scales, double* out, int S, int grid,
+                    hipStream_t st, bool fold = true);
 // fold the pairs of panel columns [J0, J1) (J = npanels: the augmentation column -> the head of
 // the flat layout) into out (f64) or out32 (f32 wire buffer, same flat indexing)
 void gram_wide_fold(WideArgs a, const float* scales, double* out, float* out32, int J0, int J1, hipStream_t st);

@@ -103,7 +103,10 @@ struct StageFrags {
 
 // One (pair, split) block's K loop + epilogue.  MODE 0: off-diagonal panel pair; 3: diagonal pair
 // (one panel, loaded once); 1: (I, augmentation);
-// 2: (augmentation, augmentation).  Separate instantiations keep the accumulators in AGPRs with no
+// 2: (augmentation, augmentation).  Gang schedule (8 waves): a diagonal unit also carries the
+// augmentation products of its panel — it loads panel I plus the augmentation tile, and the two
+// waves whose 128 x 64 tiles lie entirely below the diagonal (wm = 1, wn < 2) compute (I, aug)
+// instead (MODE 5; panel I = 0 adds (aug, aug)); the other six are MODE 4.  Separate instantiations keep the accumulators in AGPRs with no
 // control-flow merge inside the loop (a merge there costs a full AGPR<->VGPR copy per stage).
 //
 // Schedule per stage i (fragments of stage i already in registers `cur`):
@@ -132,6 +135,8 @@ __device__ __forceinline__ void syrk_block(const WideArgs& a, unsigned char* sme
   // read tile 1); a diagonal pair (MODE 3) loads its one panel once
   constexpr int LA = MODE == 2 ? 1 : kLoadsPerPanel;
   constexpr int LB = MODE == 3 ? 0 : (MODE >= 1 ? 1 : kLoadsPerPanel);
+  constexpr bool kDiagPanel = MODE == 3 || MODE == 4;  // B operand = the A panel
+  constexpr bool kFullWave = MODE == 0 || kDiagPanel;
   constexpr int kLoadsPerStage = LA + LB;
   typedef StageFrags<F, WN> SF;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -151,7 +156,7 @@ __device__ __forceinline__ void syrk_block(const WideArgs& a, unsigned char* sme
     const int64_t tile_off = (int64_t)(o >> 11) * Tr::kTileStride + (o & (kChunk - 1));
     srcA[r] = MODE == 2 ? (o < kChunk ? a.Xaug + o : a.zeros + o)
                         : a.X + (int64_t)I * kTilesPerPanel * Tr::kTileStride + tile_off;
-    srcB[r] = (MODE == 1 || MODE == 2) ? (o < kChunk ? a.Xaug + o : a.zeros + o)
+    srcB[r] = MODE >= 1 && MODE != 3 ? (o < kChunk ? a.Xaug + o : a.zeros + o)
                                         : a.X + (int64_t)J * kTilesPerPanel * Tr::kTileStride + tile_off;
   }
   // stages at or beyond cnt stream the zero page: the K loop then runs an even number of stages
@@ -179,9 +184,9 @@ __device__ __forceinline__ void syrk_block(const WideArgs& a, unsigned char* sme
   };
   auto read = [&](SF& f, int buf) {
     const unsigned char* A = smem + buf * kStageBytes;
-    const unsigned char* B = MODE == 3 ? A : A + kPanelStage;
-    const int ta = MODE == 2 ? (wm == 0 ? 0 : 1) : wm * 4;                        // first A tile
-    const int tb = (MODE == 1 || MODE == 2) ? (wn == 0 ? 0 : 1) : wn * WN;       // first B tile
+    const unsigned char* B = kDiagPanel ? A : A + kPanelStage;
+    const int ta = MODE == 2 ? (wm == 0 ? 0 : 1) : (MODE == 5 ? wn * 4 : wm * 4);  // first A tile
+    const int tb = (MODE == 1 || MODE == 2) ? (wn == 0 ? 0 : 1) : (MODE == 5 ? 0 : wn * WN);  // first B tile
 #pragma unroll
     for (int kk = 0; kk < Tr::kSteps; ++kk) {
 #pragma unroll
@@ -189,7 +194,7 @@ __device__ __forceinline__ void syrk_block(const WideArgs& a, unsigned char* sme
         if (MODE != 2 || x == 0) f.a[kk][x] = Tr::read(A + (ta + x) * kChunk, kk, lane);
 #pragma unroll
       for (int y = 0; y < WN; ++y)
-        if (MODE == 0 || MODE == 3 || y == 0) f.b[kk][y] = Tr::read(B + (tb + y) * kChunk, kk, lane);
+        if (kFullWave || y == 0) f.b[kk][y] = Tr::read(B + (tb + y) * kChunk, kk, lane);
     }
   };
 
@@ -218,10 +223,13 @@ __device__ __forceinline__ void syrk_block(const WideArgs& a, unsigned char* sme
         if (MODE == 2 && x != 0) continue;
 #pragma unroll
         for (int y = 0; y < WN; ++y) {
-          if ((MODE == 1 || MODE == 2) && y != 0) continue;
+          if (!kFullWave && y != 0) continue;
           acc[x][y] = Tr::mfma(f.a[kk][x], f.b[kk][y], acc[x][y]);
         }
       }
+    if (MODE == 5 && x0 == 0)  // (aug, aug) into the wave's free accumulator (kept for I == 0)
+#pragma unroll
+      for (int kk = 0; kk < Tr::kSteps; ++kk) acc[0][1] = Tr::mfma(f.b[kk][0], f.b[kk][0], acc[0][1]);
   };
   // one stage: MFMAs(A tiles 0-1 of cur) | vmcnt: stage i+1 landed | s_barrier | MFMAs(A tiles
   // 2-3 of cur) interleaved with ds_read stage i+1 -> nxt and glds stage i+RING into the buffer
@@ -240,7 +248,7 @@ __device__ __forceinline__ void syrk_block(const WideArgs& a, unsigned char* sme
     mfmas(cur, 2);
     read(nxt, nb);
     issue(i + RING, rb);
-    if (MODE == 0 || MODE == 3) {
+    if (kFullWave) {
 #pragma unroll
       for (int g = 0; g < 2 * WN; ++g) {
         __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                  // 1 MFMA
@@ -271,6 +279,19 @@ __device__ __forceinline__ void syrk_block(const WideArgs& a, unsigned char* sme
       step(f1, f0, i + 1);
     }
     wait_vm<0>();  // drain the zero-page prefetches before the block can exit
+  }
+  if constexpr (MODE == 5) {  // (I, aug): 256 rows x the augmentation tile's 32 columns
+    float* out = a.part + ((int64_t)pair_index(I, a.npanels, a.npanels) * a.splitk + split) * kPanel * kPanel;
+#pragma unroll
+    for (int x = 0; x < 4; ++x)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) out[(wn * 128 + x * 32 + mfma32_row(lane, r)) * kPanel + mfma32_col(lane)] = acc[x][0][r];
+    if (I == 0 && wn == 0) {
+      float* o2 = a.part + ((int64_t)pair_index(a.npanels, a.npanels, a.npanels) * a.splitk + split) * kPanel * kPanel;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) o2[mfma32_row(lane, r) * kPanel + mfma32_col(lane)] = acc[0][1][r];
+    }
+    return;
   }
   // f32 partial tile [256][256] of this (pair, split)
   float* out = a.part + ((int64_t)pair_index(I, J, a.npanels) * a.splitk + split) * kPanel * kPanel;
@@ -332,6 +353,35 @@ __global__ __launch_bounds__(64 * WAVES, 1) void gram_wide_queue_kernel(WideArgs
     else if (J != a.npanels) syrk_block<EB, 0, RING, WAVES>(a, smem, I, J, pos, split);
     else if (I != a.npanels) syrk_block<EB, 1, RING, WAVES>(a, smem, I, J, pos, split);
     else syrk_block<EB, 2, RING, WAVES>(a, smem, I, J, pos, split);
+  }
+}
+
+
+// Gang schedule (one block per CU, 8 waves): group g = b % 8 (one XCD under round-robin dispatch)
+// owns the row ranges [g*S, g*S+S) and its G blocks walk the unit list (range-major, then the
+// P(P+1)/2 panel pairs I <= J < P in Z-order; a diagonal unit carries its augmentation products)
+// statically: block l takes units l, l + G, l + 2G, ...  Every unit costs about the same (a
+// diagonal unit's busiest SIMD runs as many MFMAs as an off-diagonal one's), so the G blocks of a
+// group stay in step: round k runs units [kG, kG + G) of ONE row range (two at a range boundary),
+// every panel-stage is fetched from HBM / MALL once per round and served from the XCD's L2 to the
+// other blocks of the round.  The queue schedule's blocks drift apart (unequal unit costs,
+// dynamic dequeue), so there each block re-fetched its panels (L2 hit 61 %, ~6.6x the unique
+// bytes from the fabric).  S is chosen on the host so that npu * S is a multiple of G.
+template <int EB, int RING>
+__global__ __launch_bounds__(512, 1) void gram_wide_gang_kernel(WideArgs a, int S) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int g = blockIdx.x & 7, l = blockIdx.x >> 3, G = gridDim.x >> 3;
+  const int P = a.npanels, npu = P * (P + 1) / 2, units = npu * S;
+  const int wave = threadIdx.x >> 6;
+  const bool aug_wave = (wave >> 2) == 1 && (wave & 3) < 2;
+  for (int u = l; u < units; u += G) {
+    const int s = u / npu, pos = u - s * npu;
+    const int split = g * S + s;
+    const int I = a.pairs[2 * pos], J = a.pairs[2 * pos + 1];
+    if (I != J) syrk_block<EB, 0, RING, 8>(a, smem, I, J, 0, split);
+    else if (aug_wave) syrk_block<EB, 5, RING, 8>(a, smem, I, J, 0, split);
+    else syrk_block<EB, 4, RING, 8>(a, smem, I, J, 0, split);
+    __syncthreads();  // every wave is done reading the ring before the next unit's first glds
   }
 }
 
@@ -616,6 +666,26 @@ void gram_wide_queue(int eb, WideArgs a, const int* pairs_dev, const float* scal
   DQ_HIP_CHECK(hipMemsetAsync(heads, 0, 8 * sizeof(int), st));
   if (eb == 16) waves == 8 ? launch_wide_queue<16, 4, 8>(a, grid, heads, h, st) : launch_wide_queue<16, 4, 4>(a, grid, heads, h, st);
   else waves == 8 ? launch_wide_queue<8, 4, 8>(a, grid, heads, h, st) : launch_wide_queue<8, 4, 4>(a, grid, heads, h, st);
+  if (fold) launch_fold(a, scales, out, nullptr, 0, a.npanels + 1, st);
+}
+
+template <int EB>
+static void launch_wide_gang(const WideArgs& a, int grid, int S, hipStream_t st) {
+  const size_t lds = (size_t)5 * kStageBytes;
+  DQ_HIP_CHECK(hipFuncSetAttribute((const void*)gram_wide_gang_kernel<EB, 5>,
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  hipLaunchKernelGGL((gram_wide_gang_kernel<EB, 5>), dim3(grid), dim3(512), lds, st, a, S);
+  DQ_HIP_CHECK(hipGetLastError());
+}
+
+void gram_wide_gang(int eb, WideArgs a, const int* pairs_dev, const float* scales, double* out, int S, int grid,
+                    hipStream_t st, bool fold) {
+  a.pairs = pairs_dev;
+  if (S < 1 || a.splitk != 8 * S) throw std::invalid_argument("gram_wide_gang: splitk must be 8 * S");
+  if (grid < 8 || grid % 8) throw std::invalid_argument("gram_wide_gang: grid must be a positive multiple of 8");
+  if ((int64_t)a.splitk > a.nsup) throw std::invalid_argument("gram_wide_gang: more row ranges than supersteps");
+  if (eb == 16) launch_wide_gang<16>(a, grid, S, st);
+  else launch_wide_gang<8>(a, grid, S, st);
   if (fold) launch_fold(a, scales, out, nullptr, 0, a.npanels + 1, st);
 }
 

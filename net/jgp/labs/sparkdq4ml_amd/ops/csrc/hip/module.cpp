@@ -227,6 +227,14 @@ PYBIND11_MODULE(_dq4ml_hip, m) {
     gram_wide_queue(eb, a, P<const int>(pairs), P<const float>(scales), P<double>(out), P<int>(heads), h, grid,
                     as_stream(stream), waves, fold);
   });
+  m.def("gram_wide_gang", [wide_args](int eb, uintptr_t X, uintptr_t Xaug, uintptr_t zeros, int nt, int npanels,
+                                      int d, int64_t nsup, int S, uintptr_t pairs, uintptr_t part, double s1,
+                                      double syh, double syl, uintptr_t scales, uintptr_t out, int grid,
+                                      uintptr_t stream, bool fold) {
+    WideArgs a = wide_args(X, Xaug, zeros, nt, npanels, d, nsup, 8 * S, part, s1, syh, syl);
+    gram_wide_gang(eb, a, P<const int>(pairs), P<const float>(scales), P<double>(out), S, grid, as_stream(stream),
+                   fold);
+  });
   m.def("gram_wide_fold", [wide_args](int npanels, int d, int splitk, uintptr_t part, double s1, double syh,
                                       double syl, uintptr_t scales, uintptr_t out, uintptr_t out32, int J0, int J1,
                                       uintptr_t stream) {

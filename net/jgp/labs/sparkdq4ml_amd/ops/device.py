@@ -948,6 +948,29 @@ def _wide_queue_h(nsup: int) -> int:
     return max(1, min(hq, nsup // 16))
 
 
+def _wide_gang_s(P: int, nsup: int, G: int) -> int:
+    """Row ranges per XCD group of the gang schedule (0: not applicable).  The P(P+1)/2 units of a
+    range times S must be a multiple of the G blocks of a group, so every block runs the same
+    number of equal-cost units (P = 16, G = 32: S = 4, 17 units per block); f32 accumulators
+    count rows exactly only below 2^24 per split, and every split keeps >= 16 supersteps."""
+    npu = P * (P + 1) // 2
+    s_min = max(1, -(-nsup * 64 // (8 << 23)))
+    forced = int(os.environ.get("DQ4ML_WIDE_GANG_S", "0"))  # (tests / A/B) a fixed S
+    if forced:
+        return forced if s_min <= forced and 8 * forced <= nsup else 0
+    best, best_eff = 0, 0.0
+    for S in range(s_min, s_min + 32):
+        if nsup < 8 * S * 16:
+            break
+        units = npu * S
+        eff = units / (-(-units // G) * G)
+        if eff > best_eff + 1e-9:
+            best, best_eff = S, eff
+        if eff == 1.0:
+            break
+    return best if best_eff >= 0.9 else 0
+
+
 _wide_grids = {}
 
 
@@ -1000,19 +1023,31 @@ def _gram_wide(h, T: TiledWide, y, w, sel, x_zero_dead):
         pairs = [(0, 1)] * len(pairs)
     pairs_dev = _h2d(np.asarray(pairs, dtype=np.int32).reshape(-1), dev)
     out = torch.empty(5 + 2 * d + d * (d + 1) // 2, dtype=torch.float64, device=dev)
-    sched = os.environ.get("DQ4ML_WIDE_SCHED", "queue")
+    sched = os.environ.get("DQ4ML_WIDE_SCHED", "gang")
+    waves = int(os.environ.get("DQ4ML_WIDE_WAVES", "8"))
+    gs = _wide_gang_s(P, nsup, _wide_grid(h) // 8) if sched == "gang" and waves == 8 else 0
+    if sched == "gang" and not gs:
+        sched = "queue"
     hq = _wide_queue_h(nsup) if sched == "queue" else 0
     # data-parallel fit over RCCL: fold band by band and all-reduce each band while the next folds
     banded = comm.collectives_active() and comm.backend() == "nccl"
-    if hq:
+    if gs:
+        # gang schedule (gram_wide_gang_kernel): 8 groups x S row ranges, static equal-cost units
+        splitk = 8 * gs
+        gpairs = [p for p in pairs if p[1] < P]
+        gpairs_dev = _h2d(np.asarray(gpairs, dtype=np.int32).reshape(-1), dev)
+        part = torch.empty(int(h.gram_wide_partials(d, splitk)), dtype=torch.float32, device=dev)
+        h.gram_wide_gang(eb, T.buf.data_ptr(), aug.buf.data_ptr(), _zero_page(h, dev).data_ptr(), T.nt, P, d, nsup,
+                         gs, gpairs_dev.data_ptr(), part.data_ptr(), 1.0, float(s_h), float(s_l), _ptr(T.scales),
+                         out.data_ptr(), _wide_grid(h), _stream(), not banded)
+    elif hq:
         # persistent XCD-grouped schedule (gram_wide_queue_kernel): 8 groups x h row ranges
         splitk = 8 * hq
         part = torch.empty(int(h.gram_wide_partials(d, splitk)), dtype=torch.float32, device=dev)
         heads = torch.empty(8, dtype=torch.int32, device=dev)
         h.gram_wide_queue(eb, T.buf.data_ptr(), aug.buf.data_ptr(), _zero_page(h, dev).data_ptr(), T.nt, P, d, nsup,
                           hq, pairs_dev.data_ptr(), part.data_ptr(), 1.0, float(s_h), float(s_l), _ptr(T.scales),
-                          out.data_ptr(), heads.data_ptr(), _wide_grid(h), _stream(),
-                          int(os.environ.get("DQ4ML_WIDE_WAVES", "8")), not banded)
+                          out.data_ptr(), heads.data_ptr(), _wide_grid(h), _stream(), waves, not banded)
     else:
         part = torch.empty(int(h.gram_wide_partials(d, splitk)), dtype=torch.float32, device=dev)
         h.gram_wide(eb, T.buf.data_ptr(), aug.buf.data_ptr(), _zero_page(h, dev).data_ptr(), T.nt, P, d, nsup,

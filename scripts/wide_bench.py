@@ -48,7 +48,10 @@ for _ in range(reps):
         if same:
             os.environ["DQ4ML_WIDE_SAMEPAIR"] = "1"
         sched = "grid"
-        if fields[-1].startswith("q"):  # ...:q<h> = persistent XCD-grouped queue schedule, h row ranges/group
+        if fields[-1] == "gang":  # ...:gang = static equal-cost XCD gang schedule (the default)
+            sched = "gang"
+            fields = fields[:-1]
+        elif fields[-1].startswith("q"):  # ...:q<h> = persistent XCD-grouped queue schedule, h row ranges/group
             sched, hq = "queue", fields[-1][1:]
             fields = fields[:-1]
             os.environ["DQ4ML_WIDE_H"] = hq

@@ -179,3 +179,66 @@ def test_pack_mixed_dtypes_and_misaligned_columns(wide):
     dense = torch.stack([c.float() for c in cols]) * sel
     T = device.pack_wide(cols, 16, sel) if wide else device.pack_tiled(cols, sel)
     assert torch.equal(T.to_dense().float(), dense.to(torch.bfloat16).float())
+
+
+@gpu
+@pytest.mark.parametrize("eb", [16, 8])
+@pytest.mark.parametrize("sched", ["gang", "queue", "grid"])
+@pytest.mark.parametrize("d", [300, 1100])
+def test_wide_schedules_match_oracle(eb, sched, d, monkeypatch):
+    # every SYRK schedule (the gang's merged diagonal + augmentation units included) gives the
+    # same statistics as the fp64 oracle of the stored (quantized) values
+    _hip()
+    from net.jgp.labs.sparkdq4ml_amd.ops import device
+
+    monkeypatch.setenv("DQ4ML_WIDE_SCHED", sched)
+    monkeypatch.setenv("DQ4ML_WIDE_GANG_S", "2")
+    monkeypatch.setenv("DQ4ML_WIDE_H", "1")
+    n = 70_001
+    g = torch.Generator(device="cuda").manual_seed(d + eb)
+    X = torch.randn(d, n, generator=g, device="cuda") + 0.2
+    y = torch.randn(n, generator=g, device="cuda", dtype=torch.float64) * 3 + 1
+    sel = torch.rand(n, generator=g, device="cuda") > 0.2
+    T = device.pack_wide([X.to(torch.bfloat16) if eb == 16 else X], eb, sel)
+    out = device.gram_stats(T, y, None, sel, "bf16" if eb == 16 else "fp8", x_zero_dead=True)
+    Xq = T.to_dense().double()
+    live = sel.double()
+    s, a, ab, aa = _parts(out, d)
+    assert s[0] == float(sel.sum())
+    ref_a = (Xq * live).sum(1).cpu()
+    assert _rel(a, ref_a) < 1e-5
+    assert _rel(ab, (Xq * (y * live)).sum(1).cpu()) < (1e-4 if eb == 16 else 1e-2)
+    G = (Xq * live) @ Xq.T
+    ii, jj = torch.triu_indices(d, d, device="cuda")  # packed upper: (i, j), i <= j at j(j+1)/2 + i
+    ref = torch.empty(d * (d + 1) // 2, dtype=torch.float64, device="cuda")
+    ref[jj * (jj + 1) // 2 + ii] = G[ii, jj]
+    assert _rel(aa, ref.cpu()) < 1e-5
+
+
+@gpu
+def test_wide_gang_full_width_matches_queue():
+    # BASELINE config-5 width (P = 16 panels: S = 4, 17 equal units per block of the gang)
+    _hip()
+    import os
+
+    from net.jgp.labs.sparkdq4ml_amd.ops import device
+
+    d, n = 4096, 40_000
+    g = torch.Generator(device="cuda").manual_seed(5)
+    X = torch.randn(d, n, generator=g, device="cuda")
+    y = torch.randn(n, generator=g, device="cuda", dtype=torch.float64)
+    T = device.pack_wide([X], 8, None)
+    outs = {}
+    for sched in ("gang", "queue"):
+        os.environ["DQ4ML_WIDE_SCHED"] = sched
+        try:
+            outs[sched] = device.gram_stats(T, y, None, None, "fp8", x_zero_dead=True)
+        finally:
+            os.environ.pop("DQ4ML_WIDE_SCHED", None)
+    assert _rel(outs["gang"], outs["queue"]) < 1e-6
+    Xq = T.to_dense().double()
+    G = Xq @ Xq.T
+    dg = outs["gang"][5 + 2 * d:]
+    j = torch.arange(d, device="cuda")
+    assert _rel(dg[j * (j + 1) // 2 + j].cpu(), G.diagonal().cpu()) < 5e-5  # f32 sums of 1250-row splits
+    assert _rel(dg[j * (j + 1) // 2].cpu(), G[0].cpu()) < 5e-5
