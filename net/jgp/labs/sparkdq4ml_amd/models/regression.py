@@ -24,12 +24,14 @@ import os
 import numpy as np
 import torch
 
-from ..ops import kernels
+from ..ops import device, kernels, native
+from ..ops.layout import TiledBF16
 from ..parallel import comm
 from ..sql.dataframe import DataFrame
+from ..runtime import faststream
 from ..runtime.checks import defer, verify
 from ..sql.expressions import AnalysisException, ColRef, EvalContext, Expr, SparkException
-from ..sql.plan import Project, execute
+from ..sql.plan import Filter, Project, execute
 from ..sql.table import ColumnData
 from ..sql.types import DoubleType, VectorUDT, is_numeric
 from ..utils.logging import get_logger
@@ -151,6 +153,9 @@ def _fused_scan_stats(params, df: DataFrame):
     chain in its stage prologue for bf16 / f32 statistics over in-memory columns
     (``streamfuse.try_fused_stream``), when the DataFrame is that shape and the fit is an
     unweighted normal-equation one; else None."""
+    p0 = df._plan  # both fused paths need an unevaluated Project / Filter chain on top
+    if not isinstance(p0, (Project, Filter)) or p0._memo is not None:
+        return None
     if params.getOrDefault("loss") != "squaredError" or params.getOrDefault("solver") not in ("auto", "normal"):
         return None
     if params.isSet("weightCol") and params.getOrDefault("weightCol"):
@@ -223,6 +228,11 @@ class LinearRegression(_LRParams):
         return load_params_only(cls, path)
 
     def _train(self, df: DataFrame) -> "LinearRegressionModel":
+        rp = self.__dict__.get("_replay")
+        if rp is not None:
+            if rp.valid(self, df):
+                return rp.issue(self, df)
+            self._replay = None
         fused = _fused_scan_stats(self, df)
         if fused is not None:
             return self._train_wls(df, None, None, None, fused.d, fused)
@@ -240,6 +250,7 @@ class LinearRegression(_LRParams):
         return train_lbfgs(self, df, tbl, X, y, d)
 
     def _train_wls(self, df, tbl, X, y, d, fused=None):
+        self.__dict__.pop("_tiled_plan", None)  # set by THIS fit's _wls_stats only
         sess = getattr(df, "sparkSession", None)
         overlap = sess is not None and str(sess.conf.get("dq4ml.fit.overlapTail", "true")).lower() in ("1", "true")
         if fused is not None:  # statistics already reduced by the fused CSV scan kernel
@@ -251,11 +262,16 @@ class LinearRegression(_LRParams):
         else:
             pipe = _pipe_stream(df, tbl) if overlap else None
             if pipe is not None:
-                with torch.cuda.stream(pipe):
+                with faststream.use(pipe):
                     flat, checks = self._wls_stats(df, tbl, X, y, d, overlap)
                     _rank_health(df)
-                    return self._wls_finish(df, flat, d, checks, overlap)
+                    model = self._wls_finish(df, flat, d, checks, overlap)
+                plan = self.__dict__.pop("_tiled_plan", None)
+                if plan is not None and model.__dict__.get("_pending") is not None:
+                    self._replay = _FitReplay(self, df, plan, checks, d)
+                return model
             flat, checks = self._wls_stats(df, tbl, X, y, d, overlap)
+            self.__dict__.pop("_tiled_plan", None)
         _rank_health(df)
         return self._wls_finish(df, flat, d, checks, overlap)
 
@@ -287,27 +303,29 @@ class LinearRegression(_LRParams):
                 # queue behind its HBM stream (8 us alone, ~100 us co-running), and the side stream
                 # must still fit the all-reduce and the solve into one Gram period
                 defer = overlap and _async_conf(df) and d <= 64 and not comm.collectives_active()
-                flat = kernels.gram_stats(X.values, yv, w, sel, gd, x_zero_dead=x_zero_dead, defer=defer)
+                if _replayable(X.values, w):
+                    # resolve the launch once: a repeated fit of this DataFrame replays it
+                    plan = device.TiledGramPlan(native.hip(), X.values, yv, None, sel, x_zero_dead)
+                    flat = plan.launch(device._stream(), defer)
+                    self._tiled_plan = (plan, defer)
+                else:
+                    flat = kernels.gram_stats(X.values, yv, w, sel, gd, x_zero_dead=x_zero_dead, defer=defer)
         tracing.add_rows("gram", tbl.nrows)
         return flat, checks
 
     def _wls_finish(self, df, flat, d, checks, overlap):
-        args = (flat, d, self.getOrDefault("fitIntercept"), float(self.getOrDefault("regParam")),
-                float(self.getOrDefault("elasticNetParam")), bool(self.getOrDefault("standardization")), True,
-                "auto", int(self.getOrDefault("maxIter")), float(self.getOrDefault("tol")))
+        args = (flat,) + _wls_args(self, d)[1:]
         if _async_fit(df, flat, d, args):
             # dq4ml.fit.overlapTail: fit tail (Gram fold + X1 all-reduce + device solve) on a side
             # stream, so it overlaps whatever the caller enqueues next on the compute stream (the
             # next fit's Gram pass) instead of following it (in-process A/B, 1x MI355X, d = 32:
             # 159.3 -> 151.7 us per fit at 1.25e7 rows, 1033 -> 1025 us at 1e8; scripts/overlap_ab.py)
+            # (the tail stays on the side stream for a pipelined fit too: on its pipeline stream the
+            # one-workgroup solve co-runs with the next fit's whole-GPU Gram, gets a sliver of a CU
+            # and holds up the fit after that -- same-box A/B 0.142-0.184 vs 0.137 ms per fit)
             with tracing.span("solve"):
                 pending = _PendingWLS(args, overlap=overlap, checks=checks)  # resolved on first read
-            model = LinearRegressionModel(self.uid, None, 0.0)
-            model._pending = pending
-            self.copyValues(model)
-            model._set_summary(LinearRegressionTrainingSummary(model, df, pending, None, stats=pending,
-                                                               solver=pending))
-            return model
+            return _async_model(self, df, pending)
         if hasattr(flat, "finish"):
             flat = flat.finish()
         with tracing.span("allreduce"):
@@ -324,6 +342,81 @@ class LinearRegression(_LRParams):
         model._set_summary(LinearRegressionTrainingSummary(model, df, wls, wls.objectiveHistory,
                                                            stats=stats, solver=wls.solver))
         return model
+
+
+def _wls_args(est, d):
+    """``fit_wls_flat`` arguments after ``flat``, from the estimator's params."""
+    return (None, d, est.getOrDefault("fitIntercept"), float(est.getOrDefault("regParam")),
+            float(est.getOrDefault("elasticNetParam")), bool(est.getOrDefault("standardization")), True,
+            "auto", int(est.getOrDefault("maxIter")), float(est.getOrDefault("tol")))
+
+
+def _async_model(est, df, pending) -> "LinearRegressionModel":
+    """The model of an asynchronous fit: coefficients and summary resolve on first read."""
+    model = LinearRegressionModel(est.uid, None, 0.0)
+    model._pending = pending
+    est.copyValues(model)
+    model._set_summary(LinearRegressionTrainingSummary(model, df, pending, None, stats=pending, solver=pending))
+    return model
+
+
+def _replay_env():
+    # the knobs that change what a replayed fit would enqueue (DQ4ML_FORCE_COLLECTIVES acts
+    # through comm.collectives_active(), compared separately; DQ4ML_GRAM_FOLD only picks between
+    # two equal-result fold kernels and is read when the replay is recorded)
+    return os.environ.get("DQ4ML_FIT_REPLAY"), os.environ.get("DQ4ML_FIT_PIPELINE")
+
+
+def _replayable(Xv, w) -> bool:
+    """The fit's Gram pass can be captured as a :class:`ops.device.TiledGramPlan`: bf16 fragment
+    tiles on the GPU, no weights, the separate fold kernel (not the opt-in in-kernel fold)."""
+    return (isinstance(Xv, TiledBF16) and w is None and Xv.buf.is_cuda and Xv.d <= 64
+            and os.environ.get("DQ4ML_GRAM_FOLD", "separate") != "kernel"
+            and os.environ.get("DQ4ML_FIT_REPLAY", "1") != "0")
+
+
+class _FitReplay:
+    """A repeated asynchronous fit of the SAME DataFrame by the same estimator (the benchmark loop,
+    cross-validation folds over one cached table, a refit after ``transform``): the table, its
+    columns, the checks and the Gram launch are those of the first fit, so the replay only
+    allocates outputs and enqueues the pass, the fold, the all-reduce and the solve -- none of the
+    plan walking, schema resolution, column pruning and operand preparation of ``_train``.
+
+    Valid while the estimator's params, the session conf, the collectives state and the
+    dispatch-relevant ``DQ4ML_*`` knobs equal those of the recorded fit, and tracing is off (a
+    traced fit takes the full path to record its spans); anything else drops the replay."""
+
+    __slots__ = ("df", "pmap", "conf", "env", "coll", "plan", "defer", "checks", "d", "args", "ring", "dev")
+
+    def __init__(self, est, df, plan_defer, checks, d):
+        import weakref
+
+        self.df = weakref.ref(df)
+        self.pmap = dict(est._paramMap)
+        self.conf = dict(df.sparkSession.conf._conf)
+        self.env = _replay_env()
+        self.coll = comm.collectives_active()
+        self.plan, self.defer = plan_defer
+        self.checks, self.d = list(checks), d
+        self.args = _wls_args(est, d)[1:]
+        self.dev = faststream.dev_index(df.sparkSession.device)
+        self.ring = _pipe_streams[df.sparkSession.device]
+
+    def valid(self, est, df) -> bool:
+        return (self.df() is df and est._paramMap == self.pmap and df.sparkSession.conf._conf == self.conf
+                and _replay_env() == self.env and comm.collectives_active() == self.coll
+                and not tracing.enabled())
+
+    def issue(self, est, df):
+        ring = self.ring  # the pipeline streams (_pipe_stream without the conf / env reads)
+        pipe = ring[1][ring[0] % len(ring[1])]
+        ring[0] += 1
+        ps = pipe.cuda_stream
+        native.hip().stream_wait(ps, faststream.raw(self.dev))
+        with faststream.use(pipe):
+            flat = self.plan.launch(ps, self.defer)
+            pending = _PendingWLS((flat,) + self.args, overlap=True, checks=self.checks)
+        return _async_model(est, df, pending)
 
 
 def _num_features(X) -> int:
@@ -425,7 +518,7 @@ def _pipe_stream(df, tbl):
         ring = _pipe_streams[dev] = [0, [torch.cuda.Stream(device=dev) for _ in range(depth)]]
     st = ring[1][ring[0] % depth]
     ring[0] += 1
-    st.wait_stream(torch.cuda.current_stream(dev))
+    native.hip().stream_wait(st.cuda_stream, faststream.raw(faststream.dev_index(dev)))
     return st
 
 
@@ -445,8 +538,6 @@ class _PendingWLS:
     the RCCL kernel).  ``resolve()`` orders the caller's stream after the tail before reading."""
 
     def __init__(self, args, overlap: bool = False, checks=None):
-        from ..ops import device
-
         flat, d, fit_icpt, reg, enet, std_f, std_l = args[:7]
         max_iter, tol = args[8], args[9]
         self._done = None
@@ -460,18 +551,18 @@ class _PendingWLS:
         if hasattr(flat, "finish") and not overlap:
             flat = flat.finish()
         if overlap:
-            cur = torch.cuda.current_stream(flat.device)
+            h = native.hip()
+            self._dev = faststream.dev_index(flat.device)
             side = _tail_stream(flat.device)
-            side.wait_stream(cur)
-            with torch.cuda.stream(side):
+            h.stream_wait(side.cuda_stream, faststream.raw(self._dev))
+            with faststream.use(side):
                 if hasattr(flat, "finish"):
                     flat = flat.finish()  # Gram partial slabs -> flat statistics, on the side stream
                 flat.record_stream(side)  # produced on the compute stream, consumed here
                 with tracing.span("allreduce"):
                     flat = comm.all_reduce_sum(flat)
                 self.out = solve(flat)
-                self._done = torch.cuda.Event()
-                self._done.record(side)
+                self._done = h.event_record(side.cuda_stream)  # a native ring event of the side stream
         else:
             flat = comm.all_reduce_sum(flat)
             self.out = solve(flat)
@@ -482,7 +573,7 @@ class _PendingWLS:
         if self._res is None:
             flat, d = self.args[0], self.args[1]
             if self._done is not None:
-                torch.cuda.current_stream(flat.device).wait_event(self._done)
+                native.hip().stream_wait_event(faststream.raw(self._dev), self._done)
             host = self.out.cpu().numpy()
             verify(self._checks)  # data errors of the fit surface here, on first read
             if self._qn:

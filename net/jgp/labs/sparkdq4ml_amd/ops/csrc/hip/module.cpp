@@ -2,6 +2,10 @@
 // pointers (ints) plus the HIP stream handle of the calling torch stream; buffers are allocated by
 // the python side (ops/device.py) from torch's caching allocator, so there is no hipMalloc in any
 // launch path (graph-capturable) and kernels run on the same stream as the surrounding torch work.
+#include <map>
+#include <utility>
+#include <vector>
+
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
@@ -24,8 +28,49 @@ static T* P(uintptr_t p) {
   return reinterpret_cast<T*>(p);
 }
 
+// Reusable event rings for stream ordering on the asynchronous fit's issue path: torch's
+// wait_stream / Event create a Python Event object (and a HIP event) per call.  One ring per
+// (device, key): key 0 serves stream_wait (the wait is enqueued right after the record and keeps
+// the record it saw, whatever later records do); event_record keys its ring by the recording
+// stream, so a ring event is only ever re-recorded LATER on that same stream.
+static hipEvent_t ring_event(uintptr_t key) {
+  constexpr int kRing = 64;
+  struct Ring {
+    hipEvent_t ev[kRing];
+    int next = 0;
+  };
+  static std::map<std::pair<int, uintptr_t>, Ring*> rings;
+  int dev = 0;
+  DQ_HIP_CHECK(hipGetDevice(&dev));
+  Ring*& r = rings[{dev, key}];
+  if (!r) {
+    r = new Ring();
+    for (auto& e : r->ev) DQ_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  }
+  hipEvent_t e = r->ev[r->next];
+  r->next = (r->next + 1) % kRing;
+  return e;
+}
+
 PYBIND11_MODULE(_dq4ml_hip, m) {
   m.doc() = "dq4ml gfx950 kernels: MFMA Gram, fused DQ VM, compaction, pack, predict/metrics, CSV scan";
+
+  // dst waits for everything enqueued on src so far (stream.wait_stream without a torch Event)
+  m.def("stream_wait", [](uintptr_t dst, uintptr_t src) {
+    hipEvent_t e = ring_event(0);
+    DQ_HIP_CHECK(hipEventRecord(e, as_stream(src)));
+    DQ_HIP_CHECK(hipStreamWaitEvent(as_stream(dst), e, 0));
+  });
+  // a ring event recorded on st: re-recorded only on st, 64 records later, which only moves it
+  // later on the same stream -- waiting on it still orders after the original record
+  m.def("event_record", [](uintptr_t st) {
+    hipEvent_t e = ring_event(st);
+    DQ_HIP_CHECK(hipEventRecord(e, as_stream(st)));
+    return reinterpret_cast<uintptr_t>(e);
+  });
+  m.def("stream_wait_event", [](uintptr_t dst, uintptr_t ev) {
+    DQ_HIP_CHECK(hipStreamWaitEvent(as_stream(dst), reinterpret_cast<hipEvent_t>(ev), 0));
+  });
 
   m.def("device_info", []() {
     int dev = 0;

@@ -66,6 +66,9 @@ for s in $STEPS; do
             step pipe_${m}_f${r} 300 env DQ4ML_FIT_PIPELINE=$m DQ4ML_FORCE_COLLECTIVES=1 python bench.py --steps 200 --warmup 20 --rows 1.25e7 &&
             step pipe_${m}_q${r} 300 env DQ4ML_FIT_PIPELINE=$m python bench.py --steps 100 --warmup 10 --rows 2.5e7 &&
             step pipe_${m}_h${r} 300 env DQ4ML_FIT_PIPELINE=$m python bench.py --steps 30 --warmup 5 || exit $?; done; done ;;
+    pipeq) for r in 1 2; do for m in 1 2; do
+            step pipeq_${m}_s${r} 300 env DQ4ML_FIT_PIPELINE=$m python bench.py --steps 200 --warmup 20 --rows 1.25e7 &&
+            step pipeq_${m}_f${r} 300 env DQ4ML_FIT_PIPELINE=$m DQ4ML_FORCE_COLLECTIVES=1 python bench.py --steps 200 --warmup 20 --rows 1.25e7 || exit $?; done; done ;;
     cfg4rs64) step cfg4rs64 900 env DQ4ML_GRAM_STREAM_F32RS=64 python benchmarks/bench_dq_pipeline.py --steps 5 --warmup 2 ;;
     cfg4ring3) step cfg4ring3 900 env DQ4ML_GRAM_STREAM_RING=3 python benchmarks/bench_dq_pipeline.py --steps 5 --warmup 2 ;;
     cfg4nodqs) step cfg4nodqs 900 env DQ4ML_DQ_STREAM=0 python benchmarks/bench_dq_pipeline.py --steps 5 --warmup 2 ;;
@@ -98,6 +101,12 @@ for s in $STEPS; do
     bench8thasync) step bench8thasync 600 python bench.py --steps 50 --warmup 5 --rows 1.25e7 --async ;;
     bench8thrccl) step bench8thrccl 600 env DQ4ML_FORCE_COLLECTIVES=1 python bench.py --steps 50 --warmup 5 --rows 1.25e7 --async ;;
     kprof8thrccl) (export TMPDIR=/tmp DQ4ML_FORCE_COLLECTIVES=1; step kprof8thrccl 600 rocprofv3 --kernel-trace --stats -d gpurun_out/kprof8thrccl -o run --output-format csv -- python bench.py --steps 20 --warmup 5 --rows 1.25e7 --async) || exit $? ;;
+    hostt) step hostt 600 python -u -m pytest tests/test_gpu_async_fit.py tests/test_gpu_fit_pipeline.py tests/test_gpu_pipeline.py tests/test_gpu_determinism.py tests/test_gpu_owlqn.py tests/test_gpu_rccl.py tests/test_gpu_scanfuse.py -m gpu -q --timeout 120 --timeout-method thread ;;
+    replayab) for r in 1 2; do for m in 0 1; do
+            step replay_${m}_s${r} 300 env DQ4ML_FIT_REPLAY=$m python bench.py --steps 200 --warmup 20 --rows 1.25e7 &&
+            step replay_${m}_f${r} 300 env DQ4ML_FIT_REPLAY=$m DQ4ML_FORCE_COLLECTIVES=1 python bench.py --steps 200 --warmup 20 --rows 1.25e7 &&
+            step replay_${m}_i${r} 300 env DQ4ML_FIT_REPLAY=$m python scripts/host_overhead.py --rows 1e5 --steps 500 || exit $?; done; done ;;
+    hostprof) step hostprof 300 env HOSTOV_PROFILE=gpurun_out/hostprof python scripts/host_overhead.py --rows 1.25e7,1e5 --steps 300 ;;
     hostov) step hostov 300 python scripts/host_overhead.py && step hostovrccl 300 env DQ4ML_FORCE_COLLECTIVES=1 python scripts/host_overhead.py ;;
     f32pmc) (export TMPDIR=/tmp
        step f32pmc1 300 timeout -s KILL 240 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_SALU GRBM_GUI_ACTIVE -d gpurun_out/f32pmc1 -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --dtype fp32 &&

@@ -42,10 +42,26 @@ def main(argv=None):
             m = lr.fit(df)
         m.coefficients  # noqa: B018 (sync)
         torch.cuda.synchronize()
+        prof = os.environ.get("HOSTOV_PROFILE")  # write a cProfile summary of the issue loop here
+        if prof:
+            import cProfile
+            import io
+            import pstats
+
+            pr = cProfile.Profile()
+            pr.enable()
         t0 = time.perf_counter()
         for _ in range(a.steps):
             m = lr.fit(df)
         t1 = time.perf_counter()
+        if prof:
+            pr.disable()
+            buf = io.StringIO()
+            st = pstats.Stats(pr, stream=buf)
+            st.sort_stats("tottime").print_stats(45)
+            st.sort_stats("cumulative").print_stats(60)
+            with open(f"{prof}.{n}.txt", "w") as f:
+                f.write(buf.getvalue())
         torch.cuda.synchronize()
         t2 = time.perf_counter()
         print(json.dumps({"rows": n, "steps": a.steps, "issue_us_per_fit": (t1 - t0) / a.steps * 1e6,

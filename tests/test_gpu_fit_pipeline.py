@@ -32,3 +32,44 @@ def test_pipelined_fits_equal_serial_fits(gpu_session, dtype, monkeypatch):
         assert piped[-1].summary.r2 == serial[0].summary.r2
     finally:
         gpu_session.conf.set("dq4ml.fit.async", "false")
+
+
+def test_fit_replay_equals_full_path_and_invalidates(gpu_session, monkeypatch):
+    # a repeated asynchronous fit of the same DataFrame replays the recorded Gram launch
+    # (models/regression.py _FitReplay); every change of params / conf / data drops it
+    from net.jgp.labs.sparkdq4ml_amd import LinearRegression
+
+    gpu_session.conf.set("dq4ml.fit.async", "true")
+    n, d = 300_000, 24
+    g = torch.Generator(device="cuda").manual_seed(12)
+    X = torch.randn(d, n, generator=g, device="cuda")
+    y = torch.linspace(-1, 1, d, device="cuda") @ X + 0.25
+    df = gpu_session.createDataFrame({"features": X.to(torch.bfloat16), "label": y})
+    df2 = gpu_session.createDataFrame({"features": (X * 2).to(torch.bfloat16), "label": y})
+    try:
+        monkeypatch.setenv("DQ4ML_FIT_REPLAY", "0")
+        full = LinearRegression(solver="normal", gramDtype="bf16").fit(df)
+        full_reg = LinearRegression(solver="normal", gramDtype="bf16", regParam=0.1).fit(df)
+        full2 = LinearRegression(solver="normal", gramDtype="bf16").fit(df2)
+        monkeypatch.delenv("DQ4ML_FIT_REPLAY")
+        lr = LinearRegression(solver="normal", gramDtype="bf16")
+        first = lr.fit(df)
+        assert lr.__dict__.get("_replay") is not None
+        again = [lr.fit(df) for _ in range(4)]
+        for m in [first] + again:
+            np.testing.assert_array_equal(m.coefficients.toArray(), full.coefficients.toArray())
+            assert m.intercept == full.intercept
+            assert m.summary.r2 == full.summary.r2
+        lr.setRegParam(0.1)  # params changed: the full path
+        np.testing.assert_array_equal(lr.fit(df).coefficients.toArray(), full_reg.coefficients.toArray())
+        lr.setRegParam(0.0)
+        m2 = lr.fit(df2)  # another DataFrame
+        np.testing.assert_array_equal(m2.coefficients.toArray(), full2.coefficients.toArray())
+        assert lr._replay.df() is df2
+        gpu_session.conf.set("dq4ml.fit.overlapTail", "false")  # conf changed
+        m3 = lr.fit(df2)
+        assert lr.__dict__.get("_replay") is None
+        np.testing.assert_array_equal(m3.coefficients.toArray(), full2.coefficients.toArray())
+    finally:
+        gpu_session.conf.set("dq4ml.fit.overlapTail", "true")
+        gpu_session.conf.set("dq4ml.fit.async", "false")
