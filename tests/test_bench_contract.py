@@ -142,3 +142,17 @@ def test_config_bench_self_launches_and_rejects_mismatch():
                           "--steps", "1", "--warmup", "0"], capture_output=True, text=True, timeout=300,
                          env=dict(env, WORLD_SIZE="3"))
     assert bad.returncode == 2 and "WORLD_SIZE=3" in bad.stderr
+
+
+def test_scale_curve_script_runs_the_launcher_per_n(tmp_path):
+    """scripts/scale_curve.py (the 1/2/4/8 curve in one invocation) on gloo ranks: one record per
+    N with the benchmark's own JSON line, and the efficiency table."""
+    out = tmp_path / "scale.jsonl"
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "scale_curve.py"), "--gpus", "1,2",
+                        "--configs", "headline", "--quick", "--out", str(out), "--port", "29871"],
+                       capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-2000:]
+    recs = [json.loads(x) for x in out.read_text().splitlines()]
+    assert [r["n"] for r in recs] == [1, 2]
+    assert all(r["result"]["n_gpus"] == r["n"] for r in recs)
+    assert "| headline | 2 |" in p.stdout
