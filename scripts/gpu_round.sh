@@ -69,6 +69,12 @@ for s in $STEPS; do
     pipeq) for r in 1 2; do for m in 1 2; do
             step pipeq_${m}_s${r} 300 env DQ4ML_FIT_PIPELINE=$m python bench.py --steps 200 --warmup 20 --rows 1.25e7 &&
             step pipeq_${m}_f${r} 300 env DQ4ML_FIT_PIPELINE=$m DQ4ML_FORCE_COLLECTIVES=1 python bench.py --steps 200 --warmup 20 --rows 1.25e7 || exit $?; done; done ;;
+    persist) step persist_t 600 python -u -m pytest tests/test_gpu_scanfuse.py tests/test_gpu_scancut.py tests/test_gpu_semantics.py tests/test_gpu_dqvm.py -m gpu -q --maxfail=5 --timeout 120 --timeout-method thread &&
+          for r in 1 2; do
+            step persist_w8_$r 300 python benchmarks/bench_csv_pipeline.py --steps 20 --warmup 3 &&
+            step persist_w6_$r 300 env DQ4ML_SCAN_WPE=6 python benchmarks/bench_csv_pipeline.py --steps 20 --warmup 3 &&
+            step persist_pc4_$r 300 env DQ4ML_SCAN_PER_CU=4 python benchmarks/bench_csv_pipeline.py --steps 20 --warmup 3 &&
+            step persist_lb_$r 300 env DQ4ML_SCAN_GRAM_NOLB=0 python benchmarks/bench_csv_pipeline.py --steps 20 --warmup 3 || exit $?; done ;;
     cfg4rs64) step cfg4rs64 900 env DQ4ML_GRAM_STREAM_F32RS=64 python benchmarks/bench_dq_pipeline.py --steps 5 --warmup 2 ;;
     cfg4ring3) step cfg4ring3 900 env DQ4ML_GRAM_STREAM_RING=3 python benchmarks/bench_dq_pipeline.py --steps 5 --warmup 2 ;;
     cfg4nodqs) step cfg4nodqs 900 env DQ4ML_DQ_STREAM=0 python benchmarks/bench_dq_pipeline.py --steps 5 --warmup 2 ;;
