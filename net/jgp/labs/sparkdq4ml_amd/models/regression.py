@@ -228,11 +228,12 @@ class LinearRegression(_LRParams):
         return load_params_only(cls, path)
 
     def _train(self, df: DataFrame) -> "LinearRegressionModel":
-        rp = self.__dict__.get("_replay")
+        reps = df.__dict__.get("_fit_replays")
+        rp = reps.get(self.uid) if reps else None
         if rp is not None:
             if rp.valid(self, df):
                 return rp.issue(self, df)
-            self._replay = None
+            del reps[self.uid]
         fused = _fused_scan_stats(self, df)
         if fused is not None:
             return self._train_wls(df, None, None, None, fused.d, fused)
@@ -268,7 +269,8 @@ class LinearRegression(_LRParams):
                     model = self._wls_finish(df, flat, d, checks, overlap)
                 plan = self.__dict__.pop("_tiled_plan", None)
                 if plan is not None and model.__dict__.get("_pending") is not None:
-                    self._replay = _FitReplay(self, df, plan, checks, d)
+                    # kept by the DataFrame (its lifetime bounds the plan's tensors), per estimator
+                    df.__dict__.setdefault("_fit_replays", {})[self.uid] = _FitReplay(self, df, plan, checks, d)
                 return model
             flat, checks = self._wls_stats(df, tbl, X, y, d, overlap)
             self.__dict__.pop("_tiled_plan", None)
@@ -382,16 +384,15 @@ class _FitReplay:
     allocates outputs and enqueues the pass, the fold, the all-reduce and the solve -- none of the
     plan walking, schema resolution, column pruning and operand preparation of ``_train``.
 
-    Valid while the estimator's params, the session conf, the collectives state and the
-    dispatch-relevant ``DQ4ML_*`` knobs equal those of the recorded fit, and tracing is off (a
-    traced fit takes the full path to record its spans); anything else drops the replay."""
+    Held by the DataFrame (``df._fit_replays[estimator uid]``), so the plan's tensors live exactly
+    as long as the data they describe.  Valid while the estimator's params, the session conf, the
+    collectives state and the dispatch-relevant ``DQ4ML_*`` knobs equal those of the recorded fit,
+    and tracing is off (a traced fit takes the full path to record its spans); anything else
+    drops the replay."""
 
-    __slots__ = ("df", "pmap", "conf", "env", "coll", "plan", "defer", "checks", "d", "args", "ring", "dev")
+    __slots__ = ("pmap", "conf", "env", "coll", "plan", "defer", "checks", "d", "args", "ring", "dev")
 
     def __init__(self, est, df, plan_defer, checks, d):
-        import weakref
-
-        self.df = weakref.ref(df)
         self.pmap = dict(est._paramMap)
         self.conf = dict(df.sparkSession.conf._conf)
         self.env = _replay_env()
@@ -403,7 +404,7 @@ class _FitReplay:
         self.ring = _pipe_streams[df.sparkSession.device]
 
     def valid(self, est, df) -> bool:
-        return (self.df() is df and est._paramMap == self.pmap and df.sparkSession.conf._conf == self.conf
+        return (est._paramMap == self.pmap and df.sparkSession.conf._conf == self.conf
                 and _replay_env() == self.env and comm.collectives_active() == self.coll
                 and not tracing.enabled())
 

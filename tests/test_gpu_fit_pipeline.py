@@ -54,7 +54,7 @@ def test_fit_replay_equals_full_path_and_invalidates(gpu_session, monkeypatch):
         monkeypatch.delenv("DQ4ML_FIT_REPLAY")
         lr = LinearRegression(solver="normal", gramDtype="bf16")
         first = lr.fit(df)
-        assert lr.__dict__.get("_replay") is not None
+        assert df._fit_replays.get(lr.uid) is not None
         again = [lr.fit(df) for _ in range(4)]
         for m in [first] + again:
             np.testing.assert_array_equal(m.coefficients.toArray(), full.coefficients.toArray())
@@ -65,10 +65,10 @@ def test_fit_replay_equals_full_path_and_invalidates(gpu_session, monkeypatch):
         lr.setRegParam(0.0)
         m2 = lr.fit(df2)  # another DataFrame
         np.testing.assert_array_equal(m2.coefficients.toArray(), full2.coefficients.toArray())
-        assert lr._replay.df() is df2
+        assert df2._fit_replays.get(lr.uid) is not None
         gpu_session.conf.set("dq4ml.fit.overlapTail", "false")  # conf changed
         m3 = lr.fit(df2)
-        assert lr.__dict__.get("_replay") is None
+        assert df2._fit_replays.get(lr.uid) is None
         np.testing.assert_array_equal(m3.coefficients.toArray(), full2.coefficients.toArray())
     finally:
         gpu_session.conf.set("dq4ml.fit.overlapTail", "true")
