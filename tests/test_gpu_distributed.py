@@ -58,6 +58,7 @@ def test_two_rank_device_fit_matches_single_process(gpu_session, fit_async):
         outs.append(json.loads(so.strip().splitlines()[-1]))
     for o in outs:
         assert o["n"] == n
+        assert o["same"]  # every repeated fit (replayed, pipelined) equals the first
         np.testing.assert_allclose(o["coef"], ref.coefficients.toArray(), rtol=1e-12, atol=1e-12)
         assert o["intercept"] == pytest.approx(float(ref.intercept), rel=1e-12, abs=1e-12)
         assert o["rmse"] == pytest.approx(float(ref.summary.rootMeanSquaredError), rel=1e-9)
