@@ -49,7 +49,7 @@ void gram_wide_queue(int eb, WideArgs a, const int* pairs_dev, const float* scal
 // [g*S, g*S+S) (a.splitk == 8*S); pairs_dev lists the P(P+1)/2 pairs I <= J < npanels (diagonal
 // units also write the augmentation tiles)
 void gram_wide_gang(int eb, WideArgs a, const int* pairs_dev, const float* scales, double* out, int S, int grid,
-                    hipStream_t st, bool fold = true);
+                    hipStream_t st, bool fold = true, int waves = 8);
 // fold the pairs of panel columns [J0, J1) (J = npanels: the augmentation column -> the head of
 // the flat layout) into out (f64) or out32 (f32 wire buffer, same flat indexing)
 void gram_wide_fold(WideArgs a, const float* scales, double* out, float* out32, int J0, int J1, hipStream_t st);

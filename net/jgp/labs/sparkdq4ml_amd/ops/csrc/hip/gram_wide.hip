@@ -99,6 +99,7 @@ template <typename F, int WN>
 struct StageFrags {
   F a[2][4];   // [k-step][A tile]
   F b[2][WN];  // [k-step][B tile]
+  F c[2];      // [k-step] the augmentation tile of a 4-wave MODE 5 wave (unused elsewhere)
 };
 
 // One (pair, split) block's K loop + epilogue.  MODE 0: off-diagonal panel pair; 3: diagonal pair
@@ -137,6 +138,9 @@ __device__ __forceinline__ void syrk_block(const WideArgs& a, unsigned char* sme
   constexpr int LB = MODE == 3 ? 0 : (MODE >= 1 ? 1 : kLoadsPerPanel);
   constexpr bool kDiagPanel = MODE == 3 || MODE == 4;  // B operand = the A panel
   constexpr bool kFullWave = MODE == 0 || kDiagPanel;
+  // 4-wave gang: ONE augmentation wave (wm = 1, wn = 0) covers all 256 rows of panel I:
+  // A tiles 0-3 in a[], 4-7 in b[], the augmentation tile in c[]
+  constexpr bool kAug4 = MODE == 5 && WAVES == 4;
   constexpr int kLoadsPerStage = LA + LB;
   typedef StageFrags<F, WN> SF;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -187,6 +191,18 @@ __device__ __forceinline__ void syrk_block(const WideArgs& a, unsigned char* sme
     const unsigned char* B = kDiagPanel ? A : A + kPanelStage;
     const int ta = MODE == 2 ? (wm == 0 ? 0 : 1) : (MODE == 5 ? wn * 4 : wm * 4);  // first A tile
     const int tb = (MODE == 1 || MODE == 2) ? (wn == 0 ? 0 : 1) : (MODE == 5 ? 0 : wn * WN);  // first B tile
+    if constexpr (kAug4) {
+#pragma unroll
+      for (int kk = 0; kk < Tr::kSteps; ++kk) {
+#pragma unroll
+        for (int x = 0; x < 4; ++x) {
+          f.a[kk][x] = Tr::read(A + x * kChunk, kk, lane);
+          f.b[kk][x] = Tr::read(A + (4 + x) * kChunk, kk, lane);
+        }
+        f.c[kk] = Tr::read(B, kk, lane);
+      }
+      return;
+    }
 #pragma unroll
     for (int kk = 0; kk < Tr::kSteps; ++kk) {
 #pragma unroll
@@ -216,6 +232,19 @@ __device__ __forceinline__ void syrk_block(const WideArgs& a, unsigned char* sme
       }
       return;
     }
+    if constexpr (kAug4) {
+#pragma unroll
+      for (int kk = 0; kk < Tr::kSteps; ++kk)
+#pragma unroll
+        for (int x = x0; x < x0 + 2; ++x) {
+          acc[x][0] = Tr::mfma(f.a[kk][x], f.c[kk], acc[x][0]);
+          acc[x][1] = Tr::mfma(f.b[kk][x], f.c[kk], acc[x][1]);
+        }
+      if (x0 == 0)
+#pragma unroll
+        for (int kk = 0; kk < Tr::kSteps; ++kk) acc[0][2] = Tr::mfma(f.c[kk], f.c[kk], acc[0][2]);
+      return;
+    }
 #pragma unroll
     for (int kk = 0; kk < Tr::kSteps; ++kk)
 #pragma unroll
@@ -227,7 +256,7 @@ __device__ __forceinline__ void syrk_block(const WideArgs& a, unsigned char* sme
           acc[x][y] = Tr::mfma(f.a[kk][x], f.b[kk][y], acc[x][y]);
         }
       }
-    if (MODE == 5 && x0 == 0)  // (aug, aug) into the wave's free accumulator (kept for I == 0)
+    if (MODE == 5 && WAVES == 8 && x0 == 0)  // (aug, aug) into the wave's free accumulator (kept for I == 0)
 #pragma unroll
       for (int kk = 0; kk < Tr::kSteps; ++kk) acc[0][1] = Tr::mfma(f.b[kk][0], f.b[kk][0], acc[0][1]);
   };
@@ -282,14 +311,18 @@ __device__ __forceinline__ void syrk_block(const WideArgs& a, unsigned char* sme
   }
   if constexpr (MODE == 5) {  // (I, aug): 256 rows x the augmentation tile's 32 columns
     float* out = a.part + ((int64_t)pair_index(I, a.npanels, a.npanels) * a.splitk + split) * kPanel * kPanel;
+    constexpr int kHalves = WAVES == 4 ? 2 : 1;  // 4 waves: rows 0-127 in acc[x][0], 128-255 in acc[x][1]
 #pragma unroll
-    for (int x = 0; x < 4; ++x)
+    for (int hh = 0; hh < kHalves; ++hh)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) out[(wn * 128 + x * 32 + mfma32_row(lane, r)) * kPanel + mfma32_col(lane)] = acc[x][0][r];
+      for (int x = 0; x < 4; ++x)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          out[((WAVES == 4 ? hh : wn) * 128 + x * 32 + mfma32_row(lane, r)) * kPanel + mfma32_col(lane)] = acc[x][hh][r];
     if (I == 0 && wn == 0) {
       float* o2 = a.part + ((int64_t)pair_index(a.npanels, a.npanels, a.npanels) * a.splitk + split) * kPanel * kPanel;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) o2[mfma32_row(lane, r) * kPanel + mfma32_col(lane)] = acc[0][1][r];
+      for (int r = 0; r < 16; ++r) o2[mfma32_row(lane, r) * kPanel + mfma32_col(lane)] = acc[0][WAVES == 4 ? 2 : 1][r];
     }
     return;
   }
@@ -367,20 +400,21 @@ __global__ __launch_bounds__(64 * WAVES, 1) void gram_wide_queue_kernel(WideArgs
 // other blocks of the round.  The queue schedule's blocks drift apart (unequal unit costs,
 // dynamic dequeue), so there each block re-fetched its panels (L2 hit 61 %, ~6.6x the unique
 // bytes from the fabric).  S is chosen on the host so that npu * S is a multiple of G.
-template <int EB, int RING>
-__global__ __launch_bounds__(512, 1) void gram_wide_gang_kernel(WideArgs a, int S) {
+template <int EB, int RING, int WAVES>
+__global__ __launch_bounds__(64 * WAVES, 1) void gram_wide_gang_kernel(WideArgs a, int S) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int g = blockIdx.x & 7, l = blockIdx.x >> 3, G = gridDim.x >> 3;
   const int P = a.npanels, npu = P * (P + 1) / 2, units = npu * S;
   const int wave = threadIdx.x >> 6;
-  const bool aug_wave = (wave >> 2) == 1 && (wave & 3) < 2;
+  // the waves whose tiles lie entirely below a diagonal unit's diagonal
+  const bool aug_wave = WAVES == 8 ? ((wave >> 2) == 1 && (wave & 3) < 2) : wave == 2;
   for (int u = l; u < units; u += G) {
     const int s = u / npu, pos = u - s * npu;
     const int split = g * S + s;
     const int I = a.pairs[2 * pos], J = a.pairs[2 * pos + 1];
-    if (I != J) syrk_block<EB, 0, RING, 8>(a, smem, I, J, 0, split);
-    else if (aug_wave) syrk_block<EB, 5, RING, 8>(a, smem, I, J, 0, split);
-    else syrk_block<EB, 4, RING, 8>(a, smem, I, J, 0, split);
+    if (I != J) syrk_block<EB, 0, RING, WAVES>(a, smem, I, J, 0, split);
+    else if (aug_wave) syrk_block<EB, 5, RING, WAVES>(a, smem, I, J, 0, split);
+    else syrk_block<EB, 4, RING, WAVES>(a, smem, I, J, 0, split);
     __syncthreads();  // every wave is done reading the ring before the next unit's first glds
   }
 }
@@ -669,23 +703,24 @@ void gram_wide_queue(int eb, WideArgs a, const int* pairs_dev, const float* scal
   if (fold) launch_fold(a, scales, out, nullptr, 0, a.npanels + 1, st);
 }
 
-template <int EB>
+template <int EB, int WAVES>
 static void launch_wide_gang(const WideArgs& a, int grid, int S, hipStream_t st) {
   const size_t lds = (size_t)5 * kStageBytes;
-  DQ_HIP_CHECK(hipFuncSetAttribute((const void*)gram_wide_gang_kernel<EB, 5>,
+  DQ_HIP_CHECK(hipFuncSetAttribute((const void*)gram_wide_gang_kernel<EB, 5, WAVES>,
                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  hipLaunchKernelGGL((gram_wide_gang_kernel<EB, 5>), dim3(grid), dim3(512), lds, st, a, S);
+  hipLaunchKernelGGL((gram_wide_gang_kernel<EB, 5, WAVES>), dim3(grid), dim3(64 * WAVES), lds, st, a, S);
   DQ_HIP_CHECK(hipGetLastError());
 }
 
 void gram_wide_gang(int eb, WideArgs a, const int* pairs_dev, const float* scales, double* out, int S, int grid,
-                    hipStream_t st, bool fold) {
+                    hipStream_t st, bool fold, int waves) {
   a.pairs = pairs_dev;
   if (S < 1 || a.splitk != 8 * S) throw std::invalid_argument("gram_wide_gang: splitk must be 8 * S");
   if (grid < 8 || grid % 8) throw std::invalid_argument("gram_wide_gang: grid must be a positive multiple of 8");
   if ((int64_t)a.splitk > a.nsup) throw std::invalid_argument("gram_wide_gang: more row ranges than supersteps");
-  if (eb == 16) launch_wide_gang<16>(a, grid, S, st);
-  else launch_wide_gang<8>(a, grid, S, st);
+  if (waves != 4 && waves != 8) throw std::invalid_argument("gram_wide_gang: waves must be 4 or 8");
+  if (eb == 16) waves == 8 ? launch_wide_gang<16, 8>(a, grid, S, st) : launch_wide_gang<16, 4>(a, grid, S, st);
+  else waves == 8 ? launch_wide_gang<8, 8>(a, grid, S, st) : launch_wide_gang<8, 4>(a, grid, S, st);
   if (fold) launch_fold(a, scales, out, nullptr, 0, a.npanels + 1, st);
 }
 

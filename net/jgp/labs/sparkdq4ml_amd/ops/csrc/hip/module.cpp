@@ -275,10 +275,10 @@ PYBIND11_MODULE(_dq4ml_hip, m) {
   m.def("gram_wide_gang", [wide_args](int eb, uintptr_t X, uintptr_t Xaug, uintptr_t zeros, int nt, int npanels,
                                       int d, int64_t nsup, int S, uintptr_t pairs, uintptr_t part, double s1,
                                       double syh, double syl, uintptr_t scales, uintptr_t out, int grid,
-                                      uintptr_t stream, bool fold) {
+                                      uintptr_t stream, bool fold, int waves) {
     WideArgs a = wide_args(X, Xaug, zeros, nt, npanels, d, nsup, 8 * S, part, s1, syh, syl);
     gram_wide_gang(eb, a, P<const int>(pairs), P<const float>(scales), P<double>(out), S, grid, as_stream(stream),
-                   fold);
+                   fold, waves);
   });
   m.def("gram_wide_fold", [wide_args](int npanels, int d, int splitk, uintptr_t part, double s1, double syh,
                                       double syl, uintptr_t scales, uintptr_t out, uintptr_t out32, int J0, int J1,

@@ -1059,7 +1059,7 @@ def _gram_wide(h, T: TiledWide, y, w, sel, x_zero_dead):
     out = torch.empty(5 + 2 * d + d * (d + 1) // 2, dtype=torch.float64, device=dev)
     sched = os.environ.get("DQ4ML_WIDE_SCHED", "gang")
     waves = int(os.environ.get("DQ4ML_WIDE_WAVES", "8"))
-    gs = _wide_gang_s(P, nsup, _wide_grid(h) // 8) if sched == "gang" and waves == 8 else 0
+    gs = _wide_gang_s(P, nsup, _wide_grid(h) // 8) if sched == "gang" and waves in (4, 8) else 0
     if sched == "gang" and not gs:
         sched = "queue"
     hq = _wide_queue_h(nsup) if sched == "queue" else 0
@@ -1073,7 +1073,7 @@ def _gram_wide(h, T: TiledWide, y, w, sel, x_zero_dead):
         part = torch.empty(int(h.gram_wide_partials(d, splitk)), dtype=torch.float32, device=dev)
         h.gram_wide_gang(eb, T.buf.data_ptr(), aug.buf.data_ptr(), _zero_page(h, dev).data_ptr(), T.nt, P, d, nsup,
                          gs, gpairs_dev.data_ptr(), part.data_ptr(), 1.0, float(s_h), float(s_l), _ptr(T.scales),
-                         out.data_ptr(), _wide_grid(h), _stream(), not banded)
+                         out.data_ptr(), _wide_grid(h), _stream(), not banded, waves)
     elif hq:
         # persistent XCD-grouped schedule (gram_wide_queue_kernel): 8 groups x h row ranges
         splitk = 8 * hq
