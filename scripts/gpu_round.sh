@@ -87,6 +87,10 @@ for s in $STEPS; do
           step gang_ab 900 env N=1e7 D=4096 EB=8 REPS=5 VARIANTS="${VARIANTS:-5:morton:8:gang,4:morton:8:0:q2}" python scripts/wide_bench.py ;;
     gang4) step gang4_t 600 python -u -m pytest tests/test_gpu_wide.py -m gpu -q --maxfail=3 --timeout 120 --timeout-method thread -k "schedules or gang" &&
           step gang4_ab 900 env N=1e7 D=4096 EB=8 REPS=5 VARIANTS="5:morton:8:gang,5:morton:4:gang" python scripts/wide_bench.py ;;
+    augvalu) (export TMPDIR=/tmp
+       step augvalu_t 600 python -u -m pytest tests/test_gpu_scancut.py tests/test_gpu_scanfuse.py -m gpu -q --maxfail=5 --timeout 120 --timeout-method thread &&
+       step augvalu_ab32 600 env VARIANTS="base;DQ4ML_CUT_AUGVALU=0;base;DQ4ML_CUT_AUGVALU=0" python scripts/cut_bench.py --features 32 --rows 2e7 &&
+       step augvalu_ab64 600 env VARIANTS="base;DQ4ML_CUT_AUGVALU=0;base" python scripts/cut_bench.py --features 60 --rows 1e7) || exit $? ;;
     gangpmc) (export TMPDIR=/tmp N=2e6 D=4096 EB=8 REPS=2 VARIANTS="${VARIANTS:-5:morton:8:gang,4:morton:8:0:q2}"
        step gangpmc1 300 timeout -s KILL 240 rocprofv3 --kernel-trace --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA GRBM_GUI_ACTIVE -d gpurun_out/gangpmc1 -o run --output-format csv -- python scripts/wide_bench.py &&
        step gangpmc2 300 timeout -s KILL 240 rocprofv3 --kernel-trace --pmc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum GRBM_GUI_ACTIVE -d gpurun_out/gangpmc2 -o run --output-format csv -- python scripts/wide_bench.py) || exit $? ;;
