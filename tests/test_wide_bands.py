@@ -21,3 +21,25 @@ def test_bands_tile_flat_layout(d, bucket, elt):
     col_max = (P * 256) * elt * 256
     for b in bands[1:-1]:
         assert bucket <= (b[3] - b[2]) * elt <= bucket + col_max
+
+
+def test_gang_row_ranges_balance_the_units(monkeypatch):
+    # ops/device.py _wide_gang_s: S row ranges per XCD group so the P(P+1)/2 units of a range
+    # times S divide evenly over the G blocks of a group (equal-cost units stay in step)
+    from net.jgp.labs.sparkdq4ml_amd.ops.device import _wide_gang_s
+
+    monkeypatch.delenv("DQ4ML_WIDE_GANG_S", raising=False)
+    nsup = 10_000_000 // 64
+    assert _wide_gang_s(16, nsup, 32) == 4  # config 5: 136 x 4 = 544 = 17 x 32
+    for P in (2, 3, 5, 16, 40):
+        S = _wide_gang_s(P, nsup, 32)
+        units = P * (P + 1) // 2 * S
+        assert S >= 1 and units / (-(-units // 32) * 32) >= 0.9
+        assert nsup >= 8 * S * 16  # >= 16 supersteps per split
+    assert _wide_gang_s(16, 100, 32) == 0  # too few rows: the queue schedule instead
+    # f32 accumulators count rows exactly only below 2^24 per split
+    big = (1 << 30) // 64
+    S = _wide_gang_s(16, big, 32)
+    assert S and big * 64 / (8 * S) < (1 << 24)
+    monkeypatch.setenv("DQ4ML_WIDE_GANG_S", "2")
+    assert _wide_gang_s(16, nsup, 32) == 2
