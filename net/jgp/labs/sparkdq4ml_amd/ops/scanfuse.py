@@ -331,7 +331,8 @@ __device__ __forceinline__ void dq_row_swar(const unsigned char* B, int start, i
 {body}
 {stores}}}
 """
-    return (header_text() + f"""
+    return ("#define CSV_UDOT4(a, b, c) __builtin_amdgcn_udot4((a), (b), (c), false)\n"
+            "#define CSV_MUL24(a, b) __umul24((a), (b))\n" + header_text() + f"""
 using namespace dq4ml_csv;
 typedef unsigned int csv_u32x4 __attribute__((ext_vector_type(4)));
 // every global access names the global address space: generic (flat) accesses count in both
