@@ -67,6 +67,18 @@ static bool r8s(const std::string& f, double& dv, long long& lv, int& ty, bool& 
   return len == 0 || ok;
 }
 
+// csv_swar_field directly, with junk bytes after the field in the same 64-bit word (as the
+// per-line scan kernel hands it the field at the start of the line's remaining bytes)
+static bool swar8(const std::string& f, double& dv, long long& lv, int& ty) {
+  const char pool[] = "0123456789.-+,\r\n x";
+  unsigned char b[8];
+  for (auto& c : b) c = (unsigned char)pool[junk() % (sizeof(pool) - 1)];
+  memcpy(b, f.data(), f.size());
+  unsigned long long x;
+  memcpy(&x, b, 8);
+  return csv_swar_field(x, (int)f.size(), dv, lv, ty);
+}
+
 static bool swar(const std::string& f, double& dv, long long& lv, int& ty) {
   unsigned char buf[48] = {0};
   const int off = 5;  // an unaligned start, like a field inside an LDS stage
@@ -109,6 +121,17 @@ int main() {
       if (fits && (a != g || (a && (t1 != t5 || l1 != l5 || memcmp(&d1, &d5, sizeof d1) != 0)))) {
         printf("MISMATCH field '%s': fast %d ty %d %.17g %lld | r8s %d ty %d %.17g %lld\n", f.c_str(), a, t1, d1,
                l1, g, t5, d5, l5);
+        return false;
+      }
+    }
+    if (f.size() <= 8) {
+      double d6 = 0;
+      long long l6 = 0;
+      int t6 = -1;
+      const bool h = swar8(f, d6, l6, t6);
+      if (a != h || (a && (t1 != t6 || l1 != l6 || memcmp(&d1, &d6, sizeof d1) != 0))) {
+        printf("MISMATCH field '%s': fast %d ty %d %.17g %lld | swar8 %d ty %d %.17g %lld\n", f.c_str(), a, t1, d1,
+               l1, h, t6, d6, l6);
         return false;
       }
     }
