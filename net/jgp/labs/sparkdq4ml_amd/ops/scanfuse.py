@@ -331,8 +331,15 @@ __device__ __forceinline__ void dq_row_swar(const unsigned char* B, int start, i
 {body}
 {stores}}}
 """
+    # 10^k / RN(10^-k) for the SWAR converter's decimals: an LDS table (one ds_read2_b64) or VALU
+    # selects and products (DQ4ML_SCAN_P10=valu); the kernel is VALU-issue-bound
+    p10_lds = swar and os.environ.get("DQ4ML_SCAN_P10", "lds") == "lds"
+    p10_decl = ("__shared__ double dq_p10[16];\n#define CSV_P10_TAB dq_p10\n" if p10_lds else "")
+    p10_init = ("  if (threadIdx.x < 16) dq_p10[threadIdx.x] = threadIdx.x < 8 ? dq4ml_csv::csv_pow10(threadIdx.x)\n"
+                "                                                       : dq4ml_csv::csv_inv_pow10(threadIdx.x - 8);\n"
+                if p10_lds else "")
     return ("#define CSV_UDOT4(a, b, c) __builtin_amdgcn_udot4((a), (b), (c), false)\n"
-            "#define CSV_MUL24(a, b) __umul24((a), (b))\n" + header_text() + f"""
+            "#define CSV_MUL24(a, b) __umul24((a), (b))\n" + p10_decl + header_text() + f"""
 using namespace dq4ml_csv;
 typedef unsigned int csv_u32x4 __attribute__((ext_vector_type(4)));
 // every global access names the global address space: generic (flat) accesses count in both
@@ -371,7 +378,7 @@ extern "C" __global__ __launch_bounds__(256) {_wpe(fast_only)}void {ENTRY}(void*
   __shared__ int wtot[4];
   __shared__ long long sstart0, sblk, sgl0;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-{"  const long long blk = blockIdx.x;  // Gram mode: no global line numbering needed" if nolb else _ticket(lookback, ticket if not abl & 16 else "none")}
+{p10_init}{"  const long long blk = blockIdx.x;  // Gram mode: no global line numbering needed" if nolb else _ticket(lookback, ticket if not abl & 16 else "none")}
   const long long a = (long long)(reinterpret_cast<unsigned long long>(b) & 15ull);
   const DQG unsigned char* ab = b - a;                     // 16-byte aligned view
   const long long wbase = blk * {W} - a;                    // buffer index of window byte 0
@@ -637,7 +644,7 @@ def _compile(nodes, rel, gram: int = 0):
                  and os.environ.get("DQ4ML_SCAN_FASTONLY", "1") != "0")
     key = (parts, udfs, tuple(rel.schema().names), tuple(f["kinds"]), tuple(f["nullable"]),
            repr(sorted(f["opts"].items())), f["strict"], head, lookback, fast_only, _wpe(fast_only),
-           ticket, os.environ.get("DQ4ML_SCAN_ABL", "0"), gram, _scan_nt(), nolb)
+           ticket, os.environ.get("DQ4ML_SCAN_ABL", "0"), gram, _scan_nt(), nolb, os.environ.get("DQ4ML_SCAN_P10"))
     cp = _CACHE.get(key)
     if cp is None and key not in _CACHE:
         base = _ScanBase(rel.schema(), 0, f["device"])

@@ -96,6 +96,9 @@ for s in $STEPS; do
        step gangpmc2 300 timeout -s KILL 240 rocprofv3 --kernel-trace --pmc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum GRBM_GUI_ACTIVE -d gpurun_out/gangpmc2 -o run --output-format csv -- python scripts/wide_bench.py) || exit $? ;;
     cfg5) step cfg5 900 python benchmarks/bench_wide.py --steps 3 --warmup 1 --json-out gpurun_out/cfg5.json ;;
     csv) step csv 600 python benchmarks/bench_csv_pipeline.py --steps 20 --warmup 3 --json-out gpurun_out/csv.json ;;
+    p10ab) for r in 1 2; do
+         step p10_lds_$r 300 python benchmarks/bench_csv_pipeline.py --steps 20 --warmup 3 &&
+         step p10_valu_$r 300 env DQ4ML_SCAN_P10=valu python benchmarks/bench_csv_pipeline.py --steps 20 --warmup 3 || exit $?; done ;;
     csvnogram) step csvnogram 600 env DQ4ML_SCAN_GRAM=0 python benchmarks/bench_csv_pipeline.py --steps 20 --warmup 3 ;;
     cfg1) step cfg1 300 python benchmarks/bench_cpu_small.py --json-out gpurun_out/cfg1.json ;;
     prof4) step prof4 600 env WHICH=cfg4 python scripts/step_profile.py ;;
