@@ -200,7 +200,7 @@ def _gram_code(xs, yv) -> str:
 
 def kernel_source(g, kinds, nullable, used, opts: dict, strict: bool, head: int, slots: dict,
                   lookback: bool = True, fast_only: bool = False, ticket: str = "xcd", gram: int = 0,
-                  nolb: bool = False) -> str:
+                  nolb: bool = False, term_only: Optional[str] = None) -> str:
     """Source of the fused kernel.
 
     ``g``: the dqvm generator after lowering the chain (its ``lines`` use ``f<c>`` / ``m<c>`` for
@@ -312,6 +312,13 @@ def kernel_source(g, kinds, nullable, used, opts: dict, strict: bool, head: int,
         stores = "".join(f"    if (li == -7) ((DQG {t}*)p[{s}])[0] = ({t})({v});\n" for t, v, s in g.stores)
     comment = int(opts["comment"])
     H, W = int(head), WINDOW
+    # terminator masks: both bytes in general; only the file's one terminator byte when its facts
+    # say every line ends the same single way (CR only, as the reference data, or LF only) -- the
+    # other byte then occurs nowhere in the cached bytes (the kernel is VALU-issue-bound)
+    cr_scan = ("" if term_only == "lf" else
+               "      cr |= (unsigned long long)byte_eq4(v[w], 0x0D0D0D0Du) << (16 * j + 4 * w);\n")
+    lf_scan = ("" if term_only == "cr" else
+               "      lf |= (unsigned long long)byte_eq4(v[w], 0x0A0A0A0Au) << (16 * j + 4 * w);\n")
     swar_row = "" if not swar else f"""
 // a line of at most 16 bytes in the LDS stage: held in two 64-bit registers, fields cut by the
 // separator bitmask, numeric fields converted SWAR (csv_parse_dev.h) — no per-byte loop
@@ -394,8 +401,7 @@ extern "C" __global__ __launch_bounds__(256) {_wpe(fast_only)}void {ENTRY}(void*
     {"if (v[0] == 0x7F7F7F7Fu && v[1] == 3u) " if abl & 32 else ""}*reinterpret_cast<csv_u32x4*>(stage + {H} + 64 * tid + 16 * j) = v;
 #pragma unroll
     for (int w = 0; w < 4; ++w) {{
-      cr |= (unsigned long long)byte_eq4(v[w], 0x0D0D0D0Du) << (16 * j + 4 * w);
-      lf |= (unsigned long long)byte_eq4(v[w], 0x0A0A0A0Au) << (16 * j + 4 * w);
+{cr_scan}{lf_scan}
     }}
   }}
   for (int gq = tid; gq < {H // 16} + 1; gq += 256) {{  // head granules + one tail granule
@@ -640,11 +646,16 @@ def _compile(nodes, rel, gram: int = 0):
     nolb = bool(gram) and lookback and os.environ.get("DQ4ML_SCAN_GRAM_NOLB", "1") != "0"
     ticket = ticket_mode()
     o = f["opts"]
+    from .scancut import term_of
+
+    tk = term_of(f) if os.environ.get("DQ4ML_SCAN_TERM1", "1") != "0" else None
+    term_only = {(13, False): "cr", (10, False): "lf"}.get(tk)
     fast_only = (bool(f.get("fast_only")) and not o["null_value"] and not o["trim_lead"] and not o["trim_trail"]
                  and os.environ.get("DQ4ML_SCAN_FASTONLY", "1") != "0")
     key = (parts, udfs, tuple(rel.schema().names), tuple(f["kinds"]), tuple(f["nullable"]),
            repr(sorted(f["opts"].items())), f["strict"], head, lookback, fast_only, _wpe(fast_only),
-           ticket, os.environ.get("DQ4ML_SCAN_ABL", "0"), gram, _scan_nt(), nolb, os.environ.get("DQ4ML_SCAN_P10"))
+           ticket, os.environ.get("DQ4ML_SCAN_ABL", "0"), gram, _scan_nt(), nolb, os.environ.get("DQ4ML_SCAN_P10"),
+           term_only)
     cp = _CACHE.get(key)
     if cp is None and key not in _CACHE:
         base = _ScanBase(rel.schema(), 0, f["device"])
@@ -654,7 +665,7 @@ def _compile(nodes, rel, gram: int = 0):
             names = _ScanPlan.SCAN_SLOTS + (("gpart",) if gram else ())
             slots = {k: g.slot(None, (k,)) for k in names}
             src = kernel_source(g, f["kinds"], f["nullable"], g.used, f["opts"], f["strict"], head, slots, lookback,
-                                fast_only, ticket, gram, nolb)
+                                fast_only, ticket, gram, nolb, term_only)
             cp = _ScanPlan(src, g, outputs, refs, gram)
             cp.lookback = lookback
         except dqvm.Unfusable as e:

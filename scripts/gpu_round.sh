@@ -99,6 +99,9 @@ for s in $STEPS; do
     p10ab) for r in 1 2; do
          step p10_lds_$r 300 python benchmarks/bench_csv_pipeline.py --steps 20 --warmup 3 &&
          step p10_valu_$r 300 env DQ4ML_SCAN_P10=valu python benchmarks/bench_csv_pipeline.py --steps 20 --warmup 3 || exit $?; done ;;
+    termab) for r in 1 2 3; do
+         step term_one_$r 300 python benchmarks/bench_csv_pipeline.py --steps 30 --warmup 3 &&
+         step term_gen_$r 300 env DQ4ML_SCAN_TERM1=0 python benchmarks/bench_csv_pipeline.py --steps 30 --warmup 3 || exit $?; done ;;
     csvnogram) step csvnogram 600 env DQ4ML_SCAN_GRAM=0 python benchmarks/bench_csv_pipeline.py --steps 20 --warmup 3 ;;
     cfg1) step cfg1 300 python benchmarks/bench_cpu_small.py --json-out gpurun_out/cfg1.json ;;
     prof4) step prof4 600 env WHICH=cfg4 python scripts/step_profile.py ;;
