@@ -53,15 +53,24 @@ def shard_byte_range(data: bytes, rank: int, world: int) -> Tuple[int, int]:
     return align(n * rank // world), align(n * (rank + 1) // world)
 
 
-def _ncols_of(data, sep: str) -> int:
-    """Column count from the first line (a bounded, growing head search: the input may be a
-    multi-GB map with no ``\n`` at all — the reference data is CR-only)."""
+def _ncols_of(data, sep: str, comment: int = 0) -> int:
+    """Column count from the first line that is neither empty nor a comment line -- Spark drops
+    those before it tokenizes the first record (a bounded, growing head search: the input may be
+    a multi-GB map with no ``\n`` at all -- the reference data is CR-only)."""
     n, w = len(data), 1 << 16
     while True:
         head = bytes(data[:min(n, w)])
-        ends = [x for x in (head.find(b"\n"), head.find(b"\r")) if x >= 0]
-        if ends or w >= n:
-            return head.count(sep.encode(), 0, min(ends) if ends else len(head)) + 1
+        pos = 0
+        while True:
+            ends = [x for x in (head.find(b"\n", pos), head.find(b"\r", pos)) if x >= 0]
+            if not ends and w < n:
+                break  # the line may go on past the head: read more
+            e = min(ends) if ends else len(head)
+            if e > pos and not (comment and head[pos] == comment):
+                return head.count(sep.encode(), pos, e) + 1
+            if not ends:  # the whole input holds no such line
+                return 1
+            pos = e + 1
         w *= 16
 
 
@@ -243,7 +252,7 @@ def scan_device(data, sep: str = ",", infer: bool = True, device=None, ncols: Op
     h = native.hip()
     dev = torch.device(device)
     if ncols is None:
-        ncols = _ncols_of(data, sep)
+        ncols = _ncols_of(data, sep, int(_opt_args(opts)["comment"] or 0))
     if ncols > 256:
         return None
     hint = list(types_hint) if types_hint is not None and len(types_hint) == ncols else None

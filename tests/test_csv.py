@@ -436,3 +436,18 @@ def test_device_reader_options_match_host(tmp_path, case):
 
     for ra, rb in zip(dev_rows, host_rows):
         assert all(same(a, b) for a, b in zip(ra, rb)), (ra, rb)
+
+
+def test_device_column_count_skips_empty_and_comment_lines():
+    # Spark drops empty lines (and comment lines) before it tokenizes the first record; the device
+    # scanner's column count follows (a leading empty line used to give one column)
+    from net.jgp.labs.sparkdq4ml_amd.ops.csvscan import _ncols_of
+
+    assert _ncols_of(b"\n\na,b,c\n1,2,3", ",") == 3
+    assert _ncols_of(b"\r\r1,2\r", ",") == 2
+    assert _ncols_of(b"a,b\r\n1,2", ",") == 2
+    assert _ncols_of(b"#x,y\na,b,c,d\n", ",", ord("#")) == 4
+    assert _ncols_of(b"1,2,3", ",") == 3
+    assert _ncols_of(b"", ",") == 1 and _ncols_of(b"\n\n", ",") == 1
+    big = b"\n" * 5 + b"x" * (1 << 17) + b",y\n"  # the first real line runs past the first head window
+    assert _ncols_of(big, ",") == 2
