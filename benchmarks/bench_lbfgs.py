@@ -120,7 +120,7 @@ def _ingest(d, n, eb, rank, dev, native, device, TiledWide):
         y[r0:r1] = beta @ xc + 0.5 + 0.1 * torch.randn(r1 - r0, generator=g, device=dev)
         lo = r0 * per_row
         device.pack_wide([xc], eb, None, inv_scale=(1.0 / scale) if eb == 8 else None,
-                         out=buf[lo:lo + ((r1 - r0 + 63) // 64) * 64 * per_row])
+                         out=buf[lo:lo + ((r1 - r0 + 63) // 64) * 64 * per_row], shift=None)
         del xc
     return TiledWide(buf, d, n, eb, scale if eb == 8 else None), y, beta, buf
 

@@ -87,6 +87,7 @@ def train_lbfgs(est, df, tbl, X, y, d):
         log.warning("The standard deviation of the label is zero, so the coefficients will be zeros and the "
                     "intercept will be the mean of the label; as a result, training is not needed.")
         return finish(np.zeros(d), my if fit_icpt else 0.0, np.zeros(1), "none")
+    _check_constant_label(raw_ys, reg)
     ys = raw_ys if raw_ys > 0 else abs(my)
     eff_reg = reg / ys
     l1, l2 = enet * eff_reg, (1.0 - enet) * eff_reg
@@ -116,6 +117,18 @@ def train_lbfgs(est, df, tbl, X, y, d):
     coef = np.where(zero, 0.0, np.asarray(x) * ys / safe)
     icpt = my - float(np.dot(coef, mx)) if fit_icpt else 0.0
     return finish(coef, icpt, hist, "owlqn" if l1vec is not None else "l-bfgs")
+
+
+def _check_constant_label(raw_ys: float, reg: float) -> None:
+    """Spark 2.4 ``LinearRegression.train`` for a constant nonzero label without an intercept:
+    ``require(regParam == 0.0, ...)``, else a warning (the caller has already returned for the
+    fitIntercept / zero-mean cases)."""
+    if raw_ys != 0.0:
+        return
+    if reg != 0.0:
+        raise ValueError("requirement failed: The standard deviation of the label is zero. "
+                         "Model cannot be regularized.")
+    log.warning("The standard deviation of the label is zero. Consider setting fitIntercept=true.")
 
 
 def _train_passes(est, df, X, y, w, sel, d):
@@ -156,6 +169,7 @@ def _train_passes(est, df, X, y, w, sel, d):
         log.warning("The standard deviation of the label is zero, so the coefficients will be zeros and the "
                     "intercept will be the mean of the label; as a result, training is not needed.")
         return finish(np.zeros(d), my if fit_icpt else 0.0, np.zeros(1), "none")
+    _check_constant_label(raw_ys, reg)
     ys = raw_ys if raw_ys > 0 else abs(my)
     eff_reg = reg / ys
     l1, l2 = enet * eff_reg, (1.0 - enet) * eff_reg

@@ -263,21 +263,27 @@ class LinearRegression(_LRParams):
         else:
             pipe = _pipe_stream(df, tbl) if overlap else None
             if pipe is not None:
+                caller = faststream.current(faststream.dev_index(df.sparkSession.device))
                 with faststream.use(pipe):
-                    flat, checks = self._wls_stats(df, tbl, X, y, d, overlap)
+                    flat, checks = self._wls_stats(df, tbl, X, y, d, overlap, caller)
                     _rank_health(df)
                     model = self._wls_finish(df, flat, d, checks, overlap)
                 plan = self.__dict__.pop("_tiled_plan", None)
                 if plan is not None and model.__dict__.get("_pending") is not None:
-                    # kept by the DataFrame (its lifetime bounds the plan's tensors), per estimator
-                    df.__dict__.setdefault("_fit_replays", {})[self.uid] = _FitReplay(self, df, plan, checks, d)
+                    # kept by the DataFrame (its lifetime bounds the plan's tensors), per estimator;
+                    # the plan's row operands were made on `pipe`: replays on the other pipeline
+                    # streams wait for that once
+                    ready = torch.cuda.Event()
+                    ready.record(pipe)
+                    df.__dict__.setdefault("_fit_replays", {})[self.uid] = _FitReplay(self, df, plan, checks, d,
+                                                                                       (ready, pipe))
                 return model
             flat, checks = self._wls_stats(df, tbl, X, y, d, overlap)
             self.__dict__.pop("_tiled_plan", None)
         _rank_health(df)
         return self._wls_finish(df, flat, d, checks, overlap)
 
-    def _wls_stats(self, df, tbl, X, y, d, overlap):
+    def _wls_stats(self, df, tbl, X, y, d, overlap, caller=None):
         checks = _fit_checks(self, tbl, X)
         w = _weight_of(self, tbl)
         sel = tbl.sel
@@ -305,13 +311,14 @@ class LinearRegression(_LRParams):
                 # queue behind its HBM stream (8 us alone, ~100 us co-running), and the side stream
                 # must still fit the all-reduce and the solve into one Gram period
                 defer = overlap and _async_conf(df) and d <= 64 and not comm.collectives_active()
-                if _replayable(X.values, w):
+                Xv = _values(X, caller)
+                if _replayable(Xv, w):
                     # resolve the launch once: a repeated fit of this DataFrame replays it
-                    plan = device.TiledGramPlan(native.hip(), X.values, yv, None, sel, x_zero_dead)
+                    plan = device.TiledGramPlan(native.hip(), Xv, yv, None, sel, x_zero_dead)
                     flat = plan.launch(device._stream(), defer)
                     self._tiled_plan = (plan, defer)
                 else:
-                    flat = kernels.gram_stats(X.values, yv, w, sel, gd, x_zero_dead=x_zero_dead, defer=defer)
+                    flat = kernels.gram_stats(Xv, yv, w, sel, gd, x_zero_dead=x_zero_dead, defer=defer)
         tracing.add_rows("gram", tbl.nrows)
         return flat, checks
 
@@ -346,6 +353,22 @@ class LinearRegression(_LRParams):
         return model
 
 
+def _values(X, caller):
+    """``X.values``.  In a pipelined fit (``caller``: the caller's stream, the current stream being
+    a pipeline stream) a lazily assembled column is materialized on the CALLER's stream -- the
+    column memoizes the matrix for every later reader of the DataFrame, which runs there -- and
+    the pipeline stream waits for it (no cross-stream read of a pipe-made tensor)."""
+    from ..sql.table import LazyVectorColumn
+
+    if caller is None or not isinstance(X, LazyVectorColumn) or X.materialized:
+        return X.values
+    pipe = faststream.raw(caller.device_index)
+    with faststream.use(caller):
+        v = X.values
+    native.hip().stream_wait(pipe, caller.cuda_stream)
+    return v
+
+
 def _wls_args(est, d):
     """``fit_wls_flat`` arguments after ``flat``, from the estimator's params."""
     return (None, d, est.getOrDefault("fitIntercept"), float(est.getOrDefault("regParam")),
@@ -364,16 +387,14 @@ def _async_model(est, df, pending) -> "LinearRegressionModel":
 
 def _replay_env():
     # the knobs that change what a replayed fit would enqueue (DQ4ML_FORCE_COLLECTIVES acts
-    # through comm.collectives_active(), compared separately; DQ4ML_GRAM_FOLD only picks between
-    # two equal-result fold kernels and is read when the replay is recorded)
+    # through comm.collectives_active(), compared separately)
     return os.environ.get("DQ4ML_FIT_REPLAY"), os.environ.get("DQ4ML_FIT_PIPELINE")
 
 
 def _replayable(Xv, w) -> bool:
     """The fit's Gram pass can be captured as a :class:`ops.device.TiledGramPlan`: bf16 fragment
-    tiles on the GPU, no weights, the separate fold kernel (not the opt-in in-kernel fold)."""
+    tiles on the GPU, no weights."""
     return (isinstance(Xv, TiledBF16) and w is None and Xv.buf.is_cuda and Xv.d <= 64
-            and os.environ.get("DQ4ML_GRAM_FOLD", "separate") != "kernel"
             and os.environ.get("DQ4ML_FIT_REPLAY", "1") != "0")
 
 
@@ -390,9 +411,10 @@ class _FitReplay:
     and tracing is off (a traced fit takes the full path to record its spans); anything else
     drops the replay."""
 
-    __slots__ = ("pmap", "conf", "env", "coll", "plan", "defer", "checks", "d", "args", "ring", "dev")
+    __slots__ = ("pmap", "conf", "env", "coll", "plan", "defer", "checks", "d", "args", "ring", "dev", "ready",
+                 "waited")
 
-    def __init__(self, est, df, plan_defer, checks, d):
+    def __init__(self, est, df, plan_defer, checks, d, ready=None):
         self.pmap = dict(est._paramMap)
         self.conf = dict(df.sparkSession.conf._conf)
         self.env = _replay_env()
@@ -402,6 +424,10 @@ class _FitReplay:
         self.args = _wls_args(est, d)[1:]
         self.dev = faststream.dev_index(df.sparkSession.device)
         self.ring = _pipe_streams[df.sparkSession.device]
+        # (event, stream) after the recorded fit's operands were made: every other pipeline
+        # stream waits for it before its first replay
+        self.ready = ready
+        self.waited = set() if ready is None else {ready[1].cuda_stream}
 
     def valid(self, est, df) -> bool:
         return (est._paramMap == self.pmap and df.sparkSession.conf._conf == self.conf
@@ -413,6 +439,9 @@ class _FitReplay:
         pipe = ring[1][ring[0] % len(ring[1])]
         ring[0] += 1
         ps = pipe.cuda_stream
+        if self.ready is not None and ps not in self.waited:
+            pipe.wait_event(self.ready[0])
+            self.waited.add(ps)
         native.hip().stream_wait(ps, faststream.raw(self.dev))
         with faststream.use(pipe):
             flat = self.plan.launch(ps, self.defer)

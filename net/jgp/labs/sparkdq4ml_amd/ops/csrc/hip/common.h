@@ -133,6 +133,14 @@ __device__ __forceinline__ void load8_typed(const void* p, int64_t r0, int64_t n
   }
 }
 
+// x[j] -= s for the rows r0 + j < n (rows past the end stay exactly 0): the per-feature shift
+// applied before a low-precision cast (GramArgs::xshift)
+__device__ __forceinline__ void sub_shift8(float x[8], float s, int64_t r0, int64_t n) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+    if (r0 + j < n) x[j] -= s;
+}
+
 // zero the elements of x whose row is dead in the 0/1 selection (one 8-byte load when possible)
 __device__ __forceinline__ void mask8(const uint8_t* sel, int64_t r0, int64_t n, float x[8]) {
   if (sel == nullptr) return;

@@ -46,14 +46,12 @@ struct GramArgs {
   // sources of the stage's row-scalar area — [64 lanes][(base, bytes per row) x 2 instructions]
   // int64 pairs, then the region pointers the guarded tail stage copies from
   const int64_t* rawtab;
-  // in-kernel fold (tall bf16 kernel): kFoldTickets zeroed counters owned by the launching stream
-  // (the last block resets them) and the packed output; partials then holds blocks + kFoldGroups
-  // slabs.  Null: the slabs are folded by gram_reduce (a separate kernel)
-  unsigned int* ticket;
-  double* fold_out;
+  // per-feature f32 shift s (null: none): kernels that round the features (bf16 / exact-f32 /
+  // split-f32 MFMA) accumulate the statistics of x - s, so a column with |mean| >> std keeps its
+  // digits through the cast and the f32 accumulators; stats_unshift restores those of x in f64
+  // (SURVEY.md §7e.2).  Dead and padding rows stay exactly zero.
+  const float* xshift;
 };
-constexpr int kFoldGroups = 8;               // one group per XCD (blocks are dealt round-robin)
-constexpr int kFoldTickets = kFoldGroups + 1;
 
 #ifndef __HIPCC_RTC__
 // MFMA-fragment-ordered bf16 feature storage ("tiled"): for superstep s (64 rows), 32-feature
@@ -64,7 +62,9 @@ int64_t tiled_elems(int d, int64_t n);
 // GramArgs::interleave for the tall bf16 kernel (1 unless DQ4ML_GRAM_INTERLEAVE=0); the stream
 // kernels keep contiguous ranges (DQ4ML_GRAM_STREAM_INTERLEAVE=1 for A/B)
 int gram_interleave();
-void tile_bf16(const void* X, int xdt, int64_t ld, int d, int64_t n, void* out, hipStream_t st);
+// shift: per-feature f32 shift subtracted before the bf16 cast (null: none; rows >= n stay zero)
+void tile_bf16(const void* X, int xdt, int64_t ld, int d, int64_t n, void* out, hipStream_t st,
+               const float* shift = nullptr);
 
 int64_t gram_partial_stride(int mode, int d);
 int gram_default_blocks(int64_t n);
@@ -75,6 +75,11 @@ int gram_plan_blocks(int mode, int d, int64_t n, int xdt, int xmode);
 // later, possibly on another stream
 void gram_tall(int mode, GramArgs a, int xmode, int blocks, double* out, hipStream_t st, bool reduce = true);
 void gram_reduce(int mode, const double* partials, int blocks, int d, double* out, hipStream_t st);
+// flat statistics of x' = x - s (GramArgs::xshift) -> those of x, in place, in f64:
+//   Σw·x = Σw·x' + s·Σw,  Σw·x·y = Σw·x'·y + s·Σw·y,
+//   Σw·xᵢ·xⱼ = Σw·x'ᵢ·x'ⱼ + sᵢ·Σw·x'ⱼ + sⱼ·Σw·x'ᵢ + sᵢ·sⱼ·Σw
+// (exact algebra for any fixed s: DQ selections and weights are already in the sums)
+void stats_unshift(double* flat, const float* shift, int d, hipStream_t st);
 
 // LDS-DMA streamed tall kernels (gram_stream.hip): GRAM_F64 on f64/f32 features, GRAM_F32
 // (exact-f32 MFMA) on f32 features.  gram_stream_ok: operand dtypes/alignment the DMA path needs.

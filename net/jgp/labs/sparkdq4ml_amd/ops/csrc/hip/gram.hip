@@ -188,69 +188,10 @@ __device__ __forceinline__ void fold_store(int o, double t, int d, int T, int NT
   if (i <= j && j < d) out[head + i + j * (j + 1) / 2] = t;
 }
 
-// Fold of the blocks' slabs inside the Gram kernel (replaces gram_reduce's kernel and its kernel
-// boundary): the last block of each XCD group (block b is in group b % G) sums the group's slabs
-// in ascending block order into a group slab, and the last group folds the G group slabs in
-// ascending order into the packed output.  Both orders are fixed, so the result does not depend
-// on which block arrives last (run-to-run bitwise deterministic).
-// Visibility without cache maintenance: the slabs are written and read with relaxed agent-scope
-// atomic stores / loads (coherent across the XCDs' L2s), the writer waits for its stores
-// (vmcnt(0)) before its relaxed counter increment.  An agent-scope release / acquire fence instead
-// (L2 write-back + invalidate in every block) cost ~85 us per pass (measured, 1.25e7 x 32).
-constexpr int kFoldBatch = 32;  // slabs per group in flight at once (256 blocks / 8 groups)
-__device__ __forceinline__ void slab_put(double* p, double v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ double slab_get(const double* p) {
-  return __hip_atomic_load(const_cast<double*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void slab_fold_tail(const GramArgs& a, int T, int NT) {
-  __shared__ unsigned int s_last;
-  const int P = a.P, nb = gridDim.x, G = nb < kFoldGroups ? nb : kFoldGroups, g = blockIdx.x % G;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const unsigned int mine = (unsigned int)((nb - 1 - g) / G);  // this group's block count - 1
-    s_last = __hip_atomic_fetch_add(a.ticket + g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == mine;
-  }
-  __syncthreads();
-  if (!s_last) return;
-  const double* src = a.partials;
-  double* gs = a.partials + (int64_t)nb * P;
-  for (int o = threadIdx.x; o < P; o += blockDim.x) {
-    // every slab of the group in flight at once (the coherent loads miss L2: one round trip,
-    // not one per slab), then summed in ascending block order
-    double s = 0.0;
-    for (int b0 = g; b0 < nb; b0 += kFoldBatch * G) {
-      double v[kFoldBatch];
-#pragma unroll
-      for (int i = 0; i < kFoldBatch; ++i) {
-        const int b = b0 + i * G;
-        v[i] = b < nb ? slab_get(src + (int64_t)b * P + o) : 0.0;
-      }
-#pragma unroll
-      for (int i = 0; i < kFoldBatch; ++i) s += v[i];
-    }
-    slab_put(gs + (int64_t)g * P + o, s);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0)
-    s_last = __hip_atomic_fetch_add(a.ticket + kFoldGroups, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-             (unsigned int)(G - 1);
-  __syncthreads();
-  if (!s_last) return;
-  for (int o = threadIdx.x; o < P; o += blockDim.x) {
-    double v[kFoldGroups];
-#pragma unroll
-    for (int k = 0; k < kFoldGroups; ++k) v[k] = k < G ? slab_get(gs + (int64_t)k * P + o) : 0.0;
-    double s = 0.0;
-#pragma unroll
-    for (int k = 0; k < kFoldGroups; ++k) s += v[k];
-    fold_store(o, s, a.d, T, NT, a.fold_out);
-  }
-  if (threadIdx.x < kFoldTickets) a.ticket[threadIdx.x] = 0u;
-}
+// Slab stores: the slabs are folded by gram_fold_kernel after the kernel boundary (an in-kernel
+// fold by the last block of each XCD group was measured slower at the 8-GPU shard: 155 us vs
+// 142-148 us per fit, profiles/r3_fixed_cost.md; removed in round 4).
+__device__ __forceinline__ void slab_put(double* p, double v) { *p = v; }
 
 // =============================================================================================
 // bf16 MFMA kernel
@@ -474,7 +415,6 @@ __global__ __launch_bounds__((BF16Geom<NT, XMODE>::kBlock), 1) void gram_tall_bf
         for (int r = 0; r < 16; ++r) slab_put(tile + mfma32_row(lane, r) * 32 + col, (double)acc[p][r]);
       }
   }
-  if (a.ticket) slab_fold_tail(a, 32, NT);
 }
 
 // =============================================================================================
@@ -506,11 +446,13 @@ __global__ __launch_bounds__(256, (NT == 1 ? 3 : 2)) void gram_cols_kernel(GramA
 
   PackSrcG src[NT];
   bool fv[NT];
+  float sh[NT];  // the thread's feature shifts (GramArgs::xshift; 0 without one)
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
     const int feat = t * 32 + fl;
     fv[t] = feat < a.d;
     src[t] = srcs[fv[t] ? feat : 0];  // padding features load column 0 (branch-free) and stage zeros
+    sh[t] = (a.xshift && fv[t]) ? a.xshift[feat] : 0.0f;
   }
   const int64_t nsup = (a.n + 63) / 64, nfull = a.n / 64;
   const int64_t s0 = (int64_t)blockIdx.x * a.spw;
@@ -550,12 +492,15 @@ __global__ __launch_bounds__(256, (NT == 1 ? 3 : 2)) void gram_cols_kernel(GramA
     wl[2 * 64 + tid] = wy_hi;
     wl[3 * 64 + tid] = (__bf16)(float)(rv.wy - (double)(float)wy_hi);
   };
-  auto stage_x = [&](unsigned char* base, float (&x)[NT][8], uint64_t m) {
+  // x - s of the live rows to bf16 (dead rows and padding features exactly 0); sub = false: x
+  // is already shifted and masked (the guarded last superstep)
+  auto stage_x = [&](unsigned char* base, float (&x)[NT][8], uint64_t m, bool sub = true) {
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
+      const float s_t = sub ? sh[t] : 0.0f;
       bf16x8 v;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = (__bf16)(fv[t] && ((m >> (8 * j)) & 0xff) ? x[t][j] : 0.0f);
+      for (int j = 0; j < 8; ++j) v[j] = (__bf16)(fv[t] && ((m >> (8 * j)) & 0xff) ? x[t][j] - s_t : 0.0f);
       *reinterpret_cast<u32x4*>(base + (((t * 4 + (q & 3)) * 64 + 32 * (q >> 2) + fl) << 4)) = __builtin_bit_cast(u32x4, v);
     }
   };
@@ -621,9 +566,12 @@ __global__ __launch_bounds__(256, (NT == 1 ? 3 : 2)) void gram_cols_kernel(GramA
       else
 #pragma unroll
         for (int j = 0; j < 8; ++j) x[t][j] = 0.0f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (r0 + j < a.n) x[t][j] -= sh[t];  // rows past n stay 0
       mask8(a.sel, r0, a.n, x[t]);
     }
-    stage_x(smem + BUF, x, ~0ull);
+    stage_x(smem + BUF, x, ~0ull, false);
     if (tid < 64) {
       const RowVals rv = row_vals(a, st * 64 + tid);
       ra.add(rv);
@@ -702,7 +650,6 @@ __global__ __launch_bounds__(256, (NT == 1 ? 3 : 2)) void gram_cols_kernel(GramA
         for (int r = 0; r < 16; ++r) slab_put(tile + mfma32_row(lane, r) * 32 + col, (double)acc[p][r]);
       }
   }
-  if (a.ticket) slab_fold_tail(a, 32, NT);
 }
 
 constexpr int kStageLd = 66;  // f64 staging row stride (doubles): 2-double pad spreads the banks
@@ -1100,7 +1047,8 @@ __global__ __launch_bounds__(1024) void gram_fold_kernel(const double* __restric
 // feature-major [d, ld] (any dtype) -> MFMA-fragment-ordered bf16 tiles (see gram.h)
 template <typename TS>
 __global__ __launch_bounds__(256) void tile_bf16_kernel(const TS* __restrict__ X, int64_t ld, int d, int64_t n,
-                                                       int NT, int64_t nsup, uint16_t* __restrict__ out) {
+                                                       int NT, int64_t nsup, uint16_t* __restrict__ out,
+                                                       const float* __restrict__ shift) {
   // one thread = one 16-byte chunk (8 rows of one feature)
   const int64_t nchunks = nsup * NT * 4 * 64;
   for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < nchunks; c += (int64_t)gridDim.x * blockDim.x) {
@@ -1111,11 +1059,15 @@ __global__ __launch_bounds__(256) void tile_bf16_kernel(const TS* __restrict__ X
     const int64_t s = st / NT;
     const int f = t * 32 + (lane & 31);
     const int64_t r = s * 64 + 32 * (lane >> 5) + 8 * i;
+    const float sh = (shift && f < d) ? shift[f] : 0.0f;
     bf16x8 v;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       float x = 0.0f;
-      if (f < d && r + j < n) x = (float)X[(int64_t)f * ld + r + j];
+      if (f < d && r + j < n) {
+        if constexpr (sizeof(TS) == 8) x = (float)((double)X[(int64_t)f * ld + r + j] - (double)sh);
+        else x = (float)X[(int64_t)f * ld + r + j] - sh;
+      }
       v[j] = (__bf16)x;
     }
     reinterpret_cast<u32x4*>(out)[c] = __builtin_bit_cast(u32x4, v);
@@ -1125,7 +1077,8 @@ __global__ __launch_bounds__(256) void tile_bf16_kernel(const TS* __restrict__ X
 template <>
 __global__ __launch_bounds__(256) void tile_bf16_kernel<uint16_t>(const uint16_t* __restrict__ X, int64_t ld, int d,
                                                                  int64_t n, int NT, int64_t nsup,
-                                                                 uint16_t* __restrict__ out) {
+                                                                 uint16_t* __restrict__ out,
+                                                                 const float* __restrict__ shift) {
   const int64_t nchunks = nsup * NT * 4 * 64;
   for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < nchunks; c += (int64_t)gridDim.x * blockDim.x) {
     const int lane = (int)(c & 63);
@@ -1145,19 +1098,65 @@ __global__ __launch_bounds__(256) void tile_bf16_kernel<uint16_t>(const uint16_t
         for (int j = 0; j < 8; ++j) e[j] = (r + j < n) ? X[(int64_t)f * ld + r + j] : (uint16_t)0;
         v = __builtin_bit_cast(u32x4, e);
       }
+      if (shift) {  // bf16 source and a bf16-representable shift: x - s is usually exact
+        const float sh = shift[f];
+        bf16x8 b = __builtin_bit_cast(bf16x8, v);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) b[j] = (r + j < n) ? (__bf16)((float)b[j] - sh) : (__bf16)0.0f;
+        v = __builtin_bit_cast(u32x4, b);
+      }
     }
     reinterpret_cast<u32x4*>(out)[c] = v;
   }
 }
 
+// Un-shift of the packed statistics (gram.h: stats_unshift).  Pass 1 rewrites the Σxxᵀ entries
+// (reading the shifted column sums and Σw, which it does not write), pass 2 the column sums.
+__global__ __launch_bounds__(256) void unshift_aa_kernel(double* __restrict__ flat, const float* __restrict__ shift,
+                                                        int d) {
+  const double W = flat[1];
+  const double* as = flat + 5;
+  double* aa = flat + 5 + 2 * (int64_t)d;
+  const int64_t tot = (int64_t)d * (d + 1) / 2;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < tot; e += (int64_t)gridDim.x * blockDim.x) {
+    // packed upper, column-major: e = i + j (j + 1) / 2, i <= j
+    int64_t j = (int64_t)((sqrt(8.0 * (double)e + 1.0) - 1.0) * 0.5);
+    while (j * (j + 1) / 2 > e) --j;
+    while ((j + 1) * (j + 2) / 2 <= e) ++j;
+    const int64_t i = e - j * (j + 1) / 2;
+    const double si = (double)shift[i], sj = (double)shift[j];
+    aa[e] += si * as[j] + sj * as[i] + si * sj * W;
+  }
+}
+
+__global__ __launch_bounds__(256) void unshift_head_kernel(double* __restrict__ flat, const float* __restrict__ shift,
+                                                          int d) {
+  const double W = flat[1], B = flat[3];
+  for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < d; j += gridDim.x * blockDim.x) {
+    const double s = (double)shift[j];
+    flat[5 + d + j] += s * B;
+    flat[5 + j] += s * W;
+  }
+}
+
 }  // namespace
+
+void stats_unshift(double* flat, const float* shift, int d, hipStream_t st) {
+  if (d < 1) return;
+  const int64_t tot = (int64_t)d * (d + 1) / 2;
+  int64_t g = (tot + 255) / 256;
+  if (g > 4096) g = 4096;
+  hipLaunchKernelGGL(unshift_aa_kernel, dim3(g), dim3(256), 0, st, flat, shift, d);
+  hipLaunchKernelGGL(unshift_head_kernel, dim3((d + 255) / 256), dim3(256), 0, st, flat, shift, d);
+  DQ_HIP_CHECK(hipGetLastError());
+}
 
 int64_t tiled_elems(int d, int64_t n) {
   const int NT = (d + 31) / 32;
   return ((n + 63) / 64) * NT * 4 * 64 * 8;
 }
 
-void tile_bf16(const void* X, int xdt, int64_t ld, int d, int64_t n, void* out, hipStream_t st) {
+void tile_bf16(const void* X, int xdt, int64_t ld, int d, int64_t n, void* out, hipStream_t st, const float* shift) {
   const int NT = (d + 31) / 32;
   const int64_t nsup = (n + 63) / 64;
   const int64_t nchunks = nsup * NT * 256;
@@ -1166,10 +1165,10 @@ void tile_bf16(const void* X, int xdt, int64_t ld, int d, int64_t n, void* out, 
   if (g < 1) g = 1;
   uint16_t* o = reinterpret_cast<uint16_t*>(out);
   switch (xdt) {
-    case DT_BF16: hipLaunchKernelGGL(tile_bf16_kernel<uint16_t>, dim3(g), dim3(256), 0, st, (const uint16_t*)X, ld, d, n, NT, nsup, o); break;
-    case DT_F32: hipLaunchKernelGGL(tile_bf16_kernel<float>, dim3(g), dim3(256), 0, st, (const float*)X, ld, d, n, NT, nsup, o); break;
-    case DT_F64: hipLaunchKernelGGL(tile_bf16_kernel<double>, dim3(g), dim3(256), 0, st, (const double*)X, ld, d, n, NT, nsup, o); break;
-    case DT_I32: hipLaunchKernelGGL(tile_bf16_kernel<int32_t>, dim3(g), dim3(256), 0, st, (const int32_t*)X, ld, d, n, NT, nsup, o); break;
+    case DT_BF16: hipLaunchKernelGGL(tile_bf16_kernel<uint16_t>, dim3(g), dim3(256), 0, st, (const uint16_t*)X, ld, d, n, NT, nsup, o, shift); break;
+    case DT_F32: hipLaunchKernelGGL(tile_bf16_kernel<float>, dim3(g), dim3(256), 0, st, (const float*)X, ld, d, n, NT, nsup, o, shift); break;
+    case DT_F64: hipLaunchKernelGGL(tile_bf16_kernel<double>, dim3(g), dim3(256), 0, st, (const double*)X, ld, d, n, NT, nsup, o, shift); break;
+    case DT_I32: hipLaunchKernelGGL(tile_bf16_kernel<int32_t>, dim3(g), dim3(256), 0, st, (const int32_t*)X, ld, d, n, NT, nsup, o, shift); break;
     default: throw std::invalid_argument("tile_bf16: unsupported dtype");
   }
   DQ_HIP_CHECK(hipGetLastError());
@@ -1367,11 +1366,14 @@ void gram_tall(int mode, GramArgs a, int xmode, int blocks, double* out, hipStre
   a.P = (int)gram_partial_stride(mode, a.d);
   const size_t lds = mode == GRAM_BF16 ? bf16_lds(a.d, xmode) : f64_lds(a.d);
   if (a.tiled && mode != GRAM_BF16) throw std::invalid_argument("gram_tall: tiled storage needs bf16 mode");
-  // in-kernel fold: tall bf16 kernel only (the caller sized partials for blocks + kFoldGroups slabs)
-  const bool fold_in = reduce && a.ticket != nullptr && mode == GRAM_BF16 && a.cols == 0 &&
-                       !(a.xdt == DT_F32 && use_stream() && gram_stream_ok(mode, a));
-  if (!fold_in) a.ticket = nullptr;
-  a.fold_out = fold_in ? out : nullptr;
+  if (a.xshift) {
+    // only the f32 stream kernels subtract a shift (tiled storage is shifted when it is tiled)
+    if (!((mode == GRAM_F32 || mode == GRAM_BF16 || mode == GRAM_F32S) && a.xdt == DT_F32 && !a.tiled && a.cols == 0 &&
+          gram_stream_ok(mode, a)))
+      throw std::invalid_argument("gram_tall: a feature shift needs 16-byte aligned f32 features (stream kernel)");
+    gram_stream(mode, a, 1, blocks, out, st, reduce);  // XM = 1: dead / padding rows weigh 0, not -s
+    return;
+  }
   if (a.cols > 0) {
     if (mode != GRAM_F64 || a.cols != a.d || a.d > kSkinnyMaxD || a.tiled)
       throw std::invalid_argument("gram_tall: columnar sources need f64 mode and d <= 8");
@@ -1390,7 +1392,7 @@ void gram_tall(int mode, GramArgs a, int xmode, int blocks, double* out, hipStre
                 [&](auto kern) { hipLaunchKernelGGL(kern, dim3(blocks), dim3(block), lds, st, a); });
   }
   DQ_HIP_CHECK(hipGetLastError());
-  if (reduce && !fold_in) gram_reduce(mode, a.partials, blocks, a.d, out, st);
+  if (reduce) gram_reduce(mode, a.partials, blocks, a.d, out, st);
 }
 
 static size_t cols_lds(int NT) {
@@ -1438,11 +1440,10 @@ void gram_cols(GramArgs a, const PackSrcG* srcs_dev, int sdt, int blocks, double
   const int NT = (a.d + 31) / 32;
   const size_t lds = cols_lds(NT);
   if (a.ydt != DT_F64 && a.ydt != DT_F32) throw std::invalid_argument("gram_cols: label must be f32 or f64");
-  a.fold_out = a.ticket ? out : nullptr;  // in-kernel fold when the caller passed counters
   with_cols_kernel(NT, sdt, a.ydt,
                    [&](auto k) { hipLaunchKernelGGL(k, dim3(blocks), dim3(256), lds, st, a, srcs_dev); });
   DQ_HIP_CHECK(hipGetLastError());
-  if (!a.ticket) gram_reduce(GRAM_BF16, a.partials, blocks, a.d, out, st);
+  gram_reduce(GRAM_BF16, a.partials, blocks, a.d, out, st);
 }
 
 }  // namespace dq4ml

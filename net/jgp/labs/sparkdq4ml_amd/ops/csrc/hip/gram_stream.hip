@@ -471,8 +471,12 @@ __device__ __forceinline__ void gram_stream_f32_body(const GramArgs& a) {
   }
   double cs[NT], ab[NT];
   bool fvalid[NT];
+  float sh[NT];  // GramArgs::xshift of the lane's features (the host launches XM = 1 with a shift)
 #pragma unroll
-  for (int t = 0; t < NT; ++t) cs[t] = ab[t] = 0.0, fvalid[t] = t * 32 + f < a.d;
+  for (int t = 0; t < NT; ++t) {
+    cs[t] = ab[t] = 0.0, fvalid[t] = t * 32 + f < a.d;
+    sh[t] = (a.xshift && fvalid[t]) ? a.xshift[t * 32 + f] : 0.0f;
+  }
   RowAcc ra;
   int chunk = 0;
 
@@ -506,7 +510,7 @@ __device__ __forceinline__ void gram_stream_f32_body(const GramArgs& a) {
         for (int t = 0; t < NT; ++t) {
           const f32x4 v = *reinterpret_cast<const f32x4*>(st + t * G::kTileBytes + f * G::kFeatBytes + p * 16);
 #pragma unroll
-          for (int j = 0; j < 4; ++j) x[t][4 * u + j] = fvalid[t] ? v[j] : 0.0f;
+          for (int j = 0; j < 4; ++j) x[t][4 * u + j] = fvalid[t] ? v[j] - sh[t] : 0.0f;
         }
         const f32x4 w4 = *reinterpret_cast<const f32x4*>(stripe + (RS / 2) * h + RPS * i + 4 * u);
         const f32x4 wy4 = *reinterpret_cast<const f32x4*>(stripe + 64 + (RS / 2) * h + RPS * i + 4 * u);
@@ -852,7 +856,9 @@ void gram_stream(int mode, GramArgs a, int xmode, int blocks, double* out, hipSt
   }();
   a.interleave = interleave;
   a.P = (int)gram_partial_stride(mode, a.d);
-  const int xm = xmode != 0 ? 1 : 0;
+  if (a.xshift && mode == GRAM_F64) throw std::invalid_argument("gram_stream: f64 statistics take no feature shift");
+  // a shift makes the stored zeros of dead / padding rows -s: those rows must weigh 0 (XM = 1)
+  const int xm = (xmode != 0 || a.xshift) ? 1 : 0;
   with_stream_kernel(mode, a.xdt, a.d, xm, [&](auto kern, int wave_bytes) {
     const size_t lds = stream_lds(wave_bytes, mode, a.d);
     DQ_HIP_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));

@@ -30,10 +30,13 @@ constexpr int kWideZeroBytes = 16384;
 
 int64_t wide_tiled_bytes(int eb, int d, int64_t n);
 int64_t gram_wide_partials(int d, int splitk);
-void feature_amax(const PackSrcW* srcs_dev, int d, int64_t n, const uint8_t* sel, float* amax, hipStream_t st);
+// shift (null: none): per-feature f32 shift s; the amax is that of x - s and the pack stores
+// (x - s) [* inv_scale] (the Gram statistics are un-shifted in f64 afterwards: gram.h stats_unshift)
+void feature_amax(const PackSrcW* srcs_dev, int d, int64_t n, const uint8_t* sel, float* amax, hipStream_t st,
+                  const float* shift = nullptr);
 // eb = 16 (bf16) or 8 (fp8 e4m3, values multiplied by inv_scale[f] before conversion)
 void pack_wide(int eb, const PackSrcW* srcs_dev, int d, int64_t n, int nt, const uint8_t* sel, const float* inv_scale,
-               void* out, hipStream_t st);
+               void* out, hipStream_t st, const float* shift = nullptr);
 // zero the rows with sel[r] == 0 (and rows >= n) of a wide tiled matrix: in -> out (may alias)
 void wide_mask_rows(int eb, const void* in, void* out, int d, int64_t n, const uint8_t* sel, hipStream_t st);
 // out: flat WLS layout [count, wSum, wwSum, bSum, bbSum, aSum(d), abSum(d), aa packed-upper(d)]

@@ -488,8 +488,10 @@ __global__ __launch_bounds__(256) void gram_wide_reduce_kernel(WideArgs a, const
 // ---- packing into the wide tiled layouts ----------------------------------------------------
 // per-feature amax (for fp8 scales): one block per feature
 __global__ __launch_bounds__(256) void amax_kernel(const PackSrcW* __restrict__ srcs, int64_t n,
-                                                  const uint8_t* __restrict__ sel, float* __restrict__ amax) {
+                                                  const uint8_t* __restrict__ sel, float* __restrict__ amax,
+                                                  const float* __restrict__ shift) {
   const PackSrcW s = srcs[blockIdx.x];
+  const float sh = shift ? shift[blockIdx.x] : 0.0f;  // amax of the shifted column x - s
   float m = 0.0f;
   for (int64_t r = threadIdx.x; r < n; r += blockDim.x) {
     if (sel && !sel[r]) continue;
@@ -501,7 +503,7 @@ __global__ __launch_bounds__(256) void amax_kernel(const PackSrcW* __restrict__ 
       case DT_I32: v = (float)reinterpret_cast<const int32_t*>(s.ptr)[r]; break;
       default: v = 0.0f;
     }
-    m = fmaxf(m, fabsf(v));
+    m = fmaxf(m, fabsf(v - sh));
   }
   for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
   __shared__ float red[4];
@@ -519,7 +521,8 @@ template <int EB>
 __global__ __launch_bounds__(256) void pack_wide_kernel(const PackSrcW* __restrict__ srcs, int d, int64_t n, int NT,
                                                        int64_t nsup, const uint8_t* __restrict__ sel,
                                                        const float* __restrict__ inv_scale,
-                                                       unsigned char* __restrict__ out) {
+                                                       unsigned char* __restrict__ out,
+                                                       const float* __restrict__ shift) {
   const int fl = threadIdx.x >> 3, q = threadIdx.x & 7;
   const int ki = q >> 1, lane = 32 * (q & 1) + fl;
   const int64_t nchunks = nsup * NT;
@@ -532,6 +535,7 @@ __global__ __launch_bounds__(256) void pack_wide_kernel(const PackSrcW* __restri
     if (f < d) {
       const PackSrcW src = srcs[f];
       load8_f32(src.ptr, src.dt, r0, n, x);
+      if (shift) sub_shift8(x, shift[f], r0, n);
       mask8(sel, r0, n, x);
     } else {
 #pragma unroll
@@ -622,20 +626,21 @@ int64_t wide_tiled_bytes(int eb, int d, int64_t n) {
   return ((n + 63) / 64) * NT * 4 * 64 * (int64_t)eb;
 }
 
-void feature_amax(const PackSrcW* srcs_dev, int d, int64_t n, const uint8_t* sel, float* amax, hipStream_t st) {
-  hipLaunchKernelGGL(amax_kernel, dim3(d), dim3(256), 0, st, srcs_dev, n, sel, amax);
+void feature_amax(const PackSrcW* srcs_dev, int d, int64_t n, const uint8_t* sel, float* amax, hipStream_t st,
+                  const float* shift) {
+  hipLaunchKernelGGL(amax_kernel, dim3(d), dim3(256), 0, st, srcs_dev, n, sel, amax, shift);
   DQ_HIP_CHECK(hipGetLastError());
 }
 
 void pack_wide(int eb, const PackSrcW* srcs_dev, int d, int64_t n, int nt, const uint8_t* sel, const float* inv_scale,
-               void* out, hipStream_t st) {
+               void* out, hipStream_t st, const float* shift) {
   const int64_t nsup = (n + 63) / 64;
   int64_t g = nsup * nt;
   if (g > 16384) g = 16384;
   if (g < 1) g = 1;
   unsigned char* o = reinterpret_cast<unsigned char*>(out);
-  if (eb == 16) hipLaunchKernelGGL(pack_wide_kernel<16>, dim3(g), dim3(256), 0, st, srcs_dev, d, n, nt, nsup, sel, inv_scale, o);
-  else hipLaunchKernelGGL(pack_wide_kernel<8>, dim3(g), dim3(256), 0, st, srcs_dev, d, n, nt, nsup, sel, inv_scale, o);
+  if (eb == 16) hipLaunchKernelGGL(pack_wide_kernel<16>, dim3(g), dim3(256), 0, st, srcs_dev, d, n, nt, nsup, sel, inv_scale, o, shift);
+  else hipLaunchKernelGGL(pack_wide_kernel<8>, dim3(g), dim3(256), 0, st, srcs_dev, d, n, nt, nsup, sel, inv_scale, o, shift);
   DQ_HIP_CHECK(hipGetLastError());
 }
 

@@ -88,17 +88,15 @@ PYBIND11_MODULE(_dq4ml_hip, m) {
 
   // ---- Gram (K5) ---------------------------------------------------------------------------
   m.def("gram_partial_stride", &gram_partial_stride);
-  m.def("gram_fold_groups", [] { return kFoldGroups; });
-  m.def("gram_fold_tickets", [] { return kFoldTickets; });
   m.def("gram_default_blocks", &gram_default_blocks);
   m.def("gram_plan_blocks", &gram_plan_blocks);
   m.def("gram_tall",
         [](int mode, uintptr_t X, int64_t ld, int d, int64_t n, int xdt, uintptr_t y, int ydt, uintptr_t w, int wdt,
            uintptr_t sel, int xmode, uintptr_t partials, int blocks, uintptr_t out, uintptr_t stream, int tiled,
-           bool reduce, uintptr_t ticket) {
+           bool reduce, uintptr_t xshift) {
           GramArgs a{};
           a.tiled = tiled;
-          a.ticket = P<unsigned int>(ticket);
+          a.xshift = P<const float>(xshift);
           a.X = P<const void>(X);
           a.ld = ld;
           a.d = d;
@@ -114,9 +112,10 @@ PYBIND11_MODULE(_dq4ml_hip, m) {
         });
   m.def("gram_stream_cols",
         [](int mode, uintptr_t srcs, int d, int64_t n, int xdt, uintptr_t y, int ydt, uintptr_t w, int wdt,
-           uintptr_t sel, uintptr_t partials, int blocks, uintptr_t out, uintptr_t stream) {
+           uintptr_t sel, uintptr_t partials, int blocks, uintptr_t out, uintptr_t stream, uintptr_t xshift) {
           GramArgs a{};
           a.srcs = P<const int64_t>(srcs);
+          a.xshift = P<const float>(xshift);
           a.d = d;
           a.n = n;
           a.xdt = xdt;
@@ -126,14 +125,15 @@ PYBIND11_MODULE(_dq4ml_hip, m) {
           a.wdt = wdt;
           a.sel = P<const uint8_t>(sel);
           a.partials = P<double>(partials);
-          gram_stream(mode, a, (w || sel) ? 1 : 0, blocks, P<double>(out), as_stream(stream), true);
+          gram_stream(mode, a, (w || sel || xshift) ? 1 : 0, blocks, P<double>(out), as_stream(stream), true);
         });
   m.def("gram_stream_blocks", &gram_stream_blocks);
   m.def("gram_stream_rtc",
         [](int64_t handle, int mode, uintptr_t srcs, int d, int64_t n, uintptr_t rawtab, uintptr_t partials, int blocks,
-           int64_t lds, uintptr_t out, uintptr_t stream) {
+           int64_t lds, uintptr_t out, uintptr_t stream, uintptr_t xshift) {
           GramArgs a{};
           a.srcs = P<const int64_t>(srcs);
+          a.xshift = P<const float>(xshift);
           a.d = d;
           a.n = n;
           a.xdt = DT_F32;
@@ -167,11 +167,14 @@ PYBIND11_MODULE(_dq4ml_hip, m) {
   m.def("gram_reduce", [](int mode, uintptr_t partials, int blocks, int d, uintptr_t out, uintptr_t stream) {
     gram_reduce(mode, P<const double>(partials), blocks, d, P<double>(out), as_stream(stream));
   });
+  m.def("stats_unshift", [](uintptr_t flat, uintptr_t shift, int d, uintptr_t stream) {
+    stats_unshift(P<double>(flat), P<const float>(shift), d, as_stream(stream));
+  });
   m.def("gram_cols_blocks", &gram_cols_blocks);
   m.def("gram_cols", [](uintptr_t srcs, int sdt, int d, int64_t n, uintptr_t y, int ydt, uintptr_t sel,
-                        uintptr_t partials, int blocks, uintptr_t out, uintptr_t stream, uintptr_t ticket) {
+                        uintptr_t partials, int blocks, uintptr_t out, uintptr_t stream, uintptr_t xshift) {
     GramArgs a{};
-    a.ticket = P<unsigned int>(ticket);
+    a.xshift = P<const float>(xshift);
     a.d = d;
     a.n = n;
     a.xdt = DT_F32;
@@ -182,8 +185,9 @@ PYBIND11_MODULE(_dq4ml_hip, m) {
     gram_cols(a, P<const PackSrcG>(srcs), sdt, blocks, P<double>(out), as_stream(stream));
   });
   m.def("tiled_elems", &tiled_elems);
-  m.def("tile_bf16", [](uintptr_t X, int xdt, int64_t ld, int d, int64_t n, uintptr_t out, uintptr_t stream) {
-    tile_bf16(P<const void>(X), xdt, ld, d, n, P<void>(out), as_stream(stream));
+  m.def("tile_bf16", [](uintptr_t X, int xdt, int64_t ld, int d, int64_t n, uintptr_t out, uintptr_t stream,
+                        uintptr_t shift) {
+    tile_bf16(P<const void>(X), xdt, ld, d, n, P<void>(out), as_stream(stream), P<const float>(shift));
   });
   m.def("wls_small", [](uintptr_t flat, int nf, bool fit_intercept, double reg, double enet, bool std_f, bool std_l,
                         uintptr_t out, uintptr_t stream) {
@@ -230,15 +234,17 @@ PYBIND11_MODULE(_dq4ml_hip, m) {
   m.attr("WIDE_ZERO_BYTES") = kWideZeroBytes;
   m.def("gram_wide_partials", &gram_wide_partials);
   m.def("pack_wide", [](int eb, uintptr_t srcs_dev, int d, int64_t n, int nt, uintptr_t sel, uintptr_t inv_scale,
-                        uintptr_t out, uintptr_t stream) {
+                        uintptr_t out, uintptr_t stream, uintptr_t shift) {
     pack_wide(eb, P<const PackSrcW>(srcs_dev), d, n, nt, P<const uint8_t>(sel), P<const float>(inv_scale), P<void>(out),
-              as_stream(stream));
+              as_stream(stream), P<const float>(shift));
   });
   m.def("wide_mask_rows", [](int eb, uintptr_t in, uintptr_t out, int d, int64_t n, uintptr_t sel, uintptr_t stream) {
     wide_mask_rows(eb, P<const void>(in), P<void>(out), d, n, P<const uint8_t>(sel), as_stream(stream));
   });
-  m.def("feature_amax", [](uintptr_t srcs_dev, int d, int64_t n, uintptr_t sel, uintptr_t amax, uintptr_t stream) {
-    feature_amax(P<const PackSrcW>(srcs_dev), d, n, P<const uint8_t>(sel), P<float>(amax), as_stream(stream));
+  m.def("feature_amax", [](uintptr_t srcs_dev, int d, int64_t n, uintptr_t sel, uintptr_t amax, uintptr_t stream,
+                           uintptr_t shift) {
+    feature_amax(P<const PackSrcW>(srcs_dev), d, n, P<const uint8_t>(sel), P<float>(amax), as_stream(stream),
+                 P<const float>(shift));
   });
   auto wide_args = [](uintptr_t X, uintptr_t Xaug, uintptr_t zeros, int nt, int npanels, int d, int64_t nsup,
                       int splitk, uintptr_t part, double s1, double syh, double syl) {
@@ -325,8 +331,10 @@ PYBIND11_MODULE(_dq4ml_hip, m) {
   m.def("pack_src_bytes", []() { return (int)sizeof(PackSrc); });
 
   // ---- predict / metrics (K7/K8) ---------------------------------------------------------------
-  m.def("pack_tiled", [](uintptr_t srcs_dev, int d, int64_t n, uintptr_t sel, uintptr_t out, uintptr_t stream) {
-    pack_tiled(P<const PackSrc>(srcs_dev), d, n, P<const uint8_t>(sel), P<void>(out), as_stream(stream));
+  m.def("pack_tiled", [](uintptr_t srcs_dev, int d, int64_t n, uintptr_t sel, uintptr_t out, uintptr_t stream,
+                         uintptr_t shift) {
+    pack_tiled(P<const PackSrc>(srcs_dev), d, n, P<const uint8_t>(sel), P<void>(out), as_stream(stream),
+               P<const float>(shift));
   });
   m.def("predict", [](uintptr_t X, int xdt, int64_t ld, int d, int64_t n, uintptr_t coef, double b, uintptr_t out,
                       uintptr_t stream, int tiled) {

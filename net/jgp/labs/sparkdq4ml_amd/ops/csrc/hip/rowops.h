@@ -21,7 +21,9 @@ void compact_write(const uint8_t* sel, int64_t n, const int64_t* offsets, int64_
 void pack_columns(const PackSrc* srcs_dev, int d, int64_t n, void* out, int odt, int64_t ld, const uint8_t* sel,
                   hipStream_t st);
 
-void pack_tiled(const PackSrc* srcs_dev, int d, int64_t n, const uint8_t* sel, void* out, hipStream_t st);
+// shift: per-feature f32 shift subtracted before the bf16 cast (null: none)
+void pack_tiled(const PackSrc* srcs_dev, int d, int64_t n, const uint8_t* sel, void* out, hipStream_t st,
+                const float* shift = nullptr);
 void predict(const void* X, int xdt, int64_t ld, int d, int64_t n, const double* coef, double b, double* out,
              hipStream_t st, int tiled);
 int metrics_blocks(int64_t n);

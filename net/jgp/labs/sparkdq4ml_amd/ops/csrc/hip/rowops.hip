@@ -184,7 +184,7 @@ __device__ __forceinline__ double predict_row(const void* X, int xdt, int64_t ld
 // fragment of k-step q & 3 for lane half q >> 2 -> one 16-B store, no transpose.
 __global__ __launch_bounds__(256) void pack_tiled_kernel(const PackSrc* __restrict__ srcs, int d, int64_t n,
                                                         const uint8_t* __restrict__ sel, int NT, int64_t nsup,
-                                                        uint16_t* __restrict__ out) {
+                                                        uint16_t* __restrict__ out, const float* __restrict__ shift) {
   const int fl = threadIdx.x >> 3, q = threadIdx.x & 7;
   const int i = q & 3, h = q >> 2;
   const int64_t nchunks = nsup * NT;
@@ -197,6 +197,7 @@ __global__ __launch_bounds__(256) void pack_tiled_kernel(const PackSrc* __restri
     if (f < d) {
       const PackSrc src = srcs[f];
       load8_f32(src.ptr, src.dt, r0, n, x);
+      if (shift) sub_shift8(x, shift[f], r0, n);
       mask8(sel, r0, n, x);
     } else {
 #pragma unroll
@@ -421,14 +422,15 @@ void pack_columns(const PackSrc* srcs_dev, int d, int64_t n, void* out, int odt,
   DQ_HIP_CHECK(hipGetLastError());
 }
 
-void pack_tiled(const PackSrc* srcs_dev, int d, int64_t n, const uint8_t* sel, void* out, hipStream_t st) {
+void pack_tiled(const PackSrc* srcs_dev, int d, int64_t n, const uint8_t* sel, void* out, hipStream_t st,
+                const float* shift) {
   const int NT = (d + 31) / 32;
   const int64_t nsup = (n + 63) / 64;
   int64_t g = nsup * NT;
   if (g > 16384) g = 16384;
   if (g < 1) g = 1;
   hipLaunchKernelGGL(pack_tiled_kernel, dim3(g), dim3(256), 0, st, srcs_dev, d, n, sel, NT, nsup,
-                     reinterpret_cast<uint16_t*>(out));
+                     reinterpret_cast<uint16_t*>(out), shift);
   DQ_HIP_CHECK(hipGetLastError());
 }
 

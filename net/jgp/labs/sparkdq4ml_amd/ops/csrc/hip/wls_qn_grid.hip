@@ -275,7 +275,13 @@ __global__ __launch_bounds__(kQT) void wls_qn_grid_kernel(const double* __restri
   };
   record(adj);
   int why = converged();
+  int pass = 0;  // loop passes (uniform over the grid): w.scal is double-buffered by its parity
   while (why < 0 && !overflow) {
+    // scal[4 * (pass & 1) ..]: block 0 writes this pass's direction scalars while a slow block may
+    // still read the previous pass's -- a failed search runs no grid barrier between the read and
+    // block 0's next write
+    double* scal = w.scal + 4 * (pass & 1);
+    ++pass;
     // ---- block 0: two-loop recursion -> direction d (HBM), ag . d, g . g ---------------------
     if (b == 0) {
       auto dot = [&](const double* p, const double* q) {
@@ -359,15 +365,15 @@ __global__ __launch_bounds__(kQT) void wls_qn_grid_kernel(const double* __restri
       }
       const double initd = block_sum(pd, red), gg = block_sum(pg, red);
       if (t == 0) {
-        w.scal[0] = initd;
-        w.scal[1] = gg;
-        w.scal[2] = fail ? 1.0 : 0.0;
+        scal[0] = initd;
+        scal[1] = gg;
+        scal[2] = fail ? 1.0 : 0.0;
       }
     }
     __threadfence();
     grid.sync();
-    const double initd = w.scal[0], gg = w.scal[1];
-    bool fail = w.scal[2] != 0.0;
+    const double initd = scal[0], gg = scal[1];
+    bool fail = scal[2] != 0.0;
     double alpha = 0.0, nv = 0.0, nadj = 0.0, nagag = 0.0;
     if (!fail) {  // backtracking line search (Breeze BacktrackingLineSearch as OWLQN configures it)
       const double initfval = adj;
@@ -453,7 +459,11 @@ int wls_qn_grid_blocks(int k) {
   const int nb = cus;        // one block per CU: co-resident (the cooperative launch checks it)
   const int rows_min = 4;    // at least a few rows per block
   const int want = (k + rows_min - 1) / rows_min;
-  return nb < want ? nb : (want < 1 ? 1 : want);
+  const int blocks = nb < want ? nb : (want < 1 ? 1 : want);
+  // a thread owns one row of its block's A x: R = ceil(k / blocks) rows must fit kQT threads
+  if ((k + blocks - 1) / blocks > kQT)
+    throw std::runtime_error("wls_qn_grid: too few CUs for k (rows per block > threads per block)");
+  return blocks;
 }
 
 void wls_qn_grid(const double* flat, int nf, int fit_intercept, double reg, double enet, int std_f, int std_l,
@@ -461,7 +471,10 @@ void wls_qn_grid(const double* flat, int nf, int fit_intercept, double reg, doub
   const int k = fit_intercept ? nf + 1 : nf;
   if (nf < 1 || k > kWlsQnGridMaxK) throw std::invalid_argument("wls_qn_grid: k out of range");
   if (hist_cap < 1) throw std::invalid_argument("wls_qn_grid: hist_cap must be positive");
-  if (blocks < 1 || blocks > wls_qn_grid_blocks(k)) throw std::invalid_argument("wls_qn_grid: bad grid");
+  // (the caller's block count comes from wls_qn_grid_blocks, cached per device and k: no occupancy
+  // query on the launch path)
+  if (blocks < 1 || (k + blocks - 1) / blocks > kQT)
+    throw std::invalid_argument("wls_qn_grid: more rows per block than threads (each thread owns one row)");
   WlsQnWork w;
   double* p = work;
   auto take = [&](int64_t n) {

@@ -91,38 +91,45 @@ def _feature_view(X: torch.Tensor, align_elems: int):
 
 # ------------------------------------------------------------------------------------------
 from .layout import TiledBF16, TiledWide  # noqa: E402
+from .shift import column_shift  # noqa: E402
 
 FP8_MAX = 448.0
 
 
-def tile_bf16(X: torch.Tensor) -> TiledBF16:
+def _auto_shift(parts, shift, uniform=False):
+    """``shift`` = "auto": the sampled per-column shift of the sources (ops/shift.py), else as given."""
+    if isinstance(shift, str):
+        if shift != "auto":
+            raise ValueError(f"shift: 'auto', None or an ops.shift.Shift, not {shift!r}")
+        return column_shift(parts, uniform=uniform)
+    return shift
+
+
+def _sptr(shift) -> int:
+    return 0 if shift is None else shift.dev.data_ptr()
+
+
+def _unshift(h, out: torch.Tensor, shift, d: int) -> torch.Tensor:
+    """Statistics of x' = x - s -> those of x, in place on the current stream (gram.h
+    ``stats_unshift``); a no-op without a shift."""
+    if shift is not None:
+        h.stats_unshift(out.data_ptr(), shift.dev.data_ptr(), int(d), _stream())
+    return out
+
+
+def tile_bf16(X: torch.Tensor, shift="auto") -> TiledBF16:
+    """[d, n] features -> MFMA-fragment-ordered bf16 tiles of x - s (``shift``: "auto" = the
+    sampled per-column shift, None = unshifted, or an ``ops.shift.Shift``)."""
     h = native.hip()
     _check_dev(X)
     d, n = X.shape
     if X.stride(1) != 1:
         X = X.contiguous()
+    shift = _auto_shift([X], shift)
     ld = X.stride(0) if d > 1 else max(n, 1)
     buf = torch.empty(int(h.tiled_elems(d, n)), dtype=torch.bfloat16, device=X.device)
-    h.tile_bf16(X.data_ptr(), dtype_code(X), int(ld), int(d), int(n), buf.data_ptr(), _stream())
-    return TiledBF16(buf, d, n)
-
-
-_tickets = {}
-
-
-def _fold_ticket(h, dev):
-    """Counters of the Gram kernels' in-kernel slab fold (``slab_fold_tail`` in gram.hip), one
-    zeroed set per (device, stream): launches on one stream run in order and each leaves them
-    zeroed.  Opt-in (``DQ4ML_GRAM_FOLD=kernel``): same-box A/B at the 8-GPU shard (1.25e7 x 32)
-    155 us per fit vs 142-148 us with the separate ``gram_reduce`` kernel (profiles/r3_fold_ab.md)"""
-    if os.environ.get("DQ4ML_GRAM_FOLD", "separate") != "kernel":
-        return 0
-    st = torch.cuda.current_stream(dev)
-    key = (st.device.index, st.cuda_stream)
-    t = _tickets.get(key)
-    if t is None:
-        t = _tickets[key] = torch.zeros(int(h.gram_fold_tickets()), dtype=torch.int32, device=dev)
-    return t.data_ptr()
+    h.tile_bf16(X.data_ptr(), dtype_code(X), int(ld), int(d), int(n), buf.data_ptr(), _stream(), _sptr(shift))
+    return TiledBF16(buf, d, n, shift)
 
 
 class DeferredGram:
@@ -132,17 +139,22 @@ class DeferredGram:
 
     is_cuda = True
 
-    def __init__(self, h, mode, partials, nb, d, out):
+    def __init__(self, h, mode, partials, nb, d, out, shift=None):
         self._h, self.mode, self.partials, self.nb, self.d, self.out = h, mode, partials, nb, d, out
+        self.shift = shift
         self.device = out.device
 
     def finish(self) -> torch.Tensor:
-        """Enqueue the fold on the CURRENT stream (the caller orders it after the Gram kernel)."""
+        """Enqueue the fold (and the un-shift) on the CURRENT stream (the caller orders it after
+        the Gram kernel)."""
         st = faststream.current(faststream.dev_index(self.device))
         self.partials.record_stream(st)
         self.out.record_stream(st)
         self._h.gram_reduce(self.mode, self.partials.data_ptr(), int(self.nb), int(self.d), self.out.data_ptr(),
                             st.cuda_stream)
+        if self.shift is not None:
+            self.shift.dev.record_stream(st)
+            self._h.stats_unshift(self.out.data_ptr(), self.shift.dev.data_ptr(), int(self.d), st.cuda_stream)
         return self.out
 
 
@@ -183,6 +195,16 @@ def gram_stats(X, y, w, sel, compute: str = "fp64", x_zero_dead: bool = False, b
         X = X.to(torch.float32)
     if mode == 0 and X.dtype not in (torch.float64, torch.float32):
         X = X.to(torch.float64)
+    shift = None
+    if mode in (1, 2, 4):
+        # rounded features (bf16 / exact-f32 / split-f32 MFMA, f32 accumulators): centre the
+        # off-centre columns first (ops/shift.py); the stream kernels subtract in-kernel, other
+        # storage is tiled shifted once
+        shift = column_shift([X])
+        if shift is not None and X.dtype != torch.float32:
+            if mode == 2 and w is None:
+                return _gram_tiled(h, tile_bf16(X, shift), y, None, sel, False, blocks, defer)
+            X = X.to(torch.float32).contiguous()
     align = 16 // X.element_size()
     Xv, ld = _feature_view(X, align)
     y = y.contiguous()
@@ -210,14 +232,15 @@ def gram_stats(X, y, w, sel, compute: str = "fp64", x_zero_dead: bool = False, b
         xmode = 1
     else:
         xmode = 0
+    if shift is not None:
+        xmode = max(xmode, 1)  # dead / padding rows must weigh 0: their stored zeros are -s after the shift
     nb = int(blocks or _plan_blocks(h, mode, d, n, dtype_code(Xv), xmode))
     P = int(h.gram_partial_stride(mode, d))
-    tk = _fold_ticket(h, X.device) if mode == 2 else 0
-    partials = torch.empty((nb + (h.gram_fold_groups() if tk else 0)) * P, dtype=torch.float64, device=X.device)
+    partials = torch.empty(nb * P, dtype=torch.float64, device=X.device)
     h.gram_tall(mode, Xv.data_ptr(), int(ld), int(d), int(n), dtype_code(Xv), y.data_ptr(), dtype_code(y),
                 _ptr(w), dtype_code(w) if w is not None else 0, _ptr(sel), xmode, partials.data_ptr(), nb,
-                out.data_ptr(), _stream(), 0, True, tk)
-    return out
+                out.data_ptr(), _stream(), 0, True, _sptr(shift))
+    return _unshift(h, out, shift, d)
 
 
 def gram_skinny_cols(parts: List[torch.Tensor], y, w, sel, blocks: Optional[int] = None):
@@ -270,19 +293,19 @@ def gram_cols(parts: List[torch.Tensor], y, sel, blocks: Optional[int] = None):
         return out
     if sel is None:  # the kernel's loads are branch-free: an all-ones selection
         sel = _ones_sel(n, dev)
+    shift = column_shift(rows)
     desc = _srcw_desc(h, rows, dev)
     nb = int(blocks or _cols_blocks(h, d, n))
     P = int(h.gram_partial_stride(2, d))
-    tk = _fold_ticket(h, dev)
-    partials = torch.empty((nb + (h.gram_fold_groups() if tk else 0)) * P, dtype=torch.float64, device=dev)
+    partials = torch.empty(nb * P, dtype=torch.float64, device=dev)
     out = torch.empty(5 + 2 * d + d * (d + 1) // 2, dtype=torch.float64, device=dev)
     codes = {dtype_code(r) for r in rows}
     sdt = codes.pop() if len(codes) == 1 else -1
     if sdt not in (0, 1, 2) or any(r.data_ptr() % 16 for r in rows):
         sdt = -1  # mixed / unaligned columns: per-element typed loads
     h.gram_cols(desc.data_ptr(), int(sdt), d, n, y.data_ptr(), dtype_code(y), _ptr(sel), partials.data_ptr(), nb,
-                out.data_ptr(), _stream(), tk)
-    return out
+                out.data_ptr(), _stream(), _sptr(shift))
+    return _unshift(h, out, shift, d)
 
 
 _cols_plan = {}
@@ -327,10 +350,11 @@ def gram_stream_cols(parts, y, w, sel, compute: str):
         nb = _cols_plan[key] = int(h.gram_stream_blocks(mode, d, n, xc))
     P = int(h.gram_partial_stride(mode, d))
     partials = torch.empty(nb * P, dtype=torch.float64, device=dev)
+    shift = column_shift(rows) if mode in (1, 2, 4) else None  # rounded / f32-accumulated modes
     h.gram_stream_cols(mode, desc.data_ptr(), d, n, xc, y.data_ptr(), dtype_code(y), _ptr(w),
                        dtype_code(w) if w is not None else 0, _ptr(sel), partials.data_ptr(), nb, out.data_ptr(),
-                       _stream())
-    return out
+                       _stream(), _sptr(shift))
+    return _unshift(h, out, shift, d)
 
 
 def _ones_sel(n, dev):
@@ -386,12 +410,17 @@ class TiledGramPlan:
                     dtype_code(w) if w is not None else 0, _ptr(sel), xmode)
 
     def launch(self, stream: int, defer: bool):
-        """Enqueue the pass on ``stream``: a :class:`DeferredGram` (``defer``, the fold left to the
-        caller) or the folded statistics."""
+        """Enqueue the pass on ``stream``: a :class:`DeferredGram` (``defer``, the fold and the
+        un-shift left to the caller) or the folded, un-shifted statistics."""
         out = torch.empty(self.flat_len, dtype=torch.float64, device=self.dev)
         partials = torch.empty(self.part_len, dtype=torch.float64, device=self.dev)
         self.h.gram_tall(*self.pre, partials.data_ptr(), self.nb, out.data_ptr(), stream, 1, not defer, 0)
-        return DeferredGram(self.h, 2, partials, self.nb, self.d, out) if defer else out
+        sh = self.T.shift
+        if defer:
+            return DeferredGram(self.h, 2, partials, self.nb, self.d, out, sh)
+        if sh is not None:
+            self.h.stats_unshift(out.data_ptr(), sh.dev.data_ptr(), self.d, stream)
+        return out
 
 
 def _gram_tiled(h, T: "TiledBF16", y, w, sel, x_zero_dead, blocks, defer=False):
@@ -404,17 +433,14 @@ def _gram_tiled(h, T: "TiledBF16", y, w, sel, x_zero_dead, blocks, defer=False):
     xmode = 2 if w is not None else (1 if (sel is not None and not x_zero_dead) else 0)
     nb = int(blocks or _plan_blocks(h, 2, d, n, 2, xmode))
     P = int(h.gram_partial_stride(2, d))
-    # in-kernel fold (default): the kernel's last block writes the packed statistics, so there is
-    # nothing left to defer to the fit's side stream
-    tk = _fold_ticket(h, T.device)
-    defer = defer and not tk
-    partials = torch.empty((nb + (h.gram_fold_groups() if tk else 0)) * P, dtype=torch.float64, device=T.device)
+    partials = torch.empty(nb * P, dtype=torch.float64, device=T.device)
+    # (the tiles hold x - s already: the kernel takes no shift, the statistics are un-shifted after the fold)
     h.gram_tall(2, T.buf.data_ptr(), 0, int(d), int(n), 2, y.data_ptr(), dtype_code(y), _ptr(w),
                 dtype_code(w) if w is not None else 0, _ptr(sel), xmode, partials.data_ptr(), nb, out.data_ptr(),
-                _stream(), 1, not defer, tk)
+                _stream(), 1, not defer, 0)
     if defer:
-        return DeferredGram(h, 2, partials, nb, d, out)
-    return out
+        return DeferredGram(h, 2, partials, nb, d, out, T.shift)
+    return _unshift(h, out, T.shift, d)
 
 
 _syrk_pairs = {}
@@ -518,9 +544,11 @@ def _pack_desc(h, parts, dev):
     return rows, n, desc_dev
 
 
-def pack_tiled(parts: List[torch.Tensor], sel: Optional[torch.Tensor] = None) -> TiledBF16:
+def pack_tiled(parts: List[torch.Tensor], sel: Optional[torch.Tensor] = None, shift="auto") -> TiledBF16:
+    """Columns -> tiled bf16 of x - s, dead rows (``sel``) exactly 0 (``shift``: see tile_bf16)."""
     h = native.hip()
     dev = parts[0].device
+    shift = _auto_shift(parts, shift)
     rows, n, desc_dev = _pack_desc(h, parts, dev)
     d = len(rows)
     if d > 64:
@@ -531,9 +559,9 @@ def pack_tiled(parts: List[torch.Tensor], sel: Optional[torch.Tensor] = None) ->
         sel = sel.contiguous().to(torch.bool)
         if sel.numel() != n:
             raise ValueError("pack_tiled: selection length mismatch")
-    h.pack_tiled(desc_dev.data_ptr(), d, n, _ptr(sel), buf.data_ptr(), _stream())
+    h.pack_tiled(desc_dev.data_ptr(), d, n, _ptr(sel), buf.data_ptr(), _stream(), _sptr(shift))
     del rows
-    return TiledBF16(buf, d, n)
+    return TiledBF16(buf, d, n, shift)
 
 
 # ------------------------------------------------------------------------------------------
@@ -591,9 +619,16 @@ def _x_args(X):
     return X, dtype_code(X), (X.stride(0) if d > 1 else max(n, 1)), 0
 
 
+def _icpt(X, coef, intercept: float) -> float:
+    """Intercept for shifted storage: x . c + b = x' . c + (b + s . c)."""
+    sh = getattr(X, "shift", None)
+    return float(intercept) if sh is None else float(intercept) + sh.dot(coef)
+
+
 def predict(X, coef, intercept: float) -> torch.Tensor:
     h = native.hip()
     d, n = X.shape
+    intercept = _icpt(X, coef, intercept)
     Xb, xdt, ld, tiled = _x_args(X)
     _check_dev(Xb)
     c = _coef_dev(coef, X.device)
@@ -610,6 +645,7 @@ def predict(X, coef, intercept: float) -> torch.Tensor:
 def regression_metrics(X, y, coef, intercept, sel, shift):
     h = native.hip()
     d, n = X.shape
+    intercept = _icpt(X, coef, intercept)
     Xb, xdt, ld, tiled = _x_args(X)
     _check_dev(Xb, y, sel)
     y = y.contiguous()
@@ -630,6 +666,7 @@ def regression_metrics(X, y, coef, intercept, sel, shift):
 def huber_pass(X, y, w, sel, ceff, icpt, sigma, eps):
     h = native.hip()
     d, n = X.shape
+    icpt = _icpt(X, ceff, icpt)
     Xb, xdt, ld, tiled = _x_args(X)
     _check_dev(Xb, y, w, sel)
     y, w, sel = _prep_rows(y, w, sel, n)
@@ -646,6 +683,9 @@ def huber_pass(X, y, w, sel, ceff, icpt, sigma, eps):
                  mult.data_ptr(), partials.data_ptr(), out.data_ptr(), _stream())
     if fp8:  # the row pass saw q = x / scale
         out[4:] *= X.scales.to(torch.float64)
+    sh = getattr(X, "shift", None)
+    if sh is not None:  # Σ m x = Σ m x' + s Σ m  (out[2] = Σ m over the live rows)
+        out[4:] += sh.dev64 * out[2]
     return out
 
 
@@ -662,6 +702,7 @@ class LsqPasses:
         d, n = X.shape
         self.d, self.n = int(d), int(n)
         self.scales = None
+        self.shift = getattr(X, "shift", None)  # shifted storage: x = x' + s
         if isinstance(X, TiledWide):
             self._xb, self.layout, self.xdt, self.ld = X.buf, (2 if X.eb == 16 else 3), 2, 0
             if X.eb == 8:
@@ -703,13 +744,21 @@ class LsqPasses:
         if self.scales is not None:  # the pass saw q = x / scale
             out[:self.d] *= self.scales
             out[self.d:] *= self.scales * self.scales
+        if self.shift is not None:  # Σw x = Σw x' + sΣw,  Σw x² = Σw x'² + 2sΣw x' + s²Σw
+            s, W = self.shift.dev64, self.w.sum()
+            m1 = out[:self.d].clone()
+            out[self.d:] += (2.0 * s) * m1 + (s * s) * W
+            out[:self.d] += s * W
         return out
 
     def evaluate(self, cf: torch.Tensor, offset: torch.Tensor, inv_ystd: float) -> torch.Tensor:
         """[Σ ½ w diff², Σ w diff x_j (d)] with diff = x . cf + offset - y * inv_ystd (f64; ``offset``
         a one-element device tensor, read by the kernel: launching a pass needs no host sync)."""
         c = cf.to(torch.float64)
-        off = offset.to(torch.float64).reshape(1).contiguous()
+        off = offset.to(torch.float64).reshape(1)
+        if self.shift is not None:  # x . c + off = x' . c + (off + s . c)
+            off = off + (self.shift.dev64 * c).sum().reshape(1)
+        off = off.contiguous()
         if self.scales is not None:
             c = c * self.scales
         c = c.contiguous() if self.layout == 0 else c.to(torch.float32).contiguous()
@@ -721,6 +770,8 @@ class LsqPasses:
                             self._part[0].data_ptr(), out.data_ptr(), st)
         if self.scales is not None:
             out[1:] *= self.scales
+        if self.shift is not None:  # Σ v x = Σ v x' + s Σ v  (v = w diff per row)
+            out[1:] += self.shift.dev64 * self._v[:self.n].sum()
         return out
 
 
@@ -869,25 +920,34 @@ def _rows_of(parts):
 
 
 def pack_wide(parts: List[torch.Tensor], eb: int, sel: Optional[torch.Tensor] = None, nt: Optional[int] = None,
-              inv_scale: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None) -> TiledWide:
-    """Columns -> wide fragment layout (eb 16 = bf16, 8 = fp8 with per-feature scales).
+              inv_scale: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None,
+              shift="auto") -> TiledWide:
+    """Columns -> wide fragment layout (eb 16 = bf16, 8 = fp8 with per-feature scales) of x - s.
+
+    ``shift``: "auto" = the sampled per-column shift (ops/shift.py), the same on every
+    data-parallel rank (the banded wide fold all-reduces shifted statistics); None = unshifted; or
+    an ``ops.shift.Shift``.  fp8 scales are those of the shifted columns.
 
     The layout is superstep-major, so row blocks that are multiples of 64 rows pack independently
     into consecutive byte ranges of one image (``out``: a uint8 view of that range) — used to
-    stream-ingest matrices larger than one staging copy."""
+    stream-ingest matrices larger than one staging copy; such a block-wise ingest must pass the
+    whole matrix's ``shift`` (and ``inv_scale``) explicitly."""
     h = native.hip()
     dev = parts[0].device
     rows = _rows_of(parts)
     for r in rows:
         _check_dev(r)
     d, n = len(rows), rows[0].numel()
+    if isinstance(shift, str) and out is not None:
+        raise ValueError("pack_wide: a block-wise ingest (out=) needs the whole matrix's shift (None or a Shift)")
+    shift = _auto_shift(rows, shift, uniform=True)
     desc = _srcw_desc(h, rows, dev)
     if sel is not None:
         sel = sel.contiguous().to(torch.bool)
     scales = None
     if eb == 8 and inv_scale is None:
         amax = torch.empty(d, dtype=torch.float32, device=dev)
-        h.feature_amax(desc.data_ptr(), d, n, _ptr(sel), amax.data_ptr(), _stream())
+        h.feature_amax(desc.data_ptr(), d, n, _ptr(sel), amax.data_ptr(), _stream(), _sptr(shift))
         scales = torch.where(amax > 0, amax / FP8_MAX, torch.ones_like(amax))
         inv_scale = 1.0 / scales
     elif eb == 8:
@@ -900,9 +960,9 @@ def pack_wide(parts: List[torch.Tensor], eb: int, sel: Optional[torch.Tensor] = 
         buf = out
     else:
         buf = torch.empty(nbytes, dtype=torch.uint8, device=dev)
-    h.pack_wide(eb, desc.data_ptr(), d, n, nt, _ptr(sel), _ptr(inv_scale), buf.data_ptr(), _stream())
+    h.pack_wide(eb, desc.data_ptr(), d, n, nt, _ptr(sel), _ptr(inv_scale), buf.data_ptr(), _stream(), _sptr(shift))
     del rows
-    return TiledWide(buf, d, n, eb, scales)
+    return TiledWide(buf, d, n, eb, scales, shift)
 
 
 def mask_wide_rows(T: TiledWide, sel: torch.Tensor) -> TiledWide:
@@ -918,7 +978,7 @@ def mask_wide_rows(T: TiledWide, sel: torch.Tensor) -> TiledWide:
     if out.numel() != int(h.wide_tiled_bytes(T.eb, T.d, T.n)):
         raise ValueError("mask_wide_rows: storage size does not match the wide layout")
     h.wide_mask_rows(T.eb, T.buf.data_ptr(), out.data_ptr(), T.d, T.n, s.data_ptr(), _stream())
-    return TiledWide(out, T.d, T.n, T.eb, T.scales)
+    return TiledWide(out, T.d, T.n, T.eb, T.scales, T.shift)
 
 
 def tile_wide(X: torch.Tensor, eb: int, sel: Optional[torch.Tensor] = None) -> TiledWide:
@@ -1046,7 +1106,7 @@ def _gram_wide(h, T: TiledWide, y, w, sel, x_zero_dead):
         s_l = amax_l / FP8_MAX if amax_l > 0 else 1.0
         inv = _h2d(np.asarray([1.0, 1.0 / s_h, 1.0 / s_l], dtype=np.float32), dev)
     cols = [live.to(torch.float32), (y_hi * live).to(torch.float32), (y_lo * live).to(torch.float32)]
-    aug = pack_wide(cols, eb, None, nt=1, inv_scale=inv)
+    aug = pack_wide(cols, eb, None, nt=1, inv_scale=inv, shift=None)
     P = (d + 255) // 256
     pairs = _wide_pairs(P, os.environ.get("DQ4ML_WIDE_ORDER", "morton"))
     nsup = max(1, (n + 63) // 64)
@@ -1088,11 +1148,16 @@ def _gram_wide(h, T: TiledWide, y, w, sel, x_zero_dead):
                     splitk, pairs_dev.data_ptr(), part.data_ptr(), 1.0, float(s_h), float(s_l), _ptr(T.scales),
                     out.data_ptr(), _stream(), int(os.environ.get("DQ4ML_WIDE_RING", "5")),
                     int(os.environ.get("DQ4ML_WIDE_WAVES", "8")), not banded)
+    if banded and T.shift is not None and not T.shift.uniform:
+        raise ValueError("wide Gram over RCCL: the features' shift must be the same on every rank "
+                         "(pack_wide(shift='auto') agrees it; a caller-made Shift needs uniform=True)")
     if banded:
         fold = functools.partial(h.gram_wide_fold, P, d, splitk, part.data_ptr(), 1.0, float(s_h), float(s_l),
                                  _ptr(T.scales))
         _fold_all_reduce(fold, out, P, d)
-    return out
+    # statistics of x - s -> of x (f64, after the banded all-reduce too: pack_wide's shift is the
+    # same on every rank, so the un-shift of the sum is the sum of the un-shifts)
+    return _unshift(h, out, T.shift, d)
 
 
 def wide_bands(P: int, d: int, bucket_bytes: int, elt: int):

@@ -9,6 +9,12 @@ zero padded to whole supersteps, features to whole tiles.
 
 Everything that needs individual rows (show/collect/compaction) gathers them with
 :meth:`gather_rows`; the hot consumers (Gram, predict, metrics) read the tiles directly.
+
+Both layouts may store the features SHIFTED: ``shift`` (an ``ops.shift.Shift`` or None) holds a
+per-feature value ``s`` that was subtracted before the low-precision cast (``x' = x - s`` is
+what the tiles hold; dead and padding rows are exactly 0).  Consumers correct for it: the Gram
+un-shifts its statistics in f64, predictions add ``s . coef`` to the intercept, and
+:meth:`gather_rows` returns ``x' + s`` (f32).
 """
 from __future__ import annotations
 
@@ -29,10 +35,17 @@ def tiled_offsets(feats: torch.Tensor, rows: torch.Tensor, d: int) -> torch.Tens
     return ((((s * NT + t) * 4 + i) * 64 + lane) << 3) + j
 
 
+def _unshift_rows(vals: torch.Tensor, shift) -> torch.Tensor:
+    if shift is None:
+        return vals
+    return vals.to(torch.float32) + shift.dev.to(vals.device).unsqueeze(1)
+
+
 class TiledBF16:
-    def __init__(self, buf: torch.Tensor, d: int, n: int):
+    def __init__(self, buf: torch.Tensor, d: int, n: int, shift=None):
         assert buf.dtype == torch.bfloat16 and buf.dim() == 1
         self.buf, self.d, self.n = buf, int(d), int(n)
+        self.shift = shift
 
     @property
     def shape(self):
@@ -54,10 +67,10 @@ class TiledBF16:
         return 2
 
     def gather_rows(self, rows: torch.Tensor) -> torch.Tensor:
-        """Dense ``[d, k]`` bf16 of the given rows."""
+        """Dense ``[d, k]`` of the given rows: bf16, or f32 ``x' + s`` for shifted storage."""
         rows = rows.to(self.buf.device, torch.int64)
         f = torch.arange(self.d, device=self.buf.device, dtype=torch.int64).unsqueeze(1)
-        return self.buf[tiled_offsets(f, rows.unsqueeze(0), self.d)]
+        return _unshift_rows(self.buf[tiled_offsets(f, rows.unsqueeze(0), self.d)], self.shift)
 
     def to_dense(self) -> torch.Tensor:
         return self.gather_rows(torch.arange(self.n, device=self.buf.device))
@@ -89,9 +102,10 @@ def wide_offsets(feats: torch.Tensor, rows: torch.Tensor, d: int, eb: int = 16) 
 class TiledWide:
     """Wide MFMA-fragment storage: bf16 (eb=16) or fp8 e4m3 OCP with per-feature scales (eb=8)."""
 
-    def __init__(self, buf: torch.Tensor, d: int, n: int, eb: int, scales=None):
+    def __init__(self, buf: torch.Tensor, d: int, n: int, eb: int, scales=None, shift=None):
         self.buf, self.d, self.n, self.eb = buf, int(d), int(n), int(eb)
-        self.scales = scales  # f32 [d] (fp8 only): x = q * scale
+        self.scales = scales  # f32 [d] (fp8 only): x = q * scale (+ shift)
+        self.shift = shift
 
     @property
     def nt(self):
@@ -121,9 +135,9 @@ class TiledWide:
         f = torch.arange(self.d, device=self.buf.device, dtype=torch.int64).unsqueeze(1)
         off = wide_offsets(f, rows.unsqueeze(0), self.d, self.eb)
         if self.eb == 16:
-            return self.buf.view(torch.bfloat16)[off]
+            return _unshift_rows(self.buf.view(torch.bfloat16)[off], self.shift)
         q = self.buf.view(torch.float8_e4m3fn)[off].to(torch.float32)
-        return q * self.scales.unsqueeze(1)
+        return _unshift_rows(q * self.scales.unsqueeze(1), self.shift)
 
     def to_dense(self) -> torch.Tensor:
         return self.gather_rows(torch.arange(self.n, device=self.buf.device))

@@ -309,10 +309,16 @@ def try_fused_stream(plan, features_col: str, label_col: str, session, gram_dtyp
     partials = torch.empty(blocks * P, dtype=torch.float64, device=dev)
     out = torch.empty(5 + 2 * d + d * (d + 1) // 2, dtype=torch.float64, device=dev)
     from ..utils import tracing
+    from .shift import column_shift
 
+    # off-centre feature columns are shifted in-kernel before the bf16 / f32 rounding (ops/shift.py)
+    shift = column_shift([tbl.columns[k].values for k in feat_cols])
+    st = torch.cuda.current_stream(dev).cuda_stream
     with tracing.span("stream_dq_gram"):
         h.gram_stream_rtc(int(handle), cp.mode, desc.data_ptr(), d, n, rawtab.data_ptr(), partials.data_ptr(), blocks,
-                          int(lds), out.data_ptr(), torch.cuda.current_stream(dev).cuda_stream)
+                          int(lds), out.data_ptr(), st, 0 if shift is None else shift.dev.data_ptr())
+        if shift is not None:
+            h.stats_unshift(out.data_ptr(), shift.dev.data_ptr(), d, st)
     tracing.add_rows("stream_dq_gram", n)
     STATS["stream_grams"] += 1
     return FusedGram(out, d, [], n)

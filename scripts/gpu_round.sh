@@ -52,11 +52,6 @@ for s in $STEPS; do
            step f32s2_c 300 python bench.py --steps 20 --warmup 3 --dtype fp32split &&
            step f32s2_d 300 python bench.py --steps 20 --warmup 3 --dtype bf16 --storage fp32 &&
            (export TMPDIR=/tmp; step f32s2pmc 300 timeout -s KILL 240 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_SALU GRBM_GUI_ACTIVE -d gpurun_out/f32s2pmc -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --dtype fp32split) || exit $? ;;
-    fold) step fold_t 600 python -u -m pytest tests/test_gpu_fold.py tests/test_gpu_kernels.py tests/test_gpu_determinism.py tests/test_gpu_rccl.py -m gpu -q --timeout 120 --timeout-method thread &&
-          for r in 1 2; do for m in separate kernel; do
-            step fold_${m}_s${r} 300 env DQ4ML_GRAM_FOLD=$m python bench.py --steps 200 --warmup 20 --rows 1.25e7 &&
-            step fold_${m}_f${r} 300 env DQ4ML_GRAM_FOLD=$m DQ4ML_FORCE_COLLECTIVES=1 python bench.py --steps 200 --warmup 20 --rows 1.25e7 &&
-            step fold_${m}_h${r} 300 env DQ4ML_GRAM_FOLD=$m python bench.py --steps 30 --warmup 5 || exit $?; done; done ;;
     qn) step qn_t 600 python -u -m pytest tests/test_gpu_owlqn.py -m gpu -v --timeout 120 --timeout-method thread &&
         step qn_b 600 python scripts/owlqn_bench.py &&
         step qn_bt 600 env DQ4ML_QN_ENGINE=torch CASES=4096:0.01 python scripts/owlqn_bench.py || exit $? ;;

@@ -28,7 +28,7 @@ for r0 in range(0, n, chunk):
     Xc = torch.randn(d, r1 - r0, generator=g, device="cuda").to(torch.bfloat16)
     lo = r0 * per_row
     hi = lo + ((r1 - r0 + 63) // 64) * 64 * per_row
-    device.pack_wide([Xc], eb, None, inv_scale=inv if eb == 8 else None, out=buf[lo:hi])
+    device.pack_wide([Xc], eb, None, inv_scale=inv if eb == 8 else None, out=buf[lo:hi], shift=None)
     del Xc
 T = TiledWide(buf, d, n, eb, scale if eb == 8 else None)
 y = torch.randn(n, generator=g, device="cuda")

@@ -151,7 +151,8 @@ def main():
         r1 = min(n4, r0 + ch)
         xc = torch.randn(d4, r1 - r0, generator=g, device=dev)
         y4[r0:r1] = xc[0] + 1.0
-        devops.pack_wide([xc], 16, None, out=buf4[r0 * per_row:r0 * per_row + ((r1 - r0 + 63) // 64) * 64 * per_row])
+        devops.pack_wide([xc], 16, None, out=buf4[r0 * per_row:r0 * per_row + ((r1 - r0 + 63) // 64) * 64 * per_row],
+                         shift=None)
     T4 = TiledWide(buf4, d4, n4, 16)
     flat4 = devops.gram_stats(T4, y4, None, None, "bf16")
     head4 = flat4[:2].tolist()

@@ -197,3 +197,17 @@ def test_dp_lbfgs_passes_match_single_process(cpu_session):
         assert len(hist) == ref.summary.totalIterations
     # every rank runs the same optimizer on the same all-reduced evaluations
     assert res[0][1] == res[1][1] and res[0][3] == res[1][3]
+
+
+@pytest.mark.parametrize("mode", ["passes", "gram"])
+def test_constant_label_without_intercept(cpu_session, mode):
+    """Spark 2.4 ``LinearRegression.train``: a constant nonzero label with fitIntercept=false cannot
+    be regularized (``require(regParam == 0.0)``); unregularized it fits through the origin."""
+    g = torch.Generator().manual_seed(3)
+    X = torch.randn(3, 500, generator=g, dtype=torch.float64) + 2.0
+    df = cpu_session.createDataFrame({"features": X, "label": torch.full((500,), 4.0, dtype=torch.float64)})
+    with pytest.raises(ValueError, match="standard deviation of the label is zero. Model cannot be regularized"):
+        _fit(cpu_session, df, mode, fitIntercept=False, regParam=0.1)
+    m = _fit(cpu_session, df, mode, fitIntercept=False, regParam=0.0, tol=1e-12, maxIter=200)
+    ls = np.linalg.lstsq(X.numpy().T, np.full(500, 4.0), rcond=None)[0]  # through the origin
+    np.testing.assert_allclose(m.coefficients.toArray(), ls, rtol=1e-4, atol=1e-6)
