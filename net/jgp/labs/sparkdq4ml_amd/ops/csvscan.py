@@ -192,17 +192,64 @@ def _finish(parts, types, st, dev, hinted=False):
         keeps = [p[3][:p[0]] for _, p in live]
         k = torch.cat(keeps) if len(keeps) > 1 else keeps[0]
         table = Table(table.schema, table.columns, total, k.clone(), dev).compact()
-    # what a later fused scan of the same bytes relies on (ops/scanfuse.py): line count (empty
-    # lines included) and the columns holding nulls
-    nc = len(types)
-    nonempty = int(total) - int(st[:, 1].sum())
-    table.scan_facts = {"nlines": int(total), "nullable": [bool(int(st[:, 2 + c].sum())) for c in range(nc)],
-                        "fast_only": int(st[:, 2 + 2 * nc].sum()) == 0,
-                        "empty_lines": int(st[:, 1].sum()), "max_line": int(st[:, 3 + 2 * nc].max()),
-                        "uniform_fields": int(st[:, 4 + 2 * nc].sum()) == nonempty * (nc - 1),
-                        "min_line": max(1, int(st[:, 5 + 2 * nc].min())) if len(st) else 1,
-                        "term_kinds": [int(st[:, 6 + 2 * nc + k].sum()) for k in range(3)]}
+    table.scan_facts = _facts(st, len(types), int(total))
     return table
+
+
+def _facts(st: np.ndarray, nc: int, total: int) -> dict:
+    """What a later fused scan of the same bytes relies on (ops/scanfuse.py, ops/scancut.py),
+    from the chunks' parse stats: line count (empty lines included), the columns holding nulls,
+    the fast-path / field-count / line-length / terminator facts."""
+    nonempty = int(total) - int(st[:, 1].sum())
+    return {"nlines": int(total), "nullable": [bool(int(st[:, 2 + c].sum())) for c in range(nc)],
+            "fast_only": int(st[:, 2 + 2 * nc].sum()) == 0,
+            "empty_lines": int(st[:, 1].sum()), "max_line": int(st[:, 3 + 2 * nc].max()),
+            "uniform_fields": int(st[:, 4 + 2 * nc].sum()) == nonempty * (nc - 1),
+            "min_line": max(1, int(st[:, 5 + 2 * nc].min())) if len(st) else 1,
+            "term_kinds": [int(st[:, 6 + 2 * nc + k].sum()) for k in range(3)]}
+
+
+def infer_streamed(src, sep: str, ncols: Optional[int] = None, sharded: bool = False, opts: Optional[dict] = None,
+                   user_types: Optional[list] = None):
+    """Schema inference over an input that is not resident in HBM (``runtime.streams.ChunkSource``):
+    Spark's inference pass at ``load()`` (``DataQuality4MachineLearningApp.java:53-55``) as one
+    streamed device parse whose column planes are dropped chunk by chunk -- only the type masks and
+    the facts survive, so memory stays at one chunk.  Returns (type codes, facts) or None (the
+    input needs the host scanner)."""
+    if len(sep) != 1:
+        return None
+    if user_types:
+        if any(t not in STRICT_CODES for t in user_types):
+            return None
+        opts = dict(opts or {}, strict=True)
+        ncols = len(user_types)
+    h = native.hip()
+    if ncols is None:
+        head = bytes(memoryview(src.data)[:min(src.n, 1 << 20)])
+        ncols = _ncols_of(head, sep, int(_opt_args(opts)["comment"] or 0))
+    if ncols > 256 or not len(src):
+        return None
+    hint = list(user_types) if user_types else None
+    sts, total = [], 0
+    for buf, n, trailing in src.chunks():
+        nlines, _cols, _valid, _keep, stats = _scan_chunk(h, buf, n, trailing, ncols, sep, src.device, hint, opts)
+        total += nlines
+        sts.append(stats)
+    st = torch.stack(sts).cpu().numpy()
+    if user_types:
+        flag = int(st[:, 0].max())
+        if sharded:
+            flag = int(comm.all_reduce_max(torch.tensor([flag], dtype=torch.int64))[0])
+        if flag:
+            return None
+        types = list(user_types)
+    else:
+        types = _resolve_types(np.bitwise_or.reduce(st[:, 2 + ncols:2 + 2 * ncols], axis=0), int(st[:, 0].max()),
+                               sharded)
+        if types is None:
+            return None
+    STATS["streamed_inferences"] = STATS.get("streamed_inferences", 0) + 1
+    return types, _facts(st, ncols, total)
 
 
 def _resolve_types(masks: np.ndarray, flag: int, sharded: bool):

@@ -753,6 +753,8 @@ def try_fused_scan(nodes, rel, plan, session):
     consumes the sub-chain instead) or None (not fusable: the caller scans, then runs the chain)."""
     from ..sql.table import ColumnData, Table
 
+    if rel.fused.get("buf") is None:  # streamed input (§5g): rows are stored by the chunked eager scan
+        return None
     cp = _compile(nodes, rel)
     if cp is None or cp == "vector":
         return cp
@@ -826,6 +828,8 @@ def try_fused_gram(plan, features_col: str, label_col: str, session) -> Optional
     chain = list(reversed(nodes[1:])) + [gtop]
     from . import scancut
 
+    if p.fused.get("buf") is None:  # input not resident in HBM: the same kernels over a chunk ring
+        return _streamed_gram(chain, p, d)
     cut = scancut.try_cut_gram(chain, p, d)  # the byte-parallel field cutter (wide rows, any d <= 128)
     if cut is not None:
         flat, err, vflag, ccp = cut
@@ -858,3 +862,63 @@ def try_fused_gram(plan, features_col: str, label_col: str, session) -> Optional
     checks = [_fact_check(p, vflag)] + ([_udf_error_check(chain, err)] if cp.has_raise else [])
     STATS["fused_grams"] += 1
     return FusedGram(flat, d, [c for c in checks if c is not None], int(p.fused["nlines"]))
+
+
+class _ChunkRel:
+    """One row-aligned chunk of a streamed relation, as the fused-scan launchers see a relation:
+    the relation's facts with the chunk's device bytes (``buf``, ``n``, ``trailing``)."""
+
+    def __init__(self, rel, fused):
+        self.fused, self.label, self._rel = fused, rel.label, rel
+
+    def schema(self):
+        return self._rel.schema()
+
+
+def _streamed_gram(chain, rel, d: int) -> Optional[FusedGram]:
+    """the fit's one fused pass over an input that does not stay resident in HBM.
+    The relation's ``ChunkSource`` streams row-aligned chunks through a two-slot device ring (the
+    H2D copy of chunk k+1 on the side stream overlaps the kernels of chunk k on the compute
+    stream); every chunk runs the same compiled scan + DQ chain + assembler + Gram kernel as the
+    resident path (the byte-parallel cutter, or the per-line kernel for d <= 8 short rows), and the
+    chunks' f64 statistics sum into one accumulator on the device in chunk order (deterministic).
+    Spark streams the partitions of ``DataQuality4MachineLearningApp.java:53-55`` through its
+    iterators the same way, at constant memory."""
+    from . import scancut
+
+    f = rel.fused
+    src = f["stream"]
+    if not len(src):
+        return None
+    s0, e0 = src.spans[0]
+    probe = _ChunkRel(rel, dict(f, buf=None, n=e0 - s0, trailing=False, stream=None))
+    use_cut = scancut._compile(chain, probe, d) is not None
+    cp = None
+    if not use_cut:
+        if d > 8:
+            return None
+        cp = _compile(chain, probe, gram=d)
+        if cp is None or cp == "vector":
+            return None
+    acc, checks = None, []
+    for buf, n, trailing in src.chunks():
+        crel = _ChunkRel(rel, dict(f, buf=buf, n=n, trailing=trailing, stream=None))
+        if use_cut:
+            cut = scancut.try_cut_gram(chain, crel, d)
+            if cut is None:
+                raise RuntimeError("streamed fused Gram: the cutter plan did not apply to a chunk")
+            flat, err, vflag, ccp = cut
+            raising = ccp.has_raise
+        else:
+            extra = {}
+            _, _, err, vflag, _side, _cur = _launch(cp, chain, crel, extra, own_stream=False)
+            tot = extra["gpart"].sum(0)
+            flat = torch.cat([tot[:1].expand(3), tot[1:]])
+            raising = cp.has_raise
+        acc = flat.clone() if acc is None else acc.add_(flat)
+        checks.append(_fact_check(rel, vflag))
+        if raising:
+            checks.append(_udf_error_check(chain, err))
+    STATS["fused_grams"] += 1
+    STATS["streamed_grams"] = STATS.get("streamed_grams", 0) + 1
+    return FusedGram(acc, d, [c for c in checks if c is not None], int(f["nlines"]))

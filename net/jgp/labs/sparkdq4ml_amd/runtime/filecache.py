@@ -6,7 +6,7 @@ and each re-scan then streams the cached bytes to the device by direct DMA (~57 
 MI355X box, 1 GB in 17 ms) with no host copy at all.  A rewritten file gets a new entry.
 
 With ``dq4ml.csv.deviceCache`` (default on) the raw bytes of the rank's byte range also stay
-resident in HBM (288 GB per MI355X): a re-scan then parses straight from device memory — the
+resident in HBM (288 GB per MI355X; the cap is derived from the free HBM, ``device_cap_bytes``): a re-scan then parses straight from device memory — the
 parse, DQ rules, assembly and fit all still run on every action; only the transfer of unchanged
 input bytes is skipped, the way the OS page cache skips the disk read for Spark.
 
@@ -23,7 +23,8 @@ from concurrent.futures import ThreadPoolExecutor
 
 import torch
 
-__all__ = ["PinnedFile", "open_pinned", "shard_range", "map_readonly", "device_bytes_allowed", "clear"]
+__all__ = ["PinnedFile", "MappedFile", "open_pinned", "open_mapped", "shard_range", "map_readonly",
+           "device_bytes_allowed", "device_cap_bytes", "clear"]
 
 MAX_FILES = int(os.environ.get("DQ4ML_FILECACHE_FILES", "2"))
 MAX_BYTES = int(float(os.environ.get("DQ4ML_FILECACHE_BYTES", str(32 << 30))))
@@ -82,13 +83,94 @@ class PinnedFile:
         return t
 
 
-MAX_DEVICE_BYTES = int(float(os.environ.get("DQ4ML_FILECACHE_DEVICE_BYTES", str(64 << 30))))
+# HBM kept free for everything an action allocates besides the cached input bytes (parsed columns
+# of an eager scan, Gram partials, the staging ring, the caching allocator's slack)
+HEADROOM_FRACTION = 0.25
+HEADROOM_MIN = 24 << 30
 
 
-def device_bytes_allowed(nbytes: int) -> bool:
+def device_cap_bytes(device=None) -> int:
+    """Bytes of input the device cache may hold: ``DQ4ML_FILECACHE_DEVICE_BYTES`` if set, else what
+    the device has free now (plus what this cache already holds) minus a headroom of 25 % of the
+    HBM, at least 24 GiB -- about 190 GB of a 288 GB MI355X; the cap is no longer a fixed 64 GiB."""
+    env = os.environ.get("DQ4ML_FILECACHE_DEVICE_BYTES")
+    if env:
+        return int(float(env))
+    if not torch.cuda.is_available():
+        return 0
+    dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+    free, total = torch.cuda.mem_get_info(dev)
+    held = _held(dev)
+    return max(0, int(free) + held - max(int(total * HEADROOM_FRACTION), HEADROOM_MIN))
+
+
+def _held(dev=None) -> int:
+    entries = list(_cache.values()) + list(_mapped.values())
+    return sum(t.numel() for pf in entries for k, t in pf._dev.items() if dev is None or k[0] == str(dev))
+
+
+def device_bytes_allowed(nbytes: int, device=None) -> bool:
     """Device residency within the cap, counting the cached entries."""
-    used = sum(t.numel() for pf in _cache.values() for t in pf._dev.values())
-    return used + nbytes <= MAX_DEVICE_BYTES
+    return _held(None if device is None else torch.device(device)) + nbytes <= device_cap_bytes(device)
+
+
+class MappedFile:
+    """A byte range too large for the pinned host cache: a read-only map of the file, plus the same
+    per-range facts a ``PinnedFile`` keeps (the device scan's type hints and scan facts) and its
+    HBM-resident copy when the device cache allows one (filled chunk by chunk through the pinned
+    staging ring, never a whole-range host copy)."""
+
+    host = None  # no page-locked copy: chunks are staged
+
+    def __init__(self, path: str, lo: int, hi: int):
+        self.path, self.lo, self.nbytes = path, lo, hi - lo
+        self._map = map_readonly(path)
+        self.data = memoryview(self._map)[lo:hi]
+        self._dev = {}
+        self.type_hints = {}
+        self.scan_facts = {}
+
+    def device_bytes(self, device, lo: int = 0, hi: int = -1, chunk_bytes: int = 1 << 30) -> torch.Tensor:
+        hi = self.nbytes if hi < 0 else hi
+        key = (str(device), lo, hi)
+        t = self._dev.get(key)
+        if t is None:
+            from .streams import StagingRing
+
+            t = torch.empty(hi - lo, dtype=torch.uint8, device=device)
+            cb = max(1, min(chunk_bytes, hi - lo))
+            ring = StagingRing(cb, depth=2, device=torch.device(device))
+            spans = [(a, min(hi, a + cb)) for a in range(lo, hi, cb)]
+            if spans:
+                ring.put(0, self.data[spans[0][0]:spans[0][1]])
+            for i, (a, b) in enumerate(spans):
+                if i + 1 < len(spans):
+                    ring.put(i + 1, self.data[spans[i + 1][0]:spans[i + 1][1]])
+                t[a - lo:b - lo].copy_(ring.get(i))
+                ring.release(i)
+            self._dev[key] = t
+        return t
+
+
+_mapped: "OrderedDict[tuple, MappedFile]" = OrderedDict()
+
+
+def open_mapped(path: str, lo: int = 0, hi: int = -1) -> MappedFile:
+    """The (cached) :class:`MappedFile` of bytes [lo, hi) of ``path``, keyed like ``open_pinned``."""
+    st = os.stat(path)
+    hi = st.st_size if hi < 0 else hi
+    key = (os.path.realpath(path), st.st_size, st.st_mtime_ns, lo, hi)
+    with _lock:
+        mf = _mapped.get(key)
+        if mf is not None:
+            _mapped.move_to_end(key)
+            return mf
+        for k in [k for k in _mapped if k[0] == key[0] and k[1:3] != key[1:3]]:
+            del _mapped[k]
+        mf = _mapped[key] = MappedFile(path, lo, hi)
+        while len(_mapped) > MAX_FILES:
+            _mapped.popitem(last=False)
+        return mf
 
 
 def map_readonly(path: str):
@@ -152,3 +234,4 @@ def open_pinned(path: str, lo: int = 0, hi: int = -1) -> PinnedFile:
 def clear():
     with _lock:
         _cache.clear()
+        _mapped.clear()

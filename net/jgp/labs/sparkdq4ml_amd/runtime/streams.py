@@ -8,7 +8,7 @@ from typing import Dict, List, Optional
 import numpy as np
 import torch
 
-__all__ = ["side_stream", "StagingRing"]
+__all__ = ["side_stream", "StagingRing", "ChunkSource"]
 
 _side: Dict[int, "torch.cuda.Stream"] = {}
 
@@ -99,3 +99,74 @@ class StagingRing:
         ev = torch.cuda.Event()
         ev.record(torch.cuda.current_stream())
         self.consumed[k] = ev
+
+
+class ChunkSource:
+    """An input byte range that is NOT resident in HBM, streamed through the device in row-aligned
+    chunks (Spark streams partitions through iterators at constant memory,
+    ``DataQuality4MachineLearningApp.java:40, 53-55``).
+
+    ``data``: the bytes on the host (a read-only map or a page-locked copy); ``pinned``: a
+    page-locked tensor view of the same bytes when there is one (the DMA then reads it directly).
+    :meth:`chunks` yields ``(device view, nbytes, trailing)`` per chunk: chunk k+1's H2D copy runs
+    on the side stream while the caller's kernels consume chunk k on the current stream (a
+    two-slot ring of ``chunk_bytes`` device buffers, kept across actions)."""
+
+    def __init__(self, data, pinned: Optional[torch.Tensor], chunk_bytes: int, device):
+        from ..ops.csvscan import chunk_bounds
+
+        self.data, self.pinned, self.device = data, pinned, torch.device(device)
+        self.n = len(data)
+        self.bounds = chunk_bounds(data, max(1, int(chunk_bytes)))
+        self.spans = [(self.bounds[i], self.bounds[i + 1]) for i in range(len(self.bounds) - 1)]
+        self._ring = None
+
+    def __len__(self):
+        return len(self.spans)
+
+    def _ring_for(self):
+        if self._ring is None:
+            width = max((e - s for s, e in self.spans), default=1)
+            self._ring = StagingRing(width, depth=2, device=self.device, staging=self.pinned is None)
+        return self._ring
+
+    def _put(self, ring, i):
+        s, e = self.spans[i]
+        if self.pinned is not None:
+            ring.put(i, None, pinned=self.pinned[s:e])
+            return
+        with torch.cuda.device(self.device):  # (runs on the staging thread)
+            ring.put(i, memoryview(self.data)[s:e])
+
+    def chunks(self):
+        """Chunks in order.  A mapped (not page-locked) source is memcpy'd into the pinned staging
+        buffers by one background thread, so chunk k+1's host copy and DMA both overlap the
+        consumer's work on chunk k."""
+        if not self.spans:
+            return
+        ring = self._ring_for()
+        pool = None
+        if self.pinned is None:
+            if getattr(self, "_pool", None) is None:
+                from concurrent.futures import ThreadPoolExecutor
+
+                self._pool = ThreadPoolExecutor(1)
+            pool = self._pool
+        pending = {}
+
+        def stage(i):
+            if pool is None:
+                self._put(ring, i)
+            else:
+                pending[i] = pool.submit(self._put, ring, i)
+
+        stage(0)
+        for i, (s, e) in enumerate(self.spans):
+            if i + 1 < len(self.spans):
+                stage(i + 1)  # overlaps the consumer's kernels on chunk i
+            if i in pending:
+                pending.pop(i).result()
+            buf = ring.get(i)
+            trailing = e > s and self.data[e - 1] not in (10, 13)
+            yield buf, e - s, trailing
+            ring.release(i)

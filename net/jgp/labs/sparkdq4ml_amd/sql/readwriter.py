@@ -224,9 +224,10 @@ class DataFrameReader:
                 data, pinned = pf.data, pf.host
             else:
                 # larger than the pinned cache may hold: a read-only map, streamed through the
-                # pinned staging ring chunk by chunk (no copy of the whole range is ever made)
-                pf = None
-                data = memoryview(filecache.map_readonly(files[0]))[lo:hi]
+                # pinned staging ring chunk by chunk (no copy of the whole range is ever made); the
+                # entry still keeps the range's facts and, if HBM allows, its device-resident bytes
+                pf = filecache.open_mapped(files[0], lo, hi)
+                data = pf.data
         else:
             pf = None
             data = b"".join(self._read_bytes(f) for f in files)
@@ -314,6 +315,19 @@ class DataFrameReader:
                     t = Table(StructType(fields), t.columns, t.nrows, t.sel, t.device)
                 return t
 
+            # input that cannot stay resident in HBM: one streamed inference pass
+            # (types + facts, no column kept), then a lazy relation whose fused Gram action
+            # streams the bytes through a chunk ring -- one pass per action at constant memory
+            stream_min = int(float(self._session.conf.get("dq4ml.csv.streamThresholdBytes", str(1 << 30))))
+            streamed = (pf is not None and dbytes is None and len(body) >= stream_min
+                        and _truthy(self._session.conf.get("dq4ml.csv.fuseScan", "true")))
+            if shard:  # every rank takes the same (collective) path
+                streamed = all(comm.all_gather_object(bool(streamed)))
+            if streamed:
+                rel = self._streamed_relation(body, pinned, pf, fkey, dopts, sep, strict, ncols, final, shard, dev,
+                                              data, header, infer, user_types, user_names)
+                if rel is not None:
+                    return rel
             # a re-read of bytes an earlier device scan already typed: lazy relation, scanned at
             # the action — fused with the DQ chain on top of it when there is one (ops/scanfuse.py)
             facts = pf.scan_facts.get(fkey) if (pf is not None and dbytes is not None) else None
@@ -355,6 +369,56 @@ class DataFrameReader:
             if t is not None:
                 return t
         return self._host_table(data, header, infer, user_types, user_names, sep, dev, shard)
+
+    def _streamed_relation(self, body, pinned, pf, fkey, dopts, sep, strict, ncols, final, shard, dev, data, header,
+                           infer, user_types, user_names):
+        """Lazy ``CsvScanRelation`` over bytes that stream through the device (``fused["stream"]``:
+        a ``runtime.streams.ChunkSource``; ``fused["buf"]`` is None).  The inference pass runs once
+        per cached byte range (its types and facts are kept with the file entry)."""
+        from ..ops.csvscan import _KIND, _opt_args, infer_streamed
+        from ..runtime.streams import ChunkSource
+        from ..sql.plan import CsvScanRelation
+
+        chunk = int(float(self._session.conf.get("dq4ml.csv.streamChunkBytes", str(1 << 30))))
+        skey = fkey + ("stream", chunk)
+        ent = pf.scan_facts.get(skey)
+        if ent is None:
+            src = ChunkSource(body, None if pinned is None else pinned[len(data) - len(body):], chunk, dev)
+            with tracing.span("csv_infer_streamed"):
+                r = infer_streamed(src, sep, ncols=ncols, sharded=shard, opts=dopts, user_types=strict)
+            if r is None:
+                return None
+            codes, facts = r
+            ent = pf.scan_facts[skey] = (codes, facts, src)
+        codes, facts, src = ent
+        if facts["nlines"] <= 0 or len(codes) > 256:
+            return None
+        fnames = final or [f"_c{i}" for i in range(len(codes))]
+        schema = StructType([StructField(nm, csv_code_to_type(c), True) for nm, c in zip(fnames, codes)])
+        n = len(body)
+        fused = {"buf": None, "stream": src, "n": n, "nlines": facts["nlines"], "device": dev,
+                 "trailing": n > 0 and body[-1] not in (10, 13), "mean_line": n / facts["nlines"],
+                 "kinds": [_KIND.get(c, (0,))[0] for c in codes], "nullable": list(facts["nullable"]),
+                 "fast_only": bool(facts.get("fast_only")), "max_line": int(facts.get("max_line", 1 << 30)),
+                 "uniform_fields": bool(facts.get("uniform_fields")), "empty_lines": int(facts.get("empty_lines", 1)),
+                 "min_line": int(facts.get("min_line", 1)), "term_kinds": list(facts.get("term_kinds") or (1, 1, 0)),
+                 "opts": dict(_opt_args(dopts), sep=sep, strict=bool(strict)), "strict": bool(strict)}
+        if fused["opts"]["null_value"] and len(fused["opts"]["null_value"].encode()) > 16:
+            fused = None
+
+        def scan_eager():  # any action the streamed fused Gram does not cover: the chunked device scan
+            from ..ops import csvscan
+
+            with tracing.span("csv_scan"):
+                t = csvscan.scan_device(body, sep=sep, infer=infer, device=dev, sharded=shard, ncols=ncols,
+                                        chunk_bytes=int(self._session.conf.get("dq4ml.chunkBytes", str(256 << 20))),
+                                        pinned=None if pinned is None else pinned[len(data) - len(body):],
+                                        types_hint=None if strict else list(codes), opts=dopts, user_types=strict)
+            if t is None:
+                return self._host_table(data, header, infer, user_types, user_names, sep, dev, shard)
+            fields = [StructField(nm, f.dataType, True) for nm, f in zip(fnames, t.schema.fields)]
+            return Table(StructType(fields), t.columns, t.nrows, t.sel, t.device)
+        return CsvScanRelation(schema, scan_eager, fused, "Relation[csv]")
 
     def _host_table(self, data, header, infer, user_types, user_names, sep, dev, shard) -> Table:
         from ..parallel import comm
