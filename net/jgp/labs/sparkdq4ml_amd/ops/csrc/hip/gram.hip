@@ -190,8 +190,12 @@ __device__ __forceinline__ void fold_store(int o, double t, int d, int T, int NT
 
 // Slab stores: the slabs are folded by gram_fold_kernel after the kernel boundary (an in-kernel
 // fold by the last block of each XCD group was measured slower at the 8-GPU shard: 155 us vs
-// 142-148 us per fit, profiles/r3_fixed_cost.md; removed in round 4).
-__device__ __forceinline__ void slab_put(double* p, double v) { *p = v; }
+// 142-148 us per fit, profiles/r3_fixed_cost.md; removed in round 4).  Relaxed agent-scope
+// stores write through to memory (nothing is left dirty in this XCD's L2 for the fold kernel's
+// boundary to flush) -- the form the round-3 headline was measured with.
+__device__ __forceinline__ void slab_put(double* p, double v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
 // =============================================================================================
 // bf16 MFMA kernel

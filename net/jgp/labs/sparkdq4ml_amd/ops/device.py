@@ -1092,11 +1092,16 @@ def _gram_wide(h, T: TiledWide, y, w, sel, x_zero_dead):
     yd = y.to(torch.float64)
     live = torch.ones(n, dtype=torch.float64, device=dev) if sel is None else sel.to(torch.float64)
     eb = T.eb
+    t_y = 0.0
     if eb == 16:
         y_hi = yd.to(torch.bfloat16).to(torch.float64)
         inv = None
         s_h = s_l = 1.0
     else:  # y = y_hi + y_lo, each an fp8 value times its own scale (y_hi exactly representable)
+        # the label is centred first (t = its live mean): two e4m3 digits of y - t carry ~8 bits
+        # relative to the label's spread instead of to its largest magnitude (ops/shift.py)
+        t_y = float((yd * live).sum() / live.sum().clamp_min(1.0)) if n else 0.0
+        yd = (yd - t_y) * live
         amax_h = float((yd * live).abs().max()) if n else 0.0
         s_h = amax_h / FP8_MAX if amax_h > 0 else 1.0
         y_hi = (yd / s_h).clamp(-FP8_MAX, FP8_MAX).to(torch.float8_e4m3fn).to(torch.float64) * s_h
@@ -1151,10 +1156,13 @@ def _gram_wide(h, T: TiledWide, y, w, sel, x_zero_dead):
     if banded and T.shift is not None and not T.shift.uniform:
         raise ValueError("wide Gram over RCCL: the features' shift must be the same on every rank "
                          "(pack_wide(shift='auto') agrees it; a caller-made Shift needs uniform=True)")
+    head_fix = (lambda: _unshift_label(out, d, t_y)) if t_y != 0.0 else None
     if banded:
         fold = functools.partial(h.gram_wide_fold, P, d, splitk, part.data_ptr(), 1.0, float(s_h), float(s_l),
                                  _ptr(T.scales))
-        _fold_all_reduce(fold, out, P, d)
+        _fold_all_reduce(fold, out, P, d, head_fix)  # (the label shift is per rank: un-shifted before the wire)
+    elif head_fix is not None:
+        head_fix()
     # statistics of x - s -> of x (f64, after the banded all-reduce too: pack_wide's shift is the
     # same on every rank, so the un-shift of the sum is the sum of the un-shifts)
     return _unshift(h, out, T.shift, d)
@@ -1178,7 +1186,17 @@ def wide_bands(P: int, d: int, bucket_bytes: int, elt: int):
     return bands
 
 
-def _fold_all_reduce(fold, out: torch.Tensor, P: int, d: int):
+def _unshift_label(out: torch.Tensor, d: int, t: float) -> None:
+    """Head statistics of a label shifted by t (y' = y - t) -> those of y, in place (f64):
+    Σy² = Σy'² + 2tΣy' + t²W, Σy = Σy' + tW, Σx·y = Σx·y' + tΣx (Σx as folded, i.e. of the
+    features as they are stored)."""
+    W, b = out[1:2], out[3:4].clone()
+    out[4:5] += (2.0 * t) * b + (t * t) * W
+    out[3:4] += t * W
+    out[5 + d:5 + 2 * d] += t * out[5:5 + d]
+
+
+def _fold_all_reduce(fold, out: torch.Tensor, P: int, d: int, head_fix=None):
     """X1 for the wide Gram, overlapped with its own fold: band i's all-reduce is issued right
     after band i's fold is enqueued, so RCCL (its own stream, ordered after the fold at issue
     time) reduces band i over xGMI while the compute stream folds band i + 1.  Wire format
@@ -1201,6 +1219,8 @@ def _fold_all_reduce(fold, out: torch.Tensor, P: int, d: int):
             # reduced in f64: counts above 2^24 stay exact and the variances E[x²] - E[x]² keep
             # their digits; only the packed Σxx bands may take the f32 wire
             fold(out.data_ptr(), 0, J0, J1, stream)
+            if head_fix is not None and J0 == P:
+                head_fix()
             works.append(dist.all_reduce(out[lo:hi], op=dist.ReduceOp.SUM, async_op=True))
     for w in works:
         w.wait()  # the compute stream waits for every band's collective

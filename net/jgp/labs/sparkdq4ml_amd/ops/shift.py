@@ -16,8 +16,8 @@ special handling; how close ``s`` is to the true mean only decides how many digi
 ``s`` is the mean of a strided sample of the column (at most 65 536 rows, every row's position
 equally likely to be sampled), rounded to f32 -- or to bf16 for a bf16 source, so that ``x - s``
 of two bf16 values of similar magnitude is exact.  A column that the sample shows already
-centered (``|mean| <= std / 2``) gets ``s = 0``; when every column is centered there is no shift
-at all and the kernels run exactly as before.  The sample costs one small host read per source
+centred (``|mean| <= std``) gets ``s = 0``; when every column is centred (or there are fewer than
+256 rows) there is no shift at all and the kernels run exactly as before.  The sample costs one small host read per source
 matrix, memoized per source tensor.
 """
 from __future__ import annotations
@@ -31,7 +31,8 @@ import torch
 __all__ = ["Shift", "column_shift", "SAMPLE_ROWS", "CENTER_RATIO"]
 
 SAMPLE_ROWS = 65536
-CENTER_RATIO = 0.5  # |mean| <= CENTER_RATIO * std: already centered, s = 0
+CENTER_RATIO = 1.0  # |mean| <= CENTER_RATIO * std: already centred, s = 0 (bf16 keeps 2^-8 of 2 std)
+MIN_ROWS = 256      # fewer rows: no shift (f32 sums of a handful of rows stay exact enough)
 
 
 class Shift:
@@ -111,7 +112,7 @@ def column_shift(parts: Sequence[torch.Tensor], uniform: bool = False) -> Option
     where shifted statistics are all-reduced before they are un-shifted: the wide Gram's f32
     wire).  Reads one small sample back to the host (memoized per source tensor)."""
     rows = _rows_of(parts)
-    if not rows or rows[0].numel() == 0:
+    if not rows or rows[0].numel() < MIN_ROWS:
         return None
     from ..parallel import comm
 
