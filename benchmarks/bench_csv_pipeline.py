@@ -174,8 +174,12 @@ def main(argv=None):
           "value": rows * a.steps / elapsed, "unit": "rows/s", "n_gpus": world, "steps": a.steps,
           "warmup": a.warmup, "ms_per_step": elapsed / a.steps * 1e3, "higher_is_better": True,
           "scaling": "strong", "vs_baseline": None, "dtype": "fp64",
-          "data": f"synthetic CSV {nbytes / 1e9:.2f} GB (guest,price; CR terminators)",
-          "config": {"model": "DataQuality4MachineLearningApp fit path (maxIter 40, regParam 1, elasticNet 1)",
+          "data": (f"synthetic CSV {nbytes / 1e9:.2f} GB (guest,price; CR terminators)" if d == 1 else
+                   f"synthetic CSV {nbytes / 1e9:.2f} GB ({d} float features + label per row; CR terminators)"),
+          "config": {"model": ("DataQuality4MachineLearningApp fit path (maxIter 40, regParam 1, elasticNet 1)"
+                               if d == 1 else
+                               f"RangeRule(label in (0, 150]) DQ filter -> VectorAssembler({d} columns) -> "
+                               f"LinearRegression(solver=normal, regParam 1e-3)"),
                      "global_batch": rows, "csv_gbytes_per_s": nbytes * a.steps / elapsed / 1e9,
                      "rows_after_dq": int(model.summary.numInstances),
                      "coefficients": [float(v) for v in model.coefficients.toArray()],

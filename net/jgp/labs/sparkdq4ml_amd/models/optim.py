@@ -213,30 +213,24 @@ def owlqn_result(host: np.ndarray, nf: int):
     return wls, GramStats.scalars_only(host[nf + 2:nf + 7], nf)
 
 
+QN_DEVICE_MAX_K = 4608  # kWlsQnGridMaxK (wls_small.h): the device OWLQN's largest k
+
+
 def wls_owlqn_device(flat, nf, fit_intercept, reg_param, elastic_net, standardize_features, standardize_label,
                      max_iter, tol):
-    """The OWLQN branch with the statistics on the device: the HIP solvers (one wave for
-    k <= 128, one cooperative grid launch up to ``QN_DEVICE_MAX_K``; one D2H of the result), the
-    host-steered torch OWLQN only when forced (``DQ4ML_QN_ENGINE=torch``, A/B) or beyond.
-    None = the native host driver owns the case."""
+    """The OWLQN branch with the statistics on the device: one wave for k <= 128
+    (``wls_qn_kernel``), one cooperative grid launch up to ``QN_DEVICE_MAX_K`` (``wls_qn_grid.hip``);
+    one D2H of the result.  None = the native host driver owns the case (k beyond the grid
+    solver, or a short-circuit the kernel hands back).  (The round-2/3 host-steered torch OWLQN,
+    kept for A/B, lost at every k: profiles/r3_owlqn_grid.md; removed in round 4.)"""
     from ..ops import device
-    from .owlqn_device import QN_DEVICE_MAX_K, QN_TORCH_MIN_K, qn_engine, solve_owlqn_device
 
     k = nf + 1 if fit_intercept else nf
-    if k <= QN_DEVICE_MAX_K and qn_engine() == "hip":
-        out = device.wls_qn_small(flat, nf, fit_intercept, reg_param, elastic_net, standardize_features,
-                                  standardize_label, max_iter, tol)
-        return owlqn_result(out.cpu().numpy(), nf)
-    if k < QN_TORCH_MIN_K:
-        return None  # the host driver's packed dspmv is still cheaper than host-steered GEMVs here
-    r = solve_owlqn_device(flat, nf, fit_intercept, reg_param, elastic_net, standardize_features,
-                           standardize_label, max_iter, tol)
-    if r is None:
+    if k > QN_DEVICE_MAX_K:
         return None
-    coef, icpt, hist, reason = r
-    log.info("quasi-newton converged: %s after %d states", reason, len(hist))
-    head = flat[:5].cpu().numpy()
-    return WLSModel(coef, icpt, np.zeros(1), hist, "owlqn"), GramStats.scalars_only(head, nf)
+    out = device.wls_qn_small(flat, nf, fit_intercept, reg_param, elastic_net, standardize_features,
+                              standardize_label, max_iter, tol)
+    return owlqn_result(out.cpu().numpy(), nf)
 
 
 def _check_status(status: int, singular_fallback: bool = False):

@@ -519,10 +519,10 @@ def _async_fit(df, flat, d, args) -> bool:
     _, _, fit_icpt, reg, enet = args[:5]
     # L1 (OWLQN, the lab's own regParam=1 / elasticNetParam=1) runs on the device too: one wave
     # for k <= 128, one cooperative grid launch up to QN_DEVICE_MAX_K (wls_qn_grid.hip)
-    from .owlqn_device import QN_DEVICE_MAX_K, qn_engine
+    from .optim import QN_DEVICE_MAX_K
 
     if enet != 0.0 and reg != 0.0:
-        return qn_engine() == "hip" and d + (1 if fit_icpt else 0) <= QN_DEVICE_MAX_K
+        return d + (1 if fit_icpt else 0) <= QN_DEVICE_MAX_K
     return d <= 64
 
 

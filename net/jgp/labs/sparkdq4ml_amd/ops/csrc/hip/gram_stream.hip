@@ -847,14 +847,10 @@ void gram_stream(int mode, GramArgs a, int xmode, int blocks, double* out, hipSt
   a.spw = (nstage + total_waves - 1) / total_waves;
   if (a.spw < 1) a.spw = 1;
   a.nsuper = nstage;
-  // contiguous stage ranges per wave by default: interleaved stages measured neutral for f64 / f32,
-  // +1 % for bf16 on f32 storage and +2.6 % for config 4's 64 separate column streams (each wave's
-  // 256-B column pieces lose their DRAM page locality); DQ4ML_GRAM_STREAM_INTERLEAVE=1 for A/B
-  static const int interleave = [] {
-    const char* e = getenv("DQ4ML_GRAM_STREAM_INTERLEAVE");
-    return e && e[0] == '1' ? 1 : 0;
-  }();
-  a.interleave = interleave;
+  // contiguous stage ranges per wave: interleaved stages measured neutral for f64 / f32, +1 % for
+  // bf16 on f32 storage and +2.6 % for config 4's 64 separate column streams (each wave's 256-B
+  // column pieces lose their DRAM page locality); the interleaved A/B knob was removed in round 4
+  a.interleave = 0;
   a.P = (int)gram_partial_stride(mode, a.d);
   if (a.xshift && mode == GRAM_F64) throw std::invalid_argument("gram_stream: f64 statistics take no feature shift");
   // a shift makes the stored zeros of dead / padding rows -s: those rows must weigh 0 (XM = 1)

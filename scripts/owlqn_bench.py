@@ -1,8 +1,7 @@
 """OWLQN solve timing (L1 WLS): device vs the native host driver on the same statistics.
 
 k <= 128: the one-wave HIP solver (``wls_qn_kernel``); up to 4608: the cooperative grid solver
-(``wls_qn_grid.hip``); ``DQ4ML_QN_ENGINE=torch``: the host-steered torch OWLQN
-(``models/owlqn_device.py``).  Statistics from a synthetic fp64 fit of the given width."""
+(``wls_qn_grid.hip``).  Statistics from a synthetic fp64 fit of the given width."""
 import json
 import os
 import sys
@@ -16,7 +15,7 @@ from net.jgp.labs.sparkdq4ml_amd.models.optim import wls_owlqn_device  # noqa: E
 from net.jgp.labs.sparkdq4ml_amd.ops import device, native  # noqa: E402
 
 CASES = os.environ.get("CASES", "1:1.0,32:0.05,64:0.02,127:0.01,256:0.01,1024:0.01,4096:0.01").split(",")
-ENGINE = os.environ.get("DQ4ML_QN_ENGINE", "hip")
+ENGINE = "hip"
 for case in CASES:
     d, reg = case.split(":")
     d, reg = int(d), float(reg)

@@ -1,5 +1,5 @@
 """Device OWLQN (L1 WLS): the one-wave HIP solver (``wls_qn_kernel``, k <= 128) and the
-device-resident torch OWLQN (larger k) against the native host driver; the lab's own L1 fit
+cooperative grid solver (``wls_qn_grid.hip``, larger k) against the native host driver; the lab's own L1 fit
 (regParam 1, elasticNetParam 1) asynchronous and on the device end to end."""
 import os
 import sys
@@ -24,7 +24,7 @@ def _host(flat, nf, icpt, reg, enet, stdf, max_iter=100):
                                                   (30, 0.05, 0.5, True, False), (12, 0.3, 0.8, False, True),
                                                   (63, 0.02, 1.0, True, True), (100, 0.01, 1.0, True, True)])
 def test_qn_kernel_matches_native(nf, reg, enet, icpt, stdf):
-    from test_owlqn_device import _flat
+    from _qn_flat import _flat
 
     from net.jgp.labs.sparkdq4ml_amd.models.optim import owlqn_result
     from net.jgp.labs.sparkdq4ml_amd.ops import device
@@ -113,24 +113,6 @@ def test_async_l1_fit_has_no_host_sync(gpu_session):
     ref = lr.fit(df)
     for m in ms:
         np.testing.assert_allclose(m.coefficients.toArray(), ref.coefficients.toArray(), rtol=1e-10, atol=1e-13)
-
-
-def test_wide_l1_fit_uses_device_owlqn(gpu_session):
-    """k > 128: the torch OWLQN on the device vs the native host driver on the same statistics."""
-    from net.jgp.labs.sparkdq4ml_amd.models.owlqn_device import solve_owlqn_device
-    from net.jgp.labs.sparkdq4ml_amd.ops import device
-
-    d, n = 300, 20_000
-    g = torch.Generator(device="cuda").manual_seed(2)
-    X = torch.randn(d, n, generator=g, device="cuda", dtype=torch.float64)
-    beta = torch.randn(d, generator=g, device="cuda", dtype=torch.float64) * (torch.rand(d, generator=g, device="cuda") > 0.5)
-    y = beta @ X + 1.0 + 0.1 * torch.randn(n, generator=g, device="cuda", dtype=torch.float64)
-    flat = device.gram_stats(X, y, None, None, "fp64")
-    coef, icpt, hist, reason = solve_owlqn_device(flat, d, True, 0.01, 1.0, True, True, 100, 1e-6)
-    r = _host(flat.cpu().numpy(), d, True, 0.01, 1.0, True)
-    np.testing.assert_allclose(coef, r["coefficients"], rtol=1e-6, atol=1e-8)
-    assert icpt == pytest.approx(r["intercept"], rel=1e-7, abs=1e-9)
-    assert hist[0] == r["objective_history"][0]
 
 
 def _wide_flat(d, n, seed):
