@@ -199,7 +199,7 @@ class DataFrame:
         return DataFrame(plan, self.sparkSession)
 
     def col(self, name: str) -> Column:
-        if name != "*" and name not in self.columns and name.lower() not in [c.lower() for c in self.columns]:
+        if name != "*" and self.schema.resolve_ci(name) is None:
             raise AnalysisException(f'Cannot resolve column name "{name}" among ({", ".join(self.columns)});')
         return Column(ColRef(name))
 

@@ -89,6 +89,11 @@ class _Parser:
 
     # ---- query -------------------------------------------------------------------------------
     def query(self, session):
+        return _bind_query(self.query_syntax(), self.text, session)
+
+    def query_syntax(self):
+        """The statement's syntax: (select items, view name, alias, WHERE, LIMIT) -- nothing of
+        the catalog is read here, so the result is cached per text (``plan_sql``)."""
         self.expect("kw", "select")
         self.accept("kw", "distinct")
         items = self.select_list()
@@ -106,25 +111,11 @@ class _Parser:
         if self.accept("kw", "limit"):
             limit = int(self.expect("num")[1])
         self.expect("eof")
-        plan = session.catalog._views.get(tname.lower())
-        if plan is None:
-            raise AnalysisException(f"Table or view not found: {tname}; line 1 pos {self.text.lower().find(tname.lower())}")
         quals = {tname.lower()} | ({alias.lower()} if alias else set())
         items = [(_strip_qual(e, quals)) for e in items]
         if where is not None:
-            plan = Filter(plan, _strip_qual(where, quals))
-        exprs = []
-        for e in items:
-            if isinstance(e, ColRef) and e.name == "*":
-                exprs += [ColRef(n) for n in plan.schema().names]
-            else:
-                exprs.append(e)
-        plan = Project(plan, exprs)
-        for e in exprs:
-            e.data_type(plan.child.schema())
-        if limit is not None:
-            plan = Limit(plan, limit)
-        return plan
+            where = _strip_qual(where, quals)
+        return items, tname, where, limit
 
     def select_list(self):
         items = [self.select_item()]
@@ -335,8 +326,45 @@ def parse_select_item(text: str) -> Expr:
     return e
 
 
+def _bind_query(syntax, text: str, session):
+    """The plan of a parsed SELECT over the session's CURRENT view of its FROM name (a temp view
+    replaced between two runs of the same text binds to the new plan).  Expression trees are
+    immutable once parsed, so plans may share them."""
+    items, tname, where, limit = syntax
+    plan = session.catalog._views.get(tname.lower())
+    if plan is None:
+        raise AnalysisException(f"Table or view not found: {tname}; line 1 pos {text.lower().find(tname.lower())}")
+    if where is not None:
+        plan = Filter(plan, where)
+    exprs = []
+    for e in items:
+        if isinstance(e, ColRef) and e.name == "*":
+            exprs += [ColRef(n) for n in plan.schema().names]
+        else:
+            exprs.append(e)
+    plan = Project(plan, exprs)
+    cs = plan.child.schema()
+    for e in exprs:
+        e.data_type(cs)
+    if limit is not None:
+        plan = Limit(plan, limit)
+    return plan
+
+
+_SYNTAX: dict = {}
+
+
 def plan_sql(text: str, session):
-    return _Parser(text).query(session)
+    """``spark.sql(text)``: Spark re-parses every statement; the app re-runs the same two
+    statements on every action (``DataQuality4MachineLearningApp.java:77-78, 89-90``), so the
+    syntax is parsed once per text and only bound to the current catalog per call."""
+    syn = _SYNTAX.get(text)
+    if syn is None:
+        syn = _Parser(text).query_syntax()
+        if len(_SYNTAX) >= 256:
+            _SYNTAX.clear()
+        _SYNTAX[text] = syn
+    return _bind_query(syn, text, session)
 
 
 _ = Optional

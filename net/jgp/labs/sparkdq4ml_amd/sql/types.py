@@ -149,7 +149,8 @@ class StructType:
 
     @property
     def names(self):
-        return list(self._idx()[1])
+        # (a copy: callers may mutate it; the index tuple keeps its own list)
+        return self._idx()[1][:]
 
     def fieldNames(self):
         return self.names
