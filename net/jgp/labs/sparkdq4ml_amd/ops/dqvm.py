@@ -48,6 +48,18 @@ _CTYPE = {IntegerType: "int", LongType: "long long", DoubleType: "double", Float
           DecimalType: "double", TimestampType: "long long", NullType: "double"}
 
 
+
+def rtc_handle(h, plan, src: str, entry: str, slot: int = 0) -> int:
+    """The hipRTC module handle of a cached plan's source, memoized ON the plan object: the native
+    cache (``dqvm.cpp``) keys by the whole source text, which costs a copy and a hash of tens of
+    KiB per action; a plan's source never changes, so the handle is looked up once per plan."""
+    hs = plan.__dict__.setdefault("_rtc", {})
+    k = (slot, entry)
+    v = hs.get(k)
+    if v is None:
+        v = hs[k] = int(h.rtc_compile(src, entry)[0])
+    return v
+
 def _ctype(t: DataType) -> str:
     c = _CTYPE.get(type(t))
     if c is None:
@@ -679,7 +691,7 @@ def try_execute_fused(plan, session) -> Optional[Table]:
     err = torch.zeros(1, dtype=torch.int32, device=base.device)
     ptr_list, outs, sel_out, keep = cp.bind(base, err)
     vec = all(q % (8 * VEC_ROWS) == 0 for q in ptr_list)  # whole allocations: the V-consecutive-rows form
-    handle, _log = h.rtc_compile(cp.src[1] if vec else cp.src[0], ENTRY)
+    handle = rtc_handle(h, cp, cp.src[1] if vec else cp.src[0], ENTRY, 1 if vec else 0)
     from .device import _h2d
 
     ptrs = _h2d(np.asarray(ptr_list, dtype=np.int64), base.device)  # no host-device sync

@@ -871,7 +871,9 @@ def try_cut_gram(chain, rel, d: int):
             ptrs.append(x.data_ptr() if torch.is_tensor(x) else int(x))
         else:
             raise AssertionError(f"cut plan: unbound slot {tag}")
-    handle, _log = h.rtc_compile(cp.src, ENTRY)
+    from .dqvm import rtc_handle
+
+    handle = rtc_handle(h, cp, cp.src, ENTRY)
     pt = _h2d(np.asarray(ptrs, dtype=np.int64), dev)
     stream = torch.cuda.current_stream(dev)
     with tracing.span("csv_cut_gram"):

@@ -708,7 +708,7 @@ def _launch(cp, nodes, rel, extra: dict, own_stream: bool = True):
         if cp.gram:
             extra["gpart"] = scalars["gpart"] = torch.zeros(nb, gram_width(cp.gram), dtype=torch.float64, device=dev)
         ptr_list, outs, sel_out = cp.bind(nalloc, dev, scalars, err)
-        handle, _log = h.rtc_compile(cp.src, ENTRY)
+        handle = dqvm.rtc_handle(h, cp, cp.src, ENTRY)
         ptrs = _h2d(np.asarray(ptr_list, dtype=np.int64), dev)
         from ..utils import tracing
 

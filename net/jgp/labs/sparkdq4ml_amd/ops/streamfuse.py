@@ -298,7 +298,9 @@ def try_fused_stream(plan, features_col: str, label_col: str, session, gram_dtyp
             _TABS.clear()
         ent = _TABS[tkey] = (tbl, rawtab, desc)
     _, rawtab, desc = ent
-    handle, _log = h.rtc_compile(cp.src, ENTRY)
+    from .dqvm import rtc_handle
+
+    handle = rtc_handle(h, cp, cp.src, ENTRY)
     P = int(h.gram_partial_stride(cp.mode, d))
     lds = max(4 * _wave_bytes(cp.NT, cp.RING), 8 * P)
     cus = _CUS.get(dev.index)
