@@ -53,7 +53,84 @@ def shard_byte_range(data: bytes, rank: int, world: int) -> Tuple[int, int]:
     return align(n * rank // world), align(n * (rank + 1) // world)
 
 
-def _ncols_of(data, sep: str, comment: int = 0) -> int:
+def _count_fields(line: bytes, sep: int, quote: int, escape: int) -> int:
+    """Fields of one record under the univocity tokenizer's quoting (``csrc/host/csv.cpp``
+    ``split_record``): a separator inside a quoted field is content."""
+    if quote not in line:
+        return line.count(sep) + 1
+    n, i, fields = len(line), 0, 1
+    in_q = quoted = False
+    empty = True  # nothing collected in the current field yet
+    while i < n:
+        c = line[i]
+        if in_q:
+            if c == escape and escape != quote and i + 1 < n and line[i + 1] in (quote, escape):
+                i += 1
+            elif c == quote:
+                if i + 1 < n and line[i + 1] == quote:
+                    i += 1
+                else:
+                    in_q = False
+            empty = False
+        elif c == sep:
+            fields += 1
+            quoted, empty = False, True
+        elif c == quote and empty and not quoted:
+            in_q = quoted = True
+        else:
+            if c == escape and escape != quote and i + 1 < n and line[i + 1] == quote:
+                i += 1
+            empty = False
+        i += 1
+    return fields
+
+
+def split_record(line: bytes, sep: int, quote: int, escape: int, null_value: bytes = b"",
+                 trim_lead: bool = False, trim_trail: bool = False):
+    """[(text bytes, is_null)] of one record, the univocity way (``csrc/host/csv.cpp``
+    ``split_record``, which the device parser mirrors): quotes, doubled quotes, the escape before a
+    quote, a separator inside quotes kept as content; a quoted field is never null; trims after."""
+    out, cur = [], bytearray()
+    in_q = quoted = False
+    i, n = 0, len(line)
+    while i < n:
+        c = line[i]
+        if in_q:
+            if c == escape and escape != quote and i + 1 < n and line[i + 1] in (quote, escape):
+                i += 1
+                cur.append(line[i])
+            elif c == quote:
+                if i + 1 < n and line[i + 1] == quote:
+                    cur.append(quote)
+                    i += 1
+                else:
+                    in_q = False
+            else:
+                cur.append(c)
+        elif c == sep:
+            out.append((bytes(cur), not quoted and bytes(cur) == null_value))
+            cur, quoted = bytearray(), False
+        elif c == quote and not cur and not quoted:
+            in_q = quoted = True
+        elif c == escape and escape != quote and i + 1 < n and line[i + 1] == quote:
+            i += 1
+            cur.append(line[i])
+        else:
+            cur.append(c)
+        i += 1
+    out.append((bytes(cur), not quoted and bytes(cur) == null_value))
+    res = []
+    for t, null in out:
+        if not null:
+            if trim_lead:
+                t = t.lstrip(b" \t")
+            if trim_trail:
+                t = t.rstrip(b" \t")
+        res.append((t, null))
+    return res
+
+
+def _ncols_of(data, sep: str, comment: int = 0, quote: int = 34, escape: int = 92) -> int:
     """Column count from the first line that is neither empty nor a comment line -- Spark drops
     those before it tokenizes the first record (a bounded, growing head search: the input may be
     a multi-GB map with no ``\n`` at all -- the reference data is CR-only)."""
@@ -67,7 +144,7 @@ def _ncols_of(data, sep: str, comment: int = 0) -> int:
                 break  # the line may go on past the head: read more
             e = min(ends) if ends else len(head)
             if e > pos and not (comment and head[pos] == comment):
-                return head.count(sep.encode(), pos, e) + 1
+                return _count_fields(head[pos:e], ord(sep), quote, escape)
             if not ends:  # the whole input holds no such line
                 return 1
             pos = e + 1
@@ -226,7 +303,8 @@ def infer_streamed(src, sep: str, ncols: Optional[int] = None, sharded: bool = F
     h = native.hip()
     if ncols is None:
         head = bytes(memoryview(src.data)[:min(src.n, 1 << 20)])
-        ncols = _ncols_of(head, sep, int(_opt_args(opts)["comment"] or 0))
+        oa = _opt_args(opts)
+        ncols = _ncols_of(head, sep, int(oa["comment"] or 0), oa["quote"], oa["escape"])
     if ncols > 256 or not len(src):
         return None
     hint = list(user_types) if user_types else None
@@ -299,7 +377,8 @@ def scan_device(data, sep: str = ",", infer: bool = True, device=None, ncols: Op
     h = native.hip()
     dev = torch.device(device)
     if ncols is None:
-        ncols = _ncols_of(data, sep, int(_opt_args(opts)["comment"] or 0))
+        oa = _opt_args(opts)
+        ncols = _ncols_of(data, sep, int(oa["comment"] or 0), oa["quote"], oa["escape"])
     if ncols > 256:
         return None
     hint = list(types_hint) if types_hint is not None and len(types_hint) == ncols else None

@@ -70,9 +70,9 @@ def _device_csv_opts(o) -> Optional[dict]:
 
 def _split_header(data, sep: str, opts: dict):
     """(column names, byte offset of the first data line) of the header record — the first
-    non-empty, non-comment line, split the host scanner's way — or None when it needs the general
-    tokenizer (quotes / escapes in it) or the file has no data line.  A bounded head search: the
-    input may be a multi-GB map."""
+    non-empty, non-comment line, split the host scanner's way (quotes included,
+    ``ops.csvscan.split_record``) — or None when the file has no data line.  A bounded head
+    search: the input may be a multi-GB map."""
     n = len(data)
     pos, w = 0, 1 << 16
     comment = opts["comment"]
@@ -88,20 +88,13 @@ def _split_header(data, sep: str, opts: dict):
         if cut and head[e:e + 2] == b"\r\n":
             nxt += 1
         if line and not (comment and line[0] == comment):
-            text = line.decode("utf-8", "replace")
-            if opts["quote"] in text or opts["escape"] in text or nxt >= n:
+            if nxt >= n:
                 return None
-            names = []
-            for i, f in enumerate(text.split(sep)):
-                if f == opts["null_value"]:
-                    names.append(f"_c{i}")
-                    continue
-                if opts["trim_lead"]:
-                    f = f.lstrip(" \t")
-                if opts["trim_trail"]:
-                    f = f.rstrip(" \t")
-                names.append(f)
-            return names, nxt
+            from ..ops.csvscan import split_record
+
+            fields = split_record(line, ord(sep), ord(opts["quote"]), ord(opts["escape"]),
+                                  opts["null_value"].encode(), opts["trim_lead"], opts["trim_trail"])
+            return [f"_c{i}" if null else t.decode("utf-8", "replace") for i, (t, null) in enumerate(fields)], nxt
         pos = nxt
     return None
 

@@ -453,3 +453,85 @@ def test_device_column_count_skips_empty_and_comment_lines():
     assert _ncols_of(b"", ",") == 1 and _ncols_of(b"\n\n", ",") == 1
     big = b"\n" * 5 + b"x" * (1 << 17) + b",y\n"  # the first real line runs past the first head window
     assert _ncols_of(big, ",") == 2
+
+
+def _quoted(data: bytes, frac: float, seed: int, sep_inside: bool = False) -> bytes:
+    """``data`` with a fraction of its fields wrapped in quotes (CR / LF terminators kept)."""
+    rng = np.random.default_rng(seed)
+    out = []
+    for line in data.replace(b"\r\n", b"\n").replace(b"\r", b"\n").split(b"\n"):
+        fs = line.split(b",")
+        fs = [b'"' + f + b'"' if f and rng.random() < frac else f for f in fs]
+        out.append(b",".join(fs))
+    return b"\r".join(out)
+
+
+def test_split_record_matches_host_tokenizer():
+    """``ops.csvscan.split_record`` (the host-side header splitter, mirror of the device parser's
+    quoting) against the native univocity-style tokenizer on quoted / escaped records."""
+    from net.jgp.labs.sparkdq4ml_amd.ops.csvscan import _count_fields, split_record
+
+    lines = [b'1,"2.5",3', b'"a,b",c', b'"x""y",z', b'"p\\"q",1', b'a\\"b,2', b'"",7', b'"1",,""', b'"u"v,w']
+    for line in lines:
+        n, cols = _host(line + b"\n" + line, infer=True)
+        fields = split_record(line, ord(","), 34, 92)
+        assert len(fields) == len(cols) == _count_fields(line, ord(","), 34, 92), line
+        h = native.host()
+        for (t, null), c in zip(fields, cols):
+            cls = 0 if null else h.csv_infer_field(t.decode())
+            if cls != 0:  # (an all-null column's type is the host's default)
+                assert c[1] == cls, (line, t, c[1], cls)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,frac", [("dataset-full.csv", 1.0), ("dataset-full.csv", 0.4),
+                                       ("dataset-abstract.csv", 0.5), ("fuzz_numeric", 0.5)])
+def test_device_scan_of_quoted_fields_matches_host(name, frac):
+    """quoted numeric fields parse on the device (no host fallback) and equal the
+    host scanner's values and types."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from net.jgp.labs.sparkdq4ml_amd.ops import csvscan
+
+    data = CASES[name] if name in CASES else open(data_path(name), "rb").read()
+    q = _quoted(data, frac, 3)
+    before = csvscan.STATS["fallbacks"]
+    t = csvscan.scan_device(q, device="cuda")
+    assert t is not None and csvscan.STATS["fallbacks"] == before, "quoted numeric fields fell back to the host"
+    n, cols = _host(q)
+    assert t.nrows == n
+    for (name_, code, vals, valid), c in zip(cols, t.columns):
+        assert list(c.valid_mask().cpu().numpy().astype(int)) == list(valid.astype(int))
+        got, ref = c.values.cpu().numpy().astype(np.float64), np.asarray(vals).astype(np.float64)
+        np.testing.assert_array_equal(np.where(valid.astype(bool), got, 0), np.where(valid.astype(bool), ref, 0))
+
+
+@pytest.mark.gpu
+def test_device_reader_quoted_header_and_large_quoted_file(tmp_path):
+    """A quoted header and a 1e6-row quoted numeric file through the reader: device scan taken,
+    no fallback, same rows as the host scanner."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from net.jgp.labs.sparkdq4ml_amd import SparkSession
+    from net.jgp.labs.sparkdq4ml_amd.ops import csvscan
+
+    rng = np.random.default_rng(5)
+    n = 1_000_000
+    g = rng.integers(1, 36, n)
+    pr = np.round(5.0 * g + 20 + rng.normal(0, 3, n), 2)
+    body = "\r".join(f'"{a}","{b:.2f}"' for a, b in zip(g.tolist(), pr.tolist()))
+    p = tmp_path / "q.csv"
+    p.write_bytes(('"guest","price"\r' + body).encode())
+    s = SparkSession.getActiveSession()
+    if s is not None:
+        s.stop()
+    spark = SparkSession.builder().master("mi355x[*]").config("dq4ml.csv.deviceThresholdBytes", "0").getOrCreate()
+    b0, f0 = csvscan.STATS["device_scans"], csvscan.STATS["fallbacks"]
+    df = spark.read().option("header", "true").option("inferSchema", "true").csv(str(p))
+    assert df.columns == ["guest", "price"]
+    assert [t for _, t in df.dtypes] == ["int", "double"]
+    assert csvscan.STATS["device_scans"] == b0 + 1 and csvscan.STATS["fallbacks"] == f0
+    assert df.count() == n
+    got = np.asarray([r[1] for r in df.limit(1000).collect()])
+    np.testing.assert_allclose(got, pr[:1000], rtol=0, atol=1e-9)
+    spark.stop()
