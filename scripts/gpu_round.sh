@@ -126,6 +126,8 @@ for s in $STEPS; do
        step f32pmc2 300 timeout -s KILL 240 rocprofv3 --kernel-trace --pmc SQ_WAIT_INST_LDS SQ_INSTS_MFMA SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_MISC GRBM_GUI_ACTIVE -d gpurun_out/f32pmc2 -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --dtype fp32) || exit $? ;;
     reserveab) for r in 0 1 8 0 1 8; do step res$r 300 env DQ4ML_GRAM_RESERVE=$r python bench.py --steps 50 --warmup 5 --rows 1.25e7 --async; done
        for r in 0 1 8; do step resbig$r 300 env DQ4ML_GRAM_RESERVE=$r python bench.py --steps 20 --warmup 3; done ;;
+    shapeprobe) step shapeprobe 180 ./scripts/mfma_shape_probe 20000 &&
+       (export TMPDIR=/tmp; step shapepmc 120 timeout -s KILL 100 rocprofv3 --kernel-trace --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_BUSY_CYCLES -d gpurun_out/shapepmc -o run --output-format csv -- ./scripts/mfma_shape_probe 5000) || exit $? ;;
     mfmapeak) step mfmapeak 120 ./scripts/mfma_peak &&
        (export TMPDIR=/tmp; step mfmapeakpmc 120 timeout -s KILL 100 rocprofv3 --kernel-trace --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_BUSY_CYCLES -d gpurun_out/mfmapeakpmc -o run --output-format csv -- ./scripts/mfma_peak) || exit $? ;;
     syrkpmc) (export TMPDIR=/tmp CASES="256:20000000:f64:fp64" REPS=2

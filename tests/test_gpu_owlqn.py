@@ -186,3 +186,31 @@ def test_wide_async_l1_fit_has_no_host_sync(gpu_session):
     gpu_session.conf.set("dq4ml.fit.async", "false")
     ref = lr.fit(df)
     np.testing.assert_allclose(m.coefficients.toArray(), ref.coefficients.toArray(), rtol=1e-10, atol=1e-13)
+
+
+def test_qn_grid_kernel_history_reset_terminates():
+    """statistics whose standardized system is indefinite (correlations scaled past 1)
+    make s.y < 0 -> the grid solver's history reset path (no line search, no grid barrier between
+    block 0's write of the direction scalars and the other blocks' reads; double-buffered since).
+    The solve must terminate, deterministically, on a k > 128 grid."""
+    from net.jgp.labs.sparkdq4ml_amd.ops import device
+
+    d = 200
+    flat = _wide_flat(d, 20_000, 11).cpu().numpy().copy()
+    W = flat[1]
+    mean = flat[5:5 + d] / W
+    i, j = np.triu_indices(d)
+    order = np.argsort(i + j * (j + 1) // 2)
+    ii, jj = i[order], j[order]
+    aa = flat[5 + 2 * d:] / W
+    cov = aa - mean[ii] * mean[jj]
+    cov = np.where(ii == jj, cov, 3.0 * cov)  # |correlation| up to 3: indefinite
+    flat[5 + 2 * d:] = (cov + mean[ii] * mean[jj]) * W
+    t = torch.tensor(flat, device="cuda")
+    outs = [device.wls_qn_small(t, d, True, 0.01, 1.0, True, True, 60, 1e-6) for _ in range(3)]
+    torch.cuda.synchronize()
+    used = d + 9 + int(outs[0][d + 7])
+    for o in outs[1:]:
+        assert torch.equal(o[:used], outs[0][:used])  # same decisions on every run
+    H = int(outs[0][d + 7])
+    assert 1 <= H <= 2 * 60 + 8
