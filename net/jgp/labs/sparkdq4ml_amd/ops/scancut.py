@@ -141,7 +141,7 @@ class _Shape:
         # waves split into G tile groups x (4 / G) row groups, <= 32 accumulator VGPRs per wave
         self.NT16 = (d + 2 + 15) // 16
         self.tiles = [(I, J) for I in range(self.NT16) for J in range(I, self.NT16)]
-        self.mfma = self.blocked and d + 2 <= 80 and os.environ.get("DQ4ML_CUT_MFMA", "1") != "0"
+        self.mfma = self.blocked and d + 2 <= 80
         if self.mfma:
             self.G = next((g for g in (1, 2, 4) if -(-len(self.tiles) // g) * 8 <= 32), 4)
             self.RG = 4 // self.G
@@ -154,9 +154,7 @@ class _Shape:
             8 * (3 * self.PP + 16) if self.blocked else 32 * self.gw)
         # the row tiles take what keeps TARGET_PER_CU blocks resident per CU (40 KiB each at 4),
         # within [4 KiB, TILE_BYTES]: more rounds per window beat fewer resident blocks
-        per_cu = int(os.environ.get("DQ4ML_CUT_PER_CU", TARGET_PER_CU))
-        cap = int(os.environ.get("DQ4ML_CUT_TILE", TILE_BYTES))
-        tile = max(4096, min(cap, (160 * 1024) // per_cu - fixed))
+        tile = max(4096, min(TILE_BYTES, (160 * 1024) // TARGET_PER_CU - fixed))
         self.RR = int(max(1, min(rows_max, tile // per_row)))
         self.lds = fixed + 8 * self.RR * self.CU + (8 * ((self.RR + 3) * self.PP + 16) if self.blocked else 0)
         self.gw = gram_width(d)
@@ -378,9 +376,9 @@ def kernel_source(g, kinds, used, opts: dict, H: int, slots: dict, d: int, term:
     ints = [c for c, k in enumerate(kinds) if int(k) == 1]
     int_ok = "(" + " || ".join(f"c == {c}" for c in ints) + ") ? !dot : true" if 0 < len(ints) <= 8 else (
         "true" if not ints else "csv_conforms(dot ? C_DOUBLE : C_INT, DQ_KIND[c])")
-    div_expr = ("csv_div_pow10_fma((double)m, csv_pow10(fr), csv_inv_pow10(fr))"
-                if os.environ.get("DQ4ML_CUT_P10", "lds") == "valu" else
-                "csv_div_pow10_fma((double)m, p10t[fr & 15], ip10t[fr & 15])")
+    # the quotient's power-of-ten pair from an LDS table (the VALU select chain measured slower:
+    # profiles/r3_csv_cutter.md)
+    div_expr = "csv_div_pow10_fma((double)m, p10t[fr & 15], ip10t[fr & 15])"
     if abl & 16:  # (diagnostic) no table read: the quotient's LDS round trip
         div_expr = "csv_div_pow10_fma((double)m, 1.0 + fr, 1.0)"
     frame_load = ("const unsigned fw0 = fwp[0], fw1 = fwp[1], fw2 = fwp[2];\n        const int c0 = stage[start];"
@@ -390,11 +388,10 @@ def kernel_source(g, kinds, used, opts: dict, H: int, slots: dict, d: int, term:
     # the next window's prefetch: right after this window's bytes are staged ("early"), or after
     # the field conversion of its first tile round ("late": the 20 prefetch VGPRs are not live
     # across the converter, and the loads still have the row, Gram and stage phases to land)
-    late = os.environ.get("DQ4ML_CUT_PF", "late") == "late"
-    pf_early = "" if late else "    if (blk + 1 < w1) dq_fetch(ab, a, n, blk + 1, tid, pg, ph);\n"
-    pf_late = "      if (R0 == 0 && blk + 1 < w1) dq_fetch(ab, a, n, blk + 1, tid, pg, ph);\n" if late else ""
+    pf_early = ""
+    pf_late = "      if (R0 == 0 && blk + 1 < w1) dq_fetch(ab, a, n, blk + 1, tid, pg, ph);\n"
     pf_tail = ("    if ((cnt == 0 || " + ("true" if abl & 8 else "false") + ") && blk + 1 < w1) "
-               "dq_fetch(ab, a, n, blk + 1, tid, pg, ph);  // no tile round ran\n") if late else ""
+               "dq_fetch(ab, a, n, blk + 1, tid, pg, ph);  // no tile round ran\n")
     conv_call = ("ok = true; m = (unsigned)len;" if abl & 1 else
                  f"""if (__ballot(fl > 8) == 0ull) {{
           ok = csv_num_r8s_w(fw0, fw1, fw2, fsh, fl, m, fr, dot);
@@ -409,7 +406,7 @@ def kernel_source(g, kinds, used, opts: dict, H: int, slots: dict, d: int, term:
     # carried row starts (every window but a run's first) count the head's separators in phase 0
     # from the head granule registers — one barrier and phase less per window — when the head's
     # granules all sit in wave 0 (H <= 1024)
-    hf = H <= 1024 and os.environ.get("DQ4ML_CUT_HFAST", "1") != "0"
+    hf = H <= 1024
     if hf:
         hraw_code = f"""    unsigned int hraw16 = 0u;  // separators of this lane's head granule (wave 0, lanes < {H // 16})
     if (tid < {H // 16}) {{
@@ -494,13 +491,12 @@ def kernel_source(g, kinds, used, opts: dict, H: int, slots: dict, d: int, term:
             fs_expr = "ctab[2 * c + 1]"
         feat_store = (f"        const int fs = {fs_expr};\n"
                       f"        if (fs >= 0) gt[rr * {PP} + fs] = dv;\n")
-    NF = int(os.environ.get("DQ4ML_CUT_NF", "1"))
+    NF = 1  # fields per lane per conversion iteration
     # no barrier at the window top: phase 0 writes only the stage, the cut and the scan words,
     # which the previous window finished reading before its row-phase barrier, so the previous
     # window's Gram (reading the row tile, written again only after this window's cut barrier)
     # overlaps this window's staging
-    top_sync = ("    __syncthreads();  // the previous window's readers are done with every LDS array\n"
-                if os.environ.get("DQ4ML_CUT_TOPSYNC", "0") == "1" else "")
+    top_sync = ""
     conv_loop = _conv_loop(NF, C, CU, PP, FW, crlf, conv_call, frame_load, div_expr, int_ok, us_expr, feat_store)
     kind_tab = ", ".join(str(int(k)) for k in kinds)
     lb = f"__launch_bounds__(256, {waves_per_simd})" if waves_per_simd else "__launch_bounds__(256)"
@@ -788,12 +784,12 @@ def _compile(nodes, rel, d: int):
     term, crlf = term_of(f)
     min_line = int(f.get("min_line", 1))
     (parts, udfs), refs = dqvm.nodes_key(nodes)
+    # (diagnostic builds only: DQ4ML_CUT_ABLATE timing ablations, DQ4ML_CUT_STAMPS phase clocks;
+    # the losing A/B alternatives of rounds 2-3 -- VALU powers of ten, early prefetch, slow head
+    # scan, 2 fields per lane, top-of-window barrier, other tile sizes -- were removed in round 4)
     key = (parts, udfs, tuple(rel.schema().names), tuple(f["kinds"]), repr(sorted(f["opts"].items())), H, d, term,
-           crlf, min_line, int(f.get("max_line", 1 << 30)), os.environ.get("DQ4ML_CUT_PER_CU"),
-           os.environ.get("DQ4ML_CUT_TILE"), os.environ.get("DQ4ML_CUT_ABLATE"),
-           os.environ.get("DQ4ML_CUT_STAMPS"), os.environ.get("DQ4ML_CUT_P10"), os.environ.get("DQ4ML_CUT_HFAST"),
-           os.environ.get("DQ4ML_CUT_PF"), os.environ.get("DQ4ML_CUT_NF"),
-           os.environ.get("DQ4ML_CUT_TOPSYNC"))
+           crlf, min_line, int(f.get("max_line", 1 << 30)), os.environ.get("DQ4ML_CUT_ABLATE"),
+           os.environ.get("DQ4ML_CUT_STAMPS"))
     if key in _CACHE:
         return _CACHE[key]
     base = _ScanBase(rel.schema(), 0, f["device"])

@@ -126,6 +126,9 @@ for s in $STEPS; do
        step f32pmc2 300 timeout -s KILL 240 rocprofv3 --kernel-trace --pmc SQ_WAIT_INST_LDS SQ_INSTS_MFMA SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_MISC GRBM_GUI_ACTIVE -d gpurun_out/f32pmc2 -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --dtype fp32) || exit $? ;;
     reserveab) for r in 0 1 8 0 1 8; do step res$r 300 env DQ4ML_GRAM_RESERVE=$r python bench.py --steps 50 --warmup 5 --rows 1.25e7 --async; done
        for r in 0 1 8; do step resbig$r 300 env DQ4ML_GRAM_RESERVE=$r python bench.py --steps 20 --warmup 3; done ;;
+    csvhost) step csvhost 600 env DQ4ML_BENCH_CPROFILE=gpurun_out/csv.prof python benchmarks/bench_csv_pipeline.py --rows ${CSV_ROWS:-1e7} --steps 50 --warmup 5 --json-out gpurun_out/csvhost.json &&
+       python -c "import pstats; pstats.Stats('gpurun_out/csv.prof').sort_stats('tottime').print_stats(45)" > gpurun_out/csvprof_tot.txt &&
+       python -c "import pstats; pstats.Stats('gpurun_out/csv.prof').sort_stats('cumulative').print_stats(60)" > gpurun_out/csvprof_cum.txt ;;
     shapeprobe) step shapeprobe 180 ./scripts/mfma_shape_probe 20000 &&
        (export TMPDIR=/tmp; step shapepmc 120 timeout -s KILL 100 rocprofv3 --kernel-trace --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_BUSY_CYCLES -d gpurun_out/shapepmc -o run --output-format csv -- ./scripts/mfma_shape_probe 5000) || exit $? ;;
     mfmapeak) step mfmapeak 120 ./scripts/mfma_peak &&
@@ -177,10 +180,6 @@ for s in $STEPS; do
     cutpmc) (export TMPDIR=/tmp
        step cutpmc1 300 timeout -s KILL 240 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS GRBM_GUI_ACTIVE -d gpurun_out/cutpmc1 -o run --output-format csv -- python benchmarks/bench_csv_pipeline.py --features 32 --rows 2e7 --steps 2 --warmup 1 &&
        step cutpmc2 300 timeout -s KILL 240 rocprofv3 --kernel-trace --pmc SQ_INSTS_SALU SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_VMEM SQ_ACTIVE_INST_MISC GRBM_GUI_ACTIVE -d gpurun_out/cutpmc2 -o run --output-format csv -- python benchmarks/bench_csv_pipeline.py --features 32 --rows 2e7 --steps 2 --warmup 1) || exit $? ;;
-    cutsweep) for pc in 3 4; do for tl in 18432 36864; do
-         step cutsweep_lab_${pc}_${tl} 300 env DQ4ML_CUT_PER_CU=$pc DQ4ML_CUT_TILE=$tl python benchmarks/bench_csv_pipeline.py --steps 10 --warmup 2 &&
-         step cutsweep_w32_${pc}_${tl} 300 env DQ4ML_CUT_PER_CU=$pc DQ4ML_CUT_TILE=$tl python benchmarks/bench_csv_pipeline.py --features 32 --rows 2e7 --steps 10 --warmup 2 || exit $?
-       done; done ;;
     cutpmclab) (export TMPDIR=/tmp
        step cutpmclab1 300 timeout -s KILL 240 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS GRBM_GUI_ACTIVE -d gpurun_out/cutpmclab1 -o run --output-format csv -- python benchmarks/bench_csv_pipeline.py --steps 2 --warmup 1 &&
        step cutpmclab2 300 timeout -s KILL 240 rocprofv3 --kernel-trace --pmc SQ_INSTS_SALU SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_VMEM SQ_ACTIVE_INST_MISC GRBM_GUI_ACTIVE -d gpurun_out/cutpmclab2 -o run --output-format csv -- python benchmarks/bench_csv_pipeline.py --steps 2 --warmup 1) || exit $? ;;
@@ -188,15 +187,9 @@ for s in $STEPS; do
          step cutabl_lab_$ab 300 env DQ4ML_CUT_ABLATE=$ab python benchmarks/bench_csv_pipeline.py --steps 10 --warmup 2 &&
          step cutabl_w32_$ab 300 env DQ4ML_CUT_ABLATE=$ab python benchmarks/bench_csv_pipeline.py --features 32 --rows 2e7 --steps 10 --warmup 2 || exit $?
        done ;;
-    cutnf) for nf in 1 2; do for pc in 3 4; do
-         step cutnf_lab_${nf}_${pc} 300 env DQ4ML_CUT_NF=$nf DQ4ML_CUT_PER_CU=$pc python benchmarks/bench_csv_pipeline.py --steps 10 --warmup 2 &&
-         step cutnf_w32_${nf}_${pc} 300 env DQ4ML_CUT_NF=$nf DQ4ML_CUT_PER_CU=$pc python benchmarks/bench_csv_pipeline.py --features 32 --rows 2e7 --steps 10 --warmup 2 || exit $?
-       done; done ;;
     cutb) (export TMPDIR=/tmp
        step cutb_lab 300 env VARIANTS="${LABV:-base;DQ4ML_SCAN_CUT=0;DQ4ML_CUT_ABLATE=1;DQ4ML_CUT_ABLATE=4;DQ4ML_CUT_ABLATE=5}" python scripts/cut_bench.py --rows 1e8 &&
        step cutb_w32 300 env VARIANTS="${W32V:-base;DQ4ML_CUT_ABLATE=1;DQ4ML_CUT_ABLATE=2;DQ4ML_CUT_ABLATE=4;DQ4ML_CUT_ABLATE=7}" python scripts/cut_bench.py --features 32 --rows 2e7) || exit $? ;;
-    cutb64) (export TMPDIR=/tmp
-       step cutb_w64 300 env VARIANTS="${W64V:-base;DQ4ML_CUT_MFMA=0}" python scripts/cut_bench.py --features 64 --rows 1e7) || exit $? ;;
     cutpmcb) (export TMPDIR=/tmp VARIANTS=base
        step cutpmcb1 300 timeout -s KILL 240 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS GRBM_GUI_ACTIVE -d gpurun_out/cutpmcb1 -o run --output-format csv -- python scripts/cut_bench.py --features 32 --rows 2e7 --reps 3 &&
        step cutpmcb2 300 timeout -s KILL 240 rocprofv3 --kernel-trace --pmc SQ_INSTS_SALU SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_VMEM SQ_ACTIVE_INST_MISC GRBM_GUI_ACTIVE -d gpurun_out/cutpmcb2 -o run --output-format csv -- python scripts/cut_bench.py --features 32 --rows 2e7 --reps 3 &&
