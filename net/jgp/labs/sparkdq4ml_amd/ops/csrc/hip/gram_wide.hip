@@ -10,8 +10,9 @@
 //    HBM/L2 -> LDS with global_load_lds (16 B per lane, lane-linear, so every later ds_read_b128 is
 //    conflict-free with no swizzle) through a 4-deep ring (128 KiB LDS, 1 block per CU) with COUNTED
 //    vmcnt: three stages stay in flight across the one barrier per stage;
-//  * 4 waves (2 x 2) per 256x256 block, 128 x 128 per wave = 4 x 4 accumulators (256 AGPRs at 1
-//    wave/SIMD): 8 fragment reads feed 16 MFMAs, halving LDS read traffic per MFMA vs 128 x 64;
+//  * 8 waves (2 x 4) per 256x256 block, 128 x 64 per wave = 4 x 2 accumulators (2 waves/SIMD: one
+//    wave's LDS reads hide under the other's MFMAs; the 4-wave 128 x 128 tiling halved the LDS
+//    reads per MFMA but ran 86 vs 75 ms at 1 wave/SIMD, profiles/r3_wide_gang.md);
 //  * the label and the intercept column ride along as an "augmentation" panel [1, y_hi, y_lo]
 //    (a 32-feature tile of its own; the other 7 tiles stream from a zero page so every wave issues
 //    the same number of loads), so count, Σy, Σy², Σx, Σxy fall out of the same SYRK — the
@@ -37,6 +38,7 @@ constexpr int kChunk = 2048;          // bytes of one (tile, stage) image
 constexpr int kPanelStage = kTilesPerPanel * kChunk;  // 16 KiB
 constexpr int kStageBytes = 2 * kPanelStage;          // A + B images
 constexpr int kMaxRing = 5;                           // LDS stages (5 x 32 KiB = all 160 KiB)
+constexpr int kWaves = 8;                             // waves per block (2 per SIMD)
 
 typedef __attribute__((ext_vector_type(2))) unsigned int u32x2;
 typedef __attribute__((ext_vector_type(8))) int i32x8;
@@ -95,11 +97,10 @@ __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-template <typename F, int WN>
+template <typename F>
 struct StageFrags {
-  F a[2][4];   // [k-step][A tile]
-  F b[2][WN];  // [k-step][B tile]
-  F c[2];      // [k-step] the augmentation tile of a 4-wave MODE 5 wave (unused elsewhere)
+  F a[2][4];  // [k-step][A tile]
+  F b[2][2];  // [k-step][B tile]
 };
 
 // One (pair, split) block's K loop + epilogue.  MODE 0: off-diagonal panel pair; 3: diagonal pair
@@ -121,15 +122,15 @@ __device__ __forceinline__ void keep_live(const V& v) {
   for (int e = 0; e < (int)(sizeof(V) / 4); ++e) asm volatile("" ::"v"(reinterpret_cast<const unsigned*>(&v)[e]));
 }
 
-// ABL: 0 = real kernel, 3 = real kernel with s_setprio(1) around the MFMA clusters (A/B);
-// diagnostic builds only: 1 = no MFMA (loads + LDS reads), 2 = no glds
-template <int EB, int MODE, int RING, int WAVES, int ABL = 0>
+// ABL: 0 = real kernel; diagnostic builds only (timing, wrong results): 1 = no MFMA (loads + LDS
+// reads), 2 = no glds
+template <int EB, int MODE, int RING, int ABL = 0>
 __device__ __forceinline__ void syrk_block(const WideArgs& a, unsigned char* smem, int I, int J, int pair, int split) {
   typedef WideTraits<EB> Tr;
   typedef typename Tr::frag F;
-  // WAVES 4: 2 x 2 waves of 128 x 128 (1 wave/SIMD); 8: 2 x 4 waves of 128 x 64 (2 waves/SIMD)
-  constexpr int kWBlock = 64 * WAVES;
-  constexpr int WN = WAVES == 4 ? 4 : 2;              // 32-col tiles per wave
+  // 2 x 4 waves of 128 x 64 (2 waves/SIMD)
+  constexpr int kWBlock = 64 * kWaves;
+  constexpr int WN = 2;  // 32-col tiles per wave
   constexpr int kLoadsPerPanel = kPanelStage / (kWBlock * 16);
   // loads per thread per stage: an augmentation side needs only piece 0 (tile 0 = [1, y_hi, y_lo]
   // for threads < 128, the zero page into tile 1 for the rest — waves whose tiles are all zero
@@ -138,13 +139,10 @@ __device__ __forceinline__ void syrk_block(const WideArgs& a, unsigned char* sme
   constexpr int LB = MODE == 3 ? 0 : (MODE >= 1 ? 1 : kLoadsPerPanel);
   constexpr bool kDiagPanel = MODE == 3 || MODE == 4;  // B operand = the A panel
   constexpr bool kFullWave = MODE == 0 || kDiagPanel;
-  // 4-wave gang: ONE augmentation wave (wm = 1, wn = 0) covers all 256 rows of panel I:
-  // A tiles 0-3 in a[], 4-7 in b[], the augmentation tile in c[]
-  constexpr bool kAug4 = MODE == 5 && WAVES == 4;
   constexpr int kLoadsPerStage = LA + LB;
-  typedef StageFrags<F, WN> SF;
+  typedef StageFrags<F> SF;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = WAVES == 4 ? wave >> 1 : wave >> 2, wn = WAVES == 4 ? wave & 1 : wave & 3;
+  const int wm = wave >> 2, wn = wave & 3;
   const int64_t nst = a.nsup * Tr::kStagesPerSup;
   const int64_t st0 = nst * split / a.splitk, st1 = nst * (split + 1) / a.splitk;
   const int64_t cnt = st1 - st0;
@@ -191,18 +189,6 @@ __device__ __forceinline__ void syrk_block(const WideArgs& a, unsigned char* sme
     const unsigned char* B = kDiagPanel ? A : A + kPanelStage;
     const int ta = MODE == 2 ? (wm == 0 ? 0 : 1) : (MODE == 5 ? wn * 4 : wm * 4);  // first A tile
     const int tb = (MODE == 1 || MODE == 2) ? (wn == 0 ? 0 : 1) : (MODE == 5 ? 0 : wn * WN);  // first B tile
-    if constexpr (kAug4) {
-#pragma unroll
-      for (int kk = 0; kk < Tr::kSteps; ++kk) {
-#pragma unroll
-        for (int x = 0; x < 4; ++x) {
-          f.a[kk][x] = Tr::read(A + x * kChunk, kk, lane);
-          f.b[kk][x] = Tr::read(A + (4 + x) * kChunk, kk, lane);
-        }
-        f.c[kk] = Tr::read(B, kk, lane);
-      }
-      return;
-    }
 #pragma unroll
     for (int kk = 0; kk < Tr::kSteps; ++kk) {
 #pragma unroll
@@ -232,19 +218,6 @@ __device__ __forceinline__ void syrk_block(const WideArgs& a, unsigned char* sme
       }
       return;
     }
-    if constexpr (kAug4) {
-#pragma unroll
-      for (int kk = 0; kk < Tr::kSteps; ++kk)
-#pragma unroll
-        for (int x = x0; x < x0 + 2; ++x) {
-          acc[x][0] = Tr::mfma(f.a[kk][x], f.c[kk], acc[x][0]);
-          acc[x][1] = Tr::mfma(f.b[kk][x], f.c[kk], acc[x][1]);
-        }
-      if (x0 == 0)
-#pragma unroll
-        for (int kk = 0; kk < Tr::kSteps; ++kk) acc[0][2] = Tr::mfma(f.c[kk], f.c[kk], acc[0][2]);
-      return;
-    }
 #pragma unroll
     for (int kk = 0; kk < Tr::kSteps; ++kk)
 #pragma unroll
@@ -256,7 +229,7 @@ __device__ __forceinline__ void syrk_block(const WideArgs& a, unsigned char* sme
           acc[x][y] = Tr::mfma(f.a[kk][x], f.b[kk][y], acc[x][y]);
         }
       }
-    if (MODE == 5 && WAVES == 8 && x0 == 0)  // (aug, aug) into the wave's free accumulator (kept for I == 0)
+    if (MODE == 5 && x0 == 0)  // (aug, aug) into the wave's free accumulator (kept for I == 0)
 #pragma unroll
       for (int kk = 0; kk < Tr::kSteps; ++kk) acc[0][1] = Tr::mfma(f.b[kk][0], f.b[kk][0], acc[0][1]);
   };
@@ -266,14 +239,11 @@ __device__ __forceinline__ void syrk_block(const WideArgs& a, unsigned char* sme
   int rb = 0;  // ring buffer of stage i
   auto step = [&](SF& cur, SF& nxt, int64_t i) {
     const int nb = rb + 1 == RING ? 0 : rb + 1;
-    if constexpr (ABL == 3) __builtin_amdgcn_s_setprio(1);
     mfmas(cur, 0);
-    if constexpr (ABL == 3) __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_sched_barrier(0);
     wait_vm<(RING - 2) * kLoadsPerStage>();
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
-    if constexpr (ABL == 3) __builtin_amdgcn_s_setprio(1);
     mfmas(cur, 2);
     read(nxt, nb);
     issue(i + RING, rb);
@@ -287,7 +257,6 @@ __device__ __forceinline__ void syrk_block(const WideArgs& a, unsigned char* sme
       }
     }
     __builtin_amdgcn_sched_barrier(0);
-    if constexpr (ABL == 3) __builtin_amdgcn_s_setprio(0);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     rb = nb;
@@ -311,18 +280,15 @@ __device__ __forceinline__ void syrk_block(const WideArgs& a, unsigned char* sme
   }
   if constexpr (MODE == 5) {  // (I, aug): 256 rows x the augmentation tile's 32 columns
     float* out = a.part + ((int64_t)pair_index(I, a.npanels, a.npanels) * a.splitk + split) * kPanel * kPanel;
-    constexpr int kHalves = WAVES == 4 ? 2 : 1;  // 4 waves: rows 0-127 in acc[x][0], 128-255 in acc[x][1]
 #pragma unroll
-    for (int hh = 0; hh < kHalves; ++hh)
+    for (int x = 0; x < 4; ++x)
 #pragma unroll
-      for (int x = 0; x < 4; ++x)
-#pragma unroll
-        for (int r = 0; r < 16; ++r)
-          out[((WAVES == 4 ? hh : wn) * 128 + x * 32 + mfma32_row(lane, r)) * kPanel + mfma32_col(lane)] = acc[x][hh][r];
+      for (int r = 0; r < 16; ++r)
+        out[(wn * 128 + x * 32 + mfma32_row(lane, r)) * kPanel + mfma32_col(lane)] = acc[x][0][r];
     if (I == 0 && wn == 0) {
       float* o2 = a.part + ((int64_t)pair_index(a.npanels, a.npanels, a.npanels) * a.splitk + split) * kPanel * kPanel;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) o2[mfma32_row(lane, r) * kPanel + mfma32_col(lane)] = acc[0][WAVES == 4 ? 2 : 1][r];
+      for (int r = 0; r < 16; ++r) o2[mfma32_row(lane, r) * kPanel + mfma32_col(lane)] = acc[0][1][r];
     }
     return;
   }
@@ -340,8 +306,8 @@ __device__ __forceinline__ void syrk_block(const WideArgs& a, unsigned char* sme
       }
 }
 
-template <int EB, int RING, int WAVES, int ABL = 0>
-__global__ __launch_bounds__(64 * WAVES, 1) void gram_wide_kernel(WideArgs a) {
+template <int EB, int RING, int ABL = 0>
+__global__ __launch_bounds__(64 * kWaves, 1) void gram_wide_kernel(WideArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   // XCD-aware bijective remap: dispatch puts block b on XCD b % 8; give each XCD a contiguous
   // run of logical ids (split-major, pairs consecutive) so co-resident blocks share panels in L2
@@ -350,10 +316,10 @@ __global__ __launch_bounds__(64 * WAVES, 1) void gram_wide_kernel(WideArgs a) {
   const int npair = (a.npanels + 1) * (a.npanels + 2) / 2;
   const int split = L / npair, pair = L - split * npair;
   const int I = a.pairs[2 * pair], J = a.pairs[2 * pair + 1];
-  if (I == J && J != a.npanels) syrk_block<EB, 3, RING, WAVES, ABL>(a, smem, I, J, pair, split);
-  else if (J != a.npanels) syrk_block<EB, 0, RING, WAVES, ABL>(a, smem, I, J, pair, split);
-  else if (I != a.npanels) syrk_block<EB, 1, RING, WAVES, ABL>(a, smem, I, J, pair, split);
-  else syrk_block<EB, 2, RING, WAVES, ABL>(a, smem, I, J, pair, split);
+  if (I == J && J != a.npanels) syrk_block<EB, 3, RING, ABL>(a, smem, I, J, pair, split);
+  else if (J != a.npanels) syrk_block<EB, 0, RING, ABL>(a, smem, I, J, pair, split);
+  else if (I != a.npanels) syrk_block<EB, 1, RING, ABL>(a, smem, I, J, pair, split);
+  else syrk_block<EB, 2, RING, ABL>(a, smem, I, J, pair, split);
 }
 
 // Persistent, XCD-grouped schedule.  The grid is one block per CU; block b belongs to group
@@ -366,8 +332,8 @@ __global__ __launch_bounds__(64 * WAVES, 1) void gram_wide_kernel(WideArgs a) {
 // grid, co-resident blocks of an XCD mix row ranges and finish at different times (diagonal and
 // augmentation pairs are cheaper), which left the L2 hit rate at 54 % and the fabric reading each
 // input byte ~8x.  The dynamic queue also absorbs the unequal unit costs.
-template <int EB, int RING, int WAVES>
-__global__ __launch_bounds__(64 * WAVES, 1) void gram_wide_queue_kernel(WideArgs a, int* __restrict__ heads, int h) {
+template <int EB, int RING>
+__global__ __launch_bounds__(64 * kWaves, 1) void gram_wide_queue_kernel(WideArgs a, int* __restrict__ heads, int h) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   int* slot = reinterpret_cast<int*>(smem + RING * kStageBytes);  // same LDS array as the ring
   const int g = blockIdx.x & 7;
@@ -382,10 +348,10 @@ __global__ __launch_bounds__(64 * WAVES, 1) void gram_wide_queue_kernel(WideArgs
     const int k = u / npair, pos = u - k * npair;
     const int split = g * h + k;
     const int I = a.pairs[2 * pos], J = a.pairs[2 * pos + 1];
-    if (I == J && J != a.npanels) syrk_block<EB, 3, RING, WAVES>(a, smem, I, J, pos, split);
-    else if (J != a.npanels) syrk_block<EB, 0, RING, WAVES>(a, smem, I, J, pos, split);
-    else if (I != a.npanels) syrk_block<EB, 1, RING, WAVES>(a, smem, I, J, pos, split);
-    else syrk_block<EB, 2, RING, WAVES>(a, smem, I, J, pos, split);
+    if (I == J && J != a.npanels) syrk_block<EB, 3, RING>(a, smem, I, J, pos, split);
+    else if (J != a.npanels) syrk_block<EB, 0, RING>(a, smem, I, J, pos, split);
+    else if (I != a.npanels) syrk_block<EB, 1, RING>(a, smem, I, J, pos, split);
+    else syrk_block<EB, 2, RING>(a, smem, I, J, pos, split);
   }
 }
 
@@ -400,21 +366,21 @@ __global__ __launch_bounds__(64 * WAVES, 1) void gram_wide_queue_kernel(WideArgs
 // other blocks of the round.  The queue schedule's blocks drift apart (unequal unit costs,
 // dynamic dequeue), so there each block re-fetched its panels (L2 hit 61 %, ~6.6x the unique
 // bytes from the fabric).  S is chosen on the host so that npu * S is a multiple of G.
-template <int EB, int RING, int WAVES>
-__global__ __launch_bounds__(64 * WAVES, 1) void gram_wide_gang_kernel(WideArgs a, int S) {
+template <int EB, int RING>
+__global__ __launch_bounds__(64 * kWaves, 1) void gram_wide_gang_kernel(WideArgs a, int S) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int g = blockIdx.x & 7, l = blockIdx.x >> 3, G = gridDim.x >> 3;
   const int P = a.npanels, npu = P * (P + 1) / 2, units = npu * S;
   const int wave = threadIdx.x >> 6;
   // the waves whose tiles lie entirely below a diagonal unit's diagonal
-  const bool aug_wave = WAVES == 8 ? ((wave >> 2) == 1 && (wave & 3) < 2) : wave == 2;
+  const bool aug_wave = (wave >> 2) == 1 && (wave & 3) < 2;
   for (int u = l; u < units; u += G) {
     const int s = u / npu, pos = u - s * npu;
     const int split = g * S + s;
     const int I = a.pairs[2 * pos], J = a.pairs[2 * pos + 1];
-    if (I != J) syrk_block<EB, 0, RING, WAVES>(a, smem, I, J, 0, split);
-    else if (aug_wave) syrk_block<EB, 5, RING, WAVES>(a, smem, I, J, 0, split);
-    else syrk_block<EB, 4, RING, WAVES>(a, smem, I, J, 0, split);
+    if (I != J) syrk_block<EB, 0, RING>(a, smem, I, J, 0, split);
+    else if (aug_wave) syrk_block<EB, 5, RING>(a, smem, I, J, 0, split);
+    else syrk_block<EB, 4, RING>(a, smem, I, J, 0, split);
     __syncthreads();  // every wave is done reading the ring before the next unit's first glds
   }
 }
@@ -650,33 +616,29 @@ int64_t gram_wide_partials(int d, int splitk) {
   return (int64_t)npair * splitk * kPanel * kPanel;
 }
 
-template <int EB, int RING, int WAVES, int ABL = 0>
+template <int EB, int RING, int ABL = 0>
 static void launch_wide(const WideArgs& a, int nblocks, hipStream_t st) {
   const size_t lds = (size_t)RING * kStageBytes;
-  DQ_HIP_CHECK(hipFuncSetAttribute((const void*)gram_wide_kernel<EB, RING, WAVES, ABL>,
+  DQ_HIP_CHECK(hipFuncSetAttribute((const void*)gram_wide_kernel<EB, RING, ABL>,
                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  hipLaunchKernelGGL((gram_wide_kernel<EB, RING, WAVES, ABL>), dim3(nblocks), dim3(64 * WAVES), lds, st, a);
+  hipLaunchKernelGGL((gram_wide_kernel<EB, RING, ABL>), dim3(nblocks), dim3(64 * kWaves), lds, st, a);
   DQ_HIP_CHECK(hipGetLastError());
 }
 
 template <int EB>
 static void launch_wide_eb(const WideArgs& a, int nblocks, hipStream_t st, int ring, int waves) {
-  // diagnostic ablations (timing only, wrong results): waves 41 = no MFMA, 42 = no glds
-  if (waves == 41) return launch_wide<EB, 4, 4, 1>(a, nblocks, st);
-  if (waves == 42) return launch_wide<EB, 4, 4, 2>(a, nblocks, st);
-  // A/B: s_setprio(1) around the MFMA clusters (guide T5), 4 / 8 waves
-  if (waves == 43) return launch_wide<EB, 4, 4, 3>(a, nblocks, st);
-  if (waves == 83) return launch_wide<EB, 4, 8, 3>(a, nblocks, st);
-  if (waves == 8) ring == 5 ? launch_wide<EB, 5, 8>(a, nblocks, st) : launch_wide<EB, 4, 8>(a, nblocks, st);
-  else ring == 5 ? launch_wide<EB, 5, 4>(a, nblocks, st) : launch_wide<EB, 4, 4>(a, nblocks, st);
+  // diagnostic ablations (timing only, wrong results): waves 81 = no MFMA, 82 = no glds
+  if (waves == 81) return launch_wide<EB, 4, 1>(a, nblocks, st);
+  if (waves == 82) return launch_wide<EB, 4, 2>(a, nblocks, st);
+  ring == 5 ? launch_wide<EB, 5>(a, nblocks, st) : launch_wide<EB, 4>(a, nblocks, st);
 }
 
-template <int EB, int RING, int WAVES>
+template <int EB, int RING>
 static void launch_wide_queue(const WideArgs& a, int grid, int* heads, int h, hipStream_t st) {
   const size_t lds = (size_t)RING * kStageBytes + 16;
-  DQ_HIP_CHECK(hipFuncSetAttribute((const void*)gram_wide_queue_kernel<EB, RING, WAVES>,
+  DQ_HIP_CHECK(hipFuncSetAttribute((const void*)gram_wide_queue_kernel<EB, RING>,
                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  hipLaunchKernelGGL((gram_wide_queue_kernel<EB, RING, WAVES>), dim3(grid), dim3(64 * WAVES), lds, st, a, heads, h);
+  hipLaunchKernelGGL((gram_wide_queue_kernel<EB, RING>), dim3(grid), dim3(64 * kWaves), lds, st, a, heads, h);
   DQ_HIP_CHECK(hipGetLastError());
 }
 
@@ -701,19 +663,19 @@ void gram_wide_queue(int eb, WideArgs a, const int* pairs_dev, const float* scal
   a.pairs = pairs_dev;
   if (a.splitk != 8 * h) throw std::invalid_argument("gram_wide_queue: splitk must be 8 * h");
   if (grid < 8 || grid % 8) throw std::invalid_argument("gram_wide_queue: grid must be a positive multiple of 8");
-  if (waves != 4 && waves != 8) throw std::invalid_argument("gram_wide_queue: waves must be 4 or 8");
+  if (waves != kWaves) throw std::invalid_argument("gram_wide_queue: waves must be 8");
   DQ_HIP_CHECK(hipMemsetAsync(heads, 0, 8 * sizeof(int), st));
-  if (eb == 16) waves == 8 ? launch_wide_queue<16, 4, 8>(a, grid, heads, h, st) : launch_wide_queue<16, 4, 4>(a, grid, heads, h, st);
-  else waves == 8 ? launch_wide_queue<8, 4, 8>(a, grid, heads, h, st) : launch_wide_queue<8, 4, 4>(a, grid, heads, h, st);
+  if (eb == 16) launch_wide_queue<16, 4>(a, grid, heads, h, st);
+  else launch_wide_queue<8, 4>(a, grid, heads, h, st);
   if (fold) launch_fold(a, scales, out, nullptr, 0, a.npanels + 1, st);
 }
 
-template <int EB, int WAVES>
+template <int EB>
 static void launch_wide_gang(const WideArgs& a, int grid, int S, hipStream_t st) {
   const size_t lds = (size_t)5 * kStageBytes;
-  DQ_HIP_CHECK(hipFuncSetAttribute((const void*)gram_wide_gang_kernel<EB, 5, WAVES>,
+  DQ_HIP_CHECK(hipFuncSetAttribute((const void*)gram_wide_gang_kernel<EB, 5>,
                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  hipLaunchKernelGGL((gram_wide_gang_kernel<EB, 5, WAVES>), dim3(grid), dim3(64 * WAVES), lds, st, a, S);
+  hipLaunchKernelGGL((gram_wide_gang_kernel<EB, 5>), dim3(grid), dim3(64 * kWaves), lds, st, a, S);
   DQ_HIP_CHECK(hipGetLastError());
 }
 
@@ -723,9 +685,9 @@ void gram_wide_gang(int eb, WideArgs a, const int* pairs_dev, const float* scale
   if (S < 1 || a.splitk != 8 * S) throw std::invalid_argument("gram_wide_gang: splitk must be 8 * S");
   if (grid < 8 || grid % 8) throw std::invalid_argument("gram_wide_gang: grid must be a positive multiple of 8");
   if ((int64_t)a.splitk > a.nsup) throw std::invalid_argument("gram_wide_gang: more row ranges than supersteps");
-  if (waves != 4 && waves != 8) throw std::invalid_argument("gram_wide_gang: waves must be 4 or 8");
-  if (eb == 16) waves == 8 ? launch_wide_gang<16, 8>(a, grid, S, st) : launch_wide_gang<16, 4>(a, grid, S, st);
-  else waves == 8 ? launch_wide_gang<8, 8>(a, grid, S, st) : launch_wide_gang<8, 4>(a, grid, S, st);
+  if (waves != kWaves) throw std::invalid_argument("gram_wide_gang: waves must be 8");
+  if (eb == 16) launch_wide_gang<16>(a, grid, S, st);
+  else launch_wide_gang<8>(a, grid, S, st);
   if (fold) launch_fold(a, scales, out, nullptr, 0, a.npanels + 1, st);
 }
 
@@ -736,8 +698,7 @@ void gram_wide(int eb, WideArgs a, const int* pairs_dev, const float* scales, do
   const int npair = (P + 1) * (P + 2) / 2;
   const int nb = npair * a.splitk;
   if (ring != 4 && ring != 5) throw std::invalid_argument("gram_wide: ring must be 4 or 5");
-  if (waves != 4 && waves != 8 && waves != 41 && waves != 42 && waves != 43 && waves != 83)
-    throw std::invalid_argument("gram_wide: waves must be 4 or 8");
+  if (waves != kWaves && waves != 81 && waves != 82) throw std::invalid_argument("gram_wide: waves must be 8");
   if (eb == 16) launch_wide_eb<16>(a, nb, st, ring, waves);
   else launch_wide_eb<8>(a, nb, st, ring, waves);
   if (fold) launch_fold(a, scales, out, nullptr, 0, P + 1, st);

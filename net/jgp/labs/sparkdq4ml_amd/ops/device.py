@@ -1123,11 +1123,11 @@ def _gram_wide(h, T: TiledWide, y, w, sel, x_zero_dead):
     pairs_dev = _h2d(np.asarray(pairs, dtype=np.int32).reshape(-1), dev)
     out = torch.empty(5 + 2 * d + d * (d + 1) // 2, dtype=torch.float64, device=dev)
     sched = os.environ.get("DQ4ML_WIDE_SCHED", "gang")
-    waves = int(os.environ.get("DQ4ML_WIDE_WAVES", "8"))
-    gs = _wide_gang_s(P, nsup, _wide_grid(h) // 8) if sched == "gang" and waves in (4, 8) else 0
+    waves = int(os.environ.get("DQ4ML_WIDE_WAVES", "8"))  # (81 / 82: timing-only ablations of the static grid)
+    gs = _wide_gang_s(P, nsup, _wide_grid(h) // 8) if sched == "gang" and waves == 8 else 0
     if sched == "gang" and not gs:
         sched = "queue"
-    hq = _wide_queue_h(nsup) if sched == "queue" else 0
+    hq = _wide_queue_h(nsup) if sched == "queue" and waves == 8 else 0
     # data-parallel fit over RCCL: fold band by band and all-reduce each band while the next folds
     banded = comm.collectives_active() and comm.backend() == "nccl"
     if gs:
@@ -1151,8 +1151,7 @@ def _gram_wide(h, T: TiledWide, y, w, sel, x_zero_dead):
         part = torch.empty(int(h.gram_wide_partials(d, splitk)), dtype=torch.float32, device=dev)
         h.gram_wide(eb, T.buf.data_ptr(), aug.buf.data_ptr(), _zero_page(h, dev).data_ptr(), T.nt, P, d, nsup,
                     splitk, pairs_dev.data_ptr(), part.data_ptr(), 1.0, float(s_h), float(s_l), _ptr(T.scales),
-                    out.data_ptr(), _stream(), int(os.environ.get("DQ4ML_WIDE_RING", "5")),
-                    int(os.environ.get("DQ4ML_WIDE_WAVES", "8")), not banded)
+                    out.data_ptr(), _stream(), int(os.environ.get("DQ4ML_WIDE_RING", "5")), waves, not banded)
     if banded and T.shift is not None and not T.shift.uniform:
         raise ValueError("wide Gram over RCCL: the features' shift must be the same on every rank "
                          "(pack_wide(shift='auto') agrees it; a caller-made Shift needs uniform=True)")

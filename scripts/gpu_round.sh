@@ -80,8 +80,6 @@ for s in $STEPS; do
     cfg4r16) step cfg4r16 900 env DQ4ML_DQ_ROWS=16 python benchmarks/bench_dq_pipeline.py --steps 5 --warmup 2 ;;
     gang) step gang_t 600 python -u -m pytest tests/test_gpu_wide.py -m gpu -q --maxfail=3 --timeout 120 --timeout-method thread &&
           step gang_ab 900 env N=1e7 D=4096 EB=8 REPS=5 VARIANTS="${VARIANTS:-5:morton:8:gang,4:morton:8:0:q2}" python scripts/wide_bench.py ;;
-    gang4) step gang4_t 600 python -u -m pytest tests/test_gpu_wide.py -m gpu -q --maxfail=3 --timeout 120 --timeout-method thread -k "schedules or gang" &&
-          step gang4_ab 900 env N=1e7 D=4096 EB=8 REPS=5 VARIANTS="5:morton:8:gang,5:morton:4:gang" python scripts/wide_bench.py ;;
     augvalu) (export TMPDIR=/tmp
        step augvalu_t 600 python -u -m pytest tests/test_gpu_scancut.py tests/test_gpu_scanfuse.py -m gpu -q --maxfail=5 --timeout 120 --timeout-method thread &&
        step augvalu_ab32 600 env VARIANTS="base;DQ4ML_CUT_AUGVALU=0;base;DQ4ML_CUT_AUGVALU=0" python scripts/cut_bench.py --features 32 --rows 2e7 &&

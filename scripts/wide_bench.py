@@ -56,7 +56,7 @@ for _ in range(reps):
             fields = fields[:-1]
             os.environ["DQ4ML_WIDE_H"] = hq
         os.environ["DQ4ML_WIDE_SCHED"] = sched
-        ring, order, waves, splitk = (fields + ["4", "0"][len(fields) - 2:])[:4]
+        ring, order, waves, splitk = (fields + ["8", "0"][len(fields) - 2:])[:4]
         os.environ["DQ4ML_WIDE_RING"], os.environ["DQ4ML_WIDE_ORDER"] = ring, order
         os.environ["DQ4ML_WIDE_WAVES"], os.environ["DQ4ML_WIDE_SPLITK"] = waves, splitk
         if v not in outs:  # warm-up + result

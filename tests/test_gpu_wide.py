@@ -183,7 +183,7 @@ def test_pack_mixed_dtypes_and_misaligned_columns(wide):
 
 @gpu
 @pytest.mark.parametrize("eb", [16, 8])
-@pytest.mark.parametrize("sched", ["gang", "gang4", "queue", "grid"])
+@pytest.mark.parametrize("sched", ["gang", "queue", "grid"])
 @pytest.mark.parametrize("d", [300, 1100])
 def test_wide_schedules_match_oracle(eb, sched, d, monkeypatch):
     # every SYRK schedule (the gang's merged diagonal + augmentation units included) gives the
@@ -191,8 +191,7 @@ def test_wide_schedules_match_oracle(eb, sched, d, monkeypatch):
     _hip()
     from net.jgp.labs.sparkdq4ml_amd.ops import device
 
-    monkeypatch.setenv("DQ4ML_WIDE_SCHED", sched[:4] if sched.startswith("gang") else sched)
-    monkeypatch.setenv("DQ4ML_WIDE_WAVES", "4" if sched == "gang4" else "8")
+    monkeypatch.setenv("DQ4ML_WIDE_SCHED", sched)
     monkeypatch.setenv("DQ4ML_WIDE_GANG_S", "2")
     monkeypatch.setenv("DQ4ML_WIDE_H", "1")
     n = 70_001
