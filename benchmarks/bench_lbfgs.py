@@ -69,7 +69,18 @@ def main(argv=None):
     elapsed, model = timed(lambda: lr.fit(df), a.steps, a.warmup, dev)
     coef = np.asarray(model.coefficients.toArray())
     err = float(np.abs(coef - beta.double().cpu().numpy()).max())
-    # one evaluation alone (margins + columns + fold), for the per-pass bandwidth
+    evals = getattr(model, "_qn_evaluations", None)  # the device fit (lsq_qn.hip) counts its data passes
+    host_steered = None
+    if evals is not None and os.environ.get("DQ4ML_BENCH_AB", "1") != "0":
+        # same-process A/B: the round-3 host-steered optimizer over the two-pass evaluations
+        os.environ["DQ4ML_LSQ_QN"] = "0"
+        try:
+            el2, m2 = timed(lambda: lr.fit(df), 1, 0, dev)
+        finally:
+            os.environ.pop("DQ4ML_LSQ_QN", None)
+        host_steered = {"ms_per_fit": el2 * 1e3, "iterations": int(m2.summary.totalIterations),
+                        "coef_max_abs_diff_vs_device": float(np.abs(np.asarray(m2.coefficients.toArray()) - coef).max())}
+    # one two-pass evaluation alone (margins + columns + fold: the host-steered path's), per-pass bandwidth
     from net.jgp.labs.sparkdq4ml_amd.ops import kernels
 
     P = kernels.lsq_passes(X, y, None, None)
@@ -96,6 +107,9 @@ def main(argv=None):
                      "global_batch": total, "seq_len": d, "parallelism": f"dp{world}", "rows_per_gpu": n,
                      "iterations": int(model.summary.totalIterations), "solver": model.summary.solver,
                      "coef_max_abs_err": err, "eval_ms": eval_ms,
+                     "device_fit_evaluations": evals,
+                     "device_fit_ms_per_evaluation": (ms / (evals + 1)) if evals else None,
+                     "host_steered": host_steered,
                      "eval_hbm_TBps": 2 * xbytes / (eval_ms * 1e-3) / 1e12, "x_bytes_per_gpu": xbytes},
           **info}, a.json_out)
     comm.shutdown()

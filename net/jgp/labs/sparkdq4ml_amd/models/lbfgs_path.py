@@ -22,15 +22,19 @@ and keeps per-iteration device passes (``kernels.huber_pass``).
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 import torch
 
 from ..ops import kernels, native
 from ..parallel import comm
 from ..utils import tracing
+from ..runtime.checks import verify
 from ..utils.logging import get_logger
 from .linalg import DenseVector
 from .optim import GramStats, packed_upper_indices
+from .qn_device import REASONS
 
 log = get_logger("lbfgs")
 
@@ -53,21 +57,21 @@ def _sample_moments(stats: GramStats):
 
 
 def train_lbfgs(est, df, tbl, X, y, d):
-    from ..runtime.checks import verify
     from .regression import (LinearRegressionModel, LinearRegressionTrainingSummary, _fit_checks, _weight_of)
 
     loss = est.getOrDefault("loss")
-    verify(_fit_checks(est, tbl, X))  # the iterative path reads host statistics at once anyway
+    checks = _fit_checks(est, tbl, X)
     w = _weight_of(est, tbl)
     sel = tbl.sel
     if y.valid is not None:
         sel = y.valid if sel is None else (sel & y.valid)
-    if loss == "huber":
-        return _train_huber(est, df, tbl, X, y, w, sel, d)
     sess = getattr(df, "sparkSession", None)
     mode = str(sess.conf.get("dq4ml.lbfgs.mode", "passes")).lower() if sess is not None else "passes"
-    if mode != "gram":
-        return _train_passes(est, df, X, y, w, sel, d)
+    if loss != "huber" and mode != "gram":
+        return _train_passes(est, df, X, y, w, sel, d, checks)
+    verify(checks)  # the host-steered paths read statistics at once anyway
+    if loss == "huber":
+        return _train_huber(est, df, tbl, X, y, w, sel, d)
     flat = kernels.gram_stats(X.values, y.values, w, sel, est.getOrDefault("gramDtype"))
     flat = comm.all_reduce_sum(flat)
     stats = GramStats.from_flat(flat.cpu().numpy(), d)
@@ -131,25 +135,90 @@ def _check_constant_label(raw_ys: float, reg: float) -> None:
     log.warning("The standard deviation of the label is zero. Consider setting fitIntercept=true.")
 
 
-def _train_passes(est, df, X, y, w, sel, d):
+def _device_qn_ok(df, P) -> bool:
+    """The whole fit as one device launch (``LsqPasses.qn_fit``): one rank, wide tiles on a GPU,
+    no optimizer checkpoints (those read the state on the host every few iterations)."""
+    sess = getattr(df, "sparkSession", None)
+    return (P.device.type == "cuda" and P.layout in (2, 3) and not comm.collectives_active()
+            and not (sess is not None and sess.conf.get("dq4ml.lbfgs.checkpointDir", ""))
+            and os.environ.get("DQ4ML_LSQ_QN", "1") != "0")
+
+
+class _PendingLsq:
+    """A device l-bfgs / OWLQN fit (``lsq_qn.hip``) enqueued on the current stream; ``resolve()``
+    reads its result once.  Cases the kernel hands back (empty data, constant label, history
+    capacity) re-run on the host-steered path, which owns Spark's warnings and exceptions."""
+
+    def __init__(self, out, d, solver, checks, fallback):
+        self.out, self.d, self.solver, self._checks, self._fallback = out, d, solver, list(checks), fallback
+        self._res = None
+
+    def resolve(self):
+        if self._res is None:
+            from .optim import WLSModel
+
+            host = self.out.cpu().numpy()
+            verify(self._checks)
+            d = self.d
+            if int(host[d + 1]) != 0:
+                model = self._fallback()
+                self._res = (model._wls_result, model._stats_result)
+                return self._res
+            H = int(host[d + 3])
+            reason = REASONS[int(host[d + 2])]
+            self.evaluations = int(host[d + 5])
+            log.info("l-bfgs path (device, one pass per evaluation): %s after %d states, %d evaluations", reason, H,
+                     self.evaluations)
+            wls = WLSModel(host[:d].copy(), float(host[d]), np.zeros(1), host[d + 11:d + 11 + H].copy(), self.solver)
+            self._res = (wls, GramStats.scalars_only(host[d + 6:d + 11], d))
+        return self._res
+
+
+def _train_passes(est, df, X, y, w, sel, d, checks=(), device_qn=True):
     """Spark 2.4 ``LinearRegression.train`` l-bfgs branch with squared error, data pass per
     evaluation: summarizer moments -> standardization / regularization constants -> Breeze
-    L-BFGS (L2) or OWLQN (L1 > 0) over ``LeastSquaresCostFun`` -> un-standardize."""
+    L-BFGS (L2) or OWLQN (L1 > 0) over ``LeastSquaresCostFun`` -> un-standardize.
+
+    On one GPU with wide tiles the whole sequence is ONE cooperative launch (``lsq_qn.hip``: one
+    fused data pass per evaluation, the line search on the device), enqueued with the summarizer
+    pass; with ``dq4ml.fit.async`` the fit returns at once.  Otherwise the Breeze state stays on
+    the device and the host steers (``models/qn_device.py``)."""
     from .qn_device import minimize
-    from .regression import LinearRegressionModel, LinearRegressionTrainingSummary
+    from .regression import LinearRegressionModel, LinearRegressionTrainingSummary, _async_conf, _async_model
 
     P = kernels.lsq_passes(X.values, y.values, w, sel)
     dev = P.device
     with tracing.span("gram"):  # the summarizer pass (feature moments), one all-reduce with the scalars
         head = comm.all_reduce_sum(torch.cat([P.scalars(), P.moments()]))
-    host = head.cpu().numpy()
-    count, W, W2, bsum, bbsum = (float(v) for v in host[:5])
-    sx_sum, sxx_sum = host[5:5 + d], host[5 + d:5 + 2 * d]
-    stats = GramStats.scalars_only(host[:5], d)
     fit_icpt = bool(est.getOrDefault("fitIntercept"))
     std_flag = bool(est.getOrDefault("standardization"))
     reg, enet = float(est.getOrDefault("regParam")), float(est.getOrDefault("elasticNetParam"))
     max_iter, tol = int(est.getOrDefault("maxIter")), float(est.getOrDefault("tol"))
+    if device_qn and _device_qn_ok(df, P):
+        with tracing.span("solve"):
+            out = P.qn_fit(head, fit_icpt, std_flag, reg, enet, max_iter, tol)
+        if out is not None:
+            solver = "owlqn" if enet != 0.0 and reg != 0.0 else "l-bfgs"
+
+            def fallback():
+                return _train_passes(est, df, X, y, w, sel, d, (), device_qn=False)
+
+            pending = _PendingLsq(out, d, solver, checks, fallback)
+            pending._keep = P
+            if _async_conf(df):
+                return _async_model(est, df, pending)
+            wls, stats = pending.resolve()
+            model = LinearRegressionModel(est.uid, DenseVector(wls.coefficients), float(wls.intercept))
+            est.copyValues(model)
+            model._set_summary(LinearRegressionTrainingSummary(model, df, None, wls.objectiveHistory, stats=stats,
+                                                               solver=solver))
+            model._qn_evaluations = getattr(pending, "evaluations", None)
+            return model
+    verify(checks)
+    host = head.cpu().numpy()
+    count, W, W2, bsum, bbsum = (float(v) for v in host[:5])
+    sx_sum, sxx_sum = host[5:5 + d], host[5 + d:5 + 2 * d]
+    stats = GramStats.scalars_only(host[:5], d)
     if W <= 0.0:
         raise ValueError("requirement failed: The training dataset is empty (weight sum is 0).")
     denom = W - W2 / W
@@ -160,9 +229,15 @@ def _train_passes(est, df, X, y, w, sel, d):
     sx, raw_ys = np.sqrt(var_x), float(np.sqrt(var_y))
 
     def finish(coef, icpt, hist, solver):
+        from .optim import WLSModel
+
         model = LinearRegressionModel(est.uid, DenseVector(coef), float(icpt))
         est.copyValues(model)
         model._set_summary(LinearRegressionTrainingSummary(model, df, None, hist, stats=stats, solver=solver))
+        # (a device fit's fallback hands these back to its pending result)
+        model._wls_result = WLSModel(np.asarray(coef, dtype=np.float64), float(icpt), np.zeros(1),
+                                     np.asarray(hist, dtype=np.float64), solver)
+        model._stats_result = stats
         return model
 
     if raw_ys == 0.0 and (fit_icpt or my == 0.0):

@@ -376,6 +376,17 @@ PYBIND11_MODULE(_dq4ml_hip, m) {
     lsq_columns(lsqx(X, layout, xdt, ld, d, n), mode, P<const double>(v), P<const double>(lpart), nl, P<double>(part),
                 P<double>(out), as_stream(stream));
   });
+  m.attr("LSQ_QN_MAX_D") = kLsqQnMaxD;
+  m.def("lsq_qn_blocks", &lsq_qn_blocks);
+  m.def("lsq_qn_work", &lsq_qn_work);
+  m.def("lsq_qn", [lsqx](uintptr_t X, int layout, int d, int64_t n, uintptr_t y, uintptr_t w, uintptr_t scale,
+                         uintptr_t shift, uintptr_t head, bool fit_icpt, bool std_f, double reg, double enet,
+                         int max_iter, double tol, int hist_cap, uintptr_t work, int blocks, uintptr_t out,
+                         uintptr_t stream) {
+    lsq_qn(lsqx(X, layout, 2, 0, d, n), P<const double>(y), P<const double>(w), P<const double>(scale),
+           P<const double>(shift), P<const double>(head), fit_icpt, std_f, reg, enet, max_iter, tol, hist_cap,
+           P<double>(work), blocks, P<double>(out), as_stream(stream));
+  });
   m.def("regression_metrics",
         [](uintptr_t X, int xdt, int64_t ld, int d, int64_t n, uintptr_t y, int ydt, uintptr_t sel, uintptr_t coef,
            double b, double shift, uintptr_t partials, uintptr_t out, uintptr_t stream, int tiled) {

@@ -775,6 +775,37 @@ class LsqPasses:
         return out
 
 
+    def qn_fit(self, head: torch.Tensor, fit_icpt: bool, std_f: bool, reg: float, enet: float, max_iter: int,
+               tol: float) -> Optional[torch.Tensor]:
+        """The whole squared-loss l-bfgs / OWLQN fit as ONE cooperative launch (``lsq_qn.hip``):
+        standardization from the summarizer ``head`` ([scalars(5), moments(2d)], on the device),
+        one fused data pass per cost evaluation, the Breeze control flow on the device.  Enqueued
+        on the current stream, no host sync.  Returns ``[coef(d), intercept, status, reason, H,
+        iterations, spare, head(5), history(cap)]`` or None (not a wide tile layout / d too large)."""
+        h = self._h
+        if self.layout not in (2, 3) or not 1 <= self.d <= int(h.LSQ_QN_MAX_D) or self.n < 1:
+            return None
+        key = (self.device.index, self.layout, self.d)
+        nb = _lsq_qn_grid.get(key)
+        if nb is None:
+            nb = _lsq_qn_grid[key] = int(h.lsq_qn_blocks(self.layout, self.d))
+        cap = wls_qn_cap(max_iter)
+        work = torch.empty(int(h.lsq_qn_work(self.d, nb)), dtype=torch.float64, device=self.device)
+        out = torch.empty(self.d + 11 + cap, dtype=torch.float64, device=self.device)
+        head = head.to(torch.float64).contiguous()
+        if head.numel() != 5 + 2 * self.d:
+            raise ValueError("lsq_qn: the summarizer head must hold 5 + 2d values")
+        shift = None if self.shift is None else self.shift.dev64.to(self.device).contiguous()
+        h.lsq_qn(self._xb.data_ptr(), self.layout, self.d, self.n, self.y.data_ptr(), self.w.data_ptr(),
+                 _ptr(self.scales), _ptr(shift), head.data_ptr(), bool(fit_icpt), bool(std_f), float(reg), float(enet),
+                 int(max_iter), float(tol), cap, work.data_ptr(), nb, out.data_ptr(), _stream())
+        self._qn_keep = (work, head, shift)  # alive until the launch has run (caching allocator reuse)
+        return out
+
+
+_lsq_qn_grid = {}
+
+
 # ------------------------------------------------------------------------------------------
 def wls_small(flat: torch.Tensor, nf: int, fit_intercept: bool, reg: float, enet: float, std_f: bool,
               std_l: bool) -> torch.Tensor:

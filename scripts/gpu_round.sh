@@ -31,6 +31,9 @@ for s in $STEPS; do
        step widepmc1 600 rocprofv3 --kernel-trace --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE -d gpurun_out/widepmc1 -o run --output-format csv -- python scripts/wide_bench.py &&
        step widepmc2 600 rocprofv3 --kernel-trace --pmc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum -d gpurun_out/widepmc2 -o run --output-format csv -- python scripts/wide_bench.py) || exit $? ;;
     cfg4) step cfg4 900 python benchmarks/bench_dq_pipeline.py --steps ${CFG4_STEPS:-5} --warmup 2 --json-out gpurun_out/cfg4.json ;;
+    cfg4csv) step cfg4csv 1000 python benchmarks/bench_csv_pipeline.py --features 64 --rows 1.25e8 --steps 5 --warmup 1 --json-out gpurun_out/cfg4csv.json &&
+             (export TMPDIR=/tmp; step cfg4csvprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/cfg4csvprof -o run --output-format csv -- python benchmarks/bench_csv_pipeline.py --features 64 --rows 1.25e8 --steps 3 --warmup 1) &&
+             step cfg4csvstream 900 env DQ4ML_FILECACHE_DEVICE_BYTES=1 python benchmarks/bench_csv_pipeline.py --features 64 --rows 1.25e8 --steps 2 --warmup 1 --json-out gpurun_out/cfg4csvstream.json || exit $? ;;
     cfg4prof) step cfg4prof 900 env DQ4ML_BENCH_CPROFILE=gpurun_out/cfg4.prof python benchmarks/bench_dq_pipeline.py --steps 10 --warmup 2 ;;
     cfg4two) step cfg4two 900 env DQ4ML_STREAM_DQ=0 python benchmarks/bench_dq_pipeline.py --steps 5 --warmup 2 --json-out gpurun_out/cfg4two.json ;;
     kprof4sf) (export TMPDIR=/tmp; step kprof4sf 600 rocprofv3 --kernel-trace --stats -d gpurun_out/kprof4sf -o run --output-format csv -- python benchmarks/bench_dq_pipeline.py --steps 3 --warmup 1) || exit $? ;;
@@ -53,8 +56,7 @@ for s in $STEPS; do
            step f32s2_d 300 python bench.py --steps 20 --warmup 3 --dtype bf16 --storage fp32 &&
            (export TMPDIR=/tmp; step f32s2pmc 300 timeout -s KILL 240 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_SALU GRBM_GUI_ACTIVE -d gpurun_out/f32s2pmc -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --dtype fp32split) || exit $? ;;
     qn) step qn_t 600 python -u -m pytest tests/test_gpu_owlqn.py -m gpu -v --timeout 120 --timeout-method thread &&
-        step qn_b 600 python scripts/owlqn_bench.py &&
-        step qn_bt 600 env DQ4ML_QN_ENGINE=torch CASES=4096:0.01 python scripts/owlqn_bench.py || exit $? ;;
+        step qn_b 600 python scripts/owlqn_bench.py || exit $? ;;
     pipe) step pipe_t 600 python -u -m pytest tests/test_gpu_fit_pipeline.py tests/test_gpu_pipeline.py tests/test_gpu_determinism.py tests/test_gpu_owlqn.py -m gpu -q --timeout 120 --timeout-method thread &&
           for r in 1 2; do for m in 1 2; do
             step pipe_${m}_s${r} 300 env DQ4ML_FIT_PIPELINE=$m python bench.py --steps 200 --warmup 20 --rows 1.25e7 &&

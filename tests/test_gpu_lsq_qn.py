@@ -1,0 +1,97 @@
+"""the squared-loss l-bfgs / OWLQN fit as ONE cooperative launch (``lsq_qn.hip``:
+standardization from the device summarizer head, one fused data pass per cost evaluation, the
+Breeze line searches on the device) against the host-steered path (``models/qn_device.py`` over
+the two-pass ``lsq.hip`` evaluations, ``DQ4ML_LSQ_QN=0``) on the wide bf16 / fp8 tiles; an
+asynchronous fit enqueues everything with no host sync."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _data(dev, d, n, seed, eb, y0=0.5, const=False):
+    from net.jgp.labs.sparkdq4ml_amd.ops import device
+
+    g = torch.Generator(device=dev).manual_seed(seed)
+    X = torch.randn(d, n, generator=g, device=dev) * (0.5 + torch.rand(d, 1, generator=g, device=dev))
+    beta = torch.zeros(d, device=dev)
+    k = min(d, 40)
+    beta[:k] = torch.linspace(-1.0, 2.0, k, device=dev)
+    y = (beta @ X + y0 + 0.1 * torch.randn(n, generator=g, device=dev)).double()
+    if const:
+        y = torch.full((n,), 3.25, dtype=torch.float64, device=dev)
+    return device.pack_wide([X], eb, None), y
+
+
+def _fit(lr, df, monkeypatch, device_qn: bool):
+    monkeypatch.setenv("DQ4ML_LSQ_QN", "1" if device_qn else "0")
+    return lr.fit(df)
+
+
+@pytest.mark.parametrize("eb,d,n,kw", [
+    (16, 300, 60_001, dict(regParam=0.02, elasticNetParam=0.0)),                      # L-BFGS, strong Wolfe
+    (16, 300, 60_001, dict(regParam=0.02, elasticNetParam=0.6)),                      # OWLQN, backtracking
+    (8, 1100, 30_017, dict(regParam=0.01, elasticNetParam=1.0, fitIntercept=False)),
+    (16, 5000, 8_003, dict(regParam=0.001, elasticNetParam=0.0, standardization=False)),
+])
+def test_device_qn_matches_host_steered(gpu_session, monkeypatch, eb, d, n, kw):
+    from net.jgp.labs.sparkdq4ml_amd import LinearRegression
+    from net.jgp.labs.sparkdq4ml_amd.models import lbfgs_path
+
+    T, y = _data(gpu_session.device, d, n, d + eb, eb)
+    df = gpu_session.createDataFrame({"features": T, "label": y})
+    lr = LinearRegression(solver="l-bfgs", maxIter=60, tol=1e-9, **kw)
+    m_dev = _fit(lr, df, monkeypatch, True)
+    assert m_dev.summary.solver == ("owlqn" if kw["elasticNetParam"] else "l-bfgs")
+    m_host = _fit(lr, df, monkeypatch, False)
+    a, b = m_dev.coefficients.toArray(), m_host.coefficients.toArray()
+    # the device pass sums the columns in a different f32 / f64 order than the two-pass kernels:
+    # the iterates agree to the optimizer's own resolution, not bitwise
+    assert np.abs(a - b).max() <= 2e-4 * max(1.0, np.abs(b).max()), np.abs(a - b).max()
+    assert float(m_dev.intercept) == pytest.approx(float(m_host.intercept), rel=1e-4, abs=1e-5)
+    hd, hh = np.asarray(m_dev.summary.objectiveHistory), np.asarray(m_host.summary.objectiveHistory)
+    assert hd[0] == pytest.approx(hh[0], rel=1e-9)
+    assert hd[-1] == pytest.approx(hh[-1], rel=1e-6)
+    assert abs(len(hd) - len(hh)) <= 3
+    assert np.all(np.diff(hd) <= 1e-12 * abs(hd[0]))
+    # the device fit is deterministic: fixed-order reductions everywhere
+    m_again = _fit(lr, df, monkeypatch, True)
+    assert np.array_equal(m_again.coefficients.toArray(), a)
+    assert lbfgs_path._device_qn_ok is not None
+
+
+def test_device_qn_async_fit_has_no_host_sync(gpu_session, monkeypatch):
+    from net.jgp.labs.sparkdq4ml_amd import LinearRegression
+
+    monkeypatch.setenv("DQ4ML_LSQ_QN", "1")
+    T, y = _data(gpu_session.device, 4200, 20_000, 9, 16)
+    df = gpu_session.createDataFrame({"features": T, "label": y})
+    lr = LinearRegression(regParam=0.001, elasticNetParam=0.0, maxIter=40)  # numFeatures > 4096: auto -> l-bfgs
+    gpu_session.conf.set("dq4ml.fit.async", "true")
+    try:
+        lr.fit(df).coefficients  # warm-up (allocator, launch plan)
+        torch.cuda.synchronize()
+        torch.cuda.set_sync_debug_mode("error")
+        try:
+            m = lr.fit(df)
+            assert m._pending is not None
+        finally:
+            torch.cuda.set_sync_debug_mode("default")
+    finally:
+        gpu_session.conf.set("dq4ml.fit.async", "false")
+    ref = lr.fit(df)
+    np.testing.assert_array_equal(m.coefficients.toArray(), ref.coefficients.toArray())
+    assert m.summary.solver == "l-bfgs"
+    assert list(m.summary.objectiveHistory) == list(ref.summary.objectiveHistory)
+
+
+def test_device_qn_constant_label_takes_the_host_semantics(gpu_session, monkeypatch):
+    from net.jgp.labs.sparkdq4ml_amd import LinearRegression
+
+    monkeypatch.setenv("DQ4ML_LSQ_QN", "1")
+    T, y = _data(gpu_session.device, 300, 5_000, 4, 16, const=True)
+    df = gpu_session.createDataFrame({"features": T, "label": y})
+    m = LinearRegression(solver="l-bfgs", regParam=0.1).fit(df)
+    assert np.all(m.coefficients.toArray() == 0.0)
+    assert float(m.intercept) == pytest.approx(3.25)
