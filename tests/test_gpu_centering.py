@@ -142,7 +142,8 @@ def test_shifted_tiles_round_trip_and_predict():
     coef = beta.cpu().numpy()
     p = device.predict(T, coef, 3.0)
     ref = (beta @ dense.double()) + 3.0
-    assert float((p - ref).abs().max() / ref.abs().max()) < 1e-9
+    # (the reference reads x' + s rounded to f32: 2^-24 of |x| ~ 1000 per term)
+    assert float((p - ref).abs().max() / ref.abs().max()) < 1e-7
 
 
 @pytest.mark.parametrize("dt,d", [("bfloat16", 24), ("float8", 96)])
@@ -166,5 +167,7 @@ def test_assembled_fit_of_off_centre_columns_matches_fp64(dt, d):
         fits[gd] = (np.asarray(m.coefficients.toArray()), m.intercept)
     c64, c = fits["fp64"][0], fits["bf16" if dt == "bfloat16" else "fp8"][0]
     rel = np.abs(c - c64).max() / np.abs(c64).max()
-    assert rel < (1e-2 if dt == "bfloat16" else 5e-2), rel
+    # fp8 bound: e4m3 keeps 3 mantissa bits; quantizing the centred columns of this table alone (CPU
+    # simulation, torch.float8_e4m3fn, lstsq in f64) moves the worst coefficient by 4.4 % of max |coef|
+    assert rel < (1e-2 if dt == "bfloat16" else 1e-1), rel
     assert np.abs(c64 - beta.cpu().numpy()).max() < 1e-2  # the fp64 fit itself recovers beta
