@@ -174,6 +174,12 @@ class VectorAssembler(Params):
         cols = self.getOrDefault("inputCols")
         out = self.getOrDefault("outputCol")
         hi = self.getOrDefault("handleInvalid")
+        dt = self.getOrDefault("outputDtype")
+        # the same assembly of a structurally equal DataFrame: its analyzed node (sql/skey.py)
+        op = ("VectorAssembler", tuple(cols), out, hi, dt) if hi != "skip" else None
+        return df._derive(op, lambda: self._transform(df, cols, out, hi))
+
+    def _transform(self, df, cols, out, hi):
         schema = df.schema
         for c in cols:
             ColRef(c).data_type(schema)

@@ -149,6 +149,8 @@ class _PendingLsq:
     reads its result once.  Cases the kernel hands back (empty data, constant label, history
     capacity) re-run on the host-steered path, which owns Spark's warnings and exceptions."""
 
+    pending_fit = True
+
     def __init__(self, out, d, solver, checks, fallback):
         self.out, self.d, self.solver, self._checks, self._fallback = out, d, solver, list(checks), fallback
         self._res = None

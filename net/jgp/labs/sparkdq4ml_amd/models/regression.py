@@ -567,6 +567,8 @@ class _PendingWLS:
     for the next launch at once (the Gram kernel leaves CU slots for the one-workgroup solve and
     the RCCL kernel).  ``resolve()`` orders the caller's stream after the tail before reading."""
 
+    pending_fit = True
+
     def __init__(self, args, overlap: bool = False, checks=None):
         flat, d, fit_icpt, reg, enet, std_f, std_l = args[:7]
         max_iter, tol = args[8], args[9]
@@ -914,7 +916,7 @@ class _CallableDF(DataFrame):
 
 class LinearRegressionTrainingSummary(LinearRegressionSummary):
     def __init__(self, model, df, diag_inv, objective_history, stats=None, solver="auto"):
-        if isinstance(diag_inv, _PendingWLS):  # asynchronous fit: everything resolves on first read
+        if getattr(diag_inv, "pending_fit", False):  # asynchronous fit: everything resolves on first read
             self._pending_fit = diag_inv
             super().__init__(model, df, None, None)
             self._hist_v, self._solver_v = None, None

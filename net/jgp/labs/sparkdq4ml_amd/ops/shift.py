@@ -102,7 +102,8 @@ def _sample_stats(rows: List[torch.Tensor]):
     samp = torch.stack([r[::step][:SAMPLE_ROWS].to(torch.float64) for r in rows])
     fin = torch.isfinite(samp)
     z = torch.where(fin, samp, torch.zeros_like(samp))
-    return torch.stack([z.sum(1), (z * z).sum(1), fin.sum(1).to(torch.float64)])
+    frac = (z != torch.round(z)).sum(1).to(torch.float64)  # sampled values off the integer grid
+    return torch.stack([z.sum(1), (z * z).sum(1), fin.sum(1).to(torch.float64), frac])
 
 
 def column_shift(parts: Sequence[torch.Tensor], uniform: bool = False) -> Optional[Shift]:
@@ -127,7 +128,7 @@ def column_shift(parts: Sequence[torch.Tensor], uniform: bool = False) -> Option
     st = _sample_stats(rows)
     if coll:
         st = comm.all_reduce_sum(st)
-    s, ss, cnt = st.cpu().numpy()
+    s, ss, cnt, frac = st.cpu().numpy()
     cnt = np.maximum(cnt, 1.0)
     mean = s / cnt
     var = np.maximum(ss / cnt - mean * mean, 0.0)
@@ -135,6 +136,9 @@ def column_shift(parts: Sequence[torch.Tensor], uniform: bool = False) -> Option
     val = None
     if need.any():
         shift = np.where(need, mean, 0.0)
+        # an integral column (the lab's guest count) keeps exact values: x - s must stay on the
+        # integer grid, or the bf16 cast of x - s rounds what x alone kept exactly
+        shift = np.where(frac == 0.0, np.rint(shift), shift)
         bf16 = np.array([r.dtype == torch.bfloat16 for r in rows])
         if bf16.any():
             sb = torch.from_numpy(shift).to(torch.bfloat16).to(torch.float64).numpy()

@@ -15,6 +15,7 @@ from ..utils.javafmt import java_str
 from .column import Column
 from .expressions import (Alias, AnalysisException, ColRef, Expr, to_expr)
 from .plan import Filter, Limit, LocalRelation, LogicalPlan, Project, Union, execute, is_sharded, output_name
+from .skey import expr_key, exprs_key
 from .table import Table
 from .types import StructType, VectorUDT
 
@@ -168,6 +169,9 @@ class DataFrameNaFunctions:
         return out
 
 
+_DERIVED: dict = {}  # (parent plan skey, transformation) -> analyzed template node (no child)
+
+
 class DataFrame:
     def __init__(self, plan: LogicalPlan, session):
         self._plan = plan
@@ -197,6 +201,28 @@ class DataFrame:
     # ---- transformations -------------------------------------------------------------------
     def _with(self, plan):
         return DataFrame(plan, self.sparkSession)
+
+    def _derive(self, op, build):
+        """Structural sharing of analysis (``sql/skey.py``): the transformation ``op`` of a plan
+        with the same structural key was analyzed before -> a fresh copy of that analyzed node over
+        this DataFrame's plan (no execution result is shared: the copy has none).  Else ``build()``
+        analyzes, and a one-node result over this plan is kept as the template."""
+        pk = self._plan.skey() if op is not None else None
+        if pk is not None:
+            t = _DERIVED.get((pk, op))
+            if t is not None:
+                return DataFrame(t.fresh(self._plan), self.sparkSession)
+        df = build()
+        node = df._plan
+        if pk is not None and node is not self._plan and getattr(node, "child", None) is self._plan \
+                and node.skey() is not None:
+            node.schema()  # analyzed before it becomes a template
+            t = node.fresh()
+            t.child = None  # the template holds no lineage (and so no execution results)
+            if len(_DERIVED) >= 4096:
+                _DERIVED.clear()
+            _DERIVED[(pk, op)] = t
+        return df
 
     def col(self, name: str) -> Column:
         if name != "*" and self.schema.resolve_ci(name) is None:
@@ -233,8 +259,12 @@ class DataFrame:
                     exprs.append(ColRef(c))
             else:
                 exprs.append(to_expr(c))
-        self._check_refs(exprs)
-        return self._with(Project(self._plan, exprs))
+        ek = exprs_key(exprs)
+
+        def build():
+            self._check_refs(exprs)
+            return self._with(Project(self._plan, exprs))
+        return self._derive(("select", ek) if ek is not None else None, build)
 
     def selectExpr(self, *exprs):
         from .parser import parse_select_item
@@ -248,6 +278,10 @@ class DataFrame:
 
     def withColumn(self, name: str, c: Column) -> "DataFrame":
         e = to_expr(c)
+        ek = expr_key(e)
+        return self._derive(("withColumn", name, ek) if ek is not None else None, lambda: self._with_column(name, e))
+
+    def _with_column(self, name: str, e) -> "DataFrame":
         names = self.columns
         exprs = []
         replaced = False
@@ -263,10 +297,13 @@ class DataFrame:
         return self._with(Project(self._plan, exprs))
 
     def withColumnRenamed(self, existing: str, new: str) -> "DataFrame":
-        names = self.columns
-        if existing not in names:
-            return self
-        return self._with(Project(self._plan, [Alias(ColRef(n), new) if n == existing else ColRef(n) for n in names]))
+        def build():
+            names = self.columns
+            if existing not in names:
+                return self
+            return self._with(Project(self._plan, [Alias(ColRef(n), new) if n == existing else ColRef(n)
+                                                   for n in names]))
+        return self._derive(("withColumnRenamed", existing, new), build)
 
     def drop(self, *cols):
         drop = {c if isinstance(c, str) else output_name(c._expr) for c in cols}
@@ -279,7 +316,8 @@ class DataFrame:
             e = parse_expression(cond)
         else:
             e = to_expr(cond)
-        return self._with(Filter(self._plan, e))
+        ek = expr_key(e)
+        return self._derive(("filter", ek) if ek is not None else None, lambda: self._with(Filter(self._plan, e)))
 
     where = filter
 

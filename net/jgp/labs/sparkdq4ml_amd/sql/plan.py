@@ -14,6 +14,7 @@ from typing import List, Optional, Sequence, Tuple
 import torch
 
 from .expressions import (Alias, AnalysisException, ColRef, EvalContext, Expr, UdfCall)
+from .skey import expr_key, exprs_key, intern
 from .table import ColumnData, Table
 from .types import BooleanType, StructField, StructType
 
@@ -22,9 +23,26 @@ __all__ = ["LogicalPlan", "LocalRelation", "CsvScanRelation", "Project", "Filter
 
 class LogicalPlan:
     _memo: Optional[Table] = None
+    _skey = 0  # structural key (sql/skey.py): 0 = not computed yet, None = unkeyable
 
     def children(self) -> List["LogicalPlan"]:
         return []
+
+    def skey(self) -> Optional[int]:
+        """Interned structural key: equal for two nodes that denote the same computation over the
+        same input (an action's rebuilt chain), None when the node cannot be keyed."""
+        return None
+
+    def fresh(self, child: Optional["LogicalPlan"] = None) -> "LogicalPlan":
+        """A copy of this (analyzed) node with no execution result, over ``child``: the DataFrame
+        layer's structural sharing hands every action its own nodes."""
+        n = object.__new__(type(self))
+        d = n.__dict__
+        d.update(self.__dict__)
+        d.pop("_memo", None)
+        if child is not None:
+            d["child"] = child
+        return n
 
     def schema(self) -> StructType:
         raise NotImplementedError
@@ -58,6 +76,14 @@ class LocalRelation(LogicalPlan):
 
     def schema(self):
         return self.table.schema
+
+    def skey(self):
+        # one key per relation object (a serial, not the table's id: nothing is pinned); chains
+        # rebuilt over the same relation share their analysis
+        k = self.__dict__.get("_skey")
+        if k is None:
+            k = self._skey = intern(("local", next(_SERIAL)))
+        return k
 
     def _compute(self, session):
         return self.table
@@ -96,8 +122,21 @@ class CsvScanRelation(LocalRelation):
     def _compute(self, session):
         return self._scan()
 
+    def skey(self):
+        return self.__dict__.get("_skey")  # set by the reader from the cached input's identity
+
+    def fresh(self, child=None):
+        n = super().fresh()
+        n._memo = None
+        return n
+
     def _label(self):
         return f"{self.label} [{', '.join(self._schema.names)}]"
+
+
+_SCHEMAS: dict = {}   # Project skey -> analyzed schema
+_SERIAL = __import__("itertools").count(1)
+_CHECKED: set = set()  # Filter skeys whose condition type-checked
 
 
 def is_sharded(plan) -> bool:
@@ -125,8 +164,21 @@ class Project(LogicalPlan):
     def children(self):
         return [self.child]
 
+    def skey(self):
+        k = self._skey
+        if k == 0:
+            ck = self.child.skey()
+            ek = exprs_key(self.exprs) if ck is not None else None
+            k = self._skey = intern(("Project", ck, ek)) if ek is not None else None
+        return k
+
     def schema(self):
         if self._schema is None:
+            k = self.skey()
+            s = _SCHEMAS.get(k) if k is not None else None
+            if s is not None:
+                self._schema = s
+                return s
             cs = self.child.schema()
             fields = []
             for e in self.exprs:
@@ -139,6 +191,10 @@ class Project(LogicalPlan):
                     meta = base.metadata(cs)
                 fields.append(StructField(output_name(e), dt, e.nullable(cs), meta))
             self._schema = StructType(fields)
+            if k is not None:
+                if len(_SCHEMAS) >= 4096:
+                    _SCHEMAS.clear()
+                _SCHEMAS[k] = self._schema
         return self._schema
 
     def _compute(self, session):
@@ -165,13 +221,28 @@ class Filter(LogicalPlan):
     def __init__(self, child: LogicalPlan, cond: Expr):
         self.child = child
         self.cond = cond
+        k = self.skey()
+        if k is not None and k in _CHECKED:
+            return
         dt = cond.data_type(child.schema())
         if not isinstance(dt, BooleanType):
             raise AnalysisException(f"filter expression '{cond.sql_name()}' of type {dt.simpleString()} "
                                     f"is not a boolean.")
+        if k is not None:
+            if len(_CHECKED) >= 4096:
+                _CHECKED.clear()
+            _CHECKED.add(k)
 
     def children(self):
         return [self.child]
+
+    def skey(self):
+        k = self._skey
+        if k == 0:
+            ck = self.child.skey()
+            ek = expr_key(self.cond) if ck is not None else None
+            k = self._skey = intern(("Filter", ck, ek)) if ek is not None else None
+        return k
 
     def schema(self):
         return self.child.schema()
