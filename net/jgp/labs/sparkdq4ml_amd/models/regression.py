@@ -168,9 +168,15 @@ def _fused_scan_stats(params, df: DataFrame):
     from ..ops import scanfuse, streamfuse
     from ..sql.plan import prune_columns
 
-    plan = prune_columns(df._plan, {fc, lc})
     if gd == "fp64":
-        return scanfuse.try_fused_gram(plan, fc, lc, sess)
+        # an action that rebuilt a chain of the same structure over the same cached input replays
+        # the lowered kernel (sql/skey.py): only the launch and its outputs are new
+        rk = scanfuse.route_key(p0.skey(), fc, lc, sess)
+        fused = scanfuse.replay(rk, p0, sess)
+        if fused is not None:
+            return fused
+        return scanfuse.try_fused_gram(prune_columns(df._plan, {fc, lc}), fc, lc, sess, route_key=rk)
+    plan = prune_columns(df._plan, {fc, lc})
     # bf16 / exact-f32 statistics over in-memory columns: the DQ chain in the stream Gram's
     # stage prologue, one HBM pass (ops/streamfuse.py)
     return streamfuse.try_fused_stream(plan, fc, lc, sess, gd)

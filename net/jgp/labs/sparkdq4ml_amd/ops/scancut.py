@@ -842,6 +842,16 @@ def try_cut_gram(chain, rel, d: int):
     cp = _compile(chain, rel, d)
     if cp is None:
         return None
+    return launch_cut(cp, rel, d)
+
+
+def launch_cut(cp, rel, d: int):
+    """One launch of the compiled cutter ``cp`` over ``rel``'s device bytes (the part of
+    ``try_cut_gram`` a replayed action repeats)."""
+    from . import native
+    from .device import _h2d
+    from ..utils import tracing
+
     f = rel.fused
     h = native.hip()
     dev = f["device"]

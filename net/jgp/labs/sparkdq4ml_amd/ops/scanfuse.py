@@ -779,7 +779,7 @@ class FusedGram:
         self.flat, self.d, self.checks, self.nrows = flat, d, checks, nrows
 
 
-def try_fused_gram(plan, features_col: str, label_col: str, session) -> Optional[FusedGram]:
+def try_fused_gram(plan, features_col: str, label_col: str, session, route_key=None) -> Optional[FusedGram]:
     """K1 + K3 + the VectorAssembler + the normal-equation Gram pass in ONE kernel: ``plan`` (pruned
     to the features and label) must be ``Project[VectorAssembler(inputs) AS features, label]`` over
     a Project/Filter chain over a not-yet-scanned CSV relation, with at most 8 numeric inputs, no
@@ -830,19 +830,86 @@ def try_fused_gram(plan, features_col: str, label_col: str, session) -> Optional
 
     if p.fused.get("buf") is None:  # input not resident in HBM: the same kernels over a chunk ring
         return _streamed_gram(chain, p, d)
-    cut = scancut.try_cut_gram(chain, p, d)  # the byte-parallel field cutter (wide rows, any d <= 128)
-    if cut is not None:
-        flat, err, vflag, ccp = cut
-        checks = [_fact_check(p, vflag)]
-        if ccp.has_raise:
-            checks.append(_udf_error_check(chain, err))
-        STATS["fused_grams"] += 1
-        return FusedGram(flat, d, [c for c in checks if c is not None], int(p.fused["nlines"]))
+    ccp = scancut._compile(chain, p, d)  # the byte-parallel field cutter (wide rows, any d <= 128)
+    if ccp is not None:
+        route = _Route("cut", chain, ccp, d)
+        _remember(route_key, route, session)
+        return route.run(p)
     if d > 8:
         return None
     cp = _compile(chain, p, gram=d)
     if cp is None or cp == "vector":
         return None
+    route = _Route("line", chain, cp, d)
+    _remember(route_key, route, session)
+    return route.run(p)
+
+
+class _Route:
+    """An action's lowered fused-scan fit: the compiled kernel (cutter or per-line) and the chain
+    it was compiled from.  ``run(rel)`` launches it over a relation of the same structure (the
+    action's fresh leaf: same cached bytes and facts)."""
+
+    def __init__(self, kind, chain, cp, d):
+        self.kind, self.chain, self.cp, self.d = kind, chain, cp, d
+        self.conf = None
+
+    def run(self, p) -> "FusedGram":
+        if self.kind == "cut":
+            from . import scancut
+
+            flat, err, vflag, ccp = scancut.launch_cut(self.cp, p, self.d)
+            checks = [_fact_check(p, vflag)]
+            if ccp.has_raise:
+                checks.append(_udf_error_check(self.chain, err))
+            STATS["fused_grams"] += 1
+            return FusedGram(flat, self.d, [c for c in checks if c is not None], int(p.fused["nlines"]))
+        return _run_line_gram(self.cp, self.chain, p, self.d)
+
+
+_ROUTES: dict = {}
+_ROUTE_ENV = ("DQ4ML_SCAN_GRAM", "DQ4ML_SCAN_CUT", "DQ4ML_CUT_MIN_LINE", "DQ4ML_SCAN_LOOKBACK", "DQ4ML_SCAN_GRAM_NOLB",
+              "DQ4ML_SCAN_TERM1", "DQ4ML_SCAN_FASTONLY", "DQ4ML_SCAN_ABL", "DQ4ML_SCAN_P10", "DQ4ML_CUT_ABLATE",
+              "DQ4ML_CUT_STAMPS", "DQ4ML_SCAN_STREAM", "DQ4ML_SCAN_NT", "DQ4ML_SCAN_TICKET", "DQ4ML_FUSE_ROUTES")
+
+
+def route_key(plan_key, features_col: str, label_col: str, session):
+    """Replay key of a fused-scan fit: the action's plan structure, the columns, the session conf
+    and the scan knobs (None: not replayable)."""
+    if plan_key is None or os.environ.get("DQ4ML_FUSE_ROUTES", "1") == "0":
+        return None
+    return (plan_key, features_col, label_col, tuple(os.environ.get(k) for k in _ROUTE_ENV),
+            getattr(session, "device", None))
+
+
+def replay(key, plan, session) -> Optional["FusedGram"]:
+    """The remembered route of ``key`` launched over this action's leaf relation, or None."""
+    r = _ROUTES.get(key) if key is not None else None
+    if r is None or r.conf != session.conf._conf:
+        return None
+    from ..sql.plan import CsvScanRelation, Filter, Project
+
+    p = plan
+    while isinstance(p, (Project, Filter)):
+        if p._memo is not None:
+            return None
+        p = p.child
+    if not isinstance(p, CsvScanRelation) or p._memo is not None or p.fused is None or p.fused.get("buf") is None:
+        return None
+    STATS["route_replays"] = STATS.get("route_replays", 0) + 1
+    return r.run(p)
+
+
+def _remember(key, route, session):
+    if key is None:
+        return
+    route.conf = dict(session.conf._conf)
+    if len(_ROUTES) >= 256:
+        _ROUTES.clear()
+    _ROUTES[key] = route
+
+
+def _run_line_gram(cp, chain, p, d) -> "FusedGram":
     extra = {}
     # on the compute stream, after the previous action's fit tail: the one-workgroup solve
     # kernel co-running with a whole-GPU scan gets ~1/8 of a CU's issue slots (22 -> 727 us,

@@ -54,6 +54,10 @@ class PinnedFile:
         self.type_hints = {}  # (lo, hi, sep) -> column type codes of the last device scan
         self.scan_facts = {}  # (lo, hi, sep, opts, user types) -> types / nulls / line count (ops/scanfuse)
         self.host = torch.empty(nbytes, dtype=torch.uint8).pin_memory()
+
+    def live(self) -> bool:
+        """Still the cache's entry (not evicted, not superseded by a changed file, not cleared)."""
+        return _live(self, _cache)
         self.data = self.host.numpy()
         fd = os.open(path, os.O_RDONLY)
         try:
@@ -114,6 +118,11 @@ def device_bytes_allowed(nbytes: int, device=None) -> bool:
     return _held(None if device is None else torch.device(device)) + nbytes <= device_cap_bytes(device)
 
 
+def _live(entry, table) -> bool:
+    with _lock:
+        return any(v is entry for v in table.values())
+
+
 class MappedFile:
     """A byte range too large for the pinned host cache: a read-only map of the file, plus the same
     per-range facts a ``PinnedFile`` keeps (the device scan's type hints and scan facts) and its
@@ -129,6 +138,9 @@ class MappedFile:
         self._dev = {}
         self.type_hints = {}
         self.scan_facts = {}
+
+    def live(self) -> bool:
+        return _live(self, _mapped)
 
     def device_bytes(self, device, lo: int = 0, hi: int = -1, chunk_bytes: int = 1 << 30) -> torch.Tensor:
         hi = self.nbytes if hi < 0 else hi

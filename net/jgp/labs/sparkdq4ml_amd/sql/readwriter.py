@@ -31,6 +31,12 @@ from .types import (BooleanType, DecimalType, DoubleType, IntegerType, LongType,
 
 __all__ = ["DataFrameReader", "DataFrameWriter", "csv_code_to_type"]
 
+# load() of an unchanged cached CSV file: key -> (lazy relation template, file identity, cache entry)
+_LOADS: dict = {}
+_LOAD_SERIAL = __import__("itertools").count(1)
+_LOAD_CONF = ("dq4ml.csv.deviceThresholdBytes", "dq4ml.csv.deviceCache", "dq4ml.csv.fuseScan", "dq4ml.chunkBytes",
+              "dq4ml.csv.streamThresholdBytes", "dq4ml.shardInput")
+
 log = get_logger("io")
 
 _CODE2TYPE = {1: IntegerType, 2: LongType, 3: lambda: DecimalType(38, 0), 4: DoubleType, 5: BooleanType,
@@ -163,9 +169,25 @@ class DataFrameReader:
         paths = path if isinstance(path, (list, tuple)) else [path]
         files = _expand(paths)
         if self._format == "csv":
+            mk = self._load_key(files)
+            hit = _LOADS.get(mk[0]) if mk is not None else None
+            if hit is not None and hit[1] == mk[1] and hit[2] is not None and hit[2].live():
+                # the same unchanged bytes with the same options: this action's own (unscanned)
+                # copy of the lazy relation the first load built -- the device scan still runs
+                # at the action (sql/skey.py)
+                return DataFrame(hit[0].fresh(), self._session)
+            self._last_pf = None
             table = self._read_csv(files)
             if not isinstance(table, Table):  # a lazily scanned relation (sql.plan.CsvScanRelation)
                 table.label = f"Relation[csv] {','.join(paths)}"
+                pf = self._last_pf
+                if mk is not None and pf is not None and table.fused is not None and table.fused.get("buf") is not None:
+                    from .skey import intern
+
+                    table._skey = intern(("csv", next(_LOAD_SERIAL)))
+                    if len(_LOADS) >= 64:
+                        _LOADS.clear()
+                    _LOADS[mk[0]] = (table.fresh(), mk[1], pf)
                 return DataFrame(table, self._session)
         elif self._format == "parquet":
             table = self._read_parquet(files)
@@ -174,6 +196,25 @@ class DataFrameReader:
         else:
             raise ValueError(f"Failed to find data source: {self._format}")
         return DataFrame(LocalRelation(table, f"Relation[{self._format}] {','.join(paths)}"), self._session)
+
+    def _load_key(self, files):
+        """(key, file identity) of a load that may reuse an earlier lazy relation: one CSV file on
+        one GPU (a sharded read is collective: every rank must take the same path, so no rank
+        may skip it), keyed by path, reader options, user schema and the reader's conf."""
+        from ..parallel import comm
+
+        dev = self._session.device
+        if len(files) != 1 or dev.type != "cuda" or comm.world_size() > 1:
+            return None
+        try:
+            st = os.stat(files[0])
+        except OSError:
+            return None
+        conf = self._session.conf
+        ck = tuple(conf.get(k, None) for k in _LOAD_CONF)
+        sch = self._schema.simpleString() if self._schema else None
+        key = (os.path.realpath(files[0]), tuple(sorted(self._options.items())), sch, ck, str(dev))
+        return key, (st.st_size, st.st_mtime_ns, st.st_ino)
 
     def csv(self, path, schema=None, sep=None, header=None, inferSchema=None, **kw):
         if schema is not None:
@@ -224,6 +265,7 @@ class DataFrameReader:
         else:
             pf = None
             data = b"".join(self._read_bytes(f) for f in files)
+        self._last_pf = pf
         return self._read_csv_data(data, o, dev, thresh, pinned, pf, presharded)
 
     def _read_csv_data(self, data, o, dev, thresh, pinned=None, pf=None, presharded=False):

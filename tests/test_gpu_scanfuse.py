@@ -233,3 +233,44 @@ def test_fused_scan_reader_options(tmp_path, case):
     fast = d2._plan.fused["fast_only"]
     assert fast == (case in ("header", "user_schema", "nulls_fast"))
     spark.stop()
+
+
+def test_rebuilt_action_replays_the_lowered_fit(tmp_path, monkeypatch):
+    """an action that rebuilds the lab chain over the same unchanged file reuses the
+    first action's analysis and lowered kernel (sql/skey.py, scanfuse._Route) -- the kernel still
+    runs every action, results bit-identical to the full path -- and a rewritten file is re-read."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from bench_csv_pipeline import synth_csv
+
+    p = str(tmp_path / "lab.csv")
+    synth_csv(p, 200000)
+    spark = _session()
+
+    def fit():
+        _, df = _chain(spark, p)
+        df = VectorAssembler().setInputCols(["guest"]).setOutputCol("features").transform(df)
+        return LinearRegression().setMaxIter(40).setRegParam(1).setElasticNetParam(1).fit(df)
+
+    fit()  # eager first read (facts)
+    m_full = fit()  # lazy relation, lowered and remembered
+    grams, replays = scanfuse.STATS["fused_grams"], scanfuse.STATS.get("route_replays", 0)
+    ms = [fit() for _ in range(3)]
+    assert scanfuse.STATS["fused_grams"] == grams + 3  # the fused kernel ran for every action
+    assert scanfuse.STATS.get("route_replays", 0) == replays + 3
+    for m in ms:
+        assert np.array_equal(m.coefficients.toArray(), m_full.coefficients.toArray())
+        assert float(m.intercept) == float(m_full.intercept)
+    monkeypatch.setenv("DQ4ML_FUSE_ROUTES", "0")
+    m_off = fit()
+    assert np.array_equal(m_off.coefficients.toArray(), m_full.coefficients.toArray())
+    monkeypatch.delenv("DQ4ML_FUSE_ROUTES")
+    # the file changes: its identity changes, nothing stale is replayed
+    import time
+
+    time.sleep(0.01)
+    synth_csv(p, 150000)
+    fit()
+    m_new = fit()
+    assert m_new.summary.numInstances != m_full.summary.numInstances
+    spark.stop()
