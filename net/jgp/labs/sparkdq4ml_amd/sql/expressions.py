@@ -83,12 +83,11 @@ class Expr:
 
 
 def to_expr(v) -> Expr:
-    from .column import Column
-
     if isinstance(v, Expr):
         return v
-    if isinstance(v, Column):
-        return v._expr
+    e = getattr(v, "_expr", None)  # a Column
+    if isinstance(e, Expr):
+        return e
     return Lit(v)
 
 

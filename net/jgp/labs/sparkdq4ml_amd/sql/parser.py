@@ -326,14 +326,44 @@ def parse_select_item(text: str) -> Expr:
     return e
 
 
+_BOUND: dict = {}  # (statement, view plan skey) -> analyzed [Filter?, Project, Limit?] templates
+
+
 def _bind_query(syntax, text: str, session):
     """The plan of a parsed SELECT over the session's CURRENT view of its FROM name (a temp view
     replaced between two runs of the same text binds to the new plan).  Expression trees are
-    immutable once parsed, so plans may share them."""
+    immutable once parsed, so plans may share them; a statement bound over a view of the same
+    structure (sql/skey.py) reuses the analyzed nodes (fresh copies: no result is shared)."""
     items, tname, where, limit = syntax
     plan = session.catalog._views.get(tname.lower())
     if plan is None:
         raise AnalysisException(f"Table or view not found: {tname}; line 1 pos {text.lower().find(tname.lower())}")
+    vk = plan.skey()
+    key = (text, vk) if vk is not None else None
+    tmpl = _BOUND.get(key) if key is not None else None
+    if tmpl is not None:
+        for t in tmpl:
+            plan = t.fresh(plan)
+        return plan
+    out = _bind_new(items, where, limit, plan)
+    if key is not None and out.skey() is not None:
+        nodes, p = [], out
+        while p is not plan:
+            nodes.append(p)
+            p = p.child
+        tmpl = []
+        for n in reversed(nodes):  # bottom-up, detached from the lineage
+            n.schema()
+            t = n.fresh()
+            t.child = None
+            tmpl.append(t)
+        if len(_BOUND) >= 1024:
+            _BOUND.clear()
+        _BOUND[key] = tmpl
+    return out
+
+
+def _bind_new(items, where, limit, plan):
     if where is not None:
         plan = Filter(plan, where)
     exprs = []

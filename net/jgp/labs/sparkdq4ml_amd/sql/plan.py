@@ -278,6 +278,13 @@ class Limit(LogicalPlan):
     def children(self):
         return [self.child]
 
+    def skey(self):
+        k = self._skey
+        if k == 0:
+            ck = self.child.skey()
+            k = self._skey = intern(("Limit", ck, self.n)) if ck is not None else None
+        return k
+
     def schema(self):
         return self.child.schema()
 
