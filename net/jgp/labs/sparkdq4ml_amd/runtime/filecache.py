@@ -54,10 +54,6 @@ class PinnedFile:
         self.type_hints = {}  # (lo, hi, sep) -> column type codes of the last device scan
         self.scan_facts = {}  # (lo, hi, sep, opts, user types) -> types / nulls / line count (ops/scanfuse)
         self.host = torch.empty(nbytes, dtype=torch.uint8).pin_memory()
-
-    def live(self) -> bool:
-        """Still the cache's entry (not evicted, not superseded by a changed file, not cleared)."""
-        return _live(self, _cache)
         self.data = self.host.numpy()
         fd = os.open(path, os.O_RDONLY)
         try:
@@ -76,6 +72,9 @@ class PinnedFile:
         finally:
             os.close(fd)
 
+    def live(self) -> bool:
+        """Still the cache's entry (not evicted, not superseded by a changed file, not cleared)."""
+        return _live(self, _cache)
 
     def device_bytes(self, device, lo: int = 0, hi: int = -1) -> torch.Tensor:
         """The bytes [lo, hi) resident in HBM (one async DMA on first use, then reused)."""
