@@ -24,10 +24,10 @@ for s in $STEPS; do
     t) step t 600 python -u -m pytest ${TESTS} -m gpu -v --maxfail=5 --timeout 120 --timeout-method thread ;;
     widetests) step widetests 600 python -m pytest tests/test_gpu_wide.py -m gpu -q --maxfail=5 ;;
     wide16) step wide16 600 env N=2e6 D=1024 EB=16 python scripts/wide_bench.py ;;
-    wide8) step wide8 900 env N=1e7 D=4096 EB=8 VARIANTS="${VARIANTS:-4:morton:4}" python scripts/wide_bench.py ;;
-    wide16b) step wide16b 900 env N=4e6 D=4096 EB=16 VARIANTS="${VARIANTS:-4:morton:4}" python scripts/wide_bench.py ;;
+    wide8) step wide8 900 env N=1e7 D=4096 EB=8 VARIANTS="${VARIANTS:-5:morton:8:gang}" python scripts/wide_bench.py ;;
+    wide16b) step wide16b 900 env N=4e6 D=4096 EB=16 VARIANTS="${VARIANTS:-5:morton:8:gang}" python scripts/wide_bench.py ;;
     wideprof) (export TMPDIR=/tmp N=2e6 D=4096 EB=8 REPS=3; step wideprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/wideprof -o run --output-format csv -- python scripts/wide_bench.py) || exit $? ;;
-    widepmc) (export TMPDIR=/tmp N=${N:-1e6} D=4096 EB=${EB:-8} REPS=${REPS:-2} VARIANTS="${VARIANTS:-4:morton:4}"
+    widepmc) (export TMPDIR=/tmp N=${N:-1e6} D=4096 EB=${EB:-8} REPS=${REPS:-2} VARIANTS="${VARIANTS:-5:morton:8:gang}"
        step widepmc1 600 rocprofv3 --kernel-trace --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE -d gpurun_out/widepmc1 -o run --output-format csv -- python scripts/wide_bench.py &&
        step widepmc2 600 rocprofv3 --kernel-trace --pmc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum -d gpurun_out/widepmc2 -o run --output-format csv -- python scripts/wide_bench.py) || exit $? ;;
     cfg4) step cfg4 900 python benchmarks/bench_dq_pipeline.py --steps ${CFG4_STEPS:-5} --warmup 2 --json-out gpurun_out/cfg4.json ;;

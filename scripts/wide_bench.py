@@ -34,7 +34,7 @@ T = TiledWide(buf, d, n, eb, scale if eb == 8 else None)
 y = torch.randn(n, generator=g, device="cuda")
 comp = "fp8" if eb == 8 else "bf16"
 # A/B variants interleaved in one process: "ring:order:waves" (env DQ4ML_WIDE_RING/_ORDER/_WAVES)
-variants = os.environ.get("VARIANTS", "4:morton:4").split(",")
+variants = os.environ.get("VARIANTS", "5:morton:8:gang").split(",")
 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 res = {v: [] for v in variants}
 outs = {}
