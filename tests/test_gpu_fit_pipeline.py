@@ -73,3 +73,35 @@ def test_fit_replay_equals_full_path_and_invalidates(gpu_session, monkeypatch):
     finally:
         gpu_session.conf.set("dq4ml.fit.overlapTail", "true")
         gpu_session.conf.set("dq4ml.fit.async", "false")
+
+
+def test_pipelined_first_fit_of_a_fresh_lazy_assembly(gpu_session, monkeypatch):
+    """the first fit of a lazily assembled bf16 matrix materializes it on the CALLER's
+    stream and the replays on the other pipeline stream wait for the recorded operands -- the
+    pipelined fits of a fresh assembly equal the serial fit bit for bit."""
+    from net.jgp.labs.sparkdq4ml_amd import LinearRegression, VectorAssembler
+
+    n, d = 500_003, 24
+    g = torch.Generator(device="cuda").manual_seed(21)
+    cols = {f"f{i}": torch.randn(n, generator=g, device="cuda") for i in range(d)}
+    cols["label"] = sum((0.1 * i - 1.0) * cols[f"f{i}"] for i in range(d)) + 0.5
+
+    def frame():
+        df = gpu_session.createDataFrame(dict(cols))
+        return VectorAssembler(inputCols=[f"f{i}" for i in range(d)], outputCol="features",
+                               outputDtype="bfloat16").transform(df)
+
+    lr = LinearRegression(solver="normal", gramDtype="bf16")
+    gpu_session.conf.set("dq4ml.fit.async", "true")
+    try:
+        monkeypatch.setenv("DQ4ML_FIT_PIPELINE", "1")
+        ref = lr.fit(frame())
+        ref_coef = ref.coefficients.toArray()
+        monkeypatch.setenv("DQ4ML_FIT_PIPELINE", "2")
+        df = frame()  # fresh: nothing materialized yet
+        ms = [lr.fit(df) for _ in range(5)]
+        for m in ms:
+            np.testing.assert_array_equal(m.coefficients.toArray(), ref_coef)
+            assert m.intercept == ref.intercept
+    finally:
+        gpu_session.conf.set("dq4ml.fit.async", "false")
