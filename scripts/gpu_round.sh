@@ -31,9 +31,9 @@ for s in $STEPS; do
        step widepmc1 600 rocprofv3 --kernel-trace --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE -d gpurun_out/widepmc1 -o run --output-format csv -- python scripts/wide_bench.py &&
        step widepmc2 600 rocprofv3 --kernel-trace --pmc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum -d gpurun_out/widepmc2 -o run --output-format csv -- python scripts/wide_bench.py) || exit $? ;;
     cfg4) step cfg4 900 python benchmarks/bench_dq_pipeline.py --steps ${CFG4_STEPS:-5} --warmup 2 --json-out gpurun_out/cfg4.json ;;
-    cfg4csv) step cfg4csv 1000 python benchmarks/bench_csv_pipeline.py --features 64 --rows 1.25e8 --steps 5 --warmup 1 --json-out gpurun_out/cfg4csv.json &&
-             (export TMPDIR=/tmp; step cfg4csvprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/cfg4csvprof -o run --output-format csv -- python benchmarks/bench_csv_pipeline.py --features 64 --rows 1.25e8 --steps 3 --warmup 1) &&
-             step cfg4csvstream 900 env DQ4ML_FILECACHE_DEVICE_BYTES=1 python benchmarks/bench_csv_pipeline.py --features 64 --rows 1.25e8 --steps 2 --warmup 1 --json-out gpurun_out/cfg4csvstream.json || exit $? ;;
+    cfg4csv) step cfg4csv 1000 python benchmarks/bench_csv_pipeline.py --features 64 --rows 1.25e8 --steps 5 --warmup 2 --json-out gpurun_out/cfg4csv.json &&
+             (export TMPDIR=/tmp; step cfg4csvprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/cfg4csvprof -o run --output-format csv -- python benchmarks/bench_csv_pipeline.py --features 64 --rows 1.25e8 --steps 3 --warmup 2) &&
+             step cfg4csvstream 900 env DQ4ML_FILECACHE_DEVICE_BYTES=1 python benchmarks/bench_csv_pipeline.py --features 64 --rows 1.25e8 --steps 2 --warmup 2 --json-out gpurun_out/cfg4csvstream.json || exit $? ;;
     cfg4csvhost) step cfg4csvhost 900 env DQ4ML_BENCH_CPROFILE=gpurun_out/cfg4csv.prof python benchmarks/bench_csv_pipeline.py --features 64 --rows 1.25e8 --steps 3 --warmup 1 --json-out gpurun_out/cfg4csvhost.json &&
              step cfg4csvhost_txt 120 python -c "import pstats; pstats.Stats('gpurun_out/cfg4csv.prof').sort_stats('cumulative').print_stats(60)" ;;
     cfg4prof) step cfg4prof 900 env DQ4ML_BENCH_CPROFILE=gpurun_out/cfg4.prof python benchmarks/bench_dq_pipeline.py --steps 10 --warmup 2 ;;
