@@ -20,7 +20,8 @@ void csv_line_ends(const uint8_t* buf, int64_t n, int64_t* counts, void* ends, h
 // dcols: [2 * ncols] int64 — ncols device pointers to nlines values each, then ncols storage
 // kinds (0 f64, 1 int32, 2 int64, 3 bool/uint8); valid: [ncols, nlines]; stats (zeroed):
 // [slow flag, empty lines, null fields per column (ncols), class masks per column (ncols),
-// lines with a field outside the numeric fast path]
+// lines with a field outside the numeric fast path, lines with a field that is not even a quoted
+// fast-path number ("12.5")]
 // o: dialect (csv_parse_dev.h).  o.strict: the kinds are the user schema's types and a field that
 // does not convert makes its record malformed (all fields null)
 void csv_parse(const uint8_t* buf, int64_t n, const void* ends, int64_t nlines, int ncols, const dq4ml_csv::CsvOpts& o,

@@ -191,7 +191,7 @@ __device__ __forceinline__ bool parse_line(PB B, int64_t bias, int64_t n, const 
                                            int64_t li, bool active, int64_t nlines, int ncols, const CsvOpts& o,
                                            const int64_t* __restrict__ dcols, uint8_t* __restrict__ valid,
                                            uint8_t* __restrict__ keep, uint32_t* smask, int* snull, int* sempty,
-                                           int* smiss) {
+                                           int* smiss, int* shard) {
   const bool lane0 = (threadIdx.x & 63) == 0;
   int64_t start = 0, end = 0;
   bool line = false;
@@ -207,7 +207,7 @@ __device__ __forceinline__ bool parse_line(PB B, int64_t bias, int64_t n, const 
   const uint64_t empty = __ballot(active && !line);
   if (lane0 && empty) atomicAdd(sempty, (int)__popcll(empty));
   long long pos = start;
-  bool slow = false, malformed = false, miss = false;
+  bool slow = false, malformed = false, miss = false, hard = false;
   const bool plain = o.null_len == 0 && !o.trim_lead && !o.trim_trail;
   for (int c = 0; c < ncols; ++c) {
     double dv = 0.0;
@@ -217,8 +217,11 @@ __device__ __forceinline__ bool parse_line(PB B, int64_t bias, int64_t n, const 
     if (pos <= end && line) {
       const long long pb = (long long)bias, pe = (long long)end;
       if (!(plain && dq4ml_csv::csv_field_fast(B, pb, pos, pe, o.sep, dv, lv, ty))) {
-        ty = dq4ml_csv::csv_field_general(B, pb, pos, pe, o, dv, lv, slow, big, malformed);
         miss = true;  // a field outside the fast path (a later fused scan then keeps the general parser)
+        if (!(plain && dq4ml_csv::csv_field_fast_quoted(B, pb, pos, pe, o.sep, o.quote, dv, lv, ty))) {
+          ty = dq4ml_csv::csv_field_general(B, pb, pos, pe, o, dv, lv, slow, big, malformed);
+          hard = true;  // not even a quoted fast-path number (the cutter's QUOTED build)
+        }
       }
     }
     const int kind = (int)dcols[ncols + c];
@@ -253,6 +256,8 @@ __device__ __forceinline__ bool parse_line(PB B, int64_t bias, int64_t n, const 
   }
   const uint64_t misses = __ballot(active && line && miss);
   if (lane0 && misses) atomicAdd(smiss, (int)__popcll(misses));
+  const uint64_t hards = __ballot(active && line && hard);
+  if (lane0 && hards) atomicAdd(shard, (int)__popcll(hards));
   // a malformed record: every field null (valid = 0) — the null counts above already cover the
   // fields that failed; the rest are counted here
   const uint64_t bad = __ballot(active && line && malformed);
@@ -281,7 +286,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     unsigned long long* __restrict__ stats) {
   __shared__ uint32_t smask[kMaxCols];
   __shared__ int snull[kMaxCols];
-  __shared__ int sempty, sflag, smiss;
+  __shared__ int sempty, sflag, smiss, shard;
   __shared__ __attribute__((aligned(16))) uint8_t stage[LDS];
   for (int c = threadIdx.x; c < ncols; c += blockDim.x) {
     smask[c] = 0;
@@ -291,6 +296,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     sflag = 0;
     sempty = 0;
     smiss = 0;
+    shard = 0;
   }
   const uint8_t* ab = b - (reinterpret_cast<uintptr_t>(b) & 15);
   const int64_t off = b - ab;
@@ -314,16 +320,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
       }
       __syncthreads();
       slow |= parse_line(stage, glo - off, n, ends, li, li < l1, nlines, ncols, o, dcols, valid, keep, smask,
-                         snull, &sempty, &smiss);
+                         snull, &sempty, &smiss, &shard);
     } else {
       slow |= parse_line(b, 0, n, ends, li, li < l1, nlines, ncols, o, dcols, valid, keep, smask, snull, &sempty,
-                         &smiss);
+                         &smiss, &shard);
     }
   }
   if (slow) sflag = 1;
   __syncthreads();
   // stats: [0] slow flag, [1] empty lines, [2, 2+ncols) null fields, [2+ncols, 2+2*ncols) class masks,
-  // [2+2*ncols] lines with a field outside the numeric fast path
+  // [2+2*ncols] lines with a field outside the numeric fast path, [3+2*ncols] those with a field that
+  // is not even a quoted fast-path number
   for (int c = threadIdx.x; c < ncols; c += blockDim.x) {
     if (snull[c]) atomicAdd(&stats[2 + c], (unsigned long long)snull[c]);
     if (smask[c]) atomicOr(&stats[2 + ncols + c], (unsigned long long)smask[c]);
@@ -332,6 +339,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     if (sempty) atomicAdd(&stats[1], (unsigned long long)sempty);
     if (sflag) atomicOr(&stats[0], 1ull);
     if (smiss) atomicAdd(&stats[2 + 2 * ncols], (unsigned long long)smiss);
+    if (shard) atomicAdd(&stats[3 + 2 * ncols], (unsigned long long)shard);
   }
 }
 

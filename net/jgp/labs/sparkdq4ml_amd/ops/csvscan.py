@@ -187,7 +187,7 @@ def _scan_chunk(h, buf, n: int, trailing: bool, ncols: int, sep: str, dev, hint=
     ptrs = _h2d(np.array([t.data_ptr() for t in dcols] + [k for k, _ in kinds], dtype=np.int64), dev)
     valid = torch.empty(ncols, m, dtype=torch.bool, device=dev)
     keep = torch.empty(m, dtype=torch.bool, device=dev)
-    stats = torch.zeros(3 + 2 * ncols, dtype=torch.int64, device=dev)
+    stats = torch.zeros(4 + 2 * ncols, dtype=torch.int64, device=dev)
     h.csv_parse(buf.data_ptr(), n, ends.data_ptr(), nlines, ncols, ord(sep), ptrs.data_ptr(), valid.data_ptr(),
                 keep.data_ptr(), stats.data_ptr(), stream, **_opt_args(opts))
     # facts for the byte-parallel cutter (ops/scancut.py), read with the stats: the longest line
@@ -278,12 +278,15 @@ def _facts(st: np.ndarray, nc: int, total: int) -> dict:
     from the chunks' parse stats: line count (empty lines included), the columns holding nulls,
     the fast-path / field-count / line-length / terminator facts."""
     nonempty = int(total) - int(st[:, 1].sum())
+    misses, hard = int(st[:, 2 + 2 * nc].sum()), int(st[:, 3 + 2 * nc].sum())
     return {"nlines": int(total), "nullable": [bool(int(st[:, 2 + c].sum())) for c in range(nc)],
-            "fast_only": int(st[:, 2 + 2 * nc].sum()) == 0,
-            "empty_lines": int(st[:, 1].sum()), "max_line": int(st[:, 3 + 2 * nc].max()),
-            "uniform_fields": int(st[:, 4 + 2 * nc].sum()) == nonempty * (nc - 1),
-            "min_line": max(1, int(st[:, 5 + 2 * nc].min())) if len(st) else 1,
-            "term_kinds": [int(st[:, 6 + 2 * nc + k].sum()) for k in range(3)]}
+            "fast_only": misses == 0,
+            # every field off the fast path was a quoted fast-path number: the cutter's QUOTED build
+            "quoted_fast": misses > 0 and hard == 0,
+            "empty_lines": int(st[:, 1].sum()), "max_line": int(st[:, 4 + 2 * nc].max()),
+            "uniform_fields": int(st[:, 5 + 2 * nc].sum()) == nonempty * (nc - 1),
+            "min_line": max(1, int(st[:, 6 + 2 * nc].min())) if len(st) else 1,
+            "term_kinds": [int(st[:, 7 + 2 * nc + k].sum()) for k in range(3)]}
 
 
 def infer_streamed(src, sep: str, ncols: Optional[int] = None, sharded: bool = False, opts: Optional[dict] = None,

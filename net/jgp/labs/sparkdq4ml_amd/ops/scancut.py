@@ -66,7 +66,8 @@ def applicable(f: dict) -> Optional[int]:
         return None
     o = f["opts"]
     sep = o.get("sep", ",")
-    if not f.get("fast_only") or f.get("strict") or any(f["nullable"]) or f.get("empty_lines", 1) != 0:
+    if not (f.get("fast_only") or f.get("quoted_fast")) or f.get("strict") or any(f["nullable"]) \
+            or f.get("empty_lines", 1) != 0:
         return None
     if not f.get("uniform_fields") or len(f["kinds"]) < 1 or any(int(k) not in (0, 1) for k in f["kinds"]):
         return None
@@ -259,9 +260,11 @@ def _mfma_gram(sh, slots):
     return acc_decl, gram_phase, epilogue, tables
 
 
-def _conv_loop(NF, C, CU, PP, FW, crlf, conv_call, frame_load, div_expr, int_ok, us_expr, feat_store):
+def _conv_loop(NF, C, CU, PP, FW, crlf, conv_call, frame_load, div_expr, int_ok, us_expr, feat_store, quote=0):
     """The field-conversion loop: NF fields per lane per iteration (fb + 256 h), their positions
-    prefetched one iteration ahead, every field's frame + sign loads issued before any wait."""
+    prefetched one iteration ahead, every field's frame + sign loads issued before any wait.
+    ``quote`` (QUOTED build: some fields are quoted fast-path numbers, ``"12.5"``): a quoted
+    field's bounds move inside its quotes and its wave takes the position-based converter."""
     cr = 1 if crlf else 0
     L = ["      // (the next iteration's positions are loaded while this one converts)"]
     for h in range(NF):
@@ -293,11 +296,19 @@ def _conv_loop(NF, C, CU, PP, FW, crlf, conv_call, frame_load, div_expr, int_ok,
     fs = feat_store.replace("        const int fs", "            const int fs").replace(
         "        if (fs >= 0)", "            if (fs >= 0)")
     for h in range(NF):
+        if quote:
+            bounds = (f"const int qs_ = q{h}_c0 == {quote}, qe_ = stage[q{h}_end - 1] == {quote};\n"
+                      f"          const bool qany = (qs_ | qe_) != 0;\n"
+                      f"          const int f = q{h}_f, end = q{h}_end - qe_, start = q{h}_start + qs_, len = end - start, "
+                      f"c = q{h}_c, rw = q{h}_rw;")
+        else:
+            bounds = (f"const int f = q{h}_f, end = q{h}_end, start = q{h}_start, len = end - start, c = q{h}_c, "
+                      f"rw = q{h}_rw;")
         L.append(f"""        {{
-          const int f = q{h}_f, end = q{h}_end, start = q{h}_start, len = end - start, c = q{h}_c, rw = q{h}_rw;
+          {bounds}
           const int fsh = q{h}_fsh;
           const unsigned fw0 = q{h}_w0, fw1 = q{h}_w1, fw2 = q{h}_w2;
-          const int c0 = q{h}_c0;
+          const int c0 = {"qany ? stage[start] : " if quote else ""}q{h}_c0;
           const bool neg0 = c0 == '-';
           const int fl = len - ((c0 == '-' || c0 == '+') ? 1 : 0);
           unsigned m = 0u;
@@ -326,7 +337,7 @@ def _conv_loop(NF, C, CU, PP, FW, crlf, conv_call, frame_load, div_expr, int_ok,
 
 
 def kernel_source(g, kinds, used, opts: dict, H: int, slots: dict, d: int, term: int = 13, crlf: bool = False,
-                  min_line: int = 1, waves_per_simd: int = 0, max_line: int = 1 << 30):
+                  min_line: int = 1, waves_per_simd: int = 0, max_line: int = 1 << 30, quoted: bool = False):
     """Source of the cutter kernel and its ``_Shape``.  ``term``: the file's one terminator byte
     (13 CR, 10 LF; ``crlf``: every CR is followed by LF, which then opens the next row and is
     skipped); ``min_line``: the shortest line, sizing the delimiter array and the row tile."""
@@ -392,8 +403,9 @@ def kernel_source(g, kinds, used, opts: dict, H: int, slots: dict, d: int, term:
     pf_late = "      if (R0 == 0 && blk + 1 < w1) dq_fetch(ab, a, n, blk + 1, tid, pg, ph);\n"
     pf_tail = ("    if ((cnt == 0 || " + ("true" if abl & 8 else "false") + ") && blk + 1 < w1) "
                "dq_fetch(ab, a, n, blk + 1, tid, pg, ph);  // no tile round ran\n")
+    qb = int(opts.get("quote", 34)) if quoted else 0
     conv_call = ("ok = true; m = (unsigned)len;" if abl & 1 else
-                 f"""if (__ballot(fl > 8) == 0ull) {{
+                 f"""if (__ballot(fl > 8{" || qany" if qb else ""}) == 0ull) {{
           ok = csv_num_r8s_w(fw0, fw1, fw2, fsh, fl, m, fr, dot);
         }} else {{  // (re-reads its frame: no register array lives across the branch)
           ok = csv_num_r<{FW // 4}>(stage, end, len < {FW} ? len : {FW}, m, fr, neg, dot);
@@ -497,7 +509,8 @@ def kernel_source(g, kinds, used, opts: dict, H: int, slots: dict, d: int, term:
     # window's Gram (reading the row tile, written again only after this window's cut barrier)
     # overlaps this window's staging
     top_sync = ""
-    conv_loop = _conv_loop(NF, C, CU, PP, FW, crlf, conv_call, frame_load, div_expr, int_ok, us_expr, feat_store)
+    conv_loop = _conv_loop(NF, C, CU, PP, FW, crlf, conv_call, frame_load, div_expr, int_ok, us_expr, feat_store,
+                           quote=qb)
     kind_tab = ", ".join(str(int(k)) for k in kinds)
     lb = f"__launch_bounds__(256, {waves_per_simd})" if waves_per_simd else "__launch_bounds__(256)"
     src = ("#define CSV_UDOT4(a, b, c) __builtin_amdgcn_udot4((a), (b), (c), false)\n"
@@ -787,8 +800,9 @@ def _compile(nodes, rel, d: int):
     # (diagnostic builds only: DQ4ML_CUT_ABLATE timing ablations, DQ4ML_CUT_STAMPS phase clocks;
     # the losing A/B alternatives of rounds 2-3 -- VALU powers of ten, early prefetch, slow head
     # scan, 2 fields per lane, top-of-window barrier, other tile sizes -- were removed in round 4)
+    quoted = not f.get("fast_only") and bool(f.get("quoted_fast"))
     key = (parts, udfs, tuple(rel.schema().names), tuple(f["kinds"]), repr(sorted(f["opts"].items())), H, d, term,
-           crlf, min_line, int(f.get("max_line", 1 << 30)), os.environ.get("DQ4ML_CUT_ABLATE"),
+           crlf, min_line, int(f.get("max_line", 1 << 30)), quoted, os.environ.get("DQ4ML_CUT_ABLATE"),
            os.environ.get("DQ4ML_CUT_STAMPS"))
     if key in _CACHE:
         return _CACHE[key]
@@ -801,9 +815,10 @@ def _compile(nodes, rel, d: int):
             ("dbg",) if os.environ.get("DQ4ML_CUT_STAMPS", "0") == "1" else ())
         slots = {k: g.slot(None, (k,)) for k in names}
         ml = int(f.get("max_line", 1 << 30))
-        _, sh = kernel_source(g, f["kinds"], g.used, f["opts"], H, slots, d, term, crlf, min_line, 0, ml)
+        _, sh = kernel_source(g, f["kinds"], g.used, f["opts"], H, slots, d, term, crlf, min_line, 0, ml, quoted)
         per_cu = blocks_per_cu(sh.lds)
-        src, sh = kernel_source(g, f["kinds"], g.used, f["opts"], H, slots, d, term, crlf, min_line, per_cu, ml)
+        src, sh = kernel_source(g, f["kinds"], g.used, f["opts"], H, slots, d, term, crlf, min_line, per_cu, ml,
+                                quoted)
         cp = _CutPlan(src, g, refs, sh, per_cu)
     except (dqvm.Unfusable, _GramNullable):
         cp = None

@@ -386,6 +386,7 @@ class DataFrameReader:
                          "trailing": n > 0 and body[-1] not in (10, 13), "mean_line": n / facts["nlines"],
                          "kinds": [_KIND.get(c, (0,))[0] for c in codes], "nullable": list(facts["nullable"]),
                          "fast_only": bool(facts.get("fast_only")),
+                         "quoted_fast": bool(facts.get("quoted_fast")),
                          "max_line": int(facts.get("max_line", 1 << 30)),
                          "uniform_fields": bool(facts.get("uniform_fields")),
                          "empty_lines": int(facts.get("empty_lines", 1)),
@@ -434,7 +435,8 @@ class DataFrameReader:
         fused = {"buf": None, "stream": src, "n": n, "nlines": facts["nlines"], "device": dev,
                  "trailing": n > 0 and body[-1] not in (10, 13), "mean_line": n / facts["nlines"],
                  "kinds": [_KIND.get(c, (0,))[0] for c in codes], "nullable": list(facts["nullable"]),
-                 "fast_only": bool(facts.get("fast_only")), "max_line": int(facts.get("max_line", 1 << 30)),
+                 "fast_only": bool(facts.get("fast_only")), "quoted_fast": bool(facts.get("quoted_fast")),
+                 "max_line": int(facts.get("max_line", 1 << 30)),
                  "uniform_fields": bool(facts.get("uniform_fields")), "empty_lines": int(facts.get("empty_lines", 1)),
                  "min_line": int(facts.get("min_line", 1)), "term_kinds": list(facts.get("term_kinds") or (1, 1, 0)),
                  "opts": dict(_opt_args(dopts), sep=sep, strict=bool(strict)), "strict": bool(strict)}

@@ -230,3 +230,42 @@ def test_short_rows_route_to_the_per_line_kernel(spark, tmp_path, monkeypatch):
     before = scancut.STATS["cut_grams"]
     fused = regression._fused_scan_stats(LinearRegression(), _lab_df(spark, p))
     assert fused is not None and scancut.STATS["cut_grams"] == before
+
+
+def test_cutter_converts_quoted_numbers(spark, tmp_path):
+    """a wide CSV whose numbers are partly written as ``"1.25"`` keeps the cutter.
+    The eager scan records ``quoted_fast`` (every fast-path miss was a simple quoted number), the
+    QUOTED build strips the quotes in the convert loop, and the Gram equals the unquoted file's."""
+    from net.jgp.labs.sparkdq4ml_amd.ops import scancut
+
+    d, n = 32, 60_001
+    plain, X, y = _write(tmp_path, n, d)
+    lines = open(plain, "rb").read().split(b"\r")
+    out = []
+    for i, ln in enumerate(lines):
+        if not ln:
+            out.append(ln)
+            continue
+        fs = ln.split(b",")
+        out.append(b",".join(b'"' + f + b'"' if (i + j) % 2 == 0 else f for j, f in enumerate(fs)))
+    quoted = str(tmp_path / "q.csv")
+    open(quoted, "wb").write(b"\r".join(out))
+
+    res = {}
+    for name, p in (("plain", plain), ("quoted", quoted)):
+        assert spark.read().format("csv").option("inferSchema", "true").load(p).count() == n  # eager: facts
+        facts = spark.read().format("csv").option("inferSchema", "true").load(p)._plan.fused  # lazy re-read
+        if name == "quoted":
+            assert facts["fast_only"] is False and facts["quoted_fast"] is True
+        before = scancut.STATS["cut_grams"]
+        fused, lr, df = _fit_stats(spark, p, d)
+        assert fused is not None and scancut.STATS["cut_grams"] == before + 1, name
+        res[name] = (fused.flat.cpu().numpy(), lr.fit(df).coefficients.toArray())
+    (g0, c0), (g1, c1) = res["plain"], res["quoted"]
+    # same numbers, same fixed-order folds: the quoted file's Gram is the plain file's
+    assert np.allclose(g1, g0, rtol=1e-12, atol=0)
+    assert np.allclose(c1, c0, rtol=1e-10, atol=1e-12)
+    keep = (y > 0) & (y <= 150.0)
+    ref = _oracle(X, y, keep)
+    absref = _oracle(np.abs(X), np.abs(y), keep)
+    assert np.all(np.abs(g1 - ref) <= 1e-13 * np.maximum(absref, 1.0))

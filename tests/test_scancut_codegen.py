@@ -33,7 +33,7 @@ def test_gram_index_covers_layout_once(d):
             assert f"acc[{scancut._gram_index(i, j, d)}] += gx{i} * gx{j};" in code
 
 
-def _cut_source(spark, d, lab, stamps=False):
+def _cut_source(spark, d, lab, stamps=False, quoted=False):
     import torch
 
     from net.jgp.labs.sparkdq4ml_amd.ops.csvscan import _opt_args
@@ -88,15 +88,18 @@ def _cut_source(spark, d, lab, stamps=False):
     src, sh = scancut.kernel_source(g, kinds, g.used, fused["opts"], H, slots, d, 13, False, fused["min_line"],
                                     scancut.blocks_per_cu(scancut.kernel_source(g, kinds, g.used, fused["opts"], H,
                                                                                 slots, d, 13, False,
-                                                                                fused["min_line"], 0, ml)[1].lds), ml)
+                                                                                fused["min_line"], 0, ml, quoted)[1].lds),
+                                    ml, quoted)
     return src
 
 
-@pytest.mark.parametrize("d,lab,stamps", [(1, True, False), (12, False, False), (40, False, True)])
-def test_cut_kernel_compiles_for_gfx950(cpu_session, tmp_path, monkeypatch, d, lab, stamps):
+@pytest.mark.parametrize("d,lab,stamps,quoted", [(1, True, False, False), (12, False, False, False),
+                                                 (40, False, True, False), (12, False, False, True)])
+def test_cut_kernel_compiles_for_gfx950(cpu_session, tmp_path, monkeypatch, d, lab, stamps, quoted):
     if stamps:  # the diagnostic phase-clock build
         monkeypatch.setenv("DQ4ML_CUT_STAMPS", "1")
-    src = _cut_source(cpu_session, d, lab, stamps)
+    src = _cut_source(cpu_session, d, lab, stamps, quoted)
+    assert ("qany" in src) == quoted  # quoted fast-path numbers: bounds inside the quotes
     assert ("s_memtime" in src) == stamps
     assert f"void {scancut.ENTRY}(" in src
     assert "for (int r = tid; r < nr; r += 256)" in src  # a row tile larger than the block is covered
@@ -121,5 +124,7 @@ def test_cutter_preconditions():
                  ("kinds", [2, 0]), ("max_line", 5000), ("term_kinds", [4, 3, 0]), ("term_kinds", [4, 0, 3])):
         assert scancut.applicable(dict(base, **{k: v})) is None, k
     assert scancut.applicable(dict(base, opts=dict(base["opts"], sep="."))) is None
+    # every off-fast-path field a quoted fast-path number: the QUOTED build takes it
+    assert scancut.applicable(dict(base, fast_only=False, quoted_fast=True)) == 512
     assert scancut.term_of(dict(base, term_kinds=[0, 9, 0])) == (10, False)
     assert scancut.term_of(dict(base, term_kinds=[9, 0, 9])) == (13, True)
