@@ -18,8 +18,10 @@ int64_t csv_count_blocks(int64_t n);
 bool csv_ends_i32(int64_t n);
 void csv_line_ends(const uint8_t* buf, int64_t n, int64_t* counts, void* ends, hipStream_t st);
 // dcols: [2 * ncols] int64 — ncols device pointers to nlines values each, then ncols storage
-// kinds (0 f64, 1 int32, 2 int64, 3 bool/uint8); valid: [ncols, nlines]; stats (zeroed):
-// [slow flag, empty lines, null fields per column (ncols), class masks per column (ncols),
+// kinds (0 f64, 1 int32, 2 int64, 3 bool/uint8, 4 string span: int64 (fs << 25) | (raw << 24) | len,
+// fs the field's first byte in buf, see csv_field_span); valid: [ncols, nlines]; stats (zeroed):
+// [slow flag, empty lines, null fields per column (ncols), class masks per column (ncols; bit 7:
+// a field whose value or class needs the host -- harmless when the column is a string),
 // lines with a field outside the numeric fast path, lines with a field that is not even a quoted
 // fast-path number ("12.5")]
 // o: dialect (csv_parse_dev.h).  o.strict: the kinds are the user schema's types and a field that

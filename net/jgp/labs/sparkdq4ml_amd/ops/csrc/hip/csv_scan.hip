@@ -214,18 +214,47 @@ __device__ __forceinline__ bool parse_line(PB B, int64_t bias, int64_t n, const 
     long long lv = 0;
     bool big = false;
     int ty = CT_NULL;
+    const int kind = (int)dcols[ncols + c];
+    if (kind == 4) {
+      // a string column: its field's span (no conversion); the host builds the text when the
+      // column is materialized (ops/csvscan.py DeviceStrings)
+      long long fs = 0, fe = 0;
+      bool raw = false;
+      if (pos <= end && line) {
+        const bool is_null = dq4ml_csv::csv_field_span(B, (long long)bias, pos, (long long)end, o, fs, fe, raw);
+        ty = is_null ? CT_NULL : CT_STRING;
+        slow |= fe - fs >= (1ll << 24) || fs >= (1ll << 38);
+        miss = hard = true;
+      }
+      if (active) {
+        reinterpret_cast<int64_t*>(reinterpret_cast<void*>(dcols[c]))[li] =
+            (fs << 25) | ((long long)raw << 24) | ((fe - fs) & 0xFFFFFF);
+        valid[(int64_t)c * nlines + li] = ty == CT_STRING;
+      }
+      uint32_t bit = line ? (1u << ty) : 0u;
+#pragma unroll
+      for (int oo = 1; oo < 64; oo <<= 1) bit |= (uint32_t)__shfl_xor((int)bit, oo, 64);
+      const uint64_t nulls = __ballot(line && ty != CT_STRING);
+      if (lane0) {
+        if (bit) atomicOr(&smask[c], bit);
+        if (nulls) atomicAdd(&snull[c], (int)__popcll(nulls));
+      }
+      continue;
+    }
+    // fslow: this field's value (or class) needs the host -- flagged per column (class-mask bit
+    // 7): it only matters when the column does not come out a string
+    bool fslow = false;
     if (pos <= end && line) {
       const long long pb = (long long)bias, pe = (long long)end;
       if (!(plain && dq4ml_csv::csv_field_fast(B, pb, pos, pe, o.sep, dv, lv, ty))) {
         miss = true;  // a field outside the fast path (a later fused scan then keeps the general parser)
         if (!(plain && dq4ml_csv::csv_field_fast_quoted(B, pb, pos, pe, o.sep, o.quote, dv, lv, ty))) {
-          ty = dq4ml_csv::csv_field_general(B, pb, pos, pe, o, dv, lv, slow, big, malformed);
+          ty = dq4ml_csv::csv_field_general(B, pb, pos, pe, o, dv, lv, fslow, big, malformed);
           hard = true;  // not even a quoted fast-path number (the cutter's QUOTED build)
         }
       }
     }
-    const int kind = (int)dcols[ncols + c];
-    slow |= big && kind != 2;  // an f64 plane would round it; an int64 store of lv is exact
+    fslow |= big && kind != 2;  // an f64 plane would round it; an int64 store of lv is exact
     bool ok = ty != CT_NULL && ty != CT_STRING;
     if (o.strict && ty != CT_NULL && !dq4ml_csv::csv_conforms(ty, kind)) {
       malformed = true;  // a value the user schema's type does not accept
@@ -245,7 +274,7 @@ __device__ __forceinline__ bool parse_line(PB B, int64_t bias, int64_t n, const 
       }
       valid[(int64_t)c * nlines + li] = ok;
     }
-    uint32_t bit = line ? (1u << ty) : 0u;
+    uint32_t bit = line ? ((1u << ty) | (fslow ? 0x80u : 0u)) : 0u;
 #pragma unroll
     for (int oo = 1; oo < 64; oo <<= 1) bit |= (uint32_t)__shfl_xor((int)bit, oo, 64);
     const uint64_t nulls = __ballot(line && !ok);
@@ -328,7 +357,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   }
   if (slow) sflag = 1;
   __syncthreads();
-  // stats: [0] slow flag, [1] empty lines, [2, 2+ncols) null fields, [2+ncols, 2+2*ncols) class masks,
+  // stats: [0] slow flag, [1] empty lines, [2, 2+ncols) null fields, [2+ncols, 2+2*ncols) class masks
+  // (bit 7: a field whose value or class needs the host),
   // [2+2*ncols] lines with a field outside the numeric fast path, [3+2*ncols] those with a field that
   // is not even a quoted fast-path number
   for (int c = threadIdx.x; c < ncols; c += blockDim.x) {

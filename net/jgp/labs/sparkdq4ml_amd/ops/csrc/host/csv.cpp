@@ -126,6 +126,12 @@ void split_record(const char* p, size_t n, const CsvOptions& o, std::vector<Fiel
 
 }  // namespace
 
+void csv_field_text(const char* p, size_t n, const CsvOptions& o, std::string& out) {
+  std::vector<Field> f;
+  split_record(p, n, o, f);
+  out.swap(f[0].text);
+}
+
 int csv_infer_field(const char* s, size_t n) {
   if (n == 0) return T_NULL;
   int64_t iv;

@@ -48,6 +48,11 @@ struct CsvTable {
 CsvTable csv_scan(const char* data, size_t len, const CsvOptions& opt, const std::vector<int>& user_types,
                   const std::vector<std::string>& user_names);
 
+// Text of one field whose bytes [p, p + n) the device scanner cut (csrc/hip/csv_parse_dev.h
+// csv_field_span): the first field split_record yields from them, trims applied.
+void csv_field_text(const char* p, size_t n, const CsvOptions& o, std::string& out);
+
+
 // Lattice helpers shared with tests.
 int csv_infer_field(const char* s, size_t n);
 int csv_merge_types(int a, int b);

@@ -104,6 +104,58 @@ PYBIND11_MODULE(_dq4ml_host, m) {
   m.def("csv_infer_field", [](const std::string& s) { return csv_infer_field(s.data(), s.size()); });
   m.def("csv_merge_types", &csv_merge_types);
 
+  // Python strings of a device string column (ops/csvscan.py DeviceStrings), None where not valid:
+  // spans are the device scanner's packed (fs << 25) | (raw << 24) | len into data; a raw field
+  // (quoted, or holding the escape byte) goes through csv_field_text, the others are their bytes
+  // (trimmed when a trim option is set).  Same text and UTF-8 decoding as csv_scan's columns.
+  m.def(
+      "csv_strings",
+      [](py::buffer data, py::array_t<int64_t, py::array::c_style> spans, py::array_t<uint8_t, py::array::c_style> valid,
+         std::string quote, std::string escape, bool ilws, bool itws) {
+        py::buffer_info bi = data.request();
+        const char* base = static_cast<const char*>(bi.ptr);
+        const int64_t nb = bi.size * bi.itemsize;
+        const int64_t n = spans.size();
+        if (valid.size() != n) throw std::invalid_argument("csv_strings: spans / valid length mismatch");
+        CsvOptions o;
+        o.quote = quote.empty() ? '\0' : quote[0];
+        o.escape = escape.empty() ? '\\' : escape[0];
+        o.sep = '\0';  // the span holds one field: no separator outside its quotes
+        o.ignore_leading_ws = ilws;
+        o.ignore_trailing_ws = itws;
+        o.null_value = std::string("\xff\xfe", 2);  // never null here: nulls come from valid
+        const int64_t* sp = spans.data();
+        const uint8_t* vp = valid.data();
+        py::list out(n);
+        std::string t;
+        for (int64_t i = 0; i < n; ++i) {
+          if (!vp[i]) {
+            out[i] = py::none();
+            continue;
+          }
+          const int64_t fs = sp[i] >> 25, len = sp[i] & 0xFFFFFF;
+          if (fs < 0 || fs + len > nb) throw std::out_of_range("csv_strings: span outside the data");
+          const char* p = base + fs;
+          size_t a = 0, e = (size_t)len;
+          if ((sp[i] >> 24) & 1) {
+            csv_field_text(p, (size_t)len, o, t);
+            p = t.data();
+            e = t.size();
+          } else {
+            if (ilws)
+              while (a < e && (p[a] == ' ' || p[a] == '\t')) ++a;
+            if (itws)
+              while (e > a && (p[e - 1] == ' ' || p[e - 1] == '\t')) --e;
+          }
+          PyObject* s = PyUnicode_DecodeUTF8(p + a, (Py_ssize_t)(e - a), nullptr);
+          if (!s) throw py::error_already_set();
+          out[i] = py::reinterpret_steal<py::object>(s);
+        }
+        return out;
+      },
+      py::arg("data"), py::arg("spans"), py::arg("valid"), py::arg("quote") = "\"", py::arg("escape") = "\\",
+      py::arg("ignore_leading_ws") = false, py::arg("ignore_trailing_ws") = false);
+
   m.def(
       "csv_scan",
       [](py::bytes data, std::string sep, std::string quote, std::string escape, bool header, bool infer,

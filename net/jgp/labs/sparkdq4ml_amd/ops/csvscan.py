@@ -1,8 +1,11 @@
 """Device CSV scan driver (K1/K2, csrc/hip/csv_scan.hip).
 
 ``scan_device(data, ...)`` returns a :class:`Table` of typed device columns, or ``None`` when the
-input needs the general host scanner (quotes/escapes, string or boolean-mixed columns, integers
-beyond int64, decimals outside the exactly-rounded fast path, non-inferred schemas).  The type
+input needs the general host scanner (integers beyond int64, decimals outside the exactly-rounded
+fast path, a quoted field whose class only the host tokenizer can tell in a non-string column).
+String columns stay on the device as field spans into the input bytes (``csv_scan.h`` kind 4):
+:class:`~..sql.table.DeviceStringColumn` builds their Python strings (host C++ ``csv_strings``)
+only when a consumer reads them.  The type
 lattice masks are merged across data-parallel ranks with an all-reduce (X3) when the file is
 sharded by byte range (:func:`shard_byte_range`)."""
 from __future__ import annotations
@@ -23,7 +26,7 @@ STATS = {"device_scans": 0, "fallbacks": 0, "chunks": 0}
 
 def merge_type_mask(mask: int) -> int:
     """Tightest common type of the classes present in ``mask`` (bit i = class i seen)."""
-    m = int(mask) & ~1  # nulls merge into anything
+    m = int(mask) & 0x7E  # nulls merge into anything (bit 7 is the needs-the-host flag)
     if m == 0:
         return CT_STRING  # all-null column -> string (Spark: NullType -> StringType)
     if m & (1 << CT_STRING):
@@ -151,7 +154,8 @@ def _ncols_of(data, sep: str, comment: int = 0, quote: int = 34, escape: int = 9
         w *= 16
 
 
-_KIND = {CT_INT: (1, torch.int32), CT_LONG: (2, torch.int64), CT_BOOL: (3, torch.bool)}
+_KIND = {CT_INT: (1, torch.int32), CT_LONG: (2, torch.int64), CT_BOOL: (3, torch.bool), CT_STRING: (4, torch.int64)}
+SLOW_BIT = 0x80  # class-mask bit: a field whose value or class the device could not settle
 
 
 def _opt_args(opts):
@@ -161,10 +165,11 @@ def _opt_args(opts):
                 null_value=o.get("null_value", ""), strict=bool(o.get("strict", False)))
 
 
-def _scan_chunk(h, buf, n: int, trailing: bool, ncols: int, sep: str, dev, hint=None, opts=None):
+def _scan_chunk(h, buf, n: int, trailing: bool, ncols: int, sep: str, dev, hint=None, opts=None, base: int = 0):
     """K1 (line ends) + K2 (parse, type masks, null / empty-line counts) over one device byte
-    buffer; no host sync except the line count.  Returns (nlines, per-column f64 planes, valid
-    [ncols, m], keep [m], stats) — stats as documented at ``csv_parse`` (csv_scan.h)."""
+    buffer; no host sync except the line count.  Returns (nlines, per-column planes, valid
+    [ncols, m], keep [m], stats, base) — stats as documented at ``csv_parse`` (csv_scan.h); ``base``:
+    the chunk's offset in the scanned bytes (string spans are relative to the chunk)."""
     from .device import _h2d
 
     stream = torch.cuda.current_stream(dev).cuda_stream
@@ -213,13 +218,15 @@ def _scan_chunk(h, buf, n: int, trailing: bool, ncols: int, sep: str, dev, hint=
     else:
         kinds = torch.zeros(3, dtype=torch.int64, device=dev)
     stats = torch.cat([stats, maxl, nsep.to(torch.int64), minl, kinds.to(torch.int64)])
-    return nlines, dcols, valid, keep, stats
+    return nlines, dcols, valid, keep, stats, base
 
 
 def type_code_of(dt) -> int:
     """Lattice code of a device-scanned column's type (the reader's types_hint)."""
-    from ..sql.types import BooleanType, IntegerType, LongType
+    from ..sql.types import BooleanType, IntegerType, LongType, StringType
 
+    if isinstance(dt, StringType):
+        return CT_STRING
     if isinstance(dt, IntegerType):
         return CT_INT
     if isinstance(dt, LongType):
@@ -229,20 +236,32 @@ def type_code_of(dt) -> int:
     return CT_DOUBLE
 
 
-def _finish(parts, types, st, dev, hinted=False):
+def _finish(parts, types, st, dev, hinted=False, data=None, opts=None):
     """Typed columns from per-chunk parse outputs under the merged types.  ``st``: the chunks'
     stats on the host.  Int / long / boolean values convert exactly from their f64 planes (the
-    parser flags integers beyond 2^53 for the host path)."""
+    parser flags integers beyond 2^53 for the host path).  String columns (scanned as spans, always
+    hinted) become :class:`DeviceStringColumn` over ``data``, the scanned bytes."""
     from ..sql.localdata import ColumnData
-    from ..sql.table import Table
-    from ..sql.types import (BooleanType, DoubleType, IntegerType, LongType, StructField, StructType)
+    from ..sql.table import DeviceStringColumn, Table
+    from ..sql.types import (BooleanType, DoubleType, IntegerType, LongType, StringType, StructField, StructType)
 
     fields, cols = [], []
     total = sum(p[0] for p in parts)
     live = [(k, p) for k, p in enumerate(parts) if p[0]]
     for c, t in enumerate(types):
+        if t == CT_STRING:
+            # spans relative to each chunk -> offsets into ``data`` (fs is bits 25..63)
+            sp = [p[1][c][:p[0]] + (p[5] << 25) if p[5] else p[1][c][:p[0]] for _, p in live]
+            spans = torch.cat(sp) if len(sp) > 1 else (sp[0] if sp else torch.empty(0, dtype=torch.int64, device=dev))
+            vv = None
+            if int(st[:, 2 + c].sum()):
+                valid_l = [p[2][c, :p[0]] for _, p in live]
+                vv = torch.cat(valid_l) if len(valid_l) > 1 else valid_l[0].clone()
+            fields.append(StructField(f"_c{c}", StringType(), True))
+            cols.append(DeviceStringColumn(spans, vv, data, opts))
+            continue
         vals_l = []
-        for _, (nlines, dcols, _, _, _) in live:
+        for _, (nlines, dcols, _, _, _, _) in live:
             d = dcols[c][:nlines]
             if hinted:  # stored as the column's type already
                 pass
@@ -313,46 +332,55 @@ def infer_streamed(src, sep: str, ncols: Optional[int] = None, sharded: bool = F
     hint = list(user_types) if user_types else None
     sts, total = [], 0
     for buf, n, trailing in src.chunks():
-        nlines, _cols, _valid, _keep, stats = _scan_chunk(h, buf, n, trailing, ncols, sep, src.device, hint, opts)
+        nlines, _cols, _valid, _keep, stats, _ = _scan_chunk(h, buf, n, trailing, ncols, sep, src.device, hint, opts)
         total += nlines
         sts.append(stats)
     st = torch.stack(sts).cpu().numpy()
+    masks = np.bitwise_or.reduce(st[:, 2 + ncols:2 + 2 * ncols], axis=0)
     if user_types:
-        flag = int(st[:, 0].max())
-        if sharded:
-            flag = int(comm.all_reduce_max(torch.tensor([flag], dtype=torch.int64))[0])
-        if flag:
+        if _strict_flag(masks, int(st[:, 0].max()), user_types, sharded):
             return None
         types = list(user_types)
     else:
-        types = _resolve_types(np.bitwise_or.reduce(st[:, 2 + ncols:2 + 2 * ncols], axis=0), int(st[:, 0].max()),
-                               sharded)
-        if types is None:
+        types = _resolve_types(masks, int(st[:, 0].max()), sharded)
+        if types is None or CT_STRING in types:  # (the streamed fused Gram reads numeric columns)
             return None
     STATS["streamed_inferences"] = STATS.get("streamed_inferences", 0) + 1
     return types, _facts(st, ncols, total)
 
 
 def _resolve_types(masks: np.ndarray, flag: int, sharded: bool):
+    """Merged column types, or None when the host scanner must decide: the slow flag, a decimal,
+    or a column holding a field the device could not settle (SLOW_BIT) that its other fields do
+    not make a string anyway (a string is the lattice top: no field can change it)."""
     if sharded:
         flag = int(comm.all_reduce_max(torch.tensor([flag], dtype=torch.int64))[0])
         masks = _or_reduce(torch.from_numpy(masks)).numpy()
     if flag:
         return None
     types = [merge_type_mask(int(m)) for m in masks]
-    if any(t in (CT_STRING, CT_DECIMAL) for t in types):
-        return None
+    for t, m in zip(types, masks):
+        if t == CT_DECIMAL or (int(m) & SLOW_BIT and (t != CT_STRING or not int(m) & 0x7E)):
+            return None
     return types
 
 
-# user-schema type codes the device parser converts (int, long, double, boolean)
-STRICT_CODES = (CT_INT, CT_LONG, CT_DOUBLE, CT_BOOL)
+def _strict_flag(masks: np.ndarray, flag: int, user_types, sharded: bool) -> bool:
+    """A user-schema scan needs the host: the slow flag, or an unsettled field in a non-string column."""
+    bad = int(flag) or any(int(m) & SLOW_BIT and t != CT_STRING for t, m in zip(user_types, masks))
+    if sharded:
+        bad = int(comm.all_reduce_max(torch.tensor([int(bad)], dtype=torch.int64))[0])
+    return bool(bad)
+
+
+# user-schema type codes the device parser converts (int, long, double, boolean; string: spans)
+STRICT_CODES = (CT_INT, CT_LONG, CT_DOUBLE, CT_BOOL, CT_STRING)
 
 
 def scan_device(data, sep: str = ",", infer: bool = True, device=None, ncols: Optional[int] = None,
                 sharded: bool = False, chunk_bytes: Optional[int] = None, pinned: Optional[torch.Tensor] = None,
                 device_data: Optional[torch.Tensor] = None, types_hint: Optional[list] = None,
-                opts: Optional[dict] = None, user_types: Optional[list] = None):
+                opts: Optional[dict] = None, user_types: Optional[list] = None, _depth: int = 0):
     """Parse ``data`` on the device.  Inputs larger than ``chunk_bytes`` stream through a
     double-buffered pinned staging ring: chunk k+1's host->device copy runs on a side stream while
     chunk k is parsed, chunks split on row boundaries, type masks OR-merged over
@@ -361,14 +389,13 @@ def scan_device(data, sep: str = ",", infer: bool = True, device=None, ncols: Op
     ``types_hint``: column type codes from an earlier scan of the same bytes (the reader keeps
     them with its cached file): the parser then stores every column as its type directly — no
     f64 plane to convert.  Inference still runs; a hint the masks contradict re-scans unhinted.
+    String columns are scanned as spans, which needs the hint: a scan that finds a string column
+    without one re-scans once with the inferred types as the hint.
 
     ``opts``: dialect (quote, escape, comment, trim_lead, trim_trail, null_value; see
     ``csv_parse_dev.h``).  ``user_types``: a user schema (lattice codes in STRICT_CODES): the
     columns are stored as those types, a field that does not convert nulls its record (Spark's
     PERMISSIVE), no inference."""
-    # quotes / escapes need the host scanner: the parse kernel flags any field that starts with
-    # one (slow path) and a mid-field one makes the column a string — both fall back, so the
-    # input is never pre-scanned on the host
     if len(sep) != 1 or not (infer or user_types):
         return None
     if user_types:
@@ -396,7 +423,7 @@ def scan_device(data, sep: str = ",", infer: bool = True, device=None, ncols: Op
         parts = []
         for s, e in zip(bounds, bounds[1:]):
             trailing = data[e - 1] not in (10, 13)
-            parts.append(_scan_chunk(h, device_data[s:e], e - s, trailing, ncols, sep, dev, hint, opts))
+            parts.append(_scan_chunk(h, device_data[s:e], e - s, trailing, ncols, sep, dev, hint, opts, s))
     elif chunk_bytes is None or n <= chunk_bytes:
         if pinned is not None and n:
             buf = pinned.to(dev, non_blocking=True)  # page-locked mapping: direct DMA
@@ -410,27 +437,32 @@ def scan_device(data, sep: str = ",", infer: bool = True, device=None, ncols: Op
     st = torch.stack([p[4] for p in parts]).cpu().numpy()  # the one host read of the parse results
     masks = np.bitwise_or.reduce(st[:, 2 + ncols:2 + 2 * ncols], axis=0)
     if user_types:
-        flag = int(st[:, 0].max())
-        if sharded:
-            flag = int(comm.all_reduce_max(torch.tensor([flag], dtype=torch.int64))[0])
-        if flag:
+        if _strict_flag(masks, int(st[:, 0].max()), user_types, sharded):
             STATS["fallbacks"] += 1
             return None
         STATS["device_scans"] += 1
-        return _finish(parts, list(user_types), st, dev, hinted=True)
+        return _finish(parts, list(user_types), st, dev, hinted=True, data=data, opts=opts)
     types = _resolve_types(masks, int(st[:, 0].max()), sharded)
     if types is None:
         STATS["fallbacks"] += 1
         return None
-    miss = hint is not None and [_KIND.get(t, (0,))[0] for t in types] != [_KIND.get(t, (0,))[0] for t in hint]
+    kinds = [_KIND.get(t, (0,))[0] for t in types]
+    miss = hint is not None and kinds != [_KIND.get(t, (0,))[0] for t in hint]
+    spans = CT_STRING in types and (hint is None or miss)  # string columns need the span scan
     if sharded:  # every rank takes the same (collective) path
-        miss = bool(int(comm.all_reduce_max(torch.tensor([int(miss)], dtype=torch.int64))[0]))
-    if miss:
-        STATS["hint_misses"] = STATS.get("hint_misses", 0) + 1
-        return scan_device(data, sep, infer, device, ncols, sharded, chunk_bytes, pinned, device_data, None, opts)
+        flags = comm.all_reduce_max(torch.tensor([int(miss), int(spans)], dtype=torch.int64))
+        miss, spans = bool(int(flags[0])), bool(int(flags[1]))
+    if (miss or spans) and _depth < 2:  # (sharded: ``types`` are the merged ones, equal on every rank)
+        STATS["hint_misses" if miss and hint is not None else "span_rescans"] = \
+            STATS.get("hint_misses" if miss and hint is not None else "span_rescans", 0) + 1
+        return scan_device(data, sep, infer, device, ncols, sharded, chunk_bytes, pinned, device_data,
+                           types if spans else None, opts, _depth=_depth + 1)
+    if miss or spans:
+        STATS["fallbacks"] += 1
+        return None
     STATS["device_scans"] += 1
     STATS["chunks"] = STATS.get("chunks", 0) + len(parts)
-    return _finish(parts, types, st, dev, hinted=hint is not None)
+    return _finish(parts, types, st, dev, hinted=hint is not None, data=data, opts=opts)
 
 
 def chunk_bounds(data: bytes, chunk_bytes: int):
@@ -470,7 +502,7 @@ def _scan_chunked(h, data, ncols: int, sep: str, dev, chunk_bytes: int, pinned: 
             put(i + 1)  # overlaps chunk i's parse
         buf = ring.get(i)
         trailing = data[e - 1] not in (10, 13)
-        parts.append(_scan_chunk(h, buf, e - s, trailing, ncols, sep, dev, hint, opts))
+        parts.append(_scan_chunk(h, buf, e - s, trailing, ncols, sep, dev, hint, opts, s))
         ring.release(i)
     return parts
 
@@ -479,9 +511,9 @@ def _or_reduce(masks: torch.Tensor) -> torch.Tensor:
     """Bitwise-OR all-reduce of the per-column class masks via MAX over bit planes."""
     if not comm.collectives_active():
         return masks
-    bits = torch.stack([(masks >> i) & 1 for i in range(7)]).to(torch.int32)
+    bits = torch.stack([(masks >> i) & 1 for i in range(8)]).to(torch.int32)
     bits = comm.all_reduce_max(bits)
     out = torch.zeros_like(masks)
-    for i in range(7):
+    for i in range(8):
         out |= bits[i] << i
     return out

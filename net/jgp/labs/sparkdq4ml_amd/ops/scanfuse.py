@@ -239,6 +239,10 @@ def kernel_source(g, kinds, nullable, used, opts: dict, strict: bool, head: int,
     abl = int(os.environ.get("DQ4ML_SCAN_ABL", "0"))
 
     def field_code(c: int, swar: bool) -> str:
+        if int(kinds[c]) == 4:  # a string column the chain does not read: cut past its field only
+            return (f"    bool fzk{c} = false;\n"
+                    f"    if (pos <= end && line) {{ decltype(pos) fs{c} = 0, fe{c} = 0; bool rw{c} = false; "
+                    f"fzk{c} = !csv_field_span(B, (decltype(pos))bias, pos, (decltype(pos))end, O, fs{c}, fe{c}, rw{c}); }}\n")
         if swar and abl & 64:
             return (f"    double fzd{c} = 0.0; long long fzl{c} = 0; bool fzg{c} = false; int fzy{c} = C_NULL;\n"
                     f"    if (pos <= len && line) {{\n"
@@ -275,6 +279,8 @@ def kernel_source(g, kinds, nullable, used, opts: dict, strict: bool, head: int,
         for c in range(ncols):
             k = int(kinds[c])
             parse.append(field_code(c, swar))
+            if k == 4:
+                continue
             if strict:
                 parse.append(f"    if (fzy{c} != C_NULL && !csv_conforms(fzy{c}, {k})) {{ malformed = true; fzk{c} = false; }}\n")
             else:
@@ -287,6 +293,10 @@ def kernel_source(g, kinds, nullable, used, opts: dict, strict: bool, head: int,
                 parse.append(f"    bad |= line && !fzk{c};\n")
         for c in sorted(used):
             ct = used[c]
+            if int(kinds[c]) == 4:
+                from . import dqvm
+
+                raise dqvm.Unfusable("string column")  # the eager scan builds it (DeviceStringColumn)
             val = _VALUE[int(kinds[c])].format(c=c)
             parse.append(f"    const {ct} fzf{c} = fzk{c} ? ({ct})({val}) : ({ct})0;\n")
             if nullable[c]:

@@ -68,6 +68,10 @@ def _device_csv_opts(o) -> Optional[dict]:
     comment, null_value = o.get("comment", ""), o.get("nullvalue", "")
     if len(quote) != 1 or len(escape) != 1 or len(comment) > 1 or len(null_value.encode()) > 16:
         return None
+    # the device classifies a field with a quote / escape byte from its raw bytes and compares
+    # nullValue with them: exact while neither byte can be part of a number, a boolean or nullValue
+    if any(ch.isalnum() or ch in "+-." or ch in null_value for ch in (quote, escape)):
+        return None
     return {"quote": quote, "escape": escape, "comment": ord(comment) if comment else 0,
             "trim_lead": _truthy(o.get("ignoreleadingwhitespace", "false")),
             "trim_trail": _truthy(o.get("ignoretrailingwhitespace", "false")),
@@ -297,8 +301,12 @@ class DataFrameReader:
         # trims, any single-byte quote / escape (fields starting with one -> host re-scan)
         dopts = _device_csv_opts(o)
         strict = [c for c in user_types] if user_types else None
-        use_dev = (dev.type == "cuda" and dopts is not None and len(sep) == 1 and (infer or strict)
-                   and (not strict or all(c in (1, 2, 4, 5) for c in strict)))
+        # a user schema of int / long / double / boolean / string columns; no schema and no
+        # inference: every column a string (Spark's default read)
+        all_str = not infer and not strict
+        use_dev = (dev.type == "cuda" and dopts is not None and len(sep) == 1
+                   and (not strict or all(c in (1, 2, 4, 5) or (c == 6 and isinstance(f.dataType, StringType))
+                                          for c, f in zip(strict, self._schema.fields))))
         hdr = None
         if use_dev and header:
             hdr = _split_header(data, sep, dopts)
@@ -326,8 +334,17 @@ class DataFrameReader:
                     dbytes = dbytes[off:] if off else dbytes
             hkey = (lo + off, hi, sep, repr(sorted(dopts.items())))
             fkey = hkey + (tuple(strict) if strict else None,)
+            if all_str:
+                from ..ops.csvscan import CT_STRING, _ncols_of, _opt_args
+
+                oa = _opt_args(dopts)
+                nstr = len(names) if names else _ncols_of(body, sep, int(oa["comment"] or 0), oa["quote"], oa["escape"])
+                if shard:  # the first record of the file (rank 0's shard) sets the column count
+                    nstr = comm.all_gather_object(nstr)[0]
+                strict = [CT_STRING] * nstr
+                fkey = hkey + (tuple(strict),)
             ncols = len(strict) if strict else (len(names) if names else None)
-            final = user_names if strict else names
+            final = (user_names or names) if strict else names
 
             def dev_scan():
                 with tracing.span("csv_scan"):

@@ -16,12 +16,13 @@ from __future__ import annotations
 from dataclasses import dataclass, field
 from typing import List, Optional
 
+import numpy as np
 import torch
 
 from .types import (BooleanType, DataType, DoubleType, IntegerType, LongType, NullType,
                     StringType, StructField, StructType, VectorUDT)
 
-__all__ = ["ColumnData", "Table"]
+__all__ = ["ColumnData", "DeviceStringColumn", "Table"]
 
 
 @dataclass
@@ -144,6 +145,69 @@ class LazyVectorColumn(ColumnData):
     @property
     def n(self) -> int:
         return self._n
+
+
+class DeviceStringColumn(ColumnData):
+    """A string column of a device CSV scan (``ops/csvscan.py``): per row the packed span of its
+    field in the scanned input bytes (int64 ``[n]`` in HBM: ``(fs << 25) | (raw << 24) | len``,
+    ``csv_scan.h`` kind 4) and its validity.  The Python strings are built on first use of
+    ``values`` by the host tokenizer (``_dq4ml_host.csv_strings``: raw -- quoted or escaped --
+    fields through ``split_record``, the rest straight from the bytes), so a chain that never
+    reads the column (the lab's DQ -> assemble -> fit) never builds them, and row selections
+    (``index`` / ``slice``) move only the spans."""
+
+    def __init__(self, spans: torch.Tensor, valid: Optional[torch.Tensor], data, opts: Optional[dict],
+                 meta=None):  # noqa: D107
+        self.dtype = StringType()
+        self.spans = spans
+        self.valid = valid
+        self.data = data  # the scanned bytes (bytes / memoryview / numpy view of the cached file)
+        self.opts = dict(opts or {})
+        self.meta = meta or {}
+        self.checks = []
+        self._vals = None
+
+    @property
+    def values(self):
+        if self._vals is None:
+            from ..ops import native
+
+            o = self.opts
+            sp = self.spans.detach().cpu().numpy()
+            ok = (self.valid.detach().to("cpu", torch.uint8).numpy() if self.valid is not None
+                  else np.ones(sp.shape[0], dtype=np.uint8))
+            data = self.data if not isinstance(self.data, (bytes, bytearray)) else memoryview(self.data)
+            self._vals = native.host().csv_strings(data, sp, ok, quote=o.get("quote", '"'),
+                                                   escape=o.get("escape", "\\"),
+                                                   ignore_leading_ws=bool(o.get("trim_lead")),
+                                                   ignore_trailing_ws=bool(o.get("trim_trail")))
+        return self._vals
+
+    @values.setter
+    def values(self, v):
+        self._vals = v
+
+    @property
+    def materialized(self) -> bool:
+        return self._vals is not None
+
+    @property
+    def n(self) -> int:
+        return int(self.spans.numel())
+
+    def index(self, idx: torch.Tensor) -> "ColumnData":
+        if self._vals is not None:
+            return ColumnData.index(self, idx)
+        i = idx.to(self.spans.device)
+        valid = None if self.valid is None else self.valid.index_select(0, i)
+        return DeviceStringColumn(self.spans.index_select(0, i), valid, self.data, self.opts, dict(self.meta))
+
+    def slice(self, start: int, stop: int) -> "ColumnData":
+        if self._vals is not None:
+            return ColumnData.slice(self, start, stop)
+        valid = None if self.valid is None else self.valid[start:stop]
+        return DeviceStringColumn(self.spans[start:stop], valid, self.data, self.opts, dict(self.meta))
+
 
 class Table:
     def __init__(self, schema: StructType, columns: List[ColumnData], nrows: int,

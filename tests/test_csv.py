@@ -115,13 +115,16 @@ def test_device_scan_matches_host(name):
     data = CASES[name] if name in CASES else open(data_path(name), "rb").read()
     t = csvscan.scan_device(data, device="cuda")
     n, cols = _host(data)
-    if any(c[1] in (3, 6) for c in cols):
-        assert t is None  # strings / decimals go to the host scanner
+    if any(c[1] == 3 for c in cols):
+        assert t is None  # decimals go to the host scanner
         return
     assert t is not None and t.nrows == n
     for (name_, code, vals, valid), c in zip(cols, t.columns):
         v = c.valid_mask().cpu().numpy()
         assert list(v.astype(int)) == list(valid.astype(int))
+        if code == 6:  # a device string column (field spans; text built on the host)
+            assert [x for x, ok in zip(c.values, valid) if ok] == [x for x, ok in zip(vals, valid) if ok]
+            continue
         got = c.values.cpu().numpy()
         ref = np.asarray(vals)
         if code == 5:
@@ -535,3 +538,65 @@ def test_device_reader_quoted_header_and_large_quoted_file(tmp_path):
     got = np.asarray([r[1] for r in df.limit(1000).collect()])
     np.testing.assert_allclose(got, pr[:1000], rtol=0, atol=1e-9)
     spark.stop()
+
+
+def _span_ref(line: bytes, pos: int, sep: int, quote: int, escape: int):
+    """Python mirror of the device's ``csv_field_span`` (csv_parse_dev.h): (fs, fe, raw, next pos)."""
+    n, c, raw = len(line), pos, False
+    if c < n and line[c] == quote:
+        raw, c = True, c + 1
+        while c < n:
+            ch = line[c]
+            if escape != quote and ch == escape and c + 1 < n and line[c + 1] in (quote, escape):
+                c += 2
+            elif ch == quote:
+                if c + 1 < n and line[c + 1] == quote:
+                    c += 2
+                else:
+                    c += 1
+                    break
+            else:
+                c += 1
+    while c < n and line[c] != sep:
+        raw |= line[c] == escape
+        c += 1
+    return pos, c, raw, c + 1
+
+
+def _string_fuzz(rng, rows: int, ncols: int = 4) -> list:
+    """Records of string-ish fields: separators / doubled quotes / escapes inside quotes, quoted
+    empties, unquoted quotes, escape-led tokens, unicode, spaces."""
+    toks = ['a', 'plain text', '"a,b"', '"x""y"', '"p\\"q"', '"\\\\"', '""', '', 'u"v', '\\N', '\\"w',
+            '"1,5"', '"abc"tail', ' pad ', '"  sp  "', 'café', '"niño, s.a."', '7', '-3.5', '"12"', 'true']
+    out = []
+    for _ in range(rows):
+        out.append(",".join(toks[int(rng.integers(0, len(toks)))] for _ in range(ncols)).encode())
+    return out
+
+
+@pytest.mark.parametrize("trim", [False, True])
+def test_csv_strings_materializer_matches_tokenizer(trim):
+    """The host half of the device string columns: spans cut the device's way (``_span_ref``),
+    packed like the kernel stores them, then ``csv_strings`` builds the text -- equal to what the
+    univocity tokenizer (``split_record``) yields for every field."""
+    from net.jgp.labs.sparkdq4ml_amd.ops.csvscan import split_record
+
+    rng = np.random.default_rng(3)
+    lines = _string_fuzz(rng, 3000, 5)
+    data = b"\n".join(lines)
+    spans, valid, want = [], [], []
+    base = 0
+    for line in lines:
+        pos = 0
+        fields = split_record(line, ord(","), 34, 92, b"", trim, trim)
+        for text, null in fields:
+            fs, fe, raw, pos = _span_ref(line, pos, ord(","), 34, 92)
+            spans.append(((base + fs) << 25) | (int(raw) << 24) | (fe - fs))
+            quoted = line[fs:fs + 1] == b'"'
+            valid.append(0 if (not quoted and fe == fs) else 1)
+            want.append(None if null else text.decode("utf-8"))
+        assert pos == len(line) + 1  # the spans cover the record exactly as the tokenizer splits it
+        base += len(line) + 1
+    got = native.host().csv_strings(data, np.array(spans, dtype=np.int64), np.array(valid, dtype=np.uint8),
+                                    ignore_leading_ws=trim, ignore_trailing_ws=trim)
+    assert got == want

@@ -110,10 +110,13 @@ def test_scan_fused_codegen_compiles(cpu_session, tmp_path, nullable, fast, tick
     assert r.returncode == 0, r.stderr
 
 
-def test_scan_fused_gram_codegen_compiles(cpu_session, tmp_path):
+@pytest.mark.parametrize("string_col", [False, True])
+def test_scan_fused_gram_codegen_compiles(cpu_session, tmp_path, string_col):
     """Gram mode of the fused scan kernel (``scanfuse.try_fused_gram``'s shape): the lab chain,
     then ``VectorAssembler([guest])`` + label as the kernel's d = 1 feature / label outputs —
-    no row store, per-window f64 statistics in the ``gram_width`` layout; compiles for gfx950."""
+    no row store, per-window f64 statistics in the ``gram_width`` layout; compiles for gfx950.
+    ``string_col``: a third, string column the chain does not read (kind 4: the kernel only cuts
+    past its field, ``csv_field_span``)."""
     import torch
 
     from net.jgp.labs.sparkdq4ml_amd import VectorAssembler
@@ -122,13 +125,18 @@ def test_scan_fused_gram_codegen_compiles(cpu_session, tmp_path):
     from net.jgp.labs.sparkdq4ml_amd.sql.dataframe import DataFrame
     from net.jgp.labs.sparkdq4ml_amd.sql.expressions import Alias, ColRef
     from net.jgp.labs.sparkdq4ml_amd.sql.plan import CsvScanRelation, prune_columns
-    from net.jgp.labs.sparkdq4ml_amd.sql.types import DoubleType, IntegerType, StructField, StructType
+    from net.jgp.labs.sparkdq4ml_amd.sql.types import DoubleType, IntegerType, StringType, StructField, StructType
 
     spark = cpu_session
     register_lab_rules(spark)
-    schema = StructType([StructField("_c0", IntegerType(), True), StructField("_c1", DoubleType(), True)])
+    fields = [StructField("_c0", IntegerType(), True), StructField("_c1", DoubleType(), True)]
     fused = {"kinds": [1, 0], "nullable": [False, False], "strict": False,
              "opts": dict(_opt_args({"comment": 0}), sep=",", strict=False)}
+    if string_col:
+        fields.append(StructField("_c2", StringType(), True))
+        fused["kinds"].append(4)
+        fused["nullable"].append(True)
+    schema = StructType(fields)
     rel = CsvScanRelation(schema, lambda: None, fused, "Relation[csv]")
     df = DataFrame(rel, spark).withColumnRenamed("_c0", "guest").withColumnRenamed("_c1", "price")
     df = df.withColumn("price_no_min", callUDF("minimumPriceRule", df.col("price")))
@@ -149,9 +157,11 @@ def test_scan_fused_gram_codegen_compiles(cpu_session, tmp_path):
     g = scanfuse._scan_gen(base, fused["nullable"])
     _, g, outputs, _ = dqvm.compile_chain(chain, base, False, gen=g)
     slots = {k: g.slot(None, (k,)) for k in scanfuse._ScanPlan.SCAN_SLOTS + ("gpart",)}
+    fast = not string_col  # (a string column is never on the numeric fast path)
     src = scanfuse.kernel_source(g, fused["kinds"], fused["nullable"], g.used, fused["opts"], False, 256, slots,
-                                 True, True, "xcd", 1)
+                                 True, fast, "xcd", 1)
     assert scanfuse.gram_width(1) == 6 and "gred[4][6]" in src
+    assert ("= !csv_field_span(" in src) == string_col
     assert "[li] =" not in src  # no row is stored
     hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
     if not os.path.exists(hipcc):
@@ -163,7 +173,7 @@ def test_scan_fused_gram_codegen_compiles(cpu_session, tmp_path):
     assert r.returncode == 0, r.stderr
     # the default Gram-mode build: no global line numbering (no ticket, no look-back, no nalloc check)
     src2 = scanfuse.kernel_source(g, fused["kinds"], fused["nullable"], g.used, fused["opts"], False, 256, slots,
-                                  True, True, "xcd", 1, nolb=True)
+                                  True, fast, "xcd", 1, nolb=True)
     assert "__hip_atomic_fetch_add" not in src2 and "sgl0 = pre" not in src2 and "li >= nalloc" not in src2
     assert "const long long blk = blockIdx.x;" in src2 and "sgl0 = pre" in src
     f2 = tmp_path / "scan_gram_nolb.hip"
