@@ -9,7 +9,8 @@
 namespace dq4ml {
 
 // type lattice codes (same as the host scanner, csrc/host/csv.h)
-enum CsvTypeCode : int { CT_NULL = 0, CT_INT = 1, CT_LONG = 2, CT_DECIMAL = 3, CT_DOUBLE = 4, CT_BOOL = 5, CT_STRING = 6 };
+enum CsvTypeCode : int { CT_NULL = 0, CT_INT = 1, CT_LONG = 2, CT_DECIMAL = 3, CT_DOUBLE = 4, CT_BOOL = 5, CT_STRING = 6,
+                         CT_TIMESTAMP = 7 };
 
 int64_t csv_count_blocks(int64_t n);
 // Two calls: ends == null -> counts = csv_count_blocks(n)+1 int64 (exclusive per-block offsets,
@@ -18,9 +19,10 @@ int64_t csv_count_blocks(int64_t n);
 bool csv_ends_i32(int64_t n);
 void csv_line_ends(const uint8_t* buf, int64_t n, int64_t* counts, void* ends, hipStream_t st);
 // dcols: [2 * ncols] int64 — ncols device pointers to nlines values each, then ncols storage
-// kinds (0 f64, 1 int32, 2 int64, 3 bool/uint8, 4 string span: int64 (fs << 25) | (raw << 24) | len,
-// fs the field's first byte in buf, see csv_field_span); valid: [ncols, nlines]; stats (zeroed):
-// [slow flag, empty lines, null fields per column (ncols), class masks per column (ncols; bit 7:
+// kinds (0 f64, 1 int32, 2 int64, 3 bool/uint8, 4 string span: int64 (fs << 25) | (raw << 24) | len
+// with fs the field's first byte in buf (csv_field_span), 5 timestamp: int64 microseconds);
+// valid: [ncols, nlines]; stats (zeroed):
+// [slow flag, empty lines, null fields per column (ncols), class masks per column (ncols; bit 8:
 // a field whose value or class needs the host -- harmless when the column is a string),
 // lines with a field outside the numeric fast path, lines with a field that is not even a quoted
 // fast-path number ("12.5")]

@@ -242,7 +242,7 @@ __device__ __forceinline__ bool parse_line(PB B, int64_t bias, int64_t n, const 
       continue;
     }
     // fslow: this field's value (or class) needs the host -- flagged per column (class-mask bit
-    // 7): it only matters when the column does not come out a string
+    // 8): it only matters when the column does not come out a string
     bool fslow = false;
     if (pos <= end && line) {
       const long long pb = (long long)bias, pe = (long long)end;
@@ -268,13 +268,14 @@ __device__ __forceinline__ bool parse_line(PB B, int64_t bias, int64_t n, const 
       void* dst = reinterpret_cast<void*>(dcols[c]);
       switch (kind) {
         case 1: reinterpret_cast<int32_t*>(dst)[li] = ok ? (int32_t)dv : 0; break;
-        case 2: reinterpret_cast<int64_t*>(dst)[li] = ok ? (int64_t)lv : 0; break;
+        case 2:
+        case 5: reinterpret_cast<int64_t*>(dst)[li] = ok ? (int64_t)lv : 0; break;  // long / timestamp (us)
         case 3: reinterpret_cast<uint8_t*>(dst)[li] = ok && dv != 0.0; break;
         default: reinterpret_cast<double*>(dst)[li] = dv;
       }
       valid[(int64_t)c * nlines + li] = ok;
     }
-    uint32_t bit = line ? ((1u << ty) | (fslow ? 0x80u : 0u)) : 0u;
+    uint32_t bit = line ? ((1u << ty) | (fslow ? 0x100u : 0u)) : 0u;
 #pragma unroll
     for (int oo = 1; oo < 64; oo <<= 1) bit |= (uint32_t)__shfl_xor((int)bit, oo, 64);
     const uint64_t nulls = __ballot(line && !ok);
@@ -358,7 +359,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   if (slow) sflag = 1;
   __syncthreads();
   // stats: [0] slow flag, [1] empty lines, [2, 2+ncols) null fields, [2+ncols, 2+2*ncols) class masks
-  // (bit 7: a field whose value or class needs the host),
+  // (bit 8: a field whose value or class needs the host),
   // [2+2*ncols] lines with a field outside the numeric fast path, [3+2*ncols] those with a field that
   // is not even a quoted fast-path number
   for (int c = threadIdx.x; c < ncols; c += blockDim.x) {

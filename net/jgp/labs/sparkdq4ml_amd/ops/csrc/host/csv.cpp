@@ -124,7 +124,90 @@ void split_record(const char* p, size_t n, const CsvOptions& o, std::vector<Fiel
   }
 }
 
+// days from 1970-01-01 of the proleptic Gregorian y-m-d (linear in d: day 31 of a 30-day month
+// is the 1st of the next, java.util.Date's leniency)
+int64_t days_from_civil(int64_t y, int64_t m, int64_t d) {
+  y -= m <= 2;
+  const int64_t era = (y >= 0 ? y : y - 399) / 400;
+  const int64_t yoe = y - era * 400;
+  const int64_t doy = (153 * (m + (m > 2 ? -3 : 9)) + 2) / 5 + d - 1;
+  const int64_t doe = yoe * 365 + yoe / 4 - yoe / 100 + doy;
+  return era * 146097 + doe - 719468;
+}
+
+// k digits at s[i..]: their value, i advanced; false when fewer than lo or more than hi digits
+bool take_digits(const char* s, size_t n, size_t& i, int lo, int hi, int64_t& v) {
+  int k = 0;
+  v = 0;
+  while (i < n && is_digit(s[i]) && k < hi) {
+    v = v * 10 + (s[i] - '0');
+    ++i;
+    ++k;
+  }
+  return k >= lo && !(i < n && is_digit(s[i]));
+}
+
 }  // namespace
+
+bool csv_parse_timestamp(const char* s, size_t n, int64_t& us) {
+  size_t i = 0;
+  int64_t y, mo, d;
+  if (!take_digits(s, n, i, 4, 4, y) || i >= n || s[i] != '-') return false;
+  const size_t m0 = ++i;
+  if (!take_digits(s, n, i, 1, 2, mo) || i >= n || s[i] != '-') return false;
+  const bool mo2 = i - m0 == 2;
+  const size_t d0 = ++i;
+  if (!take_digits(s, n, i, 1, 2, d)) return false;
+  const bool d2 = i - d0 == 2;
+  if (y < 1600 || mo < 1 || mo > 12 || d < 1 || d > 31) return false;
+  int64_t secs = 0, ms = 0, off = 0;
+  if (i == n) {  // Date.valueOf
+  } else if (s[i] == ' ' || s[i] == 'T') {
+    const bool iso = s[i] == 'T';
+    const int lo = iso ? 2 : 1;
+    int64_t h, mi, se;
+    ++i;
+    if (iso && !(mo2 && d2)) return false;
+    if (!take_digits(s, n, i, lo, 2, h) || i >= n || s[i] != ':') return false;
+    ++i;
+    if (!take_digits(s, n, i, lo, 2, mi) || i >= n || s[i] != ':') return false;
+    ++i;
+    if (!take_digits(s, n, i, lo, 2, se)) return false;
+    if (i < n && s[i] == '.') {  // 1..9 fraction digits, millisecond precision kept
+      ++i;
+      int k = 0;
+      while (i < n && is_digit(s[i]) && k < 9) {
+        if (k < 3) ms = ms * 10 + (s[i] - '0');
+        ++i;
+        ++k;
+      }
+      if (k == 0 || (i < n && is_digit(s[i]))) return false;
+      for (; k < 3; ++k) ms *= 10;
+    }
+    if (iso) {
+      static const int dim[12] = {31, 28, 31, 30, 31, 30, 31, 31, 30, 31, 30, 31};
+      const bool leap = (y % 4 == 0 && y % 100 != 0) || y % 400 == 0;
+      if (d > dim[mo - 1] + (mo == 2 && leap) || h > 23 || mi > 59 || se > 59) return false;
+      if (i < n && s[i] == 'Z') {
+        ++i;
+      } else if (i < n && (s[i] == '+' || s[i] == '-')) {
+        const int64_t sg = s[i] == '-' ? -1 : 1;
+        int64_t oh, om;
+        ++i;
+        if (!take_digits(s, n, i, 2, 2, oh) || i >= n || s[i] != ':') return false;
+        ++i;
+        if (!take_digits(s, n, i, 2, 2, om) || oh > 23 || om > 59) return false;
+        off = sg * (oh * 3600 + om * 60);
+      }
+    }
+    if (i != n) return false;
+    secs = h * 3600 + mi * 60 + se - off;
+  } else {
+    return false;
+  }
+  us = ((days_from_civil(y, mo, d) * 86400 + secs) * 1000 + ms) * 1000;
+  return true;
+}
 
 void csv_field_text(const char* p, size_t n, const CsvOptions& o, std::string& out) {
   std::vector<Field> f;
@@ -139,6 +222,7 @@ int csv_infer_field(const char* s, size_t n) {
   if (all_digits_signed(s, n)) return T_DECIMAL;  // integer too long for long
   double dv;
   if (parse_double(s, n, dv)) return T_DOUBLE;
+  if (csv_parse_timestamp(s, n, iv)) return T_TIMESTAMP;
   if (parse_bool(s, n, iv)) return T_BOOL;
   return T_STRING;
 }
@@ -242,6 +326,12 @@ CsvTable csv_scan(const char* data, size_t len, const CsvOptions& opt, const std
         case T_BOOL: {
           int64_t v;
           ok = parse_bool(s.data(), s.size(), v);
+          if (ok) col.ivals[r] = v;
+          break;
+        }
+        case T_TIMESTAMP: {
+          int64_t v;
+          ok = csv_parse_timestamp(s.data(), s.size(), v);
           if (ok) col.ivals[r] = v;
           break;
         }

@@ -103,6 +103,11 @@ PYBIND11_MODULE(_dq4ml_host, m) {
 
   m.def("csv_infer_field", [](const std::string& s) { return csv_infer_field(s.data(), s.size()); });
   m.def("csv_merge_types", &csv_merge_types);
+  m.def("csv_parse_timestamp", [](const std::string& s) -> py::object {
+    int64_t us;
+    if (!csv_parse_timestamp(s.data(), s.size(), us)) return py::none();
+    return py::int_(us);
+  });
 
   // Python strings of a device string column (ops/csvscan.py DeviceStrings), None where not valid:
   // spans are the device scanner's packed (fs << 25) | (raw << 24) | len into data; a raw field

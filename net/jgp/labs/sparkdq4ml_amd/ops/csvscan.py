@@ -20,19 +20,21 @@ from . import native
 
 __all__ = ["scan_device", "merge_type_mask", "shard_byte_range"]
 
-CT_NULL, CT_INT, CT_LONG, CT_DECIMAL, CT_DOUBLE, CT_BOOL, CT_STRING = range(7)
+CT_NULL, CT_INT, CT_LONG, CT_DECIMAL, CT_DOUBLE, CT_BOOL, CT_STRING, CT_TIMESTAMP = range(8)
 STATS = {"device_scans": 0, "fallbacks": 0, "chunks": 0}
 
 
 def merge_type_mask(mask: int) -> int:
     """Tightest common type of the classes present in ``mask`` (bit i = class i seen)."""
-    m = int(mask) & 0x7E  # nulls merge into anything (bit 7 is the needs-the-host flag)
+    m = int(mask) & 0xFE  # nulls merge into anything (bit 8 is the needs-the-host flag)
     if m == 0:
         return CT_STRING  # all-null column -> string (Spark: NullType -> StringType)
     if m & (1 << CT_STRING):
         return CT_STRING
     if m & (1 << CT_BOOL):
         return CT_BOOL if m == (1 << CT_BOOL) else CT_STRING
+    if m & (1 << CT_TIMESTAMP):  # a timestamp merges with timestamps only
+        return CT_TIMESTAMP if m == (1 << CT_TIMESTAMP) else CT_STRING
     return max(i for i in range(1, 5) if m & (1 << i))
 
 
@@ -154,8 +156,10 @@ def _ncols_of(data, sep: str, comment: int = 0, quote: int = 34, escape: int = 9
         w *= 16
 
 
-_KIND = {CT_INT: (1, torch.int32), CT_LONG: (2, torch.int64), CT_BOOL: (3, torch.bool), CT_STRING: (4, torch.int64)}
-SLOW_BIT = 0x80  # class-mask bit: a field whose value or class the device could not settle
+_KIND = {CT_INT: (1, torch.int32), CT_LONG: (2, torch.int64), CT_BOOL: (3, torch.bool), CT_STRING: (4, torch.int64),
+         CT_TIMESTAMP: (5, torch.int64)}
+SLOW_BIT = 0x100  # class-mask bit: a field whose value or class the device could not settle
+_SPANNED = (CT_STRING, CT_TIMESTAMP)  # types scanned under a hint only (spans / exact int64 microseconds)
 
 
 def _opt_args(opts):
@@ -223,10 +227,12 @@ def _scan_chunk(h, buf, n: int, trailing: bool, ncols: int, sep: str, dev, hint=
 
 def type_code_of(dt) -> int:
     """Lattice code of a device-scanned column's type (the reader's types_hint)."""
-    from ..sql.types import BooleanType, IntegerType, LongType, StringType
+    from ..sql.types import BooleanType, IntegerType, LongType, StringType, TimestampType
 
     if isinstance(dt, StringType):
         return CT_STRING
+    if isinstance(dt, TimestampType):
+        return CT_TIMESTAMP
     if isinstance(dt, IntegerType):
         return CT_INT
     if isinstance(dt, LongType):
@@ -243,7 +249,8 @@ def _finish(parts, types, st, dev, hinted=False, data=None, opts=None):
     hinted) become :class:`DeviceStringColumn` over ``data``, the scanned bytes."""
     from ..sql.localdata import ColumnData
     from ..sql.table import DeviceStringColumn, Table
-    from ..sql.types import (BooleanType, DoubleType, IntegerType, LongType, StringType, StructField, StructType)
+    from ..sql.types import (BooleanType, DoubleType, IntegerType, LongType, StringType, StructField, StructType,
+                             TimestampType)
 
     fields, cols = [], []
     total = sum(p[0] for p in parts)
@@ -267,12 +274,13 @@ def _finish(parts, types, st, dev, hinted=False, data=None, opts=None):
                 pass
             elif t == CT_INT:
                 d = d.to(torch.int32)
-            elif t == CT_LONG:
+            elif t in (CT_LONG, CT_TIMESTAMP):
                 d = d.to(torch.int64)
             elif t == CT_BOOL:
                 d = d != 0
             vals_l.append(d)
-        dt = {CT_INT: IntegerType(), CT_LONG: LongType(), CT_BOOL: BooleanType()}.get(t, DoubleType())
+        dt = {CT_INT: IntegerType(), CT_LONG: LongType(), CT_BOOL: BooleanType(),
+              CT_TIMESTAMP: TimestampType()}.get(t, DoubleType())
         if vals_l:
             vals = torch.cat(vals_l) if len(vals_l) > 1 else vals_l[0]
         else:
@@ -343,7 +351,7 @@ def infer_streamed(src, sep: str, ncols: Optional[int] = None, sharded: bool = F
         types = list(user_types)
     else:
         types = _resolve_types(masks, int(st[:, 0].max()), sharded)
-        if types is None or CT_STRING in types:  # (the streamed fused Gram reads numeric columns)
+        if types is None or any(t in _SPANNED for t in types):  # (the streamed fused Gram: numeric columns)
             return None
     STATS["streamed_inferences"] = STATS.get("streamed_inferences", 0) + 1
     return types, _facts(st, ncols, total)
@@ -360,7 +368,7 @@ def _resolve_types(masks: np.ndarray, flag: int, sharded: bool):
         return None
     types = [merge_type_mask(int(m)) for m in masks]
     for t, m in zip(types, masks):
-        if t == CT_DECIMAL or (int(m) & SLOW_BIT and (t != CT_STRING or not int(m) & 0x7E)):
+        if t == CT_DECIMAL or (int(m) & SLOW_BIT and (t != CT_STRING or not int(m) & 0xFE)):
             return None
     return types
 
@@ -374,7 +382,7 @@ def _strict_flag(masks: np.ndarray, flag: int, user_types, sharded: bool) -> boo
 
 
 # user-schema type codes the device parser converts (int, long, double, boolean; string: spans)
-STRICT_CODES = (CT_INT, CT_LONG, CT_DOUBLE, CT_BOOL, CT_STRING)
+STRICT_CODES = (CT_INT, CT_LONG, CT_DOUBLE, CT_BOOL, CT_STRING, CT_TIMESTAMP)
 
 
 def scan_device(data, sep: str = ",", infer: bool = True, device=None, ncols: Optional[int] = None,
@@ -448,7 +456,7 @@ def scan_device(data, sep: str = ",", infer: bool = True, device=None, ncols: Op
         return None
     kinds = [_KIND.get(t, (0,))[0] for t in types]
     miss = hint is not None and kinds != [_KIND.get(t, (0,))[0] for t in hint]
-    spans = CT_STRING in types and (hint is None or miss)  # string columns need the span scan
+    spans = any(t in _SPANNED for t in types) and (hint is None or miss)  # they need the hinted scan
     if sharded:  # every rank takes the same (collective) path
         flags = comm.all_reduce_max(torch.tensor([int(miss), int(spans)], dtype=torch.int64))
         miss, spans = bool(int(flags[0])), bool(int(flags[1]))
@@ -511,9 +519,9 @@ def _or_reduce(masks: torch.Tensor) -> torch.Tensor:
     """Bitwise-OR all-reduce of the per-column class masks via MAX over bit planes."""
     if not comm.collectives_active():
         return masks
-    bits = torch.stack([(masks >> i) & 1 for i in range(8)]).to(torch.int32)
+    bits = torch.stack([(masks >> i) & 1 for i in range(9)]).to(torch.int32)
     bits = comm.all_reduce_max(bits)
     out = torch.zeros_like(masks)
-    for i in range(8):
+    for i in range(9):
         out |= bits[i] << i
     return out

@@ -167,7 +167,7 @@ def _wpe(fast_only: bool = False) -> str:
     return f"__attribute__((amdgpu_waves_per_eu({w}))) " if w > 0 else ""
 
 
-_VALUE = {1: "(int)fzl{c}", 2: "fzl{c}", 0: "fzd{c}", 3: "(fzd{c} != 0.0)"}
+_VALUE = {1: "(int)fzl{c}", 2: "fzl{c}", 0: "fzd{c}", 3: "(fzd{c} != 0.0)", 5: "fzl{c}"}
 
 
 def _scan_nt() -> bool:

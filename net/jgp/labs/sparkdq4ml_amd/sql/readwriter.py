@@ -27,7 +27,7 @@ from .localdata import column_from_numpy, column_from_pylist, table_from_data
 from .plan import LocalRelation
 from .table import ColumnData, Table
 from .types import (BooleanType, DecimalType, DoubleType, IntegerType, LongType, StringType,
-                    StructField, StructType, parse_type_name)
+                    StructField, StructType, TimestampType, parse_type_name)
 
 __all__ = ["DataFrameReader", "DataFrameWriter", "csv_code_to_type"]
 
@@ -40,7 +40,7 @@ _LOAD_CONF = ("dq4ml.csv.deviceThresholdBytes", "dq4ml.csv.deviceCache", "dq4ml.
 log = get_logger("io")
 
 _CODE2TYPE = {1: IntegerType, 2: LongType, 3: lambda: DecimalType(38, 0), 4: DoubleType, 5: BooleanType,
-              6: StringType, 0: StringType}
+              6: StringType, 7: TimestampType, 0: StringType}
 
 
 def csv_code_to_type(code: int):
@@ -58,6 +58,8 @@ def _type_to_code(t) -> int:
         return 4
     if isinstance(t, BooleanType):
         return 5
+    if isinstance(t, TimestampType):
+        return 7
     return 6
 
 
@@ -297,15 +299,14 @@ class DataFrameReader:
         if presharded:
             lo, hi = 0, len(data)  # pf holds exactly this rank's bytes
         # the device scanner takes the common dialect options (csv_parse_dev.h): header, a user
-        # schema of int / long / double / boolean columns, nullValue, comment, the whitespace
-        # trims, any single-byte quote / escape (fields starting with one -> host re-scan)
+        # schema, nullValue, comment, the whitespace trims, any single-byte quote / escape
         dopts = _device_csv_opts(o)
         strict = [c for c in user_types] if user_types else None
-        # a user schema of int / long / double / boolean / string columns; no schema and no
-        # inference: every column a string (Spark's default read)
+        # a user schema of int / long / double / boolean / timestamp / string columns; no schema
+        # and no inference: every column a string (Spark's default read)
         all_str = not infer and not strict
         use_dev = (dev.type == "cuda" and dopts is not None and len(sep) == 1
-                   and (not strict or all(c in (1, 2, 4, 5) or (c == 6 and isinstance(f.dataType, StringType))
+                   and (not strict or all(c in (1, 2, 4, 5, 7) or (c == 6 and isinstance(f.dataType, StringType))
                                           for c, f in zip(strict, self._schema.fields))))
         hdr = None
         if use_dev and header:

@@ -20,7 +20,7 @@ import numpy as np
 import torch
 
 from .types import (BooleanType, DataType, DoubleType, IntegerType, LongType, NullType,
-                    StringType, StructField, StructType, VectorUDT)
+                    StringType, StructField, StructType, TimestampType, VectorUDT)
 
 __all__ = ["ColumnData", "DeviceStringColumn", "Table"]
 
@@ -102,6 +102,8 @@ class ColumnData:  # noqa: D101 (dataclass below)
             t = self.values.detach().cpu()
             if isinstance(self.dtype, BooleanType):
                 vals = [bool(v) for v in t.tolist()]
+            elif isinstance(self.dtype, TimestampType):
+                vals = [micros_to_datetime(v) for v in t.tolist()]
             elif isinstance(self.dtype, (IntegerType, LongType)):
                 vals = [int(v) for v in t.tolist()]
             else:
@@ -111,6 +113,19 @@ class ColumnData:  # noqa: D101 (dataclass below)
             vals = [v if ok else None for v, ok in zip(vals, m)]
         return vals
 
+
+_EPOCH = None
+
+
+def micros_to_datetime(us: int):
+    """A TimestampType value (microseconds since the epoch, UTC) as the naive ``datetime`` a
+    ``collect()`` returns (PySpark: local time; the engine's session time zone is UTC)."""
+    import datetime
+
+    global _EPOCH
+    if _EPOCH is None:
+        _EPOCH = datetime.datetime(1970, 1, 1)
+    return _EPOCH + datetime.timedelta(microseconds=int(us))
 
 
 class LazyVectorColumn(ColumnData):

@@ -600,3 +600,88 @@ def test_csv_strings_materializer_matches_tokenizer(trim):
     got = native.host().csv_strings(data, np.array(spans, dtype=np.int64), np.array(valid, dtype=np.uint8),
                                     ignore_leading_ws=trim, ignore_trailing_ws=trim)
     assert got == want
+
+
+TS_CASES = {  # token -> expected datetime (None: not a timestamp)
+    "2019-01-01": (2019, 1, 1), "2019-1-5": (2019, 1, 5), "2019-02-30": (2019, 3, 2),  # Date.valueOf is lenient
+    "2019-01-01 10:20:30": (2019, 1, 1, 10, 20, 30), "2019-01-01 10:20:30.5": (2019, 1, 1, 10, 20, 30, 500000),
+    "2019-01-01 1:2:3": (2019, 1, 1, 1, 2, 3), "2019-01-01 10:20:30.123456789": (2019, 1, 1, 10, 20, 30, 123000),
+    "2019-01-01T10:20:30": (2019, 1, 1, 10, 20, 30), "2019-01-01T10:20:30Z": (2019, 1, 1, 10, 20, 30),
+    "2019-01-01T10:20:30.25+01:00": (2019, 1, 1, 9, 20, 30, 250000), "2020-02-29T23:59:59-00:30": (2020, 3, 1, 0, 29, 59),
+    "1970-01-01": (1970, 1, 1), "1600-03-01": (1600, 3, 1), "9999-12-31 23:59:59": (9999, 12, 31, 23, 59, 59),
+    "2019-1-01T10:20:30": None, "2019-02-30T00:00:00": None, "1599-12-31": None, "20190101": None,
+    "2019-13-01": None, "2019-01-01 10:20": None, "2019-01-01x": None, "2019-01-01 10:20:30.": None,
+    "2019-01-01T10:20:30+1:00": None, "2019-01-01T24:00:00": None, "2019-01-32": None, "2019/01/01": None,
+    "2019-01-01  10:20:30": None, "T10:20:30": None,
+}
+
+
+def test_timestamp_parser_and_inference():
+    """SURVEY S03's lattice step double -> timestamp -> boolean: Spark 2.4's fallback timestamp
+    parsers (Date.valueOf, Timestamp.valueOf, xsd:dateTime) in the host scanner, UTC, millisecond
+    precision; a timestamp merges only with timestamps."""
+    import datetime
+
+    h = native.host()
+    for tok, want in TS_CASES.items():
+        got = h.csv_parse_timestamp(tok)
+        if want is None:
+            assert got is None, tok
+        else:
+            ref = datetime.datetime(*want) - datetime.datetime(1970, 1, 1)
+            assert got == (ref.days * 86400 + ref.seconds) * 1_000_000 + ref.microseconds, tok
+            assert h.csv_infer_field(tok) == 7, tok
+    assert h.csv_merge_types(7, 7) == 7 and h.csv_merge_types(7, 0) == 7
+    assert h.csv_merge_types(7, 4) == 6 and h.csv_merge_types(1, 7) == 6 and h.csv_merge_types(7, 5) == 6
+    assert merge_type_mask((1 << 7) | 1) == 7 and merge_type_mask((1 << 7) | (1 << 4)) == 6
+    n, cols = _host(b"2019-01-01,1\n2019-02-01 10:00:00.5,2019-01-01\n,x")
+    assert [c[1] for c in cols] == [7, 6]
+    assert list(cols[0][3]) == [1, 1, 0]
+
+
+def test_timestamp_column_collect_and_show(cpu_session, tmp_path):
+    """A timestamp column through the reader (host scanner on CPU): collect() gives datetimes,
+    show() prints Spark's ``yyyy-MM-dd HH:mm:ss[.fff]``."""
+    import datetime
+
+    p = tmp_path / "ts.csv"
+    p.write_bytes(b"2019-01-01,1\r2019-06-15 08:30:00.25,2\r,3")
+    df = cpu_session.read().option("inferSchema", "true").csv(str(p))
+    assert df.dtypes == [("_c0", "timestamp"), ("_c1", "int")]
+    rows = df.collect()
+    assert rows[0][0] == datetime.datetime(2019, 1, 1) and rows[2][0] is None
+    assert rows[1][0] == datetime.datetime(2019, 6, 15, 8, 30, 0, 250000)
+    out = df._show_string(20, 20) if hasattr(df, "_show_string") else None
+    if out is None:
+        from net.jgp.labs.sparkdq4ml_amd.sql.dataframe import _cell_str
+
+        assert _cell_str(rows[1][0]) == "2019-06-15 08:30:00.25" and _cell_str(rows[0][0]) == "2019-01-01 00:00:00"
+    else:
+        assert "2019-06-15 08:30:00.25" in out and "2019-01-01 00:00:00|" in out
+
+
+@pytest.mark.gpu
+def test_device_timestamps_match_host():
+    """The device parser's timestamps (csv_parse_dev.h csv_parse_ts) equal the host scanner's:
+    every TS_CASES token's class, a 5000-row column of mixed formats (inferred, then under a user
+    schema), values in microseconds."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from net.jgp.labs.sparkdq4ml_amd.ops import csvscan
+
+    for tok in TS_CASES:
+        data = f"{tok},1\n{tok},2".encode()
+        t = csvscan.scan_device(data, device="cuda")
+        _, cols = _host(data)
+        assert t is not None and csvscan.type_code_of(t.schema.fields[0].dataType) == cols[0][1], tok
+    valid = [t for t, w in TS_CASES.items() if w is not None]
+    data = "\n".join(f"{valid[i % len(valid)]},{i}" if i % 7 else f",{i}" for i in range(5000)).encode()
+    _, cols = _host(data)
+    assert cols[0][1] == csvscan.CT_TIMESTAMP
+    for t in (csvscan.scan_device(data, device="cuda"),
+              csvscan.scan_device(data, device="cuda", user_types=[csvscan.CT_TIMESTAMP, csvscan.CT_INT])):
+        assert t is not None and csvscan.type_code_of(t.schema.fields[0].dataType) == csvscan.CT_TIMESTAMP
+        c = t.columns[0]
+        ok = cols[0][3].astype(bool)
+        assert np.array_equal(c.valid_mask().cpu().numpy(), ok)
+        np.testing.assert_array_equal(c.values.cpu().numpy()[ok], np.asarray(cols[0][2])[ok])
