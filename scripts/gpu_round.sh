@@ -109,6 +109,9 @@ for s in $STEPS; do
     syrkbench) step syrkbench 600 python scripts/syrk_bench.py ;;
     kprofsyrk) (export TMPDIR=/tmp CASES="1024:2000000:f64:fp64" REPS=2; step kprofsyrk 600 rocprofv3 --kernel-trace --stats -d gpurun_out/kprofsyrk -o run --output-format csv -- python scripts/syrk_bench.py) || exit $? ;;
     owlqn) step owlqn 600 python scripts/owlqn_bench.py ;;
+    csvstr) step csvstr 600 python scripts/csv_strings_bench.py --rows ${CSVSTR_ROWS:-1e7} ;;
+    pipedepth) for r in 1 2; do for m in 2 3 4; do
+            step pipedepth_${m}_r${r} 300 env DQ4ML_FIT_PIPELINE=$m python bench.py --steps 200 --warmup 20 --rows 1.25e7 || exit $?; done; done ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" ;;
     bench) step bench 600 python bench.py --steps 20 --warmup 3 ;;
     benchasync) step benchasync 600 python bench.py --steps 20 --warmup 3 --async ;;
