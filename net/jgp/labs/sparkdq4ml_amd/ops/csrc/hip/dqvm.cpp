@@ -89,4 +89,19 @@ void rtc_launch(int64_t handle, int grid, int block, void* const* ptrs_dev, int6
   DQ_HIP_CHECK(hipModuleLaunchKernel(fn, grid, 1, 1, block, 1, 1, 0, st, args, nullptr));
 }
 
+void rtc_launch_args(int64_t handle, int grid, int block, const int64_t* ptrs_host, int nptr, int64_t n,
+                     hipStream_t st) {
+  if (nptr < 1 || nptr * 8 + 8 > 4096) throw std::invalid_argument("rtc_launch_args: pointer slots do not fit the kernarg segment");
+  hipFunction_t fn;
+  {
+    std::lock_guard<std::mutex> g(g_mu);
+    if (handle < 0 || handle >= (int64_t)g_mods.size()) throw std::invalid_argument("rtc_launch_args: bad handle");
+    fn = g_mods[handle].fn;
+  }
+  long long nn = (long long)n;
+  // the struct argument's bytes are read from ptrs_host when the launch is enqueued
+  void* args[] = {const_cast<int64_t*>(ptrs_host), &nn};
+  DQ_HIP_CHECK(hipModuleLaunchKernel(fn, grid, 1, 1, block, 1, 1, 0, st, args, nullptr));
+}
+
 }  // namespace dq4ml

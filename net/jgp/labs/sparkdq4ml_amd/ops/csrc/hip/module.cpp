@@ -429,6 +429,12 @@ PYBIND11_MODULE(_dq4ml_hip, m) {
     int64_t h = rtc_compile(src, entry, &log);
     return py::make_tuple(h, log);
   });
+  m.def("rtc_launch_args", [](int64_t handle, int grid, int block, py::buffer ptrs, int64_t n, uintptr_t stream) {
+    py::buffer_info bi = ptrs.request();  // a contiguous int64 array of the pointer slots
+    if (bi.itemsize != 8 || bi.ndim != 1 || (bi.ndim == 1 && bi.strides[0] != 8))
+      throw std::invalid_argument("rtc_launch_args: ptrs must be a contiguous 1-d int64 array");
+    rtc_launch_args(handle, grid, block, static_cast<const int64_t*>(bi.ptr), (int)bi.size, n, as_stream(stream));
+  });
   m.def("rtc_launch", [](int64_t handle, int grid, int block, uintptr_t ptrs_dev, int64_t n, uintptr_t stream) {
     rtc_launch(handle, grid, block, P<void* const>(ptrs_dev), n, as_stream(stream));
   });

@@ -475,10 +475,11 @@ def _kernel_source(g: _Gen) -> str:
     use = "".join(f"        const {ct} {v} = {v}_a[u];\n" for ct, v, _, _ in g.loads)
     body = "\n".join("    " + ln for ln in g.lines).replace("P[", "p[") + "\n" + "".join(
         f"        (({t}*)p[{s}])[r] = ({t})({v});\n" for t, v, s in g.stores)
-    return (f'extern "C" __global__ __launch_bounds__(256) void {ENTRY}(void* const* P, long long n) {{\n'
+    return (ptr_struct(ns) +
+            f'extern "C" __global__ __launch_bounds__(256) void {ENTRY}(const DqPtrs P, long long n) {{\n'
             f"  void* p[{ns}];\n"
             f"#pragma unroll\n"
-            f"  for (int i = 0; i < {ns}; ++i) p[i] = P[i];\n"
+            f"  for (int i = 0; i < {ns}; ++i) p[i] = P.v[i];\n"
             f"  const long long stride = (long long)gridDim.x * blockDim.x;\n"
             f"  for (long long r0 = (long long)blockIdx.x * blockDim.x + threadIdx.x; r0 < n; r0 += {U} * stride) {{\n"
             f"    bool live_a[{U}];\n{decl}"
@@ -496,6 +497,24 @@ def _kernel_source(g: _Gen) -> str:
             f"      }}\n"
             f"    }}\n"
             f"  }}\n}}\n")
+
+
+# The generated kernels take their pointer slots BY VALUE (a struct in the kernel-argument segment,
+# read with scalar loads): no per-launch pointer table to upload (a pinned staging copy + an H2D
+# copy per action, round 3) and no global loads of it in the kernel prologue.  The kernarg segment
+# holds 4 KiB: chains with more slots do not fuse.
+MAX_SLOTS = 480
+
+
+def ptr_struct(ns: int) -> str:
+    if ns > MAX_SLOTS:
+        raise Unfusable("too many pointer slots for the kernel-argument segment")
+    return f"struct DqPtrs {{ void* v[{max(ns, 1)}]; }};\n"
+
+
+def launch(h, handle, grid: int, ptr_list, n: int, stream: int):
+    """Launch a generated kernel (``rtc_handle``) with its pointer slots by value."""
+    h.rtc_launch_args(int(handle), int(grid), 256, np.asarray(ptr_list, dtype=np.int64), int(n), int(stream))
 
 
 VEC_ROWS = int(os.environ.get("DQ4ML_DQ_ROWS", "4"))  # consecutive rows per thread, vector form
@@ -533,11 +552,11 @@ def _kernel_source_vec(g: _Gen, V: int = VEC_ROWS) -> str:
     ost = "".join(f"    *({_vec_t(t, V)}*)(({_VEC_BASE[t]}*)p[{s}] + r0) = o{s};\n" for t, _, s in g.stores)
     tail_ld = "".join(f"    const {ct} {v} = ({ct})((const {st}*)p[{s}])[r];\n" for ct, v, st, s in g.loads)
     tail_st = "".join(f"    (({t}*)p[{s}])[r] = ({t})({v});\n" for t, v, s in g.stores)
-    return (_vec_types(V) +
-            f'extern "C" __global__ __launch_bounds__(256) void {ENTRY}(void* const* P, long long n) {{\n'
+    return (_vec_types(V) + ptr_struct(ns) +
+            f'extern "C" __global__ __launch_bounds__(256) void {ENTRY}(const DqPtrs P, long long n) {{\n'
             f"  void* p[{ns}];\n"
             f"#pragma unroll\n"
-            f"  for (int i = 0; i < {ns}; ++i) p[i] = P[i];\n"
+            f"  for (int i = 0; i < {ns}; ++i) p[i] = P.v[i];\n"
             f"  const long long stride = (long long)gridDim.x * blockDim.x;\n"
             f"  const long long gt = (long long)blockIdx.x * blockDim.x + threadIdx.x;\n"
             f"  const long long nq = n / {V};\n"
@@ -692,15 +711,12 @@ def try_execute_fused(plan, session) -> Optional[Table]:
     ptr_list, outs, sel_out, keep = cp.bind(base, err)
     vec = all(q % (8 * VEC_ROWS) == 0 for q in ptr_list)  # whole allocations: the V-consecutive-rows form
     handle = rtc_handle(h, cp, cp.src[1] if vec else cp.src[0], ENTRY, 1 if vec else 0)
-    from .device import _h2d
-
-    ptrs = _h2d(np.asarray(ptr_list, dtype=np.int64), base.device)  # no host-device sync
     n = base.nrows
     grid = int(max(1, min((n + 256 * VEC_ROWS - 1) // (256 * VEC_ROWS) if vec else (n + 255) // 256, GRID_CAP)))
     from ..utils import tracing
 
     with tracing.span("dq_fused"):
-        h.rtc_launch(int(handle), grid, 256, ptrs.data_ptr(), int(n), torch.cuda.current_stream().cuda_stream)
+        launch(h, handle, grid, ptr_list, int(n), torch.cuda.current_stream().cuda_stream)
     tracing.add_rows("dq_fused", n)
     STATS["fused_launches"] += 1
     checks = []

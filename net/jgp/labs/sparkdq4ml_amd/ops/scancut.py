@@ -39,7 +39,6 @@ from __future__ import annotations
 import os
 from typing import Optional
 
-import numpy as np
 import torch
 
 __all__ = ["applicable", "kernel_source", "try_cut_gram", "STATS", "ENTRY"]
@@ -341,6 +340,7 @@ def kernel_source(g, kinds, used, opts: dict, H: int, slots: dict, d: int, term:
     """Source of the cutter kernel and its ``_Shape``.  ``term``: the file's one terminator byte
     (13 CR, 10 LF; ``crlf``: every CR is followed by LF, which then opens the next row and is
     skipped); ``min_line``: the shortest line, sizing the delimiter array and the row tile."""
+    from .dqvm import ptr_struct
     from .scanfuse import _gram_code, header_text
 
     C = len(kinds)
@@ -569,10 +569,10 @@ __device__ __forceinline__ void dq_fetch(const DQG unsigned char* ab, long long 
   }}
 }}
 
-extern "C" __global__ {lb} void {ENTRY}(void* const* P, long long n) {{
+{ptr_struct(NS)}extern "C" __global__ {lb} void {ENTRY}(const DqPtrs P, long long n) {{
   void* p[{NS}];
 #pragma unroll
-  for (int i = 0; i < {NS}; ++i) p[i] = P[i];
+  for (int i = 0; i < {NS}; ++i) p[i] = P.v[i];
   const DQG unsigned char* __restrict__ b = (const DQG unsigned char*)p[{slots['buf']}];
   const long long nwin = (long long)p[{slots['nwin']}];
   const bool trailing = (long long)p[{slots['trailing']}] != 0;
@@ -849,11 +849,6 @@ def try_cut_gram(chain, rel, d: int):
     """Launch the cutter for the Gram action (``scanfuse.try_fused_gram``'s chain with the
     features as ``__gx<i>`` and the label as ``__gy``).  Returns (flat statistics, err, vflag,
     stream) or None when the facts / chain do not allow it."""
-    from . import native
-    from .device import _h2d
-    from .scanfuse import _scan_stream  # noqa: F401 - same stream policy as the per-line kernel
-    from ..utils import tracing
-
     cp = _compile(chain, rel, d)
     if cp is None:
         return None
@@ -864,7 +859,6 @@ def launch_cut(cp, rel, d: int):
     """One launch of the compiled cutter ``cp`` over ``rel``'s device bytes (the part of
     ``try_cut_gram`` a replayed action repeats)."""
     from . import native
-    from .device import _h2d
     from ..utils import tracing
 
     f = rel.fused
@@ -892,13 +886,12 @@ def launch_cut(cp, rel, d: int):
             ptrs.append(x.data_ptr() if torch.is_tensor(x) else int(x))
         else:
             raise AssertionError(f"cut plan: unbound slot {tag}")
-    from .dqvm import rtc_handle
+    from .dqvm import launch, rtc_handle
 
     handle = rtc_handle(h, cp, cp.src, ENTRY)
-    pt = _h2d(np.asarray(ptrs, dtype=np.int64), dev)
     stream = torch.cuda.current_stream(dev)
     with tracing.span("csv_cut_gram"):
-        h.rtc_launch(int(handle), grid, 256, pt.data_ptr(), n, stream.cuda_stream)
+        launch(h, handle, grid, ptrs, n, stream.cuda_stream)
         tot = gpart.sum(0)
         flat = torch.cat([tot[:1].expand(3), tot[1:]])
     tracing.add_rows("csv_cut_gram", int(f["nlines"]))

@@ -28,7 +28,6 @@ from __future__ import annotations
 import os
 from typing import Optional
 
-import numpy as np
 import torch
 
 __all__ = ["kernel_source", "ENTRY", "WINDOW", "head_bytes", "STATS"]
@@ -225,6 +224,8 @@ def kernel_source(g, kinds, nullable, used, opts: dict, strict: bool, head: int,
     to register sums of the f64 normal-equation statistics, and each block writes its
     ``gram_width(d)`` sums (wave shuffles + LDS, fixed order) to ``p[slots['gpart']]`` at its
     window index."""
+    from .dqvm import ptr_struct
+
     ncols = len(kinds)
     ns = len(g.ptrs)
     nv = list(opts.get("null_value", "").encode())
@@ -381,10 +382,10 @@ __device__ __forceinline__ void dq_row(PB B, IT bias, IT start, IT end, long lon
 {body}
 {stores}}}
 {swar_row}
-extern "C" __global__ __launch_bounds__(256) {_wpe(fast_only)}void {ENTRY}(void* const* P, long long n) {{
+{ptr_struct(ns)}extern "C" __global__ __launch_bounds__(256) {_wpe(fast_only)}void {ENTRY}(const DqPtrs P, long long n) {{
   void* p[{ns}];
 #pragma unroll
-  for (int i = 0; i < {ns}; ++i) p[i] = P[i];
+  for (int i = 0; i < {ns}; ++i) p[i] = P.v[i];
   const DQG unsigned char* __restrict__ b = (const DQG unsigned char*)p[{slots['buf']}];
   const DQG long long* __restrict__ offs = (const DQG long long*)p[{slots['offs']}];
   const long long nalloc = (long long)p[{slots['nalloc']}];
@@ -693,7 +694,6 @@ def _launch(cp, nodes, rel, extra: dict, own_stream: bool = True):
     scan stream, compute stream) after checking a raised UDF error.  ``own_stream``: on the
     scan side stream (else on the compute stream, in order with the caller's work)."""
     from . import dqvm, native
-    from .device import _h2d
 
     f = rel.fused
     h = native.hip()
@@ -719,11 +719,10 @@ def _launch(cp, nodes, rel, extra: dict, own_stream: bool = True):
             extra["gpart"] = scalars["gpart"] = torch.zeros(nb, gram_width(cp.gram), dtype=torch.float64, device=dev)
         ptr_list, outs, sel_out = cp.bind(nalloc, dev, scalars, err)
         handle = dqvm.rtc_handle(h, cp, cp.src, ENTRY)
-        ptrs = _h2d(np.asarray(ptr_list, dtype=np.int64), dev)
         from ..utils import tracing
 
         with tracing.span("csv_scan_dq_fused"):
-            h.rtc_launch(int(handle), nb, 256, ptrs.data_ptr(), n, stream)
+            dqvm.launch(h, handle, nb, ptr_list, n, stream)
     tracing.add_rows("csv_scan_dq_fused", nalloc)
     STATS["fused_scans"] += 1
     return outs, sel_out, err, vflag, side, cur
