@@ -81,6 +81,12 @@ void gram_reduce(int mode, const double* partials, int blocks, int d, double* ou
 // (exact algebra for any fixed s: DQ selections and weights are already in the sums)
 void stats_unshift(double* flat, const float* shift, int d, hipStream_t st);
 
+// The fused CSV scans' per-window statistics part[rows][gw] (gw = 3 + 2d + d(d+1)/2: live count,
+// Σy, Σy², Σx, Σxy, packed-upper Σxx) -> the flat gram_stats layout [n, n, n, Σy, Σy², ...]
+// (unit weights), every column summed in one fixed order: one launch instead of a column-sum
+// kernel plus a concatenation (ops/scanfuse.py, ops/scancut.py)
+void gram_window_fold(const double* part, int64_t rows, int gw, double* flat, hipStream_t st);
+
 // LDS-DMA streamed tall kernels (gram_stream.hip): GRAM_F64 on f64/f32 features, GRAM_F32
 // (exact-f32 MFMA) on f32 features.  gram_stream_ok: operand dtypes/alignment the DMA path needs.
 bool gram_stream_ok(int mode, const GramArgs& a);

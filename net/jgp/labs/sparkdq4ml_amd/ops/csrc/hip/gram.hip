@@ -1048,6 +1048,32 @@ __global__ __launch_bounds__(1024) void gram_fold_kernel(const double* __restric
   }
 }
 
+// one block per statistic column: thread t sums rows t, t + 256, ... in order, then a fixed LDS
+// tree over the 256 partial sums (deterministic run to run)
+__global__ __launch_bounds__(256) void window_fold_kernel(const double* __restrict__ part, int64_t rows, int gw,
+                                                          double* __restrict__ flat) {
+  __shared__ double red[256];
+  const int c = blockIdx.x, t = threadIdx.x;
+  double s = 0.0;
+  for (int64_t r = t; r < rows; r += 256) s += part[r * gw + c];
+  red[t] = s;
+  __syncthreads();
+#pragma unroll
+  for (int w = 128; w >= 1; w >>= 1) {
+    if (t < w) red[t] += red[t + w];
+    __syncthreads();
+  }
+  if (t == 0) {
+    if (c == 0) {
+      flat[0] = red[0];
+      flat[1] = red[0];
+      flat[2] = red[0];
+    } else {
+      flat[c + 2] = red[0];
+    }
+  }
+}
+
 // feature-major [d, ld] (any dtype) -> MFMA-fragment-ordered bf16 tiles (see gram.h)
 template <typename TS>
 __global__ __launch_bounds__(256) void tile_bf16_kernel(const TS* __restrict__ X, int64_t ld, int d, int64_t n,
@@ -1337,6 +1363,12 @@ int gram_plan_blocks(int mode, int d, int64_t n, int xdt, int xmode) {
   int64_t want = (nsuper + 4 * wpb - 1) / (4 * wpb);
   if (want < 1) want = 1;
   return (int)(want < full ? want : full);
+}
+
+void gram_window_fold(const double* part, int64_t rows, int gw, double* flat, hipStream_t st) {
+  if (gw < 1 || rows < 0) throw std::invalid_argument("gram_window_fold: bad shape");
+  hipLaunchKernelGGL(window_fold_kernel, dim3(gw), dim3(256), 0, st, part, rows, gw, flat);
+  DQ_HIP_CHECK(hipGetLastError());
 }
 
 void gram_reduce(int mode, const double* partials, int blocks, int d, double* out, hipStream_t st) {

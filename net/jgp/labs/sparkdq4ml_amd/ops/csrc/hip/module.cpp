@@ -167,6 +167,9 @@ PYBIND11_MODULE(_dq4ml_hip, m) {
   m.def("gram_reduce", [](int mode, uintptr_t partials, int blocks, int d, uintptr_t out, uintptr_t stream) {
     gram_reduce(mode, P<const double>(partials), blocks, d, P<double>(out), as_stream(stream));
   });
+  m.def("gram_window_fold", [](uintptr_t part, int64_t rows, int gw, uintptr_t flat, uintptr_t stream) {
+    gram_window_fold(P<const double>(part), rows, gw, P<double>(flat), as_stream(stream));
+  });
   m.def("stats_unshift", [](uintptr_t flat, uintptr_t shift, int d, uintptr_t stream) {
     stats_unshift(P<double>(flat), P<const float>(shift), d, as_stream(stream));
   });

@@ -859,7 +859,9 @@ def launch_cut(cp, rel, d: int):
     """One launch of the compiled cutter ``cp`` over ``rel``'s device bytes (the part of
     ``try_cut_gram`` a replayed action repeats)."""
     from . import native
+    from ..runtime import faststream
     from ..utils import tracing
+    from .scanfuse import window_fold
 
     f = rel.fused
     h = native.hip()
@@ -867,10 +869,12 @@ def launch_cut(cp, rel, d: int):
     buf, n = f["buf"], int(f["n"])
     nwin = n_windows(buf.data_ptr(), n)
     grid = _grid(h, cp.per_cu, nwin)
-    err = torch.zeros(1, dtype=torch.int32, device=dev)
-    vflag = torch.zeros(1, dtype=torch.int32, device=dev)
     gw = gram_width(d)
-    gpart = torch.empty(grid * cp.rg, gw, dtype=torch.float64, device=dev)
+    # one zeroed allocation: [err, vflag | per-block partials]
+    z = torch.zeros(1 + grid * cp.rg * gw, dtype=torch.int64, device=dev)
+    ev = z[:1].view(torch.int32)
+    err, vflag = ev[0:1], ev[1:2]
+    gpart = z[1:].view(torch.float64).view(grid * cp.rg, gw)
     scalars = {"buf": buf, "nwin": nwin, "trailing": int(f["trailing"]), "vflag": vflag, "gpart": gpart}
     if any(t[0] == "dbg" for t in cp.recipe):
         LAST_STAMPS["buf"] = scalars["dbg"] = torch.zeros(grid, 8, dtype=torch.int64, device=dev)
@@ -889,11 +893,10 @@ def launch_cut(cp, rel, d: int):
     from .dqvm import launch, rtc_handle
 
     handle = rtc_handle(h, cp, cp.src, ENTRY)
-    stream = torch.cuda.current_stream(dev)
+    stream = faststream.current(faststream.dev_index(dev))
     with tracing.span("csv_cut_gram"):
         launch(h, handle, grid, ptrs, n, stream.cuda_stream)
-        tot = gpart.sum(0)
-        flat = torch.cat([tot[:1].expand(3), tot[1:]])
+        flat = window_fold(gpart, stream)
     tracing.add_rows("csv_cut_gram", int(f["nlines"]))
     STATS["cut_grams"] += 1
     return flat, err, vflag, cp

@@ -694,6 +694,7 @@ def _launch(cp, nodes, rel, extra: dict, own_stream: bool = True):
     scan stream, compute stream) after checking a raised UDF error.  ``own_stream``: on the
     scan side stream (else on the compute stream, in order with the caller's work)."""
     from . import dqvm, native
+    from ..runtime import faststream
 
     f = rel.fused
     h = native.hip()
@@ -702,21 +703,25 @@ def _launch(cp, nodes, rel, extra: dict, own_stream: bool = True):
     # stage pipeline: the scan runs on its own stream and depends only on the
     # HBM-resident input bytes, so action k+1's scan overlaps action k's Gram / fit tail on the
     # compute stream; the compute stream waits for this scan's event before its consumers
-    cur = torch.cuda.current_stream(dev)
-    side = _scan_stream(dev) if own_stream and os.environ.get("DQ4ML_SCAN_STREAM", "1") != "0" else cur
-    with torch.cuda.stream(side):
+    # (faststream: no per-call device resolution on this per-action path, profiles/r4_host_issue.md)
+    cur = faststream.current(faststream.dev_index(dev))
+    side = _scan_stream(dev) if own_stream and env(b"DQ4ML_SCAN_STREAM") != b"0" else cur
+    with faststream.use(side):
         stream = side.cuda_stream
         nb = int(h.csv_count_blocks(n))
-        if cp.lookback:  # single pass: zeroed look-back status + ticket counters
-            offs = torch.zeros(nb + TICKET_WORDS, dtype=torch.int64, device=dev)
-        else:  # two passes: per-window terminator counts -> exclusive offsets
-            offs = torch.empty(nb + 1, dtype=torch.int64, device=dev)
+        # ONE zeroed scratch allocation: [offs | err, vflag | Gram partials]; offs is the
+        # look-back status + ticket counters (single pass) or the per-window counts (two passes)
+        no = nb + TICKET_WORDS if cp.lookback else nb + 1
+        gw = gram_width(cp.gram) if cp.gram else 0
+        z = torch.zeros(no + 1 + nb * gw, dtype=torch.int64, device=dev)
+        offs = z[:no]
+        if not cp.lookback:
             h.csv_line_ends(buf.data_ptr(), n, offs.data_ptr(), 0, stream)
-        err = torch.zeros(1, dtype=torch.int32, device=dev)
-        vflag = torch.zeros(1, dtype=torch.int32, device=dev)
+        ev = z[no:no + 1].view(torch.int32)
+        err, vflag = ev[0:1], ev[1:2]
         scalars = {"buf": buf, "offs": offs, "nalloc": nalloc, "trailing": int(f["trailing"]), "vflag": vflag}
         if cp.gram:
-            extra["gpart"] = scalars["gpart"] = torch.zeros(nb, gram_width(cp.gram), dtype=torch.float64, device=dev)
+            extra["gpart"] = scalars["gpart"] = z[no + 1:].view(torch.float64).view(nb, gw)
         ptr_list, outs, sel_out = cp.bind(nalloc, dev, scalars, err)
         handle = dqvm.rtc_handle(h, cp, cp.src, ENTRY)
         from ..utils import tracing
@@ -882,13 +887,39 @@ _ROUTE_ENV = ("DQ4ML_SCAN_GRAM", "DQ4ML_SCAN_CUT", "DQ4ML_CUT_MIN_LINE", "DQ4ML_
               "DQ4ML_CUT_STAMPS", "DQ4ML_SCAN_STREAM", "DQ4ML_SCAN_NT", "DQ4ML_SCAN_TICKET", "DQ4ML_FUSE_ROUTES")
 
 
+_ENV_DATA = getattr(os.environ, "_data", None)  # the process environment as bytes (CPython)
+_ROUTE_ENV_B = tuple(k.encode() for k in _ROUTE_ENV)
+
+
+def env(key: bytes):
+    """``os.environ`` lookup of a bytes key without the str encode / decode round trip (the
+    per-action knob reads of the replay path); None when unset."""
+    if _ENV_DATA is None:
+        v = os.environ.get(key.decode())
+        return None if v is None else v.encode()
+    return _ENV_DATA.get(key)
+
+
 def route_key(plan_key, features_col: str, label_col: str, session):
     """Replay key of a fused-scan fit: the action's plan structure, the columns, the session conf
     and the scan knobs (None: not replayable)."""
-    if plan_key is None or os.environ.get("DQ4ML_FUSE_ROUTES", "1") == "0":
+    if plan_key is None or env(b"DQ4ML_FUSE_ROUTES") == b"0":
         return None
-    return (plan_key, features_col, label_col, tuple(os.environ.get(k) for k in _ROUTE_ENV),
+    return (plan_key, features_col, label_col, tuple(env(k) for k in _ROUTE_ENV_B),
             getattr(session, "device", None))
+
+
+def window_fold(gpart, side):
+    """The per-window partials [rows, gw] -> the flat gram_stats layout [n, Σw, Σw², Σwy, Σwy²,
+    Σwx, Σwxy, packed-upper Σwxx] (unit weights: Σw = Σw² = n), fixed order, on ``side``."""
+    from . import native
+    from ..runtime import faststream
+
+    with faststream.use(side):
+        flat = torch.empty(gpart.shape[1] + 2, dtype=torch.float64, device=gpart.device)
+        native.hip().gram_window_fold(gpart.data_ptr(), gpart.shape[0], gpart.shape[1], flat.data_ptr(),
+                                      side.cuda_stream)
+    return flat
 
 
 def replay(key, plan, session) -> Optional["FusedGram"]:
@@ -925,16 +956,11 @@ def _run_line_gram(cp, chain, p, d) -> "FusedGram":
     # kernel trace) and holds the pipeline longer than running alone between two scans; with
     # nothing left to overlap, a side stream would only add cross-queue waits
     _, _, err, vflag, side, cur = _launch(cp, chain, p, extra, own_stream=False)
-    gpart = extra["gpart"]
-    with torch.cuda.stream(side):
-        # fixed-order column sums of the per-window partials -> the gram_stats layout
-        # [n, Σw, Σw², Σwy, Σwy², Σwx, Σwxy, packed-upper Σwxx] (unit weights: Σw = Σw² = n)
-        tot = gpart.sum(0)
-        flat = torch.cat([tot[:1].expand(3), tot[1:]])
+    flat = window_fold(extra["gpart"], side)
     if side is not cur:
         cur.wait_stream(side)
-        for t in (err, vflag, gpart, tot, flat):
-            t.record_stream(cur)
+        for t in (err, flat):
+            t.record_stream(cur)  # (err, vflag and the partials share one allocation)
     checks = [_fact_check(p, vflag)] + ([_udf_error_check(chain, err)] if cp.has_raise else [])
     STATS["fused_grams"] += 1
     return FusedGram(flat, d, [c for c in checks if c is not None], int(p.fused["nlines"]))
@@ -987,9 +1013,8 @@ def _streamed_gram(chain, rel, d: int) -> Optional[FusedGram]:
             raising = ccp.has_raise
         else:
             extra = {}
-            _, _, err, vflag, _side, _cur = _launch(cp, chain, crel, extra, own_stream=False)
-            tot = extra["gpart"].sum(0)
-            flat = torch.cat([tot[:1].expand(3), tot[1:]])
+            _, _, err, vflag, side, _cur = _launch(cp, chain, crel, extra, own_stream=False)
+            flat = window_fold(extra["gpart"], side)
             raising = cp.has_raise
         acc = flat.clone() if acc is None else acc.add_(flat)
         checks.append(_fact_check(rel, vflag))

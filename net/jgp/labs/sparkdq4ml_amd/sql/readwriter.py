@@ -34,6 +34,7 @@ __all__ = ["DataFrameReader", "DataFrameWriter", "csv_code_to_type"]
 # load() of an unchanged cached CSV file: key -> (lazy relation template, file identity, cache entry)
 _LOADS: dict = {}
 _LOAD_SERIAL = __import__("itertools").count(1)
+_REALPATH: dict = {}
 _LOAD_CONF = ("dq4ml.csv.deviceThresholdBytes", "dq4ml.csv.deviceCache", "dq4ml.csv.fuseScan", "dq4ml.chunkBytes",
               "dq4ml.csv.streamThresholdBytes", "dq4ml.shardInput")
 
@@ -219,7 +220,12 @@ class DataFrameReader:
         conf = self._session.conf
         ck = tuple(conf.get(k, None) for k in _LOAD_CONF)
         sch = self._schema.simpleString() if self._schema else None
-        key = (os.path.realpath(files[0]), tuple(sorted(self._options.items())), sch, ck, str(dev))
+        rp = _REALPATH.get(files[0])
+        if rp is None:  # (a path's symlinks are resolved once per process; the stat above is per load)
+            if len(_REALPATH) >= 1024:
+                _REALPATH.clear()
+            rp = _REALPATH[files[0]] = os.path.realpath(files[0])
+        key = (rp, tuple(sorted(self._options.items())), sch, ck, str(dev))
         return key, (st.st_size, st.st_mtime_ns, st.st_ino)
 
     def csv(self, path, schema=None, sep=None, header=None, inferSchema=None, **kw):

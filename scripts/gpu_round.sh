@@ -134,6 +134,9 @@ for s in $STEPS; do
     csvhost) step csvhost 600 env DQ4ML_BENCH_CPROFILE=gpurun_out/csv.prof python benchmarks/bench_csv_pipeline.py --rows ${CSV_ROWS:-1e7} --steps 50 --warmup 5 --json-out gpurun_out/csvhost.json &&
        python -c "import pstats; pstats.Stats('gpurun_out/csv.prof').sort_stats('tottime').print_stats(45)" > gpurun_out/csvprof_tot.txt &&
        python -c "import pstats; pstats.Stats('gpurun_out/csv.prof').sort_stats('cumulative').print_stats(60)" > gpurun_out/csvprof_cum.txt ;;
+    csvhost2) step csvhost2 600 env DQ4ML_BENCH_CPROFILE=gpurun_out/csv2.prof python benchmarks/bench_csv_pipeline.py --rows ${CSV_ROWS:-1e6} --steps 500 --warmup 20 --json-out gpurun_out/csvhost2.json &&
+       python -c "import pstats; pstats.Stats('gpurun_out/csv2.prof').sort_stats('tottime').print_stats(60)" > gpurun_out/csv2prof_tot.txt &&
+       python -c "import pstats; pstats.Stats('gpurun_out/csv2.prof').sort_stats('cumulative').print_stats(80)" > gpurun_out/csv2prof_cum.txt ;;
     shapeprobe) step shapeprobe 180 ./scripts/mfma_shape_probe 20000 &&
        (export TMPDIR=/tmp; step shapepmc 120 timeout -s KILL 100 rocprofv3 --kernel-trace --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_BUSY_CYCLES -d gpurun_out/shapepmc -o run --output-format csv -- ./scripts/mfma_shape_probe 5000) || exit $? ;;
     mfmapeak) step mfmapeak 120 ./scripts/mfma_peak &&
