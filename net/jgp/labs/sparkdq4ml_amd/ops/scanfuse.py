@@ -949,7 +949,87 @@ def _remember(key, route, session):
     _ROUTES[key] = route
 
 
+class _GramLaunch:
+    """The per-action part of a Gram-mode per-line fused scan, resolved once per (plan, cached
+    bytes): every pointer slot is either constant (the HBM-resident input, scalars, unused row
+    outputs) or a fixed offset into the action's one zeroed scratch allocation, so an action is one
+    allocation, one pointer-array fill, the kernel launch and the window fold (the host-issue path
+    of a rebuilt lab action, ``profiles/r4_host_issue.md``)."""
+
+    def __init__(self, cp, rel):
+        import numpy as np
+
+        from . import dqvm, native
+
+        f = rel.fused
+        self.h = h = native.hip()
+        self.dev = f["device"]
+        buf, n, nalloc = f["buf"], int(f["n"]), int(f["nlines"])
+        self.key = (buf.data_ptr(), n, nalloc, bool(f["trailing"]))
+        self.n, self.nb = n, int(h.csv_count_blocks(n))
+        self.no = self.nb + TICKET_WORDS
+        self.gw = gram_width(cp.gram)
+        self.words = self.no + 1 + self.nb * self.gw
+        scratch = {"offs": 0, "vflag": 8 * self.no + 4, "gpart": 8 * (self.no + 1)}
+        tmpl, zi, zo = [], [], []
+        for tag in cp.recipe:
+            k = tag[0]
+            if k in ("sel", "out", "outvalid", "selout"):
+                v = 0
+            elif k == "err":
+                zi.append(len(tmpl))
+                zo.append(8 * self.no)
+                v = 0
+            elif k in scratch:
+                zi.append(len(tmpl))
+                zo.append(scratch[k])
+                v = 0
+            elif k == "buf":
+                v = buf.data_ptr()
+            elif k == "nalloc":
+                v = nalloc
+            elif k == "trailing":
+                v = int(f["trailing"])
+            else:
+                raise AssertionError(f"gram scan plan: unbound slot {tag}")
+            tmpl.append(v)
+        self.tmpl = np.asarray(tmpl, dtype=np.int64)
+        self.zi, self.zo = np.asarray(zi, dtype=np.int64), np.asarray(zo, dtype=np.int64)
+        # (the input's address is part of the key: the plan holds no reference to the bytes -- a
+        # launch reads the bytes of the relation it is called for, which the file cache owns)
+        self.handle = int(dqvm.rtc_handle(h, cp, cp.src, ENTRY))
+
+    def __call__(self):
+        """(flat statistics, err, vflag) of one launch on the current stream."""
+        from ..runtime import faststream
+        from ..utils import tracing
+
+        di = faststream.dev_index(self.dev)
+        z = torch.zeros(self.words, dtype=torch.int64, device=self.dev)
+        arr = self.tmpl.copy()
+        arr[self.zi] = self.zo + z.data_ptr()
+        stream = faststream.raw(di)
+        with tracing.span("csv_scan_dq_fused"):
+            self.h.rtc_launch_args(self.handle, self.nb, 256, arr, self.n, stream)
+        flat = torch.empty(self.gw + 2, dtype=torch.float64, device=self.dev)
+        self.h.gram_window_fold(z.data_ptr() + 8 * (self.no + 1), self.nb, self.gw, flat.data_ptr(), stream)
+        ev = z[self.no:self.no + 1].view(torch.int32)
+        tracing.add_rows("csv_scan_dq_fused", int(self.key[2]))
+        STATS["fused_scans"] += 1
+        return flat, ev[0:1], ev[1:2]
+
+
 def _run_line_gram(cp, chain, p, d) -> "FusedGram":
+    gl = getattr(cp, "_gram_launch", None)
+    f = p.fused
+    if cp.gram and cp.lookback:
+        key = (f["buf"].data_ptr(), int(f["n"]), int(f["nlines"]), bool(f["trailing"]))
+        if gl is None or gl.key != key:
+            gl = cp._gram_launch = _GramLaunch(cp, p)
+        flat, err, vflag = gl()
+        checks = [_fact_check(p, vflag)] + ([_udf_error_check(chain, err)] if cp.has_raise else [])
+        STATS["fused_grams"] += 1
+        return FusedGram(flat, d, [c for c in checks if c is not None], int(f["nlines"]))
     extra = {}
     # on the compute stream, after the previous action's fit tail: the one-workgroup solve
     # kernel co-running with a whole-GPU scan gets ~1/8 of a CU's issue slots (22 -> 727 us,
