@@ -210,6 +210,11 @@ class DeviceStringColumn(ColumnData):
     def n(self) -> int:
         return int(self.spans.numel())
 
+    def valid_mask(self, device=None) -> torch.Tensor:
+        if self.valid is not None:
+            return self.valid
+        return torch.ones(self.n, dtype=torch.bool, device=device if device is not None else self.spans.device)
+
     def index(self, idx: torch.Tensor) -> "ColumnData":
         if self._vals is not None:
             return ColumnData.index(self, idx)

@@ -685,3 +685,23 @@ def test_device_timestamps_match_host():
         ok = cols[0][3].astype(bool)
         assert np.array_equal(c.valid_mask().cpu().numpy(), ok)
         np.testing.assert_array_equal(c.values.cpu().numpy()[ok], np.asarray(cols[0][2])[ok])
+
+
+def test_device_string_column_moves_spans_until_read():
+    """``DeviceStringColumn`` (the device scan's string column): row selections move only the
+    spans, the validity mask needs no text, and the strings are built once, on first read."""
+    from net.jgp.labs.sparkdq4ml_amd.sql.table import DeviceStringColumn, Table
+    from net.jgp.labs.sparkdq4ml_amd.sql.types import StringType, StructField, StructType
+
+    data = b'ab,"c,d",x""y,\xc3\xa9'
+    fields = [(0, 2, 0), (3, 5, 1), (9, 4, 0), (14, 2, 0)]  # (fs, len, raw)
+    spans = torch.tensor([(fs << 25) | (raw << 24) | ln for fs, ln, raw in fields], dtype=torch.int64)
+    col = DeviceStringColumn(spans, None, data, {"quote": '"', "escape": "\\"})
+    assert col.n == 4 and bool(col.valid_mask().all()) and not col.materialized
+    sub = col.index(torch.tensor([3, 1]))
+    assert isinstance(sub, DeviceStringColumn) and not col.materialized
+    assert sub.values == ["é", "c,d"]
+    assert col.slice(0, 2).values == ["ab", "c,d"] and not col.materialized
+    assert col.values == ["ab", "c,d", 'x""y', "é"]  # (x""y is unquoted: its bytes as they stand)
+    t = Table(StructType([StructField("s", StringType(), True)]), [col], 4, torch.tensor([True, False, True, True]))
+    assert [r[0] for r in t.to_rows()] == ["ab", 'x""y', "é"]
