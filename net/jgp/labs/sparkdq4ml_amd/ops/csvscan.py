@@ -242,7 +242,7 @@ def type_code_of(dt) -> int:
     return CT_DOUBLE
 
 
-def _finish(parts, types, st, dev, hinted=False, data=None, opts=None):
+def _finish(parts, types, st, dev, hinted=False, data=None, opts=None, check=None):
     """Typed columns from per-chunk parse outputs under the merged types.  ``st``: the chunks'
     stats on the host.  Int / long / boolean values convert exactly from their f64 planes (the
     parser flags integers beyond 2^53 for the host path).  String columns (scanned as spans, always
@@ -265,7 +265,7 @@ def _finish(parts, types, st, dev, hinted=False, data=None, opts=None):
                 valid_l = [p[2][c, :p[0]] for _, p in live]
                 vv = torch.cat(valid_l) if len(valid_l) > 1 else valid_l[0].clone()
             fields.append(StructField(f"_c{c}", StringType(), True))
-            cols.append(DeviceStringColumn(spans, vv, data, opts))
+            cols.append(DeviceStringColumn(spans, vv, data, opts, check=check))
             continue
         vals_l = []
         for _, (nlines, dcols, _, _, _, _) in live:
@@ -388,7 +388,8 @@ STRICT_CODES = (CT_INT, CT_LONG, CT_DOUBLE, CT_BOOL, CT_STRING, CT_TIMESTAMP)
 def scan_device(data, sep: str = ",", infer: bool = True, device=None, ncols: Optional[int] = None,
                 sharded: bool = False, chunk_bytes: Optional[int] = None, pinned: Optional[torch.Tensor] = None,
                 device_data: Optional[torch.Tensor] = None, types_hint: Optional[list] = None,
-                opts: Optional[dict] = None, user_types: Optional[list] = None, _depth: int = 0):
+                opts: Optional[dict] = None, user_types: Optional[list] = None, _depth: int = 0,
+                source_check=None):
     """Parse ``data`` on the device.  Inputs larger than ``chunk_bytes`` stream through a
     double-buffered pinned staging ring: chunk k+1's host->device copy runs on a side stream while
     chunk k is parsed, chunks split on row boundaries, type masks OR-merged over
@@ -398,7 +399,9 @@ def scan_device(data, sep: str = ",", infer: bool = True, device=None, ncols: Op
     them with its cached file): the parser then stores every column as its type directly — no
     f64 plane to convert.  Inference still runs; a hint the masks contradict re-scans unhinted.
     String columns are scanned as spans, which needs the hint: a scan that finds a string column
-    without one re-scans once with the inferred types as the hint.
+    without one re-scans once with the inferred types as the hint.  ``source_check``: called before
+    their text is built from ``data`` when ``data`` is a map of a file the process does not own
+    (raises when the file changed since the scan).
 
     ``opts``: dialect (quote, escape, comment, trim_lead, trim_trail, null_value; see
     ``csv_parse_dev.h``).  ``user_types``: a user schema (lattice codes in STRICT_CODES): the
@@ -449,7 +452,7 @@ def scan_device(data, sep: str = ",", infer: bool = True, device=None, ncols: Op
             STATS["fallbacks"] += 1
             return None
         STATS["device_scans"] += 1
-        return _finish(parts, list(user_types), st, dev, hinted=True, data=data, opts=opts)
+        return _finish(parts, list(user_types), st, dev, hinted=True, data=data, opts=opts, check=source_check)
     types = _resolve_types(masks, int(st[:, 0].max()), sharded)
     if types is None:
         STATS["fallbacks"] += 1
@@ -464,13 +467,13 @@ def scan_device(data, sep: str = ",", infer: bool = True, device=None, ncols: Op
         STATS["hint_misses" if miss and hint is not None else "span_rescans"] = \
             STATS.get("hint_misses" if miss and hint is not None else "span_rescans", 0) + 1
         return scan_device(data, sep, infer, device, ncols, sharded, chunk_bytes, pinned, device_data,
-                           types if spans else None, opts, _depth=_depth + 1)
+                           types if spans else None, opts, _depth=_depth + 1, source_check=source_check)
     if miss or spans:
         STATS["fallbacks"] += 1
         return None
     STATS["device_scans"] += 1
     STATS["chunks"] = STATS.get("chunks", 0) + len(parts)
-    return _finish(parts, types, st, dev, hinted=hint is not None, data=data, opts=opts)
+    return _finish(parts, types, st, dev, hinted=hint is not None, data=data, opts=opts, check=source_check)
 
 
 def chunk_bounds(data: bytes, chunk_bytes: int):

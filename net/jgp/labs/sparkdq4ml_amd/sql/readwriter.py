@@ -112,6 +112,24 @@ def _split_header(data, sep: str, opts: dict):
     return None
 
 
+def _map_check(pf):
+    """For input read through a file map (``filecache.MappedFile``, ranges above the pinned cache):
+    a check run before a device string column builds its text from the map -- it raises if the
+    file changed since it was mapped (the bytes under a map are the file's own).  None for owned
+    copies (the pinned cache, plain reads)."""
+    if pf is None or getattr(pf, "host", None) is not None:
+        return None
+    path = pf.path
+    st = os.stat(path)
+    ident = (st.st_size, st.st_mtime_ns, st.st_ino)
+
+    def check():
+        s = os.stat(path)
+        if (s.st_size, s.st_mtime_ns, s.st_ino) != ident:
+            raise RuntimeError(f"{path} changed after it was scanned: its string columns can no longer be read")
+    return check
+
+
 def _truthy(v) -> bool:
     return str(v).lower() in ("true", "1", "yes")
 
@@ -359,7 +377,8 @@ class DataFrameReader:
                                             chunk_bytes=int(self._session.conf.get("dq4ml.chunkBytes", str(256 << 20))),
                                             pinned=None if pinned is None else pinned[off:], device_data=dbytes,
                                             types_hint=(pf.type_hints.get(hkey) if pf is not None and not strict
-                                                        else None), opts=dopts, user_types=strict)
+                                                        else None), opts=dopts, user_types=strict,
+                                            source_check=_map_check(pf))
                 if t is None:
                     return None
                 codes = [csvscan.type_code_of(f.dataType) for f in t.schema.fields]
@@ -474,7 +493,8 @@ class DataFrameReader:
                 t = csvscan.scan_device(body, sep=sep, infer=infer, device=dev, sharded=shard, ncols=ncols,
                                         chunk_bytes=int(self._session.conf.get("dq4ml.chunkBytes", str(256 << 20))),
                                         pinned=None if pinned is None else pinned[len(data) - len(body):],
-                                        types_hint=None if strict else list(codes), opts=dopts, user_types=strict)
+                                        types_hint=None if strict else list(codes), opts=dopts, user_types=strict,
+                                        source_check=_map_check(pf))
             if t is None:
                 return self._host_table(data, header, infer, user_types, user_names, sep, dev, shard)
             fields = [StructField(nm, f.dataType, True) for nm, f in zip(fnames, t.schema.fields)]

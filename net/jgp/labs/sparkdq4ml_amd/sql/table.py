@@ -172,8 +172,9 @@ class DeviceStringColumn(ColumnData):
     (``index`` / ``slice``) move only the spans."""
 
     def __init__(self, spans: torch.Tensor, valid: Optional[torch.Tensor], data, opts: Optional[dict],
-                 meta=None):  # noqa: D107
+                 meta=None, check=None):  # noqa: D107
         self.dtype = StringType()
+        self.check = check  # () -> None, raises when a mapped input file changed since the scan
         self.spans = spans
         self.valid = valid
         self.data = data  # the scanned bytes (bytes / memoryview / numpy view of the cached file)
@@ -187,6 +188,8 @@ class DeviceStringColumn(ColumnData):
         if self._vals is None:
             from ..ops import native
 
+            if self.check is not None:
+                self.check()
             o = self.opts
             sp = self.spans.detach().cpu().numpy()
             ok = (self.valid.detach().to("cpu", torch.uint8).numpy() if self.valid is not None
@@ -220,13 +223,14 @@ class DeviceStringColumn(ColumnData):
             return ColumnData.index(self, idx)
         i = idx.to(self.spans.device)
         valid = None if self.valid is None else self.valid.index_select(0, i)
-        return DeviceStringColumn(self.spans.index_select(0, i), valid, self.data, self.opts, dict(self.meta))
+        return DeviceStringColumn(self.spans.index_select(0, i), valid, self.data, self.opts, dict(self.meta),
+                                  self.check)
 
     def slice(self, start: int, stop: int) -> "ColumnData":
         if self._vals is not None:
             return ColumnData.slice(self, start, stop)
         valid = None if self.valid is None else self.valid[start:stop]
-        return DeviceStringColumn(self.spans[start:stop], valid, self.data, self.opts, dict(self.meta))
+        return DeviceStringColumn(self.spans[start:stop], valid, self.data, self.opts, dict(self.meta), self.check)
 
 
 class Table:

@@ -705,3 +705,29 @@ def test_device_string_column_moves_spans_until_read():
     assert col.values == ["ab", "c,d", 'x""y', "é"]  # (x""y is unquoted: its bytes as they stand)
     t = Table(StructType([StructField("s", StringType(), True)]), [col], 4, torch.tensor([True, False, True, True]))
     assert [r[0] for r in t.to_rows()] == ["ab", 'x""y', "é"]
+
+
+def test_mapped_input_string_check(tmp_path):
+    """Strings of a device scan over a file MAP (inputs above the pinned cache) are built from the
+    file's own pages: a changed file raises instead of yielding other bytes (or a SIGBUS)."""
+    from net.jgp.labs.sparkdq4ml_amd.runtime import filecache
+    from net.jgp.labs.sparkdq4ml_amd.sql.readwriter import _map_check
+
+    p = tmp_path / "m.csv"
+    p.write_bytes(b"a,1\nb,2\n")
+    mf = filecache.open_mapped(str(p))
+    chk = _map_check(mf)
+    chk()
+    class Owned:  # a pinned-cache entry: an owned host copy
+        host = object()
+
+    assert _map_check(Owned()) is None and _map_check(None) is None
+    import os
+    import time
+
+    time.sleep(0.01)
+    p.write_bytes(b"a,1\nb,2\nc,3\n")
+    os.utime(p)
+    with pytest.raises(RuntimeError, match="changed after it was scanned"):
+        chk()
+    filecache.clear()
