@@ -7,7 +7,6 @@ Every DataFrame call the lab makes is here: ``withColumnRenamed`` (``...App.java
 """
 from __future__ import annotations
 
-import datetime as _dt
 from typing import List, Optional, Sequence
 
 import torch
@@ -89,9 +88,6 @@ def _cell_str(v) -> str:
         return v
     if isinstance(v, (bytes, bytearray)):
         return "[" + " ".join(f"{b:02X}" for b in v) + "]"
-    if isinstance(v, _dt.datetime):  # Spark 2.4 timestampToString: the fraction without trailing zeros
-        s = v.strftime("%Y-%m-%d %H:%M:%S")
-        return s + ("." + f"{v.microsecond:06d}".rstrip("0") if v.microsecond else "")
     if hasattr(v, "toString"):
         return v.toString()
     return java_str(v)

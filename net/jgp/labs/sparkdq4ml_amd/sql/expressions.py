@@ -411,6 +411,8 @@ def cast_column(c: ColumnData, to: DataType, device) -> ColumnData:
         vals = c.to_pylist()
         return ColumnData(to, [None if v is None else (java_str(v) if not isinstance(v, str) else v) for v in vals],
                           c.valid)
+    if isinstance(to, TimestampType) or isinstance(src, TimestampType):
+        return _cast_timestamp(c, src, to, device)
     if isinstance(src, StringType):
         vals, ok = [], []
         for s in c.values:
@@ -451,6 +453,39 @@ def cast_column(c: ColumnData, to: DataType, device) -> ColumnData:
     if isinstance(to, BooleanType):
         return ColumnData(to, vals != 0, c.valid)
     return ColumnData(to, vals.to(to.torch_dtype), c.valid)
+
+
+def _cast_timestamp(c: ColumnData, src: DataType, to: DataType, device) -> ColumnData:
+    """Spark 2.4 casts to / from TimestampType (int64 microseconds, UTC): a string parses as the
+    CSV reader's timestamps do (``csv_parse_timestamp``; null when it does not); a number is
+    seconds since the epoch (integral: exact, fractional: ``(d * 1e6).toLong``); a timestamp as a
+    long / int is whole seconds (floor), as a double fractional seconds."""
+    if isinstance(src, StringType):
+        from ..ops import native
+
+        h = native.host()
+        vals, ok = [], []
+        for s in c.values:
+            us = None if s is None else h.csv_parse_timestamp(s.strip())
+            vals.append(0 if us is None else us)
+            ok.append(us is not None)
+        return ColumnData(to, torch.tensor(vals, dtype=torch.int64, device=device),
+                          torch.tensor(ok, dtype=torch.bool, device=device))
+    vals = c.values
+    if isinstance(to, TimestampType):
+        if isinstance(src, BooleanType):
+            raise AnalysisException(f"cannot resolve 'CAST(... AS TIMESTAMP)' due to data type mismatch: "
+                                    f"cannot cast {src.simpleString()} to timestamp")
+        us = vals.to(torch.int64) * 1_000_000 if not vals.is_floating_point() else \
+            torch.nan_to_num(vals.to(torch.float64) * 1e6, nan=0.0).to(torch.int64)
+        return ColumnData(to, us, c.valid)
+    # from a timestamp
+    if isinstance(to, (LongType, IntegerType)):
+        return ColumnData(to, torch.div(vals, 1_000_000, rounding_mode="floor").to(to.torch_dtype), c.valid)
+    if isinstance(to, (DoubleType, FloatType)):
+        return ColumnData(to, (vals.to(torch.float64) / 1e6).to(to.torch_dtype), c.valid)
+    raise AnalysisException(f"cannot resolve 'CAST(... AS {to.simpleString().upper()})' due to data type "
+                            f"mismatch: cannot cast timestamp to {to.simpleString()}")
 
 
 class Alias(Expr):

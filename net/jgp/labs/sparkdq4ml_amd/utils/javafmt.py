@@ -13,12 +13,13 @@ exact Java rendering:
 """
 from __future__ import annotations
 
+import datetime as _dt
 import math
 from decimal import Decimal
 
 import numpy as np
 
-__all__ = ["java_double_str", "java_float_str", "java_str", "format_vector"]
+__all__ = ["java_double_str", "java_float_str", "java_str", "format_vector", "timestamp_str"]
 
 
 def _digits_exp(shortest: str):
@@ -89,7 +90,16 @@ def java_str(v) -> str:
         return java_float_str(v)
     if isinstance(v, (float, np.floating)):
         return java_double_str(v)
+    if isinstance(v, _dt.datetime):
+        return timestamp_str(v)
     return str(v)
+
+
+def timestamp_str(v) -> str:
+    """Spark 2.4 ``DateTimeUtils.timestampToString``: ``yyyy-MM-dd HH:mm:ss`` plus the fraction of a
+    second without its trailing zeros."""
+    s = v.strftime("%Y-%m-%d %H:%M:%S")
+    return s + ("." + f"{v.microsecond:06d}".rstrip("0") if v.microsecond else "")
 
 
 def format_vector(values) -> str:

@@ -731,3 +731,22 @@ def test_mapped_input_string_check(tmp_path):
     with pytest.raises(RuntimeError, match="changed after it was scanned"):
         chk()
     filecache.clear()
+
+
+def test_timestamp_casts(cpu_session, tmp_path):
+    """Spark 2.4 casts around TimestampType: to string (``yyyy-MM-dd HH:mm:ss[.f]``), to long
+    (whole seconds, floor) and double (fractional seconds), from strings (the reader's parser;
+    null when it does not parse) and from seconds."""
+    import datetime
+
+    p = tmp_path / "ts.csv"
+    p.write_bytes(b"1969-12-31 23:59:59.5,2019-06-15\r2019-06-15 08:30:00.25,bad\r")
+    df = cpu_session.read().option("inferSchema", "true").csv(str(p))
+    assert df.dtypes == [("_c0", "timestamp"), ("_c1", "string")]
+    df.createOrReplaceTempView("t")
+    rows = cpu_session.sql("SELECT CAST(_c0 AS STRING) s, CAST(_c0 AS LONG) l, CAST(_c0 AS DOUBLE) d, "
+                           "CAST(_c1 AS TIMESTAMP) t2, CAST(CAST(_c0 AS LONG) AS TIMESTAMP) t3 FROM t").collect()
+    assert [tuple(r) for r in rows] == [
+        ("1969-12-31 23:59:59.5", -1, -0.5, datetime.datetime(2019, 6, 15), datetime.datetime(1969, 12, 31, 23, 59, 59)),
+        ("2019-06-15 08:30:00.25", 1560587400, 1560587400.25, None, datetime.datetime(2019, 6, 15, 8, 30)),
+    ]
