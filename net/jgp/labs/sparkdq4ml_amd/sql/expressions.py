@@ -240,6 +240,9 @@ class BinOp(Expr):
         lt, rt = self.left.data_type(schema), self.right.data_type(schema)
         if isinstance(lt, StringType) and isinstance(rt, StringType):
             return lt
+        if (isinstance(lt, TimestampType) and isinstance(rt, (TimestampType, StringType))) or \
+                (isinstance(rt, TimestampType) and isinstance(lt, StringType)):
+            return TimestampType()  # Spark 2.4 PromoteStrings: the string side becomes a timestamp
         if isinstance(lt, StringType) or isinstance(rt, StringType):
             # Spark casts the string side to the numeric type (or double)
             return DoubleType()
@@ -289,6 +292,13 @@ class BinOp(Expr):
             lm, rm = l.valid_mask(ctx.device), r.valid_mask(ctx.device)
             eq = _spark_cmp("=", _num(l, t), _num(r, t))
             return ColumnData(BooleanType(), (lm & rm & eq) | (~lm & ~rm), None)
+        if isinstance(l.dtype, TimestampType) or isinstance(r.dtype, TimestampType):
+            t = self.operand_type(schema)
+            if not isinstance(t, TimestampType) or self.op not in _CMP:
+                raise AnalysisException(f"cannot resolve '{self.sql_name()}' due to data type mismatch")
+            l = l if isinstance(l.dtype, TimestampType) else _cast_timestamp(l, l.dtype, t, ctx.device)
+            r = r if isinstance(r.dtype, TimestampType) else _cast_timestamp(r, r.dtype, t, ctx.device)
+            return ColumnData(BooleanType(), _spark_cmp(self.op, l.values, r.values), _and_valid(l, r))
         if isinstance(l.dtype, StringType) and isinstance(r.dtype, StringType):
             if self.op not in _CMP:
                 raise AnalysisException(f"operator {self.op} on strings")

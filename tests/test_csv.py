@@ -750,3 +750,16 @@ def test_timestamp_casts(cpu_session, tmp_path):
         ("1969-12-31 23:59:59.5", -1, -0.5, datetime.datetime(2019, 6, 15), datetime.datetime(1969, 12, 31, 23, 59, 59)),
         ("2019-06-15 08:30:00.25", 1560587400, 1560587400.25, None, datetime.datetime(2019, 6, 15, 8, 30)),
     ]
+
+
+def test_timestamp_comparisons(cpu_session, tmp_path):
+    """A timestamp compared with a string literal: the string side is cast to a timestamp (Spark
+    2.4 ``PromoteStrings``); timestamps compare as instants."""
+    p = tmp_path / "ts.csv"
+    p.write_bytes(b"2019-01-01,1\r2019-06-15 08:30:00,2\r2020-02-29T12:00:00Z,3\r")
+    df = cpu_session.read().option("inferSchema", "true").csv(str(p))
+    df.createOrReplaceTempView("t")
+    got = [r[0] for r in cpu_session.sql("SELECT _c1 FROM t WHERE _c0 >= '2019-06-15 08:30:00'").collect()]
+    assert got == [2, 3]
+    got = [r[0] for r in cpu_session.sql("SELECT _c1 FROM t WHERE _c0 < '2019-03-01'").collect()]
+    assert got == [1]
