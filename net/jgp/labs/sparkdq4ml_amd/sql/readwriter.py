@@ -130,6 +130,17 @@ def _map_check(pf):
     return check
 
 
+def _csv_cell(v, java_str) -> str:
+    """One written CSV value: a timestamp in the CSV source's default ``timestampFormat``
+    (``yyyy-MM-dd'T'HH:mm:ss.SSSXXX``, UTC -> ``Z``), which the reader parses back; else Java's
+    string form."""
+    import datetime
+
+    if isinstance(v, datetime.datetime):
+        return v.strftime("%Y-%m-%dT%H:%M:%S.") + f"{v.microsecond // 1000:03d}Z"
+    return java_str(v)
+
+
 def _truthy(v) -> bool:
     return str(v).lower() in ("true", "1", "yes")
 
@@ -577,6 +588,9 @@ class DataFrameWriter:
         self._format = "parquet"
         self._options = {}
 
+    def __call__(self):  # ``df.write()`` (the Java API form) as well as ``df.write``
+        return self
+
     def mode(self, m):
         self._mode = m.lower()
         return self
@@ -637,7 +651,7 @@ class DataFrameWriter:
             if _truthy(self._options.get("header", "false")):
                 f.write(sep.join(t.schema.names) + "\n")
             for r in zip(*cols):
-                f.write(sep.join("" if v is None else java_str(v) for v in r) + "\n")
+                f.write(sep.join("" if v is None else _csv_cell(v, java_str) for v in r) + "\n")
 
     def _write_parquet(self, path):
         import pyarrow as pa

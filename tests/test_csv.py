@@ -763,3 +763,18 @@ def test_timestamp_comparisons(cpu_session, tmp_path):
     assert got == [2, 3]
     got = [r[0] for r in cpu_session.sql("SELECT _c1 FROM t WHERE _c0 < '2019-03-01'").collect()]
     assert got == [1]
+
+
+def test_timestamp_csv_write_round_trip(cpu_session, tmp_path):
+    """The CSV writer prints timestamps in the source's default ``timestampFormat``
+    (``yyyy-MM-dd'T'HH:mm:ss.SSSXXX``); reading them back gives the same instants."""
+    p = tmp_path / "ts.csv"
+    p.write_bytes(b"2019-06-15 08:30:00.25,1\r1999-12-31,2\r")
+    df = cpu_session.read().option("inferSchema", "true").csv(str(p))
+    out = str(tmp_path / "out")
+    df.write().csv(out)
+    text = open(tmp_path / "out" / "part-00000.csv").read()
+    assert text.splitlines()[0] == "2019-06-15T08:30:00.250Z,1"
+    back = cpu_session.read().option("inferSchema", "true").csv(out)
+    assert back.dtypes == df.dtypes
+    assert [tuple(r) for r in back.collect()] == [tuple(r) for r in df.collect()]
