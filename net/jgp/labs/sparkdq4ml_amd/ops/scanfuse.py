@@ -733,13 +733,8 @@ def _launch(cp, nodes, rel, extra: dict, own_stream: bool = True):
     return outs, sel_out, err, vflag, side, cur
 
 
-def _udf_error_check(nodes, err):
-    """A raising rule (``RaiseIfNull``: ``MinimumPriceDataQualityUdf``'s NPE on a null price,
-    ``MinimumPriceDataQualityUdf.java:11-13``) as a deferred device check (``runtime/checks.py``):
-    the action stays asynchronous and the SparkException surfaces with the first host read of
-    its results — the job fails exactly as Spark's does, without a sync per action."""
-    from ..runtime.checks import defer
-    from ..sql.expressions import SparkException
+def _raise_message(nodes) -> str:
+    """The message of the chain's raising rule (the last one found), or Spark's generic one."""
     from . import dqvm
 
     msg = "Failed to execute user defined function"
@@ -748,6 +743,19 @@ def _udf_error_check(nodes, err):
             r = dqvm._find_raise(ex)
             if r is not None:
                 msg = r.message
+    return msg
+
+
+def _udf_error_check(nodes, err):
+    """A raising rule (``RaiseIfNull``: ``MinimumPriceDataQualityUdf``'s NPE on a null price,
+    ``MinimumPriceDataQualityUdf.java:11-13``) as a deferred device check (``runtime/checks.py``):
+    the action stays asynchronous and the SparkException surfaces with the first host read of
+    its results — the job fails exactly as Spark's does, without a sync per action.  ``nodes``:
+    the chain, or its precomputed ``_raise_message``."""
+    from ..runtime.checks import defer
+    from ..sql.expressions import SparkException
+
+    msg = nodes if isinstance(nodes, str) else _raise_message(nodes)
     return defer(err, lambda: SparkException(msg))
 
 
@@ -865,7 +873,10 @@ class _Route:
     action's fresh leaf: same cached bytes and facts)."""
 
     def __init__(self, kind, chain, cp, d):
-        self.kind, self.chain, self.cp, self.d = kind, chain, cp, d
+        # the chain itself is not kept: its leaf is the first action's relation, whose fused
+        # dict points at the cached HBM bytes (a remembered route must not keep them alive)
+        self.kind, self.cp, self.d = kind, cp, d
+        self.msg = _raise_message(chain)
         self.conf = None
 
     def run(self, p) -> "FusedGram":
@@ -875,10 +886,10 @@ class _Route:
             flat, err, vflag, ccp = scancut.launch_cut(self.cp, p, self.d)
             checks = [_fact_check(p, vflag)]
             if ccp.has_raise:
-                checks.append(_udf_error_check(self.chain, err))
+                checks.append(_udf_error_check(self.msg, err))
             STATS["fused_grams"] += 1
             return FusedGram(flat, self.d, [c for c in checks if c is not None], int(p.fused["nlines"]))
-        return _run_line_gram(self.cp, self.chain, p, self.d)
+        return _run_line_gram(self.cp, self.msg, p, self.d)
 
 
 _ROUTES: dict = {}

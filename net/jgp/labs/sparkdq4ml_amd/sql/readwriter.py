@@ -16,6 +16,7 @@ import glob
 import json
 import os
 import shutil
+import weakref
 from typing import Dict, List, Optional
 
 import numpy as np
@@ -31,7 +32,9 @@ from .types import (BooleanType, DecimalType, DoubleType, IntegerType, LongType,
 
 __all__ = ["DataFrameReader", "DataFrameWriter", "csv_code_to_type"]
 
-# load() of an unchanged cached CSV file: key -> (lazy relation template, file identity, cache entry)
+# load() of an unchanged cached CSV file: key -> (weak reference to the cache entry, file identity);
+# the lazy relation template lives ON the entry (``load_templates``), so an evicted file's template
+# (and the HBM bytes its relation points at) goes with it -- nothing here keeps them alive
 _LOADS: dict = {}
 _LOAD_SERIAL = __import__("itertools").count(1)
 _REALPATH: dict = {}
@@ -207,11 +210,13 @@ class DataFrameReader:
         if self._format == "csv":
             mk = self._load_key(files)
             hit = _LOADS.get(mk[0]) if mk is not None else None
-            if hit is not None and hit[1] == mk[1] and hit[2] is not None and hit[2].live():
+            hpf = hit[0]() if hit is not None else None
+            tmpl = getattr(hpf, "load_templates", {}).get(mk[0]) if hpf is not None else None
+            if tmpl is not None and hit[1] == mk[1] and hpf.live():
                 # the same unchanged bytes with the same options: this action's own (unscanned)
                 # copy of the lazy relation the first load built -- the device scan still runs
                 # at the action (sql/skey.py)
-                return DataFrame(hit[0].fresh(), self._session)
+                return DataFrame(tmpl.fresh(), self._session)
             self._last_pf = None
             table = self._read_csv(files)
             if not isinstance(table, Table):  # a lazily scanned relation (sql.plan.CsvScanRelation)
@@ -223,7 +228,8 @@ class DataFrameReader:
                     table._skey = intern(("csv", next(_LOAD_SERIAL)))
                     if len(_LOADS) >= 64:
                         _LOADS.clear()
-                    _LOADS[mk[0]] = (table.fresh(), mk[1], pf)
+                    pf.__dict__.setdefault("load_templates", {})[mk[0]] = table.fresh()
+                    _LOADS[mk[0]] = (weakref.ref(pf), mk[1])
                 return DataFrame(table, self._session)
         elif self._format == "parquet":
             table = self._read_parquet(files)
