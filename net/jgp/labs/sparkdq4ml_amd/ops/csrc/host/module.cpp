@@ -1,5 +1,7 @@
 // pybind11 bindings of the host runtime library (_dq4ml_host): normal-equation solvers and the
 // CSV scanner.  Device kernels live in the separate gfx950 module (_dq4ml_hip).
+#include <cstring>
+
 #include <pybind11/numpy.h>
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
@@ -135,7 +137,8 @@ PYBIND11_MODULE(_dq4ml_host, m) {
         std::string t;
         for (int64_t i = 0; i < n; ++i) {
           if (!vp[i]) {
-            out[i] = py::none();
+            Py_INCREF(Py_None);
+            PyList_SET_ITEM(out.ptr(), (Py_ssize_t)i, Py_None);
             continue;
           }
           const int64_t fs = sp[i] >> 25, len = sp[i] & 0xFFFFFF;
@@ -152,9 +155,20 @@ PYBIND11_MODULE(_dq4ml_host, m) {
             if (itws)
               while (e > a && (p[e - 1] == ' ' || p[e - 1] == '\t')) --e;
           }
-          PyObject* s = PyUnicode_DecodeUTF8(p + a, (Py_ssize_t)(e - a), nullptr);
+          // ASCII text (the common case): a compact 1-byte string filled by memcpy, no decoder
+          const char* q = p + a;
+          const size_t m = e - a;
+          bool ascii = true;
+          for (size_t k = 0; k < m && ascii; ++k) ascii = (unsigned char)q[k] < 0x80;
+          PyObject* s;
+          if (ascii) {
+            s = PyUnicode_New((Py_ssize_t)m, 127);
+            if (s) std::memcpy(PyUnicode_DATA(s), q, m);
+          } else {
+            s = PyUnicode_DecodeUTF8(q, (Py_ssize_t)m, nullptr);
+          }
           if (!s) throw py::error_already_set();
-          out[i] = py::reinterpret_steal<py::object>(s);
+          PyList_SET_ITEM(out.ptr(), (Py_ssize_t)i, s);  // steals the reference (PyList_New left the slot NULL)
         }
         return out;
       },
