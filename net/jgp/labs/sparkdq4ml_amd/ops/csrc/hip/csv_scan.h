@@ -30,5 +30,8 @@ void csv_line_ends(const uint8_t* buf, int64_t n, int64_t* counts, void* ends, h
 // does not convert makes its record malformed (all fields null)
 void csv_parse(const uint8_t* buf, int64_t n, const void* ends, int64_t nlines, int ncols, const dq4ml_csv::CsvOpts& o,
                const int64_t* dcols, uint8_t* valid, uint8_t* keep, int64_t* stats, hipStream_t st);
+// string column (kind-4 spans into buf[0, nbuf)) == lit[0, L): out 1 / 0, or 2 for a raw field
+void csv_span_eq(const uint8_t* buf, int64_t nbuf, const int64_t* spans, int64_t n, const uint8_t* lit, int L,
+                 uint8_t* out, hipStream_t st);
 
 }  // namespace dq4ml

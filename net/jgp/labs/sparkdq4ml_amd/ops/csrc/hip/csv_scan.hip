@@ -374,7 +374,38 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   }
 }
 
+// A device string column (kind-4 spans into buf) compared with a constant: 1 equal, 0 not equal,
+// 2 undetermined -- a raw (quoted / escaped) field, whose text only the host tokenizer builds
+__global__ __launch_bounds__(256) void csv_span_eq_kernel(const uint8_t* __restrict__ buf, int64_t nbuf,
+                                                          const int64_t* __restrict__ spans, int64_t n,
+                                                          const uint8_t* __restrict__ lit, int L,
+                                                          uint8_t* __restrict__ out) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t v = spans[i];
+    const int64_t fs = v >> 25, len = v & 0xFFFFFF;
+    uint8_t r;
+    if ((v >> 24) & 1) {
+      r = 2;
+    } else if (len != L || fs < 0 || fs + len > nbuf) {
+      r = 0;
+    } else {
+      r = 1;
+      for (int k = 0; k < L && r; ++k) r = buf[fs + k] == lit[k];
+    }
+    out[i] = r;
+  }
+}
+
 }  // namespace
+
+void csv_span_eq(const uint8_t* buf, int64_t nbuf, const int64_t* spans, int64_t n, const uint8_t* lit, int L,
+                 uint8_t* out, hipStream_t st) {
+  if (n <= 0) return;
+  int64_t g = (n + 255) / 256;
+  if (g > 65536) g = 65536;
+  hipLaunchKernelGGL(csv_span_eq_kernel, dim3(g), dim3(256), 0, st, buf, nbuf, spans, n, lit, L, out);
+  DQ_HIP_CHECK(hipGetLastError());
+}
 
 // + 1: the window grid starts at the granule boundary below the buffer start
 int64_t csv_count_blocks(int64_t n) { return (n + kChunk - 1) / kChunk + 1; }

@@ -400,6 +400,11 @@ PYBIND11_MODULE(_dq4ml_hip, m) {
 
   // ---- CSV scan (K1/K2) ------------------------------------------------------------------------
   m.def("csv_count_blocks", &csv_count_blocks);
+  m.def("csv_span_eq", [](uintptr_t buf, int64_t nbuf, uintptr_t spans, int64_t n, uintptr_t lit, int L, uintptr_t out,
+                          uintptr_t stream) {
+    csv_span_eq(P<const uint8_t>(buf), nbuf, P<const int64_t>(spans), n, P<const uint8_t>(lit), L, P<uint8_t>(out),
+                as_stream(stream));
+  });
   m.def("csv_line_ends", [](uintptr_t buf, int64_t n, uintptr_t counts, uintptr_t ends, uintptr_t stream) {
     csv_line_ends(P<const uint8_t>(buf), n, P<int64_t>(counts), P<void>(ends), as_stream(stream));
   });

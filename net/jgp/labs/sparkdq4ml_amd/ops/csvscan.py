@@ -242,7 +242,7 @@ def type_code_of(dt) -> int:
     return CT_DOUBLE
 
 
-def _finish(parts, types, st, dev, hinted=False, data=None, opts=None, check=None):
+def _finish(parts, types, st, dev, hinted=False, data=None, opts=None, check=None, dbuf=None):
     """Typed columns from per-chunk parse outputs under the merged types.  ``st``: the chunks'
     stats on the host.  Int / long / boolean values convert exactly from their f64 planes (the
     parser flags integers beyond 2^53 for the host path).  String columns (scanned as spans, always
@@ -265,7 +265,7 @@ def _finish(parts, types, st, dev, hinted=False, data=None, opts=None, check=Non
                 valid_l = [p[2][c, :p[0]] for _, p in live]
                 vv = torch.cat(valid_l) if len(valid_l) > 1 else valid_l[0].clone()
             fields.append(StructField(f"_c{c}", StringType(), True))
-            cols.append(DeviceStringColumn(spans, vv, data, opts, check=check))
+            cols.append(DeviceStringColumn(spans, vv, data, opts, check=check, dbuf=dbuf))
             continue
         vals_l = []
         for _, (nlines, dcols, _, _, _, _) in live:
@@ -452,7 +452,8 @@ def scan_device(data, sep: str = ",", infer: bool = True, device=None, ncols: Op
             STATS["fallbacks"] += 1
             return None
         STATS["device_scans"] += 1
-        return _finish(parts, list(user_types), st, dev, hinted=True, data=data, opts=opts, check=source_check)
+        return _finish(parts, list(user_types), st, dev, hinted=True, data=data, opts=opts, check=source_check,
+                       dbuf=device_data)
     types = _resolve_types(masks, int(st[:, 0].max()), sharded)
     if types is None:
         STATS["fallbacks"] += 1
@@ -473,7 +474,8 @@ def scan_device(data, sep: str = ",", infer: bool = True, device=None, ncols: Op
         return None
     STATS["device_scans"] += 1
     STATS["chunks"] = STATS.get("chunks", 0) + len(parts)
-    return _finish(parts, types, st, dev, hinted=hint is not None, data=data, opts=opts, check=source_check)
+    return _finish(parts, types, st, dev, hinted=hint is not None, data=data, opts=opts, check=source_check,
+                   dbuf=device_data)
 
 
 def chunk_bounds(data: bytes, chunk_bytes: int):

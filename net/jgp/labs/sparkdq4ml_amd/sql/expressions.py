@@ -299,6 +299,10 @@ class BinOp(Expr):
             l = l if isinstance(l.dtype, TimestampType) else _cast_timestamp(l, l.dtype, t, ctx.device)
             r = r if isinstance(r.dtype, TimestampType) else _cast_timestamp(r, r.dtype, t, ctx.device)
             return ColumnData(BooleanType(), _spark_cmp(self.op, l.values, r.values), _and_valid(l, r))
+        if self.op in ("=", "==", "!=", "<>"):  # a device string column against a constant
+            eq = _device_string_eq(self, l, r)
+            if eq is not None:
+                return ColumnData(BooleanType(), eq if self.op in ("=", "==") else ~eq, valid)
         if isinstance(l.dtype, StringType) and isinstance(r.dtype, StringType):
             if self.op not in _CMP:
                 raise AnalysisException(f"operator {self.op} on strings")
@@ -333,6 +337,17 @@ class BinOp(Expr):
             nv = ~zero if valid is None else (valid & ~zero)
             return ColumnData(t, out, None if bool(nv.all()) else nv)
         raise AnalysisException(f"unsupported operator {self.op}")
+
+
+def _device_string_eq(op: "BinOp", l: ColumnData, r: ColumnData):
+    """``col = 'text'`` over a device-scanned string column (``DeviceStringColumn.eq_literal``:
+    compared in HBM, the strings never built), else None."""
+    from .table import DeviceStringColumn
+
+    for col, other in ((l, op.right), (r, op.left)):
+        if isinstance(col, DeviceStringColumn) and isinstance(other, Lit) and isinstance(other.value, str):
+            return col.eq_literal(other.value)
+    return None
 
 
 def _string_to_double(c: ColumnData, ctx) -> ColumnData:

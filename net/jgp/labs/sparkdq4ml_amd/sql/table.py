@@ -172,9 +172,10 @@ class DeviceStringColumn(ColumnData):
     (``index`` / ``slice``) move only the spans."""
 
     def __init__(self, spans: torch.Tensor, valid: Optional[torch.Tensor], data, opts: Optional[dict],
-                 meta=None, check=None):  # noqa: D107
+                 meta=None, check=None, dbuf: Optional[torch.Tensor] = None):  # noqa: D107
         self.dtype = StringType()
         self.check = check  # () -> None, raises when a mapped input file changed since the scan
+        self.dbuf = dbuf  # the same bytes resident in HBM (the file cache's copy), when there is one
         self.spans = spans
         self.valid = valid
         self.data = data  # the scanned bytes (bytes / memoryview / numpy view of the cached file)
@@ -224,13 +225,40 @@ class DeviceStringColumn(ColumnData):
         i = idx.to(self.spans.device)
         valid = None if self.valid is None else self.valid.index_select(0, i)
         return DeviceStringColumn(self.spans.index_select(0, i), valid, self.data, self.opts, dict(self.meta),
-                                  self.check)
+                                  self.check, self.dbuf)
 
     def slice(self, start: int, stop: int) -> "ColumnData":
         if self._vals is not None:
             return ColumnData.slice(self, start, stop)
         valid = None if self.valid is None else self.valid[start:stop]
-        return DeviceStringColumn(self.spans[start:stop], valid, self.data, self.opts, dict(self.meta), self.check)
+        return DeviceStringColumn(self.spans[start:stop], valid, self.data, self.opts, dict(self.meta), self.check,
+                                  self.dbuf)
+
+    def eq_literal(self, lit: str) -> Optional[torch.Tensor]:
+        """``column = lit`` on the device (bool [n]; validity is the column's), without building
+        the strings: the spans' bytes in HBM are compared with the literal's UTF-8 bytes; only raw
+        (quoted / escaped) fields get their text built on the host.  None when the column has no
+        HBM-resident bytes or a whitespace trim applies (then the strings are compared on the host)."""
+        if self._vals is not None or self.dbuf is None or self.opts.get("trim_lead") or self.opts.get("trim_trail"):
+            return None
+        from ..ops import native
+
+        dev = self.spans.device
+        b = lit.encode("utf-8")
+        lt = torch.tensor(list(b) or [0], dtype=torch.uint8).to(dev, non_blocking=True)
+        out = torch.empty(self.n, dtype=torch.uint8, device=dev)
+        native.hip().csv_span_eq(self.dbuf.data_ptr(), self.dbuf.numel(), self.spans.data_ptr(), self.n,
+                                 lt.data_ptr(), len(b), out.data_ptr(), torch.cuda.current_stream(dev).cuda_stream)
+        eq = out == 1
+        raw = torch.nonzero(out == 2).flatten()
+        if raw.numel():  # raw fields: the host builds just their text
+            sub = self.index(raw)
+            sub.dbuf = None
+            vals = sub.values
+            hits = [i for i, v in enumerate(vals) if v == lit]
+            if hits:
+                eq[raw[torch.tensor(hits, dtype=torch.long, device=raw.device)]] = True
+        return eq
 
 
 class Table:

@@ -162,3 +162,31 @@ def test_ten_million_quoted_rows_scan_on_the_device(tmp_path):
         want = [v if ok else None for v, ok in zip(vals, valid)] * 10_000
         assert c.values == want, name
     spark.stop()
+
+
+@pytest.mark.parametrize("lit", ["a", "a,b", "café", 'x"y', "", "7", "zzz"])
+def test_string_equality_filter_runs_on_the_device(tmp_path, lit):
+    """``filter(col = 'text')`` over a device string column compares the spans' bytes in HBM
+    (``csv_span_eq``); only raw (quoted / escaped) fields get their text built, the column itself
+    is never materialized, and the rows equal the host scanner's."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from net.jgp.labs.sparkdq4ml_amd import col
+
+    p = tmp_path / "eq.csv"
+    p.write_bytes(_mixed_csv(20_000, seed=4))
+
+    def ids(threshold, check_lazy=False):
+        spark = _session(threshold)
+        df = spark.read().option("inferSchema", "true").csv(str(p))
+        base = df._plan.table.columns[1]
+        got = [r[0] for r in df.filter(col("_c1") == lit).select("_c0").collect()]
+        neq = df.filter(col("_c3") != lit).count()
+        if check_lazy:
+            assert not base.materialized  # the filter never built the column's strings
+        spark.stop()
+        return got, neq
+
+    dev = ids("0", check_lazy=True)
+    host = ids(str(1 << 40))
+    assert dev == host
