@@ -29,8 +29,6 @@
 #include <hip/hip_cooperative_groups.h>
 #include <hip/hip_runtime.h>
 
-#include <cstdlib>
-
 #include "common.h"
 #include "lsq.h"
 
@@ -386,16 +384,12 @@ __device__ void apply_dir(const QnArgs& a, Ctl& C, double* scal, double* red, bo
   __threadfence();
 }
 
-// HU (half units): a unit is ONE 8-row (bf16) / 16-row (fp8) half of a fragment row group, and
-// the two lane halves of a wave take different tiles of it -- half the bytes between a unit's two
-// reads, so twice the share of the re-read the XCD's L2 still holds (DQ4ML_LSQ_QN_HALF)
-template <int L, int TPW, bool HU>
+template <int L, int TPW>
 __global__ __launch_bounds__(kT, 1) void lsq_qn_kernel(QnArgs a) {
   cg::grid_group grid = cg::this_grid();
   constexpr int E = L == 3 ? 16 : 8;
   constexpr int64_t CH = L == 3 ? 2048 : 4096;
   constexpr int UPS = L == 3 ? 2 : 4;
-  constexpr int TL = HU ? TPW / 2 : TPW;  // tiles per lane per unit
   constexpr int NC = 8 * TPW * 32;  // coefficient slots (tiles padded to whole wave strides)
   __shared__ double colacc[NC];  // the block's f64 column sums (<= 128 KiB)
   __shared__ double red[kW];
@@ -488,21 +482,19 @@ __global__ __launch_bounds__(kT, 1) void lsq_qn_kernel(QnArgs a) {
     // E2: the fused pass (margins, then the column sums of the same tiles)
     double loss = 0.0, vsum = 0.0;
     for (int64_t u = b; u < a.nunits; u += B) {
-      const int64_t s = HU ? u / (2 * UPS) : u / UPS;
-      const int sub = HU ? (int)((u % (2 * UPS)) >> 1) : (int)(u % UPS);
-      const int hh = HU ? (int)(u & 1) : hf;  // the unit's row half (HU) / the lane's (full units)
-      const int tb = HU ? hf * TL : 0;         // HU: the lane half's first tile slot
-      const unsigned char* p = a.X + s * a.NT * CH + ((sub * 64 + (HU ? hh * 32 + fl : lane)) << 4);
+      const int64_t s = u / UPS;
+      const int sub = (int)(u % UPS);
+      const unsigned char* p = a.X + s * a.NT * CH + ((sub * 64 + lane) << 4);
       double acc[E];
 #pragma unroll
       for (int e = 0; e < E; ++e) acc[e] = 0.0;
 #pragma unroll 1
-      for (int i0 = 0; i0 < TL; i0 += 8) {
+      for (int i0 = 0; i0 < TPW; i0 += 8) {
         u32x4 q[8];
         float c[8];
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-          const int tt = wave + 8 * (tb + i0 + k);
+          const int tt = wave + 8 * (i0 + k);
           q[k] = tt < a.ntl ? *gptr<u32x4>(p + (int64_t)tt * CH) : u32x4{0u, 0u, 0u, 0u};
           c[k] = *gptr<float>(gcs + tt * 32 + fl);
         }
@@ -519,23 +511,22 @@ __global__ __launch_bounds__(kT, 1) void lsq_qn_kernel(QnArgs a) {
 #pragma unroll
         for (int e = 0; e < E; ++e) acc[e] += (double)s8[e];
       }
-      // feature sum across the 32 lanes of each half (HU: across all 64 -- both halves hold the
-      // same rows), then the 8 waves' partials in LDS
+      // feature sum across the 32 lanes of each half, then the 8 waves' partials in LDS
 #pragma unroll
       for (int e = 0; e < E; ++e) {
 #pragma unroll
-        for (int o = 1; o < (HU ? 64 : 32); o <<= 1) acc[e] += __shfl_xor(acc[e], o, 64);
+        for (int o = 1; o < 32; o <<= 1) acc[e] += __shfl_xor(acc[e], o, 64);
       }
       double m = acc[0];
 #pragma unroll
       for (int e = 1; e < E; ++e) m = fl == e ? acc[e] : m;
-      if (fl < E && (!HU || hf == 0)) mrow[wave][(HU ? 0 : hf * E) + fl] = m;
+      if (fl < E) mrow[wave][hf * E + fl] = m;
       __syncthreads();
-      if (t < (HU ? E : 2 * E)) {
+      if (t < 2 * E) {
         double mm = 0.0;
 #pragma unroll
         for (int i = 0; i < kW; ++i) mm += mrow[i][t];
-        const int64_t r = HU ? frag_row<L>(s, sub, hh, t) : frag_row<L>(s, sub, t / E, t % E);
+        const int64_t r = frag_row<L>(s, sub, t / E, t % E);
         double vv = 0.0;
         if (r < a.n) {
           const double wr = a.w[r];
@@ -551,16 +542,16 @@ __global__ __launch_bounds__(kT, 1) void lsq_qn_kernel(QnArgs a) {
       __syncthreads();
       float vr[E];
 #pragma unroll
-      for (int e = 0; e < E; ++e) vr[e] = vrow[(HU ? 0 : hf * E) + e];
-      // column sums of the same tiles, most recently read first; the two lane halves (full units:
-      // the feature's other rows) combine, then one f64 LDS accumulator per feature (this wave's
-      // tiles only: no other wave touches them; HU: each lane half owns its tiles)
+      for (int e = 0; e < E; ++e) vr[e] = vrow[hf * E + e];
+      // column sums of the same tiles, most recently read first; the two lane halves (the
+      // feature's other rows) combine, then one f64 LDS accumulator per feature (this wave's
+      // tiles only: no other wave touches them)
 #pragma unroll 1
-      for (int i0 = TL - 8; i0 >= 0; i0 -= 8) {
+      for (int i0 = TPW - 8; i0 >= 0; i0 -= 8) {
         u32x4 q[8];
 #pragma unroll
         for (int k = 7; k >= 0; --k) {
-          const int tt = wave + 8 * (tb + i0 + k);
+          const int tt = wave + 8 * (i0 + k);
           q[k] = tt < a.ntl ? *gptr<u32x4>(p + (int64_t)tt * CH) : u32x4{0u, 0u, 0u, 0u};
         }
 #pragma unroll
@@ -570,8 +561,8 @@ __global__ __launch_bounds__(kT, 1) void lsq_qn_kernel(QnArgs a) {
           float sa = 0.0f;
 #pragma unroll
           for (int e = 0; e < E; ++e) sa += vr[e] * xv[e];
-          if (!HU) sa += __shfl_xor(sa, 32, 64);
-          if (HU || hf == 0) colacc[(wave + 8 * (tb + i0 + k)) * 32 + fl] += (double)sa;
+          sa += __shfl_xor(sa, 32, 64);
+          if (hf == 0) colacc[(wave + 8 * (i0 + k)) * 32 + fl] += (double)sa;
         }
       }
     }
@@ -749,35 +740,25 @@ __global__ __launch_bounds__(kT, 1) void lsq_qn_kernel(QnArgs a) {
   }
 }
 
-template <int L, int TPW, bool HU>
+template <int L, int TPW>
 const void* kernel_of() {
-  return (const void*)lsq_qn_kernel<L, TPW, HU>;
-}
-
-// half units need >= 8 tile slots per lane half (TPW >= 16: d > 2048, the l-bfgs path's widths)
-bool use_half(int tpw) {
-  static const int on = [] {
-    const char* e = getenv("DQ4ML_LSQ_QN_HALF");
-    return e ? atoi(e) : 0;
-  }();
-  return on != 0 && tpw >= 16;
+  return (const void*)lsq_qn_kernel<L, TPW>;
 }
 
 const void* pick(int layout, int tpw) {
-  const bool hu = use_half(tpw);
   if (layout == 2) {
     switch (tpw) {
-      case 8: return kernel_of<2, 8, false>();
-      case 16: return hu ? kernel_of<2, 16, true>() : kernel_of<2, 16, false>();
-      case 32: return hu ? kernel_of<2, 32, true>() : kernel_of<2, 32, false>();
-      default: return hu ? kernel_of<2, 64, true>() : kernel_of<2, 64, false>();
+      case 8: return kernel_of<2, 8>();
+      case 16: return kernel_of<2, 16>();
+      case 32: return kernel_of<2, 32>();
+      default: return kernel_of<2, 64>();
     }
   }
   switch (tpw) {
-    case 8: return kernel_of<3, 8, false>();
-    case 16: return hu ? kernel_of<3, 16, true>() : kernel_of<3, 16, false>();
-    case 32: return hu ? kernel_of<3, 32, true>() : kernel_of<3, 32, false>();
-    default: return hu ? kernel_of<3, 64, true>() : kernel_of<3, 64, false>();
+    case 8: return kernel_of<3, 8>();
+    case 16: return kernel_of<3, 16>();
+    case 32: return kernel_of<3, 32>();
+    default: return kernel_of<3, 64>();
   }
 }
 
@@ -818,7 +799,7 @@ void lsq_qn(const LsqX& x, const double* y, const double* w, const double* scale
   a.ntl = (d + 31) / 32;
   a.NT = ((d + 255) / 256) * 8;
   a.n = x.n;
-  a.nunits = ((x.n + 63) / 64) * (x.layout == 3 ? 2 : 4) * (use_half(tpw) ? 2 : 1);
+  a.nunits = ((x.n + 63) / 64) * (x.layout == 3 ? 2 : 4);
   a.y = y, a.w = w, a.scale = scale, a.shift = shift, a.head = head;
   a.fit_icpt = fit_icpt, a.std_f = std_f, a.owlqn = enet != 0.0 && reg != 0.0;
   a.reg = reg, a.enet = enet, a.tol = tol, a.max_iter = max_iter, a.hist_cap = hist_cap;
