@@ -631,13 +631,23 @@ def _udfs_of(e, acc):
     return acc
 
 
+def _storage_tag(c) -> str:
+    """A column's storage dtype for the chain key -- without building a device string column's
+    Python strings (``DeviceStringColumn.values`` materializes them; string storage is never a
+    tensor)."""
+    if isinstance(c.dtype, StringType):
+        return "-"
+    v = c.values
+    return str(v.dtype) if torch.is_tensor(v) else "-"
+
+
 def _chain_key(nodes, base: Table):
     """Structural key of (chain, base layout): expression SQL text + output names per node, the
     resolved UDF objects (a re-registered name is a new object), base column types / storage
     dtypes / validity, selection presence."""
     (parts, udfs), refs = nodes_key(nodes)
-    cols = tuple((f.name, f.dataType.simpleString(), str(c.values.dtype) if torch.is_tensor(c.values) else "-",
-                  c.valid is not None) for f, c in zip(base.schema.fields, base.columns))
+    cols = tuple((f.name, f.dataType.simpleString(), _storage_tag(c), c.valid is not None)
+                 for f, c in zip(base.schema.fields, base.columns))
     return (parts, cols, base.sel is not None, udfs), refs
 
 

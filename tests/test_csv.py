@@ -707,6 +707,42 @@ def test_device_string_column_moves_spans_until_read():
     assert [r[0] for r in t.to_rows()] == ["ab", 'x""y', "é"]
 
 
+def test_string_equality_filter_keeps_device_strings_lazy(monkeypatch):
+    """``filter(col = 'text')`` over a device string column: the engine's planning (the fused
+    chain's structural key, the filter, the projection) never builds the column's strings; the
+    comparison itself is ``eq_literal`` (here a CPU stand-in for the HBM span compare)."""
+    from net.jgp.labs.sparkdq4ml_amd import SparkSession, col
+    from net.jgp.labs.sparkdq4ml_amd.sql.dataframe import DataFrame
+    from net.jgp.labs.sparkdq4ml_amd.sql.plan import LocalRelation
+    from net.jgp.labs.sparkdq4ml_amd.sql.table import ColumnData, DeviceStringColumn, Table
+    from net.jgp.labs.sparkdq4ml_amd.sql.types import IntegerType, StringType, StructField, StructType
+
+    data = b"ab,x,ab,abc"
+    fields = [(0, 2), (3, 1), (5, 2), (8, 3)]
+    spans = torch.tensor([(fs << 25) | ln for fs, ln in fields], dtype=torch.int64)
+
+    def eq_literal(self, lit):
+        b = lit.encode()
+        out = []
+        for v in self.spans.tolist():
+            fs, ln = v >> 25, v & 0xFFFFFF
+            out.append(data[fs:fs + ln] == b)
+        return torch.tensor(out, dtype=torch.bool)
+
+    monkeypatch.setattr(DeviceStringColumn, "eq_literal", eq_literal)
+    s = DeviceStringColumn(spans, None, data, {"quote": '"', "escape": "\\"})
+    ids = ColumnData(IntegerType(), torch.arange(4, dtype=torch.int32))
+    schema = StructType([StructField("i", IntegerType(), False), StructField("s", StringType(), True)])
+    spark = SparkSession.builder().master("local[*]").getOrCreate()
+    df = DataFrame(LocalRelation(Table(schema, [ids, s], 4)), spark)
+    assert [r[0] for r in df.filter(col("s") == "ab").select("i").collect()] == [0, 2]
+    assert df.filter(col("s") != "ab").count() == 2
+    from net.jgp.labs.sparkdq4ml_amd.ops import dqvm
+
+    dqvm._chain_key([df.filter(col("s") == "ab")._plan], df._plan.table)  # (the GPU executor's key)
+    assert not s.materialized
+
+
 def test_mapped_input_string_check(tmp_path):
     """Strings of a device scan over a file MAP (inputs above the pinned cache) are built from the
     file's own pages: a changed file raises instead of yielding other bytes (or a SIGBUS)."""
