@@ -180,7 +180,6 @@ for s in $STEPS; do
     sweep1) step sweep1 600 env DQ4ML_FORCE_COLLECTIVES=1 python scripts/bucket_sweep.py --rows 2e6 --buckets-mb 4,16,64 ;;
     bandprof) (export TMPDIR=/tmp DQ4ML_FORCE_COLLECTIVES=1; step bandprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/bandprof -o run --output-format csv -- python scripts/bucket_sweep.py --rows 1e6 --buckets-mb 4 --wires f32 --reps 2) || exit $? ;;
     lsq) step lsq 600 python -u -m pytest tests/test_gpu_lsq.py -m gpu -v --maxfail=5 --timeout 120 --timeout-method thread ;;
-    streqdbg) step streqdbg 300 python -u scripts/dbg_streq.py ;;
     lbfgssmall) step lbfgssmall 600 python benchmarks/bench_lbfgs.py --rows 2e5 --features 8192 --steps 2 --warmup 1 ;;
     lbfgs) step lbfgs 900 python benchmarks/bench_lbfgs.py --steps 2 --warmup 1 --json-out gpurun_out/lbfgs.json ;;
     lbfgs8) step lbfgs8 900 python benchmarks/bench_lbfgs.py --steps 2 --warmup 1 --dtype fp8 --json-out gpurun_out/lbfgs8.json ;;
