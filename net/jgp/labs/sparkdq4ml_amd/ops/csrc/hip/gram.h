@@ -60,7 +60,7 @@ struct GramArgs {
 int64_t tiled_elems(int d, int64_t n);
 
 // GramArgs::interleave for the tall bf16 kernel (1 unless DQ4ML_GRAM_INTERLEAVE=0); the stream
-// kernels keep contiguous ranges (DQ4ML_GRAM_STREAM_INTERLEAVE=1 for A/B)
+// kernels always keep contiguous ranges (their interleaved A/B lost and was removed)
 int gram_interleave();
 // shift: per-feature f32 shift subtracted before the bf16 cast (null: none; rows >= n stay zero)
 void tile_bf16(const void* X, int xdt, int64_t ld, int d, int64_t n, void* out, hipStream_t st,
