@@ -176,10 +176,15 @@ def _fused_scan_stats(params, df: DataFrame):
         if fused is not None:
             return fused
         return scanfuse.try_fused_gram(prune_columns(df._plan, {fc, lc}), fc, lc, sess, route_key=rk)
-    plan = prune_columns(df._plan, {fc, lc})
     # bf16 / exact-f32 statistics over in-memory columns: the DQ chain in the stream Gram's
-    # stage prologue, one HBM pass (ops/streamfuse.py)
-    return streamfuse.try_fused_stream(plan, fc, lc, sess, gd)
+    # stage prologue, one HBM pass (ops/streamfuse.py); a rebuilt chain of the same structure
+    # replays the analyzed launch
+    sk = p0.skey()
+    rk = (sk, fc, lc, gd, sess.device.index) if sk is not None else None
+    fused = streamfuse.replay(rk)
+    if fused is not None:
+        return fused
+    return streamfuse.try_fused_stream(prune_columns(df._plan, {fc, lc}), fc, lc, sess, gd, route_key=rk)
 
 
 def _features_label(params, df: DataFrame):

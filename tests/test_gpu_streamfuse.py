@@ -70,3 +70,41 @@ def test_one_pass_equals_two_pass(spark, monkeypatch, d, n, gd):
     m1, m2 = lr.fit(df), lr.fit(df)
     assert np.array_equal(m1.coefficients.toArray(), m2.coefficients.toArray())  # fixed-order folds
     assert np.abs(m1.coefficients.toArray() - (0.5 + np.arange(d) / d)).max() < 0.05
+
+
+def test_rebuilt_chain_replays_the_analyzed_launch(spark):
+    """An action that rebuilds the same chain over the same in-memory relation (config 4's loop)
+    replays the analyzed stream launch (``streamfuse.replay``: no pruning, chain key or table
+    walk); the statistics are bitwise the first action's.  A re-registered rule is a new
+    structure: it is analyzed again and its own filter applies."""
+    from net.jgp.labs.sparkdq4ml_amd import LinearRegression, VectorAssembler, callUDF, col
+    from net.jgp.labs.sparkdq4ml_amd.dq.rules import RangeRule
+    from net.jgp.labs.sparkdq4ml_amd.models import regression
+    from net.jgp.labs.sparkdq4ml_amd.ops import streamfuse
+    from net.jgp.labs.sparkdq4ml_amd.sql.types import DataTypes
+
+    d, n = 24, 200_003
+    base = _df(spark, n, d)
+    src = base._plan
+    while type(src).__name__ != "LocalRelation":
+        src = src.child
+    from net.jgp.labs.sparkdq4ml_amd.sql.dataframe import DataFrame
+
+    raw = DataFrame(src, spark)
+
+    def chain():
+        df = raw.withColumn("price_ok", callUDF("rangeRule", col("price")))
+        df = df.withColumn("guest_ok", callUDF("notNullRule", col("guest")))
+        df = df.filter((col("price_ok") > 0) & (col("guest_ok") > 0))
+        return VectorAssembler(inputCols=[f"f{j}" for j in range(d)], outputCol="features").transform(df)
+
+    lr = LinearRegression(solver="normal", gramDtype="bf16", labelCol="price_ok")
+    r0 = streamfuse.STATS["stream_replays"]
+    one = regression._fused_scan_stats(lr, chain()).flat.cpu().numpy()
+    two = regression._fused_scan_stats(lr, chain()).flat.cpu().numpy()
+    assert streamfuse.STATS["stream_replays"] == r0 + 1
+    assert np.array_equal(one, two)
+    spark.udf().register("rangeRule", RangeRule(0.0, 100.0, name="rangeRule"), DataTypes.DoubleType)
+    three = regression._fused_scan_stats(lr, chain()).flat.cpu().numpy()
+    assert streamfuse.STATS["stream_replays"] == r0 + 1  # a new rule object: analyzed again
+    assert three[0] < one[0]  # the narrower range keeps fewer rows
