@@ -102,6 +102,10 @@ for s in $STEPS; do
     csvnogram) step csvnogram 600 env DQ4ML_SCAN_GRAM=0 python benchmarks/bench_csv_pipeline.py --steps 20 --warmup 3 ;;
     cfg1) step cfg1 300 python benchmarks/bench_cpu_small.py --json-out gpurun_out/cfg1.json ;;
     prof4) step prof4 600 env WHICH=cfg4 python scripts/step_profile.py ;;
+    prof4h) step prof4h 600 env WHICH=cfg4 ROWS=1e6 REPS=50 SORT=tottime TOP=45 python scripts/step_profile.py &&
+            step prof4hc 600 env WHICH=cfg4 ROWS=1e6 REPS=50 SORT=cumulative TOP=60 python scripts/step_profile.py ;;
+    proflab) step proflab 600 env WHICH=lab ROWS=1e7 REPS=100 SORT=tottime TOP=50 python scripts/step_profile.py &&
+            step proflabc 600 env WHICH=lab ROWS=1e7 REPS=100 SORT=cumulative TOP=70 python scripts/step_profile.py ;;
     prof5) step prof5 600 env WHICH=cfg5 python scripts/step_profile.py ;;
     kprof4) (export TMPDIR=/tmp; step kprof4 600 rocprofv3 --kernel-trace --stats -d gpurun_out/kprof4 -o run --output-format csv -- python benchmarks/bench_dq_pipeline.py --steps 2 --warmup 1) || exit $? ;;
     kprof5) (export TMPDIR=/tmp; step kprof5 600 rocprofv3 --kernel-trace --stats -d gpurun_out/kprof5 -o run --output-format csv -- python benchmarks/bench_wide.py --steps 1 --warmup 1) || exit $? ;;

@@ -1,4 +1,4 @@
-"""Host-side profile (cProfile) of one benchmark step: WHICH=cfg4|cfg5, after warm-up."""
+"""Host-side profile (cProfile) of one benchmark step: WHICH=cfg4|cfg5|lab, after warm-up."""
 import cProfile
 import os
 import pstats
@@ -15,6 +15,9 @@ which = os.environ.get("WHICH", "cfg4")
 if which == "cfg4":
     import bench_dq_pipeline as B
     argv = ["--steps", "1", "--warmup", "1", "--rows-per-gpu", os.environ.get("ROWS", "1.25e8")]
+elif which == "lab":
+    import bench_csv_pipeline as B
+    argv = ["--steps", "1", "--warmup", "1", "--rows", os.environ.get("ROWS", "1e6")]
 else:
     import bench_wide as B
     argv = ["--steps", "1", "--warmup", "1", "--rows", os.environ.get("ROWS", "1e7")]
@@ -33,11 +36,16 @@ def grab(step, steps, warmup, dev):
     step()
     torch.cuda.synchronize()
     print(f"[{which}] step wall ms {1e3 * (time.perf_counter() - t0):.2f}", flush=True)
+    reps = int(os.environ.get("REPS", "1"))  # >1: issue REPS steps back to back (host cost per step)
     pr = cProfile.Profile()
+    t0 = time.perf_counter()
     pr.enable()
-    out = step()
-    torch.cuda.synchronize()
+    for _ in range(reps):
+        out = step()
     pr.disable()
+    t1 = time.perf_counter()
+    torch.cuda.synchronize()
+    print(f"[{which}] {reps} steps issued in {1e3 * (t1 - t0) / reps:.3f} ms each (profiled)", flush=True)
     pstats.Stats(pr).sort_stats(os.environ.get("SORT", "cumulative")).print_stats(int(os.environ.get("TOP", "40")))
     return 1.0, out
 
