@@ -106,6 +106,7 @@ for s in $STEPS; do
             step prof4hc 600 env WHICH=cfg4 ROWS=1e6 REPS=50 SORT=cumulative TOP=60 python scripts/step_profile.py ;;
     proflab) step proflab 600 env WHICH=lab ROWS=1e7 REPS=100 SORT=tottime TOP=50 python scripts/step_profile.py &&
             step proflabc 600 env WHICH=lab ROWS=1e7 REPS=100 SORT=cumulative TOP=70 python scripts/step_profile.py ;;
+    graphprobe) step graphprobe 300 timeout -k 10 240 python scripts/graph_probe.py ;;
     prof5) step prof5 600 env WHICH=cfg5 python scripts/step_profile.py ;;
     kprof4) (export TMPDIR=/tmp; step kprof4 600 rocprofv3 --kernel-trace --stats -d gpurun_out/kprof4 -o run --output-format csv -- python benchmarks/bench_dq_pipeline.py --steps 2 --warmup 1) || exit $? ;;
     kprof5) (export TMPDIR=/tmp; step kprof5 600 rocprofv3 --kernel-trace --stats -d gpurun_out/kprof5 -o run --output-format csv -- python benchmarks/bench_wide.py --steps 1 --warmup 1) || exit $? ;;
