@@ -36,10 +36,10 @@ void lsq_columns(const LsqX& x, int mode, const double* v, const double* lpart, 
 // layouts (2 bf16, 3 fp8), d <= kLsqQnMaxD, one rank.  head: the summarizer pass [count, W, W2,
 // Σwy, Σwy², Σwx (d), Σwx² (d)]; out: [coef(d), intercept, status, reason, H, iterations, evaluations,
 // head(5), history(hist_cap)] (status 0 ok, 1 empty data, 2 constant label, 8 history overflow:
-// the host path owns those).  work: lsq_qn_work(d, blocks) doubles.
+// the host path owns those).  work: lsq_qn_work(d, blocks, n) doubles.
 constexpr int kLsqQnMaxD = 16384;
 int lsq_qn_blocks(int layout, int d);
-int64_t lsq_qn_work(int d, int blocks);
+int64_t lsq_qn_work(int d, int blocks, int64_t n);
 void lsq_qn(const LsqX& x, const double* y, const double* w, const double* scale, const double* shift,
             const double* head, bool fit_icpt, bool std_f, double reg, double enet, int max_iter, double tol,
             int hist_cap, double* work, int blocks, double* out, hipStream_t st);

@@ -62,6 +62,10 @@ struct QnArgs {
   float* cs;  // [NC] the trial's f32 effective coefficients
   double *inv_sx, *sx, *mx, *regw, *l1, *x, *g, *ag, *dir, *cx, *cg, *cag, *S, *Y, *part, *lpart, *dpart, *scal;
   double* out;  // [coef(d), intercept, status, reason, H, iters, evaluations, head(5), history(hist_cap)]
+  // L-BFGS (not OWLQN): per row, the margin of the accepted point (no offset) and X . dir of the
+  // current line search -- a trial's margins are mvec + alpha dvec, so only the first trial of a
+  // search reads X twice (it forms dvec); every other evaluation reads X once (the column pass)
+  double *mvec, *dvec;
 };
 
 __device__ __forceinline__ double block_sum(double v, double* red) {
@@ -120,6 +124,7 @@ struct Ctl {
   double value, adj, gnorm, init_adj;
   double fv[kFv];
   int nfv, iter, H, head, hh, pass, search_failed, failed_once, overflow, why, nev;
+  int first;  // L-BFGS: the next evaluation is the first of its line search (it forms dvec)
   double last_v, last_adj, last_gg;  // the last evaluation (the accepted step's values)
   // line search: backtracking (initfval, initd, shrink, it, force) / strong Wolfe (f0, d0, bracket
   // counter, lo / hi points, zoom counter), |g| of the state for the step checks
@@ -312,6 +317,7 @@ __device__ void ctl_start_search(Ctl& C, const double* scal, const QnArgs& a, do
     return;
   }
   C.ls = kLsBracket;
+  C.first = 1;
   C.f0 = C.value, C.d0 = initd;
   if (initd > 0.0) {  // "Line search invoked with non-descent direction"
     ctl_fail(C, a, hist);
@@ -438,6 +444,7 @@ __global__ __launch_bounds__(kT, 1) void lsq_qn_kernel(QnArgs a) {
       a.ag[j] = 0.0;
     }
   }
+  for (int64_t r = (int64_t)b * kT + t; r < a.n; r += (int64_t)B * kT) a.mvec[r] = 0.0, a.dvec[r] = 0.0;  // x0 = 0
   __threadfence();
   grid.sync();
 
@@ -464,7 +471,10 @@ __global__ __launch_bounds__(kT, 1) void lsq_qn_kernel(QnArgs a) {
           const double cf = nx * a.inv_sx[j];
           pm += cf * a.mx[j];
           if (a.shift) ps += a.shift[j] * cf;
-          c32 = (float)(a.scale ? cf * a.scale[j] : cf);
+          // L-BFGS: the margin loop forms X . dir (a trial is mvec + alpha dvec); OWLQN's projected
+          // trial is not affine in alpha: its margins come from the trial's coefficients
+          const double cm = owlqn ? cf : a.dir[j] * a.inv_sx[j];
+          c32 = (float)(a.scale ? cm * a.scale[j] : cm);
         }
         a.cs[j] = c32;
       }
@@ -479,7 +489,10 @@ __global__ __launch_bounds__(kT, 1) void lsq_qn_kernel(QnArgs a) {
     const double offset = a.scal[16];
     const float* __restrict__ gcs = a.cs;
 
-    // E2: the fused pass (margins, then the column sums of the same tiles)
+    // E2: the fused pass (margins, then the column sums of the same tiles).  L-BFGS: margins
+    // only on the first trial of a line search (X . dir -> dvec); the others read X once
+    const bool first = !owlqn && mode == 1 && C.first;
+    const bool skip = !owlqn && !first;
     double loss = 0.0, vsum = 0.0;
     for (int64_t u = b; u < a.nunits; u += B) {
       const int64_t s = u / UPS;
@@ -489,7 +502,7 @@ __global__ __launch_bounds__(kT, 1) void lsq_qn_kernel(QnArgs a) {
 #pragma unroll
       for (int e = 0; e < E; ++e) acc[e] = 0.0;
 #pragma unroll 1
-      for (int i0 = 0; i0 < TPW; i0 += 8) {
+      for (int i0 = 0; i0 < (skip ? 0 : TPW); i0 += 8) {
         u32x4 q[8];
         float c[8];
 #pragma unroll
@@ -524,9 +537,15 @@ __global__ __launch_bounds__(kT, 1) void lsq_qn_kernel(QnArgs a) {
       __syncthreads();
       if (t < 2 * E) {
         double mm = 0.0;
-#pragma unroll
-        for (int i = 0; i < kW; ++i) mm += mrow[i][t];
         const int64_t r = frag_row<L>(s, sub, t / E, t % E);
+        if (!skip)
+#pragma unroll
+          for (int i = 0; i < kW; ++i) mm += mrow[i][t];
+        if (!owlqn && r < a.n) {  // mm: this unit's X . dir (first trial) -> the trial's margin
+          const double md = skip ? a.dvec[r] : mm;
+          if (first) a.dvec[r] = mm;
+          mm = a.mvec[r] + alpha * md;
+        }
         double vv = 0.0;
         if (r < a.n) {
           const double wr = a.w[r];
@@ -676,7 +695,7 @@ __global__ __launch_bounds__(kT, 1) void lsq_qn_kernel(QnArgs a) {
     C.alpha = 0.0;
     C.ls = kLsInit;
     C.head = 0, C.hh = 0, C.H = 0, C.iter = 0, C.nfv = 1, C.pass = 0;
-    C.search_failed = 0, C.failed_once = 0, C.overflow = 0, C.why = -1, C.nev = 0;
+    C.search_failed = 0, C.failed_once = 0, C.overflow = 0, C.why = -1, C.nev = 0, C.first = 0;
     for (int i = 0; i < kFv; ++i) C.fv[i] = 0.0;
     C.fv[kFv - 1] = __builtin_inf();
   }
@@ -688,6 +707,7 @@ __global__ __launch_bounds__(kT, 1) void lsq_qn_kernel(QnArgs a) {
       const Eval ev = evaluate(C.mode, C.alpha);
       if (t == 0) {
         ++C.nev;
+        C.first = 0;
         ctl_after_eval(C, ev, a, b == 0 ? a.out + d + 11 : nullptr);
       }
     } else if (act == kActAccept) {
@@ -706,6 +726,10 @@ __global__ __launch_bounds__(kT, 1) void lsq_qn_kernel(QnArgs a) {
           a.ag[j] = a.cag[j];
         }
         __threadfence();
+      }
+      if (!owlqn && C.ls != kLsInit) {  // the accepted trial's margins: mvec + alpha dvec
+        const double al = C.alpha;
+        for (int64_t r = (int64_t)b * kT + t; r < a.n; r += (int64_t)B * kT) a.mvec[r] = a.mvec[r] + al * a.dvec[r];
       }
       __syncthreads();
       if (t == 0) ctl_after_accept(C, a, b == 0 ? a.out + d + 11 : nullptr);
@@ -781,9 +805,10 @@ int lsq_qn_blocks(int layout, int d) {
   return cus;  // one block per CU (co-resident: the cooperative launch checks it)
 }
 
-int64_t lsq_qn_work(int d, int blocks) {
+int64_t lsq_qn_work(int d, int blocks, int64_t n) {
   const int64_t slab = 8LL * tpw_of(d) * 32;
-  return 12LL * d + 2LL * kMem * d + (int64_t)blocks * slab + 2LL * blocks + (int64_t)blocks * kDParts + 24 + (8LL * tpw_of(d) * 32 + 1) / 2;
+  return 12LL * d + 2LL * kMem * d + (int64_t)blocks * slab + 2LL * blocks + (int64_t)blocks * kDParts + 24 +
+         (8LL * tpw_of(d) * 32 + 1) / 2 + 2 * n;
 }
 
 void lsq_qn(const LsqX& x, const double* y, const double* w, const double* scale, const double* shift,
@@ -817,6 +842,7 @@ void lsq_qn(const LsqX& x, const double* y, const double* w, const double* scale
   a.dpart = take((int64_t)blocks * kDParts);
   a.scal = take(24);
   a.cs = reinterpret_cast<float*>(take((8LL * tpw * 32 + 1) / 2));
+  a.mvec = take(x.n), a.dvec = take(x.n);
   a.out = out;
   void* args[] = {&a};
   DQ_HIP_CHECK(hipLaunchCooperativeKernel(pick(x.layout, tpw), dim3(blocks), dim3(kT), args, 0, st));

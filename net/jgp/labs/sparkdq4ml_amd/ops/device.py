@@ -790,7 +790,7 @@ class LsqPasses:
         if nb is None:
             nb = _lsq_qn_grid[key] = int(h.lsq_qn_blocks(self.layout, self.d))
         cap = wls_qn_cap(max_iter)
-        work = torch.empty(int(h.lsq_qn_work(self.d, nb)), dtype=torch.float64, device=self.device)
+        work = torch.empty(int(h.lsq_qn_work(self.d, nb, self.n)), dtype=torch.float64, device=self.device)
         out = torch.empty(self.d + 11 + cap, dtype=torch.float64, device=self.device)
         head = head.to(torch.float64).contiguous()
         if head.numel() != 5 + 2 * self.d:
