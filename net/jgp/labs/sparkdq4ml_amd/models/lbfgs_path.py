@@ -260,11 +260,37 @@ def _train_passes(est, df, X, y, w, sel, d, checks=(), device_qn=True):
     icpt0 = torch.tensor(my / ys if fit_icpt else 0.0, dtype=torch.float64, device=dev)
     inv_ys, inv_w = 1.0 / ys, 1.0 / W
 
-    def fg(x):
+    # L-BFGS line searches (not OWLQN: its projected trial is not affine in alpha): a trial x + a d
+    # has u = w (x' . cf) = u(x) + a u(d), so only a search's first trial forms u(d) (a margin
+    # pass); every trial then runs the column pass alone, and the loss along the search is an
+    # exact quadratic in a (no per-trial rounding noise: the searches accept at once)
+    ucache = {}   # id(x) -> (x, u(x)) of the current base point and its trials
+    udir = [None]  # (d, base x, u(d)) of the current search
+
+    def fg(x, line=None):
         cf = x * inv_sx
         offset = icpt0 - torch.dot(cf, mx_t) if fit_icpt else icpt0
-        with tracing.span("lsq_pass"):
-            out = P.evaluate(cf, offset, inv_ys)
+        if line is not None and l1vec is None:
+            bx, dvec, a = line
+            ent = ucache.get(id(bx))
+            if ent is None or ent[0] is not bx:
+                with tracing.span("lsq_pass"):
+                    ent = (bx, P.wmargins(bx * inv_sx))
+                ucache.clear()
+                ucache[id(bx)] = ent
+            cur = udir[0]
+            if cur is None or cur[0] is not dvec or cur[1] is not bx:
+                with tracing.span("lsq_pass"):
+                    cur = udir[0] = (dvec, bx, P.wmargins(dvec * inv_sx))
+                for k in [k for k, e in ucache.items() if e[0] is not bx]:  # a new search: old trials go
+                    del ucache[k]
+            u = ent[1] + a * cur[2]
+            ucache[id(x)] = (x, u)
+            with tracing.span("lsq_pass"):
+                out = P.evaluate_u(u, cf, offset, inv_ys)
+        else:
+            with tracing.span("lsq_pass"):
+                out = P.evaluate(cf, offset, inv_ys)
         with tracing.span("allreduce"):
             out = comm.all_reduce_sum(out)  # X4: (d + 1) f64 per evaluation
         tracing.add_rows("lsq_pass", P.n)
@@ -283,7 +309,10 @@ def _train_passes(est, df, X, y, w, sel, d, checks=(), device_qn=True):
     resume = ck.load() if ck is not None else None
     if resume is not None:
         log.info("resuming l-bfgs at iteration %d from %s", int(resume["iter"]), ck.path)
-    x, hist, reason = minimize(fg, torch.zeros(d, dtype=torch.float64, device=dev), max_iter, tol, l1vec,
+    fg.line_aware = True
+    x0 = torch.zeros(d, dtype=torch.float64, device=dev)
+    ucache[id(x0)] = (x0, torch.zeros(P.n, dtype=torch.float64, device=dev))  # u(0) = 0
+    x, hist, reason = minimize(fg, x0, max_iter, tol, l1vec,
                                resume=resume, on_iteration=ck.maybe_save if ck is not None else None)
     if ck is not None:
         ck.clear()

@@ -60,8 +60,11 @@ def minimize(fg: Callable[[torch.Tensor], Tuple[torch.Tensor, torch.Tensor]], x0
         ag = torch.where(x == 0, at0, g + torch.sign(x) * l1)
         return av, torch.where(lz, g, ag)
 
-    def evaluate(x):
-        v, g = fg(x)
+    line_aware = getattr(fg, "line_aware", False)
+
+    def evaluate(x, line=None):
+        # line = (x, d, a) of a trial x + a d: a line-aware fg may combine its passes along the line
+        v, g = fg(x, line) if (line_aware and line is not None) else fg(x)
         av, ag = adjust(x, g, v)
         return v, g, av, ag
 
@@ -102,7 +105,7 @@ def minimize(fg: Callable[[torch.Tensor], Tuple[torch.Tensor, torch.Tensor]], x0
             dd = torch.dot(st.adj_grad if owlqn else st.grad, d)
             return (st.adj_h if owlqn else st.value_h), float(dd)
         nx = take_step(st, d, a)
-        v, g, av, ag = evaluate(nx)
+        v, g, av, ag = evaluate(nx, None if owlqn else (st.x, d, a))
         f, dd = torch.stack([av if owlqn else v, torch.dot(ag if owlqn else g, d)]).tolist()
         last.clear()
         last.update(a=a, x=nx, v=v, g=g, av=av, ag=ag)
@@ -239,7 +242,7 @@ def minimize(fg: Callable[[torch.Tensor], Tuple[torch.Tensor, torch.Tensor]], x0
                 nx, v, g, av, ag = last["x"], last["v"], last["g"], last["av"], last["ag"]
             else:
                 nx = take_step(st, d, step)
-                v, g, av, ag = evaluate(nx)
+                v, g, av, ag = evaluate(nx, None if owlqn else (st.x, d, step))
             hist_s.insert(0, nx - st.x)
             hist_y.insert(0, g - st.grad)
             del hist_s[memory:], hist_y[memory:]

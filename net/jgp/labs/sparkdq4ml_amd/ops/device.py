@@ -774,6 +774,40 @@ class LsqPasses:
             out[1:] += self.shift.dev64 * self._v[:self.n].sum()
         return out
 
+    def wmargins(self, cf: torch.Tensor) -> torch.Tensor:
+        """u = w (x' . cf) per row (f64 [n], a fresh tensor): the coefficient-linear part of a
+        trial's v = w diff, so a line search's trials are u(x) + alpha u(dir) (``evaluate_u``)."""
+        c = cf.to(torch.float64)
+        if self.scales is not None:
+            c = c * self.scales
+        c = c.contiguous() if self.layout == 0 else c.to(torch.float32).contiguous()
+        zero = torch.zeros(1, dtype=torch.float64, device=self.device)
+        self._h.lsq_margin(*self._desc, c.data_ptr(), zero.data_ptr(), 0.0, self.y.data_ptr(), self.w.data_ptr(),
+                           self._v.data_ptr(), self._lpart.data_ptr(), _stream())
+        return self._v[:self.n].clone()
+
+    def evaluate_u(self, u: torch.Tensor, cf: torch.Tensor, offset: torch.Tensor, inv_ystd: float) -> torch.Tensor:
+        """``evaluate`` from the trial's u = w (x' . cf) (``wmargins``, combined along the line): v =
+        u + w (offset - y inv_ystd), the loss Σ ½ v² / w, then the column pass alone (one read of X)."""
+        c = cf.to(torch.float64)
+        off = offset.to(torch.float64).reshape(())
+        if self.shift is not None:
+            off = off + (self.shift.dev64 * c).sum()
+        v = u + self.w * (off - self.y * inv_ystd)
+        live = self.w != 0
+        loss = torch.where(live, 0.5 * v * v / torch.where(live, self.w, torch.ones_like(self.w)), torch.zeros_like(v)).sum()
+        self._v[:self.n].copy_(v)
+        self._lpart.zero_()
+        self._lpart[:1].copy_(loss.reshape(1))
+        out = torch.empty(1 + self.d, dtype=torch.float64, device=self.device)
+        self._h.lsq_columns(*self._desc, 0, self._v.data_ptr(), self._lpart.data_ptr(), self.nl,
+                            self._part[0].data_ptr(), out.data_ptr(), _stream())
+        if self.scales is not None:
+            out[1:] *= self.scales
+        if self.shift is not None:
+            out[1:] += self.shift.dev64 * v.sum()
+        return out
+
 
     def qn_fit(self, head: torch.Tensor, fit_icpt: bool, std_f: bool, reg: float, enet: float, max_iter: int,
                tol: float) -> Optional[torch.Tensor]:

@@ -252,6 +252,19 @@ class _HostLsq:
         out[1:] = self._Xz @ v
         return out
 
+    def wmargins(self, cf):
+        return self.w * (cf.to(torch.float64) @ self._Xz)
+
+    def evaluate_u(self, u, cf, offset, inv_ystd):
+        live = self.w != 0
+        v = torch.where(live, u + self.w * (torch.as_tensor(offset, dtype=torch.float64).reshape(()) - self.y * inv_ystd),
+                        torch.zeros_like(u))
+        out = torch.empty(1 + self.d, dtype=torch.float64)
+        out[0] = torch.where(live, 0.5 * v * v / torch.where(live, self.w, torch.ones_like(self.w)),
+                             torch.zeros_like(v)).sum()
+        out[1:] = self._Xz @ v
+        return out
+
 
 def lsq_passes(X, y: torch.Tensor, w: Optional[torch.Tensor], sel: Optional[torch.Tensor]):
     """Per-fit state of the squared-loss l-bfgs path: ``.scalars()``,
