@@ -75,6 +75,16 @@ def test_lsq_passes_match_oracle(kind, d, n):
     assert np.all(np.abs(mo[d:].numpy() - mref[d:].numpy()) <= rt * mref[d:].numpy() + 1e-30)
     sc = P.scalars().cpu()
     np.testing.assert_allclose(sc.numpy(), H.scalars().numpy(), rtol=1e-12)
+    # a line-search trial cf + a dcf from u(cf) + a u(dcf) (wmargins) and the column pass alone
+    dcf = torch.randn(d, generator=g, device=dev, dtype=torch.float64) / np.sqrt(d)
+    a = 0.37
+    u = P.wmargins(cf) + a * P.wmargins(dcf)
+    got_u = P.evaluate_u(u, cf + a * dcf, off, 0.7).cpu()
+    ref_u = H.evaluate(cf.cpu() + a * dcf.cpu(), off.cpu(), 0.7)
+    diff_u = (cf.cpu() + a * dcf.cpu()) @ Xd + 0.3 - 0.7 * H.y
+    v_u = H.w * diff_u
+    assert abs(float(got_u[0]) - float(ref_u[0])) <= 2 * rt * float((0.5 * v_u.abs() * diff_u.abs()).sum()) + 1e-12
+    assert np.all(np.abs(got_u[1:].numpy() - ref_u[1:].numpy()) <= 2 * rt * ((Xd.abs() @ v_u.abs()).numpy() + 1e-30))
 
 
 @pytest.mark.parametrize("kw", [dict(regParam=0.02, elasticNetParam=0.0), dict(regParam=0.02, elasticNetParam=0.6)])

@@ -140,6 +140,12 @@ def test_host_lsq_oracle_matches_definition(cpu_session):
     mo = P.moments()
     np.testing.assert_allclose(mo[:d].numpy(), (Xs @ ws).numpy(), rtol=1e-12)
     np.testing.assert_allclose(mo[d:].numpy(), ((Xs * Xs) @ ws).numpy(), rtol=1e-12)
+    # line-search trials: u(cf) + a u(dcf) (wmargins) then the column pass (evaluate_u) = evaluate
+    dcf = torch.randn(d, generator=g, dtype=torch.float64)
+    u = P.wmargins(cf) + 0.6 * P.wmargins(dcf)
+    lu = P.evaluate_u(u, cf + 0.6 * dcf, torch.tensor(0.25, dtype=torch.float64), 0.5)
+    np.testing.assert_allclose(lu.numpy(), P.evaluate(cf + 0.6 * dcf, torch.tensor(0.25, dtype=torch.float64), 0.5).numpy(),
+                               rtol=1e-10)
 
 
 # ---- X4 across processes (gloo here; RCCL on the MI355X node) ---------------------------------
