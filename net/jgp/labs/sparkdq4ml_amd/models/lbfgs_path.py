@@ -154,11 +154,16 @@ class _PendingLsq:
     def __init__(self, out, d, solver, checks, fallback):
         self.out, self.d, self.solver, self._checks, self._fallback = out, d, solver, list(checks), fallback
         self._res = None
+        # the fit's stream: resolve() may run under another stream context, so its read waits on
+        # this event instead of on whatever stream is current then
+        self._done = torch.cuda.Event()
+        self._done.record()
 
     def resolve(self):
         if self._res is None:
             from .optim import WLSModel
 
+            torch.cuda.current_stream(self.out.device).wait_event(self._done)
             host = self.out.cpu().numpy()
             verify(self._checks)
             d = self.d
@@ -285,6 +290,10 @@ def _train_passes(est, df, X, y, w, sel, d, checks=(), device_qn=True):
                 for k in [k for k, e in ucache.items() if e[0] is not bx]:  # a new search: old trials go
                     del ucache[k]
             u = ent[1] + a * cur[2]
+            # keep the base point and THIS trial only (a search accepts its last trial, which is
+            # the next search's base): an n-f64 margin vector per earlier trial would pile up
+            for k in [k for k, e in ucache.items() if e[0] is not bx]:
+                del ucache[k]
             ucache[id(x)] = (x, u)
             with tracing.span("lsq_pass"):
                 out = P.evaluate_u(u, cf, offset, inv_ys)

@@ -206,7 +206,7 @@ def minimize(fg: Callable[[torch.Tensor], Tuple[torch.Tensor, torch.Tensor]], x0
         initial_adj = float(resume["initial_adj"])
         search_failed, failed_once = bool(resume["search_failed"]), bool(resume["failed_once"])
     else:
-        st.x = x0.clone()
+        st.x = x0  # never modified in place (every step builds a new tensor): a line-aware fg may key on it
         st.value, st.grad, st.adj_value, st.adj_grad = evaluate(st.x)
         st.value_h, st.adj_h, st.gnorm = torch.stack([st.value, st.adj_value,
                                                       torch.linalg.vector_norm(st.adj_grad)]).tolist()

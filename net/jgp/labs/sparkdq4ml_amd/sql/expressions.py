@@ -240,9 +240,14 @@ class BinOp(Expr):
         lt, rt = self.left.data_type(schema), self.right.data_type(schema)
         if isinstance(lt, StringType) and isinstance(rt, StringType):
             return lt
-        if (isinstance(lt, TimestampType) and isinstance(rt, (TimestampType, StringType))) or \
+        if isinstance(lt, TimestampType) and isinstance(rt, TimestampType):
+            return lt
+        if (isinstance(lt, TimestampType) and isinstance(rt, StringType)) or \
                 (isinstance(rt, TimestampType) and isinstance(lt, StringType)):
-            return TimestampType()  # Spark 2.4 PromoteStrings: the string side becomes a timestamp
+            # Spark 2.4 findCommonTypeForBinaryComparison: (Timestamp, String) -> StringType, the
+            # timestamp side is printed (yyyy-MM-dd HH:mm:ss[.f]) and the two compare as text
+            # (casting the string to a timestamp instead is Spark 3.0)
+            return StringType()
         if isinstance(lt, StringType) or isinstance(rt, StringType):
             # Spark casts the string side to the numeric type (or double)
             return DoubleType()
@@ -294,6 +299,9 @@ class BinOp(Expr):
             return ColumnData(BooleanType(), (lm & rm & eq) | (~lm & ~rm), None)
         if isinstance(l.dtype, TimestampType) or isinstance(r.dtype, TimestampType):
             t = self.operand_type(schema)
+            if isinstance(t, StringType) and self.op in _CMP:
+                l, r = cast_column(l, t, ctx.device), cast_column(r, t, ctx.device)
+                return BinOp._string_cmp(self.op, l, r, valid, ctx.device)
             if not isinstance(t, TimestampType) or self.op not in _CMP:
                 raise AnalysisException(f"cannot resolve '{self.sql_name()}' due to data type mismatch")
             l = l if isinstance(l.dtype, TimestampType) else _cast_timestamp(l, l.dtype, t, ctx.device)
@@ -306,15 +314,7 @@ class BinOp(Expr):
         if isinstance(l.dtype, StringType) and isinstance(r.dtype, StringType):
             if self.op not in _CMP:
                 raise AnalysisException(f"operator {self.op} on strings")
-            py = {"<": lambda a, b: a < b, ">": lambda a, b: a > b, "<=": lambda a, b: a <= b,
-                  ">=": lambda a, b: a >= b, "=": lambda a, b: a == b, "==": lambda a, b: a == b,
-                  "!=": lambda a, b: a != b, "<>": lambda a, b: a != b}[self.op]
-            vals = [bool(py(a, b)) if a is not None and b is not None else False for a, b in zip(l.values, r.values)]
-            vmask = [a is not None and b is not None for a, b in zip(l.values, r.values)]
-            vt = torch.tensor(vmask, dtype=torch.bool, device=ctx.device)
-            if valid is not None:
-                vt = vt & valid
-            return ColumnData(BooleanType(), torch.tensor(vals, dtype=torch.bool, device=ctx.device), vt)
+            return BinOp._string_cmp(self.op, l, r, valid, ctx.device)
         t = self.operand_type(schema)
         if isinstance(l.dtype, StringType) or isinstance(r.dtype, StringType):
             l, r = _string_to_double(l, ctx), _string_to_double(r, ctx)
@@ -337,6 +337,21 @@ class BinOp(Expr):
             nv = ~zero if valid is None else (valid & ~zero)
             return ColumnData(t, out, None if bool(nv.all()) else nv)
         raise AnalysisException(f"unsupported operator {self.op}")
+
+    @staticmethod
+    def _string_cmp(op, l: ColumnData, r: ColumnData, valid, device) -> ColumnData:
+        """Lexicographic comparison of two string columns (UTF-16 order = code-point order for
+        the BMP text the reader produces); a null on either side gives null."""
+        py = {"<": lambda a, b: a < b, ">": lambda a, b: a > b, "<=": lambda a, b: a <= b,
+              ">=": lambda a, b: a >= b, "=": lambda a, b: a == b, "==": lambda a, b: a == b,
+              "!=": lambda a, b: a != b, "<>": lambda a, b: a != b}[op]
+        lv, rv = l.to_pylist(), r.to_pylist()
+        vals = [bool(py(a, b)) if a is not None and b is not None else False for a, b in zip(lv, rv)]
+        vmask = [a is not None and b is not None for a, b in zip(lv, rv)]
+        vt = torch.tensor(vmask, dtype=torch.bool, device=device)
+        if valid is not None:
+            vt = vt & valid
+        return ColumnData(BooleanType(), torch.tensor(vals, dtype=torch.bool, device=device), vt)
 
 
 def _device_string_eq(op: "BinOp", l: ColumnData, r: ColumnData):

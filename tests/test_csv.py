@@ -789,8 +789,9 @@ def test_timestamp_casts(cpu_session, tmp_path):
 
 
 def test_timestamp_comparisons(cpu_session, tmp_path):
-    """A timestamp compared with a string literal: the string side is cast to a timestamp (Spark
-    2.4 ``PromoteStrings``); timestamps compare as instants."""
+    """A timestamp compared with a string literal: Spark 2.4's ``findCommonTypeForBinaryComparison``
+    maps (timestamp, string) to string, so the timestamp is printed (``yyyy-MM-dd HH:mm:ss[.f]``)
+    and the two compare as text (Spark 3.0 would cast the string to a timestamp instead)."""
     p = tmp_path / "ts.csv"
     p.write_bytes(b"2019-01-01,1\r2019-06-15 08:30:00,2\r2020-02-29T12:00:00Z,3\r")
     df = cpu_session.read().option("inferSchema", "true").csv(str(p))
@@ -799,6 +800,14 @@ def test_timestamp_comparisons(cpu_session, tmp_path):
     assert got == [2, 3]
     got = [r[0] for r in cpu_session.sql("SELECT _c1 FROM t WHERE _c0 < '2019-03-01'").collect()]
     assert got == [1]
+    # the rules differ on date-only literals: a midnight timestamp prints as '2019-01-01 00:00:00',
+    # which is neither equal to nor <= the text '2019-01-01' (3.0's instant rule gives row 1 both times)
+    assert cpu_session.sql("SELECT _c1 FROM t WHERE _c0 = '2019-01-01'").collect() == []
+    assert cpu_session.sql("SELECT _c1 FROM t WHERE _c0 <= '2019-01-01'").collect() == []
+    got = [r[0] for r in cpu_session.sql("SELECT _c1 FROM t WHERE _c0 > '2019'").collect()]
+    assert got == [1, 2, 3]  # text order: every '2019-…' / '2020-…' string sorts after '2019'
+    got = [r[0] for r in cpu_session.sql("SELECT _c1 FROM t WHERE '2019-06-15 08:30:00' = _c0").collect()]
+    assert got == [2]
 
 
 def test_timestamp_csv_write_round_trip(cpu_session, tmp_path):

@@ -29,6 +29,40 @@ def _fit(lr, df, monkeypatch, device_qn: bool):
     return lr.fit(df)
 
 
+def _oracle(T, y, regParam, elasticNetParam, fitIntercept=True, standardization=True):
+    """Independent fp64 optimum of Spark 2.4's standardized l-bfgs objective on the DEQUANTIZED
+    tiles (``T.to_dense()``): sample-std standardization, ``effectiveRegParam = regParam / yStd``,
+    0.5 c'Ac - b'c + L2 + L1 — a direct solve without L1, proximal gradient (ISTA, fp64) with it.
+    Shares no code with either fit path."""
+    X = T.to_dense().double()  # [d, n]
+    y = y.double()
+    n = X.shape[1]
+    mx, my = X.mean(1), y.mean()
+    sx = ((X - mx[:, None]) ** 2).sum(1).div(n - 1).sqrt()
+    sy = float(((y - my) ** 2).sum().div(n - 1).sqrt())
+    safe = torch.where(sx == 0, torch.ones_like(sx), sx)
+    Xs = ((X - mx[:, None]) if fitIntercept else X) / safe[:, None]
+    ys = ((y - my) if fitIntercept else y) / sy
+    A = Xs @ Xs.T / n
+    b = Xs @ ys / n
+    eff = regParam / sy
+    l1, l2 = elasticNetParam * eff, (1.0 - elasticNetParam) * eff
+    w2 = torch.ones_like(sx) if standardization else 1.0 / (safe * safe)
+    w1 = torch.full_like(sx, l1) if standardization else l1 / safe
+    H = A + torch.diag(l2 * w2)
+    if l1 == 0.0:
+        c = torch.linalg.solve(H, b)
+    else:
+        L = float(torch.linalg.eigvalsh(H).max())
+        c = torch.zeros_like(b)
+        for _ in range(4000):
+            z = c - (H @ c - b) / L
+            c = torch.sign(z) * torch.clamp(z.abs() - w1 / L, min=0.0)
+    coef = torch.where(sx == 0, torch.zeros_like(c), c * sy / safe)
+    icpt = float(my - coef @ mx) if fitIntercept else 0.0
+    return coef.cpu().numpy(), icpt
+
+
 @pytest.mark.parametrize("eb,d,n,kw", [
     (16, 300, 60_001, dict(regParam=0.02, elasticNetParam=0.0)),                      # L-BFGS, strong Wolfe
     (16, 300, 60_001, dict(regParam=0.02, elasticNetParam=0.6)),                      # OWLQN, backtracking
@@ -37,14 +71,15 @@ def _fit(lr, df, monkeypatch, device_qn: bool):
 ])
 def test_device_qn_matches_host_steered(gpu_session, monkeypatch, eb, d, n, kw):
     from net.jgp.labs.sparkdq4ml_amd import LinearRegression
-    from net.jgp.labs.sparkdq4ml_amd.models import lbfgs_path
-
     T, y = _data(gpu_session.device, d, n, d + eb, eb)
     df = gpu_session.createDataFrame({"features": T, "label": y})
     lr = LinearRegression(solver="l-bfgs", maxIter=60, tol=1e-9, **kw)
     m_dev = _fit(lr, df, monkeypatch, True)
     assert m_dev.summary.solver == ("owlqn" if kw["elasticNetParam"] else "l-bfgs")
+    # the cooperative lsq_qn launch ran (set only by its pending result, lbfgs_path._PendingLsq)
+    assert m_dev._qn_evaluations is not None and m_dev._qn_evaluations > 0
     m_host = _fit(lr, df, monkeypatch, False)
+    assert getattr(m_host, "_qn_evaluations", None) is None  # the host-steered path really ran
     a, b = m_dev.coefficients.toArray(), m_host.coefficients.toArray()
     # the device pass sums the columns in a different f32 / f64 order than the two-pass kernels:
     # the iterates agree to the optimizer's own resolution, not bitwise
@@ -58,7 +93,12 @@ def test_device_qn_matches_host_steered(gpu_session, monkeypatch, eb, d, n, kw):
     # the device fit is deterministic: fixed-order reductions everywhere
     m_again = _fit(lr, df, monkeypatch, True)
     assert np.array_equal(m_again.coefficients.toArray(), a)
-    assert lbfgs_path._device_qn_ok is not None
+    # independent fp64 oracle of the same dequantized problem (no code shared with either path)
+    oc, oi = _oracle(T, y, **kw)
+    scale = max(1.0, np.abs(oc).max())
+    err = np.abs(a - oc).max()
+    assert err <= 2e-3 * scale, (err, scale)
+    assert float(m_dev.intercept) == pytest.approx(oi, rel=2e-3, abs=2e-3 * scale)
 
 
 def test_device_qn_async_fit_has_no_host_sync(gpu_session, monkeypatch):
