@@ -136,10 +136,12 @@ def _check_constant_label(raw_ys: float, reg: float) -> None:
 
 
 def _device_qn_ok(df, P) -> bool:
-    """The whole fit as one device launch (``LsqPasses.qn_fit``): one rank, wide tiles on a GPU,
-    no optimizer checkpoints (those read the state on the host every few iterations)."""
+    """The whole fit on the device: wide tiles on a GPU, no optimizer checkpoints (those read the
+    state on the host every few iterations).  One rank: ONE cooperative launch
+    (``LsqPasses.qn_fit``); with collectives active: the data-parallel form
+    (``LsqPasses.qn_fit_dp``: pass, fold, all-reduce, control kernel per evaluation)."""
     sess = getattr(df, "sparkSession", None)
-    return (P.device.type == "cuda" and P.layout in (2, 3) and not comm.collectives_active()
+    return (P.device.type == "cuda" and P.layout in (2, 3)
             and not (sess is not None and sess.conf.get("dq4ml.lbfgs.checkpointDir", ""))
             and os.environ.get("DQ4ML_LSQ_QN", "1") != "0")
 
@@ -203,7 +205,10 @@ def _train_passes(est, df, X, y, w, sel, d, checks=(), device_qn=True):
     max_iter, tol = int(est.getOrDefault("maxIter")), float(est.getOrDefault("tol"))
     if device_qn and _device_qn_ok(df, P):
         with tracing.span("solve"):
-            out = P.qn_fit(head, fit_icpt, std_flag, reg, enet, max_iter, tol)
+            if comm.collectives_active():  # X4: one (d + 2)-f64 all-reduce per evaluation, no host read
+                out = P.qn_fit_dp(head, fit_icpt, std_flag, reg, enet, max_iter, tol, comm.all_reduce_sum)
+            else:
+                out = P.qn_fit(head, fit_icpt, std_flag, reg, enet, max_iter, tol)
         if out is not None:
             solver = "owlqn" if enet != 0.0 and reg != 0.0 else "l-bfgs"
 

@@ -28,7 +28,7 @@ from ..ops import device, kernels, native
 from ..ops.layout import TiledBF16
 from ..parallel import comm
 from ..sql.dataframe import DataFrame
-from ..runtime import faststream
+from ..runtime import faststream, streams
 from ..runtime.checks import defer, verify
 from ..sql.expressions import AnalysisException, ColRef, EvalContext, Expr, SparkException
 from ..sql.plan import Filter, Project, execute
@@ -434,7 +434,8 @@ class _FitReplay:
         self.checks, self.d = list(checks), d
         self.args = _wls_args(est, d)[1:]
         self.dev = faststream.dev_index(df.sparkSession.device)
-        self.ring = _pipe_streams[df.sparkSession.device]
+        dev = df.sparkSession.device
+        self.ring = _pipe_streams[(dev, _tail_masks(dev) is not None)]
         # (event, stream) after the recorded fit's operands were made: every other pipeline
         # stream waits for it before its first replay
         self.ready = ready
@@ -554,19 +555,69 @@ def _pipe_stream(df, tbl):
     dev = getattr(sess, "device", None)
     if depth < 2 or dev is None or dev.type != "cuda":
         return None
-    ring = _pipe_streams.get(dev)
+    masks = _tail_masks(dev)
+    key = (dev, masks is not None)
+    ring = _pipe_streams.get(key)
     if ring is None or len(ring[1]) != depth:
-        ring = _pipe_streams[dev] = [0, [torch.cuda.Stream(device=dev) for _ in range(depth)]]
+        if masks is not None:  # Gram passes off the CUs reserved for the fit tail
+            ring = [0, [streams.cu_masked_stream(masks[0], masks[2], dev, tag=i) for i in range(depth)]]
+        else:
+            ring = [0, [torch.cuda.Stream(device=dev) for _ in range(depth)]]
+        _pipe_streams[key] = ring
     st = ring[1][ring[0] % depth]
     ring[0] += 1
     native.hip().stream_wait(st.cuda_stream, faststream.raw(faststream.dev_index(dev)))
     return st
 
 
+# DQ4ML_TAIL_STANDIN=blocks:usec -- after each overlapped fit's all-reduce, a stand-in kernel of
+# `blocks` workgroups holding a CU slot for `usec` us (rowops.hip standin) runs on the tail
+# stream, bracketed by timing events: (end - start) - usec is how long the emulated collective
+# waited for CUs beside the next fit's Gram pass (tests/test_gpu_pipeline.py, ops/device.py
+# set_gram_reserve).  None: off.
+_STANDIN = None
+STANDIN_EVENTS = []
+
+
+def set_tail_standin(spec):
+    global _STANDIN
+    _STANDIN = None if not spec else tuple(int(v) for v in str(spec).split(":"))
+    STANDIN_EVENTS.clear()
+
+
+def _standin(h, side):
+    blocks, usec = _STANDIN
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(side)
+    h.standin(blocks, usec, side.cuda_stream)
+    e1.record(side)
+    STANDIN_EVENTS.append((e0, e1, usec))
+
+
+set_tail_standin(os.environ.get("DQ4ML_TAIL_STANDIN"))
+
+
+def _tail_masks(dev):
+    """(Gram CUs, tail CUs, CU count) when ``dq4ml.gram.reserveCUs`` > 0 and CU masking is on
+    (``DQ4ML_CU_MASK``, default 1), else None: the pipelined Gram passes and the fit tail then run
+    on disjoint CUs, so a tail kernel never holds a CU a Gram block waits for and vice versa
+    (profiles/r5_tail_reserve.md)."""
+    reserve = device.gram_reserve()
+    if reserve <= 0 or os.environ.get("DQ4ML_CU_MASK", "1") == "0" or dev is None or dev.type != "cuda":
+        return None
+    cus = device._cus(native.hip())
+    tail = streams.reserved_cu_ids(reserve, cus)
+    keep = [c for c in range(cus) if c not in set(tail)]
+    return keep, tail, cus
+
+
 def _tail_stream(dev) -> "torch.cuda.Stream":
-    st = _tail_streams.get(dev)
+    masks = _tail_masks(dev)
+    key = (dev, masks is not None)
+    st = _tail_streams.get(key)
     if st is None:
-        st = _tail_streams[dev] = torch.cuda.Stream(device=dev)
+        st = _tail_streams[key] = (streams.cu_masked_stream(masks[1], masks[2], dev, tag=99) if masks is not None
+                                   else torch.cuda.Stream(device=dev))
     return st
 
 
@@ -604,6 +655,8 @@ class _PendingWLS:
                 flat.record_stream(side)  # produced on the compute stream, consumed here
                 with tracing.span("allreduce"):
                     flat = comm.all_reduce_sum(flat)
+                if _STANDIN is not None:  # (diagnostics) a collective's channel blocks, emulated
+                    _standin(h, side)
                 self.out = solve(flat)
                 self._done = h.event_record(side.cuda_stream)  # a native ring event of the side stream
         else:

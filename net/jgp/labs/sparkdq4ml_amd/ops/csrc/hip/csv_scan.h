@@ -17,7 +17,10 @@ int64_t csv_count_blocks(int64_t n);
 // total at [nb]); then ends (total entries) -> the ordered line-end offsets, reusing counts.
 // ends are int32 when csv_ends_i32(n) (inputs below 2 GiB), else int64
 bool csv_ends_i32(int64_t n);
-void csv_line_ends(const uint8_t* buf, int64_t n, int64_t* counts, void* ends, hipStream_t st);
+// facts (pass 2 only, or null): csv_count_blocks(n) x 4 int32, per block [separator bytes (sep),
+// CR ends, lone-LF ends, CR LF ends]
+void csv_line_ends(const uint8_t* buf, int64_t n, int64_t* counts, void* ends, hipStream_t st, int sep = -1,
+                   int32_t* facts = nullptr);
 // dcols: [2 * ncols] int64 — ncols device pointers to nlines values each, then ncols storage
 // kinds (0 f64, 1 int32, 2 int64, 3 bool/uint8, 4 string span: int64 (fs << 25) | (raw << 24) | len
 // with fs the field's first byte in buf (csv_field_span), 5 timestamp: int64 microseconds);
@@ -25,7 +28,8 @@ void csv_line_ends(const uint8_t* buf, int64_t n, int64_t* counts, void* ends, h
 // [slow flag, empty lines, null fields per column (ncols), class masks per column (ncols; bit 8:
 // a field whose value or class needs the host -- harmless when the column is a string),
 // lines with a field outside the numeric fast path, lines with a field that is not even a quoted
-// fast-path number ("12.5")]
+// fast-path number ("12.5"), the longest line [4 + 2 ncols] and, when the caller made room and set
+// it high, the shortest [6 + 2 ncols] (terminator to terminator)]
 // o: dialect (csv_parse_dev.h).  o.strict: the kinds are the user schema's types and a field that
 // does not convert makes its record malformed (all fields null)
 void csv_parse(const uint8_t* buf, int64_t n, const void* ends, int64_t nlines, int ncols, const dq4ml_csv::CsvOpts& o,

@@ -41,12 +41,20 @@ constexpr int kChunk = 256 * kBytesPerThread;  // bytes per block
 using dq4ml_csv::byte_eq4;
 
 // terminator bitmask of the thread's 64-byte window; window byte k <-> buffer index base + k.
-// Terminators: \r, and \n not preceded by \r (CR LF is one terminator, at the CR).
-__device__ __forceinline__ uint64_t term_mask(const uint8_t* __restrict__ b, int64_t n, int64_t base) {
+// Terminators: \r, and \n not preceded by \r (CR LF is one terminator, at the CR).  With facts:
+// the window's separator count and its terminator kinds (CR, lone LF, CR followed by LF -- a
+// CR LF pair across two windows counts in the second) for the cutter's scan facts.
+struct WinFacts {
+  int sep, cr, lf, crlf;
+};
+
+template <bool FACTS = false>
+__device__ __forceinline__ uint64_t term_mask(const uint8_t* __restrict__ b, int64_t n, int64_t base,
+                                              uint32_t sep4 = 0, WinFacts* wf = nullptr) {
   const uint8_t* ab = b - (reinterpret_cast<uintptr_t>(b) & 15);  // granule-aligned view
   const int64_t off = b - ab;                                    // 0..15
   const int64_t g0 = base + off;                                  // aligned position of window byte 0
-  uint64_t cr = 0, lf = 0;
+  uint64_t cr = 0, lf = 0, sp = 0;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int64_t ga = g0 + 16 * j;  // aligned, multiple of 16
@@ -56,6 +64,7 @@ __device__ __forceinline__ uint64_t term_mask(const uint8_t* __restrict__ b, int
     for (int w = 0; w < 4; ++w) {
       cr |= (uint64_t)byte_eq4(v[w], 0x0D0D0D0Du) << (16 * j + 4 * w);
       lf |= (uint64_t)byte_eq4(v[w], 0x0A0A0A0Au) << (16 * j + 4 * w);
+      if (FACTS) sp |= (uint64_t)byte_eq4(v[w], sep4) << (16 * j + 4 * w);
     }
   }
   // bytes outside [0, n) of the edge windows
@@ -65,9 +74,17 @@ __device__ __forceinline__ uint64_t term_mask(const uint8_t* __restrict__ b, int
     const uint64_t keep_hi = hi <= 0 ? 0ull : (hi >= 64 ? ~0ull : ((1ull << hi) - 1));
     cr &= keep_lo & keep_hi;
     lf &= keep_lo & keep_hi;
+    if (FACTS) sp &= keep_lo & keep_hi;
   }
   const uint64_t prev_cr = (base >= 1 && base - 1 < n && b[base - 1] == '\r') ? 1ull : 0ull;
-  return cr | (lf & ~((cr << 1) | prev_cr));
+  const uint64_t lone_lf = lf & ~((cr << 1) | prev_cr);
+  if (FACTS) {
+    wf->sep = __popcll(sp);
+    wf->cr = __popcll(cr);
+    wf->lf = __popcll(lone_lf);
+    wf->crlf = __popcll(cr & (lf >> 1)) + (int)(prev_cr & lf & 1ull);
+  }
+  return cr | lone_lf;
 }
 
 __global__ __launch_bounds__(256) void csv_count_kernel(const uint8_t* __restrict__ b, int64_t n,
@@ -128,15 +145,33 @@ constexpr int kEndsStage = 8192;  // line ends per block staged in LDS (block-re
 // Each thread finds its window's line ends; a block with at most kEndsStage of them collects them
 // in LDS (in order) and writes them out as one coalesced run — per-thread direct stores put 64
 // lanes on 64 different cache lines per instruction.
+//
+// facts (or null): per block [separators, CR ends, lone-LF ends, CR LF ends] (int32 x 4), the
+// scan facts the host used to derive with whole-chunk torch passes (ops/csvscan.py _scan_chunk)
 template <typename IT>
 __global__ __launch_bounds__(256) void csv_ends_kernel(const uint8_t* __restrict__ b, int64_t n,
-                                                      const int64_t* __restrict__ offsets, IT* __restrict__ ends) {
+                                                      const int64_t* __restrict__ offsets, IT* __restrict__ ends,
+                                                      uint32_t sep4, int32_t* __restrict__ facts) {
   __shared__ int wtot[4];
+  __shared__ int wfact[4][4];
   __shared__ int sends[kEndsStage];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int64_t bbase = (int64_t)blockIdx.x * kChunk - (int64_t)(reinterpret_cast<uintptr_t>(b) & 15);
   const int64_t base = bbase + (int64_t)threadIdx.x * kBytesPerThread;
-  uint64_t m = term_mask(b, n, base);
+  uint64_t m;
+  if (facts != nullptr) {
+    WinFacts wf;
+    m = term_mask<true>(b, n, base, sep4, &wf);
+    int f[4] = {wf.sep, wf.cr, wf.lf, wf.crlf};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) f[k] += __shfl_xor(f[k], o, 64);
+      if (lane == 0) wfact[wave][k] = f[k];
+    }
+  } else {
+    m = term_mask(b, n, base);
+  }
   const int c = __popcll(m);
   // exclusive prefix of the per-thread counts: wave scan (shfl_up) + wave totals in LDS
   int inc = c;
@@ -147,6 +182,9 @@ __global__ __launch_bounds__(256) void csv_ends_kernel(const uint8_t* __restrict
   }
   if (lane == 63) wtot[wave] = inc;
   __syncthreads();
+  if (facts != nullptr && threadIdx.x < 4)
+    facts[(int64_t)blockIdx.x * 4 + threadIdx.x] =
+        wfact[0][threadIdx.x] + wfact[1][threadIdx.x] + wfact[2][threadIdx.x] + wfact[3][threadIdx.x];
   int before = inc - c;
   for (int w = 0; w < wave; ++w) before += wtot[w];
   const int64_t o0 = offsets[blockIdx.x];
@@ -191,18 +229,34 @@ __device__ __forceinline__ bool parse_line(PB B, int64_t bias, int64_t n, const 
                                            int64_t li, bool active, int64_t nlines, int ncols, const CsvOpts& o,
                                            const int64_t* __restrict__ dcols, uint8_t* __restrict__ valid,
                                            uint8_t* __restrict__ keep, uint32_t* smask, int* snull, int* sempty,
-                                           int* smiss, int* shard) {
+                                           int* smiss, int* shard, unsigned long long* smaxl,
+                                           unsigned long long* sminl) {
   const bool lane0 = (threadIdx.x & 63) == 0;
   int64_t start = 0, end = 0;
   bool line = false;
+  int64_t span = 0;  // terminator to terminator (the first line: its end + 1), for the line-length facts
   if (active) {
+    int64_t pe = -1;
     if (li > 0) {
-      const int64_t pe = ends[li - 1];
+      pe = ends[li - 1];
       start = pe + 1 + ((B[pe - bias] == '\r' && pe + 1 < n && B[pe + 1 - bias] == '\n') ? 1 : 0);
     }
     end = ends[li];  // exclusive (position of the terminator or n)
+    span = end - pe;
     line = end > start && !(o.comment && B[start - bias] == o.comment);
     keep[li] = line;
+  }
+  {
+    int64_t mx = active ? span : 0, mn = active ? span : ((int64_t)1 << 62);
+#pragma unroll
+    for (int oo = 1; oo < 64; oo <<= 1) {
+      mx = max(mx, (int64_t)__shfl_xor((long long)mx, oo, 64));
+      mn = min(mn, (int64_t)__shfl_xor((long long)mn, oo, 64));
+    }
+    if (lane0) {
+      atomicMax(smaxl, (unsigned long long)mx);
+      atomicMin(sminl, (unsigned long long)mn);
+    }
   }
   const uint64_t empty = __ballot(active && !line);
   if (lane0 && empty) atomicAdd(sempty, (int)__popcll(empty));
@@ -317,6 +371,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   __shared__ uint32_t smask[kMaxCols];
   __shared__ int snull[kMaxCols];
   __shared__ int sempty, sflag, smiss, shard;
+  __shared__ unsigned long long smaxl, sminl;
   __shared__ __attribute__((aligned(16))) uint8_t stage[LDS];
   for (int c = threadIdx.x; c < ncols; c += blockDim.x) {
     smask[c] = 0;
@@ -327,6 +382,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     sempty = 0;
     smiss = 0;
     shard = 0;
+    smaxl = 0;
+    sminl = 1ull << 62;
   }
   const uint8_t* ab = b - (reinterpret_cast<uintptr_t>(b) & 15);
   const int64_t off = b - ab;
@@ -350,10 +407,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
       }
       __syncthreads();
       slow |= parse_line(stage, glo - off, n, ends, li, li < l1, nlines, ncols, o, dcols, valid, keep, smask,
-                         snull, &sempty, &smiss, &shard);
+                         snull, &sempty, &smiss, &shard, &smaxl, &sminl);
     } else {
       slow |= parse_line(b, 0, n, ends, li, li < l1, nlines, ncols, o, dcols, valid, keep, smask, snull, &sempty,
-                         &smiss, &shard);
+                         &smiss, &shard, &smaxl, &sminl);
     }
   }
   if (slow) sflag = 1;
@@ -371,6 +428,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     if (sflag) atomicOr(&stats[0], 1ull);
     if (smiss) atomicAdd(&stats[2 + 2 * ncols], (unsigned long long)smiss);
     if (shard) atomicAdd(&stats[3 + 2 * ncols], (unsigned long long)shard);
+    atomicMax(&stats[4 + 2 * ncols], smaxl);  // longest line (terminator to terminator)
+    atomicMin(&stats[6 + 2 * ncols], sminl);  // shortest (the caller initializes it high)
   }
 }
 
@@ -412,17 +471,20 @@ int64_t csv_count_blocks(int64_t n) { return (n + kChunk - 1) / kChunk + 1; }
 
 bool csv_ends_i32(int64_t n) { return n < ((int64_t)1 << 31) - 1; }
 
-void csv_line_ends(const uint8_t* buf, int64_t n, int64_t* counts, void* ends, hipStream_t st) {
+void csv_line_ends(const uint8_t* buf, int64_t n, int64_t* counts, void* ends, hipStream_t st, int sep,
+                   int32_t* facts) {
   const int64_t nb = csv_count_blocks(n);
+  const uint32_t sep4 = (uint32_t)(sep & 0xFF) * 0x01010101u;
+  if (facts != nullptr && (sep < 0 || sep > 255)) throw std::invalid_argument("csv_line_ends: facts need a separator byte");
   if (ends == nullptr) {  // pass 1: per-block counts -> exclusive offsets, total at counts[nb]
     hipLaunchKernelGGL(csv_count_kernel, dim3(nb), dim3(256), 0, st, buf, n, counts);
     hipLaunchKernelGGL(csv_scan_counts_kernel, dim3(1), dim3(1024), 0, st, counts, nb);
   } else if (csv_ends_i32(n)) {  // pass 2 (ends sized from counts[nb]); int32 offsets below 2 GiB
     hipLaunchKernelGGL((csv_ends_kernel<int32_t>), dim3(nb), dim3(256), 0, st, buf, n, counts,
-                       static_cast<int32_t*>(ends));
+                       static_cast<int32_t*>(ends), sep4, facts);
   } else {
     hipLaunchKernelGGL((csv_ends_kernel<int64_t>), dim3(nb), dim3(256), 0, st, buf, n, counts,
-                       static_cast<int64_t*>(ends));
+                       static_cast<int64_t*>(ends), sep4, facts);
   }
   DQ_HIP_CHECK(hipGetLastError());
 }

@@ -108,7 +108,8 @@ struct StageFrags {
 // 2: (augmentation, augmentation).  Gang schedule (8 waves): a diagonal unit also carries the
 // augmentation products of its panel — it loads panel I plus the augmentation tile, and the two
 // waves whose 128 x 64 tiles lie entirely below the diagonal (wm = 1, wn < 2) compute (I, aug)
-// instead (MODE 5; panel I = 0 adds (aug, aug)); the other six are MODE 4.  Separate instantiations keep the accumulators in AGPRs with no
+// instead (MODE 5; panel I = 0 adds (aug, aug)); the other six are MODE 4 (waves 0-1, which also load
+// the augmentation tile) and MODE 6.  Separate instantiations keep the accumulators in AGPRs with no
 // control-flow merge inside the loop (a merge there costs a full AGPR<->VGPR copy per stage).
 //
 // Schedule per stage i (fragments of stage i already in registers `cur`):
@@ -123,7 +124,9 @@ __device__ __forceinline__ void keep_live(const V& v) {
 }
 
 // ABL: 0 = real kernel; diagnostic builds only (timing, wrong results): 1 = no MFMA (loads + LDS
-// reads), 2 = no glds
+// reads), 2 = no glds after the ring prologue (MFMAs + LDS reads on the first RING stages' data)
+// ABL: 0 = real kernel; diagnostic builds only: 1 = no MFMA (loads + LDS reads), 2 = no glds after
+// the ring prologue (timing only, wrong results); 16 = tid laundering; 64 = staggered start
 template <int EB, int MODE, int RING, int ABL = 0>
 __device__ __forceinline__ void syrk_block(const WideArgs& a, unsigned char* smem, int I, int J, int pair, int split) {
   typedef WideTraits<EB> Tr;
@@ -135,53 +138,78 @@ __device__ __forceinline__ void syrk_block(const WideArgs& a, unsigned char* sme
   // loads per thread per stage: an augmentation side needs only piece 0 (tile 0 = [1, y_hi, y_lo]
   // for threads < 128, the zero page into tile 1 for the rest — waves whose tiles are all zero
   // read tile 1); a diagonal pair (MODE 3) loads its one panel once
+  //
+  // gang diagonal unit (MODE 4 / 5 / 6): the B region holds only the augmentation tile, read by
+  // the MODE-5 waves; its 2 KiB are loaded by waves 0-1 alone (MODE 4).  The other waves (MODE
+  // 5 / 6) issue no B piece -- theirs would be the zero page: 14 KiB of L2 -> LDS traffic per
+  // stage for nothing.  vmcnt is per wave, so each mode's counted waits use its own loads.
   constexpr int LA = MODE == 2 ? 1 : kLoadsPerPanel;
-  constexpr int LB = MODE == 3 ? 0 : (MODE >= 1 ? 1 : kLoadsPerPanel);
-  constexpr bool kDiagPanel = MODE == 3 || MODE == 4;  // B operand = the A panel
+  constexpr int LB = (MODE == 3 || MODE == 5 || MODE == 6) ? 0 : (MODE >= 1 ? 1 : kLoadsPerPanel);
+  constexpr bool kDiagPanel = MODE == 3 || MODE == 4 || MODE == 6;  // B operand = the A panel
   constexpr bool kFullWave = MODE == 0 || kDiagPanel;
   constexpr int kLoadsPerStage = LA + LB;
   typedef StageFrags<F> SF;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // The wave index is a scalar (readfirstlane): every LDS-DMA destination (M0) is SALU
+  // arithmetic.  (ABL & 16, diagnostic: the thread id laundered through an asm barrier so no
+  // tid-derived value is hoisted out of the gang's unit loop.  The K loop compiles to the same
+  // instructions, yet on the box the laundered build ran 8-10 % slower with the L2 hit rate at
+  // 25 % instead of 46 %: profiles/r5_wide_limiter.md.)
+  int tid = threadIdx.x;
+  if constexpr ((ABL & 16) != 0) asm volatile("" : "+v"(tid));
+  const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 2, wn = wave & 3;
   const int64_t nst = a.nsup * Tr::kStagesPerSup;
   const int64_t st0 = nst * split / a.splitk, st1 = nst * (split + 1) / a.splitk;
   const int64_t cnt = st1 - st0;
 
-  // per-thread global sources of its kLoadsPerPanel 16-byte pieces of each panel-stage image; a
-  // stage adds the wave-uniform Tr::sdelta (augmentation: only piece 0 of the first 128 threads is
-  // real data, the rest stream the zero page and never advance)
-  const unsigned char* srcA[kLoadsPerPanel];
-  const unsigned char* srcB[kLoadsPerPanel];
+  // Each thread moves kLoadsPerPanel 16-byte pieces of every panel-stage image: piece r is byte o
+  // = (r * 512 + tid) * 16 of the 16 KiB image, at a 32-bit panel-relative offset that never
+  // changes; the stage adds a wave-uniform base (X + panel + Tr::sdelta, or the zero page for the
+  // padding stages past cnt, or the augmentation tile), so a load is one uniform base + one
+  // lane offset (no 64-bit per-lane address math and no per-lane select in the K loop).
+  uint32_t offT[kLoadsPerPanel];  // panel-relative offset of piece r in the tiled image
+  uint32_t offO[kLoadsPerPanel];  // o itself (augmentation tile / zero page, 2 KiB stride images)
 #pragma unroll
   for (int r = 0; r < kLoadsPerPanel; ++r) {
-    const int o = (r * kWBlock + tid) * 16;
-    const int64_t tile_off = (int64_t)(o >> 11) * Tr::kTileStride + (o & (kChunk - 1));
-    srcA[r] = MODE == 2 ? (o < kChunk ? a.Xaug + o : a.zeros + o)
-                        : a.X + (int64_t)I * kTilesPerPanel * Tr::kTileStride + tile_off;
-    srcB[r] = MODE >= 1 && MODE != 3 ? (o < kChunk ? a.Xaug + o : a.zeros + o)
-                                        : a.X + (int64_t)J * kTilesPerPanel * Tr::kTileStride + tile_off;
+    const uint32_t o = (uint32_t)(r * kWBlock + tid) * 16u;
+    offO[r] = o;
+    offT[r] = (o >> 11) * (uint32_t)Tr::kTileStride + (o & (kChunk - 1));
   }
+  // (I, J come from a table every lane loads: readfirstlane keeps the panel bases scalar)
+  const int Iu = __builtin_amdgcn_readfirstlane(I), Ju = __builtin_amdgcn_readfirstlane(J);
+  const unsigned char* pA = a.X + (int64_t)Iu * kTilesPerPanel * Tr::kTileStride;
+  const unsigned char* pB = a.X + (int64_t)Ju * kTilesPerPanel * Tr::kTileStride;
+  const int cnt32 = (int)cnt;  // (a 32-bit scalar compare per stage: s_cmp, not a 64-bit v_cmp)
   // stages at or beyond cnt stream the zero page: the K loop then runs an even number of stages
   // with no branch at all (a branch there lets the compiler sink MFMAs past the barrier) and
   // every wait is the same counted vmcnt — the extra stage multiplies zeros
   auto issue = [&](int64_t st, int buf) {
-    if (ABL == 2) return;
+    if ((ABL & 3) == 2 && st >= RING) return;  // (the ablation still fills the ring once: real operands)
     unsigned char* base = smem + buf * kStageBytes;
-    const bool live = st < cnt;
+    const bool live = (int)st < cnt32;
     const int64_t dx = Tr::sdelta(st0 + st, a.NT), dg = Tr::sdelta(st0 + st, 1);
+    const unsigned char* zx = a.zeros;
 #pragma unroll
     for (int r = 0; r < LA; ++r) {
-      const int o = (r * kWBlock + tid) * 16;
-      const bool real = o < kChunk;
-      const unsigned char* s = MODE == 2 ? (real ? srcA[r] + dg : srcA[r]) : srcA[r] + dx;
-      glds16(live ? s : a.zeros + o, base + (r * kWBlock + wave * 64) * 16);
+      unsigned char* dst = base + (r * kWBlock + wave * 64) * 16;
+      if constexpr (MODE == 2) {  // (aug, aug): piece 0 of the first 128 threads is real
+        const bool real = offO[r] < (uint32_t)kChunk;
+        glds16((live && real ? a.Xaug + dg : zx) + offO[r], dst);
+      } else {
+        glds16((live ? pA + dx : zx) + offT[r], dst);
+      }
     }
 #pragma unroll
     for (int r = 0; r < LB; ++r) {
-      const int o = (r * kWBlock + tid) * 16;
-      const bool real = o < kChunk;
-      const unsigned char* s = MODE >= 1 ? (real ? srcB[r] + dg : srcB[r]) : srcB[r] + dx;
-      glds16(live ? s : a.zeros + o, base + kPanelStage + (r * kWBlock + wave * 64) * 16);
+      unsigned char* dst = base + kPanelStage + (r * kWBlock + wave * 64) * 16;
+      if constexpr (MODE == 0) {
+        glds16((live ? pB + dx : zx) + offT[r], dst);
+      } else if constexpr (MODE == 4) {  // waves 0-1 of a gang diagonal unit: all real aug rows
+        glds16((live ? a.Xaug + dg : zx) + offO[r], dst);
+      } else {  // MODE 1: the first 128 threads real, the rest the zero page
+        const bool real = offO[r] < (uint32_t)kChunk;
+        glds16((live && real ? a.Xaug + dg : zx) + offO[r], dst);
+      }
     }
   };
   auto read = [&](SF& f, int buf) {
@@ -208,7 +236,7 @@ __device__ __forceinline__ void syrk_block(const WideArgs& a, unsigned char* sme
   // (augmentation modes: waves whose B (or A) tiles come from the zero page multiply zeros —
   // cheaper than a data-dependent branch around the accumulators)
   auto mfmas = [&](const SF& f, int x0) {
-    if (ABL == 1) {
+    if ((ABL & 3) == 1) {
 #pragma unroll
       for (int kk = 0; kk < Tr::kSteps; ++kk) {
 #pragma unroll
@@ -366,21 +394,115 @@ __global__ __launch_bounds__(64 * kWaves, 1) void gram_wide_queue_kernel(WideArg
 // other blocks of the round.  The queue schedule's blocks drift apart (unequal unit costs,
 // dynamic dequeue), so there each block re-fetched its panels (L2 hit 61 %, ~6.6x the unique
 // bytes from the fabric).  S is chosen on the host so that npu * S is a multiple of G.
-template <int EB, int RING>
-__global__ __launch_bounds__(64 * kWaves, 1) void gram_wide_gang_kernel(WideArgs a, int S) {
+// unit u of a gang group -> (row range s, pair index pos): the S * P(P-1)/2 off-diagonal units
+// first (range-major, Z-order pairs), then the S * P diagonal ones.  A diagonal unit streams one
+// panel instead of two: the K loop is data-bound, so it ran in 3.1 ms against 4.6 ms (per-unit
+// stamps, profiles/r5_wide_limiter.md); mixed into a round it let its block run ahead into the
+// next round, and the blocks of an XCD drifted ~0.5 ms apart -- out of reach of each other's
+// panel-stages in L2.  Segregated, every round holds units of one cost.  The pair table lists the
+// off-diagonal pairs, then the diagonal ones.
+__device__ __forceinline__ void gang_unit(int u, int S, int P, int& s, int& pos) {
+  const int noff = P * (P - 1) / 2;
+  if (u < S * noff) {
+    s = u / noff;
+    pos = u - s * noff;
+  } else {
+    const int v = u - S * noff;
+    s = v / P;
+    pos = noff + (v - s * P);
+  }
+}
+
+// round barrier of a gang group (bar: 8 groups x 32 ints, zeroed per launch, or null): the block
+// arrives after its unit k - 1 and waits until all G blocks of its group have -- the round's
+// blocks then start their units together and share each panel-stage through the XCD's L2.  For
+// speed only: the wait is bounded, so any placement or residency still completes.
+__device__ __forceinline__ void gang_round_sync(int* bar, int g, int k, int G) {
+  if (bar == nullptr || k == 0) return;
+  if (threadIdx.x == 0) {
+    int* c = bar + g * 32;
+    __hip_atomic_fetch_add(c, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int target = k * G;
+    for (int it = 0; it < (1 << 20) && __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target; ++it)
+      __builtin_amdgcn_s_sleep(4);
+  }
+  __syncthreads();
+}
+
+template <int EB, int RING, int ABL = 0>
+__global__ __launch_bounds__(64 * kWaves, 1) void gram_wide_gang_kernel(WideArgs a, int S, int* __restrict__ bar) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int g = blockIdx.x & 7, l = blockIdx.x >> 3, G = gridDim.x >> 3;
   const int P = a.npanels, npu = P * (P + 1) / 2, units = npu * S;
   const int wave = threadIdx.x >> 6;
   // the waves whose tiles lie entirely below a diagonal unit's diagonal
   const bool aug_wave = (wave >> 2) == 1 && (wave & 3) < 2;
-  for (int u = l; u < units; u += G) {
-    const int s = u / npu, pos = u - s * npu;
+  if constexpr ((ABL & 64) != 0) {  // (diagnostic) stagger: block l of a group starts ~2 (l & 3) stages late
+    for (int k = 0; k < (l & 3); ++k) __builtin_amdgcn_s_sleep(40);  // 64 x 40 clocks ~ 2 stages
+  }
+  int k = 0;
+  for (int u = l; u < units; u += G, ++k) {
+    int s, pos;
+    gang_unit(u, S, P, s, pos);
     const int split = g * S + s;
+    const int I = a.pairs[2 * pos], J = a.pairs[2 * pos + 1];
+    gang_round_sync(bar, g, k, G);
+    if (a.stamps != nullptr && threadIdx.x == 0 && k < 64)
+      a.stamps[((int64_t)blockIdx.x * 64 + k) * 2] = (int64_t)__builtin_amdgcn_s_memrealtime();
+    if (I != J) syrk_block<EB, 0, RING, ABL>(a, smem, I, J, 0, split);
+    else if (aug_wave) syrk_block<EB, 5, RING, ABL>(a, smem, I, J, 0, split);
+    else if (wave < 2) syrk_block<EB, 4, RING, ABL>(a, smem, I, J, 0, split);  // + the aug tile's loads
+    else syrk_block<EB, 6, RING, ABL>(a, smem, I, J, 0, split);
+    __syncthreads();  // every wave is done reading the ring before the next unit's first glds
+    if (a.stamps != nullptr && threadIdx.x == 0 && k < 64)
+      a.stamps[((int64_t)blockIdx.x * 64 + k) * 2 + 1] = (int64_t)__builtin_amdgcn_s_memrealtime();
+  }
+}
+
+// XCD-keyed gang schedule: the same equal-cost units as gram_wide_gang_kernel, but the group is
+// the XCD the block actually runs on (HW_REG_XCC_ID), not blockIdx % 8: the static form assumes
+// round-robin dispatch, and where a box deals blocks otherwise the 32 blocks of a "group" spread
+// over every XCD, 8 row ranges share each L2 and its hit rate halves (measured 70 % -> 38 %,
+// profiles/r5_wide_limiter.md).  Each XCD dequeues its own units (range-major, Z-order pairs:
+// the blocks of an XCD stay on one row range, as the gang's do) from a head on its own 64-byte
+// line; a block whose XCD's queue is empty steals from the next XCD's, so any placement -- and
+// any number of blocks per XCD -- covers every unit exactly once.  Correctness never depends on
+// placement; only L2 locality does.
+template <int EB, int RING>
+__global__ __launch_bounds__(64 * kWaves, 1) void gram_wide_gangx_kernel(WideArgs a, int S, int* __restrict__ q,
+                                                                        int* __restrict__ xcc_dbg) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int P = a.npanels, npu = P * (P + 1) / 2, units = npu * S;
+  const int wave = threadIdx.x >> 6;
+  const bool aug_wave = (wave >> 2) == 1 && (wave & 3) < 2;
+  int xcc;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+  xcc &= 7;
+  if (xcc_dbg != nullptr && threadIdx.x == 0) xcc_dbg[blockIdx.x] = xcc;
+  int* slot = q + 8 * 16 + blockIdx.x * 16;  // this block's broadcast word (a line of its own)
+  int g = xcc;
+  for (;;) {
+    if (threadIdx.x == 0) {
+      int u = atomicAdd(&q[g * 16], 1), tries = 0;
+      while (u >= units && ++tries < 8) {
+        g = (g + 1) & 7;
+        u = atomicAdd(&q[g * 16], 1);
+      }
+      __hip_atomic_store(slot, tries < 8 ? (g << 24) | u : -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    const int v = __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();  // every wave has read the word before thread 0 rewrites it
+    if (v < 0) break;
+    const int gg = v >> 24, u = v & 0xffffff;
+    int s, pos;
+    gang_unit(u, S, P, s, pos);
+    const int split = gg * S + s;
     const int I = a.pairs[2 * pos], J = a.pairs[2 * pos + 1];
     if (I != J) syrk_block<EB, 0, RING>(a, smem, I, J, 0, split);
     else if (aug_wave) syrk_block<EB, 5, RING>(a, smem, I, J, 0, split);
-    else syrk_block<EB, 4, RING>(a, smem, I, J, 0, split);
+    else if (wave < 2) syrk_block<EB, 4, RING>(a, smem, I, J, 0, split);
+    else syrk_block<EB, 6, RING>(a, smem, I, J, 0, split);
     __syncthreads();  // every wave is done reading the ring before the next unit's first glds
   }
 }
@@ -572,6 +694,10 @@ __global__ __launch_bounds__(256) void wide_mask_rows_kernel(const u32x4* __rest
 
 }  // namespace
 
+static int64_t* g_stamps = nullptr;
+void gram_wide_set_stamps(int64_t* stamps) { g_stamps = stamps; }
+int64_t* wide_stamps() { return g_stamps; }
+
 void wide_mask_rows(int eb, const void* in, void* out, int d, int64_t n, const uint8_t* sel, hipStream_t st) {
   const int NT = ((d + 255) / 256) * 8;
   const int64_t units = wide_tiled_bytes(eb, d, n) / 16;
@@ -670,24 +796,57 @@ void gram_wide_queue(int eb, WideArgs a, const int* pairs_dev, const float* scal
   if (fold) launch_fold(a, scales, out, nullptr, 0, a.npanels + 1, st);
 }
 
-template <int EB>
-static void launch_wide_gang(const WideArgs& a, int grid, int S, hipStream_t st) {
+template <int EB, int ABL = 0>
+static void launch_wide_gang(const WideArgs& a, int grid, int S, hipStream_t st, int* bar = nullptr) {
   const size_t lds = (size_t)5 * kStageBytes;
-  DQ_HIP_CHECK(hipFuncSetAttribute((const void*)gram_wide_gang_kernel<EB, 5>,
+  DQ_HIP_CHECK(hipFuncSetAttribute((const void*)gram_wide_gang_kernel<EB, 5, ABL>,
                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  hipLaunchKernelGGL((gram_wide_gang_kernel<EB, 5>), dim3(grid), dim3(64 * kWaves), lds, st, a, S);
+  if (bar != nullptr) DQ_HIP_CHECK(hipMemsetAsync(bar, 0, 8 * 32 * sizeof(int), st));
+  hipLaunchKernelGGL((gram_wide_gang_kernel<EB, 5, ABL>), dim3(grid), dim3(64 * kWaves), lds, st, a, S, bar);
   DQ_HIP_CHECK(hipGetLastError());
 }
 
 void gram_wide_gang(int eb, WideArgs a, const int* pairs_dev, const float* scales, double* out, int S, int grid,
-                    hipStream_t st, bool fold, int waves) {
+                    hipStream_t st, bool fold, int waves, int* bar) {
   a.pairs = pairs_dev;
   if (S < 1 || a.splitk != 8 * S) throw std::invalid_argument("gram_wide_gang: splitk must be 8 * S");
   if (grid < 8 || grid % 8) throw std::invalid_argument("gram_wide_gang: grid must be a positive multiple of 8");
   if ((int64_t)a.splitk > a.nsup) throw std::invalid_argument("gram_wide_gang: more row ranges than supersteps");
-  if (waves != kWaves) throw std::invalid_argument("gram_wide_gang: waves must be 8");
-  if (eb == 16) launch_wide_gang<16>(a, grid, S, st);
-  else launch_wide_gang<8>(a, grid, S, st);
+  // diagnostic ablations (timing only, wrong results): waves 81 = no MFMA, 82 = no glds in the loop
+  if (waves != kWaves && waves != 81 && waves != 82 && !((waves == 91 || waves == 94 || waves == 95) && eb == 8))
+    throw std::invalid_argument("gram_wide_gang: waves must be 8");
+  if (waves == 81) eb == 16 ? launch_wide_gang<16, 1>(a, grid, S, st) : launch_wide_gang<8, 1>(a, grid, S, st);
+  else if (waves == 82) eb == 16 ? launch_wide_gang<16, 2>(a, grid, S, st) : launch_wide_gang<8, 2>(a, grid, S, st);
+  // (diagnostic code-shape variants, fp8 only: 91 tid laundering, 94 staggered start, 95 both)
+  else if (waves == 91 && eb == 8) launch_wide_gang<8, 16>(a, grid, S, st);
+  else if (waves == 94 && eb == 8) launch_wide_gang<8, 64>(a, grid, S, st);
+  else if (waves == 95 && eb == 8) launch_wide_gang<8, 80>(a, grid, S, st);
+  else if (eb == 16) launch_wide_gang<16>(a, grid, S, st, bar);
+  else launch_wide_gang<8>(a, grid, S, st, bar);
+  if (fold) launch_fold(a, scales, out, nullptr, 0, a.npanels + 1, st);
+}
+
+template <int EB>
+static void launch_wide_gangx(const WideArgs& a, int grid, int S, int* q, int* xcc_dbg, hipStream_t st) {
+  const size_t lds = (size_t)5 * kStageBytes;
+  DQ_HIP_CHECK(hipFuncSetAttribute((const void*)gram_wide_gangx_kernel<EB, 5>,
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  hipLaunchKernelGGL((gram_wide_gangx_kernel<EB, 5>), dim3(grid), dim3(64 * kWaves), lds, st, a, S, q, xcc_dbg);
+  DQ_HIP_CHECK(hipGetLastError());
+}
+
+int gram_wide_gangx_ints(int grid) { return 8 * 16 + grid * 16; }
+
+void gram_wide_gangx(int eb, WideArgs a, const int* pairs_dev, const float* scales, double* out, int S, int grid,
+                     int* q, int* xcc_dbg, hipStream_t st, bool fold) {
+  a.pairs = pairs_dev;
+  if (S < 1 || a.splitk != 8 * S) throw std::invalid_argument("gram_wide_gangx: splitk must be 8 * S");
+  if (grid < 1) throw std::invalid_argument("gram_wide_gangx: empty grid");
+  if ((int64_t)a.splitk > a.nsup) throw std::invalid_argument("gram_wide_gangx: more row ranges than supersteps");
+  if ((int64_t)a.npanels * (a.npanels + 1) / 2 * S >= (1 << 24)) throw std::invalid_argument("gram_wide_gangx: too many units");
+  DQ_HIP_CHECK(hipMemsetAsync(q, 0, 8 * 16 * sizeof(int), st));  // the 8 XCD heads
+  if (eb == 16) launch_wide_gangx<16>(a, grid, S, q, xcc_dbg, st);
+  else launch_wide_gangx<8>(a, grid, S, q, xcc_dbg, st);
   if (fold) launch_fold(a, scales, out, nullptr, 0, a.npanels + 1, st);
 }
 

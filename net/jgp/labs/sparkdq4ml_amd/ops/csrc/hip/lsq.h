@@ -44,4 +44,17 @@ void lsq_qn(const LsqX& x, const double* y, const double* w, const double* scale
             const double* head, bool fit_icpt, bool std_f, double reg, double enet, int max_iter, double tol,
             int hist_cap, double* work, int blocks, double* out, hipStream_t st);
 
+// Data-parallel form of lsq_qn (X4, lsq_qn.hip): the same fit as separate launches around an
+// all-reduce.  phase 0 starts the fit (head = the ALL-REDUCED summarizer head), phase 1 enqueues
+// one evaluation's pass over this rank's rows and leaves [Σ v x_j (d), loss, Σ v] at
+// work + lsq_qn_dp_red_offset (the caller all-reduces those d + 2 doubles), phase 2 the control
+// step; the state's action (int, 3 = done) is the first word at work + lsq_qn_dp_ctl_offset.
+// Every kernel returns at once after the fit is done.  work: lsq_qn_dp_work doubles.
+int64_t lsq_qn_dp_work(int d, int blocks, int64_t n);
+int64_t lsq_qn_dp_red_offset(int d, int blocks, int64_t n);
+int64_t lsq_qn_dp_ctl_offset(int d, int blocks, int64_t n);
+void lsq_qn_dp(int phase, const LsqX& x, const double* y, const double* w, const double* scale, const double* shift,
+               const double* head, bool fit_icpt, bool std_f, double reg, double enet, int max_iter, double tol,
+               int hist_cap, double* work, int blocks, double* out, hipStream_t st);
+
 }  // namespace dq4ml

@@ -46,27 +46,6 @@ constexpr int kMem = 10;
 constexpr int kFv = 20;
 constexpr int kDParts = 4;  // per-block partials of an evaluation: x.(regw x), Σ|l1 x|, dir . g, g . g
 
-struct QnArgs {
-  const unsigned char* X;
-  int d, NT, ntl;
-  int64_t n, nunits;
-  const double* y;
-  const double* w;
-  const double* scale;  // fp8 per-feature scale (x = q * scale), or null
-  const double* shift;  // per-feature storage shift (x = x' + s), or null
-  const double* head;   // [count, W, W2, Σwy, Σwy², Σwx (d), Σwx² (d)]
-  int fit_icpt, std_f, owlqn;
-  double reg, enet, tol;
-  int max_iter, hist_cap;
-  // workspace (doubles): vectors of d, the history, the per-block slabs
-  float* cs;  // [NC] the trial's f32 effective coefficients
-  double *inv_sx, *sx, *mx, *regw, *l1, *x, *g, *ag, *dir, *cx, *cg, *cag, *S, *Y, *part, *lpart, *dpart, *scal;
-  double* out;  // [coef(d), intercept, status, reason, H, iters, evaluations, head(5), history(hist_cap)]
-  // L-BFGS (not OWLQN): per row, the margin of the accepted point (no offset) and X . dir of the
-  // current line search -- a trial's margins are mvec + alpha dvec, so only the first trial of a
-  // search reads X twice (it forms dvec); every other evaluation reads X once (the column pass)
-  double *mvec, *dvec;
-};
 
 __device__ __forceinline__ double block_sum(double v, double* red) {
   v = wave_sum_f64(v);
@@ -125,6 +104,8 @@ struct Ctl {
   double fv[kFv];
   int nfv, iter, H, head, hh, pass, search_failed, failed_once, overflow, why, nev;
   int first;  // L-BFGS: the next evaluation is the first of its line search (it forms dvec)
+  double pend;  // data-parallel form: the accepted step not yet folded into mvec (the next
+                // search's first pass adds pend * dvec: one grid pass fewer per iteration)
   double last_v, last_adj, last_gg;  // the last evaluation (the accepted step's values)
   // line search: backtracking (initfval, initd, shrink, it, force) / strong Wolfe (f0, d0, bracket
   // counter, lo / hi points, zoom counter), |g| of the state for the step checks
@@ -132,6 +113,33 @@ struct Ctl {
   int it, force, bi, zi;
   // two-loop scratch (block 0)
   double as_[kMem], rho[kMem];
+};
+
+struct QnArgs {
+  const unsigned char* X;
+  int d, NT, ntl;
+  int64_t n, nunits;
+  const double* y;
+  const double* w;
+  const double* scale;  // fp8 per-feature scale (x = q * scale), or null
+  const double* shift;  // per-feature storage shift (x = x' + s), or null
+  const double* head;   // [count, W, W2, Σwy, Σwy², Σwx (d), Σwx² (d)]
+  int fit_icpt, std_f, owlqn;
+  double reg, enet, tol;
+  int max_iter, hist_cap;
+  // workspace (doubles): vectors of d, the history, the per-block slabs
+  float* cs;  // [NC] the trial's f32 effective coefficients
+  double *inv_sx, *sx, *mx, *regw, *l1, *x, *g, *ag, *dir, *cx, *cg, *cag, *S, *Y, *part, *lpart, *dpart, *scal;
+  double* out;  // [coef(d), intercept, status, reason, H, iters, evaluations, head(5), history(hist_cap)]
+  // L-BFGS (not OWLQN): per row, the margin of the accepted point (no offset) and X . dir of the
+  // current line search -- a trial's margins are mvec + alpha dvec, so only the first trial of a
+  // search reads X twice (it forms dvec); every other evaluation reads X once (the column pass)
+  double *mvec, *dvec;
+  // data-parallel form (lsq_qn_dp_*): the optimizer state in HBM between launches, and the
+  // per-evaluation buffer all-reduced between the pass and the control kernel: [Σ v x_j (d),
+  // Σ ½ w diff², Σ v]
+  Ctl* ctl;
+  double* red;
 };
 
 __device__ void ctl_record(Ctl& C, const QnArgs& a, double* hist) {
@@ -390,59 +398,344 @@ __device__ void apply_dir(const QnArgs& a, Ctl& C, double* scal, double* red, bo
   __threadfence();
 }
 
+// ---- pieces shared by the one-launch kernel and the data-parallel kernels ------------------
+
+// standardization constants from the summarizer head (lbfgs_path._train_passes' expression order)
+struct Std {
+  double W, my, denom, ys, l1c, l2, icpt0, inv_ys, inv_w;
+  int status;  // 0 ok, 1 empty data, 2 constant label (the host path owns those)
+};
+
+__device__ __forceinline__ Std std_of(const QnArgs& a) {
+  const double* hd = a.head;
+  Std S;
+  S.W = hd[1];
+  const double W2 = hd[2], bsum = hd[3], bbsum = hd[4];
+  S.denom = S.W - W2 / S.W;
+  S.my = bsum / S.W;
+  const double var_y = S.denom > 0.0 ? fmax(bbsum - S.W * S.my * S.my, 0.0) / S.denom : 0.0;
+  S.ys = sqrt(var_y);
+  S.status = !(S.W > 0.0) ? 1 : (S.ys == 0.0 ? 2 : 0);
+  const double eff_reg = a.reg / S.ys;
+  S.l1c = a.enet * eff_reg;
+  S.l2 = (1.0 - a.enet) * eff_reg;
+  S.icpt0 = a.fit_icpt ? S.my / S.ys : 0.0;
+  S.inv_ys = 1.0 / S.ys;
+  S.inv_w = 1.0 / S.W;
+  return S;
+}
+
+// per-feature constants of features [j0, j1) (threads of one block stride the range)
+__device__ __forceinline__ void feature_consts(const QnArgs& a, const Std& S, int j0, int j1) {
+  const double* hd = a.head;
+  const int d = a.d;
+  const bool owlqn = a.owlqn != 0;
+  for (int j = j0 + (int)threadIdx.x; j < j1; j += kT) {
+    const double m = hd[5 + j] / S.W;
+    const double vx = S.denom > 0.0 ? fmax(hd[5 + d + j] - S.W * m * m, 0.0) / S.denom : 0.0;
+    const double sx = sqrt(vx);
+    const bool nz = sx != 0.0;
+    const double safe = nz ? sx : 1.0;
+    a.mx[j] = m;
+    a.sx[j] = safe;
+    a.inv_sx[j] = nz ? 1.0 / safe : 0.0;
+    a.regw[j] = S.l2 != 0.0 ? (a.std_f ? 1.0 : (nz ? 1.0 / (safe * safe) : 0.0)) : 0.0;
+    a.l1[j] = owlqn ? (a.std_f ? S.l1c : (nz ? S.l1c / safe : 0.0)) : 0.0;
+    a.x[j] = 0.0;
+    a.dir[j] = 0.0;
+    a.ag[j] = 0.0;
+  }
+}
+
+__device__ __forceinline__ void ctl_init(Ctl& C) {
+  C.act = kActEval;
+  C.mode = 0;
+  C.alpha = 0.0;
+  C.ls = kLsInit;
+  C.head = 0, C.hh = 0, C.H = 0, C.iter = 0, C.nfv = 1, C.pass = 0;
+  C.search_failed = 0, C.failed_once = 0, C.overflow = 0, C.why = -1, C.nev = 0, C.first = 0;
+  C.pend = 0.0;
+  for (int i = 0; i < kFv; ++i) C.fv[i] = 0.0;
+  C.fv[kFv - 1] = __builtin_inf();
+}
+
+// E1 (one block): the trial point x + alpha dir (mode 1, projected for OWLQN) or x0 = 0 (mode 0),
+// kept for the acceptance; the f32 effective coefficients (every pass block reads them through
+// its L2) over the nc coefficient slots; the margin offset -> scal[16]
+__device__ void build_trial(const QnArgs& a, const Std& S, int mode, double alpha, int nc, double* red) {
+  const int t = threadIdx.x, d = a.d;
+  const bool owlqn = a.owlqn != 0;
+  double pm = 0.0, ps = 0.0;
+#pragma unroll 2
+  for (int j = t; j < nc; j += kT) {
+    float c32 = 0.0f;
+    if (j < d) {
+      double nx = 0.0;
+      if (mode == 1) {
+        const double xj = a.x[j];
+        nx = xj + a.dir[j] * alpha;
+        if (owlqn) {
+          const double orth = xj != 0.0 ? sgn(xj) : sgn(-a.ag[j]);
+          if (sgn(nx) != orth) nx = 0.0;
+        }
+      }
+      a.cx[j] = nx;
+      const double cf = nx * a.inv_sx[j];
+      pm += cf * a.mx[j];
+      if (a.shift) ps += a.shift[j] * cf;
+      // L-BFGS: the margin loop forms X . dir (a trial is mvec + alpha dvec); OWLQN's projected
+      // trial is not affine in alpha: its margins come from the trial's coefficients
+      const double cm = owlqn ? cf : a.dir[j] * a.inv_sx[j];
+      c32 = (float)(a.scale ? cm * a.scale[j] : cm);
+    }
+    a.cs[j] = c32;
+  }
+  const double cfmx = block_sum(pm, red);
+  double off = a.fit_icpt ? S.icpt0 - cfmx : S.icpt0;
+  if (a.shift) off = off + block_sum(ps, red);
+  if (t == 0) a.scal[16] = off;
+  __threadfence();
+}
+
+// E2: the fused pass of block b of B over its fragment units (margins, then the column sums of
+// the same tiles) -> the block's column slab part[b] and (loss, Σv) in lpart[b].  L-BFGS: margins
+// only on the first trial of a line search (X . dir -> dvec; with pend != 0 the accepted step is
+// folded into mvec first); the other trials read X once.  colacc must be zeroed by the caller.
+template <int L, int TPW>
+__device__ __forceinline__ void qn_pass(const QnArgs& a, const Std& S, int mode, double alpha, bool first, double pend,
+                                        double offset, double* colacc, double* mrow, float* vrow, double* red,
+                                        int b, int B) {
+  constexpr int E = L == 3 ? 16 : 8;
+  constexpr int64_t CH = L == 3 ? 2048 : 4096;
+  constexpr int UPS = L == 3 ? 2 : 4;
+  constexpr int NC = 8 * TPW * 32;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6, fl = lane & 31, hf = lane >> 5;
+  const bool owlqn = a.owlqn != 0;
+  const float* __restrict__ gcs = a.cs;
+  const bool skip = !owlqn && !first;
+  double loss = 0.0, vsum = 0.0;
+  for (int64_t u = b; u < a.nunits; u += B) {
+    const int64_t s = u / UPS;
+    const int sub = (int)(u % UPS);
+    const unsigned char* p = a.X + s * a.NT * CH + ((sub * 64 + lane) << 4);
+    double acc[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) acc[e] = 0.0;
+#pragma unroll 1
+    for (int i0 = 0; i0 < (skip ? 0 : TPW); i0 += 8) {
+      u32x4 q[8];
+      float c[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int tt = wave + 8 * (i0 + k);
+        q[k] = tt < a.ntl ? *gptr<u32x4>(p + (int64_t)tt * CH) : u32x4{0u, 0u, 0u, 0u};
+        c[k] = *gptr<float>(gcs + tt * 32 + fl);
+      }
+      float s8[E];
+#pragma unroll
+      for (int e = 0; e < E; ++e) s8[e] = 0.0f;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        float xv[E];
+        unpack<L>(q[k], xv);
+#pragma unroll
+        for (int e = 0; e < E; ++e) s8[e] = fmaf(xv[e], c[k], s8[e]);
+      }
+#pragma unroll
+      for (int e = 0; e < E; ++e) acc[e] += (double)s8[e];
+    }
+    // feature sum across the 32 lanes of each half, then the 8 waves' partials in LDS
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+#pragma unroll
+      for (int o = 1; o < 32; o <<= 1) acc[e] += __shfl_xor(acc[e], o, 64);
+    }
+    double m = acc[0];
+#pragma unroll
+    for (int e = 1; e < E; ++e) m = fl == e ? acc[e] : m;
+    if (fl < E) mrow[wave * 2 * E + hf * E + fl] = m;
+    __syncthreads();
+    if (t < 2 * E) {
+      double mm = 0.0;
+      const int64_t r = frag_row<L>(s, sub, t / E, t % E);
+      if (!skip)
+#pragma unroll
+        for (int i = 0; i < kW; ++i) mm += mrow[i * 2 * E + t];
+      if (!owlqn && r < a.n) {  // mm: this unit's X . dir (first trial) -> the trial's margin
+        double mv = a.mvec[r];
+        if (first && pend != 0.0) {  // (data-parallel form) the accepted step's margins, folded now
+          mv = mv + pend * a.dvec[r];
+          a.mvec[r] = mv;
+        }
+        const double md = skip ? a.dvec[r] : mm;
+        if (first) a.dvec[r] = mm;
+        mm = mv + alpha * md;
+      }
+      double vv = 0.0;
+      if (r < a.n) {
+        const double wr = a.w[r];
+        if (wr != 0.0) {
+          const double diff = mm + offset - a.y[r] * S.inv_ys;
+          vv = wr * diff;
+          loss += 0.5 * vv * diff;
+          vsum += vv;
+        }
+      }
+      vrow[t] = (float)vv;
+    }
+    __syncthreads();
+    float vr[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) vr[e] = vrow[hf * E + e];
+    // column sums of the same tiles, most recently read first; the two lane halves (the
+    // feature's other rows) combine, then one f64 LDS accumulator per feature (this wave's
+    // tiles only: no other wave touches them)
+#pragma unroll 1
+    for (int i0 = TPW - 8; i0 >= 0; i0 -= 8) {
+      u32x4 q[8];
+#pragma unroll
+      for (int k = 7; k >= 0; --k) {
+        const int tt = wave + 8 * (i0 + k);
+        q[k] = tt < a.ntl ? *gptr<u32x4>(p + (int64_t)tt * CH) : u32x4{0u, 0u, 0u, 0u};
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        float xv[E];
+        unpack<L>(q[k], xv);
+        float sa = 0.0f;
+#pragma unroll
+        for (int e = 0; e < E; ++e) sa += vr[e] * xv[e];
+        sa += __shfl_xor(sa, 32, 64);
+        if (hf == 0) colacc[(wave + 8 * (i0 + k)) * 32 + fl] += (double)sa;
+      }
+    }
+  }
+  __syncthreads();
+  // the block's column slab
+  double* slab = a.part + (int64_t)b * NC;
+  for (int j = t; j < NC; j += kT) slab[j] = colacc[j];
+  const double bl = block_sum(loss, red), bv = block_sum(vsum, red);
+  if (t == 0) a.lpart[2 * b] = bl, a.lpart[2 * b + 1] = bv;
+}
+
+// a column sum of the STORED values (q = x / scale, x' = x - shift) -> Σ v x_j
+__device__ __forceinline__ double unscale_col(const QnArgs& a, int j, double graw, double vs) {
+  if (a.scale) graw = graw * a.scale[j];
+  if (a.shift) graw = graw + a.shift[j] * vs;
+  return graw;
+}
+
+// E3 per feature: the column sum Σ v x_j -> gradient / adjusted gradient (cg, cag) and the partial
+// evaluation scalars x.(regw x), Σ|l1 x|, dir . ag, ag . ag
+__device__ __forceinline__ void grad_j(const QnArgs& a, const Std& S, int j, double graw, double& pr, double& pl,
+                                       double& pd, double& pg) {
+  const double nx = a.cx[j];
+  double gj = graw * a.inv_sx[j] * S.inv_w;
+  if (S.l2 != 0.0) {
+    const double rx = a.regw[j] * nx;
+    pr += nx * rx;
+    gj = gj + S.l2 * rx;
+  }
+  double agj = gj;
+  const double l = a.l1[j];
+  if (a.owlqn) {
+    pl += fabs(l * nx);
+    if (l != 0.0) {
+      if (nx == 0.0) {
+        const double dp = gj + l, dm = gj - l;
+        agj = dm > 0.0 ? dm : (dp < 0.0 ? dp : 0.0);
+      } else {
+        agj = gj + sgn(nx) * l;
+      }
+    }
+  }
+  a.cg[j] = gj;
+  a.cag[j] = agj;
+  pd += agj * a.dir[j];
+  pg += agj * agj;
+}
+
+__device__ __forceinline__ Eval eval_of(const QnArgs& a, const Std& S, double lsum, double sr, double sl, double sd,
+                                        double sg) {
+  Eval ev;
+  ev.v = lsum * S.inv_w;
+  if (S.l2 != 0.0) ev.v = ev.v + 0.5 * S.l2 * sr;
+  ev.adj = a.owlqn ? ev.v + sl : ev.v;
+  ev.dd = sd;
+  ev.gg = sg;
+  return ev;
+}
+
+// the last evaluated trial becomes the state (history pair pushed first): one block
+__device__ void accept_block(const QnArgs& a, const Ctl& C) {
+  const int t = threadIdx.x, d = a.d;
+  const bool push = C.ls != kLsInit;
+  int hd0 = C.head;
+  if (push) hd0 = (hd0 + kMem - 1) % kMem;
+  for (int j = t; j < d; j += kT) {
+    const double nx = a.cx[j], gj = a.cg[j];
+    if (push) {
+      a.S[(int64_t)hd0 * d + j] = nx - a.x[j];
+      a.Y[(int64_t)hd0 * d + j] = gj - a.g[j];
+    }
+    a.x[j] = nx;
+    a.g[j] = gj;
+    a.ag[j] = a.cag[j];
+  }
+  __threadfence();
+}
+
+// un-standardize into out: coef = x ys / sigma (0 for constant features), intercept = ȳ - coef . x̄
+__device__ void finalize_block(const QnArgs& a, const Ctl& C, const Std& S, double* red) {
+  const int t = threadIdx.x, d = a.d;
+  if (C.overflow) {
+    if (t == 0) a.out[d + 1] = 8.0;
+    return;
+  }
+  double pc = 0.0;
+  for (int j = t; j < d; j += kT) {
+    const double c = a.inv_sx[j] != 0.0 ? a.x[j] * S.ys / a.sx[j] : 0.0;
+    a.out[j] = c;
+    pc += c * a.mx[j];
+  }
+  const double cm = block_sum(pc, red);
+  if (t == 0) {
+    a.out[d] = a.fit_icpt ? S.my - cm : 0.0;
+    a.out[d + 1] = 0.0;
+    a.out[d + 2] = (double)C.why;
+    a.out[d + 3] = (double)C.H;
+    a.out[d + 4] = (double)C.iter;
+    a.out[d + 5] = (double)C.nev;  // cost evaluations (data passes)
+  }
+}
+
 template <int L, int TPW>
 __global__ __launch_bounds__(kT, 1) void lsq_qn_kernel(QnArgs a) {
   cg::grid_group grid = cg::this_grid();
   constexpr int E = L == 3 ? 16 : 8;
-  constexpr int64_t CH = L == 3 ? 2048 : 4096;
-  constexpr int UPS = L == 3 ? 2 : 4;
   constexpr int NC = 8 * TPW * 32;  // coefficient slots (tiles padded to whole wave strides)
   __shared__ double colacc[NC];  // the block's f64 column sums (<= 128 KiB)
   __shared__ double red[kW];
-  __shared__ double mrow[kW][2 * E];
+  __shared__ double mrow[kW * 2 * E];
   __shared__ float vrow[2 * E];
   __shared__ double fold[kW][64];
   __shared__ double bcast[4];
   __shared__ Ctl C;
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6, fl = lane & 31, hf = lane >> 5;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int B = gridDim.x, b = blockIdx.x;
   const int d = a.d;
 
   // ---- standardization constants (lbfgs_path._train_passes, in the same expression order) ----
-  const double* hd = a.head;
-  const double W = hd[1], W2 = hd[2], bsum = hd[3], bbsum = hd[4];
-  if (b == 0 && t < 5) a.out[d + 6 + t] = hd[t];
-  const double denom = W - W2 / W;
-  const double my = bsum / W;
-  const double var_y = denom > 0.0 ? fmax(bbsum - W * my * my, 0.0) / denom : 0.0;
-  const double raw_ys = sqrt(var_y);
-  if (!(W > 0.0) || raw_ys == 0.0) {  // empty data / constant label: the host path owns the semantics
-    if (b == 0 && t == 0) a.out[d + 1] = !(W > 0.0) ? 1.0 : 2.0;
+  const Std S = std_of(a);
+  if (b == 0 && t < 5) a.out[d + 6 + t] = a.head[t];
+  if (S.status != 0) {  // empty data / constant label: the host path owns the semantics
+    if (b == 0 && t == 0) a.out[d + 1] = (double)S.status;
     return;  // uniform across the grid: no barrier has been reached
   }
-  const double ys = raw_ys;
-  const double eff_reg = a.reg / ys;
-  const double l1c = a.enet * eff_reg, l2 = (1.0 - a.enet) * eff_reg;
-  const double icpt0 = a.fit_icpt ? my / ys : 0.0;
-  const double inv_ys = 1.0 / ys, inv_w = 1.0 / W;
   const bool owlqn = a.owlqn != 0;
   {
     const int per = (d + B - 1) / B, j0 = b * per, j1 = min(d, j0 + per);
-    for (int j = j0 + t; j < j1; j += kT) {
-      const double m = hd[5 + j] / W;
-      const double vx = denom > 0.0 ? fmax(hd[5 + d + j] - W * m * m, 0.0) / denom : 0.0;
-      const double sx = sqrt(vx);
-      const bool nz = sx != 0.0;
-      const double safe = nz ? sx : 1.0;
-      a.mx[j] = m;
-      a.sx[j] = safe;
-      a.inv_sx[j] = nz ? 1.0 / safe : 0.0;
-      a.regw[j] = l2 != 0.0 ? (a.std_f ? 1.0 : (nz ? 1.0 / (safe * safe) : 0.0)) : 0.0;
-      a.l1[j] = owlqn ? (a.std_f ? l1c : (nz ? l1c / safe : 0.0)) : 0.0;
-      a.x[j] = 0.0;
-      a.dir[j] = 0.0;
-      a.ag[j] = 0.0;
-    }
+    feature_consts(a, S, j0, j1);
   }
   for (int64_t r = (int64_t)b * kT + t; r < a.n; r += (int64_t)B * kT) a.mvec[r] = 0.0, a.dvec[r] = 0.0;  // x0 = 0
   __threadfence();
@@ -450,149 +743,13 @@ __global__ __launch_bounds__(kT, 1) void lsq_qn_kernel(QnArgs a) {
 
   // ---- one cost evaluation at x + alpha dir (mode 1, projected for OWLQN) or at x0 = 0 -------
   auto evaluate = [&](int mode, double alpha) -> Eval {
-    // E1: block 0 builds the trial point (kept for the acceptance), the f32 effective
-    // coefficients (global: every block reads them through its L2) and the margin offset
-    if (b == 0) {
-      double pm = 0.0, ps = 0.0;
-#pragma unroll 2
-      for (int j = t; j < NC; j += kT) {
-        float c32 = 0.0f;
-        if (j < d) {
-          double nx = 0.0;
-          if (mode == 1) {
-            const double xj = a.x[j];
-            nx = xj + a.dir[j] * alpha;
-            if (owlqn) {
-              const double orth = xj != 0.0 ? sgn(xj) : sgn(-a.ag[j]);
-              if (sgn(nx) != orth) nx = 0.0;
-            }
-          }
-          a.cx[j] = nx;
-          const double cf = nx * a.inv_sx[j];
-          pm += cf * a.mx[j];
-          if (a.shift) ps += a.shift[j] * cf;
-          // L-BFGS: the margin loop forms X . dir (a trial is mvec + alpha dvec); OWLQN's projected
-          // trial is not affine in alpha: its margins come from the trial's coefficients
-          const double cm = owlqn ? cf : a.dir[j] * a.inv_sx[j];
-          c32 = (float)(a.scale ? cm * a.scale[j] : cm);
-        }
-        a.cs[j] = c32;
-      }
-      const double cfmx = block_sum(pm, red);
-      double off = a.fit_icpt ? icpt0 - cfmx : icpt0;
-      if (a.shift) off = off + block_sum(ps, red);
-      if (t == 0) a.scal[16] = off;
-      __threadfence();
-    }
+    // E1: block 0 builds the trial point, the f32 effective coefficients and the margin offset
+    if (b == 0) build_trial(a, S, mode, alpha, NC, red);
     for (int j = t; j < NC; j += kT) colacc[j] = 0.0;
     grid.sync();
-    const double offset = a.scal[16];
-    const float* __restrict__ gcs = a.cs;
-
-    // E2: the fused pass (margins, then the column sums of the same tiles).  L-BFGS: margins
-    // only on the first trial of a line search (X . dir -> dvec); the others read X once
-    const bool first = !owlqn && mode == 1 && C.first;
-    const bool skip = !owlqn && !first;
-    double loss = 0.0, vsum = 0.0;
-    for (int64_t u = b; u < a.nunits; u += B) {
-      const int64_t s = u / UPS;
-      const int sub = (int)(u % UPS);
-      const unsigned char* p = a.X + s * a.NT * CH + ((sub * 64 + lane) << 4);
-      double acc[E];
-#pragma unroll
-      for (int e = 0; e < E; ++e) acc[e] = 0.0;
-#pragma unroll 1
-      for (int i0 = 0; i0 < (skip ? 0 : TPW); i0 += 8) {
-        u32x4 q[8];
-        float c[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          const int tt = wave + 8 * (i0 + k);
-          q[k] = tt < a.ntl ? *gptr<u32x4>(p + (int64_t)tt * CH) : u32x4{0u, 0u, 0u, 0u};
-          c[k] = *gptr<float>(gcs + tt * 32 + fl);
-        }
-        float s8[E];
-#pragma unroll
-        for (int e = 0; e < E; ++e) s8[e] = 0.0f;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          float xv[E];
-          unpack<L>(q[k], xv);
-#pragma unroll
-          for (int e = 0; e < E; ++e) s8[e] = fmaf(xv[e], c[k], s8[e]);
-        }
-#pragma unroll
-        for (int e = 0; e < E; ++e) acc[e] += (double)s8[e];
-      }
-      // feature sum across the 32 lanes of each half, then the 8 waves' partials in LDS
-#pragma unroll
-      for (int e = 0; e < E; ++e) {
-#pragma unroll
-        for (int o = 1; o < 32; o <<= 1) acc[e] += __shfl_xor(acc[e], o, 64);
-      }
-      double m = acc[0];
-#pragma unroll
-      for (int e = 1; e < E; ++e) m = fl == e ? acc[e] : m;
-      if (fl < E) mrow[wave][hf * E + fl] = m;
-      __syncthreads();
-      if (t < 2 * E) {
-        double mm = 0.0;
-        const int64_t r = frag_row<L>(s, sub, t / E, t % E);
-        if (!skip)
-#pragma unroll
-          for (int i = 0; i < kW; ++i) mm += mrow[i][t];
-        if (!owlqn && r < a.n) {  // mm: this unit's X . dir (first trial) -> the trial's margin
-          const double md = skip ? a.dvec[r] : mm;
-          if (first) a.dvec[r] = mm;
-          mm = a.mvec[r] + alpha * md;
-        }
-        double vv = 0.0;
-        if (r < a.n) {
-          const double wr = a.w[r];
-          if (wr != 0.0) {
-            const double diff = mm + offset - a.y[r] * inv_ys;
-            vv = wr * diff;
-            loss += 0.5 * vv * diff;
-            vsum += vv;
-          }
-        }
-        vrow[t] = (float)vv;
-      }
-      __syncthreads();
-      float vr[E];
-#pragma unroll
-      for (int e = 0; e < E; ++e) vr[e] = vrow[hf * E + e];
-      // column sums of the same tiles, most recently read first; the two lane halves (the
-      // feature's other rows) combine, then one f64 LDS accumulator per feature (this wave's
-      // tiles only: no other wave touches them)
-#pragma unroll 1
-      for (int i0 = TPW - 8; i0 >= 0; i0 -= 8) {
-        u32x4 q[8];
-#pragma unroll
-        for (int k = 7; k >= 0; --k) {
-          const int tt = wave + 8 * (i0 + k);
-          q[k] = tt < a.ntl ? *gptr<u32x4>(p + (int64_t)tt * CH) : u32x4{0u, 0u, 0u, 0u};
-        }
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          float xv[E];
-          unpack<L>(q[k], xv);
-          float sa = 0.0f;
-#pragma unroll
-          for (int e = 0; e < E; ++e) sa += vr[e] * xv[e];
-          sa += __shfl_xor(sa, 32, 64);
-          if (hf == 0) colacc[(wave + 8 * (i0 + k)) * 32 + fl] += (double)sa;
-        }
-      }
-    }
-    __syncthreads();
-    // the block's column slab
-    double* slab = a.part + (int64_t)b * NC;
-    for (int j = t; j < NC; j += kT) slab[j] = colacc[j];
-    {
-      const double bl = block_sum(loss, red), bv = block_sum(vsum, red);
-      if (t == 0) a.lpart[2 * b] = bl, a.lpart[2 * b + 1] = bv;
-    }
+    // E2: the fused pass
+    qn_pass<L, TPW>(a, S, mode, alpha, !owlqn && mode == 1 && C.first, 0.0, a.scal[16], colacc, mrow, vrow, red,
+                    b, B);
     __threadfence();
     grid.sync();
 
@@ -621,35 +778,10 @@ __global__ __launch_bounds__(kT, 1) void lsq_qn_kernel(QnArgs a) {
       __syncthreads();
       const int j = jb + t;
       if (t < 64 && j < j1) {
-      double graw = 0.0;
+        double graw = 0.0;
 #pragma unroll
-      for (int i = 0; i < kW; ++i) graw += fold[i][t];
-      if (a.scale) graw = graw * a.scale[j];
-      if (a.shift) graw = graw + a.shift[j] * vs;
-      const double nx = a.cx[j];
-      double gj = graw * a.inv_sx[j] * inv_w;
-      if (l2 != 0.0) {
-        const double rx = a.regw[j] * nx;
-        pr += nx * rx;
-        gj = gj + l2 * rx;
-      }
-      double agj = gj;
-      const double l = a.l1[j];
-      if (owlqn) {
-        pl += fabs(l * nx);
-        if (l != 0.0) {
-          if (nx == 0.0) {
-            const double dp = gj + l, dm = gj - l;
-            agj = dm > 0.0 ? dm : (dp < 0.0 ? dp : 0.0);
-          } else {
-            agj = gj + sgn(nx) * l;
-          }
-        }
-      }
-      a.cg[j] = gj;
-      a.cag[j] = agj;
-      pd += agj * a.dir[j];
-      pg += agj * agj;
+        for (int i = 0; i < kW; ++i) graw += fold[i][t];
+        grad_j(a, S, j, unscale_col(a, j, graw, vs), pr, pl, pd, pg);
       }
       __syncthreads();
     }
@@ -677,28 +809,13 @@ __global__ __launch_bounds__(kT, 1) void lsq_qn_kernel(QnArgs a) {
     __syncthreads();
     const double sr = bcast[0], sl = bcast[1], sd = bcast[2], sg = bcast[3];
     __syncthreads();  // bcast is rewritten by the next evaluation
-    Eval ev;
-    ev.v = lsum * inv_w;
-    if (l2 != 0.0) ev.v = ev.v + 0.5 * l2 * sr;
-    ev.adj = owlqn ? ev.v + sl : ev.v;
-    ev.dd = sd;
-    ev.gg = sg;
-    return ev;
+    return eval_of(a, S, lsum, sr, sl, sd, sg);
   };
 
   // ---- the optimizer as a state machine: thread 0 of every block runs the same scalar logic on
   // the same inputs (its block's LDS copy of the state), so every block takes the same next
   // action; ONE evaluate call site keeps the control state out of the pass's registers ----------
-  if (t == 0) {
-    C.act = kActEval;
-    C.mode = 0;
-    C.alpha = 0.0;
-    C.ls = kLsInit;
-    C.head = 0, C.hh = 0, C.H = 0, C.iter = 0, C.nfv = 1, C.pass = 0;
-    C.search_failed = 0, C.failed_once = 0, C.overflow = 0, C.why = -1, C.nev = 0, C.first = 0;
-    for (int i = 0; i < kFv; ++i) C.fv[i] = 0.0;
-    C.fv[kFv - 1] = __builtin_inf();
-  }
+  if (t == 0) ctl_init(C);
   __syncthreads();
   for (;;) {
     const int act = C.act;
@@ -711,22 +828,7 @@ __global__ __launch_bounds__(kT, 1) void lsq_qn_kernel(QnArgs a) {
         ctl_after_eval(C, ev, a, b == 0 ? a.out + d + 11 : nullptr);
       }
     } else if (act == kActAccept) {
-      if (b == 0) {  // the last evaluated trial becomes the state (history pair pushed first)
-        const bool push = C.ls != kLsInit;
-        int hd0 = C.head;
-        if (push) hd0 = (hd0 + kMem - 1) % kMem;
-        for (int j = t; j < d; j += kT) {
-          const double nx = a.cx[j], gj = a.cg[j];
-          if (push) {
-            a.S[(int64_t)hd0 * d + j] = nx - a.x[j];
-            a.Y[(int64_t)hd0 * d + j] = gj - a.g[j];
-          }
-          a.x[j] = nx;
-          a.g[j] = gj;
-          a.ag[j] = a.cag[j];
-        }
-        __threadfence();
-      }
+      if (b == 0) accept_block(a, C);
       if (!owlqn && C.ls != kLsInit) {  // the accepted trial's margins: mvec + alpha dvec
         const double al = C.alpha;
         for (int64_t r = (int64_t)b * kT + t; r < a.n; r += (int64_t)B * kT) a.mvec[r] = a.mvec[r] + al * a.dvec[r];
@@ -742,26 +844,155 @@ __global__ __launch_bounds__(kT, 1) void lsq_qn_kernel(QnArgs a) {
     __syncthreads();
   }
   if (b != 0) return;
-  if (C.overflow) {
-    if (t == 0) a.out[d + 1] = 8.0;
-    return;
+  finalize_block(a, C, S, red);
+}
+
+// ---- data-parallel form (X4): the same fit split at the reduction ---------------------------
+// Spark's l-bfgs sums every evaluation's loss and gradient over the partitions (treeAggregate,
+// DataQuality4MachineLearningApp.java:120-126); across ranks that is an RCCL all-reduce, which a
+// cooperative launch cannot contain.  Per evaluation the host enqueues, on one stream with no
+// host read in between:
+//   lsq_qn_dp_pass_kernel  (grid)    the fused E2 pass over this rank's rows -> per-block slabs
+//   lsq_qn_dp_fold_kernel  (d / 64)  fixed-order slab fold -> red = [Σ v x_j (d), loss, Σ v]
+//   RCCL all-reduce(red)             (d + 2) f64
+//   lsq_qn_dp_ctl_kernel   (1 block) E3 on the summed red, the Breeze state machine (after_eval,
+//                                    accept, two-loop recursion, next line-search step), the next
+//                                    trial point -- or the un-standardized result when done
+// The optimizer state (Ctl) lives in HBM between launches; every rank's control kernel reads the
+// same all-reduced bytes, so the ranks take identical decisions.  Once the state is done every
+// kernel returns at once: the host enqueues evaluations in batches ahead of the device and stops
+// when a pinned copy of the state's action says so (models/lbfgs_path.py).  The accepted step's
+// margin update (mvec += alpha dvec, a grid pass in the one-launch kernel) is folded into the
+// next search's first pass (Ctl.pend).
+
+__global__ __launch_bounds__(kT) void lsq_qn_dp_init_kernel(QnArgs a, int nc) {
+  __shared__ double red[kW];
+  __shared__ Ctl C;
+  const int t = threadIdx.x, d = a.d;
+  const Std S = std_of(a);
+  if (t < 5) a.out[d + 6 + t] = a.head[t];
+  if (t == 0) ctl_init(C);
+  __syncthreads();
+  if (S.status != 0) {
+    if (t == 0) {
+      a.out[d + 1] = (double)S.status;
+      C.act = kActDone;
+    }
+  } else {
+    feature_consts(a, S, 0, d);
+    __syncthreads();
+    build_trial(a, S, 0, 0.0, nc, red);
   }
-  // un-standardize: coef = x ys / sigma (0 for constant features), intercept = ȳ - coef . x̄
-  double pc = 0.0;
-  for (int j = t; j < d; j += kT) {
-    const double c = a.inv_sx[j] != 0.0 ? a.x[j] * ys / a.sx[j] : 0.0;
-    a.out[j] = c;
-    pc += c * a.mx[j];
+  __syncthreads();
+  if (t == 0) *a.ctl = C;
+}
+
+template <int L, int TPW>
+__global__ __launch_bounds__(kT, 1) void lsq_qn_dp_pass_kernel(QnArgs a) {
+  constexpr int E = L == 3 ? 16 : 8;
+  constexpr int NC = 8 * TPW * 32;
+  __shared__ double colacc[NC];
+  __shared__ double red[kW];
+  __shared__ double mrow[kW * 2 * E];
+  __shared__ float vrow[2 * E];
+  const Ctl* C = a.ctl;  // written by the previous kernel on this stream
+  if (C->act != kActEval) return;
+  const int mode = C->mode;
+  const double alpha = C->alpha, pend = C->pend;
+  const bool first = a.owlqn == 0 && mode == 1 && C->first;
+  const Std S = std_of(a);
+  for (int j = threadIdx.x; j < NC; j += kT) colacc[j] = 0.0;
+  __syncthreads();
+  qn_pass<L, TPW>(a, S, mode, alpha, first, pend, a.scal[16], colacc, mrow, vrow, red, blockIdx.x, gridDim.x);
+}
+
+// one block per 64 features (block 0 also sums the loss partials); the same summation order as
+// the one-launch kernel's E3
+//
+// The per-rank storage scale / shift is applied HERE, before the all-reduce: ranks may hold
+// different fp8 scales (each shard's amax) and the shift term needs this rank's Σ v.
+__global__ __launch_bounds__(kT) void lsq_qn_dp_fold_kernel(QnArgs a, int B, int nc) {
+  __shared__ double fold[kW][64];
+  __shared__ double lv[2];
+  if (a.ctl->act != kActEval) return;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6, d = a.d;
+  const int jb = blockIdx.x * 64;
+  if (wave == 0) {  // this rank's loss and Σ v (every block: the shift term needs Σ v)
+    double l0 = 0.0, l1s = 0.0;
+    for (int i = lane; i < B; i += kWave) l0 += a.lpart[2 * i], l1s += a.lpart[2 * i + 1];
+    l0 = wave_sum_f64(l0);
+    l1s = wave_sum_f64(l1s);
+    if (lane == 0) lv[0] = l0, lv[1] = l1s;
   }
-  const double cm = block_sum(pc, red);
+  {
+    const int j = jb + lane;
+    double sp = 0.0;
+    if (j < d)
+#pragma unroll 4
+      for (int i = wave; i < B; i += kW) sp += a.part[(int64_t)i * nc + j];
+    fold[wave][lane] = sp;
+  }
+  __syncthreads();
+  if (t < 64 && jb + t < d) {
+    double graw = 0.0;
+#pragma unroll
+    for (int i = 0; i < kW; ++i) graw += fold[i][t];
+    a.red[jb + t] = unscale_col(a, jb + t, graw, lv[1]);
+  }
+  if (blockIdx.x == 0 && t == 0) a.red[d] = lv[0], a.red[d + 1] = lv[1];
+}
+
+__global__ __launch_bounds__(kT) void lsq_qn_dp_ctl_kernel(QnArgs a, int nc) {
+  __shared__ double red[kW];
+  __shared__ Ctl C;
+  const int t = threadIdx.x, d = a.d;
+  if (t == 0) C = *a.ctl;
+  __syncthreads();
+  if (C.act != kActEval) return;
+  const Std S = std_of(a);
+  const bool owlqn = a.owlqn != 0;
+  double* hist = a.out + d + 11;
+  // E3 on the all-reduced sums
+  const double lsum = a.red[d];
+  double pr = 0.0, pl = 0.0, pd = 0.0, pg = 0.0;
+  for (int j = t; j < d; j += kT) grad_j(a, S, j, a.red[j], pr, pl, pd, pg);
+  const double sr = block_sum(pr, red), sl = block_sum(pl, red), sd = block_sum(pd, red), sg = block_sum(pg, red);
+  const Eval ev = eval_of(a, S, lsum, sr, sl, sd, sg);
+  __threadfence();
+  __syncthreads();
   if (t == 0) {
-    a.out[d] = a.fit_icpt ? my - cm : 0.0;
-    a.out[d + 1] = 0.0;
-    a.out[d + 2] = (double)C.why;
-    a.out[d + 3] = (double)C.H;
-    a.out[d + 4] = (double)C.iter;
-    a.out[d + 5] = (double)C.nev;  // cost evaluations (data passes)
+    ++C.nev;
+    C.first = 0;
+    C.pend = 0.0;  // the pass just run folded it (only a search's first pass sees pend != 0)
+    ctl_after_eval(C, ev, a, hist);
   }
+  __syncthreads();
+  for (;;) {
+    const int act = C.act;
+    if (act == kActEval) {
+      build_trial(a, S, C.mode, C.alpha, nc, red);
+      break;
+    }
+    if (act == kActDone) {
+      finalize_block(a, C, S, red);
+      break;
+    }
+    if (act == kActAccept) {
+      accept_block(a, C);
+      __syncthreads();
+      if (t == 0) {
+        if (!owlqn && C.ls != kLsInit) C.pend = C.alpha;  // mvec += alpha dvec, in the next first pass
+        ctl_after_accept(C, a, hist);
+      }
+    } else {  // kActApply
+      apply_dir(a, C, a.scal, red, owlqn);
+      __syncthreads();
+      if (t == 0) ctl_start_search(C, a.scal, a, hist);
+    }
+    __syncthreads();
+  }
+  __syncthreads();
+  if (t == 0) *a.ctl = C;
 }
 
 template <int L, int TPW>
@@ -811,9 +1042,13 @@ int64_t lsq_qn_work(int d, int blocks, int64_t n) {
          (8LL * tpw_of(d) * 32 + 1) / 2 + 2 * n;
 }
 
-void lsq_qn(const LsqX& x, const double* y, const double* w, const double* scale, const double* shift,
-            const double* head, bool fit_icpt, bool std_f, double reg, double enet, int max_iter, double tol,
-            int hist_cap, double* work, int blocks, double* out, hipStream_t st) {
+namespace {
+
+constexpr int64_t kCtlDoubles = (int64_t)((sizeof(Ctl) + 7) / 8);
+
+QnArgs make_args(const LsqX& x, const double* y, const double* w, const double* scale, const double* shift,
+                 const double* head, bool fit_icpt, bool std_f, double reg, double enet, int max_iter, double tol,
+                 int hist_cap, double* work, int blocks, double* out, bool dp) {
   if (x.layout != 2 && x.layout != 3) throw std::invalid_argument("lsq_qn: wide tile layouts only");
   if (x.d < 1 || x.d > kLsqQnMaxD) throw std::invalid_argument("lsq_qn: d out of range");
   if (hist_cap < 1 || blocks < 1) throw std::invalid_argument("lsq_qn: bad history capacity / grid");
@@ -843,9 +1078,72 @@ void lsq_qn(const LsqX& x, const double* y, const double* w, const double* scale
   a.scal = take(24);
   a.cs = reinterpret_cast<float*>(take((8LL * tpw * 32 + 1) / 2));
   a.mvec = take(x.n), a.dvec = take(x.n);
+  if (dp) {
+    a.red = take(d + 2);
+    a.ctl = reinterpret_cast<Ctl*>(take(kCtlDoubles));
+  }
   a.out = out;
+  return a;
+}
+
+template <int L, int TPW>
+const void* dp_pass_of() {
+  return (const void*)lsq_qn_dp_pass_kernel<L, TPW>;
+}
+
+const void* pick_dp(int layout, int tpw) {
+  if (layout == 2) {
+    switch (tpw) {
+      case 8: return dp_pass_of<2, 8>();
+      case 16: return dp_pass_of<2, 16>();
+      case 32: return dp_pass_of<2, 32>();
+      default: return dp_pass_of<2, 64>();
+    }
+  }
+  switch (tpw) {
+    case 8: return dp_pass_of<3, 8>();
+    case 16: return dp_pass_of<3, 16>();
+    case 32: return dp_pass_of<3, 32>();
+    default: return dp_pass_of<3, 64>();
+  }
+}
+
+}  // namespace
+
+void lsq_qn(const LsqX& x, const double* y, const double* w, const double* scale, const double* shift,
+            const double* head, bool fit_icpt, bool std_f, double reg, double enet, int max_iter, double tol,
+            int hist_cap, double* work, int blocks, double* out, hipStream_t st) {
+  QnArgs a = make_args(x, y, w, scale, shift, head, fit_icpt, std_f, reg, enet, max_iter, tol, hist_cap, work, blocks,
+                       out, false);
   void* args[] = {&a};
-  DQ_HIP_CHECK(hipLaunchCooperativeKernel(pick(x.layout, tpw), dim3(blocks), dim3(kT), args, 0, st));
+  DQ_HIP_CHECK(hipLaunchCooperativeKernel(pick(x.layout, tpw_of(x.d)), dim3(blocks), dim3(kT), args, 0, st));
+}
+
+int64_t lsq_qn_dp_work(int d, int blocks, int64_t n) { return lsq_qn_work(d, blocks, n) + d + 2 + kCtlDoubles; }
+
+int64_t lsq_qn_dp_red_offset(int d, int blocks, int64_t n) { return lsq_qn_work(d, blocks, n); }
+
+int64_t lsq_qn_dp_ctl_offset(int d, int blocks, int64_t n) { return lsq_qn_work(d, blocks, n) + d + 2; }
+
+void lsq_qn_dp(int phase, const LsqX& x, const double* y, const double* w, const double* scale, const double* shift,
+               const double* head, bool fit_icpt, bool std_f, double reg, double enet, int max_iter, double tol,
+               int hist_cap, double* work, int blocks, double* out, hipStream_t st) {
+  QnArgs a = make_args(x, y, w, scale, shift, head, fit_icpt, std_f, reg, enet, max_iter, tol, hist_cap, work, blocks,
+                       out, true);
+  const int tpw = tpw_of(x.d), nc = 8 * tpw * 32;
+  if (phase == 0) {  // start: mvec = dvec = 0 (x0), constants, the state, the first trial point
+    DQ_HIP_CHECK(hipMemsetAsync(a.mvec, 0, 2 * (size_t)x.n * sizeof(double), st));
+    hipLaunchKernelGGL(lsq_qn_dp_init_kernel, dim3(1), dim3(kT), 0, st, a, nc);
+  } else if (phase == 1) {  // one evaluation's pass over this rank's rows + the slab fold -> red
+    void* args[] = {&a};
+    DQ_HIP_CHECK(hipLaunchKernel(pick_dp(x.layout, tpw), dim3(blocks), dim3(kT), args, 0, st));
+    hipLaunchKernelGGL(lsq_qn_dp_fold_kernel, dim3((x.d + 63) / 64), dim3(kT), 0, st, a, blocks, nc);
+  } else if (phase == 2) {  // the control step on the all-reduced red
+    hipLaunchKernelGGL(lsq_qn_dp_ctl_kernel, dim3(1), dim3(kT), 0, st, a, nc);
+  } else {
+    throw std::invalid_argument("lsq_qn_dp: phase 0, 1 or 2");
+  }
+  DQ_HIP_CHECK(hipGetLastError());
 }
 
 }  // namespace dq4ml

@@ -72,6 +72,13 @@ PYBIND11_MODULE(_dq4ml_hip, m) {
     DQ_HIP_CHECK(hipStreamWaitEvent(as_stream(dst), reinterpret_cast<hipEvent_t>(ev), 0));
   });
 
+  m.def("standin", [](int blocks, int usec, uintptr_t st) { standin(blocks, usec, as_stream(st)); });
+  // a stream whose kernels only dispatch to the CUs set in mask (32 CUs per word, logical CU order)
+  m.def("stream_create_cumask", [](const std::vector<uint32_t>& mask) {
+    hipStream_t s = nullptr;
+    DQ_HIP_CHECK(hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data()));
+    return reinterpret_cast<uintptr_t>(s);
+  });
   m.def("device_info", []() {
     int dev = 0;
     DQ_HIP_CHECK(hipGetDevice(&dev));
@@ -264,8 +271,10 @@ PYBIND11_MODULE(_dq4ml_hip, m) {
     a.aug_scale[0] = s1;
     a.aug_scale[1] = syh;
     a.aug_scale[2] = syl;
+    a.stamps = wide_stamps();
     return a;
   };
+  m.def("gram_wide_set_stamps", [](uintptr_t p) { gram_wide_set_stamps(P<int64_t>(p)); });
   m.def("gram_wide", [wide_args](int eb, uintptr_t X, uintptr_t Xaug, uintptr_t zeros, int nt, int npanels, int d,
                                  int64_t nsup, int splitk, uintptr_t pairs, uintptr_t part, double s1, double syh,
                                  double syl, uintptr_t scales, uintptr_t out, uintptr_t stream, int ring, int waves,
@@ -284,10 +293,19 @@ PYBIND11_MODULE(_dq4ml_hip, m) {
   m.def("gram_wide_gang", [wide_args](int eb, uintptr_t X, uintptr_t Xaug, uintptr_t zeros, int nt, int npanels,
                                       int d, int64_t nsup, int S, uintptr_t pairs, uintptr_t part, double s1,
                                       double syh, double syl, uintptr_t scales, uintptr_t out, int grid,
-                                      uintptr_t stream, bool fold, int waves) {
+                                      uintptr_t stream, bool fold, int waves, uintptr_t bar) {
     WideArgs a = wide_args(X, Xaug, zeros, nt, npanels, d, nsup, 8 * S, part, s1, syh, syl);
     gram_wide_gang(eb, a, P<const int>(pairs), P<const float>(scales), P<double>(out), S, grid, as_stream(stream),
-                   fold, waves);
+                   fold, waves, P<int>(bar));
+  });
+  m.def("gram_wide_gangx_ints", &gram_wide_gangx_ints);
+  m.def("gram_wide_gangx", [wide_args](int eb, uintptr_t X, uintptr_t Xaug, uintptr_t zeros, int nt, int npanels,
+                                       int d, int64_t nsup, int S, uintptr_t pairs, uintptr_t part, double s1,
+                                       double syh, double syl, uintptr_t scales, uintptr_t out, int grid, uintptr_t q,
+                                       uintptr_t xcc_dbg, uintptr_t stream, bool fold) {
+    WideArgs a = wide_args(X, Xaug, zeros, nt, npanels, d, nsup, 8 * S, part, s1, syh, syl);
+    gram_wide_gangx(eb, a, P<const int>(pairs), P<const float>(scales), P<double>(out), S, grid, P<int>(q),
+                    P<int>(xcc_dbg), as_stream(stream), fold);
   });
   m.def("gram_wide_fold", [wide_args](int npanels, int d, int splitk, uintptr_t part, double s1, double syh,
                                       double syl, uintptr_t scales, uintptr_t out, uintptr_t out32, int J0, int J1,
@@ -390,6 +408,17 @@ PYBIND11_MODULE(_dq4ml_hip, m) {
            P<const double>(shift), P<const double>(head), fit_icpt, std_f, reg, enet, max_iter, tol, hist_cap,
            P<double>(work), blocks, P<double>(out), as_stream(stream));
   });
+  m.def("lsq_qn_dp_work", &lsq_qn_dp_work);
+  m.def("lsq_qn_dp_red_offset", &lsq_qn_dp_red_offset);
+  m.def("lsq_qn_dp_ctl_offset", &lsq_qn_dp_ctl_offset);
+  m.def("lsq_qn_dp", [lsqx](int phase, uintptr_t X, int layout, int d, int64_t n, uintptr_t y, uintptr_t w,
+                            uintptr_t scale, uintptr_t shift, uintptr_t head, bool fit_icpt, bool std_f, double reg,
+                            double enet, int max_iter, double tol, int hist_cap, uintptr_t work, int blocks,
+                            uintptr_t out, uintptr_t stream) {
+    lsq_qn_dp(phase, lsqx(X, layout, 2, 0, d, n), P<const double>(y), P<const double>(w), P<const double>(scale),
+              P<const double>(shift), P<const double>(head), fit_icpt, std_f, reg, enet, max_iter, tol, hist_cap,
+              P<double>(work), blocks, P<double>(out), as_stream(stream));
+  });
   m.def("regression_metrics",
         [](uintptr_t X, int xdt, int64_t ld, int d, int64_t n, uintptr_t y, int ydt, uintptr_t sel, uintptr_t coef,
            double b, double shift, uintptr_t partials, uintptr_t out, uintptr_t stream, int tiled) {
@@ -405,8 +434,10 @@ PYBIND11_MODULE(_dq4ml_hip, m) {
     csv_span_eq(P<const uint8_t>(buf), nbuf, P<const int64_t>(spans), n, P<const uint8_t>(lit), L, P<uint8_t>(out),
                 as_stream(stream));
   });
-  m.def("csv_line_ends", [](uintptr_t buf, int64_t n, uintptr_t counts, uintptr_t ends, uintptr_t stream) {
-    csv_line_ends(P<const uint8_t>(buf), n, P<int64_t>(counts), P<void>(ends), as_stream(stream));
+  m.def("csv_line_ends", [](uintptr_t buf, int64_t n, uintptr_t counts, uintptr_t ends, uintptr_t stream, int sep,
+                            uintptr_t facts) {
+    csv_line_ends(P<const uint8_t>(buf), n, P<int64_t>(counts), P<void>(ends), as_stream(stream), sep,
+                  P<int32_t>(facts));
   });
   m.def("csv_ends_i32", &csv_ends_i32);
   m.def("csv_parse", [](uintptr_t buf, int64_t n, uintptr_t ends, int64_t nlines, int ncols, int sep, uintptr_t dcols,

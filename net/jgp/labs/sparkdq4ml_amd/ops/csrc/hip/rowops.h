@@ -36,4 +36,7 @@ void huber_pass(const void* X, int xdt, int64_t ld, int d, int64_t n, int tiled,
                 const void* w, int wdt, const uint8_t* sel, const double* ceff, double icpt, double sigma, double eps,
                 double* mult, double* partials, double* out, hipStream_t st);
 
+// a bounded stand-in for a collective's channel blocks (diagnostics): blocks x 256 threads, usec each
+void standin(int blocks, int usec, hipStream_t st);
+
 }  // namespace dq4ml

@@ -571,4 +571,24 @@ void huber_pass(const void* X, int xdt, int64_t ld, int d, int64_t n, int tiled,
   DQ_HIP_CHECK(hipGetLastError());
 }
 
+// Stand-in for a collective kernel of the fit tail (diagnostics / tests: models/regression.py
+// DQ4ML_TAIL_STANDIN): `blocks` workgroups that each hold a CU slot for `usec` microseconds
+// (s_memrealtime runs at 100 MHz), the shape of an RCCL all-reduce's channel blocks.  The wait is
+// bounded (<= 1 ms) so the grid always drains.
+namespace {
+__global__ __launch_bounds__(256) void standin_kernel(int64_t ticks) {
+  if (threadIdx.x == 0) {
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while ((int64_t)(__builtin_amdgcn_s_memrealtime() - t0) < ticks) __builtin_amdgcn_s_sleep(2);
+  }
+  __syncthreads();
+}
+}  // namespace
+
+void standin(int blocks, int usec, hipStream_t st) {
+  if (blocks < 1 || blocks > 4096 || usec < 0 || usec > 1000) throw std::invalid_argument("standin: bad shape");
+  hipLaunchKernelGGL(standin_kernel, dim3(blocks), dim3(256), 0, st, (int64_t)usec * 100);
+  DQ_HIP_CHECK(hipGetLastError());
+}
+
 }  // namespace dq4ml

@@ -179,13 +179,15 @@ def _scan_chunk(h, buf, n: int, trailing: bool, ncols: int, sep: str, dev, hint=
     stream = torch.cuda.current_stream(dev).cuda_stream
     nb = int(h.csv_count_blocks(n))
     counts = torch.empty(nb + 1, dtype=torch.int64, device=dev)
-    h.csv_line_ends(buf.data_ptr(), n, counts.data_ptr(), 0, stream)
+    h.csv_line_ends(buf.data_ptr(), n, counts.data_ptr(), 0, stream, -1, 0)
     nterm = int(counts[nb].item())
     nlines = nterm + (1 if trailing else 0)
     # int32 line-end offsets below 2 GiB (half the bytes of the ends pass and of the parse's reads)
     ends = torch.empty(max(nlines, 1), dtype=torch.int32 if h.csv_ends_i32(n) else torch.int64, device=dev)
-    if nterm:
-        h.csv_line_ends(buf.data_ptr(), n, counts.data_ptr(), ends.data_ptr(), stream)
+    # the ends pass also counts, per block, the separators and the terminator kinds (the cutter's
+    # scan facts): no whole-chunk torch passes over the bytes / ends afterwards
+    facts = torch.empty(nb, 4, dtype=torch.int32, device=dev)
+    h.csv_line_ends(buf.data_ptr(), n, counts.data_ptr(), ends.data_ptr(), stream, ord(sep), facts.data_ptr())
     if trailing:
         ends[nterm:].fill_(n)  # a fill kernel: ``ends[nterm] = n`` is a blocking pageable copy
     m = max(nlines, 1)
@@ -196,32 +198,17 @@ def _scan_chunk(h, buf, n: int, trailing: bool, ncols: int, sep: str, dev, hint=
     ptrs = _h2d(np.array([t.data_ptr() for t in dcols] + [k for k, _ in kinds], dtype=np.int64), dev)
     valid = torch.empty(ncols, m, dtype=torch.bool, device=dev)
     keep = torch.empty(m, dtype=torch.bool, device=dev)
-    stats = torch.zeros(4 + 2 * ncols, dtype=torch.int64, device=dev)
+    # [parse stats (4 + 2 ncols), longest line, separators, shortest line, CR ends, LF ends, CR LF
+    # ends]: the facts the byte-parallel cutter (ops/scancut.py) relies on -- the separator count
+    # is nlines * (ncols - 1) when every line has exactly ncols fields; line lengths run terminator
+    # to terminator; a CR LF pair ends at its CR.  The parse kernel writes the line lengths.
+    stats = torch.zeros(10 + 2 * ncols, dtype=torch.int64, device=dev)
+    stats[6 + 2 * ncols:7 + 2 * ncols].fill_(1 << 30)  # the shortest line: a min from above
     h.csv_parse(buf.data_ptr(), n, ends.data_ptr(), nlines, ncols, ord(sep), ptrs.data_ptr(), valid.data_ptr(),
                 keep.data_ptr(), stats.data_ptr(), stream, **_opt_args(opts))
-    # facts for the byte-parallel cutter (ops/scancut.py), read with the stats: the longest line
-    # (terminator included) and the separator count (= nlines * (ncols - 1) when every line has
-    # exactly ncols fields, given that no column holds nulls)
-    # plus the shortest line and the terminator kinds (line ends are the CR of a CR LF pair):
-    # [longest, separators, shortest, CR ends, LF ends, CR LF ends]
-    z = torch.zeros(1, dtype=torch.int64, device=dev)
-    if nlines:
-        e = ends[:nlines].to(torch.int64)
-        d1 = e[1:] - e[:-1] if nlines > 1 else e[:1] + 1
-        maxl = torch.maximum(e[:1] + 1, d1.max()).reshape(1)
-        minl = torch.minimum(e[:1] + 1, d1.min()).reshape(1)
-    else:
-        maxl, minl = z, torch.full_like(z, 1 << 30)
-    nsep = (buf[:n] == ord(sep)).sum().reshape(1) if n else z
-    if nterm:
-        te = ends[:nterm].to(torch.int64)
-        tb = buf[te]
-        nx = buf[(te + 1).clamp(max=max(n - 1, 0))]
-        cr = tb == 13
-        kinds = torch.stack([cr.sum(), (tb == 10).sum(), (cr & (nx == 10) & (te + 1 < n)).sum()])
-    else:
-        kinds = torch.zeros(3, dtype=torch.int64, device=dev)
-    stats = torch.cat([stats, maxl, nsep.to(torch.int64), minl, kinds.to(torch.int64)])
+    fs = facts.sum(0, dtype=torch.int64)  # [separators, CR, LF, CR LF] over the ends pass's blocks
+    stats[5 + 2 * ncols:6 + 2 * ncols].copy_(fs[:1])
+    stats[7 + 2 * ncols:10 + 2 * ncols].copy_(fs[1:])
     return nlines, dcols, valid, keep, stats, base
 
 

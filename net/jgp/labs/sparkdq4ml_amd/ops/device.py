@@ -27,11 +27,46 @@ GRAM_MODES = {"fp64": 0, "fp32": 1, "bf16": 2, "fp8": 3, "fp32split": 4}
 _plan_cache = {}
 
 
+# CUs a full-chip Gram pass leaves to the fit tail (``dq4ml.gram.reserveCUs`` /
+# DQ4ML_GRAM_RESERVE_CUS).  The pipelined tail of fit k (fold, RCCL all-reduce, one-block solve;
+# models/regression.py _PendingWLS) runs beside fit k+1's pass; with a reserve the Gram grid is
+# `reserve` CUs' worth of blocks short and the pipeline / tail streams are CU-masked onto disjoint
+# CUs, so neither side ever holds a CU the other waits for.  The HBM-bound pass streams at the
+# same rate on 248 of 256 CUs (profiles/r5_tail_reserve.md).
+_gram_reserve = int(os.environ.get("DQ4ML_GRAM_RESERVE_CUS", "-1"))
+_cus_cache = {}
+
+
+def set_gram_reserve(n: int) -> None:
+    """CUs the full-chip Gram grids leave free for the fit tail (-1: the default, 0)."""
+    global _gram_reserve
+    _gram_reserve = int(n)
+    _plan_cache.clear()
+
+
+def gram_reserve() -> int:
+    return max(0, _gram_reserve)
+
+
+def _cus(h) -> int:
+    dev = torch.cuda.current_device()
+    c = _cus_cache.get(dev)
+    if c is None:
+        c = _cus_cache[dev] = int(h.device_info()["multiProcessorCount"])
+    return c
+
+
 def _plan_blocks(h, mode, d, n, xdt, xmode):
-    key = (torch.cuda.current_device(), mode, d, n, xdt, xmode)
+    reserve = gram_reserve()
+    key = (torch.cuda.current_device(), mode, d, n, xdt, xmode, reserve)
     nb = _plan_cache.get(key)
     if nb is None:
-        nb = _plan_cache[key] = int(h.gram_plan_blocks(mode, int(d), int(n), xdt, xmode))
+        nb = int(h.gram_plan_blocks(mode, int(d), int(n), xdt, xmode))
+        cus = _cus(h)
+        if reserve > 0 and nb >= cus:  # a full residency wave of blocks: give `reserve` CUs back
+            per = nb // cus
+            nb = max(1, nb - reserve * per)
+        _plan_cache[key] = nb
     return nb
 
 
@@ -837,6 +872,69 @@ class LsqPasses:
         return out
 
 
+    def qn_fit_dp(self, head: torch.Tensor, fit_icpt: bool, std_f: bool, reg: float, enet: float, max_iter: int,
+                  tol: float, all_reduce, batch: int = 4) -> Optional[torch.Tensor]:
+        """Data-parallel form of :meth:`qn_fit` (X4, ``lsq_qn.hip`` ``lsq_qn_dp_*``): per cost
+        evaluation the pass + fold kernels over THIS rank's rows, ``all_reduce`` (in place, on the
+        current stream) of the (d + 2) f64 partials, then a one-block control kernel holding the
+        Breeze state machine in HBM.  ``head`` must already be summed over the ranks.  Nothing is
+        read back per evaluation: evaluations are enqueued ``batch`` at a time, at most two batches
+        ahead of the device, and enqueueing stops once a pinned copy of the state's action reads
+        "done" (the kernels of a batch enqueued past the end return at once).  Same output layout
+        as :meth:`qn_fit`."""
+        import time
+
+        h = self._h
+        if self.layout not in (2, 3) or not 1 <= self.d <= int(h.LSQ_QN_MAX_D) or self.n < 1:
+            return None
+        key = (self.device.index, self.layout, self.d)
+        nb = _lsq_qn_grid.get(key)
+        if nb is None:
+            nb = _lsq_qn_grid[key] = int(h.lsq_qn_blocks(self.layout, self.d))
+        cap = wls_qn_cap(max_iter)
+        d, n = self.d, self.n
+        work = torch.empty(int(h.lsq_qn_dp_work(d, nb, n)), dtype=torch.float64, device=self.device)
+        red_off, ctl_off = int(h.lsq_qn_dp_red_offset(d, nb, n)), int(h.lsq_qn_dp_ctl_offset(d, nb, n))
+        red = work[red_off:red_off + d + 2]
+        act = work[ctl_off:ctl_off + 1].view(torch.int32)[:1]  # Ctl.act: the struct's first word
+        out = torch.zeros(d + 11 + cap, dtype=torch.float64, device=self.device)
+        out[d + 1:d + 2].fill_(9.0)  # status "not finished" (evaluation bound reached: the host path re-runs)
+        head = head.to(torch.float64).contiguous()
+        if head.numel() != 5 + 2 * d:
+            raise ValueError("lsq_qn: the summarizer head must hold 5 + 2d values")
+        shift = None if self.shift is None else self.shift.dev64.to(self.device).contiguous()
+        st = _stream()
+        args = (self._xb.data_ptr(), self.layout, d, n, self.y.data_ptr(), self.w.data_ptr(), _ptr(self.scales),
+                _ptr(shift), head.data_ptr(), bool(fit_icpt), bool(std_f), float(reg), float(enet), int(max_iter),
+                float(tol), cap, work.data_ptr(), nb, out.data_ptr())
+        h.lsq_qn_dp(0, *args, st)
+        # every line search ends within 21 evaluations and a fit within cap loop passes
+        bound = cap * 22 + 2
+        flags = torch.empty(2, dtype=torch.int32, pin_memory=True)
+        inflight = []  # (event, flag slot) per enqueued batch
+        done, k, slot = False, 0, 0
+        while not done and k < bound:
+            for _ in range(min(batch, bound - k)):
+                h.lsq_qn_dp(1, *args, st)
+                r = all_reduce(red)
+                if r.data_ptr() != red.data_ptr():  # (gloo reduces a host copy)
+                    red.copy_(r)
+                h.lsq_qn_dp(2, *args, st)
+                k += 1
+            flags[slot].copy_(act[0], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+            inflight.append((ev, slot))
+            slot ^= 1
+            if len(inflight) == 2:  # the device has the newer batch queued: wait for the older one
+                ev0, s0 = inflight.pop(0)
+                while not ev0.query():
+                    time.sleep(20e-6)
+                done = int(flags[s0]) == 3
+        self._qn_keep = (work, head, shift, flags)
+        return out
+
+
 _lsq_qn_grid = {}
 
 
@@ -1131,6 +1229,7 @@ def _wide_gang_s(P: int, nsup: int, G: int) -> int:
 
 
 _wide_grids = {}
+_last_xcc = None  # (diagnostics, DQ4ML_WIDE_XCCDBG=1) each gangx block's XCD from the last wide Gram
 
 
 def _wide_grid(h) -> int:
@@ -1188,22 +1287,46 @@ def _gram_wide(h, T: TiledWide, y, w, sel, x_zero_dead):
     pairs_dev = _h2d(np.asarray(pairs, dtype=np.int32).reshape(-1), dev)
     out = torch.empty(5 + 2 * d + d * (d + 1) // 2, dtype=torch.float64, device=dev)
     sched = os.environ.get("DQ4ML_WIDE_SCHED", "gang")
-    waves = int(os.environ.get("DQ4ML_WIDE_WAVES", "8"))  # (81 / 82: timing-only ablations of the static grid)
-    gs = _wide_gang_s(P, nsup, _wide_grid(h) // 8) if sched == "gang" and waves == 8 else 0
-    if sched == "gang" and not gs:
+    waves = int(os.environ.get("DQ4ML_WIDE_WAVES", "8"))  # (81 / 82: timing-only ablations, grid and gang)
+    gs = (_wide_gang_s(P, nsup, _wide_grid(h) // 8)
+          if sched in ("gang", "gangx") and waves in (8, 81, 82, 91, 94, 95) else 0)
+    if sched == "gangx" and waves != 8:
+        sched = "gang"
+    if sched in ("gang", "gangx") and not gs:
         sched = "queue"
     hq = _wide_queue_h(nsup) if sched == "queue" and waves == 8 else 0
     # data-parallel fit over RCCL: fold band by band and all-reduce each band while the next folds
     banded = comm.collectives_active() and comm.backend() == "nccl"
-    if gs:
+    if gs:  # gang units: the off-diagonal pairs first, then the diagonal ones (gram_wide.hip gang_unit)
+        pairs = [p for p in pairs if p[0] != p[1]] + [p for p in pairs if p[0] == p[1]]
+    if gs and sched == "gangx":
+        # XCD-keyed gang (gram_wide_gangx_kernel): the group is the XCD a block runs on, units
+        # dequeued per XCD (steal when empty) -- locality that does not assume round-robin dispatch
+        global _last_xcc
+        splitk = 8 * gs
+        gpairs = [p for p in pairs if p[1] < P]
+        gpairs_dev = _h2d(np.asarray(gpairs, dtype=np.int32).reshape(-1), dev)
+        part = torch.empty(int(h.gram_wide_partials(d, splitk)), dtype=torch.float32, device=dev)
+        grid = _wide_grid(h)
+        q = torch.empty(int(h.gram_wide_gangx_ints(grid)), dtype=torch.int32, device=dev)
+        dbg = torch.full((grid,), -1, dtype=torch.int32, device=dev) if os.environ.get("DQ4ML_WIDE_XCCDBG") else None
+        _last_xcc = dbg
+        h.gram_wide_gangx(eb, T.buf.data_ptr(), aug.buf.data_ptr(), _zero_page(h, dev).data_ptr(), T.nt, P, d, nsup,
+                          gs, gpairs_dev.data_ptr(), part.data_ptr(), 1.0, float(s_h), float(s_l), _ptr(T.scales),
+                          out.data_ptr(), grid, q.data_ptr(), _ptr(dbg), _stream(), not banded)
+    elif gs:
         # gang schedule (gram_wide_gang_kernel): 8 groups x S row ranges, static equal-cost units
         splitk = 8 * gs
         gpairs = [p for p in pairs if p[1] < P]
         gpairs_dev = _h2d(np.asarray(gpairs, dtype=np.int32).reshape(-1), dev)
         part = torch.empty(int(h.gram_wide_partials(d, splitk)), dtype=torch.float32, device=dev)
+        # per-round group barrier (DQ4ML_WIDE_GANG_SYNC, default on): the blocks of an XCD start
+        # every round together (profiles/r5_wide_limiter.md)
+        bar = (torch.empty(256, dtype=torch.int32, device=dev)
+               if os.environ.get("DQ4ML_WIDE_GANG_SYNC", "1") != "0" else None)
         h.gram_wide_gang(eb, T.buf.data_ptr(), aug.buf.data_ptr(), _zero_page(h, dev).data_ptr(), T.nt, P, d, nsup,
                          gs, gpairs_dev.data_ptr(), part.data_ptr(), 1.0, float(s_h), float(s_l), _ptr(T.scales),
-                         out.data_ptr(), _wide_grid(h), _stream(), not banded, waves)
+                         out.data_ptr(), _wide_grid(h), _stream(), not banded, waves, _ptr(bar))
     elif hq:
         # persistent XCD-grouped schedule (gram_wide_queue_kernel): 8 groups x h row ranges
         splitk = 8 * hq

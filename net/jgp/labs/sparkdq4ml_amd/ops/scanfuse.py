@@ -716,7 +716,7 @@ def _launch(cp, nodes, rel, extra: dict, own_stream: bool = True):
         z = torch.zeros(no + 1 + nb * gw, dtype=torch.int64, device=dev)
         offs = z[:no]
         if not cp.lookback:
-            h.csv_line_ends(buf.data_ptr(), n, offs.data_ptr(), 0, stream)
+            h.csv_line_ends(buf.data_ptr(), n, offs.data_ptr(), 0, stream, -1, 0)
         ev = z[no:no + 1].view(torch.int32)
         err, vflag = ev[0:1], ev[1:2]
         scalars = {"buf": buf, "offs": offs, "nalloc": nalloc, "trailing": int(f["trailing"]), "vflag": vflag}

@@ -120,7 +120,10 @@ def column_shift(parts: Sequence[torch.Tensor], uniform: bool = False) -> Option
     coll = uniform and comm.collectives_active()
     key = (tuple(_key(r) for r in rows), coll)
     bases = [_root(r) for r in rows]
-    hit = _memo.get(key)
+    # a rank-uniform shift never comes from the memo: whether a lookup hits depends on this
+    # process's tensor lifetimes (and the memo's clearing), so ranks could disagree on whether to
+    # issue the all-reduce below and hang; the collective is one small sample per pack_wide
+    hit = None if coll else _memo.get(key)
     if hit is not None:
         refs, val = hit
         if all(ref() is b for ref, b in zip(refs, bases)):  # same live tensors, not a reused address
@@ -144,9 +147,10 @@ def column_shift(parts: Sequence[torch.Tensor], uniform: bool = False) -> Option
             sb = torch.from_numpy(shift).to(torch.bfloat16).to(torch.float64).numpy()
             shift = np.where(bf16, sb, shift)
         val = Shift(shift, rows[0].device, uniform=coll or not comm.collectives_active())
-    if len(_memo) >= 256:
-        _memo.clear()
-    _memo[key] = ([weakref.ref(b) for b in bases], val)
+    if not coll:
+        if len(_memo) >= 256:
+            _memo.clear()
+        _memo[key] = ([weakref.ref(b) for b in bases], val)
     return val
 
 

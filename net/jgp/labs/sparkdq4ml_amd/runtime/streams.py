@@ -8,7 +8,7 @@ from typing import Dict, List, Optional
 import numpy as np
 import torch
 
-__all__ = ["side_stream", "StagingRing", "ChunkSource"]
+__all__ = ["side_stream", "StagingRing", "ChunkSource", "cu_masked_stream", "reserved_cu_ids"]
 
 _side: Dict[int, "torch.cuda.Stream"] = {}
 
@@ -19,6 +19,45 @@ def side_stream(device: Optional[torch.device] = None) -> "torch.cuda.Stream":
     if s is None:
         s = _side[idx] = torch.cuda.Stream(device=idx)
     return s
+
+
+def reserved_cu_ids(reserve: int, cus: int):
+    """The CUs held back for the fit tail: the last CU of each 32-CU block of the logical CU order
+    (one per XCD when that order is XCD-major), then the next-to-last ones, ... -- any choice is
+    correct, the two masks only have to be disjoint."""
+    per = max(1, cus // 32)
+    ids = []
+    k = 0
+    while len(ids) < min(reserve, cus):
+        for x in range(per):
+            c = x * 32 + 31 - k
+            if 0 <= c < cus and c not in ids and len(ids) < reserve:
+                ids.append(c)
+        k += 1
+    return ids
+
+
+_masked: Dict[tuple, "torch.cuda.Stream"] = {}
+
+
+def cu_masked_stream(cu_ids, cus: int, device=None, tag: int = 0) -> "torch.cuda.Stream":
+    """A stream whose kernels dispatch only to the CUs in ``cu_ids`` (``hipExtStreamCreateWithCUMask``),
+    cached per (device, CU set, tag).  Used to keep the pipelined fit tail (fold, RCCL kernels'
+    neighbours, solve) and the full-chip Gram passes on disjoint CUs (``dq4ml.gram.reserveCUs``)."""
+    from ..ops import native
+
+    idx = torch.cuda.current_device() if device is None or torch.device(device).index is None \
+        else torch.device(device).index
+    key = (idx, tuple(sorted(cu_ids)), tag)
+    st = _masked.get(key)
+    if st is None:
+        words = [0] * ((cus + 31) // 32)
+        for c in cu_ids:
+            words[c // 32] |= 1 << (c % 32)
+        with torch.cuda.device(idx):
+            ptr = native.hip().stream_create_cumask(words)
+        st = _masked[key] = torch.cuda.ExternalStream(ptr, device=torch.device("cuda", idx))
+    return st
 
 
 _pool = None

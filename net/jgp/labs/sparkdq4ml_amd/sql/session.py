@@ -14,7 +14,9 @@ all-reduce bucket size), ``dq4ml.trace`` (per-stage tracing, ``utils.tracing``),
 ``dq4ml.csv.deviceThresholdBytes`` (smallest file the device CSV scanner takes),
 ``dq4ml.chunkBytes`` (device CSV streaming chunk, default 256 MiB), ``dq4ml.shardInput`` (byte-range
 sharded reads across ranks, default true), ``dq4ml.fit.async`` (asynchronous normal-equation fits),
-``dq4ml.healthCheck`` (once|always|never rank-health barrier before distributed fits).
+``dq4ml.healthCheck`` (once|always|never rank-health barrier before distributed fits),
+``dq4ml.gram.reserveCUs`` (CUs the full-chip Gram passes leave free for the fit tail: fold, RCCL
+all-reduce and solve start at once beside the next pass; default 0 on one GPU, see ops/device.py).
 """
 from __future__ import annotations
 
@@ -229,6 +231,10 @@ class SparkSession:
             from ..parallel import comm
 
             comm.set_bucket_bytes(int(conf["dq4ml.bucketBytes"]))
+        if conf.get("dq4ml.gram.reserveCUs") is not None:
+            from ..ops import device as _dev
+
+            _dev.set_gram_reserve(int(conf["dq4ml.gram.reserveCUs"]))
         if conf.get("dq4ml.allreduceWire"):
             from ..parallel import comm
 

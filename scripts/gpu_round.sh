@@ -30,6 +30,12 @@ for s in $STEPS; do
     widepmc) (export TMPDIR=/tmp N=${N:-1e6} D=4096 EB=${EB:-8} REPS=${REPS:-2} VARIANTS="${VARIANTS:-5:morton:8:gang}"
        step widepmc1 600 rocprofv3 --kernel-trace --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE -d gpurun_out/widepmc1 -o run --output-format csv -- python scripts/wide_bench.py &&
        step widepmc2 600 rocprofv3 --kernel-trace --pmc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum -d gpurun_out/widepmc2 -o run --output-format csv -- python scripts/wide_bench.py) || exit $? ;;
+    widediag) step widediag 600 env N=${N:-1e7} D=4096 EB=8 DUR=${DUR:-4} VARIANTS="${VARIANTS:-5:morton:8:gang,5:morton:82:gang,5:morton:81:gang,4:morton:8:same}" python scripts/wide_diag.py ;;
+    widepmc5) (export TMPDIR=/tmp N=${N:-2e6} D=4096 EB=8 REPS=${REPS:-2} VARIANTS="${VARIANTS:-5:morton:8:gang}"
+       step widepmc5a 300 timeout -s KILL 240 rocprofv3 --kernel-trace --pmc GRBM_GUI_ACTIVE SQ_WAVE_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_INSTS_MFMA -d gpurun_out/widepmc5a -o run --output-format csv -- python scripts/wide_bench.py &&
+       step widepmc5b 300 timeout -s KILL 240 rocprofv3 --kernel-trace --pmc GRBM_GUI_ACTIVE TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCP_TCC_READ_REQ_sum SQ_LDS_IDX_ACTIVE SQ_INSTS_VMEM -d gpurun_out/widepmc5b -o run --output-format csv -- python scripts/wide_bench.py) || exit $? ;;
+    tailres) step tailres 600 env ROWS=${ROWS:-1.25e7} FITS=${FITS:-200} python scripts/tail_reserve_probe.py ;;
+    tailresprof) (export TMPDIR=/tmp; step tailresprof 300 timeout -s KILL 240 rocprofv3 --kernel-trace -d gpurun_out/tailresprof -o run --output-format csv -- python scripts/tail_reserve_probe.py) || exit $? ;;
     cfg4) step cfg4 900 python benchmarks/bench_dq_pipeline.py --steps ${CFG4_STEPS:-5} --warmup 2 --json-out gpurun_out/cfg4.json ;;
     cfg4csv) step cfg4csv 1000 python benchmarks/bench_csv_pipeline.py --features 64 --rows 1.25e8 --steps 5 --warmup 2 --json-out gpurun_out/cfg4csv.json &&
              (export TMPDIR=/tmp; step cfg4csvprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/cfg4csvprof -o run --output-format csv -- python benchmarks/bench_csv_pipeline.py --features 64 --rows 1.25e8 --steps 3 --warmup 2) &&

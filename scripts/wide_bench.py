@@ -41,6 +41,10 @@ outs = {}
 for _ in range(reps):
     for v in variants:
         fields = v.split(":")
+        os.environ.pop("DQ4ML_WIDE_GANG_SYNC", None)
+        if fields[-1] == "nosync":
+            os.environ["DQ4ML_WIDE_GANG_SYNC"] = "0"
+            fields = fields[:-1]
         same = fields[-1] == "same"
         if same:
             fields = fields[:-1]
@@ -48,8 +52,8 @@ for _ in range(reps):
         if same:
             os.environ["DQ4ML_WIDE_SAMEPAIR"] = "1"
         sched = "grid"
-        if fields[-1] == "gang":  # ...:gang = static equal-cost XCD gang schedule (the default)
-            sched = "gang"
+        if fields[-1] in ("gang", "gangx"):  # ...:gang = static equal-cost XCD gang, :gangx = XCD-keyed
+            sched = fields[-1]
             fields = fields[:-1]
         elif fields[-1].startswith("q"):  # ...:q<h> = persistent XCD-grouped queue schedule, h row ranges/group
             sched, hq = "queue", fields[-1][1:]

@@ -135,3 +135,107 @@ def test_device_qn_constant_label_takes_the_host_semantics(gpu_session, monkeypa
     m = LinearRegression(solver="l-bfgs", regParam=0.1).fit(df)
     assert np.all(m.coefficients.toArray() == 0.0)
     assert float(m.intercept) == pytest.approx(3.25)
+
+
+# ---- X4: the data-parallel form (pass, fold, all-reduce, one-block control kernel per evaluation)
+
+@pytest.mark.parametrize("eb,d,n,kw", [
+    (16, 300, 60_001, dict(regParam=0.02, elasticNetParam=0.0)),
+    (16, 300, 60_001, dict(regParam=0.02, elasticNetParam=0.6)),
+    (8, 1100, 30_017, dict(regParam=0.01, elasticNetParam=1.0, fitIntercept=False)),
+])
+def test_device_qn_dp_equals_one_launch(eb, d, n, kw):
+    """At one rank the split form runs the same passes as the cooperative launch (fold order,
+    deferred margin update, per-rank un-scaling before the identity reduce); only the four
+    evaluation scalars are summed by one block instead of per-block partials, so the fits agree to
+    rounding with the same evaluations -- enqueued with no host sync."""
+    from net.jgp.labs.sparkdq4ml_amd.ops import kernels
+
+    T, y = _data(torch.device("cuda"), d, n, d + eb, eb)
+    P = kernels.lsq_passes(T, y, None, None)
+    head = torch.cat([P.scalars(), P.moments()])
+    fit_icpt = kw.get("fitIntercept", True)
+    args = (head, fit_icpt, True, kw["regParam"], kw["elasticNetParam"], 60, 1e-9)
+    one = P.qn_fit(*args).cpu()
+    torch.cuda.synchronize()
+    torch.cuda.set_sync_debug_mode("error")
+    try:
+        dp = P.qn_fit_dp(*args, all_reduce=lambda t: t)
+    finally:
+        torch.cuda.set_sync_debug_mode("default")
+    dp = dp.cpu()
+    assert int(dp[d + 1]) == 0 and int(one[d + 1]) == 0
+    assert int(dp[d + 5]) == int(one[d + 5]) > 0  # the same number of evaluations
+    H = int(one[d + 3])
+    assert int(dp[d + 3]) == H and int(dp[d + 2]) == int(one[d + 2])  # history length, stop reason
+    torch.testing.assert_close(dp[:d + 1], one[:d + 1], rtol=1e-9, atol=1e-12)  # coefficients, intercept
+    torch.testing.assert_close(dp[d + 11:d + 11 + H], one[d + 11:d + 11 + H], rtol=1e-12, atol=0.0)
+
+
+def _run_workers(args, world, timeout=150):
+    import json
+    import os
+    import socket
+    import subprocess
+    import sys
+
+    here = os.path.dirname(os.path.abspath(__file__))
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r in range(world):
+        env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(r), WORLD_SIZE=str(world),
+                   LOCAL_RANK="0", DQ4ML_COMM_TIMEOUT="60")
+        procs.append(subprocess.Popen([sys.executable, os.path.join(here, "_gpu_qn_dp_worker.py"), *args], env=env,
+                                      stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
+    outs = []
+    for p in procs:
+        try:
+            so, se = p.communicate(timeout=timeout)
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise
+        assert p.returncode == 0, se[-3000:]
+        outs.append(json.loads(so.strip().splitlines()[-1]))
+    return outs
+
+
+@pytest.mark.parametrize("case", ["lbfgs", "owlqn"])
+def test_device_qn_two_rank_gloo_matches_single_process(gpu_session, monkeypatch, case):
+    """Two processes on the one GPU, each fitting its row shard (gloo: RCCL refuses two ranks on
+    one device): every rank ends with the single-process device fit of all rows."""
+    import sys
+
+    sys.path.insert(0, __import__("os").path.dirname(__import__("os").path.abspath(__file__)))
+    from _gpu_qn_dp_worker import CASES, data
+
+    from net.jgp.labs.sparkdq4ml_amd import LinearRegression
+    from net.jgp.labs.sparkdq4ml_amd.ops import device
+
+    c = CASES[case]
+    X, y = data(case, "cuda")
+    T = device.pack_wide([X], c["eb"], None, shift=None)
+    df = gpu_session.createDataFrame({"features": T, "label": y})
+    ref = _fit(LinearRegression(solver="l-bfgs", maxIter=60, tol=1e-9, **c["kw"]), df, monkeypatch, True)
+    assert ref._qn_evaluations is not None
+    outs = _run_workers(["gloo", case], 2)
+    b = ref.coefficients.toArray()
+    for o in outs:
+        assert o["evaluations"] is not None and o["evaluations"] > 0  # the device DP form ran
+        assert o["solver"] == ref.summary.solver
+        a = np.asarray(o["coef"])
+        assert np.abs(a - b).max() <= 2e-4 * max(1.0, np.abs(b).max()), np.abs(a - b).max()
+        assert o["intercept"] == pytest.approx(float(ref.intercept), rel=1e-4, abs=1e-5)
+        assert o["history"][0] == pytest.approx(float(ref.summary.objectiveHistory[0]), rel=1e-9)
+    assert outs[0]["coef"] == outs[1]["coef"]  # identical decisions on every rank
+
+
+@pytest.mark.parametrize("case", ["lbfgs", "fp8"])
+def test_device_qn_forced_rccl_has_no_host_sync(case):
+    """Every collective forced through a one-rank RCCL communicator (DQ4ML_FORCE_COLLECTIVES): the
+    l-bfgs fit takes the data-parallel device form and runs under sync_debug_mode("error")."""
+    o = _run_workers(["rccl", case], 1)[0]
+    assert o["evaluations"] is not None and o["evaluations"] > 0
