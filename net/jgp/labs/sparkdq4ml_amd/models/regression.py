@@ -598,12 +598,13 @@ set_tail_standin(os.environ.get("DQ4ML_TAIL_STANDIN"))
 
 
 def _tail_masks(dev):
-    """(Gram CUs, tail CUs, CU count) when ``dq4ml.gram.reserveCUs`` > 0 and CU masking is on
-    (``DQ4ML_CU_MASK``, default 1), else None: the pipelined Gram passes and the fit tail then run
-    on disjoint CUs, so a tail kernel never holds a CU a Gram block waits for and vice versa
-    (profiles/r5_tail_reserve.md)."""
+    """(Gram CUs, tail CUs, CU count) when ``dq4ml.gram.reserveCUs`` > 0 and CU masking is asked
+    for (``DQ4ML_CU_MASK=1``), else None: the pipelined Gram passes and the fit tail then run on
+    disjoint CUs.  Off by default: measured, the masked Gram pass ran 0.46-0.49 ms instead of
+    0.14 ms and the masked tail waited 100-136 us (profiles/r5_tail_reserve.md); unmasked, a
+    tail kernel starts within ~6 us beside a running pass."""
     reserve = device.gram_reserve()
-    if reserve <= 0 or os.environ.get("DQ4ML_CU_MASK", "1") == "0" or dev is None or dev.type != "cuda":
+    if reserve <= 0 or os.environ.get("DQ4ML_CU_MASK", "0") != "1" or dev is None or dev.type != "cuda":
         return None
     cus = device._cus(native.hip())
     tail = streams.reserved_cu_ids(reserve, cus)

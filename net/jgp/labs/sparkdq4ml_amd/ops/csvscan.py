@@ -376,7 +376,7 @@ def scan_device(data, sep: str = ",", infer: bool = True, device=None, ncols: Op
                 sharded: bool = False, chunk_bytes: Optional[int] = None, pinned: Optional[torch.Tensor] = None,
                 device_data: Optional[torch.Tensor] = None, types_hint: Optional[list] = None,
                 opts: Optional[dict] = None, user_types: Optional[list] = None, _depth: int = 0,
-                source_check=None):
+                source_check=None, device_ready=None):
     """Parse ``data`` on the device.  Inputs larger than ``chunk_bytes`` stream through a
     double-buffered pinned staging ring: chunk k+1's host->device copy runs on a side stream while
     chunk k is parsed, chunks split on row boundaries, type masks OR-merged over
@@ -393,7 +393,10 @@ def scan_device(data, sep: str = ",", infer: bool = True, device=None, ncols: Op
     ``opts``: dialect (quote, escape, comment, trim_lead, trim_trail, null_value; see
     ``csv_parse_dev.h``).  ``user_types``: a user schema (lattice codes in STRICT_CODES): the
     columns are stored as those types, a field that does not convert nulls its record (Spark's
-    PERMISSIVE), no inference."""
+    PERMISSIVE), no inference.
+
+    ``device_ready``: [(end offset, event)] of a ``device_data`` upload still in flight: each
+    chunk waits only for the pieces it covers (runtime.filecache progressive upload)."""
     if len(sep) != 1 or not (infer or user_types):
         return None
     if user_types:
@@ -419,9 +422,17 @@ def scan_device(data, sep: str = ",", infer: bool = True, device=None, ncols: Op
         cb = max(int(chunk_bytes or n), 1 << 30)
         bounds = chunk_bounds(data, cb) if n > cb else [0, n]
         parts = []
+        pending = list(device_ready or [])
+        cur = torch.cuda.current_stream(dev)
         for s, e in zip(bounds, bounds[1:]):
+            while pending and pending[0][0] < e:  # pieces wholly before this chunk's end
+                cur.wait_event(pending.pop(0)[1])
+            if pending:  # the piece holding the chunk's last bytes
+                cur.wait_event(pending[0][1])
             trailing = data[e - 1] not in (10, 13)
             parts.append(_scan_chunk(h, device_data[s:e], e - s, trailing, ncols, sep, dev, hint, opts, s))
+        for _, ev in pending:
+            cur.wait_event(ev)
     elif chunk_bytes is None or n <= chunk_bytes:
         if pinned is not None and n:
             buf = pinned.to(dev, non_blocking=True)  # page-locked mapping: direct DMA

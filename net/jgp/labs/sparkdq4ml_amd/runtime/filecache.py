@@ -51,6 +51,7 @@ class PinnedFile:
         self.lo = lo
         self.nbytes = nbytes = hi - lo
         self._dev = {}  # (device, lo, hi) -> uint8 device tensor
+        self._ready = {}  # (device, lo, hi) -> [(end, event)] of an upload not yet waited on
         self.type_hints = {}  # (lo, hi, sep) -> column type codes of the last device scan
         self.scan_facts = {}  # (lo, hi, sep, opts, user types) -> types / nulls / line count (ops/scanfuse)
         self.host = torch.empty(nbytes, dtype=torch.uint8).pin_memory()
@@ -76,15 +77,56 @@ class PinnedFile:
         """Still the cache's entry (not evicted, not superseded by a changed file, not cleared)."""
         return _live(self, _cache)
 
-    def device_bytes(self, device, lo: int = 0, hi: int = -1) -> torch.Tensor:
-        """The bytes [lo, hi) resident in HBM (one async DMA on first use, then reused)."""
+    def device_bytes(self, device, lo: int = 0, hi: int = -1, progressive: bool = False) -> torch.Tensor:
+        """The bytes [lo, hi) resident in HBM (async DMA on first use, then reused).
+
+        The first upload runs in 1 GiB pieces on a side stream (direct DMA from the page-locked
+        copy).  ``progressive``: the caller consumes the bytes in order and waits per piece
+        (:meth:`take_ready`: the first action's device scan parses piece k while piece k + 1 is
+        in flight, instead of after the whole file); otherwise the current stream waits for the
+        whole upload here."""
         hi = self.nbytes if hi < 0 else hi
         key = (str(device), lo, hi)
         t = self._dev.get(key)
         if t is None:
-            t = self._dev[key] = self.host[lo:hi].to(device, non_blocking=True)
+            from .streams import side_stream
+
+            dev = torch.device(device)
+            t = torch.empty(hi - lo, dtype=torch.uint8, device=dev)
+            side = side_stream(dev)
+            side.wait_stream(torch.cuda.current_stream(dev))  # t's allocation is ordered before the copies
+            ready = []
+            with torch.cuda.stream(side):
+                for a in range(lo, hi, _UPLOAD_PIECE):
+                    b = min(hi, a + _UPLOAD_PIECE)
+                    t[a - lo:b - lo].copy_(self.host[a:b], non_blocking=True)
+                    ev = torch.cuda.Event()
+                    ev.record(side)
+                    ready.append((b - lo, ev))
+            t.record_stream(side)
+            self._dev[key] = t
+            self._ready[key] = ready
+            if not progressive:
+                self.wait_ready(device, lo, hi)
+        elif not progressive:
+            self.wait_ready(device, lo, hi)
         return t
 
+    def take_ready(self, device, lo: int = 0, hi: int = -1):
+        """[(end offset, event)] of an upload still to be waited on by a progressive consumer
+        (empty once waited)."""
+        hi = self.nbytes if hi < 0 else hi
+        return list(self._ready.get((str(device), lo, hi), []))
+
+    def wait_ready(self, device, lo: int = 0, hi: int = -1):
+        """Order the current stream after the whole upload of [lo, hi) (a no-op once done)."""
+        hi = self.nbytes if hi < 0 else hi
+        r = self._ready.pop((str(device), lo, hi), None)
+        if r:
+            torch.cuda.current_stream(torch.device(device)).wait_event(r[-1][1])
+
+
+_UPLOAD_PIECE = 1 << 30  # first-upload piece (one event each; the device scan's chunks are >= 1 GiB)
 
 # HBM kept free for everything an action allocates besides the cached input bytes (parsed columns
 # of an eager scan, Gram partials, the staging ring, the caching allocator's slack)

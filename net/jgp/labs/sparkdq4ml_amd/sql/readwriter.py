@@ -368,11 +368,17 @@ class DataFrameReader:
                 names = comm.all_gather_object(names)[0]
             body = data[off:] if off else data
             dbytes = None
+            dready = None
             if pf is not None and _truthy(self._session.conf.get("dq4ml.csv.deviceCache", "true")):
                 from ..runtime import filecache
 
                 if filecache.device_bytes_allowed(hi - lo) or (str(dev), lo, hi) in pf._dev:
-                    dbytes = pf.device_bytes(dev, lo, hi)  # HBM-resident input bytes
+                    # HBM-resident input bytes; a first upload is consumed progressively by the
+                    # scan below (chunk k parsed while chunk k + 1 is copied)
+                    prog = hasattr(pf, "take_ready")
+                    dbytes = pf.device_bytes(dev, lo, hi, progressive=True) if prog else pf.device_bytes(dev, lo, hi)
+                    if prog:
+                        dready = [(e - off, ev) for e, ev in pf.take_ready(dev, lo, hi)]
                     dbytes = dbytes[off:] if off else dbytes
             hkey = (lo + off, hi, sep, repr(sorted(dopts.items())))
             fkey = hkey + (tuple(strict) if strict else None,)
@@ -390,12 +396,17 @@ class DataFrameReader:
 
             def dev_scan():
                 with tracing.span("csv_scan"):
-                    t = csvscan.scan_device(body, sep=sep, infer=infer, device=dev, sharded=shard, ncols=ncols,
-                                            chunk_bytes=int(self._session.conf.get("dq4ml.chunkBytes", str(256 << 20))),
-                                            pinned=None if pinned is None else pinned[off:], device_data=dbytes,
-                                            types_hint=(pf.type_hints.get(hkey) if pf is not None and not strict
-                                                        else None), opts=dopts, user_types=strict,
-                                            source_check=_map_check(pf))
+                    try:
+                        t = csvscan.scan_device(body, sep=sep, infer=infer, device=dev, sharded=shard, ncols=ncols,
+                                                chunk_bytes=int(self._session.conf.get("dq4ml.chunkBytes",
+                                                                                       str(256 << 20))),
+                                                pinned=None if pinned is None else pinned[off:], device_data=dbytes,
+                                                types_hint=(pf.type_hints.get(hkey) if pf is not None and not strict
+                                                            else None), opts=dopts, user_types=strict,
+                                                source_check=_map_check(pf), device_ready=dready)
+                    finally:
+                        if dready is not None:  # every later use of the cached bytes is ordered after the upload
+                            pf.wait_ready(dev, lo, hi)
                 if t is None:
                     return None
                 codes = [csvscan.type_code_of(f.dataType) for f in t.schema.fields]
@@ -437,6 +448,9 @@ class DataFrameReader:
             if lazy:
                 from ..ops.csvscan import _KIND, _opt_args
                 from ..sql.plan import CsvScanRelation
+
+                if dready:  # (a fresh upload the fused scans will read: order them after it)
+                    pf.wait_ready(dev, lo, hi)
 
                 codes = facts["types"]
                 fnames = final or [f"_c{i}" for i in range(len(codes))]

@@ -97,7 +97,7 @@ for s in $STEPS; do
     gangpmc) (export TMPDIR=/tmp N=2e6 D=4096 EB=8 REPS=2 VARIANTS="${VARIANTS:-5:morton:8:gang,4:morton:8:0:q2}"
        step gangpmc1 300 timeout -s KILL 240 rocprofv3 --kernel-trace --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA GRBM_GUI_ACTIVE -d gpurun_out/gangpmc1 -o run --output-format csv -- python scripts/wide_bench.py &&
        step gangpmc2 300 timeout -s KILL 240 rocprofv3 --kernel-trace --pmc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum GRBM_GUI_ACTIVE -d gpurun_out/gangpmc2 -o run --output-format csv -- python scripts/wide_bench.py) || exit $? ;;
-    cfg5) step cfg5 900 python benchmarks/bench_wide.py --steps 3 --warmup 1 --json-out gpurun_out/cfg5.json ;;
+    cfg5) step cfg5 900 python benchmarks/bench_wide.py --steps ${CFG5_STEPS:-10} --warmup 2 --json-out gpurun_out/cfg5.json ;;
     csv) step csv 600 python benchmarks/bench_csv_pipeline.py --steps 20 --warmup 3 --json-out gpurun_out/csv.json ;;
     p10ab) for r in 1 2; do
          step p10_lds_$r 300 python benchmarks/bench_csv_pipeline.py --steps 20 --warmup 3 &&

@@ -1,7 +1,7 @@
-"""Compute headroom for the fit tail: with ``dq4ml.gram.reserveCUs``
-the full-chip Gram grid leaves CUs free, so the pipelined tail of fit k -- fold, the RCCL
-all-reduce (emulated by the ``standin`` kernel: the shape of its channel blocks) and the solve --
-starts beside fit k+1's Gram pass instead of after its drain.  Results are unchanged."""
+"""Compute headroom for the fit tail: the pipelined tail of fit k --
+fold, the RCCL all-reduce (emulated by the ``standin`` kernel: the shape of its channel blocks)
+and the solve -- must start beside fit k+1's Gram pass, not after its drain.  Checked with the
+default grid and with ``dq4ml.gram.reserveCUs`` = 8; results are unchanged."""
 import numpy as np
 import pytest
 import torch
@@ -54,8 +54,8 @@ def test_reserved_cus_start_the_tail_beside_the_next_gram(async_session):
     w0, m0 = _waits(lr, df, 0)
     med8, med0 = w8[len(w8) // 2], w0[len(w0) // 2]
     # the stand-in collective starts within 10 us of its stream reaching it, beside the next
-    # fit's Gram pass -- on the masked reserve and (measured, profiles/r5_tail_reserve.md) even
-    # without one: a pass never leaves every CU slot taken
+    # fit's Gram pass -- with 8 CUs' worth of Gram blocks held back and (measured,
+    # profiles/r5_tail_reserve.md) without: a running pass never holds every CU slot
     assert med8 <= 10.0, (med8, med0)
     assert med0 <= 10.0, (med8, med0)
     # (a different grid sums the f32 block partials in a different grouping: same model to f32 noise)
