@@ -21,6 +21,9 @@ bool csv_ends_i32(int64_t n);
 // CR ends, lone-LF ends, CR LF ends]
 void csv_line_ends(const uint8_t* buf, int64_t n, int64_t* counts, void* ends, hipStream_t st, int sep = -1,
                    int32_t* facts = nullptr);
+// stats (10 + 2 ncols int64) initialised for csv_parse with the ends pass's nb x 4 facts summed in
+// (separators at 5 + 2 ncols, the shortest-line slot at 1 << 30, terminator kinds at 7 + 2 ncols ..)
+void csv_stats_init(const int32_t* facts, int64_t nb, int64_t* stats, int ncols, hipStream_t st);
 // dcols: [2 * ncols] int64 — ncols device pointers to nlines values each, then ncols storage
 // kinds (0 f64, 1 int32, 2 int64, 3 bool/uint8, 4 string span: int64 (fs << 25) | (raw << 24) | len
 // with fs the field's first byte in buf (csv_field_span), 5 timestamp: int64 microseconds);

@@ -489,6 +489,45 @@ void csv_line_ends(const uint8_t* buf, int64_t n, int64_t* counts, void* ends, h
   DQ_HIP_CHECK(hipGetLastError());
 }
 
+// The parse stats' initial values plus the ends pass's per-block facts folded in: one block,
+// launched between the ends pass and the parse (whose atomics then accumulate on top) -- it
+// replaces a zero fill, a min-slot fill, a column sum of the facts and two copies (five launches).
+// Layout (csv_scan.h): [parse counters 0 .. 4 + 2 ncols], 5 + 2 ncols separators, 6 + 2 ncols the
+// shortest line (a min from above), 7 + 2 ncols .. 9 + 2 ncols CR / lone-LF / CR LF ends.
+__global__ __launch_bounds__(256) void csv_stats_init_kernel(const int32_t* __restrict__ facts, int64_t nb,
+                                                            int64_t* __restrict__ stats, int ncols) {
+  __shared__ long long part[4][4];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  long long f[4] = {0, 0, 0, 0};
+  for (int64_t i = threadIdx.x; i < nb; i += 256) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) f[k] += facts[4 * i + k];
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) f[k] += __shfl_xor(f[k], o, 64);
+    if (lane == 0) part[wave][k] = f[k];
+  }
+  __syncthreads();
+  const int nstat = 10 + 2 * ncols;
+  for (int i = threadIdx.x; i < nstat; i += 256) {
+    int64_t v = 0;
+    if (i == 5 + 2 * ncols) v = part[0][0] + part[1][0] + part[2][0] + part[3][0];
+    else if (i == 6 + 2 * ncols) v = (int64_t)1 << 30;
+    else if (i >= 7 + 2 * ncols) {
+      const int k = i - (6 + 2 * ncols);
+      v = part[0][k] + part[1][k] + part[2][k] + part[3][k];
+    }
+    stats[i] = v;
+  }
+}
+
+void csv_stats_init(const int32_t* facts, int64_t nb, int64_t* stats, int ncols, hipStream_t st) {
+  hipLaunchKernelGGL(csv_stats_init_kernel, dim3(1), dim3(256), 0, st, facts, nb, stats, ncols);
+  DQ_HIP_CHECK(hipGetLastError());
+}
+
 template <typename IT>
 static void launch_parse(bool small, int64_t g, hipStream_t st, const uint8_t* buf, int64_t n, const IT* ends,
                          int64_t nlines, int ncols, const CsvOpts& o, const int64_t* dcols, uint8_t* valid,

@@ -439,6 +439,9 @@ PYBIND11_MODULE(_dq4ml_hip, m) {
     csv_line_ends(P<const uint8_t>(buf), n, P<int64_t>(counts), P<void>(ends), as_stream(stream), sep,
                   P<int32_t>(facts));
   });
+  m.def("csv_stats_init", [](uintptr_t facts, int64_t nb, uintptr_t stats, int ncols, uintptr_t stream) {
+    csv_stats_init(P<const int32_t>(facts), nb, P<int64_t>(stats), ncols, as_stream(stream));
+  });
   m.def("csv_ends_i32", &csv_ends_i32);
   m.def("csv_parse", [](uintptr_t buf, int64_t n, uintptr_t ends, int64_t nlines, int ncols, int sep, uintptr_t dcols,
                         uintptr_t valid, uintptr_t keep, uintptr_t stats, uintptr_t stream, int quote, int escape,

@@ -202,13 +202,11 @@ def _scan_chunk(h, buf, n: int, trailing: bool, ncols: int, sep: str, dev, hint=
     # ends]: the facts the byte-parallel cutter (ops/scancut.py) relies on -- the separator count
     # is nlines * (ncols - 1) when every line has exactly ncols fields; line lengths run terminator
     # to terminator; a CR LF pair ends at its CR.  The parse kernel writes the line lengths.
-    stats = torch.zeros(10 + 2 * ncols, dtype=torch.int64, device=dev)
-    stats[6 + 2 * ncols:7 + 2 * ncols].fill_(1 << 30)  # the shortest line: a min from above
+    # (initialised on the device with the ends pass's facts folded in: csv_stats_init)
+    stats = torch.empty(10 + 2 * ncols, dtype=torch.int64, device=dev)
+    h.csv_stats_init(facts.data_ptr(), nb, stats.data_ptr(), ncols, stream)
     h.csv_parse(buf.data_ptr(), n, ends.data_ptr(), nlines, ncols, ord(sep), ptrs.data_ptr(), valid.data_ptr(),
                 keep.data_ptr(), stats.data_ptr(), stream, **_opt_args(opts))
-    fs = facts.sum(0, dtype=torch.int64)  # [separators, CR, LF, CR LF] over the ends pass's blocks
-    stats[5 + 2 * ncols:6 + 2 * ncols].copy_(fs[:1])
-    stats[7 + 2 * ncols:10 + 2 * ncols].copy_(fs[1:])
     return nlines, dcols, valid, keep, stats, base
 
 
@@ -395,7 +393,7 @@ def scan_device(data, sep: str = ",", infer: bool = True, device=None, ncols: Op
     columns are stored as those types, a field that does not convert nulls its record (Spark's
     PERMISSIVE), no inference.
 
-    ``device_ready``: [(end offset, event)] of a ``device_data`` upload still in flight: each
+    ``device_ready``: [(end offset, piece)] of a ``device_data`` upload still in flight: each
     chunk waits only for the pieces it covers (runtime.filecache progressive upload)."""
     if len(sep) != 1 or not (infer or user_types):
         return None
@@ -424,15 +422,17 @@ def scan_device(data, sep: str = ",", infer: bool = True, device=None, ncols: Op
         parts = []
         pending = list(device_ready or [])
         cur = torch.cuda.current_stream(dev)
+        # (a piece's ``wait(stream)``: a torch event, or a runtime.filecache._Piece whose uploader
+        # thread may not have enqueued the DMA yet -- then the host blocks until it has)
         for s, e in zip(bounds, bounds[1:]):
             while pending and pending[0][0] < e:  # pieces wholly before this chunk's end
-                cur.wait_event(pending.pop(0)[1])
+                pending.pop(0)[1].wait(cur)
             if pending:  # the piece holding the chunk's last bytes
-                cur.wait_event(pending[0][1])
+                pending[0][1].wait(cur)
             trailing = data[e - 1] not in (10, 13)
             parts.append(_scan_chunk(h, device_data[s:e], e - s, trailing, ncols, sep, dev, hint, opts, s))
         for _, ev in pending:
-            cur.wait_event(ev)
+            ev.wait(cur)
     elif chunk_bytes is None or n <= chunk_bytes:
         if pinned is not None and n:
             buf = pinned.to(dev, non_blocking=True)  # page-locked mapping: direct DMA

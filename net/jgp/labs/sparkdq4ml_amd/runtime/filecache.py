@@ -21,6 +21,7 @@ import threading
 from collections import OrderedDict
 from concurrent.futures import ThreadPoolExecutor
 
+import numpy as np
 import torch
 
 __all__ = ["PinnedFile", "MappedFile", "open_pinned", "open_mapped", "shard_range", "map_readonly",
@@ -41,7 +42,51 @@ def _readers() -> ThreadPoolExecutor:
     return _pool
 
 
-class PinnedFile:
+class _Resident:
+    """The HBM-resident copies of an input's byte ranges and the pieces of a first upload still
+    to be waited on.  A piece is ``(end offset, p)`` where ``p.wait(stream)`` orders ``stream``
+    after that piece's DMA (a ``torch.cuda.Event``, or an :class:`_Piece` that a background
+    uploader fills)."""
+
+    def take_ready(self, device, lo: int = 0, hi: int = -1):
+        """[(end offset, piece)] of an upload still to be waited on by a progressive consumer
+        (empty once waited)."""
+        hi = self.nbytes if hi < 0 else hi
+        return list(self._ready.get((str(device), lo, hi), []))
+
+    def wait_ready(self, device, lo: int = 0, hi: int = -1):
+        """Order the current stream after the whole upload of [lo, hi) (a no-op once done)."""
+        hi = self.nbytes if hi < 0 else hi
+        r = self._ready.pop((str(device), lo, hi), None)
+        if r:  # (pieces are copied in order on one stream: the last one's completion covers all)
+            r[-1][1].wait(torch.cuda.current_stream(torch.device(device)))
+
+
+class _Piece:
+    """One piece of a background upload: the host learns that its DMA has been ENQUEUED (an
+    event set by the uploader thread) and then orders a stream after the DMA itself."""
+
+    def __init__(self):
+        self._enq = threading.Event()
+        self._ev = None
+        self._err = None
+
+    def done(self, ev):
+        self._ev = ev
+        self._enq.set()
+
+    def fail(self, err):
+        self._err = err
+        self._enq.set()
+
+    def wait(self, stream):
+        self._enq.wait()
+        if self._err is not None:
+            raise RuntimeError("device upload of the input bytes failed") from self._err
+        stream.wait_event(self._ev)
+
+
+class PinnedFile(_Resident):
     """``host``: pinned uint8 tensor with the file's bytes; ``data``: a numpy view of it (what the
     scanner indexes/slices on the host)."""
 
@@ -106,24 +151,9 @@ class PinnedFile:
             t.record_stream(side)
             self._dev[key] = t
             self._ready[key] = ready
-            if not progressive:
-                self.wait_ready(device, lo, hi)
-        elif not progressive:
+        if not progressive:
             self.wait_ready(device, lo, hi)
         return t
-
-    def take_ready(self, device, lo: int = 0, hi: int = -1):
-        """[(end offset, event)] of an upload still to be waited on by a progressive consumer
-        (empty once waited)."""
-        hi = self.nbytes if hi < 0 else hi
-        return list(self._ready.get((str(device), lo, hi), []))
-
-    def wait_ready(self, device, lo: int = 0, hi: int = -1):
-        """Order the current stream after the whole upload of [lo, hi) (a no-op once done)."""
-        hi = self.nbytes if hi < 0 else hi
-        r = self._ready.pop((str(device), lo, hi), None)
-        if r:
-            torch.cuda.current_stream(torch.device(device)).wait_event(r[-1][1])
 
 
 _UPLOAD_PIECE = 1 << 30  # first-upload piece (one event each; the device scan's chunks are >= 1 GiB)
@@ -164,45 +194,80 @@ def _live(entry, table) -> bool:
         return any(v is entry for v in table.values())
 
 
-class MappedFile:
+class MappedFile(_Resident):
     """A byte range too large for the pinned host cache: a read-only map of the file, plus the same
     per-range facts a ``PinnedFile`` keeps (the device scan's type hints and scan facts) and its
-    HBM-resident copy when the device cache allows one (filled chunk by chunk through the pinned
-    staging ring, never a whole-range host copy)."""
+    HBM-resident copy when the device cache allows one (filled piece by piece through two pinned
+    bounce buffers, never a whole-range host copy)."""
 
-    host = None  # no page-locked copy: chunks are staged
+    host = None  # no page-locked copy: pieces are staged
 
     def __init__(self, path: str, lo: int, hi: int):
         self.path, self.lo, self.nbytes = path, lo, hi - lo
         self._map = map_readonly(path)
         self.data = memoryview(self._map)[lo:hi]
         self._dev = {}
+        self._ready = {}
         self.type_hints = {}
         self.scan_facts = {}
 
     def live(self) -> bool:
         return _live(self, _mapped)
 
-    def device_bytes(self, device, lo: int = 0, hi: int = -1, chunk_bytes: int = 1 << 30) -> torch.Tensor:
+    def device_bytes(self, device, lo: int = 0, hi: int = -1, progressive: bool = False) -> torch.Tensor:
+        """The bytes [lo, hi) resident in HBM.  The first call starts an uploader thread: per
+        1 GiB piece, a parallel host memcpy from the map into a pinned bounce buffer, then a DMA
+        straight into the resident tensor on the side stream (two bounce buffers: piece k + 1's
+        memcpy overlaps piece k's DMA).  ``progressive`` as for :meth:`PinnedFile.device_bytes`:
+        the caller's scan parses piece k while later pieces are still being read and copied."""
         hi = self.nbytes if hi < 0 else hi
         key = (str(device), lo, hi)
         t = self._dev.get(key)
         if t is None:
-            from .streams import StagingRing
+            from .streams import side_stream
 
-            t = torch.empty(hi - lo, dtype=torch.uint8, device=device)
-            cb = max(1, min(chunk_bytes, hi - lo))
-            ring = StagingRing(cb, depth=2, device=torch.device(device))
-            spans = [(a, min(hi, a + cb)) for a in range(lo, hi, cb)]
-            if spans:
-                ring.put(0, self.data[spans[0][0]:spans[0][1]])
-            for i, (a, b) in enumerate(spans):
-                if i + 1 < len(spans):
-                    ring.put(i + 1, self.data[spans[i + 1][0]:spans[i + 1][1]])
-                t[a - lo:b - lo].copy_(ring.get(i))
-                ring.release(i)
+            dev = torch.device(device)
+            t = torch.empty(hi - lo, dtype=torch.uint8, device=dev)
+            side = side_stream(dev)
+            side.wait_stream(torch.cuda.current_stream(dev))  # t's allocation is ordered before the copies
+            t.record_stream(side)
+            spans = [(a, min(hi, a + _UPLOAD_PIECE)) for a in range(lo, hi, _UPLOAD_PIECE)]
+            pieces = [_Piece() for _ in spans]
             self._dev[key] = t
+            self._ready[key] = [(b - lo, p) for (_, b), p in zip(spans, pieces)]
+            threading.Thread(target=self._upload, args=(t, dev, side, lo, spans, pieces), daemon=True,
+                             name="dq4ml-upload").start()
+        if not progressive:
+            self.wait_ready(device, lo, hi)
         return t
+
+    def _upload(self, t, dev, side, lo, spans, pieces):
+        from .streams import _parallel_copy
+
+        try:
+            with torch.cuda.device(dev):
+                width = max(b - a for a, b in spans)
+                bounce = [torch.empty(width, dtype=torch.uint8, pin_memory=True) for _ in range(min(2, len(spans)))]
+                copied = [None] * len(bounce)
+                for i, ((a, b), p) in enumerate(zip(spans, pieces)):
+                    k = i % len(bounce)
+                    if copied[k] is not None:
+                        copied[k].synchronize()  # the bounce buffer's previous DMA has drained
+                    _parallel_copy(bounce[k][:b - a].numpy(), np.frombuffer(self.data, dtype=np.uint8, count=b - a,
+                                                                            offset=a))
+                    with torch.cuda.stream(side):
+                        t[a - lo:b - lo].copy_(bounce[k][:b - a], non_blocking=True)
+                        ev = torch.cuda.Event()
+                        ev.record(side)
+                    copied[k] = ev
+                    p.done(ev)
+                for ev in copied:
+                    if ev is not None:
+                        ev.synchronize()
+        except BaseException as e:  # every waiter raises instead of hanging
+            for p in pieces:
+                if not p._enq.is_set():
+                    p.fail(e)
 
 
 _mapped: "OrderedDict[tuple, MappedFile]" = OrderedDict()

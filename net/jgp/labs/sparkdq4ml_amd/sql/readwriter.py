@@ -375,10 +375,8 @@ class DataFrameReader:
                 if filecache.device_bytes_allowed(hi - lo) or (str(dev), lo, hi) in pf._dev:
                     # HBM-resident input bytes; a first upload is consumed progressively by the
                     # scan below (chunk k parsed while chunk k + 1 is copied)
-                    prog = hasattr(pf, "take_ready")
-                    dbytes = pf.device_bytes(dev, lo, hi, progressive=True) if prog else pf.device_bytes(dev, lo, hi)
-                    if prog:
-                        dready = [(e - off, ev) for e, ev in pf.take_ready(dev, lo, hi)]
+                    dbytes = pf.device_bytes(dev, lo, hi, progressive=True)
+                    dready = [(e - off, ev) for e, ev in pf.take_ready(dev, lo, hi)]
                     dbytes = dbytes[off:] if off else dbytes
             hkey = (lo + off, hi, sep, repr(sorted(dopts.items())))
             fkey = hkey + (tuple(strict) if strict else None,)

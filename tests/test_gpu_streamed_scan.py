@@ -93,3 +93,33 @@ def test_streamed_relation_other_actions_scan_eagerly(spark, tmp_path, monkeypat
     assert df.count() == 60_000
     rows = df.take(3)
     assert len(rows) == 3 and len(rows[0]) == 9
+
+
+@pytest.mark.parametrize("mapped", [False, True])
+def test_first_upload_in_pieces_is_exact(spark, tmp_path, monkeypatch, mapped):
+    """runtime.filecache first upload in many pieces (pinned: events on the side stream; mapped:
+    the uploader thread's bounce buffers) consumed progressively by the first scan: the resident
+    bytes equal the file and the scan equals a fresh host-staged one."""
+    import csv_synth
+
+    from net.jgp.labs.sparkdq4ml_amd.runtime import filecache
+
+    p = str(tmp_path / "u.csv")
+    csv_synth.write_wide_csv(p, 50_000, 6, seed=5, device="cuda", keep=False, y0=60.0, chunk=1 << 16)
+    size = os.path.getsize(p)
+    monkeypatch.setattr(filecache, "_UPLOAD_PIECE", 1 << 20)  # ~ size / 1 MiB pieces
+    if mapped:
+        monkeypatch.setattr(filecache, "MAX_BYTES", size // 2)
+    df = spark.read().format("csv").option("inferSchema", "true").load(p)
+    got = np.array([list(r) for r in df.collect()], dtype=np.float64)
+    entries = list((filecache._mapped if mapped else filecache._cache).values())
+    assert len(entries) == 1 and len(entries[0]._dev) == 1
+    resident = next(iter(entries[0]._dev.values()))
+    with open(p, "rb") as f:
+        raw = np.frombuffer(f.read(), dtype=np.uint8)
+    assert np.array_equal(resident.cpu().numpy(), raw)
+    filecache.clear()
+    monkeypatch.setenv("DQ4ML_FILECACHE_DEVICE_BYTES", "1")  # reference: nothing resident
+    df2 = spark.read().format("csv").option("inferSchema", "true").load(p)
+    ref = np.array([list(r) for r in df2.collect()], dtype=np.float64)
+    assert got.shape == (50_000, 7) and np.array_equal(got, ref)
