@@ -160,11 +160,20 @@ def main(argv=None):
 
     if dev.type == "cuda":
         torch.cuda.synchronize()
+    prof = None
+    if os.environ.get("DQ4ML_BENCH_FIRST_PROFILE"):  # host-side profile of the first action only
+        import cProfile
+
+        prof = cProfile.Profile()
+        prof.enable()
     t0 = time.perf_counter()
     step()
     if dev.type == "cuda":
         torch.cuda.synchronize()
     first_ms = (time.perf_counter() - t0) * 1e3
+    if prof is not None:
+        prof.disable()
+        prof.dump_stats(os.environ["DQ4ML_BENCH_FIRST_PROFILE"])
     elapsed, model = timed(step, a.steps, max(0, a.warmup - 1), dev)
     info = world_info(dev)
     from net.jgp.labs.sparkdq4ml_amd.ops import scancut

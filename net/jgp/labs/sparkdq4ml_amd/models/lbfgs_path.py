@@ -205,7 +205,9 @@ def _train_passes(est, df, X, y, w, sel, d, checks=(), device_qn=True):
     max_iter, tol = int(est.getOrDefault("maxIter")), float(est.getOrDefault("tol"))
     if device_qn and _device_qn_ok(df, P):
         with tracing.span("solve"):
-            if comm.collectives_active():  # X4: one (d + 2)-f64 all-reduce per evaluation, no host read
+            # X4: one (d + 2)-f64 all-reduce per evaluation, no host read.  DQ4ML_QN_SPLIT=1 runs
+            # the same split form on one rank without a group (plain launches: counter runs)
+            if comm.collectives_active() or os.environ.get("DQ4ML_QN_SPLIT") == "1":
                 out = P.qn_fit_dp(head, fit_icpt, std_flag, reg, enet, max_iter, tol, comm.all_reduce_sum)
             else:
                 out = P.qn_fit(head, fit_icpt, std_flag, reg, enet, max_iter, tol)

@@ -3,14 +3,22 @@
 from __future__ import annotations
 
 import copy as _copy
-import uuid
+import itertools
+import os
 from typing import Any, Callable, Dict, Optional
 
 __all__ = ["Param", "Params", "random_uid", "param_accessors"]
 
 
+# Spark's Identifiable.randomUID takes 12 hex digits of a random UUID; uids only need to be
+# distinct, so a per-process random base plus a counter gives the same form without an
+# os.urandom call per estimator (two per rebuilt lab action)
+_UID_BASE = int.from_bytes(os.urandom(6), "little")
+_uid_seq = itertools.count()
+
+
 def random_uid(prefix: str) -> str:
-    return f"{prefix}_{uuid.uuid4().hex[-12:]}"
+    return f"{prefix}_{(_UID_BASE + 0x9E3779B97F4A * next(_uid_seq)) & 0xFFFFFFFFFFFF:012x}"
 
 
 class Param:

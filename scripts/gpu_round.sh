@@ -40,6 +40,8 @@ for s in $STEPS; do
     cfg4csv) step cfg4csv 1000 python benchmarks/bench_csv_pipeline.py --features 64 --rows 1.25e8 --steps 5 --warmup 2 --json-out gpurun_out/cfg4csv.json &&
              (export TMPDIR=/tmp; step cfg4csvprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/cfg4csvprof -o run --output-format csv -- python benchmarks/bench_csv_pipeline.py --features 64 --rows 1.25e8 --steps 3 --warmup 2) &&
              step cfg4csvstream 900 env DQ4ML_FILECACHE_DEVICE_BYTES=1 python benchmarks/bench_csv_pipeline.py --features 64 --rows 1.25e8 --steps 2 --warmup 2 --json-out gpurun_out/cfg4csvstream.json || exit $? ;;
+    firstprof) step firstprof 900 env DQ4ML_BENCH_FIRST_PROFILE=gpurun_out/first.prof python benchmarks/bench_csv_pipeline.py --features 64 --rows 1.25e8 --steps 1 --warmup 1 --json-out gpurun_out/firstprof.json &&
+               step firstprof_txt 120 python -c "import pstats; s=pstats.Stats('gpurun_out/first.prof'); s.sort_stats('cumulative').print_stats(70); s.sort_stats('tottime').print_stats(40)" ;;
     cfg4csvhost) step cfg4csvhost 900 env DQ4ML_BENCH_CPROFILE=gpurun_out/cfg4csv.prof python benchmarks/bench_csv_pipeline.py --features 64 --rows 1.25e8 --steps 3 --warmup 1 --json-out gpurun_out/cfg4csvhost.json &&
              step cfg4csvhost_txt 120 python -c "import pstats; pstats.Stats('gpurun_out/cfg4csv.prof').sort_stats('cumulative').print_stats(60)" ;;
     cfg4prof) step cfg4prof 900 env DQ4ML_BENCH_CPROFILE=gpurun_out/cfg4.prof python benchmarks/bench_dq_pipeline.py --steps 10 --warmup 2 ;;
