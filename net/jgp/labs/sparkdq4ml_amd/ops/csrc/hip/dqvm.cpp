@@ -38,11 +38,15 @@ std::vector<Compiled> g_mods;
 
 }  // namespace
 
+// The cache lookup and insert hold the lock; the compile itself does not, so a compile on one
+// thread (the process's hipRTC warm-up, dqvm.prewarm) never blocks another thread's launches.
 int64_t rtc_compile(const std::string& src, const std::string& entry, std::string* log) {
-  std::lock_guard<std::mutex> g(g_mu);
   const std::string key = entry + "\n" + src;
-  auto it = g_by_src.find(key);
-  if (it != g_by_src.end()) return it->second;
+  {
+    std::lock_guard<std::mutex> g(g_mu);
+    auto it = g_by_src.find(key);
+    if (it != g_by_src.end()) return it->second;
+  }
   hiprtcProgram prog;
   RTC_CHECK(hiprtcCreateProgram(&prog, src.c_str(), "dq_fused.hip", 0, nullptr, nullptr));
   const char* opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17"};
@@ -64,6 +68,12 @@ int64_t rtc_compile(const std::string& src, const std::string& entry, std::strin
   Compiled c;
   DQ_HIP_CHECK(hipModuleLoadData(&c.mod, code.data()));
   DQ_HIP_CHECK(hipModuleGetFunction(&c.fn, c.mod, entry.c_str()));
+  std::lock_guard<std::mutex> g(g_mu);
+  auto it = g_by_src.find(key);
+  if (it != g_by_src.end()) {  // another thread compiled the same source meanwhile: keep theirs
+    hipModuleUnload(c.mod);
+    return it->second;
+  }
   g_mods.push_back(c);
   const int64_t h = (int64_t)g_mods.size() - 1;
   g_by_src[key] = h;

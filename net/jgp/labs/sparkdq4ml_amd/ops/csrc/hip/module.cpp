@@ -468,7 +468,11 @@ PYBIND11_MODULE(_dq4ml_hip, m) {
   // ---- fused DQ chains: hipRTC whole-stage codegen ----------------------------------------------
   m.def("rtc_compile", [](const std::string& src, const std::string& entry) {
     std::string log;
-    int64_t h = rtc_compile(src, entry, &log);
+    int64_t h;
+    {
+      py::gil_scoped_release nogil;  // (seconds for a cold hipRTC: other Python threads keep running)
+      h = rtc_compile(src, entry, &log);
+    }
     return py::make_tuple(h, log);
   });
   m.def("rtc_launch_args", [](int64_t handle, int grid, int block, py::buffer ptrs, int64_t n, uintptr_t stream) {

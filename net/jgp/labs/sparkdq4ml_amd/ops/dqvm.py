@@ -60,6 +60,38 @@ def rtc_handle(h, plan, src: str, entry: str, slot: int = 0) -> int:
         v = hs[k] = int(h.rtc_compile(src, entry)[0])
     return v
 
+_PREWARM = []
+
+
+def prewarm() -> None:
+    """Compile a trivial kernel through hipRTC on a background thread, once per process.  A
+    process's first hipRTC compile also loads and initialises the compiler (comgr + LLVM): 0.1 s
+    on one box, ~1.8 s on another with a cold page cache (the first action of the 77 GB config-4
+    CSV, profiles/r5_first_action.md).  Started with the session, it overlaps the first action's
+    upload-bound scan instead of sitting between the scan and the DQ chain.  The native compile
+    releases the GIL and holds its cache lock only around lookups (dqvm.cpp)."""
+    if _PREWARM:
+        return
+    import atexit
+    import threading
+
+    from . import native
+
+    def run():
+        try:
+            native.hip().rtc_compile('extern "C" __global__ void dq_prewarm(int* p) { if (p) p[0] = 0; }\n',
+                                     "dq_prewarm")
+        except Exception as e:  # (a missing compiler surfaces at the first real compile)
+            from ..utils.logging import get_logger
+
+            get_logger("dqvm").debug("hipRTC prewarm failed: %s", e)
+
+    t = threading.Thread(target=run, name="dq4ml-rtc-prewarm", daemon=True)
+    _PREWARM.append(t)
+    t.start()
+    atexit.register(t.join, 60.0)  # never tear the runtime down under a compile in flight
+
+
 def _ctype(t: DataType) -> str:
     c = _CTYPE.get(type(t))
     if c is None:

@@ -239,6 +239,10 @@ class SparkSession:
             from ..parallel import comm
 
             comm.set_wire_dtype(str(conf["dq4ml.allreduceWire"]).lower())
+        if self.device.type == "cuda" and str(conf.get("dq4ml.rtc.prewarm", "true")).lower() in ("1", "true", "yes"):
+            from ..ops import dqvm
+
+            dqvm.prewarm()  # hipRTC's first compile loads the compiler: off the first action's path
         self.udf = UDFRegistration(self)
         self.catalog = Catalog()
         self._stopped = False

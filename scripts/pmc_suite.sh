@@ -33,6 +33,6 @@ for w in ${PMC_SET:-wide tall span cut lsq}; do
     cut) run cut 420 python benchmarks/bench_csv_pipeline.py --features 64 --rows 1.25e8 --steps 2 --warmup 1 ;;
     span) run span 240 python scripts/csv_strings_bench.py --rows 1e7 ;;
     tall) run tall 240 python bench.py --steps 10 --warmup 3 ;;
-    wide) run wide 240 env N=2e6 D=4096 EB=8 REPS=2 python scripts/wide_bench.py ;;
+    wide) (export N=2e6 D=4096 EB=8 REPS=2; run wide 240 python scripts/wide_bench.py) || exit $? ;;  # (no env hop after --)
   esac
 done
