@@ -169,7 +169,47 @@ def _opt_args(opts):
                 null_value=o.get("null_value", ""), strict=bool(o.get("strict", False)))
 
 
-def _scan_chunk(h, buf, n: int, trailing: bool, ncols: int, sep: str, dev, hint=None, opts=None, base: int = 0):
+MIN_RESIDENT_CHUNK = 1 << 30  # chunk floor of a scan over HBM-resident bytes (bounds per-chunk outputs only)
+
+
+class _Planes:
+    """Shared column storage of a multi-chunk eager scan: every chunk's parse writes its rows at a
+    running offset of ONE allocation per column, so the table's columns are views of these planes
+    -- no per-chunk allocations and no concatenation (which read and wrote every parsed byte once
+    more and held two copies at the peak: 2 x 65 GB for the 77 GB config-4 CSV).  Sized at the
+    first chunk from its line density over the whole input (+3 %); a chunk that does not fit
+    gets its own planes and the table falls back to concatenating."""
+
+    def __init__(self, kinds, total_bytes: int, dev):
+        self.kinds, self.total, self.dev = kinds, total_bytes, dev
+        self.cols = None
+        self.off = 0
+        self.whole = True  # every chunk so far landed in the planes
+
+    def take(self, nlines: int, chunk_bytes: int):
+        """Views for the next ``nlines`` rows, or None (the chunk allocates its own)."""
+        if self.cols is None:
+            cap = int(nlines * (self.total / max(1, chunk_bytes)) * 1.03) + 4096
+            self.cols = [torch.empty(cap, dtype=dt, device=self.dev) for _, dt in self.kinds]
+        if not self.whole or self.off + max(nlines, 1) > self.cols[0].numel():
+            self.whole = False
+            return None
+        o = self.off
+        self.off += nlines
+        return [c[o:o + max(nlines, 1)] for c in self.cols]
+
+
+class _Shared(list):
+    """The chunks' parse outputs (a list, as everywhere) whose column planes are consecutive rows
+    of ``planes`` (:class:`_Planes`): ``_finish`` takes each column as one view."""
+
+    def __init__(self, parts, planes):
+        super().__init__(parts)
+        self.planes = planes
+
+
+def _scan_chunk(h, buf, n: int, trailing: bool, ncols: int, sep: str, dev, hint=None, opts=None, base: int = 0,
+                planes: "Optional[_Planes]" = None):
     """K1 (line ends) + K2 (parse, type masks, null / empty-line counts) over one device byte
     buffer; no host sync except the line count.  Returns (nlines, per-column planes, valid
     [ncols, m], keep [m], stats, base) — stats as documented at ``csv_parse`` (csv_scan.h); ``base``:
@@ -194,7 +234,9 @@ def _scan_chunk(h, buf, n: int, trailing: bool, ncols: int, sep: str, dev, hint=
     # one exact-size allocation per column: a column IS its plane (no copy, and no other
     # column's storage kept alive by it) — f64, or the hinted type (see scan_device)
     kinds = [_KIND.get(t, (0, torch.float64)) for t in (hint or [CT_DOUBLE] * ncols)]
-    dcols = [torch.empty(m, dtype=dt, device=dev) for _, dt in kinds]
+    dcols = planes.take(nlines, n) if planes is not None else None
+    if dcols is None:
+        dcols = [torch.empty(m, dtype=dt, device=dev) for _, dt in kinds]
     ptrs = _h2d(np.array([t.data_ptr() for t in dcols] + [k for k, _ in kinds], dtype=np.int64), dev)
     valid = torch.empty(ncols, m, dtype=torch.bool, device=dev)
     keep = torch.empty(m, dtype=torch.bool, device=dev)
@@ -252,24 +294,26 @@ def _finish(parts, types, st, dev, hinted=False, data=None, opts=None, check=Non
             fields.append(StructField(f"_c{c}", StringType(), True))
             cols.append(DeviceStringColumn(spans, vv, data, opts, check=check, dbuf=dbuf))
             continue
-        vals_l = []
-        for _, (nlines, dcols, _, _, _, _) in live:
-            d = dcols[c][:nlines]
+        def typed(d):
             if hinted:  # stored as the column's type already
-                pass
-            elif t == CT_INT:
-                d = d.to(torch.int32)
-            elif t in (CT_LONG, CT_TIMESTAMP):
-                d = d.to(torch.int64)
-            elif t == CT_BOOL:
-                d = d != 0
-            vals_l.append(d)
+                return d
+            if t == CT_INT:
+                return d.to(torch.int32)
+            if t in (CT_LONG, CT_TIMESTAMP):
+                return d.to(torch.int64)
+            if t == CT_BOOL:
+                return d != 0
+            return d
         dt = {CT_INT: IntegerType(), CT_LONG: LongType(), CT_BOOL: BooleanType(),
               CT_TIMESTAMP: TimestampType()}.get(t, DoubleType())
-        if vals_l:
-            vals = torch.cat(vals_l) if len(vals_l) > 1 else vals_l[0]
+        if isinstance(parts, _Shared) and total:  # the chunks wrote consecutive rows of one plane
+            vals = typed(parts.planes.cols[c][:total])
         else:
-            vals = torch.empty(0, dtype=dt.torch_dtype, device=dev)
+            vals_l = [typed(dcols[c][:nlines]) for _, (nlines, dcols, _, _, _, _) in live]
+            if vals_l:
+                vals = torch.cat(vals_l) if len(vals_l) > 1 else vals_l[0]
+            else:
+                vals = torch.empty(0, dtype=dt.torch_dtype, device=dev)
         vv = None
         if int(st[:, 2 + c].sum()):  # null fields in this column: materialize its validity
             valid_l = [p[2][c, :p[0]] for _, p in live]
@@ -417,20 +461,25 @@ def scan_device(data, sep: str = ",", infer: bool = True, device=None, ncols: Op
         # no staging, no H2D; chunking only bounds the per-chunk parse outputs
         if device_data.numel() != n:
             raise ValueError("scan_device: device_data does not match data")
-        cb = max(int(chunk_bytes or n), 1 << 30)
+        cb = max(int(chunk_bytes or n), MIN_RESIDENT_CHUNK)
         bounds = chunk_bounds(data, cb) if n > cb else [0, n]
         parts = []
         pending = list(device_ready or [])
         cur = torch.cuda.current_stream(dev)
         # (a piece's ``wait(stream)``: a torch event, or a runtime.filecache._Piece whose uploader
         # thread may not have enqueued the DMA yet -- then the host blocks until it has)
+        kinds = [_KIND.get(t, (0, torch.float64)) for t in (hint or [CT_DOUBLE] * ncols)]
+        # (string spans are chunk-relative: their columns keep the per-chunk form)
+        planes = _Planes(kinds, n, dev) if len(bounds) > 2 and all(k != 4 for k, _ in kinds) else None
         for s, e in zip(bounds, bounds[1:]):
             while pending and pending[0][0] < e:  # pieces wholly before this chunk's end
                 pending.pop(0)[1].wait(cur)
             if pending:  # the piece holding the chunk's last bytes
                 pending[0][1].wait(cur)
             trailing = data[e - 1] not in (10, 13)
-            parts.append(_scan_chunk(h, device_data[s:e], e - s, trailing, ncols, sep, dev, hint, opts, s))
+            parts.append(_scan_chunk(h, device_data[s:e], e - s, trailing, ncols, sep, dev, hint, opts, s, planes))
+        if planes is not None and planes.whole:
+            parts = _Shared(parts, planes)
         for _, ev in pending:
             ev.wait(cur)
     elif chunk_bytes is None or n <= chunk_bytes:

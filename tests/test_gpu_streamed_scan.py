@@ -123,3 +123,37 @@ def test_first_upload_in_pieces_is_exact(spark, tmp_path, monkeypatch, mapped):
     df2 = spark.read().format("csv").option("inferSchema", "true").load(p)
     ref = np.array([list(r) for r in df2.collect()], dtype=np.float64)
     assert got.shape == (50_000, 7) and np.array_equal(got, ref)
+
+
+@pytest.mark.parametrize("hinted", [False, True])
+def test_resident_multichunk_scan_writes_shared_planes(spark, tmp_path, monkeypatch, hinted):
+    """A resident input scanned in many chunks: every chunk parses straight into one plane per
+    column (csvscan._Planes, no per-chunk allocation, no concatenation); the table equals the
+    one-chunk scan exactly, for the inferring scan and the hinted (typed) re-scan."""
+    import csv_synth
+
+    from net.jgp.labs.sparkdq4ml_amd.ops import csvscan
+    from net.jgp.labs.sparkdq4ml_amd.runtime import filecache
+
+    p = str(tmp_path / "m.csv")
+    csv_synth.write_wide_csv(p, 40_000, 5, seed=9, device="cuda", keep=False, y0=60.0, chunk=1 << 16)
+
+    def read():
+        df = spark.read().format("csv").option("inferSchema", "true").load(p)
+        if hinted:  # a second load of the same bytes: the typed (hinted) device scan
+            df = spark.read().format("csv").option("inferSchema", "true").load(p)
+        return np.array([list(r) for r in df.collect()], dtype=np.float64), df
+
+    ref, _ = read()
+    filecache.clear()
+    monkeypatch.setattr(csvscan, "MIN_RESIDENT_CHUNK", 1 << 18)  # ~8 chunks
+    seen = []
+    orig = csvscan._finish
+
+    def spy(parts, *a, **k):
+        seen.append(isinstance(parts, csvscan._Shared) and len(parts))
+        return orig(parts, *a, **k)
+    monkeypatch.setattr(csvscan, "_finish", spy)
+    got, _ = read()
+    assert seen and all(x and x > 2 for x in seen), seen  # every eager scan took the shared planes
+    assert np.array_equal(got, ref)
