@@ -1,29 +1,38 @@
 #!/usr/bin/env python3
 """Markdown row per kernel from the two rocprofv3 --pmc passes of ``scripts/pmc_suite.sh``:
 dispatch time, effective clock, HBM-side bytes (FETCH_SIZE doubled: gfx950 reports half the bytes
-of a wide streaming read, MI355X_MICROARCH.md §HBM), bytes per row, % of the 6.3 TB/s measured HBM
-peak, L2 hit rate, MFMA busy share, VALU instructions per row.
+of a wide streaming read -- the headline Gram's 6.8 GB per dispatch reads back as 3.4 GB -- see
+MI355X_MICROARCH.md §HBM), bytes per row, % of the 8 TB/s HBM3E peak and of the ~6.3 TB/s a
+streaming kernel sustains, L2 hit rate, fabric and L1->L2 request bytes, MFMA busy share, VALU
+wave-instructions per row.
 
-    python scripts/pmc_report.py gpurun_out/pmc_lsq_a gpurun_out/pmc_lsq_b --kernel lsq_qn_kernel --rows 1e6
+Dispatches shorter than ``--min-ms`` are left out (the data-parallel l-bfgs enqueues a few
+evaluations past the end that return at once); counters and times are averaged over the same
+dispatches (joined by dispatch id).
+
+    python scripts/pmc_report.py gpurun_out/pmc_lsq_a gpurun_out/pmc_lsq_b --kernel lsq_qn_dp_pass --rows 1e6 --min-ms 1
 """
 import argparse
 import collections
 import csv
 import os
 
-HBM_PEAK = 6.3e12
+HBM_PEAK = 8.0e12
+HBM_SUSTAINED = 6.3e12
 
 
-def load(d, sub):
-    vals = collections.defaultdict(list)
-    durs = []
-    for r in csv.DictReader(open(os.path.join(d, "run_counter_collection.csv"))):
-        if sub in r["Kernel_Name"]:
-            vals[r["Counter_Name"]].append(float(r["Counter_Value"]))
+def load(d, sub, min_ms):
+    durs = {}
     for r in csv.DictReader(open(os.path.join(d, "run_kernel_trace.csv"))):
         if sub in r["Kernel_Name"]:
-            durs.append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9)
-    return {k: sum(v) / len(v) for k, v in vals.items()}, durs
+            t = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9
+            if t * 1e3 >= min_ms:
+                durs[r["Dispatch_Id"]] = t
+    vals = collections.defaultdict(list)
+    for r in csv.DictReader(open(os.path.join(d, "run_counter_collection.csv"))):
+        if sub in r["Kernel_Name"] and r["Dispatch_Id"] in durs:
+            vals[r["Counter_Name"]].append(float(r["Counter_Value"]))
+    return {k: sum(v) / len(v) for k, v in vals.items()}, list(durs.values())
 
 
 def main():
@@ -33,27 +42,30 @@ def main():
     ap.add_argument("--kernel", required=True)
     ap.add_argument("--rows", type=float, default=0.0, help="rows one dispatch covers (bytes / row)")
     ap.add_argument("--cus", type=int, default=256)
+    ap.add_argument("--min-ms", type=float, default=0.0)
     x = ap.parse_args()
-    va, da = load(x.a, x.kernel)
-    vb, db = load(x.b, x.kernel)
+    va, da = load(x.a, x.kernel, x.min_ms)
+    vb, db = load(x.b, x.kernel, x.min_ms)
     t = sum(da) / max(1, len(da))
-    clk = va.get("GRBM_GUI_ACTIVE", 0) / 8 / t if t else 0.0
+    cyc = va.get("GRBM_GUI_ACTIVE", 0) / 8
+    clk = cyc / t if t else 0.0
     fetch = 2 * va.get("FETCH_SIZE", 0.0) * 1024  # KiB -> B, doubled (see module doc)
     hit, miss = vb.get("TCC_HIT_sum", 0.0), vb.get("TCC_MISS_sum", 0.0)
-    cyc = va.get("GRBM_GUI_ACTIVE", 0) / 8
     out = collections.OrderedDict()
     out["kernel"] = x.kernel
     out["dispatches"] = len(da)
     out["ms"] = round(t * 1e3, 4)
     out["clock_GHz"] = round(clk / 1e9, 3)
     out["HBM_bytes"] = f"{fetch:.4g}"
-    out["HBM_TB/s"] = round(fetch / t / 1e12, 3) if t else None
-    out["%_of_6.3TB/s"] = round(100 * fetch / t / HBM_PEAK, 1) if t else None
+    out["TB/s"] = round(fetch / t / 1e12, 3) if t else None
+    out["%_of_8TB/s"] = round(100 * fetch / t / HBM_PEAK, 1) if t else None
+    out["%_of_6.3TB/s"] = round(100 * fetch / t / HBM_SUSTAINED, 1) if t else None
     if x.rows:
         out["bytes/row"] = round(fetch / x.rows, 2)
-        out["VALU_instr/row"] = round(va.get("SQ_INSTS_VALU", 0) * 64 / x.rows, 2) if "SQ_INSTS_VALU" in va else None
+        if "SQ_INSTS_VALU" in va:
+            out["VALU_wave_instr/row"] = round(va["SQ_INSTS_VALU"] / x.rows, 3)
     out["L2_hit_%"] = round(100 * hit / (hit + miss), 1) if hit + miss else None
-    out["L2_fabric_req_B"] = f"{vb.get('TCC_EA0_RDREQ_sum', 0) * 128:.4g}"
+    out["fabric_req_B"] = f"{vb.get('TCC_EA0_RDREQ_sum', 0) * 128:.4g}"
     out["L1->L2_req_B"] = f"{vb.get('TCP_TCC_READ_REQ_sum', 0) * 128:.4g}"
     if cyc and "SQ_VALU_MFMA_BUSY_CYCLES" in va:
         out["MFMA_busy_%"] = round(100 * va["SQ_VALU_MFMA_BUSY_CYCLES"] / (4 * x.cus * cyc), 1)

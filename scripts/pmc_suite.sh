@@ -31,7 +31,7 @@ for w in ${PMC_SET:-wide tall span cut lsq}; do
   case $w in
     lsq) run lsq 240 python benchmarks/bench_lbfgs.py --steps 1 --warmup 1 ;;
     cut) run cut 420 python benchmarks/bench_csv_pipeline.py --features 64 --rows 1.25e8 --steps 2 --warmup 1 ;;
-    span) run span 240 python scripts/csv_strings_bench.py --rows 1e7 ;;
+    span) run span 240 python scripts/span_bench.py --rows 1e7 ;;
     tall) run tall 240 python bench.py --steps 10 --warmup 3 ;;
     wide) (export N=2e6 D=4096 EB=8 REPS=2; run wide 240 python scripts/wide_bench.py) || exit $? ;;  # (no env hop after --)
   esac

@@ -147,6 +147,7 @@ def test_resident_multichunk_scan_writes_shared_planes(spark, tmp_path, monkeypa
     ref, _ = read()
     filecache.clear()
     monkeypatch.setattr(csvscan, "MIN_RESIDENT_CHUNK", 1 << 18)  # ~8 chunks
+    spark.conf.set("dq4ml.chunkBytes", str(1 << 18))
     seen = []
     orig = csvscan._finish
 
@@ -154,6 +155,9 @@ def test_resident_multichunk_scan_writes_shared_planes(spark, tmp_path, monkeypa
         seen.append(isinstance(parts, csvscan._Shared) and len(parts))
         return orig(parts, *a, **k)
     monkeypatch.setattr(csvscan, "_finish", spy)
-    got, _ = read()
+    try:
+        got, _ = read()
+    finally:
+        spark.conf.set("dq4ml.chunkBytes", str(256 << 20))
     assert seen and all(x and x > 2 for x in seen), seen  # every eager scan took the shared planes
     assert np.array_equal(got, ref)
