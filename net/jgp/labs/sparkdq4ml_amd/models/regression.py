@@ -24,14 +24,14 @@ import os
 import numpy as np
 import torch
 
-from ..ops import device, kernels, native
+from ..ops import device, kernels, native, scanfuse, streamfuse
 from ..ops.layout import TiledBF16
 from ..parallel import comm
 from ..sql.dataframe import DataFrame
 from ..runtime import faststream, streams
 from ..runtime.checks import defer, verify
 from ..sql.expressions import AnalysisException, ColRef, EvalContext, Expr, SparkException
-from ..sql.plan import Filter, Project, execute
+from ..sql.plan import Filter, Project, execute, prune_columns
 from ..sql.table import ColumnData
 from ..sql.types import DoubleType, VectorUDT, is_numeric
 from ..utils.logging import get_logger
@@ -165,9 +165,6 @@ def _fused_scan_stats(params, df: DataFrame):
     if sess is None or getattr(sess, "device", None) is None or sess.device.type != "cuda":
         return None
     fc, lc = _check_features_label(params, df)
-    from ..ops import scanfuse, streamfuse
-    from ..sql.plan import prune_columns
-
     if gd == "fp64":
         # an action that rebuilt a chain of the same structure over the same cached input replays
         # the lowered kernel (sql/skey.py): only the launch and its outputs are new
@@ -193,8 +190,6 @@ def _features_label(params, df: DataFrame):
     need = {fc, lc}
     if params.isSet("weightCol") and params.getOrDefault("weightCol"):
         need.add(params.getOrDefault("weightCol"))
-    from ..sql.plan import execute, prune_columns
-
     tbl = execute(prune_columns(df._plan, need), df.sparkSession)
     X = tbl.column(fc)
     y = tbl.column(lc)

@@ -37,8 +37,9 @@ void csv_stats_init(const int32_t* facts, int64_t nb, int64_t* stats, int ncols,
 // does not convert makes its record malformed (all fields null)
 void csv_parse(const uint8_t* buf, int64_t n, const void* ends, int64_t nlines, int ncols, const dq4ml_csv::CsvOpts& o,
                const int64_t* dcols, uint8_t* valid, uint8_t* keep, int64_t* stats, hipStream_t st);
-// string column (kind-4 spans into buf[0, nbuf)) == lit[0, L): out 1 / 0, or 2 for a raw field
+// string column (kind-4 spans into buf[0, nbuf)) == lit[0, L): out 1 / 0; a raw (quoted /
+// escaped) field compares its unescaped text (quote / escape bytes, -1: none)
 void csv_span_eq(const uint8_t* buf, int64_t nbuf, const int64_t* spans, int64_t n, const uint8_t* lit, int L,
-                 uint8_t* out, hipStream_t st);
+                 int quote, int escape, uint8_t* out, hipStream_t st);
 
 }  // namespace dq4ml

@@ -433,19 +433,61 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   }
 }
 
-// A device string column (kind-4 spans into buf) compared with a constant: 1 equal, 0 not equal,
-// 2 undetermined -- a raw (quoted / escaped) field, whose text only the host tokenizer builds
+// A raw (quoted / escaped) field's text compared with the literal as it is produced: the host
+// tokenizer's state machine for one field (ops/csrc/host/csv.cpp split_record with no separator,
+// so a NUL outside quotes ends the field), emitting bytes straight into the comparison.
+__device__ __forceinline__ uint8_t raw_field_eq(const uint8_t* __restrict__ p, int64_t n,
+                                                const uint8_t* __restrict__ lit, int L, int quote, int escape) {
+  bool in_q = false, was_q = false;
+  int k = 0;  // bytes of the field's text produced (and matched) so far
+  for (int64_t i = 0; i < n; ++i) {
+    int c = p[i], e = -1;  // e: the byte this step appends to the text, if any
+    if (in_q) {
+      if (c == escape && escape != quote && i + 1 < n && (p[i + 1] == quote || p[i + 1] == escape)) {
+        e = p[++i];
+      } else if (c == quote) {
+        if (i + 1 < n && p[i + 1] == quote) {
+          e = quote;
+          ++i;
+        } else {
+          in_q = false;
+        }
+      } else {
+        e = c;
+      }
+    } else if (c == 0) {
+      break;  // the separator of a one-field record
+    } else if (c == quote && k == 0 && !was_q) {
+      in_q = was_q = true;
+    } else if (c == escape && escape != quote && i + 1 < n && p[i + 1] == quote) {
+      e = p[++i];
+    } else {
+      e = c;
+    }
+    if (e >= 0) {
+      if (k >= L || lit[k] != (uint8_t)e) return 0;
+      ++k;
+    }
+  }
+  return k == L ? 1 : 0;
+}
+
+// A device string column (kind-4 spans into buf) compared with a constant: 1 equal, 0 not equal.
+// Plain fields compare their bytes; raw (quoted / escaped) ones their unescaped text, produced on
+// the fly -- no field's text is ever built on the host.
 __global__ __launch_bounds__(256) void csv_span_eq_kernel(const uint8_t* __restrict__ buf, int64_t nbuf,
                                                           const int64_t* __restrict__ spans, int64_t n,
-                                                          const uint8_t* __restrict__ lit, int L,
-                                                          uint8_t* __restrict__ out) {
+                                                          const uint8_t* __restrict__ lit, int L, int quote,
+                                                          int escape, uint8_t* __restrict__ out) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t v = spans[i];
     const int64_t fs = v >> 25, len = v & 0xFFFFFF;
     uint8_t r;
-    if ((v >> 24) & 1) {
-      r = 2;
-    } else if (len != L || fs < 0 || fs + len > nbuf) {
+    if (fs < 0 || fs + len > nbuf) {
+      r = 0;
+    } else if ((v >> 24) & 1) {
+      r = raw_field_eq(buf + fs, len, lit, L, quote, escape);
+    } else if (len != L) {
       r = 0;
     } else {
       r = 1;
@@ -458,11 +500,11 @@ __global__ __launch_bounds__(256) void csv_span_eq_kernel(const uint8_t* __restr
 }  // namespace
 
 void csv_span_eq(const uint8_t* buf, int64_t nbuf, const int64_t* spans, int64_t n, const uint8_t* lit, int L,
-                 uint8_t* out, hipStream_t st) {
+                 int quote, int escape, uint8_t* out, hipStream_t st) {
   if (n <= 0) return;
   int64_t g = (n + 255) / 256;
   if (g > 65536) g = 65536;
-  hipLaunchKernelGGL(csv_span_eq_kernel, dim3(g), dim3(256), 0, st, buf, nbuf, spans, n, lit, L, out);
+  hipLaunchKernelGGL(csv_span_eq_kernel, dim3(g), dim3(256), 0, st, buf, nbuf, spans, n, lit, L, quote, escape, out);
   DQ_HIP_CHECK(hipGetLastError());
 }
 

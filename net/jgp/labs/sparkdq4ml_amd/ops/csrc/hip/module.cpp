@@ -429,15 +429,19 @@ PYBIND11_MODULE(_dq4ml_hip, m) {
 
   // ---- CSV scan (K1/K2) ------------------------------------------------------------------------
   m.def("csv_count_blocks", &csv_count_blocks);
-  m.def("csv_span_eq", [](uintptr_t buf, int64_t nbuf, uintptr_t spans, int64_t n, uintptr_t lit, int L, uintptr_t out,
-                          uintptr_t stream) {
-    csv_span_eq(P<const uint8_t>(buf), nbuf, P<const int64_t>(spans), n, P<const uint8_t>(lit), L, P<uint8_t>(out),
-                as_stream(stream));
+  m.def("csv_span_eq", [](uintptr_t buf, int64_t nbuf, uintptr_t spans, int64_t n, uintptr_t lit, int L, int quote,
+                          int escape, uintptr_t out, uintptr_t stream) {
+    csv_span_eq(P<const uint8_t>(buf), nbuf, P<const int64_t>(spans), n, P<const uint8_t>(lit), L, quote, escape,
+                P<uint8_t>(out), as_stream(stream));
   });
   m.def("csv_line_ends", [](uintptr_t buf, int64_t n, uintptr_t counts, uintptr_t ends, uintptr_t stream, int sep,
                             uintptr_t facts) {
     csv_line_ends(P<const uint8_t>(buf), n, P<int64_t>(counts), P<void>(ends), as_stream(stream), sep,
                   P<int32_t>(facts));
+  });
+  m.def("memset_async", [](uintptr_t p, int v, int64_t nbytes, uintptr_t stream) {
+    // (an action's zeroed scratch without torch's fill dispatch: one runtime call)
+    if (nbytes > 0) DQ_HIP_CHECK(hipMemsetAsync(P<void>(p), v, (size_t)nbytes, as_stream(stream)));
   });
   m.def("csv_stats_init", [](uintptr_t facts, int64_t nb, uintptr_t stats, int ncols, uintptr_t stream) {
     csv_stats_init(P<const int32_t>(facts), nb, P<int64_t>(stats), ncols, as_stream(stream));

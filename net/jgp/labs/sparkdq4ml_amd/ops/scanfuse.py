@@ -30,6 +30,10 @@ from typing import Optional
 
 import torch
 
+from ..runtime import faststream
+from ..runtime.checks import defer
+from ..utils import tracing
+
 __all__ = ["kernel_source", "ENTRY", "WINDOW", "head_bytes", "STATS"]
 
 ENTRY = "dq_scan_fused"
@@ -694,7 +698,6 @@ def _launch(cp, nodes, rel, extra: dict, own_stream: bool = True):
     scan stream, compute stream) after checking a raised UDF error.  ``own_stream``: on the
     scan side stream (else on the compute stream, in order with the caller's work)."""
     from . import dqvm, native
-    from ..runtime import faststream
 
     f = rel.fused
     h = native.hip()
@@ -724,8 +727,6 @@ def _launch(cp, nodes, rel, extra: dict, own_stream: bool = True):
             extra["gpart"] = scalars["gpart"] = z[no + 1:].view(torch.float64).view(nb, gw)
         ptr_list, outs, sel_out = cp.bind(nalloc, dev, scalars, err)
         handle = dqvm.rtc_handle(h, cp, cp.src, ENTRY)
-        from ..utils import tracing
-
         with tracing.span("csv_scan_dq_fused"):
             dqvm.launch(h, handle, nb, ptr_list, n, stream)
     tracing.add_rows("csv_scan_dq_fused", nalloc)
@@ -752,7 +753,6 @@ def _udf_error_check(nodes, err):
     the action stays asynchronous and the SparkException surfaces with the first host read of
     its results — the job fails exactly as Spark's does, without a sync per action.  ``nodes``:
     the chain, or its precomputed ``_raise_message``."""
-    from ..runtime.checks import defer
     from ..sql.expressions import SparkException
 
     msg = nodes if isinstance(nodes, str) else _raise_message(nodes)
@@ -760,8 +760,6 @@ def _udf_error_check(nodes, err):
 
 
 def _fact_check(rel, vflag):
-    from ..runtime.checks import defer
-
     # safety net: the earlier scan's facts (types, null-free columns, line count) are re-verified
     # by the kernel; a disagreement surfaces with the first host read of any output
     return defer(vflag, lambda: RuntimeError(
@@ -924,7 +922,6 @@ def window_fold(gpart, side):
     """The per-window partials [rows, gw] -> the flat gram_stats layout [n, Σw, Σw², Σwy, Σwy²,
     Σwx, Σwxy, packed-upper Σwxx] (unit weights: Σw = Σw² = n), fixed order, on ``side``."""
     from . import native
-    from ..runtime import faststream
 
     with faststream.use(side):
         flat = torch.empty(gpart.shape[1] + 2, dtype=torch.float64, device=gpart.device)
@@ -933,13 +930,24 @@ def window_fold(gpart, side):
     return flat
 
 
+_PLAN_CLASSES = []
+
+
+def _plan_classes():
+    """(CsvScanRelation, Filter, Project), imported once (sql.plan imports this package lazily)."""
+    if not _PLAN_CLASSES:
+        from ..sql.plan import CsvScanRelation, Filter, Project
+
+        _PLAN_CLASSES.extend((CsvScanRelation, Filter, Project))
+    return _PLAN_CLASSES
+
+
 def replay(key, plan, session) -> Optional["FusedGram"]:
     """The remembered route of ``key`` launched over this action's leaf relation, or None."""
     r = _ROUTES.get(key) if key is not None else None
     if r is None or r.conf != session.conf._conf:
         return None
-    from ..sql.plan import CsvScanRelation, Filter, Project
-
+    CsvScanRelation, Filter, Project = _plan_classes()
     p = plan
     while isinstance(p, (Project, Filter)):
         if p._memo is not None:
@@ -1012,14 +1020,12 @@ class _GramLaunch:
 
     def __call__(self):
         """(flat statistics, err, vflag) of one launch on the current stream."""
-        from ..runtime import faststream
-        from ..utils import tracing
-
         di = faststream.dev_index(self.dev)
-        z = torch.zeros(self.words, dtype=torch.int64, device=self.dev)
+        z = torch.empty(self.words, dtype=torch.int64, device=self.dev)
         arr = self.tmpl.copy()
         arr[self.zi] = self.zo + z.data_ptr()
         stream = faststream.raw(di)
+        self.h.memset_async(z.data_ptr(), 0, 8 * self.words, stream)
         with tracing.span("csv_scan_dq_fused"):
             self.h.rtc_launch_args(self.handle, self.nb, 256, arr, self.n, stream)
         flat = torch.empty(self.gw + 2, dtype=torch.float64, device=self.dev)

@@ -35,7 +35,9 @@ def defer(flag: torch.Tensor, make_exc: Callable[[], BaseException]) -> Optional
         if bool(flag.reshape(-1).any()):
             raise make_exc()
         return None
-    return DeviceCheck(flag.reshape(-1)[:1].to(torch.bool), make_exc)
+    # a view of the flag, kept as it is (no conversion kernel per deferred check: one per fit of
+    # a rebuilt lab action); verify() reads every pending flag, any dtype, in one copy
+    return DeviceCheck(flag.reshape(-1)[:1], make_exc)
 
 
 def verify(checks: Iterable[Optional[DeviceCheck]]) -> None:
@@ -43,7 +45,7 @@ def verify(checks: Iterable[Optional[DeviceCheck]]) -> None:
     cs: List[DeviceCheck] = [c for c in checks if c is not None]
     if not cs:
         return
-    flags = torch.cat([c.flag for c in cs]).cpu().tolist()
+    flags = torch.cat([c.flag for c in cs]).cpu().tolist()  # (cat promotes mixed flag dtypes)
     for c, f in zip(cs, flags):
         if f:
             raise c.make_exc()

@@ -236,9 +236,10 @@ class DeviceStringColumn(ColumnData):
 
     def eq_literal(self, lit: str) -> Optional[torch.Tensor]:
         """``column = lit`` on the device (bool [n]; validity is the column's), without building
-        the strings: the spans' bytes in HBM are compared with the literal's UTF-8 bytes; only raw
-        (quoted / escaped) fields get their text built on the host.  None when the column has no
-        HBM-resident bytes or a whitespace trim applies (then the strings are compared on the host)."""
+        the strings: the spans' bytes in HBM are compared with the literal's UTF-8 bytes, and a raw
+        (quoted / escaped) field's unescaped text as the kernel produces it (``csv_span_eq``: the
+        host tokenizer's rules).  None when the column has no HBM-resident bytes or a whitespace
+        trim applies (then the strings are compared on the host)."""
         if self._vals is not None or self.dbuf is None or self.opts.get("trim_lead") or self.opts.get("trim_trail"):
             return None
         from ..ops import native
@@ -247,18 +248,16 @@ class DeviceStringColumn(ColumnData):
         b = lit.encode("utf-8")
         lt = torch.tensor(list(b) or [0], dtype=torch.uint8).to(dev, non_blocking=True)
         out = torch.empty(self.n, dtype=torch.uint8, device=dev)
+        # (the host tokenizer's option bytes: an empty quote disables quoting, the escape defaults
+        # to a backslash -- _dq4ml_host.csv_strings)
+        q, e = self.opts.get("quote", '"'), self.opts.get("escape", "\\")
+        qb, eb = (ord(q[0]) if q else 0), (ord(e[0]) if e else 92)
+        if qb > 127 or eb > 127:
+            return None  # a quote / escape outside ASCII (several UTF-8 bytes): the host compares
         native.hip().csv_span_eq(self.dbuf.data_ptr(), self.dbuf.numel(), self.spans.data_ptr(), self.n,
-                                 lt.data_ptr(), len(b), out.data_ptr(), torch.cuda.current_stream(dev).cuda_stream)
-        eq = out == 1
-        raw = torch.nonzero(out == 2).flatten()
-        if raw.numel():  # raw fields: the host builds just their text
-            sub = self.index(raw)
-            sub.dbuf = None
-            vals = sub.values
-            hits = [i for i, v in enumerate(vals) if v == lit]
-            if hits:
-                eq[raw[torch.tensor(hits, dtype=torch.long, device=raw.device)]] = True
-        return eq
+                                 lt.data_ptr(), len(b), qb, eb, out.data_ptr(),
+                                 torch.cuda.current_stream(dev).cuda_stream)
+        return out == 1
 
 
 class Table:

@@ -176,6 +176,11 @@ def test_string_equality_filter_runs_on_the_device(tmp_path, lit):
     p = tmp_path / "eq.csv"
     p.write_bytes(_mixed_csv(20_000, seed=4))
 
+    from net.jgp.labs.sparkdq4ml_amd.sql.table import DeviceStringColumn
+
+    built = []
+    real = DeviceStringColumn.values
+
     def ids(threshold, check_lazy=False):
         spark = _session(threshold)
         df = spark.read().option("inferSchema", "true").csv(str(p))
@@ -187,6 +192,12 @@ def test_string_equality_filter_runs_on_the_device(tmp_path, lit):
         spark.stop()
         return got, neq
 
-    dev = ids("0", check_lazy=True)
+    # no string of any field -- raw (quoted / escaped) ones included -- is built on the host
+    DeviceStringColumn.values = property(lambda self: built.append(1) or real.fget(self), real.fset)
+    try:
+        dev = ids("0", check_lazy=True)
+    finally:
+        DeviceStringColumn.values = real
+    assert not built
     host = ids(str(1 << 40))
     assert dev == host
