@@ -197,6 +197,8 @@ for s in $STEPS; do
     oversub) for r in 1 2; do for m in 1 2 4; do
             step oversub_${m}_s${r} 300 env DQ4ML_GRAM_OVERSUB=$m python bench.py --steps 200 --warmup 20 --rows 1.25e7 &&
             step oversub_${m}_h${r} 300 env DQ4ML_GRAM_OVERSUB=$m python bench.py --steps 30 --warmup 5 || exit $?; done; done ;;
+    csvshard) step csvshard 600 python benchmarks/bench_csv_pipeline.py --rows 1.25e7 --steps 200 --warmup 20 --json-out gpurun_out/csvshard.json &&
+              step csvshard2 600 python benchmarks/bench_csv_pipeline.py --rows 1.25e7 --steps 200 --warmup 20 --json-out gpurun_out/csvshard2.json || exit $? ;;
     x4) step lbfgs1 900 env DQ4ML_BENCH_AB=0 python benchmarks/bench_lbfgs.py --steps 3 --warmup 1 --json-out gpurun_out/lbfgs1.json &&
         step lbfgsdp 900 env DQ4ML_BENCH_AB=0 DQ4ML_FORCE_COLLECTIVES=1 python benchmarks/bench_lbfgs.py --steps 3 --warmup 1 --json-out gpurun_out/lbfgsdp.json &&
         step lbfgs1b 900 env DQ4ML_BENCH_AB=0 python benchmarks/bench_lbfgs.py --steps 3 --warmup 1 --json-out gpurun_out/lbfgs1b.json || exit $? ;;

@@ -35,11 +35,22 @@ def main(argv=None):
     df = spark.read().option("inferSchema", "true").csv(path)
     want = df.filter(col("_c1") == "word").count()  # warm-up (and the kernel's first launch)
     torch.cuda.synchronize()
+    prof = None
+    if os.environ.get("SPAN_PROFILE"):  # host-side cProfile of the timed actions
+        import cProfile
+
+        prof = cProfile.Profile()
+        prof.enable()
     t0 = time.perf_counter()
     for _ in range(a.reps):
         got = df.filter(col("_c1") == "word").count()
     torch.cuda.synchronize()
     ms = (time.perf_counter() - t0) * 1e3 / a.reps
+    if prof is not None:
+        import pstats
+
+        prof.disable()
+        pstats.Stats(prof).sort_stats("cumulative").print_stats(35)
     print(json.dumps({"rows": n, "matches": int(got), "ms_per_action": round(ms, 4), "csv_bytes": os.path.getsize(path),
                       "check": int(got) == int(want)}), flush=True)
     spark.stop()
