@@ -272,8 +272,8 @@ class LinearRegression(_LRParams):
                 caller = faststream.current(faststream.dev_index(df.sparkSession.device))
                 with faststream.use(pipe):
                     flat, checks = self._wls_stats(df, tbl, X, y, d, overlap, caller)
-                    _rank_health(df)
-                    model = self._wls_finish(df, flat, d, checks, overlap)
+                    hc = _rank_health(df)
+                    model = self._wls_finish(df, flat, d, checks + ([hc] if hc is not None else []), overlap)
                 plan = self.__dict__.pop("_tiled_plan", None)
                 if plan is not None and model.__dict__.get("_pending") is not None:
                     # kept by the DataFrame (its lifetime bounds the plan's tensors), per estimator;
@@ -286,8 +286,8 @@ class LinearRegression(_LRParams):
                 return model
             flat, checks = self._wls_stats(df, tbl, X, y, d, overlap)
             self.__dict__.pop("_tiled_plan", None)
-        _rank_health(df)
-        return self._wls_finish(df, flat, d, checks, overlap)
+        hc = _rank_health(df)  # (a deferred flag: read with the fit's first host read)
+        return self._wls_finish(df, flat, d, checks + ([hc] if hc is not None else []), overlap)
 
     def _wls_stats(self, df, tbl, X, y, d, overlap, caller=None):
         checks = _fit_checks(self, tbl, X)
@@ -501,10 +501,12 @@ def _rank_health(df):
     sess = getattr(df, "sparkSession", None)
     mode = str(sess.conf.get("dq4ml.healthCheck", "once")).lower() if sess is not None else "once"
     if mode == "never" or (mode == "once" and getattr(sess, "_health_checked", False)):
-        return
-    comm.health_check(float(sess.conf.get("dq4ml.healthCheckTimeout", "30")) if sess is not None else 30.0)
+        return None
+    chk = comm.health_check(float(sess.conf.get("dq4ml.healthCheckTimeout", "30")) if sess is not None else 30.0,
+                            deferred=True)
     if sess is not None:
         sess._health_checked = True
+    return chk
 
 
 def _async_conf(df) -> bool:

@@ -124,25 +124,36 @@ def shutdown():
         dist.destroy_process_group()
 
 
-def health_check(timeout_s: float = 30.0):
+def health_check(timeout_s: float = 30.0, deferred: bool = False):
     """Rank-health barrier: every rank contributes 1; raises :class:`RankFailure` (naming the
-    missing ranks where the backend can tell) instead of blocking forever on a dead peer."""
+    missing ranks where the backend can tell) instead of blocking forever on a dead peer.
+    ``deferred`` (RCCL): a peer that never answers still raises here (the wait's timeout), but the
+    sum is not read back -- the returned ``runtime.checks`` flag raises at the fit's first host
+    read, so an asynchronous fit stays free of host syncs."""
     if not collectives_active():
-        return
+        return None
     if dist.get_backend() == "gloo":
         try:
             dist.monitored_barrier(timeout=datetime.timedelta(seconds=timeout_s), wait_all_ranks=True)
         except RuntimeError as e:
             raise RankFailure(f"rank health check failed: {e}") from e
-        return
+        return None
     x = torch.ones(1, device=torch.device("cuda", torch.cuda.current_device()))
     work = dist.all_reduce(x, async_op=True)
     try:
         ok = work.wait(timeout=datetime.timedelta(seconds=timeout_s))
     except RuntimeError as e:
         raise RankFailure(f"rank health check failed: {e}") from e
-    if ok is False or int(x.item()) != world_size():
+    if ok is False:
+        raise RankFailure("rank health check: the all-reduce did not complete")
+    if deferred:
+        from ..runtime.checks import defer
+
+        n = world_size()
+        return defer(x != float(n), lambda: RankFailure(f"rank health check: the all-reduce of ones did not sum to {n}"))
+    if int(x.item()) != world_size():
         raise RankFailure(f"rank health check: {int(x.item())} of {world_size()} ranks answered")
+    return None
 
 
 def _fault(point: str):
