@@ -95,13 +95,16 @@ def test_streamed_relation_other_actions_scan_eagerly(spark, tmp_path, monkeypat
     assert len(rows) == 3 and len(rows[0]) == 9
 
 
-@pytest.mark.parametrize("mapped", [False, True])
-def test_first_upload_in_pieces_is_exact(spark, tmp_path, monkeypatch, mapped):
+@pytest.mark.parametrize("mapped,chunked", [(False, False), (True, False), (True, True)])
+def test_first_upload_in_pieces_is_exact(spark, tmp_path, monkeypatch, mapped, chunked):
     """runtime.filecache first upload in many pieces (pinned: events on the side stream; mapped:
-    the uploader thread's bounce buffers) consumed progressively by the first scan: the resident
-    bytes equal the file and the scan equals a fresh host-staged one."""
+    the uploader thread's bounce buffers) consumed progressively by the first scan -- with
+    ``chunked``, scan chunks (256 KiB) smaller than the pieces (1 MiB), so each chunk waits for the
+    piece holding its last byte: the resident bytes equal the file and the scan equals a fresh
+    host-staged one."""
     import csv_synth
 
+    from net.jgp.labs.sparkdq4ml_amd.ops import csvscan
     from net.jgp.labs.sparkdq4ml_amd.runtime import filecache
 
     p = str(tmp_path / "u.csv")
@@ -110,8 +113,14 @@ def test_first_upload_in_pieces_is_exact(spark, tmp_path, monkeypatch, mapped):
     monkeypatch.setattr(filecache, "_UPLOAD_PIECE", 1 << 20)  # ~ size / 1 MiB pieces
     if mapped:
         monkeypatch.setattr(filecache, "MAX_BYTES", size // 2)
-    df = spark.read().format("csv").option("inferSchema", "true").load(p)
-    got = np.array([list(r) for r in df.collect()], dtype=np.float64)
+    if chunked:
+        monkeypatch.setattr(csvscan, "MIN_RESIDENT_CHUNK", 1 << 18)
+        spark.conf.set("dq4ml.chunkBytes", str(1 << 18))
+    try:
+        df = spark.read().format("csv").option("inferSchema", "true").load(p)
+        got = np.array([list(r) for r in df.collect()], dtype=np.float64)
+    finally:
+        spark.conf.set("dq4ml.chunkBytes", str(256 << 20))
     entries = list((filecache._mapped if mapped else filecache._cache).values())
     assert len(entries) == 1 and len(entries[0]._dev) == 1
     resident = next(iter(entries[0]._dev.values()))
