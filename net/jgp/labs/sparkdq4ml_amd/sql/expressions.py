@@ -274,7 +274,23 @@ class BinOp(Expr):
         return f"({self.left.sql_name()} {op} {self.right.sql_name()})"
 
     def eval(self, ctx):
-        l, r = self.left.eval(ctx), self.right.eval(ctx)
+        l = r = None
+        if self.op in ("=", "==", "!=", "<>"):
+            # a column against a string constant: a device string column compares in HBM, and the
+            # constant is never expanded to a row-length list of Python strings
+            if isinstance(self.right, Lit) and isinstance(self.right.value, str):
+                l = self.left.eval(ctx)
+                eq = _device_string_eq(self, l, None)
+            elif isinstance(self.left, Lit) and isinstance(self.left.value, str):
+                r = self.right.eval(ctx)
+                eq = _device_string_eq(self, None, r)
+            else:
+                eq = None
+            if eq is not None:
+                c = l if l is not None else r
+                return ColumnData(BooleanType(), eq if self.op in ("=", "==") else ~eq, c.valid)
+        l = self.left.eval(ctx) if l is None else l
+        r = self.right.eval(ctx) if r is None else r
         schema = ctx.table.schema
         if self.op in ("and", "or"):
             lv = l.values.to(torch.bool)
@@ -290,7 +306,8 @@ class BinOp(Expr):
                 val = lv | rv
                 valid = (lm & rm) | true_l | true_r
                 val = (val & lm & rm) | true_l | true_r
-            return ColumnData(BooleanType(), val, None if bool(valid.all()) else valid)
+            # (a device mask stays as it is: dropping an all-true one would cost a host sync)
+            return ColumnData(BooleanType(), val, None if (not valid.is_cuda and bool(valid.all())) else valid)
         valid = _and_valid(l, r)
         if self.op == "<=>":
             t = self.operand_type(schema)
@@ -360,7 +377,8 @@ def _device_string_eq(op: "BinOp", l: ColumnData, r: ColumnData):
     from .table import DeviceStringColumn
 
     for col, other in ((l, op.right), (r, op.left)):
-        if isinstance(col, DeviceStringColumn) and isinstance(other, Lit) and isinstance(other.value, str):
+        if col is not None and isinstance(col, DeviceStringColumn) and isinstance(other, Lit) \
+                and isinstance(other.value, str):
             return col.eq_literal(other.value)
     return None
 
