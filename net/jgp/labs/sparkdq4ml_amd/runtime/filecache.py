@@ -235,13 +235,13 @@ class MappedFile(_Resident):
             pieces = [_Piece() for _ in spans]
             self._dev[key] = t
             self._ready[key] = [(b - lo, p) for (_, b), p in zip(spans, pieces)]
-            threading.Thread(target=self._upload, args=(t, dev, side, lo, spans, pieces), daemon=True,
+            threading.Thread(target=self._upload, args=(t, dev, side, lo, spans, pieces, key), daemon=True,
                              name="dq4ml-upload").start()
         if not progressive:
             self.wait_ready(device, lo, hi)
         return t
 
-    def _upload(self, t, dev, side, lo, spans, pieces):
+    def _upload(self, t, dev, side, lo, spans, pieces, key):
         from .streams import _parallel_copy
 
         try:
@@ -265,6 +265,9 @@ class MappedFile(_Resident):
                     if ev is not None:
                         ev.synchronize()
         except BaseException as e:  # every waiter raises instead of hanging
+            if self._dev.get(key) is t:  # an incomplete copy must never serve a later read
+                self._dev.pop(key, None)
+                self._ready.pop(key, None)
             for p in pieces:
                 if not p._enq.is_set():
                     p.fail(e)
