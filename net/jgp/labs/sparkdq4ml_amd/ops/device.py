@@ -35,7 +35,6 @@ _plan_cache = {}
 # HBM-bound pass streams at the same rate on 248 of 256 CUs (profiles/r5_tail_reserve.md).
 _gram_reserve = int(os.environ.get("DQ4ML_GRAM_RESERVE_CUS", "-1"))
 _cus_cache = {}
-_GRAM_OVERSUB = int(os.environ.get("DQ4ML_GRAM_OVERSUB", "1"))
 
 
 def set_gram_reserve(n: int) -> None:
@@ -64,10 +63,6 @@ def _plan_blocks(h, mode, d, n, xdt, xmode):
     if nb is None:
         nb = int(h.gram_plan_blocks(mode, int(d), int(n), xdt, xmode))
         cus = _cus(h)
-        if _GRAM_OVERSUB > 1 and nb >= cus:
-            # (A/B knob) more blocks than resident slots: a CU that finishes early takes the next
-            # block, so the drain balances, and each block still owns fixed rows and its own slab
-            nb *= _GRAM_OVERSUB
         if reserve > 0 and nb >= cus:  # a full residency wave of blocks: give `reserve` CUs back
             per = nb // cus
             nb = max(1, nb - reserve * per)

@@ -194,9 +194,6 @@ for s in $STEPS; do
     bandprof) (export TMPDIR=/tmp DQ4ML_FORCE_COLLECTIVES=1; step bandprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/bandprof -o run --output-format csv -- python scripts/bucket_sweep.py --rows 1e6 --buckets-mb 4 --wires f32 --reps 2) || exit $? ;;
     lsq) step lsq 600 python -u -m pytest tests/test_gpu_lsq.py -m gpu -v --maxfail=5 --timeout 120 --timeout-method thread ;;
     lbfgssmall) step lbfgssmall 600 python benchmarks/bench_lbfgs.py --rows 2e5 --features 8192 --steps 2 --warmup 1 ;;
-    oversub) for r in 1 2; do for m in 1 2 4; do
-            step oversub_${m}_s${r} 300 env DQ4ML_GRAM_OVERSUB=$m python bench.py --steps 200 --warmup 20 --rows 1.25e7 &&
-            step oversub_${m}_h${r} 300 env DQ4ML_GRAM_OVERSUB=$m python bench.py --steps 30 --warmup 5 || exit $?; done; done ;;
     csvshard) step csvshard 600 python benchmarks/bench_csv_pipeline.py --rows 1.25e7 --steps 200 --warmup 20 --json-out gpurun_out/csvshard.json &&
               step csvshard2 600 python benchmarks/bench_csv_pipeline.py --rows 1.25e7 --steps 200 --warmup 20 --json-out gpurun_out/csvshard2.json || exit $? ;;
     x4) step lbfgs1 900 env DQ4ML_BENCH_AB=0 python benchmarks/bench_lbfgs.py --steps 3 --warmup 1 --json-out gpurun_out/lbfgs1.json &&
