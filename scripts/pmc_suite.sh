@@ -4,7 +4,7 @@
 # and FETCH_SIZE takes 3 TCC ones), each pass under its own hard time limit.  Summaries:
 #   python scripts/pmc_report.py gpurun_out/pmc_<name>_{a,b} --kernel <substring>
 # Workloads (PMC_SET): lsq (lsq_qn_dp_pass_kernel, 1e6 x 16384 bf16 l-bfgs), cut (dq_scan_cut, the 77 GB config-4 CSV),
-# span (csv_span_eq, string column filter), tall (centred gram_tall_bf16_kernel, the headline),
+# cut32 (dq_scan_cut, the BASELINE-shape 1e8 x 32 CSV), span (csv_span_eq, string column filter), tall (centred gram_tall_bf16_kernel, the headline),
 # wide (gram_wide_gang_kernel, config 5 at 2e6 rows).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
@@ -31,6 +31,7 @@ for w in ${PMC_SET:-wide tall span cut lsq}; do
   case $w in
     lsq) run lsq 240 python benchmarks/bench_lbfgs.py --steps 1 --warmup 1 ;;
     cut) run cut 420 python benchmarks/bench_csv_pipeline.py --features 64 --rows 1.25e8 --steps 2 --warmup 1 ;;
+    cut32) run cut32 420 python benchmarks/bench_csv_pipeline.py --features 32 --rows 1e8 --steps 2 --warmup 1 ;;
     span) run span 240 python scripts/span_bench.py --rows 1e7 ;;
     tall) run tall 240 python bench.py --steps 10 --warmup 3 ;;
     wide) (export N=2e6 D=4096 EB=8 REPS=2; run wide 240 python scripts/wide_bench.py) || exit $? ;;  # (no env hop after --)
