@@ -37,12 +37,23 @@ constexpr int kBlock = 256;  // f64 kernel: 4 waves
 constexpr int kWavesPerBlock = kBlock / kWave;
 // bf16 kernel: one block fills a CU (fewer slabs to reduce): 16 waves at <=128 VGPRs (d <= 32),
 // 8 waves at <=256 VGPRs (d <= 64)
-template <int NT, int XMODE>
+// HALF (d <= 32 unmasked only; DQ4ML_GRAM_BF16_HALF=1, A/B): 8-wave blocks, two resident per CU,
+// so one block's ramp and reduction overlap the other's stream, and the next pass's blocks start
+// beside this pass's last ones
+template <int NT, int XMODE, bool HALF = false>
 struct BF16Geom {
-  static constexpr int kBlock = (NT == 1 && XMODE == 0) ? 1024 : 512;
+  static constexpr int kBlock = (NT == 1 && XMODE == 0 && !HALF) ? 1024 : 512;
   static constexpr int kWaves = kBlock / kWave;
+  static constexpr int kMinBlocks = HALF ? 2 : 1;
 };
-static int bf16_block(int d, int xmode) { return (d <= 32 && xmode == 0) ? 1024 : 512; }
+static bool bf16_half() {
+  static const bool on = [] {
+    const char* e = getenv("DQ4ML_GRAM_BF16_HALF");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+static int bf16_block(int d, int xmode) { return (d <= 32 && xmode == 0 && !bf16_half()) ? 1024 : 512; }
 
 __device__ __forceinline__ double load_as_f64(const void* p, int dt, int64_t i) {
   switch (dt) {
@@ -200,8 +211,10 @@ __device__ __forceinline__ void slab_put(double* p, double v) {
 // =============================================================================================
 // bf16 MFMA kernel
 // =============================================================================================
-template <typename TX, int NT, int XMODE, bool TILED>
-__global__ __launch_bounds__((BF16Geom<NT, XMODE>::kBlock), 1) void gram_tall_bf16_kernel(GramArgs a) {
+template <typename TX, int NT, int XMODE, bool TILED, bool HALF = false>
+__global__ __launch_bounds__((BF16Geom<NT, XMODE, HALF>::kBlock), (BF16Geom<NT, XMODE, HALF>::kMinBlocks)) void
+gram_tall_bf16_kernel(GramArgs a) {
+  typedef BF16Geom<NT, XMODE, HALF> Geo;
   constexpr int NPAIR = NT * (NT + 1) / 2;
   // LDS: per wave 4 cols x 64 rows bf16 (W fragments) + 64 f32 row weights; reused for the
   // block reduction afterwards.
@@ -210,7 +223,7 @@ __global__ __launch_bounds__((BF16Geom<NT, XMODE>::kBlock), 1) void gram_tall_bf
   const int wave = threadIdx.x >> 6;
   const int f = lane & 31, h = lane >> 5;
   __bf16* wl = reinterpret_cast<__bf16*>(smem) + wave * (4 * 64);
-  float* wrow = reinterpret_cast<float*>(smem + BF16Geom<NT, XMODE>::kWaves * 4 * 64 * 2) + wave * 64;
+  float* wrow = reinterpret_cast<float*>(smem + Geo::kWaves * 4 * 64 * 2) + wave * 64;
 
   f32x16 acc[NPAIR];
   f32x16 accw[NT];
@@ -230,8 +243,8 @@ __global__ __launch_bounds__((BF16Geom<NT, XMODE>::kBlock), 1) void gram_tall_bf
     fp[t] = X + (int64_t)(fvalid[t] ? feat : 0) * a.ld + 32 * h;
   }
 
-  const int64_t gw = (int64_t)blockIdx.x * BF16Geom<NT, XMODE>::kWaves + wave;
-  const int64_t total_waves = (int64_t)gridDim.x * BF16Geom<NT, XMODE>::kWaves;
+  const int64_t gw = (int64_t)blockIdx.x * Geo::kWaves + wave;
+  const int64_t total_waves = (int64_t)gridDim.x * Geo::kWaves;
   int64_t s0 = gw * a.spw;
   int64_t s1 = s0 + a.spw;
   if (s1 > a.nsuper) s1 = a.nsuper;
@@ -345,7 +358,7 @@ __global__ __launch_bounds__((BF16Geom<NT, XMODE>::kBlock), 1) void gram_tall_bf
   }
 
   // ---- block reduction: fixed-shape tree over the waves (deterministic), 4 rounds ------------
-  constexpr int W = BF16Geom<NT, XMODE>::kWaves;
+  constexpr int W = Geo::kWaves;
   constexpr int NV = (NPAIR + NT) * 16;  // f32 accumulator values per lane
   const int d = a.d;
   double sc[5] = {ra.cnt, ra.ws, ra.wws, ra.bs, ra.bbs};
@@ -1252,6 +1265,7 @@ static void with_kernel(int mode, int xdt, int d, int xmode, bool tiled, F&& f) 
   if (mode == GRAM_BF16) {
     const int NT = (d + 31) / 32;
 #define DQ_BF16_CASE(TX, NTV, TL)                                                 \
+    if (xmode == 0 && NTV == 1 && bf16_half()) return f(gram_tall_bf16_kernel<TX, 1, 0, TL, true>); \
     if (xmode == 0) return f(gram_tall_bf16_kernel<TX, NTV, 0, TL>);              \
     if (xmode == 1) return f(gram_tall_bf16_kernel<TX, NTV, 1, TL>);              \
     return f(gram_tall_bf16_kernel<TX, NTV, 2, TL>);

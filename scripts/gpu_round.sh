@@ -194,6 +194,10 @@ for s in $STEPS; do
     bandprof) (export TMPDIR=/tmp DQ4ML_FORCE_COLLECTIVES=1; step bandprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/bandprof -o run --output-format csv -- python scripts/bucket_sweep.py --rows 1e6 --buckets-mb 4 --wires f32 --reps 2) || exit $? ;;
     lsq) step lsq 600 python -u -m pytest tests/test_gpu_lsq.py -m gpu -v --maxfail=5 --timeout 120 --timeout-method thread ;;
     lbfgssmall) step lbfgssmall 600 python benchmarks/bench_lbfgs.py --rows 2e5 --features 8192 --steps 2 --warmup 1 ;;
+    half) step half_t 600 env DQ4ML_GRAM_BF16_HALF=1 python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_determinism.py tests/test_gpu_fit_pipeline.py -m gpu -q --timeout 120 --timeout-method thread &&
+          for r in 1 2; do for m in 0 1; do
+            step half_${m}_s${r} 300 env DQ4ML_GRAM_BF16_HALF=$m python bench.py --steps 200 --warmup 20 --rows 1.25e7 &&
+            step half_${m}_h${r} 300 env DQ4ML_GRAM_BF16_HALF=$m python bench.py --steps 30 --warmup 5 || exit $?; done; done ;;
     cutstamps) step cutstamps 600 env VARIANTS="base;DQ4ML_CUT_STAMPS=1" python scripts/cut_bench.py --features 32 --rows 1e8 --reps 5 ;;
     csvshard) step csvshard 600 python benchmarks/bench_csv_pipeline.py --rows 1.25e7 --steps 200 --warmup 20 --json-out gpurun_out/csvshard.json &&
               step csvshard2 600 python benchmarks/bench_csv_pipeline.py --rows 1.25e7 --steps 200 --warmup 20 --json-out gpurun_out/csvshard2.json || exit $? ;;
