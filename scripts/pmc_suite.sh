@@ -14,14 +14,14 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp HSA_ENABLE_IPC_MODE_LEGACY=0 DQ4ML_BENCH_AB=0 DQ4ML_QN_SPLIT=1
 A="GRBM_GUI_ACTIVE FETCH_SIZE SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_VMEM SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_ANY"
 B="GRBM_GUI_ACTIVE TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCP_TCC_READ_REQ_sum SQ_INSTS_LDS SQ_ACTIVE_INST_VALU"
-run() {  # name seconds cmd...
-  local name=$1 to=$2; shift 2
+run() {  # name seconds kernel-regex cmd...  (counters only for the matching kernels: the 64 MiB
+  local name=$1 to=$2 kre=$3; shift 3  # limit on what a call copies back)
   for pass in a b; do
     local ctr=$A
     [ $pass = b ] && ctr=$B
     echo "=== pmc $name $pass"
-    timeout -s KILL "$to" rocprofv3 --kernel-trace --pmc $ctr -d "gpurun_out/pmc_${name}_$pass" -o run \
-      --output-format csv -- "$@" > "gpurun_out/pmc_${name}_$pass.log" 2>&1
+    timeout -s KILL "$to" rocprofv3 --kernel-trace --pmc $ctr --kernel-include-regex "$kre" \
+      -d "gpurun_out/pmc_${name}_$pass" -o run --output-format csv -- "$@" > "gpurun_out/pmc_${name}_$pass.log" 2>&1
     local rc=$?
     tail -2 "gpurun_out/pmc_${name}_$pass.log"
     if [ $rc -ne 0 ]; then echo "pmc $name $pass rc=$rc"; exit $rc; fi
@@ -29,11 +29,11 @@ run() {  # name seconds cmd...
 }
 for w in ${PMC_SET:-wide tall span cut lsq}; do
   case $w in
-    lsq) run lsq 240 python benchmarks/bench_lbfgs.py --steps 1 --warmup 1 ;;
-    cut) run cut 420 python benchmarks/bench_csv_pipeline.py --features 64 --rows 1.25e8 --steps 2 --warmup 1 ;;
-    cut32) run cut32 420 python benchmarks/bench_csv_pipeline.py --features 32 --rows 1e8 --steps 2 --warmup 1 ;;
-    span) run span 240 python scripts/span_bench.py --rows 1e7 ;;
-    tall) run tall 240 python bench.py --steps 10 --warmup 3 ;;
-    wide) (export N=2e6 D=4096 EB=8 REPS=2; run wide 240 python scripts/wide_bench.py) || exit $? ;;  # (no env hop after --)
+    lsq) run lsq 240 lsq_qn_dp_pass python benchmarks/bench_lbfgs.py --steps 1 --warmup 1 ;;
+    cut) run cut 420 dq_scan_cut python benchmarks/bench_csv_pipeline.py --features 64 --rows 1.25e8 --steps 2 --warmup 1 ;;
+    cut32) run cut32 420 dq_scan_cut python benchmarks/bench_csv_pipeline.py --features 32 --rows 1e8 --steps 2 --warmup 1 ;;
+    span) run span 240 csv_span_eq python scripts/span_bench.py --rows 1e7 ;;
+    tall) run tall 240 gram_tall_bf16 python bench.py --steps 10 --warmup 3 ;;
+    wide) (export N=2e6 D=4096 EB=8 REPS=2; run wide 240 gram_wide_gang python scripts/wide_bench.py) || exit $? ;;  # (no env hop after --)
   esac
 done
