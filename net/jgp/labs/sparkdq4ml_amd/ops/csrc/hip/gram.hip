@@ -35,11 +35,13 @@ namespace {
 
 constexpr int kBlock = 256;  // f64 kernel: 4 waves
 constexpr int kWavesPerBlock = kBlock / kWave;
-// bf16 kernel: one block fills a CU (fewer slabs to reduce): 16 waves at <=128 VGPRs (d <= 32),
-// 8 waves at <=256 VGPRs (d <= 64)
-// HALF (d <= 32 unmasked only; DQ4ML_GRAM_BF16_HALF=1, A/B): 8-wave blocks, two resident per CU,
-// so one block's ramp and reduction overlap the other's stream, and the next pass's blocks start
-// beside this pass's last ones
+// bf16 kernel: 8 waves per block -- two co-resident per CU at <= 128 VGPRs for d <= 32 (HALF
+// below), one per CU at <= 256 VGPRs for d <= 64; the round-4 16-wave block filled a CU alone
+// HALF (d <= 32 unmasked; the default since round 5, DQ4ML_GRAM_BF16_HALF=0 restores the 16-wave
+// block): 8-wave blocks, two resident per CU, so one block's ramp and reduction overlap the other's
+// stream and the next pass's blocks start beside this pass's last ones.  Same box, two reps
+// (profiles/r5_shard_drain.md): 1.25e7-row shard 0.1297 / 0.1292 vs 0.1347 / 0.1365 ms per fit,
+// 1e8 headline 0.987 / 0.989 vs 0.994 / 0.992 ms.
 template <int NT, int XMODE, bool HALF = false>
 struct BF16Geom {
   static constexpr int kBlock = (NT == 1 && XMODE == 0 && !HALF) ? 1024 : 512;
@@ -49,7 +51,7 @@ struct BF16Geom {
 static bool bf16_half() {
   static const bool on = [] {
     const char* e = getenv("DQ4ML_GRAM_BF16_HALF");
-    return e && e[0] == '1';
+    return !(e && e[0] == '0');
   }();
   return on;
 }
