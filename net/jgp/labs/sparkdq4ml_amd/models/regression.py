@@ -260,12 +260,13 @@ class LinearRegression(_LRParams):
         self.__dict__.pop("_tiled_plan", None)  # set by THIS fit's _wls_stats only
         sess = getattr(df, "sparkSession", None)
         overlap = sess is not None and str(sess.conf.get("dq4ml.fit.overlapTail", "true")).lower() in ("1", "true")
-        if fused is not None:  # statistics already reduced by the fused CSV scan kernel
+        if fused is not None:  # statistics already reduced by the fused scan / stream kernel
             flat, checks = fused.flat, list(fused.checks)
             tracing.add_rows("gram", fused.nrows)
-            # no side-stream tail: nothing is left to overlap with (the next action's scan waits
-            # for this solve, see scanfuse.try_fused_gram)
-            overlap = False
+            # a fused CSV scan keeps its tail on the compute stream (the next action's scan waits for
+            # this solve, see scanfuse.try_fused_gram); the in-memory stream route (config 4) puts it
+            # on the side stream beside the next step's pass -- at N > 1 its all-reduce too
+            overlap = overlap and bool(getattr(fused, "overlap_ok", False))
         else:
             pipe = _pipe_stream(df, tbl) if overlap else None
             if pipe is not None:

@@ -274,7 +274,11 @@ def _launch(r):
             h.stats_unshift(out.data_ptr(), shift.dev.data_ptr(), d, st)
     tracing.add_rows("stream_dq_gram", n)
     STATS["stream_grams"] += 1
-    return FusedGram(out, d, [], n)
+    fg = FusedGram(out, d, [], n)
+    # the next step's pass reads only the in-memory columns: the fit tail (all-reduce, solve) may
+    # run on the side stream beside it (models/regression.py overlapTail)
+    fg.overlap_ok = os.environ.get("DQ4ML_STREAM_OVERLAP", "1") != "0"
+    return fg
 
 
 def try_fused_stream(plan, features_col: str, label_col: str, session, gram_dtype: str, route_key=None):
