@@ -33,7 +33,7 @@ def test_gram_index_covers_layout_once(d):
             assert f"acc[{scancut._gram_index(i, j, d)}] += gx{i} * gx{j};" in code
 
 
-def _cut_source(spark, d, lab, stamps=False, quoted=False):
+def _cut_source(spark, d, lab, stamps=False, quoted=False, max_line=None):
     import torch
 
     from net.jgp.labs.sparkdq4ml_amd.ops.csvscan import _opt_args
@@ -47,7 +47,7 @@ def _cut_source(spark, d, lab, stamps=False, quoted=False):
     schema = StructType([StructField(f"_c{i}", IntegerType() if k == 1 else DoubleType(), True)
                          for i, k in enumerate(kinds)])
     fused = {"kinds": kinds, "nullable": [False] * ncol, "strict": False, "fast_only": True, "empty_lines": 0,
-             "uniform_fields": True, "max_line": 10 if lab else 11 * ncol, "device": torch.device("cpu"),
+             "uniform_fields": True, "max_line": max_line or (10 if lab else 11 * ncol), "device": torch.device("cpu"),
              "min_line": 6 if lab else 9 * ncol, "term_kinds": [100, 0, 0],
              "opts": dict(_opt_args({"comment": 0}), sep=",", strict=False)}
     rel = CsvScanRelation(schema, lambda: None, fused, "Relation[csv]")
