@@ -211,9 +211,9 @@ def _mfma_gram(sh, slots):
     """The augmented Gram of the row tile on the matrix cores: v_mfma_f64_16x16x4_f64 per upper
     16 x 16 feature tile, 4 rows per k-step.  Lane l holds row (l >> 4) of the k-step and feature
     16 X + (l & 15) of panel X — one conflict-free ds_read_b64 per panel — for both operands
-    (A = tile rows, B = tile columns), and accumulates D[(l >> 4) + 4 e][l & 15] in f64.  Rows past
-    the tile are zeroed by a select (stale LDS never enters); feature columns past d + 2 read the
-    next row's bytes and only reach discarded (padding) entries.  Waves split into G tile groups x
+    (A = tile rows, B = tile columns), and accumulates D[(l >> 4) + 4 e][l & 15] in f64.  The three
+    rows past the tile's last row are zeroed by the row phase (stale LDS never enters); feature
+    columns past d + 2 read the next row's bytes and only reach discarded (padding) entries.  Waves split into G tile groups x
     4/G row groups; each row group writes a complete gram_width slab."""
     d, PP, GW, G, RG = sh.d, sh.PP, sh.gw, sh.G, sh.RG
     tiles = sh.tiles
@@ -225,15 +225,21 @@ def _mfma_gram(sh, slots):
     bodies = []
     for g, tl in enumerate(groups):
         panels = sorted({x for t in tl for x in t})
-        reads = "".join(f"          const double pv{x} = rv ? gr[{16 * x}] : 0.0;\n" for x in panels)
-        mf = "".join(f"          gacc[{k}] = __builtin_amdgcn_mfma_f64_16x16x4f64(pv{I}, pv{J}, gacc[{k}], 0, 0, 0);\n"
+        first = "".join(f"          double pv{x} = gr[{16 * x}];\n" for x in panels)
+        reads = "".join(f"            const double qv{x} = gq[{16 * x}];\n" for x in panels)
+        mf = "".join(f"            gacc[{k}] = __builtin_amdgcn_mfma_f64_16x16x4f64(pv{I}, pv{J}, gacc[{k}], 0, 0, 0);\n"
                      for k, (I, J) in enumerate(tl))
+        shift = "".join(f"            pv{x} = qv{x};\n" for x in panels)
+        # unconditional panel reads (rows nr .. nr + 2 of the tile are zeroed by the row phase, so
+        # no per-row select, which compiled to exec-masked loads and branches); the next k-step's
+        # reads are issued beside this step's MFMAs (the last step re-reads its own rows)
         bodies.append(f"""        if (gtg == {g}) {{{{
-          for (int k0 = 4 * grg; k0 < nr; k0 += {4 * RG}) {{{{
-            const int r = k0 + (lane >> 4);
-            const bool rv = r < nr;
-            const double* __restrict__ gr = gt + r * {PP} + (lane & 15);
-{reads}{mf}          }}}}
+          const int ki = 4 * grg < nr ? 4 * grg : 0;
+          const double* __restrict__ gr = gt + (ki + (lane >> 4)) * {PP} + (lane & 15);
+{first}          for (int k0 = 4 * grg; k0 < nr; k0 += {4 * RG}) {{{{
+            const int kn = k0 + {4 * RG} < nr ? k0 + {4 * RG} : k0;
+            const double* __restrict__ gq = gt + (kn + (lane >> 4)) * {PP} + (lane & 15);
+{reads}{mf}{shift}          }}}}
         }}}}
 """)
     gram_phase = "".join(bodies).replace("{{", "{").replace("}}", "}")
@@ -404,9 +410,11 @@ def kernel_source(g, kinds, used, opts: dict, H: int, slots: dict, d: int, term:
     pf_tail = ("    if ((cnt == 0 || " + ("true" if abl & 8 else "false") + ") && blk + 1 < w1) "
                "dq_fetch(ab, a, n, blk + 1, tid, pg, ph);  // no tile round ran\n")
     qb = int(opts.get("quote", 34)) if quoted else 0
+    # the 8-byte frame's converter: the 32-bit SWAR form (q, default) or the 64-bit one (s)
+    r8 = "csv_num_r8s_w" if os.environ.get("DQ4ML_CUT_CONV", "q") == "s" else "csv_num_r8q_w"
     conv_call = ("ok = true; m = (unsigned)len;" if abl & 1 else
                  f"""if (__ballot(fl > 8{" || qany" if qb else ""}) == 0ull) {{
-          ok = csv_num_r8s_w(fw0, fw1, fw2, fsh, fl, m, fr, dot);
+          ok = {r8}(fw0, fw1, fw2, fsh, fl, m, fr, dot);
         }} else {{  // (re-reads its frame: no register array lives across the branch)
           ok = csv_num_r<{FW // 4}>(stage, end, len < {FW} ? len : {FW}, m, fr, neg, dot);
         }}""")
@@ -470,6 +478,8 @@ def kernel_source(g, kinds, used, opts: dict, H: int, slots: dict, d: int, term:
             acc_decl, gram_phase, epilogue, tables = _valu_gram(sh, slots)
         # (+3 rows + 16: the MFMA Gram's k-step and padding-column reads stay inside the array)
         gt_decl = f"  __shared__ __attribute__((aligned(16))) double gt[{(RR + 3) * PP + 16}];\n"
+        # the MFMA Gram's last k-step reads up to three rows past the tile's rows: zeros
+        gt_zero = (f"      for (int i = tid; i < {3 * PP}; i += 256) gt[nr * {PP} + i] = 0.0;\n" if sh.mfma else "")
     else:
         outs = _gram_code(xs, yv).replace("    if (live)", "      if (live)")
         acc_decl = f"  double acc[{GW}];\n#pragma unroll\n  for (int k = 0; k < {GW}; ++k) acc[k] = 0.0;\n"
@@ -488,7 +498,7 @@ def kernel_source(g, kinds, used, opts: dict, H: int, slots: dict, d: int, term:
         (gred[0][tid] + gred[1][tid]) + (gred[2][tid] + gred[3][tid]);
 """
         tables = ""
-        gt_decl = ""
+        gt_decl = gt_zero = ""
     # column -> vt slot / Gram-tile feature slot: VALU selects for the common shapes, else the
     # LDS table
     if len(ucols) <= 6:
@@ -503,7 +513,7 @@ def kernel_source(g, kinds, used, opts: dict, H: int, slots: dict, d: int, term:
             fs_expr = "ctab[2 * c + 1]"
         feat_store = (f"        const int fs = {fs_expr};\n"
                       f"        if (fs >= 0) gt[rr * {PP} + fs] = dv;\n")
-    NF = 1  # fields per lane per conversion iteration
+    NF = int(os.environ.get("DQ4ML_CUT_NF", "1"))  # fields per lane per conversion iteration
     # no barrier at the window top: phase 0 writes only the stage, the cut and the scan words,
     # which the previous window finished reading before its row-phase barrier, so the previous
     # window's Gram (reading the row tile, written again only after this window's cut barrier)
@@ -514,7 +524,9 @@ def kernel_source(g, kinds, used, opts: dict, H: int, slots: dict, d: int, term:
     kind_tab = ", ".join(str(int(k)) for k in kinds)
     lb = f"__launch_bounds__(256, {waves_per_simd})" if waves_per_simd else "__launch_bounds__(256)"
     src = ("#define CSV_UDOT4(a, b, c) __builtin_amdgcn_udot4((a), (b), (c), false)\n"
-           "#define CSV_MUL24(a, b) __umul24((a), (b))\n") + header_text() + f"""
+           "#define CSV_MUL24(a, b) __umul24((a), (b))\n"
+           "#define CSV_ALIGNBIT(a, b, s) __builtin_amdgcn_alignbit((a), (b), (s))\n"
+           "#define CSV_PERM(a, b, s) __builtin_amdgcn_perm((a), (b), (s))\n") + header_text() + f"""
 using namespace dq4ml_csv;
 typedef unsigned int csv_u32x4 __attribute__((ext_vector_type(4)));
 typedef double f64x2 __attribute__((ext_vector_type(2)));
@@ -750,7 +762,7 @@ __device__ __forceinline__ void dq_fetch(const DQG unsigned char* ab, long long 
         bool live = line;
 {body if not abl & 4 else ""}
 {outs if not abl & 4 else ""}      }}
-      __syncthreads();
+{gt_zero}      __syncthreads();
       DQ_STAMP(4);
 {gram_phase if not abl & 2 else ""}    }}
 {pf_tail}    st0 = nst0;
@@ -803,7 +815,7 @@ def _compile(nodes, rel, d: int):
     quoted = not f.get("fast_only") and bool(f.get("quoted_fast"))
     key = (parts, udfs, tuple(rel.schema().names), tuple(f["kinds"]), repr(sorted(f["opts"].items())), H, d, term,
            crlf, min_line, int(f.get("max_line", 1 << 30)), quoted, os.environ.get("DQ4ML_CUT_ABLATE"),
-           os.environ.get("DQ4ML_CUT_STAMPS"))
+           os.environ.get("DQ4ML_CUT_STAMPS"), os.environ.get("DQ4ML_CUT_CONV"), os.environ.get("DQ4ML_CUT_NF"))
     if key in _CACHE:
         return _CACHE[key]
     base = _ScanBase(rel.schema(), 0, f["device"])

@@ -100,6 +100,11 @@ def main():
         rec = {"variant": v, "features": d, "rows": rows, "ms": round(ms, 4),
                "csv_gbytes_per_s": round(nbytes / ms / 1e6, 1),
                "cutter": scancut.STATS["cut_grams"] > before, "count": float(fused.flat[0]) if fused else None}
+        if fused is not None:  # bit-identity of the statistics across variants
+            import hashlib
+
+            flat = fused.flat if torch.is_tensor(fused.flat) else torch.as_tensor(fused.flat)
+            rec["digest"] = hashlib.sha1(flat.detach().cpu().double().numpy().tobytes()).hexdigest()[:16]
         if os.environ.get("DQ4ML_CUT_STAMPS") == "1" and "buf" in scancut.LAST_STAMPS:
             st = scancut.LAST_STAMPS["buf"].cpu().double()
             win = float(st[:, 6].sum())

@@ -201,6 +201,9 @@ for s in $STEPS; do
     cfg4ov) step cfg4ov_t 600 python -u -m pytest tests/test_gpu_streamfuse.py tests/test_gpu_fit_pipeline.py -m gpu -q --timeout 120 --timeout-method thread &&
           for r in 1 2; do for m in 0 1; do
             step cfg4ov_${m}_${r} 600 env DQ4ML_STREAM_OVERLAP=$m python benchmarks/bench_dq_pipeline.py --steps 10 --warmup 2 --json-out gpurun_out/cfg4ov_${m}_${r}.json || exit $?; done; done ;;
+    cutab) (export TMPDIR=/tmp
+       step cutab_t 600 python -u -m pytest tests/test_gpu_scancut.py tests/test_gpu_scanfuse.py -m gpu -q --maxfail=5 --timeout 120 --timeout-method thread &&
+       step cutab_w32 900 env VARIANTS="${CUTV:-base}" python scripts/cut_bench.py --features 32 --rows ${CUT_ROWS:-1e8} --reps ${CUT_REPS:-5}) || exit $? ;;
     cutstamps) step cutstamps 600 env VARIANTS="base;DQ4ML_CUT_STAMPS=1" python scripts/cut_bench.py --features 32 --rows 1e8 --reps 5 ;;
     csvshard) step csvshard 600 python benchmarks/bench_csv_pipeline.py --rows 1.25e7 --steps 200 --warmup 20 --json-out gpurun_out/csvshard.json &&
               step csvshard2 600 python benchmarks/bench_csv_pipeline.py --rows 1.25e7 --steps 200 --warmup 20 --json-out gpurun_out/csvshard2.json || exit $? ;;

@@ -67,6 +67,29 @@ static bool r8s(const std::string& f, double& dv, long long& lv, int& ty, bool& 
   return len == 0 || ok;
 }
 
+// csv_num_r8q (the 32-bit-SWAR form of the same path), same caller
+static bool r8q(const std::string& f, double& dv, long long& lv, int& ty, bool& fits) {
+  alignas(16) unsigned char buf[64];
+  const char pool[] = "0123456789.-+,\r\n x";
+  for (auto& c : buf) c = (unsigned char)pool[junk() % (sizeof(pool) - 1)];
+  const int off = 16 + (int)(junk() % 16);
+  memcpy(buf + off, f.data(), f.size());
+  const int len = (int)f.size();
+  const unsigned char c0 = len ? buf[off] : 0;
+  const int sg = (c0 == '-' || c0 == '+') ? 1 : 0;
+  fits = len - sg <= 8;
+  if (!fits) return false;
+  unsigned m;
+  int fr;
+  bool dot;
+  const bool ok = csv_num_r8q(buf, off + len, len - sg, m, fr, dot);
+  const double v = dot ? csv_div_pow10((double)m, fr) : (double)m;
+  dv = ok ? (c0 == '-' ? -v : v) : 0.0;
+  lv = ok && !dot ? (c0 == '-' ? -(long long)m : (long long)m) : 0;
+  ty = len == 0 ? C_NULL : (dot ? C_DOUBLE : C_INT);
+  return len == 0 || ok;
+}
+
 // csv_swar_field directly, with junk bytes after the field in the same 64-bit word (as the
 // per-line scan kernel hands it the field at the start of the line's remaining bytes)
 static bool swar8(const std::string& f, double& dv, long long& lv, int& ty) {
@@ -124,6 +147,18 @@ int main() {
         return false;
       }
     }
+    {
+      double d7 = 0;
+      long long l7 = 0;
+      int t7 = -1;
+      bool fits = false;
+      const bool g = r8q(f, d7, l7, t7, fits);
+      if (fits && (a != g || (a && (t1 != t7 || l1 != l7 || memcmp(&d1, &d7, sizeof d1) != 0)))) {
+        printf("MISMATCH field '%s': fast %d ty %d %.17g %lld | r8q %d ty %d %.17g %lld\n", f.c_str(), a, t1, d1,
+               l1, g, t7, d7, l7);
+        return false;
+      }
+    }
     if (f.size() <= 8) {
       double d6 = 0;
       long long l6 = 0;
@@ -173,6 +208,29 @@ int main() {
     for (int k = 0; k < len; ++k) f += alpha[rng() % (sizeof(alpha) - 1)];
     if (f.find(',') != std::string::npos) continue;  // the cutter never hands over a separator
     if (!check(f)) return 1;
+  }
+  // csv_num_r8q_w against csv_num_r8s_w on raw frames: every shift, every field length 0..8,
+  // bytes from the field alphabet
+  {
+    const char pool[] = "0123456789.-+,\r x/";
+    for (int it = 0; it < 4000000; ++it) {
+      unsigned w[3];
+      for (auto& x : w) {
+        x = 0;
+        for (int k = 0; k < 4; ++k) x |= (unsigned)(unsigned char)pool[rng() % (sizeof(pool) - 1)] << (8 * k);
+      }
+      const int sft = (int)(rng() % 4), fl = (int)(rng() % 9);
+      unsigned m1 = 0, m2 = 0;
+      int f1 = 0, f2 = 0;
+      bool o1, o2, d1 = false, d2 = false;
+      o1 = csv_num_r8s_w(w[0], w[1], w[2], sft, fl, m1, f1, d1);
+      o2 = csv_num_r8q_w(w[0], w[1], w[2], sft, fl, m2, f2, d2);
+      if (o1 != o2 || (o1 && (m1 != m2 || f1 != f2 || d1 != d2))) {
+        printf("MISMATCH frame %08x %08x %08x s %d fl %d: r8s %d %u %d %d | r8q %d %u %d %d\n", w[0], w[1], w[2], sft, fl,
+               o1, m1, f1, d1, o2, m2, f2, d2);
+        return 1;
+      }
+    }
   }
   printf("swar16 ok: %ld fields, %ld accepted\n", checked, accepted);
   return 0;
