@@ -265,55 +265,53 @@ def _mfma_gram(sh, slots):
     return acc_decl, gram_phase, epilogue, tables
 
 
-def _conv_loop(NF, C, CU, PP, FW, crlf, conv_call, frame_load, div_expr, int_ok, us_expr, feat_store, quote=0):
-    """The field-conversion loop: NF fields per lane per iteration (fb + 256 h), their positions
-    prefetched one iteration ahead, every field's frame + sign loads issued before any wait.
+def _conv_loop(C, CU, PP, FW, crlf, conv_call, frame_load, div_expr, int_ok, us_expr, feat_store, quote=0):
+    """The field-conversion loop: one field per lane per iteration (field fb, then fb + 256), its
+    positions prefetched one iteration ahead and its frame + sign loads issued before any wait.
+    The field's row and column advance by 256 fields per iteration (a constant quotient and
+    remainder of C: no per-field division, and the tile row bases by additions, no multiply).
     ``quote`` (QUOTED build: some fields are quoted fast-path numbers, ``"12.5"``): a quoted
-    field's bounds move inside its quotes and its wave takes the position-based converter."""
+    field's bounds move inside its quotes and its wave takes the position-based converter.
+    (Two or three fields per lane per iteration lost to register spills: profiles/r3_csv_cutter.md.)"""
     cr = 1 if crlf else 0
-    L = ["      // (the next iteration's positions are loaded while this one converts)"]
-    for h in range(NF):
-        L.append(f"      int q{h}_p = 0, q{h}_e = 0;")
-        L.append(f"      if (f0 + tid + {256 * h} < f1) {{ q{h}_p = dposx[f0 + tid + {256 * h}]; "
-                 f"q{h}_e = dposx[f0 + tid + {256 * h} + 1]; }}")
-    L.append(f"      for (int fb = f0 + tid; fb < f1; fb += {256 * NF}) {{")
-    for h in range(NF):
-        L.append(f"        const bool q{h}_act = fb + {256 * h} < f1;")
-        L.append(f"        const int q{h}_f = q{h}_act ? fb + {256 * h} : fb;  // (a spare lane repeats fb)")
-        L.append(f"        const int q{h}_fn = fb + {256 * (NF + h)} < f1 ? fb + {256 * (NF + h)} : fb;")
-        L.append(f"        const int q{h}_pn = dposx[q{h}_fn], q{h}_en = dposx[q{h}_fn + 1];")
-    for h in range(NF):
-        fl_ = (frame_load.replace("fw0", f"q{h}_w0").replace("fw1", f"q{h}_w1").replace("fw2", f"q{h}_w2")
-               .replace("const int c0 =", f"const int q{h}_c0 =").replace("stage[start]", f"stage[q{h}_start]")
-               .replace("fwp", f"q{h}_wp").replace("+ end", f"+ q{h}_end").replace("^ start", f"^ q{h}_start")
-               .replace("+ f;", f"+ q{h}_f;").replace("(f & 1)", f"(q{h}_f & 1)"))
-        L.append(f"        const int q{h}_end = q{h}_e;")
-        L.append(f"        const int q{h}_rw = q{h}_f / {C}, q{h}_c = q{h}_f - q{h}_rw * {C};")
-        L.append(f"        const int q{h}_start = q{h}_p + 1 + ({cr} && q{h}_c == 0 ? 1 : 0);")
-        L.append(f"        q{h}_p = q{h}_pn;")
-        L.append(f"        q{h}_e = q{h}_en;")
-        L.append(f"        const int q{h}_fsh = (q{h}_end - 8) & 3;")
-        L.append(f"        const unsigned* q{h}_wp = reinterpret_cast<const unsigned*>(stage + (q{h}_end - 8 - q{h}_fsh));")
-        L.append("        " + fl_)
-    keep = ", ".join(f'"v"(q{h}_w0), "v"(q{h}_w1), "v"(q{h}_w2), "v"(q{h}_c0)' for h in range(NF))
-    L.append(f"        asm volatile(\"\" ::{keep});  // one wait for every frame (else they sink past the branch)")
+    dq, dr = 256 // C, 256 % C
+    fl_ = (frame_load.replace("fw0", "q_w0").replace("fw1", "q_w1").replace("fw2", "q_w2")
+           .replace("const int c0 =", "const int q_c0 =").replace("stage[start]", "stage[q_start]")
+           .replace("fwp", "q_wp").replace("+ end", "+ q_end").replace("^ start", "^ q_start")
+           .replace("+ f;", "+ fb;").replace("(f & 1)", "(fb & 1)"))
     cc = conv_call.replace(chr(10) + "        ", chr(10) + "          ")
-    fs = feat_store.replace("        const int fs", "            const int fs").replace(
-        "        if (fs >= 0)", "            if (fs >= 0)")
-    for h in range(NF):
-        if quote:
-            bounds = (f"const int qs_ = q{h}_c0 == {quote}, qe_ = stage[q{h}_end - 1] == {quote};\n"
-                      f"          const bool qany = (qs_ | qe_) != 0;\n"
-                      f"          const int f = q{h}_f, end = q{h}_end - qe_, start = q{h}_start + qs_, len = end - start, "
-                      f"c = q{h}_c, rw = q{h}_rw;")
-        else:
-            bounds = (f"const int f = q{h}_f, end = q{h}_end, start = q{h}_start, len = end - start, c = q{h}_c, "
-                      f"rw = q{h}_rw;")
-        L.append(f"""        {{
+    fs = (feat_store.replace(f"rr * {PP}", "q_gb").replace("        const int fs", "            const int fs")
+          .replace("        if (fs >= 0)", "            if (fs >= 0)"))
+    if quote:
+        bounds = (f"const int qs_ = q_c0 == {quote}, qe_ = stage[q_end - 1] == {quote};\n"
+                  f"          const bool qany = (qs_ | qe_) != 0;\n"
+                  f"          const int end = q_end - qe_, start = q_start + qs_, len = end - start, c = q_c;")
+    else:
+        bounds = "const int end = q_end, start = q_start, len = end - start, c = q_c;"
+    return f"""      // (the next iteration's positions are loaded while this one converts)
+      int q_p = 0, q_e = 0;
+      if (f0 + tid < f1) {{
+        q_p = dposx[f0 + tid];
+        q_e = dposx[f0 + tid + 1];
+      }}
+      int q_c = (f0 + tid) % {C};                            // the field's column
+      int q_vb = ((f0 + tid) / {C} - R0) * {CU}, q_gb = ((f0 + tid) / {C} - R0) * {PP};  // its tile rows
+      for (int fb = f0 + tid; fb < f1; fb += 256) {{
+        const int q_fn = fb + 256 < f1 ? fb + 256 : fb;
+        const int q_pn = dposx[q_fn], q_en = dposx[q_fn + 1];
+        const int q_end = q_e;
+        const int q_start = q_p + 1 + ({cr} && q_c == 0 ? 1 : 0);
+        q_p = q_pn;
+        q_e = q_en;
+        const int q_fsh = (q_end - 8) & 3;
+        const unsigned* q_wp = reinterpret_cast<const unsigned*>(stage + (q_end - 8 - q_fsh));
+        {fl_}
+        asm volatile("" :: "v"(q_w0), "v"(q_w1), "v"(q_w2), "v"(q_c0));  // one wait for the frame (else it sinks past the branch)
+        {{
           {bounds}
-          const int fsh = q{h}_fsh;
-          const unsigned fw0 = q{h}_w0, fw1 = q{h}_w1, fw2 = q{h}_w2;
-          const int c0 = {"qany ? stage[start] : " if quote else ""}q{h}_c0;
+          const int fsh = q_fsh;
+          const unsigned fw0 = q_w0, fw1 = q_w1, fw2 = q_w2;
+          const int c0 = {"qany ? stage[start] : " if quote else ""}q_c0;
           const bool neg0 = c0 == '-';
           const int fl = len - ((c0 == '-' || c0 == '+') ? 1 : 0);
           unsigned m = 0u;
@@ -329,16 +327,21 @@ def _conv_loop(NF, C, CU, PP, FW, crlf, conv_call, frame_load, div_expr, int_ok,
             int ty = C_NULL;
             ok = csv_field_fast(stage, 0, ps, end, O.sep, dv, lv, ty) && ty != C_NULL && csv_conforms(ty, DQ_KIND[c]);
           }}
-          if (q{h}_act) {{
-            bad |= !ok;
-            const int rr = rw - R0;
-            const int us = {us_expr};
-            if (us >= 0) vt[rr * {CU} + us] = dv;
-{fs}          }}
-          (void)f;
-        }}""")
-    L.append("      }")
-    return "\n".join(L) + "\n"
+          bad |= !ok;
+          const int us = {us_expr};
+          if (us >= 0) vt[q_vb + us] = dv;
+{fs}        }}
+        // the next field: 256 fields on = {dq} rows and {dr} columns on
+        q_c += {dr};
+        q_vb += {dq * CU};
+        q_gb += {dq * PP};
+        if (q_c >= {C}) {{
+          q_c -= {C};
+          q_vb += {CU};
+          q_gb += {PP};
+        }}
+      }}
+"""
 
 
 def kernel_source(g, kinds, used, opts: dict, H: int, slots: dict, d: int, term: int = 13, crlf: bool = False,
@@ -513,13 +516,12 @@ def kernel_source(g, kinds, used, opts: dict, H: int, slots: dict, d: int, term:
             fs_expr = "ctab[2 * c + 1]"
         feat_store = (f"        const int fs = {fs_expr};\n"
                       f"        if (fs >= 0) gt[rr * {PP} + fs] = dv;\n")
-    NF = int(os.environ.get("DQ4ML_CUT_NF", "1"))  # fields per lane per conversion iteration
     # no barrier at the window top: phase 0 writes only the stage, the cut and the scan words,
     # which the previous window finished reading before its row-phase barrier, so the previous
     # window's Gram (reading the row tile, written again only after this window's cut barrier)
     # overlaps this window's staging
     top_sync = ""
-    conv_loop = _conv_loop(NF, C, CU, PP, FW, crlf, conv_call, frame_load, div_expr, int_ok, us_expr, feat_store,
+    conv_loop = _conv_loop(C, CU, PP, FW, crlf, conv_call, frame_load, div_expr, int_ok, us_expr, feat_store,
                            quote=qb)
     kind_tab = ", ".join(str(int(k)) for k in kinds)
     lb = f"__launch_bounds__(256, {waves_per_simd})" if waves_per_simd else "__launch_bounds__(256)"
@@ -815,7 +817,7 @@ def _compile(nodes, rel, d: int):
     quoted = not f.get("fast_only") and bool(f.get("quoted_fast"))
     key = (parts, udfs, tuple(rel.schema().names), tuple(f["kinds"]), repr(sorted(f["opts"].items())), H, d, term,
            crlf, min_line, int(f.get("max_line", 1 << 30)), quoted, os.environ.get("DQ4ML_CUT_ABLATE"),
-           os.environ.get("DQ4ML_CUT_STAMPS"), os.environ.get("DQ4ML_CUT_CONV"), os.environ.get("DQ4ML_CUT_NF"))
+           os.environ.get("DQ4ML_CUT_STAMPS"), os.environ.get("DQ4ML_CUT_CONV"))
     if key in _CACHE:
         return _CACHE[key]
     base = _ScanBase(rel.schema(), 0, f["device"])
