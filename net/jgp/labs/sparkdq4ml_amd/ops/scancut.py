@@ -265,7 +265,8 @@ def _mfma_gram(sh, slots):
     return acc_decl, gram_phase, epilogue, tables
 
 
-def _conv_loop(C, CU, PP, FW, crlf, conv_call, frame_load, div_expr, int_ok, us_expr, feat_store, quote=0):
+def _conv_loop(C, CU, PP, FW, crlf, conv_call, frame_load, div_expr, int_ok, us_expr, feat_store, quote=0,
+               one_store=False):
     """The field-conversion loop: one field per lane per iteration (field fb, then fb + 256), its
     positions prefetched one iteration ahead and its frame + sign loads issued before any wait.
     The field's row and column advance by 256 fields per iteration (a constant quotient and
@@ -282,6 +283,12 @@ def _conv_loop(C, CU, PP, FW, crlf, conv_call, frame_load, div_expr, int_ok, us_
     cc = conv_call.replace(chr(10) + "        ", chr(10) + "          ")
     fs = (feat_store.replace(f"rr * {PP}", "q_gb").replace("        const int fs", "            const int fs")
           .replace("        if (fs >= 0)", "            if (fs >= 0)"))
+    if one_store:  # every column goes to exactly one tile (or nowhere): one store through a selected address
+        store = (f"          const int us = {us_expr};\n"
+                 + fs.replace("            if (fs >= 0) gt[q_gb + fs] = dv;\n", "").replace("            const", "          const")
+                 + "          *(fs >= 0 ? gt + q_gb + fs : (us >= 0 ? vt + q_vb + us : &dq_sink)) = dv;\n")
+    else:
+        store = f"          const int us = {us_expr};\n          if (us >= 0) vt[q_vb + us] = dv;\n{fs}"
     if quote:
         bounds = (f"const int qs_ = q_c0 == {quote}, qe_ = stage[q_end - 1] == {quote};\n"
                   f"          const bool qany = (qs_ | qe_) != 0;\n"
@@ -328,9 +335,7 @@ def _conv_loop(C, CU, PP, FW, crlf, conv_call, frame_load, div_expr, int_ok, us_
             ok = csv_field_fast(stage, 0, ps, end, O.sep, dv, lv, ty) && ty != C_NULL && csv_conforms(ty, DQ_KIND[c]);
           }}
           bad |= !ok;
-          const int us = {us_expr};
-          if (us >= 0) vt[q_vb + us] = dv;
-{fs}        }}
+{store}        }}
         // the next field: 256 fields on = {dq} rows and {dr} columns on
         q_c += {dr};
         q_vb += {dq * CU};
@@ -435,7 +440,7 @@ def kernel_source(g, kinds, used, opts: dict, H: int, slots: dict, d: int, term:
     if (tid < {H // 16}) {{
       const csv_u32x4 v = ph[0];
 #pragma unroll
-      for (int w = 0; w < 4; ++w) hraw16 |= dq_gather4(dq_eq80(v[w], {sep4})) << (4 * w);
+      for (int w = 0; w < 4; w += 2) hraw16 |= dq_gather8(dq_eq80(v[w], {sep4}), dq_eq80(v[w + 1], {sep4})) << (4 * w);
     }}
 """
         hscan_code = f"""    const bool hfast = st0 >= 0;  // a carried row start (block-uniform)
@@ -521,8 +526,11 @@ def kernel_source(g, kinds, used, opts: dict, H: int, slots: dict, d: int, term:
     # window's Gram (reading the row tile, written again only after this window's cut barrier)
     # overlaps this window's staging
     top_sync = ""
+    # one store per field when no column feeds both the chain and the Gram tile directly
+    one_store = (sh.blocked and feat is not None and not set(feat) & set(ucols)
+                 and os.environ.get("DQ4ML_CUT_STORE1", "1") != "0")
     conv_loop = _conv_loop(C, CU, PP, FW, crlf, conv_call, frame_load, div_expr, int_ok, us_expr, feat_store,
-                           quote=qb)
+                           quote=qb, one_store=one_store)
     kind_tab = ", ".join(str(int(k)) for k in kinds)
     lb = f"__launch_bounds__(256, {waves_per_simd})" if waves_per_simd else "__launch_bounds__(256)"
     src = ("#define CSV_UDOT4(a, b, c) __builtin_amdgcn_udot4((a), (b), (c), false)\n"
@@ -560,9 +568,11 @@ __device__ __forceinline__ int dq_wave_prefix(int c, int& total) {{
   total = tot;
   return pre;
 }}
-// the four 0x80 flags of z gathered to bits 0..3
-__device__ __forceinline__ unsigned int dq_gather4(unsigned int z) {{
-  return (((z >> 7) * 0x00204081u) >> 21) & 0xFu;
+// the 0x80 flags of two consecutive dwords gathered to bits 0..7 in byte order by ONE multiply:
+// z0's flags sit at bits 8k, z1's at 8k + 4, and every (flag, magic bit) product lands on its own
+// bit (none collide below bit 29), so bits 21..28 are the eight flags in order
+__device__ __forceinline__ unsigned int dq_gather8(unsigned int z0, unsigned int z1) {{
+  return ((((z0 >> 7) | (z1 >> 3)) * 0x00204081u) >> 21) & 0xFFu;
 }}
 // one window's granules: 64 bytes per lane, then the head (the row straddling into the window)
 // and two tail granules; zero outside [0, n)
@@ -599,6 +609,7 @@ __device__ __forceinline__ void dq_fetch(const DQG unsigned char* ab, long long 
   __shared__ __attribute__((aligned(16))) double vt[{RR * CU}];
 {gt_decl}  __shared__ short ctab[{2 * C}];
   __shared__ int wtot[4], shtot, sst0;
+  __shared__ double dq_sink;  // the store of a field no tile reads
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const long long a = (long long)(reinterpret_cast<unsigned long long>(b) & 15ull);
   const DQG unsigned char* ab = b - a;  // 16-byte aligned view
@@ -629,10 +640,11 @@ __device__ __forceinline__ void dq_fetch(const DQG unsigned char* ab, long long 
       const csv_u32x4 v = pg[j];
       *reinterpret_cast<csv_u32x4*>(stage + {H} + 64 * tid + 16 * j) = v;
 #pragma unroll
-      for (int w = 0; w < 4; ++w) {{
-        const unsigned int g4 = dq_gather4(dq_eq80(v[w], {sep4}) | dq_eq80(v[w], {term4}));
-        if (j < 2) dlo |= g4 << (16 * j + 4 * w);
-        else dhi |= g4 << (16 * (j - 2) + 4 * w);
+      for (int w = 0; w < 4; w += 2) {{
+        const unsigned int g8 = dq_gather8(dq_eq80(v[w], {sep4}) | dq_eq80(v[w], {term4}),
+                                           dq_eq80(v[w + 1], {sep4}) | dq_eq80(v[w + 1], {term4}));
+        if (j < 2) dlo |= g8 << (16 * j + 4 * w);
+        else dhi |= g8 << (16 * (j - 2) + 4 * w);
       }}
     }}
 #pragma unroll
@@ -693,7 +705,8 @@ __device__ __forceinline__ void dq_fetch(const DQG unsigned char* ab, long long 
       for (int j = 0; j < 4; ++j) {{
         const csv_u32x4 v = *reinterpret_cast<const csv_u32x4*>(stage + 64 * tid + 16 * j);
 #pragma unroll
-        for (int w = 0; w < 4; ++w) hm |= (unsigned long long)dq_gather4(dq_eq80(v[w], {sep4})) << (16 * j + 4 * w);
+        for (int w = 0; w < 4; w += 2)
+          hm |= (unsigned long long)dq_gather8(dq_eq80(v[w], {sep4}), dq_eq80(v[w + 1], {sep4})) << (16 * j + 4 * w);
       }}
       const int lo = st0 - 64 * tid;
       hm = lo >= 64 ? 0ull : (lo > 0 ? (hm & (~0ull << lo)) : hm);
@@ -817,7 +830,7 @@ def _compile(nodes, rel, d: int):
     quoted = not f.get("fast_only") and bool(f.get("quoted_fast"))
     key = (parts, udfs, tuple(rel.schema().names), tuple(f["kinds"]), repr(sorted(f["opts"].items())), H, d, term,
            crlf, min_line, int(f.get("max_line", 1 << 30)), quoted, os.environ.get("DQ4ML_CUT_ABLATE"),
-           os.environ.get("DQ4ML_CUT_STAMPS"), os.environ.get("DQ4ML_CUT_CONV"))
+           os.environ.get("DQ4ML_CUT_STAMPS"), os.environ.get("DQ4ML_CUT_CONV"), os.environ.get("DQ4ML_CUT_STORE1"))
     if key in _CACHE:
         return _CACHE[key]
     base = _ScanBase(rel.schema(), 0, f["device"])
