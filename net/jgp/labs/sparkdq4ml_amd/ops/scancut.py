@@ -13,9 +13,12 @@ numeric fields.  Here the unit of parallel work is the FIELD:
 2. the delimiter counts are prefix-summed across the block (wave ``shfl_up`` scans + one LDS
    word per wave) and each lane scatters its delimiter positions into an LDS position array —
    the cut: field f of the window spans (pos[f-1], pos[f]);
-3. every lane converts its own field: one 16-byte funnel-shifted LDS read and the 16-byte SWAR
-   converter (``csv_swar_field16``, exact and bit-identical to the byte-walking fast path), the
-   value lands in an LDS row tile [row][column] (f64);
+3. every lane converts its own field (fields ``tid + 256 k``, row and column advanced by constant
+   steps): one 12-byte LDS frame ending at the field's delimiter and the 32-bit SWAR converter
+   ``csv_num_r8q_w`` (digits and the dot by per-dword masks, the dot squeezed out by two
+   ``v_perm_b32``, ``v_dot4`` digit combine, the quotient by the fma-corrected reciprocal of
+   10^k; exact and bit-identical to the byte-walking fast path), the value stored once into an
+   LDS row tile [row][column] (f64);
 4. one thread per row runs the DQ chain (``ops/dqvm.py`` lowering, rule bodies and filters in
    registers) on its row of the tile, which gives the features, the label and the live flag;
 5. the normal-equation statistics: for d <= 8 every row thread adds to f64 register sums (the
@@ -418,11 +421,9 @@ def kernel_source(g, kinds, used, opts: dict, H: int, slots: dict, d: int, term:
     pf_tail = ("    if ((cnt == 0 || " + ("true" if abl & 8 else "false") + ") && blk + 1 < w1) "
                "dq_fetch(ab, a, n, blk + 1, tid, pg, ph);  // no tile round ran\n")
     qb = int(opts.get("quote", 34)) if quoted else 0
-    # the 8-byte frame's converter: the 32-bit SWAR form (q, default) or the 64-bit one (s)
-    r8 = "csv_num_r8s_w" if os.environ.get("DQ4ML_CUT_CONV", "q") == "s" else "csv_num_r8q_w"
     conv_call = ("ok = true; m = (unsigned)len;" if abl & 1 else
                  f"""if (__ballot(fl > 8{" || qany" if qb else ""}) == 0ull) {{
-          ok = {r8}(fw0, fw1, fw2, fsh, fl, m, fr, dot);
+          ok = csv_num_r8q_w(fw0, fw1, fw2, fsh, fl, m, fr, dot);
         }} else {{  // (re-reads its frame: no register array lives across the branch)
           ok = csv_num_r<{FW // 4}>(stage, end, len < {FW} ? len : {FW}, m, fr, neg, dot);
         }}""")
@@ -527,10 +528,19 @@ def kernel_source(g, kinds, used, opts: dict, H: int, slots: dict, d: int, term:
     # overlaps this window's staging
     top_sync = ""
     # one store per field when no column feeds both the chain and the Gram tile directly
-    one_store = (sh.blocked and feat is not None and not set(feat) & set(ucols)
-                 and os.environ.get("DQ4ML_CUT_STORE1", "1") != "0")
+    one_store = sh.blocked and feat is not None and not set(feat) & set(ucols)
     conv_loop = _conv_loop(C, CU, PP, FW, crlf, conv_call, frame_load, div_expr, int_ok, us_expr, feat_store,
                            quote=qb, one_store=one_store)
+    win_scatter = f"""    {{
+      int idx = htot + before;
+      unsigned long long mm = dm;
+      while (mm) {{
+        const int bit = __builtin_ctzll(mm);
+        mm &= mm - 1;
+        dcut[idx++] = (unsigned short)({H} + 64 * tid + bit);
+      }}
+    }}
+"""
     kind_tab = ", ".join(str(int(k)) for k in kinds)
     lb = f"__launch_bounds__(256, {waves_per_simd})" if waves_per_simd else "__launch_bounds__(256)"
     src = ("#define CSV_UDOT4(a, b, c) __builtin_amdgcn_udot4((a), (b), (c), false)\n"
@@ -749,15 +759,7 @@ __device__ __forceinline__ void dq_fetch(const DQG unsigned char* ab, long long 
         dcut[idx++] = (unsigned short)(16 * tid + bit);
       }}
     }}
-    {{
-      int idx = htot + before;
-      unsigned long long mm = dm;
-      while (mm) {{
-        const int bit = __builtin_ctzll(mm);
-        mm &= mm - 1;
-        dcut[idx++] = (unsigned short)({H} + 64 * tid + bit);
-      }}
-    }}
+{win_scatter}
     __syncthreads();
     DQ_STAMP(2);
     // the next window's first row starts after this window's last complete row
@@ -826,11 +828,13 @@ def _compile(nodes, rel, d: int):
     (parts, udfs), refs = dqvm.nodes_key(nodes)
     # (diagnostic builds only: DQ4ML_CUT_ABLATE timing ablations, DQ4ML_CUT_STAMPS phase clocks;
     # the losing A/B alternatives of rounds 2-3 -- VALU powers of ten, early prefetch, slow head
-    # scan, 2 fields per lane, top-of-window barrier, other tile sizes -- were removed in round 4)
+    # scan, 2 fields per lane, top-of-window barrier, other tile sizes -- were removed in round 4;
+    # round 5's -- lane-owned conversion without the position array, the split-half scatter --
+    # are measured in profiles/r5_cutter.md and were not kept)
     quoted = not f.get("fast_only") and bool(f.get("quoted_fast"))
     key = (parts, udfs, tuple(rel.schema().names), tuple(f["kinds"]), repr(sorted(f["opts"].items())), H, d, term,
            crlf, min_line, int(f.get("max_line", 1 << 30)), quoted, os.environ.get("DQ4ML_CUT_ABLATE"),
-           os.environ.get("DQ4ML_CUT_STAMPS"), os.environ.get("DQ4ML_CUT_CONV"), os.environ.get("DQ4ML_CUT_STORE1"))
+           os.environ.get("DQ4ML_CUT_STAMPS"))
     if key in _CACHE:
         return _CACHE[key]
     base = _ScanBase(rel.schema(), 0, f["device"])
