@@ -232,6 +232,7 @@ for s in $STEPS; do
        step cutpmcb2 300 timeout -s KILL 240 rocprofv3 --kernel-trace --pmc SQ_INSTS_SALU SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_VMEM SQ_ACTIVE_INST_MISC GRBM_GUI_ACTIVE -d gpurun_out/cutpmcb2 -o run --output-format csv -- python scripts/cut_bench.py --features 32 --rows 2e7 --reps 3 &&
        step cutpmcb3 300 timeout -s KILL 240 rocprofv3 --kernel-trace --pmc SQ_INST_CYCLES_VMEM SQ_ACTIVE_INST_SCA SQ_INSTS_SMEM SQ_INST_LEVEL_LDS SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA GRBM_GUI_ACTIVE -d gpurun_out/cutpmcb3 -o run --output-format csv -- python scripts/cut_bench.py --features 32 --rows 2e7 --reps 3) || exit $? ;;
     csv32s) step csv32s 600 python benchmarks/bench_csv_pipeline.py --features 32 --rows 2e7 --steps 10 --warmup 2 ;;
+    cfg4csvb) step cfg4csvb 1000 python benchmarks/bench_csv_pipeline.py --features 64 --rows 1.25e8 --steps 5 --warmup 2 --json-out gpurun_out/cfg4csvb.json ;;
     csv32) step csv32 900 python benchmarks/bench_csv_pipeline.py --features 32 --rows 1e8 --steps 10 --warmup 2 --json-out gpurun_out/csv32.json ;;
     csv64) step csv64 900 python benchmarks/bench_csv_pipeline.py --features 64 --rows ${CSV64_ROWS:-5e7} --steps 10 --warmup 2 --json-out gpurun_out/csv64.json ;;
     kprofcsv32) (export TMPDIR=/tmp; step kprofcsv32 600 rocprofv3 --kernel-trace --stats -d gpurun_out/kprofcsv32 -o run --output-format csv -- python benchmarks/bench_csv_pipeline.py --features 32 --rows 2e7 --steps 5 --warmup 2) || exit $? ;;
