@@ -204,6 +204,9 @@ for s in $STEPS; do
     cutab) (export TMPDIR=/tmp
        step cutab_t 600 python -u -m pytest tests/test_gpu_scancut.py tests/test_gpu_scanfuse.py -m gpu -q --maxfail=5 --timeout 120 --timeout-method thread &&
        step cutab_w32 900 env VARIANTS="${CUTV:-base}" python scripts/cut_bench.py --features 32 --rows ${CUT_ROWS:-1e8} --reps ${CUT_REPS:-5}) || exit $? ;;
+    labab) (export TMPDIR=/tmp
+       step labab_t 600 python -u -m pytest tests/test_gpu_scanfuse.py tests/test_gpu_scancut.py tests/test_gpu_dqvm.py tests/test_gpu_semantics.py -m gpu -q --maxfail=5 --timeout 120 --timeout-method thread &&
+       step labab 900 env VARIANTS="${LABV:-base}" python scripts/cut_bench.py --rows ${LAB_ROWS:-1e8} --reps ${LAB_REPS:-20}) || exit $? ;;
     cutstamps) step cutstamps 600 env VARIANTS="base;DQ4ML_CUT_STAMPS=1" python scripts/cut_bench.py --features 32 --rows 1e8 --reps 5 ;;
     csvshard) step csvshard 600 python benchmarks/bench_csv_pipeline.py --rows 1.25e7 --steps 200 --warmup 20 --json-out gpurun_out/csvshard.json &&
               step csvshard2 600 python benchmarks/bench_csv_pipeline.py --rows 1.25e7 --steps 200 --warmup 20 --json-out gpurun_out/csvshard2.json || exit $? ;;
