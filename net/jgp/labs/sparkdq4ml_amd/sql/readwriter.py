@@ -16,6 +16,7 @@ import glob
 import json
 import os
 import shutil
+import stat
 import weakref
 from typing import Dict, List, Optional
 
@@ -148,19 +149,27 @@ def _truthy(v) -> bool:
     return str(v).lower() in ("true", "1", "yes")
 
 
+_STATS: dict = {}  # path -> its os.stat of this load (one stat per plain file per load)
+
+
 def _expand(paths) -> List[str]:
     out = []
+    _STATS.clear()
     for p in paths:
-        if os.path.isdir(p):
+        if any(ch in p for ch in "*?["):
+            out += sorted(glob.glob(p))
+            continue
+        try:
+            st = os.stat(p)
+        except OSError:
+            from .expressions import AnalysisException
+
+            raise AnalysisException(f"Path does not exist: file:{os.path.abspath(p)};") from None
+        if stat.S_ISDIR(st.st_mode):
             out += sorted(f for f in glob.glob(os.path.join(p, "*"))
                           if not os.path.basename(f).startswith(("_", ".")))
-        elif any(ch in p for ch in "*?["):
-            out += sorted(glob.glob(p))
         else:
-            if not os.path.exists(p):
-                from .expressions import AnalysisException
-
-                raise AnalysisException(f"Path does not exist: file:{os.path.abspath(p)};")
+            _STATS[p] = st
             out.append(p)
     return out
 
@@ -248,10 +257,12 @@ class DataFrameReader:
         dev = self._session.device
         if len(files) != 1 or dev.type != "cuda" or comm.world_size() > 1:
             return None
-        try:
-            st = os.stat(files[0])
-        except OSError:
-            return None
+        st = _STATS.get(files[0])  # (the stat _expand took for this load)
+        if st is None:
+            try:
+                st = os.stat(files[0])
+            except OSError:
+                return None
         conf = self._session.conf
         ck = tuple(conf.get(k, None) for k in _LOAD_CONF)
         sch = self._schema.simpleString() if self._schema else None
