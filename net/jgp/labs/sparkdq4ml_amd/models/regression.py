@@ -129,9 +129,14 @@ def _fit_checks(params, tbl, X) -> list:
     return [c for c in checks if c is not None]
 
 
+_FL_CHECKED: dict = {}  # (id(schema), features, label) -> the schema that passed (rebuilt actions share it)
+
+
 def _check_features_label(params, df: DataFrame):
     schema = df.schema
     fc, lc = params.getOrDefault("featuresCol"), params.getOrDefault("labelCol")
+    if _FL_CHECKED.get((id(schema), fc, lc)) is schema:
+        return fc, lc
     try:
         ft = ColRef(fc).data_type(schema)
     except AnalysisException:
@@ -143,6 +148,9 @@ def _check_features_label(params, df: DataFrame):
     if not is_numeric(lt):
         raise ValueError(f"requirement failed: Column {lc} must be of type numeric but was actually of type "
                          f"{lt.simpleString()}.")
+    if len(_FL_CHECKED) >= 256:
+        _FL_CHECKED.clear()
+    _FL_CHECKED[(id(schema), fc, lc)] = schema
     return fc, lc
 
 
