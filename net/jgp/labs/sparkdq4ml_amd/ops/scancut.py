@@ -406,7 +406,7 @@ def kernel_source(g, kinds, used, opts: dict, H: int, slots: dict, d: int, term:
         "true" if not ints else "csv_conforms(dot ? C_DOUBLE : C_INT, DQ_KIND[c])")
     # the quotient's power-of-ten pair from an LDS table (the VALU select chain measured slower:
     # profiles/r3_csv_cutter.md)
-    div_expr = "csv_div_pow10_fma((double)m, p10t[fr & 15], ip10t[fr & 15])"
+    div_expr = "csv_div_pow10_fma((double)m, p10t[fr], ip10t[fr])"  # (both converters give fr <= 15)
     if abl & 16:  # (diagnostic) no table read: the quotient's LDS round trip
         div_expr = "csv_div_pow10_fma((double)m, 1.0 + fr, 1.0)"
     frame_load = ("const unsigned fw0 = fwp[0], fw1 = fwp[1], fw2 = fwp[2];\n        const int c0 = stage[start];"
@@ -541,6 +541,12 @@ def kernel_source(g, kinds, used, opts: dict, H: int, slots: dict, d: int, term:
       }}
     }}
 """
+    if sep < 0x80 and term < 0x80:
+        delim_body = (f"  const unsigned int a = ((v ^ {sep4}) & 0x7F7F7F7Fu) + 0x7F7F7F7Fu;\n"
+                      f"  const unsigned int t = ((v ^ {term4}) & 0x7F7F7F7Fu) + 0x7F7F7F7Fu;\n"
+                      f"  return ~((a & t) | v) & 0x80808080u;")
+    else:
+        delim_body = f"  return dq_eq80(v, {sep4}) | dq_eq80(v, {term4});"
     kind_tab = ", ".join(str(int(k)) for k in kinds)
     lb = f"__launch_bounds__(256, {waves_per_simd})" if waves_per_simd else "__launch_bounds__(256)"
     src = ("#define CSV_UDOT4(a, b, c) __builtin_amdgcn_udot4((a), (b), (c), false)\n"
@@ -577,6 +583,12 @@ __device__ __forceinline__ int dq_wave_prefix(int c, int& total) {{
   }}
   total = tot;
   return pre;
+}}
+// 0x80 in every byte of v that is the separator or the terminator.  A byte's low seven bits
+// differ from a pattern's iff bit 7 of ((x & 0x7F) + 0x7F) is set (x = byte ^ pattern); both
+// patterns are ASCII, so a match also needs bit 7 of the byte clear: 6 ops for both patterns
+__device__ __forceinline__ unsigned int dq_delim80(unsigned int v) {{
+{delim_body}
 }}
 // the 0x80 flags of two consecutive dwords gathered to bits 0..7 in byte order by ONE multiply:
 // z0's flags sit at bits 8k, z1's at 8k + 4, and every (flag, magic bit) product lands on its own
@@ -651,8 +663,7 @@ __device__ __forceinline__ void dq_fetch(const DQG unsigned char* ab, long long 
       *reinterpret_cast<csv_u32x4*>(stage + {H} + 64 * tid + 16 * j) = v;
 #pragma unroll
       for (int w = 0; w < 4; w += 2) {{
-        const unsigned int g8 = dq_gather8(dq_eq80(v[w], {sep4}) | dq_eq80(v[w], {term4}),
-                                           dq_eq80(v[w + 1], {sep4}) | dq_eq80(v[w + 1], {term4}));
+        const unsigned int g8 = dq_gather8(dq_delim80(v[w]), dq_delim80(v[w + 1]));
         if (j < 2) dlo |= g8 << (16 * j + 4 * w);
         else dhi |= g8 << (16 * (j - 2) + 4 * w);
       }}
