@@ -331,7 +331,7 @@ def _conv_loop(C, CU, PP, FW, crlf, conv_call, frame_load, div_expr, int_ok, us_
           const double v = {div_expr};  // fr = 0 without a dot: 10^0 = 1, exact
           double dv = neg ? -v : v;
           ok = ok && {int_ok};
-          if (len > {FW}) {{
+          if (slowp && len > {FW}) {{  // (an 8-byte-frame field is exact whatever its sign makes len)
             int ps = start;
             long long lv = 0;
             int ty = C_NULL;
@@ -421,8 +421,11 @@ def kernel_source(g, kinds, used, opts: dict, H: int, slots: dict, d: int, term:
     pf_tail = ("    if ((cnt == 0 || " + ("true" if abl & 8 else "false") + ") && blk + 1 < w1) "
                "dq_fetch(ab, a, n, blk + 1, tid, pg, ph);  // no tile round ran\n")
     qb = int(opts.get("quote", 34)) if quoted else 0
-    conv_call = ("ok = true; m = (unsigned)len;" if abl & 1 else
-                 f"""if (__ballot(fl > 8{" || qany" if qb else ""}) == 0ull) {{
+    # slowp (wave-uniform): some field of the wave is longer than the 8-byte frame (or quoted);
+    # only such a wave can hold a field for the byte-walking path
+    conv_call = ("const bool slowp = false;\n        ok = true; m = (unsigned)len;" if abl & 1 else
+                 f"""const bool slowp = __ballot(fl > 8{" || qany" if qb else ""}) != 0ull;
+        if (!slowp) {{
           ok = csv_num_r8q_w(fw0, fw1, fw2, fsh, fl, m, fr, dot);
         }} else {{  // (re-reads its frame: no register array lives across the branch)
           ok = csv_num_r<{FW // 4}>(stage, end, len < {FW} ? len : {FW}, m, fr, neg, dot);
