@@ -112,6 +112,20 @@ def _gram_index(i: int, j: int, d: int) -> Optional[int]:
     return 1 if i == d else 2
 
 
+def _tile_slot(sh, i: int, j: int):
+    """gram_width slot of entry (i <= j) of the row tile's upper Gram.  The tile's columns are the
+    augmented vector [x | 1 | y], or [x | y | 1] when ``sh.yfirst`` (the label column then sits
+    right after the features, where the cutter stores the CSV's last column)."""
+    d = sh.d
+    if i > j:
+        return None
+    if sh.yfirst:
+        sw = {d: d + 1, d + 1: d}
+        i, j = sw.get(i, i), sw.get(j, j)
+        i, j = min(i, j), max(i, j)
+    return _gram_index(i, j, d)
+
+
 def _passthrough(xs, used, d):
     """Feature columns when every feature is a bare column read (``fzf<c>``, each column at most
     once), else None."""
@@ -151,6 +165,11 @@ class _Shape:
         self.ucols = ucols                              # columns the chain reads, in vt order
         self.CU = max(1, len(ucols))
         self.feat = feat                                # passthrough feature columns (blocked only)
+        # every CSV column has a row-tile slot: features 0..d-1 pass through and the last column
+        # (the label's source) lands at slot d, so the converter stores each field straight into
+        # the tile ([x | y | 1] order) and the chain reads its inputs from there
+        self.yfirst = (d > 8 and feat == list(range(d)) and C == d + 1
+                       and os.environ.get("DQ4ML_CUT_TILEORD", "1") != "0")
         per_row = 8 * (self.CU + (self.PP if self.blocked else 0))
         self.gw = gram_width(d)
         fixed = (16 + H + self.W + 32) + 2 * self.DCAP + 4 * C + 384 + (
@@ -195,7 +214,7 @@ def _valu_gram(sh, slots):
             for u in range(4):
                 for v in range(4):
                     i, j = 4 * bI + u, 4 * bJ + v
-                    k = _gram_index(i, j, d) if i <= j else None
+                    k = _tile_slot(sh, i, j)
                     idx_tab.append(-1 if k is None else k)
     epilogue = f"""  if (gact) {{
 DQG double* __restrict__ gp = (DQG double*)p[{slots['gpart']}] + ((long long)blockIdx.x * {RG} + grg) * {GW};
@@ -252,7 +271,7 @@ def _mfma_gram(sh, slots):
         for lane in range(64):
             for e in range(4):
                 i, j = 16 * I + (lane >> 4) + 4 * e, 16 * J + (lane & 15)
-                k = _gram_index(i, j, d) if i <= j else None
+                k = _tile_slot(sh, i, j)
                 tabs.append(-1 if k is None else k)
     tables = f"__device__ const short DQ_TIDX[{len(tiles) * 256}] = {{{', '.join(str(x) for x in tabs)}}};\n"
     ep = []
@@ -269,7 +288,7 @@ def _mfma_gram(sh, slots):
 
 
 def _conv_loop(C, CU, PP, FW, crlf, conv_call, frame_load, div_expr, int_ok, us_expr, feat_store, quote=0,
-               one_store=False):
+               one_store=False, tile_all=False):
     """The field-conversion loop: one field per lane per iteration (field fb, then fb + 256), its
     positions prefetched one iteration ahead and its frame + sign loads issued before any wait.
     The field's row and column advance by 256 fields per iteration (a constant quotient and
@@ -279,6 +298,16 @@ def _conv_loop(C, CU, PP, FW, crlf, conv_call, frame_load, div_expr, int_ok, us_
     (Two or three fields per lane per iteration lost to register spills: profiles/r3_csv_cutter.md.)"""
     cr = 1 if crlf else 0
     dq, dr = 256 // C, 256 % C
+    if tile_all:
+        q_init = f"      int q_ga = ((f0 + tid) / {C} - R0) * {PP} + q_c;  // its row-tile slot\n"
+        q_step = (f"        q_c += {dr};\n        q_ga += {dq * PP + dr};\n"
+                  f"        if (q_c >= {C}) {{\n          q_c -= {C};\n          q_ga += {PP - C};\n        }}\n")
+    else:
+        q_init = (f"      int q_vb = ((f0 + tid) / {C} - R0) * {CU}, q_gb = ((f0 + tid) / {C} - R0) * {PP};"
+                  f"  // its tile rows\n")
+        q_step = (f"        q_c += {dr};\n        q_vb += {dq * CU};\n        q_gb += {dq * PP};\n"
+                  f"        if (q_c >= {C}) {{\n          q_c -= {C};\n          q_vb += {CU};\n          q_gb += {PP};\n"
+                  f"        }}\n")
     fl_ = (frame_load.replace("fw0", "q_w0").replace("fw1", "q_w1").replace("fw2", "q_w2")
            .replace("const int c0 =", "const int q_c0 =").replace("stage[start]", "stage[q_start]")
            .replace("fwp", "q_wp").replace("+ end", "+ q_end").replace("^ start", "^ q_start")
@@ -286,7 +315,9 @@ def _conv_loop(C, CU, PP, FW, crlf, conv_call, frame_load, div_expr, int_ok, us_
     cc = conv_call.replace(chr(10) + "        ", chr(10) + "          ")
     fs = (feat_store.replace(f"rr * {PP}", "q_gb").replace("        const int fs", "            const int fs")
           .replace("        if (fs >= 0)", "            if (fs >= 0)"))
-    if one_store:  # every column goes to exactly one tile (or nowhere): one store through a selected address
+    if tile_all:  # every column has its own row-tile slot ([x | y | 1] order): the field's tile address
+        store = "          gt[q_ga] = dv;\n"
+    elif one_store:  # every column goes to exactly one tile (or nowhere): one store through a selected address
         store = (f"          const int us = {us_expr};\n"
                  + fs.replace("            if (fs >= 0) gt[q_gb + fs] = dv;\n", "").replace("            const", "          const")
                  + "          *(fs >= 0 ? gt + q_gb + fs : (us >= 0 ? vt + q_vb + us : &dq_sink)) = dv;\n")
@@ -305,7 +336,7 @@ def _conv_loop(C, CU, PP, FW, crlf, conv_call, frame_load, div_expr, int_ok, us_
         q_e = dposx[f0 + tid + 1];
       }}
       int q_c = (f0 + tid) % {C};                            // the field's column
-      int q_vb = ((f0 + tid) / {C} - R0) * {CU}, q_gb = ((f0 + tid) / {C} - R0) * {PP};  // its tile rows
+{q_init}
       for (int fb = f0 + tid; fb < f1; fb += 256) {{
         const int q_fn = fb + 256 < f1 ? fb + 256 : fb;
         const int q_pn = dposx[q_fn], q_en = dposx[q_fn + 1];
@@ -340,14 +371,7 @@ def _conv_loop(C, CU, PP, FW, crlf, conv_call, frame_load, div_expr, int_ok, us_
           bad |= !ok;
 {store}        }}
         // the next field: 256 fields on = {dq} rows and {dr} columns on
-        q_c += {dr};
-        q_vb += {dq * CU};
-        q_gb += {dq * PP};
-        if (q_c >= {C}) {{
-          q_c -= {C};
-          q_vb += {CU};
-          q_gb += {PP};
-        }}
+{q_step}
       }}
 """
 
@@ -468,7 +492,8 @@ def kernel_source(g, kinds, used, opts: dict, H: int, slots: dict, d: int, term:
          f"{{{', '.join('0' for _ in range(16))}}}}}")
     body = ("\n".join("      " + ln.strip() for ln in g.lines).replace("P[", "p[")
             .replace("atomicOr((int*)p[", "dq_flag((unsigned int*)p["))
-    loads = "".join(f"      const {ct} fzf{c} = ({ct})(vt[rb + {usl[c]}]);\n"
+    loads = "".join((f"      const {ct} fzf{c} = ({ct})(gt[r * {sh.PP} + {c}]);\n" if sh.yfirst else
+                     f"      const {ct} fzf{c} = ({ct})(vt[rb + {usl[c]}]);\n")
                     for c, ct in sorted(used.items()) if c in usl)
     # per column: its vt slot (-1: the chain does not read it) and its feature slot in the Gram
     # tile (-1: not a passthrough feature)
@@ -482,7 +507,10 @@ def kernel_source(g, kinds, used, opts: dict, H: int, slots: dict, d: int, term:
             outs += "".join(f"      gr[{i}] = live ? (double)({v}) : 0.0;\n" for i, v in enumerate(xs))
         else:
             outs += f"      if (!live) {{\n#pragma unroll\n        for (int i = 0; i < {d}; ++i) gr[i] = 0.0;\n      }}\n"
-        outs += f"      gr[{d}] = live ? 1.0 : 0.0;\n      gr[{d + 1}] = live ? (double)({yv}) : 0.0;\n"
+        if sh.yfirst:  # (gr[d] held the label column, read above as a chain input)
+            outs += f"      gr[{d}] = live ? (double)({yv}) : 0.0;\n      gr[{d + 1}] = live ? 1.0 : 0.0;\n"
+        else:
+            outs += f"      gr[{d}] = live ? 1.0 : 0.0;\n      gr[{d + 1}] = live ? (double)({yv}) : 0.0;\n"
         outs += "".join(f"      gr[{i}] = 0.0;\n" for i in range(d + 2, PP))
         if sh.mfma:
             acc_decl, gram_phase, epilogue, tables = _mfma_gram(sh, slots)
@@ -533,7 +561,7 @@ def kernel_source(g, kinds, used, opts: dict, H: int, slots: dict, d: int, term:
     # one store per field when no column feeds both the chain and the Gram tile directly
     one_store = sh.blocked and feat is not None and not set(feat) & set(ucols)
     conv_loop = _conv_loop(C, CU, PP, FW, crlf, conv_call, frame_load, div_expr, int_ok, us_expr, feat_store,
-                           quote=qb, one_store=one_store)
+                           quote=qb, one_store=one_store, tile_all=sh.yfirst)
     win_scatter = f"""    {{
       int idx = htot + before;
       unsigned long long mm = dm;
@@ -848,7 +876,7 @@ def _compile(nodes, rel, d: int):
     quoted = not f.get("fast_only") and bool(f.get("quoted_fast"))
     key = (parts, udfs, tuple(rel.schema().names), tuple(f["kinds"]), repr(sorted(f["opts"].items())), H, d, term,
            crlf, min_line, int(f.get("max_line", 1 << 30)), quoted, os.environ.get("DQ4ML_CUT_ABLATE"),
-           os.environ.get("DQ4ML_CUT_STAMPS"))
+           os.environ.get("DQ4ML_CUT_STAMPS"), os.environ.get("DQ4ML_CUT_TILEORD"))
     if key in _CACHE:
         return _CACHE[key]
     base = _ScanBase(rel.schema(), 0, f["device"])

@@ -33,6 +33,30 @@ def test_gram_index_covers_layout_once(d):
             assert f"acc[{scancut._gram_index(i, j, d)}] += gx{i} * gx{j};" in code
 
 
+@pytest.mark.parametrize("d", [9, 32, 64])
+def test_tile_slot_map_covers_layout_once(d):
+    """The [x | y | 1] row tile (the label column stored at slot d by the converter) maps every
+    upper entry of the tile onto the gram_width layout exactly once, like [x | 1 | y]."""
+    class Sh:
+        pass
+
+    for yfirst in (False, True):
+        sh = Sh()
+        sh.d, sh.yfirst = d, yfirst
+        seen = {}
+        for j in range(d + 2):
+            for i in range(j + 1):
+                k = scancut._tile_slot(sh, i, j)
+                assert k is not None and k not in seen, (yfirst, i, j, k)
+                seen[k] = (i, j)
+        assert sorted(seen) == list(range(scancut.gram_width(d)))
+        assert scancut._tile_slot(sh, d + 1, d) is None  # the tile's lower half is not read
+    sh = Sh()
+    sh.d, sh.yfirst = d, True
+    assert scancut._tile_slot(sh, d, d) == 2 and scancut._tile_slot(sh, d + 1, d + 1) == 0  # Σy², count
+    assert scancut._tile_slot(sh, d, d + 1) == 1 and scancut._tile_slot(sh, 0, d) == 3 + d  # Σy, Σx0y
+
+
 def _cut_source(spark, d, lab, stamps=False, quoted=False, max_line=None):
     import torch
 
@@ -105,6 +129,7 @@ def test_cut_kernel_compiles_for_gfx950(cpu_session, tmp_path, monkeypatch, d, l
     assert "for (int r = tid; r < nr; r += 256)" in src  # a row tile larger than the block is covered
     assert ("DQ_TIDX" in src) == (d > 8)  # the MFMA Gram of the row tile
     assert ("csv_num_r<2>(stage, end" in src) == lab  # 8-byte converter frame for the lab's short fields
+    assert ("gt[q_ga] = dv;" in src) == (d > 8)  # every column stored straight into its row-tile slot
     hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
     if not os.path.exists(hipcc):
         pytest.skip("no hipcc")
