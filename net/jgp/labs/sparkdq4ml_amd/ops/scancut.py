@@ -562,10 +562,9 @@ def kernel_source(g, kinds, used, opts: dict, H: int, slots: dict, d: int, term:
     one_store = sh.blocked and feat is not None and not set(feat) & set(ucols)
     conv_loop = _conv_loop(C, CU, PP, FW, crlf, conv_call, frame_load, div_expr, int_ok, us_expr, feat_store,
                            quote=qb, one_store=one_store, tile_all=sh.yfirst)
-    if os.environ.get("DQ4ML_CUT_SCATSEQ", "1") != "0":
-        # the lane's two 32-byte halves one after the other, each with 32-bit steps (find-first,
-        # clear, store): ~5 VALU per delimiter instead of the 64-bit find-first's ~10
-        win_scatter = f"""    {{
+    # the lane's two 32-byte halves one after the other, each with 32-bit steps (find-first,
+    # clear, store): ~5 VALU per delimiter instead of the 64-bit find-first's ~10
+    win_scatter = f"""    {{
       int idx = htot + before;
       unsigned int mm = (unsigned int)dm;
       const int pa = {H} + 64 * tid;
@@ -577,17 +576,6 @@ def kernel_source(g, kinds, used, opts: dict, H: int, slots: dict, d: int, term:
       while (mm) {{
         dcut[idx++] = (unsigned short)(pa + 32 + __builtin_ctz(mm));
         mm &= mm - 1u;
-      }}
-    }}
-"""
-    else:
-        win_scatter = f"""    {{
-      int idx = htot + before;
-      unsigned long long mm = dm;
-      while (mm) {{
-        const int bit = __builtin_ctzll(mm);
-        mm &= mm - 1;
-        dcut[idx++] = (unsigned short)({H} + 64 * tid + bit);
       }}
     }}
 """
@@ -896,7 +884,7 @@ def _compile(nodes, rel, d: int):
     quoted = not f.get("fast_only") and bool(f.get("quoted_fast"))
     key = (parts, udfs, tuple(rel.schema().names), tuple(f["kinds"]), repr(sorted(f["opts"].items())), H, d, term,
            crlf, min_line, int(f.get("max_line", 1 << 30)), quoted, os.environ.get("DQ4ML_CUT_ABLATE"),
-           os.environ.get("DQ4ML_CUT_STAMPS"), os.environ.get("DQ4ML_CUT_TILEORD"), os.environ.get("DQ4ML_CUT_SCATSEQ"))
+           os.environ.get("DQ4ML_CUT_STAMPS"), os.environ.get("DQ4ML_CUT_TILEORD"))
     if key in _CACHE:
         return _CACHE[key]
     base = _ScanBase(rel.schema(), 0, f["device"])
