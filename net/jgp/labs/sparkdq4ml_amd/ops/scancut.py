@@ -585,6 +585,9 @@ def kernel_source(g, kinds, used, opts: dict, H: int, slots: dict, d: int, term:
                       f"  return ~((a & t) | v) & 0x80808080u;")
     else:
         delim_body = f"  return dq_eq80(v, {sep4}) | dq_eq80(v, {term4});"
+    # wave prefix sums: DPP row shifts / broadcasts (default) or ballot bit planes
+    scan_impl = ("dq_wave_prefix_ballot<B>" if os.environ.get("DQ4ML_CUT_SCAN", "dpp") == "ballot"
+                 else "dq_wave_prefix_dpp")
     kind_tab = ", ".join(str(int(k)) for k in kinds)
     lb = f"__launch_bounds__(256, {waves_per_simd})" if waves_per_simd else "__launch_bounds__(256)"
     src = ("#define CSV_UDOT4(a, b, c) __builtin_amdgcn_udot4((a), (b), (c), false)\n"
@@ -612,7 +615,7 @@ __device__ __forceinline__ unsigned int dq_eq80(unsigned int v, unsigned int pat
 // no cross-lane data movement: c's bit planes are ballots, and mbcnt counts the set lanes below
 // (a __shfl_up scan is six dependent ds_bpermute round trips)
 template <int B>
-__device__ __forceinline__ int dq_wave_prefix(int c, int& total) {{
+__device__ __forceinline__ int dq_wave_prefix_ballot(int c, int& total) {{
   int pre = 0, tot = 0;
 #pragma unroll
   for (int b = 0; b < B; ++b) {{
@@ -622,6 +625,23 @@ __device__ __forceinline__ int dq_wave_prefix(int c, int& total) {{
   }}
   total = tot;
   return pre;
+}}
+// the same by an inclusive DPP scan: row_shr 1, 2, 4, 8 within each 16-lane row (zero fill),
+// then row_bcast 15 / 31 across rows -- six DPP adds, and the wave total from lane 63
+__device__ __forceinline__ int dq_wave_prefix_dpp(int c, int& total) {{
+  int v = c;
+  v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, false);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, false);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xF, 0xF, false);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xF, 0xF, false);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xA, 0xF, false);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xC, 0xF, false);
+  total = __builtin_amdgcn_readlane(v, 63);
+  return v - c;
+}}
+template <int B>
+__device__ __forceinline__ int dq_wave_prefix(int c, int& total) {{
+  return {scan_impl}(c, total);
 }}
 // 0x80 in every byte of v that is the separator or the terminator.  A byte's low seven bits
 // differ from a pattern's iff bit 7 of ((x & 0x7F) + 0x7F) is set (x = byte ^ pattern); both
@@ -884,7 +904,7 @@ def _compile(nodes, rel, d: int):
     quoted = not f.get("fast_only") and bool(f.get("quoted_fast"))
     key = (parts, udfs, tuple(rel.schema().names), tuple(f["kinds"]), repr(sorted(f["opts"].items())), H, d, term,
            crlf, min_line, int(f.get("max_line", 1 << 30)), quoted, os.environ.get("DQ4ML_CUT_ABLATE"),
-           os.environ.get("DQ4ML_CUT_STAMPS"), os.environ.get("DQ4ML_CUT_TILEORD"))
+           os.environ.get("DQ4ML_CUT_STAMPS"), os.environ.get("DQ4ML_CUT_TILEORD"), os.environ.get("DQ4ML_CUT_SCAN"))
     if key in _CACHE:
         return _CACHE[key]
     base = _ScanBase(rel.schema(), 0, f["device"])
