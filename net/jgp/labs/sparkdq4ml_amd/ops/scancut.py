@@ -579,28 +579,6 @@ def kernel_source(g, kinds, used, opts: dict, H: int, slots: dict, d: int, term:
       }}
     }}
 """
-    if os.environ.get("DQ4ML_CUT_SCAT2X", "1") != "0":
-        # two delimiters per step: the second store goes to a spare slot past the array when the
-        # half has no second bit left (branch-free), so a wave runs half the steps
-        win_scatter = f"""    {{
-      int idx = htot + before;
-      const int pa = {H} + 64 * tid;
-#pragma unroll
-      for (int hf = 0; hf < 2; ++hf) {{
-        unsigned int mm = hf ? (unsigned int)(dm >> 32) : (unsigned int)dm;
-        const int ph = pa + 32 * hf;
-        while (mm) {{
-          const int b0 = __builtin_ctz(mm);
-          const unsigned int m1 = mm & (mm - 1u);
-          const int b1 = __builtin_ctz(m1 | 0x80000000u);
-          dcut[idx] = (unsigned short)(ph + b0);
-          dcut[m1 ? idx + 1 : {sh.DCAP}] = (unsigned short)(ph + b1);
-          idx += m1 ? 2 : 1;
-          mm = m1 & (m1 - 1u);
-        }}
-      }}
-    }}
-"""
     if sep < 0x80 and term < 0x80:
         delim_body = (f"  const unsigned int a = ((v ^ {sep4}) & 0x7F7F7F7Fu) + 0x7F7F7F7Fu;\n"
                       f"  const unsigned int t = ((v ^ {term4}) & 0x7F7F7F7Fu) + 0x7F7F7F7Fu;\n"
@@ -706,7 +684,7 @@ __device__ __forceinline__ void dq_fetch(const DQG unsigned char* ab, long long 
   unsigned int* vflag = (unsigned int*)p[{slots['vflag']}];
   __shared__ __attribute__((aligned(16))) unsigned char stage_raw[16 + {H} + {W} + 32];
   unsigned char* const stage = stage_raw + 16;  // 16 readable bytes below stage[0] (right-aligned reads)
-  __shared__ unsigned short dpos[{DCAP} + 2];  // (+1: the scatter's spare slot dcut[{DCAP}])
+  __shared__ unsigned short dpos[{DCAP} + 1];
   unsigned short* const dposx = dpos;  // dposx[0]: the delimiter before the window's first field
   unsigned short* const dcut = dpos + 1;  // the window's delimiters
   __shared__ __attribute__((aligned(16))) double vt[{RR * CU}];
@@ -926,8 +904,7 @@ def _compile(nodes, rel, d: int):
     quoted = not f.get("fast_only") and bool(f.get("quoted_fast"))
     key = (parts, udfs, tuple(rel.schema().names), tuple(f["kinds"]), repr(sorted(f["opts"].items())), H, d, term,
            crlf, min_line, int(f.get("max_line", 1 << 30)), quoted, os.environ.get("DQ4ML_CUT_ABLATE"),
-           os.environ.get("DQ4ML_CUT_STAMPS"), os.environ.get("DQ4ML_CUT_TILEORD"), os.environ.get("DQ4ML_CUT_SCAN"),
-           os.environ.get("DQ4ML_CUT_SCAT2X"))
+           os.environ.get("DQ4ML_CUT_STAMPS"), os.environ.get("DQ4ML_CUT_TILEORD"), os.environ.get("DQ4ML_CUT_SCAN"))
     if key in _CACHE:
         return _CACHE[key]
     base = _ScanBase(rel.schema(), 0, f["device"])
