@@ -511,7 +511,7 @@ def kernel_source(g, kinds, used, opts: dict, H: int, slots: dict, d: int, term:
             outs += f"      gr[{d}] = live ? (double)({yv}) : 0.0;\n      gr[{d + 1}] = live ? 1.0 : 0.0;\n"
         else:
             outs += f"      gr[{d}] = live ? 1.0 : 0.0;\n      gr[{d + 1}] = live ? (double)({yv}) : 0.0;\n"
-        outs += "".join(f"      gr[{i}] = 0.0;\n" for i in range(d + 2, PP))
+        # (the padding columns d + 2 .. PP - 1 are zeroed once at kernel start: nothing writes them)
         if sh.mfma:
             acc_decl, gram_phase, epilogue, tables = _mfma_gram(sh, slots)
         else:
@@ -520,6 +520,8 @@ def kernel_source(g, kinds, used, opts: dict, H: int, slots: dict, d: int, term:
         gt_decl = f"  __shared__ __attribute__((aligned(16))) double gt[{(RR + 3) * PP + 16}];\n"
         # the MFMA Gram's last k-step reads up to three rows past the tile's rows: zeros
         gt_zero = (f"      for (int i = tid; i < {3 * PP}; i += 256) gt[nr * {PP} + i] = 0.0;\n" if sh.mfma else "")
+        gt_init = (f"  for (int i = tid; i < {(RR + 3) * PP + 16}; i += 256) gt[i] = 0.0;  // (padding columns stay 0)\n"
+                   f"  __syncthreads();\n")
     else:
         outs = _gram_code(xs, yv).replace("    if (live)", "      if (live)")
         acc_decl = f"  double acc[{GW}];\n#pragma unroll\n  for (int k = 0; k < {GW}; ++k) acc[k] = 0.0;\n"
@@ -538,7 +540,7 @@ def kernel_source(g, kinds, used, opts: dict, H: int, slots: dict, d: int, term:
         (gred[0][tid] + gred[1][tid]) + (gred[2][tid] + gred[3][tid]);
 """
         tables = ""
-        gt_decl = gt_zero = ""
+        gt_decl = gt_zero = gt_init = ""
     # column -> vt slot / Gram-tile feature slot: VALU selects for the common shapes, else the
     # LDS table
     if len(ucols) <= 6:
@@ -702,7 +704,7 @@ __device__ __forceinline__ void dq_fetch(const DQG unsigned char* ab, long long 
     p10t[tid] = tid <= 9 ? csv_pow10(tid) : 1.0;
     ip10t[tid] = tid <= 9 ? csv_inv_pow10(tid) : 1.0;
   }}
-{acc_decl}
+{acc_decl}{gt_init}
   // a CONTIGUOUS run of windows per block: the row start of window k+1 is carried from the cut
   // of window k (only the first window searches back for it), and window k+1's bytes are in
   // flight (registers) while window k is cut
