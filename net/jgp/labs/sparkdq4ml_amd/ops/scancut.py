@@ -168,8 +168,7 @@ class _Shape:
         # every CSV column has a row-tile slot: features 0..d-1 pass through and the last column
         # (the label's source) lands at slot d, so the converter stores each field straight into
         # the tile ([x | y | 1] order) and the chain reads its inputs from there
-        self.yfirst = (d > 8 and feat == list(range(d)) and C == d + 1
-                       and os.environ.get("DQ4ML_CUT_TILEORD", "1") != "0")
+        self.yfirst = d > 8 and feat == list(range(d)) and C == d + 1
         per_row = 8 * (self.CU + (self.PP if self.blocked else 0))
         self.gw = gram_width(d)
         fixed = (16 + H + self.W + 32) + 2 * self.DCAP + 4 * C + 384 + (
@@ -587,9 +586,6 @@ def kernel_source(g, kinds, used, opts: dict, H: int, slots: dict, d: int, term:
                       f"  return ~((a & t) | v) & 0x80808080u;")
     else:
         delim_body = f"  return dq_eq80(v, {sep4}) | dq_eq80(v, {term4});"
-    # wave prefix sums: DPP row shifts / broadcasts (default) or ballot bit planes
-    scan_impl = ("dq_wave_prefix_ballot<B>" if os.environ.get("DQ4ML_CUT_SCAN", "dpp") == "ballot"
-                 else "dq_wave_prefix_dpp")
     kind_tab = ", ".join(str(int(k)) for k in kinds)
     lb = f"__launch_bounds__(256, {waves_per_simd})" if waves_per_simd else "__launch_bounds__(256)"
     src = ("#define CSV_UDOT4(a, b, c) __builtin_amdgcn_udot4((a), (b), (c), false)\n"
@@ -613,24 +609,12 @@ __device__ __forceinline__ unsigned int dq_eq80(unsigned int v, unsigned int pat
   const unsigned int x = v ^ pat;
   return ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x | 0x7F7F7F7Fu);
 }}
-// exclusive prefix sum of c (0 <= c < 2^B) over the wave's 64 lanes, and the wave total, with
-// no cross-lane data movement: c's bit planes are ballots, and mbcnt counts the set lanes below
-// (a __shfl_up scan is six dependent ds_bpermute round trips)
+// exclusive prefix sum of c over the wave's 64 lanes, and the wave total: an inclusive DPP scan,
+// row_shr 1, 2, 4, 8 within each 16-lane row (zero fill), then row_bcast 15 / 31 across rows --
+// six DPP adds, the total from lane 63 (seven ballot bit planes with mbcnt measured 3 % slower
+// over the whole action, profiles/r5_cutter.md)
 template <int B>
-__device__ __forceinline__ int dq_wave_prefix_ballot(int c, int& total) {{
-  int pre = 0, tot = 0;
-#pragma unroll
-  for (int b = 0; b < B; ++b) {{
-    const unsigned long long bal = __ballot((c >> b) & 1);
-    pre += (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bal, 0u)) << b;
-    tot += __popcll(bal) << b;
-  }}
-  total = tot;
-  return pre;
-}}
-// the same by an inclusive DPP scan: row_shr 1, 2, 4, 8 within each 16-lane row (zero fill),
-// then row_bcast 15 / 31 across rows -- six DPP adds, and the wave total from lane 63
-__device__ __forceinline__ int dq_wave_prefix_dpp(int c, int& total) {{
+__device__ __forceinline__ int dq_wave_prefix(int c, int& total) {{
   int v = c;
   v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, false);
   v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, false);
@@ -640,10 +624,6 @@ __device__ __forceinline__ int dq_wave_prefix_dpp(int c, int& total) {{
   v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xC, 0xF, false);
   total = __builtin_amdgcn_readlane(v, 63);
   return v - c;
-}}
-template <int B>
-__device__ __forceinline__ int dq_wave_prefix(int c, int& total) {{
-  return {scan_impl}(c, total);
 }}
 // 0x80 in every byte of v that is the separator or the terminator.  A byte's low seven bits
 // differ from a pattern's iff bit 7 of ((x & 0x7F) + 0x7F) is set (x = byte ^ pattern); both
@@ -906,7 +886,7 @@ def _compile(nodes, rel, d: int):
     quoted = not f.get("fast_only") and bool(f.get("quoted_fast"))
     key = (parts, udfs, tuple(rel.schema().names), tuple(f["kinds"]), repr(sorted(f["opts"].items())), H, d, term,
            crlf, min_line, int(f.get("max_line", 1 << 30)), quoted, os.environ.get("DQ4ML_CUT_ABLATE"),
-           os.environ.get("DQ4ML_CUT_STAMPS"), os.environ.get("DQ4ML_CUT_TILEORD"), os.environ.get("DQ4ML_CUT_SCAN"))
+           os.environ.get("DQ4ML_CUT_STAMPS"))
     if key in _CACHE:
         return _CACHE[key]
     base = _ScanBase(rel.schema(), 0, f["device"])
