@@ -242,6 +242,15 @@ def kernel_source(g, kinds, nullable, used, opts: dict, strict: bool, head: int,
     # work, 2 no stores, 4 no look-back, 8 no line-end scatter / line loop, 16 no ticket, 32 no LDS
     # staging stores, 64 no SWAR field conversion, 128 no Gram accumulation, 256 no Gram epilogue
     abl = int(os.environ.get("DQ4ML_SCAN_ABL", "0"))
+    if _dpp():
+        scan_code = "  int inc = dq_scan_incl(c);"
+    else:
+        scan_code = """  int inc = c;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int t = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += t;
+  }"""
 
     def field_code(c: int, swar: bool) -> str:
         if int(kinds[c]) == 4:  # a string column the chain does not read: cut past its field only
@@ -371,6 +380,33 @@ typedef unsigned int csv_u32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ void dq_flag(unsigned int* f, unsigned int v) {{
   __hip_atomic_fetch_or((DQG unsigned int*)f, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }}
+// inclusive wave scan by DPP: row_shr 1, 2, 4, 8 inside each 16-lane row (zero fill), then
+// row_bcast 15 / 31 across rows; lane 63 ends with the wave total
+__device__ __forceinline__ int dq_scan_incl(int v) {{
+  v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, false);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, false);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xF, 0xF, false);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xF, 0xF, false);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xA, 0xF, false);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xC, 0xF, false);
+  return v;
+}}
+// the f64 wave sum by the same DPP steps on the two halves (fixed order); the total in lane 63
+template <int CTRL, int RM>
+__device__ __forceinline__ double dq_dpp_f64(double x) {{
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(x), CTRL, RM, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(x), CTRL, RM, 0xF, false);
+  return __hiloint2double(hi, lo);
+}}
+__device__ __forceinline__ double dq_sum63(double x) {{
+  x += dq_dpp_f64<0x111, 0xF>(x);
+  x += dq_dpp_f64<0x112, 0xF>(x);
+  x += dq_dpp_f64<0x114, 0xF>(x);
+  x += dq_dpp_f64<0x118, 0xF>(x);
+  x += dq_dpp_f64<0x142, 0xA>(x);
+  x += dq_dpp_f64<0x143, 0xC>(x);
+  return x;
+}}
 
 // one line: parse every field into registers, run the DQ chain, store the needed outputs at li
 template <typename PB, typename IT>
@@ -445,12 +481,7 @@ __device__ __forceinline__ void dq_row(PB B, IT bias, IT start, IT end, long lon
     if (r >= 0 && r < 64) m |= 1ull << r;
   }}
   const int c = __popcll(m);
-  int inc = c;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {{
-    const int t = __shfl_up(inc, o, 64);
-    if (lane >= o) inc += t;
-  }}
+{scan_code}
   if (lane == 63) wtot[wave] = inc;
   if (wave == 0) {{
     // the terminator before the window's first line: nearest first, through the staged head
@@ -541,7 +572,14 @@ __device__ __forceinline__ void dq_row(PB B, IT bias, IT start, IT end, long lon
 
 def _gram_epilogue(d: int, slots: dict) -> str:
     nv = gram_width(d)
-    red = "".join(f"""  {{
+    if _dpp():  # DPP steps, the sum in lane 63 (no ds_bpermute round trips)
+        red = "".join(f"""  {{
+    const double t = dq_sum63(acc[{k}]);
+    if (lane == 63) gred[wave][{k}] = t;
+  }}
+""" for k in range(nv))
+    else:
+        red = "".join(f"""  {{
     double t = acc[{k}];
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o, 64);
@@ -569,6 +607,11 @@ class _ScanBase:
         self.nrows = int(nrows)
         self.sel = None
         self.device = device
+
+
+def _dpp() -> bool:
+    """Wave scans and sums of the per-line kernel by DPP (default) or by ds_bpermute shuffles."""
+    return os.environ.get("DQ4ML_SCAN_DPP", "1") != "0"
 
 
 def _scan_gen(base: _ScanBase, nullable):
@@ -670,7 +713,7 @@ def _compile(nodes, rel, gram: int = 0):
     key = (parts, udfs, tuple(rel.schema().names), tuple(f["kinds"]), tuple(f["nullable"]),
            repr(sorted(f["opts"].items())), f["strict"], head, lookback, fast_only, _wpe(fast_only),
            ticket, os.environ.get("DQ4ML_SCAN_ABL", "0"), gram, _scan_nt(), nolb, os.environ.get("DQ4ML_SCAN_P10"),
-           term_only)
+           term_only, _dpp())
     cp = _CACHE.get(key)
     if cp is None and key not in _CACHE:
         base = _ScanBase(rel.schema(), 0, f["device"])
@@ -892,7 +935,7 @@ class _Route:
 
 _ROUTES: dict = {}
 _ROUTE_ENV = ("DQ4ML_SCAN_GRAM", "DQ4ML_SCAN_CUT", "DQ4ML_CUT_MIN_LINE", "DQ4ML_SCAN_LOOKBACK", "DQ4ML_SCAN_GRAM_NOLB",
-              "DQ4ML_SCAN_TERM1", "DQ4ML_SCAN_FASTONLY", "DQ4ML_SCAN_ABL", "DQ4ML_SCAN_P10", "DQ4ML_CUT_ABLATE",
+              "DQ4ML_SCAN_TERM1", "DQ4ML_SCAN_FASTONLY", "DQ4ML_SCAN_ABL", "DQ4ML_SCAN_P10", "DQ4ML_SCAN_DPP", "DQ4ML_CUT_ABLATE",
               "DQ4ML_CUT_STAMPS", "DQ4ML_SCAN_STREAM", "DQ4ML_SCAN_NT", "DQ4ML_SCAN_TICKET",
               "DQ4ML_FUSE_ROUTES")
 
