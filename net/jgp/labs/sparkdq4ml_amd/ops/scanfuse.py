@@ -242,15 +242,9 @@ def kernel_source(g, kinds, nullable, used, opts: dict, strict: bool, head: int,
     # work, 2 no stores, 4 no look-back, 8 no line-end scatter / line loop, 16 no ticket, 32 no LDS
     # staging stores, 64 no SWAR field conversion, 128 no Gram accumulation, 256 no Gram epilogue
     abl = int(os.environ.get("DQ4ML_SCAN_ABL", "0"))
-    if _dpp():
-        scan_code = "  int inc = dq_scan_incl(c);"
-    else:
-        scan_code = """  int inc = c;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int t = __shfl_up(inc, o, 64);
-    if (lane >= o) inc += t;
-  }"""
+    # the window's line-end counts scanned by DPP (six __shfl_up ds_bpermute steps measured 1.2 %
+    # slower over the lab action: profiles/r5/lab_dpp_ab.jsonl)
+    scan_code = "  int inc = dq_scan_incl(c);"
 
     def field_code(c: int, swar: bool) -> str:
         if int(kinds[c]) == 4:  # a string column the chain does not read: cut past its field only
@@ -572,18 +566,10 @@ __device__ __forceinline__ void dq_row(PB B, IT bias, IT start, IT end, long lon
 
 def _gram_epilogue(d: int, slots: dict) -> str:
     nv = gram_width(d)
-    if _dpp():  # DPP steps, the sum in lane 63 (no ds_bpermute round trips)
-        red = "".join(f"""  {{
+    # DPP steps, the sum in lane 63 (no ds_bpermute round trips)
+    red = "".join(f"""  {{
     const double t = dq_sum63(acc[{k}]);
     if (lane == 63) gred[wave][{k}] = t;
-  }}
-""" for k in range(nv))
-    else:
-        red = "".join(f"""  {{
-    double t = acc[{k}];
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o, 64);
-    if (lane == 0) gred[wave][{k}] = t;
   }}
 """ for k in range(nv))
     return f"""  // this window's statistics: wave sums, then the 4 waves in a fixed order (deterministic)
@@ -607,11 +593,6 @@ class _ScanBase:
         self.nrows = int(nrows)
         self.sel = None
         self.device = device
-
-
-def _dpp() -> bool:
-    """Wave scans and sums of the per-line kernel by DPP (default) or by ds_bpermute shuffles."""
-    return os.environ.get("DQ4ML_SCAN_DPP", "1") != "0"
 
 
 def _scan_gen(base: _ScanBase, nullable):
@@ -713,7 +694,7 @@ def _compile(nodes, rel, gram: int = 0):
     key = (parts, udfs, tuple(rel.schema().names), tuple(f["kinds"]), tuple(f["nullable"]),
            repr(sorted(f["opts"].items())), f["strict"], head, lookback, fast_only, _wpe(fast_only),
            ticket, os.environ.get("DQ4ML_SCAN_ABL", "0"), gram, _scan_nt(), nolb, os.environ.get("DQ4ML_SCAN_P10"),
-           term_only, _dpp())
+           term_only)
     cp = _CACHE.get(key)
     if cp is None and key not in _CACHE:
         base = _ScanBase(rel.schema(), 0, f["device"])
@@ -935,7 +916,7 @@ class _Route:
 
 _ROUTES: dict = {}
 _ROUTE_ENV = ("DQ4ML_SCAN_GRAM", "DQ4ML_SCAN_CUT", "DQ4ML_CUT_MIN_LINE", "DQ4ML_SCAN_LOOKBACK", "DQ4ML_SCAN_GRAM_NOLB",
-              "DQ4ML_SCAN_TERM1", "DQ4ML_SCAN_FASTONLY", "DQ4ML_SCAN_ABL", "DQ4ML_SCAN_P10", "DQ4ML_SCAN_DPP", "DQ4ML_CUT_ABLATE",
+              "DQ4ML_SCAN_TERM1", "DQ4ML_SCAN_FASTONLY", "DQ4ML_SCAN_ABL", "DQ4ML_SCAN_P10", "DQ4ML_CUT_ABLATE",
               "DQ4ML_CUT_STAMPS", "DQ4ML_SCAN_STREAM", "DQ4ML_SCAN_NT", "DQ4ML_SCAN_TICKET",
               "DQ4ML_FUSE_ROUTES")
 
