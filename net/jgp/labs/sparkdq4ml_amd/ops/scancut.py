@@ -156,12 +156,6 @@ class _Shape:
         self.RG = max(1, 256 // self.U) if self.blocked else 1
         # the MFMA Gram (v_mfma_f64_16x16x4_f64 over 16-feature tiles of the row tile): d + 2 <= 80;
         # waves split into G tile groups x (4 / G) row groups, <= 32 accumulator VGPRs per wave
-        self.NT16 = (d + 2 + 15) // 16
-        self.tiles = [(I, J) for I in range(self.NT16) for J in range(I, self.NT16)]
-        self.mfma = self.blocked and d + 2 <= 80
-        if self.mfma:
-            self.G = next((g for g in (1, 2, 4) if -(-len(self.tiles) // g) * 8 <= 32), 4)
-            self.RG = 4 // self.G
         self.ucols = ucols                              # columns the chain reads, in vt order
         self.CU = max(1, len(ucols))
         self.feat = feat                                # passthrough feature columns (blocked only)
@@ -169,6 +163,16 @@ class _Shape:
         # (the label's source) lands at slot d, so the converter stores each field straight into
         # the tile ([x | y | 1] order) and the chain reads its inputs from there
         self.yfirst = d > 8 and feat == list(range(d)) and C == d + 1
+        self.mfma = self.blocked and d + 2 <= 80
+        # the [y | 1] strip (sums of x y, x, y, y^2 and the count: 2 d + 3 of the gram_width slots)
+        # on the VALU beside the MFMA tiles of x x^T: the strip's MFMA panel is mostly padding
+        # (2 of 16 columns at d = 32, a third of the tiles)
+        self.vstrip = self.mfma and self.yfirst and os.environ.get("DQ4ML_CUT_VSTRIP", "1") != "0"
+        self.NT16 = (d + (0 if self.vstrip else 2) + 15) // 16
+        self.tiles = [(I, J) for I in range(self.NT16) for J in range(I, self.NT16)]
+        if self.mfma:
+            self.G = next((g for g in (1, 2, 4) if -(-len(self.tiles) // g) * 8 <= 32), 4)
+            self.RG = 4 // self.G
         per_row = 8 * (self.CU + (self.PP if self.blocked else 0))
         self.gw = gram_width(d)
         fixed = (16 + H + self.W + 32) + 2 * self.DCAP + 4 * C + 384 + (
@@ -264,15 +268,58 @@ def _mfma_gram(sh, slots):
         }}}}
 """)
     gram_phase = "".join(bodies).replace("{{", "{").replace("}}", "}")
-    # (lane, e) -> gram_width slot of each tile (-1: lower half of a diagonal tile or padding)
+    # (lane, e) -> gram_width slot of each tile (-1: lower half of a diagonal tile or padding;
+    # with the VALU strip, also the tiles' y and 1 columns)
     tabs = []
     for I, J in tiles:
         for lane in range(64):
             for e in range(4):
                 i, j = 16 * I + (lane >> 4) + 4 * e, 16 * J + (lane & 15)
-                k = _tile_slot(sh, i, j)
+                k = None if sh.vstrip and max(i, j) >= d else _tile_slot(sh, i, j)
                 tabs.append(-1 if k is None else k)
     tables = f"__device__ const short DQ_TIDX[{len(tiles) * 256}] = {{{', '.join(str(x) for x in tabs)}}};\n"
+    if sh.vstrip:
+        # the strip: lane l of every wave owns sums s = l + 64 k (x_c y for s < d, x_c for
+        # d <= s < 2 d) over the rows r = wave (mod 4) of every tile; the row phase sums y, y^2
+        # and the live rows per thread; both reduce once at the end in a fixed order
+        KS = -(-2 * d // 64)
+        assert 4 * 64 * KS + 12 <= (sh.RR + 3) * PP + 16  # the epilogue's scratch (the tile array)
+        acc_decl += "".join(f"  double sacc{k} = 0.0;\n  const int sc{k} = (lane + {64 * k}) % {d}, "
+                            f"sw{k} = lane + {64 * k} < {d} ? {d} : {d + 1};\n" for k in range(KS))
+        acc_decl += "  double sn_ = 0.0, sy_ = 0.0, syy_ = 0.0;\n"
+        fm = "".join(f"          sacc{k} = __builtin_fma(gs[sc{k}], gs[sw{k}], sacc{k});\n" for k in range(KS))
+        gram_phase += f"""        for (int r = wave; r < nr; r += 4) {{
+          const double* __restrict__ gs = gt + r * {PP};
+{fm}        }}
+"""
+        sl = []
+        for s_ in range(64 * KS):
+            k = _tile_slot(sh, s_ % d, d if s_ < d else d + 1) if s_ < 2 * d else None
+            sl.append(-1 if k is None else k)
+        sl += [_tile_slot(sh, d + 1, d + 1), _tile_slot(sh, d, d + 1), _tile_slot(sh, d, d)]
+        tables += f"__device__ const short DQ_SSLOT[{len(sl)}] = {{{', '.join(str(x) for x in sl)}}};\n"
+        red = "".join(f"""    {{
+      double t = {v};
+      for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o, 64);
+      if (lane == 0) gt[{4 * 64 * KS} + wave * 3 + {j}] = t;
+    }}
+""" for j, v in enumerate(("sn_", "sy_", "syy_")))
+        strip_ep = (f"""  __syncthreads();  // (the tile array is the reduction scratch from here)
+  {{
+""" + "".join(f"    gt[wave * {64 * KS} + {64 * k} + lane] = sacc{k};\n" for k in range(KS)) + red + f"""  }}
+  __syncthreads();
+  if (wave == 0) {{
+    DQG double* __restrict__ g0 = (DQG double*)p[{slots['gpart']}] + (long long)blockIdx.x * {RG * GW};
+    for (int s = lane; s < {64 * KS + 3}; s += 64) {{
+      const int slot = DQ_SSLOT[s];
+      const int b = s < {64 * KS} ? s : {4 * 64 * KS} + (s - {64 * KS});
+      const int st = s < {64 * KS} ? {64 * KS} : 3;
+      if (slot >= 0) g0[slot] = (gt[b] + gt[b + st]) + (gt[b + 2 * st] + gt[b + 3 * st]);
+    }}
+  }}
+""")
+    else:
+        strip_ep = ""
     ep = []
     for g, tl in enumerate(groups):
         wr = "".join(f"""      for (int e = 0; e < 4; ++e) {{
@@ -282,7 +329,7 @@ def _mfma_gram(sh, slots):
 """ for k, t in enumerate(tl))
         ep.append(f"    if (gtg == {g}) {{\n{wr}    }}\n")
     epilogue = (f"  {{\n    DQG double* __restrict__ gp = (DQG double*)p[{slots['gpart']}] + "
-                f"((long long)blockIdx.x * {RG} + grg) * {GW};\n" + "".join(ep) + "  }\n")
+                f"((long long)blockIdx.x * {RG} + grg) * {GW};\n" + "".join(ep) + "  }\n" + strip_ep)
     return acc_decl, gram_phase, epilogue, tables
 
 
@@ -506,7 +553,11 @@ def kernel_source(g, kinds, used, opts: dict, H: int, slots: dict, d: int, term:
             outs += "".join(f"      gr[{i}] = live ? (double)({v}) : 0.0;\n" for i, v in enumerate(xs))
         else:
             outs += f"      if (!live) {{\n#pragma unroll\n        for (int i = 0; i < {d}; ++i) gr[i] = 0.0;\n      }}\n"
-        if sh.yfirst:  # (gr[d] held the label column, read above as a chain input)
+        if sh.vstrip:  # (+ the strip's y, y^2 and count sums of this thread's rows)
+            outs += (f"      const double yv_ = live ? (double)({yv}) : 0.0;\n      gr[{d}] = yv_;\n"
+                     f"      gr[{d + 1}] = live ? 1.0 : 0.0;\n      sn_ += live ? 1.0 : 0.0;\n"
+                     f"      sy_ += yv_;\n      syy_ = __builtin_fma(yv_, yv_, syy_);\n")
+        elif sh.yfirst:  # (gr[d] held the label column, read above as a chain input)
             outs += f"      gr[{d}] = live ? (double)({yv}) : 0.0;\n      gr[{d + 1}] = live ? 1.0 : 0.0;\n"
         else:
             outs += f"      gr[{d}] = live ? 1.0 : 0.0;\n      gr[{d + 1}] = live ? (double)({yv}) : 0.0;\n"
@@ -886,7 +937,7 @@ def _compile(nodes, rel, d: int):
     quoted = not f.get("fast_only") and bool(f.get("quoted_fast"))
     key = (parts, udfs, tuple(rel.schema().names), tuple(f["kinds"]), repr(sorted(f["opts"].items())), H, d, term,
            crlf, min_line, int(f.get("max_line", 1 << 30)), quoted, os.environ.get("DQ4ML_CUT_ABLATE"),
-           os.environ.get("DQ4ML_CUT_STAMPS"))
+           os.environ.get("DQ4ML_CUT_STAMPS"), os.environ.get("DQ4ML_CUT_VSTRIP"))
     if key in _CACHE:
         return _CACHE[key]
     base = _ScanBase(rel.schema(), 0, f["device"])

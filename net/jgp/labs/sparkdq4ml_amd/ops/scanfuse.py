@@ -917,7 +917,7 @@ class _Route:
 _ROUTES: dict = {}
 _ROUTE_ENV = ("DQ4ML_SCAN_GRAM", "DQ4ML_SCAN_CUT", "DQ4ML_CUT_MIN_LINE", "DQ4ML_SCAN_LOOKBACK", "DQ4ML_SCAN_GRAM_NOLB",
               "DQ4ML_SCAN_TERM1", "DQ4ML_SCAN_FASTONLY", "DQ4ML_SCAN_ABL", "DQ4ML_SCAN_P10", "DQ4ML_CUT_ABLATE",
-              "DQ4ML_CUT_STAMPS", "DQ4ML_SCAN_STREAM", "DQ4ML_SCAN_NT", "DQ4ML_SCAN_TICKET",
+              "DQ4ML_CUT_STAMPS", "DQ4ML_CUT_VSTRIP", "DQ4ML_SCAN_STREAM", "DQ4ML_SCAN_NT", "DQ4ML_SCAN_TICKET",
               "DQ4ML_FUSE_ROUTES")
 
 

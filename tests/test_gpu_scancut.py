@@ -70,7 +70,7 @@ def _write(tmp_path, n, d, term=b"\r", seed=5):
 
 
 @pytest.mark.parametrize("d,n,term", [(32, 150_001, b"\r"), (8, 90_000, b"\n"), (9, 90_000, b"\r\n"),
-                                      (64, 40_003, b"\r"), (3, 70_000, b"\r")])
+                                      (64, 40_003, b"\r"), (3, 70_000, b"\r"), (40, 40_001, b"\n")])
 def test_cutter_gram_matches_fp64_oracle(spark, tmp_path, d, n, term):
     from net.jgp.labs.sparkdq4ml_amd.ops import scancut
 
