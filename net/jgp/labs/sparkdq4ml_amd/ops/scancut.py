@@ -246,7 +246,7 @@ def _mfma_gram(sh, slots):
     TW = max(len(t) for t in groups)
     acc_decl = (f"  typedef double f64x4 __attribute__((ext_vector_type(4)));\n"
                 f"  f64x4 gacc[{TW}];\n#pragma unroll\n  for (int t = 0; t < {TW}; ++t) gacc[t] = f64x4{{0.0, 0.0, 0.0, 0.0}};\n"
-                f"  const int gtg = wave % {G}, grg = wave / {G};\n")
+                f"  const int gtg = __builtin_amdgcn_readfirstlane(wave) % {G}, grg = __builtin_amdgcn_readfirstlane(wave) / {G};\n")
     bodies = []
     for g, tl in enumerate(groups):
         panels = sorted({x for t in tl for x in t})
@@ -287,8 +287,17 @@ def _mfma_gram(sh, slots):
         acc_decl += "".join(f"  double sacc{k} = 0.0;\n  const int sc{k} = (lane + {64 * k}) % {d}, "
                             f"sw{k} = lane + {64 * k} < {d} ? {d} : {d + 1};\n" for k in range(KS))
         acc_decl += "  double sn_ = 0.0, sy_ = 0.0, syy_ = 0.0;\n"
+        # (a wave-uniform loop, 4 rows per trip with every read issued before the FMAs: one row
+        # per trip waited on each read pair)
+        rd = "".join(f"          const double a{k}{u} = gs[{u * 4 * PP} + sc{k}], b{k}{u} = gs[{u * 4 * PP} + sw{k}];\n"
+                     for u in range(4) for k in range(KS))
+        fm4 = "".join(f"          sacc{k} = __builtin_fma(a{k}{u}, b{k}{u}, sacc{k});\n" for u in range(4) for k in range(KS))
         fm = "".join(f"          sacc{k} = __builtin_fma(gs[sc{k}], gs[sw{k}], sacc{k});\n" for k in range(KS))
-        gram_phase += f"""        for (int r = wave; r < nr; r += 4) {{
+        gram_phase += f"""        int r = __builtin_amdgcn_readfirstlane(wave);
+        for (; r + 12 < nr; r += 16) {{
+          const double* __restrict__ gs = gt + r * {PP};
+{rd}{fm4}        }}
+        for (; r < nr; r += 4) {{
           const double* __restrict__ gs = gt + r * {PP};
 {fm}        }}
 """
