@@ -153,3 +153,21 @@ def test_cutter_preconditions():
     assert scancut.applicable(dict(base, fast_only=False, quoted_fast=True)) == 512
     assert scancut.term_of(dict(base, term_kinds=[0, 9, 0])) == (10, False)
     assert scancut.term_of(dict(base, term_kinds=[9, 0, 9])) == (13, True)
+
+
+@pytest.mark.parametrize("d", [9, 32, 40, 64])
+def test_vstrip_tables_cover_gram_width_once(cpu_session, d):
+    """With the [y | 1] strip on the VALU, the MFMA tiles' index table writes only the x x^T
+    slots and the strip's table the 2 d + 3 others: together every gram_width slot once."""
+    import re
+
+    src = _cut_source(cpu_session, d, False)
+    tab = {}
+    for name in ("DQ_TIDX", "DQ_SSLOT"):
+        m = re.search(name + r"\[\d+\] = \{([^}]*)\}", src)
+        assert m is not None, name
+        tab[name] = [int(v) for v in m.group(1).split(",") if int(v) >= 0]
+    GW = scancut.gram_width(d)
+    assert sorted(tab["DQ_SSLOT"]) == list(range(3 + 2 * d))
+    assert sorted(tab["DQ_TIDX"]) == list(range(3 + 2 * d, GW))
+    assert "sn_ += live ? 1.0 : 0.0;" in src  # the count, Σy and Σy² from the row phase
