@@ -262,9 +262,11 @@ def _mfma_gram(sh, slots):
           const int ki = 4 * grg < nr ? 4 * grg : 0;
           const double* __restrict__ gr = gt + (ki + (lane >> 4)) * {PP} + (lane & 15);
 {first}          for (int k0 = 4 * grg; k0 < nr; k0 += {4 * RG}) {{{{
+/*SRD*/
             const int kn = k0 + {4 * RG} < nr ? k0 + {4 * RG} : k0;
             const double* __restrict__ gq = gt + (kn + (lane >> 4)) * {PP} + (lane & 15);
-{reads}{mf}{shift}          }}}}
+{reads}{mf}/*SFM*/
+{shift}          }}}}
         }}}}
 """)
     gram_phase = "".join(bodies).replace("{{", "{").replace("}}", "}")
@@ -287,19 +289,21 @@ def _mfma_gram(sh, slots):
         acc_decl += "".join(f"  double sacc{k} = 0.0;\n  const int sc{k} = (lane + {64 * k}) % {d}, "
                             f"sw{k} = lane + {64 * k} < {d} ? {d} : {d + 1};\n" for k in range(KS))
         acc_decl += "  double sn_ = 0.0, sy_ = 0.0, syy_ = 0.0;\n"
-        # (a wave-uniform loop, 4 rows per trip with every read issued before the FMAs: one row
-        # per trip waited on each read pair)
-        rd = "".join(f"          const double a{k}{u} = gs[{u * 4 * PP} + sc{k}], b{k}{u} = gs[{u * 4 * PP} + sw{k}];\n"
+        # 4 rows per trip with every read issued before the FMAs (one row per trip had waited on
+        # each read pair); wave w takes rows 4 w .. 4 w + 3 (mod 16), so a trip never passes the
+        # three zeroed rows past the tile
+        rd = "".join(f"            const double a{k}{u} = gs[{u * PP} + sc{k}], b{k}{u} = gs[{u * PP} + sw{k}];\n"
                      for u in range(4) for k in range(KS))
-        fm4 = "".join(f"          sacc{k} = __builtin_fma(a{k}{u}, b{k}{u}, sacc{k});\n" for u in range(4) for k in range(KS))
-        fm = "".join(f"          sacc{k} = __builtin_fma(gs[sc{k}], gs[sw{k}], sacc{k});\n" for k in range(KS))
-        gram_phase += f"""        int r = __builtin_amdgcn_readfirstlane(wave);
-        for (; r + 12 < nr; r += 16) {{
+        fm4 = "".join(f"            sacc{k} = __builtin_fma(a{k}{u}, b{k}{u}, sacc{k});\n" for u in range(4) for k in range(KS))
+        if G == 1:
+            # inside the MFMA k-loop: the wave's k-steps are its strip rows, and the strip's
+            # reads and FMAs run beside the k-step's MFMAs
+            gram_phase = gram_phase.replace("/*SRD*/\n", f"            const double* __restrict__ gs = gt + k0 * {PP};\n" + rd)
+            gram_phase = gram_phase.replace("/*SFM*/\n", fm4)
+        else:
+            gram_phase += f"""        for (int r = 4 * __builtin_amdgcn_readfirstlane(wave); r < nr; r += 16) {{
           const double* __restrict__ gs = gt + r * {PP};
 {rd}{fm4}        }}
-        for (; r < nr; r += 4) {{
-          const double* __restrict__ gs = gt + r * {PP};
-{fm}        }}
 """
         sl = []
         for s_ in range(64 * KS):
@@ -339,6 +343,7 @@ def _mfma_gram(sh, slots):
         ep.append(f"    if (gtg == {g}) {{\n{wr}    }}\n")
     epilogue = (f"  {{\n    DQG double* __restrict__ gp = (DQG double*)p[{slots['gpart']}] + "
                 f"((long long)blockIdx.x * {RG} + grg) * {GW};\n" + "".join(ep) + "  }\n" + strip_ep)
+    gram_phase = gram_phase.replace("/*SRD*/\n", "").replace("/*SFM*/\n", "")
     return acc_decl, gram_phase, epilogue, tables
 
 
