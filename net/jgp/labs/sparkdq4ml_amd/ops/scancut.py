@@ -181,7 +181,13 @@ class _Shape:
         # within [4 KiB, TILE_BYTES]: more rounds per window beat fewer resident blocks
         tile = max(4096, min(TILE_BYTES, (160 * 1024) // TARGET_PER_CU - fixed))
         self.RR = int(max(1, min(rows_max, tile // per_row)))
-        self.lds = fixed + 8 * self.RR * self.CU + (8 * ((self.RR + 3) * self.PP + 16) if self.blocked else 0)
+        # (fixed holds the row tile's 3 zero rows and 16 padding doubles; round 5 counted them twice,
+        # which held d = 64 at 3 blocks per CU: 22.68 -> 20.96 ms at 5e7 x 64 with 4)
+        self.lds = fixed + 8 * self.RR * self.CU + (8 * self.RR * self.PP if self.blocked else 0)
+        if self.blocked and (not self.mfma or len(self.tiles) > 10):
+            # 15 MFMA tiles (d > 64) or the VALU Gram: the accumulators spill at the 128 VGPRs of
+            # 4 blocks per CU
+            self.lds = max(self.lds, (160 * 1024) // 3)
         self.gw = gram_width(d)
 
 
