@@ -31,6 +31,9 @@ def main(argv=None):
     ap.add_argument("--features", type=int, default=4096)
     ap.add_argument("--dtype", default="fp8", choices=["fp8", "bf16"])
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--sync", action="store_true",
+                    help="synchronous fits (host-checked PCG chunks; default: asynchronous, the whole "
+                         "fit enqueued with no host read and its tail on a side stream beside the next SYRK)")
     a = ap.parse_args(argv)
     rc = self_launch(a.gpus, __file__, argv)  # --gpus N: one process per GPU, before any GPU call
     if rc is not None:
@@ -47,7 +50,8 @@ def main(argv=None):
     if not check_world(a.gpus):
         return 2
     rank, world = comm.rank(), comm.world_size()
-    spark = SparkSession.builder().appName("bench-wide").master("local[*]").getOrCreate()
+    spark = SparkSession.builder().appName("bench-wide").master("local[*]") \
+        .config("dq4ml.fit.async", "false" if a.sync else "true").getOrCreate()
     dev = spark.device
     d, total = a.features, int(a.rows)
     if dev.type != "cuda":  # host-engine rehearsal of the launcher / JSON contract: small dense shape
@@ -99,7 +103,8 @@ def _report(a, lr, df, beta, total, world, d, n, dev, timed, emit, world_info, c
           "data": "synthetic (N(0,1) features, random-init coefficients)",
           "config": {"model": f"LinearRegression(normal equations, L2 0.01) d={d}", "global_batch": total,
                      "seq_len": d, "parallelism": f"dp{world}", "rows_per_gpu": n,
-                     "useful_tflops": total * d * (d + 1) / (ms * 1e-3) / 1e12, "coef_max_abs_err": err},
+                     "useful_tflops": total * d * (d + 1) / (ms * 1e-3) / 1e12, "coef_max_abs_err": err,
+                     "fit_mode": "sync" if a.sync or dev.type != "cuda" else "async"},
           **info}, a.json_out)
     comm.shutdown()
     return 0

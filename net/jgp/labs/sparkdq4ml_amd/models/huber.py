@@ -2,12 +2,14 @@
 
     L(c, b, σ) = 1/W Σ_i w_i [ σ + H_ε(y_i - x_i·c/σ_x - b)/σ ... ] / 2 + L2(c)
 
-optimized over (coefficients in the std-scaled space, intercept, σ) with σ > 0 — Spark uses
-Breeze ``LBFGSB``; here a projected L-BFGS (two-loop direction, projection of σ onto its lower
-bound, backtracking Armijo search).  The optimum is the same (the problem is convex in that
-parametrization); iteration counts / objectiveHistory lengths are not pinned to Breeze's.
-Each evaluation is one fused device pass (``kernels.huber_pass``: margin -> loss/multipliers,
-then Xᵀm) plus one all-reduce of d+4 f64.
+optimized over (coefficients in the std-scaled space, intercept, σ) from all ones, with the bounds
+Spark passes to Breeze's ``LBFGSB`` (every coordinate in [Double.MinValue, Double.MaxValue], σ >=
+Double.MinPositiveValue) and memory 10: :class:`.lbfgsb.LBFGSB` reproduces that optimizer's
+algorithm -- generalized Cauchy point, direct primal subspace minimization, strong-Wolfe search
+on the unprojected ray, Breeze's convergence checks -- so iteration counts and
+``objectiveHistory`` follow it.  Each evaluation is one fused device pass
+(``kernels.huber_pass``: margin -> loss/multipliers, then Xᵀm) plus one all-reduce of d+4 f64;
+the optimizer's O(k m) bookkeeping runs on the host between passes.
 """
 from __future__ import annotations
 
@@ -16,11 +18,13 @@ import numpy as np
 from ..ops import kernels
 from ..parallel import comm
 from ..utils.logging import get_logger
+from .lbfgsb import LBFGSB, LBFGSBState
 from .linalg import DenseVector
 from .optim import GramStats
 
 log = get_logger("huber")
-MIN_SIGMA = np.finfo(np.float64).tiny
+MIN_SIGMA = 5e-324  # Double.MinPositiveValue: Spark's lower bound of σ
+_DMAX = float(np.finfo(np.float64).max)
 
 
 def train_huber(est, df, tbl, X, y, w, sel, d):
@@ -59,69 +63,28 @@ def train_huber(est, df, tbl, X, y, w, sel, d):
         g[-1] = g_sigma / wsum
         return f, g
 
-    lo = np.full(dim, -np.inf)
-    lo[-1] = MIN_SIGMA
+    lower = np.full(dim, -_DMAX)
+    lower[-1] = MIN_SIGMA
+    upper = np.full(dim, _DMAX)
     max_iter, tol = int(est.getOrDefault("maxIter")), float(est.getOrDefault("tol"))
+    opt = LBFGSB(lower, upper, max_iter, 10, tol)
     ck = _Checkpoint.of(df, flat, (d, dim, fit_icpt, eps, reg, std_flag, max_iter, tol))
-    state = ck.load() if ck is not None else None
+    resumed = ck.load() if ck is not None else None
+    state, hist0 = (resumed if resumed is not None else (None, []))
     if state is not None:  # resume: the exact optimizer state of the last checkpoint
-        start, theta, f, g, S, Y, hist, f_hist = state
-        log.info("resuming huber l-bfgs at iteration %d from %s", start, ck.path)
-    else:
-        start = 0
-        theta = np.ones(dim)
-        f, g = fg(theta)
-        hist = [f]
-        S, Y = [], []
-        f_hist = [np.inf]
-    for it in range(start, max_iter):
-        if ck is not None and it > start and it % ck.every == 0:
-            ck.save(it, theta, f, g, S, Y, hist, f_hist)
-        if _FAIL_AT_ITER is not None and it == _FAIL_AT_ITER:  # fault injection (tests)
-            raise RuntimeError(f"injected failure at huber iteration {it}")
-        # projected gradient convergence
-        pg = np.where((theta <= lo) & (g > 0), 0.0, g)
-        if np.linalg.norm(pg) <= max(tol * abs(f), 1e-8):
-            break
-        q = g.copy()
-        alphas = []
-        for s, yv in zip(reversed(S), reversed(Y)):
-            rho = 1.0 / np.dot(yv, s)
-            a = rho * np.dot(s, q)
-            alphas.append((a, rho, s, yv))
-            q -= a * yv
-        if S:
-            q *= np.dot(S[-1], Y[-1]) / np.dot(Y[-1], Y[-1])
-        for a, rho, s, yv in reversed(alphas):
-            b = rho * np.dot(yv, q)
-            q += (a - b) * s
-        direction = -q
-        direction = np.where((theta <= lo) & (direction < 0), 0.0, direction)
-        if np.dot(direction, g) >= 0:
-            direction = -pg
-            S, Y = [], []
-        step = 1.0 if it > 0 else min(1.0, 1.0 / max(np.linalg.norm(g), 1e-12))
-        while True:
-            cand = np.maximum(theta + step * direction, lo)
-            fc, gc = fg(cand)
-            if fc <= f + 1e-4 * np.dot(g, cand - theta) or step < 1e-12:
-                break
-            step *= 0.5
-        s, yv = cand - theta, gc - g
-        if np.dot(s, yv) > 1e-12:
-            S.append(s)
-            Y.append(yv)
-            if len(S) > 10:
-                S.pop(0)
-                Y.pop(0)
-        theta, f, g = cand, fc, gc
-        hist.append(f)
-        f_hist.append(f)
-        f_hist = f_hist[-20:]
-        if len(f_hist) >= 2 and abs(f - max(f_hist)) <= tol * abs(hist[0]):
-            break
+        log.info("resuming huber l-bfgs-b at iteration %d from %s", state.iter, ck.path)
+
+    def on_state(st, hist):
+        if ck is not None and st.iter % ck.every == 0:
+            ck.save(st, hist0[:-1] + hist if hist0 else hist)
+        if _FAIL_AT_ITER is not None and st.iter == _FAIL_AT_ITER:  # fault injection (tests)
+            raise RuntimeError(f"injected failure at huber iteration {st.iter}")
+    st, hist, why = opt.minimize(fg, np.ones(dim), state=state, on_state=on_state)
+    hist = hist0[:-1] + hist if hist0 else hist
+    log.info("l-bfgs-b (huber) converged: %s after %d iterations", why, st.iter)
     if ck is not None:
         ck.clear()
+    theta = st.x
     coef = np.where(sx != 0.0, theta[:d] / safe, 0.0)
     icpt = float(theta[d]) if fit_icpt else 0.0
     model = LinearRegressionModel(est.uid, DenseVector(coef), icpt, float(theta[-1]))
@@ -135,8 +98,9 @@ _FAIL_AT_ITER = None  # tests: raise at this iteration (simulated crash between 
 
 class _Checkpoint:
     """Optimizer-state checkpoints of the iterative (data-pass per evaluation) Huber fit
-    (SURVEY.md §5d): with ``dq4ml.lbfgs.checkpointDir`` set, the complete L-BFGS state (iterate,
-    value, gradient, the s/y memory, objective histories, next iteration) is written every
+    (SURVEY.md §5d): with ``dq4ml.lbfgs.checkpointDir`` set, the complete L-BFGS-B state (iterate,
+    value, gradient, θ and the s/y memory, the function-value window, failure flags, objective
+    history, iteration) is written every
     ``dq4ml.lbfgs.checkpointInterval`` iterations (atomic rename; rank 0 writes, every rank
     reads).  A re-run of the same fit — same parameters and the same data, fingerprinted by its
     all-reduced Gram statistics — resumes from it and finishes exactly as the uninterrupted run
@@ -160,27 +124,29 @@ class _Checkpoint:
         return cls(os.path.join(root, f"huber-{h.hexdigest()[:20]}.npz"),
                    int(sess.conf.get("dq4ml.lbfgs.checkpointInterval", "10")))
 
-    def save(self, it, theta, f, g, S, Y, hist, f_hist):
+    def save(self, st: LBFGSBState, hist):
         import os
 
         if comm.rank() != 0:
             return
-        dim = theta.shape[0]
+        dim = st.x.shape[0]
         tmp = self.path + ".tmp.npz"
-        np.savez(tmp, it=np.array(it), theta=theta, f=np.array(f), g=g,
-                 S=np.array(S).reshape(-1, dim), Y=np.array(Y).reshape(-1, dim),
-                 hist=np.array(hist), f_hist=np.array(f_hist))
+        np.savez(tmp, it=np.array(st.iter), x=st.x, f=np.array(st.value), g=st.grad, f0=np.array(st.initial_value),
+                 theta=np.array(st.theta), S=np.array(st.S).reshape(-1, dim), Y=np.array(st.Y).reshape(-1, dim),
+                 fvals=np.array(st.fvals), flags=np.array([st.failed_once, st.search_failed]), hist=np.array(hist))
         os.replace(tmp, self.path)
 
     def load(self):
+        """(state, objective history up to and including it) of the last checkpoint, or None."""
         import os
 
         comm.barrier()  # a rank-0 write of an earlier attempt is complete before anyone reads
         if not os.path.exists(self.path):
             return None
         z = np.load(self.path)  # allow_pickle=False: plain arrays only
-        return (int(z["it"]), z["theta"], float(z["f"]), z["g"], list(z["S"]), list(z["Y"]),
-                list(z["hist"]), list(z["f_hist"]))
+        st = LBFGSBState(z["x"], float(z["f"]), z["g"], int(z["it"]), float(z["f0"]), float(z["theta"]), list(z["S"]),
+                         list(z["Y"]), [float(v) for v in z["fvals"]], bool(z["flags"][0]), bool(z["flags"][1]))
+        return st, [float(v) for v in z["hist"]]
 
     def clear(self):
         import os

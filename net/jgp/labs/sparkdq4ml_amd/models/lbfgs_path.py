@@ -203,7 +203,13 @@ def _train_passes(est, df, X, y, w, sel, d, checks=(), device_qn=True):
     std_flag = bool(est.getOrDefault("standardization"))
     reg, enet = float(est.getOrDefault("regParam")), float(est.getOrDefault("elasticNetParam"))
     max_iter, tol = int(est.getOrDefault("maxIter")), float(est.getOrDefault("tol"))
-    if device_qn and _device_qn_ok(df, P):
+    use_dev = device_qn and _device_qn_ok(df, P) and P.qn_eligible()
+    if comm.collectives_active():
+        # the device fit and the host-steered one issue different collectives: every rank must
+        # take the same branch (a rank whose shard is empty, or holds another layout, would
+        # otherwise deadlock its peers) -- a host-side vote, no device sync
+        use_dev = comm.all_agree(use_dev)
+    if use_dev:
         with tracing.span("solve"):
             # X4: one (d + 2)-f64 all-reduce per evaluation, no host read.  DQ4ML_QN_SPLIT=1 runs
             # the same split form on one rank without a group (plain launches: counter runs)

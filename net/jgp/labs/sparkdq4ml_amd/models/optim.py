@@ -288,38 +288,49 @@ def _wls_device(flat, nf, fit_intercept, reg_param, elastic_net, standardize_fea
                 solver_type, max_iter, tol):
     """Large-k Cholesky branch of WLS on the device (f64; same algebra as ``wls.cpp``).
 
-    The standardized dense system is assembled by ``wls_large.hip`` (one prep + one tiled kernel,
-    no index scatter) and solved by the device Jacobi-PCG (two kernels per iteration, one host
-    read of the control block per chunk); rocSOLVER Cholesky is the fallback with dppsv's exact
-    non-SPD semantics."""
+    The standardized dense system is assembled by ``wls_large.hip`` (head scalars, one prep and one
+    tiled kernel, no index scatter, no host read) and solved by the device Jacobi-PCG (two kernels
+    per iteration, one host read of the control block per chunk); rocSOLVER Cholesky is the
+    fallback with dppsv's exact non-SPD semantics."""
+    from ..ops import device
+
+    sysm = device.wls_assemble(flat, nf, fit_intercept, reg_param, elastic_net, standardize_features,
+                               standardize_label)
+    if solver_type == "auto":
+        o = device.wls_pcg(sysm, nf, PCG_RTOL)
+    else:
+        o = sysm.o[:device.PCG_STATE_WORDS].cpu().numpy()
+    return wls_large_result(flat, sysm, o, nf, fit_intercept, reg_param, elastic_net, standardize_features,
+                            standardize_label, solver_type, max_iter, tol)
+
+
+def wls_large_result(flat, sysm, o, nf, fit_intercept, reg_param, elastic_net, standardize_features,
+                     standardize_label, solver_type, max_iter, tol):
+    """``(WLSModel, GramStats)`` of a large-k device solve from its host control block ``o``: the
+    PCG solution when it converged and passed its residual check, else the rocSOLVER Cholesky of
+    the assembled system; a short-circuit head (no weight, constant label) and a Cholesky failure
+    go to the native host driver, which owns those cases' warnings and errors."""
     import torch
 
     from ..ops import device
 
-    head = flat[:5].cpu().numpy()
+    head = np.asarray(o[device.PCG_HEAD:device.PCG_HEAD + 5], dtype=np.float64)
     stats = GramStats.scalars_only(head, nf)
-    count, wSum, _, bSum, bbSum = (float(v) for v in head)
-    rawBBar = bSum / wSum if wSum > 0 else 0.0
-    rawBStd = float(np.sqrt(max(bbSum / wSum - rawBBar * rawBBar, 0.0))) if wSum > 0 else 0.0
-    if wSum <= 0.0 or rawBStd == 0.0:  # rare short-circuits: the native driver owns their semantics
+    if o[device.PCG_STATUS] != 0.0:  # rare short-circuits: the native driver owns their semantics
         host = flat.cpu().numpy()
         full = GramStats.from_flat(host, nf)
         return _wls_native(host, full, fit_intercept, reg_param, elastic_net, standardize_features,
                            standardize_label, solver_type, max_iter, tol), full
     if reg_param == 0.0:
         log.warning("regParam is zero, which might cause numerical instability and overfitting.")
-    bStd = rawBStd
-    k = nf + 1 if fit_intercept else nf
-    eff_l2 = (1.0 - elastic_net) * reg_param / bStd
-    sysm = device.wls_assemble(flat, nf, fit_intercept, wSum, bStd, rawBBar, eff_l2, standardize_features,
-                               standardize_label)
+    wSum, bStd = float(o[device.PCG_WSUM]), float(o[device.PCG_BSTD])
+    k = sysm.k
     A, b, aStd = sysm.A, sysm.b, sysm.aStd
-    o = device.wls_pcg(sysm, nf, bStd, PCG_RTOL) if solver_type == "auto" else None
     L = None
-    if o is not None:
+    if solver_type == "auto" and device.pcg_ok(o):
         w = device.PCG_STATE_WORDS
         x = o[w:w + k]
-        coef = o[w + k:w + k + nf].copy()
+        coef = np.array(o[w + k:w + k + nf], dtype=np.float64)
         intercept = float(x[nf] * bStd) if fit_intercept else 0.0
     else:
         L, info = torch.linalg.cholesky_ex(A)

@@ -37,7 +37,7 @@ from ..sql.types import DoubleType, VectorUDT, is_numeric
 from ..utils.logging import get_logger
 from .linalg import DenseVector, Vector, Vectors
 from ..utils import tracing
-from .optim import MAX_NUM_FEATURES, GramStats, fit_wls_flat
+from .optim import DEVICE_SOLVE_MIN_K, MAX_NUM_FEATURES, PCG_RTOL, GramStats, fit_wls_flat
 from .param import Param, Params, param_accessors
 
 __all__ = ["LinearRegression", "LinearRegressionModel", "LinearRegressionTrainingSummary",
@@ -276,7 +276,9 @@ class LinearRegression(_LRParams):
             # on the side stream beside the next step's pass -- at N > 1 its all-reduce too
             overlap = overlap and bool(getattr(fused, "overlap_ok", False))
         else:
-            pipe = _pipe_stream(df, tbl) if overlap else None
+            # (not the wide SYRK: two of them co-running would split the CUs, each block of the
+            # one-block-per-CU grid needs a whole CU's LDS)
+            pipe = _pipe_stream(df, tbl) if overlap and d <= 64 else None
             if pipe is not None:
                 caller = faststream.current(faststream.dev_index(df.sparkSession.device))
                 with faststream.use(pipe):
@@ -326,6 +328,11 @@ class LinearRegression(_LRParams):
                 # queue behind its HBM stream (8 us alone, ~100 us co-running), and the side stream
                 # must still fit the all-reduce and the solve into one Gram period
                 defer = overlap and _async_conf(df) and d <= 64 and not comm.collectives_active()
+                # the wide (MFMA-bound) SYRK: its fold, all-reduce and solve go to the side stream
+                # with the solve at any world size -- the memory-bound fold co-runs with the next
+                # fit's SYRK instead of following it
+                if d > 64 and overlap and _async_fit(df, _DEVICE_FLAT, d, _wls_args(self, d)):
+                    defer = True
                 Xv = _values(X, caller)
                 if _replayable(Xv, w):
                     # resolve the launch once: a repeated fit of this DataFrame replays it
@@ -526,7 +533,8 @@ def _async_conf(df) -> bool:
 def _async_fit(df, flat, d, args) -> bool:
     """Asynchronous normal-equation fit (session config ``dq4ml.fit.async``): device statistics
     and a device solver for the branch -- Cholesky (no L1) for <= 64 features, OWLQN (L1) up to
-    k = QN_DEVICE_MAX_K -> the solve is enqueued on the device and the host does not wait for the
+    k = QN_DEVICE_MAX_K, the large-k assembly + Jacobi-PCG (no L1, k >= DEVICE_SOLVE_MIN_K: the
+    wide config-5 fit) -> the solve is enqueued on the device and the host does not wait for the
     fit; coefficients, summary and any Spark warning/exception materialize on first read (edge
     cases re-solve on the host with identical semantics)."""
     sess = getattr(df, "sparkSession", None)
@@ -541,9 +549,14 @@ def _async_fit(df, flat, d, args) -> bool:
 
     if enet != 0.0 and reg != 0.0:
         return d + (1 if fit_icpt else 0) <= QN_DEVICE_MAX_K
-    return d <= 64
+    return d <= 64 or d + (1 if fit_icpt else 0) >= DEVICE_SOLVE_MIN_K
 
 
+class _DeviceFlat:  # (_async_fit's eligibility probe before the statistics exist)
+    is_cuda = True
+
+
+_DEVICE_FLAT = _DeviceFlat()
 _tail_streams = {}
 _pipe_streams = {}
 
@@ -644,10 +657,16 @@ class _PendingWLS:
         self._done = None
         self._checks = list(checks or [])
         self._qn = enet != 0.0 and reg != 0.0  # OWLQN branch (wls_qn_kernel) instead of Cholesky
+        self._sysm = None  # large-k branch: the assembled system (wls_large.hip)
 
         def solve(flat):
             if self._qn:
                 return device.wls_qn_small(flat, d, fit_icpt, reg, enet, std_f, std_l, max_iter, tol)
+            if d > 64:  # large k: assembly + Jacobi-PCG, budgeted from the last solve of this order
+                self._sysm = device.wls_assemble(flat, d, fit_icpt, reg, enet, std_f, std_l)
+                self._budget = _pcg_budget.get(self._sysm.k, 16)
+                device.wls_pcg_enqueue(self._sysm, d, PCG_RTOL, self._budget)
+                return self._sysm.o
             return device.wls_small(flat, d, fit_icpt, reg, enet, std_f, std_l)
         if hasattr(flat, "finish") and not overlap:
             flat = flat.finish()
@@ -679,6 +698,9 @@ class _PendingWLS:
                 native.hip().stream_wait_event(faststream.raw(self._dev), self._done)
             host = self.out.cpu().numpy()
             verify(self._checks)  # data errors of the fit surface here, on first read
+            if self._sysm is not None:
+                self._res = self._resolve_large(host)
+                return self._res
             if self._qn:
                 from .optim import owlqn_result
 
@@ -699,6 +721,29 @@ class _PendingWLS:
                 wls = WLSModel(host[:d].copy(), float(host[d]), diag_inv, np.zeros(1), "cholesky")
                 self._res = (wls, GramStats.scalars_only(host[d + 2:d + 7], d))
         return self._res
+
+
+    def _resolve_large(self, o):
+        """The large-k solve's control block -> model: PCG not done within the enqueued budget
+        continues from its state (host-checked chunks); every fallback is ``wls_large_result``'s."""
+        from .optim import wls_large_result
+
+        flat, d = self.args[0], self.args[1]
+        sysm = self._sysm
+        if self._done is not None:  # the continuation chunks run on the caller's (now ordered) stream
+            cur = torch.cuda.current_stream(flat.device)
+            for t in (sysm.A, sysm.b, sysm.minv, sysm.aStd, sysm.o, sysm.work):
+                t.record_stream(cur)
+        o = device.wls_pcg_drive(sysm, d, o, self._budget)
+        if o[device.PCG_CONV] != 0.0 and o[device.PCG_STATUS] == 0.0:
+            # the next fit of this order enqueues what this one needed (+2): converged iterations
+            # after that are no-op launches, too few only costs a host-checked continuation
+            _pcg_budget[sysm.k] = int(min(96, max(8, o[device.PCG_ITERS] + 2)))
+        return wls_large_result(flat, sysm, o, d, *self.args[2:])
+
+
+# Jacobi-PCG iterations to enqueue for an asynchronous large-k solve, per system order k
+_pcg_budget = {}
 
 
 class PredictExpr(Expr):

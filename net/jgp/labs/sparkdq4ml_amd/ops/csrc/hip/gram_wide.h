@@ -23,14 +23,9 @@ struct WideArgs {
   int splitk;
   const int* pairs;           // [npair][2] panel pairs I <= J over [0, npanels] (npanels = augmentation)
   float* part;                // [npair * splitk][256][256] f32 partial tiles
-  double aug_scale[3];        // scales of [1, y_hi, y_lo]
-  int64_t* stamps;            // (diagnostics, null) gang kernels: s_memrealtime at each unit's start / end,
-                              // [block][64 units][2]
+  const double* aug_scale;    // device f64[3]: scales of [1, y_hi, y_lo] (made on the device with the
+                              // label split, so no launch reads them on the host)
 };
-
-// (diagnostics) the stamp buffer the next wide launches record into (null: off)
-void gram_wide_set_stamps(int64_t* stamps);
-int64_t* wide_stamps();
 
 constexpr int kWideZeroBytes = 32768;  // >= the largest panel-relative piece offset (bf16 tiles: 30 KiB)
 
@@ -48,25 +43,19 @@ void wide_mask_rows(int eb, const void* in, void* out, int d, int64_t n, const u
 // out: flat WLS layout [count, wSum, wwSum, bSum, bbSum, aSum(d), abSum(d), aa packed-upper(d)]
 // fold = false: partial tiles only (the caller folds them band by band with gram_wide_fold)
 void gram_wide(int eb, WideArgs a, const int* pairs_dev, const float* scales, double* out, hipStream_t st,
-               int ring = 4, int waves = 4, bool fold = true);
+               int ring = 4, bool fold = true);
 // persistent XCD-grouped schedule: grid blocks (one per CU, a multiple of 8), group b % 8 owns
 // splits [g*h, g*h+h) (a.splitk == 8*h) and dequeues (split, pair) units from heads[g] (8 ints,
 // zeroed here on the stream)
 void gram_wide_queue(int eb, WideArgs a, const int* pairs_dev, const float* scales, double* out, int* heads, int h,
-                     int grid, hipStream_t st, int waves = 8, bool fold = true);
+                     int grid, hipStream_t st, bool fold = true);
 // gang schedule: grid blocks (one per CU, a multiple of 8) of 8 waves; group b % 8 owns splits
 // [g*S, g*S+S) (a.splitk == 8*S); pairs_dev lists the P(P-1)/2 off-diagonal pairs I < J < npanels,
 // then the P diagonal ones (diagonal units also write the augmentation tiles); bar (or null): 256
-// ints of scratch for the per-round group barrier (zeroed here on the stream)
+// ints of scratch for the per-round group barrier (zeroed here on the stream; full rounds only,
+// bounded, self-disabling: gram_wide.hip gang_round_sync)
 void gram_wide_gang(int eb, WideArgs a, const int* pairs_dev, const float* scales, double* out, int S, int grid,
-                    hipStream_t st, bool fold = true, int waves = 8, int* bar = nullptr);
-// XCD-keyed gang schedule (gram_wide_gangx_kernel): the group is the XCD the block runs on
-// (HW_REG_XCC_ID) and each XCD dequeues its own units, stealing when its queue is empty; q:
-// gram_wide_gangx_ints(grid) ints of scratch (heads zeroed here on the stream); xcc_dbg (or null):
-// [grid] ints, each block's XCD (diagnostics)
-int gram_wide_gangx_ints(int grid);
-void gram_wide_gangx(int eb, WideArgs a, const int* pairs_dev, const float* scales, double* out, int S, int grid,
-                     int* q, int* xcc_dbg, hipStream_t st, bool fold = true);
+                    hipStream_t st, bool fold = true, int* bar = nullptr);
 // fold the pairs of panel columns [J0, J1) (J = npanels: the augmentation column -> the head of
 // the flat layout) into out (f64) or out32 (f32 wire buffer, same flat indexing)
 void gram_wide_fold(WideArgs a, const float* scales, double* out, float* out32, int J0, int J1, hipStream_t st);

@@ -117,17 +117,7 @@ struct StageFrags {
 //   glds stage i+4 into the buffer stage i vacated | MFMAs on A tiles 2-3 | lgkmcnt(0)
 // so the LDS reads and the barrier skew hide under half a stage of MFMAs, and three stages of
 // global_load_lds stay in flight across every barrier.
-template <typename V>
-__device__ __forceinline__ void keep_live(const V& v) {
-#pragma unroll
-  for (int e = 0; e < (int)(sizeof(V) / 4); ++e) asm volatile("" ::"v"(reinterpret_cast<const unsigned*>(&v)[e]));
-}
-
-// ABL: 0 = real kernel; diagnostic builds only (timing, wrong results): 1 = no MFMA (loads + LDS
-// reads), 2 = no glds after the ring prologue (MFMAs + LDS reads on the first RING stages' data)
-// ABL: 0 = real kernel; diagnostic builds only: 1 = no MFMA (loads + LDS reads), 2 = no glds after
-// the ring prologue (timing only, wrong results); 16 = tid laundering; 64 = staggered start
-template <int EB, int MODE, int RING, int ABL = 0>
+template <int EB, int MODE, int RING>
 __device__ __forceinline__ void syrk_block(const WideArgs& a, unsigned char* smem, int I, int J, int pair, int split) {
   typedef WideTraits<EB> Tr;
   typedef typename Tr::frag F;
@@ -150,12 +140,8 @@ __device__ __forceinline__ void syrk_block(const WideArgs& a, unsigned char* sme
   constexpr int kLoadsPerStage = LA + LB;
   typedef StageFrags<F> SF;
   // The wave index is a scalar (readfirstlane): every LDS-DMA destination (M0) is SALU
-  // arithmetic.  (ABL & 16, diagnostic: the thread id laundered through an asm barrier so no
-  // tid-derived value is hoisted out of the gang's unit loop.  The K loop compiles to the same
-  // instructions, yet on the box the laundered build ran 8-10 % slower with the L2 hit rate at
-  // 25 % instead of 46 %: profiles/r5_wide_limiter.md.)
-  int tid = threadIdx.x;
-  if constexpr ((ABL & 16) != 0) asm volatile("" : "+v"(tid));
+  // arithmetic.
+  const int tid = threadIdx.x;
   const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 2, wn = wave & 3;
   const int64_t nst = a.nsup * Tr::kStagesPerSup;
@@ -184,7 +170,6 @@ __device__ __forceinline__ void syrk_block(const WideArgs& a, unsigned char* sme
   // with no branch at all (a branch there lets the compiler sink MFMAs past the barrier) and
   // every wait is the same counted vmcnt — the extra stage multiplies zeros
   auto issue = [&](int64_t st, int buf) {
-    if ((ABL & 3) == 2 && st >= RING) return;  // (the ablation still fills the ring once: real operands)
     unsigned char* base = smem + buf * kStageBytes;
     const bool live = (int)st < cnt32;
     const int64_t dx = Tr::sdelta(st0 + st, a.NT), dg = Tr::sdelta(st0 + st, 1);
@@ -236,16 +221,6 @@ __device__ __forceinline__ void syrk_block(const WideArgs& a, unsigned char* sme
   // (augmentation modes: waves whose B (or A) tiles come from the zero page multiply zeros —
   // cheaper than a data-dependent branch around the accumulators)
   auto mfmas = [&](const SF& f, int x0) {
-    if ((ABL & 3) == 1) {
-#pragma unroll
-      for (int kk = 0; kk < Tr::kSteps; ++kk) {
-#pragma unroll
-        for (int x = x0; x < x0 + 2; ++x) keep_live(f.a[kk][x]);
-#pragma unroll
-        for (int y = 0; y < WN; ++y) keep_live(f.b[kk][y]);
-      }
-      return;
-    }
 #pragma unroll
     for (int kk = 0; kk < Tr::kSteps; ++kk)
 #pragma unroll
@@ -334,7 +309,7 @@ __device__ __forceinline__ void syrk_block(const WideArgs& a, unsigned char* sme
       }
 }
 
-template <int EB, int RING, int ABL = 0>
+template <int EB, int RING>
 __global__ __launch_bounds__(64 * kWaves, 1) void gram_wide_kernel(WideArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   // XCD-aware bijective remap: dispatch puts block b on XCD b % 8; give each XCD a contiguous
@@ -344,10 +319,10 @@ __global__ __launch_bounds__(64 * kWaves, 1) void gram_wide_kernel(WideArgs a) {
   const int npair = (a.npanels + 1) * (a.npanels + 2) / 2;
   const int split = L / npair, pair = L - split * npair;
   const int I = a.pairs[2 * pair], J = a.pairs[2 * pair + 1];
-  if (I == J && J != a.npanels) syrk_block<EB, 3, RING, ABL>(a, smem, I, J, pair, split);
-  else if (J != a.npanels) syrk_block<EB, 0, RING, ABL>(a, smem, I, J, pair, split);
-  else if (I != a.npanels) syrk_block<EB, 1, RING, ABL>(a, smem, I, J, pair, split);
-  else syrk_block<EB, 2, RING, ABL>(a, smem, I, J, pair, split);
+  if (I == J && J != a.npanels) syrk_block<EB, 3, RING>(a, smem, I, J, pair, split);
+  else if (J != a.npanels) syrk_block<EB, 0, RING>(a, smem, I, J, pair, split);
+  else if (I != a.npanels) syrk_block<EB, 1, RING>(a, smem, I, J, pair, split);
+  else syrk_block<EB, 2, RING>(a, smem, I, J, pair, split);
 }
 
 // Persistent, XCD-grouped schedule.  The grid is one block per CU; block b belongs to group
@@ -416,20 +391,32 @@ __device__ __forceinline__ void gang_unit(int u, int S, int P, int& s, int& pos)
 // round barrier of a gang group (bar: 8 groups x 32 ints, zeroed per launch, or null): the block
 // arrives after its unit k - 1 and waits until all G blocks of its group have -- the round's
 // blocks then start their units together and share each panel-stage through the XCD's L2.  For
-// speed only: the wait is bounded, so any placement or residency still completes.
-__device__ __forceinline__ void gang_round_sync(int* bar, int g, int k, int G) {
-  if (bar == nullptr || k == 0) return;
+// speed only, never for correctness:
+//  * only FULL rounds synchronize (round k runs G units iff k*G + G <= units): the blocks of a
+//    partial last round would wait for arrivals that never come;
+//  * the wait is bounded (kGangSpin polls), and a group whose wait ever times out -- its blocks
+//    are not all co-resident: another kernel holds CU slots, a CU-masked stream, a placement that
+//    is not round-robin -- turns its barrier off for the rest of the launch (bar[g*32 + 1]), so a
+//    non-co-resident grid loses one bounded wait per group, not one per round.
+constexpr int kGangSpin = 1 << 13;
+
+__device__ __forceinline__ void gang_round_sync(int* bar, int g, int k, int G, int units) {
+  if (bar == nullptr || k == 0 || k * G + G > units) return;
   if (threadIdx.x == 0) {
     int* c = bar + g * 32;
     __hip_atomic_fetch_add(c, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int target = k * G;
-    for (int it = 0; it < (1 << 20) && __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target; ++it)
-      __builtin_amdgcn_s_sleep(4);
+    if (__hip_atomic_load(c + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
+      const int target = k * G;
+      int it = 0;
+      for (; it < kGangSpin && __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target; ++it)
+        __builtin_amdgcn_s_sleep(4);
+      if (it == kGangSpin) __hip_atomic_store(c + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
   __syncthreads();
 }
 
-template <int EB, int RING, int ABL = 0>
+template <int EB, int RING>
 __global__ __launch_bounds__(64 * kWaves, 1) void gram_wide_gang_kernel(WideArgs a, int S, int* __restrict__ bar) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int g = blockIdx.x & 7, l = blockIdx.x >> 3, G = gridDim.x >> 3;
@@ -437,71 +424,16 @@ __global__ __launch_bounds__(64 * kWaves, 1) void gram_wide_gang_kernel(WideArgs
   const int wave = threadIdx.x >> 6;
   // the waves whose tiles lie entirely below a diagonal unit's diagonal
   const bool aug_wave = (wave >> 2) == 1 && (wave & 3) < 2;
-  if constexpr ((ABL & 64) != 0) {  // (diagnostic) stagger: block l of a group starts ~2 (l & 3) stages late
-    for (int k = 0; k < (l & 3); ++k) __builtin_amdgcn_s_sleep(40);  // 64 x 40 clocks ~ 2 stages
-  }
   int k = 0;
   for (int u = l; u < units; u += G, ++k) {
     int s, pos;
     gang_unit(u, S, P, s, pos);
     const int split = g * S + s;
     const int I = a.pairs[2 * pos], J = a.pairs[2 * pos + 1];
-    gang_round_sync(bar, g, k, G);
-    if (a.stamps != nullptr && threadIdx.x == 0 && k < 64)
-      a.stamps[((int64_t)blockIdx.x * 64 + k) * 2] = (int64_t)__builtin_amdgcn_s_memrealtime();
-    if (I != J) syrk_block<EB, 0, RING, ABL>(a, smem, I, J, 0, split);
-    else if (aug_wave) syrk_block<EB, 5, RING, ABL>(a, smem, I, J, 0, split);
-    else if (wave < 2) syrk_block<EB, 4, RING, ABL>(a, smem, I, J, 0, split);  // + the aug tile's loads
-    else syrk_block<EB, 6, RING, ABL>(a, smem, I, J, 0, split);
-    __syncthreads();  // every wave is done reading the ring before the next unit's first glds
-    if (a.stamps != nullptr && threadIdx.x == 0 && k < 64)
-      a.stamps[((int64_t)blockIdx.x * 64 + k) * 2 + 1] = (int64_t)__builtin_amdgcn_s_memrealtime();
-  }
-}
-
-// XCD-keyed gang schedule: the same equal-cost units as gram_wide_gang_kernel, but the group is
-// the XCD the block actually runs on (HW_REG_XCC_ID), not blockIdx % 8: the static form assumes
-// round-robin dispatch, and where a box deals blocks otherwise the 32 blocks of a "group" spread
-// over every XCD, 8 row ranges share each L2 and its hit rate halves (measured 70 % -> 38 %,
-// profiles/r5_wide_limiter.md).  Each XCD dequeues its own units (range-major, Z-order pairs:
-// the blocks of an XCD stay on one row range, as the gang's do) from a head on its own 64-byte
-// line; a block whose XCD's queue is empty steals from the next XCD's, so any placement -- and
-// any number of blocks per XCD -- covers every unit exactly once.  Correctness never depends on
-// placement; only L2 locality does.
-template <int EB, int RING>
-__global__ __launch_bounds__(64 * kWaves, 1) void gram_wide_gangx_kernel(WideArgs a, int S, int* __restrict__ q,
-                                                                        int* __restrict__ xcc_dbg) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int P = a.npanels, npu = P * (P + 1) / 2, units = npu * S;
-  const int wave = threadIdx.x >> 6;
-  const bool aug_wave = (wave >> 2) == 1 && (wave & 3) < 2;
-  int xcc;
-  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-  xcc &= 7;
-  if (xcc_dbg != nullptr && threadIdx.x == 0) xcc_dbg[blockIdx.x] = xcc;
-  int* slot = q + 8 * 16 + blockIdx.x * 16;  // this block's broadcast word (a line of its own)
-  int g = xcc;
-  for (;;) {
-    if (threadIdx.x == 0) {
-      int u = atomicAdd(&q[g * 16], 1), tries = 0;
-      while (u >= units && ++tries < 8) {
-        g = (g + 1) & 7;
-        u = atomicAdd(&q[g * 16], 1);
-      }
-      __hip_atomic_store(slot, tries < 8 ? (g << 24) | u : -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    __syncthreads();
-    const int v = __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __syncthreads();  // every wave has read the word before thread 0 rewrites it
-    if (v < 0) break;
-    const int gg = v >> 24, u = v & 0xffffff;
-    int s, pos;
-    gang_unit(u, S, P, s, pos);
-    const int split = gg * S + s;
-    const int I = a.pairs[2 * pos], J = a.pairs[2 * pos + 1];
+    gang_round_sync(bar, g, k, G, units);
     if (I != J) syrk_block<EB, 0, RING>(a, smem, I, J, 0, split);
     else if (aug_wave) syrk_block<EB, 5, RING>(a, smem, I, J, 0, split);
-    else if (wave < 2) syrk_block<EB, 4, RING>(a, smem, I, J, 0, split);
+    else if (wave < 2) syrk_block<EB, 4, RING>(a, smem, I, J, 0, split);  // + the aug tile's loads
     else syrk_block<EB, 6, RING>(a, smem, I, J, 0, split);
     __syncthreads();  // every wave is done reading the ring before the next unit's first glds
   }
@@ -532,7 +464,7 @@ __global__ __launch_bounds__(256) void gram_wide_reduce_kernel(WideArgs a, const
   int64_t npb = 0;  // pairs of the band's panel columns: column J holds pairs I = 0..J
   for (int J = J0; J < J1; ++J) npb += J + 1;
   const int64_t tot = npb * kPanel * kPanel;
-  const double s1 = a.aug_scale[0], syh = a.aug_scale[1], syl = a.aug_scale[2];
+  const double s1 = a.aug_scale[0], syh = a.aug_scale[1], syl = a.aug_scale[2];  // device f64[3]
   const int64_t slab = (int64_t)kPanel * kPanel;
   for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < tot; g += (int64_t)gridDim.x * blockDim.x) {
     const int q = (int)(g / slab);
@@ -694,9 +626,6 @@ __global__ __launch_bounds__(256) void wide_mask_rows_kernel(const u32x4* __rest
 
 }  // namespace
 
-static int64_t* g_stamps = nullptr;
-void gram_wide_set_stamps(int64_t* stamps) { g_stamps = stamps; }
-int64_t* wide_stamps() { return g_stamps; }
 
 void wide_mask_rows(int eb, const void* in, void* out, int d, int64_t n, const uint8_t* sel, hipStream_t st) {
   const int NT = ((d + 255) / 256) * 8;
@@ -742,21 +671,13 @@ int64_t gram_wide_partials(int d, int splitk) {
   return (int64_t)npair * splitk * kPanel * kPanel;
 }
 
-template <int EB, int RING, int ABL = 0>
+template <int EB, int RING>
 static void launch_wide(const WideArgs& a, int nblocks, hipStream_t st) {
   const size_t lds = (size_t)RING * kStageBytes;
-  DQ_HIP_CHECK(hipFuncSetAttribute((const void*)gram_wide_kernel<EB, RING, ABL>,
+  DQ_HIP_CHECK(hipFuncSetAttribute((const void*)gram_wide_kernel<EB, RING>,
                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  hipLaunchKernelGGL((gram_wide_kernel<EB, RING, ABL>), dim3(nblocks), dim3(64 * kWaves), lds, st, a);
+  hipLaunchKernelGGL((gram_wide_kernel<EB, RING>), dim3(nblocks), dim3(64 * kWaves), lds, st, a);
   DQ_HIP_CHECK(hipGetLastError());
-}
-
-template <int EB>
-static void launch_wide_eb(const WideArgs& a, int nblocks, hipStream_t st, int ring, int waves) {
-  // diagnostic ablations (timing only, wrong results): waves 81 = no MFMA, 82 = no glds
-  if (waves == 81) return launch_wide<EB, 4, 1>(a, nblocks, st);
-  if (waves == 82) return launch_wide<EB, 4, 2>(a, nblocks, st);
-  ring == 5 ? launch_wide<EB, 5>(a, nblocks, st) : launch_wide<EB, 4>(a, nblocks, st);
 }
 
 template <int EB, int RING>
@@ -785,81 +706,46 @@ void gram_wide_fold(WideArgs a, const float* scales, double* out, float* out32, 
 }
 
 void gram_wide_queue(int eb, WideArgs a, const int* pairs_dev, const float* scales, double* out, int* heads, int h,
-                     int grid, hipStream_t st, int waves, bool fold) {
+                     int grid, hipStream_t st, bool fold) {
   a.pairs = pairs_dev;
   if (a.splitk != 8 * h) throw std::invalid_argument("gram_wide_queue: splitk must be 8 * h");
   if (grid < 8 || grid % 8) throw std::invalid_argument("gram_wide_queue: grid must be a positive multiple of 8");
-  if (waves != kWaves) throw std::invalid_argument("gram_wide_queue: waves must be 8");
   DQ_HIP_CHECK(hipMemsetAsync(heads, 0, 8 * sizeof(int), st));
   if (eb == 16) launch_wide_queue<16, 4>(a, grid, heads, h, st);
   else launch_wide_queue<8, 4>(a, grid, heads, h, st);
   if (fold) launch_fold(a, scales, out, nullptr, 0, a.npanels + 1, st);
 }
 
-template <int EB, int ABL = 0>
-static void launch_wide_gang(const WideArgs& a, int grid, int S, hipStream_t st, int* bar = nullptr) {
+template <int EB>
+static void launch_wide_gang(const WideArgs& a, int grid, int S, hipStream_t st, int* bar) {
   const size_t lds = (size_t)5 * kStageBytes;
-  DQ_HIP_CHECK(hipFuncSetAttribute((const void*)gram_wide_gang_kernel<EB, 5, ABL>,
+  DQ_HIP_CHECK(hipFuncSetAttribute((const void*)gram_wide_gang_kernel<EB, 5>,
                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   if (bar != nullptr) DQ_HIP_CHECK(hipMemsetAsync(bar, 0, 8 * 32 * sizeof(int), st));
-  hipLaunchKernelGGL((gram_wide_gang_kernel<EB, 5, ABL>), dim3(grid), dim3(64 * kWaves), lds, st, a, S, bar);
+  hipLaunchKernelGGL((gram_wide_gang_kernel<EB, 5>), dim3(grid), dim3(64 * kWaves), lds, st, a, S, bar);
   DQ_HIP_CHECK(hipGetLastError());
 }
 
 void gram_wide_gang(int eb, WideArgs a, const int* pairs_dev, const float* scales, double* out, int S, int grid,
-                    hipStream_t st, bool fold, int waves, int* bar) {
+                    hipStream_t st, bool fold, int* bar) {
   a.pairs = pairs_dev;
   if (S < 1 || a.splitk != 8 * S) throw std::invalid_argument("gram_wide_gang: splitk must be 8 * S");
   if (grid < 8 || grid % 8) throw std::invalid_argument("gram_wide_gang: grid must be a positive multiple of 8");
   if ((int64_t)a.splitk > a.nsup) throw std::invalid_argument("gram_wide_gang: more row ranges than supersteps");
-  // diagnostic ablations (timing only, wrong results): waves 81 = no MFMA, 82 = no glds in the loop
-  if (waves != kWaves && waves != 81 && waves != 82 && !((waves == 91 || waves == 94 || waves == 95) && eb == 8))
-    throw std::invalid_argument("gram_wide_gang: waves must be 8");
-  if (waves == 81) eb == 16 ? launch_wide_gang<16, 1>(a, grid, S, st) : launch_wide_gang<8, 1>(a, grid, S, st);
-  else if (waves == 82) eb == 16 ? launch_wide_gang<16, 2>(a, grid, S, st) : launch_wide_gang<8, 2>(a, grid, S, st);
-  // (diagnostic code-shape variants, fp8 only: 91 tid laundering, 94 staggered start, 95 both)
-  else if (waves == 91 && eb == 8) launch_wide_gang<8, 16>(a, grid, S, st);
-  else if (waves == 94 && eb == 8) launch_wide_gang<8, 64>(a, grid, S, st);
-  else if (waves == 95 && eb == 8) launch_wide_gang<8, 80>(a, grid, S, st);
-  else if (eb == 16) launch_wide_gang<16>(a, grid, S, st, bar);
+  if (eb == 16) launch_wide_gang<16>(a, grid, S, st, bar);
   else launch_wide_gang<8>(a, grid, S, st, bar);
   if (fold) launch_fold(a, scales, out, nullptr, 0, a.npanels + 1, st);
 }
 
-template <int EB>
-static void launch_wide_gangx(const WideArgs& a, int grid, int S, int* q, int* xcc_dbg, hipStream_t st) {
-  const size_t lds = (size_t)5 * kStageBytes;
-  DQ_HIP_CHECK(hipFuncSetAttribute((const void*)gram_wide_gangx_kernel<EB, 5>,
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  hipLaunchKernelGGL((gram_wide_gangx_kernel<EB, 5>), dim3(grid), dim3(64 * kWaves), lds, st, a, S, q, xcc_dbg);
-  DQ_HIP_CHECK(hipGetLastError());
-}
-
-int gram_wide_gangx_ints(int grid) { return 8 * 16 + grid * 16; }
-
-void gram_wide_gangx(int eb, WideArgs a, const int* pairs_dev, const float* scales, double* out, int S, int grid,
-                     int* q, int* xcc_dbg, hipStream_t st, bool fold) {
-  a.pairs = pairs_dev;
-  if (S < 1 || a.splitk != 8 * S) throw std::invalid_argument("gram_wide_gangx: splitk must be 8 * S");
-  if (grid < 1) throw std::invalid_argument("gram_wide_gangx: empty grid");
-  if ((int64_t)a.splitk > a.nsup) throw std::invalid_argument("gram_wide_gangx: more row ranges than supersteps");
-  if ((int64_t)a.npanels * (a.npanels + 1) / 2 * S >= (1 << 24)) throw std::invalid_argument("gram_wide_gangx: too many units");
-  DQ_HIP_CHECK(hipMemsetAsync(q, 0, 8 * 16 * sizeof(int), st));  // the 8 XCD heads
-  if (eb == 16) launch_wide_gangx<16>(a, grid, S, q, xcc_dbg, st);
-  else launch_wide_gangx<8>(a, grid, S, q, xcc_dbg, st);
-  if (fold) launch_fold(a, scales, out, nullptr, 0, a.npanels + 1, st);
-}
-
 void gram_wide(int eb, WideArgs a, const int* pairs_dev, const float* scales, double* out, hipStream_t st, int ring,
-               int waves, bool fold) {
+               bool fold) {
   a.pairs = pairs_dev;
   const int P = a.npanels;
   const int npair = (P + 1) * (P + 2) / 2;
   const int nb = npair * a.splitk;
   if (ring != 4 && ring != 5) throw std::invalid_argument("gram_wide: ring must be 4 or 5");
-  if (waves != kWaves && waves != 81 && waves != 82) throw std::invalid_argument("gram_wide: waves must be 8");
-  if (eb == 16) launch_wide_eb<16>(a, nb, st, ring, waves);
-  else launch_wide_eb<8>(a, nb, st, ring, waves);
+  if (eb == 16) ring == 5 ? launch_wide<16, 5>(a, nb, st) : launch_wide<16, 4>(a, nb, st);
+  else ring == 5 ? launch_wide<8, 5>(a, nb, st) : launch_wide<8, 4>(a, nb, st);
   if (fold) launch_fold(a, scales, out, nullptr, 0, P + 1, st);
 }
 

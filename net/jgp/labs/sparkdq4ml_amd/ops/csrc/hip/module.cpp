@@ -203,27 +203,31 @@ PYBIND11_MODULE(_dq4ml_hip, m) {
                         uintptr_t out, uintptr_t stream) {
     wls_small(P<const double>(flat), nf, fit_intercept, reg, enet, std_f, std_l, P<double>(out), as_stream(stream));
   });
-  m.def("wls_assemble", [](uintptr_t flat, int nf, bool fit_intercept, double wSum, double bStd, double rawBBar,
-                           double eff_l2, bool std_f, bool std_l, uintptr_t A, uintptr_t b, uintptr_t minv,
-                           uintptr_t aStd, uintptr_t aBar, uintptr_t lam, uintptr_t o, uintptr_t stream) {
-    wls_assemble(P<const double>(flat), nf, fit_intercept, wSum, bStd, rawBBar, eff_l2, std_f, std_l, P<double>(A),
-                 P<double>(b), P<double>(minv), P<double>(aStd), P<double>(aBar), P<double>(lam), P<double>(o),
-                 as_stream(stream));
+  m.def("wls_assemble", [](uintptr_t flat, int nf, bool fit_intercept, double reg, double enet, bool std_f,
+                           bool std_l, uintptr_t A, uintptr_t b, uintptr_t minv, uintptr_t aStd, uintptr_t aBar,
+                           uintptr_t lam, uintptr_t o, uintptr_t stream) {
+    wls_assemble(P<const double>(flat), nf, fit_intercept, reg, enet, std_f, std_l, P<double>(A), P<double>(b),
+                 P<double>(minv), P<double>(aStd), P<double>(aBar), P<double>(lam), P<double>(o), as_stream(stream));
   });
   m.def("wls_pcg_init", [](uintptr_t b, uintptr_t minv, int k, double rtol, uintptr_t o, uintptr_t r, uintptr_t p,
                            uintptr_t stream) {
     wls_pcg_init(P<const double>(b), P<const double>(minv), k, rtol, P<double>(o), P<double>(r), P<double>(p),
                  as_stream(stream));
   });
-  m.def("wls_pcg_chunk", [](uintptr_t A, uintptr_t b, uintptr_t minv, uintptr_t aStd, int k, int nf, double bStd,
-                            int iters, uintptr_t o, uintptr_t r, uintptr_t p, uintptr_t Ap, uintptr_t stream) {
-    wls_pcg_chunk(P<const double>(A), P<const double>(b), P<const double>(minv), P<const double>(aStd), k, nf, bStd,
-                  iters, P<double>(o), P<double>(r), P<double>(p), P<double>(Ap), as_stream(stream));
+  m.def("wls_pcg_chunk", [](uintptr_t A, uintptr_t b, uintptr_t minv, uintptr_t aStd, int k, int nf, int iters,
+                            uintptr_t o, uintptr_t r, uintptr_t p, uintptr_t Ap, uintptr_t stream) {
+    wls_pcg_chunk(P<const double>(A), P<const double>(b), P<const double>(minv), P<const double>(aStd), k, nf, iters,
+                  P<double>(o), P<double>(r), P<double>(p), P<double>(Ap), as_stream(stream));
   });
   m.attr("PCG_STATE_WORDS") = (int)PCG_STATE_WORDS;
   m.attr("PCG_CONV") = (int)PCG_CONV;
   m.attr("PCG_BAD") = (int)PCG_BAD;
   m.attr("PCG_OK") = (int)PCG_OK;
+  m.attr("PCG_ITERS") = (int)PCG_ITERS;
+  m.attr("PCG_STATUS") = (int)PCG_STATUS;
+  m.attr("PCG_HEAD") = (int)PCG_HEAD;
+  m.attr("PCG_WSUM") = (int)PCG_WSUM;
+  m.attr("PCG_BSTD") = (int)PCG_BSTD;
   m.def("wls_qn_small", [](uintptr_t flat, int nf, bool fit_intercept, double reg, double enet, bool std_f,
                            bool std_l, int max_iter, double tol, int hist_cap, uintptr_t out, uintptr_t stream) {
     wls_qn_small(P<const double>(flat), nf, fit_intercept, reg, enet, std_f, std_l, max_iter, tol, hist_cap,
@@ -257,7 +261,7 @@ PYBIND11_MODULE(_dq4ml_hip, m) {
                  P<const float>(shift));
   });
   auto wide_args = [](uintptr_t X, uintptr_t Xaug, uintptr_t zeros, int nt, int npanels, int d, int64_t nsup,
-                      int splitk, uintptr_t part, double s1, double syh, double syl) {
+                      int splitk, uintptr_t part, uintptr_t aug_scale) {
     WideArgs a{};
     a.X = P<const unsigned char>(X);
     a.Xaug = P<const unsigned char>(Xaug);
@@ -268,49 +272,36 @@ PYBIND11_MODULE(_dq4ml_hip, m) {
     a.nsup = nsup;
     a.splitk = splitk;
     a.part = P<float>(part);
-    a.aug_scale[0] = s1;
-    a.aug_scale[1] = syh;
-    a.aug_scale[2] = syl;
-    a.stamps = wide_stamps();
+    a.aug_scale = P<const double>(aug_scale);
     return a;
   };
-  m.def("gram_wide_set_stamps", [](uintptr_t p) { gram_wide_set_stamps(P<int64_t>(p)); });
+  // aug_scale: device f64[3] scales of the augmentation columns [1, y_hi, y_lo] (read by the fold)
   m.def("gram_wide", [wide_args](int eb, uintptr_t X, uintptr_t Xaug, uintptr_t zeros, int nt, int npanels, int d,
-                                 int64_t nsup, int splitk, uintptr_t pairs, uintptr_t part, double s1, double syh,
-                                 double syl, uintptr_t scales, uintptr_t out, uintptr_t stream, int ring, int waves,
-                                 bool fold) {
-    WideArgs a = wide_args(X, Xaug, zeros, nt, npanels, d, nsup, splitk, part, s1, syh, syl);
-    gram_wide(eb, a, P<const int>(pairs), P<const float>(scales), P<double>(out), as_stream(stream), ring, waves, fold);
+                                 int64_t nsup, int splitk, uintptr_t pairs, uintptr_t part, uintptr_t aug_scale,
+                                 uintptr_t scales, uintptr_t out, uintptr_t stream, int ring, bool fold) {
+    WideArgs a = wide_args(X, Xaug, zeros, nt, npanels, d, nsup, splitk, part, aug_scale);
+    gram_wide(eb, a, P<const int>(pairs), P<const float>(scales), P<double>(out), as_stream(stream), ring, fold);
   });
   m.def("gram_wide_queue", [wide_args](int eb, uintptr_t X, uintptr_t Xaug, uintptr_t zeros, int nt, int npanels,
-                                       int d, int64_t nsup, int h, uintptr_t pairs, uintptr_t part, double s1,
-                                       double syh, double syl, uintptr_t scales, uintptr_t out, uintptr_t heads,
-                                       int grid, uintptr_t stream, int waves, bool fold) {
-    WideArgs a = wide_args(X, Xaug, zeros, nt, npanels, d, nsup, 8 * h, part, s1, syh, syl);
+                                       int d, int64_t nsup, int h, uintptr_t pairs, uintptr_t part, uintptr_t aug_scale,
+                                       uintptr_t scales, uintptr_t out, uintptr_t heads, int grid, uintptr_t stream,
+                                       bool fold) {
+    WideArgs a = wide_args(X, Xaug, zeros, nt, npanels, d, nsup, 8 * h, part, aug_scale);
     gram_wide_queue(eb, a, P<const int>(pairs), P<const float>(scales), P<double>(out), P<int>(heads), h, grid,
-                    as_stream(stream), waves, fold);
+                    as_stream(stream), fold);
   });
   m.def("gram_wide_gang", [wide_args](int eb, uintptr_t X, uintptr_t Xaug, uintptr_t zeros, int nt, int npanels,
-                                      int d, int64_t nsup, int S, uintptr_t pairs, uintptr_t part, double s1,
-                                      double syh, double syl, uintptr_t scales, uintptr_t out, int grid,
-                                      uintptr_t stream, bool fold, int waves, uintptr_t bar) {
-    WideArgs a = wide_args(X, Xaug, zeros, nt, npanels, d, nsup, 8 * S, part, s1, syh, syl);
+                                      int d, int64_t nsup, int S, uintptr_t pairs, uintptr_t part, uintptr_t aug_scale,
+                                      uintptr_t scales, uintptr_t out, int grid, uintptr_t stream, bool fold,
+                                      uintptr_t bar) {
+    WideArgs a = wide_args(X, Xaug, zeros, nt, npanels, d, nsup, 8 * S, part, aug_scale);
     gram_wide_gang(eb, a, P<const int>(pairs), P<const float>(scales), P<double>(out), S, grid, as_stream(stream),
-                   fold, waves, P<int>(bar));
+                   fold, P<int>(bar));
   });
-  m.def("gram_wide_gangx_ints", &gram_wide_gangx_ints);
-  m.def("gram_wide_gangx", [wide_args](int eb, uintptr_t X, uintptr_t Xaug, uintptr_t zeros, int nt, int npanels,
-                                       int d, int64_t nsup, int S, uintptr_t pairs, uintptr_t part, double s1,
-                                       double syh, double syl, uintptr_t scales, uintptr_t out, int grid, uintptr_t q,
-                                       uintptr_t xcc_dbg, uintptr_t stream, bool fold) {
-    WideArgs a = wide_args(X, Xaug, zeros, nt, npanels, d, nsup, 8 * S, part, s1, syh, syl);
-    gram_wide_gangx(eb, a, P<const int>(pairs), P<const float>(scales), P<double>(out), S, grid, P<int>(q),
-                    P<int>(xcc_dbg), as_stream(stream), fold);
-  });
-  m.def("gram_wide_fold", [wide_args](int npanels, int d, int splitk, uintptr_t part, double s1, double syh,
-                                      double syl, uintptr_t scales, uintptr_t out, uintptr_t out32, int J0, int J1,
+  m.def("gram_wide_fold", [wide_args](int npanels, int d, int splitk, uintptr_t part, uintptr_t aug_scale,
+                                      uintptr_t scales, uintptr_t out, uintptr_t out32, int J0, int J1,
                                       uintptr_t stream) {
-    WideArgs a = wide_args(0, 0, 0, 0, npanels, d, 0, splitk, part, s1, syh, syl);
+    WideArgs a = wide_args(0, 0, 0, 0, npanels, d, 0, splitk, part, aug_scale);
     gram_wide_fold(a, P<const float>(scales), P<double>(out), P<float>(out32), J0, J1, as_stream(stream));
   });
 

@@ -6,6 +6,10 @@
 // that follows was ~200 small torch launches (an 8.4 M-entry index scatter to build the dense
 // system, then ~12 elementwise / dot / gemv ops per CG iteration) and took ~5 ms, almost all of
 // it host issue and launch gaps (kernel trace: 1.65 ms of kernel time in a 5.0 ms tail).  Here:
+//  * wls_head_kernel      one thread: the label / weight statistics of the head -> wSum, bStd, the
+//                         label mean, the effective L2 and the short-circuit status (no weight,
+//                         constant label: the host driver's cases), into the control block -- no
+//                         launch of the solve needs a host read, so a fit enqueues it whole;
 //  * wls_prep_kernel      one thread per feature: population std, standardized means, the L2
 //                         diagonal, the right-hand side (same algebra and operation order as
 //                         csrc/host/wls.cpp and models/optim.py);
@@ -18,7 +22,8 @@
 //                         and axpys of the iteration, block reductions in LDS).  Converged
 //                         iterations exit at their first instruction, so a fixed chunk of
 //                         iterations needs no host check; the host reads one control block per
-//                         chunk (state + x + coefficients).
+//                         chunk (state + x + coefficients) -- or, for an asynchronous fit, once,
+//                         when the model is first read (models/regression.py _PendingWLS).
 // Everything is fixed-order (no atomics): bitwise deterministic run to run.
 #include <hip/hip_runtime.h>
 
@@ -50,16 +55,30 @@ __device__ __forceinline__ double block_sum(double v, double* red) {
   return t;
 }
 
+// same algebra as models/optim.py _wls_device / csrc/host/wls.cpp: population label std, the
+// elastic-net L2 part of the standardized regularization
+__global__ void wls_head_kernel(const double* __restrict__ flat, double reg, double enet, double* __restrict__ o) {
+  const double wSum = flat[1], bSum = flat[3], bbSum = flat[4];
+  const double bBar = wSum > 0.0 ? bSum / wSum : 0.0;
+  const double bStd = wSum > 0.0 ? sqrt(fmax(bbSum / wSum - bBar * bBar, 0.0)) : 0.0;
+  const bool sc = !(wSum > 0.0) || bStd == 0.0;  // the native driver owns these cases' semantics
+  for (int i = 0; i < 5; ++i) o[PCG_HEAD + i] = flat[i];
+  o[PCG_WSUM] = wSum;
+  o[PCG_BSTD] = sc ? 1.0 : bStd;
+  o[PCG_BBAR] = bBar;
+  o[PCG_EFFL2] = sc ? 0.0 : (1.0 - enet) * reg / bStd;
+  o[PCG_STATUS] = sc ? 1.0 : 0.0;
+  o[PCG_BAD] = 0.0;
+  o[PCG_ITERS] = 0.0;
+}
+
 __global__ __launch_bounds__(256) void wls_prep_kernel(const double* __restrict__ flat, int nf, int fit_intercept,
-                                                       double wSum, double bStd, double rawBBar, double eff_l2,
                                                        int std_f, int std_l, double* __restrict__ aStd,
                                                        double* __restrict__ aBar, double* __restrict__ lam,
                                                        double* __restrict__ b, double* __restrict__ o) {
   const int j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j == 0) {
-    o[PCG_BAD] = 0.0;
-    if (fit_intercept) b[nf] = rawBBar / bStd;
-  }
+  const double wSum = o[PCG_WSUM], bStd = o[PCG_BSTD], eff_l2 = o[PCG_EFFL2];
+  if (j == 0 && fit_intercept) b[nf] = o[PCG_BBAR] / bStd;
   if (j >= nf) return;
   const double* aSum = flat + 5;
   const double* abSum = flat + 5 + nf;
@@ -94,7 +113,7 @@ __device__ __forceinline__ double dense_val(const double* __restrict__ aaP, cons
 
 // block t = one lower tile (tr >= tc) of the T x T tile grid; writes tile (tr, tc) and its mirror
 __global__ __launch_bounds__(256) void wls_dense_kernel(const double* __restrict__ flat, int nf, int k,
-                                                        double wSum, const double* __restrict__ aStd,
+                                                        const double* __restrict__ aStd,
                                                         const double* __restrict__ aBar,
                                                         const double* __restrict__ lam, double* __restrict__ A,
                                                         double* __restrict__ minv, double* __restrict__ o) {
@@ -106,6 +125,7 @@ __global__ __launch_bounds__(256) void wls_dense_kernel(const double* __restrict
   const int tc = (int)(t - (int64_t)tr * (tr + 1) / 2);
   const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
   const double* aaP = flat + 5 + 2 * nf;
+  const double wSum = o[PCG_WSUM];
   const int c = tc * 32 + tx;
 #pragma unroll
   for (int m = 0; m < 4; ++m) {
@@ -116,7 +136,7 @@ __global__ __launch_bounds__(256) void wls_dense_kernel(const double* __restrict
       tile[rr][tx] = v;
       if (r == c) {
         minv[r] = 1.0 / v;
-        if (!(v > 0.0)) o[PCG_BAD] = 1.0;
+        if (!(v > 0.0)) o[PCG_BAD] = 1.0;  // (a short-circuit head leaves BAD alone: STATUS rules)
       }
     }
   }
@@ -152,7 +172,9 @@ __global__ __launch_bounds__(kUpdThreads) void pcg_init_kernel(const double* __r
     o[PCG_RZ] = rz;
     o[PCG_THR] = thr;
     o[PCG_RR] = bb;
-    o[PCG_CONV] = bb <= thr ? 1.0 : 0.0;
+    // a short-circuit head or a non-positive diagonal: nothing to iterate (every later kernel of
+    // the solve exits at once; the host reads STATUS / BAD and takes the exact fallback)
+    o[PCG_CONV] = (bb <= thr || o[PCG_STATUS] != 0.0 || o[PCG_BAD] != 0.0) ? 1.0 : 0.0;
     o[PCG_OK] = 0.0;
   }
 }
@@ -206,6 +228,7 @@ __global__ __launch_bounds__(kUpdThreads) void pcg_update_kernel(const double* _
     o[PCG_RZ] = rzn;
     o[PCG_RR] = rrn;
     o[PCG_CONV] = rrn <= thr ? 1.0 : 0.0;
+    o[PCG_ITERS] += 1.0;
   }
 }
 
@@ -213,8 +236,10 @@ __global__ __launch_bounds__(kUpdThreads) void pcg_update_kernel(const double* _
 __global__ __launch_bounds__(kUpdThreads) void pcg_residual_kernel(const double* __restrict__ b,
                                                                    const double* __restrict__ Ax,
                                                                    const double* __restrict__ aStd, int k, int nf,
-                                                                   double bStd, double* __restrict__ o) {
+                                                                   double* __restrict__ o) {
   __shared__ double red[kUpdThreads / 64];
+  if (o[PCG_STATUS] != 0.0 || o[PCG_BAD] != 0.0) return;  // block-uniform
+  const double bStd = o[PCG_BSTD];
   const double* x = o + PCG_STATE_WORDS;
   double* coef = o + PCG_STATE_WORDS + k;
   double s = 0.0;
@@ -229,14 +254,15 @@ __global__ __launch_bounds__(kUpdThreads) void pcg_residual_kernel(const double*
 
 }  // namespace
 
-void wls_assemble(const double* flat, int nf, int fit_intercept, double wSum, double bStd, double rawBBar,
-                  double eff_l2, int std_f, int std_l, double* A, double* b, double* minv, double* aStd,
-                  double* aBar, double* lam, double* o, hipStream_t st) {
+void wls_assemble(const double* flat, int nf, int fit_intercept, double reg, double enet, int std_f, int std_l,
+                  double* A, double* b, double* minv, double* aStd, double* aBar, double* lam, double* o,
+                  hipStream_t st) {
   const int k = fit_intercept ? nf + 1 : nf;
+  hipLaunchKernelGGL(wls_head_kernel, dim3(1), dim3(1), 0, st, flat, reg, enet, o);
   hipLaunchKernelGGL(wls_prep_kernel, dim3((nf + 255) / 256 > 0 ? (nf + 255) / 256 : 1), dim3(256), 0, st, flat, nf,
-                     fit_intercept, wSum, bStd, rawBBar, eff_l2, std_f, std_l, aStd, aBar, lam, b, o);
+                     fit_intercept, std_f, std_l, aStd, aBar, lam, b, o);
   const int64_t T = (k + 31) / 32;
-  hipLaunchKernelGGL(wls_dense_kernel, dim3((unsigned)(T * (T + 1) / 2)), dim3(256), 0, st, flat, nf, k, wSum, aStd,
+  hipLaunchKernelGGL(wls_dense_kernel, dim3((unsigned)(T * (T + 1) / 2)), dim3(256), 0, st, flat, nf, k, aStd,
                      aBar, lam, A, minv, o);
   DQ_HIP_CHECK(hipGetLastError());
 }
@@ -247,15 +273,15 @@ void wls_pcg_init(const double* b, const double* minv, int k, double rtol, doubl
   DQ_HIP_CHECK(hipGetLastError());
 }
 
-void wls_pcg_chunk(const double* A, const double* b, const double* minv, const double* aStd, int k, int nf,
-                   double bStd, int iters, double* o, double* r, double* p, double* Ap, hipStream_t st) {
+void wls_pcg_chunk(const double* A, const double* b, const double* minv, const double* aStd, int k, int nf, int iters,
+                   double* o, double* r, double* p, double* Ap, hipStream_t st) {
   const dim3 mv((k + 3) / 4);
   for (int i = 0; i < iters; ++i) {
     hipLaunchKernelGGL(pcg_matvec_kernel, mv, dim3(256), 0, st, A, p, Ap, k, o, 1);
     hipLaunchKernelGGL(pcg_update_kernel, dim3(1), dim3(kUpdThreads), 0, st, minv, Ap, k, o, r, p);
   }
   hipLaunchKernelGGL(pcg_matvec_kernel, mv, dim3(256), 0, st, A, o + PCG_STATE_WORDS, Ap, k, o, 0);
-  hipLaunchKernelGGL(pcg_residual_kernel, dim3(1), dim3(kUpdThreads), 0, st, b, Ap, aStd, k, nf, bStd, o);
+  hipLaunchKernelGGL(pcg_residual_kernel, dim3(1), dim3(kUpdThreads), 0, st, b, Ap, aStd, k, nf, o);
   DQ_HIP_CHECK(hipGetLastError());
 }
 

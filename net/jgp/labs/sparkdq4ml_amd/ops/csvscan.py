@@ -352,7 +352,7 @@ def infer_streamed(src, sep: str, ncols: Optional[int] = None, sharded: bool = F
     streamed device parse whose column planes are dropped chunk by chunk -- only the type masks and
     the facts survive, so memory stays at one chunk.  Returns (type codes, facts) or None (the
     input needs the host scanner)."""
-    if len(sep) != 1:
+    if len(sep) != 1 or ord(sep) >= 128:  # (the device tokenizer matches one ASCII byte)
         return None
     if user_types:
         if any(t not in STRICT_CODES for t in user_types):
@@ -439,7 +439,7 @@ def scan_device(data, sep: str = ",", infer: bool = True, device=None, ncols: Op
 
     ``device_ready``: [(end offset, piece)] of a ``device_data`` upload still in flight: each
     chunk waits only for the pieces it covers (runtime.filecache progressive upload)."""
-    if len(sep) != 1 or not (infer or user_types):
+    if len(sep) != 1 or ord(sep) >= 128 or not (infer or user_types):  # (one ASCII separator byte)
         return None
     if user_types:
         if any(t not in STRICT_CODES for t in user_types):

@@ -195,11 +195,12 @@ class DeferredGram:
 
 def gram_stats(X, y, w, sel, compute: str = "fp64", x_zero_dead: bool = False, blocks: Optional[int] = None,
                defer: bool = False):
-    """WLS statistics.  ``defer``: the tiled bf16 path may return a :class:`DeferredGram` (call
-    ``finish()``); every other path returns the final tensor."""
+    """WLS statistics.  ``defer``: the tiled bf16 path may return a :class:`DeferredGram`, the wide
+    fragment path a :class:`DeferredWide` (call ``finish()``); every other path returns the final
+    tensor."""
     h = native.hip()
     if isinstance(X, TiledWide):
-        return _gram_wide(h, X, y, w, sel, x_zero_dead)
+        return _gram_wide(h, X, y, w, sel, x_zero_dead, defer)
     if isinstance(X, TiledBF16):
         return _gram_tiled(h, X, y, w, sel, x_zero_dead, blocks, defer)
     _check_dev(X, y, w, sel)
@@ -844,6 +845,11 @@ class LsqPasses:
         return out
 
 
+    def qn_eligible(self) -> bool:
+        """The device l-bfgs / OWLQN forms apply: wide tile layout, 1 <= d <= LSQ_QN_MAX_D (an empty
+        row shard is eligible: its passes contribute zero partials)."""
+        return self.layout in (2, 3) and 1 <= self.d <= int(self._h.LSQ_QN_MAX_D)
+
     def qn_fit(self, head: torch.Tensor, fit_icpt: bool, std_f: bool, reg: float, enet: float, max_iter: int,
                tol: float) -> Optional[torch.Tensor]:
         """The whole squared-loss l-bfgs / OWLQN fit as ONE cooperative launch (``lsq_qn.hip``):
@@ -881,11 +887,17 @@ class LsqPasses:
         read back per evaluation: evaluations are enqueued ``batch`` at a time, at most two batches
         ahead of the device, and enqueueing stops once a pinned copy of the state's action reads
         "done" (the kernels of a batch enqueued past the end return at once).  Same output layout
-        as :meth:`qn_fit`."""
+        as :meth:`qn_fit`.
+
+        Host-synchronous in time, not in API: no call here blocks on the device (events are
+        polled, copies are pinned and non-blocking, so ``sync_debug_mode("error")`` stays quiet),
+        but the host keeps enqueueing until the optimizer is done -- under collectives an
+        ``dq4ml.fit.async`` l-bfgs fit therefore returns only after the device fit has run.  (The
+        one-launch single-rank form, :meth:`qn_fit`, returns at once.)"""
         import time
 
         h = self._h
-        if self.layout not in (2, 3) or not 1 <= self.d <= int(h.LSQ_QN_MAX_D) or self.n < 1:
+        if not self.qn_eligible():  # (the caller has agreed eligibility over the ranks)
             return None
         key = (self.device.index, self.layout, self.d)
         nb = _lsq_qn_grid.get(key)
@@ -997,7 +1009,8 @@ def _qn_grid_blocks(h, k):
 
 
 # control-block layout of wls_large.h (WlsPcgState), checked against the module on first use
-PCG_STATE_WORDS, PCG_CONV, PCG_BAD, PCG_OK = 8, 3, 4, 5
+PCG_STATE_WORDS, PCG_CONV, PCG_BAD, PCG_OK, PCG_ITERS, PCG_STATUS, PCG_HEAD = 24, 3, 4, 5, 6, 7, 12
+PCG_WSUM, PCG_BSTD = 8, 9
 
 
 @dataclass
@@ -1007,17 +1020,22 @@ class WlsSystem:
     b: torch.Tensor      # [k]
     minv: torch.Tensor   # [k] Jacobi preconditioner
     aStd: torch.Tensor   # [nf] population std of every feature
-    o: torch.Tensor      # control block [state(8) | x(k) | coef(nf)]
+    o: torch.Tensor      # control block [state(PCG_STATE_WORDS) | x(k) | coef(nf)]
     k: int
+    work: torch.Tensor   # [3k] PCG vectors r | p | Ap
 
 
-def wls_assemble(flat: torch.Tensor, nf: int, fit_intercept: bool, wSum: float, bStd: float, rawBBar: float,
-                 eff_l2: float, std_f: bool, std_l: bool) -> WlsSystem:
-    """Standardized dense system of the large-k WLS branch from the flat statistics (no host sync)."""
+def wls_assemble(flat: torch.Tensor, nf: int, fit_intercept: bool, reg: float, enet: float, std_f: bool,
+                 std_l: bool) -> WlsSystem:
+    """Standardized dense system of the large-k WLS branch from the flat statistics, enqueued with
+    NO host read: the head scalars (wSum, label mean and std, effective L2) and the short-circuit
+    status are computed on the device into the control block (``o[PCG_STATUS]`` set: the host
+    driver owns the case; ``o[PCG_HEAD:+5]`` the raw head statistics)."""
     h = native.hip()
     _check_dev(flat)
-    if (int(h.PCG_STATE_WORDS), int(h.PCG_CONV), int(h.PCG_BAD), int(h.PCG_OK)) != (
-            PCG_STATE_WORDS, PCG_CONV, PCG_BAD, PCG_OK):
+    if (int(h.PCG_STATE_WORDS), int(h.PCG_CONV), int(h.PCG_BAD), int(h.PCG_OK), int(h.PCG_ITERS),
+            int(h.PCG_STATUS), int(h.PCG_HEAD), int(h.PCG_WSUM), int(h.PCG_BSTD)) != (
+                PCG_STATE_WORDS, PCG_CONV, PCG_BAD, PCG_OK, PCG_ITERS, PCG_STATUS, PCG_HEAD, PCG_WSUM, PCG_BSTD):
         raise RuntimeError("wls_large: control-block layout mismatch between device.py and the HIP module")
     if flat.dtype != torch.float64 or flat.numel() != 5 + 2 * nf + nf * (nf + 1) // 2:
         raise ValueError("wls_assemble: flat statistics have the wrong dtype/length")
@@ -1028,36 +1046,53 @@ def wls_assemble(flat: torch.Tensor, nf: int, fit_intercept: bool, wSum: float, 
     b, minv = vec[:k], vec[k:2 * k]
     aStd, aBar, lam = vec[2 * k:2 * k + nf], vec[2 * k + nf:2 * k + 2 * nf], vec[2 * k + 2 * nf:]
     o = torch.zeros(PCG_STATE_WORDS + k + nf, dtype=torch.float64, device=dev)
-    h.wls_assemble(flat.data_ptr(), int(nf), bool(fit_intercept), float(wSum), float(bStd), float(rawBBar),
-                   float(eff_l2), bool(std_f), bool(std_l), A.data_ptr(), b.data_ptr(), minv.data_ptr(),
-                   aStd.data_ptr(), aBar.data_ptr(), lam.data_ptr(), o.data_ptr(), _stream())
-    return WlsSystem(A, b, minv, aStd, o, k)
+    h.wls_assemble(flat.data_ptr(), int(nf), bool(fit_intercept), float(reg), float(enet), bool(std_f), bool(std_l),
+                   A.data_ptr(), b.data_ptr(), minv.data_ptr(), aStd.data_ptr(), aBar.data_ptr(), lam.data_ptr(),
+                   o.data_ptr(), _stream())
+    return WlsSystem(A, b, minv, aStd, o, k, torch.empty(3 * k, dtype=torch.float64, device=dev))
 
 
-def wls_pcg(sysm: WlsSystem, nf: int, bStd: float, rtol: float, chunk: int = 8,
-            max_iter: int = 96) -> Optional[np.ndarray]:
-    """Jacobi-PCG on the assembled system: ``chunk`` iterations per host check (one D2H of the
-    control block).  Returns the host control block ``[state | x | coef]`` once CG has converged
-    AND the true residual passes, None when a diagonal entry is not > 0 or CG has not converged
-    within ``max_iter`` (the caller falls back to Cholesky)."""
+def wls_pcg_enqueue(sysm: WlsSystem, nf: int, rtol: float, iters: int) -> None:
+    """Jacobi-PCG start + ``iters`` iterations + the true-residual check, enqueued with no host
+    read (iterations after convergence -- or on a STATUS / BAD system -- exit at once)."""
     h = native.hip()
-    k, dev = sysm.k, sysm.A.device
-    r = torch.empty(k, dtype=torch.float64, device=dev)
-    p = torch.empty_like(r)
-    Ap = torch.empty_like(r)
-    st = _stream()
+    k = sysm.k
+    r, p = sysm.work[:k], sysm.work[k:2 * k]
     h.wls_pcg_init(sysm.b.data_ptr(), sysm.minv.data_ptr(), k, float(rtol), sysm.o.data_ptr(), r.data_ptr(),
-                   p.data_ptr(), st)
-    for _ in range(0, max_iter, chunk):
-        h.wls_pcg_chunk(sysm.A.data_ptr(), sysm.b.data_ptr(), sysm.minv.data_ptr(), sysm.aStd.data_ptr(), k,
-                        int(nf), float(bStd), int(chunk), sysm.o.data_ptr(), r.data_ptr(), p.data_ptr(),
-                        Ap.data_ptr(), st)
+                   p.data_ptr(), _stream())
+    wls_pcg_more(sysm, nf, iters)
+
+
+def wls_pcg_more(sysm: WlsSystem, nf: int, iters: int) -> None:
+    """``iters`` more PCG iterations (+ the residual check) on the current stream."""
+    h = native.hip()
+    k = sysm.k
+    r, p, Ap = sysm.work[:k], sysm.work[k:2 * k], sysm.work[2 * k:]
+    h.wls_pcg_chunk(sysm.A.data_ptr(), sysm.b.data_ptr(), sysm.minv.data_ptr(), sysm.aStd.data_ptr(), k, int(nf),
+                    int(iters), sysm.o.data_ptr(), r.data_ptr(), p.data_ptr(), Ap.data_ptr(), _stream())
+
+
+def wls_pcg_drive(sysm: WlsSystem, nf: int, o: np.ndarray, done: int, chunk: int = 8, max_iter: int = 96) -> np.ndarray:
+    """Continue a PCG whose host control block ``o`` (after ``done`` iterations) has not converged:
+    ``chunk`` iterations per host check, up to ``max_iter``.  Returns the last host control block."""
+    while (o[PCG_CONV] == 0.0 and o[PCG_STATUS] == 0.0 and o[PCG_BAD] == 0.0 and done < max_iter):
+        wls_pcg_more(sysm, nf, chunk)
+        done += chunk
         o = sysm.o.cpu().numpy()
-        if o[PCG_BAD] != 0.0:  # a diagonal entry <= 0 (or NaN)
-            return None
-        if o[PCG_CONV] != 0.0:
-            return o if o[PCG_OK] != 0.0 else None  # the true residual check
-    return None
+    return o
+
+
+def wls_pcg(sysm: WlsSystem, nf: int, rtol: float, chunk: int = 8, max_iter: int = 96) -> np.ndarray:
+    """Jacobi-PCG on the assembled system, ``chunk`` iterations per host check (one D2H of the
+    control block).  Returns the host control block ``[state | x | coef]``; it holds a usable
+    solution iff ``pcg_ok(o)`` -- CG converged AND the true residual passed, no short-circuit
+    status, every diagonal entry > 0 (else the caller takes the host driver / Cholesky)."""
+    wls_pcg_enqueue(sysm, nf, rtol, chunk)
+    return wls_pcg_drive(sysm, nf, sysm.o.cpu().numpy(), chunk, chunk, max_iter)
+
+
+def pcg_ok(o: np.ndarray) -> bool:
+    return o[PCG_STATUS] == 0.0 and o[PCG_BAD] == 0.0 and o[PCG_CONV] != 0.0 and o[PCG_OK] != 0.0
 
 
 # ------------------------------------------------------------------------------------------
@@ -1229,7 +1264,6 @@ def _wide_gang_s(P: int, nsup: int, G: int) -> int:
 
 
 _wide_grids = {}
-_last_xcc = None  # (diagnostics, DQ4ML_WIDE_XCCDBG=1) each gangx block's XCD from the last wide Gram
 
 
 def _wide_grid(h) -> int:
@@ -1241,7 +1275,108 @@ def _wide_grid(h) -> int:
     return _wide_grids[dev]
 
 
-def _gram_wide(h, T: TiledWide, y, w, sel, x_zero_dead):
+@dataclass
+class _WideSchedule:
+    """Launch constants of one wide Gram shape (cached: a repeated fit re-uses the device pair table
+    and the split choice instead of rebuilding and re-uploading them)."""
+    sched: str            # "gang" | "queue" | "grid"
+    splitk: int
+    S: int                # gang row ranges per group (0: not the gang schedule)
+    hq: int               # queue row ranges per group (0: not the queue schedule)
+    pairs_dev: torch.Tensor
+
+
+_wide_sched_cache = {}
+
+
+def _wide_schedule(h, P: int, nsup: int, eb: int, dev) -> _WideSchedule:
+    """Gang (default; equal-cost units, 8 XCD groups x S row ranges) when the unit count fills the
+    groups to >= 90 %, else the persistent queue, else the static split-K grid (few rows)."""
+    grid = _wide_grid(h)
+    forced = os.environ.get("DQ4ML_WIDE_SCHED", "gang")
+    key = (dev, P, nsup, eb, grid, forced, os.environ.get("DQ4ML_WIDE_GANG_S"), os.environ.get("DQ4ML_WIDE_H"))
+    sc = _wide_sched_cache.get(key)
+    if sc is not None:
+        return sc
+    pairs = _wide_pairs(P)
+    gs = _wide_gang_s(P, nsup, grid // 8) if forced == "gang" else 0
+    hq = _wide_queue_h(nsup) if not gs and forced in ("gang", "queue") else 0
+    if gs:  # gang units: the off-diagonal pairs first, then the diagonal ones (gram_wide.hip gang_unit)
+        pairs = [p for p in pairs if p[0] != p[1] and p[1] < P] + [p for p in pairs if p[0] == p[1] and p[1] < P]
+        sched, splitk = "gang", 8 * gs
+    elif hq:
+        sched, splitk = "queue", 8 * hq
+    else:
+        sched = "grid"
+        splitk = _wide_splitk(P, nsup, eb)
+        # f32 MFMA accumulators count rows exactly only below 2^24 per split
+        splitk = max(1, min(max(splitk, -(-nsup * 64 // (1 << 23))), nsup))
+    sc = _WideSchedule(sched, splitk, gs, hq, _h2d(np.asarray(pairs, dtype=np.int32).reshape(-1), dev))
+    _wide_sched_cache[key] = sc
+    return sc
+
+
+_aug_ones = {}
+
+
+def _label_split(yd: torch.Tensor, live: torch.Tensor, eb: int):
+    """The label's augmentation columns for the wide SYRK, entirely on the device (no host read):
+    ``(cols, inv_scale, aug_scale, t)`` with cols = [live, y_hi, y_lo] (f32), ``aug_scale`` the
+    device f64[3] scales of those columns that the fold applies, ``inv_scale`` their f32 inverses
+    for the fp8 pack (None for bf16) and ``t`` the label shift (device scalar, None for bf16).
+
+    bf16: y = y_hi + y_lo, y_hi = bf16(y).  fp8: the label is centred first (t = its live mean: two
+    e4m3 digits of y - t carry ~8 bits relative to the label's spread instead of to its largest
+    magnitude), then y - t = y_hi + y_lo, each an e4m3 value times its own scale (the amax of the
+    part / 448)."""
+    dev = yd.device
+    if eb == 16:
+        ones = _aug_ones.get(dev)
+        if ones is None:
+            ones = _aug_ones[dev] = torch.ones(3, dtype=torch.float64, device=dev)
+        y_hi = yd.to(torch.bfloat16).to(torch.float64)
+        return [live.to(torch.float32), (y_hi * live).to(torch.float32), ((yd - y_hi) * live).to(torch.float32)], \
+            None, ones, None
+    one = torch.ones((), dtype=torch.float64, device=dev)
+    t = (yd * live).sum() / live.sum().clamp_min(1.0)
+    yc = (yd - t) * live
+    amax_h = yc.abs().max()
+    s_h = torch.where(amax_h > 0, amax_h / FP8_MAX, one)
+    y_hi = (yc / s_h).clamp(-FP8_MAX, FP8_MAX).to(torch.float8_e4m3fn).to(torch.float64) * s_h
+    y_lo = yc - y_hi
+    amax_l = y_lo.abs().max()
+    s_l = torch.where(amax_l > 0, amax_l / FP8_MAX, one)
+    aug = torch.stack([one, s_h, s_l])
+    return [live.to(torch.float32), y_hi.to(torch.float32), y_lo.to(torch.float32)], \
+        (1.0 / aug).to(torch.float32), aug, t
+
+
+class DeferredWide:
+    """Wide SYRK partials whose split-K fold (+ RCCL all-reduce, band by band) has not been
+    enqueued yet: an asynchronous overlapped fit runs it on its side stream with the solve, so the
+    compute stream goes on to the next fit's SYRK at once -- the fold kernels (no LDS, 22 VGPRs)
+    co-reside with the SYRK's one block per CU in its spare wave slots."""
+
+    is_cuda = True
+
+    def __init__(self, run, keep, out):
+        self._run, self._keep, self.out = run, keep, out
+        self.device = out.device
+
+    def finish(self) -> torch.Tensor:
+        st = faststream.current(faststream.dev_index(self.device))
+        for t in self._keep:
+            if t is not None:
+                t.record_stream(st)
+        return self._run()
+
+
+def _gram_wide(h, T: TiledWide, y, w, sel, x_zero_dead, defer: bool = False):
+    """Wide (d > 64) statistics: the LDS-tiled MFMA SYRK over the fragment storage plus the label's
+    augmentation panel, folded to the flat WLS layout (band by band under RCCL, each band's
+    all-reduce in flight while the next folds).  Enqueued on the current stream with NO host read:
+    the label split, its scales and the label shift stay on the device, so an asynchronous fit
+    (``dq4ml.fit.async``) runs ahead of the GPU."""
     if w is not None:
         # instance weights: the exact-f32 MFMA SYRK (per-row weight in-kernel) on the stored values
         return _gram_syrk(h, T.to_dense(), y, w, sel, compute_f64=False)
@@ -1256,103 +1391,54 @@ def _gram_wide(h, T: TiledWide, y, w, sel, x_zero_dead):
     yd = y.to(torch.float64)
     live = torch.ones(n, dtype=torch.float64, device=dev) if sel is None else sel.to(torch.float64)
     eb = T.eb
-    t_y = 0.0
-    if eb == 16:
-        y_hi = yd.to(torch.bfloat16).to(torch.float64)
-        inv = None
-        s_h = s_l = 1.0
-    else:  # y = y_hi + y_lo, each an fp8 value times its own scale (y_hi exactly representable)
-        # the label is centred first (t = its live mean): two e4m3 digits of y - t carry ~8 bits
-        # relative to the label's spread instead of to its largest magnitude (ops/shift.py)
-        t_y = float((yd * live).sum() / live.sum().clamp_min(1.0)) if n else 0.0
-        yd = (yd - t_y) * live
-        amax_h = float((yd * live).abs().max()) if n else 0.0
-        s_h = amax_h / FP8_MAX if amax_h > 0 else 1.0
-        y_hi = (yd / s_h).clamp(-FP8_MAX, FP8_MAX).to(torch.float8_e4m3fn).to(torch.float64) * s_h
-    y_lo = yd - y_hi
-    if eb == 8:
-        amax_l = float((y_lo * live).abs().max()) if n else 0.0
-        s_l = amax_l / FP8_MAX if amax_l > 0 else 1.0
-        inv = _h2d(np.asarray([1.0, 1.0 / s_h, 1.0 / s_l], dtype=np.float32), dev)
-    cols = [live.to(torch.float32), (y_hi * live).to(torch.float32), (y_lo * live).to(torch.float32)]
+    cols, inv, aug_scale, t_y = _label_split(yd, live, eb)
     aug = pack_wide(cols, eb, None, nt=1, inv_scale=inv, shift=None)
     P = (d + 255) // 256
-    pairs = _wide_pairs(P, os.environ.get("DQ4ML_WIDE_ORDER", "morton"))
     nsup = max(1, (n + 63) // 64)
-    splitk = int(os.environ.get("DQ4ML_WIDE_SPLITK", "0")) or _wide_splitk(P, nsup, eb)
-    # f32 MFMA accumulators count rows exactly only below 2^24 per split
-    splitk = max(1, min(max(splitk, -(-nsup * 64 // (1 << 23))), nsup))
-    if os.environ.get("DQ4ML_WIDE_SAMEPAIR"):  # diagnostic only (wrong results): every block reads panels 0, 1
-        pairs = [(0, 1)] * len(pairs)
-    pairs_dev = _h2d(np.asarray(pairs, dtype=np.int32).reshape(-1), dev)
+    sc = _wide_schedule(h, P, nsup, eb, dev)
+    splitk = sc.splitk
     out = torch.empty(5 + 2 * d + d * (d + 1) // 2, dtype=torch.float64, device=dev)
-    sched = os.environ.get("DQ4ML_WIDE_SCHED", "gang")
-    waves = int(os.environ.get("DQ4ML_WIDE_WAVES", "8"))  # (81 / 82: timing-only ablations, grid and gang)
-    gs = (_wide_gang_s(P, nsup, _wide_grid(h) // 8)
-          if sched in ("gang", "gangx") and waves in (8, 81, 82, 91, 94, 95) else 0)
-    if sched == "gangx" and waves != 8:
-        sched = "gang"
-    if sched in ("gang", "gangx") and not gs:
-        sched = "queue"
-    hq = _wide_queue_h(nsup) if sched == "queue" and waves == 8 else 0
+    part = torch.empty(int(h.gram_wide_partials(d, splitk)), dtype=torch.float32, device=dev)
     # data-parallel fit over RCCL: fold band by band and all-reduce each band while the next folds
     banded = comm.collectives_active() and comm.backend() == "nccl"
-    if gs:  # gang units: the off-diagonal pairs first, then the diagonal ones (gram_wide.hip gang_unit)
-        pairs = [p for p in pairs if p[0] != p[1]] + [p for p in pairs if p[0] == p[1]]
-    if gs and sched == "gangx":
-        # XCD-keyed gang (gram_wide_gangx_kernel): the group is the XCD a block runs on, units
-        # dequeued per XCD (steal when empty) -- locality that does not assume round-robin dispatch
-        global _last_xcc
-        splitk = 8 * gs
-        gpairs = [p for p in pairs if p[1] < P]
-        gpairs_dev = _h2d(np.asarray(gpairs, dtype=np.int32).reshape(-1), dev)
-        part = torch.empty(int(h.gram_wide_partials(d, splitk)), dtype=torch.float32, device=dev)
-        grid = _wide_grid(h)
-        q = torch.empty(int(h.gram_wide_gangx_ints(grid)), dtype=torch.int32, device=dev)
-        dbg = torch.full((grid,), -1, dtype=torch.int32, device=dev) if os.environ.get("DQ4ML_WIDE_XCCDBG") else None
-        _last_xcc = dbg
-        h.gram_wide_gangx(eb, T.buf.data_ptr(), aug.buf.data_ptr(), _zero_page(h, dev).data_ptr(), T.nt, P, d, nsup,
-                          gs, gpairs_dev.data_ptr(), part.data_ptr(), 1.0, float(s_h), float(s_l), _ptr(T.scales),
-                          out.data_ptr(), grid, q.data_ptr(), _ptr(dbg), _stream(), not banded)
-    elif gs:
-        # gang schedule (gram_wide_gang_kernel): 8 groups x S row ranges, static equal-cost units
-        splitk = 8 * gs
-        gpairs = [p for p in pairs if p[1] < P]
-        gpairs_dev = _h2d(np.asarray(gpairs, dtype=np.int32).reshape(-1), dev)
-        part = torch.empty(int(h.gram_wide_partials(d, splitk)), dtype=torch.float32, device=dev)
-        # per-round group barrier (DQ4ML_WIDE_GANG_SYNC, default on): the blocks of an XCD start
-        # every round together (profiles/r5_wide_limiter.md)
-        bar = (torch.empty(256, dtype=torch.int32, device=dev)
-               if os.environ.get("DQ4ML_WIDE_GANG_SYNC", "1") != "0" else None)
-        h.gram_wide_gang(eb, T.buf.data_ptr(), aug.buf.data_ptr(), _zero_page(h, dev).data_ptr(), T.nt, P, d, nsup,
-                         gs, gpairs_dev.data_ptr(), part.data_ptr(), 1.0, float(s_h), float(s_l), _ptr(T.scales),
-                         out.data_ptr(), _wide_grid(h), _stream(), not banded, waves, _ptr(bar))
-    elif hq:
+    fold_in = not banded and not defer  # the launch folds into `out` itself
+    args = (eb, T.buf.data_ptr(), aug.buf.data_ptr(), _zero_page(h, dev).data_ptr(), T.nt, P, d, nsup)
+    if sc.sched == "gang":
+        # gang schedule (gram_wide_gang_kernel): 8 groups x S row ranges, static equal-cost units,
+        # per-round group barrier (full rounds, bounded: the blocks of an XCD start every round
+        # together, profiles/r5_wide_limiter.md)
+        bar = torch.empty(256, dtype=torch.int32, device=dev)
+        h.gram_wide_gang(*args, sc.S, sc.pairs_dev.data_ptr(), part.data_ptr(), aug_scale.data_ptr(), _ptr(T.scales),
+                         out.data_ptr(), _wide_grid(h), _stream(), fold_in, bar.data_ptr())
+    elif sc.sched == "queue":
         # persistent XCD-grouped schedule (gram_wide_queue_kernel): 8 groups x h row ranges
-        splitk = 8 * hq
-        part = torch.empty(int(h.gram_wide_partials(d, splitk)), dtype=torch.float32, device=dev)
         heads = torch.empty(8, dtype=torch.int32, device=dev)
-        h.gram_wide_queue(eb, T.buf.data_ptr(), aug.buf.data_ptr(), _zero_page(h, dev).data_ptr(), T.nt, P, d, nsup,
-                          hq, pairs_dev.data_ptr(), part.data_ptr(), 1.0, float(s_h), float(s_l), _ptr(T.scales),
-                          out.data_ptr(), heads.data_ptr(), _wide_grid(h), _stream(), waves, not banded)
+        h.gram_wide_queue(*args, sc.hq, sc.pairs_dev.data_ptr(), part.data_ptr(), aug_scale.data_ptr(),
+                          _ptr(T.scales), out.data_ptr(), heads.data_ptr(), _wide_grid(h), _stream(), fold_in)
     else:
-        part = torch.empty(int(h.gram_wide_partials(d, splitk)), dtype=torch.float32, device=dev)
-        h.gram_wide(eb, T.buf.data_ptr(), aug.buf.data_ptr(), _zero_page(h, dev).data_ptr(), T.nt, P, d, nsup,
-                    splitk, pairs_dev.data_ptr(), part.data_ptr(), 1.0, float(s_h), float(s_l), _ptr(T.scales),
-                    out.data_ptr(), _stream(), int(os.environ.get("DQ4ML_WIDE_RING", "5")), waves, not banded)
+        h.gram_wide(*args, splitk, sc.pairs_dev.data_ptr(), part.data_ptr(), aug_scale.data_ptr(), _ptr(T.scales),
+                    out.data_ptr(), _stream(), 5, fold_in)
     if banded and T.shift is not None and not T.shift.uniform:
         raise ValueError("wide Gram over RCCL: the features' shift must be the same on every rank "
                          "(pack_wide(shift='auto') agrees it; a caller-made Shift needs uniform=True)")
-    head_fix = (lambda: _unshift_label(out, d, t_y)) if t_y != 0.0 else None
-    if banded:
-        fold = functools.partial(h.gram_wide_fold, P, d, splitk, part.data_ptr(), 1.0, float(s_h), float(s_l),
-                                 _ptr(T.scales))
-        _fold_all_reduce(fold, out, P, d, head_fix)  # (the label shift is per rank: un-shifted before the wire)
-    elif head_fix is not None:
-        head_fix()
-    # statistics of x - s -> of x (f64, after the banded all-reduce too: pack_wide's shift is the
-    # same on every rank, so the un-shift of the sum is the sum of the un-shifts)
-    return _unshift(h, out, T.shift, d)
+    head_fix = (lambda: _unshift_label(out, d, t_y)) if t_y is not None else None
+    fold = functools.partial(h.gram_wide_fold, P, d, splitk, part.data_ptr(), aug_scale.data_ptr(), _ptr(T.scales))
+
+    def finish():
+        if banded:
+            _fold_all_reduce(fold, out, P, d, head_fix)  # (the label shift is per rank: un-shifted before the wire)
+        else:
+            if not fold_in:
+                fold(out.data_ptr(), 0, 0, P + 1, _stream())
+            if head_fix is not None:
+                head_fix()
+        # statistics of x - s -> of x (f64, after the banded all-reduce too: pack_wide's shift is the
+        # same on every rank, so the un-shift of the sum is the sum of the un-shifts)
+        return _unshift(h, out, T.shift, d)
+    if defer:
+        return DeferredWide(finish, (part, aug_scale, T.scales, t_y, out,
+                                     None if T.shift is None else T.shift.dev), out)
+    return finish()
 
 
 def wide_bands(P: int, d: int, bucket_bytes: int, elt: int):
@@ -1373,8 +1459,8 @@ def wide_bands(P: int, d: int, bucket_bytes: int, elt: int):
     return bands
 
 
-def _unshift_label(out: torch.Tensor, d: int, t: float) -> None:
-    """Head statistics of a label shifted by t (y' = y - t) -> those of y, in place (f64):
+def _unshift_label(out: torch.Tensor, d: int, t) -> None:
+    """Head statistics of a label shifted by t (y' = y - t; a device scalar) -> those of y, in place (f64):
     Σy² = Σy'² + 2tΣy' + t²W, Σy = Σy' + tW, Σx·y = Σx·y' + tΣx (Σx as folded, i.e. of the
     features as they are stored)."""
     W, b = out[1:2], out[3:4].clone()

@@ -43,6 +43,7 @@ import os
 from typing import Optional
 
 import torch
+from ..utils import diag
 
 __all__ = ["applicable", "kernel_source", "try_cut_gram", "STATS", "ENTRY"]
 
@@ -476,7 +477,7 @@ def kernel_source(g, kinds, used, opts: dict, H: int, slots: dict, d: int, term:
     # diagnostic ablations (timing only, results are wrong): 1 no field conversion, 2 no Gram
     # phase (the compiler then also drops the feature conversions: nothing reads the tile), 4 no
     # row phase, 8 nothing after the cut (stage, masks, scans, scatter only)
-    abl = int(os.environ.get("DQ4ML_CUT_ABLATE", "0"))
+    abl = diag.ablation("DQ4ML_CUT_ABLATE")  # (refused without DQ4ML_DIAG=1)
     # diagnostic phase clocks (DQ4ML_CUT_STAMPS=1): s_memtime after each block barrier, per-phase
     # sums of wave 0 of every block -> the dbg slot ([grid][8] u64: phases 0-5, windows)
     stamps = os.environ.get("DQ4ML_CUT_STAMPS", "0") == "1" and "dbg" in slots

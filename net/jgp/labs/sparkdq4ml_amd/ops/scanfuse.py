@@ -33,6 +33,7 @@ import torch
 from ..runtime import faststream
 from ..runtime.checks import defer
 from ..utils import tracing
+from ..utils import diag
 
 __all__ = ["kernel_source", "ENTRY", "WINDOW", "head_bytes", "STATS"]
 
@@ -241,7 +242,7 @@ def kernel_source(g, kinds, nullable, used, opts: dict, strict: bool, head: int,
     # diagnostic ablation builds (wrong results; scripts/scan_ablation.py), bit flags: 1 no per-line
     # work, 2 no stores, 4 no look-back, 8 no line-end scatter / line loop, 16 no ticket, 32 no LDS
     # staging stores, 64 no SWAR field conversion, 128 no Gram accumulation, 256 no Gram epilogue
-    abl = int(os.environ.get("DQ4ML_SCAN_ABL", "0"))
+    abl = diag.ablation("DQ4ML_SCAN_ABL")  # (refused without DQ4ML_DIAG=1)
     # the window's line-end counts scanned by DPP (six __shfl_up ds_bpermute steps measured 1.2 %
     # slower over the lab action: profiles/r5/lab_dpp_ab.jsonl)
     scan_code = "  int inc = dq_scan_incl(c);"

@@ -26,7 +26,7 @@ __all__ = ["init", "is_initialized", "rank", "world_size", "local_rank", "barrie
            "collectives_active", "force_collectives", "backend", "rccl_version", "all_reduce_sum",
            "all_reduce_max", "broadcast", "all_gather_object", "gather_rows_to_root", "shutdown",
            "DEFAULT_BUCKET_BYTES", "set_bucket_bytes", "bucket_bytes", "set_wire_dtype", "wire_dtype",
-           "mark_reduced"]
+           "mark_reduced", "host_group", "all_agree"]
 
 DEFAULT_BUCKET_BYTES = int(os.environ.get("DQ4ML_BUCKET_BYTES", str(16 << 20)))
 _side_stream = None
@@ -120,39 +120,53 @@ def _free_port() -> int:
 
 
 def shutdown():
+    global _host_group
     if is_initialized():
         dist.destroy_process_group()
+    _host_group = None
+
+
+_host_group = None
+
+
+def host_group():
+    """A gloo group over all ranks for HOST-side control traffic (eligibility votes, the rank-health
+    barrier): nothing on it touches the GPU, so a vote needs no device sync and cannot queue behind
+    a rank's in-flight kernels.  Created on first use -- a collective call: every rank must reach
+    it in the same order (the fit paths that use it run on every rank)."""
+    global _host_group
+    if _host_group is None:
+        _host_group = dist.new_group(backend="gloo") if dist.get_backend() != "gloo" else dist.group.WORLD
+    return _host_group
+
+
+def all_agree(flag: bool) -> bool:
+    """True iff ``flag`` is true on EVERY rank (a host-side MIN over :func:`host_group`).  Per-rank
+    state that picks between code paths issuing different collectives (a device fit vs its host
+    fallback: an empty shard, a layout one rank lacks) must be agreed first, or the ranks deadlock
+    on mismatched collectives."""
+    if not collectives_active():
+        return bool(flag)
+    t = torch.tensor([1 if flag else 0], dtype=torch.int32)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=host_group())
+    return bool(int(t.item()))
 
 
 def health_check(timeout_s: float = 30.0, deferred: bool = False):
-    """Rank-health barrier: every rank contributes 1; raises :class:`RankFailure` (naming the
-    missing ranks where the backend can tell) instead of blocking forever on a dead peer.
-    ``deferred`` (RCCL): a peer that never answers still raises here (the wait's timeout), but the
-    sum is not read back -- the returned ``runtime.checks`` flag raises at the fit's first host
-    read, so an asynchronous fit stays free of host syncs."""
+    """Rank-health barrier: raises :class:`RankFailure` (naming the missing ranks) instead of
+    blocking forever on a dead peer.  Host-only (gloo control group), so it adds no device sync to
+    an asynchronous fit; ``deferred`` is accepted for the callers' API and returns None (nothing is
+    left to read on the device)."""
     if not collectives_active():
         return None
-    if dist.get_backend() == "gloo":
-        try:
-            dist.monitored_barrier(timeout=datetime.timedelta(seconds=timeout_s), wait_all_ranks=True)
-        except RuntimeError as e:
-            raise RankFailure(f"rank health check failed: {e}") from e
-        return None
-    x = torch.ones(1, device=torch.device("cuda", torch.cuda.current_device()))
-    work = dist.all_reduce(x, async_op=True)
+    # a host-side barrier over the gloo control group: it names the ranks that did not answer
+    # within the timeout, and -- unlike a device all-reduce, whose wait() only orders a stream
+    # after the collective -- it raises here, on the host, without any device sync
     try:
-        ok = work.wait(timeout=datetime.timedelta(seconds=timeout_s))
+        dist.monitored_barrier(group=host_group(), timeout=datetime.timedelta(seconds=timeout_s),
+                               wait_all_ranks=True)
     except RuntimeError as e:
         raise RankFailure(f"rank health check failed: {e}") from e
-    if ok is False:
-        raise RankFailure("rank health check: the all-reduce did not complete")
-    if deferred:
-        from ..runtime.checks import defer
-
-        n = world_size()
-        return defer(x != float(n), lambda: RankFailure(f"rank health check: the all-reduce of ones did not sum to {n}"))
-    if int(x.item()) != world_size():
-        raise RankFailure(f"rank health check: {int(x.item())} of {world_size()} ranks answered")
     return None
 
 

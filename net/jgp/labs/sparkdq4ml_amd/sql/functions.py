@@ -60,5 +60,4 @@ def udf(f=None, returnType=None):
         if f is not None and returnType is None:
             returnType = f
         return wrap
-    _ = DoubleType
     return wrap(f)

@@ -357,7 +357,7 @@ class DataFrameReader:
         # a user schema of int / long / double / boolean / timestamp / string columns; no schema
         # and no inference: every column a string (Spark's default read)
         all_str = not infer and not strict
-        use_dev = (dev.type == "cuda" and dopts is not None and len(sep) == 1
+        use_dev = (dev.type == "cuda" and dopts is not None and len(sep) == 1 and ord(sep) < 128
                    and (not strict or all(c in (1, 2, 4, 5, 7) or (c == 6 and isinstance(f.dataType, StringType))
                                           for c, f in zip(strict, self._schema.fields))))
         hdr = None

@@ -4,7 +4,7 @@ byte-parallel cutter, or the per-line fused scan with DQ4ML_SCAN_CUT=0) on the l
 BASELINE-shape wide CSV, for several environment variants in ONE process (the cutter's compile
 cache is keyed by its knobs), e.g.
 
-    VARIANTS="base;DQ4ML_SCAN_CUT=0;DQ4ML_CUT_ABLATE=1" python scripts/cut_bench.py --features 32 --rows 2e7
+    DQ4ML_DIAG=1 VARIANTS="base;DQ4ML_SCAN_CUT=0;DQ4ML_CUT_ABLATE=1" python scripts/cut_bench.py --features 32 --rows 2e7
 
 Prints one JSON line per variant: ms per action (median of --reps), CSV GB/s.
 """

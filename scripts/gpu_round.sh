@@ -34,6 +34,9 @@ for s in $STEPS; do
     widepmc5) (export TMPDIR=/tmp N=${N:-2e6} D=4096 EB=8 REPS=${REPS:-2} VARIANTS="${VARIANTS:-5:morton:8:gang}"
        step widepmc5a 300 timeout -s KILL 240 rocprofv3 --kernel-trace --pmc GRBM_GUI_ACTIVE SQ_WAVE_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_INSTS_MFMA -d gpurun_out/widepmc5a -o run --output-format csv -- python scripts/wide_bench.py &&
        step widepmc5b 300 timeout -s KILL 240 rocprofv3 --kernel-trace --pmc GRBM_GUI_ACTIVE TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCP_TCC_READ_REQ_sum SQ_LDS_IDX_ACTIVE SQ_INSTS_VMEM -d gpurun_out/widepmc5b -o run --output-format csv -- python scripts/wide_bench.py) || exit $? ;;
+    wideshard) step wideshard 600 env DQ4ML_FORCE_COLLECTIVES=1 python benchmarks/bench_wide.py --rows 1.25e6 --steps 20 --warmup 3 --json-out gpurun_out/wideshard.json &&
+               step wideshard_local 600 python benchmarks/bench_wide.py --rows 1.25e6 --steps 20 --warmup 3 --json-out gpurun_out/wideshard_local.json &&
+               (export TMPDIR=/tmp DQ4ML_FORCE_COLLECTIVES=1; step wideshardprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/wideshardprof -o run --output-format csv -- python benchmarks/bench_wide.py --rows 1.25e6 --steps 10 --warmup 2) || exit $? ;;
     tailres) step tailres 600 env ROWS=${ROWS:-1.25e7} FITS=${FITS:-200} python scripts/tail_reserve_probe.py ;;
     tailresprof) (export TMPDIR=/tmp; step tailresprof 300 timeout -s KILL 240 rocprofv3 --kernel-trace -d gpurun_out/tailresprof -o run --output-format csv -- python scripts/tail_reserve_probe.py) || exit $? ;;
     cfg4) step cfg4 900 python benchmarks/bench_dq_pipeline.py --steps ${CFG4_STEPS:-5} --warmup 2 --json-out gpurun_out/cfg4.json ;;
@@ -158,8 +161,8 @@ for s in $STEPS; do
        step syrkpmc1 300 timeout -s KILL 240 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE -d gpurun_out/syrkpmc1 -o run --output-format csv -- python scripts/syrk_bench.py &&
        step syrkpmc2 300 timeout -s KILL 240 rocprofv3 --kernel-trace --pmc SQ_WAIT_ANY SQ_INSTS_VMEM SQ_INSTS_MFMA SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE -d gpurun_out/syrkpmc2 -o run --output-format csv -- python scripts/syrk_bench.py) || exit $? ;;
     cpubase) step cpubase 600 python scripts/cpu_baseline.py --rows 2e7 --threads 16 ;;
-    scangram) for v in ${SCANABL:-0}; do step scangram$v 300 env DQ4ML_SCAN_ABL=$v python scripts/scan_ablation.py --gram; done && step scantable 300 python scripts/scan_ablation.py ;;
-    scanabl) for v in ${SCANABL:-0 1 5 9 13 0}; do step scanabl${DQ4ML_SCAN_TICKET:-xcd}$v 300 env DQ4ML_SCAN_ABL=$v python scripts/scan_ablation.py; done ;;
+    scangram) for v in ${SCANABL:-0}; do step scangram$v 300 env DQ4ML_DIAG=1 DQ4ML_SCAN_ABL=$v python scripts/scan_ablation.py --gram; done && step scantable 300 python scripts/scan_ablation.py ;;
+    scanabl) for v in ${SCANABL:-0 1 5 9 13 0}; do step scanabl${DQ4ML_SCAN_TICKET:-xcd}$v 300 env DQ4ML_DIAG=1 DQ4ML_SCAN_ABL=$v python scripts/scan_ablation.py; done ;;
     asynctests) step asynctests 600 python -m pytest tests/test_gpu_async_fit.py -q -m gpu ;;
     fitprof) step fitprof 300 env N=1.25e7 python scripts/fit_profile.py ;;
     dist2) step dist2 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 scripts/dist_rehearsal.py ;;
@@ -224,12 +227,12 @@ for s in $STEPS; do
        step cutpmclab1 300 timeout -s KILL 240 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS GRBM_GUI_ACTIVE -d gpurun_out/cutpmclab1 -o run --output-format csv -- python benchmarks/bench_csv_pipeline.py --steps 2 --warmup 1 &&
        step cutpmclab2 300 timeout -s KILL 240 rocprofv3 --kernel-trace --pmc SQ_INSTS_SALU SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_VMEM SQ_ACTIVE_INST_MISC GRBM_GUI_ACTIVE -d gpurun_out/cutpmclab2 -o run --output-format csv -- python benchmarks/bench_csv_pipeline.py --steps 2 --warmup 1) || exit $? ;;
     cutabl) for ab in 0 1 2 4 7; do
-         step cutabl_lab_$ab 300 env DQ4ML_CUT_ABLATE=$ab python benchmarks/bench_csv_pipeline.py --steps 10 --warmup 2 &&
-         step cutabl_w32_$ab 300 env DQ4ML_CUT_ABLATE=$ab python benchmarks/bench_csv_pipeline.py --features 32 --rows 2e7 --steps 10 --warmup 2 || exit $?
+         step cutabl_lab_$ab 300 env DQ4ML_DIAG=1 DQ4ML_CUT_ABLATE=$ab python benchmarks/bench_csv_pipeline.py --steps 10 --warmup 2 &&
+         step cutabl_w32_$ab 300 env DQ4ML_DIAG=1 DQ4ML_CUT_ABLATE=$ab python benchmarks/bench_csv_pipeline.py --features 32 --rows 2e7 --steps 10 --warmup 2 || exit $?
        done ;;
     cutb) (export TMPDIR=/tmp
-       step cutb_lab 300 env VARIANTS="${LABV:-base;DQ4ML_SCAN_CUT=0;DQ4ML_CUT_ABLATE=1;DQ4ML_CUT_ABLATE=4;DQ4ML_CUT_ABLATE=5}" python scripts/cut_bench.py --rows 1e8 &&
-       step cutb_w32 300 env VARIANTS="${W32V:-base;DQ4ML_CUT_ABLATE=1;DQ4ML_CUT_ABLATE=2;DQ4ML_CUT_ABLATE=4;DQ4ML_CUT_ABLATE=7}" python scripts/cut_bench.py --features 32 --rows 2e7) || exit $? ;;
+       step cutb_lab 300 env DQ4ML_DIAG=1 VARIANTS="${LABV:-base;DQ4ML_SCAN_CUT=0;DQ4ML_CUT_ABLATE=1;DQ4ML_CUT_ABLATE=4;DQ4ML_CUT_ABLATE=5}" python scripts/cut_bench.py --rows 1e8 &&
+       step cutb_w32 300 env DQ4ML_DIAG=1 VARIANTS="${W32V:-base;DQ4ML_CUT_ABLATE=1;DQ4ML_CUT_ABLATE=2;DQ4ML_CUT_ABLATE=4;DQ4ML_CUT_ABLATE=7}" python scripts/cut_bench.py --features 32 --rows 2e7) || exit $? ;;
     cutpmcb) (export TMPDIR=/tmp VARIANTS=base
        step cutpmcb1 300 timeout -s KILL 240 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS GRBM_GUI_ACTIVE -d gpurun_out/cutpmcb1 -o run --output-format csv -- python scripts/cut_bench.py --features 32 --rows 2e7 --reps 3 &&
        step cutpmcb2 300 timeout -s KILL 240 rocprofv3 --kernel-trace --pmc SQ_INSTS_SALU SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_VMEM SQ_ACTIVE_INST_MISC GRBM_GUI_ACTIVE -d gpurun_out/cutpmcb2 -o run --output-format csv -- python scripts/cut_bench.py --features 32 --rows 2e7 --reps 3 &&

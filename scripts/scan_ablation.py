@@ -3,7 +3,7 @@
 optionally as a diagnostic ablation build (``DQ4ML_SCAN_ABL=1``: line finding only, no per-line
 work; ``=2``: parse + rules without the stores) — to see where the kernel's time goes.
 
-    DQ4ML_SCAN_ABL=0|1|2 python scripts/scan_ablation.py [--rows 1e8] [--reps 20]
+    DQ4ML_DIAG=1 DQ4ML_SCAN_ABL=0|1|2 python scripts/scan_ablation.py [--rows 1e8] [--reps 20]
 """
 from __future__ import annotations
 

@@ -1,8 +1,10 @@
 """One rank of the data-parallel device l-bfgs / OWLQN fit (``lsq_qn.hip`` ``lsq_qn_dp_*``, X4) in
 ``test_gpu_lsq_qn.py``, started with ``subprocess`` (the parent has already initialised the GPU).
 
-    _gpu_qn_dp_worker.py gloo <solver-case>   rank of a 2-process gloo world (RANK/WORLD_SIZE env): this
-                                              rank's row shard of the wide tiles on cuda:0
+    _gpu_qn_dp_worker.py gloo <solver-case> [empty]
+                                              rank of a 2-process gloo world (RANK/WORLD_SIZE env): this
+                                              rank's row shard of the wide tiles on cuda:0 (empty: rank 0
+                                              holds every row, rank 1 none)
     _gpu_qn_dp_worker.py rccl <solver-case>   one process, every collective forced through a one-rank
                                               RCCL communicator, the fit under sync_debug_mode("error")
 
@@ -54,6 +56,8 @@ def main():
     X, y = data(case, "cuda")
     n = c["n"]
     lo, hi = (n * r // w, n * (r + 1) // w) if mode == "gloo" else (0, n)
+    if mode == "gloo" and len(sys.argv) > 3 and sys.argv[3] == "empty":
+        lo, hi = (0, n) if r == 0 else (n, n)  # the last rank's shard is empty: same branch, zero partials
     # gloo: unshifted bf16 storage, element for element what the parent's single-process reference
     # stores; rccl: the default shift, agreed over the (forced) communicator
     T = device.pack_wide([X[:, lo:hi].contiguous()], c["eb"], None, shift=None if mode == "gloo" else "auto")

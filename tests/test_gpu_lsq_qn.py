@@ -203,10 +203,12 @@ def _run_workers(args, world, timeout=150):
     return outs
 
 
-@pytest.mark.parametrize("case", ["lbfgs", "owlqn"])
-def test_device_qn_two_rank_gloo_matches_single_process(gpu_session, monkeypatch, case):
+@pytest.mark.parametrize("case,shards", [("lbfgs", "split"), ("owlqn", "split"), ("lbfgs", "empty")])
+def test_device_qn_two_rank_gloo_matches_single_process(gpu_session, monkeypatch, case, shards):
     """Two processes on the one GPU, each fitting its row shard (gloo: RCCL refuses two ranks on
-    one device): every rank ends with the single-process device fit of all rows."""
+    one device): every rank ends with the single-process device fit of all rows.  ``empty``: rank 1
+    holds no row -- the ranks still agree on the device branch (an empty shard used to
+    drop to the host path alone and deadlock its peer)."""
     import sys
 
     sys.path.insert(0, __import__("os").path.dirname(__import__("os").path.abspath(__file__)))
@@ -221,7 +223,7 @@ def test_device_qn_two_rank_gloo_matches_single_process(gpu_session, monkeypatch
     df = gpu_session.createDataFrame({"features": T, "label": y})
     ref = _fit(LinearRegression(solver="l-bfgs", maxIter=60, tol=1e-9, **c["kw"]), df, monkeypatch, True)
     assert ref._qn_evaluations is not None
-    outs = _run_workers(["gloo", case], 2)
+    outs = _run_workers(["gloo", case] + (["empty"] if shards == "empty" else []), 2)
     b = ref.coefficients.toArray()
     for o in outs:
         assert o["evaluations"] is not None and o["evaluations"] > 0  # the device DP form ran

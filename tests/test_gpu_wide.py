@@ -183,16 +183,18 @@ def test_pack_mixed_dtypes_and_misaligned_columns(wide):
 
 @gpu
 @pytest.mark.parametrize("eb", [16, 8])
-@pytest.mark.parametrize("sched", ["gang", "gangx", "queue", "grid"])
+@pytest.mark.parametrize("sched", ["gang", "gang3", "queue", "grid"])
 @pytest.mark.parametrize("d", [300, 1100])
 def test_wide_schedules_match_oracle(eb, sched, d, monkeypatch):
     # every SYRK schedule (the gang's merged diagonal + augmentation units included) gives the
-    # same statistics as the fp64 oracle of the stored (quantized) values
+    # same statistics as the fp64 oracle of the stored (quantized) values.  gang3 at d = 1100: 15
+    # units x 3 row ranges = 45 units over 32 blocks per group -- a partial last round, which the
+    # round barrier must skip (its blocks would wait for arrivals that never come)
     _hip()
     from net.jgp.labs.sparkdq4ml_amd.ops import device
 
-    monkeypatch.setenv("DQ4ML_WIDE_SCHED", sched)
-    monkeypatch.setenv("DQ4ML_WIDE_GANG_S", "2")
+    monkeypatch.setenv("DQ4ML_WIDE_SCHED", sched[:4] if sched.startswith("gang") else sched)
+    monkeypatch.setenv("DQ4ML_WIDE_GANG_S", "3" if sched == "gang3" else "2")
     monkeypatch.setenv("DQ4ML_WIDE_H", "1")
     n = 70_001
     g = torch.Generator(device="cuda").manual_seed(d + eb)
@@ -229,15 +231,13 @@ def test_wide_gang_full_width_matches_queue():
     y = torch.randn(n, generator=g, device="cuda", dtype=torch.float64)
     T = device.pack_wide([X], 8, None)
     outs = {}
-    for sched in ("gang", "gangx", "queue"):
+    for sched in ("gang", "queue"):
         os.environ["DQ4ML_WIDE_SCHED"] = sched
         try:
             outs[sched] = device.gram_stats(T, y, None, None, "fp8", x_zero_dead=True)
         finally:
             os.environ.pop("DQ4ML_WIDE_SCHED", None)
     assert _rel(outs["gang"], outs["queue"]) < 1e-6
-    # the XCD-keyed gang runs the same units (any block, any XCD): the same per-split sums, bit for bit
-    assert torch.equal(outs["gangx"], outs["gang"])
     Xq = T.to_dense().double()
     G = Xq @ Xq.T
     dg = outs["gang"][5 + 2 * d:]

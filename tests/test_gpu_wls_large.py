@@ -65,8 +65,12 @@ def test_assemble_matches_numpy(nf, fit_intercept, std_f, std_l, zero_col):
     flat = _stats(nf, 4000, seed=nf, zero_col=zero_col)
     host = flat.cpu().numpy()
     eff_l2 = 0.05
-    A_ref, b_ref, aStd_ref, bStd, rawBBar = _ref_system(host, nf, fit_intercept, eff_l2, std_f, std_l)
-    s = device.wls_assemble(flat, nf, fit_intercept, float(host[1]), float(bStd), float(rawBBar), eff_l2, std_f, std_l)
+    A_ref, b_ref, aStd_ref, bStd, _ = _ref_system(host, nf, fit_intercept, eff_l2, std_f, std_l)
+    # (reg, enet) with (1 - enet) reg / bStd = eff_l2: the head scalars are the device's own
+    s = device.wls_assemble(flat, nf, fit_intercept, eff_l2 * float(bStd), 0.0, std_f, std_l)
+    o = s.o[:device.PCG_STATE_WORDS].cpu().numpy()
+    assert o[device.PCG_STATUS] == 0.0 and o[device.PCG_BSTD] == pytest.approx(bStd, rel=1e-14)
+    np.testing.assert_array_equal(o[device.PCG_HEAD:device.PCG_HEAD + 5], host[:5])
     A = s.A.cpu().numpy()
     np.testing.assert_allclose(A, A_ref, rtol=1e-13, atol=1e-15)
     assert np.array_equal(A, A.T)
@@ -84,10 +88,10 @@ def test_pcg_matches_direct_solve(nf, fit_intercept):
 
     flat = _stats(nf, 3 * nf, seed=7)
     host = flat.cpu().numpy()
-    A_ref, b_ref, aStd, bStd, rawBBar = _ref_system(host, nf, fit_intercept, 0.02, True, True)
-    s = device.wls_assemble(flat, nf, fit_intercept, float(host[1]), float(bStd), float(rawBBar), 0.02, True, True)
-    o = device.wls_pcg(s, nf, float(bStd), optim.PCG_RTOL)
-    assert o is not None
+    A_ref, b_ref, aStd, bStd, _ = _ref_system(host, nf, fit_intercept, 0.02, True, True)
+    s = device.wls_assemble(flat, nf, fit_intercept, 0.02 * float(bStd), 0.0, True, True)
+    o = device.wls_pcg(s, nf, optim.PCG_RTOL)
+    assert device.pcg_ok(o)
     k = s.k
     x = o[device.PCG_STATE_WORDS:device.PCG_STATE_WORDS + k]
     ref = torch.linalg.solve(torch.as_tensor(A_ref), torch.as_tensor(b_ref)).numpy()
@@ -95,8 +99,15 @@ def test_pcg_matches_direct_solve(nf, fit_intercept):
     coef = o[device.PCG_STATE_WORDS + k:]
     np.testing.assert_allclose(coef, x[:nf] * bStd / aStd, rtol=1e-12, atol=1e-14)
     # deterministic: the same control block bit for bit on a second solve
-    s2 = device.wls_assemble(flat, nf, fit_intercept, float(host[1]), float(bStd), float(rawBBar), 0.02, True, True)
-    assert np.array_equal(device.wls_pcg(s2, nf, float(bStd), optim.PCG_RTOL), o)
+    s2 = device.wls_assemble(flat, nf, fit_intercept, 0.02 * float(bStd), 0.0, True, True)
+    assert np.array_equal(device.wls_pcg(s2, nf, optim.PCG_RTOL), o)
+    # enqueued whole (the asynchronous fit's form): the same iterates, converged ones are no-ops
+    s3 = device.wls_assemble(flat, nf, fit_intercept, 0.02 * float(bStd), 0.0, True, True)
+    device.wls_pcg_enqueue(s3, nf, optim.PCG_RTOL, 64)
+    o3 = s3.o.cpu().numpy()
+    w = device.PCG_STATE_WORDS
+    assert device.pcg_ok(o3) and 0 < o3[device.PCG_ITERS] < 64
+    assert np.array_equal(o3[w:], o[w:])
 
 
 def test_pcg_declines_non_positive_diagonal_and_fit_falls_back():
@@ -105,10 +116,10 @@ def test_pcg_declines_non_positive_diagonal_and_fit_falls_back():
     nf = 1040
     flat = _stats(nf, 3000, seed=11, zero_col=5)
     host = flat.cpu().numpy()
-    _, _, _, bStd, rawBBar = _ref_system(host, nf, False, 0.0, False, True)
     # no intercept, no L2, unstandardized: the constant feature's diagonal is exactly 0
-    s = device.wls_assemble(flat, nf, False, float(host[1]), float(bStd), float(rawBBar), 0.0, False, True)
-    assert device.wls_pcg(s, nf, float(bStd), optim.PCG_RTOL) is None
+    s = device.wls_assemble(flat, nf, False, 0.0, 0.0, False, True)
+    o = device.wls_pcg(s, nf, optim.PCG_RTOL)
+    assert o[device.PCG_BAD] != 0.0 and not device.pcg_ok(o)
     # the fit itself still returns Spark's answer (Cholesky fails -> quasi-newton on the host)
     got, _ = optim.fit_wls_flat(flat, nf, False, 0.0, 0.0, False, True, "auto", 200, 1e-10)
     assert got.solver in ("l-bfgs", "quasi-newton") and np.isfinite(got.coefficients).all()
@@ -124,3 +135,22 @@ def test_device_fit_l2_matches_reference_no_intercept():
                                            True, "auto", 100, 1e-6)
         np.testing.assert_allclose(got.coefficients, ref.coefficients, rtol=1e-8, atol=1e-10)
         assert got.intercept == 0.0
+
+
+def test_constant_label_short_circuits_to_host_driver():
+    """A constant label: the device head sets STATUS, every solve kernel exits, and the fit takes the
+    native driver's semantics (coefficients 0, intercept = the label)."""
+    import torch
+
+    from net.jgp.labs.sparkdq4ml_amd.ops import device
+
+    nf = 1030
+    g = torch.Generator(device="cuda").manual_seed(3)
+    X = torch.randn(nf, 3000, generator=g, device="cuda", dtype=torch.float64)
+    y = torch.full((3000,), 4.25, device="cuda", dtype=torch.float64)
+    flat = device.gram_stats(X, y, None, None, "fp64")
+    s = device.wls_assemble(flat, nf, True, 0.1, 0.0, True, False)
+    o = device.wls_pcg(s, nf, optim.PCG_RTOL)
+    assert o[device.PCG_STATUS] == 1.0
+    got, _ = optim.fit_wls_flat(flat, nf, True, 0.1, 0.0, True, False, "auto", 100, 1e-6)
+    assert np.all(got.coefficients == 0.0) and got.intercept == pytest.approx(4.25, rel=1e-12)
