@@ -631,14 +631,31 @@ def _tail_masks(dev):
     return keep, tail, cus
 
 
-def _tail_stream(dev) -> "torch.cuda.Stream":
+def _tail_stream(dev, wide: bool = False) -> "torch.cuda.Stream":
+    """The fit tail's side stream.  ``wide``: the large-k tail (fold, all-reduce, assembly, PCG) of
+    the MFMA-bound wide SYRK gets a HIGH-priority stream of its own.  HIP deals the streams of a
+    process round-robin over its few hardware queues, and a plain side stream landed on the
+    compute stream's queue, where the tail serialized behind the next fit's prologue (10.5 ->
+    9.5 ms per 1.25e6 x 4096 fit once the host reads were gone).  A separate queue at normal
+    priority (a CU-masked stream over every CU) measured 9.74 ms: the tail's LDS-using kernels
+    then interleave with the next fit's SYRK and stall its gang rounds; at high priority the
+    tail drains first and the next SYRK runs undisturbed (9.07 ms; profiles/r6_wide_async.md)."""
     masks = _tail_masks(dev)
-    key = (dev, masks is not None)
+    key = (dev, masks is not None, wide, _WIDE_TAIL if wide else None)
     st = _tail_streams.get(key)
     if st is None:
-        st = _tail_streams[key] = (streams.cu_masked_stream(masks[1], masks[2], dev, tag=99) if masks is not None
-                                   else torch.cuda.Stream(device=dev))
+        if masks is not None:
+            st = streams.cu_masked_stream(masks[1], masks[2], dev, tag=98 if wide else 99)
+        elif wide and _WIDE_TAIL == "queue" and dev.type == "cuda":  # (A/B: scripts/wide_tail_ab.py)
+            cus = device._cus(native.hip())
+            st = streams.cu_masked_stream(list(range(cus)), cus, dev, tag=97)
+        else:
+            st = torch.cuda.Stream(device=dev, priority=-1) if wide else torch.cuda.Stream(device=dev)
+        _tail_streams[key] = st
     return st
+
+
+_WIDE_TAIL = "high"  # the wide tail's stream: "high" priority, or its own normal-priority "queue"
 
 
 class _PendingWLS:
@@ -673,7 +690,7 @@ class _PendingWLS:
         if overlap:
             h = native.hip()
             self._dev = faststream.dev_index(flat.device)
-            side = _tail_stream(flat.device)
+            side = _tail_stream(flat.device, wide=d > 64)
             h.stream_wait(side.cuda_stream, faststream.raw(self._dev))
             with faststream.use(side):
                 if hasattr(flat, "finish"):

@@ -37,8 +37,7 @@ constexpr int kBlock = 256;  // f64 kernel: 4 waves
 constexpr int kWavesPerBlock = kBlock / kWave;
 // bf16 kernel: 8 waves per block -- two co-resident per CU at <= 128 VGPRs for d <= 32 (HALF
 // below), one per CU at <= 256 VGPRs for d <= 64; the round-4 16-wave block filled a CU alone
-// HALF (d <= 32 unmasked; the default since round 5, DQ4ML_GRAM_BF16_HALF=0 restores the 16-wave
-// block): 8-wave blocks, two resident per CU, so one block's ramp and reduction overlap the other's
+// HALF (d <= 32 unmasked; since round 5 -- the 16-wave block lost): 8-wave blocks, two resident per CU, so one block's ramp and reduction overlap the other's
 // stream and the next pass's blocks start beside this pass's last ones.  Same box, two reps
 // (profiles/r5_shard_drain.md): 1.25e7-row shard 0.1297 / 0.1292 vs 0.1347 / 0.1365 ms per fit,
 // 1e8 headline 0.987 / 0.989 vs 0.994 / 0.992 ms.
@@ -48,14 +47,7 @@ struct BF16Geom {
   static constexpr int kWaves = kBlock / kWave;
   static constexpr int kMinBlocks = HALF ? 2 : 1;
 };
-static bool bf16_half() {
-  static const bool on = [] {
-    const char* e = getenv("DQ4ML_GRAM_BF16_HALF");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
-static int bf16_block(int d, int xmode) { return (d <= 32 && xmode == 0 && !bf16_half()) ? 1024 : 512; }
+static int bf16_block(int, int) { return 512; }  // (HALF at d <= 32, the 8-wave block elsewhere)
 
 __device__ __forceinline__ double load_as_f64(const void* p, int dt, int64_t i) {
   switch (dt) {
@@ -1267,7 +1259,7 @@ static void with_kernel(int mode, int xdt, int d, int xmode, bool tiled, F&& f) 
   if (mode == GRAM_BF16) {
     const int NT = (d + 31) / 32;
 #define DQ_BF16_CASE(TX, NTV, TL)                                                 \
-    if (xmode == 0 && NTV == 1 && bf16_half()) return f(gram_tall_bf16_kernel<TX, 1, 0, TL, true>); \
+    if (xmode == 0 && NTV == 1) return f(gram_tall_bf16_kernel<TX, 1, 0, TL, true>); \
     if (xmode == 0) return f(gram_tall_bf16_kernel<TX, NTV, 0, TL>);              \
     if (xmode == 1) return f(gram_tall_bf16_kernel<TX, NTV, 1, TL>);              \
     return f(gram_tall_bf16_kernel<TX, NTV, 2, TL>);
@@ -1397,13 +1389,9 @@ void gram_reduce(int mode, const double* partials, int blocks, int d, double* ou
 }
 
 int gram_interleave() {
-  // default on: same-box A/B (scripts/interleave_ab.sh, 5 alternations) 1e8 rows 1.011-1.015 vs
+  // always on: same-box A/B against contiguous ranges (5 alternations) 1e8 rows 1.011-1.015 vs
   // 1.020-1.026 ms, 1.25e7 rows 0.1426-0.1441 vs 0.1471-0.1476 ms per fit (tall bf16 kernel)
-  static const int interleave = [] {
-    const char* e = getenv("DQ4ML_GRAM_INTERLEAVE");
-    return e && e[0] == '0' ? 0 : 1;
-  }();
-  return interleave;
+  return 1;
 }
 
 void gram_tall(int mode, GramArgs a, int xmode, int blocks, double* out, hipStream_t st, bool reduce) {

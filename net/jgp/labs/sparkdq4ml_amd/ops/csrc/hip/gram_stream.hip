@@ -702,19 +702,11 @@ static void pick_ring(F&& f, K2 k2, int wb2, K3 k3, bool mfma_heavy = false) {
   return f(k2, wb2);
 }
 
-// f32 storage, 64 features (NT = 2): DQ4ML_GRAM_STREAM_F32RS=32 takes 32-row stages, so a deeper
-// DMA ring fits four waves per CU (ring 4: 3 stages, 28 KiB, in flight per wave instead of one
-// 17 KiB stage at ring 2).  Measured and kept off: config 4 (1.25e8 x 64, one box, one run)
-// 6.18 ms at 64 rows / ring 2, 6.45 at 32 / ring 3, 6.53 at 32 / ring 4 — the per-stage fixed
-// work (row scalars, waits) doubles and the extra bytes in flight buy nothing.
-static int f32_rs(int d) {
-  static const int rs = [] {
-    const char* e = getenv("DQ4ML_GRAM_STREAM_F32RS");
-    return e ? atoi(e) : 64;
-  }();
-  (void)d;
-  return rs == 32 ? 32 : 64;
-}
+// f32 storage, 64 features (NT = 2): 64-row stages.  32-row stages (a deeper DMA ring, four waves
+// per CU) were measured and lost: config 4 (1.25e8 x 64, one box, one run) 6.18 ms at 64 rows /
+// ring 2, 6.45 at 32 / ring 3, 6.53 at 32 / ring 4 -- the per-stage fixed work (row scalars,
+// waits) doubles and the extra bytes in flight buy nothing.
+static int f32_rs(int) { return 64; }
 
 template <int NT, int CMP, int XM, typename F>
 static void f32_rs32(F&& f) {

@@ -35,6 +35,15 @@ int64_t gram_wide_partials(int d, int splitk);
 // (x - s) [* inv_scale] (the Gram statistics are un-shifted in f64 afterwards: gram.h stats_unshift)
 void feature_amax(const PackSrcW* srcs_dev, int d, int64_t n, const uint8_t* sel, float* amax, hipStream_t st,
                   const float* shift = nullptr);
+// the label's augmentation panel [1, y_hi, y_lo] (1 tile, eb's layout) of rows with sel != 0
+// (null: all), split on the device: aux (f64[6]) = [1, s_h, s_l | t, 1/s_h, 1/s_l] -- aux[0:3] is
+// the fold's aug_scale, aux[3] the label shift t (fp8: the live mean; bf16: 0); part:
+// wide_label_part_doubles() f64 of scratch.  y: f64 (ydt 0) or f32 (ydt 1).
+// head statistics of the label shifted by aux[3] -> those of the label, in place (after the head fold)
+void wide_unshift_label(double* out, int d, const double* aux, hipStream_t st);
+int wide_label_part_doubles();
+void wide_label_aug(int eb, const void* y, int ydt, int64_t n, const uint8_t* sel, double* part, double* aux,
+                    void* out, hipStream_t st);
 // eb = 16 (bf16) or 8 (fp8 e4m3, values multiplied by inv_scale[f] before conversion)
 void pack_wide(int eb, const PackSrcW* srcs_dev, int d, int64_t n, int nt, const uint8_t* sel, const float* inv_scale,
                void* out, hipStream_t st, const float* shift = nullptr);

@@ -460,38 +460,60 @@ __device__ __forceinline__ void wide_store(double* __restrict__ out, float* __re
 __global__ __launch_bounds__(256) void gram_wide_reduce_kernel(WideArgs a, const float* __restrict__ scales,
                                                               double* __restrict__ out, float* __restrict__ out32,
                                                               int J0, int J1) {
+  // one thread = 4 consecutive columns of one partial-tile row: float4 loads, 4 independent f64
+  // chains per slab walk (the same k order per element as a scalar fold: bitwise the same sums).
+  // Quads with nothing to fold skip their loads: the strictly-lower quads of a diagonal tile
+  // (only i <= j is stored), and every augmentation quad but the first (columns 0-2 carry
+  // [1, y_hi, y_lo]).
   const int d = a.d, P = a.npanels;
   int64_t npb = 0;  // pairs of the band's panel columns: column J holds pairs I = 0..J
   for (int J = J0; J < J1; ++J) npb += J + 1;
-  const int64_t tot = npb * kPanel * kPanel;
-  const double s1 = a.aug_scale[0], syh = a.aug_scale[1], syl = a.aug_scale[2];  // device f64[3]
   const int64_t slab = (int64_t)kPanel * kPanel;
+  const int64_t tot = npb * (slab / 4);
+  const double s1 = a.aug_scale[0], syh = a.aug_scale[1], syl = a.aug_scale[2];  // device f64[3]
   for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < tot; g += (int64_t)gridDim.x * blockDim.x) {
-    const int q = (int)(g / slab);
-    const int e = (int)(g - (int64_t)q * slab), r = e >> 8, c = e & (kPanel - 1);
+    const int q = (int)(g / (slab / 4));
+    const int e = (int)(g - (int64_t)q * (slab / 4)) * 4, r = e >> 8, c0 = e & (kPanel - 1);
     int J = J0, I = q;  // band-local pair index (column-major) -> (I, J)
     while (I >= J + 1) { I -= J + 1; ++J; }
     const int pr = I * (P + 1) - I * (I - 1) / 2 + (J - I);  // row-major storage index of (I, J)
     const float* base = a.part + (int64_t)pr * a.splitk * slab + e;
+    const int i = I * kPanel + r;
+    if (J < P) {  // Gram block
+      if (i >= d || (I == J && r > c0 + 3)) continue;
+      double v0 = 0.0, v1 = 0.0, v2 = 0.0, v3 = 0.0;
+      for (int k = 0; k < a.splitk; ++k) {
+        const float4 x = *reinterpret_cast<const float4*>(base + (int64_t)k * slab);
+        v0 += (double)x.x;
+        v1 += (double)x.y;
+        v2 += (double)x.z;
+        v3 += (double)x.w;
+      }
+      const double v[4] = {v0, v1, v2, v3};
+      const double si = scales ? (double)scales[i] : 1.0;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int j = J * kPanel + c0 + t;
+        if (j < d && i <= j) {
+          const double sc = scales ? si * (double)scales[j] : 1.0;
+          wide_store(out, out32, 5 + 2 * (int64_t)d + i + (int64_t)j * (j + 1) / 2, v[t] * sc);
+        }
+      }
+      continue;
+    }
+    if (c0 != 0) continue;  // augmentation column: only columns 0-2 hold data
     auto sum = [&](int off) {
       double v = 0.0;
       for (int k = 0; k < a.splitk; ++k) v += (double)base[(int64_t)k * slab + off];
       return v;
     };
-    const int i = I * kPanel + r;
-    if (J < P) {  // Gram block
-      const int j = J * kPanel + c;
-      if (i < d && j < d && i <= j) {
-        const double sc = scales ? (double)scales[i] * (double)scales[j] : 1.0;
-        wide_store(out, out32, 5 + 2 * (int64_t)d + i + (int64_t)j * (j + 1) / 2, sum(0) * sc);
-      }
-    } else if (I < P) {  // (X panel, augmentation): column 0 -> aSum, columns 1 + 2 -> abSum
-      if (i < d && c < 2) {
+    if (I < P) {  // (X panel, augmentation): column 0 -> aSum, columns 1 + 2 -> abSum
+      if (i < d) {
         const double si = scales ? (double)scales[i] : 1.0;
-        if (c == 0) wide_store(out, out32, 5 + i, sum(0) * si * s1);
-        else wide_store(out, out32, 5 + d + i, (sum(0) * syh + sum(1) * syl) * si);
+        wide_store(out, out32, 5 + i, sum(0) * si * s1);
+        wide_store(out, out32, 5 + d + i, (sum(1) * syh + sum(2) * syl) * si);
       }
-    } else if (r == 0 && c == 0) {  // (augmentation, augmentation): the five scalars
+    } else if (r == 0) {  // (augmentation, augmentation): the five scalars
       const double g11 = sum(0) * s1 * s1;
       const double g1h = sum(1) * s1 * syh, g1l = sum(2) * s1 * syl;
       const double ghh = sum(kPanel + 1) * syh * syh, ghl = sum(kPanel + 2) * syh * syl;
@@ -582,6 +604,140 @@ __global__ __launch_bounds__(256) void pack_wide_kernel(const PackSrcW* __restri
   }
 }
 
+// ---- the label's augmentation panel [1, y_hi, y_lo] of the wide SYRK, on the device --------
+// (the label split of models/regression -> ops/device.py _label_split, fused: three launches and
+// no host read instead of ~40 elementwise / reduction ops between the fit's SYRKs)
+//  1. wide_label_stats_kernel: per-block f64 partials [Σ live y, Σ live, max live y, min live y]
+//     over a fixed grid (fixed summation order: deterministic);
+//  2. wide_label_scales_kernel (one thread): fp8 -- the live mean t (the label is centred before
+//     its split: two e4m3 digits of y - t carry ~8 bits relative to the label's spread), s_h =
+//     max|y - t| / 448, s_l = s_h / 28 (the e4m3 rounding error of a value in [-448, 448] is at
+//     most half an ulp of the top binade, 16, so (y - t) - y_hi stays within 16 s_h = 448 s_l);
+//     bf16 -- t = 0 and unit scales.  aux = [1, s_h, s_l | t, 1/s_h, 1/s_l];
+//  3. wide_label_pack_kernel: the 1-tile fragment panel (columns 0-2 live, y_hi, y_lo; 3-31 zero).
+constexpr int kLabelBlocks = 256;
+
+__global__ __launch_bounds__(256) void wide_label_stats_kernel(const void* __restrict__ y, int ydt, int64_t n,
+                                                               const uint8_t* __restrict__ sel,
+                                                               double* __restrict__ part) {
+  __shared__ double red[4][4];
+  double sy = 0.0, sw = 0.0, mx = -INFINITY, mn = INFINITY;
+  for (int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x; r < n; r += (int64_t)gridDim.x * 256) {
+    if (sel != nullptr && !sel[r]) continue;
+    const double v = ydt == 0 ? reinterpret_cast<const double*>(y)[r] : (double)reinterpret_cast<const float*>(y)[r];
+    sy += v;
+    sw += 1.0;
+    mx = fmax(mx, v);
+    mn = fmin(mn, v);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    sy += __shfl_xor(sy, o);
+    sw += __shfl_xor(sw, o);
+    mx = fmax(mx, __shfl_xor(mx, o));
+    mn = fmin(mn, __shfl_xor(mn, o));
+  }
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) red[w][0] = sy, red[w][1] = sw, red[w][2] = mx, red[w][3] = mn;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int i = 1; i < 4; ++i) {
+      red[0][0] += red[i][0];
+      red[0][1] += red[i][1];
+      red[0][2] = fmax(red[0][2], red[i][2]);
+      red[0][3] = fmin(red[0][3], red[i][3]);
+    }
+    for (int i = 0; i < 4; ++i) part[blockIdx.x * 4 + i] = red[0][i];
+  }
+}
+
+__global__ __launch_bounds__(64) void wide_label_scales_kernel(const double* __restrict__ part, int nb, int eb,
+                                                                double* __restrict__ aux) {
+  // one wave: lane l folds blocks l, l + 64, ... then a fixed butterfly (deterministic)
+  double sy = 0.0, sw = 0.0, mx = -INFINITY, mn = INFINITY;
+  for (int b = threadIdx.x; b < nb; b += 64) {
+    sy += part[4 * b];
+    sw += part[4 * b + 1];
+    mx = fmax(mx, part[4 * b + 2]);
+    mn = fmin(mn, part[4 * b + 3]);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    sy += __shfl_xor(sy, o);
+    sw += __shfl_xor(sw, o);
+    mx = fmax(mx, __shfl_xor(mx, o));
+    mn = fmin(mn, __shfl_xor(mn, o));
+  }
+  if (threadIdx.x != 0) return;
+  double t = 0.0, sh = 1.0, sl = 1.0;
+  if (eb == 8) {
+    t = sy / fmax(sw, 1.0);
+    const double amax = sw > 0.0 ? fmax(mx - t, t - mn) : 0.0;
+    sh = amax > 0.0 ? amax / 448.0 : 1.0;
+    sl = sh / 28.0;
+  }
+  aux[0] = 1.0;
+  aux[1] = sh;
+  aux[2] = sl;
+  aux[3] = t;
+  aux[4] = 1.0 / sh;
+  aux[5] = 1.0 / sl;
+}
+
+template <int EB>
+__global__ __launch_bounds__(256) void wide_label_pack_kernel(const void* __restrict__ y, int ydt, int64_t n,
+                                                              int64_t nsup, const uint8_t* __restrict__ sel,
+                                                              const double* __restrict__ aux,
+                                                              unsigned char* __restrict__ out) {
+  const int fl = threadIdx.x >> 3, q = threadIdx.x & 7;
+  const int ki = q >> 1, lane = 32 * (q & 1) + fl;
+  const double t = aux[3], sh = aux[1], ish = aux[4], isl = aux[5];
+  for (int64_t s = blockIdx.x; s < nsup; s += gridDim.x) {  // one 64-row superstep per iteration
+    const int64_t r0 = s * 64 + 8 * q;
+    float x[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int64_t r = r0 + j;
+      const bool live = r < n && (sel == nullptr || sel[r]);
+      float v = 0.0f;
+      if (live && fl < 3) {
+        if (fl == 0) {
+          v = 1.0f;
+        } else {
+          const double yv = (ydt == 0 ? reinterpret_cast<const double*>(y)[r]
+                                      : (double)reinterpret_cast<const float*>(y)[r]) - t;
+          if constexpr (EB == 16) {
+            const double hi = (double)(float)(__bf16)(float)yv;
+            v = fl == 1 ? (float)hi : (float)(yv - hi);
+          } else {
+            const float qh = fminf(fmaxf((float)(yv * ish), -448.0f), 448.0f);
+            if (fl == 1) {
+              v = qh;
+            } else {
+              const float dh = __builtin_amdgcn_cvt_f32_fp8(__builtin_amdgcn_cvt_pk_fp8_f32(qh, 0.0f, 0, false), 0);
+              v = fminf(fmaxf((float)((yv - (double)dh * sh) * isl), -448.0f), 448.0f);
+            }
+          }
+        }
+      }
+      x[j] = v;
+    }
+    if constexpr (EB == 16) {
+      bf16x8 v;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = (__bf16)x[j];
+      reinterpret_cast<u32x4*>(out)[s * 256 + ki * 64 + lane] = __builtin_bit_cast(u32x4, v);
+    } else {
+      int lo = __builtin_amdgcn_cvt_pk_fp8_f32(x[0], x[1], 0, false);
+      lo = __builtin_amdgcn_cvt_pk_fp8_f32(x[2], x[3], lo, true);
+      int hi = __builtin_amdgcn_cvt_pk_fp8_f32(x[4], x[5], 0, false);
+      hi = __builtin_amdgcn_cvt_pk_fp8_f32(x[6], x[7], hi, true);
+      const int64_t o = s * 2048 + (((ki >> 1) * 64 + lane) << 4) + ((ki & 1) << 3);
+      *reinterpret_cast<u32x2*>(out + o) = u32x2{(unsigned)lo, (unsigned)hi};
+    }
+  }
+}
+
 // Zero the dead rows of a wide fragment-ordered matrix (a DQ selection applied AFTER the pack):
 // one pass over the storage, 16 B per thread, no dequantize / re-pack.  In both layouts a 16-B
 // unit holds 8-row runs of ONE feature: bf16 = rows s*64 + 16ki + 8h + [0, 8) (unit = (s, t, ki,
@@ -665,6 +821,43 @@ void pack_wide(int eb, const PackSrcW* srcs_dev, int d, int64_t n, int nt, const
   DQ_HIP_CHECK(hipGetLastError());
 }
 
+// statistics of a label shifted by t = aux[3] (y' = y - t) -> those of y, in place (f64), after the
+// head fold: Σy² += 2tΣy' + t²W, Σy += tW, Σx·y += tΣx (one thread per feature; thread 0 the
+// scalars, reading Σy' before anyone writes it)
+__global__ __launch_bounds__(256) void wide_unshift_label_kernel(double* __restrict__ out, int d,
+                                                                 const double* __restrict__ aux) {
+  const double t = aux[3];
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j < d) out[5 + d + j] += t * out[5 + j];
+  if (j == 0) {
+    const double W = out[1], b = out[3];
+    out[4] += (2.0 * t) * b + (t * t) * W;
+    out[3] = b + t * W;
+  }
+}
+
+void wide_unshift_label(double* out, int d, const double* aux, hipStream_t st) {
+  hipLaunchKernelGGL(wide_unshift_label_kernel, dim3((d + 255) / 256 > 0 ? (d + 255) / 256 : 1), dim3(256), 0, st,
+                     out, d, aux);
+  DQ_HIP_CHECK(hipGetLastError());
+}
+
+int wide_label_part_doubles() { return 4 * kLabelBlocks; }
+
+void wide_label_aug(int eb, const void* y, int ydt, int64_t n, const uint8_t* sel, double* part, double* aux,
+                    void* out, hipStream_t st) {
+  if (eb != 8 && eb != 16) throw std::invalid_argument("wide_label_aug: eb must be 8 or 16");
+  if (ydt != 0 && ydt != 1) throw std::invalid_argument("wide_label_aug: label must be f64 or f32");
+  const int64_t nsup = (n + 63) / 64;
+  hipLaunchKernelGGL(wide_label_stats_kernel, dim3(kLabelBlocks), dim3(256), 0, st, y, ydt, n, sel, part);
+  hipLaunchKernelGGL(wide_label_scales_kernel, dim3(1), dim3(64), 0, st, part, kLabelBlocks, eb, aux);
+  int64_t g = nsup < 1 ? 1 : (nsup > 2048 ? 2048 : nsup);  // (grid-stride: ~10 supersteps per block)
+  unsigned char* o = reinterpret_cast<unsigned char*>(out);
+  if (eb == 16) hipLaunchKernelGGL(wide_label_pack_kernel<16>, dim3(g), dim3(256), 0, st, y, ydt, n, nsup, sel, aux, o);
+  else hipLaunchKernelGGL(wide_label_pack_kernel<8>, dim3(g), dim3(256), 0, st, y, ydt, n, nsup, sel, aux, o);
+  DQ_HIP_CHECK(hipGetLastError());
+}
+
 int64_t gram_wide_partials(int d, int splitk) {
   const int P = (d + kPanel - 1) / kPanel;
   const int npair = (P + 1) * (P + 2) / 2;
@@ -693,7 +886,7 @@ static void launch_fold(const WideArgs& a, const float* scales, double* out, flo
                         hipStream_t st) {
   int64_t npb = 0;
   for (int J = J0; J < J1; ++J) npb += J + 1;
-  int64_t g = (npb * kPanel * kPanel + 255) / 256;
+  int64_t g = (npb * kPanel * kPanel / 4 + 255) / 256;  // one thread per 4 columns
   if (g > 16384) g = 16384;
   hipLaunchKernelGGL(gram_wide_reduce_kernel, dim3(g), dim3(256), 0, st, a, scales, out, out32, J0, J1);
   DQ_HIP_CHECK(hipGetLastError());

@@ -79,6 +79,12 @@ PYBIND11_MODULE(_dq4ml_hip, m) {
     DQ_HIP_CHECK(hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data()));
     return reinterpret_cast<uintptr_t>(s);
   });
+  // drain and destroy a stream this module created (runtime/streams.py releases its CU-masked
+  // streams at interpreter exit, before the HIP runtime's own teardown)
+  m.def("stream_destroy", [](uintptr_t st) {
+    DQ_HIP_CHECK(hipStreamSynchronize(as_stream(st)));
+    DQ_HIP_CHECK(hipStreamDestroy(as_stream(st)));
+  });
   m.def("device_info", []() {
     int dev = 0;
     DQ_HIP_CHECK(hipGetDevice(&dev));
@@ -251,6 +257,15 @@ PYBIND11_MODULE(_dq4ml_hip, m) {
                         uintptr_t out, uintptr_t stream, uintptr_t shift) {
     pack_wide(eb, P<const PackSrcW>(srcs_dev), d, n, nt, P<const uint8_t>(sel), P<const float>(inv_scale), P<void>(out),
               as_stream(stream), P<const float>(shift));
+  });
+  m.def("wide_label_part_doubles", &wide_label_part_doubles);
+  m.def("wide_unshift_label", [](uintptr_t out, int d, uintptr_t aux, uintptr_t stream) {
+    wide_unshift_label(P<double>(out), d, P<const double>(aux), as_stream(stream));
+  });
+  m.def("wide_label_aug", [](int eb, uintptr_t y, int ydt, int64_t n, uintptr_t sel, uintptr_t part, uintptr_t aux,
+                             uintptr_t out, uintptr_t stream) {
+    wide_label_aug(eb, P<const void>(y), ydt, n, P<const uint8_t>(sel), P<double>(part), P<double>(aux), P<void>(out),
+                   as_stream(stream));
   });
   m.def("wide_mask_rows", [](int eb, uintptr_t in, uintptr_t out, int d, int64_t n, uintptr_t sel, uintptr_t stream) {
     wide_mask_rows(eb, P<const void>(in), P<void>(out), d, n, P<const uint8_t>(sel), as_stream(stream));

@@ -18,8 +18,8 @@
 //                         transpose — its mirror, both coalesced; the Jacobi preconditioner and
 //                         the "diagonal not > 0" flag fall out of the diagonal tiles;
 //  * PCG                  per iteration ONE memory-bound GEMV (one wave per row, 4 independent
-//                         accumulator chains) and ONE single-workgroup vector update (all dots
-//                         and axpys of the iteration, block reductions in LDS).  Converged
+//                         accumulator chains) and ONE one-wave vector update (all dots and axpys
+//                         of the iteration, shuffle reductions, no LDS).  Converged
 //                         iterations exit at their first instruction, so a fixed chunk of
 //                         iterations needs no host check; the host reads one control block per
 //                         chunk (state + x + coefficients) -- or, for an asynchronous fit, once,
@@ -34,25 +34,12 @@ namespace dq4ml {
 
 namespace {
 
-constexpr int kUpdThreads = 1024;
+constexpr int kUpdThreads = 64;  // the PCG vector kernels: one wave, no LDS
 
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
   for (int s = 32; s > 0; s >>= 1) v += __shfl_xor(v, s);
   return v;
-}
-
-// every thread gets the block-wide sum; `red` holds one double per wave
-__device__ __forceinline__ double block_sum(double v, double* red) {
-  v = wave_sum(v);
-  const int w = threadIdx.x >> 6;
-  __syncthreads();  // the previous call's readers are done with `red`
-  if ((threadIdx.x & 63) == 0) red[w] = v;
-  __syncthreads();
-  double t = 0.0;
-  const int nw = blockDim.x >> 6;
-  for (int i = 0; i < nw; ++i) t += red[i];
-  return t;
 }
 
 // same algebra as models/optim.py _wls_device / csrc/host/wls.cpp: population label std, the
@@ -150,11 +137,13 @@ __global__ __launch_bounds__(256) void wls_dense_kernel(const double* __restrict
   }
 }
 
+// The PCG vector kernels are ONE wave with no LDS (wave_sum over shuffles): in an asynchronous
+// wide fit they run beside the next fit's SYRK, whose one block per CU holds the whole LDS --
+// a kernel needing any LDS would wait for that SYRK to end (profiles/r6_wide_async.md).
 __global__ __launch_bounds__(kUpdThreads) void pcg_init_kernel(const double* __restrict__ b,
                                                                const double* __restrict__ minv, int k, double rtol,
                                                                double* __restrict__ o, double* __restrict__ r,
                                                                double* __restrict__ p) {
-  __shared__ double red[kUpdThreads / 64];
   double* x = o + PCG_STATE_WORDS;
   double rz = 0.0, bb = 0.0;
   for (int e = threadIdx.x; e < k; e += kUpdThreads) {
@@ -165,8 +154,8 @@ __global__ __launch_bounds__(kUpdThreads) void pcg_init_kernel(const double* __r
     rz += be * z;
     bb += be * be;
   }
-  rz = block_sum(rz, red);
-  bb = block_sum(bb, red);
+  rz = wave_sum(rz);
+  bb = wave_sum(bb);
   if (threadIdx.x == 0) {
     const double thr = (rtol * rtol) * bb;
     o[PCG_RZ] = rz;
@@ -205,13 +194,12 @@ __global__ __launch_bounds__(kUpdThreads) void pcg_update_kernel(const double* _
                                                                  const double* __restrict__ Ap, int k,
                                                                  double* __restrict__ o, double* __restrict__ r,
                                                                  double* __restrict__ p) {
-  __shared__ double red[kUpdThreads / 64];
   const double rr = o[PCG_RR], thr = o[PCG_THR], rz = o[PCG_RZ];
-  if (!(rr > thr)) return;  // converged (or NaN): the iteration is a no-op, block-uniform
+  if (!(rr > thr)) return;  // converged (or NaN): the iteration is a no-op, wave-uniform
   double* x = o + PCG_STATE_WORDS;
   double s = 0.0;
   for (int e = threadIdx.x; e < k; e += kUpdThreads) s += p[e] * Ap[e];
-  const double alpha = rz / block_sum(s, red);
+  const double alpha = rz / wave_sum(s);
   double rzn = 0.0, rrn = 0.0;
   for (int e = threadIdx.x; e < k; e += kUpdThreads) {
     x[e] += alpha * p[e];
@@ -220,8 +208,8 @@ __global__ __launch_bounds__(kUpdThreads) void pcg_update_kernel(const double* _
     rzn += re * (minv[e] * re);
     rrn += re * re;
   }
-  rzn = block_sum(rzn, red);
-  rrn = block_sum(rrn, red);
+  rzn = wave_sum(rzn);
+  rrn = wave_sum(rrn);
   const double beta = rzn / rz;
   for (int e = threadIdx.x; e < k; e += kUpdThreads) p[e] = minv[e] * r[e] + beta * p[e];
   if (threadIdx.x == 0) {
@@ -237,8 +225,7 @@ __global__ __launch_bounds__(kUpdThreads) void pcg_residual_kernel(const double*
                                                                    const double* __restrict__ Ax,
                                                                    const double* __restrict__ aStd, int k, int nf,
                                                                    double* __restrict__ o) {
-  __shared__ double red[kUpdThreads / 64];
-  if (o[PCG_STATUS] != 0.0 || o[PCG_BAD] != 0.0) return;  // block-uniform
+  if (o[PCG_STATUS] != 0.0 || o[PCG_BAD] != 0.0) return;  // wave-uniform
   const double bStd = o[PCG_BSTD];
   const double* x = o + PCG_STATE_WORDS;
   double* coef = o + PCG_STATE_WORDS + k;
@@ -248,7 +235,7 @@ __global__ __launch_bounds__(kUpdThreads) void pcg_residual_kernel(const double*
     s += re * re;
   }
   for (int j = threadIdx.x; j < nf; j += kUpdThreads) coef[j] = aStd[j] != 0.0 ? x[j] * bStd / aStd[j] : 0.0;
-  s = block_sum(s, red);
+  s = wave_sum(s);
   if (threadIdx.x == 0) o[PCG_OK] = s <= 100.0 * o[PCG_THR] ? 1.0 : 0.0;
 }
 

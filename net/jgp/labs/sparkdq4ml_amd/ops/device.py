@@ -519,7 +519,7 @@ def _gram_syrk(h, X, y, w, sel, compute_f64: bool):
     npair = P * (P + 1) // 2
     nst = int(h.syrk_stages(n))
     target = 4 * _wide_grid(h)  # >= 4 blocks per CU slot wave (2 resident per CU at f64)
-    splitk = int(os.environ.get("DQ4ML_SYRK_SPLITK", "0")) or max(1, min(-(-target // npair), max(1, nst // 8)))
+    splitk = max(1, min(-(-target // npair), max(1, nst // 8)))
     splitk = max(1, min(splitk, nst))
     part = torch.empty(int(h.syrk_partials(d, splitk)), dtype=torch.float64, device=dev)
     h.gram_syrk(1 if compute_f64 else 0, Xv.data_ptr(), int(ld), int(d), int(n), dtype_code(Xv), yd.data_ptr(),
@@ -1316,41 +1316,6 @@ def _wide_schedule(h, P: int, nsup: int, eb: int, dev) -> _WideSchedule:
     return sc
 
 
-_aug_ones = {}
-
-
-def _label_split(yd: torch.Tensor, live: torch.Tensor, eb: int):
-    """The label's augmentation columns for the wide SYRK, entirely on the device (no host read):
-    ``(cols, inv_scale, aug_scale, t)`` with cols = [live, y_hi, y_lo] (f32), ``aug_scale`` the
-    device f64[3] scales of those columns that the fold applies, ``inv_scale`` their f32 inverses
-    for the fp8 pack (None for bf16) and ``t`` the label shift (device scalar, None for bf16).
-
-    bf16: y = y_hi + y_lo, y_hi = bf16(y).  fp8: the label is centred first (t = its live mean: two
-    e4m3 digits of y - t carry ~8 bits relative to the label's spread instead of to its largest
-    magnitude), then y - t = y_hi + y_lo, each an e4m3 value times its own scale (the amax of the
-    part / 448)."""
-    dev = yd.device
-    if eb == 16:
-        ones = _aug_ones.get(dev)
-        if ones is None:
-            ones = _aug_ones[dev] = torch.ones(3, dtype=torch.float64, device=dev)
-        y_hi = yd.to(torch.bfloat16).to(torch.float64)
-        return [live.to(torch.float32), (y_hi * live).to(torch.float32), ((yd - y_hi) * live).to(torch.float32)], \
-            None, ones, None
-    one = torch.ones((), dtype=torch.float64, device=dev)
-    t = (yd * live).sum() / live.sum().clamp_min(1.0)
-    yc = (yd - t) * live
-    amax_h = yc.abs().max()
-    s_h = torch.where(amax_h > 0, amax_h / FP8_MAX, one)
-    y_hi = (yc / s_h).clamp(-FP8_MAX, FP8_MAX).to(torch.float8_e4m3fn).to(torch.float64) * s_h
-    y_lo = yc - y_hi
-    amax_l = y_lo.abs().max()
-    s_l = torch.where(amax_l > 0, amax_l / FP8_MAX, one)
-    aug = torch.stack([one, s_h, s_l])
-    return [live.to(torch.float32), y_hi.to(torch.float32), y_lo.to(torch.float32)], \
-        (1.0 / aug).to(torch.float32), aug, t
-
-
 class DeferredWide:
     """Wide SYRK partials whose split-K fold (+ RCCL all-reduce, band by band) has not been
     enqueued yet: an asynchronous overlapped fit runs it on its side stream with the solve, so the
@@ -1388,11 +1353,17 @@ def _gram_wide(h, T: TiledWide, y, w, sel, x_zero_dead, defer: bool = False):
     dev = T.device
     _check_dev(T.buf, y, sel)
     y, _, sel = _prep_rows(y, None, sel, n)
-    yd = y.to(torch.float64)
-    live = torch.ones(n, dtype=torch.float64, device=dev) if sel is None else sel.to(torch.float64)
     eb = T.eb
-    cols, inv, aug_scale, t_y = _label_split(yd, live, eb)
-    aug = pack_wide(cols, eb, None, nt=1, inv_scale=inv, shift=None)
+    # the label's augmentation panel, split and packed on the device (gram_wide.hip
+    # wide_label_*): aux = [1, s_h, s_l | t, 1/s_h, 1/s_l], no host read
+    aux = torch.empty(6, dtype=torch.float64, device=dev)
+    lpart = torch.empty(int(h.wide_label_part_doubles()), dtype=torch.float64, device=dev)
+    aug = TiledWide(torch.empty(max(1, (n + 63) // 64) * 256 * eb, dtype=torch.uint8, device=dev), 3, n, eb, None,
+                    None)  # (one 32-feature tile per 64-row superstep)
+    h.wide_label_aug(eb, y.data_ptr(), 0 if y.dtype == torch.float64 else 1, n, _ptr(sel), lpart.data_ptr(),
+                     aux.data_ptr(), aug.buf.data_ptr(), _stream())
+    aug_scale = aux[:3]
+    t_y = aux[3:4] if eb == 8 else None
     P = (d + 255) // 256
     nsup = max(1, (n + 63) // 64)
     sc = _wide_schedule(h, P, nsup, eb, dev)
@@ -1421,7 +1392,7 @@ def _gram_wide(h, T: TiledWide, y, w, sel, x_zero_dead, defer: bool = False):
     if banded and T.shift is not None and not T.shift.uniform:
         raise ValueError("wide Gram over RCCL: the features' shift must be the same on every rank "
                          "(pack_wide(shift='auto') agrees it; a caller-made Shift needs uniform=True)")
-    head_fix = (lambda: _unshift_label(out, d, t_y)) if t_y is not None else None
+    head_fix = (lambda: h.wide_unshift_label(out.data_ptr(), d, aux.data_ptr(), _stream())) if t_y is not None else None
     fold = functools.partial(h.gram_wide_fold, P, d, splitk, part.data_ptr(), aug_scale.data_ptr(), _ptr(T.scales))
 
     def finish():
@@ -1436,8 +1407,7 @@ def _gram_wide(h, T: TiledWide, y, w, sel, x_zero_dead, defer: bool = False):
         # same on every rank, so the un-shift of the sum is the sum of the un-shifts)
         return _unshift(h, out, T.shift, d)
     if defer:
-        return DeferredWide(finish, (part, aug_scale, T.scales, t_y, out,
-                                     None if T.shift is None else T.shift.dev), out)
+        return DeferredWide(finish, (part, aux, T.scales, out, None if T.shift is None else T.shift.dev), out)
     return finish()
 
 
@@ -1457,16 +1427,6 @@ def wide_bands(P: int, d: int, bucket_bytes: int, elt: int):
             bands.append((J0, J + 1, base + a * (a + 1) // 2, base + b * (b + 1) // 2))
             J0, acc = J + 1, 0
     return bands
-
-
-def _unshift_label(out: torch.Tensor, d: int, t) -> None:
-    """Head statistics of a label shifted by t (y' = y - t; a device scalar) -> those of y, in place (f64):
-    Σy² = Σy'² + 2tΣy' + t²W, Σy = Σy' + tW, Σx·y = Σx·y' + tΣx (Σx as folded, i.e. of the
-    features as they are stored)."""
-    W, b = out[1:2], out[3:4].clone()
-    out[4:5] += (2.0 * t) * b + (t * t) * W
-    out[3:4] += t * W
-    out[5 + d:5 + 2 * d] += t * out[5:5 + d]
 
 
 def _fold_all_reduce(fold, out: torch.Tensor, P: int, d: int, head_fix=None):

@@ -549,9 +549,8 @@ def launch(h, handle, grid: int, ptr_list, n: int, stream: int):
     h.rtc_launch_args(int(handle), int(grid), 256, np.asarray(ptr_list, dtype=np.int64), int(n), int(stream))
 
 
-VEC_ROWS = int(os.environ.get("DQ4ML_DQ_ROWS", "4"))  # consecutive rows per thread, vector form
-VEC_NT = os.environ.get("DQ4ML_DQ_NT", "0") != "0"  # non-temporal column loads (A/B knob)
-GRID_CAP = int(os.environ.get("DQ4ML_DQ_GRID", "131072"))  # grid-stride cap (blocks); config 4 A/B 2x: 8192 5.997 / 5.925, 32768 5.894 / 5.910, 131072 5.872 / 5.859 ms
+VEC_ROWS = 4  # consecutive rows per thread, vector form
+GRID_CAP = 131072  # grid-stride cap (blocks); config 4 A/B 2x: 8192 5.997 / 5.925, 32768 5.894 / 5.910, 131072 5.872 / 5.859 ms
 _VEC_BASE = {"double": "double", "float": "float", "int": "int", "long long": "long long", "bool": "unsigned char",
              "unsigned char": "unsigned char"}
 _VEC_NAME = {"double": "f64", "float": "f32", "int": "i32", "long long": "i64", "bool": "u8", "unsigned char": "u8"}
@@ -574,7 +573,7 @@ def _kernel_source_vec(g: _Gen, V: int = VEC_ROWS) -> str:
     n % V tail rows run the scalar body."""
     ns = len(g.ptrs)
     decl = "".join(f"    {ct} {v}_a[{V}];\n" for ct, v, _, _ in g.loads)
-    ldf = "__builtin_nontemporal_load(" if VEC_NT else "*("
+    ldf = "*("  # (non-temporal column loads measured no better)
     ld = "".join(f"    {{ const {_vec_t(st, V)} q = {ldf}(const {_vec_t(st, V)}*)((const {_VEC_BASE[st]}*)p[{s}] + r0));\n"
                  f"      for (int u = 0; u < {V}; ++u) {v}_a[u] = ({ct})q[u]; }}\n" for ct, v, st, s in g.loads)
     use = "".join(f"      const {ct} {v} = {v}_a[u];\n" for ct, v, _, _ in g.loads)

@@ -30,8 +30,11 @@ from typing import Optional
 import numpy as np
 import torch
 
+from ..utils.logging import get_logger
+
 __all__ = ["try_fused_stream", "kernel_source", "raw_layout", "STATS", "ENTRY"]
 
+log = get_logger("streamfuse")
 ENTRY = "dq_gram_stream"
 STATS = {"stream_grams": 0, "stream_replays": 0}
 _HERE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "csrc", "hip")
@@ -214,8 +217,7 @@ def _compile(chain, rel, feat_cols, mode):
         src = kernel_source(g, layout, ctypes, yv, NT, RING, {2: 1, 1: 0, 4: 2}[mode], yvalid)
         plan = _Plan(src, layout, d, NT, RING, mode)
     except (dqvm.Unfusable, _GramNullable, KeyError) as e:
-        if os.environ.get("DQ4ML_STREAM_DQ_DEBUG"):
-            print("streamfuse: not fusable:", repr(e))
+        log.debug("streamfuse: not fusable: %r", e)
         plan = None
     if len(_CACHE) >= 32:
         _CACHE.clear()
@@ -277,7 +279,7 @@ def _launch(r):
     fg = FusedGram(out, d, [], n)
     # the next step's pass reads only the in-memory columns: the fit tail (all-reduce, solve) may
     # run on the side stream beside it (models/regression.py overlapTail)
-    fg.overlap_ok = os.environ.get("DQ4ML_STREAM_OVERLAP", "1") != "0"
+    fg.overlap_ok = True
     return fg
 
 

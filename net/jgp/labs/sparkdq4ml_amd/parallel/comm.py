@@ -136,8 +136,18 @@ def host_group():
     it in the same order (the fit paths that use it run on every rank)."""
     global _host_group
     if _host_group is None:
-        _host_group = dist.new_group(backend="gloo") if dist.get_backend() != "gloo" else dist.group.WORLD
-    return _host_group
+        if dist.get_backend() == "gloo":
+            _host_group = dist.group.WORLD
+        else:
+            try:
+                _host_group = dist.new_group(backend="gloo")
+            except Exception as e:  # noqa: BLE001 -- no usable gloo transport on this host
+                import logging
+
+                logging.getLogger("dq4ml.comm").warning("no gloo control group (%s): host votes go through the "
+                                                        "device backend", e)
+                _host_group = False
+    return _host_group or None
 
 
 def all_agree(flag: bool) -> bool:
@@ -147,8 +157,11 @@ def all_agree(flag: bool) -> bool:
     on mismatched collectives."""
     if not collectives_active():
         return bool(flag)
+    g = host_group()
     t = torch.tensor([1 if flag else 0], dtype=torch.int32)
-    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=host_group())
+    if g is None:  # (fallback: a device all-reduce and one small read)
+        t = _comm_tensor(t)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=g)
     return bool(int(t.item()))
 
 
@@ -162,9 +175,19 @@ def health_check(timeout_s: float = 30.0, deferred: bool = False):
     # a host-side barrier over the gloo control group: it names the ranks that did not answer
     # within the timeout, and -- unlike a device all-reduce, whose wait() only orders a stream
     # after the collective -- it raises here, on the host, without any device sync
+    g = host_group()
+    if g is None:  # (no gloo transport: a device all-reduce of ones, its wait bounded)
+        x = torch.ones(1, device=torch.device("cuda", torch.cuda.current_device()))
+        work = dist.all_reduce(x, async_op=True)
+        try:
+            work.wait(timeout=datetime.timedelta(seconds=timeout_s))
+        except RuntimeError as e:
+            raise RankFailure(f"rank health check failed: {e}") from e
+        if int(x.item()) != world_size():
+            raise RankFailure(f"rank health check: {int(x.item())} of {world_size()} ranks answered")
+        return None
     try:
-        dist.monitored_barrier(group=host_group(), timeout=datetime.timedelta(seconds=timeout_s),
-                               wait_all_ranks=True)
+        dist.monitored_barrier(group=g, timeout=datetime.timedelta(seconds=timeout_s), wait_all_ranks=True)
     except RuntimeError as e:
         raise RankFailure(f"rank health check failed: {e}") from e
     return None

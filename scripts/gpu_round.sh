@@ -36,7 +36,8 @@ for s in $STEPS; do
        step widepmc5b 300 timeout -s KILL 240 rocprofv3 --kernel-trace --pmc GRBM_GUI_ACTIVE TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCP_TCC_READ_REQ_sum SQ_LDS_IDX_ACTIVE SQ_INSTS_VMEM -d gpurun_out/widepmc5b -o run --output-format csv -- python scripts/wide_bench.py) || exit $? ;;
     wideshard) step wideshard 600 env DQ4ML_FORCE_COLLECTIVES=1 python benchmarks/bench_wide.py --rows 1.25e6 --steps 20 --warmup 3 --json-out gpurun_out/wideshard.json &&
                step wideshard_local 600 python benchmarks/bench_wide.py --rows 1.25e6 --steps 20 --warmup 3 --json-out gpurun_out/wideshard_local.json &&
-               (export TMPDIR=/tmp DQ4ML_FORCE_COLLECTIVES=1; step wideshardprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/wideshardprof -o run --output-format csv -- python benchmarks/bench_wide.py --rows 1.25e6 --steps 10 --warmup 2) || exit $? ;;
+               (export TMPDIR=/tmp DQ4ML_FORCE_COLLECTIVES=1; step wideshardprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/wideshardprof -o run --output-format csv -- python benchmarks/bench_wide.py --rows 1.25e6 --steps 10 --warmup 2) &&
+               (export TMPDIR=/tmp; step wideshardprof_local 600 rocprofv3 --kernel-trace --stats -d gpurun_out/wideshardprof_local -o run --output-format csv -- python benchmarks/bench_wide.py --rows 1.25e6 --steps 10 --warmup 2) || exit $? ;;
     tailres) step tailres 600 env ROWS=${ROWS:-1.25e7} FITS=${FITS:-200} python scripts/tail_reserve_probe.py ;;
     tailresprof) (export TMPDIR=/tmp; step tailresprof 300 timeout -s KILL 240 rocprofv3 --kernel-trace -d gpurun_out/tailresprof -o run --output-format csv -- python scripts/tail_reserve_probe.py) || exit $? ;;
     cfg4) step cfg4 900 python benchmarks/bench_dq_pipeline.py --steps ${CFG4_STEPS:-5} --warmup 2 --json-out gpurun_out/cfg4.json ;;
@@ -85,14 +86,8 @@ for s in $STEPS; do
             step persist_w6_$r 300 env DQ4ML_SCAN_WPE=6 python benchmarks/bench_csv_pipeline.py --steps 20 --warmup 3 &&
             step persist_pc4_$r 300 env DQ4ML_SCAN_PER_CU=4 python benchmarks/bench_csv_pipeline.py --steps 20 --warmup 3 &&
             step persist_lb_$r 300 env DQ4ML_SCAN_GRAM_NOLB=0 python benchmarks/bench_csv_pipeline.py --steps 20 --warmup 3 || exit $?; done ;;
-    cfg4rs64) step cfg4rs64 900 env DQ4ML_GRAM_STREAM_F32RS=64 python benchmarks/bench_dq_pipeline.py --steps 5 --warmup 2 ;;
     cfg4ring3) step cfg4ring3 900 env DQ4ML_GRAM_STREAM_RING=3 python benchmarks/bench_dq_pipeline.py --steps 5 --warmup 2 ;;
     cfg4nodqs) step cfg4nodqs 900 env DQ4ML_DQ_STREAM=0 python benchmarks/bench_dq_pipeline.py --steps 5 --warmup 2 ;;
-    cfg4nt) step cfg4nt 900 env DQ4ML_DQ_NT=1 python benchmarks/bench_dq_pipeline.py --steps 5 --warmup 2 ;;
-    cfg4g32) step cfg4g32 900 env DQ4ML_DQ_GRID=32768 python benchmarks/bench_dq_pipeline.py --steps 5 --warmup 2 ;;
-    cfg4g2) step cfg4g2 900 env DQ4ML_DQ_GRID=2048 python benchmarks/bench_dq_pipeline.py --steps 5 --warmup 2 ;;
-    cfg4r8) step cfg4r8 900 env DQ4ML_DQ_ROWS=8 python benchmarks/bench_dq_pipeline.py --steps 5 --warmup 2 ;;
-    cfg4r16) step cfg4r16 900 env DQ4ML_DQ_ROWS=16 python benchmarks/bench_dq_pipeline.py --steps 5 --warmup 2 ;;
     gang) step gang_t 600 python -u -m pytest tests/test_gpu_wide.py -m gpu -q --maxfail=3 --timeout 120 --timeout-method thread &&
           step gang_ab 900 env N=1e7 D=4096 EB=8 REPS=5 VARIANTS="${VARIANTS:-5:morton:8:gang,4:morton:8:0:q2}" python scripts/wide_bench.py ;;
     augvalu) (export TMPDIR=/tmp
@@ -168,8 +163,6 @@ for s in $STEPS; do
     dist2) step dist2 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 scripts/dist_rehearsal.py ;;
     benchf32) step benchf32 600 python bench.py --steps 10 --warmup 2 --dtype fp32 ;;
     benchf32r3) step benchf32r3 600 env DQ4ML_GRAM_STREAM_RING=3 python bench.py --steps 10 --warmup 2 --dtype fp32 ;;
-    benchf32rs) for r in 2 3 4; do step benchf32rs32r$r 600 env DQ4ML_GRAM_STREAM_F32RS=32 DQ4ML_GRAM_STREAM_RING=$r python bench.py --steps 10 --warmup 2 --dtype fp32; done
-       step benchs32rs32 600 env DQ4ML_GRAM_STREAM_F32RS=32 python bench.py --steps 10 --warmup 2 --dtype bf16 --storage fp32 ;;
     benchf64) step benchf64 600 python bench.py --steps 10 --warmup 2 --dtype fp64 ;;
     benchf64old) step benchf64old 600 env DQ4ML_GRAM_STREAM=0 python bench.py --steps 10 --warmup 2 --dtype fp64 ;;
     benchf64s32) step benchf64s32 600 python bench.py --steps 10 --warmup 2 --dtype fp64 --storage fp32 ;;
@@ -196,11 +189,10 @@ for s in $STEPS; do
     sweep1) step sweep1 600 env DQ4ML_FORCE_COLLECTIVES=1 python scripts/bucket_sweep.py --rows 2e6 --buckets-mb 4,16,64 ;;
     bandprof) (export TMPDIR=/tmp DQ4ML_FORCE_COLLECTIVES=1; step bandprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/bandprof -o run --output-format csv -- python scripts/bucket_sweep.py --rows 1e6 --buckets-mb 4 --wires f32 --reps 2) || exit $? ;;
     lsq) step lsq 600 python -u -m pytest tests/test_gpu_lsq.py -m gpu -v --maxfail=5 --timeout 120 --timeout-method thread ;;
+    tailab) step tailab 600 python scripts/wide_tail_ab.py --rows 1.25e6 --fits 20 --reps 3 ;;
+    exitprobe) (export TMPDIR=/tmp; for m in plain cumask coop; do step exitprobe_$m 200 timeout -k 10 150 rocprofv3 --kernel-trace -d gpurun_out/exitprobe_$m -o run --output-format csv -- python scripts/prof_exit_probe.py $m || exit $?; done) || exit $? ;;
+    qncrash) (export TMPDIR=/tmp DQ4ML_BENCH_AB=0; step qncrash 300 timeout -k 10 240 rocprofv3 --kernel-trace -d gpurun_out/qncrash -o run --output-format csv -- python benchmarks/bench_lbfgs.py --rows 2e5 --features 2048 --steps 1 --warmup 1) || exit $? ;;
     lbfgssmall) step lbfgssmall 600 python benchmarks/bench_lbfgs.py --rows 2e5 --features 8192 --steps 2 --warmup 1 ;;
-    half) step half_t 600 env DQ4ML_GRAM_BF16_HALF=1 python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_determinism.py tests/test_gpu_fit_pipeline.py -m gpu -q --timeout 120 --timeout-method thread &&
-          for r in 1 2; do for m in 0 1; do
-            step half_${m}_s${r} 300 env DQ4ML_GRAM_BF16_HALF=$m python bench.py --steps 200 --warmup 20 --rows 1.25e7 &&
-            step half_${m}_h${r} 300 env DQ4ML_GRAM_BF16_HALF=$m python bench.py --steps 30 --warmup 5 || exit $?; done; done ;;
     cfg4ov) step cfg4ov_t 600 python -u -m pytest tests/test_gpu_streamfuse.py tests/test_gpu_fit_pipeline.py -m gpu -q --timeout 120 --timeout-method thread &&
           for r in 1 2; do for m in 0 1; do
             step cfg4ov_${m}_${r} 600 env DQ4ML_STREAM_OVERLAP=$m python benchmarks/bench_dq_pipeline.py --steps 10 --warmup 2 --json-out gpurun_out/cfg4ov_${m}_${r}.json || exit $?; done; done ;;

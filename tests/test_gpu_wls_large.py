@@ -103,10 +103,10 @@ def test_pcg_matches_direct_solve(nf, fit_intercept):
     assert np.array_equal(device.wls_pcg(s2, nf, optim.PCG_RTOL), o)
     # enqueued whole (the asynchronous fit's form): the same iterates, converged ones are no-ops
     s3 = device.wls_assemble(flat, nf, fit_intercept, 0.02 * float(bStd), 0.0, True, True)
-    device.wls_pcg_enqueue(s3, nf, optim.PCG_RTOL, 64)
+    device.wls_pcg_enqueue(s3, nf, optim.PCG_RTOL, 96)
     o3 = s3.o.cpu().numpy()
     w = device.PCG_STATE_WORDS
-    assert device.pcg_ok(o3) and 0 < o3[device.PCG_ITERS] < 64
+    assert device.pcg_ok(o3) and 0 < o3[device.PCG_ITERS] < 96
     assert np.array_equal(o3[w:], o[w:])
 
 
