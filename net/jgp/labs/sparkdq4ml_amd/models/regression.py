@@ -637,25 +637,21 @@ def _tail_stream(dev, wide: bool = False) -> "torch.cuda.Stream":
     process round-robin over its few hardware queues, and a plain side stream landed on the
     compute stream's queue, where the tail serialized behind the next fit's prologue (10.5 ->
     9.5 ms per 1.25e6 x 4096 fit once the host reads were gone).  A separate queue at normal
-    priority (a CU-masked stream over every CU) measured 9.74 ms: the tail's LDS-using kernels
-    then interleave with the next fit's SYRK and stall its gang rounds; at high priority the
-    tail drains first and the next SYRK runs undisturbed (9.07 ms; profiles/r6_wide_async.md)."""
+    priority (a CU-masked stream over every CU) lost in a same-process A/B, 10.45-10.51 against
+    8.97-9.01 ms per fit (profiles/r6/wide_tail_ab.log, profiles/r6_wide_async.md): the tail's fold
+    then interleaves with the next fit's SYRK and stalls its gang rounds; at high priority the
+    fold drains first, and the LDS-free PCG runs beside the SYRK."""
     masks = _tail_masks(dev)
-    key = (dev, masks is not None, wide, _WIDE_TAIL if wide else None)
+    key = (dev, masks is not None, wide)
     st = _tail_streams.get(key)
     if st is None:
         if masks is not None:
             st = streams.cu_masked_stream(masks[1], masks[2], dev, tag=98 if wide else 99)
-        elif wide and _WIDE_TAIL == "queue" and dev.type == "cuda":  # (A/B: scripts/wide_tail_ab.py)
-            cus = device._cus(native.hip())
-            st = streams.cu_masked_stream(list(range(cus)), cus, dev, tag=97)
         else:
             st = torch.cuda.Stream(device=dev, priority=-1) if wide else torch.cuda.Stream(device=dev)
         _tail_streams[key] = st
     return st
 
-
-_WIDE_TAIL = "high"  # the wide tail's stream: "high" priority, or its own normal-priority "queue"
 
 
 class _PendingWLS:

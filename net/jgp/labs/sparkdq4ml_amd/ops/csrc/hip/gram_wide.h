@@ -25,6 +25,8 @@ struct WideArgs {
   float* part;                // [npair * splitk][256][256] f32 partial tiles
   const double* aug_scale;    // device f64[3]: scales of [1, y_hi, y_lo] (made on the device with the
                               // label split, so no launch reads them on the host)
+  const int* tile_base;       // (or null: splitk slots per pair) [npair + 1] prefix table of the
+                              // partial tiles per pair (the gang schedule's merged units)
 };
 
 constexpr int kWideZeroBytes = 32768;  // >= the largest panel-relative piece offset (bf16 tiles: 30 KiB)
@@ -59,11 +61,13 @@ void gram_wide(int eb, WideArgs a, const int* pairs_dev, const float* scales, do
 void gram_wide_queue(int eb, WideArgs a, const int* pairs_dev, const float* scales, double* out, int* heads, int h,
                      int grid, hipStream_t st, bool fold = true);
 // gang schedule: grid blocks (one per CU, a multiple of 8) of 8 waves; group b % 8 owns splits
-// [g*S, g*S+S) (a.splitk == 8*S); pairs_dev lists the P(P-1)/2 off-diagonal pairs I < J < npanels,
-// then the P diagonal ones (diagonal units also write the augmentation tiles); bar (or null): 256
-// ints of scratch for the per-round group barrier (zeroed here on the stream; full rounds only,
-// bounded, self-disabling: gram_wide.hip gang_round_sync)
-void gram_wide_gang(int eb, WideArgs a, const int* pairs_dev, const float* scales, double* out, int S, int grid,
+// [g*S, g*S+S) (a.splitk == 8*S) and its blocks walk `units` entries of `table` (int4 per unit:
+// I, J, s0 | ns << 16, kk | K << 16 -- panels, row ranges [s0, s0 + ns) of the group, the unit's
+// slot kk of the K its pair has per group) statically, block l taking l, l + G, ...; partial
+// tiles at a.tile_base[pair] + g K + kk; bar (or null): 256 ints of scratch for the per-round
+// group barrier (zeroed here on the stream; full rounds only, bounded, self-disabling:
+// gram_wide.hip gang_round_sync)
+void gram_wide_gang(int eb, WideArgs a, const int* table, int units, const float* scales, double* out, int S, int grid,
                     hipStream_t st, bool fold = true, int* bar = nullptr);
 // fold the pairs of panel columns [J0, J1) (J = npanels: the augmentation column -> the head of
 // the flat layout) into out (f64) or out32 (f32 wire buffer, same flat indexing)

@@ -92,6 +92,12 @@ __device__ __forceinline__ int pair_index(int I, int J, int P) {
   return I * (P + 1) - I * (I - 1) / 2 + (J - I);
 }
 
+// partial tile of (pair, slot): uniform layouts hold splitk slots per pair; the gang schedule's
+// merged units give every pair its own slot count, from the tile_base prefix table
+__device__ __forceinline__ int64_t wide_tile(const WideArgs& a, int pair, int slot) {
+  return (a.tile_base ? (int64_t)a.tile_base[pair] : (int64_t)pair * a.splitk) + slot;
+}
+
 template <int N>
 __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
@@ -118,7 +124,8 @@ struct StageFrags {
 // so the LDS reads and the barrier skew hide under half a stage of MFMAs, and three stages of
 // global_load_lds stay in flight across every barrier.
 template <int EB, int MODE, int RING>
-__device__ __forceinline__ void syrk_block(const WideArgs& a, unsigned char* smem, int I, int J, int pair, int split) {
+__device__ __forceinline__ void syrk_block(const WideArgs& a, unsigned char* smem, int I, int J, int s_lo, int s_hi,
+                                           int slot) {
   typedef WideTraits<EB> Tr;
   typedef typename Tr::frag F;
   // 2 x 4 waves of 128 x 64 (2 waves/SIMD)
@@ -145,7 +152,7 @@ __device__ __forceinline__ void syrk_block(const WideArgs& a, unsigned char* sme
   const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 2, wn = wave & 3;
   const int64_t nst = a.nsup * Tr::kStagesPerSup;
-  const int64_t st0 = nst * split / a.splitk, st1 = nst * (split + 1) / a.splitk;
+  const int64_t st0 = nst * s_lo / a.splitk, st1 = nst * s_hi / a.splitk;  // rows of splits [s_lo, s_hi)
   const int64_t cnt = st1 - st0;
 
   // Each thread moves kLoadsPerPanel 16-byte pieces of every panel-stage image: piece r is byte o
@@ -282,21 +289,21 @@ __device__ __forceinline__ void syrk_block(const WideArgs& a, unsigned char* sme
     wait_vm<0>();  // drain the zero-page prefetches before the block can exit
   }
   if constexpr (MODE == 5) {  // (I, aug): 256 rows x the augmentation tile's 32 columns
-    float* out = a.part + ((int64_t)pair_index(I, a.npanels, a.npanels) * a.splitk + split) * kPanel * kPanel;
+    float* out = a.part + wide_tile(a, pair_index(I, a.npanels, a.npanels), slot) * kPanel * kPanel;
 #pragma unroll
     for (int x = 0; x < 4; ++x)
 #pragma unroll
       for (int r = 0; r < 16; ++r)
         out[(wn * 128 + x * 32 + mfma32_row(lane, r)) * kPanel + mfma32_col(lane)] = acc[x][0][r];
     if (I == 0 && wn == 0) {
-      float* o2 = a.part + ((int64_t)pair_index(a.npanels, a.npanels, a.npanels) * a.splitk + split) * kPanel * kPanel;
+      float* o2 = a.part + wide_tile(a, pair_index(a.npanels, a.npanels, a.npanels), slot) * kPanel * kPanel;
 #pragma unroll
       for (int r = 0; r < 16; ++r) o2[mfma32_row(lane, r) * kPanel + mfma32_col(lane)] = acc[0][1][r];
     }
     return;
   }
-  // f32 partial tile [256][256] of this (pair, split)
-  float* out = a.part + ((int64_t)pair_index(I, J, a.npanels) * a.splitk + split) * kPanel * kPanel;
+  // f32 partial tile [256][256] of this (pair, slot)
+  float* out = a.part + wide_tile(a, pair_index(I, J, a.npanels), slot) * kPanel * kPanel;
 #pragma unroll
   for (int x = 0; x < 4; ++x)
 #pragma unroll
@@ -319,10 +326,10 @@ __global__ __launch_bounds__(64 * kWaves, 1) void gram_wide_kernel(WideArgs a) {
   const int npair = (a.npanels + 1) * (a.npanels + 2) / 2;
   const int split = L / npair, pair = L - split * npair;
   const int I = a.pairs[2 * pair], J = a.pairs[2 * pair + 1];
-  if (I == J && J != a.npanels) syrk_block<EB, 3, RING>(a, smem, I, J, pair, split);
-  else if (J != a.npanels) syrk_block<EB, 0, RING>(a, smem, I, J, pair, split);
-  else if (I != a.npanels) syrk_block<EB, 1, RING>(a, smem, I, J, pair, split);
-  else syrk_block<EB, 2, RING>(a, smem, I, J, pair, split);
+  if (I == J && J != a.npanels) syrk_block<EB, 3, RING>(a, smem, I, J, split, split + 1, split);
+  else if (J != a.npanels) syrk_block<EB, 0, RING>(a, smem, I, J, split, split + 1, split);
+  else if (I != a.npanels) syrk_block<EB, 1, RING>(a, smem, I, J, split, split + 1, split);
+  else syrk_block<EB, 2, RING>(a, smem, I, J, split, split + 1, split);
 }
 
 // Persistent, XCD-grouped schedule.  The grid is one block per CU; block b belongs to group
@@ -351,10 +358,10 @@ __global__ __launch_bounds__(64 * kWaves, 1) void gram_wide_queue_kernel(WideArg
     const int k = u / npair, pos = u - k * npair;
     const int split = g * h + k;
     const int I = a.pairs[2 * pos], J = a.pairs[2 * pos + 1];
-    if (I == J && J != a.npanels) syrk_block<EB, 3, RING>(a, smem, I, J, pos, split);
-    else if (J != a.npanels) syrk_block<EB, 0, RING>(a, smem, I, J, pos, split);
-    else if (I != a.npanels) syrk_block<EB, 1, RING>(a, smem, I, J, pos, split);
-    else syrk_block<EB, 2, RING>(a, smem, I, J, pos, split);
+    if (I == J && J != a.npanels) syrk_block<EB, 3, RING>(a, smem, I, J, split, split + 1, split);
+    else if (J != a.npanels) syrk_block<EB, 0, RING>(a, smem, I, J, split, split + 1, split);
+    else if (I != a.npanels) syrk_block<EB, 1, RING>(a, smem, I, J, split, split + 1, split);
+    else syrk_block<EB, 2, RING>(a, smem, I, J, split, split + 1, split);
   }
 }
 
@@ -376,18 +383,6 @@ __global__ __launch_bounds__(64 * kWaves, 1) void gram_wide_queue_kernel(WideArg
 // next round, and the blocks of an XCD drifted ~0.5 ms apart -- out of reach of each other's
 // panel-stages in L2.  Segregated, every round holds units of one cost.  The pair table lists the
 // off-diagonal pairs, then the diagonal ones.
-__device__ __forceinline__ void gang_unit(int u, int S, int P, int& s, int& pos) {
-  const int noff = P * (P - 1) / 2;
-  if (u < S * noff) {
-    s = u / noff;
-    pos = u - s * noff;
-  } else {
-    const int v = u - S * noff;
-    s = v / P;
-    pos = noff + (v - s * P);
-  }
-}
-
 // round barrier of a gang group (bar: 8 groups x 32 ints, zeroed per launch, or null): the block
 // arrives after its unit k - 1 and waits until all G blocks of its group have -- the round's
 // blocks then start their units together and share each panel-stage through the XCD's L2.  For
@@ -417,24 +412,26 @@ __device__ __forceinline__ void gang_round_sync(int* bar, int g, int k, int G, i
 }
 
 template <int EB, int RING>
-__global__ __launch_bounds__(64 * kWaves, 1) void gram_wide_gang_kernel(WideArgs a, int S, int* __restrict__ bar) {
+__global__ __launch_bounds__(64 * kWaves, 1) void gram_wide_gang_kernel(WideArgs a, int S, int units,
+                                                                       const int4* __restrict__ table,
+                                                                       int* __restrict__ bar) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int g = blockIdx.x & 7, l = blockIdx.x >> 3, G = gridDim.x >> 3;
-  const int P = a.npanels, npu = P * (P + 1) / 2, units = npu * S;
   const int wave = threadIdx.x >> 6;
   // the waves whose tiles lie entirely below a diagonal unit's diagonal
   const bool aug_wave = (wave >> 2) == 1 && (wave & 3) < 2;
   int k = 0;
   for (int u = l; u < units; u += G, ++k) {
-    int s, pos;
-    gang_unit(u, S, P, s, pos);
-    const int split = g * S + s;
-    const int I = a.pairs[2 * pos], J = a.pairs[2 * pos + 1];
+    // unit u of every group: panels (I, J), row ranges [s0, s0 + ns) of the group's S, and the
+    // unit's slot kk among the K units its pair has per group (slot g K + kk of the pair's tiles)
+    const int4 e = table[u];
+    const int I = e.x, J = e.y, s0 = e.z & 0xffff, ns = e.z >> 16, kk = e.w & 0xffff, K = e.w >> 16;
+    const int lo = g * S + s0, slot = g * K + kk;
     gang_round_sync(bar, g, k, G, units);
-    if (I != J) syrk_block<EB, 0, RING>(a, smem, I, J, 0, split);
-    else if (aug_wave) syrk_block<EB, 5, RING>(a, smem, I, J, 0, split);
-    else if (wave < 2) syrk_block<EB, 4, RING>(a, smem, I, J, 0, split);  // + the aug tile's loads
-    else syrk_block<EB, 6, RING>(a, smem, I, J, 0, split);
+    if (I != J) syrk_block<EB, 0, RING>(a, smem, I, J, lo, lo + ns, slot);
+    else if (aug_wave) syrk_block<EB, 5, RING>(a, smem, I, J, lo, lo + ns, slot);
+    else if (wave < 2) syrk_block<EB, 4, RING>(a, smem, I, J, lo, lo + ns, slot);  // + the aug tile's loads
+    else syrk_block<EB, 6, RING>(a, smem, I, J, lo, lo + ns, slot);
     __syncthreads();  // every wave is done reading the ring before the next unit's first glds
   }
 }
@@ -477,12 +474,14 @@ __global__ __launch_bounds__(256) void gram_wide_reduce_kernel(WideArgs a, const
     int J = J0, I = q;  // band-local pair index (column-major) -> (I, J)
     while (I >= J + 1) { I -= J + 1; ++J; }
     const int pr = I * (P + 1) - I * (I - 1) / 2 + (J - I);  // row-major storage index of (I, J)
-    const float* base = a.part + (int64_t)pr * a.splitk * slab + e;
+    const int64_t t0 = a.tile_base ? (int64_t)a.tile_base[pr] : (int64_t)pr * a.splitk;
+    const int nsl = a.tile_base ? a.tile_base[pr + 1] - a.tile_base[pr] : a.splitk;  // this pair's slots
+    const float* base = a.part + t0 * slab + e;
     const int i = I * kPanel + r;
     if (J < P) {  // Gram block
       if (i >= d || (I == J && r > c0 + 3)) continue;
       double v0 = 0.0, v1 = 0.0, v2 = 0.0, v3 = 0.0;
-      for (int k = 0; k < a.splitk; ++k) {
+      for (int k = 0; k < nsl; ++k) {
         const float4 x = *reinterpret_cast<const float4*>(base + (int64_t)k * slab);
         v0 += (double)x.x;
         v1 += (double)x.y;
@@ -504,7 +503,7 @@ __global__ __launch_bounds__(256) void gram_wide_reduce_kernel(WideArgs a, const
     if (c0 != 0) continue;  // augmentation column: only columns 0-2 hold data
     auto sum = [&](int off) {
       double v = 0.0;
-      for (int k = 0; k < a.splitk; ++k) v += (double)base[(int64_t)k * slab + off];
+      for (int k = 0; k < nsl; ++k) v += (double)base[(int64_t)k * slab + off];
       return v;
     };
     if (I < P) {  // (X panel, augmentation): column 0 -> aSum, columns 1 + 2 -> abSum
@@ -910,23 +909,25 @@ void gram_wide_queue(int eb, WideArgs a, const int* pairs_dev, const float* scal
 }
 
 template <int EB>
-static void launch_wide_gang(const WideArgs& a, int grid, int S, hipStream_t st, int* bar) {
+static void launch_wide_gang(const WideArgs& a, int grid, int S, int units, const int4* table, hipStream_t st,
+                             int* bar) {
   const size_t lds = (size_t)5 * kStageBytes;
   DQ_HIP_CHECK(hipFuncSetAttribute((const void*)gram_wide_gang_kernel<EB, 5>,
                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   if (bar != nullptr) DQ_HIP_CHECK(hipMemsetAsync(bar, 0, 8 * 32 * sizeof(int), st));
-  hipLaunchKernelGGL((gram_wide_gang_kernel<EB, 5>), dim3(grid), dim3(64 * kWaves), lds, st, a, S, bar);
+  hipLaunchKernelGGL((gram_wide_gang_kernel<EB, 5>), dim3(grid), dim3(64 * kWaves), lds, st, a, S, units, table, bar);
   DQ_HIP_CHECK(hipGetLastError());
 }
 
-void gram_wide_gang(int eb, WideArgs a, const int* pairs_dev, const float* scales, double* out, int S, int grid,
+void gram_wide_gang(int eb, WideArgs a, const int* table, int units, const float* scales, double* out, int S, int grid,
                     hipStream_t st, bool fold, int* bar) {
-  a.pairs = pairs_dev;
   if (S < 1 || a.splitk != 8 * S) throw std::invalid_argument("gram_wide_gang: splitk must be 8 * S");
   if (grid < 8 || grid % 8) throw std::invalid_argument("gram_wide_gang: grid must be a positive multiple of 8");
   if ((int64_t)a.splitk > a.nsup) throw std::invalid_argument("gram_wide_gang: more row ranges than supersteps");
-  if (eb == 16) launch_wide_gang<16>(a, grid, S, st, bar);
-  else launch_wide_gang<8>(a, grid, S, st, bar);
+  if (a.tile_base == nullptr || units < 1) throw std::invalid_argument("gram_wide_gang: needs the unit and tile tables");
+  const int4* t = reinterpret_cast<const int4*>(table);
+  if (eb == 16) launch_wide_gang<16>(a, grid, S, units, t, st, bar);
+  else launch_wide_gang<8>(a, grid, S, units, t, st, bar);
   if (fold) launch_fold(a, scales, out, nullptr, 0, a.npanels + 1, st);
 }
 

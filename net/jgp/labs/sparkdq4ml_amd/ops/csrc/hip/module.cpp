@@ -276,7 +276,7 @@ PYBIND11_MODULE(_dq4ml_hip, m) {
                  P<const float>(shift));
   });
   auto wide_args = [](uintptr_t X, uintptr_t Xaug, uintptr_t zeros, int nt, int npanels, int d, int64_t nsup,
-                      int splitk, uintptr_t part, uintptr_t aug_scale) {
+                      int splitk, uintptr_t part, uintptr_t aug_scale, uintptr_t tile_base = 0) {
     WideArgs a{};
     a.X = P<const unsigned char>(X);
     a.Xaug = P<const unsigned char>(Xaug);
@@ -288,6 +288,7 @@ PYBIND11_MODULE(_dq4ml_hip, m) {
     a.splitk = splitk;
     a.part = P<float>(part);
     a.aug_scale = P<const double>(aug_scale);
+    a.tile_base = P<const int>(tile_base);
     return a;
   };
   // aug_scale: device f64[3] scales of the augmentation columns [1, y_hi, y_lo] (read by the fold)
@@ -306,17 +307,17 @@ PYBIND11_MODULE(_dq4ml_hip, m) {
                     as_stream(stream), fold);
   });
   m.def("gram_wide_gang", [wide_args](int eb, uintptr_t X, uintptr_t Xaug, uintptr_t zeros, int nt, int npanels,
-                                      int d, int64_t nsup, int S, uintptr_t pairs, uintptr_t part, uintptr_t aug_scale,
-                                      uintptr_t scales, uintptr_t out, int grid, uintptr_t stream, bool fold,
-                                      uintptr_t bar) {
-    WideArgs a = wide_args(X, Xaug, zeros, nt, npanels, d, nsup, 8 * S, part, aug_scale);
-    gram_wide_gang(eb, a, P<const int>(pairs), P<const float>(scales), P<double>(out), S, grid, as_stream(stream),
-                   fold, P<int>(bar));
+                                      int d, int64_t nsup, int S, uintptr_t table, int units, uintptr_t tile_base,
+                                      uintptr_t part, uintptr_t aug_scale, uintptr_t scales, uintptr_t out, int grid,
+                                      uintptr_t stream, bool fold, uintptr_t bar) {
+    WideArgs a = wide_args(X, Xaug, zeros, nt, npanels, d, nsup, 8 * S, part, aug_scale, tile_base);
+    gram_wide_gang(eb, a, P<const int>(table), units, P<const float>(scales), P<double>(out), S, grid,
+                   as_stream(stream), fold, P<int>(bar));
   });
   m.def("gram_wide_fold", [wide_args](int npanels, int d, int splitk, uintptr_t part, uintptr_t aug_scale,
-                                      uintptr_t scales, uintptr_t out, uintptr_t out32, int J0, int J1,
-                                      uintptr_t stream) {
-    WideArgs a = wide_args(0, 0, 0, 0, npanels, d, 0, splitk, part, aug_scale);
+                                      uintptr_t tile_base, uintptr_t scales, uintptr_t out, uintptr_t out32, int J0,
+                                      int J1, uintptr_t stream) {
+    WideArgs a = wide_args(0, 0, 0, 0, npanels, d, 0, splitk, part, aug_scale, tile_base);
     gram_wide_fold(a, P<const float>(scales), P<double>(out), P<float>(out32), J0, J1, as_stream(stream));
   });
 

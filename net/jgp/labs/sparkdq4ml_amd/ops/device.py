@@ -1277,13 +1277,54 @@ def _wide_grid(h) -> int:
 
 @dataclass
 class _WideSchedule:
-    """Launch constants of one wide Gram shape (cached: a repeated fit re-uses the device pair table
+    """Launch constants of one wide Gram shape (cached: a repeated fit re-uses the device tables
     and the split choice instead of rebuilding and re-uploading them)."""
     sched: str            # "gang" | "queue" | "grid"
     splitk: int
     S: int                # gang row ranges per group (0: not the gang schedule)
     hq: int               # queue row ranges per group (0: not the queue schedule)
-    pairs_dev: torch.Tensor
+    pairs_dev: torch.Tensor  # pair list (queue / grid) or the gang's int4 unit table
+    units: int = 0        # gang units per group
+    tile_base: Optional[torch.Tensor] = None  # gang: [npair + 1] partial-tile prefix per pair
+    tiles: int = 0        # partial tiles in all
+
+
+def _gang_table(P: int, S: int, G: int):
+    """The gang schedule's unit table and per-pair partial-tile prefix (gram_wide.hip
+    gram_wide_gang_kernel).  A group of G blocks covers S row ranges of the panel pairs:
+
+    * off-diagonal pairs, as many whole multiples of G as there are: one LONG unit each over all
+      S ranges (block l takes G-strided pairs; every block of a round sweeps the same rows, so
+      each panel-stage still comes from HBM once per round) -- ONE partial tile per group instead
+      of S, so the split-K fold reads up to S x fewer bytes;
+    * the remaining off-diagonal pairs, then the diagonal ones (which carry the augmentation
+      products), one unit per range, range-major -- the round-5 equal-cost units.
+    Every block runs the same number of range-units (the G-multiples keep the long units even,
+    the short ones deal round-robin as before).  Returns (int4 rows, units, tile_base, tiles)."""
+    pairs = _wide_pairs(P)
+    off = [p for p in pairs if p[0] != p[1] and p[1] < P]
+    diag = [p for p in pairs if p[0] == p[1] and p[1] < P]
+    n_long = (len(off) // G) * G if S > 1 else 0
+    units = [(p, 0, S) for p in off[:n_long]]
+    units += [(p, s, 1) for s in range(S) for p in off[n_long:]]
+    units += [(p, s, 1) for s in range(S) for p in diag]
+    K, kk, rows = {}, {}, []
+    for p, _, _ in units:
+        K[p] = K.get(p, 0) + 1
+    for p, s0, ns in units:
+        k = kk.get(p, 0)
+        kk[p] = k + 1
+        rows.append((p[0], p[1], s0 | (ns << 16), k | (K[p] << 16)))
+    # tiles per pair, row-major over I <= J in [0, P]: 8 groups x K; the augmentation column's
+    # pairs (I, P) are written by (I, I)'s units, (P, P) by (0, 0)'s
+    base, t = [], 0
+    for i in range(P + 1):
+        for j in range(i, P + 1):
+            base.append(t)
+            src = (i, j) if j < P else ((i, i) if i < P else (0, 0))
+            t += 8 * K.get(src, 0)
+    base.append(t)
+    return rows, len(units), base, t
 
 
 _wide_sched_cache = {}
@@ -1301,9 +1342,12 @@ def _wide_schedule(h, P: int, nsup: int, eb: int, dev) -> _WideSchedule:
     pairs = _wide_pairs(P)
     gs = _wide_gang_s(P, nsup, grid // 8) if forced == "gang" else 0
     hq = _wide_queue_h(nsup) if not gs and forced in ("gang", "queue") else 0
-    if gs:  # gang units: the off-diagonal pairs first, then the diagonal ones (gram_wide.hip gang_unit)
-        pairs = [p for p in pairs if p[0] != p[1] and p[1] < P] + [p for p in pairs if p[0] == p[1] and p[1] < P]
-        sched, splitk = "gang", 8 * gs
+    if gs:  # (gram_wide.hip gram_wide_gang_kernel: long off-diagonal units, then equal-cost short ones)
+        rows, units, base, tiles = _gang_table(P, gs, grid // 8)
+        sc = _WideSchedule("gang", 8 * gs, gs, 0, _h2d(np.asarray(rows, dtype=np.int32).reshape(-1), dev), units,
+                           _h2d(np.asarray(base, dtype=np.int32), dev), tiles)
+        _wide_sched_cache[key] = sc
+        return sc
     elif hq:
         sched, splitk = "queue", 8 * hq
     else:
@@ -1312,6 +1356,7 @@ def _wide_schedule(h, P: int, nsup: int, eb: int, dev) -> _WideSchedule:
         # f32 MFMA accumulators count rows exactly only below 2^24 per split
         splitk = max(1, min(max(splitk, -(-nsup * 64 // (1 << 23))), nsup))
     sc = _WideSchedule(sched, splitk, gs, hq, _h2d(np.asarray(pairs, dtype=np.int32).reshape(-1), dev))
+    sc.tiles = (P + 1) * (P + 2) // 2 * splitk
     _wide_sched_cache[key] = sc
     return sc
 
@@ -1369,7 +1414,7 @@ def _gram_wide(h, T: TiledWide, y, w, sel, x_zero_dead, defer: bool = False):
     sc = _wide_schedule(h, P, nsup, eb, dev)
     splitk = sc.splitk
     out = torch.empty(5 + 2 * d + d * (d + 1) // 2, dtype=torch.float64, device=dev)
-    part = torch.empty(int(h.gram_wide_partials(d, splitk)), dtype=torch.float32, device=dev)
+    part = torch.empty(sc.tiles * 256 * 256, dtype=torch.float32, device=dev)
     # data-parallel fit over RCCL: fold band by band and all-reduce each band while the next folds
     banded = comm.collectives_active() and comm.backend() == "nccl"
     fold_in = not banded and not defer  # the launch folds into `out` itself
@@ -1379,8 +1424,9 @@ def _gram_wide(h, T: TiledWide, y, w, sel, x_zero_dead, defer: bool = False):
         # per-round group barrier (full rounds, bounded: the blocks of an XCD start every round
         # together, profiles/r5_wide_limiter.md)
         bar = torch.empty(256, dtype=torch.int32, device=dev)
-        h.gram_wide_gang(*args, sc.S, sc.pairs_dev.data_ptr(), part.data_ptr(), aug_scale.data_ptr(), _ptr(T.scales),
-                         out.data_ptr(), _wide_grid(h), _stream(), fold_in, bar.data_ptr())
+        h.gram_wide_gang(*args, sc.S, sc.pairs_dev.data_ptr(), sc.units, sc.tile_base.data_ptr(), part.data_ptr(),
+                         aug_scale.data_ptr(), _ptr(T.scales), out.data_ptr(), _wide_grid(h), _stream(), fold_in,
+                         bar.data_ptr())
     elif sc.sched == "queue":
         # persistent XCD-grouped schedule (gram_wide_queue_kernel): 8 groups x h row ranges
         heads = torch.empty(8, dtype=torch.int32, device=dev)
@@ -1393,7 +1439,8 @@ def _gram_wide(h, T: TiledWide, y, w, sel, x_zero_dead, defer: bool = False):
         raise ValueError("wide Gram over RCCL: the features' shift must be the same on every rank "
                          "(pack_wide(shift='auto') agrees it; a caller-made Shift needs uniform=True)")
     head_fix = (lambda: h.wide_unshift_label(out.data_ptr(), d, aux.data_ptr(), _stream())) if t_y is not None else None
-    fold = functools.partial(h.gram_wide_fold, P, d, splitk, part.data_ptr(), aug_scale.data_ptr(), _ptr(T.scales))
+    fold = functools.partial(h.gram_wide_fold, P, d, splitk, part.data_ptr(), aug_scale.data_ptr(), _ptr(sc.tile_base),
+                             _ptr(T.scales))
 
     def finish():
         if banded:
@@ -1407,7 +1454,8 @@ def _gram_wide(h, T: TiledWide, y, w, sel, x_zero_dead, defer: bool = False):
         # same on every rank, so the un-shift of the sum is the sum of the un-shifts)
         return _unshift(h, out, T.shift, d)
     if defer:
-        return DeferredWide(finish, (part, aux, T.scales, out, None if T.shift is None else T.shift.dev), out)
+        return DeferredWide(finish, (part, aux, T.scales, out, None if T.shift is None else T.shift.dev, sc.tile_base),
+                            out)
     return finish()
 
 

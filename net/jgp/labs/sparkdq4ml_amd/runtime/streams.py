@@ -57,31 +57,7 @@ def cu_masked_stream(cu_ids, cus: int, device=None, tag: int = 0) -> "torch.cuda
         with torch.cuda.device(idx):
             ptr = native.hip().stream_create_cumask(words)
         st = _masked[key] = torch.cuda.ExternalStream(ptr, device=torch.device("cuda", idx))
-        _masked_raw.append((idx, ptr))
-        if len(_masked_raw) == 1:
-            import atexit
-
-            atexit.register(release_masked_streams)
     return st
-
-
-_masked_raw: list = []
-
-
-def release_masked_streams() -> None:
-    """Drain and destroy the CU-masked streams (interpreter exit): each is a hardware queue of its
-    own, and one left to the HIP runtime's static teardown crashed rocprofv3's finalization at
-    process exit (SIGSEGV in __cxa_finalize; profiles/r6_wide_async.md)."""
-    from ..ops import native
-
-    while _masked_raw:
-        idx, ptr = _masked_raw.pop()
-        try:
-            with torch.cuda.device(idx):
-                native.hip().stream_destroy(ptr)
-        except Exception:  # noqa: BLE001 -- exit path: a dead context has nothing left to destroy
-            pass
-    _masked.clear()
 
 
 _pool = None

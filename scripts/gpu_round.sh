@@ -189,8 +189,8 @@ for s in $STEPS; do
     sweep1) step sweep1 600 env DQ4ML_FORCE_COLLECTIVES=1 python scripts/bucket_sweep.py --rows 2e6 --buckets-mb 4,16,64 ;;
     bandprof) (export TMPDIR=/tmp DQ4ML_FORCE_COLLECTIVES=1; step bandprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/bandprof -o run --output-format csv -- python scripts/bucket_sweep.py --rows 1e6 --buckets-mb 4 --wires f32 --reps 2) || exit $? ;;
     lsq) step lsq 600 python -u -m pytest tests/test_gpu_lsq.py -m gpu -v --maxfail=5 --timeout 120 --timeout-method thread ;;
-    tailab) step tailab 600 python scripts/wide_tail_ab.py --rows 1.25e6 --fits 20 --reps 3 ;;
-    exitprobe) (export TMPDIR=/tmp; for m in plain cumask coop; do step exitprobe_$m 200 timeout -k 10 150 rocprofv3 --kernel-trace -d gpurun_out/exitprobe_$m -o run --output-format csv -- python scripts/prof_exit_probe.py $m || exit $?; done) || exit $? ;;
+    exitprobe) (export TMPDIR=/tmp; for m in plain coop cumask; do step exitprobe_$m 200 timeout -k 10 150 rocprofv3 --kernel-trace -d gpurun_out/exitprobe_$m -o run --output-format csv -- python scripts/prof_exit_probe.py $m || exit $?; done) || exit $? ;;
+    exitnoprof) for m in coop cumask; do step exitnoprof_$m 200 timeout -k 10 150 python scripts/prof_exit_probe.py $m || exit $?; done ;;
     qncrash) (export TMPDIR=/tmp DQ4ML_BENCH_AB=0; step qncrash 300 timeout -k 10 240 rocprofv3 --kernel-trace -d gpurun_out/qncrash -o run --output-format csv -- python benchmarks/bench_lbfgs.py --rows 2e5 --features 2048 --steps 1 --warmup 1) || exit $? ;;
     lbfgssmall) step lbfgssmall 600 python benchmarks/bench_lbfgs.py --rows 2e5 --features 8192 --steps 2 --warmup 1 ;;
     cfg4ov) step cfg4ov_t 600 python -u -m pytest tests/test_gpu_streamfuse.py tests/test_gpu_fit_pipeline.py -m gpu -q --timeout 120 --timeout-method thread &&

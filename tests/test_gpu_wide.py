@@ -214,6 +214,36 @@ def test_wide_schedules_match_oracle(eb, sched, d, monkeypatch):
     ii, jj = torch.triu_indices(d, d, device="cuda")  # packed upper: (i, j), i <= j at j(j+1)/2 + i
     ref = torch.empty(d * (d + 1) // 2, dtype=torch.float64, device="cuda")
     ref[jj * (jj + 1) // 2 + ii] = G[ii, jj]
+    # a long unit's f32 MFMA accumulators sum all S ranges of its group (3 x 2 084 rows here):
+    # f32 rounding of the longer chains, ~1e-5 relative (the fp8 inputs' own quantization is ~1e-2)
+    assert _rel(aa, ref.cpu()) < 5e-5
+
+
+@gpu
+@pytest.mark.parametrize("eb", [16, 8])
+def test_wide_gang_long_units_match_oracle(eb, monkeypatch):
+    # d = 2100: 36 off-diagonal panel pairs >= the 32 blocks of a group, so 32 of them run as LONG
+    # units (all S row ranges in one K loop, one partial tile per group) beside short ones
+    _hip()
+    from net.jgp.labs.sparkdq4ml_amd.ops import device
+
+    monkeypatch.setenv("DQ4ML_WIDE_GANG_S", "3")
+    d, n = 2100, 50_003
+    rows, units, base, tiles = device._gang_table((d + 255) // 256, 3, device._wide_grid(device.native.hip()) // 8)
+    assert any((r[2] >> 16) == 3 for r in rows) and any((r[2] >> 16) == 1 for r in rows)
+    g = torch.Generator(device="cuda").manual_seed(eb)
+    X = torch.randn(d, n, generator=g, device="cuda") - 0.1
+    y = torch.randn(n, generator=g, device="cuda", dtype=torch.float64) + 2
+    T = device.pack_wide([X.to(torch.bfloat16) if eb == 16 else X], eb, None)
+    out = device.gram_stats(T, y, None, None, "bf16" if eb == 16 else "fp8", x_zero_dead=True)
+    Xq = T.to_dense().double()
+    s, a, ab, aa = _parts(out, d)
+    assert s[0] == n
+    assert _rel(a, Xq.sum(1).cpu()) < 1e-5
+    G = Xq @ Xq.T
+    ii, jj = torch.triu_indices(d, d, device="cuda")
+    ref = torch.empty(d * (d + 1) // 2, dtype=torch.float64, device="cuda")
+    ref[jj * (jj + 1) // 2 + ii] = G[ii, jj]
     assert _rel(aa, ref.cpu()) < 1e-5
 
 
