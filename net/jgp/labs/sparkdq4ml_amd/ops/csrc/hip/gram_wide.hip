@@ -501,27 +501,40 @@ __global__ __launch_bounds__(256) void gram_wide_reduce_kernel(WideArgs a, const
       continue;
     }
     if (c0 != 0) continue;  // augmentation column: only columns 0-2 hold data
-    auto sum = [&](int off) {
-      double v = 0.0;
-      for (int k = 0; k < nsl; ++k) v += (double)base[(int64_t)k * slab + off];
-      return v;
-    };
     if (I < P) {  // (X panel, augmentation): column 0 -> aSum, columns 1 + 2 -> abSum
-      if (i < d) {
-        const double si = scales ? (double)scales[i] : 1.0;
-        wide_store(out, out32, 5 + i, sum(0) * si * s1);
-        wide_store(out, out32, 5 + d + i, (sum(1) * syh + sum(2) * syl) * si);
+      if (i >= d) continue;
+      double v0 = 0.0, v1 = 0.0, v2 = 0.0;  // one float4 per slab (the same k order per element)
+#pragma unroll 4
+      for (int k = 0; k < nsl; ++k) {
+        const float4 x = *reinterpret_cast<const float4*>(base + (int64_t)k * slab);
+        v0 += (double)x.x;
+        v1 += (double)x.y;
+        v2 += (double)x.z;
       }
-    } else if (r == 0) {  // (augmentation, augmentation): the five scalars
-      const double g11 = sum(0) * s1 * s1;
-      const double g1h = sum(1) * s1 * syh, g1l = sum(2) * s1 * syl;
-      const double ghh = sum(kPanel + 1) * syh * syh, ghl = sum(kPanel + 2) * syh * syl;
-      const double gll = sum(2 * kPanel + 2) * syl * syl;
-      wide_store(out, out32, 0, g11);  // count, wSum, wwSum (unit weights; dead rows are zero)
-      wide_store(out, out32, 1, g11);
-      wide_store(out, out32, 2, g11);
-      wide_store(out, out32, 3, g1h + g1l);              // Σy
-      wide_store(out, out32, 4, ghh + 2.0 * ghl + gll);  // Σy²
+      const double si = scales ? (double)scales[i] : 1.0;
+      wide_store(out, out32, 5 + i, v0 * si * s1);
+      wide_store(out, out32, 5 + d + i, (v1 * syh + v2 * syl) * si);
+    } else if (r == 0) {  // (augmentation, augmentation): the five scalars from rows 0-2
+      double g00 = 0.0, g01 = 0.0, g02 = 0.0, g11 = 0.0, g12 = 0.0, g22 = 0.0;
+#pragma unroll 2
+      for (int k = 0; k < nsl; ++k) {
+        const float* t = base + (int64_t)k * slab;
+        const float4 x0 = *reinterpret_cast<const float4*>(t);
+        const float4 x1 = *reinterpret_cast<const float4*>(t + kPanel);
+        const float4 x2 = *reinterpret_cast<const float4*>(t + 2 * kPanel);
+        g00 += (double)x0.x;
+        g01 += (double)x0.y;
+        g02 += (double)x0.z;
+        g11 += (double)x1.y;
+        g12 += (double)x1.z;
+        g22 += (double)x2.z;
+      }
+      const double w = g00 * s1 * s1;
+      wide_store(out, out32, 0, w);  // count, wSum, wwSum (unit weights; dead rows are zero)
+      wide_store(out, out32, 1, w);
+      wide_store(out, out32, 2, w);
+      wide_store(out, out32, 3, g01 * s1 * syh + g02 * s1 * syl);                            // Σy
+      wide_store(out, out32, 4, g11 * syh * syh + 2.0 * (g12 * syh * syl) + g22 * syl * syl);  // Σy²
     }
   }
 }

@@ -214,9 +214,7 @@ def test_wide_schedules_match_oracle(eb, sched, d, monkeypatch):
     ii, jj = torch.triu_indices(d, d, device="cuda")  # packed upper: (i, j), i <= j at j(j+1)/2 + i
     ref = torch.empty(d * (d + 1) // 2, dtype=torch.float64, device="cuda")
     ref[jj * (jj + 1) // 2 + ii] = G[ii, jj]
-    # a long unit's f32 MFMA accumulators sum all S ranges of its group (3 x 2 084 rows here):
-    # f32 rounding of the longer chains, ~1e-5 relative (the fp8 inputs' own quantization is ~1e-2)
-    assert _rel(aa, ref.cpu()) < 5e-5
+    assert _rel(aa, ref.cpu()) < 1e-5
 
 
 @gpu
@@ -244,7 +242,9 @@ def test_wide_gang_long_units_match_oracle(eb, monkeypatch):
     ii, jj = torch.triu_indices(d, d, device="cuda")
     ref = torch.empty(d * (d + 1) // 2, dtype=torch.float64, device="cuda")
     ref[jj * (jj + 1) // 2 + ii] = G[ii, jj]
-    assert _rel(aa, ref.cpu()) < 1e-5
+    # a long unit's f32 MFMA accumulators sum all S ranges of its group (3 x 2 084 rows here):
+    # f32 rounding of the longer chains, ~1e-5 relative (the fp8 inputs' own quantization is ~1e-2)
+    assert _rel(aa, ref.cpu()) < 5e-5
 
 
 @gpu
