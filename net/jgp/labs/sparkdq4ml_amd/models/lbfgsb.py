@@ -83,17 +83,11 @@ class LBFGSB:
     def _cauchy_point(self, st: LBFGSBState, W: np.ndarray, M: np.ndarray):
         x, g, theta = st.x, st.grad, st.theta
         n = x.size
-        d = np.zeros(n)
-        t = np.empty(n)
         with np.errstate(divide="ignore", invalid="ignore", over="ignore"):
-            for i in range(n):
-                gi = g[i]
-                if gi == 0.0:
-                    t[i] = np.finfo(np.float64).max
-                else:
-                    ti = (x[i] - self.upper[i]) / gi if gi < 0 else (x[i] - self.lower[i]) / gi
-                    d[i] = 0.0 if ti == 0.0 else -gi
-                    t[i] = ti
+            # breakpoint of every coordinate along -g (Double.MaxValue where g_i = 0)
+            t = np.where(g < 0, (x - self.upper) / g, (x - self.lower) / g)
+            t = np.where(g == 0.0, np.finfo(np.float64).max, t)
+        d = np.where((g != 0.0) & (t != 0.0), -g, 0.0)
         p = W.T @ d
         c = np.zeros(M.shape[0])
         f1 = np.float64(g @ d)
@@ -101,8 +95,9 @@ class LBFGSB:
         with np.errstate(divide="ignore", invalid="ignore"):
             dt_min = -(f1 / f2)
         old_t = 0.0
-        order = sorted(range(n), key=lambda k: t[k])  # (a stable sort, as Scala's sortWith)
-        i = next(j for j, k in enumerate(order) if t[k] != 0.0)
+        order = np.argsort(t, kind="stable")  # (a stable sort, as Scala's sortWith)
+        nz = np.nonzero(t[order] != 0.0)[0]
+        i = int(nz[0])  # (Breeze: indexWhere(t != 0))
         b = order[i]
         min_t = t[b]
         delta_t = min_t - old_t
@@ -127,9 +122,8 @@ class LBFGSB:
                 delta_t = min_t - old_t
         dt_min = max(dt_min, 0.0)
         old_t += dt_min
-        for j in range(i, n):
-            k = order[j]
-            xc[k] = x[k] + old_t * d[k]
+        rest = order[i:]
+        xc[rest] = x[rest] + old_t * d[rest]
         c = c + p * dt_min
         return xc, c
 
