@@ -8,32 +8,39 @@ Double.MinPositiveValue) and memory 10: :class:`.lbfgsb.LBFGSB` reproduces that 
 algorithm -- generalized Cauchy point, direct primal subspace minimization, strong-Wolfe search
 on the unprojected ray, Breeze's convergence checks -- so iteration counts and
 ``objectiveHistory`` follow it.  Each evaluation is one fused device pass
-(``kernels.huber_pass``: margin -> loss/multipliers, then Xᵀm) plus one all-reduce of d+4 f64;
-the optimizer's O(k m) bookkeeping runs on the host between passes.
+(``kernels.huber_pass``: margin -> loss/multipliers, then Xᵀm) plus one all-reduce of d+4 f64.
+
+On GPU data the optimizer runs on the device too (``ops/csrc/hip/huber_qn.hip``, the same
+algorithm as :class:`.lbfgsb.LBFGSB`): the row pass reads its trial point from HBM, a one-block
+control kernel consumes the all-reduced evaluation and writes the next trial, and the host only
+enqueues -- no read per evaluation, so with ``dq4ml.fit.async`` the fit returns before the device
+has run it and the model resolves on first read.  The host-steered optimizer below stays the path
+for CPU data, checkpointed fits (``dq4ml.lbfgs.checkpointDir``) and the cases the device hands
+back (empty data, history capacity).
 """
 from __future__ import annotations
 
 import numpy as np
+import torch
 
-from ..ops import kernels
+from ..ops import kernels, native
 from ..parallel import comm
+from ..runtime.checks import verify
+from ..utils import tracing
 from ..utils.logging import get_logger
 from .lbfgsb import LBFGSB, LBFGSBState
 from .linalg import DenseVector
-from .optim import GramStats
+from .optim import GramStats, WLSModel
 
 log = get_logger("huber")
 MIN_SIGMA = 5e-324  # Double.MinPositiveValue: Spark's lower bound of σ
 _DMAX = float(np.finfo(np.float64).max)
 
 
-def train_huber(est, df, tbl, X, y, w, sel, d):
+def train_huber(est, df, tbl, X, y, w, sel, d, checks=(), device=True):
     from .lbfgs_path import _sample_moments
-    from .regression import LinearRegressionModel, LinearRegressionTrainingSummary
+    from .regression import LinearRegressionModel, LinearRegressionTrainingSummary, _async_conf, _async_model
 
-    flat = comm.all_reduce_sum(kernels.gram_stats(X.values, y.values, w, sel, "fp64"))
-    stats = GramStats.from_flat(flat.cpu().numpy(), d)
-    _, sx, _, _, _, _, _ = _sample_moments(stats)
     fit_icpt = bool(est.getOrDefault("fitIntercept"))
     eps = float(est.getOrDefault("epsilon"))
     reg, enet = float(est.getOrDefault("regParam")), float(est.getOrDefault("elasticNetParam"))
@@ -41,12 +48,50 @@ def train_huber(est, df, tbl, X, y, w, sel, d):
         raise ValueError("requirement failed: LinearRegression with huber loss only supports L2 regularization, "
                          "but got elasticNetParam = " + str(enet) + ".")
     std_flag = bool(est.getOrDefault("standardization"))
+    max_iter, tol = int(est.getOrDefault("maxIter")), float(est.getOrDefault("tol"))
+    flat = comm.all_reduce_sum(kernels.gram_stats(X.values, y.values, w, sel, "fp64"))
+    use_dev = device and _device_ok(df, X.values, d)
+    if comm.collectives_active():  # the two paths issue different collectives: one branch for all
+        use_dev = comm.all_agree(use_dev)
+    if use_dev:
+        from ..ops import device as dv
+
+        with tracing.span("solve"):
+            sxd, lamd = _device_moments(flat, d, reg, std_flag)
+            all_reduce = comm.all_reduce_sum if comm.collectives_active() else None
+            out, keep = dv.huber_fit_dp(X.values, y.values, w, sel, sxd, lamd, fit_icpt, eps, max_iter, tol, all_reduce)
+
+        def fallback():
+            return train_huber(est, df, tbl, X, y, w, sel, d, (), device=False)
+
+        pending = _PendingHuber(out, flat, d, checks, fallback)
+        pending._keep = keep
+        if _async_conf(df):
+            return _async_model(est, df, pending)
+        wls, stats = pending.resolve()
+        model = LinearRegressionModel(est.uid, DenseVector(wls.coefficients), float(wls.intercept), wls.scale)
+        est.copyValues(model)
+        model._set_summary(LinearRegressionTrainingSummary(model, df, None, wls.objectiveHistory, stats=stats,
+                                                           solver="l-bfgs-b"))
+        model._huber_evaluations = pending.evaluations
+        return model
+    verify(checks)
+    stats = GramStats.from_flat(flat.cpu().numpy(), d)
+    _, sx, _, _, _, _, _ = _sample_moments(stats)
     l2 = reg
     safe = np.where(sx == 0.0, 1.0, sx)
     lam = np.full(d, l2) if std_flag else np.where(sx != 0.0, l2 / (safe * safe), 0.0)
     dim = d + (2 if fit_icpt else 1)
 
+    cache = [None, None]  # Breeze CachedDiffFunction: the last point and its (f, g)
+
     def fg(theta):
+        if cache[0] is not None and np.array_equal(cache[0], theta):
+            return cache[1]
+        cache[0], cache[1] = np.array(theta, dtype=np.float64), _fg(theta)
+        return cache[1]
+
+    def _fg(theta):
         c = theta[:d]
         icpt = theta[d] if fit_icpt else 0.0
         sigma = theta[-1]
@@ -66,7 +111,6 @@ def train_huber(est, df, tbl, X, y, w, sel, d):
     lower = np.full(dim, -_DMAX)
     lower[-1] = MIN_SIGMA
     upper = np.full(dim, _DMAX)
-    max_iter, tol = int(est.getOrDefault("maxIter")), float(est.getOrDefault("tol"))
     opt = LBFGSB(lower, upper, max_iter, 10, tol)
     ck = _Checkpoint.of(df, flat, (d, dim, fit_icpt, eps, reg, std_flag, max_iter, tol))
     resumed = ck.load() if ck is not None else None
@@ -90,7 +134,83 @@ def train_huber(est, df, tbl, X, y, w, sel, d):
     model = LinearRegressionModel(est.uid, DenseVector(coef), icpt, float(theta[-1]))
     est.copyValues(model)
     model._set_summary(LinearRegressionTrainingSummary(model, df, None, np.array(hist), stats=stats, solver="l-bfgs-b"))
+    # (a device fit's fallback hands these back to its pending result)
+    res = WLSModel(np.asarray(coef, dtype=np.float64), icpt, np.zeros(1), np.asarray(hist, dtype=np.float64),
+                   "l-bfgs-b")
+    res.scale = float(theta[-1])
+    model._wls_result, model._stats_result = res, stats
     return model
+
+
+def _ck_root(df) -> str:
+    sess = getattr(df, "sparkSession", None)
+    return sess.conf.get("dq4ml.lbfgs.checkpointDir", "") if sess is not None else ""
+
+
+def _device_ok(df, Xv, d) -> bool:
+    """The device optimizer runs GPU data without checkpoints or fault injection (the
+    host-steered loop owns both); ``dq4ml.huber.device=false`` turns it off."""
+    sess = getattr(df, "sparkSession", None)
+    if sess is not None and str(sess.conf.get("dq4ml.huber.device", "true")).lower() in ("0", "false", "no"):
+        return False
+    if _FAIL_AT_ITER is not None or _ck_root(df) or d < 1 or not kernels._on_gpu(Xv if torch.is_tensor(Xv) else Xv.buf):
+        return False
+    return native.hip_available()
+
+
+def _device_moments(flat: torch.Tensor, d: int, reg: float, std_flag: bool):
+    """Feature std (Spark's weighted unbiased variance) and the L2 weights, on the device, from
+    the all-reduced statistics -- the same elementwise expressions as ``_sample_moments``."""
+    W, W2 = flat[1], flat[2]
+    mx = flat[5:5 + d] / W
+    j = torch.arange(d, device=flat.device)
+    diag = flat[5 + 2 * d + j + j * (j + 1) // 2]
+    denom = W - W2 / W
+    var = torch.where(denom > 0, torch.clamp(diag - W * mx * mx, min=0.0) / denom, torch.zeros_like(mx))
+    sx = torch.sqrt(var)
+    safe = torch.where(sx == 0.0, torch.ones_like(sx), sx)
+    lam = torch.full_like(sx, reg) if std_flag else torch.where(sx != 0.0, reg / (safe * safe), torch.zeros_like(sx))
+    return sx.contiguous(), lam.contiguous()
+
+
+_WHY = {0: "projected step converged", 1: "max iterations", 2: "function values converged", 3: "gradient converged",
+        4: "search failed", -1: "history capacity"}
+
+
+class _PendingHuber:
+    """A device Huber fit (``huber_qn.hip``) enqueued on the current stream; ``resolve()`` reads
+    its output once.  Cases the device hands back (status != 0, empty data) re-run on the host-
+    steered optimizer, which owns Spark's behavior there."""
+
+    pending_fit = True
+
+    def __init__(self, out, flat, d, checks, fallback):
+        self.out, self.flat, self.d, self._checks, self._fallback = out, flat, d, list(checks), fallback
+        self._res = None
+        self.evaluations = None
+        self._done = torch.cuda.Event()
+        self._done.record()
+
+    def resolve(self):
+        if self._res is None:
+            torch.cuda.current_stream(self.out.device).wait_event(self._done)
+            host = self.out.cpu().numpy()
+            flat = self.flat.cpu().numpy()
+            self._keep = None
+            verify(self._checks)
+            d = self.d
+            stats = GramStats.from_flat(flat, d)
+            if int(host[d + 2]) != 0 or not stats.wSum > 0.0:
+                model = self._fallback()
+                self._res = (model._wls_result, model._stats_result)
+                return self._res
+            H, iters, self.evaluations = int(host[d + 4]), int(host[d + 5]), int(host[d + 6])
+            log.info("l-bfgs-b (huber, device) converged: %s after %d iterations, %d evaluations",
+                     _WHY.get(int(host[d + 3]), "?"), iters, self.evaluations)
+            res = WLSModel(host[:d].copy(), float(host[d]), np.zeros(1), host[d + 8:d + 8 + H].copy(), "l-bfgs-b")
+            res.scale = float(host[d + 1])
+            self._res = (res, stats)
+        return self._res
 
 
 _FAIL_AT_ITER = None  # tests: raise at this iteration (simulated crash between checkpoints)

@@ -69,9 +69,9 @@ def train_lbfgs(est, df, tbl, X, y, d):
     mode = str(sess.conf.get("dq4ml.lbfgs.mode", "passes")).lower() if sess is not None else "passes"
     if loss != "huber" and mode != "gram":
         return _train_passes(est, df, X, y, w, sel, d, checks)
+    if loss == "huber":  # (verifies the checks itself: its device path reads nothing at once)
+        return _train_huber(est, df, tbl, X, y, w, sel, d, checks)
     verify(checks)  # the host-steered paths read statistics at once anyway
-    if loss == "huber":
-        return _train_huber(est, df, tbl, X, y, w, sel, d)
     flat = kernels.gram_stats(X.values, y.values, w, sel, est.getOrDefault("gramDtype"))
     flat = comm.all_reduce_sum(flat)
     stats = GramStats.from_flat(flat.cpu().numpy(), d)
@@ -409,10 +409,10 @@ class _QNCheckpoint:
             os.remove(self.path)
 
 
-def _train_huber(est, df, tbl, X, y, w, sel, d):
+def _train_huber(est, df, tbl, X, y, w, sel, d, checks=()):
     from .huber import train_huber
 
-    return train_huber(est, df, tbl, X, y, w, sel, d)
+    return train_huber(est, df, tbl, X, y, w, sel, d, checks)
 
 
 _ = torch

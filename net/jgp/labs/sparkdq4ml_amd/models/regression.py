@@ -794,7 +794,7 @@ class LinearRegressionModel(_LRParams):
         self._coef_v = None if coefficients is None else (
             coefficients if isinstance(coefficients, Vector) else DenseVector(coefficients))
         self._icpt_v = _JavaFloat(intercept)
-        self.scale = scale
+        self._scale_v = scale
         self._summary = None
 
     def _materialize(self):
@@ -802,7 +802,18 @@ class LinearRegressionModel(_LRParams):
             wls, _ = self._pending.resolve()
             self._coef_v = DenseVector(np.asarray(wls.coefficients, dtype=np.float64))
             self._icpt_v = _JavaFloat(float(wls.intercept))
+            self._scale_v = float(getattr(wls, "scale", self._scale_v))  # (huber: sigma)
             self._pending = None
+
+    @property
+    def scale(self):
+        self._materialize()
+        return self._scale_v
+
+    @scale.setter
+    def scale(self, v):
+        self._materialize()
+        self._scale_v = v
 
     @property
     def _coefficients(self) -> Vector:

@@ -376,6 +376,32 @@ PYBIND11_MODULE(_dq4ml_hip, m) {
                P<const uint8_t>(sel), P<const double>(ceff), icpt, sigma, eps, P<double>(mult), P<double>(partials),
                P<double>(out), as_stream(stream));
   });
+  m.def("huber_pass_dev", [](uintptr_t X, int xdt, int64_t ld, int d, int64_t n, int tiled, uintptr_t y, int ydt,
+                             uintptr_t w, int wdt, uintptr_t sel, uintptr_t trial, uintptr_t act, double eps,
+                             uintptr_t scale, uintptr_t shift, uintptr_t mult, uintptr_t partials, uintptr_t out,
+                             uintptr_t stream) {
+    huber_pass_dev(P<const void>(X), xdt, ld, d, n, tiled, P<const void>(y), ydt, P<const void>(w), wdt,
+                   P<const uint8_t>(sel), P<const double>(trial), P<const int>(act), eps, P<const double>(scale),
+                   P<const double>(shift), P<double>(mult), P<double>(partials), P<double>(out), as_stream(stream));
+  });
+  m.def("huber_qn_work", &huber_qn_work);
+  m.def("huber_qn_out", &huber_qn_out);
+  m.attr("HUBER_EVAL") = kHuberEval;
+  m.attr("HUBER_DONE") = kHuberDone;
+  m.def("huber_qn_init", [](int d, bool fit_icpt, int max_iter, double tol, int hist_cap, uintptr_t sx, uintptr_t lam,
+                            uintptr_t scale, uintptr_t shift, uintptr_t work, uintptr_t trial, uintptr_t out,
+                            uintptr_t stream) {
+    huber_qn_init(d, fit_icpt, max_iter, tol, hist_cap, P<const double>(sx), P<const double>(lam),
+                  P<const double>(scale), P<const double>(shift), P<double>(work), P<double>(trial), P<double>(out),
+                  as_stream(stream));
+  });
+  m.def("huber_qn_ctl", [](int d, bool fit_icpt, int max_iter, double tol, int hist_cap, uintptr_t sx, uintptr_t lam,
+                           uintptr_t scale, uintptr_t shift, uintptr_t work, uintptr_t trial, uintptr_t red,
+                           uintptr_t out, uintptr_t stream) {
+    huber_qn_ctl(d, fit_icpt, max_iter, tol, hist_cap, P<const double>(sx), P<const double>(lam),
+                 P<const double>(scale), P<const double>(shift), P<double>(work), P<double>(trial),
+                 P<const double>(red), P<double>(out), as_stream(stream));
+  });
   // ---- K9: squared-loss l-bfgs evaluation passes ----------------------------------------------
   auto lsqx = [](uintptr_t X, int layout, int xdt, int64_t ld, int d, int64_t n) {
     LsqX x{};

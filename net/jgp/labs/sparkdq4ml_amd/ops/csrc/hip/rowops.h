@@ -4,6 +4,8 @@
 
 #include <cstdint>
 
+#include "huber_qn.h"
+
 namespace dq4ml {
 
 struct PackSrc {
@@ -35,6 +37,14 @@ void regression_metrics(const void* X, int xdt, int64_t ld, int d, int64_t n, co
 void huber_pass(const void* X, int xdt, int64_t ld, int d, int64_t n, int tiled, const void* y, int ydt,
                 const void* w, int wdt, const uint8_t* sel, const double* ceff, double icpt, double sigma, double eps,
                 double* mult, double* partials, double* out, hipStream_t st);
+
+// the same pass steered by the device l-bfgs-b (huber_qn.hip): trial = [c_eff * scale (d) | intercept
+// (shift folded in) | sigma], skipped when *act != kHuberEval; out[4 + j] gets the fp8 scale and the
+// storage shift applied (either may be null)
+void huber_pass_dev(const void* X, int xdt, int64_t ld, int d, int64_t n, int tiled, const void* y, int ydt,
+                    const void* w, int wdt, const uint8_t* sel, const double* trial, const int* act, double eps,
+                    const double* scale, const double* shift, double* mult, double* partials, double* out,
+                    hipStream_t st);
 
 // a bounded stand-in for a collective's channel blocks (diagnostics): blocks x 256 threads, usec each
 void standin(int blocks, int usec, hipStream_t st);

@@ -498,7 +498,15 @@ __global__ __launch_bounds__(256) void huber_rows_kernel(const void* __restrict_
                                                         const uint8_t* __restrict__ sel,
                                                         const double* __restrict__ ceff /* c_j/σ_j */,
                                                         double icpt, double sigma, double eps,
-                                                        double* __restrict__ mult, double* __restrict__ partials) {
+                                                        double* __restrict__ mult, double* __restrict__ partials,
+                                                        const int* __restrict__ act) {
+  // device-steered form (huber_qn.hip): ceff = the trial [c_eff (d) | intercept | sigma] in HBM,
+  // skipped once the optimizer is done (act != kHuberEval)
+  if (act != nullptr) {
+    if (*act != kHuberEval) return;
+    icpt = ceff[d];
+    sigma = ceff[d + 1];
+  }
   double acc[4] = {0, 0, 0, 0};
   for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
     double m = 0.0;
@@ -539,7 +547,10 @@ __global__ __launch_bounds__(256) void huber_rows_kernel(const void* __restrict_
 
 // phase B: out[j] = Σ_r X[j][r] * v[r]   (one block per feature, fixed-order reduction)
 __global__ __launch_bounds__(256) void xt_vec_kernel(const void* __restrict__ X, int xdt, int64_t ld, int d, int64_t n,
-                                                    int tiled, const double* __restrict__ v, double* __restrict__ out) {
+                                                    int tiled, const double* __restrict__ v, double* __restrict__ out,
+                                                    const int* __restrict__ act, const double* __restrict__ scale,
+                                                    const double* __restrict__ shift) {
+  if (act != nullptr && *act != kHuberEval) return;
   const int j = blockIdx.x;
   const int NT = (d + 31) >> 5;
   double s = 0.0;
@@ -555,7 +566,14 @@ __global__ __launch_bounds__(256) void xt_vec_kernel(const void* __restrict__ X,
   s = wave_sum_f64(s);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
   __syncthreads();
-  if (threadIdx.x == 0) out[j] = red[0] + red[1] + red[2] + red[3];
+  if (threadIdx.x == 0) {
+#pragma clang fp contract(off)  // two roundings each, as the host-steered fold's torch expressions
+    double t = red[0] + red[1] + red[2] + red[3];
+    // fp8 storage q = x / scale; shifted storage x = x' + s: Σ m x = Σ m x' + s Σ m (out[-2] = Σ m)
+    if (scale != nullptr) t *= scale[j];
+    if (shift != nullptr) t += shift[j] * out[-2];
+    out[j] = t;
+  }
 }
 
 }  // namespace
@@ -565,9 +583,24 @@ void huber_pass(const void* X, int xdt, int64_t ld, int d, int64_t n, int tiled,
                 double* mult, double* partials, double* out /* [4 + d] */, hipStream_t st) {
   const int g = metrics_blocks(n);
   hipLaunchKernelGGL(huber_rows_kernel, dim3(g), dim3(256), 0, st, X, xdt, ld, d, n, tiled, y, ydt, w, wdt, sel, ceff,
-                     icpt, sigma, eps, mult, partials);
+                     icpt, sigma, eps, mult, partials, nullptr);
   hipLaunchKernelGGL(sum_slabs_kernel, dim3(1), dim3(256), 0, st, partials, g, 4, out);
-  hipLaunchKernelGGL(xt_vec_kernel, dim3(d), dim3(256), 0, st, X, xdt, ld, d, n, tiled, mult, out + 4);
+  hipLaunchKernelGGL(xt_vec_kernel, dim3(d), dim3(256), 0, st, X, xdt, ld, d, n, tiled, mult, out + 4, nullptr,
+                     nullptr, nullptr);
+  DQ_HIP_CHECK(hipGetLastError());
+}
+
+void huber_pass_dev(const void* X, int xdt, int64_t ld, int d, int64_t n, int tiled, const void* y, int ydt,
+                    const void* w, int wdt, const uint8_t* sel, const double* trial, const int* act, double eps,
+                    const double* scale, const double* shift, double* mult, double* partials, double* out,
+                    hipStream_t st) {
+  if (act == nullptr || trial == nullptr) throw std::invalid_argument("huber_pass_dev: trial and act are required");
+  const int g = metrics_blocks(n);
+  hipLaunchKernelGGL(huber_rows_kernel, dim3(g), dim3(256), 0, st, X, xdt, ld, d, n, tiled, y, ydt, w, wdt, sel,
+                     trial, 0.0, 1.0, eps, mult, partials, act);
+  hipLaunchKernelGGL(sum_slabs_kernel, dim3(1), dim3(256), 0, st, partials, g, 4, out);
+  hipLaunchKernelGGL(xt_vec_kernel, dim3(d), dim3(256), 0, st, X, xdt, ld, d, n, tiled, mult, out + 4, act, scale,
+                     shift);
   DQ_HIP_CHECK(hipGetLastError());
 }
 

@@ -725,6 +725,77 @@ def huber_pass(X, y, w, sel, ceff, icpt, sigma, eps):
     return out
 
 
+def huber_fit_dp(X, y, w, sel, sx: torch.Tensor, lam: torch.Tensor, fit_icpt: bool, eps: float, max_iter: int,
+                 tol: float, all_reduce=None, batch: int = 4):
+    """The Huber fit with the L-BFGS-B state on the device (``huber_qn.hip``): per evaluation the
+    row pass over THIS rank's rows at the trial the control kernel wrote (``huber_pass_dev``), the
+    all-reduce of its (d + 4) f64 (``all_reduce``: in place on the current stream, or None on one
+    rank), then the control kernel.  ``sx`` / ``lam``: f64 device vectors (feature std, L2
+    weights).  Nothing is read back per evaluation: evaluations are enqueued ``batch`` at a time,
+    at most two batches ahead of the device, until a pinned copy of the control word reads done.
+    Returns the output block ``[coef (d) | intercept | scale | status | why | states | iterations |
+    evaluations | - | history]`` (status 9: evaluation bound reached, 2: history capacity) and
+    the workspaces the enqueued kernels use (keep them alive until the output is read)."""
+    import time
+
+    h = native.hip()
+    d, n = X.shape
+    d, n = int(d), int(n)
+    Xb, xdt, ld, tiled = _x_args(X)
+    _check_dev(Xb, y, w, sel)
+    y, w, sel = _prep_rows(y, w, sel, n)
+    dev = Xb.device
+    if sx.numel() != d or lam.numel() != d:
+        raise ValueError("huber_fit_dp: sx / lam must hold d values")
+    sx = sx.to(device=dev, dtype=torch.float64).contiguous()
+    lam = lam.to(device=dev, dtype=torch.float64).contiguous()
+    scale = X.scales.to(torch.float64).contiguous() if isinstance(X, TiledWide) and X.eb == 8 else None
+    sh = getattr(X, "shift", None)
+    shift = None if sh is None else sh.dev64.to(dev).contiguous()
+    cap = wls_qn_cap(max_iter)
+    work = torch.zeros(int(h.huber_qn_work(d, bool(fit_icpt))), dtype=torch.float64, device=dev)
+    act = work[:1].view(torch.int32)[:1]  # HCtl.act: the struct's first word
+    trial = torch.zeros(d + 2, dtype=torch.float64, device=dev)
+    red = torch.zeros(4 + d, dtype=torch.float64, device=dev)
+    nb = int(h.metrics_blocks(n))
+    mult = torch.empty(max(n, 1), dtype=torch.float64, device=dev)
+    partials = torch.empty(nb * 4, dtype=torch.float64, device=dev)
+    out = torch.zeros(int(h.huber_qn_out(d, cap)), dtype=torch.float64, device=dev)
+    out[d + 2:d + 3].fill_(9.0)
+    st = _stream()
+    qn = (d, bool(fit_icpt), int(max_iter), float(tol), cap, sx.data_ptr(), lam.data_ptr(), _ptr(scale), _ptr(shift),
+          work.data_ptr(), trial.data_ptr())
+    rows = (Xb.data_ptr(), xdt, int(ld), d, n, tiled, y.data_ptr(), dtype_code(y), _ptr(w),
+            dtype_code(w) if w is not None else 0, _ptr(sel), trial.data_ptr(), act.data_ptr(), float(eps),
+            _ptr(scale), _ptr(shift), mult.data_ptr(), partials.data_ptr(), red.data_ptr(), st)
+    h.huber_qn_init(*qn, out.data_ptr(), st)
+    # a loop pass costs at most 1 + 64 + 64 + 1 evaluations (bracket, zoom, projected point)
+    bound = cap * 130 + 2
+    flags = torch.empty(2, dtype=torch.int32, pin_memory=True)
+    inflight = []
+    done, k, slot = False, 0, 0
+    while not done and k < bound:
+        for _ in range(min(batch, bound - k)):
+            h.huber_pass_dev(*rows)
+            if all_reduce is not None:
+                r = all_reduce(red)
+                if r.data_ptr() != red.data_ptr():  # (gloo reduces a host copy)
+                    red.copy_(r)
+            h.huber_qn_ctl(*qn, red.data_ptr(), out.data_ptr(), st)
+            k += 1
+        flags[slot].copy_(act[0], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        inflight.append((ev, slot))
+        slot ^= 1
+        if len(inflight) == 2:
+            ev0, s0 = inflight.pop(0)
+            while not ev0.query():
+                time.sleep(20e-6)
+            done = int(flags[s0]) == int(h.HUBER_DONE)
+    return out, (work, trial, red, mult, partials, sx, lam, scale, shift, flags, y, w, sel)
+
+
 # ------------------------------------------------------------------------------------------
 # K9 -- squared-loss l-bfgs evaluation passes (lsq.hip)
 class LsqPasses:
