@@ -32,7 +32,7 @@ namespace dq4ml {
 
 namespace {
 
-constexpr int kT = 1024;
+constexpr int kT = 256;
 constexpr int kW = kT / 64;
 constexpr int kM = 10;  // Spark's LBFGSB memory
 constexpr int kFv = 20;
@@ -63,6 +63,7 @@ struct HArgs {
 struct HV {
   HCtl* C;
   double *x, *g, *dir, *xe, *ge, *xc, *tb, *dd, *done, *S, *Y, *M;
+  double* Ms;  // M in LDS (the control kernel loads it once)
 };
 
 constexpr int64_t kCtlDoubles = (int64_t)((sizeof(HCtl) + 7) / 8);
@@ -95,7 +96,7 @@ __device__ __forceinline__ double wsum(double v) {
 }
 
 // every thread gets the block-wide sum (fixed order)
-__device__ double bsum(double v, double* red) {
+__device__ __forceinline__ double bsum(double v, double* red) {
   v = wsum(v);
   __syncthreads();
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
@@ -119,7 +120,7 @@ __device__ __forceinline__ double wrow(const HV& v, const HCtl& C, int n, int i,
 }
 
 // the trial point of the next pass: theta -> scaled effective coefficients, intercept, sigma
-__device__ void write_trial(const HArgs& a, const double* th, double* red) {
+__device__ __forceinline__ void write_trial(const HArgs& a, const double* th, double* red) {
   const int d = a.d;
   double sd = 0.0;
   for (int j = threadIdx.x; j < d; j += kT) {
@@ -135,7 +136,7 @@ __device__ void write_trial(const HArgs& a, const double* th, double* red) {
 }
 
 // the evaluation in red at xe -> (f, ge)
-__device__ double eval_of(const HArgs& a, const HV& v, double* red) {
+__device__ __forceinline__ double eval_of(const HArgs& a, const HV& v, double* red) {
   const int d = a.d;
   const double W = a.red[1];
   double reg = 0.0;
@@ -154,7 +155,7 @@ __device__ double eval_of(const HArgs& a, const HV& v, double* red) {
   return a.red[0] / W + 0.5 * reg;
 }
 
-__device__ int converged(const HArgs& a, const HV& v, const HCtl& C, double* red) {
+__device__ __forceinline__ int converged(const HArgs& a, const HV& v, const HCtl& C, double* red) {
   double pm = 0.0, gg = 0.0;
   for (int i = threadIdx.x; i < a.dim; i += kT) {
     pm = fmax(pm, fabs(clampb(a, i, v.x[i] - v.g[i]) - v.x[i]));
@@ -180,75 +181,105 @@ __device__ int converged(const HArgs& a, const HV& v, const HCtl& C, double* red
   return -1;
 }
 
-// M = inv(MM) of the current history (thread 0; S^T Y and S^T S by block sums first)
-__device__ void rebuild_m(const HArgs& a, const HV& v, HCtl& C, double* red, double* sh) {
-  const int n = a.dim, h = C.hh, m2 = 2 * h;
+// Wave-parallel dot products: wave w takes pairs w, w + kW, ... (lanes stride the n coordinates,
+// then a fixed-order wave sum); `put(pair, value)` runs on lane 0.  No block barrier inside.
+template <class F, class P>
+__device__ __forceinline__ void wave_dots(int npairs, int n, F term, P put) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  for (int q = wave; q < npairs; q += kW) {
+    double s = 0.0;
+    for (int e = lane; e < n; e += 64) s += term(q, e);
+    s = wsum(s);
+    if (lane == 0) put(q, s);
+  }
+}
+
+// M = inv(MM) of the current history: S^T Y and S^T S by wave dot products, then Gauss-Jordan
+// with partial pivoting on [MM | I] in LDS, row operations spread over the block (each element
+// takes the same operations in the same order as the one-thread elimination)
+__device__ __forceinline__ void rebuild_m(const HArgs& a, const HV& v, HCtl& C, double* sh) {
+  const int n = a.dim, h = C.hh, m2 = 2 * h, w2 = 2 * m2;
   double* A = sh;            // [h][h] S^T Y
   double* SS = sh + kM * kM;  // [h][h] S^T S
-  for (int i = 0; i < h; ++i)
-    for (int j = 0; j < h; ++j) {
-      double sy = 0.0, ss = 0.0;
-      for (int e = threadIdx.x; e < n; e += kT) {
-        sy += v.S[(int64_t)i * n + e] * v.Y[(int64_t)j * n + e];
-        ss += v.S[(int64_t)i * n + e] * v.S[(int64_t)j * n + e];
-      }
-      sy = bsum(sy, red);
-      ss = bsum(ss, red);
-      if (threadIdx.x == 0) A[i * kM + j] = sy, SS[i * kM + j] = ss;
-    }
+  double* T = sh + 2 * kM * kM;  // [m2][2 m2] augmented [MM | I]
+  __shared__ double fac[2 * kM];
+  __shared__ int s_piv;
+  wave_dots(h * h, n,
+            [&](int q, int e) {
+              const int i = q / h, j = q % h;
+              return v.S[(int64_t)i * n + e] * v.Y[(int64_t)j * n + e];
+            },
+            [&](int q, double s) { A[(q / h) * kM + q % h] = s; });
+  wave_dots(h * h, n,
+            [&](int q, int e) {
+              const int i = q / h, j = q % h;
+              return v.S[(int64_t)i * n + e] * v.S[(int64_t)j * n + e];
+            },
+            [&](int q, double s) { SS[(q / h) * kM + q % h] = s; });
   __syncthreads();
-  if (threadIdx.x == 0) {
-    double* T = sh + 2 * kM * kM;  // [m2][2 m2] augmented [MM | I]
-    const int w2 = 2 * m2;
-    for (int r = 0; r < m2; ++r)
-      for (int c = 0; c < w2; ++c) {
-        double val;
-        if (c >= m2) {
-          val = (c - m2 == r) ? 1.0 : 0.0;
-        } else if (r < h && c < h) {
-          val = r == c ? -A[r * kM + r] : 0.0;  // -D
-        } else if (r < h) {
-          const int cc = c - h;                 // L^T: (r, cc) = L[cc][r] = A[cc][r] if cc > r
-          val = cc > r ? A[cc * kM + r] : 0.0;
-        } else if (c < h) {
-          const int rr = r - h;                 // L: A[rr][c] if rr > c
-          val = rr > c ? A[rr * kM + c] : 0.0;
-        } else {
-          val = SS[(r - h) * kM + (c - h)] * C.theta;
-        }
-        T[r * w2 + c] = val;
-      }
-    for (int col = 0; col < m2; ++col) {  // Gauss-Jordan, partial pivoting
+  for (int e = threadIdx.x; e < m2 * w2; e += kT) {
+    const int r = e / w2, c = e % w2;
+    double val;
+    if (c >= m2) {
+      val = (c - m2 == r) ? 1.0 : 0.0;
+    } else if (r < h && c < h) {
+      val = r == c ? -A[r * kM + r] : 0.0;  // -D
+    } else if (r < h) {
+      const int cc = c - h;                 // L^T: (r, cc) = L[cc][r] = A[cc][r] if cc > r
+      val = cc > r ? A[cc * kM + r] : 0.0;
+    } else if (c < h) {
+      const int rr = r - h;                 // L: A[rr][c] if rr > c
+      val = rr > c ? A[rr * kM + c] : 0.0;
+    } else {
+      val = SS[(r - h) * kM + (c - h)] * C.theta;
+    }
+    T[e] = val;
+  }
+  __syncthreads();
+  for (int col = 0; col < m2; ++col) {
+    if (threadIdx.x == 0) {
       int piv = col;
       for (int r = col + 1; r < m2; ++r)
         if (fabs(T[r * w2 + col]) > fabs(T[piv * w2 + col])) piv = r;
-      if (piv != col)
-        for (int c = 0; c < w2; ++c) {
-          const double tmp = T[col * w2 + c];
-          T[col * w2 + c] = T[piv * w2 + c];
-          T[piv * w2 + c] = tmp;
-        }
-      const double pv = T[col * w2 + col];
-      for (int c = 0; c < w2; ++c) T[col * w2 + c] /= pv;
-      for (int r = 0; r < m2; ++r) {
-        if (r == col) continue;
-        const double f = T[r * w2 + col];
-        if (f == 0.0) continue;
-        for (int c = 0; c < w2; ++c) T[r * w2 + c] -= f * T[col * w2 + c];
-      }
+      s_piv = piv;
     }
-    for (int r = 0; r < m2; ++r)
-      for (int c = 0; c < m2; ++c) v.M[r * (2 * kM) + c] = T[r * w2 + m2 + c];
+    __syncthreads();
+    const int piv = s_piv;
+    if (piv != col)
+      for (int c = threadIdx.x; c < w2; c += kT) {
+        const double t0 = T[col * w2 + c];
+        T[col * w2 + c] = T[piv * w2 + c];
+        T[piv * w2 + c] = t0;
+      }
+    __syncthreads();
+    if (threadIdx.x < m2) fac[threadIdx.x] = T[threadIdx.x * w2 + col];
+    __syncthreads();
+    for (int c = threadIdx.x; c < w2; c += kT) T[col * w2 + c] /= fac[col];
+    __syncthreads();
+    for (int e = threadIdx.x; e < m2 * w2; e += kT) {
+      const int r = e / w2;
+      if (r != col && fac[r] != 0.0) T[e] -= fac[r] * T[col * w2 + e % w2];
+    }
+    __syncthreads();
+  }
+  for (int e = threadIdx.x; e < m2 * m2; e += kT) {
+    const int r = e / m2, c = e % m2;
+    v.M[r * (2 * kM) + c] = v.Ms[r * (2 * kM) + c] = T[r * w2 + m2 + c];
   }
   __syncthreads();
 }
 
-__device__ __forceinline__ double mget(const HV& v, int r, int c) { return v.M[r * (2 * kM) + c]; }
+__device__ __forceinline__ double mget(const HV& v, int r, int c) { return v.Ms[r * (2 * kM) + c]; }
+
+// the elimination factor of row r at column col (forward elimination of the subspace system)
+__device__ __forceinline__ void fac_of(const double* NN, int r, int col, double* f) {
+  f[r] = NN[r * kM * 2 + col] / NN[col * kM * 2 + col];
+}
 
 // generalized Cauchy point (xc) and c; then the direction into v.dir.  Returns g . dir.
-__device__ double direction(const HArgs& a, const HV& v, HCtl& C, double* red, double* sh) {
+__device__ __forceinline__ double direction(const HArgs& a, const HV& v, HCtl& C, double* red, double* sh) {
   const int n = a.dim, m2 = 2 * C.hh;
-  __shared__ double p[2 * kM], c[2 * kM], tmp[2 * kM], tmp2[2 * kM];
+  __shared__ double p[2 * kM], c[2 * kM], tmp[2 * kM], tmp2[2 * kM], wb[2 * kM], rc3[3][2 * kM];
   __shared__ double s_f1, s_f2, s_dtmin, s_oldt;
   __shared__ int s_b;
   for (int i = threadIdx.x; i < n; i += kT) {
@@ -266,22 +297,20 @@ __device__ double direction(const HArgs& a, const HV& v, HCtl& C, double* red, d
     v.xc[i] = v.x[i];
   }
   __syncthreads();
-  for (int k = 0; k < m2; ++k) {
-    double s = 0.0;
-    for (int i = threadIdx.x; i < n; i += kT) s += wrow(v, C, n, i, k) * v.dd[i];
-    s = bsum(s, red);
-    if (threadIdx.x == 0) p[k] = s, c[k] = 0.0;
-  }
+  wave_dots(m2, n, [&](int k, int i) { return wrow(v, C, n, i, k) * v.dd[i]; },
+            [&](int k, double s) { p[k] = s, c[k] = 0.0; });
   double f1 = 0.0;
   for (int i = threadIdx.x; i < n; i += kT) f1 += v.g[i] * v.dd[i];
-  f1 = bsum(f1, red);
+  f1 = bsum(f1, red);  // (its barriers also publish p)
+  if (threadIdx.x < m2) {
+    double mp = 0.0;
+    for (int q = 0; q < m2; ++q) mp += mget(v, threadIdx.x, q) * p[q];
+    tmp[threadIdx.x] = mp;
+  }
+  __syncthreads();
   if (threadIdx.x == 0) {
     double pmp = 0.0;
-    for (int r = 0; r < m2; ++r) {
-      double mp = 0.0;
-      for (int q = 0; q < m2; ++q) mp += mget(v, r, q) * p[q];
-      pmp += p[r] * mp;
-    }
+    for (int r = 0; r < m2; ++r) pmp += p[r] * tmp[r];
     s_f1 = f1;
     s_f2 = -C.theta * f1 - pmp;
     s_dtmin = -(s_f1 / s_f2);
@@ -323,28 +352,34 @@ __device__ double direction(const HArgs& a, const HV& v, HCtl& C, double* red, d
     if (b < 0) break;
     const double min_t = v.tb[b], delta_t = min_t - s_oldt;
     const bool go = delta_t <= s_dtmin;
-    __syncthreads();  // every thread has read s_oldt / s_dtmin before thread 0 moves them
+    __syncthreads();  // every thread has read s_oldt / s_dtmin before they move
     if (!go) break;
+    if (threadIdx.x < m2) {
+      c[threadIdx.x] += p[threadIdx.x] * delta_t;
+      wb[threadIdx.x] = wrow(v, C, n, b, threadIdx.x);
+    }
+    __syncthreads();
+    if (threadIdx.x < m2) {  // rows of M c, M p, M wb
+      double mc = 0.0, mp = 0.0, mw = 0.0;
+      for (int q = 0; q < m2; ++q) {
+        const double mv = mget(v, threadIdx.x, q);
+        mc += mv * c[q];
+        mp += mv * p[q];
+        mw += mv * wb[q];
+      }
+      rc3[0][threadIdx.x] = mc, rc3[1][threadIdx.x] = mp, rc3[2][threadIdx.x] = mw;
+    }
+    __syncthreads();
     if (threadIdx.x == 0) {
       const double xb = v.dd[b] > 0.0 ? upper_of(a, b) : lower_of(a, b);
       v.xc[b] = xb;
       const double zb = xb - v.x[b];
-      for (int k = 0; k < m2; ++k) c[k] += p[k] * delta_t;
       const double gb = v.g[b];
       double wMc = 0.0, wMp = 0.0, wMw = 0.0;
-      for (int r = 0; r < m2; ++r) {
-        double mc = 0.0, mp = 0.0, mw = 0.0;
-        for (int q = 0; q < m2; ++q) {
-          mc += mget(v, r, q) * c[q];
-          mp += mget(v, r, q) * p[q];
-          mw += mget(v, r, q) * wrow(v, C, n, b, q);
-        }
-        const double wr = wrow(v, C, n, b, r);
-        wMc += wr * mc, wMp += wr * mp, wMw += wr * mw;
-      }
+      for (int r = 0; r < m2; ++r) wMc += wb[r] * rc3[0][r], wMp += wb[r] * rc3[1][r], wMw += wb[r] * rc3[2][r];
       s_f1 += delta_t * s_f2 + gb * gb + C.theta * gb * zb - gb * wMc;
       s_f2 += -1.0 * C.theta * gb * gb - 2.0 * (gb * wMp) - gb * gb * wMw;
-      for (int k = 0; k < m2; ++k) p[k] += wrow(v, C, n, b, k) * gb;
+      for (int k = 0; k < m2; ++k) p[k] += wb[k] * gb;
       v.dd[b] = 0.0;
       v.done[b] = 1.0;
       s_dtmin = -s_f1 / s_f2;
@@ -376,12 +411,11 @@ __device__ double direction(const HArgs& a, const HV& v, HCtl& C, double* red, d
   // subspace minimization over the free variables of the Cauchy point
   const double it = 1.0 / C.theta;
   // Mc, then r = g + theta (xc - x) - W (M c) on the free variables (kept in v.tb)
-  if (threadIdx.x == 0)
-    for (int r = 0; r < m2; ++r) {
-      double s = 0.0;
-      for (int q = 0; q < m2; ++q) s += mget(v, r, q) * c[q];
-      tmp[r] = s;
-    }
+  if (threadIdx.x < m2) {
+    double s = 0.0;
+    for (int q = 0; q < m2; ++q) s += mget(v, threadIdx.x, q) * c[q];
+    tmp[threadIdx.x] = s;
+  }
   __syncthreads();
   for (int i = threadIdx.x; i < n; i += kT) {
     const bool fr = v.xc[i] != upper_of(a, i) && v.xc[i] != lower_of(a, i);
@@ -392,61 +426,72 @@ __device__ double direction(const HArgs& a, const HV& v, HCtl& C, double* red, d
   }
   __syncthreads();
   // WZ rc and WZ WZ^T over the free variables
-  double* N = sh;  // [m2][m2]
-  for (int k = 0; k < m2; ++k) {
+  double* N = sh;             // [m2][2 kM]
+  double* NN = sh + 4 * kM * kM;  // [m2][2 kM]
+  wave_dots(m2, n, [&](int k, int i) { return v.done[i] != 0.0 ? wrow(v, C, n, i, k) * v.tb[i] : 0.0; },
+            [&](int k, double s) { tmp2[k] = s; });
+  wave_dots(m2 * m2, n,
+            [&](int q, int i) {
+              const int k = q / m2, l = q % m2;
+              return (l >= k && v.done[i] != 0.0) ? wrow(v, C, n, i, k) * wrow(v, C, n, i, l) : 0.0;
+            },
+            [&](int q, double s) {
+              const int k = q / m2, l = q % m2;
+              if (l >= k) N[k * kM * 2 + l] = s, N[l * kM * 2 + k] = s;
+            });
+  __syncthreads();
+  // v = M (WZ rc);  N = I - M (WZ WZ^T) / theta;  v = N \ v (partial pivoting)
+  __shared__ double vv[2 * kM];
+  __shared__ int s_piv;
+  if (threadIdx.x < m2) {
     double s = 0.0;
-    for (int i = threadIdx.x; i < n; i += kT)
-      if (v.done[i] != 0.0) s += wrow(v, C, n, i, k) * v.tb[i];
-    s = bsum(s, red);
-    if (threadIdx.x == 0) tmp2[k] = s;
-    for (int q = k; q < m2; ++q) {
-      double z = 0.0;
-      for (int i = threadIdx.x; i < n; i += kT)
-        if (v.done[i] != 0.0) z += wrow(v, C, n, i, k) * wrow(v, C, n, i, q);
-      z = bsum(z, red);
-      if (threadIdx.x == 0) N[k * kM * 2 + q] = z, N[q * kM * 2 + k] = z;
-    }
+    for (int q = 0; q < m2; ++q) s += mget(v, threadIdx.x, q) * tmp2[q];
+    vv[threadIdx.x] = s;
+  }
+  for (int e = threadIdx.x; e < m2 * m2; e += kT) {
+    const int r = e / m2, q = e % m2;
+    double z = 0.0;
+    for (int k = 0; k < m2; ++k) z += mget(v, r, k) * (N[k * kM * 2 + q] * it);
+    NN[r * kM * 2 + q] = (r == q ? 1.0 : 0.0) - z;
   }
   __syncthreads();
-  if (threadIdx.x == 0) {
-    // v = M (WZ rc);  N = I - M (WZ WZ^T) / theta;  v = N \\ v (partial pivoting)
-    double vv[2 * kM], NN[2 * kM][2 * kM];
-    for (int r = 0; r < m2; ++r) {
-      double s = 0.0;
-      for (int q = 0; q < m2; ++q) s += mget(v, r, q) * tmp2[q];
-      vv[r] = s;
-      for (int q = 0; q < m2; ++q) {
-        double z = 0.0;
-        for (int k = 0; k < m2; ++k) z += mget(v, r, k) * (N[k * kM * 2 + q] * it);
-        NN[r][q] = (r == q ? 1.0 : 0.0) - z;
-      }
-    }
-    for (int col = 0; col < m2; ++col) {
+  for (int col = 0; col < m2; ++col) {
+    if (threadIdx.x == 0) {
       int piv = col;
       for (int r = col + 1; r < m2; ++r)
-        if (fabs(NN[r][col]) > fabs(NN[piv][col])) piv = r;
-      if (piv != col) {
-        for (int q = 0; q < m2; ++q) {
-          const double t0 = NN[col][q];
-          NN[col][q] = NN[piv][q];
-          NN[piv][q] = t0;
-        }
+        if (fabs(NN[r * kM * 2 + col]) > fabs(NN[piv * kM * 2 + col])) piv = r;
+      s_piv = piv;
+    }
+    __syncthreads();
+    const int piv = s_piv;
+    if (piv != col) {
+      for (int q = threadIdx.x; q < m2; q += kT) {
+        const double t0 = NN[col * kM * 2 + q];
+        NN[col * kM * 2 + q] = NN[piv * kM * 2 + q];
+        NN[piv * kM * 2 + q] = t0;
+      }
+      if (threadIdx.x == 0) {
         const double t1 = vv[col];
         vv[col] = vv[piv];
         vv[piv] = t1;
       }
-      for (int r = col + 1; r < m2; ++r) {
-        const double f = NN[r][col] / NN[col][col];
-        for (int q = col; q < m2; ++q) NN[r][q] -= f * NN[col][q];
-        vv[r] -= f * vv[col];
-      }
     }
+    __syncthreads();
+    if (threadIdx.x > col && threadIdx.x < m2) fac_of(NN, threadIdx.x, col, tmp);
+    __syncthreads();
+    for (int e = threadIdx.x; e < m2 * m2; e += kT) {
+      const int r = e / m2, q = e % m2;
+      if (r > col && q >= col) NN[r * kM * 2 + q] -= tmp[r] * NN[col * kM * 2 + q];
+    }
+    if (threadIdx.x > col && threadIdx.x < m2) vv[threadIdx.x] -= tmp[threadIdx.x] * vv[col];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
     for (int r = m2 - 1; r >= 0; --r) {
       double s = vv[r];
-      for (int q = r + 1; q < m2; ++q) s -= NN[r][q] * vv[q];
-      vv[r] = s / NN[r][r];
+      for (int q = r + 1; q < m2; ++q) s -= NN[r * kM * 2 + q] * vv[q];
+      vv[r] = s / NN[r * kM * 2 + r];
     }
-    for (int r = 0; r < m2; ++r) tmp[r] = vv[r];
   }
   __syncthreads();
   double gd = 0.0;
@@ -454,7 +499,7 @@ __device__ double direction(const HArgs& a, const HV& v, HCtl& C, double* red, d
     double sub = v.xc[i];
     if (v.done[i] != 0.0) {
       double wv = 0.0;
-      for (int k = 0; k < m2; ++k) wv += wrow(v, C, n, i, k) * tmp[k];
+      for (int k = 0; k < m2; ++k) wv += wrow(v, C, n, i, k) * vv[k];
       const double du = -(v.tb[i] * it + wv * (it * it));
       sub = v.xc[i] + du;  // findAlpha: 1.0
     }
@@ -465,7 +510,7 @@ __device__ double direction(const HArgs& a, const HV& v, HCtl& C, double* red, d
   return bsum(gd, red);
 }
 
-__device__ void record(const HArgs& a, HCtl& C) {
+__device__ __forceinline__ void record(const HArgs& a, HCtl& C) {
   if (C.H >= a.hist_cap) {
     C.overflow = 1;
     return;
@@ -475,7 +520,7 @@ __device__ void record(const HArgs& a, HCtl& C) {
 }
 
 // the output [coef(d) | intercept | scale | status | why | H | iter | nev | hist(H)]
-__device__ void finalize(const HArgs& a, const HV& v, HCtl& C) {
+__device__ __forceinline__ void finalize(const HArgs& a, const HV& v, HCtl& C) {
   const int d = a.d;
   for (int j = threadIdx.x; j < d; j += kT) a.out[j] = a.sx[j] != 0.0 ? v.x[j] / a.sx[j] : 0.0;
   if (threadIdx.x == 0) {
@@ -491,7 +536,7 @@ __device__ void finalize(const HArgs& a, const HV& v, HCtl& C) {
 }
 
 // the trial at x + t dir (the line search evaluates the UNPROJECTED ray)
-__device__ void set_trial(const HArgs& a, const HV& v, HCtl& C, double t, double* red) {
+__device__ __forceinline__ void set_trial(const HArgs& a, const HV& v, HCtl& C, double t, double* red) {
   for (int i = threadIdx.x; i < a.dim; i += kT) v.xe[i] = v.x[i] + v.dir[i] * t;
   __syncthreads();
   write_trial(a, v.xe, red);
@@ -502,7 +547,7 @@ __device__ void set_trial(const HArgs& a, const HV& v, HCtl& C, double t, double
 }
 
 // a FirstOrderException (line search failed / zoom failed / non-descent direction)
-__device__ bool fail(const HArgs& a, HCtl& C) {
+__device__ __forceinline__ bool fail(const HArgs& a, HCtl& C) {
   if (!C.failed_once) {
     C.failed_once = 1;
     C.hh = 0;
@@ -513,7 +558,7 @@ __device__ bool fail(const HArgs& a, HCtl& C) {
   return true;
 }
 
-__device__ double interp(double at, double ad, double af, double bt, double bd, double bf) {
+__device__ __forceinline__ double interp(double at, double ad, double af, double bt, double bd, double bf) {
   const double d1 = ad + bd - 3.0 * (af - bf) / (at - bt);
   const double d2 = sqrt(d1 * d1 - ad * bd);
   const double mul = bt - at;
@@ -530,7 +575,7 @@ namespace {
 
 // state -> (convergence) -> the next direction and the first trial of its search, repeated while
 // the direction fails (memory reset, then search failed)
-__device__ void next_search(const HArgs& a, const HV& v, HCtl& C, double* red, double* sh) {
+__device__ __forceinline__ void next_search(const HArgs& a, const HV& v, HCtl& C, double* red, double* sh) {
   for (;;) {
     __syncthreads();
     if (threadIdx.x == 0) record(a, C);
@@ -563,7 +608,8 @@ __device__ void next_search(const HArgs& a, const HV& v, HCtl& C, double* red, d
 __global__ __launch_bounds__(kT) void huber_qn_init_kernel(HArgs a) {
   __shared__ double red[2 * kW];
   __shared__ HCtl C;
-  const HV v = views(a);
+  HV v = views(a);
+  v.Ms = nullptr;
   if (threadIdx.x == 0) {
     HCtl z = {};
     z.act = kHuberEval;
@@ -582,11 +628,14 @@ __global__ __launch_bounds__(kT) void huber_qn_init_kernel(HArgs a) {
 __global__ __launch_bounds__(kT) void huber_qn_ctl_kernel(HArgs a) {
   __shared__ double red[2 * kW];
   __shared__ double sh[4 * kM * kM + 2 * kM * 4 * kM];
+  __shared__ double Ms[4 * kM * kM];
   __shared__ HCtl C;
-  const HV v = views(a);
+  HV v = views(a);
+  v.Ms = Ms;
   if (threadIdx.x == 0) C = *v.C;
   __syncthreads();
   if (C.act != kHuberEval) return;  // done: evaluations enqueued past the end
+  for (int e = threadIdx.x; e < 4 * kM * kM; e += kT) Ms[e] = v.M[e];
   const double f = eval_of(a, v, red);
   double dd = 0.0;
   for (int i = threadIdx.x; i < a.dim; i += kT) dd += v.ge[i] * v.dir[i];
@@ -721,7 +770,7 @@ __global__ __launch_bounds__(kT) void huber_qn_ctl_kernel(HArgs a) {
       C.theta = yy / sy;
     }
     __syncthreads();
-    rebuild_m(a, v, C, red, sh);
+    rebuild_m(a, v, C, sh);
   }
   for (int i = threadIdx.x; i < n; i += kT) v.x[i] = v.xe[i], v.g[i] = v.ge[i];
   if (threadIdx.x == 0) {

@@ -384,6 +384,7 @@ PYBIND11_MODULE(_dq4ml_hip, m) {
                    P<const uint8_t>(sel), P<const double>(trial), P<const int>(act), eps, P<const double>(scale),
                    P<const double>(shift), P<double>(mult), P<double>(partials), P<double>(out), as_stream(stream));
   });
+  m.def("huber_partials", &huber_partials);
   m.def("huber_qn_work", &huber_qn_work);
   m.def("huber_qn_out", &huber_qn_out);
   m.attr("HUBER_EVAL") = kHuberEval;

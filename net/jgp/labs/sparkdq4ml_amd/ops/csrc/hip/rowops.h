@@ -33,7 +33,9 @@ void regression_metrics(const void* X, int xdt, int64_t ld, int d, int64_t n, co
                         const uint8_t* sel, const double* coef, double b, double shift, double* partials,
                         double* out, hipStream_t st, int tiled);
 
-// K9 huber: out = [lossSum, weightSum, g_intercept, g_sigma, Σ_r m_r x_jr (d)]
+// K9 huber: out = [lossSum, weightSum, g_intercept, g_sigma, Σ_r m_r x_jr (d)]; `partials` holds
+// huber_partials(n, d) doubles, `mult` n (used for d > 16 only)
+int64_t huber_partials(int64_t n, int d);
 void huber_pass(const void* X, int xdt, int64_t ld, int d, int64_t n, int tiled, const void* y, int ydt,
                 const void* w, int wdt, const uint8_t* sel, const double* ceff, double icpt, double sigma, double eps,
                 double* mult, double* partials, double* out, hipStream_t st);

@@ -490,8 +490,44 @@ void regression_metrics(const void* X, int xdt, int64_t ld, int d, int64_t n, co
 namespace dq4ml {
 namespace {
 
-// phase A: per row margin -> loss, per-row gradient multiplier m_r (coefficient of x_j/σ_j),
-// intercept and σ gradient contributions; 5 block partials: loss, wsum, g_icpt, g_sigma, count
+__device__ __forceinline__ double load_x(const void* X, int xdt, int64_t ld, int d, int f, int64_t r, int tiled) {
+  if (tiled == 1) return (double)bf16_bits_to_f32(reinterpret_cast<const uint16_t*>(X)[tiled_offset(f, r, (d + 31) >> 5)]);
+  if (tiled == 2)
+    return (double)bf16_bits_to_f32(reinterpret_cast<const uint16_t*>(X)[wide_offset(f, r, ((d + 255) >> 8) * 8)]);
+  if (tiled == 3)
+    return (double)fp8_to_f32(reinterpret_cast<const uint8_t*>(X)[wide_offset_fp8(f, r, ((d + 255) >> 8) * 8)]);
+  return ld_f64(X, xdt, (int64_t)f * ld + r);
+}
+
+// One row's Huber terms (Spark HuberAggregator): loss, the gradient multiplier m_r of x_r (the
+// coefficient of x_j / σ_j), the intercept and σ contributions.
+__device__ __forceinline__ double huber_row(double lin, double wt, double sigma, double eps, double acc[4]) {
+  double m;
+  if (fabs(lin) <= sigma * eps) {
+    const double q = lin / sigma;
+    acc[0] += 0.5 * wt * (sigma + lin * lin / sigma);
+    m = -wt * q;
+    acc[2] += -wt * q;
+    acc[3] += 0.5 * wt * (1.0 - q * q);
+  } else {
+    const double sgn = lin >= 0 ? -1.0 : 1.0;
+    acc[0] += 0.5 * wt * (sigma + 2.0 * eps * fabs(lin) - sigma * eps * eps);
+    m = wt * sgn * eps;
+    acc[2] += wt * sgn * eps;
+    acc[3] += 0.5 * wt * (1.0 - eps * eps);
+  }
+  acc[1] += wt;
+  return m;
+}
+
+// The Huber pass over rows.  D > 0 (d <= D): fused -- after a row's margin each thread adds
+// m_r x_r (the row's features again, from cache) into D per-thread sums: one block partial of
+// 4 + d values (loss, W, g_b, g_sigma, Σ m x), the features read from HBM once.  D = 0: the margin pass only
+// (4 partials + the multipliers in `mult`), Xᵀm by xt_part_kernel.
+//
+// Device-steered form (huber_qn.hip): `act` non-null -> ceff = the trial [c_eff (d) | intercept |
+// sigma] in HBM, and the pass is skipped once the optimizer is done (act != kHuberEval).
+template <int D>
 __global__ __launch_bounds__(256) void huber_rows_kernel(const void* __restrict__ X, int xdt, int64_t ld, int d,
                                                         int64_t n, int tiled, const void* __restrict__ y, int ydt,
                                                         const void* __restrict__ w, int wdt,
@@ -500,93 +536,222 @@ __global__ __launch_bounds__(256) void huber_rows_kernel(const void* __restrict_
                                                         double icpt, double sigma, double eps,
                                                         double* __restrict__ mult, double* __restrict__ partials,
                                                         const int* __restrict__ act) {
-  // device-steered form (huber_qn.hip): ceff = the trial [c_eff (d) | intercept | sigma] in HBM,
-  // skipped once the optimizer is done (act != kHuberEval)
+  if (act != nullptr) {
+    if (*act != kHuberEval) return;
+    icpt = ceff[d];
+    sigma = ceff[d + 1];
+  }
+  constexpr int W = D > 0 ? D : 1;
+  double acc[4] = {0, 0, 0, 0};
+  double ax[W];
+#pragma unroll
+  for (int j = 0; j < W; ++j) ax[j] = 0.0;
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
+    double m = 0.0;
+    const bool live = sel == nullptr || sel[r] != 0;
+    const double wt = live ? (w ? ld_f64(w, wdt, r) : 1.0) : 0.0;
+    if (wt != 0.0) {
+      if constexpr (D > 0) {
+        const double margin = predict_row(X, xdt, ld, d, ceff, icpt, r, tiled);
+        m = huber_row(ld_f64(y, ydt, r) - margin, wt, sigma, eps, acc);
+#pragma unroll
+        for (int f = 0; f < D; ++f)  // (the row's features again: cache hits)
+          if (f < d) ax[f] += m * load_x(X, xdt, ld, d, f, r, tiled);
+      } else {
+        const double margin = predict_row(X, xdt, ld, d, ceff, icpt, r, tiled);
+        m = huber_row(ld_f64(y, ydt, r) - margin, wt, sigma, eps, acc);
+      }
+    }
+    if constexpr (D == 0) mult[r] = m;
+  }
+  constexpr int K = 4 + (D > 0 ? D : 0);
+  __shared__ double red[4][K];
+  const int width = D > 0 ? 4 + d : 4;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) acc[k] = wave_sum_f64(acc[k]);
+#pragma unroll
+  for (int j = 0; j < (D > 0 ? D : 0); ++j)
+    if (j < d) ax[j] = wave_sum_f64(ax[j]);
+  if ((threadIdx.x & 63) == 0) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) red[threadIdx.x >> 6][k] = acc[k];
+#pragma unroll
+    for (int j = 0; j < (D > 0 ? D : 0); ++j)
+      if (j < d) red[threadIdx.x >> 6][4 + j] = ax[j];
+  }
+  __syncthreads();
+  if (threadIdx.x < width)
+    partials[(int64_t)blockIdx.x * width + threadIdx.x] =
+        red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+}
+
+// The fused pass over dense feature-major columns of T (f32 / f64), d <= D: a row's d features
+// are loaded together into registers (no per-element dtype switch between the loads, so they are
+// all in flight at once), used for the margin and again for Σ m x.  Same partial layout and the
+// same per-row arithmetic as huber_rows_kernel<D>.
+template <typename T, int D>
+__global__ __launch_bounds__(256) void huber_rows_dense_kernel(const T* __restrict__ X, int64_t ld, int d, int64_t n,
+                                                              const void* __restrict__ y, int ydt,
+                                                              const void* __restrict__ w, int wdt,
+                                                              const uint8_t* __restrict__ sel,
+                                                              const double* __restrict__ ceff, double icpt,
+                                                              double sigma, double eps,
+                                                              double* __restrict__ partials,
+                                                              const int* __restrict__ act) {
   if (act != nullptr) {
     if (*act != kHuberEval) return;
     icpt = ceff[d];
     sigma = ceff[d + 1];
   }
   double acc[4] = {0, 0, 0, 0};
+  double ax[D];
+  double cf[D];
+#pragma unroll
+  for (int j = 0; j < D; ++j) ax[j] = 0.0, cf[j] = j < d ? ceff[j] : 0.0;
   for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
-    double m = 0.0;
     const bool live = sel == nullptr || sel[r] != 0;
     const double wt = live ? (w ? ld_f64(w, wdt, r) : 1.0) : 0.0;
-    if (wt != 0.0) {
-      const double margin = predict_row(X, xdt, ld, d, ceff, icpt, r, tiled);
-      const double lin = ld_f64(y, ydt, r) - margin;
-      if (fabs(lin) <= sigma * eps) {
-        const double q = lin / sigma;
-        acc[0] += 0.5 * wt * (sigma + lin * lin / sigma);
-        m = -wt * q;
-        acc[2] += -wt * q;
-        acc[3] += 0.5 * wt * (1.0 - q * q);
-      } else {
-        const double sgn = lin >= 0 ? -1.0 : 1.0;
-        acc[0] += 0.5 * wt * (sigma + 2.0 * eps * fabs(lin) - sigma * eps * eps);
-        m = wt * sgn * eps;
-        acc[2] += wt * sgn * eps;
-        acc[3] += 0.5 * wt * (1.0 - eps * eps);
-      }
-      acc[1] += wt;
-    }
-    mult[r] = m;
+    if (wt == 0.0) continue;
+    T xs[D];
+#pragma unroll
+    for (int f = 0; f < D; ++f) xs[f] = f < d ? X[(int64_t)f * ld + r] : T(0);
+    double margin = icpt;
+#pragma unroll
+    for (int f = 0; f < D; ++f)
+      if (f < d) margin += cf[f] * (double)xs[f];
+    const double m = huber_row(ld_f64(y, ydt, r) - margin, wt, sigma, eps, acc);
+#pragma unroll
+    for (int f = 0; f < D; ++f)
+      if (f < d) ax[f] += m * (double)xs[f];
   }
-  __shared__ double red[4][4];
+  __shared__ double red[4][4 + D];
+  const int width = 4 + d;
 #pragma unroll
   for (int k = 0; k < 4; ++k) acc[k] = wave_sum_f64(acc[k]);
+#pragma unroll
+  for (int j = 0; j < D; ++j)
+    if (j < d) ax[j] = wave_sum_f64(ax[j]);
   if ((threadIdx.x & 63) == 0) {
 #pragma unroll
     for (int k = 0; k < 4; ++k) red[threadIdx.x >> 6][k] = acc[k];
+#pragma unroll
+    for (int j = 0; j < D; ++j)
+      if (j < d) red[threadIdx.x >> 6][4 + j] = ax[j];
   }
   __syncthreads();
-  if (threadIdx.x < 4)
-    partials[(int64_t)blockIdx.x * 4 + threadIdx.x] =
+  if (threadIdx.x < width)
+    partials[(int64_t)blockIdx.x * width + threadIdx.x] =
         red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
 }
 
-// phase B: out[j] = Σ_r X[j][r] * v[r]   (one block per feature, fixed-order reduction)
-__global__ __launch_bounds__(256) void xt_vec_kernel(const void* __restrict__ X, int xdt, int64_t ld, int d, int64_t n,
-                                                    int tiled, const double* __restrict__ v, double* __restrict__ out,
-                                                    const int* __restrict__ act, const double* __restrict__ scale,
-                                                    const double* __restrict__ shift) {
+// Xᵀm for d > kHuberFuseD: block (c, j) sums feature j over row chunk c (fixed order), xt_fold_kernel
+// adds the chunks of each feature in order
+__global__ __launch_bounds__(256) void xt_part_kernel(const void* __restrict__ X, int xdt, int64_t ld, int d, int64_t n,
+                                                     int tiled, const double* __restrict__ v, int64_t chunk,
+                                                     double* __restrict__ part, const int* __restrict__ act) {
   if (act != nullptr && *act != kHuberEval) return;
-  const int j = blockIdx.x;
-  const int NT = (d + 31) >> 5;
+  const int c = blockIdx.x, j = blockIdx.y;
+  const int64_t r0 = (int64_t)c * chunk, r1 = r0 + chunk < n ? r0 + chunk : n;
   double s = 0.0;
-  for (int64_t r = threadIdx.x; r < n; r += blockDim.x) {
-    double x;
-    if (tiled == 1) x = (double)bf16_bits_to_f32(reinterpret_cast<const uint16_t*>(X)[tiled_offset(j, r, NT)]);
-    else if (tiled == 2) x = (double)bf16_bits_to_f32(reinterpret_cast<const uint16_t*>(X)[wide_offset(j, r, ((d + 255) >> 8) * 8)]);
-    else if (tiled == 3) x = (double)fp8_to_f32(reinterpret_cast<const uint8_t*>(X)[wide_offset_fp8(j, r, ((d + 255) >> 8) * 8)]);
-    else x = ld_f64(X, xdt, (int64_t)j * ld + r);
-    s += x * v[r];
-  }
+  for (int64_t r = r0 + threadIdx.x; r < r1; r += blockDim.x)
+    if (v[r] != 0.0) s += load_x(X, xdt, ld, d, j, r, tiled) * v[r];
   __shared__ double red[4];
   s = wave_sum_f64(s);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
   __syncthreads();
-  if (threadIdx.x == 0) {
+  if (threadIdx.x == 0) part[(int64_t)j * gridDim.x + c] = red[0] + red[1] + red[2] + red[3];
+}
+
+__global__ __launch_bounds__(256) void xt_fold_kernel(const double* __restrict__ part, int d, int chunks,
+                                                     double* __restrict__ out, const int* __restrict__ act) {
+  if (act != nullptr && *act != kHuberEval) return;
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= d) return;
+  double s = 0.0;
+  for (int c = 0; c < chunks; ++c) s += part[(int64_t)j * chunks + c];
+  out[j] = s;
+}
+
+// the storage epilogue of the device-steered pass: fp8 storage q = x / scale; shifted storage x =
+// x' + s: Σ m x = Σ m x' + s Σ m (out[2] = Σ m)
+__global__ __launch_bounds__(256) void huber_epilogue_kernel(double* __restrict__ out, int d,
+                                                            const double* __restrict__ scale,
+                                                            const double* __restrict__ shift,
+                                                            const int* __restrict__ act) {
 #pragma clang fp contract(off)  // two roundings each, as the host-steered fold's torch expressions
-    double t = red[0] + red[1] + red[2] + red[3];
-    // fp8 storage q = x / scale; shifted storage x = x' + s: Σ m x = Σ m x' + s Σ m (out[-2] = Σ m)
-    if (scale != nullptr) t *= scale[j];
-    if (shift != nullptr) t += shift[j] * out[-2];
-    out[j] = t;
+  if (*act != kHuberEval) return;
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= d) return;
+  double t = out[4 + j];
+  if (scale != nullptr) t *= scale[j];
+  if (shift != nullptr) t += shift[j] * out[2];
+  out[4 + j] = t;
+}
+
+// sum_slabs_kernel with one block per column (the same fixed-order sum of each column)
+__global__ __launch_bounds__(256) void sum_cols_kernel(const double* __restrict__ partials, int nslab, int width,
+                                                      double* __restrict__ out, const int* __restrict__ act) {
+  if (act != nullptr && *act != kHuberEval) return;
+  const int k = blockIdx.x;
+  __shared__ double wsum[4];
+  double s = 0.0;
+  for (int b = threadIdx.x; b < nslab; b += blockDim.x) s += partials[(int64_t)b * width + k];
+  s = wave_sum_f64(s);
+  if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) out[k] = (wsum[0] + wsum[1]) + (wsum[2] + wsum[3]);
+}
+
+constexpr int kHuberFuseD = 16;
+
+int64_t xt_chunks(int64_t n, int d) {
+  int64_t c = (n + 65535) / 65536;
+  const int64_t cap = d >= 2048 ? 1 : 2048 / d;
+  if (c > cap) c = cap;
+  return c < 1 ? 1 : c;
+}
+
+void launch_huber(const void* X, int xdt, int64_t ld, int d, int64_t n, int tiled, const void* y, int ydt,
+                  const void* w, int wdt, const uint8_t* sel, const double* ceff, double icpt, double sigma,
+                  double eps, double* mult, double* partials, double* out, const int* act, hipStream_t st) {
+  const int g = metrics_blocks(n);
+  if (d <= kHuberFuseD && tiled == 0 && (xdt == DT_F32 || xdt == DT_F64)) {
+    if (xdt == DT_F32)
+      hipLaunchKernelGGL((huber_rows_dense_kernel<float, kHuberFuseD>), dim3(g), dim3(256), 0, st,
+                         reinterpret_cast<const float*>(X), ld, d, n, y, ydt, w, wdt, sel, ceff, icpt, sigma, eps,
+                         partials, act);
+    else
+      hipLaunchKernelGGL((huber_rows_dense_kernel<double, kHuberFuseD>), dim3(g), dim3(256), 0, st,
+                         reinterpret_cast<const double*>(X), ld, d, n, y, ydt, w, wdt, sel, ceff, icpt, sigma, eps,
+                         partials, act);
+    hipLaunchKernelGGL(sum_cols_kernel, dim3(4 + d), dim3(256), 0, st, partials, g, 4 + d, out, act);
+  } else if (d <= kHuberFuseD) {
+    hipLaunchKernelGGL(huber_rows_kernel<kHuberFuseD>, dim3(g), dim3(256), 0, st, X, xdt, ld, d, n, tiled, y, ydt, w, wdt, sel, ceff, icpt, sigma,
+                       eps, mult, partials, act);
+    hipLaunchKernelGGL(sum_cols_kernel, dim3(4 + d), dim3(256), 0, st, partials, g, 4 + d, out, act);
+  } else {
+    hipLaunchKernelGGL(huber_rows_kernel<0>, dim3(g), dim3(256), 0, st, X, xdt, ld, d, n, tiled, y, ydt, w, wdt, sel,
+                       ceff, icpt, sigma, eps, mult, partials, act);
+    hipLaunchKernelGGL(sum_slabs_kernel, dim3(1), dim3(256), 0, st, partials, g, 4, out);
+    const int64_t c = xt_chunks(n, d), chunk = (n + c - 1) / c;
+    double* part = partials + (int64_t)g * 4;
+    hipLaunchKernelGGL(xt_part_kernel, dim3((unsigned)c, (unsigned)d), dim3(256), 0, st, X, xdt, ld, d, n, tiled,
+                       mult, chunk, part, act);
+    hipLaunchKernelGGL(xt_fold_kernel, dim3((d + 255) / 256), dim3(256), 0, st, part, d, (int)c, out + 4, act);
   }
 }
 
 }  // namespace
 
+int64_t huber_partials(int64_t n, int d) {
+  const int64_t g = metrics_blocks(n);
+  return d <= kHuberFuseD ? g * (4 + d) : g * 4 + (int64_t)d * xt_chunks(n, d);
+}
+
 void huber_pass(const void* X, int xdt, int64_t ld, int d, int64_t n, int tiled, const void* y, int ydt,
                 const void* w, int wdt, const uint8_t* sel, const double* ceff, double icpt, double sigma, double eps,
                 double* mult, double* partials, double* out /* [4 + d] */, hipStream_t st) {
-  const int g = metrics_blocks(n);
-  hipLaunchKernelGGL(huber_rows_kernel, dim3(g), dim3(256), 0, st, X, xdt, ld, d, n, tiled, y, ydt, w, wdt, sel, ceff,
-                     icpt, sigma, eps, mult, partials, nullptr);
-  hipLaunchKernelGGL(sum_slabs_kernel, dim3(1), dim3(256), 0, st, partials, g, 4, out);
-  hipLaunchKernelGGL(xt_vec_kernel, dim3(d), dim3(256), 0, st, X, xdt, ld, d, n, tiled, mult, out + 4, nullptr,
-                     nullptr, nullptr);
+  launch_huber(X, xdt, ld, d, n, tiled, y, ydt, w, wdt, sel, ceff, icpt, sigma, eps, mult, partials, out, nullptr, st);
   DQ_HIP_CHECK(hipGetLastError());
 }
 
@@ -595,12 +760,9 @@ void huber_pass_dev(const void* X, int xdt, int64_t ld, int d, int64_t n, int ti
                     const double* scale, const double* shift, double* mult, double* partials, double* out,
                     hipStream_t st) {
   if (act == nullptr || trial == nullptr) throw std::invalid_argument("huber_pass_dev: trial and act are required");
-  const int g = metrics_blocks(n);
-  hipLaunchKernelGGL(huber_rows_kernel, dim3(g), dim3(256), 0, st, X, xdt, ld, d, n, tiled, y, ydt, w, wdt, sel,
-                     trial, 0.0, 1.0, eps, mult, partials, act);
-  hipLaunchKernelGGL(sum_slabs_kernel, dim3(1), dim3(256), 0, st, partials, g, 4, out);
-  hipLaunchKernelGGL(xt_vec_kernel, dim3(d), dim3(256), 0, st, X, xdt, ld, d, n, tiled, mult, out + 4, act, scale,
-                     shift);
+  launch_huber(X, xdt, ld, d, n, tiled, y, ydt, w, wdt, sel, trial, 0.0, 1.0, eps, mult, partials, out, act, st);
+  if (scale != nullptr || shift != nullptr)
+    hipLaunchKernelGGL(huber_epilogue_kernel, dim3((d + 255) / 256), dim3(256), 0, st, out, d, scale, shift, act);
   DQ_HIP_CHECK(hipGetLastError());
 }
 

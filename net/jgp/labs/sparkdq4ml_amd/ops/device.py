@@ -710,9 +710,8 @@ def huber_pass(X, y, w, sel, ceff, icpt, sigma, eps):
     fp8 = isinstance(X, TiledWide) and X.eb == 8
     if fp8:
         c = c * X.scales.to(torch.float64)
-    nb = int(h.metrics_blocks(n))
-    mult = torch.empty(n, dtype=torch.float64, device=Xb.device)
-    partials = torch.empty(nb * 4, dtype=torch.float64, device=Xb.device)
+    mult = torch.empty(max(n, 1) if d > 16 else 1, dtype=torch.float64, device=Xb.device)
+    partials = torch.empty(int(h.huber_partials(n, d)), dtype=torch.float64, device=Xb.device)
     out = torch.empty(4 + d, dtype=torch.float64, device=Xb.device)
     h.huber_pass(Xb.data_ptr(), xdt, int(ld), int(d), int(n), tiled, y.data_ptr(), dtype_code(y), _ptr(w),
                  dtype_code(w) if w is not None else 0, _ptr(sel), c.data_ptr(), float(icpt), float(sigma), float(eps),
@@ -757,9 +756,8 @@ def huber_fit_dp(X, y, w, sel, sx: torch.Tensor, lam: torch.Tensor, fit_icpt: bo
     act = work[:1].view(torch.int32)[:1]  # HCtl.act: the struct's first word
     trial = torch.zeros(d + 2, dtype=torch.float64, device=dev)
     red = torch.zeros(4 + d, dtype=torch.float64, device=dev)
-    nb = int(h.metrics_blocks(n))
-    mult = torch.empty(max(n, 1), dtype=torch.float64, device=dev)
-    partials = torch.empty(nb * 4, dtype=torch.float64, device=dev)
+    mult = torch.empty(max(n, 1) if d > 16 else 1, dtype=torch.float64, device=dev)  # (d > 16: the Xᵀm pass)
+    partials = torch.empty(int(h.huber_partials(n, d)), dtype=torch.float64, device=dev)
     out = torch.zeros(int(h.huber_qn_out(d, cap)), dtype=torch.float64, device=dev)
     out[d + 2:d + 3].fill_(9.0)
     st = _stream()

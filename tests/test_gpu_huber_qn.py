@@ -3,7 +3,8 @@ device, checked against the host implementation of the same algorithm (``models/
 oracle: ``dq4ml.huber.device=false``) -- same objective history up to rounding, same optimum --
 on dense f64 columns, bf16 wide tiles and fp8 wide tiles with shifted storage; then the
 data-parallel form: two gloo ranks over row shards, and a forced one-rank RCCL fit that runs
-under ``sync_debug_mode("error")`` (no host read anywhere in the fit)."""
+under ``sync_debug_mode("error")`` (no host read anywhere in the fit); and an independent fp64
+oracle (scipy L-BFGS-B on a numpy Huber objective)."""
 import json
 import os
 import socket
@@ -57,6 +58,50 @@ def test_device_huber_matches_host_lbfgsb(gpu_session, case):
         beta = np.linspace(-1.0, 2.0, c["d"])
         assert np.abs(dev.coefficients.toArray() - beta).max() < 0.02
         assert float(dev.intercept) == pytest.approx(0.7, abs=0.05)
+
+
+def _oracle(X, y, reg, fit_icpt=True):
+    """Independent fp64 optimum of Spark 2.4's Huber objective (HuberAggregator + L2 in the
+    standardized space, epsilon 1.35): scipy's L-BFGS-B (Fortran, not Breeze's algorithm) driven
+    to a tight tolerance on a numpy implementation that shares no code with either fit path.
+    Returns (coefficients, intercept, scale)."""
+    from scipy.optimize import minimize
+
+    X, y = X.double().cpu().numpy(), y.double().cpu().numpy()
+    d, n = X.shape
+    sx = X.std(axis=1, ddof=1)
+    Z = X / sx[:, None]
+    eps = 1.35
+
+    def fg(t):
+        c, b, s = t[:d], (t[d] if fit_icpt else 0.0), t[-1]
+        r = y - c @ Z - b
+        inside = np.abs(r) <= s * eps
+        loss = np.where(inside, 0.5 * (s + r * r / s), 0.5 * (s + 2 * eps * np.abs(r) - s * eps * eps))
+        m = np.where(inside, -r / s, -eps * np.sign(r))
+        gs = np.where(inside, 0.5 * (1 - (r / s) ** 2), 0.5 * (1 - eps * eps))
+        f = loss.mean() + 0.5 * reg * c @ c
+        g = np.concatenate([Z @ m / n + reg * c, [m.mean()] if fit_icpt else [], [gs.mean()]])
+        return f, g
+
+    t0 = np.ones(d + (2 if fit_icpt else 1))
+    bounds = [(None, None)] * (t0.size - 1) + [(1e-12, None)]
+    res = minimize(fg, t0, jac=True, method="L-BFGS-B", bounds=bounds,
+                   options=dict(maxiter=5000, maxcor=20, ftol=1e-15, gtol=1e-12))
+    t = res.x
+    return t[:d] / sx, (t[d] if fit_icpt else 0.0), t[-1]
+
+
+@pytest.mark.parametrize("reg", [0.0, 0.05])
+def test_device_huber_matches_fp64_oracle(gpu_session, reg):
+    X, y = data("dense", "cuda")
+    m = _fit(gpu_session, frame(gpu_session, "dense", X, y), dict(maxIter=200, regParam=reg), True)
+    assert getattr(m, "_huber_evaluations", None)
+    c, b, s = _oracle(X, y, reg)
+    coef = m.coefficients.toArray()
+    assert np.abs(coef - c).max() <= 2e-5 * max(1.0, np.abs(c).max()), np.abs(coef - c).max()
+    assert float(m.intercept) == pytest.approx(b, abs=2e-5)
+    assert float(m.scale) == pytest.approx(s, rel=5e-5)
 
 
 @pytest.mark.parametrize("kw", [dict(fitIntercept=False, maxIter=50), dict(standardization=False, regParam=0.1),
