@@ -28,7 +28,7 @@ CONFIGS = {
     "headline": ("bench.py", ["--steps", "50", "--warmup", "5"], ["--rows", "40000", "--steps", "2", "--warmup", "1"]),
     "cfg4": ("benchmarks/bench_dq_pipeline.py", ["--steps", "5", "--warmup", "2"],
              ["--rows-per-gpu", "20000", "--features", "16", "--steps", "1", "--warmup", "1"]),
-    "cfg5": ("benchmarks/bench_wide.py", ["--steps", "3", "--warmup", "1"], ["--steps", "1", "--warmup", "1"]),
+    "cfg5": ("benchmarks/bench_wide.py", ["--steps", "12", "--warmup", "3"], ["--steps", "1", "--warmup", "1"]),
     "csv32": ("benchmarks/bench_csv_pipeline.py", ["--features", "32", "--rows", "1e8", "--steps", "5", "--warmup", "1"],
               ["--rows", "40000", "--steps", "1", "--warmup", "1"]),
     "lbfgs": ("benchmarks/bench_lbfgs.py", ["--steps", "2", "--warmup", "1"],
