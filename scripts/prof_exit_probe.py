@@ -6,6 +6,8 @@
 
 cumask: a kernel on a CU-masked stream (its own hardware queue), then exit;
 coop:   the one-launch cooperative l-bfgs fit (lsq_qn.hip), its result read, then exit;
+coopreset: coop, then hipDeviceReset() before interpreter exit (the runtime's queues -- the
+        cooperative-launch queue among them -- destroyed while the profiler is still attached);
 plain:  the same work on the default stream only (control).
 Prints "probe done" before interpreter exit: a crash after that line is a teardown crash."""
 import os
@@ -31,7 +33,7 @@ def main():
             y = (x * 2.0).sum()
         st.synchronize()
         print("sum", float(y))
-    elif mode == "coop":
+    elif mode in ("coop", "coopreset"):
         d, n = 512, 100_000
         X = torch.randn(d, n, device="cuda")
         y = torch.linspace(-1, 1, d, device="cuda") @ X + 0.5
@@ -43,6 +45,11 @@ def main():
     else:
         print("sum", float((x * 2.0).sum()))
     torch.cuda.synchronize()
+    if mode == "coopreset":
+        import ctypes
+
+        rc = ctypes.CDLL("libamdhip64.so").hipDeviceReset()
+        print("hipDeviceReset", rc, flush=True)
     print("probe done", flush=True)
 
 
