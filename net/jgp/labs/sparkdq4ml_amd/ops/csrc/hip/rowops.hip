@@ -608,13 +608,23 @@ __global__ __launch_bounds__(256) void huber_rows_dense_kernel(const T* __restri
   double cf[D];
 #pragma unroll
   for (int j = 0; j < D; ++j) ax[j] = 0.0, cf[j] = j < d ? ceff[j] : 0.0;
-  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
+  // software-pipelined: the next row's features are in flight while this row computes (two rows'
+  // loads per thread outstanding; the last trip re-loads its own row)
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  T xn[D];
+#pragma unroll
+  for (int f = 0; f < D; ++f) xn[f] = (f < d && r < n) ? X[(int64_t)f * ld + r] : T(0);
+  for (; r < n; r += stride) {
+    T xs[D];
+#pragma unroll
+    for (int f = 0; f < D; ++f) xs[f] = xn[f];
+    const int64_t rn = r + stride < n ? r + stride : r;
+#pragma unroll
+    for (int f = 0; f < D; ++f) xn[f] = f < d ? X[(int64_t)f * ld + rn] : T(0);
     const bool live = sel == nullptr || sel[r] != 0;
     const double wt = live ? (w ? ld_f64(w, wdt, r) : 1.0) : 0.0;
     if (wt == 0.0) continue;
-    T xs[D];
-#pragma unroll
-    for (int f = 0; f < D; ++f) xs[f] = f < d ? X[(int64_t)f * ld + r] : T(0);
     double margin = icpt;
 #pragma unroll
     for (int f = 0; f < D; ++f)

@@ -118,6 +118,24 @@ def test_device_huber_options(gpu_session, kw):
         assert len(dev.summary.objectiveHistory) == len(host.summary.objectiveHistory) == 4
 
 
+def test_device_huber_weights_and_filter(gpu_session):
+    """Instance weights (``weightCol``) and a DQ-style row filter (the selection vector the pass
+    skips) on the device path, against the host-steered optimizer on the same frame."""
+    import torch
+
+    from net.jgp.labs.sparkdq4ml_amd.sql import functions as F
+
+    X, y = data("dense", "cuda")
+    n = X.shape[1]
+    w = (0.5 + torch.rand(n, generator=torch.Generator().manual_seed(3), dtype=torch.float64)).cuda()
+    df = gpu_session.createDataFrame({"features": X, "label": y, "w": w}).filter(F.col("label") > -3.0)
+    kw = dict(weightCol="w", maxIter=80)
+    dev = _fit(gpu_session, df, kw, True)
+    host = _fit(gpu_session, df, kw, False)
+    assert getattr(dev, "_huber_evaluations", None)
+    _close(dev, host)
+
+
 def _run_workers(args, world, timeout=180):
     here = os.path.dirname(os.path.abspath(__file__))
     s = socket.socket()
