@@ -92,10 +92,10 @@ __device__ __forceinline__ int pair_index(int I, int J, int P) {
   return I * (P + 1) - I * (I - 1) / 2 + (J - I);
 }
 
-// partial tile of (pair, slot): uniform layouts hold splitk slots per pair; the gang schedule's
-// merged units give every pair its own slot count, from the tile_base prefix table
-__device__ __forceinline__ int64_t wide_tile(const WideArgs& a, int pair, int slot) {
-  return (a.tile_base ? (int64_t)a.tile_base[pair] : (int64_t)pair * a.splitk) + slot;
+template <bool TABLE>
+__device__ __forceinline__ int64_t tile_of(const WideArgs& a, int pair, int slot) {
+  if constexpr (TABLE) return (int64_t)a.tile_base[pair] + slot;
+  else return (int64_t)pair * a.splitk + slot;
 }
 
 template <int N>
@@ -123,7 +123,7 @@ struct StageFrags {
 //   glds stage i+4 into the buffer stage i vacated | MFMAs on A tiles 2-3 | lgkmcnt(0)
 // so the LDS reads and the barrier skew hide under half a stage of MFMAs, and three stages of
 // global_load_lds stay in flight across every barrier.
-template <int EB, int MODE, int RING>
+template <int EB, int MODE, int RING, bool TABLE = false>
 __device__ __forceinline__ void syrk_block(const WideArgs& a, unsigned char* smem, int I, int J, int s_lo, int s_hi,
                                            int slot) {
   typedef WideTraits<EB> Tr;
@@ -289,21 +289,21 @@ __device__ __forceinline__ void syrk_block(const WideArgs& a, unsigned char* sme
     wait_vm<0>();  // drain the zero-page prefetches before the block can exit
   }
   if constexpr (MODE == 5) {  // (I, aug): 256 rows x the augmentation tile's 32 columns
-    float* out = a.part + wide_tile(a, pair_index(I, a.npanels, a.npanels), slot) * kPanel * kPanel;
+    float* out = a.part + tile_of<TABLE>(a, pair_index(I, a.npanels, a.npanels), slot) * kPanel * kPanel;
 #pragma unroll
     for (int x = 0; x < 4; ++x)
 #pragma unroll
       for (int r = 0; r < 16; ++r)
         out[(wn * 128 + x * 32 + mfma32_row(lane, r)) * kPanel + mfma32_col(lane)] = acc[x][0][r];
     if (I == 0 && wn == 0) {
-      float* o2 = a.part + wide_tile(a, pair_index(a.npanels, a.npanels, a.npanels), slot) * kPanel * kPanel;
+      float* o2 = a.part + tile_of<TABLE>(a, pair_index(a.npanels, a.npanels, a.npanels), slot) * kPanel * kPanel;
 #pragma unroll
       for (int r = 0; r < 16; ++r) o2[mfma32_row(lane, r) * kPanel + mfma32_col(lane)] = acc[0][1][r];
     }
     return;
   }
   // f32 partial tile [256][256] of this (pair, slot)
-  float* out = a.part + wide_tile(a, pair_index(I, J, a.npanels), slot) * kPanel * kPanel;
+  float* out = a.part + tile_of<TABLE>(a, pair_index(I, J, a.npanels), slot) * kPanel * kPanel;
 #pragma unroll
   for (int x = 0; x < 4; ++x)
 #pragma unroll
@@ -411,7 +411,24 @@ __device__ __forceinline__ void gang_round_sync(int* bar, int g, int k, int G, i
   __syncthreads();
 }
 
-template <int EB, int RING>
+// unit u of the classic gang list (no long units): the S * P(P-1)/2 off-diagonal units range-major,
+// then the S * P diagonal ones; `pos` indexes a.pairs (off-diagonal pairs in Z-order, then the
+// diagonal ones)
+__device__ __forceinline__ void gang_unit(int u, int S, int P, int& s, int& pos) {
+  const int noff = P * (P - 1) / 2;
+  if (u < S * noff) {
+    s = u / noff;
+    pos = u - s * noff;
+  } else {
+    const int v = u - S * noff;
+    s = v / P;
+    pos = noff + (v - s * P);
+  }
+}
+
+// TABLE: units from the int4 table (long units over all S ranges for some pairs, per-pair tile
+// prefix); else the classic list decoded from u (one range per unit, uniform tile layout)
+template <int EB, int RING, bool TABLE>
 __global__ __launch_bounds__(64 * kWaves, 1) void gram_wide_gang_kernel(WideArgs a, int S, int units,
                                                                        const int4* __restrict__ table,
                                                                        int* __restrict__ bar) {
@@ -422,16 +439,26 @@ __global__ __launch_bounds__(64 * kWaves, 1) void gram_wide_gang_kernel(WideArgs
   const bool aug_wave = (wave >> 2) == 1 && (wave & 3) < 2;
   int k = 0;
   for (int u = l; u < units; u += G, ++k) {
-    // unit u of every group: panels (I, J), row ranges [s0, s0 + ns) of the group's S, and the
-    // unit's slot kk among the K units its pair has per group (slot g K + kk of the pair's tiles)
-    const int4 e = table[u];
-    const int I = e.x, J = e.y, s0 = e.z & 0xffff, ns = e.z >> 16, kk = e.w & 0xffff, K = e.w >> 16;
-    const int lo = g * S + s0, slot = g * K + kk;
+    int I, J, lo, ns, slot;
+    if constexpr (TABLE) {
+      // unit u of every group: panels (I, J), row ranges [s0, s0 + ns) of the group's S, and the
+      // unit's slot kk among the K units its pair has per group (slot g K + kk of the pair's tiles)
+      const int4 e = table[u];
+      I = e.x, J = e.y;
+      const int s0 = e.z & 0xffff, kk = e.w & 0xffff, K = e.w >> 16;
+      ns = e.z >> 16;
+      lo = g * S + s0, slot = g * K + kk;
+    } else {
+      int s, pos;
+      gang_unit(u, S, a.npanels, s, pos);
+      I = a.pairs[2 * pos], J = a.pairs[2 * pos + 1];
+      lo = g * S + s, ns = 1, slot = lo;
+    }
     gang_round_sync(bar, g, k, G, units);
-    if (I != J) syrk_block<EB, 0, RING>(a, smem, I, J, lo, lo + ns, slot);
-    else if (aug_wave) syrk_block<EB, 5, RING>(a, smem, I, J, lo, lo + ns, slot);
-    else if (wave < 2) syrk_block<EB, 4, RING>(a, smem, I, J, lo, lo + ns, slot);  // + the aug tile's loads
-    else syrk_block<EB, 6, RING>(a, smem, I, J, lo, lo + ns, slot);
+    if (I != J) syrk_block<EB, 0, RING, TABLE>(a, smem, I, J, lo, lo + ns, slot);
+    else if (aug_wave) syrk_block<EB, 5, RING, TABLE>(a, smem, I, J, lo, lo + ns, slot);
+    else if (wave < 2) syrk_block<EB, 4, RING, TABLE>(a, smem, I, J, lo, lo + ns, slot);  // + the aug tile's loads
+    else syrk_block<EB, 6, RING, TABLE>(a, smem, I, J, lo, lo + ns, slot);
     __syncthreads();  // every wave is done reading the ring before the next unit's first glds
   }
 }
@@ -925,10 +952,18 @@ template <int EB>
 static void launch_wide_gang(const WideArgs& a, int grid, int S, int units, const int4* table, hipStream_t st,
                              int* bar) {
   const size_t lds = (size_t)5 * kStageBytes;
-  DQ_HIP_CHECK(hipFuncSetAttribute((const void*)gram_wide_gang_kernel<EB, 5>,
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   if (bar != nullptr) DQ_HIP_CHECK(hipMemsetAsync(bar, 0, 8 * 32 * sizeof(int), st));
-  hipLaunchKernelGGL((gram_wide_gang_kernel<EB, 5>), dim3(grid), dim3(64 * kWaves), lds, st, a, S, units, table, bar);
+  if (table != nullptr) {
+    DQ_HIP_CHECK(hipFuncSetAttribute((const void*)gram_wide_gang_kernel<EB, 5, true>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    hipLaunchKernelGGL((gram_wide_gang_kernel<EB, 5, true>), dim3(grid), dim3(64 * kWaves), lds, st, a, S, units,
+                       table, bar);
+  } else {
+    DQ_HIP_CHECK(hipFuncSetAttribute((const void*)gram_wide_gang_kernel<EB, 5, false>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    hipLaunchKernelGGL((gram_wide_gang_kernel<EB, 5, false>), dim3(grid), dim3(64 * kWaves), lds, st, a, S, units,
+                       table, bar);
+  }
   DQ_HIP_CHECK(hipGetLastError());
 }
 
@@ -937,7 +972,12 @@ void gram_wide_gang(int eb, WideArgs a, const int* table, int units, const float
   if (S < 1 || a.splitk != 8 * S) throw std::invalid_argument("gram_wide_gang: splitk must be 8 * S");
   if (grid < 8 || grid % 8) throw std::invalid_argument("gram_wide_gang: grid must be a positive multiple of 8");
   if ((int64_t)a.splitk > a.nsup) throw std::invalid_argument("gram_wide_gang: more row ranges than supersteps");
-  if (a.tile_base == nullptr || units < 1) throw std::invalid_argument("gram_wide_gang: needs the unit and tile tables");
+  if (units < 1) throw std::invalid_argument("gram_wide_gang: no units");
+  // the table form needs its tile prefix; the classic form decodes units from a.pairs (off-diagonal
+  // pairs, then diagonal ones) over the uniform splitk tile layout
+  if (table != nullptr && a.tile_base == nullptr) throw std::invalid_argument("gram_wide_gang: table needs tile_base");
+  if (table == nullptr && (a.pairs == nullptr || a.tile_base != nullptr || units != S * a.npanels * (a.npanels + 1) / 2))
+    throw std::invalid_argument("gram_wide_gang: the classic unit list needs the pair list and the uniform layout");
   const int4* t = reinterpret_cast<const int4*>(table);
   if (eb == 16) launch_wide_gang<16>(a, grid, S, units, t, st, bar);
   else launch_wide_gang<8>(a, grid, S, units, t, st, bar);

@@ -307,10 +307,11 @@ PYBIND11_MODULE(_dq4ml_hip, m) {
                     as_stream(stream), fold);
   });
   m.def("gram_wide_gang", [wide_args](int eb, uintptr_t X, uintptr_t Xaug, uintptr_t zeros, int nt, int npanels,
-                                      int d, int64_t nsup, int S, uintptr_t table, int units, uintptr_t tile_base,
-                                      uintptr_t part, uintptr_t aug_scale, uintptr_t scales, uintptr_t out, int grid,
-                                      uintptr_t stream, bool fold, uintptr_t bar) {
+                                      int d, int64_t nsup, int S, uintptr_t table, uintptr_t pairs, int units,
+                                      uintptr_t tile_base, uintptr_t part, uintptr_t aug_scale, uintptr_t scales,
+                                      uintptr_t out, int grid, uintptr_t stream, bool fold, uintptr_t bar) {
     WideArgs a = wide_args(X, Xaug, zeros, nt, npanels, d, nsup, 8 * S, part, aug_scale, tile_base);
+    a.pairs = P<const int>(pairs);
     gram_wide_gang(eb, a, P<const int>(table), units, P<const float>(scales), P<double>(out), S, grid,
                    as_stream(stream), fold, P<int>(bar));
   });

@@ -1356,9 +1356,18 @@ class _WideSchedule:
     units: int = 0        # gang units per group
     tile_base: Optional[torch.Tensor] = None  # gang: [npair + 1] partial-tile prefix per pair
     tiles: int = 0        # partial tiles in all
+    pairs_list: Optional[torch.Tensor] = None  # classic gang: off-diagonal pairs, then diagonal ones
 
 
-def _gang_table(P: int, S: int, G: int):
+# Long gang units (the table form of the gang kernel) only while a row range is short: a long unit
+# runs its S ranges back to back with no round barrier inside.  At the 8-GPU shard (610 supersteps
+# per range) the 4x smaller fold pays; at 1e7 rows (4883 per range) long units ran 67.1 -> 69.2 ms
+# per pass, sclk -2 % at the same board power (same-box A/B, profiles/r6/ab_energy_long_units_fixed.log),
+# so long row ranges run the classic gang list (units decoded from u, uniform tile layout).
+_LONG_UNIT_MAX_SUP = 1024
+
+
+def _gang_table(P: int, S: int, G: int, long_units: bool = True):
     """The gang schedule's unit table and per-pair partial-tile prefix (gram_wide.hip
     gram_wide_gang_kernel).  A group of G blocks covers S row ranges of the panel pairs:
 
@@ -1373,7 +1382,7 @@ def _gang_table(P: int, S: int, G: int):
     pairs = _wide_pairs(P)
     off = [p for p in pairs if p[0] != p[1] and p[1] < P]
     diag = [p for p in pairs if p[0] == p[1] and p[1] < P]
-    n_long = (len(off) // G) * G if S > 1 else 0
+    n_long = (len(off) // G) * G if S > 1 and long_units else 0
     units = [(p, 0, S) for p in off[:n_long]]
     units += [(p, s, 1) for s in range(S) for p in off[n_long:]]
     units += [(p, s, 1) for s in range(S) for p in diag]
@@ -1397,6 +1406,7 @@ def _gang_table(P: int, S: int, G: int):
 
 
 _wide_sched_cache = {}
+_last_gang_bar = None
 
 
 def _wide_schedule(h, P: int, nsup: int, eb: int, dev) -> _WideSchedule:
@@ -1404,17 +1414,27 @@ def _wide_schedule(h, P: int, nsup: int, eb: int, dev) -> _WideSchedule:
     groups to >= 90 %, else the persistent queue, else the static split-K grid (few rows)."""
     grid = _wide_grid(h)
     forced = os.environ.get("DQ4ML_WIDE_SCHED", "gang")
-    key = (dev, P, nsup, eb, grid, forced, os.environ.get("DQ4ML_WIDE_GANG_S"), os.environ.get("DQ4ML_WIDE_H"))
+    key = (dev, P, nsup, eb, grid, forced, os.environ.get("DQ4ML_WIDE_GANG_S"), os.environ.get("DQ4ML_WIDE_H"),
+           _LONG_UNIT_MAX_SUP)
     sc = _wide_sched_cache.get(key)
     if sc is not None:
         return sc
     pairs = _wide_pairs(P)
     gs = _wide_gang_s(P, nsup, grid // 8) if forced == "gang" else 0
     hq = _wide_queue_h(nsup) if not gs and forced in ("gang", "queue") else 0
-    if gs:  # (gram_wide.hip gram_wide_gang_kernel: long off-diagonal units, then equal-cost short ones)
+    if gs and nsup // (8 * gs) <= _LONG_UNIT_MAX_SUP:
+        # (gram_wide.hip gram_wide_gang_kernel<TABLE>: long off-diagonal units, then equal-cost short ones)
         rows, units, base, tiles = _gang_table(P, gs, grid // 8)
         sc = _WideSchedule("gang", 8 * gs, gs, 0, _h2d(np.asarray(rows, dtype=np.int32).reshape(-1), dev), units,
                            _h2d(np.asarray(base, dtype=np.int32), dev), tiles)
+        sc.pairs_list = None
+        _wide_sched_cache[key] = sc
+        return sc
+    if gs:  # the classic gang list: one row range per unit, decoded in the kernel, uniform tile layout
+        gp = [p for p in pairs if p[0] != p[1] and p[1] < P] + [p for p in pairs if p[0] == p[1] and p[1] < P]
+        sc = _WideSchedule("gang", 8 * gs, gs, 0, None, P * (P + 1) // 2 * gs)
+        sc.pairs_list = _h2d(np.asarray(gp, dtype=np.int32).reshape(-1), dev)
+        sc.tiles = (P + 1) * (P + 2) // 2 * 8 * gs
         _wide_sched_cache[key] = sc
         return sc
     elif hq:
@@ -1493,7 +1513,10 @@ def _gram_wide(h, T: TiledWide, y, w, sel, x_zero_dead, defer: bool = False):
         # per-round group barrier (full rounds, bounded: the blocks of an XCD start every round
         # together, profiles/r5_wide_limiter.md)
         bar = torch.empty(256, dtype=torch.int32, device=dev)
-        h.gram_wide_gang(*args, sc.S, sc.pairs_dev.data_ptr(), sc.units, sc.tile_base.data_ptr(), part.data_ptr(),
+        global _last_gang_bar
+        _last_gang_bar = bar  # (diagnostics: bar[32 g + 1] != 0 -- group g's barrier timed out and went off)
+        h.gram_wide_gang(*args, sc.S, _ptr(sc.pairs_dev), _ptr(sc.pairs_list), sc.units, _ptr(sc.tile_base),
+                         part.data_ptr(),
                          aug_scale.data_ptr(), _ptr(T.scales), out.data_ptr(), _wide_grid(h), _stream(), fold_in,
                          bar.data_ptr())
     elif sc.sched == "queue":

@@ -79,6 +79,8 @@ def main():
     n = int(float(os.environ.get("N", "1e7")))
     d = int(os.environ.get("D", "4096"))
     reps = int(os.environ.get("REPS", "20"))
+    if os.environ.get("LONG_MAX"):  # (A/B) the long-unit threshold, supersteps per row range
+        device._LONG_UNIT_MAX_SUP = int(os.environ["LONG_MAX"])
     h = native.hip()
     eb = 8
     buf = torch.empty(int(h.wide_tiled_bytes(eb, d, n)), dtype=torch.uint8, device="cuda")
@@ -112,12 +114,14 @@ def main():
     if smp:
         smp.__exit__()
     ms = e0.elapsed_time(e1) / reps
+    bar = getattr(device, "_last_gang_bar", None)
+    bar_off = None if bar is None else [int(v) for v in bar.view(8, 32)[:, 1].cpu()]
     w = Sampler.mid(smp.w) if smp else None
     print(json.dumps({"rows": n, "features": d, "reps": reps, "ms_per_pass": round(ms, 3),
                       "board_w": None if w is None else round(w, 1),
                       "j_per_pass": None if w is None else round(w * ms * 1e-3, 2),
                       "sclk_mhz": None if not smp or not smp.f else round(Sampler.mid(smp.f)),
-                      "samples": len(smp.w) if smp else 0, "hwmon": hw}))
+                      "samples": len(smp.w) if smp else 0, "hwmon": hw, "gang_barrier_off": bar_off}))
 
 
 if __name__ == "__main__":

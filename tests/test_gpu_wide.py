@@ -183,18 +183,21 @@ def test_pack_mixed_dtypes_and_misaligned_columns(wide):
 
 @gpu
 @pytest.mark.parametrize("eb", [16, 8])
-@pytest.mark.parametrize("sched", ["gang", "gang3", "queue", "grid"])
+@pytest.mark.parametrize("sched", ["gang", "gang3", "gangc", "gangc3", "queue", "grid"])
 @pytest.mark.parametrize("d", [300, 1100])
 def test_wide_schedules_match_oracle(eb, sched, d, monkeypatch):
     # every SYRK schedule (the gang's merged diagonal + augmentation units included) gives the
     # same statistics as the fp64 oracle of the stored (quantized) values.  gang3 at d = 1100: 15
     # units x 3 row ranges = 45 units over 32 blocks per group -- a partial last round, which the
-    # round barrier must skip (its blocks would wait for arrivals that never come)
+    # round barrier must skip (its blocks would wait for arrivals that never come).  gangc: the
+    # classic unit list (what long row ranges run), forced at this size
     _hip()
     from net.jgp.labs.sparkdq4ml_amd.ops import device
 
     monkeypatch.setenv("DQ4ML_WIDE_SCHED", sched[:4] if sched.startswith("gang") else sched)
-    monkeypatch.setenv("DQ4ML_WIDE_GANG_S", "3" if sched == "gang3" else "2")
+    monkeypatch.setenv("DQ4ML_WIDE_GANG_S", "3" if sched.endswith("3") else "2")
+    if sched.startswith("gangc"):
+        monkeypatch.setattr(device, "_LONG_UNIT_MAX_SUP", -1)
     monkeypatch.setenv("DQ4ML_WIDE_H", "1")
     n = 70_001
     g = torch.Generator(device="cuda").manual_seed(d + eb)
