@@ -169,7 +169,8 @@ def _device_moments(flat: torch.Tensor, d: int, reg: float, std_flag: bool):
     var = torch.where(denom > 0, torch.clamp(diag - W * mx * mx, min=0.0) / denom, torch.zeros_like(mx))
     sx = torch.sqrt(var)
     safe = torch.where(sx == 0.0, torch.ones_like(sx), sx)
-    lam = torch.full_like(sx, reg) if std_flag else torch.where(sx != 0.0, reg / (safe * safe), torch.zeros_like(sx))
+    full = torch.full_like(sx, reg)  # (tensor / tensor: the host's numpy division, bit for bit)
+    lam = full if std_flag else torch.where(sx != 0.0, full / (safe * safe), torch.zeros_like(sx))
     return sx.contiguous(), lam.contiguous()
 
 
