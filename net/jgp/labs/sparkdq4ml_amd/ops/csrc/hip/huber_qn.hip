@@ -181,6 +181,68 @@ __device__ __forceinline__ int converged(const HArgs& a, const HV& v, const HCtl
   return -1;
 }
 
+// Partial pivot of column `col` of an m-row matrix (row stride ld) in LDS, computed by EVERY wave
+// (lanes read the rows, shuffle arg-max: the first strict maximum, as the one-thread scan): no
+// block barrier, no serial LDS walk.
+__device__ __forceinline__ int wave_pivot(const double* M, int ld, int m, int col) {
+  const int lane = threadIdx.x & 63;
+  double bv = -1.0;
+  int bi = 0x7fffffff;
+  if (lane >= col && lane < m) bv = fabs(M[lane * ld + col]), bi = lane;
+#pragma unroll
+  for (int s = 32; s > 0; s >>= 1) {
+    const double ov = __shfl_xor(bv, s);
+    const int oi = __shfl_xor(bi, s);
+    if (ov > bv || (ov == bv && oi < bi)) bv = ov, bi = oi;
+  }
+  return bi;
+}
+
+// One Gauss-Jordan / forward-elimination step on [M | aug] (m rows, w columns, stride ld) at column
+// col with partial pivoting, staged through registers: every thread reads the (swapped) values of
+// its elements from the old matrix, one barrier, writes the new values, one barrier.  Each element
+// gets the same operations in the same order as the one-thread elimination (pivot row normalized by
+// its pivot / rows below eliminated by f = M'[r][col] / M'[col][col]).
+template <bool GJ>
+__device__ __forceinline__ void elim_step(double* M, int ld, int m, int w, int col) {
+  const int piv = wave_pivot(M, ld, m, col);
+  constexpr int kE = (2 * kM) * (4 * kM + 1) / kT + 1;  // elements per thread
+  double nv[kE];
+  const double pv = M[piv * ld + col];  // M'[col][col]
+#pragma unroll
+  for (int k = 0; k < kE; ++k) {
+    const int e = threadIdx.x + k * kT;
+    nv[k] = 0.0;
+    if (e >= m * w) continue;
+    const int r = e / w, c = e % w;
+    const int src = r == col ? piv : (r == piv ? col : r);  // row r after the swap
+    const double x = M[src * ld + c];
+    if constexpr (GJ) {
+      const double prow = M[piv * ld + c] / pv;  // the normalized pivot row
+      if (r == col) {
+        nv[k] = prow;
+      } else {
+        const double f = M[src * ld + col];
+        nv[k] = f != 0.0 ? x - f * prow : x;
+      }
+    } else {
+      if (r > col && c >= col) {
+        const double f = M[src * ld + col] / pv;
+        nv[k] = x - f * M[piv * ld + c];
+      } else {
+        nv[k] = x;
+      }
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < kE; ++k) {
+    const int e = threadIdx.x + k * kT;
+    if (e < m * w) M[(e / w) * ld + e % w] = nv[k];
+  }
+  __syncthreads();
+}
+
 // Wave-parallel dot products: wave w takes pairs w, w + kW, ... (lanes stride the n coordinates,
 // then a fixed-order wave sum); `put(pair, value)` runs on lane 0.  No block barrier inside.
 template <class F, class P>
@@ -194,6 +256,24 @@ __device__ __forceinline__ void wave_dots(int npairs, int n, F term, P put) {
   }
 }
 
+// The same dot products for a short vector (n <= kShortN: Huber's dim is d + 2): one thread per
+// pair walks i in order -- its loads are independent, so they are all in flight at once, where the
+// wave-per-pair form pays one memory round trip (plus a wave reduction) per pair, serially per wave
+// (~1 us each: 100 pairs per wave at m = 20 made M's rebuild ~45 us and the direction ~90 us).
+constexpr int kShortN = 128;
+template <class F, class P>
+__device__ __forceinline__ void dots(int npairs, int n, F term, P put) {
+  if (n <= kShortN) {
+    for (int q = threadIdx.x; q < npairs; q += kT) {
+      double s = 0.0;
+      for (int e = 0; e < n; ++e) s += term(q, e);
+      put(q, s);
+    }
+  } else {
+    wave_dots(npairs, n, term, put);
+  }
+}
+
 // M = inv(MM) of the current history: S^T Y and S^T S by wave dot products, then Gauss-Jordan
 // with partial pivoting on [MM | I] in LDS, row operations spread over the block (each element
 // takes the same operations in the same order as the one-thread elimination)
@@ -202,15 +282,13 @@ __device__ __forceinline__ void rebuild_m(const HArgs& a, const HV& v, HCtl& C, 
   double* A = sh;            // [h][h] S^T Y
   double* SS = sh + kM * kM;  // [h][h] S^T S
   double* T = sh + 2 * kM * kM;  // [m2][2 m2] augmented [MM | I]
-  __shared__ double fac[2 * kM];
-  __shared__ int s_piv;
-  wave_dots(h * h, n,
+  dots(h * h, n,
             [&](int q, int e) {
               const int i = q / h, j = q % h;
               return v.S[(int64_t)i * n + e] * v.Y[(int64_t)j * n + e];
             },
             [&](int q, double s) { A[(q / h) * kM + q % h] = s; });
-  wave_dots(h * h, n,
+  dots(h * h, n,
             [&](int q, int e) {
               const int i = q / h, j = q % h;
               return v.S[(int64_t)i * n + e] * v.S[(int64_t)j * n + e];
@@ -236,32 +314,7 @@ __device__ __forceinline__ void rebuild_m(const HArgs& a, const HV& v, HCtl& C, 
     T[e] = val;
   }
   __syncthreads();
-  for (int col = 0; col < m2; ++col) {
-    if (threadIdx.x == 0) {
-      int piv = col;
-      for (int r = col + 1; r < m2; ++r)
-        if (fabs(T[r * w2 + col]) > fabs(T[piv * w2 + col])) piv = r;
-      s_piv = piv;
-    }
-    __syncthreads();
-    const int piv = s_piv;
-    if (piv != col)
-      for (int c = threadIdx.x; c < w2; c += kT) {
-        const double t0 = T[col * w2 + c];
-        T[col * w2 + c] = T[piv * w2 + c];
-        T[piv * w2 + c] = t0;
-      }
-    __syncthreads();
-    if (threadIdx.x < m2) fac[threadIdx.x] = T[threadIdx.x * w2 + col];
-    __syncthreads();
-    for (int c = threadIdx.x; c < w2; c += kT) T[col * w2 + c] /= fac[col];
-    __syncthreads();
-    for (int e = threadIdx.x; e < m2 * w2; e += kT) {
-      const int r = e / w2;
-      if (r != col && fac[r] != 0.0) T[e] -= fac[r] * T[col * w2 + e % w2];
-    }
-    __syncthreads();
-  }
+  for (int col = 0; col < m2; ++col) elim_step<true>(T, w2, m2, w2, col);
   for (int e = threadIdx.x; e < m2 * m2; e += kT) {
     const int r = e / m2, c = e % m2;
     v.M[r * (2 * kM) + c] = v.Ms[r * (2 * kM) + c] = T[r * w2 + m2 + c];
@@ -271,10 +324,6 @@ __device__ __forceinline__ void rebuild_m(const HArgs& a, const HV& v, HCtl& C, 
 
 __device__ __forceinline__ double mget(const HV& v, int r, int c) { return v.Ms[r * (2 * kM) + c]; }
 
-// the elimination factor of row r at column col (forward elimination of the subspace system)
-__device__ __forceinline__ void fac_of(const double* NN, int r, int col, double* f) {
-  f[r] = NN[r * kM * 2 + col] / NN[col * kM * 2 + col];
-}
 
 // generalized Cauchy point (xc) and c; then the direction into v.dir.  Returns g . dir.
 __device__ __forceinline__ double direction(const HArgs& a, const HV& v, HCtl& C, double* red, double* sh) {
@@ -297,7 +346,7 @@ __device__ __forceinline__ double direction(const HArgs& a, const HV& v, HCtl& C
     v.xc[i] = v.x[i];
   }
   __syncthreads();
-  wave_dots(m2, n, [&](int k, int i) { return wrow(v, C, n, i, k) * v.dd[i]; },
+  dots(m2, n, [&](int k, int i) { return wrow(v, C, n, i, k) * v.dd[i]; },
             [&](int k, double s) { p[k] = s, c[k] = 0.0; });
   double f1 = 0.0;
   for (int i = threadIdx.x; i < n; i += kT) f1 += v.g[i] * v.dd[i];
@@ -427,10 +476,10 @@ __device__ __forceinline__ double direction(const HArgs& a, const HV& v, HCtl& C
   __syncthreads();
   // WZ rc and WZ WZ^T over the free variables
   double* N = sh;             // [m2][2 kM]
-  double* NN = sh + 4 * kM * kM;  // [m2][2 kM]
-  wave_dots(m2, n, [&](int k, int i) { return v.done[i] != 0.0 ? wrow(v, C, n, i, k) * v.tb[i] : 0.0; },
+  double* NN = sh + 4 * kM * kM;  // [m2][2 kM + 1]: the subspace system and its right-hand side
+  dots(m2, n, [&](int k, int i) { return v.done[i] != 0.0 ? wrow(v, C, n, i, k) * v.tb[i] : 0.0; },
             [&](int k, double s) { tmp2[k] = s; });
-  wave_dots(m2 * m2, n,
+  dots(m2 * m2, n,
             [&](int q, int i) {
               const int k = q / m2, l = q % m2;
               return (l >= k && v.done[i] != 0.0) ? wrow(v, C, n, i, k) * wrow(v, C, n, i, l) : 0.0;
@@ -440,57 +489,27 @@ __device__ __forceinline__ double direction(const HArgs& a, const HV& v, HCtl& C
               if (l >= k) N[k * kM * 2 + l] = s, N[l * kM * 2 + k] = s;
             });
   __syncthreads();
-  // v = M (WZ rc);  N = I - M (WZ WZ^T) / theta;  v = N \ v (partial pivoting)
+  // v = M (WZ rc);  N = I - M (WZ WZ^T) / theta;  v = N \ v (partial pivoting) on [N | v]
+  constexpr int LA = 2 * kM + 1;  // row stride of the augmented system (v is column m2)
   __shared__ double vv[2 * kM];
-  __shared__ int s_piv;
   if (threadIdx.x < m2) {
     double s = 0.0;
     for (int q = 0; q < m2; ++q) s += mget(v, threadIdx.x, q) * tmp2[q];
-    vv[threadIdx.x] = s;
+    NN[threadIdx.x * LA + m2] = s;
   }
   for (int e = threadIdx.x; e < m2 * m2; e += kT) {
     const int r = e / m2, q = e % m2;
     double z = 0.0;
     for (int k = 0; k < m2; ++k) z += mget(v, r, k) * (N[k * kM * 2 + q] * it);
-    NN[r * kM * 2 + q] = (r == q ? 1.0 : 0.0) - z;
+    NN[r * LA + q] = (r == q ? 1.0 : 0.0) - z;
   }
   __syncthreads();
-  for (int col = 0; col < m2; ++col) {
-    if (threadIdx.x == 0) {
-      int piv = col;
-      for (int r = col + 1; r < m2; ++r)
-        if (fabs(NN[r * kM * 2 + col]) > fabs(NN[piv * kM * 2 + col])) piv = r;
-      s_piv = piv;
-    }
-    __syncthreads();
-    const int piv = s_piv;
-    if (piv != col) {
-      for (int q = threadIdx.x; q < m2; q += kT) {
-        const double t0 = NN[col * kM * 2 + q];
-        NN[col * kM * 2 + q] = NN[piv * kM * 2 + q];
-        NN[piv * kM * 2 + q] = t0;
-      }
-      if (threadIdx.x == 0) {
-        const double t1 = vv[col];
-        vv[col] = vv[piv];
-        vv[piv] = t1;
-      }
-    }
-    __syncthreads();
-    if (threadIdx.x > col && threadIdx.x < m2) fac_of(NN, threadIdx.x, col, tmp);
-    __syncthreads();
-    for (int e = threadIdx.x; e < m2 * m2; e += kT) {
-      const int r = e / m2, q = e % m2;
-      if (r > col && q >= col) NN[r * kM * 2 + q] -= tmp[r] * NN[col * kM * 2 + q];
-    }
-    if (threadIdx.x > col && threadIdx.x < m2) vv[threadIdx.x] -= tmp[threadIdx.x] * vv[col];
-    __syncthreads();
-  }
+  for (int col = 0; col < m2; ++col) elim_step<false>(NN, LA, m2, m2 + 1, col);
   if (threadIdx.x == 0) {
     for (int r = m2 - 1; r >= 0; --r) {
-      double s = vv[r];
-      for (int q = r + 1; q < m2; ++q) s -= NN[r * kM * 2 + q] * vv[q];
-      vv[r] = s / NN[r * kM * 2 + r];
+      double s = NN[r * LA + m2];
+      for (int q = r + 1; q < m2; ++q) s -= NN[r * LA + q] * vv[q];
+      vv[r] = s / NN[r * LA + r];
     }
   }
   __syncthreads();

@@ -123,6 +123,12 @@ for s in $STEPS; do
     csvstr) step csvstr 600 python scripts/csv_strings_bench.py --rows ${CSVSTR_ROWS:-1e7} ;;
     pipedepth) for r in 1 2; do for m in 2 3 4; do
             step pipedepth_${m}_r${r} 300 env DQ4ML_FIT_PIPELINE=$m python bench.py --steps 200 --warmup 20 --rows 1.25e7 || exit $?; done; done ;;
+    huber) step huber_t 300 python -u -m pytest tests/test_gpu_huber_qn.py -m gpu -q --timeout 150 --timeout-method thread &&
+           step huber_dev 300 python benchmarks/bench_huber.py --steps 5 --json-out gpurun_out/huber_dev.json &&
+           step huber_host 300 python benchmarks/bench_huber.py --steps 5 --host --json-out gpurun_out/huber_host.json &&
+           step huber_dev_small 300 python benchmarks/bench_huber.py --steps 5 --rows 1e5 --json-out gpurun_out/huber_dev_small.json &&
+           step huber_host_small 300 python benchmarks/bench_huber.py --steps 5 --rows 1e5 --host --json-out gpurun_out/huber_host_small.json &&
+           (export TMPDIR=/tmp; step huber_prof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/huber_prof -o run --output-format csv -- python benchmarks/bench_huber.py --steps 2) || exit $? ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" ;;
     bench) step bench 600 python bench.py --steps 20 --warmup 3 ;;
     benchasync) step benchasync 600 python bench.py --steps 20 --warmup 3 --async ;;
