@@ -118,6 +118,33 @@ def test_device_huber_options(gpu_session, kw):
         assert len(dev.summary.objectiveHistory) == len(host.summary.objectiveHistory) == 4
 
 
+@pytest.mark.parametrize("layout", ["tiled_bf16", "wide_fp8", "wide_bf16_d40"])
+def test_device_huber_fragment_layouts(gpu_session, layout):
+    """The generic fused pass (fragment-tiled storage, d <= 16: ``huber_rows_kernel<16>``) and the
+    chunked X^T m above it on narrow wide tiles, with shifted storage, against the host LBFGSB."""
+    import torch
+
+    from net.jgp.labs.sparkdq4ml_amd.ops import device
+
+    d = 40 if layout.endswith("d40") else 12
+    n = 30_011
+    g = torch.Generator().manual_seed(d + 3)
+    X = (torch.randn(d, n, generator=g) * (0.5 + torch.rand(d, 1, generator=g)) + 1.5).cuda()
+    beta = torch.linspace(-1.0, 2.0, d).cuda()
+    y = (beta @ X + 0.7 + 0.2 * torch.randn(n, generator=g).cuda()).double()
+    y[::37] += 25.0
+    if layout == "tiled_bf16":
+        T = device.pack_tiled([X], None, shift="auto")
+    else:
+        T = device.pack_wide([X], 8 if layout == "wide_fp8" else 16, None, shift="auto")
+    df = gpu_session.createDataFrame({"features": T, "label": y})
+    kw = dict(maxIter=60, regParam=0.02)
+    dev = _fit(gpu_session, df, kw, True)
+    host = _fit(gpu_session, df, kw, False)
+    assert getattr(dev, "_huber_evaluations", None)
+    _close(dev, host, hist_rtol=1e-6)
+
+
 def test_device_huber_weights_and_filter(gpu_session):
     """Instance weights (``weightCol``) and a DQ-style row filter (the selection vector the pass
     skips) on the device path, against the host-steered optimizer on the same frame."""
