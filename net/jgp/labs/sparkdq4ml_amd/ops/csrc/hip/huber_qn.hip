@@ -644,17 +644,8 @@ __global__ __launch_bounds__(kT) void huber_qn_init_kernel(HArgs a) {
   if (threadIdx.x == 0) *v.C = C;
 }
 
-__global__ __launch_bounds__(kT) void huber_qn_ctl_kernel(HArgs a) {
-  __shared__ double red[2 * kW];
-  __shared__ double sh[4 * kM * kM + 2 * kM * 4 * kM];
-  __shared__ double Ms[4 * kM * kM];
-  __shared__ HCtl C;
-  HV v = views(a);
-  v.Ms = Ms;
-  if (threadIdx.x == 0) C = *v.C;
-  __syncthreads();
-  if (C.act != kHuberEval) return;  // done: evaluations enqueued past the end
-  for (int e = threadIdx.x; e < 4 * kM * kM; e += kT) Ms[e] = v.M[e];
+// The control step (one evaluation consumed): everything between the kernel's state load and store.
+__device__ __forceinline__ void ctl_body(const HArgs& a, const HV& v, HCtl& C, double* red, double* sh) {
   const double f = eval_of(a, v, red);
   double dd = 0.0;
   for (int i = threadIdx.x; i < a.dim; i += kT) dd += v.ge[i] * v.dir[i];
@@ -803,6 +794,51 @@ __global__ __launch_bounds__(kT) void huber_qn_ctl_kernel(HArgs a) {
   next_search(a, v, C, red, sh);
   __syncthreads();
   if (threadIdx.x == 0) *v.C = C;
+}
+
+// Huber's short vectors (dim <= kShortN): the per-coordinate state and the s / y memory live in LDS
+// for the call (one copy in, one copy out): every wrow / dot product / vector loop of the step then
+// reads LDS instead of paying a memory round trip per access.
+constexpr int kLocalDoubles = (9 + 2 * kM) * kShortN;
+
+__global__ __launch_bounds__(kT) void huber_qn_ctl_kernel(HArgs a) {
+  __shared__ double red[2 * kW];
+  __shared__ double sh[4 * kM * kM + 2 * kM * 4 * kM];
+  __shared__ double Ms[4 * kM * kM];
+  __shared__ double vl[kLocalDoubles];
+  __shared__ HCtl C;
+  HV v = views(a);
+  v.Ms = Ms;
+  if (threadIdx.x == 0) C = *v.C;
+  __syncthreads();
+  if (C.act != kHuberEval) return;  // done: evaluations enqueued past the end
+  for (int e = threadIdx.x; e < 4 * kM * kM; e += kT) Ms[e] = v.M[e];
+  const int n = a.dim;
+  const bool local = n <= kShortN;
+  const int64_t nv = (9 + 2 * kM) * (int64_t)n;  // x .. done, S, Y: contiguous after the control block
+  double* gv = v.x;
+  if (local) {
+    for (int64_t e = threadIdx.x; e < nv; e += kT) vl[e] = gv[e];
+    HV w = v;
+    double* p = vl;
+    w.x = p, p += n;
+    w.g = p, p += n;
+    w.dir = p, p += n;
+    w.xe = p, p += n;
+    w.ge = p, p += n;
+    w.xc = p, p += n;
+    w.tb = p, p += n;
+    w.dd = p, p += n;
+    w.done = p, p += n;
+    w.S = p, p += (int64_t)kM * n;
+    w.Y = p;
+    v = w;
+  }
+  __syncthreads();
+  ctl_body(a, v, C, red, sh);
+  __syncthreads();
+  if (local)
+    for (int64_t e = threadIdx.x; e < nv; e += kT) gv[e] = vl[e];
 }
 
 HArgs make(int d, bool fit_icpt, int max_iter, double tol, int hist_cap, const double* sx, const double* lam,
