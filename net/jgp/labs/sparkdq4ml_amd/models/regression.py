@@ -640,7 +640,11 @@ def _tail_stream(dev, wide: bool = False) -> "torch.cuda.Stream":
     priority (a CU-masked stream over every CU) lost in a same-process A/B, 10.45-10.51 against
     8.97-9.01 ms per fit (profiles/r6/wide_tail_ab.log, profiles/r6_wide_async.md): the tail's fold
     then interleaves with the next fit's SYRK and stalls its gang rounds; at high priority the
-    fold drains first, and the LDS-free PCG runs beside the SYRK."""
+    fold drains first, and the LDS-free PCG runs beside the SYRK.
+
+    The tall (d <= 64) fits' tail gets a high-priority stream too: with every collective forced
+    through RCCL the 1.25e7-row shard ran 0.158 -> 0.149-0.152 ms per fit, single-GPU 0.130 -> 0.129
+    and 1e8 rows 1.018-1.026 -> 1.018 (same-box A/B, profiles/r6/tall_tail_prio_ab.log)."""
     masks = _tail_masks(dev)
     key = (dev, masks is not None, wide)
     st = _tail_streams.get(key)
@@ -648,7 +652,7 @@ def _tail_stream(dev, wide: bool = False) -> "torch.cuda.Stream":
         if masks is not None:
             st = streams.cu_masked_stream(masks[1], masks[2], dev, tag=98 if wide else 99)
         else:
-            st = torch.cuda.Stream(device=dev, priority=-1) if wide else torch.cuda.Stream(device=dev)
+            st = torch.cuda.Stream(device=dev, priority=-1)
         _tail_streams[key] = st
     return st
 
