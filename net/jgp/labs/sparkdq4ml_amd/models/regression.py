@@ -563,14 +563,19 @@ _pipe_streams = {}
 
 def _pipe_stream(df, tbl):
     """Compute stream for this asynchronous fit's statistics pass (``dq4ml.fit.pipeline``, default
-    2): consecutive fits alternate over that many streams, each ordered after the caller's stream,
-    so fit k+1's Gram blocks start on the CUs that fit k's drain frees instead of waiting for
-    fit k's last block (the drain and launch are most of the ~25 us fixed cost of a pass).  Every
-    fit still runs its whole pass; results are per fit and unchanged.  None: the caller's stream."""
+    2, or 3 with collectives): consecutive fits alternate over that many streams, each ordered after
+    the caller's stream, so fit k+1's Gram blocks start on the CUs that fit k's drain frees instead
+    of waiting for fit k's last block (the drain and launch are most of the ~25 us fixed cost of a
+    pass).  Data-parallel fits fold on their compute stream before the all-reduce, which holds that
+    stream ~100 us while the next pass streams HBM: a third stream keeps a pass in flight meanwhile
+    (forced-RCCL shard 0.151 -> 0.143 ms per fit; without collectives depth 3 loses, 0.130 -> 0.133,
+    profiles/r6/pipeline_depth_ab.log).  Every fit still runs its whole pass; results are per fit
+    and unchanged.  None: the caller's stream."""
     if not _async_conf(df):
         return None
     sess = df.sparkSession
-    depth = int(os.environ.get("DQ4ML_FIT_PIPELINE") or sess.conf.get("dq4ml.fit.pipeline", "2"))
+    depth = int(os.environ.get("DQ4ML_FIT_PIPELINE")
+                or sess.conf.get("dq4ml.fit.pipeline", "3" if comm.collectives_active() else "2"))
     dev = getattr(sess, "device", None)
     if depth < 2 or dev is None or dev.type != "cuda":
         return None
