@@ -137,7 +137,7 @@ def _check_constant_label(raw_ys: float, reg: float) -> None:
 
 def _device_qn_ok(df, P) -> bool:
     """The whole fit on the device: wide tiles on a GPU, no optimizer checkpoints (those read the
-    state on the host every few iterations).  One rank: ONE cooperative launch
+    state on the host every few iterations).  One rank: ONE grid launch
     (``LsqPasses.qn_fit``); with collectives active: the data-parallel form
     (``LsqPasses.qn_fit_dp``: pass, fold, all-reduce, control kernel per evaluation)."""
     sess = getattr(df, "sparkSession", None)
@@ -188,7 +188,7 @@ def _train_passes(est, df, X, y, w, sel, d, checks=(), device_qn=True):
     evaluation: summarizer moments -> standardization / regularization constants -> Breeze
     L-BFGS (L2) or OWLQN (L1 > 0) over ``LeastSquaresCostFun`` -> un-standardize.
 
-    On one GPU with wide tiles the whole sequence is ONE cooperative launch (``lsq_qn.hip``: one
+    On one GPU with wide tiles the whole sequence is ONE grid launch (``lsq_qn.hip``: one
     fused data pass per evaluation, the line search on the device), enqueued with the summarizer
     pass; with ``dq4ml.fit.async`` the fit returns at once.  Otherwise the Breeze state stays on
     the device and the host steers (``models/qn_device.py``)."""

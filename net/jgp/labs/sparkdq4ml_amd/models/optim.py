@@ -219,7 +219,7 @@ QN_DEVICE_MAX_K = 4608  # kWlsQnGridMaxK (wls_small.h): the device OWLQN's large
 def wls_owlqn_device(flat, nf, fit_intercept, reg_param, elastic_net, standardize_features, standardize_label,
                      max_iter, tol):
     """The OWLQN branch with the statistics on the device: one wave for k <= 128
-    (``wls_qn_kernel``), one cooperative grid launch up to ``QN_DEVICE_MAX_K`` (``wls_qn_grid.hip``);
+    (``wls_qn_kernel``), one co-resident grid launch up to ``QN_DEVICE_MAX_K`` (``wls_qn_grid.hip``);
     one D2H of the result.  None = the native host driver owns the case (k beyond the grid
     solver, or a short-circuit the kernel hands back).  (The round-2/3 host-steered torch OWLQN,
     kept for A/B, lost at every k: profiles/r3_owlqn_grid.md; removed in round 4.)"""

@@ -544,7 +544,7 @@ def _async_fit(df, flat, d, args) -> bool:
         return False
     _, _, fit_icpt, reg, enet = args[:5]
     # L1 (OWLQN, the lab's own regParam=1 / elasticNetParam=1) runs on the device too: one wave
-    # for k <= 128, one cooperative grid launch up to QN_DEVICE_MAX_K (wls_qn_grid.hip)
+    # for k <= 128, one co-resident grid launch up to QN_DEVICE_MAX_K (wls_qn_grid.hip)
     from .optim import QN_DEVICE_MAX_K
 
     if enet != 0.0 and reg != 0.0:

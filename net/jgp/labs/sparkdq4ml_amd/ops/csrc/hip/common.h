@@ -169,4 +169,40 @@ __device__ __forceinline__ double wave_sum_f64(double v) {
   return v;
 }
 
+// Grid-wide barrier of a plain launch whose blocks are co-resident (at most one block per CU, as
+// the launchers size it).  bar = [arrivals, abandoned], zeroed by a stream-ordered memset before
+// the launch; gen counts the barriers this block has passed (thread 0's copy).  Writes before the
+// barrier are released at agent scope (L2 write-back across the XCDs) and acquired after it.  A
+// wait longer than kGridSpin polls (seconds) marks the barrier abandoned: every later barrier of
+// the launch passes at once, the kernel drains, and the launcher's status word reports it.
+// (hipLaunchCooperativeKernel gave the same guarantee through a dedicated runtime queue whose
+// teardown crashed rocprofv3 at process exit: profiles/r6_coop_exit.md.)
+constexpr unsigned kGridSpin = 1u << 22;
+
+__device__ __forceinline__ void grid_barrier(unsigned* bar, unsigned& gen, unsigned nblocks) {
+  __threadfence();  // release: every thread's writes (the fence's L2 write-back), then the arrival
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned target = ++gen * nblocks;
+    __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // relaxed polls: an acquiring load would invalidate the XCD's L2 on every poll, under the
+    // blocks of that XCD still re-reading their tiles from it (the l-bfgs pass: 9.30 ms per
+    // evaluation with acquiring polls)
+    for (unsigned it = 0; __hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target; ++it) {
+      if (__hip_atomic_load(bar + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) break;
+      if (it >= kGridSpin) {
+        __hip_atomic_store(bar + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+  }
+  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // once, after the wait
+}
+
+__device__ __forceinline__ bool grid_abandoned(const unsigned* bar) {
+  return __hip_atomic_load(bar + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
+}
+
 }  // namespace dq4ml

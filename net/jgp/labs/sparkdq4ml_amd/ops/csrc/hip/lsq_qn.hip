@@ -1,6 +1,6 @@
 // K9 on the device end to end: the squared-loss l-bfgs / OWLQN fit of LinearRegression
 // (solver="l-bfgs", or "auto" with numFeatures > 4096: DataQuality4MachineLearningApp.java:120-126,
-// SURVEY.md S13/K9) as ONE cooperative launch over the HBM-resident wide tiles.  Round 3 ran every
+// SURVEY.md S13/K9) as ONE grid launch over the HBM-resident wide tiles.  Round 3 ran every
 // cost evaluation as two streaming kernels (margins, then column sums: X read twice) and steered
 // the Breeze line search from the host (one D2H per evaluation), so an l-bfgs fit could never be
 // asynchronous.  Here:
@@ -26,7 +26,6 @@
 // effective coefficients go to LDS), a distributed fixed-order fold of the per-block column slabs.
 // Loop passes are bounded by hist_cap and every line search by 21 (backtracking) or 20 (strong
 // Wolfe) evaluations, so the kernel terminates on any input.
-#include <hip/hip_cooperative_groups.h>
 #include <hip/hip_runtime.h>
 
 #include "common.h"
@@ -37,8 +36,6 @@
 namespace dq4ml {
 
 namespace {
-
-namespace cg = cooperative_groups;
 
 constexpr int kT = 512;
 constexpr int kW = kT / kWave;
@@ -140,6 +137,7 @@ struct QnArgs {
   // Σ ½ w diff², Σ v]
   Ctl* ctl;
   double* red;
+  unsigned* gbar;  // the one-launch form's grid barrier [arrivals, abandoned] (grid_barrier)
 };
 
 __device__ void ctl_record(Ctl& C, const QnArgs& a, double* hist) {
@@ -711,7 +709,8 @@ __device__ void finalize_block(const QnArgs& a, const Ctl& C, const Std& S, doub
 
 template <int L, int TPW>
 __global__ __launch_bounds__(kT, 1) void lsq_qn_kernel(QnArgs a) {
-  cg::grid_group grid = cg::this_grid();
+  unsigned gen = 0;
+  auto grid_sync = [&]() { grid_barrier(a.gbar, gen, gridDim.x); };
   constexpr int E = L == 3 ? 16 : 8;
   constexpr int NC = 8 * TPW * 32;  // coefficient slots (tiles padded to whole wave strides)
   __shared__ double colacc[NC];  // the block's f64 column sums (<= 128 KiB)
@@ -739,19 +738,19 @@ __global__ __launch_bounds__(kT, 1) void lsq_qn_kernel(QnArgs a) {
   }
   for (int64_t r = (int64_t)b * kT + t; r < a.n; r += (int64_t)B * kT) a.mvec[r] = 0.0, a.dvec[r] = 0.0;  // x0 = 0
   __threadfence();
-  grid.sync();
+  grid_sync();
 
   // ---- one cost evaluation at x + alpha dir (mode 1, projected for OWLQN) or at x0 = 0 -------
   auto evaluate = [&](int mode, double alpha) -> Eval {
     // E1: block 0 builds the trial point, the f32 effective coefficients and the margin offset
     if (b == 0) build_trial(a, S, mode, alpha, NC, red);
     for (int j = t; j < NC; j += kT) colacc[j] = 0.0;
-    grid.sync();
+    grid_sync();
     // E2: the fused pass
     qn_pass<L, TPW>(a, S, mode, alpha, !owlqn && mode == 1 && C.first, 0.0, a.scal[16], colacc, mrow, vrow, red,
                     b, B);
     __threadfence();
-    grid.sync();
+    grid_sync();
 
     // E3: fixed-order fold of the slabs over this block's features -> gradient, adjusted gradient
     // (grid totals: wave 0, lane l sums entries l, l + 64, ...; the same order in every block)
@@ -794,7 +793,7 @@ __global__ __launch_bounds__(kT, 1) void lsq_qn_kernel(QnArgs a) {
       }
     }
     __threadfence();
-    grid.sync();
+    grid_sync();
     if (wave == 0) {
       double q[kDParts] = {0.0, 0.0, 0.0, 0.0};
       for (int i = lane; i < B; i += kWave)
@@ -838,19 +837,20 @@ __global__ __launch_bounds__(kT, 1) void lsq_qn_kernel(QnArgs a) {
     } else {  // kActApply
       double* scal = a.scal + 8 * (C.pass & 1);  // parity: a pass with no evaluation has no barrier after the read
       if (b == 0) apply_dir(a, C, scal, red, owlqn);
-      grid.sync();
+      grid_sync();
       if (t == 0) ctl_start_search(C, scal, a, b == 0 ? a.out + d + 11 : nullptr);
     }
     __syncthreads();
   }
   if (b != 0) return;
   finalize_block(a, C, S, red);
+  if (t == 0 && grid_abandoned(a.gbar)) a.out[d + 1] = 9.0;  // not finished: the host path re-runs
 }
 
 // ---- data-parallel form (X4): the same fit split at the reduction ---------------------------
 // Spark's l-bfgs sums every evaluation's loss and gradient over the partitions (treeAggregate,
 // DataQuality4MachineLearningApp.java:120-126); across ranks that is an RCCL all-reduce, which a
-// cooperative launch cannot contain.  Per evaluation the host enqueues, on one stream with no
+// single grid launch cannot contain.  Per evaluation the host enqueues, on one stream with no
 // host read in between:
 //   lsq_qn_dp_pass_kernel  (grid)    the fused E2 pass over this rank's rows -> per-block slabs
 //   lsq_qn_dp_fold_kernel  (d / 64)  fixed-order slab fold -> red = [Σ v x_j (d), loss, Σ v]
@@ -1033,12 +1033,12 @@ int lsq_qn_blocks(int layout, int d) {
   DQ_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
   DQ_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, pick(layout, tpw_of(d)), kT, 0));
   if (per < 1) throw std::runtime_error("lsq_qn: the kernel does not fit a CU");
-  return cus;  // one block per CU (co-resident: the cooperative launch checks it)
+  return cus;  // one block per CU: the grid is co-resident (grid_barrier relies on it)
 }
 
 int64_t lsq_qn_work(int d, int blocks, int64_t n) {
   const int64_t slab = 8LL * tpw_of(d) * 32;
-  return 12LL * d + 2LL * kMem * d + (int64_t)blocks * slab + 2LL * blocks + (int64_t)blocks * kDParts + 24 +
+  return 12LL * d + 2LL * kMem * d + (int64_t)blocks * slab + 2LL * blocks + (int64_t)blocks * kDParts + 24 + 1 +
          (8LL * tpw_of(d) * 32 + 1) / 2 + 2 * n;
 }
 
@@ -1076,6 +1076,7 @@ QnArgs make_args(const LsqX& x, const double* y, const double* w, const double* 
   a.lpart = take(2LL * blocks);
   a.dpart = take((int64_t)blocks * kDParts);
   a.scal = take(24);
+  a.gbar = reinterpret_cast<unsigned*>(take(1));
   a.cs = reinterpret_cast<float*>(take((8LL * tpw * 32 + 1) / 2));
   a.mvec = take(x.n), a.dvec = take(x.n);
   if (dp) {
@@ -1116,7 +1117,9 @@ void lsq_qn(const LsqX& x, const double* y, const double* w, const double* scale
   QnArgs a = make_args(x, y, w, scale, shift, head, fit_icpt, std_f, reg, enet, max_iter, tol, hist_cap, work, blocks,
                        out, false);
   void* args[] = {&a};
-  DQ_HIP_CHECK(hipLaunchCooperativeKernel(pick(x.layout, tpw_of(x.d)), dim3(blocks), dim3(kT), args, 0, st));
+  // a plain launch of a co-resident grid (one block per CU, lsq_qn_blocks) with its own barrier
+  DQ_HIP_CHECK(hipMemsetAsync(a.gbar, 0, 2 * sizeof(unsigned), st));
+  DQ_HIP_CHECK(hipLaunchKernel(pick(x.layout, tpw_of(x.d)), dim3(blocks), dim3(kT), args, 0, st));
 }
 
 int64_t lsq_qn_dp_work(int d, int blocks, int64_t n) { return lsq_qn_work(d, blocks, n) + d + 2 + kCtlDoubles; }

@@ -1,13 +1,13 @@
 // K6: the OWLQN branch of WeightedLeastSquares (regParam > 0, elasticNetParam > 0: the lab's own
 // LinearRegression at DataQuality4MachineLearningApp.java:120-126) for
-// 128 < k <= kWlsQnGridMaxK, entirely on the device: ONE cooperative launch runs standardize ->
+// 128 < k <= kWlsQnGridMaxK, entirely on the device: ONE grid launch runs standardize ->
 // Breeze OWLQN -> un-standardize with no host round trip, so an L1 fit at any k the tall path
 // reaches can be asynchronous.  Same algorithm and decisions as the one-wave wls_qn_kernel
 // (wls_small.hip) and the host driver (csrc/host/solvers.cpp): m = 10 two-loop recursion on the
 // pseudo-gradient, orthant projection, backtracking line search seeded with 0.5 / |g| on the first
 // iteration, FunctionValuesConverged over 20 values, one history reset on a failed search.
 //
-// Work split (one block per CU, grid-wide barriers from cooperative groups):
+// Work split (one block per CU, co-resident; grid-wide barriers by common.h grid_barrier):
 //  * the dense standardized k x k system lives in HBM (134 MB at k = 4097 -- MALL resident);
 //    block b owns rows [b R, b R + R) and computes their part of every A x (all threads stride
 //    the columns of a row, several rows' loads in flight, the full trial point staged in LDS);
@@ -23,7 +23,6 @@
 // search by 21 evaluations, so the kernel terminates on any input (NaNs included).
 // out = [coef(nf), intercept, status, count, wSum, wwSum, bSum, bbSum, H, reason, history(H)] --
 // the wls_qn_small layout (ops/device.py, models/optim.py owlqn_result read both).
-#include <hip/hip_cooperative_groups.h>
 #include <hip/hip_runtime.h>
 
 #include "common.h"
@@ -32,8 +31,6 @@
 namespace dq4ml {
 
 namespace {
-
-namespace cg = cooperative_groups;
 
 constexpr int kQT = 512;  // threads per block
 constexpr int kQW = kQT / kWave;
@@ -62,7 +59,8 @@ __global__ __launch_bounds__(kQT) void wls_qn_grid_kernel(const double* __restri
                                                           double reg, double enet, int std_f, int std_l, int max_iter,
                                                           double tol, int hist_cap, WlsQnWork w,
                                                           double* __restrict__ out) {
-  cg::grid_group grid = cg::this_grid();
+  unsigned gen = 0;
+  auto grid_sync = [&]() { grid_barrier(w.gbar, gen, gridDim.x); };
   extern __shared__ double sm[];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const int B = gridDim.x, b = blockIdx.x;
@@ -104,7 +102,7 @@ __global__ __launch_bounds__(kQT) void wls_qn_grid_kernel(const double* __restri
     w.l1[i] = l;
   }
   __threadfence();
-  grid.sync();
+  grid_sync();
   for (int r = r0; r < r1; ++r)
     for (int j = t; j < k; j += kQT) {
       double v;
@@ -209,7 +207,7 @@ __global__ __launch_bounds__(kQT) void wls_qn_grid_kernel(const double* __restri
       if (t == 0) slab[q] = s;
     }
     __threadfence();
-    grid.sync();
+    grid_sync();
     const double* all = w.part + (int64_t)parity * B * kParts;
     double s[kParts] = {0.0, 0.0, 0.0, 0.0, 0.0};
     for (int i = 0; i < B; ++i)
@@ -371,7 +369,7 @@ __global__ __launch_bounds__(kQT) void wls_qn_grid_kernel(const double* __restri
       }
     }
     __threadfence();
-    grid.sync();
+    grid_sync();
     const double initd = scal[0], gg = scal[1];
     bool fail = scal[2] != 0.0;
     double alpha = 0.0, nv = 0.0, nadj = 0.0, nagag = 0.0;
@@ -432,7 +430,7 @@ __global__ __launch_bounds__(kQT) void wls_qn_grid_kernel(const double* __restri
   }
   if (t == 0) {
     if (!fit_intercept) out[nf] = 0.0;
-    out[nf + 1] = 0.0;
+    out[nf + 1] = grid_abandoned(w.gbar) ? 9.0 : 0.0;  // 9: not finished (the host path re-runs)
     out[nf + 7] = (double)H;
     out[nf + 8] = (double)why;
   }
@@ -447,7 +445,7 @@ size_t qn_lds(int k, int blocks) {
 }  // namespace
 
 int64_t wls_qn_grid_work(int k, int blocks) {
-  return (int64_t)k * k + (int64_t)k * (13 + 2 * kMem) + (int64_t)2 * blocks * kParts + 8;
+  return (int64_t)k * k + (int64_t)k * (13 + 2 * kMem) + (int64_t)2 * blocks * kParts + 8 + 1;
 }
 
 int wls_qn_grid_blocks(int k) {
@@ -456,7 +454,7 @@ int wls_qn_grid_blocks(int k) {
   DQ_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
   DQ_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, wls_qn_grid_kernel<9>, kQT, qn_lds(k, cus)));
   if (per < 1) throw std::runtime_error("wls_qn_grid: the kernel does not fit a CU");
-  const int nb = cus;        // one block per CU: co-resident (the cooperative launch checks it)
+  const int nb = cus;        // one block per CU: co-resident (grid_barrier relies on it)
   const int rows_min = 4;    // at least a few rows per block
   const int want = (k + rows_min - 1) / rows_min;
   const int blocks = nb < want ? nb : (want < 1 ? 1 : want);
@@ -489,13 +487,17 @@ void wls_qn_grid(const double* flat, int nf, int fit_intercept, double reg, doub
   w.S = take((int64_t)kMem * k), w.Y = take((int64_t)kMem * k);
   w.part = take((int64_t)2 * blocks * kParts);
   w.scal = take(8);
+  w.gbar = reinterpret_cast<unsigned*>(take(1));
   const size_t lds = qn_lds(k, blocks);
   void* args[] = {&flat, &nf, &fit_intercept, &reg, &enet, &std_f, &std_l, &max_iter, &tol, &hist_cap, &w, &out};
   const void* kern = k <= kQT       ? (const void*)wls_qn_grid_kernel<1>
                      : k <= 2 * kQT ? (const void*)wls_qn_grid_kernel<2>
                      : k <= 4 * kQT ? (const void*)wls_qn_grid_kernel<4>
                                     : (const void*)wls_qn_grid_kernel<9>;
-  DQ_HIP_CHECK(hipLaunchCooperativeKernel(kern, dim3(blocks), dim3(kQT), args, (unsigned)lds, st));
+  // a plain launch of a co-resident grid (at most one block per CU, wls_qn_grid_blocks) with its
+  // own barrier
+  DQ_HIP_CHECK(hipMemsetAsync(w.gbar, 0, 2 * sizeof(unsigned), st));
+  DQ_HIP_CHECK(hipLaunchKernel(kern, dim3(blocks), dim3(kQT), args, (unsigned)lds, st));
 }
 
 }  // namespace dq4ml

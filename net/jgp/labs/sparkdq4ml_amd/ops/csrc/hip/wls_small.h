@@ -24,6 +24,7 @@ void wls_qn_small(const double* flat, int nf, int fit_intercept, double reg, dou
 constexpr int kWlsQnGridMaxK = 4608;
 struct WlsQnWork {
   double *A, *ab, *l1, *bar, *sstd, *x, *g, *ag, *d, *cx, *cg, *cag, *S, *Y, *part, *scal;
+  unsigned* gbar;  // grid barrier [arrivals, abandoned] (common.h grid_barrier)
 };
 int64_t wls_qn_grid_work(int k, int blocks);
 int wls_qn_grid_blocks(int k);

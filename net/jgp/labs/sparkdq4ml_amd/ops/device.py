@@ -921,7 +921,7 @@ class LsqPasses:
 
     def qn_fit(self, head: torch.Tensor, fit_icpt: bool, std_f: bool, reg: float, enet: float, max_iter: int,
                tol: float) -> Optional[torch.Tensor]:
-        """The whole squared-loss l-bfgs / OWLQN fit as ONE cooperative launch (``lsq_qn.hip``):
+        """The whole squared-loss l-bfgs / OWLQN fit as ONE grid launch (``lsq_qn.hip``):
         standardization from the summarizer ``head`` ([scalars(5), moments(2d)], on the device),
         one fused data pass per cost evaluation, the Breeze control flow on the device.  Enqueued
         on the current stream, no host sync.  Returns ``[coef(d), intercept, status, reason, H,
@@ -1045,7 +1045,7 @@ def wls_qn_small(flat: torch.Tensor, nf: int, fit_intercept: bool, reg: float, e
     """Device OWLQN (L1 WLS) from the flat statistics, enqueued on the current stream, no host
     round trip: ``[coef(nf), intercept, status, count, wSum, wwSum, bSum, bbSum, H, reason,
     history...]``.  k <= 128: one wave (``wls_qn_kernel``); up to ``WLS_QN_GRID_MAX_K``: one
-    cooperative grid launch (``wls_qn_grid.hip``) with its scratch allocated here."""
+    co-resident grid launch (``wls_qn_grid.hip``) with its scratch allocated here."""
     h = native.hip()
     _check_dev(flat)
     k = nf + 1 if fit_intercept else nf

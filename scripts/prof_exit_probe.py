@@ -50,6 +50,9 @@ def main():
 
         rc = ctypes.CDLL("libamdhip64.so").hipDeviceReset()
         print("hipDeviceReset", rc, flush=True)
+    if os.environ.get("PROBE_MAPS"):  # the process map, to place the crash's PCs in their libraries
+        with open("/proc/self/maps") as f, open(os.environ["PROBE_MAPS"], "w") as o:
+            o.write(f.read())
     print("probe done", flush=True)
 
 
