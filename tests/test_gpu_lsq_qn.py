@@ -1,4 +1,4 @@
-"""the squared-loss l-bfgs / OWLQN fit as ONE cooperative launch (``lsq_qn.hip``:
+"""the squared-loss l-bfgs / OWLQN fit as ONE grid launch (``lsq_qn.hip``:
 standardization from the device summarizer head, one fused data pass per cost evaluation, the
 Breeze line searches on the device) against the host-steered path (``models/qn_device.py`` over
 the two-pass ``lsq.hip`` evaluations, ``DQ4ML_LSQ_QN=0``) on the wide bf16 / fp8 tiles; an
@@ -76,7 +76,7 @@ def test_device_qn_matches_host_steered(gpu_session, monkeypatch, eb, d, n, kw):
     lr = LinearRegression(solver="l-bfgs", maxIter=60, tol=1e-9, **kw)
     m_dev = _fit(lr, df, monkeypatch, True)
     assert m_dev.summary.solver == ("owlqn" if kw["elasticNetParam"] else "l-bfgs")
-    # the cooperative lsq_qn launch ran (set only by its pending result, lbfgs_path._PendingLsq)
+    # the one-launch lsq_qn fit ran (set only by its pending result, lbfgs_path._PendingLsq)
     assert m_dev._qn_evaluations is not None and m_dev._qn_evaluations > 0
     m_host = _fit(lr, df, monkeypatch, False)
     assert getattr(m_host, "_qn_evaluations", None) is None  # the host-steered path really ran
@@ -137,6 +137,29 @@ def test_device_qn_constant_label_takes_the_host_semantics(gpu_session, monkeypa
     assert float(m.intercept) == pytest.approx(3.25)
 
 
+def test_device_qn_grid_barrier_is_bounded_when_the_grid_is_not_co_resident(monkeypatch):
+    """``grid_barrier`` (common.h) relies on the launcher's one-block-per-CU grid being
+    co-resident.  A grid five times the CU count (more blocks than a CU can ever hold at once)
+    must not hang: the resident blocks give up on the first barrier after the poll bound, every
+    later barrier passes, the launch drains and reports status 9 ("not finished", which re-runs
+    the fit on the host-steered path).  A normal launch afterwards is unaffected."""
+    from net.jgp.labs.sparkdq4ml_amd.ops import device, kernels, native
+
+    d, n = 300, 20_000
+    T, y = _data(torch.device("cuda"), d, n, 7, 16)
+    P = kernels.lsq_passes(T, y, None, None)
+    head = torch.cat([P.scalars(), P.moments()])
+    args = (head, True, True, 0.02, 0.0, 20, 1e-9)
+    cus = int(native.hip().device_info()["multiProcessorCount"])
+    key = (P.device.index, P.layout, P.d)
+    monkeypatch.setitem(device._lsq_qn_grid, key, 5 * cus)
+    over = P.qn_fit(*args).cpu()
+    assert int(over[d + 1]) == 9
+    monkeypatch.delitem(device._lsq_qn_grid, key)
+    ok = P.qn_fit(*args).cpu()
+    assert int(ok[d + 1]) == 0 and int(ok[d + 5]) > 0
+
+
 # ---- X4: the data-parallel form (pass, fold, all-reduce, one-block control kernel per evaluation)
 
 @pytest.mark.parametrize("eb,d,n,kw", [
@@ -145,7 +168,7 @@ def test_device_qn_constant_label_takes_the_host_semantics(gpu_session, monkeypa
     (8, 1100, 30_017, dict(regParam=0.01, elasticNetParam=1.0, fitIntercept=False)),
 ])
 def test_device_qn_dp_equals_one_launch(eb, d, n, kw):
-    """At one rank the split form runs the same passes as the cooperative launch (fold order,
+    """At one rank the split form runs the same passes as the one-launch fit (fold order,
     deferred margin update, per-rank un-scaling before the identity reduce); only the four
     evaluation scalars are summed by one block instead of per-block partials, so the fits agree to
     rounding with the same evaluations -- enqueued with no host sync."""
