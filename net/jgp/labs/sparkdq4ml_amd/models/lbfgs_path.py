@@ -170,6 +170,8 @@ class _PendingLsq:
             verify(self._checks)
             d = self.d
             if int(host[d + 1]) != 0:
+                if int(host[d + 1]) == 9:  # evaluation bound, or a grid barrier gave up (grid_barrier)
+                    log.warning("device l-bfgs fit did not finish (status 9); re-running it host-steered")
                 model = self._fallback()
                 self._res = (model._wls_result, model._stats_result)
                 return self._res
