@@ -588,7 +588,9 @@ __global__ __launch_bounds__(256) void huber_rows_kernel(const void* __restrict_
 // The fused pass over dense feature-major columns of T (f32 / f64), d <= D: a row's d features
 // are loaded together into registers (no per-element dtype switch between the loads, so they are
 // all in flight at once), used for the margin and again for Σ m x.  Same partial layout and the
-// same per-row arithmetic as huber_rows_kernel<D>.
+// same per-row arithmetic as huber_rows_kernel<D>.  The feature loads are non-temporal (each
+// evaluation streams X once and X exceeds the MALL): 3.66 -> 3.51-3.55 ms per 1e7 x 16 fit on
+// one box, 4.00 -> 3.66 (mean of three noisy pairs) on another (profiles/r6_huber_device.md).
 template <typename T, int D>
 __global__ __launch_bounds__(256) void huber_rows_dense_kernel(const T* __restrict__ X, int64_t ld, int d, int64_t n,
                                                               const void* __restrict__ y, int ydt,
@@ -614,14 +616,14 @@ __global__ __launch_bounds__(256) void huber_rows_dense_kernel(const T* __restri
   int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   T xn[D];
 #pragma unroll
-  for (int f = 0; f < D; ++f) xn[f] = (f < d && r < n) ? X[(int64_t)f * ld + r] : T(0);
+  for (int f = 0; f < D; ++f) xn[f] = (f < d && r < n) ? __builtin_nontemporal_load(X + (int64_t)f * ld + r) : T(0);
   for (; r < n; r += stride) {
     T xs[D];
 #pragma unroll
     for (int f = 0; f < D; ++f) xs[f] = xn[f];
     const int64_t rn = r + stride < n ? r + stride : r;
 #pragma unroll
-    for (int f = 0; f < D; ++f) xn[f] = f < d ? X[(int64_t)f * ld + rn] : T(0);
+    for (int f = 0; f < D; ++f) xn[f] = f < d ? __builtin_nontemporal_load(X + (int64_t)f * ld + rn) : T(0);
     const bool live = sel == nullptr || sel[r] != 0;
     const double wt = live ? (w ? ld_f64(w, wdt, r) : 1.0) : 0.0;
     if (wt == 0.0) continue;
